@@ -1,0 +1,75 @@
+# Native build for gpumon (MI355X / gfx950).
+#   make            -> python extension gpumon/_core*.so + bin/gpumon-exporter + HIP library
+#   make core       -> C++ core only (no hipcc needed)
+#   make hip        -> gpumon/_hip*.so (HIP kernels: probe + synthetic load, gfx950)
+#   make asan       -> bin/gpumon-exporter-asan (host-only sanitizers)
+# Everything builds IN-TREE so the .so files travel with the repo snapshot to the GPU box.
+
+PY        ?= python3
+CXX       ?= g++
+HIPCC     ?= /opt/rocm/bin/hipcc
+ROCM      ?= /opt/rocm
+GPUMON_ARCH ?= gfx950
+PYINC     := $(shell $(PY) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND    := $(shell $(PY) -c "import pybind11;print(pybind11.get_include())")
+EXT       := $(shell $(PY) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+CXXFLAGS  ?= -O2 -g0 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -Wno-missing-field-initializers
+INC       := -I$(ROCM)/include -Icsrc
+LIBS      := -ldl -lpthread -lz
+
+CORE_SRC  := $(wildcard csrc/core/*.cpp)
+CORE_OBJ  := $(patsubst csrc/%.cpp,build/obj/%.o,$(CORE_SRC))
+CORE_HDR  := $(wildcard csrc/core/*.h)
+
+PYEXT     := gpumon/_core$(EXT)
+HIPEXT    := gpumon/_hip$(EXT)
+BIN       := bin/gpumon-exporter
+HIP_SRC   := $(wildcard csrc/hip/*.hip)
+HIP_HDR   := $(wildcard csrc/hip/*.h)
+
+.PHONY: all core hip clean asan
+all: core hip
+core: $(PYEXT) $(BIN)
+hip: $(HIPEXT)
+
+build/obj/%.o: csrc/%.cpp $(CORE_HDR)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(INC) -c $< -o $@
+
+build/obj/bindings/core_module.o: csrc/bindings/core_module.cpp $(CORE_HDR)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -fvisibility=hidden $(INC) -I$(PYINC) -I$(PYBIND) -c $< -o $@
+
+$(PYEXT): $(CORE_OBJ) build/obj/bindings/core_module.o
+	$(CXX) -shared -o $@ $^ $(LIBS)
+
+$(BIN): $(CORE_OBJ) build/obj/exporter_main.o
+	@mkdir -p bin
+	$(CXX) -o $@ $^ $(LIBS)
+
+# HIP kernels + their pybind11 wrapper in one hipcc-built extension (gfx950 only).
+HIPFLAGS  := --offload-arch=$(GPUMON_ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -Icsrc
+build/obj/hip/kernels.o: csrc/hip/kernels.hip $(HIP_HDR)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+build/obj/bindings/hip_module.o: csrc/bindings/hip_module.cpp $(HIP_HDR)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -I$(PYINC) -I$(PYBIND) -c $< -o $@
+
+$(HIPEXT): build/obj/hip/kernels.o build/obj/bindings/hip_module.o
+	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -shared -fPIC $^ -o $@
+
+asan: $(CORE_SRC) csrc/exporter_main.cpp
+	@mkdir -p bin
+	$(CXX) -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer $(INC) \
+	  $(CORE_SRC) csrc/exporter_main.cpp -o bin/gpumon-exporter-asan $(LIBS)
+
+tsan: $(CORE_SRC) csrc/exporter_main.cpp
+	@mkdir -p bin
+	$(CXX) -O1 -g -std=c++17 -fsanitize=thread $(INC) \
+	  $(CORE_SRC) csrc/exporter_main.cpp -o bin/gpumon-exporter-tsan $(LIBS)
+
+clean:
+	rm -rf build bin gpumon/_core*.so gpumon/_hip*.so

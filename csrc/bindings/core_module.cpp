@@ -1,0 +1,476 @@
+// pybind11 bindings: gpumon._core
+//
+// The Python control plane (config, CLI, CRI / PodResources clients, probe/PMC plugins, bench)
+// drives the C++ core through this module. Every blocking call releases the GIL; the sampler,
+// renderer and HTTP server never take it.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../core/attribution.h"
+#include "../core/common.h"
+#include "../core/exporter.h"
+#include "../core/http_client.h"
+#include "../core/render.h"
+#include "../core/snapshot.h"
+
+namespace py = pybind11;
+using namespace gpumon;
+
+namespace {
+
+template <typename T>
+void get(const py::dict& d, const char* k, T* out) {
+  if (d.contains(k) && !d[k].is_none()) *out = d[k].cast<T>();
+}
+
+MockProc mock_proc_from(const py::dict& d) {
+  MockProc p;
+  get(d, "pid", &p.pid);
+  get(d, "device", &p.device);
+  get(d, "name", &p.name);
+  get(d, "vram_bytes", &p.vram_bytes);
+  get(d, "gfx_share", &p.gfx_share);
+  return p;
+}
+
+ExporterConfig config_from(const py::dict& d) {
+  ExporterConfig c;
+  get(d, "backend", &c.backend);
+  get(d, "amdsmi_lib", &c.amdsmi_lib);
+  get(d, "devices", &c.devices);
+  get(d, "interval_s", &c.interval_s);
+  get(d, "serve_http", &c.serve_http);
+  get(d, "listen_addr", &c.listen_addr);
+  get(d, "port", &c.port);
+  get(d, "http_threads", &c.http_threads);
+  get(d, "host", &c.host);
+  get(d, "gzip", &c.gzip);
+  get(d, "compat_families", &c.compat_families);
+  get(d, "extended_families", &c.extended_families);
+  get(d, "processes", &c.processes);
+  get(d, "link_every", &c.link_every);
+  get(d, "sample_threads", &c.sample_threads);
+  get(d, "influx_url", &c.influx_url);
+  get(d, "influx_extended", &c.influx_extended);
+  get(d, "influx_every", &c.influx_every);
+  get(d, "influx_timeout_s", &c.influx_timeout_s);
+  get(d, "init_retry_s", &c.init_retry_s);
+  get(d, "health_stale_s", &c.health_stale_s);
+  get(d, "version", &c.version);
+  get(d, "activity_acc_scale", &c.rates.activity_acc_scale);
+  get(d, "xgmi_kb_bytes", &c.rates.xgmi_kb_bytes);
+  auto& a = c.attribution;
+  get(d, "procfs_root", &a.procfs_root);
+  get(d, "opt_in", &a.opt_in);
+  get(d, "user_label", &a.user_label);
+  get(d, "user_regex", &a.user_regex);
+  get(d, "user_prefix", &a.user_prefix);
+  get(d, "compat_user_rule", &a.compat_user_rule);
+  get(d, "procfs_env_fallback", &a.procfs_env_fallback);
+  get(d, "include_host_processes", &a.include_host_processes);
+  if (d.contains("mock") && !d["mock"].is_none()) {
+    py::dict m = d["mock"].cast<py::dict>();
+    get(m, "gpus", &c.mock.gpus);
+    get(m, "seed", &c.mock.seed);
+    get(m, "mode", &c.mock.mode);
+    get(m, "const_util", &c.mock.const_util);
+    get(m, "hang_ms", &c.mock.hang_ms);
+    get(m, "fail_device", &c.mock.fail_device);
+    get(m, "fail_every", &c.mock.fail_every);
+    get(m, "unsupported", &c.mock.unsupported);
+    get(m, "n_xcd", &c.mock.n_xcd);
+    get(m, "n_links", &c.mock.n_links);
+    get(m, "firmware_hz", &c.mock.firmware_hz);
+    if (m.contains("procs"))
+      for (auto p : m["procs"].cast<py::list>()) c.mock.procs.push_back(mock_proc_from(p.cast<py::dict>()));
+  }
+  return c;
+}
+
+py::object num(double v) { return has(v) ? py::object(py::float_(v)) : py::object(py::none()); }
+
+py::dict static_to_dict(const DeviceStatic& s) {
+  py::dict d;
+  d["index"] = s.index;
+  d["hip_id"] = s.hip_id;
+  d["gpu_id"] = s.gpu_id;
+  d["uuid"] = s.uuid;
+  d["bdf"] = s.bdf;
+  d["model"] = s.model;
+  d["serial"] = s.serial;
+  d["gfx_target"] = s.gfx_target;
+  d["compute_partition"] = s.compute_partition;
+  d["memory_partition"] = s.memory_partition;
+  d["drm_card"] = s.drm_card;
+  d["drm_render"] = s.drm_render;
+  d["kfd_node"] = s.kfd_node;
+  d["partition_id"] = s.partition_id;
+  d["num_cu"] = s.num_cu;
+  d["vram_total_bytes"] = num(s.vram_total_bytes);
+  d["power_limit_w"] = num(s.power_limit_w);
+  return d;
+}
+
+py::dict sample_to_dict(const DeviceSample& s) {
+  py::dict d;
+  d["ok"] = s.ok;
+  d["fresh"] = s.fresh;
+  d["sample_ns"] = s.sample_ns;
+  d["errors"] = s.errors;
+  d["last_error"] = s.last_error;
+  py::dict f;
+  for (int i = 0; i < F_COUNT; ++i) f[field_name(i)] = num(s.v[i]);
+  d["fields"] = f;
+  py::list xb, gc, ht;
+  for (int k = 0; k < s.n_xcd; ++k) xb.append(num(s.xcd_busy[k]));
+  for (int k = 0; k < kMaxGfxClks; ++k) gc.append(num(s.gfxclks[k]));
+  for (int k = 0; k < kMaxHbm; ++k) ht.append(num(s.hbm_temp[k]));
+  d["xcd_busy"] = xb;
+  d["gfxclks"] = gc;
+  d["hbm_temp"] = ht;
+  py::list links;
+  for (int k = 0; k < s.n_links; ++k) {
+    py::dict l;
+    l["peer_bdf"] = s.links[k].peer_bdf;
+    l["status"] = s.links[k].status;
+    l["bit_rate_gbps"] = num(s.links[k].bit_rate_gbps);
+    l["max_bandwidth_gbps"] = num(s.links[k].max_bandwidth_gbps);
+    l["read_kb"] = s.acc.xgmi_rd_kb[k];
+    l["write_kb"] = s.acc.xgmi_wr_kb[k];
+    links.append(l);
+  }
+  d["links"] = links;
+  py::dict a;
+  a["energy"] = s.acc.energy;
+  a["accumulation_counter"] = s.acc.accumulation_counter;
+  a["gfx_activity_acc"] = s.acc.gfx_activity_acc;
+  a["mem_activity_acc"] = s.acc.mem_activity_acc;
+  a["firmware_ts"] = s.acc.firmware_ts;
+  a["system_clock_ns"] = s.acc.system_clock_ns;
+  a["ppt_res"] = s.acc.ppt_res;
+  py::list xa;
+  for (int k = 0; k < s.acc.n_xcd_acc; ++k) xa.append(s.acc.xcd_busy_acc[k]);
+  a["xcd_busy_acc"] = xa;
+  d["acc"] = a;
+  return d;
+}
+
+py::dict rates_to_dict(const DeviceRates& r) {
+  py::dict d;
+  d["valid"] = r.valid;
+  d["dt_s"] = r.dt_s;
+  d["power_from_energy_w"] = num(r.power_from_energy_w);
+  d["ppt_violation_pct"] = num(r.ppt_violation_pct);
+  d["thermal_violation_pct"] = num(r.thermal_violation_pct);
+  d["gfx_activity_avg_pct"] = num(r.gfx_activity_avg_pct);
+  d["mem_activity_avg_pct"] = num(r.mem_activity_avg_pct);
+  py::list xb, rd, wr;
+  for (int k = 0; k < r.n_xcd; ++k) xb.append(num(r.xcd_busy_avg[k]));
+  for (int k = 0; k < r.n_links; ++k) {
+    rd.append(num(r.xgmi_rd_Bps[k]));
+    wr.append(num(r.xgmi_wr_Bps[k]));
+  }
+  d["xcd_busy_avg"] = xb;
+  d["xgmi_rd_Bps"] = rd;
+  d["xgmi_wr_Bps"] = wr;
+  return d;
+}
+
+py::dict row_to_dict(const PodRow& r) {
+  py::dict d;
+  d["dev"] = r.dev;
+  d["idle"] = r.idle;
+  d["pid"] = r.pid;
+  d["procname"] = r.procname;
+  d["namespace"] = r.pod_namespace;
+  d["podname"] = r.pod_name;
+  d["container"] = r.container;
+  d["containerid"] = r.containerid;
+  d["user_name"] = r.user_name;
+  d["used_memory_bytes"] = r.used_memory_bytes;
+  d["gpu_util"] = r.gpu_util;
+  d["proc_gfx_util"] = num(r.proc_gfx_util);
+  d["cu_occupancy"] = num(r.cu_occupancy);
+  return d;
+}
+
+std::map<std::string, std::string> str_map(const py::dict& d, const char* k) {
+  std::map<std::string, std::string> m;
+  if (d.contains(k) && !d[k].is_none())
+    for (auto kv : d[k].cast<py::dict>()) m[kv.first.cast<std::string>()] = kv.second.cast<std::string>();
+  return m;
+}
+
+MockBackend* mock_of(Exporter& e) {
+  auto* m = dynamic_cast<MockBackend*>(e.backend());
+  if (!m) throw std::runtime_error("exporter backend is not the mock backend");
+  return m;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_core, m) {
+  m.doc() = "gpumon C++ core (MI355X telemetry exporter)";
+
+  m.def("set_log_level", [](int lvl) { g_log_level.store(lvl); });
+  m.def("parse_cgroup", [](const std::string& text) {
+    CgroupInfo c = parse_cgroup(text);
+    py::dict d;
+    d["found"] = c.found;
+    d["runtime"] = c.runtime;
+    d["container_id"] = c.container_id;
+    d["pod_uid"] = c.pod_uid;
+    d["qos"] = c.qos;
+    return d;
+  });
+  m.def("compat_user_from_pod", &compat_user_from_pod, py::arg("pod_name"),
+        py::arg("prefix") = "turing-gpu-notebook-");
+  m.def("escape_label_value", [](const std::string& s) {
+    std::string o;
+    escape_label_value(s, &o);
+    return o;
+  });
+  m.def("escape_influx_tag", [](const std::string& s) {
+    std::string o;
+    escape_influx_tag(s, &o);
+    return o;
+  });
+  m.def("escape_influx_field_str", [](const std::string& s) {
+    std::string o;
+    escape_influx_field_str(s, &o);
+    return o;
+  });
+  m.def("format_double", [](double v) {
+    std::string o;
+    append_double(v, &o);
+    return o;
+  });
+  m.def("gzip", [](const std::string& s) {
+    std::string o;
+    if (!gzip_compress(s, &o)) throw std::runtime_error("gzip failed");
+    return py::bytes(o);
+  });
+  m.def(
+      "scrape_load",
+      [](const std::string& host, int port, const std::string& path, int n, double duration_s,
+         int concurrency, double rate_hz, bool keep_alive, bool gzip) {
+        ScrapeStats s;
+        {
+          py::gil_scoped_release nogil;
+          s = scrape_load(host, port, path, n, duration_s, concurrency, rate_hz, keep_alive, gzip);
+        }
+        py::dict d;
+        d["latencies_s"] = s.latencies_s;
+        d["errors"] = s.errors;
+        d["bytes"] = s.bytes;
+        d["wall_s"] = s.wall_s;
+        return d;
+      },
+      py::arg("host"), py::arg("port"), py::arg("path") = "/metrics", py::arg("n_requests") = 100,
+      py::arg("duration_s") = 0.0, py::arg("concurrency") = 1, py::arg("rate_hz") = 0.0,
+      py::arg("keep_alive") = true, py::arg("gzip") = false);
+  m.def(
+      "http_request",
+      [](const std::string& method, const std::string& url, const std::string& body,
+         const std::string& headers, double timeout_s) {
+        HttpClient c(timeout_s);
+        std::string resp, err;
+        int st;
+        {
+          py::gil_scoped_release nogil;
+          st = c.request(method, parse_url(url), body, headers, &resp, &err);
+        }
+        return py::make_tuple(st, py::bytes(resp), err);
+      },
+      py::arg("method"), py::arg("url"), py::arg("body") = "", py::arg("headers") = "",
+      py::arg("timeout_s") = 5.0);
+
+  py::class_<Exporter>(m, "Exporter")
+      .def(py::init([](const py::dict& cfg) { return new Exporter(config_from(cfg)); }))
+      .def("start",
+           [](Exporter& e) {
+             std::string err;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = e.start(&err);
+             }
+             if (!ok) throw std::runtime_error("exporter start failed: " + err);
+             return err;  // non-fatal backend error (retrying), or ""
+           })
+      .def("stop", [](Exporter& e) {
+        py::gil_scoped_release nogil;
+        e.stop();
+      })
+      .def("tick",
+           [](Exporter& e) {
+             TickInfo t;
+             {
+               py::gil_scoped_release nogil;
+               t = e.tick();
+             }
+             py::dict d;
+             d["seq"] = t.seq;
+             d["duration_s"] = t.duration_s;
+             d["devices"] = t.devices;
+             d["devices_ok"] = t.devices_ok;
+             d["pod_rows"] = t.pod_rows;
+             d["body_bytes"] = t.body_bytes;
+             return d;
+           })
+      .def("wait_for_seq",
+           [](Exporter& e, uint64_t seq, double timeout_s) {
+             py::gil_scoped_release nogil;
+             return e.wait_for_seq(seq, timeout_s);
+           })
+      .def_property_readonly("port", &Exporter::port)
+      .def_property_readonly("seq", &Exporter::seq)
+      .def("healthy", &Exporter::healthy)
+      .def("ready", &Exporter::ready)
+      .def("metrics_text",
+           [](Exporter& e) {
+             auto s = e.snapshot();
+             return s ? s->body : std::string();
+           })
+      .def("metrics_gzip",
+           [](Exporter& e) {
+             auto s = e.snapshot();
+             return py::bytes(s ? s->body_gz : std::string());
+           })
+      .def("influx_text", &Exporter::render_influx_now)
+      .def("statics",
+           [](Exporter& e) {
+             py::list l;
+             for (const auto& s : e.statics()) l.append(static_to_dict(s));
+             return l;
+           })
+      .def("samples",
+           [](Exporter& e) {
+             py::list l;
+             for (const auto& s : e.samples()) l.append(sample_to_dict(s));
+             return l;
+           })
+      .def("rates",
+           [](Exporter& e) {
+             py::list l;
+             for (const auto& r : e.rates()) l.append(rates_to_dict(r));
+             return l;
+           })
+      .def("pod_rows",
+           [](Exporter& e) {
+             py::list l;
+             for (const auto& r : e.pod_rows()) l.append(row_to_dict(r));
+             return l;
+           })
+      .def("self_stats",
+           [](Exporter& e) {
+             SelfStats s = e.self_stats();
+             py::dict d;
+             d["ticks"] = s.ticks;
+             d["samples"] = s.samples;
+             d["stale_samples"] = s.stale_samples;
+             d["overruns"] = s.overruns;
+             d["scrapes"] = s.scrapes;
+             d["http_connections"] = s.http_connections;
+             d["pods_attributed"] = s.pods_attributed;
+             d["backend"] = s.backend;
+             d["backend_version"] = s.backend_version;
+             d["backend_up"] = s.backend_up;
+             d["influx_ok"] = s.influx_ok;
+             d["influx_fail"] = s.influx_fail;
+             d["influx_dropped"] = s.influx_dropped;
+             d["device_errors"] = s.device_errors;
+             d["sample_count"] = s.sample_hist.count;
+             d["sample_sum_s"] = s.sample_hist.sum;
+             d["attribution_cache_hits"] = s.attribution_cache_hits;
+             d["attribution_cache_misses"] = s.attribution_cache_misses;
+             return d;
+           })
+      .def("scrape_quantile", &Exporter::scrape_quantile)
+      .def("sample_quantile", &Exporter::sample_quantile)
+      .def("set_container_meta",
+           [](Exporter& e, const py::list& metas) {
+             std::vector<ContainerMeta> v;
+             for (auto it : metas) {
+               py::dict d = it.cast<py::dict>();
+               ContainerMeta c;
+               get(d, "container_id", &c.container_id);
+               get(d, "container_name", &c.container_name);
+               get(d, "pod_name", &c.pod_name);
+               get(d, "pod_namespace", &c.pod_namespace);
+               get(d, "pod_uid", &c.pod_uid);
+               get(d, "user_name", &c.user_name);
+               c.labels = str_map(d, "labels");
+               v.push_back(std::move(c));
+             }
+             e.set_container_meta(std::move(v));
+           })
+      .def("set_allocations",
+           [](Exporter& e, const py::list& allocs) {
+             std::vector<Allocation> v;
+             for (auto it : allocs) {
+               py::dict d = it.cast<py::dict>();
+               Allocation a;
+               get(d, "pod_namespace", &a.pod_namespace);
+               get(d, "pod_name", &a.pod_name);
+               get(d, "container_name", &a.container_name);
+               get(d, "container_id", &a.container_id);
+               get(d, "pod_uid", &a.pod_uid);
+               get(d, "gpu_index", &a.gpu_index);
+               get(d, "user_name", &a.user_name);
+               a.labels = str_map(d, "labels");
+               v.push_back(std::move(a));
+             }
+             e.set_allocations(std::move(v));
+           })
+      .def("set_extra",
+           [](Exporter& e, const std::string& source, const py::list& series) {
+             std::vector<ExtraSeries> v;
+             for (auto it : series) {
+               py::dict d = it.cast<py::dict>();
+               ExtraSeries s;
+               get(d, "name", &s.name);
+               get(d, "help", &s.help);
+               get(d, "type", &s.type);
+               get(d, "dev", &s.dev);
+               get(d, "value", &s.value);
+               for (auto kv : str_map(d, "labels")) s.labels.emplace_back(kv.first, kv.second);
+               v.push_back(std::move(s));
+             }
+             e.set_extra(source, std::move(v));
+           })
+      .def("resolve_pid",
+           [](Exporter& e, uint32_t pid) {
+             ProcIdentity id = e.attributor().resolve(pid);
+             py::dict d;
+             d["valid"] = id.valid;
+             d["in_container"] = id.in_container;
+             d["opted_in"] = id.opted_in;
+             d["comm"] = id.comm;
+             d["runtime"] = id.runtime;
+             d["container_id"] = id.container_id;
+             d["container_name"] = id.container_name;
+             d["pod_name"] = id.pod_name;
+             d["pod_namespace"] = id.pod_namespace;
+             d["pod_uid"] = id.pod_uid;
+             d["user_name"] = id.user_name;
+             d["source"] = id.source;
+             return d;
+           })
+      .def("derive_user",
+           [](Exporter& e, const std::string& pod, const py::dict& labels) {
+             std::map<std::string, std::string> m;
+             for (auto kv : labels) m[kv.first.cast<std::string>()] = kv.second.cast<std::string>();
+             return e.attributor().derive_user(pod, m);
+           })
+      .def("mock_set_util", [](Exporter& e, int dev, double pct) { mock_of(e)->set_util(dev, pct); })
+      .def("mock_set_procs",
+           [](Exporter& e, const py::list& procs) {
+             std::vector<MockProc> v;
+             for (auto p : procs) v.push_back(mock_proc_from(p.cast<py::dict>()));
+             mock_of(e)->set_procs(v);
+           })
+      .def("mock_set_fail", [](Exporter& e, int dev, int every) { mock_of(e)->set_fail(dev, every); })
+      .def("mock_set_hang_ms", [](Exporter& e, double ms) { mock_of(e)->set_hang_ms(ms); })
+      .def("mock_calls", [](Exporter& e, int dev) { return mock_of(e)->calls(dev); });
+}

@@ -1,0 +1,90 @@
+// pybind11 bindings: gpumon._hip (gfx950 kernels: K1 probe, K2 synthetic load).
+// Pointers/streams are passed as integers (torch tensor .data_ptr(), torch.cuda stream handle) so
+// the kernels can be checked against PyTorch fp32 references on the same tensors.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../hip/hip_api.h"
+
+namespace py = pybind11;
+using namespace gpumon_hip;
+
+static void* P(uintptr_t x) { return reinterpret_cast<void*>(x); }
+
+PYBIND11_MODULE(_hip, m) {
+  m.doc() = "gpumon gfx950 HIP kernels (probe ring buffer + synthetic MFMA/HBM load)";
+  m.def("device_count", &device_count);
+  m.def("device_arch", &device_arch);
+  m.def("device_cu_count", &device_cu_count);
+
+  m.def("mfma_tile", [](int dev, uintptr_t a, uintptr_t b, uintptr_t c, int iters, uintptr_t stream) {
+    launch_mfma_tile(dev, P(a), P(b), static_cast<float*>(P(c)), iters, P(stream));
+  }, py::arg("dev"), py::arg("a"), py::arg("b"), py::arg("c"), py::arg("iters"), py::arg("stream") = 0);
+  m.def("mfma_burn", [](int dev, uintptr_t a, uintptr_t b, uintptr_t out, int blocks, int iters, uintptr_t stream) {
+    launch_mfma_burn(dev, P(a), P(b), static_cast<float*>(P(out)), blocks, iters, P(stream));
+  }, py::arg("dev"), py::arg("a"), py::arg("b"), py::arg("out"), py::arg("blocks"), py::arg("iters"),
+     py::arg("stream") = 0);
+  m.def("stream_copy", [](int dev, uintptr_t src, uintptr_t dst, size_t n16, int blocks, uintptr_t stream) {
+    launch_stream_copy(dev, P(src), P(dst), n16, blocks, P(stream));
+  }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("n16"), py::arg("blocks") = 4096,
+     py::arg("stream") = 0);
+  m.def("stream_triad", [](int dev, uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n, int blocks,
+                           uintptr_t stream) {
+    launch_stream_triad(dev, static_cast<const float*>(P(a)), static_cast<const float*>(P(b)),
+                        static_cast<float*>(P(c)), s, n, blocks, P(stream));
+  }, py::arg("dev"), py::arg("a"), py::arg("b"), py::arg("c"), py::arg("s"), py::arg("n"),
+     py::arg("blocks") = 4096, py::arg("stream") = 0);
+
+  py::class_<LoadGen>(m, "LoadGen")
+      .def(py::init<int, std::string, double, size_t, int>(), py::arg("dev"), py::arg("kind") = "mixed",
+           py::arg("duty") = 1.0, py::arg("hbm_bytes") = size_t(1) << 30, py::arg("mfma_iters") = 8192)
+      .def("start", [](LoadGen& g) {
+        py::gil_scoped_release nogil;
+        g.start();
+      })
+      .def("stop", [](LoadGen& g) {
+        py::gil_scoped_release nogil;
+        g.stop();
+      })
+      .def_property_readonly("running", &LoadGen::running)
+      .def("stats", [](LoadGen& g) {
+        LoadStats s = g.stats();
+        py::dict d;
+        d["launches"] = s.launches;
+        d["busy_s"] = s.busy_s;
+        d["flops"] = s.flops;
+        d["bytes"] = s.bytes;
+        d["tflops"] = s.busy_s > 0 ? s.flops / s.busy_s / 1e12 : 0.0;
+        d["tbps"] = s.busy_s > 0 ? s.bytes / s.busy_s / 1e12 : 0.0;
+        return d;
+      });
+
+  py::class_<Probe>(m, "Probe")
+      .def(py::init<int, int, int, int>(), py::arg("dev"), py::arg("blocks") = 1024, py::arg("slots") = 4,
+           py::arg("spin_ticks") = 200)
+      .def("launch", &Probe::launch)
+      .def_property_readonly("blocks", &Probe::blocks)
+      .def("poll", [](Probe& p, int slot, double timeout_s) -> py::object {
+        ProbeResult r;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = timeout_s > 0 ? p.wait(slot, timeout_s, &r) : p.poll(slot, &r);
+        }
+        if (!ok) return py::none();
+        py::dict d;
+        d["seq"] = r.seq;
+        d["blocks"] = r.blocks;
+        d["arrived"] = r.arrived;
+        d["host_latency_s"] = (r.host_done_ns - r.host_launch_ns) * 1e-9;
+        d["gpu_span_s"] = r.gpu_span_ticks * 1e-8;
+        d["xcc_blocks"] = r.xcc_blocks;
+        d["xcc_clock_mhz"] = r.xcc_clock_mhz;
+        d["unique_cus"] = r.unique_cus;
+        py::list recs;
+        for (const auto& x : r.records)
+          recs.append(py::make_tuple(x.xcc_id, x.hw_id, x.t0_real, x.t1_real, x.c0, x.c1, x.seq, x.block));
+        d["records"] = recs;
+        return d;
+      }, py::arg("slot"), py::arg("timeout_s") = 0.0);
+}

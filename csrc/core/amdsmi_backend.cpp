@@ -1,0 +1,497 @@
+// AmdSmiBackend: direct libamd_smi sampling for MI355X (gfx950).
+//
+// Reference parity: replaces `nvidia-smi --query-gpu=...` and `--query-compute-apps=...`
+// subprocesses (/root/reference/gpu.py:104-116) with in-process calls. One tick per device costs
+// one amdsmi_get_gpu_metrics_info (the firmware table: activity, clocks, temps, power, energy,
+// per-XCD busy, xGMI accumulators, PCIe, throttle residencies; ~0.3 ms measured on MI355X) +
+// amdsmi_get_gpu_vram_usage (~0.1 ms) + amdsmi_get_gpu_process_list (~0.7 ms). The slow
+// amdsmi_get_violation_status (~100 ms measured) is deliberately NOT used: the same residency
+// accumulators are in the metrics table and rates are derived from them (rates.cpp).
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "backend.h"
+#include "common.h"
+#include "smi_table.h"
+
+namespace gpumon {
+
+// ---------------------------------------------------------------------------------------------
+// SmiTable
+// ---------------------------------------------------------------------------------------------
+bool SmiTable::load(const std::string& explicit_path, std::string* err) {
+  if (dl) return true;
+  std::vector<std::string> candidates;
+  if (!explicit_path.empty()) candidates.push_back(explicit_path);
+  if (const char* e = getenv("GPUMON_AMDSMI_LIB")) candidates.emplace_back(e);
+  candidates.emplace_back("libamd_smi.so.26");
+  candidates.emplace_back("libamd_smi.so");
+  if (const char* r = getenv("ROCM_PATH")) candidates.push_back(std::string(r) + "/lib/libamd_smi.so");
+  candidates.emplace_back("/opt/rocm/lib/libamd_smi.so.26");
+  candidates.emplace_back("/opt/rocm/lib/libamd_smi.so");
+  std::string errs;
+  for (const auto& c : candidates) {
+    dl = dlopen(c.c_str(), RTLD_NOW | RTLD_LOCAL);
+    if (dl) {
+      path = c;
+      break;
+    }
+    const char* e = dlerror();
+    errs += c + ": " + (e ? e : "?") + "; ";
+  }
+  if (!dl) {
+    if (err) *err = "cannot dlopen libamd_smi (" + errs + ")";
+    return false;
+  }
+#define GPUMON_REQ(fn)                                                        \
+  fn = reinterpret_cast<decltype(fn)>(dlsym(dl, #fn));                        \
+  if (!fn) {                                                                  \
+    if (err) *err = std::string("libamd_smi missing required symbol ") + #fn; \
+    unload();                                                                 \
+    return false;                                                             \
+  }
+  GPUMON_SMI_REQUIRED(GPUMON_REQ)
+#undef GPUMON_REQ
+#define GPUMON_OPT(fn) fn = reinterpret_cast<decltype(fn)>(dlsym(dl, #fn));
+  GPUMON_SMI_OPTIONAL(GPUMON_OPT)
+#undef GPUMON_OPT
+  return true;
+}
+
+void SmiTable::unload() {
+  if (dl) dlclose(dl);
+  dl = nullptr;
+#define GPUMON_NULL(fn) fn = nullptr;
+  GPUMON_SMI_REQUIRED(GPUMON_NULL)
+  GPUMON_SMI_OPTIONAL(GPUMON_NULL)
+#undef GPUMON_NULL
+}
+
+const char* smi_status_str(int s) {
+  switch (s) {
+    case AMDSMI_STATUS_SUCCESS: return "SUCCESS";
+    case AMDSMI_STATUS_INVAL: return "INVAL";
+    case AMDSMI_STATUS_NOT_SUPPORTED: return "NOT_SUPPORTED";
+    case AMDSMI_STATUS_NOT_YET_IMPLEMENTED: return "NOT_YET_IMPLEMENTED";
+    case AMDSMI_STATUS_FAIL_LOAD_MODULE: return "FAIL_LOAD_MODULE";
+    case AMDSMI_STATUS_NO_PERM: return "NO_PERM";
+    case AMDSMI_STATUS_OUT_OF_RESOURCES: return "OUT_OF_RESOURCES";
+    case AMDSMI_STATUS_INIT_ERROR: return "INIT_ERROR";
+    case AMDSMI_STATUS_NOT_FOUND: return "NOT_FOUND";
+    case AMDSMI_STATUS_BUSY: return "BUSY";
+    case AMDSMI_STATUS_TIMEOUT: return "TIMEOUT";
+    case AMDSMI_STATUS_DRIVER_NOT_LOADED: return "DRIVER_NOT_LOADED";
+    default: return "ERROR";
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// helpers: firmware N/A sentinels are all-ones of the field width
+// ---------------------------------------------------------------------------------------------
+static inline double u16v(uint16_t x, double scale = 1.0) {
+  return x == 0xFFFF ? kNaN : static_cast<double>(x) * scale;
+}
+static inline double u32v(uint32_t x, double scale = 1.0) {
+  return x == 0xFFFFFFFFu ? kNaN : static_cast<double>(x) * scale;
+}
+static inline double u64v(uint64_t x, double scale = 1.0) {
+  return x == ~0ull ? kNaN : static_cast<double>(x) * scale;
+}
+static inline bool ok16(uint16_t x) { return x != 0xFFFF; }
+static inline bool ok32(uint32_t x) { return x != 0xFFFFFFFFu; }
+static inline bool ok64(uint64_t x) { return x != ~0ull; }
+
+static std::string bdf_str(const amdsmi_bdf_t& b) {
+  char buf[32];
+  snprintf(buf, sizeof buf, "%04llx:%02llx:%02llx.%llx",
+           static_cast<unsigned long long>(b.domain_number),
+           static_cast<unsigned long long>(b.bus_number),
+           static_cast<unsigned long long>(b.device_number),
+           static_cast<unsigned long long>(b.function_number));
+  return buf;
+}
+
+// ---------------------------------------------------------------------------------------------
+// AmdSmiBackend
+// ---------------------------------------------------------------------------------------------
+AmdSmiBackend::AmdSmiBackend(std::string lib_path) : lib_path_(std::move(lib_path)) {}
+
+AmdSmiBackend::~AmdSmiBackend() { shutdown(); }
+
+void AmdSmiBackend::shutdown() {
+  if (t_ && inited_) t_->amdsmi_shut_down();
+  inited_ = false;
+  handles_.clear();
+  devs_.clear();
+  caps_.clear();
+}
+
+bool AmdSmiBackend::init(std::string* err) {
+  shutdown();
+  if (!t_) t_ = std::make_unique<SmiTable>();
+  if (!t_->load(lib_path_, err)) return false;
+  amdsmi_status_t st = t_->amdsmi_init(AMDSMI_INIT_AMD_GPUS);
+  if (st != AMDSMI_STATUS_SUCCESS) {
+    if (err) *err = std::string("amdsmi_init: ") + smi_status_str(st);
+    return false;
+  }
+  inited_ = true;
+  if (t_->amdsmi_get_lib_version) {
+    amdsmi_version_t v{};
+    if (t_->amdsmi_get_lib_version(&v) == AMDSMI_STATUS_SUCCESS)
+      lib_version_ = std::to_string(v.major) + "." + std::to_string(v.minor) + "." +
+                     std::to_string(v.release);
+  }
+  uint32_t nsock = 0;
+  st = t_->amdsmi_get_socket_handles(&nsock, nullptr);
+  if (st != AMDSMI_STATUS_SUCCESS) {
+    if (err) *err = std::string("amdsmi_get_socket_handles: ") + smi_status_str(st);
+    return false;
+  }
+  std::vector<amdsmi_socket_handle> socks(nsock);
+  if (nsock) t_->amdsmi_get_socket_handles(&nsock, socks.data());
+  std::vector<std::pair<int, void*>> found;  // (hip_id, handle)
+  for (uint32_t s = 0; s < nsock; ++s) {
+    uint32_t np = 0;
+    if (t_->amdsmi_get_processor_handles(socks[s], &np, nullptr) != AMDSMI_STATUS_SUCCESS) continue;
+    std::vector<amdsmi_processor_handle> ph(np);
+    if (np && t_->amdsmi_get_processor_handles(socks[s], &np, ph.data()) != AMDSMI_STATUS_SUCCESS)
+      continue;
+    for (auto h : ph) {
+      if (t_->amdsmi_get_processor_type) {
+        processor_type_t pt{};
+        if (t_->amdsmi_get_processor_type(h, &pt) == AMDSMI_STATUS_SUCCESS &&
+            pt != AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+          continue;
+      }
+      int hip = static_cast<int>(found.size());
+      if (t_->amdsmi_get_gpu_enumeration_info) {
+        amdsmi_enumeration_info_t ei{};
+        if (t_->amdsmi_get_gpu_enumeration_info(h, &ei) == AMDSMI_STATUS_SUCCESS && ok32(ei.hip_id))
+          hip = static_cast<int>(ei.hip_id);
+      }
+      found.emplace_back(hip, h);
+    }
+  }
+  std::sort(found.begin(), found.end(),
+            [](const auto& a, const auto& b) { return a.first < b.first; });
+  for (auto& [hip, h] : found) {
+    if (!keep(hip)) continue;
+    DeviceStatic d;
+    d.index = static_cast<int>(devs_.size());
+    d.hip_id = hip;
+    d.gpu_id = std::to_string(hip);
+    if (t_->amdsmi_get_gpu_enumeration_info) {
+      amdsmi_enumeration_info_t ei{};
+      if (t_->amdsmi_get_gpu_enumeration_info(h, &ei) == AMDSMI_STATUS_SUCCESS) {
+        d.drm_card = ok32(ei.drm_card) ? static_cast<int>(ei.drm_card) : -1;
+        d.drm_render = ok32(ei.drm_render) ? static_cast<int>(ei.drm_render) : -1;
+      }
+    }
+    if (t_->amdsmi_get_gpu_device_uuid) {
+      char uuid[AMDSMI_MAX_STRING_LENGTH] = {0};
+      unsigned int len = sizeof uuid;
+      if (t_->amdsmi_get_gpu_device_uuid(h, &len, uuid) == AMDSMI_STATUS_SUCCESS) d.uuid = uuid;
+    }
+    if (t_->amdsmi_get_gpu_device_bdf) {
+      amdsmi_bdf_t b{};
+      if (t_->amdsmi_get_gpu_device_bdf(h, &b) == AMDSMI_STATUS_SUCCESS) d.bdf = bdf_str(b);
+    }
+    if (t_->amdsmi_get_gpu_asic_info) {
+      amdsmi_asic_info_t ai{};
+      if (t_->amdsmi_get_gpu_asic_info(h, &ai) == AMDSMI_STATUS_SUCCESS) {
+        d.model = ai.market_name;
+        d.serial = ai.asic_serial;
+        if (ok32(ai.num_of_compute_units)) d.num_cu = static_cast<int>(ai.num_of_compute_units);
+        if (ok64(ai.target_graphics_version)) {
+          char gfx[32];
+          snprintf(gfx, sizeof gfx, "gfx%llx", static_cast<unsigned long long>(ai.target_graphics_version));
+          d.gfx_target = gfx;
+        }
+      }
+    }
+    if (t_->amdsmi_get_gpu_kfd_info) {
+      amdsmi_kfd_info_t ki{};
+      if (t_->amdsmi_get_gpu_kfd_info(h, &ki) == AMDSMI_STATUS_SUCCESS) {
+        d.kfd_node = ok32(ki.node_id) ? static_cast<int>(ki.node_id) : -1;
+        d.partition_id = ok32(ki.current_partition_id) ? static_cast<int>(ki.current_partition_id) : 0;
+      }
+    }
+    if (t_->amdsmi_get_gpu_compute_partition) {
+      char buf[64] = {0};
+      if (t_->amdsmi_get_gpu_compute_partition(h, buf, sizeof buf) == AMDSMI_STATUS_SUCCESS)
+        d.compute_partition = buf;
+    }
+    if (t_->amdsmi_get_gpu_memory_partition) {
+      char buf[64] = {0};
+      if (t_->amdsmi_get_gpu_memory_partition(h, buf, sizeof buf) == AMDSMI_STATUS_SUCCESS)
+        d.memory_partition = buf;
+    }
+    if (t_->amdsmi_get_gpu_driver_info) {
+      amdsmi_driver_info_t di{};
+      if (t_->amdsmi_get_gpu_driver_info(h, &di) == AMDSMI_STATUS_SUCCESS) {
+        d.driver_version = di.driver_version;
+        if (d.driver_version.size() > 64) d.driver_version.resize(64);
+      }
+    }
+    if (t_->amdsmi_get_power_info) {
+      amdsmi_power_info_t pi{};
+      if (t_->amdsmi_get_power_info(h, &pi) == AMDSMI_STATUS_SUCCESS && ok32(pi.power_limit)) {
+        // ROCm 7.2 reports power_limit in microwatts despite the header comment (1400000000).
+        double pl = static_cast<double>(pi.power_limit);
+        d.power_limit_w = pl > 1e5 ? pl / 1e6 : pl;
+      }
+    }
+    if (t_->amdsmi_get_gpu_vram_usage) {
+      amdsmi_vram_usage_t vu{};
+      if (t_->amdsmi_get_gpu_vram_usage(h, &vu) == AMDSMI_STATUS_SUCCESS)
+        d.vram_total_bytes = static_cast<double>(vu.vram_total) * 1048576.0;
+    }
+    handles_.push_back(h);
+    devs_.push_back(std::move(d));
+    caps_.emplace_back();
+    proc_buf_.emplace_back(sizeof(amdsmi_proc_info_t) * 64);
+  }
+  if (devs_.empty()) {
+    if (err) *err = "amdsmi: no AMD GPUs found (after device filter)";
+    return false;
+  }
+  // Energy resolution is device-global on MI3xx/MI355X; read it once.
+  if (t_->amdsmi_get_energy_count) {
+    uint64_t e = 0, ts = 0;
+    float res = 0;
+    if (t_->amdsmi_get_energy_count(handles_[0], &e, &res, &ts) == AMDSMI_STATUS_SUCCESS && res > 0)
+      energy_res_uj_ = res;
+  }
+  GPUMON_LOG(LogLevel::kInfo, "amdsmi",
+             "loaded " + t_->path + " version=" + lib_version_ + " gpus=" +
+                 std::to_string(devs_.size()));
+  return true;
+}
+
+void AmdSmiBackend::sample(int i, DeviceSample* out) {
+  out->reset();
+  int64_t t0 = mono_ns();
+  out->host_mono_ns = t0;
+  out->host_wall_ns = wall_ns();
+  void* h = handles_[i];
+  Caps& c = caps_[i];
+  auto& v = out->v;
+  bool any = false;
+
+  if (c.metrics && t_->amdsmi_get_gpu_metrics_info) {
+    amdsmi_gpu_metrics_t m;
+    amdsmi_status_t st = t_->amdsmi_get_gpu_metrics_info(h, &m);
+    if (st == AMDSMI_STATUS_SUCCESS) {
+      any = true;
+      v[F_GFX_UTIL] = u16v(m.average_gfx_activity);
+      v[F_UMC_UTIL] = u16v(m.average_umc_activity);
+      v[F_MM_UTIL] = u16v(m.average_mm_activity);
+      v[F_TEMP_EDGE] = u16v(m.temperature_edge);
+      v[F_TEMP_HOTSPOT] = u16v(m.temperature_hotspot);
+      v[F_TEMP_MEM] = u16v(m.temperature_mem);
+      v[F_TEMP_VRGFX] = u16v(m.temperature_vrgfx);
+      v[F_TEMP_VRSOC] = u16v(m.temperature_vrsoc);
+      v[F_TEMP_VRMEM] = u16v(m.temperature_vrmem);
+      for (int k = 0; k < kMaxHbm; ++k) out->hbm_temp[k] = u16v(m.temperature_hbm[k]);
+      v[F_POWER_CUR] = u16v(m.current_socket_power);
+      v[F_POWER_AVG] = u16v(m.average_socket_power);
+      v[F_POWER_LIMIT] = devs_[i].power_limit_w;
+      v[F_GFXCLK_CUR] = u16v(m.current_gfxclk);
+      v[F_GFXCLK_AVG] = u16v(m.average_gfxclk_frequency);
+      v[F_SOCCLK_CUR] = u16v(m.current_socclk);
+      v[F_UCLK_CUR] = u16v(m.current_uclk);
+      v[F_VCLK0_CUR] = u16v(m.current_vclk0);
+      v[F_DCLK0_CUR] = u16v(m.current_dclk0);
+      v[F_THROTTLE_STATUS] = u32v(m.throttle_status);
+      v[F_INDEP_THROTTLE] = u64v(m.indep_throttle_status);
+      v[F_FAN_RPM] = u16v(m.current_fan_speed);
+      v[F_PCIE_WIDTH] = u16v(m.pcie_link_width);
+      v[F_PCIE_SPEED_GTS] = u16v(m.pcie_link_speed, 0.1);
+      v[F_PCIE_BW_INST] = u64v(m.pcie_bandwidth_inst);
+      v[F_PCIE_REPLAY] = u64v(m.pcie_replay_count_acc);
+      v[F_PCIE_L0_RECOV] = u64v(m.pcie_l0_to_recov_count_acc);
+      v[F_PCIE_NAK_SENT] = u32v(m.pcie_nak_sent_count_acc);
+      v[F_PCIE_NAK_RCVD] = u32v(m.pcie_nak_rcvd_count_acc);
+      v[F_VOLT_SOC] = u16v(m.voltage_soc, 1e-3);
+      v[F_VOLT_GFX] = u16v(m.voltage_gfx, 1e-3);
+      v[F_VOLT_MEM] = u16v(m.voltage_mem, 1e-3);
+      v[F_XGMI_LINK_WIDTH] = u16v(m.xgmi_link_width);
+      v[F_XGMI_LINK_SPEED] = u16v(m.xgmi_link_speed);
+      v[F_VRAM_MAX_BW] = u64v(m.vram_max_bandwidth);
+      v[F_NUM_PARTITION] = u16v(m.num_partition);
+      v[F_GFXCLK_LOCK] = u32v(m.gfxclk_lock_status);
+      for (int k = 0; k < kMaxGfxClks; ++k) out->gfxclks[k] = u16v(m.current_gfxclks[k]);
+
+      Accumulators& a = out->acc;
+      a.valid = true;
+      if (ok64(m.energy_accumulator)) {
+        a.energy = m.energy_accumulator;
+        a.energy_resolution_uj = energy_res_uj_;
+        v[F_ENERGY_J] = static_cast<double>(a.energy) * energy_res_uj_ * 1e-6;
+      }
+      a.firmware_ts = ok64(m.firmware_timestamp) ? m.firmware_timestamp : 0;
+      a.system_clock_ns = ok64(m.system_clock_counter) ? m.system_clock_counter : 0;
+      if (ok64(m.accumulation_counter)) {
+        a.accumulation_counter = m.accumulation_counter;
+        a.has_residency = ok64(m.ppt_residency_acc);
+        a.prochot_res = ok64(m.prochot_residency_acc) ? m.prochot_residency_acc : 0;
+        a.ppt_res = ok64(m.ppt_residency_acc) ? m.ppt_residency_acc : 0;
+        a.socket_thm_res = ok64(m.socket_thm_residency_acc) ? m.socket_thm_residency_acc : 0;
+        a.vr_thm_res = ok64(m.vr_thm_residency_acc) ? m.vr_thm_residency_acc : 0;
+        a.hbm_thm_res = ok64(m.hbm_thm_residency_acc) ? m.hbm_thm_residency_acc : 0;
+      }
+      if (ok32(m.gfx_activity_acc)) {
+        a.has_activity_acc = true;
+        a.gfx_activity_acc = m.gfx_activity_acc;
+        a.mem_activity_acc = ok32(m.mem_activity_acc) ? m.mem_activity_acc : 0;
+      }
+      if (ok64(m.pcie_bandwidth_acc)) {
+        a.has_pcie_bw_acc = true;
+        a.pcie_bw_acc = m.pcie_bandwidth_acc;
+      }
+      // Per-XCD (XCC) busy: the XCP this device is, partition_id in CPX modes, else XCP 0.
+      int xcp = devs_[i].partition_id;
+      if (xcp < 0 || xcp >= AMDSMI_MAX_NUM_XCP || !ok32(m.xcp_stats[xcp].gfx_busy_inst[0])) xcp = 0;
+      const auto& xs = m.xcp_stats[xcp];
+      int nx = 0;
+      for (int k = 0; k < kMaxXcc; ++k) {
+        if (!ok32(xs.gfx_busy_inst[k])) break;
+        out->xcd_busy[k] = static_cast<double>(xs.gfx_busy_inst[k]);
+        a.xcd_busy_acc[k] = ok64(xs.gfx_busy_acc[k]) ? xs.gfx_busy_acc[k] : 0;
+        nx = k + 1;
+      }
+      out->n_xcd = nx;
+      a.n_xcd_acc = nx;
+      // xGMI accumulators (KB), link status. Slot 0 on MI355X is the (N/A) self slot.
+      int nl = 0;
+      for (int k = 0; k < kMaxLinks; ++k) {
+        a.xgmi_rd_kb[k] = ok64(m.xgmi_read_data_acc[k]) ? m.xgmi_read_data_acc[k] : 0;
+        a.xgmi_wr_kb[k] = ok64(m.xgmi_write_data_acc[k]) ? m.xgmi_write_data_acc[k] : 0;
+        out->links[k].status = ok16(m.xgmi_link_status[k]) ? m.xgmi_link_status[k] : -1;
+        if (ok16(m.xgmi_link_status[k]) || m.xgmi_read_data_acc[k] || m.xgmi_write_data_acc[k])
+          nl = k + 1;
+      }
+      out->n_links = nl;
+      a.n_links_acc = nl;
+      if (ok16(m.xgmi_link_speed))
+        for (int k = 0; k < nl; ++k) out->links[k].bit_rate_gbps = m.xgmi_link_speed;
+    } else if (st == AMDSMI_STATUS_NOT_SUPPORTED) {
+      c.metrics = false;
+    } else {
+      out->errors++;
+      out->last_error = std::string("gpu_metrics: ") + smi_status_str(st);
+    }
+  }
+  // Fallbacks for devices without a metrics table.
+  if (!c.metrics && c.activity && t_->amdsmi_get_gpu_activity) {
+    amdsmi_engine_usage_t u{};
+    amdsmi_status_t st = t_->amdsmi_get_gpu_activity(h, &u);
+    if (st == AMDSMI_STATUS_SUCCESS) {
+      any = true;
+      v[F_GFX_UTIL] = u32v(u.gfx_activity);
+      v[F_UMC_UTIL] = u32v(u.umc_activity);
+      v[F_MM_UTIL] = u32v(u.mm_activity);
+    } else if (st == AMDSMI_STATUS_NOT_SUPPORTED) {
+      c.activity = false;
+    } else {
+      out->errors++;
+      out->last_error = std::string("gpu_activity: ") + smi_status_str(st);
+    }
+  }
+  if (!c.metrics && c.power && t_->amdsmi_get_power_info) {
+    amdsmi_power_info_t p{};
+    amdsmi_status_t st = t_->amdsmi_get_power_info(h, &p);
+    if (st == AMDSMI_STATUS_SUCCESS) {
+      v[F_POWER_CUR] = u32v(p.current_socket_power);
+      v[F_POWER_AVG] = u32v(p.average_socket_power);
+    } else if (st == AMDSMI_STATUS_NOT_SUPPORTED) {
+      c.power = false;
+    }
+  }
+  if (c.vram && t_->amdsmi_get_gpu_vram_usage) {
+    amdsmi_vram_usage_t vu{};
+    amdsmi_status_t st = t_->amdsmi_get_gpu_vram_usage(h, &vu);
+    if (st == AMDSMI_STATUS_SUCCESS) {
+      any = true;
+      v[F_VRAM_USED] = static_cast<double>(vu.vram_used) * 1048576.0;
+      v[F_VRAM_TOTAL] = static_cast<double>(vu.vram_total) * 1048576.0;
+    } else if (st == AMDSMI_STATUS_NOT_SUPPORTED) {
+      c.vram = false;
+    } else {
+      out->errors++;
+      out->last_error = std::string("vram_usage: ") + smi_status_str(st);
+    }
+  }
+  out->ok = any;
+  out->sample_ns = mono_ns() - t0;
+}
+
+bool AmdSmiBackend::processes(int i, std::vector<ProcSample>* out) {
+  out->clear();
+  if (!caps_[i].procs || !t_->amdsmi_get_gpu_process_list) return false;
+  auto& buf = proc_buf_[i];
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    uint32_t cap = static_cast<uint32_t>(buf.size() / sizeof(amdsmi_proc_info_t));
+    uint32_t n = cap;
+    auto* list = reinterpret_cast<amdsmi_proc_info_t*>(buf.data());
+    amdsmi_status_t st = t_->amdsmi_get_gpu_process_list(handles_[i], &n, list);
+    if (st == AMDSMI_STATUS_OUT_OF_RESOURCES) {
+      buf.resize(sizeof(amdsmi_proc_info_t) * std::max<size_t>(n + 16, cap * 2));
+      continue;
+    }
+    if (st == AMDSMI_STATUS_NOT_SUPPORTED) {
+      caps_[i].procs = false;
+      return false;
+    }
+    if (st != AMDSMI_STATUS_SUCCESS) return false;
+    out->reserve(n);
+    for (uint32_t k = 0; k < n && k < cap; ++k) {
+      const amdsmi_proc_info_t& p = list[k];
+      ProcSample ps;
+      ps.pid = p.pid;
+      ps.name.assign(p.name, strnlen(p.name, sizeof p.name));
+      if (ps.name == "N/A") ps.name.clear();
+      ps.mem_bytes = static_cast<double>(p.mem);
+      ps.vram_bytes = static_cast<double>(p.memory_usage.vram_mem);
+      ps.gtt_bytes = static_cast<double>(p.memory_usage.gtt_mem);
+      ps.cpu_bytes = static_cast<double>(p.memory_usage.cpu_mem);
+      ps.gfx_ns = p.engine_usage.gfx;
+      ps.has_gfx_ns = true;
+      ps.cu_occupancy = ok32(p.cu_occupancy) ? static_cast<double>(p.cu_occupancy) : kNaN;
+      out->push_back(std::move(ps));
+    }
+    return true;
+  }
+  return false;
+}
+
+bool AmdSmiBackend::supports_links() const { return t_ && t_->amdsmi_get_link_metrics; }
+
+void AmdSmiBackend::sample_links(int i, DeviceSample* out) {
+  if (!caps_[i].links || !t_->amdsmi_get_link_metrics) return;
+  amdsmi_link_metrics_t lm;
+  memset(&lm, 0, sizeof lm);
+  amdsmi_status_t st = t_->amdsmi_get_link_metrics(handles_[i], &lm);
+  if (st == AMDSMI_STATUS_NOT_SUPPORTED) {
+    caps_[i].links = false;
+    return;
+  }
+  if (st != AMDSMI_STATUS_SUCCESS) return;
+  int n = std::min<int>(static_cast<int>(lm.num_links), kMaxLinks);
+  for (int k = 0; k < n; ++k) {
+    auto& L = out->links[k];
+    const auto& s = lm.links[k];
+    L.peer_bdf = s.bdf.as_uint == ~0ull ? "" : bdf_str(s.bdf);
+    if (L.peer_bdf.rfind("ffffffffffff", 0) == 0) L.peer_bdf.clear();
+    L.bit_rate_gbps = ok32(s.bit_rate) ? s.bit_rate : kNaN;
+    L.max_bandwidth_gbps = ok32(s.max_bandwidth) ? s.max_bandwidth : kNaN;
+    L.link_type = static_cast<int>(s.link_type);
+  }
+  if (n > out->n_links) out->n_links = n;
+}
+
+}  // namespace gpumon

@@ -1,0 +1,149 @@
+// Device backends: where samples come from.
+//
+// Reference equivalent: the nvidia-smi CLI subprocesses (/root/reference/gpu.py:104-116) behind
+// the commandexists() probe (gpu.py:28-33,260). Here a backend is an in-process C++ object:
+//   - AmdSmiBackend: libamd_smi resolved at run time through SmiTable (dlopen; the role the
+//     vendored libltdl.so.7 played for the reference's docker CLI).
+//   - MockBackend:   N scripted fake GPUs for CPU tests, benches and fault injection.
+#pragma once
+
+#include <atomic>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "sample.h"
+
+namespace gpumon {
+
+class Backend {
+ public:
+  virtual ~Backend() = default;
+  virtual std::string name() const = 0;
+  // (Re)initialise; returns false with *err set if the device layer is unavailable.
+  virtual bool init(std::string* err) = 0;
+  virtual void shutdown() {}
+  virtual int device_count() const = 0;
+  virtual const DeviceStatic& static_info(int i) const = 0;
+  // Fill one device sample. Must not throw; failures are reported in out->ok / errors.
+  virtual void sample(int i, DeviceSample* out) = 0;
+  // GPU processes on device i. Returns false if the call failed.
+  virtual bool processes(int i, std::vector<ProcSample>* out) = 0;
+  // Optional: per-link metrics are expensive (~1 ms); sampled every `link_every` ticks.
+  virtual bool supports_links() const { return false; }
+  virtual void sample_links(int, DeviceSample*) {}
+  // Restrict to a subset of device hip_ids (empty = all). Applied at init().
+  void set_device_filter(const std::vector<int>& ids) { filter_ = ids; }
+
+ protected:
+  std::vector<int> filter_;
+  bool keep(int hip_id) const {
+    if (filter_.empty()) return true;
+    for (int x : filter_)
+      if (x == hip_id) return true;
+    return false;
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Mock backend
+// ---------------------------------------------------------------------------------------------
+struct MockProc {
+  uint32_t pid = 0;
+  int device = 0;
+  std::string name = "python3";
+  double vram_bytes = 1024.0 * 1024 * 1024;
+  double gfx_share = 0.5;  // fraction of device busy time attributed to this process
+};
+
+struct MockConfig {
+  int gpus = 1;
+  uint64_t seed = 1;
+  std::string mode = "wave";          // "wave" (sinusoid), "const", "idle", "load"
+  double const_util = 50.0;
+  double hang_ms = 0.0;               // sleep inside sample() (watchdog / latency tests)
+  int fail_device = -1;               // device whose sample() fails ...
+  int fail_every = 0;                 // ... every N calls (0 = never); -1 = always
+  std::vector<std::string> unsupported;  // field names forced to NaN, e.g. "temp_edge"
+  std::vector<MockProc> procs;
+  int n_xcd = 8;
+  int n_links = 7;
+  double firmware_hz = 50.0;          // how fast the fake firmware table advances
+};
+
+class MockBackend : public Backend {
+ public:
+  explicit MockBackend(MockConfig cfg);
+  std::string name() const override { return "mock"; }
+  bool init(std::string* err) override;
+  int device_count() const override { return static_cast<int>(devs_.size()); }
+  const DeviceStatic& static_info(int i) const override { return devs_[i]; }
+  void sample(int i, DeviceSample* out) override;
+  bool processes(int i, std::vector<ProcSample>* out) override;
+  bool supports_links() const override { return true; }
+  void sample_links(int i, DeviceSample* out) override;
+
+  // Test controls (thread-safe).
+  void set_util(int dev, double pct);
+  void set_procs(const std::vector<MockProc>& procs);
+  void set_fail(int dev, int every);
+  void set_hang_ms(double ms);
+  uint64_t calls(int dev) const;
+
+ private:
+  MockConfig cfg_;
+  std::vector<DeviceStatic> devs_;
+  mutable std::mutex mu_;
+  std::vector<double> forced_util_;
+  std::vector<uint64_t> calls_;
+  std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_;
+  std::map<std::pair<uint32_t, int>, uint64_t> proc_gfx_ns_;
+  int64_t t0_ns_ = 0;
+  std::vector<int64_t> last_ns_;
+};
+
+// ---------------------------------------------------------------------------------------------
+// amdsmi backend (dlopen'd libamd_smi)
+// ---------------------------------------------------------------------------------------------
+struct SmiTable;  // smi_table.h
+
+class AmdSmiBackend : public Backend {
+ public:
+  explicit AmdSmiBackend(std::string lib_path = "");
+  ~AmdSmiBackend() override;
+  std::string name() const override { return "amdsmi"; }
+  bool init(std::string* err) override;
+  void shutdown() override;
+  int device_count() const override { return static_cast<int>(devs_.size()); }
+  const DeviceStatic& static_info(int i) const override { return devs_[i]; }
+  void sample(int i, DeviceSample* out) override;
+  bool processes(int i, std::vector<ProcSample>* out) override;
+  bool supports_links() const override;
+  void sample_links(int i, DeviceSample* out) override;
+  std::string lib_version() const { return lib_version_; }
+
+ private:
+  std::string lib_path_;
+  std::unique_ptr<SmiTable> t_;
+  bool inited_ = false;
+  std::vector<void*> handles_;
+  std::vector<DeviceStatic> devs_;
+  std::string lib_version_;
+  double energy_res_uj_ = 15.3;  // amdsmi_get_energy_count counter_resolution (MI355X: 15.3 uJ)
+  // Per device: calls that returned NOT_SUPPORTED are not retried.
+  struct Caps {
+    bool metrics = true, vram = true, activity = true, power = true, procs = true, links = true;
+  };
+  std::vector<Caps> caps_;
+  std::vector<std::vector<char>> proc_buf_;  // reusable process-list buffers
+};
+
+std::unique_ptr<Backend> make_backend(const std::string& spec, std::string* err);
+
+// Field-name registry (used by mock "unsupported" lists and tests).
+int field_by_name(const std::string& name);
+const char* field_name(int f);
+
+}  // namespace gpumon

@@ -1,0 +1,52 @@
+// Shared utilities for the gpumon C++ core: clocks, logging, small string helpers.
+//
+// The reference agent (/root/reference/gpu.py:21-22,144,146) logs with bare print() calls and
+// has no time base other than time.sleep(10) (gpu.py:263). Here every component stamps with a
+// monotonic ns clock for rates/latencies and a realtime ns clock for exported timestamps.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace gpumon {
+
+inline int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+inline int64_t wall_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::system_clock::now().time_since_epoch())
+      .count();
+}
+
+enum class LogLevel : int { kDebug = 0, kInfo = 1, kWarn = 2, kError = 3, kOff = 4 };
+
+// Global log threshold; set from config (--log-level). Structured "key=value" lines to stderr.
+extern std::atomic<int> g_log_level;
+
+void log_line(LogLevel lvl, const char* component, const std::string& msg);
+
+#define GPUMON_LOG(lvl, comp, msg)                                              \
+  do {                                                                          \
+    if (static_cast<int>(lvl) >= ::gpumon::g_log_level.load(std::memory_order_relaxed)) \
+      ::gpumon::log_line(lvl, comp, msg);                                       \
+  } while (0)
+
+// Splits on a single character; empty fields kept.
+std::vector<std::string> split(std::string_view s, char sep);
+std::string_view trim(std::string_view s);
+bool starts_with(std::string_view s, std::string_view p);
+bool ends_with(std::string_view s, std::string_view p);
+
+// Reads a whole (small) file; returns false if it cannot be opened.
+bool read_file(const std::string& path, std::string* out, size_t max_bytes = 1 << 20);
+
+}  // namespace gpumon

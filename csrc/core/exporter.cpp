@@ -1,0 +1,615 @@
+#include "exporter.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <functional>
+
+#include "common.h"
+#include "http_client.h"
+
+namespace gpumon {
+
+// ---------------------------------------------------------------------------------------------
+// Small persistent fork-join pool for per-device sampling (amdsmi calls are per-device I/O).
+// ---------------------------------------------------------------------------------------------
+struct Exporter::Pool {
+  explicit Pool(int n) {
+    for (int i = 0; i < n; ++i) th.emplace_back([this] { work(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      quit = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  void run(int n, const std::function<void(int)>& fn) {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      job = &fn;
+      total = n;
+      next = 0;
+      done = 0;
+      ++gen;
+    }
+    cv.notify_all();
+    // the caller participates
+    while (true) {
+      int i;
+      {
+        std::lock_guard<std::mutex> g(mu);
+        if (next >= total) break;
+        i = next++;
+      }
+      fn(i);
+      std::lock_guard<std::mutex> g(mu);
+      if (++done == total) done_cv.notify_all();
+    }
+    std::unique_lock<std::mutex> lk(mu);
+    done_cv.wait(lk, [&] { return done >= total; });
+    job = nullptr;
+  }
+  void work() {
+    uint64_t seen = 0;
+    while (true) {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return quit || (gen != seen && job && next < total); });
+      if (quit) return;
+      seen = gen;
+      while (job && next < total) {
+        int i = next++;
+        const auto* f = job;
+        lk.unlock();
+        (*f)(i);
+        lk.lock();
+        if (++done == total) done_cv.notify_all();
+      }
+    }
+  }
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  const std::function<void(int)>* job = nullptr;
+  int total = 0, next = 0, done = 0;
+  uint64_t gen = 0;
+  bool quit = false;
+};
+
+// ---------------------------------------------------------------------------------------------
+static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
+  // "mock" or "mock:gpus=8,mode=load,n_xcd=8,fail_device=1,fail_every=3,hang_ms=5,unsupported=a;b"
+  size_t colon = spec.find(':');
+  if (colon == std::string::npos) return base;
+  for (const auto& kv : split(spec.substr(colon + 1), ',')) {
+    size_t eq = kv.find('=');
+    if (eq == std::string::npos) continue;
+    std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
+    if (k == "gpus") base.gpus = atoi(v.c_str());
+    else if (k == "mode") base.mode = v;
+    else if (k == "const_util") base.const_util = atof(v.c_str());
+    else if (k == "n_xcd") base.n_xcd = atoi(v.c_str());
+    else if (k == "n_links") base.n_links = atoi(v.c_str());
+    else if (k == "fail_device") base.fail_device = atoi(v.c_str());
+    else if (k == "fail_every") base.fail_every = atoi(v.c_str());
+    else if (k == "hang_ms") base.hang_ms = atof(v.c_str());
+    else if (k == "seed") base.seed = strtoull(v.c_str(), nullptr, 10);
+    else if (k == "unsupported") base.unsupported = split(v, ';');
+  }
+  return base;
+}
+
+std::unique_ptr<Backend> make_backend_from_config(const ExporterConfig& cfg, std::string* err) {
+  std::unique_ptr<Backend> b;
+  if (starts_with(cfg.backend, "mock")) {
+    b = std::make_unique<MockBackend>(parse_mock_spec(cfg.backend, cfg.mock));
+  } else if (cfg.backend == "amdsmi" || cfg.backend == "auto") {
+    b = std::make_unique<AmdSmiBackend>(cfg.amdsmi_lib);
+  } else {
+    if (err) *err = "unknown backend '" + cfg.backend + "' (amdsmi | mock[:k=v,...] | auto)";
+    return nullptr;
+  }
+  b->set_device_filter(cfg.devices);
+  return b;
+}
+
+std::unique_ptr<Backend> make_backend(const std::string& spec, std::string* err) {
+  ExporterConfig c;
+  c.backend = spec;
+  return make_backend_from_config(c, err);
+}
+
+// ---------------------------------------------------------------------------------------------
+Exporter::Exporter(ExporterConfig cfg)
+    : cfg_(std::move(cfg)),
+      attr_(std::make_unique<Attributor>(cfg_.attribution)),
+      sample_hist_(latency_buckets()),
+      scrape_hist_(latency_buckets()) {
+  if (cfg_.host.empty()) cfg_.host = "no_name";
+}
+
+Exporter::~Exporter() { stop(); }
+
+bool Exporter::ensure_backend() {
+  if (backend_up_) return true;
+  int64_t now = mono_ns();
+  if (now < next_init_ns_) return false;
+  next_init_ns_ = now + static_cast<int64_t>(cfg_.init_retry_s * 1e9);
+  std::string err;
+  if (!backend_) backend_ = make_backend_from_config(cfg_, &err);
+  if (!backend_ || !backend_->init(&err)) {
+    if (err != backend_err_)
+      GPUMON_LOG(LogLevel::kError, "exporter", "backend init failed: " + err);
+    backend_err_ = err;
+    return false;
+  }
+  backend_err_.clear();
+  std::vector<DeviceStatic> st;
+  for (int i = 0; i < backend_->device_count(); ++i) st.push_back(backend_->static_info(i));
+  {
+    std::lock_guard<std::mutex> g(state_mu_);
+    statics_ = st;
+    prev_.assign(st.size(), DeviceSample{});
+    cur_.assign(st.size(), DeviceSample{});
+    rates_.assign(st.size(), DeviceRates{});
+    dev_errors_.assign(st.size(), 0);
+    proc_counts_.assign(st.size(), 0);
+  }
+  if (cfg_.sample_threads > 0 && !pool_) pool_ = std::make_unique<Pool>(cfg_.sample_threads);
+  backend_up_ = true;
+  GPUMON_LOG(LogLevel::kInfo, "exporter",
+             "backend " + backend_->name() + " up with " + std::to_string(st.size()) + " GPU(s)");
+  return true;
+}
+
+bool Exporter::start(std::string* err) {
+  if (running_) return true;
+  if (!ensure_backend() && cfg_.backend != "auto" && !starts_with(cfg_.backend, "mock")) {
+    // explicit amdsmi: keep running (retry with backoff) but report the error to the caller
+    if (err) *err = backend_err_;
+  }
+  if (!backend_up_ && starts_with(cfg_.backend, "mock")) {
+    if (err) *err = backend_err_;
+    return false;
+  }
+  if (cfg_.serve_http) {
+    server_ = std::make_unique<HttpServer>(
+        cfg_.listen_addr, cfg_.port, cfg_.http_threads,
+        [this](const HttpRequest& r, HttpResponse* w) { handle_http(r, w); },
+        [this](const std::string& path, double s) {
+          if (path == "/metrics") scrape_hist_.observe(s);
+        });
+    std::string e;
+    if (!server_->start(&e)) {
+      if (err) *err = e;
+      server_.reset();
+      return false;
+    }
+  }
+  running_ = true;
+  // First tick synchronously so /metrics is ready as soon as start() returns.
+  tick();
+  if (cfg_.interval_s > 0) sampler_ = std::thread([this] { sampler_loop(); });
+  if (!cfg_.influx_url.empty()) pusher_ = std::thread([this] { influx_loop(); });
+  return true;
+}
+
+void Exporter::stop() {
+  if (!running_.exchange(false)) return;
+  seq_cv_.notify_all();
+  push_cv_.notify_all();
+  if (sampler_.joinable()) sampler_.join();
+  if (pusher_.joinable()) pusher_.join();
+  if (server_) server_->stop();
+  server_.reset();
+  pool_.reset();
+  if (backend_) backend_->shutdown();
+  backend_up_ = false;
+}
+
+void Exporter::sampler_loop() {
+  const int64_t period = static_cast<int64_t>(cfg_.interval_s * 1e9);
+  int64_t next = mono_ns() + period;
+  while (running_) {
+    int64_t now = mono_ns();
+    if (now < next) {
+      // sleep in short slices so stop() is prompt
+      int64_t left = next - now;
+      std::this_thread::sleep_for(std::chrono::nanoseconds(std::min<int64_t>(left, 50000000)));
+      continue;
+    }
+    tick();
+    next += period;
+    int64_t after = mono_ns();
+    if (after > next) {
+      // overran: skip missed slots, stay on the grid (deadline-based, unlike gpu.py:263)
+      int64_t missed = (after - next) / period + 1;
+      overruns_ += static_cast<uint64_t>(missed);
+      next += missed * period;
+    }
+  }
+}
+
+void Exporter::sample_devices(std::vector<DeviceSample>* out) {
+  int n = backend_->device_count();
+  out->resize(n);
+  bool links_tick = backend_->supports_links() && cfg_.link_every > 0 &&
+                    (ticks_.load() % static_cast<uint64_t>(cfg_.link_every) == 0);
+  auto one = [&](int i) {
+    backend_->sample(i, &(*out)[i]);
+    if (links_tick) backend_->sample_links(i, &(*out)[i]);
+  };
+  if (pool_ && n > 1) pool_->run(n, one);
+  else
+    for (int i = 0; i < n; ++i) one(i);
+}
+
+void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
+                              const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows) {
+  rows->clear();
+  std::vector<uint32_t> alive;
+  std::unordered_map<ProcKey, ProcPrev, ProcKeyHash> next_prev;
+  // (ns, pod, container, dev) with an active process -> suppress the idle row for it
+  std::vector<std::tuple<std::string, std::string, std::string, int>> active;
+  for (size_t d = 0; d < procs.size(); ++d) {
+    double dev_util = d < samples.size() ? samples[d].v[F_GFX_UTIL] : kNaN;
+    for (const auto& p : procs[d]) {
+      alive.push_back(p.pid);
+      ProcIdentity id = attr_->resolve(p.pid);
+      // per-process gfx util from engine_usage.gfx ns deltas
+      double util = kNaN;
+      int64_t now = mono_ns();
+      if (p.has_gfx_ns) {
+        ProcKey k{p.pid, static_cast<int>(d)};
+        auto it = proc_prev_.find(k);
+        if (it != proc_prev_.end() && it->second.starttime == id.starttime &&
+            p.gfx_ns >= it->second.gfx_ns && now > it->second.t_ns)
+          util = std::min(100.0, (p.gfx_ns - it->second.gfx_ns) * 100.0 / (now - it->second.t_ns));
+        next_prev[k] = ProcPrev{p.gfx_ns, now, id.starttime};
+      }
+      if (!id.opted_in) continue;
+      PodRow r;
+      r.dev = static_cast<int>(d);
+      r.idle = false;
+      r.pid = std::to_string(p.pid);
+      std::string name = !p.name.empty() ? p.name : id.comm;
+      // reference strips spaces from process names (gpu.py:203); keep them but escape properly
+      r.procname = name.empty() ? "-" : name;
+      r.pod_namespace = id.pod_namespace;
+      r.pod_name = id.pod_name;
+      r.container = id.container_name.empty() ? "-" : id.container_name;
+      r.containerid = id.container_id.empty() ? "-" : id.container_id.substr(0, 12);
+      r.user_name = id.user_name;
+      r.used_memory_bytes = has(p.vram_bytes) ? p.vram_bytes : (has(p.mem_bytes) ? p.mem_bytes : 0);
+      r.gpu_util = has(dev_util) ? dev_util : 0;
+      r.proc_gfx_util = util;
+      r.cu_occupancy = p.cu_occupancy;
+      active.emplace_back(r.pod_namespace, r.pod_name, r.container, r.dev);
+      rows->push_back(std::move(r));
+    }
+  }
+  proc_prev_.swap(next_prev);
+  attr_->gc(alive);
+  // Allocated-but-idle GPUs (reference gpu.py:220-253 via `docker exec nvidia-smi -L`; here the
+  // kubelet PodResources allocation list pushed by the control plane).
+  for (const auto& a : attr_->allocations()) {
+    if (a.gpu_index < 0 || a.gpu_index >= static_cast<int>(procs.size())) continue;  // Q5
+    if (!attr_->opted_in(a.labels)) continue;
+    std::string ns = a.pod_namespace.empty() ? "-" : a.pod_namespace;
+    std::string pod = a.pod_name.empty() ? "-" : a.pod_name;
+    std::string ctr = a.container_name.empty() ? "-" : a.container_name;
+    bool busy = false;
+    for (const auto& t : active)
+      if (std::get<0>(t) == ns && std::get<1>(t) == pod && std::get<3>(t) == a.gpu_index &&
+          (std::get<2>(t) == ctr || std::get<2>(t) == "-")) {
+        busy = true;
+        break;
+      }
+    if (busy) continue;
+    PodRow r;
+    r.dev = a.gpu_index;
+    r.idle = true;
+    r.pod_namespace = ns;
+    r.pod_name = pod;
+    r.container = ctr;
+    r.containerid = a.container_id.empty() ? "-" : a.container_id.substr(0, 12);
+    r.user_name = !a.user_name.empty() ? a.user_name : attr_->derive_user(pod, a.labels);
+    r.used_memory_bytes = 0;
+    r.gpu_util = 0;
+    rows->push_back(std::move(r));
+  }
+}
+
+TickInfo Exporter::tick() {
+  std::lock_guard<std::mutex> tl(tick_mu_);
+  TickInfo info;
+  int64_t t0 = mono_ns();
+  std::vector<DeviceSample> cur;
+  std::vector<DeviceRates> rates;
+  std::vector<std::vector<ProcSample>> procs;
+  std::vector<PodRow> rows;
+  std::vector<DeviceStatic> statics;
+  std::vector<size_t> proc_counts;
+  bool up = ensure_backend();
+  if (up) {
+    {
+      std::lock_guard<std::mutex> g(state_mu_);
+      statics = statics_;
+    }
+    sample_devices(&cur);
+    int n = static_cast<int>(cur.size());
+    rates.resize(n);
+    procs.resize(n);
+    proc_counts.assign(n, 0);
+    std::vector<DeviceSample> prev;
+    {
+      std::lock_guard<std::mutex> g(state_mu_);
+      prev = cur_;  // the previous tick's samples
+    }
+    for (int i = 0; i < n; ++i) {
+      DeviceSample& s = cur[i];
+      if (i < static_cast<int>(prev.size())) {
+        const DeviceSample& p = prev[i];
+        // keep link identity (peer bdf, max bw) between link refreshes
+        for (int k = 0; k < kMaxLinks; ++k) {
+          if (s.links[k].peer_bdf.empty()) s.links[k].peer_bdf = p.links[k].peer_bdf;
+          if (!has(s.links[k].max_bandwidth_gbps))
+            s.links[k].max_bandwidth_gbps = p.links[k].max_bandwidth_gbps;
+          if (s.links[k].link_type < 0) s.links[k].link_type = p.links[k].link_type;
+        }
+        if (s.ok && p.ok && s.acc.firmware_ts && s.acc.firmware_ts == p.acc.firmware_ts) {
+          s.fresh = false;
+          stale_++;
+        }
+        compute_rates(p, s, cfg_.rates, &rates[i]);
+      }
+      samples_++;
+      if (!s.ok) {
+        std::lock_guard<std::mutex> g(state_mu_);
+        if (i < static_cast<int>(dev_errors_.size())) dev_errors_[i] += std::max<uint32_t>(1, s.errors);
+      } else {
+        info.devices_ok++;
+      }
+      if (cfg_.processes && s.ok) {
+        backend_->processes(i, &procs[i]);
+        proc_counts[i] = procs[i].size();
+      }
+    }
+    build_pod_rows(procs, cur, &rows);
+    info.devices = n;
+  }
+
+  SelfStats self = self_stats();
+  std::vector<ExtraSeries> extras;
+  {
+    std::lock_guard<std::mutex> g(extra_mu_);
+    for (const auto& [src, v] : extras_) extras.insert(extras.end(), v.begin(), v.end());
+  }
+  self.pods_attributed = rows.size();
+  RenderInput in;
+  in.host = cfg_.host;
+  static const std::vector<DeviceStatic> kNoStatics;
+  static const std::vector<DeviceSample> kNoSamples;
+  in.statics = up ? &statics : &kNoStatics;
+  in.samples = up ? &cur : &kNoSamples;
+  in.rates = &rates;
+  in.pod_rows = &rows;
+  in.proc_counts = &proc_counts;
+  in.extras = &extras;
+  in.self = &self;
+  in.compat_families = cfg_.compat_families;
+  in.extended_families = cfg_.extended_families;
+  auto snap = std::make_shared<Snapshot>();
+  snap->body.reserve(64 * 1024);
+  render_prometheus(in, &snap->body);
+  if (cfg_.gzip) gzip_compress(snap->body, &snap->body_gz, 1);
+  snap->wall_ns = wall_ns();
+  std::string influx;
+  if (!cfg_.influx_url.empty() && cfg_.influx_every > 0 &&
+      ticks_.load() % static_cast<uint64_t>(cfg_.influx_every) == 0) {
+    render_influx(in, snap->wall_ns, cfg_.influx_extended, &influx);
+  }
+  {
+    std::lock_guard<std::mutex> g(state_mu_);
+    if (up) {
+      prev_.swap(cur_);
+      cur_ = cur;
+      rates_ = rates;
+      rows_ = rows;
+      proc_counts_ = proc_counts;
+    }
+  }
+  info.pod_rows = rows.size();
+  info.body_bytes = snap->body.size();
+  uint64_t s = seq_.load() + 1;
+  snap->seq = s;
+  store_.publish(std::move(snap));
+  ticks_++;
+  last_tick_wall_ns_ = wall_ns();
+  last_tick_mono_ns_ = mono_ns();
+  info.duration_s = (mono_ns() - t0) * 1e-9;
+  sample_hist_.observe(info.duration_s);
+  info.seq = s;
+  {
+    std::lock_guard<std::mutex> g(seq_mu_);
+    seq_ = s;
+  }
+  seq_cv_.notify_all();
+  if (!influx.empty()) {
+    std::lock_guard<std::mutex> g(push_mu_);
+    last_influx_ = influx;
+    if (push_q_.size() >= 60) {
+      push_q_.pop_front();
+      influx_dropped_++;
+    }
+    push_q_.push_back(std::move(influx));
+    push_cv_.notify_one();
+  }
+  return info;
+}
+
+bool Exporter::wait_for_seq(uint64_t want, double timeout_s) {
+  std::unique_lock<std::mutex> lk(seq_mu_);
+  return seq_cv_.wait_for(lk, std::chrono::duration<double>(timeout_s),
+                          [&] { return seq_.load() >= want || !running_; }) &&
+         seq_.load() >= want;
+}
+
+void Exporter::influx_loop() {
+  Url u = parse_url(cfg_.influx_url);
+  if (!u.ok) {
+    GPUMON_LOG(LogLevel::kError, "influx", "unsupported INFLUXDB_URL " + cfg_.influx_url);
+    return;
+  }
+  HttpClient client(cfg_.influx_timeout_s);
+  while (running_) {
+    std::string body;
+    {
+      std::unique_lock<std::mutex> lk(push_mu_);
+      push_cv_.wait_for(lk, std::chrono::milliseconds(200), [&] { return !push_q_.empty() || !running_; });
+      if (!running_) break;
+      if (push_q_.empty()) continue;
+      body = std::move(push_q_.front());
+      push_q_.pop_front();
+    }
+    std::string err, resp;
+    int st = client.request("POST", u, body, "Content-Type: text/plain; charset=utf-8\r\n", &resp, &err);
+    if (st >= 200 && st < 300) {
+      influx_ok_++;
+    } else {
+      influx_fail_++;
+      GPUMON_LOG(LogLevel::kWarn, "influx",
+                 "push failed: " + (st < 0 ? err : ("HTTP " + std::to_string(st) + " " + resp.substr(0, 200))));
+    }
+  }
+}
+
+bool Exporter::healthy() const {
+  if (!running_) return false;
+  double stale = cfg_.health_stale_s > 0 ? cfg_.health_stale_s
+                                         : std::max(3.0 * cfg_.interval_s, 10.0);
+  int64_t last = last_tick_mono_ns_.load();
+  if (cfg_.interval_s <= 0) return last != 0;
+  return last != 0 && (mono_ns() - last) * 1e-9 < stale;
+}
+
+void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
+  if (req.path == "/metrics") {
+    auto s = store_.get();
+    if (!s) {
+      resp->status = 503;
+      resp->inline_body = "no sample yet\n";
+      return;
+    }
+    resp->content_type = "text/plain; version=0.0.4; charset=utf-8";
+    if (req.accept_gzip && !s->body_gz.empty()) {
+      resp->extra_headers = "Content-Encoding: gzip\r\n";
+      resp->data = s->body_gz.data();
+      resp->len = s->body_gz.size();
+    } else {
+      resp->data = s->body.data();
+      resp->len = s->body.size();
+    }
+    resp->owner = s;
+    return;
+  }
+  if (req.path == "/healthz" || req.path == "/livez") {
+    bool ok = healthy();
+    resp->status = ok ? 200 : 503;
+    resp->inline_body = ok ? "ok\n" : "sampler stalled\n";
+    return;
+  }
+  if (req.path == "/readyz") {
+    bool ok = ready() && backend_up_;
+    resp->status = ok ? 200 : 503;
+    resp->inline_body = ok ? "ready\n" : ("not ready: " + backend_err_ + "\n");
+    return;
+  }
+  if (req.path == "/" || req.path.empty()) {
+    resp->content_type = "text/html; charset=utf-8";
+    resp->inline_body =
+        "<html><head><title>gpumon MI355X exporter</title></head><body><h1>gpumon</h1>"
+        "<p><a href=\"/metrics\">/metrics</a> &middot; <a href=\"/healthz\">/healthz</a> &middot; "
+        "<a href=\"/readyz\">/readyz</a></p></body></html>\n";
+    return;
+  }
+  resp->status = 404;
+  resp->inline_body = "not found\n";
+}
+
+void Exporter::set_extra(const std::string& source, std::vector<ExtraSeries> series) {
+  std::lock_guard<std::mutex> g(extra_mu_);
+  if (series.empty()) extras_.erase(source);
+  else extras_[source] = std::move(series);
+}
+
+std::vector<DeviceStatic> Exporter::statics() const {
+  std::lock_guard<std::mutex> g(state_mu_);
+  return statics_;
+}
+std::vector<DeviceSample> Exporter::samples() const {
+  std::lock_guard<std::mutex> g(state_mu_);
+  return cur_;
+}
+std::vector<DeviceRates> Exporter::rates() const {
+  std::lock_guard<std::mutex> g(state_mu_);
+  return rates_;
+}
+std::vector<PodRow> Exporter::pod_rows() const {
+  std::lock_guard<std::mutex> g(state_mu_);
+  return rows_;
+}
+
+std::string Exporter::render_influx_now() {
+  std::vector<DeviceStatic> st;
+  std::vector<DeviceSample> sm;
+  std::vector<PodRow> rows;
+  {
+    std::lock_guard<std::mutex> g(state_mu_);
+    st = statics_;
+    sm = cur_;
+    rows = rows_;
+  }
+  RenderInput in;
+  in.host = cfg_.host;
+  in.statics = &st;
+  in.samples = &sm;
+  in.pod_rows = &rows;
+  std::string out;
+  render_influx(in, wall_ns(), cfg_.influx_extended, &out);
+  return out;
+}
+
+SelfStats Exporter::self_stats() const {
+  SelfStats s;
+  s.version = cfg_.version;
+  s.backend = backend_ ? backend_->name() : cfg_.backend;
+  if (auto* a = dynamic_cast<AmdSmiBackend*>(backend_.get())) s.backend_version = a->lib_version();
+  s.backend_up = backend_up_;
+  s.ticks = ticks_;
+  s.samples = samples_;
+  s.stale_samples = stale_;
+  s.overruns = overruns_;
+  s.last_tick_wall_s = last_tick_wall_ns_.load() * 1e-9;
+  s.interval_s = cfg_.interval_s;
+  sample_hist_.snapshot(&s.sample_hist.bounds, &s.sample_hist.counts, &s.sample_hist.count,
+                        &s.sample_hist.sum);
+  scrape_hist_.snapshot(&s.scrape_hist.bounds, &s.scrape_hist.counts, &s.scrape_hist.count,
+                        &s.scrape_hist.sum);
+  s.scrapes = s.scrape_hist.count;
+  s.http_connections = server_ ? server_->connections() : 0;
+  s.attribution_cache_hits = attr_->cache_hits();
+  s.attribution_cache_misses = attr_->cache_misses();
+  s.influx_ok = influx_ok_;
+  s.influx_fail = influx_fail_;
+  s.influx_dropped = influx_dropped_;
+  {
+    std::lock_guard<std::mutex> g(state_mu_);
+    s.device_errors = dev_errors_;
+    s.pods_attributed = rows_.size();
+  }
+  return s;
+}
+
+}  // namespace gpumon

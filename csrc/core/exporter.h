@@ -1,0 +1,174 @@
+// Exporter: the sampler loop + snapshot publication + HTTP endpoints + Influx compat push.
+//
+// Reference call stack being replaced (/root/reference/gpu.py:258-263):
+//     while 1: main(); time.sleep(10)
+// where main() forks ~4+2C+P subprocesses and does one blocking HTTP POST per line.
+// Here: a deadline-scheduled sampler thread (default 1 Hz, 10 Hz stress) samples every GPU
+// in-process, attributes processes via /proc, renders Prometheus text + gzip once, and swaps an
+// immutable snapshot that the epoll server hands out. Sampling cost is decoupled from scrapes,
+// so /metrics p99 does not grow with the GPU count.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "attribution.h"
+#include "backend.h"
+#include "http_server.h"
+#include "rates.h"
+#include "render.h"
+#include "snapshot.h"
+
+namespace gpumon {
+
+struct ExporterConfig {
+  std::string backend = "auto";       // auto | amdsmi | mock
+  std::string amdsmi_lib;
+  MockConfig mock;
+  std::vector<int> devices;           // hip_id filter; empty = all
+  double interval_s = 1.0;            // <= 0: no sampler thread (ticks driven by tick())
+  bool serve_http = true;
+  std::string listen_addr = "0.0.0.0";
+  int port = 9400;
+  int http_threads = 2;
+  std::string host = "no_name";       // NODE_NAME (reference fallback "no_name", gpu.py:23-24)
+  bool gzip = true;
+  bool compat_families = true;
+  bool extended_families = true;
+  bool processes = true;
+  int link_every = 30;                // ticks between amdsmi_get_link_metrics refreshes
+  int sample_threads = 0;             // parallel device sampling; 0 = sequential
+  AttributionConfig attribution;
+  RateConfig rates;
+  std::string influx_url;             // INFLUXDB_URL; empty = push disabled
+  bool influx_extended = false;
+  int influx_every = 1;               // ticks per push
+  double influx_timeout_s = 2.0;
+  double init_retry_s = 5.0;
+  double health_stale_s = 0;          // 0 = max(3*interval, 10 s)
+  std::string version = "0.1.0";
+};
+
+struct TickInfo {
+  uint64_t seq = 0;
+  double duration_s = 0;
+  int devices = 0;
+  int devices_ok = 0;
+  size_t pod_rows = 0;
+  size_t body_bytes = 0;
+};
+
+class Exporter {
+ public:
+  explicit Exporter(ExporterConfig cfg);
+  ~Exporter();
+
+  bool start(std::string* err);       // backend init (retried later if it fails) + threads
+  void stop();
+  TickInfo tick();                    // one synchronous tick (manual mode or tests)
+  bool wait_for_seq(uint64_t seq, double timeout_s);  // until a snapshot with seq >= `seq`
+
+  int port() const { return server_ ? server_->port() : -1; }
+  std::shared_ptr<const Snapshot> snapshot() const { return store_.get(); }
+  std::string render_influx_now();    // line protocol of the latest tick (tests / CLI)
+  bool healthy() const;
+  bool ready() const { return store_.get() != nullptr; }
+  uint64_t seq() const { return seq_.load(); }
+
+  // Control-plane inputs.
+  void set_container_meta(std::vector<ContainerMeta> metas) { attr_->set_container_meta(std::move(metas)); }
+  void set_allocations(std::vector<Allocation> a) { attr_->set_allocations(std::move(a)); }
+  void set_extra(const std::string& source, std::vector<ExtraSeries> series);
+  Attributor& attributor() { return *attr_; }
+
+  // Introspection.
+  std::vector<DeviceStatic> statics() const;
+  std::vector<DeviceSample> samples() const;
+  std::vector<DeviceRates> rates() const;
+  std::vector<PodRow> pod_rows() const;
+  SelfStats self_stats() const;
+  Backend* backend() { return backend_.get(); }
+  const ExporterConfig& config() const { return cfg_; }
+  double scrape_quantile(double q) const { return scrape_hist_.quantile(q); }
+  double sample_quantile(double q) const { return sample_hist_.quantile(q); }
+
+ private:
+  void sampler_loop();
+  void influx_loop();
+  bool ensure_backend();
+  void handle_http(const HttpRequest& req, HttpResponse* resp);
+  void sample_devices(std::vector<DeviceSample>* out);
+  void build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
+                      const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows);
+
+  ExporterConfig cfg_;
+  std::unique_ptr<Backend> backend_;
+  std::unique_ptr<Attributor> attr_;
+  std::unique_ptr<HttpServer> server_;
+  SnapshotStore store_;
+  Histogram sample_hist_;
+  Histogram scrape_hist_;
+
+  mutable std::mutex state_mu_;       // guards the "latest" introspection copies below
+  std::vector<DeviceStatic> statics_;
+  std::vector<DeviceSample> prev_, cur_;
+  std::vector<DeviceRates> rates_;
+  std::vector<PodRow> rows_;
+  std::vector<size_t> proc_counts_;
+  std::vector<uint64_t> dev_errors_;
+  std::string last_influx_;
+
+  std::mutex tick_mu_;                // serialises ticks
+  std::mutex extra_mu_;
+  std::map<std::string, std::vector<ExtraSeries>> extras_;
+  struct ProcKey {
+    uint32_t pid;
+    int dev;
+    bool operator==(const ProcKey& o) const { return pid == o.pid && dev == o.dev; }
+  };
+  struct ProcKeyHash {
+    size_t operator()(const ProcKey& k) const { return (static_cast<size_t>(k.pid) << 8) ^ k.dev; }
+  };
+  struct ProcPrev {
+    uint64_t gfx_ns = 0;
+    int64_t t_ns = 0;
+    uint64_t starttime = 0;
+  };
+  std::unordered_map<ProcKey, ProcPrev, ProcKeyHash> proc_prev_;
+
+  std::atomic<bool> running_{false};
+  std::atomic<bool> backend_up_{false};
+  int64_t next_init_ns_ = 0;
+  std::string backend_err_;
+  std::thread sampler_;
+  std::atomic<uint64_t> seq_{0};
+  std::mutex seq_mu_;
+  std::condition_variable seq_cv_;
+  std::atomic<uint64_t> ticks_{0}, samples_{0}, stale_{0}, overruns_{0};
+  std::atomic<int64_t> last_tick_wall_ns_{0}, last_tick_mono_ns_{0};
+
+  // Influx pusher
+  std::thread pusher_;
+  std::mutex push_mu_;
+  std::condition_variable push_cv_;
+  std::deque<std::string> push_q_;
+  std::atomic<uint64_t> influx_ok_{0}, influx_fail_{0}, influx_dropped_{0};
+
+  // parallel sampling pool
+  struct Pool;
+  std::unique_ptr<Pool> pool_;
+};
+
+// "auto": amdsmi if it initialises, else error (never silently mock on a GPU host);
+// "mock" / "mock:gpus=8" etc.
+std::unique_ptr<Backend> make_backend_from_config(const ExporterConfig& cfg, std::string* err);
+
+}  // namespace gpumon

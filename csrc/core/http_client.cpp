@@ -1,0 +1,224 @@
+#include "http_client.h"
+
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <cstring>
+#include <strings.h>
+#include <thread>
+
+#include "common.h"
+
+namespace gpumon {
+
+Url parse_url(const std::string& url) {
+  Url u;
+  std::string s = url;
+  if (starts_with(s, "http://")) s = s.substr(7);
+  else if (s.find("://") != std::string::npos) return u;  // https etc. unsupported
+  size_t slash = s.find('/');
+  std::string hp = slash == std::string::npos ? s : s.substr(0, slash);
+  u.path = slash == std::string::npos ? "/" : s.substr(slash);
+  size_t colon = hp.rfind(':');
+  if (colon != std::string::npos) {
+    u.host = hp.substr(0, colon);
+    u.port = atoi(hp.c_str() + colon + 1);
+  } else {
+    u.host = hp;
+  }
+  u.ok = !u.host.empty() && u.port > 0;
+  return u;
+}
+
+HttpClient::~HttpClient() { close_conn(); }
+
+void HttpClient::close_conn() {
+  if (fd_ >= 0) close(fd_);
+  fd_ = -1;
+}
+
+bool HttpClient::connect_to(const Url& u, std::string* err) {
+  if (fd_ >= 0 && u.host == cur_host_ && u.port == cur_port_) return true;
+  close_conn();
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_UNSPEC;
+  hints.ai_socktype = SOCK_STREAM;
+  std::string port = std::to_string(u.port);
+  int rc = getaddrinfo(u.host.c_str(), port.c_str(), &hints, &res);
+  if (rc != 0 || !res) {
+    *err = std::string("resolve ") + u.host + ": " + gai_strerror(rc);
+    return false;
+  }
+  for (addrinfo* p = res; p; p = p->ai_next) {
+    int fd = socket(p->ai_family, p->ai_socktype | SOCK_CLOEXEC, p->ai_protocol);
+    if (fd < 0) continue;
+    timeval tv;
+    tv.tv_sec = static_cast<long>(timeout_s_);
+    tv.tv_usec = static_cast<long>((timeout_s_ - tv.tv_sec) * 1e6);
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
+    int one = 1;
+    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    if (connect(fd, p->ai_addr, p->ai_addrlen) == 0) {
+      fd_ = fd;
+      break;
+    }
+    close(fd);
+  }
+  freeaddrinfo(res);
+  if (fd_ < 0) {
+    *err = "connect " + u.host + ":" + port + ": " + strerror(errno);
+    return false;
+  }
+  cur_host_ = u.host;
+  cur_port_ = u.port;
+  return true;
+}
+
+static bool send_all(int fd, const char* p, size_t n) {
+  while (n) {
+    ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return false;
+    }
+    p += w;
+    n -= static_cast<size_t>(w);
+  }
+  return true;
+}
+
+int HttpClient::request(const std::string& method, const Url& u, const std::string& body,
+                        const std::string& extra_headers, std::string* resp_body,
+                        std::string* err) {
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    bool reused = fd_ >= 0;
+    if (!connect_to(u, err)) return -1;
+    std::string req = method + " " + u.path + " HTTP/1.1\r\nHost: " + u.host + ":" +
+                      std::to_string(u.port) + "\r\nConnection: keep-alive\r\n" + extra_headers;
+    if (!body.empty() || method == "POST")
+      req += "Content-Length: " + std::to_string(body.size()) + "\r\n";
+    req += "\r\n";
+    if (!send_all(fd_, req.data(), req.size()) || !send_all(fd_, body.data(), body.size())) {
+      close_conn();
+      if (reused) continue;  // stale keep-alive connection: retry once on a fresh one
+      *err = std::string("send: ") + strerror(errno);
+      return -1;
+    }
+    std::string in;
+    char buf[16384];
+    size_t hdr_end = std::string::npos;
+    while (hdr_end == std::string::npos) {
+      ssize_t r = recv(fd_, buf, sizeof buf, 0);
+      if (r <= 0) break;
+      in.append(buf, static_cast<size_t>(r));
+      hdr_end = in.find("\r\n\r\n");
+    }
+    if (hdr_end == std::string::npos) {
+      close_conn();
+      if (reused && in.empty()) continue;
+      *err = "no response header";
+      return -1;
+    }
+    int status = 0;
+    if (in.size() > 12) status = atoi(in.c_str() + 9);
+    long clen = -1;
+    bool close_after = false;
+    size_t pos = in.find("\r\n") + 2;
+    while (pos < hdr_end) {
+      size_t e = in.find("\r\n", pos);
+      std::string_view h(in.data() + pos, e - pos);
+      if (h.size() > 15 && strncasecmp(h.data(), "content-length:", 15) == 0)
+        clen = strtol(std::string(h.substr(15)).c_str(), nullptr, 10);
+      if (h.size() > 11 && strncasecmp(h.data(), "connection:", 11) == 0 &&
+          h.find("close") != std::string_view::npos)
+        close_after = true;
+      pos = e + 2;
+    }
+    std::string rb = in.substr(hdr_end + 4);
+    if (clen >= 0) {
+      while (static_cast<long>(rb.size()) < clen) {
+        ssize_t r = recv(fd_, buf, sizeof buf, 0);
+        if (r <= 0) {
+          close_conn();
+          *err = "short body";
+          return -1;
+        }
+        rb.append(buf, static_cast<size_t>(r));
+      }
+    } else if (status != 204 && status != 304) {
+      // no length: read to EOF
+      while (true) {
+        ssize_t r = recv(fd_, buf, sizeof buf, 0);
+        if (r <= 0) break;
+        rb.append(buf, static_cast<size_t>(r));
+      }
+      close_after = true;
+    }
+    if (resp_body) *resp_body = std::move(rb);
+    if (close_after) close_conn();
+    return status;
+  }
+  *err = "request failed";
+  return -1;
+}
+
+ScrapeStats scrape_load(const std::string& host, int port, const std::string& path, int n_requests,
+                        double duration_s, int concurrency, double rate_hz, bool keep_alive,
+                        bool gzip) {
+  ScrapeStats total;
+  concurrency = std::max(1, concurrency);
+  std::atomic<int> issued{0};
+  std::vector<ScrapeStats> per(concurrency);
+  int64_t t0 = mono_ns();
+  int64_t deadline = duration_s > 0 ? t0 + static_cast<int64_t>(duration_s * 1e9) : INT64_MAX;
+  double per_thread_period = rate_hz > 0 ? concurrency / rate_hz : 0.0;
+  std::vector<std::thread> th;
+  Url u;
+  u.host = host;
+  u.port = port;
+  u.path = path;
+  u.ok = true;
+  std::string hdr = gzip ? "Accept-Encoding: gzip\r\n" : "";
+  for (int t = 0; t < concurrency; ++t) {
+    th.emplace_back([&, t] {
+      HttpClient c(5.0);
+      int64_t next = t0 + static_cast<int64_t>(per_thread_period * 1e9 * t / concurrency);
+      while (true) {
+        if (n_requests > 0 && issued.fetch_add(1) >= n_requests) break;
+        if (mono_ns() >= deadline) break;
+        if (per_thread_period > 0) {
+          int64_t now = mono_ns();
+          if (next > now) std::this_thread::sleep_for(std::chrono::nanoseconds(next - now));
+          next += static_cast<int64_t>(per_thread_period * 1e9);
+        }
+        std::string body, err;
+        int64_t a = mono_ns();
+        int st = c.request("GET", u, "", hdr, &body, &err);
+        int64_t b = mono_ns();
+        if (st == 200) {
+          per[t].latencies_s.push_back((b - a) * 1e-9);
+          per[t].bytes += body.size();
+        } else {
+          per[t].errors++;
+        }
+        if (!keep_alive) c.close_conn();
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  total.wall_s = (mono_ns() - t0) * 1e-9;
+  for (auto& p : per) {
+    total.latencies_s.insert(total.latencies_s.end(), p.latencies_s.begin(), p.latencies_s.end());
+    total.errors += p.errors;
+    total.bytes += p.bytes;
+  }
+  return total;
+}
+
+}  // namespace gpumon

@@ -1,0 +1,54 @@
+// Tiny blocking HTTP/1.1 client: Influx compat push (keep-alive POST) and the scrape load
+// generator used by bench.py (p50/p99 /metrics latency measured from the client side, the way a
+// Prometheus server sees it).
+//
+// Reference parity: the reference opens a NEW TCP connection and blocks for every single line it
+// posts (requests.post per line, /root/reference/gpu.py:145,218,252; ~35-40 ms per pod_gpu line,
+// BASELINE.md). Here one batched POST per tick reuses one connection.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace gpumon {
+
+struct Url {
+  std::string host;
+  int port = 80;
+  std::string path = "/";   // including ?query
+  bool ok = false;
+};
+Url parse_url(const std::string& url);
+
+class HttpClient {
+ public:
+  explicit HttpClient(double timeout_s = 2.0) : timeout_s_(timeout_s) {}
+  ~HttpClient();
+  // Returns HTTP status (or -1 on transport error, with *err).
+  int request(const std::string& method, const Url& u, const std::string& body,
+              const std::string& extra_headers, std::string* resp_body, std::string* err);
+  void close_conn();
+
+ private:
+  bool connect_to(const Url& u, std::string* err);
+  int fd_ = -1;
+  std::string cur_host_;
+  int cur_port_ = -1;
+  double timeout_s_;
+};
+
+struct ScrapeStats {
+  std::vector<double> latencies_s;   // successful requests
+  uint64_t errors = 0;
+  uint64_t bytes = 0;
+  double wall_s = 0;
+};
+
+// `concurrency` client threads, each issuing requests back-to-back (or paced to `rate_hz`
+// total when > 0) until `n_requests` total have completed or `duration_s` elapsed.
+ScrapeStats scrape_load(const std::string& host, int port, const std::string& path, int n_requests,
+                        double duration_s, int concurrency, double rate_hz, bool keep_alive,
+                        bool gzip);
+
+}  // namespace gpumon

@@ -1,0 +1,398 @@
+#include "http_server.h"
+
+#include <arpa/inet.h>
+#include <fcntl.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <sys/uio.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstring>
+#include <strings.h>
+#include <unordered_map>
+
+#include "common.h"
+
+namespace gpumon {
+
+namespace {
+
+constexpr size_t kMaxHeader = 16 * 1024;
+constexpr int64_t kIdleTimeoutNs = 60LL * 1000000000LL;
+constexpr size_t kMaxConnsPerLoop = 4096;
+
+const char* status_text(int s) {
+  switch (s) {
+    case 200: return "OK";
+    case 400: return "Bad Request";
+    case 404: return "Not Found";
+    case 405: return "Method Not Allowed";
+    case 431: return "Request Header Fields Too Large";
+    case 503: return "Service Unavailable";
+    default: return "Error";
+  }
+}
+
+struct Conn {
+  int fd = -1;
+  std::string in;
+  std::string head;                       // pending response header
+  std::shared_ptr<const void> owner;      // pending body owner
+  std::string inline_body;
+  const char* body = nullptr;
+  size_t body_len = 0;
+  size_t head_off = 0, body_off = 0;
+  bool writing = false;
+  bool close_after = false;
+  int64_t last_ns = 0;
+  int64_t req_ns = 0;
+  std::string path;
+};
+
+bool set_nonblock(int fd) {
+  int fl = fcntl(fd, F_GETFL, 0);
+  return fl >= 0 && fcntl(fd, F_SETFL, fl | O_NONBLOCK) == 0;
+}
+
+// Parses one request from c->in. Returns bytes consumed (0 = incomplete, -1 = bad, -2 = too big).
+long parse_request(const std::string& in, HttpRequest* r) {
+  size_t end = in.find("\r\n\r\n");
+  if (end == std::string::npos) return in.size() > kMaxHeader ? -2 : 0;
+  size_t le = in.find("\r\n");
+  std::string_view line(in.data(), le);
+  size_t s1 = line.find(' ');
+  if (s1 == std::string_view::npos) return -1;
+  size_t s2 = line.find(' ', s1 + 1);
+  if (s2 == std::string_view::npos) return -1;
+  r->method = std::string(line.substr(0, s1));
+  std::string_view target = line.substr(s1 + 1, s2 - s1 - 1);
+  std::string_view ver = line.substr(s2 + 1);
+  size_t q = target.find('?');
+  r->path = std::string(target.substr(0, q));
+  r->query = q == std::string_view::npos ? "" : std::string(target.substr(q + 1));
+  r->keep_alive = ver == "HTTP/1.1";
+  r->accept_gzip = false;
+  size_t pos = le + 2;
+  long content_len = 0;
+  while (pos < end) {
+    size_t e = in.find("\r\n", pos);
+    if (e == std::string::npos || e > end) e = end;
+    std::string_view h(in.data() + pos, e - pos);
+    size_t colon = h.find(':');
+    if (colon != std::string_view::npos) {
+      std::string_view name = h.substr(0, colon);
+      std::string_view val = trim(h.substr(colon + 1));
+      auto ieq = [](std::string_view a, const char* b) {
+        return a.size() == strlen(b) && strncasecmp(a.data(), b, a.size()) == 0;
+      };
+      if (ieq(name, "connection")) {
+        if (val.size() >= 5 && strncasecmp(val.data(), "close", 5) == 0) r->keep_alive = false;
+        if (val.size() >= 10 && strncasecmp(val.data(), "keep-alive", 10) == 0) r->keep_alive = true;
+      } else if (ieq(name, "accept-encoding")) {
+        std::string v(val);
+        for (auto& ch : v) ch = static_cast<char>(tolower(ch));
+        r->accept_gzip = v.find("gzip") != std::string::npos;
+      } else if (ieq(name, "content-length")) {
+        content_len = strtol(std::string(val).c_str(), nullptr, 10);
+      }
+    }
+    pos = e + 2;
+  }
+  long consumed = static_cast<long>(end + 4);
+  if (content_len > 0) {
+    if (in.size() < static_cast<size_t>(consumed + content_len)) return 0;
+    consumed += content_len;
+  }
+  return consumed;
+}
+
+}  // namespace
+
+struct HttpServer::Loop {
+  int ep = -1;
+  int lfd = -1;
+  int wake = -1;
+  std::thread th;
+  std::unordered_map<int, Conn> conns;
+};
+
+HttpServer::HttpServer(std::string addr, int port, int threads, Handler h, Observer obs)
+    : addr_(std::move(addr)),
+      port_(port),
+      nthreads_(std::max(1, threads)),
+      handler_(std::move(h)),
+      observer_(std::move(obs)) {}
+
+HttpServer::~HttpServer() { stop(); }
+
+bool HttpServer::start(std::string* err) {
+  if (running_) return true;
+  for (int t = 0; t < nthreads_; ++t) {
+    auto L = std::make_unique<Loop>();
+    L->lfd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (L->lfd < 0) {
+      *err = std::string("socket: ") + strerror(errno);
+      return false;
+    }
+    int one = 1;
+    setsockopt(L->lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    setsockopt(L->lfd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+    sockaddr_in sa{};
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons(static_cast<uint16_t>(port_));
+    if (inet_pton(AF_INET, addr_.empty() ? "0.0.0.0" : addr_.c_str(), &sa.sin_addr) != 1) {
+      *err = "bad listen address " + addr_;
+      close(L->lfd);
+      return false;
+    }
+    if (bind(L->lfd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) {
+      *err = "bind " + addr_ + ":" + std::to_string(port_) + ": " + strerror(errno);
+      close(L->lfd);
+      return false;
+    }
+    if (port_ == 0) {
+      socklen_t sl = sizeof sa;
+      getsockname(L->lfd, reinterpret_cast<sockaddr*>(&sa), &sl);
+      port_ = ntohs(sa.sin_port);
+    }
+    if (listen(L->lfd, 1024) != 0) {
+      *err = std::string("listen: ") + strerror(errno);
+      close(L->lfd);
+      return false;
+    }
+    set_nonblock(L->lfd);
+    L->ep = epoll_create1(EPOLL_CLOEXEC);
+    L->wake = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    epoll_event ev{};
+    ev.events = EPOLLIN;
+    ev.data.fd = L->lfd;
+    epoll_ctl(L->ep, EPOLL_CTL_ADD, L->lfd, &ev);
+    ev.data.fd = L->wake;
+    epoll_ctl(L->ep, EPOLL_CTL_ADD, L->wake, &ev);
+    loops_.push_back(std::move(L));
+  }
+  running_ = true;
+  for (auto& L : loops_) {
+    Loop* p = L.get();
+    p->th = std::thread([this, p] { run(p); });
+  }
+  return true;
+}
+
+void HttpServer::stop() {
+  if (!running_.exchange(false)) return;
+  for (auto& L : loops_) {
+    uint64_t one = 1;
+    ssize_t w = write(L->wake, &one, sizeof one);
+    (void)w;
+  }
+  for (auto& L : loops_) {
+    if (L->th.joinable()) L->th.join();
+    for (auto& [fd, c] : L->conns) close(fd);
+    L->conns.clear();
+    close(L->lfd);
+    close(L->ep);
+    close(L->wake);
+  }
+  loops_.clear();
+}
+
+void HttpServer::run(Loop* L) {
+  epoll_event evs[256];
+  int64_t last_sweep = mono_ns();
+  auto close_conn = [&](int fd) {
+    epoll_ctl(L->ep, EPOLL_CTL_DEL, fd, nullptr);
+    close(fd);
+    L->conns.erase(fd);
+    conns_.fetch_sub(1);
+  };
+  auto set_events = [&](int fd, uint32_t e) {
+    epoll_event ev{};
+    ev.events = e;
+    ev.data.fd = fd;
+    epoll_ctl(L->ep, EPOLL_CTL_MOD, fd, &ev);
+  };
+  // Writes pending output; returns false if the connection must be closed.
+  auto flush = [&](Conn& c) -> bool {
+    while (c.head_off < c.head.size() || c.body_off < c.body_len) {
+      iovec iov[2];
+      int n = 0;
+      if (c.head_off < c.head.size()) {
+        iov[n].iov_base = const_cast<char*>(c.head.data() + c.head_off);
+        iov[n].iov_len = c.head.size() - c.head_off;
+        ++n;
+      }
+      if (c.body_off < c.body_len) {
+        iov[n].iov_base = const_cast<char*>(c.body + c.body_off);
+        iov[n].iov_len = c.body_len - c.body_off;
+        ++n;
+      }
+      ssize_t w = writev(c.fd, iov, n);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        if (errno == EAGAIN || errno == EWOULDBLOCK) return true;
+        return false;
+      }
+      size_t ww = static_cast<size_t>(w);
+      size_t hrem = c.head.size() - c.head_off;
+      if (ww <= hrem) {
+        c.head_off += ww;
+      } else {
+        c.head_off = c.head.size();
+        c.body_off += ww - hrem;
+      }
+    }
+    // complete
+    if (observer_ && c.req_ns) observer_(c.path, (mono_ns() - c.req_ns) * 1e-9);
+    c.writing = false;
+    c.owner.reset();
+    c.inline_body.clear();
+    c.body = nullptr;
+    c.body_len = 0;
+    c.head.clear();
+    c.head_off = c.body_off = 0;
+    c.req_ns = 0;
+    return !c.close_after;
+  };
+  // Parses and answers as many complete requests as are buffered (pipelining).
+  auto serve = [&](Conn& c) -> bool {
+    while (!c.writing) {
+      HttpRequest req;
+      long used = parse_request(c.in, &req);
+      if (used == 0) return true;
+      HttpResponse resp;
+      if (used < 0) {
+        resp.status = used == -2 ? 431 : 400;
+        resp.inline_body = status_text(resp.status);
+        req.keep_alive = false;
+        used = static_cast<long>(c.in.size());
+      } else if (req.method != "GET" && req.method != "HEAD") {
+        resp.status = 405;
+        resp.inline_body = "method not allowed\n";
+        req.keep_alive = false;
+      } else {
+        handler_(req, &resp);
+      }
+      requests_.fetch_add(1, std::memory_order_relaxed);
+      c.req_ns = mono_ns();
+      c.path = req.path;
+      c.in.erase(0, static_cast<size_t>(used));
+      const char* body = resp.data;
+      size_t blen = resp.len;
+      if (!body) {
+        c.inline_body = std::move(resp.inline_body);
+        body = c.inline_body.data();
+        blen = c.inline_body.size();
+      } else {
+        c.owner = resp.owner;
+      }
+      c.head.reserve(256);
+      c.head = "HTTP/1.1 ";
+      c.head += std::to_string(resp.status);
+      c.head += ' ';
+      c.head += status_text(resp.status);
+      c.head += "\r\nContent-Type: ";
+      c.head += resp.content_type;
+      c.head += "\r\nContent-Length: ";
+      c.head += std::to_string(blen);
+      c.head += "\r\n";
+      c.head += resp.extra_headers;
+      c.head += req.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
+      c.body = req.method == "HEAD" ? nullptr : body;
+      c.body_len = req.method == "HEAD" ? 0 : blen;
+      c.close_after = !req.keep_alive;
+      c.writing = true;
+      if (!flush(c)) return false;
+      if (c.writing) {
+        set_events(c.fd, EPOLLOUT | EPOLLRDHUP);
+        return true;
+      }
+    }
+    return true;
+  };
+
+  while (running_.load(std::memory_order_relaxed)) {
+    int n = epoll_wait(L->ep, evs, 256, 1000);
+    int64_t now = mono_ns();
+    for (int i = 0; i < n; ++i) {
+      int fd = evs[i].data.fd;
+      if (fd == L->wake) continue;
+      if (fd == L->lfd) {
+        while (true) {
+          int cfd = accept4(L->lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+          if (cfd < 0) break;
+          if (L->conns.size() >= kMaxConnsPerLoop) {
+            close(cfd);
+            continue;
+          }
+          int one = 1;
+          setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+          Conn c;
+          c.fd = cfd;
+          c.last_ns = now;
+          L->conns.emplace(cfd, std::move(c));
+          conns_.fetch_add(1);
+          epoll_event ev{};
+          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.data.fd = cfd;
+          epoll_ctl(L->ep, EPOLL_CTL_ADD, cfd, &ev);
+        }
+        continue;
+      }
+      auto it = L->conns.find(fd);
+      if (it == L->conns.end()) continue;
+      Conn& c = it->second;
+      c.last_ns = now;
+      if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+        close_conn(fd);
+        continue;
+      }
+      if (c.writing) {
+        if (evs[i].events & EPOLLOUT) {
+          if (!flush(c)) {
+            close_conn(fd);
+            continue;
+          }
+          if (!c.writing) {
+            set_events(fd, EPOLLIN | EPOLLRDHUP);
+            if (!serve(c)) close_conn(fd);
+          }
+        }
+        continue;
+      }
+      bool peer_closed = false;
+      if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) {
+        char buf[8192];
+        while (true) {
+          ssize_t r = read(fd, buf, sizeof buf);
+          if (r > 0) {
+            c.in.append(buf, static_cast<size_t>(r));
+            if (c.in.size() > kMaxHeader * 4) break;
+            continue;
+          }
+          if (r == 0) peer_closed = true;
+          else if (errno == EINTR) continue;
+          break;
+        }
+      }
+      if (!serve(c)) {
+        close_conn(fd);
+        continue;
+      }
+      if (peer_closed && !c.writing) close_conn(fd);
+    }
+    if (now - last_sweep > 1000000000LL) {
+      last_sweep = now;
+      std::vector<int> idle;
+      for (auto& [fd, c] : L->conns)
+        if (now - c.last_ns > kIdleTimeoutNs) idle.push_back(fd);
+      for (int fd : idle) close_conn(fd);
+    }
+  }
+}
+
+}  // namespace gpumon

@@ -1,0 +1,63 @@
+// Minimal epoll HTTP/1.1 server for /metrics, /healthz, /readyz.
+//
+// The reference has no server (push-only). This one is built for flat scrape latency: responses
+// reference immutable pre-rendered buffers (zero-copy writev), keep-alive and pipelining are
+// supported, gzip is pre-computed once per tick, and N event-loop threads share the port via
+// SO_REUSEPORT. No Python / GIL on this path.
+#pragma once
+
+#include <atomic>
+#include <functional>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace gpumon {
+
+struct HttpRequest {
+  std::string method;
+  std::string path;        // without query string
+  std::string query;
+  bool keep_alive = true;
+  bool accept_gzip = false;
+};
+
+struct HttpResponse {
+  int status = 200;
+  std::string content_type = "text/plain; charset=utf-8";
+  std::string extra_headers;                // each "Name: value\r\n"
+  std::shared_ptr<const void> owner;        // keeps `data` alive
+  const char* data = nullptr;
+  size_t len = 0;
+  std::string inline_body;                  // used when data == nullptr
+};
+
+class HttpServer {
+ public:
+  using Handler = std::function<void(const HttpRequest&, HttpResponse*)>;
+  using Observer = std::function<void(const std::string& path, double seconds)>;
+
+  HttpServer(std::string addr, int port, int threads, Handler h, Observer obs);
+  ~HttpServer();
+  bool start(std::string* err);
+  void stop();
+  int port() const { return port_; }
+  uint64_t connections() const { return conns_.load(); }
+  uint64_t requests() const { return requests_.load(); }
+
+ private:
+  struct Loop;
+  void run(Loop* L);
+  std::string addr_;
+  int port_;
+  int nthreads_;
+  Handler handler_;
+  Observer observer_;
+  std::vector<std::unique_ptr<Loop>> loops_;
+  std::atomic<bool> running_{false};
+  std::atomic<uint64_t> conns_{0};
+  std::atomic<uint64_t> requests_{0};
+};
+
+}  // namespace gpumon

@@ -1,0 +1,267 @@
+// MockBackend: N scripted fake MI355X devices.
+//
+// The reference has no fake backend and no tests at all; this backend is what
+// lets the whole pipeline (sampler -> attribution -> render -> HTTP) run and be tested on a CPU
+// box: BASELINE config #1 "mock backend, 1 fake GPU, Prometheus /metrics on CPU".
+// Values follow MI355X shapes: 288 GiB HBM3E, 8 XCDs, 7 xGMI peer links, 1400 W limit.
+#include <chrono>
+#include <cmath>
+#include <thread>
+
+#include "backend.h"
+#include "common.h"
+
+namespace gpumon {
+
+static const char* kFieldNames[F_COUNT] = {
+    "gfx_util",      "umc_util",       "mm_util",        "vram_used",      "vram_total",
+    "gtt_used",      "temp_edge",      "temp_hotspot",   "temp_mem",       "temp_vrgfx",
+    "temp_vrsoc",    "temp_vrmem",     "power_cur",      "power_avg",      "power_limit",
+    "energy_j",      "gfxclk_cur",     "gfxclk_avg",     "socclk_cur",     "uclk_cur",
+    "vclk0_cur",     "dclk0_cur",      "throttle_status", "indep_throttle", "fan_rpm",
+    "pcie_width",    "pcie_speed_gts", "pcie_bw_inst",   "pcie_replay",    "pcie_l0_recov",
+    "pcie_nak_sent", "pcie_nak_rcvd",  "volt_soc",       "volt_gfx",       "volt_mem",
+    "xgmi_link_width", "xgmi_link_speed", "vram_max_bw", "num_partition",  "gfxclk_lock"};
+
+int field_by_name(const std::string& name) {
+  for (int i = 0; i < F_COUNT; ++i)
+    if (name == kFieldNames[i]) return i;
+  return -1;
+}
+const char* field_name(int f) { return (f >= 0 && f < F_COUNT) ? kFieldNames[f] : "?"; }
+
+MockBackend::MockBackend(MockConfig cfg) : cfg_(std::move(cfg)) {}
+
+bool MockBackend::init(std::string* err) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (cfg_.gpus < 0 || cfg_.gpus > 64) {
+    if (err) *err = "mock: gpus must be in [0, 64]";
+    return false;
+  }
+  devs_.clear();
+  for (int i = 0; i < cfg_.gpus; ++i) {
+    if (!keep(i)) continue;
+    DeviceStatic d;
+    d.index = static_cast<int>(devs_.size());
+    d.hip_id = i;
+    d.gpu_id = std::to_string(i);
+    char buf[64];
+    snprintf(buf, sizeof buf, "mock-%04x-0000-1000-80d2-%012llx", 0x75a3 + i,
+             static_cast<unsigned long long>(cfg_.seed * 1000 + i));
+    d.uuid = buf;
+    snprintf(buf, sizeof buf, "0000:%02x:00.0", 0x05 + 0x20 * i);
+    d.bdf = buf;
+    d.model = "AMD Instinct MI355 OAM (mock)";
+    d.serial = "MOCK" + std::to_string(i);
+    d.gfx_target = "gfx950";
+    d.compute_partition = "SPX";
+    d.memory_partition = "NPS1";
+    d.driver_version = "mock";
+    d.vram_total_bytes = 294896.0 * 1048576.0;
+    d.power_limit_w = 1400.0;
+    d.num_cu = 256;
+    d.num_xcc = cfg_.n_xcd;
+    d.drm_card = i;
+    d.drm_render = 128 + i;
+    devs_.push_back(d);
+  }
+  size_t n = devs_.size();
+  forced_util_.assign(n, kNaN);
+  calls_.assign(n, 0);
+  energy_.assign(n, 1000000);
+  xgmi_rd_.assign(n * kMaxLinks, 0);
+  xgmi_wr_.assign(n * kMaxLinks, 0);
+  busy_acc_.assign(n * kMaxXcc, 0);
+  acc_counter_.assign(n, 0);
+  t0_ns_ = mono_ns();
+  last_ns_.assign(n, t0_ns_);
+  return true;
+}
+
+void MockBackend::set_util(int dev, double pct) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (dev >= 0 && dev < static_cast<int>(forced_util_.size())) forced_util_[dev] = pct;
+}
+void MockBackend::set_procs(const std::vector<MockProc>& procs) {
+  std::lock_guard<std::mutex> g(mu_);
+  cfg_.procs = procs;
+}
+void MockBackend::set_fail(int dev, int every) {
+  std::lock_guard<std::mutex> g(mu_);
+  cfg_.fail_device = dev;
+  cfg_.fail_every = every;
+}
+void MockBackend::set_hang_ms(double ms) {
+  std::lock_guard<std::mutex> g(mu_);
+  cfg_.hang_ms = ms;
+}
+uint64_t MockBackend::calls(int dev) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return dev >= 0 && dev < static_cast<int>(calls_.size()) ? calls_[dev] : 0;
+}
+
+static double mock_util(const MockConfig& c, int dev, double t) {
+  if (c.mode == "idle") return 0.0;
+  if (c.mode == "load") return 100.0;
+  if (c.mode == "const") return c.const_util;
+  double u = 50.0 + 45.0 * std::sin(0.7 * t + 1.3 * dev);
+  return std::floor(std::max(0.0, std::min(100.0, u)));
+}
+
+void MockBackend::sample(int i, DeviceSample* out) {
+  out->reset();
+  int64_t t0 = mono_ns();
+  double hang;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    hang = cfg_.hang_ms;
+  }
+  if (hang > 0) std::this_thread::sleep_for(std::chrono::microseconds(static_cast<int64_t>(hang * 1000)));
+  std::lock_guard<std::mutex> g(mu_);
+  uint64_t call = ++calls_[i];
+  out->host_mono_ns = mono_ns();
+  out->host_wall_ns = wall_ns();
+  if (cfg_.fail_device == devs_[i].hip_id &&
+      (cfg_.fail_every < 0 || (cfg_.fail_every > 0 && call % static_cast<uint64_t>(cfg_.fail_every) == 0))) {
+    out->ok = false;
+    out->errors = 1;
+    out->last_error = "gpu_metrics: MOCK_INJECTED_FAILURE";
+    out->sample_ns = mono_ns() - t0;
+    return;
+  }
+  double t = (out->host_mono_ns - t0_ns_) * 1e-9;
+  double util = has(forced_util_[i]) ? forced_util_[i] : mock_util(cfg_, devs_[i].hip_id, t);
+  auto& v = out->v;
+  v[F_GFX_UTIL] = util;
+  v[F_UMC_UTIL] = std::floor(util * 0.6);
+  v[F_VRAM_TOTAL] = devs_[i].vram_total_bytes;
+  double used = 283.0 * 1048576.0;
+  for (const auto& p : cfg_.procs)
+    if (p.device == devs_[i].hip_id) used += p.vram_bytes;
+  v[F_VRAM_USED] = used;
+  v[F_GTT_USED] = 23.0 * 1048576.0;
+  v[F_TEMP_HOTSPOT] = 40.0 + util * 0.45;
+  v[F_TEMP_MEM] = 33.0 + util * 0.25;
+  v[F_TEMP_VRSOC] = 38.0 + util * 0.2;
+  double power = 250.0 + util * 11.0;
+  v[F_POWER_CUR] = power;
+  v[F_POWER_LIMIT] = devs_[i].power_limit_w;
+  v[F_GFXCLK_CUR] = util > 0 ? 2100.0 : 95.0;
+  v[F_SOCCLK_CUR] = 1200.0;
+  v[F_UCLK_CUR] = 2000.0;
+  v[F_PCIE_WIDTH] = 16;
+  v[F_PCIE_SPEED_GTS] = 32.0;
+  v[F_PCIE_BW_INST] = 18;
+  v[F_PCIE_REPLAY] = 0;
+  v[F_PCIE_L0_RECOV] = 0;
+  v[F_XGMI_LINK_WIDTH] = 16;
+  v[F_XGMI_LINK_SPEED] = 38;
+  v[F_VRAM_MAX_BW] = 8192;
+  v[F_NUM_PARTITION] = 1;
+  v[F_THROTTLE_STATUS] = 0;
+
+  // Advance accumulators by elapsed time since the previous sample of this device.
+  Accumulators& a = out->acc;
+  a.valid = true;
+  int64_t now = out->host_mono_ns;
+  double elapsed = std::max(0.0, (now - last_ns_[i]) * 1e-9);
+  last_ns_[i] = now;
+  // firmware time advances in quanta of 1/firmware_hz
+  uint64_t fw_tick = static_cast<uint64_t>(t * cfg_.firmware_hz);
+  a.firmware_ts = fw_tick * static_cast<uint64_t>(1e8 / std::max(1.0, cfg_.firmware_hz));
+  a.system_clock_ns = static_cast<uint64_t>(now);
+  energy_[i] += static_cast<uint64_t>(power * elapsed / 15.3e-6);
+  a.energy = energy_[i];
+  a.energy_resolution_uj = 15.3;
+  v[F_ENERGY_J] = static_cast<double>(a.energy) * 15.3e-6;
+  acc_counter_[i] += static_cast<uint64_t>(elapsed * 100000.0);  // 10 us units
+  a.accumulation_counter = acc_counter_[i];
+  a.has_residency = true;
+  a.ppt_res = util > 90 ? acc_counter_[i] / 10 : 0;
+  a.has_activity_acc = true;
+  a.gfx_activity_acc = static_cast<uint64_t>(acc_counter_[i] * util / 100.0);
+  int nx = cfg_.n_xcd;
+  out->n_xcd = nx;
+  a.n_xcd_acc = nx;
+  for (int k = 0; k < nx && k < kMaxXcc; ++k) {
+    double xb = std::max(0.0, std::min(100.0, util + (k - nx / 2) * 0.5));
+    out->xcd_busy[k] = std::floor(xb);
+    busy_acc_[i * kMaxXcc + k] += static_cast<uint64_t>(xb * elapsed * 100.0);
+    a.xcd_busy_acc[k] = busy_acc_[i * kMaxXcc + k];
+    out->gfxclks[k] = v[F_GFXCLK_CUR];
+  }
+  int nl = std::min(cfg_.n_links + 1, kMaxLinks);  // slot 0 = self, as on MI355X
+  out->n_links = nl;
+  a.n_links_acc = nl;
+  for (int k = 0; k < nl; ++k) {
+    if (k > 0) {
+      // ~util% of 64 GB/s per link, in KB
+      uint64_t kb = static_cast<uint64_t>(util / 100.0 * 64e6 * elapsed);
+      xgmi_rd_[i * kMaxLinks + k] += kb;
+      xgmi_wr_[i * kMaxLinks + k] += kb / 2;
+    }
+    a.xgmi_rd_kb[k] = xgmi_rd_[i * kMaxLinks + k];
+    a.xgmi_wr_kb[k] = xgmi_wr_[i * kMaxLinks + k];
+    out->links[k].status = k == 0 ? -1 : 1;
+    out->links[k].bit_rate_gbps = 38;
+  }
+  for (const auto& name : cfg_.unsupported) {
+    int f = field_by_name(name);
+    if (f >= 0) v[f] = kNaN;
+    if (name == "xcd") {
+      out->n_xcd = 0;
+      a.n_xcd_acc = 0;
+    }
+    if (name == "xgmi") {
+      out->n_links = 0;
+      a.n_links_acc = 0;
+    }
+  }
+  out->ok = true;
+  out->sample_ns = mono_ns() - t0;
+}
+
+bool MockBackend::processes(int i, std::vector<ProcSample>* out) {
+  std::lock_guard<std::mutex> g(mu_);
+  out->clear();
+  double util = has(forced_util_[i]) ? forced_util_[i]
+                                     : mock_util(cfg_, devs_[i].hip_id, (mono_ns() - t0_ns_) * 1e-9);
+  for (const auto& p : cfg_.procs) {
+    if (p.device != devs_[i].hip_id) continue;
+    ProcSample ps;
+    ps.pid = p.pid;
+    ps.name = p.name;
+    ps.vram_bytes = p.vram_bytes;
+    ps.mem_bytes = p.vram_bytes;
+    ps.gtt_bytes = 0;
+    ps.cpu_bytes = 0;
+    auto key = std::make_pair(p.pid, i);
+    // gfx ns advance at util * share of wall time
+    uint64_t& ns = proc_gfx_ns_[key];
+    ns += static_cast<uint64_t>(util / 100.0 * p.gfx_share * 1e7);
+    ps.gfx_ns = ns + static_cast<uint64_t>((mono_ns() - t0_ns_) * (util / 100.0) * p.gfx_share);
+    ps.has_gfx_ns = true;
+    ps.cu_occupancy = std::floor(256.0 * util / 100.0 * p.gfx_share);
+    out->push_back(std::move(ps));
+  }
+  return true;
+}
+
+void MockBackend::sample_links(int i, DeviceSample* out) {
+  std::lock_guard<std::mutex> g(mu_);
+  int nl = std::min(cfg_.n_links + 1, kMaxLinks);
+  for (int k = 0; k < nl; ++k) {
+    auto& L = out->links[k];
+    if (k == 0) continue;
+    char buf[32];
+    int peer = (devs_[i].hip_id + k) % std::max(2, cfg_.gpus + 1);
+    snprintf(buf, sizeof buf, "0000:%02x:00.0", 0x05 + 0x20 * peer);
+    L.peer_bdf = buf;
+    L.bit_rate_gbps = 38;
+    L.max_bandwidth_gbps = 608;
+    L.link_type = 2;
+  }
+  if (nl > out->n_links) out->n_links = nl;
+}
+
+}  // namespace gpumon

@@ -1,0 +1,27 @@
+// Accumulator -> rate conversion (energy, throttle residencies, per-XCD busy, xGMI bytes).
+//
+// The reference computes no rates at all: it re-reads instantaneous nvidia-smi values every
+// ~13-19 s (/root/reference/gpu.py:104-109). MI355X firmware exposes monotone
+// accumulators in the gpu_metrics table; rates over the sampling interval are both more accurate
+// than instantaneous values and free (no extra calls). First tick after start/reset: no rate.
+#pragma once
+
+#include "sample.h"
+
+namespace gpumon {
+
+// Counts-per-percent scale of gfx_activity_acc / gfx_busy_acc relative to accumulation_counter.
+// Calibrated on MI355X (see tests/gpu/test_amdsmi_backend.py); overridable for other firmware.
+struct RateConfig {
+  double activity_acc_scale = 1.0;   // avg% = d(acc) / d(accumulation_counter) * scale
+  double xgmi_kb_bytes = 1024.0;     // bytes per xGMI "KB" accumulator unit
+};
+
+// Unsigned delta that tolerates a 32-bit firmware wrap when `bits32` is set; returns false on a
+// backwards step (device reset / driver reload) so the caller skips the rate for this tick.
+bool acc_delta(uint64_t prev, uint64_t cur, bool bits32, uint64_t* out);
+
+void compute_rates(const DeviceSample& prev, const DeviceSample& cur, const RateConfig& cfg,
+                   DeviceRates* out);
+
+}  // namespace gpumon

@@ -1,0 +1,718 @@
+#include "render.h"
+
+#include <charconv>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <set>
+#include <tuple>
+
+namespace gpumon {
+
+// ---------------------------------------------------------------------------------------------
+// formatting helpers
+// ---------------------------------------------------------------------------------------------
+void append_double(double v, std::string* out) {
+  if (std::isnan(v)) {
+    out->append("NaN");
+    return;
+  }
+  if (std::isinf(v)) {
+    out->append(v > 0 ? "+Inf" : "-Inf");
+    return;
+  }
+  char buf[64];
+  // Integral values (the common case: %, MHz, bytes) print without exponent or fraction.
+  if (v == std::floor(v) && std::fabs(v) < 9.007199254740992e15) {
+    auto r = std::to_chars(buf, buf + sizeof buf, static_cast<long long>(v));
+    out->append(buf, r.ptr);
+    return;
+  }
+  auto r = std::to_chars(buf, buf + sizeof buf, v);
+  out->append(buf, r.ptr);
+}
+
+void escape_label_value(const std::string& v, std::string* out) {
+  for (char c : v) {
+    switch (c) {
+      case '\\': out->append("\\\\"); break;
+      case '"': out->append("\\\""); break;
+      case '\n': out->append("\\n"); break;
+      default: out->push_back(c);
+    }
+  }
+}
+
+void escape_influx_tag(const std::string& v, std::string* out) {
+  if (v.empty()) {
+    out->push_back('-');  // empty tag values are invalid in line protocol
+    return;
+  }
+  for (char c : v) {
+    if (c == ',' || c == ' ' || c == '=') out->push_back('\\');
+    if (c == '\n') {
+      out->append("\\n");
+      continue;
+    }
+    out->push_back(c);
+  }
+}
+
+void escape_influx_field_str(const std::string& v, std::string* out) {
+  for (char c : v) {
+    if (c == '"' || c == '\\') out->push_back('\\');
+    if (c == '\n') {
+      out->append("\\n");
+      continue;
+    }
+    out->push_back(c);
+  }
+}
+
+namespace {
+
+using Labels = std::vector<std::pair<const char*, std::string>>;
+
+// A metric family whose header is dropped again if no sample line follows it.
+class Family {
+ public:
+  Family(std::string* o, const char* name, const char* help, const char* type)
+      : o_(o), name_(name), mark_(o->size()) {
+    o_->append("# HELP ").append(name).push_back(' ');
+    o_->append(help).push_back('\n');
+    o_->append("# TYPE ").append(name).push_back(' ');
+    o_->append(type).push_back('\n');
+  }
+  ~Family() {
+    if (!any_) o_->resize(mark_);
+  }
+  // base: preformatted `k="v",...` (may be empty); extra: additional label pairs.
+  void add(const std::string& base, const Labels& extra, double v, const char* suffix = nullptr) {
+    if (std::isnan(v)) return;
+    any_ = true;
+    o_->append(name_);
+    if (suffix) o_->append(suffix);
+    if (!base.empty() || !extra.empty()) {
+      o_->push_back('{');
+      o_->append(base);
+      bool first = base.empty();
+      for (const auto& kv : extra) {
+        if (!first) o_->push_back(',');
+        first = false;
+        o_->append(kv.first).append("=\"");
+        escape_label_value(kv.second, o_);
+        o_->push_back('"');
+      }
+      o_->push_back('}');
+    }
+    o_->push_back(' ');
+    append_double(v, o_);
+    o_->push_back('\n');
+  }
+  void add(const std::string& base, double v) { add(base, Labels{}, v); }
+
+ private:
+  std::string* o_;
+  const char* name_;
+  size_t mark_;
+  bool any_ = false;
+};
+
+std::string label_str(const Labels& l) {
+  std::string s;
+  bool first = true;
+  for (const auto& kv : l) {
+    if (!first) s.push_back(',');
+    first = false;
+    s.append(kv.first).append("=\"");
+    escape_label_value(kv.second, &s);
+    s.push_back('"');
+  }
+  return s;
+}
+
+void histogram(std::string* o, const char* name, const char* help, const HistSnapshot& h,
+               const std::string& base) {
+  o->append("# HELP ").append(name).append(" ").append(help).append("\n");
+  o->append("# TYPE ").append(name).append(" histogram\n");
+  uint64_t cum = 0;
+  for (size_t i = 0; i < h.bounds.size(); ++i) {
+    cum += i < h.counts.size() ? h.counts[i] : 0;
+    o->append(name).append("_bucket{");
+    if (!base.empty()) o->append(base).push_back(',');
+    o->append("le=\"");
+    append_double(h.bounds[i], o);
+    o->append("\"} ");
+    append_double(static_cast<double>(cum), o);
+    o->push_back('\n');
+  }
+  o->append(name).append("_bucket{");
+  if (!base.empty()) o->append(base).push_back(',');
+  o->append("le=\"+Inf\"} ");
+  append_double(static_cast<double>(h.count), o);
+  o->push_back('\n');
+  o->append(name).append("_sum");
+  if (!base.empty()) o->append("{").append(base).append("}");
+  o->push_back(' ');
+  append_double(h.sum, o);
+  o->push_back('\n');
+  o->append(name).append("_count");
+  if (!base.empty()) o->append("{").append(base).append("}");
+  o->push_back(' ');
+  append_double(static_cast<double>(h.count), o);
+  o->push_back('\n');
+}
+
+const double kMiB = 1048576.0;
+
+}  // namespace
+
+void render_prometheus(const RenderInput& in, std::string* o) {
+  const auto& st = *in.statics;
+  const auto& sm = *in.samples;
+  const size_t n = std::min(st.size(), sm.size());
+  std::vector<std::string> dl(n);
+  for (size_t d = 0; d < n; ++d)
+    dl[d] = label_str({{"host", in.host}, {"gpu_id", st[d].gpu_id}, {"gpu_uuid", st[d].uuid},
+                       {"bdf", st[d].bdf}});
+  auto devf = [&](const char* name, const char* help, const char* type, auto get) {
+    Family f(o, name, help, type);
+    for (size_t d = 0; d < n; ++d)
+      if (sm[d].ok) f.add(dl[d], get(d));
+  };
+  const DeviceRates kNoRates;
+  auto rate = [&](size_t d) -> const DeviceRates& {
+    return (in.rates && d < in.rates->size()) ? (*in.rates)[d] : kNoRates;
+  };
+
+  // ---------------- node_gpu (reference measurement, gpu.py:136-143) ----------------
+  if (in.compat_families) {
+    devf("node_gpu_gpu_util", "GPU (gfx) utilization in percent. Reference node_gpu.gpu_util.",
+         "gauge", [&](size_t d) { return sm[d].v[F_GFX_UTIL]; });
+    devf("node_gpu_mem_util", "VRAM used / total in percent. Reference node_gpu.mem_util.", "gauge",
+         [&](size_t d) {
+           double u = sm[d].v[F_VRAM_USED], t = sm[d].v[F_VRAM_TOTAL];
+           return (has(u) && has(t) && t > 0) ? u * 100.0 / t : kNaN;  // Q9 guard
+         });
+    devf("node_gpu_mem_used", "VRAM used in MiB. Reference node_gpu.mem_used.", "gauge",
+         [&](size_t d) { return std::floor(sm[d].v[F_VRAM_USED] / kMiB); });
+    devf("node_gpu_mem_total", "VRAM total in MiB. Reference node_gpu.mem_total.", "gauge",
+         [&](size_t d) { return std::floor(sm[d].v[F_VRAM_TOTAL] / kMiB); });
+    devf("node_gpu_mem_free", "VRAM free in MiB. Reference node_gpu.mem_free.", "gauge",
+         [&](size_t d) {
+           double u = sm[d].v[F_VRAM_USED], t = sm[d].v[F_VRAM_TOTAL];
+           return (has(u) && has(t)) ? std::floor((t - u) / kMiB) : kNaN;
+         });
+    devf("node_gpu_mem_bw_util",
+         "Memory controller (UMC/HBM) activity in percent (reference queried utilization.memory but "
+         "dropped it).",
+         "gauge", [&](size_t d) { return sm[d].v[F_UMC_UTIL]; });
+  }
+
+  // ---------------- MI355X extras ----------------
+  if (in.extended_families) {
+    {
+      Family f(o, "gpu_up", "1 if the last sample of this GPU succeeded.", "gauge");
+      for (size_t d = 0; d < n; ++d) f.add(dl[d], sm[d].ok ? 1.0 : 0.0);
+    }
+    {
+      Family f(o, "gpu_info", "Static GPU identity (value is always 1).", "gauge");
+      for (size_t d = 0; d < n; ++d)
+        f.add(dl[d],
+              {{"model", st[d].model},
+               {"serial", st[d].serial},
+               {"gfx_target", st[d].gfx_target},
+               {"hip_id", std::to_string(st[d].hip_id)},
+               {"drm_card", std::to_string(st[d].drm_card)},
+               {"compute_partition", st[d].compute_partition},
+               {"memory_partition", st[d].memory_partition},
+               {"driver_version", st[d].driver_version}},
+              1.0);
+    }
+    devf("gpu_sample_fresh", "1 if the firmware metrics table advanced since the previous tick.",
+         "gauge", [&](size_t d) { return sm[d].fresh ? 1.0 : 0.0; });
+    devf("gpu_vram_used_bytes", "VRAM (HBM3E) used in bytes.", "gauge",
+         [&](size_t d) { return sm[d].v[F_VRAM_USED]; });
+    devf("gpu_vram_total_bytes", "VRAM (HBM3E) total in bytes.", "gauge",
+         [&](size_t d) { return sm[d].v[F_VRAM_TOTAL]; });
+    devf("gpu_gtt_used_bytes", "GTT (host-mapped) memory used in bytes.", "gauge",
+         [&](size_t d) { return sm[d].v[F_GTT_USED]; });
+    devf("gpu_mm_activity_percent", "Multimedia engine activity in percent.", "gauge",
+         [&](size_t d) { return sm[d].v[F_MM_UTIL]; });
+    devf("gpu_gfx_activity_avg_percent",
+         "GFX activity averaged over the sampling interval (firmware accumulator).", "gauge",
+         [&](size_t d) { return rate(d).gfx_activity_avg_pct; });
+    devf("gpu_umc_activity_avg_percent",
+         "Memory activity averaged over the sampling interval (firmware accumulator).", "gauge",
+         [&](size_t d) { return rate(d).mem_activity_avg_pct; });
+    {
+      Family f(o, "gpu_temperature_celsius", "Temperature in degrees Celsius by sensor.", "gauge");
+      static const std::pair<Field, const char*> kT[] = {
+          {F_TEMP_EDGE, "edge"},   {F_TEMP_HOTSPOT, "hotspot"}, {F_TEMP_MEM, "mem"},
+          {F_TEMP_VRGFX, "vrgfx"}, {F_TEMP_VRSOC, "vrsoc"},     {F_TEMP_VRMEM, "vrmem"}};
+      for (size_t d = 0; d < n; ++d) {
+        if (!sm[d].ok) continue;
+        for (const auto& t : kT) f.add(dl[d], {{"sensor", t.second}}, sm[d].v[t.first]);
+        for (int k = 0; k < kMaxHbm; ++k)
+          f.add(dl[d], {{"sensor", "hbm" + std::to_string(k)}}, sm[d].hbm_temp[k]);
+      }
+    }
+    devf("gpu_power_watts", "Current socket power in watts.", "gauge",
+         [&](size_t d) { return sm[d].v[F_POWER_CUR]; });
+    devf("gpu_power_average_watts", "Firmware-averaged socket power in watts.", "gauge",
+         [&](size_t d) { return sm[d].v[F_POWER_AVG]; });
+    devf("gpu_power_interval_watts",
+         "Socket power averaged over the sampling interval from the energy accumulator.", "gauge",
+         [&](size_t d) { return rate(d).power_from_energy_w; });
+    devf("gpu_power_limit_watts", "Socket power cap in watts.", "gauge",
+         [&](size_t d) { return sm[d].v[F_POWER_LIMIT]; });
+    devf("gpu_energy_joules_total", "Energy consumed since driver load in joules.", "counter",
+         [&](size_t d) { return sm[d].v[F_ENERGY_J]; });
+    {
+      Family f(o, "gpu_clock_mhz", "Current clock frequency in MHz by clock domain.", "gauge");
+      static const std::pair<Field, const char*> kC[] = {{F_GFXCLK_CUR, "gfx"},
+                                                         {F_SOCCLK_CUR, "soc"},
+                                                         {F_UCLK_CUR, "mem"},
+                                                         {F_VCLK0_CUR, "vclk0"},
+                                                         {F_DCLK0_CUR, "dclk0"}};
+      for (size_t d = 0; d < n; ++d) {
+        if (!sm[d].ok) continue;
+        for (const auto& c : kC) f.add(dl[d], {{"clock", c.second}}, sm[d].v[c.first]);
+        f.add(dl[d], {{"clock", "gfx_avg"}}, sm[d].v[F_GFXCLK_AVG]);
+      }
+    }
+    {
+      Family f(o, "gpu_xcd_clock_mhz", "Current gfx clock per XCD (XCC) in MHz.", "gauge");
+      for (size_t d = 0; d < n; ++d)
+        if (sm[d].ok)
+          for (int k = 0; k < kMaxGfxClks; ++k)
+            f.add(dl[d], {{"xcd", std::to_string(k)}}, sm[d].gfxclks[k]);
+    }
+    {
+      Family f(o, "gpu_xcd_busy_percent", "Instantaneous GFX busy per XCD (XCC) in percent.",
+               "gauge");
+      for (size_t d = 0; d < n; ++d)
+        if (sm[d].ok)
+          for (int k = 0; k < sm[d].n_xcd; ++k)
+            f.add(dl[d], {{"xcd", std::to_string(k)}}, sm[d].xcd_busy[k]);
+    }
+    {
+      Family f(o, "gpu_xcd_busy_avg_percent",
+               "GFX busy per XCD averaged over the sampling interval (firmware accumulator).",
+               "gauge");
+      for (size_t d = 0; d < n; ++d) {
+        const auto& r = rate(d);
+        if (sm[d].ok && r.valid)
+          for (int k = 0; k < r.n_xcd; ++k)
+            f.add(dl[d], {{"xcd", std::to_string(k)}}, r.xcd_busy_avg[k]);
+      }
+    }
+    devf("gpu_throttle_status", "Firmware throttle status bitfield.", "gauge",
+         [&](size_t d) { return sm[d].v[F_THROTTLE_STATUS]; });
+    {
+      Family f(o, "gpu_violation_percent",
+               "Share of the interval spent in a power/thermal limit (PVIOL/TVIOL).", "gauge");
+      for (size_t d = 0; d < n; ++d) {
+        const auto& r = rate(d);
+        if (!sm[d].ok || !r.valid) continue;
+        f.add(dl[d], {{"kind", "ppt"}}, r.ppt_violation_pct);
+        f.add(dl[d], {{"kind", "socket_thermal"}}, r.thermal_violation_pct);
+        f.add(dl[d], {{"kind", "prochot"}}, r.prochot_violation_pct);
+        f.add(dl[d], {{"kind", "vr_thermal"}}, r.vr_thm_violation_pct);
+        f.add(dl[d], {{"kind", "hbm_thermal"}}, r.hbm_thm_violation_pct);
+      }
+    }
+    devf("gpu_fan_rpm", "Fan speed in RPM.", "gauge", [&](size_t d) { return sm[d].v[F_FAN_RPM]; });
+    devf("gpu_pcie_link_width", "PCIe link width in lanes.", "gauge",
+         [&](size_t d) { return sm[d].v[F_PCIE_WIDTH]; });
+    devf("gpu_pcie_link_speed_gts", "PCIe link speed in GT/s.", "gauge",
+         [&](size_t d) { return sm[d].v[F_PCIE_SPEED_GTS]; });
+    devf("gpu_pcie_bandwidth_gbytes_per_second", "Instantaneous PCIe bandwidth (firmware) in GB/s.",
+         "gauge", [&](size_t d) { return sm[d].v[F_PCIE_BW_INST]; });
+    devf("gpu_pcie_replay_total", "PCIe replay count.", "counter",
+         [&](size_t d) { return sm[d].v[F_PCIE_REPLAY]; });
+    devf("gpu_pcie_recovery_total", "PCIe L0-to-recovery transitions.", "counter",
+         [&](size_t d) { return sm[d].v[F_PCIE_L0_RECOV]; });
+    {
+      Family f(o, "gpu_voltage_volts", "Rail voltage in volts.", "gauge");
+      for (size_t d = 0; d < n; ++d) {
+        if (!sm[d].ok) continue;
+        f.add(dl[d], {{"rail", "soc"}}, sm[d].v[F_VOLT_SOC]);
+        f.add(dl[d], {{"rail", "gfx"}}, sm[d].v[F_VOLT_GFX]);
+        f.add(dl[d], {{"rail", "mem"}}, sm[d].v[F_VOLT_MEM]);
+      }
+    }
+    devf("gpu_vram_max_bandwidth_bytes_per_second", "HBM peak bandwidth at max memory clock.",
+         "gauge", [&](size_t d) {
+           double g = sm[d].v[F_VRAM_MAX_BW];
+           return has(g) ? g * 1e9 : kNaN;
+         });
+    // ---- xGMI (replaces the reference's absent NVLink fields) ----
+    {
+      Family fs(o, "gpu_xgmi_link_up", "xGMI link status (1 up, 0 down/disabled).", "gauge");
+      for (size_t d = 0; d < n; ++d)
+        if (sm[d].ok)
+          for (int k = 0; k < sm[d].n_links; ++k) {
+            const auto& L = sm[d].links[k];
+            if (L.status < 0) continue;
+            fs.add(dl[d], {{"link", std::to_string(k)}, {"peer_bdf", L.peer_bdf}},
+                   L.status == 1 ? 1.0 : 0.0);
+          }
+    }
+    auto link_acc = [&](const char* name, const char* help, bool rd) {
+      Family f(o, name, help, "counter");
+      for (size_t d = 0; d < n; ++d)
+        if (sm[d].ok && sm[d].acc.valid)
+          for (int k = 0; k < sm[d].acc.n_links_acc; ++k) {
+            if (sm[d].links[k].status < 0) continue;
+            double kb = static_cast<double>(rd ? sm[d].acc.xgmi_rd_kb[k] : sm[d].acc.xgmi_wr_kb[k]);
+            f.add(dl[d], {{"link", std::to_string(k)}}, kb * 1024.0);
+          }
+    };
+    link_acc("gpu_xgmi_read_bytes_total", "Bytes received over the xGMI link.", true);
+    link_acc("gpu_xgmi_write_bytes_total", "Bytes sent over the xGMI link.", false);
+    auto link_rate = [&](const char* name, const char* help, int which) {
+      Family f(o, name, help, "gauge");
+      for (size_t d = 0; d < n; ++d) {
+        const auto& r = rate(d);
+        if (!sm[d].ok || !r.valid) continue;
+        for (int k = 0; k < r.n_links; ++k) {
+          const auto& L = sm[d].links[k];
+          if (L.status < 0) continue;
+          double v = kNaN;
+          if (which == 0) v = r.xgmi_rd_Bps[k];
+          else if (which == 1) v = r.xgmi_wr_Bps[k];
+          else if (has(L.max_bandwidth_gbps) && L.max_bandwidth_gbps > 0)
+            v = (r.xgmi_rd_Bps[k] + r.xgmi_wr_Bps[k]) * 8.0 / (L.max_bandwidth_gbps * 1e9 * 2.0);
+          f.add(dl[d], {{"link", std::to_string(k)}}, v);
+        }
+      }
+    };
+    link_rate("gpu_xgmi_read_bytes_per_second", "xGMI receive rate over the sampling interval.", 0);
+    link_rate("gpu_xgmi_write_bytes_per_second", "xGMI send rate over the sampling interval.", 1);
+    link_rate("gpu_xgmi_link_utilization_ratio",
+              "(rx+tx)/(2*link max bandwidth) over the sampling interval.", 2);
+    {
+      Family f(o, "gpu_xgmi_link_max_bandwidth_bytes_per_second", "xGMI link max bandwidth.",
+               "gauge");
+      for (size_t d = 0; d < n; ++d)
+        if (sm[d].ok)
+          for (int k = 0; k < sm[d].n_links; ++k) {
+            const auto& L = sm[d].links[k];
+            if (L.status < 0 || !has(L.max_bandwidth_gbps)) continue;
+            f.add(dl[d], {{"link", std::to_string(k)}}, L.max_bandwidth_gbps * 1e9 / 8.0);
+          }
+    }
+    devf("gpu_xgmi_link_speed_gbps", "xGMI per-lane bit rate in Gb/s.", "gauge",
+         [&](size_t d) { return sm[d].v[F_XGMI_LINK_SPEED]; });
+    if (in.proc_counts) {
+      Family f(o, "gpu_process_count", "GPU processes seen on this device.", "gauge");
+      for (size_t d = 0; d < n && d < in.proc_counts->size(); ++d)
+        f.add(dl[d], static_cast<double>((*in.proc_counts)[d]));
+    }
+  }
+
+  // ---------------- pod_gpu (reference measurement, gpu.py:206-216 / 240-250) ----------------
+  if (in.pod_rows) {
+    const auto& rows = *in.pod_rows;
+    std::vector<std::string> rl(rows.size());
+    for (size_t r = 0; r < rows.size(); ++r) {
+      const auto& p = rows[r];
+      const DeviceStatic* s = p.dev < static_cast<int>(n) ? &st[p.dev] : nullptr;
+      rl[r] = label_str({{"host", in.host},
+                         {"namespace", p.pod_namespace},
+                         {"gpu_id", s ? s->gpu_id : "-"},
+                         {"containerid", p.containerid},
+                         {"pid", p.pid},
+                         {"user_name", p.user_name},
+                         {"procressname", p.procname},  // sic: reference field name (gpu.py:209)
+                         {"podname", p.pod_name},
+                         {"container", p.container}});
+    }
+    if (in.compat_families) {
+      Family fm(o, "pod_gpu_used_memory", "GPU memory used by the process in MiB (0 for idle rows).",
+                "gauge");
+      for (size_t r = 0; r < rows.size(); ++r)
+        fm.add(rl[r], std::floor(rows[r].used_memory_bytes / kMiB));
+    }
+    if (in.compat_families) {
+      Family fu(o, "pod_gpu_gpu_util",
+                "Device-wide GPU utilization copied to each process row (reference semantics; 0 for "
+                "idle rows).",
+                "gauge");
+      for (size_t r = 0; r < rows.size(); ++r) fu.add(rl[r], rows[r].gpu_util);
+    }
+    {
+      Family f(o, "pod_gpu_used_memory_bytes", "GPU memory (VRAM) used by the process in bytes.",
+               "gauge");
+      for (size_t r = 0; r < rows.size(); ++r) f.add(rl[r], rows[r].used_memory_bytes);
+    }
+    {
+      Family f(o, "pod_gpu_proc_gfx_util",
+               "Per-process GFX engine utilization in percent over the sampling interval.", "gauge");
+      for (size_t r = 0; r < rows.size(); ++r) f.add(rl[r], rows[r].proc_gfx_util);
+    }
+    {
+      Family f(o, "pod_gpu_proc_cu_occupancy", "Compute units occupied by the process.", "gauge");
+      for (size_t r = 0; r < rows.size(); ++r) f.add(rl[r], rows[r].cu_occupancy);
+    }
+    // One series per (pod, container, gpu): the allocation view behind the reference dashboard's
+    // "GPUs per user" and "allocated / in use" panels.
+    {
+      struct Key {
+        std::string ns, pod, container, cid, user;
+        int dev;
+        bool operator<(const Key& o) const {
+          return std::tie(ns, pod, container, cid, user, dev) <
+                 std::tie(o.ns, o.pod, o.container, o.cid, o.user, o.dev);
+        }
+      };
+      std::map<Key, bool> alloc;  // -> active
+      for (const auto& p : rows) {
+        if (p.pod_name == "-" && p.containerid == "-") continue;  // host process
+        Key k{p.pod_namespace, p.pod_name, p.container, p.containerid, p.user_name, p.dev};
+        alloc[k] = alloc[k] || !p.idle;
+      }
+      std::set<int> devs_alloc, devs_active;
+      {
+        Family f(o, "pod_gpu_allocated",
+                 "1 per (pod, container, GPU) holding a GPU; state=active|idle.", "gauge");
+        for (const auto& [k, active] : alloc) {
+          const DeviceStatic* s = k.dev < static_cast<int>(n) ? &st[k.dev] : nullptr;
+          f.add(label_str({{"host", in.host},
+                           {"namespace", k.ns},
+                           {"podname", k.pod},
+                           {"container", k.container},
+                           {"containerid", k.cid},
+                           {"user_name", k.user},
+                           {"gpu_id", s ? s->gpu_id : "-"},
+                           {"state", active ? "active" : "idle"}}),
+                1.0);
+          devs_alloc.insert(k.dev);
+          if (active) devs_active.insert(k.dev);
+        }
+      }
+      Family g(o, "gpumon_gpus", "GPU counts on this node: total / allocated / allocated_idle / "
+                                  "allocated_active (reference dashboard stat panels).",
+               "gauge");
+      std::string hl = label_str({{"host", in.host}});
+      g.add(hl, {{"state", "total"}}, static_cast<double>(n));
+      g.add(hl, {{"state", "allocated"}}, static_cast<double>(devs_alloc.size()));
+      g.add(hl, {{"state", "allocated_active"}}, static_cast<double>(devs_active.size()));
+      g.add(hl, {{"state", "allocated_idle"}},
+            static_cast<double>(devs_alloc.size() - devs_active.size()));
+    }
+  }
+
+  // ---------------- extras (probe kernel, PMC, plugins) ----------------
+  if (in.extras && !in.extras->empty()) {
+    std::map<std::string, std::vector<const ExtraSeries*>> byname;
+    for (const auto& e : *in.extras) byname[e.name].push_back(&e);
+    for (const auto& [name, vec] : byname) {
+      Family f(o, name.c_str(), vec[0]->help.empty() ? name.c_str() : vec[0]->help.c_str(),
+               vec[0]->type.c_str());
+      for (const auto* e : vec) {
+        std::string base = (e->dev >= 0 && e->dev < static_cast<int>(n))
+                               ? dl[e->dev]
+                               : label_str({{"host", in.host}});
+        Labels extra;
+        for (const auto& kv : e->labels) extra.emplace_back(kv.first.c_str(), kv.second);
+        f.add(base, extra, e->value);
+      }
+    }
+  }
+
+  // ---------------- exporter self-metrics ----------------
+  if (in.self) {
+    const SelfStats& s = *in.self;
+    std::string hl = label_str({{"host", in.host}});
+    {
+      Family f(o, "gpumon_build_info", "Exporter build and backend identity.", "gauge");
+      f.add(hl, {{"version", s.version}, {"backend", s.backend}, {"backend_version", s.backend_version}},
+            1.0);
+    }
+    {
+      Family f(o, "gpumon_backend_up", "1 if the device backend is initialised.", "gauge");
+      f.add(hl, s.backend_up ? 1.0 : 0.0);
+    }
+    {
+      Family f(o, "gpumon_sample_interval_seconds", "Configured sampling interval.", "gauge");
+      f.add(hl, s.interval_s);
+    }
+    {
+      Family f(o, "gpumon_ticks_total", "Sampler ticks completed.", "counter");
+      f.add(hl, static_cast<double>(s.ticks));
+    }
+    {
+      Family f(o, "gpumon_samples_total", "Device samples taken (one per GPU per tick).", "counter");
+      f.add(hl, static_cast<double>(s.samples));
+    }
+    {
+      Family f(o, "gpumon_stale_samples_total",
+               "Device samples whose firmware table had not advanced since the previous tick.",
+               "counter");
+      f.add(hl, static_cast<double>(s.stale_samples));
+    }
+    {
+      Family f(o, "gpumon_tick_overruns_total", "Ticks that took longer than the interval.",
+               "counter");
+      f.add(hl, static_cast<double>(s.overruns));
+    }
+    {
+      Family f(o, "gpumon_last_sample_timestamp_seconds", "Wall time of the last completed tick.",
+               "gauge");
+      f.add(hl, s.last_tick_wall_s);
+    }
+    {
+      Family f(o, "gpumon_sample_errors_total", "Failed backend calls per GPU.", "counter");
+      for (size_t d = 0; d < s.device_errors.size() && d < n; ++d)
+        f.add(dl[d], static_cast<double>(s.device_errors[d]));
+    }
+    histogram(o, "gpumon_sample_duration_seconds",
+              "Time to sample all GPUs, attribute processes and render one tick.", s.sample_hist, hl);
+    histogram(o, "gpumon_scrape_duration_seconds",
+              "Server-side /metrics latency (request parsed -> response written).", s.scrape_hist, hl);
+    {
+      Family f(o, "gpumon_scrapes_total", "HTTP /metrics requests served.", "counter");
+      f.add(hl, static_cast<double>(s.scrapes));
+    }
+    {
+      Family f(o, "gpumon_http_connections", "Open HTTP connections.", "gauge");
+      f.add(hl, static_cast<double>(s.http_connections));
+    }
+    {
+      Family f(o, "gpumon_pods_attributed", "pod_gpu rows produced in the last tick.", "gauge");
+      f.add(hl, static_cast<double>(s.pods_attributed));
+    }
+    {
+      Family f(o, "gpumon_attribution_cache_total", "PID attribution cache lookups by result.",
+               "counter");
+      f.add(hl, {{"result", "hit"}}, static_cast<double>(s.attribution_cache_hits));
+      f.add(hl, {{"result", "miss"}}, static_cast<double>(s.attribution_cache_misses));
+    }
+    {
+      Family f(o, "gpumon_influx_push_total", "InfluxDB compat pushes by result.", "counter");
+      if (s.influx_ok || s.influx_fail || s.influx_dropped) {
+        f.add(hl, {{"result", "ok"}}, static_cast<double>(s.influx_ok));
+        f.add(hl, {{"result", "error"}}, static_cast<double>(s.influx_fail));
+        f.add(hl, {{"result", "dropped"}}, static_cast<double>(s.influx_dropped));
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Influx line protocol (reference-compatible)
+// ---------------------------------------------------------------------------------------------
+void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::string* o) {
+  const auto& st = *in.statics;
+  const auto& sm = *in.samples;
+  const size_t n = std::min(st.size(), sm.size());
+  auto num = [&](double v) { append_double(has(v) ? v : 0.0, o); };
+  for (size_t d = 0; d < n; ++d) {
+    if (!sm[d].ok) continue;
+    const auto& v = sm[d].v;
+    double used = std::floor(v[F_VRAM_USED] / kMiB), total = std::floor(v[F_VRAM_TOTAL] / kMiB);
+    // node_gpu,host=H,gpu_id=K gpu_util=U,mem_util=F,mem_used=M,mem_total=T,node="H",gid=K,mem_free=F
+    o->append("node_gpu,host=");
+    escape_influx_tag(in.host, o);
+    o->append(",gpu_id=");
+    escape_influx_tag(st[d].gpu_id, o);
+    o->append(" gpu_util=");
+    num(v[F_GFX_UTIL]);
+    o->append(",mem_util=");
+    num(has(used) && total > 0 ? v[F_VRAM_USED] * 100.0 / v[F_VRAM_TOTAL] : 0.0);
+    o->append(",mem_used=");
+    num(used);
+    o->append(",mem_total=");
+    num(total);
+    o->append(",node=\"");
+    escape_influx_field_str(in.host, o);
+    o->append("\",gid=");
+    o->append(st[d].gpu_id);
+    o->append(",mem_free=");
+    num(total - used);
+    o->push_back(' ');
+    o->append(std::to_string(ts_ns));
+    o->push_back('\n');
+    if (extended) {
+      o->append("gpu_ext,host=");
+      escape_influx_tag(in.host, o);
+      o->append(",gpu_id=");
+      escape_influx_tag(st[d].gpu_id, o);
+      o->append(",gpu_uuid=");
+      escape_influx_tag(st[d].uuid, o);
+      bool first = true;
+      auto field = [&](const char* k, double x) {
+        if (!has(x)) return;
+        o->push_back(first ? ' ' : ',');
+        first = false;
+        o->append(k).push_back('=');
+        append_double(x, o);
+      };
+      field("mem_bw_util", v[F_UMC_UTIL]);
+      field("temp_hotspot", v[F_TEMP_HOTSPOT]);
+      field("temp_mem", v[F_TEMP_MEM]);
+      field("power_w", v[F_POWER_CUR]);
+      field("energy_j", v[F_ENERGY_J]);
+      field("gfxclk_mhz", v[F_GFXCLK_CUR]);
+      field("uclk_mhz", v[F_UCLK_CUR]);
+      for (int k = 0; k < sm[d].n_xcd; ++k) {
+        std::string key = "xcd" + std::to_string(k) + "_busy";
+        field(key.c_str(), sm[d].xcd_busy[k]);
+      }
+      if (!first) {
+        o->push_back(' ');
+        o->append(std::to_string(ts_ns));
+        o->push_back('\n');
+      } else {
+        // no fields: drop the partial line
+        size_t p = o->rfind("gpu_ext,");
+        if (p != std::string::npos) o->resize(p);
+      }
+    }
+  }
+  if (!in.pod_rows) return;
+  for (const auto& p : *in.pod_rows) {
+    const std::string gid = p.dev < static_cast<int>(n) ? st[p.dev].gpu_id : "-";
+    // pod_gpu,host,namespace,gpu_id,containerid,pid_t,gpu_util_t,user_name_t  (gpu.py:207-208)
+    o->append("pod_gpu,host=");
+    escape_influx_tag(in.host, o);
+    o->append(",namespace=");
+    escape_influx_tag(p.pod_namespace, o);
+    o->append(",gpu_id=");
+    escape_influx_tag(gid, o);
+    o->append(",containerid=");
+    escape_influx_tag(p.containerid, o);
+    o->append(",pid_t=");
+    escape_influx_tag(p.pid, o);
+    o->append(",gpu_util_t=");
+    std::string gu;
+    append_double(p.idle ? 0.0 : p.gpu_util, &gu);
+    escape_influx_tag(gu, o);
+    o->append(",user_name_t=");
+    escape_influx_tag(p.user_name, o);
+    // fields (gpu.py:209-216)
+    o->append(" procressname=\"");
+    escape_influx_field_str(p.procname, o);
+    o->append("\",podname=\"");
+    escape_influx_field_str(p.pod_name, o);
+    o->append("\",pid=\"");
+    escape_influx_field_str(p.pid, o);
+    o->append("\",gpu_id_v=\"");
+    escape_influx_field_str(gid, o);
+    o->append("\",node=\"");
+    escape_influx_field_str(in.host, o);
+    o->append("\",user_name=\"");
+    escape_influx_field_str(p.user_name, o);
+    o->append("\",gpu_util=");
+    append_double(p.idle ? 0.0 : p.gpu_util, o);
+    o->append(",used_memory=");
+    append_double(std::floor(p.used_memory_bytes / kMiB), o);
+    o->push_back(' ');
+    o->append(std::to_string(ts_ns));
+    o->push_back('\n');
+  }
+}
+
+}  // namespace gpumon

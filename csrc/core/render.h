@@ -1,0 +1,101 @@
+// Exposition renderers: Prometheus text format 0.0.4 and InfluxDB line protocol.
+//
+// Reference parity: the reference hand-builds two InfluxDB measurements with string
+// concatenation and no escaping (/root/reference/gpu.py:136-143 node_gpu, gpu.py:206-216 and
+// 240-250 pod_gpu; quirks Q7/Q8). Here both sinks are rendered from the same sample set once per
+// tick into a buffer that scrapes / pushes only copy:
+//   - Prometheus: node_gpu_* / pod_gpu_* keep the reference field names (dashboard compat) and
+//     gpu_* families carry the MI355X extras.
+//   - Influx:     byte-compatible node_gpu / pod_gpu measurements (tags/fields as the reference,
+//     properly escaped, with timestamps) plus an optional gpu_ext measurement.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "sample.h"
+
+namespace gpumon {
+
+// One pod_gpu series: an attributed GPU process, or an allocated-but-idle GPU (pid "-").
+struct PodRow {
+  int dev = 0;                      // device index
+  bool idle = false;
+  std::string pid = "-";
+  std::string procname = "-";
+  std::string pod_namespace = "-";
+  std::string pod_name = "-";
+  std::string container = "-";
+  std::string containerid = "-";    // 12-char short id (reference docker short id)
+  std::string user_name = "-";
+  double used_memory_bytes = 0;
+  double gpu_util = 0;              // device-wide util (reference semantics, Q4)
+  double proc_gfx_util = kNaN;      // true per-process util from engine_usage.gfx ns
+  double cu_occupancy = kNaN;
+};
+
+// Histogram with fixed upper bounds (seconds).
+struct HistSnapshot {
+  std::vector<double> bounds;
+  std::vector<uint64_t> counts;     // cumulative-ready: per-bucket (non-cumulative) counts
+  uint64_t count = 0;
+  double sum = 0;
+};
+
+struct SelfStats {
+  std::string version;
+  std::string backend;
+  std::string backend_version;
+  bool backend_up = false;
+  uint64_t ticks = 0;
+  uint64_t samples = 0;
+  uint64_t stale_samples = 0;
+  uint64_t overruns = 0;
+  double last_tick_wall_s = 0;
+  double interval_s = 1.0;
+  HistSnapshot sample_hist;         // whole-tick duration
+  HistSnapshot scrape_hist;         // server-side /metrics latency
+  uint64_t scrapes = 0;
+  uint64_t http_connections = 0;
+  uint64_t pods_attributed = 0;
+  uint64_t attribution_cache_hits = 0, attribution_cache_misses = 0;
+  uint64_t influx_ok = 0, influx_fail = 0, influx_dropped = 0;
+  std::vector<uint64_t> device_errors;  // per device
+};
+
+// Values supplied from outside the sampler (probe kernel, PMC device counting, plugins).
+struct ExtraSeries {
+  std::string name;                 // full metric name
+  std::string help;
+  std::string type = "gauge";
+  int dev = -1;                     // -1 = node-level (no device labels)
+  std::vector<std::pair<std::string, std::string>> labels;
+  double value = 0;
+};
+
+struct RenderInput {
+  std::string host;
+  const std::vector<DeviceStatic>* statics = nullptr;
+  const std::vector<DeviceSample>* samples = nullptr;
+  const std::vector<DeviceRates>* rates = nullptr;
+  const std::vector<PodRow>* pod_rows = nullptr;
+  const std::vector<size_t>* proc_counts = nullptr;  // per device
+  const std::vector<ExtraSeries>* extras = nullptr;
+  const SelfStats* self = nullptr;
+  bool compat_families = true;      // node_gpu_* / pod_gpu_*
+  bool extended_families = true;    // gpu_* MI355X extras
+};
+
+void render_prometheus(const RenderInput& in, std::string* out);
+// Line protocol; one line per node_gpu / pod_gpu row (+ gpu_ext when extended), ns timestamps.
+void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::string* out);
+
+// Escapers (exposed for tests).
+void escape_label_value(const std::string& v, std::string* out);
+void escape_influx_tag(const std::string& v, std::string* out);
+void escape_influx_field_str(const std::string& v, std::string* out);
+void append_double(double v, std::string* out);
+
+}  // namespace gpumon

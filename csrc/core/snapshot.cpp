@@ -1,0 +1,74 @@
+#include "snapshot.h"
+
+#include <zlib.h>
+
+#include <algorithm>
+#include <cmath>
+
+namespace gpumon {
+
+Histogram::Histogram(std::vector<double> bounds)
+    : bounds_(std::move(bounds)), counts_(new std::atomic<uint64_t>[bounds_.size() + 1]) {
+  for (size_t i = 0; i <= bounds_.size(); ++i) counts_[i].store(0);
+}
+
+void Histogram::observe(double s) {
+  size_t i = std::lower_bound(bounds_.begin(), bounds_.end(), s) - bounds_.begin();
+  counts_[i].fetch_add(1, std::memory_order_relaxed);
+  count_.fetch_add(1, std::memory_order_relaxed);
+  sum_ns_.fetch_add(static_cast<uint64_t>(std::max(0.0, s) * 1e9), std::memory_order_relaxed);
+}
+
+void Histogram::snapshot(std::vector<double>* bounds, std::vector<uint64_t>* counts,
+                         uint64_t* count, double* sum) const {
+  *bounds = bounds_;
+  counts->resize(bounds_.size());
+  uint64_t total = 0;
+  for (size_t i = 0; i < bounds_.size(); ++i) {
+    (*counts)[i] = counts_[i].load(std::memory_order_relaxed);
+    total += (*counts)[i];
+  }
+  total += counts_[bounds_.size()].load(std::memory_order_relaxed);
+  *count = total;
+  *sum = sum_ns_.load(std::memory_order_relaxed) * 1e-9;
+}
+
+double Histogram::quantile(double q) const {
+  std::vector<uint64_t> c(bounds_.size() + 1);
+  uint64_t total = 0;
+  for (size_t i = 0; i <= bounds_.size(); ++i) total += (c[i] = counts_[i].load());
+  if (!total) return NAN;
+  double target = q * total;
+  uint64_t cum = 0;
+  for (size_t i = 0; i <= bounds_.size(); ++i) {
+    if (cum + c[i] >= target && c[i] > 0) {
+      double lo = i == 0 ? 0.0 : bounds_[i - 1];
+      double hi = i < bounds_.size() ? bounds_[i] : bounds_.back() * 2;
+      return lo + (hi - lo) * (target - cum) / c[i];
+    }
+    cum += c[i];
+  }
+  return bounds_.back();
+}
+
+std::vector<double> latency_buckets() {
+  return {50e-6, 100e-6, 250e-6, 500e-6, 1e-3, 2.5e-3, 5e-3, 10e-3, 25e-3,
+          50e-3, 100e-3, 250e-3, 500e-3, 1.0,  2.5,    5.0,  10.0};
+}
+
+bool gzip_compress(const std::string& in, std::string* out, int level) {
+  z_stream zs{};
+  if (deflateInit2(&zs, level, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) return false;
+  out->resize(deflateBound(&zs, in.size()) + 32);
+  zs.next_in = reinterpret_cast<Bytef*>(const_cast<char*>(in.data()));
+  zs.avail_in = static_cast<uInt>(in.size());
+  zs.next_out = reinterpret_cast<Bytef*>(&(*out)[0]);
+  zs.avail_out = static_cast<uInt>(out->size());
+  int r = deflate(&zs, Z_FINISH);
+  deflateEnd(&zs);
+  if (r != Z_STREAM_END) return false;
+  out->resize(zs.total_out);
+  return true;
+}
+
+}  // namespace gpumon

@@ -1,0 +1,63 @@
+// Pre-rendered exposition snapshot shared between the sampler (writer) and HTTP workers (readers).
+//
+// The reference has no scrape endpoint (push-only, /root/reference/gpu.py:145). The design goal
+// for /metrics p99 is that a scrape never touches the device or re-renders: the sampler renders
+// (and gzips) once per tick, then publishes an immutable Snapshot; a scrape takes a reference
+// under a tiny critical section and writes the bytes.
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace gpumon {
+
+struct Snapshot {
+  std::string body;       // text/plain; version=0.0.4
+  std::string body_gz;    // gzip of body (empty if compression disabled)
+  uint64_t seq = 0;
+  int64_t wall_ns = 0;
+};
+
+class SnapshotStore {
+ public:
+  std::shared_ptr<const Snapshot> get() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return cur_;
+  }
+  void publish(std::shared_ptr<const Snapshot> s) {
+    std::lock_guard<std::mutex> g(mu_);
+    cur_ = std::move(s);
+  }
+
+ private:
+  mutable std::mutex mu_;
+  std::shared_ptr<const Snapshot> cur_;
+};
+
+// Lock-free fixed-bucket histogram (observations in seconds).
+class Histogram {
+ public:
+  explicit Histogram(std::vector<double> bounds);
+  void observe(double seconds);
+  void snapshot(std::vector<double>* bounds, std::vector<uint64_t>* counts, uint64_t* count,
+                double* sum) const;
+  // Quantile estimate from the buckets (linear interpolation inside the bucket).
+  double quantile(double q) const;
+
+ private:
+  std::vector<double> bounds_;
+  std::unique_ptr<std::atomic<uint64_t>[]> counts_;  // bounds_.size() + 1 (overflow)
+  std::atomic<uint64_t> count_{0};
+  std::atomic<uint64_t> sum_ns_{0};
+};
+
+std::vector<double> latency_buckets();  // 50us .. 10s
+
+// gzip (RFC 1952) of `in`; returns false if zlib fails.
+bool gzip_compress(const std::string& in, std::string* out, int level = 1);
+
+}  // namespace gpumon

@@ -1,0 +1,109 @@
+// Host-side API over the gfx950 kernels (implemented in kernels.hip, bound in hip_module.cpp).
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "kernels.h"
+
+namespace gpumon_hip {
+
+void check(int err, const char* what);  // throws std::runtime_error on a HIP error
+
+int device_count();
+std::string device_arch(int dev);
+int device_cu_count(int dev);
+
+// --- numerics-testable launches on caller-provided device pointers / streams -------------------
+// C[32x32] (fp32, row-major) = iters * A[32x16] @ B[16x32] (bf16, row-major), one wave.
+void launch_mfma_tile(int dev, const void* a, const void* b, float* c, int iters, void* stream);
+// Burn: `blocks` x 256 threads; each wave runs iters x 4 MFMAs; wave sums go to out[blocks*4].
+void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blocks, int iters, void* stream);
+// dst = src (n16 = number of 16-byte vectors)
+void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream);
+// c = a + s * b  (fp32, n elements, n % 4 == 0)
+void launch_stream_triad(int dev, const float* a, const float* b, float* c, float s, size_t n, int blocks,
+                         void* stream);
+
+// --- background synthetic load ----------------------------------------------------------------
+struct LoadStats {
+  uint64_t launches = 0;
+  double busy_s = 0;        // GPU time measured with events
+  double flops = 0;         // MFMA FLOP issued
+  double bytes = 0;         // HBM bytes moved (read + write)
+};
+
+class LoadGen {
+ public:
+  // kind: "mfma" | "hbm" | "mixed" ; duty in (0, 1]: fraction of wall time the GPU is kept busy
+  LoadGen(int dev, std::string kind, double duty, size_t hbm_bytes, int mfma_iters);
+  ~LoadGen();
+  void start();
+  void stop();
+  LoadStats stats() const;
+  bool running() const { return running_; }
+
+ private:
+  void loop();
+  int dev_;
+  std::string kind_;
+  double duty_;
+  size_t bytes_;
+  int iters_;
+  void* stream_ = nullptr;
+  void* a_ = nullptr;
+  void* b_ = nullptr;
+  float* out_ = nullptr;
+  void* src_ = nullptr;
+  void* dst_ = nullptr;
+  std::thread th_;
+  std::atomic<bool> running_{false};
+  mutable std::atomic<uint64_t> launches_{0};
+  std::atomic<uint64_t> busy_ns_{0};
+  std::atomic<uint64_t> flops_{0};
+  std::atomic<uint64_t> bytes_moved_{0};
+  std::string err_;
+};
+
+// --- K1 probe: pinned ring buffer ----------------------------------------------------------------
+struct ProbeResult {
+  bool complete = false;
+  uint32_t seq = 0;
+  int blocks = 0;
+  int arrived = 0;
+  int64_t host_launch_ns = 0;   // CLOCK_MONOTONIC before the launch call
+  int64_t host_done_ns = 0;     // when the host observed the last arrival
+  uint64_t gpu_span_ticks = 0;  // max(t1) - min(t0), 100 MHz ticks
+  uint64_t gpu_first_start = 0; // min(t0) in ticks
+  std::vector<int> xcc_blocks;  // blocks seen per XCC id (index 0..15)
+  std::vector<double> xcc_clock_mhz;  // mean effective shader clock per XCC (0 if none)
+  int unique_cus = 0;
+  std::vector<ProbeRecord> records;
+};
+
+class Probe {
+ public:
+  Probe(int dev, int blocks, int slots, int spin_ticks);
+  ~Probe();
+  int launch();                              // returns slot; non-blocking
+  bool poll(int slot, ProbeResult* out);     // true when complete (no device sync)
+  bool wait(int slot, double timeout_s, ProbeResult* out);
+  int blocks() const { return blocks_; }
+
+ private:
+  int dev_, blocks_, slots_, spin_;
+  void* stream_ = nullptr;
+  ProbeRecord* ring_ = nullptr;         // host pinned, device mapped
+  uint32_t* arrivals_ = nullptr;        // host pinned, one counter per slot
+  ProbeRecord* ring_dev_ = nullptr;
+  uint32_t* arrivals_dev_ = nullptr;
+  std::vector<uint32_t> slot_seq_;
+  std::vector<int64_t> slot_launch_ns_;
+  uint32_t seq_ = 0;
+  int next_ = 0;
+};
+
+}  // namespace gpumon_hip

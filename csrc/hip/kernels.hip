@@ -1,0 +1,414 @@
+// gfx950 kernels + host wrappers. See kernels.h for the design notes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <set>
+#include <stdexcept>
+#include <tuple>
+
+#include "hip_api.h"
+
+namespace gpumon_hip {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+static int64_t mono_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+void check(int err, const char* what) {
+  if (err != hipSuccess)
+    throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(static_cast<hipError_t>(err)));
+}
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+std::string device_arch(int dev) {
+  hipDeviceProp_t p;
+  check(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");
+  return p.gcnArchName;
+}
+
+int device_cu_count(int dev) {
+  hipDeviceProp_t p;
+  check(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");
+  return p.multiProcessorCount;
+}
+
+// ============================================================================================
+// K2a: bf16 MFMA. Operand fragments for v_mfma_f32_32x32x16_bf16 (lane l, r = l&31, h = l>>5):
+//   A[row r][k = 8h + j], B[k = 8h + j][col r], j = 0..7;  C/D: col = l&31,
+//   row = (reg&3) + 8*(reg>>2) + 4*(l>>5), reg = 0..15   (cdna_hip_programming.md §3)
+// ============================================================================================
+__device__ __forceinline__ void load_frags(const __bf16* __restrict__ a, const __bf16* __restrict__ b,
+                                           int lane, bf16x8* av, bf16x8* bv) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    (*av)[j] = a[r * 16 + 8 * h + j];
+    (*bv)[j] = b[(8 * h + j) * 32 + r];
+  }
+}
+
+__global__ void __launch_bounds__(64) mfma_tile_kernel(const __bf16* __restrict__ a, const __bf16* __restrict__ b,
+                                                       float* __restrict__ c, int iters) {
+  const int lane = threadIdx.x;
+  bf16x8 av, bv;
+  load_frags(a, b, lane, &av, &bv);
+  f32x16 acc = {};
+  for (int i = 0; i < iters; ++i) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc, 0, 0, 0);
+#pragma unroll
+  for (int reg = 0; reg < 16; ++reg) {
+    const int row = (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+    c[row * 32 + (lane & 31)] = acc[reg];
+  }
+}
+
+// Burn: 4 independent accumulators per wave keep the per-SIMD matrix pipe issuing back-to-back
+// (32 cycles per 32x32x16 MFMA). Two waves per SIMD (8 per CU) at 2048 blocks of 256 threads.
+__global__ void __launch_bounds__(256) mfma_burn_kernel(const __bf16* __restrict__ a, const __bf16* __restrict__ b,
+                                                        float* __restrict__ out, int iters) {
+  const int lane = threadIdx.x & 63;
+  bf16x8 av, bv;
+  load_frags(a, b, lane, &av, &bv);
+  f32x16 acc0 = {}, acc1 = {}, acc2 = {}, acc3 = {};
+  acc1[0] = 1.f;
+  acc2[0] = 2.f;
+  acc3[0] = 3.f;
+  for (int i = 0; i < iters; ++i) {
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc1, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc2, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc3, 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s += acc0[r] + acc1[r] + acc2[r] + acc3[r];
+  if (lane == 0) out[blockIdx.x * 4 + (threadIdx.x >> 6)] = s;
+}
+
+// ============================================================================================
+// K2b: HBM stream. 16 B per lane, non-temporal (streamed once), grid-stride.
+// ============================================================================================
+__global__ void __launch_bounds__(256) stream_copy_kernel(const i32x4* __restrict__ src, i32x4* __restrict__ dst,
+                                                          size_t n) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    i32x4 v = __builtin_nontemporal_load(src + i);
+    __builtin_nontemporal_store(v, dst + i);
+  }
+}
+
+__global__ void __launch_bounds__(256) stream_triad_kernel(const f32x4* __restrict__ a,
+                                                           const f32x4* __restrict__ b,
+                                                           f32x4* __restrict__ c, float s, size_t n4) {
+  const size_t stride = static_cast<size_t>(gridDim.x) * blockDim.x;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 x = __builtin_nontemporal_load(a + i);
+    f32x4 y = __builtin_nontemporal_load(b + i);
+    f32x4 z;
+    z.x = fmaf(s, y.x, x.x);
+    z.y = fmaf(s, y.y, x.y);
+    z.z = fmaf(s, y.z, x.z);
+    z.w = fmaf(s, y.w, x.w);
+    __builtin_nontemporal_store(z, c + i);
+  }
+}
+
+// ============================================================================================
+// K1: probe. One wave per workgroup; lane 0 does the work (stamps are wave-uniform SGPR reads).
+// Publication to the pinned host ring: plain stores -> vmcnt(0) drain -> system-scope release
+// fetch_add on the slot's arrival counter (the counter is what the host polls).
+// ============================================================================================
+__global__ void __launch_bounds__(64) probe_kernel(ProbeRecord* __restrict__ recs, uint32_t* arrivals,
+                                                   uint32_t seq, uint32_t spin_ticks) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t c0 = __builtin_amdgcn_s_memtime();
+  uint32_t xcc, hw;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+  uint64_t t1 = t0;
+  // Bounded spin on the constant 100 MHz clock: exit condition reached by every wave.
+  for (int guard = 0; guard < (1 << 20); ++guard) {
+    t1 = __builtin_amdgcn_s_memrealtime();
+    if (t1 - t0 >= spin_ticks) break;
+  }
+  const uint64_t c1 = __builtin_amdgcn_s_memtime();
+  ProbeRecord* r = recs + blockIdx.x;
+  r->xcc_id = xcc & 0xF;
+  r->hw_id = hw;
+  r->t0_real = t0;
+  r->t1_real = t1;
+  r->c0 = c0;
+  r->c1 = c1;
+  r->seq = seq;
+  r->block = blockIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// ============================================================================================
+// host wrappers
+// ============================================================================================
+void launch_mfma_tile(int dev, const void* a, const void* b, float* c, int iters, void* stream) {
+  check(hipSetDevice(dev), "hipSetDevice");
+  hipLaunchKernelGGL(mfma_tile_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const __bf16*>(a), static_cast<const __bf16*>(b), c, iters);
+  check(hipGetLastError(), "mfma_tile_kernel");
+}
+
+void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blocks, int iters, void* stream) {
+  check(hipSetDevice(dev), "hipSetDevice");
+  hipLaunchKernelGGL(mfma_burn_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const __bf16*>(a), static_cast<const __bf16*>(b), out, iters);
+  check(hipGetLastError(), "mfma_burn_kernel");
+}
+
+void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream) {
+  check(hipSetDevice(dev), "hipSetDevice");
+  hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const i32x4*>(src), static_cast<i32x4*>(dst), n16);
+  check(hipGetLastError(), "stream_copy_kernel");
+}
+
+void launch_stream_triad(int dev, const float* a, const float* b, float* c, float s, size_t n, int blocks,
+                         void* stream) {
+  if (n % 4) throw std::invalid_argument("stream_triad: n must be a multiple of 4");
+  check(hipSetDevice(dev), "hipSetDevice");
+  hipLaunchKernelGGL(stream_triad_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     reinterpret_cast<const f32x4*>(a), reinterpret_cast<const f32x4*>(b),
+                     reinterpret_cast<f32x4*>(c), s, n / 4);
+  check(hipGetLastError(), "stream_triad_kernel");
+}
+
+// ---------------------------------------------------------------------------------------------
+// LoadGen
+// ---------------------------------------------------------------------------------------------
+LoadGen::LoadGen(int dev, std::string kind, double duty, size_t hbm_bytes, int mfma_iters)
+    : dev_(dev), kind_(std::move(kind)), duty_(std::clamp(duty, 0.01, 1.0)), bytes_(hbm_bytes), iters_(mfma_iters) {
+  if (kind_ != "mfma" && kind_ != "hbm" && kind_ != "mixed")
+    throw std::invalid_argument("LoadGen kind must be mfma | hbm | mixed");
+  bytes_ = std::max<size_t>(bytes_ / 16 * 16, 1 << 20);
+}
+
+LoadGen::~LoadGen() { stop(); }
+
+void LoadGen::start() {
+  if (running_) return;
+  check(hipSetDevice(dev_), "hipSetDevice");
+  hipStream_t s;
+  check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  stream_ = s;
+  // bf16 operand tile with non-trivial values (keeps the MFMA datapath toggling: realistic power)
+  std::vector<uint16_t> h(32 * 16 + 16 * 32);
+  for (size_t i = 0; i < h.size(); ++i) {
+    float f = std::sin(0.37f * static_cast<float>(i)) * 0.5f;
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    h[i] = static_cast<uint16_t>(u >> 16);
+  }
+  check(hipMalloc(&a_, h.size() * 2), "hipMalloc");
+  b_ = static_cast<char*>(a_) + 32 * 16 * 2;
+  check(hipMemcpy(a_, h.data(), h.size() * 2, hipMemcpyHostToDevice), "hipMemcpy");
+  check(hipMalloc(reinterpret_cast<void**>(&out_), 4096 * 4 * sizeof(float)), "hipMalloc");
+  if (kind_ != "mfma") {
+    check(hipMalloc(&src_, bytes_), "hipMalloc");
+    check(hipMalloc(&dst_, bytes_), "hipMalloc");
+    check(hipMemsetAsync(src_, 1, bytes_, s), "hipMemset");
+    check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  }
+  running_ = true;
+  th_ = std::thread([this] { loop(); });
+}
+
+void LoadGen::loop() {
+  try {
+    check(hipSetDevice(dev_), "hipSetDevice");
+    hipStream_t s = static_cast<hipStream_t>(stream_);
+    hipEvent_t e0, e1;
+    check(hipEventCreate(&e0), "hipEventCreate");
+    check(hipEventCreate(&e1), "hipEventCreate");
+    const int cus = device_cu_count(dev_);
+    const int burn_blocks = cus * 8;     // 8 waves/CU = 2 per SIMD
+    const int stream_blocks = cus * 16;  // >> 256 workgroups across all 8 XCDs
+    bool flip = false;
+    while (running_) {
+      check(hipEventRecord(e0, s), "hipEventRecord");
+      double fl = 0, by = 0;
+      for (int k = 0; k < 4; ++k) {
+        bool do_mfma = kind_ == "mfma" || (kind_ == "mixed" && !flip);
+        if (do_mfma) {
+          launch_mfma_burn(dev_, a_, b_, out_, burn_blocks, iters_, s);
+          fl += static_cast<double>(burn_blocks) * 4 * 4 * iters_ * 32768.0;
+        } else {
+          launch_stream_copy(dev_, src_, dst_, bytes_ / 16, stream_blocks, s);
+          by += 2.0 * static_cast<double>(bytes_);
+        }
+        flip = !flip;
+        launches_++;
+      }
+      check(hipEventRecord(e1, s), "hipEventRecord");
+      check(hipEventSynchronize(e1), "hipEventSynchronize");
+      float ms = 0;
+      check(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+      busy_ns_ += static_cast<uint64_t>(ms * 1e6);
+      flops_ += static_cast<uint64_t>(fl);
+      bytes_moved_ += static_cast<uint64_t>(by);
+      if (duty_ < 0.999) {
+        double idle_ms = ms * (1.0 / duty_ - 1.0);
+        auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(static_cast<int64_t>(idle_ms * 1e3));
+        while (running_ && std::chrono::steady_clock::now() < until)
+          std::this_thread::sleep_for(std::chrono::milliseconds(1));
+      }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  } catch (const std::exception& e) {
+    err_ = e.what();
+    running_ = false;
+  }
+}
+
+void LoadGen::stop() {
+  if (th_.joinable()) {
+    running_ = false;
+    th_.join();
+  }
+  running_ = false;
+  if (stream_) {
+    (void)hipSetDevice(dev_);
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(stream_));
+    (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
+    stream_ = nullptr;
+  }
+  if (a_) (void)hipFree(a_);
+  if (out_) (void)hipFree(out_);
+  if (src_) (void)hipFree(src_);
+  if (dst_) (void)hipFree(dst_);
+  a_ = b_ = src_ = dst_ = nullptr;
+  out_ = nullptr;
+}
+
+LoadStats LoadGen::stats() const {
+  if (!err_.empty()) throw std::runtime_error("LoadGen failed: " + err_);
+  LoadStats s;
+  s.launches = launches_;
+  s.busy_s = busy_ns_ * 1e-9;
+  s.flops = static_cast<double>(flops_.load());
+  s.bytes = static_cast<double>(bytes_moved_.load());
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Probe
+// ---------------------------------------------------------------------------------------------
+Probe::Probe(int dev, int blocks, int slots, int spin_ticks)
+    : dev_(dev), blocks_(std::max(1, blocks)), slots_(std::max(1, slots)), spin_(std::max(1, spin_ticks)) {
+  check(hipSetDevice(dev_), "hipSetDevice");
+  hipStream_t s;
+  check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  stream_ = s;
+  const size_t rb = sizeof(ProbeRecord) * static_cast<size_t>(blocks_) * slots_;
+  check(hipHostMalloc(reinterpret_cast<void**>(&ring_), rb, hipHostMallocMapped | hipHostMallocCoherent),
+        "hipHostMalloc(ring)");
+  check(hipHostMalloc(reinterpret_cast<void**>(&arrivals_), sizeof(uint32_t) * slots_,
+                      hipHostMallocMapped | hipHostMallocCoherent),
+        "hipHostMalloc(arrivals)");
+  memset(ring_, 0, rb);
+  memset(arrivals_, 0, sizeof(uint32_t) * slots_);
+  check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_dev_), ring_, 0), "hipHostGetDevicePointer");
+  check(hipHostGetDevicePointer(reinterpret_cast<void**>(&arrivals_dev_), arrivals_, 0), "hipHostGetDevicePointer");
+  slot_seq_.assign(slots_, 0);
+  slot_launch_ns_.assign(slots_, 0);
+}
+
+Probe::~Probe() {
+  (void)hipSetDevice(dev_);
+  if (stream_) {
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(stream_));
+    (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
+  }
+  if (ring_) (void)hipHostFree(ring_);
+  if (arrivals_) (void)hipHostFree(arrivals_);
+}
+
+int Probe::launch() {
+  const int slot = next_;
+  // A slot is reusable only when its previous launch fully arrived.
+  if (slot_seq_[slot] != 0 && __atomic_load_n(&arrivals_[slot], __ATOMIC_ACQUIRE) < static_cast<uint32_t>(blocks_))
+    return -1;
+  next_ = (next_ + 1) % slots_;
+  const uint32_t seq = ++seq_;
+  __atomic_store_n(&arrivals_[slot], 0u, __ATOMIC_RELEASE);
+  slot_seq_[slot] = seq;
+  check(hipSetDevice(dev_), "hipSetDevice");
+  slot_launch_ns_[slot] = mono_ns();
+  hipLaunchKernelGGL(probe_kernel, dim3(blocks_), dim3(64), 0, static_cast<hipStream_t>(stream_),
+                     ring_dev_ + static_cast<size_t>(slot) * blocks_, arrivals_dev_ + slot, seq,
+                     static_cast<uint32_t>(spin_));
+  check(hipGetLastError(), "probe_kernel");
+  return slot;
+}
+
+bool Probe::poll(int slot, ProbeResult* out) {
+  if (slot < 0 || slot >= slots_) return false;
+  const uint32_t arrived = __atomic_load_n(&arrivals_[slot], __ATOMIC_ACQUIRE);
+  out->seq = slot_seq_[slot];
+  out->blocks = blocks_;
+  out->arrived = static_cast<int>(arrived);
+  out->host_launch_ns = slot_launch_ns_[slot];
+  if (arrived < static_cast<uint32_t>(blocks_)) {
+    out->complete = false;
+    return false;
+  }
+  out->complete = true;
+  out->host_done_ns = mono_ns();
+  const ProbeRecord* r = ring_ + static_cast<size_t>(slot) * blocks_;
+  out->records.assign(r, r + blocks_);
+  out->xcc_blocks.assign(16, 0);
+  std::vector<double> clk_sum(16, 0.0);
+  uint64_t tmin = ~0ull, tmax = 0;
+  std::set<std::tuple<uint32_t, uint32_t>> cus;
+  for (const auto& x : out->records) {
+    if (x.seq != out->seq) continue;  // torn / stale record (should not happen after the counter)
+    const uint32_t xc = x.xcc_id & 0xF;
+    out->xcc_blocks[xc]++;
+    const uint64_t dt = x.t1_real - x.t0_real;
+    if (dt) clk_sum[xc] += static_cast<double>(x.c1 - x.c0) / static_cast<double>(dt) * 100.0;  // MHz
+    tmin = std::min(tmin, x.t0_real);
+    tmax = std::max(tmax, x.t1_real);
+    // CU identity inside an XCC: HW_ID bits [15:8] = cu_id | sh_id | se_id
+    cus.insert({xc, (x.hw_id >> 8) & 0xFF});
+  }
+  out->xcc_clock_mhz.assign(16, 0.0);
+  for (int k = 0; k < 16; ++k)
+    if (out->xcc_blocks[k]) out->xcc_clock_mhz[k] = clk_sum[k] / out->xcc_blocks[k];
+  out->gpu_first_start = tmin;
+  out->gpu_span_ticks = tmax > tmin ? tmax - tmin : 0;
+  out->unique_cus = static_cast<int>(cus.size());
+  return true;
+}
+
+bool Probe::wait(int slot, double timeout_s, ProbeResult* out) {
+  const int64_t deadline = mono_ns() + static_cast<int64_t>(timeout_s * 1e9);
+  while (!poll(slot, out)) {
+    if (mono_ns() > deadline) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  return true;
+}
+
+}  // namespace gpumon_hip

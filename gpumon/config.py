@@ -1,0 +1,219 @@
+"""Typed configuration: defaults < YAML file < environment < CLI flags.
+
+Reference configuration (/root/reference/gpu.py:17-26, gpu_monitor.yaml:29-37):
+  * ``NODE_NAME``    — node name tag (fieldRef spec.nodeName); fallback ``"no_name"`` (gpu.py:23-24).
+    The reference re-reads the env inside main() so its fallback never reached the emitted lines
+    (quirk Q1); here the resolved value is used everywhere, falling back to the hostname.
+  * ``INFLUXDB_URL`` — InfluxDB write endpoint; default hard-coded in gpu.py:18,26.
+    Here: when set, the Influx compat push is enabled (batched, one POST per tick).
+  * sampling interval hard-coded to 10 s (gpu.py:263) -> ``interval`` (default 1 s).
+  * opt-in docker label mlgpu=mlgpu hard-coded (gpu.py:186-188) -> ``opt_in_label`` (default off;
+    ``--compat`` sets ``mlgpu=mlgpu``).
+  * pod-name prefix ``turing-gpu-notebook-`` hard-coded (gpu.py:196,230) -> ``user_prefix``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import os
+import socket
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import yaml
+
+REFERENCE_DEFAULT_INFLUX = "http://10.0.4.235:9000/write?db=gpu_process"  # gpu.py:18 (not used unless --compat)
+
+
+@dataclass
+class Config:
+    # device backend
+    backend: str = "auto"                 # auto | amdsmi | mock[:k=v,...]
+    amdsmi_lib: str = ""
+    devices: List[int] = field(default_factory=list)
+    interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
+    processes: bool = True
+    link_every: int = 30
+    sample_threads: int = 0
+    # exposition
+    listen: str = "0.0.0.0:9400"
+    http_threads: int = 2
+    host: str = ""
+    gzip: bool = True
+    compat_families: bool = True
+    extended_families: bool = True
+    # influx compat push
+    influx_url: str = ""
+    influx_extended: bool = False
+    influx_every: int = 1
+    # attribution
+    procfs_root: str = "/proc"
+    opt_in_label: str = ""
+    user_label: str = ""
+    user_regex: str = ""
+    user_prefix: str = "turing-gpu-notebook-"
+    compat_user_rule: bool = True
+    procfs_env_fallback: bool = True
+    include_host_processes: bool = True
+    # control plane (k8s)
+    cri_socket: str = ""                  # e.g. unix:///run/containerd/containerd.sock ; "" = autodetect
+    pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
+    resource_names: List[str] = field(default_factory=lambda: ["amd.com/gpu"])
+    metadata_refresh: float = 10.0
+    # on-device probe / PMC
+    enable_probe: bool = False
+    probe_every: int = 1
+    enable_pmc: bool = False
+    pmc_counters: List[str] = field(default_factory=lambda: ["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_BUSY_CYCLES"])
+    # rates calibration
+    activity_acc_scale: float = 1.0
+    xgmi_kb_bytes: float = 1024.0
+    log_level: str = "info"
+
+    # ------------------------------------------------------------------ helpers
+    @property
+    def listen_addr(self) -> str:
+        return self.listen.rsplit(":", 1)[0] if ":" in self.listen else "0.0.0.0"
+
+    @property
+    def port(self) -> int:
+        return int(self.listen.rsplit(":", 1)[1]) if ":" in self.listen else int(self.listen)
+
+    def resolved_host(self) -> str:
+        return self.host or os.environ.get("NODE_NAME") or socket.gethostname() or "no_name"
+
+    def to_core(self) -> Dict[str, Any]:
+        """Dict consumed by gpumon._core.Exporter."""
+        return {
+            "backend": self.backend,
+            "amdsmi_lib": self.amdsmi_lib,
+            "devices": list(self.devices),
+            "interval_s": float(self.interval),
+            "processes": self.processes,
+            "link_every": int(self.link_every),
+            "sample_threads": int(self.sample_threads),
+            "listen_addr": self.listen_addr,
+            "port": self.port,
+            "http_threads": int(self.http_threads),
+            "host": self.resolved_host(),
+            "gzip": self.gzip,
+            "compat_families": self.compat_families,
+            "extended_families": self.extended_families,
+            "influx_url": self.influx_url,
+            "influx_extended": self.influx_extended,
+            "influx_every": int(self.influx_every),
+            "procfs_root": self.procfs_root,
+            "opt_in": self.opt_in_label,
+            "user_label": self.user_label,
+            "user_regex": self.user_regex,
+            "user_prefix": self.user_prefix,
+            "compat_user_rule": self.compat_user_rule,
+            "procfs_env_fallback": self.procfs_env_fallback,
+            "include_host_processes": self.include_host_processes,
+            "activity_acc_scale": float(self.activity_acc_scale),
+            "xgmi_kb_bytes": float(self.xgmi_kb_bytes),
+            "version": _version(),
+        }
+
+    # ------------------------------------------------------------------ sources
+    def apply_dict(self, d: Dict[str, Any]) -> "Config":
+        names = {f.name: f for f in dataclasses.fields(self)}
+        for k, v in (d or {}).items():
+            key = k.replace("-", "_")
+            if key not in names:
+                raise ValueError(f"unknown config key: {k}")
+            setattr(self, key, _coerce(names[key], v))
+        return self
+
+    def apply_env(self, env: Optional[Dict[str, str]] = None) -> "Config":
+        env = os.environ if env is None else env
+        if env.get("NODE_NAME"):
+            self.host = env["NODE_NAME"]
+        if env.get("INFLUXDB_URL"):
+            self.influx_url = env["INFLUXDB_URL"]
+        names = {f.name: f for f in dataclasses.fields(self)}
+        for k, v in env.items():
+            if k.startswith("GPUMON_") and k != "GPUMON_CONFIG" and k != "GPUMON_AMDSMI_LIB":
+                key = k[len("GPUMON_"):].lower()
+                if key in names:
+                    setattr(self, key, _coerce(names[key], v))
+        return self
+
+
+def _version() -> str:
+    from . import __version__
+
+    return __version__
+
+
+def _coerce(f: dataclasses.Field, v: Any) -> Any:
+    t = f.type if isinstance(f.type, str) else getattr(f.type, "__name__", str(f.type))
+    if v is None:
+        return v
+    if t in ("bool",):
+        if isinstance(v, bool):
+            return v
+        return str(v).strip().lower() in ("1", "true", "yes", "on")
+    if t in ("int",):
+        return int(v)
+    if t in ("float",):
+        return float(v)
+    if t.startswith("List[int]"):
+        if isinstance(v, str):
+            return [int(x) for x in v.split(",") if x.strip()]
+        return [int(x) for x in v]
+    if t.startswith("List[str]"):
+        if isinstance(v, str):
+            return [x.strip() for x in v.split(",") if x.strip()]
+        return [str(x) for x in v]
+    return str(v)
+
+
+def load_yaml(path: str) -> Dict[str, Any]:
+    with open(path, "r", encoding="utf-8") as fh:
+        data = yaml.safe_load(fh) or {}
+    if not isinstance(data, dict):
+        raise ValueError(f"{path}: top level must be a mapping")
+    return data.get("gpumon", data)
+
+
+def add_cli_args(p: argparse.ArgumentParser) -> None:
+    d = Config()
+    p.add_argument("--config", default=os.environ.get("GPUMON_CONFIG", ""), help="YAML config file")
+    p.add_argument("--backend", help=f"amdsmi | mock[:gpus=N,...] | auto (default {d.backend})")
+    p.add_argument("--devices", help="comma-separated hip ids to monitor (default all)")
+    p.add_argument("--interval", type=float, help=f"sampling interval seconds (default {d.interval})")
+    p.add_argument("--listen", help=f"ADDR:PORT for /metrics (default {d.listen})")
+    p.add_argument("--host", help="node name label (default $NODE_NAME, then hostname)")
+    p.add_argument("--influx-url", dest="influx_url", help="enable InfluxDB line-protocol push (default $INFLUXDB_URL)")
+    p.add_argument("--influx-extended", dest="influx_extended", action="store_true", default=None)
+    p.add_argument("--opt-in-label", dest="opt_in_label", help="only report pods with label KEY=VALUE")
+    p.add_argument("--user-regex", dest="user_regex", help="regex on pod name; group 1 = user")
+    p.add_argument("--user-label", dest="user_label", help="pod label holding the user name")
+    p.add_argument("--procfs-root", dest="procfs_root")
+    p.add_argument("--cri-socket", dest="cri_socket")
+    p.add_argument("--pod-resources-socket", dest="pod_resources_socket")
+    p.add_argument("--no-processes", dest="processes", action="store_false", default=None)
+    p.add_argument("--no-gzip", dest="gzip", action="store_false", default=None)
+    p.add_argument("--sample-threads", dest="sample_threads", type=int)
+    p.add_argument("--enable-probe-kernel", dest="enable_probe", action="store_true", default=None)
+    p.add_argument("--enable-pmc", dest="enable_pmc", action="store_true", default=None)
+    p.add_argument("--compat", action="store_true",
+                   help="reference behaviour: opt-in label mlgpu=mlgpu and 10 s interval")
+    p.add_argument("--log-level", dest="log_level")
+
+
+def from_args(ns: argparse.Namespace, env: Optional[Dict[str, str]] = None) -> Config:
+    cfg = Config()
+    if getattr(ns, "config", ""):
+        cfg.apply_dict(load_yaml(ns.config))
+    cfg.apply_env(env)
+    if getattr(ns, "compat", False):
+        cfg.opt_in_label = cfg.opt_in_label or "mlgpu=mlgpu"
+        cfg.interval = 10.0
+    names = {f.name: f for f in dataclasses.fields(cfg)}
+    for k, v in vars(ns).items():
+        if k in names and v is not None:
+            setattr(cfg, k, _coerce(names[k], v))
+    return cfg

@@ -1,0 +1,93 @@
+"""High-level Python handle over the native exporter + control plane + optional probe/PMC plugins.
+
+    from gpumon.config import Config
+    from gpumon.monitor import GpuMonitor
+    with GpuMonitor(Config(backend="mock:gpus=8", listen="127.0.0.1:0")) as mon:
+        print(mon.url, mon.metrics()[:200])
+
+Replaces the reference's process entrypoint (/root/reference/gpu.py:258-267): instead of a
+`while 1: main(); sleep(10)` loop that crashes on the first exception, the native sampler runs
+on its own thread with per-GPU error isolation, and this object only wires the pieces together.
+"""
+
+from __future__ import annotations
+
+import logging
+from typing import Optional
+
+from ._native import core
+from .config import Config
+
+log = logging.getLogger("gpumon")
+
+_LEVELS = {"debug": 0, "info": 1, "warn": 2, "warning": 2, "error": 3, "off": 4}
+
+
+class GpuMonitor:
+    def __init__(self, cfg: Optional[Config] = None, control_plane: bool = True):
+        self.cfg = cfg or Config()
+        self._core = core()
+        self._core.set_log_level(_LEVELS.get(self.cfg.log_level.lower(), 1))
+        self.ex = self._core.Exporter(self.cfg.to_core())
+        self.plane = None
+        self.probe = None
+        self.pmc = None
+        self._want_plane = control_plane
+        self.start_error = ""
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self) -> "GpuMonitor":
+        self.start_error = self.ex.start()
+        if self.start_error:
+            log.warning("backend not ready yet (will retry): %s", self.start_error)
+        if self._want_plane:
+            from .attribution.plane import ControlPlane
+
+            plane = ControlPlane(self.ex, self.cfg)
+            if plane.enabled:
+                self.plane = plane.start()
+        if self.cfg.enable_probe:
+            from .ops.probe import ProbeRunner
+
+            self.probe = ProbeRunner(self.ex, every_s=max(self.cfg.interval, 0.1) * self.cfg.probe_every).start()
+        if self.cfg.enable_pmc:
+            from .ops.pmc import PmcRunner
+
+            self.pmc = PmcRunner(self.ex, self.cfg.pmc_counters, every_s=max(self.cfg.interval, 0.1)).start()
+        return self
+
+    def stop(self) -> None:
+        for p in (self.pmc, self.probe, self.plane):
+            if p is not None:
+                try:
+                    p.stop()
+                except Exception:  # noqa: BLE001
+                    log.exception("plugin stop failed")
+        self.ex.stop()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+
+    # ------------------------------------------------------------------ accessors
+    @property
+    def port(self) -> int:
+        return self.ex.port
+
+    @property
+    def url(self) -> str:
+        host = self.cfg.listen_addr
+        if host in ("0.0.0.0", ""):
+            host = "127.0.0.1"
+        return f"http://{host}:{self.port}/metrics"
+
+    def metrics(self) -> str:
+        return self.ex.metrics_text()
+
+    def tick(self) -> dict:
+        return self.ex.tick()
+
+    def wait_ticks(self, n: int = 1, timeout_s: float = 30.0) -> bool:
+        return self.ex.wait_for_seq(self.ex.seq + n, timeout_s)

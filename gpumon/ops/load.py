@@ -1,0 +1,37 @@
+"""K2 synthetic HIP load used to validate the exporter under known conditions (bench + GPU tests).
+
+``SyntheticLoad(dev, kind)`` drives one GPU from a native C++ thread (no GIL) with back-to-back
+launches of the gfx950 kernels in ``csrc/hip/kernels.hip``:
+
+* ``mfma``  — bf16 ``v_mfma_f32_32x32x16_bf16`` burn, 2 waves per SIMD, 4 accumulators per wave;
+* ``hbm``   — 16 B/lane non-temporal copy over a ``hbm_bytes`` buffer pair (HBM3E bound);
+* ``mixed`` — alternating; ``duty`` < 1 inserts idle gaps (partial-utilisation validation).
+"""
+
+from __future__ import annotations
+
+from .._native import hip
+
+
+class SyntheticLoad:
+    def __init__(self, dev: int = 0, kind: str = "mixed", duty: float = 1.0, hbm_bytes: int = 1 << 30,
+                 mfma_iters: int = 8192):
+        self._g = hip().LoadGen(dev, kind, duty, hbm_bytes, mfma_iters)
+        self.dev = dev
+        self.kind = kind
+
+    def start(self) -> "SyntheticLoad":
+        self._g.start()
+        return self
+
+    def stop(self) -> None:
+        self._g.stop()
+
+    def stats(self) -> dict:
+        return self._g.stats()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *a):
+        self.stop()

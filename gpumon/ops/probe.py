@@ -1,0 +1,121 @@
+"""K1 probe runner: launches the gfx950 probe microkernel on every monitored GPU and exports its
+pinned-ring-buffer results as ``gpu_probe_*`` series.
+
+Per tick and device: one launch of ``blocks`` one-wave workgroups on a private non-blocking stream;
+completion is detected by polling a host-pinned arrival counter written with system-scope release
+atomics by the kernel (no hipDeviceSynchronize, no stall of the workload). Exported:
+
+* ``gpu_probe_xcd_blocks{xcd}``       — workgroups that ran on each XCD (per-XCD liveness)
+* ``gpu_probe_xcd_clock_mhz{xcd}``    — effective shader clock per XCD (Δs_memtime / Δs_memrealtime)
+* ``gpu_probe_latency_seconds``       — host launch -> all workgroups arrived (queueing behind the
+                                        workload is the contention signal)
+* ``gpu_probe_kernel_span_seconds``   — first start -> last end on the GPU's 100 MHz clock
+* ``gpu_probe_unique_cus``            — distinct (XCD, SE, CU) ids seen
+* ``gpu_probe_pending`` / ``gpu_probe_timeouts_total``
+
+SQ/GRBM perf counters are not readable from shader code on CDNA4; MFMA-busy and occupancy come
+from :mod:`gpumon.ops.pmc` (rocprofiler-sdk device counting).
+"""
+
+from __future__ import annotations
+
+import logging
+import threading
+import time
+from typing import Dict, List
+
+from .._native import hip
+
+log = logging.getLogger("gpumon.probe")
+
+
+class ProbeRunner:
+    def __init__(self, exporter, every_s: float = 1.0, blocks: int = 1024, spin_ticks: int = 200,
+                 timeout_s: float = 0.5):
+        self.ex = exporter
+        self.every_s = every_s
+        self.timeout_s = min(timeout_s, every_s)
+        self._hip = hip()
+        self.devs: List[dict] = [s for s in exporter.statics()]
+        n_hip = self._hip.device_count()
+        self.probes: Dict[int, object] = {}
+        for s in self.devs:
+            hid = s["hip_id"]
+            if 0 <= hid < n_hip:
+                self.probes[s["index"]] = self._hip.Probe(hid, blocks, 4, spin_ticks)
+        self.pending: Dict[int, int] = {}
+        self.timeouts: Dict[int, int] = {i: 0 for i in self.probes}
+        self.last: Dict[int, dict] = {}
+        self._stop = threading.Event()
+        self._th = None
+
+    def step(self) -> Dict[int, dict]:
+        """Launch (if the previous launch completed) and collect one round; returns results."""
+        for i, p in self.probes.items():
+            if i not in self.pending:
+                slot = p.launch()
+                if slot >= 0:
+                    self.pending[i] = slot
+        deadline = time.monotonic() + self.timeout_s
+        out = {}
+        for i, p in self.probes.items():
+            if i not in self.pending:
+                continue
+            r = p.poll(self.pending[i], max(0.0, deadline - time.monotonic()))
+            if r is not None:
+                out[i] = r
+                self.last[i] = r
+                del self.pending[i]
+            else:
+                self.timeouts[i] += 1
+        self._export()
+        return out
+
+    def _export(self):
+        series = []
+
+        def add(name, help_, dev, value, labels=None, typ="gauge"):
+            series.append({"name": name, "help": help_, "dev": dev, "value": float(value), "labels": labels or {},
+                           "type": typ})
+
+        for i in self.probes:
+            add("gpu_probe_pending", "1 if the last probe launch has not completed yet.", i, 1 if i in self.pending else 0)
+            add("gpu_probe_timeouts_total", "Probe polls that timed out (GPU saturated or hung).", i,
+                self.timeouts[i], typ="counter")
+            r = self.last.get(i)
+            if not r:
+                continue
+            add("gpu_probe_latency_seconds", "Probe host launch -> all workgroups arrived (pinned ring).", i,
+                r["host_latency_s"])
+            add("gpu_probe_kernel_span_seconds", "Probe first start -> last end on the GPU 100 MHz clock.", i,
+                r["gpu_span_s"])
+            add("gpu_probe_unique_cus", "Distinct compute units that ran probe workgroups.", i, r["unique_cus"])
+            for x, nb in enumerate(r["xcc_blocks"]):
+                if nb:
+                    add("gpu_probe_xcd_blocks", "Probe workgroups executed per XCD (liveness).", i, nb, {"xcd": str(x)})
+                    add("gpu_probe_xcd_clock_mhz", "Effective shader clock per XCD measured in-kernel.", i,
+                        r["xcc_clock_mhz"][x], {"xcd": str(x)})
+        self.ex.set_extra("probe", series)
+
+    def start(self):
+        self._th = threading.Thread(target=self._loop, name="gpumon-probe", daemon=True)
+        self._th.start()
+        return self
+
+    def _loop(self):
+        while not self._stop.is_set():
+            t0 = time.monotonic()
+            try:
+                self.step()
+            except Exception:  # noqa: BLE001
+                log.exception("probe step failed")
+            self._stop.wait(max(0.0, self.every_s - (time.monotonic() - t0)))
+
+    def stop(self):
+        self._stop.set()
+        if self._th:
+            self._th.join(timeout=5)
+        # drain in-flight launches before the Probe objects (and their pinned ring) go away
+        for i, slot in list(self.pending.items()):
+            self.probes[i].poll(slot, 2.0)
+        self.ex.set_extra("probe", [])

@@ -1,0 +1,45 @@
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box with -m gpu)")
+    config.addinivalue_line("markers", "slow: takes more than a few seconds")
+    # The native core is built in-tree; build it once if this checkout has not been built yet.
+    try:
+        import gpumon._core  # noqa: F401
+    except ImportError:
+        subprocess.run(["make", "-C", ROOT, "-j8", "core"], check=True, stdout=subprocess.DEVNULL)
+
+
+@pytest.fixture
+def core():
+    from gpumon import core as _c
+
+    return _c()
+
+
+@pytest.fixture
+def mock_exporter(core):
+    """Factory for started mock exporters on an ephemeral localhost port; stopped at teardown."""
+    made = []
+
+    def make(**over):
+        cfg = {"backend": "mock:gpus=2", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0.0,
+               "host": "node-a", "http_threads": 1}
+        cfg.update(over)
+        ex = core.Exporter(cfg)
+        ex.start()
+        made.append(ex)
+        return ex
+
+    yield make
+    for ex in made:
+        ex.stop()

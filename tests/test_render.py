@@ -1,0 +1,109 @@
+"""Exposition format: Prometheus text validity, reference-compatible names, escaping, Influx lines.
+
+Reference schema: node_gpu (/root/reference/gpu.py:136-143) and pod_gpu (gpu.py:206-216).
+"""
+
+import math
+import re
+
+import pytest
+
+from gpumon.export import promtext
+
+
+def test_prometheus_text_is_valid_and_has_reference_families(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=4")
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    for name in ["node_gpu_gpu_util", "node_gpu_mem_util", "node_gpu_mem_used", "node_gpu_mem_total",
+                 "node_gpu_mem_free"]:
+        assert name in fam, name
+        assert len(fam[name]["samples"]) == 4
+        assert fam[name]["type"] == "gauge"
+    # labels: host + gpu_id on every device series (reference tags host, gpu_id)
+    for _, labels, _ in fam["node_gpu_gpu_util"]["samples"]:
+        assert labels["host"] == "node-a"
+        assert labels["gpu_id"] in {"0", "1", "2", "3"}
+        assert "gpu_uuid" in labels and "bdf" in labels
+
+
+def test_mem_fields_consistent(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1")
+    fam = promtext.parse(ex.metrics_text())
+    total = promtext.one(fam, "node_gpu_mem_total", gpu_id="0")
+    used = promtext.one(fam, "node_gpu_mem_used", gpu_id="0")
+    free = promtext.one(fam, "node_gpu_mem_free", gpu_id="0")
+    util = promtext.one(fam, "node_gpu_mem_util", gpu_id="0")
+    assert total == 294896  # MI355X: 288 GiB HBM3E in MiB
+    assert used + free == total
+    assert util == pytest.approx(used * 100.0 / total, rel=1e-3)
+    assert promtext.one(fam, "gpu_vram_total_bytes", gpu_id="0") == total * 1048576
+
+
+def test_mi355x_families_present(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1")
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert len(promtext.values(fam, "gpu_xcd_busy_percent")) == 8          # 8 XCDs
+    assert len(promtext.values(fam, "gpu_xgmi_link_up")) == 7              # 7 peer links
+    assert promtext.values(fam, "gpu_temperature_celsius", sensor="hotspot")
+    assert promtext.one(fam, "gpu_power_limit_watts") == 1400
+    assert promtext.values(fam, "gpu_energy_joules_total")[0] > 0
+    assert fam["gpu_energy_joules_total"]["type"] == "counter"
+    assert promtext.one(fam, "gpumon_gpus", state="total") == 1
+
+
+def test_unsupported_fields_are_omitted_not_zero(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1,unsupported=temp_hotspot;xcd")
+    fam = promtext.parse(ex.metrics_text())
+    assert not promtext.values(fam, "gpu_temperature_celsius", sensor="hotspot")
+    assert promtext.values(fam, "gpu_temperature_celsius", sensor="mem")
+    assert "gpu_xcd_busy_percent" not in fam  # empty families are dropped entirely
+
+
+def test_label_escaping(core):
+    assert core.escape_label_value('a"b\\c\nd') == 'a\\"b\\\\c\\nd'
+    assert core.escape_influx_tag("a b,c=d") == "a\\ b\\,c\\=d"
+    assert core.escape_influx_tag("") == "-"
+    assert core.escape_influx_field_str('x"y\\') == 'x\\"y\\\\'
+
+
+@pytest.mark.parametrize("v,s", [(0.0, "0"), (42.0, "42"), (1.5, "1.5"), (float("nan"), "NaN"),
+                                 (float("inf"), "+Inf"), (-3.0, "-3"), (309220868096.0, "309220868096")])
+def test_number_format(core, v, s):
+    assert core.format_double(v) == s
+
+
+def test_influx_node_gpu_line_matches_reference_layout(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=2")
+    lines = [l for l in ex.influx_text().splitlines() if l.startswith("node_gpu,")]
+    assert len(lines) == 2
+    # gpu.py:136-143: node_gpu,host=H,gpu_id=K gpu_util=..,mem_util=..,mem_used=..,mem_total=..,node="H",gid=K,mem_free=..
+    pat = re.compile(r'^node_gpu,host=node-a,gpu_id=(\d) gpu_util=[\d.]+,mem_util=[\d.e-]+,mem_used=\d+,'
+                     r'mem_total=\d+,node="node-a",gid=\1,mem_free=\d+ \d{19}$')
+    for l in lines:
+        assert pat.match(l), l
+
+
+def test_influx_pod_gpu_line_matches_reference_layout(mock_exporter):
+    import os
+
+    ex = mock_exporter(backend="mock:gpus=1")
+    ex.mock_set_procs([{"pid": os.getpid(), "device": 0, "name": "python train.py", "vram_bytes": 2 ** 30}])
+    ex.tick()
+    lines = [l for l in ex.influx_text().splitlines() if l.startswith("pod_gpu,")]
+    assert len(lines) == 1
+    l = lines[0]
+    # tags (gpu.py:207-208) then fields (gpu.py:209-216), escaped
+    assert re.match(r"^pod_gpu,host=node-a,namespace=-,gpu_id=0,containerid=[-0-9a-f]+,pid_t=\d+,gpu_util_t=[\d.]+,"
+                    r"user_name_t=- procressname=\"python train.py\",podname=\"-\",pid=\"\d+\",gpu_id_v=\"0\","
+                    r"node=\"node-a\",user_name=\"-\",gpu_util=[\d.]+,used_memory=1024 \d{19}$", l), l
+
+
+def test_no_nan_in_exposition(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=3")
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    for f in fam.values():
+        for _, _, v in f["samples"]:
+            assert not math.isnan(v)
