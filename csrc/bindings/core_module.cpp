@@ -68,6 +68,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "compat_user_rule", &a.compat_user_rule);
   get(d, "procfs_env_fallback", &a.procfs_env_fallback);
   get(d, "include_host_processes", &a.include_host_processes);
+  get(d, "verify_kfd", &a.verify_kfd);
   if (d.contains("mock") && !d["mock"].is_none()) {
     py::dict m = d["mock"].cast<py::dict>();
     get(m, "gpus", &c.mock.gpus);
@@ -444,6 +445,7 @@ PYBIND11_MODULE(_core, m) {
              ProcIdentity id = e.attributor().resolve(pid);
              py::dict d;
              d["valid"] = id.valid;
+             d["pid_mismatch"] = id.pid_mismatch;
              d["in_container"] = id.in_container;
              d["opted_in"] = id.opted_in;
              d["comm"] = id.comm;

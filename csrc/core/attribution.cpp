@@ -1,7 +1,11 @@
 #include "attribution.h"
 
+#include <dirent.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cctype>
+#include <cstring>
 #include <unordered_set>
 
 #include "common.h"
@@ -202,6 +206,28 @@ bool Attributor::read_stat(uint32_t pid, uint64_t* starttime, std::string* comm)
   return true;
 }
 
+int Attributor::holds_kfd(uint32_t pid) const {
+  std::string dir = cfg_.procfs_root + "/" + std::to_string(pid) + "/fd";
+  DIR* d = opendir(dir.c_str());
+  if (!d) return -1;
+  int found = 0;
+  char link[256];
+  int scanned = 0;
+  while (struct dirent* ent = readdir(d)) {
+    if (ent->d_name[0] == '.') continue;
+    if (++scanned > 65536) break;
+    ssize_t n = readlink((dir + "/" + ent->d_name).c_str(), link, sizeof link - 1);
+    if (n <= 0) continue;
+    link[n] = 0;
+    if (strcmp(link, "/dev/kfd") == 0) {
+      found = 1;
+      break;
+    }
+  }
+  closedir(d);
+  return found;
+}
+
 void Attributor::read_env_fallback(uint32_t pid, CacheEntry* e) const {
   e->env_done = true;
   std::string base = cfg_.procfs_root + "/" + std::to_string(pid);
@@ -248,14 +274,25 @@ ProcIdentity Attributor::resolve(uint32_t pid) {
       CacheEntry ne;
       ne.starttime = st;
       ne.comm = comm;
+      if (cfg_.verify_kfd) ne.kfd = holds_kfd(pid);
       std::string cg;
-      if (read_file(cfg_.procfs_root + "/" + std::to_string(pid) + "/cgroup", &cg, 65536))
+      if (ne.kfd != 0 &&
+          read_file(cfg_.procfs_root + "/" + std::to_string(pid) + "/cgroup", &cg, 65536))
         ne.cg = parse_cgroup(cg);
       cache_[pid] = std::move(ne);
       e = &cache_[pid];
     }
   }
   // `e` stays valid: only this (sampler) thread inserts/erases cache entries.
+  if (e->kfd == 0) {
+    // Same number, different process (exporter not in the host PID namespace): attribute nothing.
+    id.valid = false;
+    id.pid_mismatch = true;
+    id.comm.clear();
+    id.source = "pidns";
+    id.opted_in = opted_in({}) && cfg_.include_host_processes;
+    return id;
+  }
   const CgroupInfo& cg = e->cg;
   id.in_container = cg.found;
   id.runtime = cg.runtime;

@@ -66,10 +66,15 @@ struct AttributionConfig {
   bool compat_user_rule = true;
   bool procfs_env_fallback = true;          // HOSTNAME + SA namespace of the process
   bool include_host_processes = true;       // GPU processes not in any container
+  // amdsmi reports KFD (host-namespace) PIDs. Without hostPID the same number in our /proc can be
+  // an unrelated process: require /proc/<pid>/fd to hold /dev/kfd before trusting /proc/<pid>
+  // (an unreadable fd dir is treated as "unknown", not as a mismatch).
+  bool verify_kfd = true;
 };
 
 struct ProcIdentity {
   bool valid = false;           // /proc/<pid> readable
+  bool pid_mismatch = false;    // /proc/<pid> exists but does not hold /dev/kfd (other pid ns)
   bool in_container = false;
   bool opted_in = true;
   uint64_t starttime = 0;
@@ -112,7 +117,9 @@ class Attributor {
     std::string comm;
     std::string env_pod, env_ns;  // procfs fallback values
     bool env_done = false;
+    int kfd = -1;                 // 1 holds /dev/kfd, 0 does not, -1 unknown (unreadable)
   };
+  int holds_kfd(uint32_t pid) const;
   AttributionConfig cfg_;
   std::unique_ptr<std::regex> user_re_;
   std::string opt_key_, opt_val_;

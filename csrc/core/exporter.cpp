@@ -122,11 +122,11 @@ std::unique_ptr<Backend> make_backend(const std::string& spec, std::string* err)
 
 // ---------------------------------------------------------------------------------------------
 Exporter::Exporter(ExporterConfig cfg)
-    : cfg_(std::move(cfg)),
-      attr_(std::make_unique<Attributor>(cfg_.attribution)),
-      sample_hist_(latency_buckets()),
-      scrape_hist_(latency_buckets()) {
+    : cfg_(std::move(cfg)), sample_hist_(latency_buckets()), scrape_hist_(latency_buckets()) {
   if (cfg_.host.empty()) cfg_.host = "no_name";
+  // Mock processes are fake PIDs: there is no /dev/kfd handle to verify.
+  if (starts_with(cfg_.backend, "mock")) cfg_.attribution.verify_kfd = false;
+  attr_ = std::make_unique<Attributor>(cfg_.attribution);
 }
 
 Exporter::~Exporter() { stop(); }

@@ -62,6 +62,7 @@ bool set_nonblock(int fd) {
 long parse_request(const std::string& in, HttpRequest* r) {
   size_t end = in.find("\r\n\r\n");
   if (end == std::string::npos) return in.size() > kMaxHeader ? -2 : 0;
+  if (end > kMaxHeader) return -2;
   size_t le = in.find("\r\n");
   std::string_view line(in.data(), le);
   size_t s1 = line.find(' ');

@@ -1,0 +1,174 @@
+"""/metrics server: endpoints, keep-alive, gzip, HEAD, errors, concurrency, and latency.
+
+The reference has no scrape endpoint (push-only, /root/reference/gpu.py:145); BASELINE.json's
+headline metric is p99 /metrics latency, so the server is tested for correctness under load and
+for not tearing responses while the sampler swaps snapshots.
+"""
+
+import gzip
+import http.client
+import socket
+import threading
+
+import pytest
+
+from gpumon.export import promtext
+
+
+def _get(port, path, headers=None, method="GET"):
+    c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+    c.request(method, path, headers=headers or {})
+    r = c.getresponse()
+    body = r.read()
+    c.close()
+    return r.status, dict(r.getheaders()), body
+
+
+def test_metrics_endpoint(mock_exporter):
+    ex = mock_exporter()
+    st, h, body = _get(ex.port, "/metrics")
+    assert st == 200
+    assert h["Content-Type"].startswith("text/plain; version=0.0.4")
+    promtext.parse(body.decode())
+    assert int(h["Content-Length"]) == len(body)
+
+
+def test_gzip_negotiation(mock_exporter):
+    ex = mock_exporter()
+    st, h, body = _get(ex.port, "/metrics", {"Accept-Encoding": "gzip, deflate"})
+    assert st == 200 and h.get("Content-Encoding") == "gzip"
+    plain = gzip.decompress(body).decode()
+    assert plain == ex.metrics_text()
+    assert len(body) < len(plain) / 3
+
+
+def test_gzip_disabled(mock_exporter):
+    ex = mock_exporter(gzip=False)
+    st, h, body = _get(ex.port, "/metrics", {"Accept-Encoding": "gzip"})
+    assert st == 200 and "Content-Encoding" not in h
+
+
+def test_head_and_404_and_index(mock_exporter):
+    ex = mock_exporter()
+    st, h, body = _get(ex.port, "/metrics", method="HEAD")
+    assert st == 200 and body == b"" and int(h["Content-Length"]) > 0
+    assert _get(ex.port, "/nope")[0] == 404
+    assert _get(ex.port, "/")[0] == 200
+    assert _get(ex.port, "/metrics?x=1")[0] == 200
+
+
+def test_method_not_allowed(mock_exporter):
+    ex = mock_exporter()
+    assert _get(ex.port, "/metrics", method="POST")[0] == 405
+
+
+def test_health_endpoints(mock_exporter):
+    ex = mock_exporter()
+    assert _get(ex.port, "/healthz")[0] == 200
+    assert _get(ex.port, "/readyz")[0] == 200
+
+
+def test_keepalive_many_requests_one_connection(mock_exporter):
+    ex = mock_exporter()
+    c = http.client.HTTPConnection("127.0.0.1", ex.port, timeout=5)
+    for _ in range(50):
+        c.request("GET", "/metrics")
+        r = c.getresponse()
+        assert r.status == 200
+        r.read()
+    c.close()
+
+
+def test_pipelined_requests(mock_exporter):
+    ex = mock_exporter()
+    s = socket.create_connection(("127.0.0.1", ex.port), timeout=5)
+    s.sendall(b"GET /healthz HTTP/1.1\r\nHost: x\r\n\r\nGET /healthz HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+    data = b""
+    while True:
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    s.close()
+    assert data.count(b"HTTP/1.1 200 OK") == 2
+
+
+def test_http10_closes(mock_exporter):
+    ex = mock_exporter()
+    s = socket.create_connection(("127.0.0.1", ex.port), timeout=5)
+    s.sendall(b"GET /healthz HTTP/1.0\r\n\r\n")
+    data = b""
+    while True:
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        data += chunk
+    assert b"Connection: close" in data
+
+
+def test_bad_request_and_oversized_header(mock_exporter):
+    ex = mock_exporter()
+    s = socket.create_connection(("127.0.0.1", ex.port), timeout=5)
+    s.sendall(b"GARBAGE\r\n\r\n")
+    assert b"400" in s.recv(4096)
+    s.close()
+    s = socket.create_connection(("127.0.0.1", ex.port), timeout=5)
+    s.sendall(b"GET /metrics HTTP/1.1\r\nX: " + b"a" * 20000 + b"\r\n\r\n")
+    assert b"431" in s.recv(4096)
+    s.close()
+
+
+def test_concurrent_scrapes_while_ticking_no_torn_bodies(mock_exporter, core):
+    """Snapshots are immutable: every response body must be one complete, parseable exposition."""
+    ex = mock_exporter(backend="mock:gpus=8", interval_s=0.01, http_threads=2)
+    errors = []
+
+    def worker():
+        c = http.client.HTTPConnection("127.0.0.1", ex.port, timeout=5)
+        for _ in range(12):
+            c.request("GET", "/metrics")
+            r = c.getresponse()
+            body = r.read()
+            try:
+                promtext.parse(body.decode())
+                assert body.endswith(b"\n")
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+        c.close()
+
+    ts = [threading.Thread(target=worker) for _ in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors[:3]
+    assert ex.self_stats()["ticks"] > 5
+
+
+def test_native_scrape_load_latency(mock_exporter, core):
+    ex = mock_exporter(backend="mock:gpus=8", interval_s=0.05)
+    r = core.scrape_load("127.0.0.1", ex.port, "/metrics", n_requests=400, concurrency=4)
+    lat = sorted(r["latencies_s"])
+    assert r["errors"] == 0 and len(lat) == 400
+    p99 = lat[int(0.99 * (len(lat) - 1))]
+    assert p99 < 0.05, p99  # pre-rendered snapshot: sub-millisecond typical, generous CI bound
+    assert ex.self_stats()["scrapes"] >= 400
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.values(fam, "gpumon_scrape_duration_seconds_count")[0] >= 1
+
+
+def test_port_conflict_reports_error(core):
+    a = core.Exporter({"backend": "mock", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0})
+    a.start()
+    try:
+        b = core.Exporter({"backend": "mock", "listen_addr": "127.0.0.1", "port": a.port, "interval_s": 0})
+        # SO_REUSEPORT lets a second exporter bind the same port only for the same user; either it
+        # starts (shared port) or it fails loudly -- it must never hang.
+        try:
+            b.start()
+            b.stop()
+        except RuntimeError as e:
+            assert "bind" in str(e)
+    finally:
+        a.stop()
