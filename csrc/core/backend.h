@@ -98,7 +98,7 @@ class MockBackend : public Backend {
   mutable std::mutex mu_;
   std::vector<double> forced_util_;
   std::vector<uint64_t> calls_;
-  std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_;
+  std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
   std::map<std::pair<uint32_t, int>, uint64_t> proc_gfx_ns_;
   int64_t t0_ns_ = 0;
   std::vector<int64_t> last_ns_;

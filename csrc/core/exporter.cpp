@@ -95,6 +95,7 @@ static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
     else if (k == "fail_every") base.fail_every = atoi(v.c_str());
     else if (k == "hang_ms") base.hang_ms = atof(v.c_str());
     else if (k == "seed") base.seed = strtoull(v.c_str(), nullptr, 10);
+    else if (k == "firmware_hz") base.firmware_hz = atof(v.c_str());
     else if (k == "unsupported") base.unsupported = split(v, ';');
   }
   return base;

@@ -73,6 +73,7 @@ bool MockBackend::init(std::string* err) {
   xgmi_wr_.assign(n * kMaxLinks, 0);
   busy_acc_.assign(n * kMaxXcc, 0);
   acc_counter_.assign(n, 0);
+  gfx_act_acc_.assign(n, 0);
   t0_ns_ = mono_ns();
   last_ns_.assign(n, t0_ns_);
   return true;
@@ -168,7 +169,7 @@ void MockBackend::sample(int i, DeviceSample* out) {
   last_ns_[i] = now;
   // firmware time advances in quanta of 1/firmware_hz
   uint64_t fw_tick = static_cast<uint64_t>(t * cfg_.firmware_hz);
-  a.firmware_ts = fw_tick * static_cast<uint64_t>(1e8 / std::max(1.0, cfg_.firmware_hz));
+  a.firmware_ts = (fw_tick + 1) * static_cast<uint64_t>(1e8 / std::max(1e-3, cfg_.firmware_hz));
   a.system_clock_ns = static_cast<uint64_t>(now);
   energy_[i] += static_cast<uint64_t>(power * elapsed / 15.3e-6);
   a.energy = energy_[i];
@@ -179,14 +180,15 @@ void MockBackend::sample(int i, DeviceSample* out) {
   a.has_residency = true;
   a.ppt_res = util > 90 ? acc_counter_[i] / 10 : 0;
   a.has_activity_acc = true;
-  a.gfx_activity_acc = static_cast<uint64_t>(acc_counter_[i] * util / 100.0);
+  gfx_act_acc_[i] += static_cast<uint64_t>(util * elapsed * 100000.0);
+  a.gfx_activity_acc = gfx_act_acc_[i];
   int nx = cfg_.n_xcd;
   out->n_xcd = nx;
   a.n_xcd_acc = nx;
   for (int k = 0; k < nx && k < kMaxXcc; ++k) {
     double xb = std::max(0.0, std::min(100.0, util + (k - nx / 2) * 0.5));
     out->xcd_busy[k] = std::floor(xb);
-    busy_acc_[i * kMaxXcc + k] += static_cast<uint64_t>(xb * elapsed * 100.0);
+    busy_acc_[i * kMaxXcc + k] += static_cast<uint64_t>(xb * elapsed * 100000.0);
     a.xcd_busy_acc[k] = busy_acc_[i * kMaxXcc + k];
     out->gfxclks[k] = v[F_GFXCLK_CUR];
   }

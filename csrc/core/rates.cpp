@@ -50,9 +50,9 @@ void compute_rates(const DeviceSample& prev, const DeviceSample& cur, const Rate
   if (have_acc && a.has_activity_acc && b.has_activity_acc) {
     uint64_t dg = 0, dm = 0;
     if (acc_delta(a.gfx_activity_acc, b.gfx_activity_acc, true, &dg))
-      out->gfx_activity_avg_pct = std::min(100.0, dg * cfg.activity_acc_scale / dacc * 100.0);
+      out->gfx_activity_avg_pct = std::min(100.0, dg * cfg.activity_acc_scale / dacc);
     if (acc_delta(a.mem_activity_acc, b.mem_activity_acc, true, &dm))
-      out->mem_activity_avg_pct = std::min(100.0, dm * cfg.activity_acc_scale / dacc * 100.0);
+      out->mem_activity_avg_pct = std::min(100.0, dm * cfg.activity_acc_scale / dacc);
   }
   if (have_acc) {
     int nx = std::min(a.n_xcd_acc, b.n_xcd_acc);
@@ -60,7 +60,7 @@ void compute_rates(const DeviceSample& prev, const DeviceSample& cur, const Rate
     for (int k = 0; k < nx; ++k) {
       uint64_t dx = 0;
       out->xcd_busy_avg[k] = acc_delta(a.xcd_busy_acc[k], b.xcd_busy_acc[k], false, &dx)
-                                 ? std::min(100.0, dx * cfg.activity_acc_scale / dacc * 100.0)
+                                 ? std::min(100.0, dx * cfg.activity_acc_scale / dacc)
                                  : kNaN;
     }
   }

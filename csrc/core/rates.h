@@ -10,7 +10,9 @@
 
 namespace gpumon {
 
-// Counts-per-percent scale of gfx_activity_acc / gfx_busy_acc relative to accumulation_counter.
+// gfx_activity_acc / gfx_busy_acc accumulate the instantaneous busy % once per
+// accumulation_counter tick, so avg% = d(acc) / d(accumulation_counter) (MI355X: ~3.45 % lifetime
+// average read on an idle box = 724166309 / 209992046). `activity_acc_scale` is a correction hook.
 // Calibrated on MI355X (see tests/gpu/test_amdsmi_backend.py); overridable for other firmware.
 struct RateConfig {
   double activity_acc_scale = 1.0;   // avg% = d(acc) / d(accumulation_counter) * scale

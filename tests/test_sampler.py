@@ -1,0 +1,152 @@
+"""Sampler loop behaviour: deadline cadence, rates from accumulators, per-GPU fault isolation,
+stale-firmware detection, watchdog/health, backend init failure.
+
+Reference failure model: no try/except anywhere, one failure kills the agent and
+the pod restarts; the cadence is `sleep(10)` after a variable-length cycle (gpu.py:261-263).
+"""
+
+import time
+
+import pytest
+
+from gpumon.export import promtext
+
+
+def test_deadline_cadence(core):
+    ex = core.Exporter({"backend": "mock:gpus=2", "serve_http": False, "interval_s": 0.05})
+    ex.start()
+    t0 = time.monotonic()
+    s0 = ex.seq
+    assert ex.wait_for_seq(s0 + 10, 5.0)
+    dt = time.monotonic() - t0
+    ex.stop()
+    assert 0.4 < dt < 1.0, dt  # 10 ticks at 50 ms, on a fixed grid
+
+
+def test_overrun_is_counted_and_grid_kept(core):
+    ex = core.Exporter({"backend": "mock:gpus=1,hang_ms=30", "serve_http": False, "interval_s": 0.01})
+    ex.start()
+    time.sleep(0.5)
+    st = ex.self_stats()
+    ex.stop()
+    assert st["overruns"] > 0
+    assert 8 <= st["ticks"] <= 20
+
+
+def test_power_rate_from_energy_accumulator(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1,mode=load")
+    ex.tick()
+    time.sleep(0.2)
+    ex.tick()
+    r = ex.rates()[0]
+    f = ex.samples()[0]["fields"]
+    assert r["valid"]
+    assert r["power_from_energy_w"] == pytest.approx(f["power_cur"], rel=0.1)
+    assert all(x == pytest.approx(100.0, abs=5) for x in r["xcd_busy_avg"])
+    assert len(r["xgmi_rd_Bps"]) == 8 and r["xgmi_rd_Bps"][1] > 1e9
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_power_interval_watts") > 0
+    assert promtext.one(fam, "gpu_violation_percent", kind="ppt") > 0  # mock: PPT residency at 100 % util
+    assert promtext.values(fam, "gpu_xgmi_read_bytes_per_second", link="1")[0] > 1e9
+    util = promtext.values(fam, "gpu_xgmi_link_utilization_ratio")
+    assert util and all(0 <= u <= 1.5 for u in util)
+
+
+def test_one_failing_gpu_does_not_hide_others(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=3,fail_device=1,fail_every=-1")
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_up", gpu_id="0") == 1
+    assert promtext.one(fam, "gpu_up", gpu_id="1") == 0
+    assert promtext.one(fam, "gpu_up", gpu_id="2") == 1
+    assert len(promtext.values(fam, "node_gpu_gpu_util")) == 2
+    assert promtext.one(fam, "gpumon_sample_errors_total", gpu_id="1") >= 1
+
+
+def test_intermittent_failure_recovers(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1")
+    ex.mock_set_fail(0, 2)  # every 2nd call fails
+    oks = []
+    for _ in range(6):
+        ex.tick()
+        oks.append(ex.samples()[0]["ok"])
+    assert oks.count(True) == 3 and oks.count(False) == 3
+
+
+def test_stale_firmware_table_detected(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1,firmware_hz=0.5")
+    ex.tick()
+    ex.tick()  # back-to-back: the fake firmware table (refreshing every 2 s) has not advanced
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_sample_fresh") == 0
+    assert promtext.one(fam, "gpumon_stale_samples_total") >= 1
+
+
+def test_health_goes_503_when_sampler_stalls(core):
+    import http.client
+
+    ex = core.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0.05,
+                        "health_stale_s": 0.3})
+    ex.start()
+    try:
+        def status(path):
+            c = http.client.HTTPConnection("127.0.0.1", ex.port, timeout=5)
+            c.request("GET", path)
+            r = c.getresponse()
+            r.read()
+            return r.status
+
+        assert status("/healthz") == 200
+        ex.mock_set_hang_ms(1500)  # a hung device call
+        time.sleep(0.9)
+        assert status("/healthz") == 503
+        assert status("/metrics") == 200  # last good snapshot still served
+        ex.mock_set_hang_ms(0)
+        time.sleep(2.0)
+        assert status("/healthz") == 200
+    finally:
+        ex.mock_set_hang_ms(0)
+        ex.stop()
+
+
+def test_amdsmi_unavailable_is_loud_not_silent(core):
+    """On a host without libamd_smi / GPUs the exporter keeps serving self-metrics, reports
+    backend_up 0 / readyz 503, and never pretends with mock data."""
+    import http.client
+    import os
+
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("GPU host")
+    ex = core.Exporter({"backend": "amdsmi", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                        "init_retry_s": 60})
+    err = ex.start()
+    try:
+        assert err  # reason is reported
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpumon_backend_up") == 0
+        assert "node_gpu_gpu_util" not in fam
+        c = http.client.HTTPConnection("127.0.0.1", ex.port, timeout=5)
+        c.request("GET", "/readyz")
+        assert c.getresponse().status == 503
+    finally:
+        ex.stop()
+
+
+def test_parallel_device_sampling(core):
+    ex = core.Exporter({"backend": "mock:gpus=8,hang_ms=20", "serve_http": False, "interval_s": 0,
+                        "sample_threads": 8})
+    ex.start()
+    t0 = time.monotonic()
+    info = ex.tick()
+    dt = time.monotonic() - t0
+    ex.stop()
+    assert info["devices_ok"] == 8
+    assert dt < 0.12, dt  # 8 x 20 ms sequential would be >= 160 ms
+
+
+def test_device_filter(core):
+    ex = core.Exporter({"backend": "mock:gpus=8", "serve_http": False, "interval_s": 0, "devices": [1, 3]})
+    ex.start()
+    st = ex.statics()
+    ex.stop()
+    assert [s["gpu_id"] for s in st] == ["1", "3"]
