@@ -28,8 +28,8 @@ BIN       := bin/gpumon-exporter
 HIP_SRC   := $(wildcard csrc/hip/*.hip)
 HIP_HDR   := $(wildcard csrc/hip/*.h)
 
-.PHONY: all core hip clean asan
-all: core hip
+.PHONY: all core hip pmc clean asan tsan
+all: core hip pmc
 core: $(PYEXT) $(BIN)
 hip: $(HIPEXT)
 
@@ -72,4 +72,11 @@ tsan: $(CORE_SRC) csrc/exporter_main.cpp
 	  $(CORE_SRC) csrc/exporter_main.cpp -o bin/gpumon-exporter-tsan $(LIBS)
 
 clean:
-	rm -rf build bin gpumon/_core*.so gpumon/_hip*.so
+	rm -rf build bin gpumon/_core*.so gpumon/_hip*.so gpumon/_pmc*.so
+
+# rocprofiler-sdk device counting module (host-only C++; links the ROCm profiler + HSA runtime).
+PMCEXT := gpumon/_pmc$(EXT)
+pmc: $(PMCEXT)
+$(PMCEXT): csrc/pmc/pmc_module.cpp
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared -fvisibility=hidden -I$(ROCM)/include -I$(PYINC) -I$(PYBIND) $< \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrocprofiler-sdk -lhsa-runtime64 -o $@

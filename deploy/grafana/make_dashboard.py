@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Generate deploy/grafana/gpumon-dashboard.json (Grafana 10 schema, Prometheus datasource).
+
+Recreates the reference dashboards (described in SURVEY.md §2.5 from /root/reference/img/*.png)
+in PromQL, then adds MI355X panels:
+  * grafana.png              — per-card gauges "当前使用显存" (VRAM used) and "GPU使用率" (GPU util)
+  * 2019 screenshot          — table "容器使用GPU情况", stats GPU总数 / 已占GPU数量 / 占GPU未开始使用 /
+                               占GPU已使用完毕, time series "每个用户占用GPU的数量"
+  * [new] per-XCD busy, xGMI per-link bandwidth, power/energy, temperatures, probe clocks,
+          exporter self-metrics (sample + scrape latency p99).
+"""
+
+import json
+import os
+
+DS = {"type": "prometheus", "uid": "${datasource}"}
+HOST = 'host=~"$host"'
+_id = [0]
+
+
+def panel(title, typ, targets, x, y, w, h, **kw):
+    _id[0] += 1
+    p = {"id": _id[0], "title": title, "type": typ, "datasource": DS,
+         "gridPos": {"x": x, "y": y, "w": w, "h": h},
+         "targets": [{"expr": e, "legendFormat": lf, "refId": chr(65 + i), "datasource": DS,
+                      **({"format": "table", "instant": True} if typ == "table" else {})}
+                     for i, (e, lf) in enumerate(targets)]}
+    p.update(kw)
+    return p
+
+
+def build():
+    panels = []
+    y = 0
+    # --- reference: allocation stat panels (2019 screenshot) ---
+    stats = [("GPU总数 (GPUs total)", f'sum(gpumon_gpus{{{HOST},state="total"}})'),
+             ("已占GPU数量 (allocated)", f'sum(gpumon_gpus{{{HOST},state="allocated"}})'),
+             ("占GPU未开始使用 (allocated, idle)", f'sum(gpumon_gpus{{{HOST},state="allocated_idle"}})'),
+             ("占GPU已使用完毕 (allocated, in use)", f'sum(gpumon_gpus{{{HOST},state="allocated_active"}})')]
+    for i, (t, e) in enumerate(stats):
+        panels.append(panel(t, "stat", [(e, "")], 6 * i, y, 6, 4))
+    y += 4
+    # --- reference: per-card gauges (grafana.png) ---
+    panels.append(panel("当前使用显存 (VRAM used, MiB)", "gauge",
+                        [(f'node_gpu_mem_used{{{HOST}}}', "{{host}} gpu{{gpu_id}}")], 0, y, 12, 7,
+                        fieldConfig={"defaults": {"unit": "mbytes", "min": 0, "max": 294896}, "overrides": []}))
+    panels.append(panel("GPU使用率 (GPU utilization %)", "gauge",
+                        [(f'node_gpu_gpu_util{{{HOST}}}', "{{host}} gpu{{gpu_id}}")], 12, y, 12, 7,
+                        fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
+    y += 7
+    # --- reference: container table + GPUs per user ---
+    panels.append(panel("容器使用GPU情况 (GPU usage by container)", "table",
+                        [(f'pod_gpu_used_memory{{{HOST}}}', ""), (f'pod_gpu_gpu_util{{{HOST}}}', "")], 0, y, 16, 9,
+                        transformations=[{"id": "merge"}, {"id": "organize", "options": {
+                            "excludeByName": {"Time": False, "__name__": True, "gpu_uuid": True},
+                            "renameByName": {"Value #A": "used_memory", "Value #B": "gpu_util"},
+                            "indexByName": {"Time": 0, "host": 1, "gpu_id": 2, "user_name": 3, "podname": 4,
+                                            "containerid": 5, "pid": 6, "procressname": 7, "Value #B": 8,
+                                            "Value #A": 9}}}]))
+    panels.append(panel("每个用户占用GPU的数量 (GPUs held per user)", "timeseries",
+                        [(f'count by (user_name) (pod_gpu_allocated{{{HOST}}})', "{{user_name}}")], 16, y, 8, 9))
+    y += 9
+    # --- MI355X extras ---
+    panels.append(panel("Per-XCD GFX busy %", "heatmap",
+                        [(f'gpu_xcd_busy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} xcd{{xcd}}")], 0, y, 12, 8))
+    panels.append(panel("xGMI per-link bandwidth (rx+tx)", "timeseries",
+                        [(f'sum by (host, gpu_id, link) (gpu_xgmi_read_bytes_per_second{{{HOST}}} + '
+                          f'gpu_xgmi_write_bytes_per_second{{{HOST}}})', "{{host}} gpu{{gpu_id}} link{{link}}")],
+                        12, y, 12, 8, fieldConfig={"defaults": {"unit": "Bps"}, "overrides": []}))
+    y += 8
+    panels.append(panel("Socket power (W) / cap", "timeseries",
+                        [(f'gpu_power_watts{{{HOST}}}', "{{host}} gpu{{gpu_id}}"),
+                         (f'max(gpu_power_limit_watts{{{HOST}}})', "limit")], 0, y, 8, 8,
+                        fieldConfig={"defaults": {"unit": "watt"}, "overrides": []}))
+    panels.append(panel("Temperatures (°C)", "timeseries",
+                        [(f'gpu_temperature_celsius{{{HOST}}}', "{{host}} gpu{{gpu_id}} {{sensor}}")], 8, y, 8, 8,
+                        fieldConfig={"defaults": {"unit": "celsius"}, "overrides": []}))
+    panels.append(panel("Throttle / violation %", "timeseries",
+                        [(f'gpu_violation_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} {{kind}}")], 16, y, 8, 8))
+    y += 8
+    panels.append(panel("Energy rate (W, from accumulator)", "timeseries",
+                        [(f'rate(gpu_energy_joules_total{{{HOST}}}[1m])', "{{host}} gpu{{gpu_id}}")], 0, y, 8, 8))
+    panels.append(panel("HBM used (bytes)", "timeseries",
+                        [(f'gpu_vram_used_bytes{{{HOST}}}', "{{host}} gpu{{gpu_id}}")], 8, y, 8, 8,
+                        fieldConfig={"defaults": {"unit": "bytes"}, "overrides": []}))
+    panels.append(panel("Memory controller activity %", "timeseries",
+                        [(f'node_gpu_mem_bw_util{{{HOST}}}', "{{host}} gpu{{gpu_id}}")], 16, y, 8, 8))
+    y += 8
+    panels.append(panel("Probe: effective shader clock per XCD (MHz)", "timeseries",
+                        [(f'gpu_probe_xcd_clock_mhz{{{HOST}}}', "{{host}} gpu{{gpu_id}} xcd{{xcd}}")], 0, y, 12, 8))
+    panels.append(panel("PMC: MFMA busy % / occupancy %", "timeseries",
+                        [(f'gpu_mfma_busy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} mfma"),
+                         (f'gpu_occupancy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} occupancy")], 12, y, 12, 8))
+    y += 8
+    panels.append(panel("Exporter: /metrics p99 and tick p99 (s)", "timeseries",
+                        [(f'histogram_quantile(0.99, sum by (le, host) (rate(gpumon_scrape_duration_seconds_bucket{{{HOST}}}[5m])))',
+                          "{{host}} scrape p99"),
+                         (f'histogram_quantile(0.99, sum by (le, host) (rate(gpumon_sample_duration_seconds_bucket{{{HOST}}}[5m])))',
+                          "{{host}} tick p99")], 0, y, 12, 8,
+                        fieldConfig={"defaults": {"unit": "s"}, "overrides": []}))
+    panels.append(panel("Exporter: samples/s and errors", "timeseries",
+                        [(f'rate(gpumon_samples_total{{{HOST}}}[1m])', "{{host}} samples/s"),
+                         (f'sum by (host) (rate(gpumon_sample_errors_total{{{HOST}}}[5m]))', "{{host}} errors/s")],
+                        12, y, 12, 8))
+    return {
+        "title": "gpumon — MI355X GPU cluster",
+        "uid": "gpumon-mi355x",
+        "schemaVersion": 39,
+        "version": 1,
+        "refresh": "5s",
+        "time": {"from": "now-1h", "to": "now"},
+        "tags": ["gpu", "amd", "mi355x", "kubernetes"],
+        "templating": {"list": [
+            {"name": "datasource", "type": "datasource", "query": "prometheus", "label": "Datasource"},
+            {"name": "host", "type": "query", "datasource": DS, "label": "Node", "multi": True, "includeAll": True,
+             "query": {"query": "label_values(node_gpu_gpu_util, host)", "refId": "hosts"}, "refresh": 2},
+        ]},
+        "panels": panels,
+    }
+
+
+if __name__ == "__main__":
+    out = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gpumon-dashboard.json")
+    with open(out, "w", encoding="utf-8") as fh:
+        json.dump(build(), fh, ensure_ascii=False, indent=1)
+    print(out)

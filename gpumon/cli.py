@@ -1,0 +1,238 @@
+"""``python -m gpumon`` — command line.
+
+    gpumon serve   [--backend amdsmi] [--interval 1] [--listen 0.0.0.0:9400] ...   run the exporter
+    gpumon once    [--format prom|influx|json]                                       one sample to stdout
+    gpumon top     [--interval 1]                                                    live console table
+    gpumon scrape  URL [-n 1000] [-c 4]                                              scrape-latency probe
+    gpumon demo    [--gpus 8]                                                        mock node + fake kubelet
+    gpumon probe   [--blocks 1024]                                                   run the K1 probe once
+    gpumon load    [--kind mixed --seconds 10]                                       synthetic gfx950 load
+
+Reference: the agent had no CLI, only ``python3 /gpu.py`` with env vars (Dockerfile:7,
+gpu.py:17-26); its display-table formatter (gpu.py:155-168) was dead code — ``gpumon top`` is
+that view, implemented.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import signal
+import sys
+import threading
+import time
+
+from .config import Config, add_cli_args, from_args
+
+
+def _setup_logging(level: str):
+    logging.basicConfig(level=getattr(logging, level.upper(), logging.INFO),
+                        format="ts=%(asctime)s level=%(levelname)s component=%(name)s msg=%(message)r")
+
+
+def cmd_serve(args) -> int:
+    from .monitor import GpuMonitor
+
+    cfg = from_args(args)
+    _setup_logging(cfg.log_level)
+    mon = GpuMonitor(cfg).start()
+    log = logging.getLogger("gpumon")
+    log.info("serving %s backend=%s host=%s interval=%.3fs influx=%s control_plane=%s", mon.url, cfg.backend,
+             cfg.resolved_host(), cfg.interval, cfg.influx_url or "-", bool(mon.plane))
+    stop = threading.Event()
+    for s in (signal.SIGINT, signal.SIGTERM):
+        signal.signal(s, lambda *_: stop.set())
+    while not stop.wait(1.0):
+        pass
+    mon.stop()
+    return 0
+
+
+def cmd_once(args) -> int:
+    from .monitor import GpuMonitor
+
+    cfg = from_args(args)
+    cfg.interval = 0
+    cfg.listen = "127.0.0.1:0"
+    _setup_logging(cfg.log_level)
+    with GpuMonitor(cfg) as mon:
+        time.sleep(0.05)
+        mon.tick()  # second tick: rates populated
+        if args.format == "influx":
+            sys.stdout.write(mon.ex.influx_text())
+        elif args.format == "json":
+            json.dump({"devices": mon.ex.statics(), "samples": mon.ex.samples(), "rates": mon.ex.rates(),
+                       "pods": mon.ex.pod_rows(), "self": mon.ex.self_stats()}, sys.stdout, indent=1, default=str)
+            sys.stdout.write("\n")
+        else:
+            sys.stdout.write(mon.metrics())
+    return 0
+
+
+def _fmt(v, w, p=0):
+    if v is None:
+        return "-".rjust(w)
+    return f"{v:{w}.{p}f}"
+
+
+def render_top(statics, samples, rates, rows) -> str:
+    """Console table (the reference's unused displayfmt columns, gpu.py:156-168, plus MI355X fields)."""
+    lines = []
+    hdr = f"{'GPU':>3} {'UTIL%':>6} {'XCD busy% (0-7)':<32} {'VRAM MiB':>17} {'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8}"
+    lines.append(hdr)
+    for st, sm, rt in zip(statics, samples, rates):
+        f = sm["fields"]
+        xcd = " ".join(f"{int(x):3d}" if x is not None else "  -" for x in sm["xcd_busy"][:8])
+        used = (f["vram_used"] or 0) / 1048576
+        tot = (f["vram_total"] or 0) / 1048576
+        lines.append(f"{st['gpu_id']:>3} {_fmt(f['gfx_util'], 6)} {xcd:<32} {used:8.0f}/{tot:8.0f} "
+                     f"{_fmt(f['power_cur'], 6)} {_fmt(f['temp_hotspot'], 6)} {_fmt(f['gfxclk_cur'], 8)}")
+    lines.append("")
+    lines.append(f"{'CONTAINER':<13}{'POD':<32}{'NAMESPACE':<14}{'USER':<10}{'PID':>8} {'GPU':>3} {'MEM MiB':>9} {'UTIL%':>6}  PROCESS")
+    for r in rows:
+        lines.append(f"{r['containerid'][:12]:<13}{r['podname'][:31]:<32}{r['namespace'][:13]:<14}{r['user_name'][:9]:<10}"
+                     f"{r['pid']:>8} {r['dev']:>3} {r['used_memory_bytes'] / 1048576:9.0f} "
+                     f"{_fmt(r['proc_gfx_util'], 6, 1)}  {r['procname'][:30]}")
+    return "\n".join(lines)
+
+
+def cmd_top(args) -> int:
+    from .monitor import GpuMonitor
+
+    cfg = from_args(args)
+    cfg.listen = "127.0.0.1:0"
+    with GpuMonitor(cfg) as mon:
+        n = 0
+        while args.iterations <= 0 or n < args.iterations:
+            mon.wait_ticks(1, timeout_s=cfg.interval * 5 + 5)
+            text = render_top(mon.ex.statics(), mon.ex.samples(), mon.ex.rates(), mon.ex.pod_rows())
+            if sys.stdout.isatty():
+                sys.stdout.write("\x1b[2J\x1b[H")
+            sys.stdout.write(text + "\n")
+            sys.stdout.flush()
+            n += 1
+    return 0
+
+
+def cmd_scrape(args) -> int:
+    from urllib.parse import urlparse
+
+    from ._native import core
+
+    u = urlparse(args.url)
+    r = core().scrape_load(u.hostname or "127.0.0.1", u.port or 80, u.path or "/metrics", n_requests=args.n,
+                           concurrency=args.c, keep_alive=not args.no_keepalive, gzip=args.gzip)
+    lat = sorted(r["latencies_s"])
+
+    def q(p):
+        return lat[min(len(lat) - 1, int(p * (len(lat) - 1)))] * 1e3 if lat else float("nan")
+
+    print(json.dumps({"requests": len(lat), "errors": r["errors"], "p50_ms": q(0.5), "p99_ms": q(0.99),
+                      "max_ms": lat[-1] * 1e3 if lat else None, "rps": len(lat) / r["wall_s"] if r["wall_s"] else 0,
+                      "bytes_per_req": r["bytes"] / max(1, len(lat))}))
+    return 0 if r["errors"] == 0 else 1
+
+
+def cmd_demo(args) -> int:
+    """Mock node with a fake kubelet/CRI: the full pod_gpu path without a cluster."""
+    import tempfile
+
+    from .attribution.fake_kubelet import FakeKubelet, FakePod
+    from .monitor import GpuMonitor
+
+    d = tempfile.mkdtemp(prefix="gpumon-demo-")
+    k = FakeKubelet(podres_socket=f"{d}/kubelet.sock", cri_socket=f"{d}/cri.sock").start()
+    cid = "%064x" % 0xC0FFEE
+    k.pods = [FakePod("turing-gpu-notebook-alice-5d8f-x1", "ml", "uid-alice", labels={"mlgpu": "mlgpu"},
+                      containers={"notebook": (cid, ["0000:05:00.0"])}),
+              FakePod("jupyter-q-0", "research", "uid-q", containers={"main": ("%064x" % 0xBEEF, ["0000:25:00.0"])})]
+    cfg = Config(backend=f"mock:gpus={args.gpus}", listen=args.listen, interval=args.interval,
+                 cri_socket=k.cri_socket, pod_resources_socket=k.podres_socket, metadata_refresh=2.0)
+    mon = GpuMonitor(cfg).start()
+    mon.ex.mock_set_procs([{"pid": os.getpid(), "device": 0, "name": "python train.py", "vram_bytes": 12 << 30}])
+    print(f"demo exporter at {mon.url} (fake kubelet in {d}); Ctrl-C to stop", flush=True)
+    stop = threading.Event()
+    for s in (signal.SIGINT, signal.SIGTERM):
+        signal.signal(s, lambda *_: stop.set())
+    end = time.time() + args.seconds if args.seconds > 0 else float("inf")
+    while not stop.wait(0.5) and time.time() < end:
+        pass
+    mon.stop()
+    k.stop()
+    return 0
+
+
+def cmd_probe(args) -> int:
+    from ._native import hip
+
+    H = hip()
+    p = H.Probe(args.device, args.blocks, 2, args.spin_ticks)
+    slot = p.launch()
+    r = p.poll(slot, 5.0)
+    if r is None:
+        print("probe timed out", file=sys.stderr)
+        return 1
+    r.pop("records")
+    print(json.dumps(r))
+    return 0
+
+
+def cmd_load(args) -> int:
+    from .ops.load import SyntheticLoad
+
+    with SyntheticLoad(args.device, args.kind, duty=args.duty) as load:
+        time.sleep(args.seconds)
+        print(json.dumps(load.stats()))
+    return 0
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(prog="gpumon", description="MI355X Kubernetes GPU telemetry exporter")
+    sub = p.add_subparsers(dest="cmd", required=True)
+    s = sub.add_parser("serve", help="run the exporter")
+    add_cli_args(s)
+    s.set_defaults(fn=cmd_serve)
+    s = sub.add_parser("once", help="take one sample and print it")
+    add_cli_args(s)
+    s.add_argument("--format", choices=["prom", "influx", "json"], default="prom")
+    s.set_defaults(fn=cmd_once)
+    s = sub.add_parser("top", help="live console view")
+    add_cli_args(s)
+    s.add_argument("--iterations", type=int, default=0)
+    s.set_defaults(fn=cmd_top)
+    s = sub.add_parser("scrape", help="measure /metrics latency")
+    s.add_argument("url")
+    s.add_argument("-n", type=int, default=1000)
+    s.add_argument("-c", type=int, default=1)
+    s.add_argument("--gzip", action="store_true")
+    s.add_argument("--no-keepalive", action="store_true")
+    s.set_defaults(fn=cmd_scrape)
+    s = sub.add_parser("demo", help="mock node + fake kubelet")
+    s.add_argument("--gpus", type=int, default=8)
+    s.add_argument("--listen", default="127.0.0.1:9400")
+    s.add_argument("--interval", type=float, default=1.0)
+    s.add_argument("--seconds", type=float, default=0)
+    s.set_defaults(fn=cmd_demo)
+    s = sub.add_parser("probe", help="run the gfx950 probe kernel once")
+    s.add_argument("--device", type=int, default=0)
+    s.add_argument("--blocks", type=int, default=1024)
+    s.add_argument("--spin-ticks", type=int, default=200)
+    s.set_defaults(fn=cmd_probe)
+    s = sub.add_parser("load", help="synthetic gfx950 load")
+    s.add_argument("--device", type=int, default=0)
+    s.add_argument("--kind", choices=["mfma", "hbm", "mixed"], default="mixed")
+    s.add_argument("--duty", type=float, default=1.0)
+    s.add_argument("--seconds", type=float, default=10.0)
+    s.set_defaults(fn=cmd_load)
+    return p
+
+
+def main(argv=None) -> int:
+    args = build_parser().parse_args(argv)
+    return args.fn(args)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

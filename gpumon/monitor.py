@@ -46,14 +46,15 @@ class GpuMonitor:
             plane = ControlPlane(self.ex, self.cfg)
             if plane.enabled:
                 self.plane = plane.start()
-        if self.cfg.enable_probe:
-            from .ops.probe import ProbeRunner
-
-            self.probe = ProbeRunner(self.ex, every_s=max(self.cfg.interval, 0.1) * self.cfg.probe_every).start()
+        # PMC first: rocprofiler must register before anything in this process initialises HSA/HIP.
         if self.cfg.enable_pmc:
             from .ops.pmc import PmcRunner
 
             self.pmc = PmcRunner(self.ex, self.cfg.pmc_counters, every_s=max(self.cfg.interval, 0.1)).start()
+        if self.cfg.enable_probe:
+            from .ops.probe import ProbeRunner
+
+            self.probe = ProbeRunner(self.ex, every_s=max(self.cfg.interval, 0.1) * self.cfg.probe_every).start()
         return self
 
     def stop(self) -> None:

@@ -1,0 +1,111 @@
+"""Static checks of the deployment artefacts (no cluster needed).
+
+Reference manifest (/root/reference/gpu_monitor.yaml) used extensions/v1beta1 with no selector,
+probes, resources or ports and mounted the host docker socket; these tests pin the replacements.
+"""
+
+import json
+import os
+import re
+
+import yaml
+
+from gpumon.export import promtext
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _docs(path):
+    with open(os.path.join(ROOT, path)) as fh:
+        return [d for d in yaml.safe_load_all(fh) if d]
+
+
+def test_daemonset_is_apps_v1_and_complete():
+    docs = _docs("deploy/k8s/gpumon-daemonset.yaml")
+    kinds = {d["kind"]: d for d in docs}
+    assert set(kinds) == {"ConfigMap", "DaemonSet", "Service"}
+    ds = kinds["DaemonSet"]
+    assert ds["apiVersion"] == "apps/v1"
+    sel = ds["spec"]["selector"]["matchLabels"]
+    tpl = ds["spec"]["template"]
+    assert all(tpl["metadata"]["labels"][k] == v for k, v in sel.items())
+    spec = tpl["spec"]
+    assert spec["hostPID"] is True
+    assert any(t["key"] == "CriticalAddonsOnly" for t in spec["tolerations"])  # reference toleration
+    c = spec["containers"][0]
+    env = {e["name"]: e for e in c["env"]}
+    assert env["NODE_NAME"]["valueFrom"]["fieldRef"]["fieldPath"] == "spec.nodeName"  # reference env
+    assert c["ports"][0]["containerPort"] == 9400
+    assert c["readinessProbe"]["httpGet"]["path"] == "/readyz"
+    assert c["livenessProbe"]["httpGet"]["path"] == "/healthz"
+    mounts = {m["mountPath"] for m in c["volumeMounts"]}
+    assert "/var/lib/kubelet/pod-resources" in mounts
+    assert "/var/run/docker.sock" not in mounts and "/usr/bin/docker" not in mounts
+    assert tpl["metadata"]["annotations"]["prometheus.io/port"] == "9400"
+
+
+def test_configmap_keys_are_valid_config():
+    from gpumon.config import Config
+
+    cm = [d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "ConfigMap"][0]
+    data = yaml.safe_load(cm["data"]["config.yaml"])["gpumon"]
+    Config().apply_dict(data)  # raises on unknown keys
+
+
+def test_servicemonitor():
+    sm = _docs("deploy/k8s/gpumon-servicemonitor.yaml")[0]
+    assert sm["kind"] == "ServiceMonitor"
+    assert sm["spec"]["endpoints"][0]["port"] == "metrics"
+
+
+def _plugin_metric_names():
+    names = set()
+    for f in os.listdir(os.path.join(ROOT, "gpumon/ops")):
+        if f.endswith(".py"):
+            names |= set(re.findall(r'"(gpu_[a-z0-9_]+)"', open(os.path.join(ROOT, "gpumon/ops", f)).read()))
+    return names
+
+
+def test_dashboard_queries_resolve_against_exposition(mock_exporter):
+    """Every metric a dashboard panel queries is produced by the exporter (mock scrape) or by one
+    of the optional device plugins (probe kernel / PMC)."""
+    import subprocess
+    import sys
+
+    subprocess.run([sys.executable, os.path.join(ROOT, "deploy/grafana/make_dashboard.py")], check=True,
+                   stdout=subprocess.DEVNULL)
+    dash = json.load(open(os.path.join(ROOT, "deploy/grafana/gpumon-dashboard.json")))
+    ex = mock_exporter(backend="mock:gpus=2")
+    ex.set_allocations([{"pod_namespace": "ml", "pod_name": "jupyter-e-0", "container_name": "c", "gpu_index": 0}])
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    produced = set()
+    for f, v in fam.items():
+        produced.add(f)
+        for n, _, _ in v["samples"]:
+            produced.add(n)
+    plugins = _plugin_metric_names()
+    words = {"sum", "by", "count", "rate", "max", "histogram_quantile", "le", "host", "user_name", "link",
+             "gpu_id", "state", "m", "s"}
+    missing = []
+    titles = []
+    for p in dash["panels"]:
+        titles.append(p["title"])
+        for t in p["targets"]:
+            for name in re.findall(r"\b([a-z_][a-z0-9_]*)\s*[{(\[]", t["expr"]):
+                if name in words:
+                    continue
+                if name not in produced and name not in plugins:
+                    missing.append((p["title"], name))
+    assert not missing, missing
+    # reference panels recreated
+    for t in ["GPU总数", "已占GPU数量", "占GPU未开始使用", "占GPU已使用完毕", "当前使用显存", "GPU使用率",
+              "容器使用GPU情况", "每个用户占用GPU的数量"]:
+        assert any(t in x for x in titles), t
+
+
+def test_dockerfile_entrypoint():
+    txt = open(os.path.join(ROOT, "deploy/Dockerfile")).read()
+    assert 'ENTRYPOINT ["python3", "-m", "gpumon", "serve"]' in txt
+    assert "libltdl" not in txt.split("\n", 5)[-1] or "no vendored" in txt
+    assert "EXPOSE 9400" in txt

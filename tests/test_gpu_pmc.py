@@ -1,0 +1,28 @@
+"""PMC (rocprofiler-sdk device counting) on a real MI355X, in a fresh subprocess because the tool
+must register before HSA initialises. MFMA-busy must separate idle / bf16 burn / HBM stream."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from gpumon.ops.pmc import derive
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_pmc_separates_idle_mfma_hbm():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools/pmc_check.py")], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["agents"][0]["cu_count"] == 256 and d["agents"][0]["num_xcc"] == 8
+    assert d["idle"].get("mfma_busy", 0) < 5
+    assert d["mfma"]["mfma_busy"] > 60, d["mfma"]
+    assert d["hbm"].get("mfma_busy", 0) < 5
+    assert d["hbm"]["occupancy"] > 20
+    assert d["mfma"]["gui_active"] > 90
+    print("pmc:", {k: d[k] for k in ("idle", "mfma", "hbm")})

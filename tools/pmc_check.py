@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""PMC validation in a fresh process (rocprofiler must register before HSA init):
+idle vs bf16-MFMA burn vs HBM stream, device-wide MFMA-busy / occupancy via device counting.
+Prints one JSON line. Used by tests/test_gpu_pmc.py and for profiles/."""
+
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from gpumon.ops.pmc import DEFAULT_COUNTERS, derive, pmc_module
+
+    P = pmc_module()
+    n = P.init()
+    agents = P.agents()
+    out = {"agents": agents, "n": n}
+    counters = DEFAULT_COUNTERS
+    raw = P.sample(0, counters, 0.2)
+    out["idle"] = derive(raw, agents[0])
+    out["idle_raw"] = raw
+    from gpumon.ops.load import SyntheticLoad
+
+    for kind in ("mfma", "hbm"):
+        with SyntheticLoad(0, kind) as load:
+            time.sleep(1.0)
+            raw = P.sample(0, counters, 0.2)
+            out[kind] = derive(raw, agents[0])
+            out[kind + "_raw"] = {k: {"sum": v["sum"], "max": v["max"], "n": v["n"]} for k, v in raw.items()}
+            out[kind + "_load"] = load.stats()
+    print(json.dumps(out, default=str))
+
+
+if __name__ == "__main__":
+    main()
