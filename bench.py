@@ -56,6 +56,9 @@ def main() -> int:
     ap.add_argument("--scrape-concurrency", type=int, default=2)
     ap.add_argument("--gzip", action="store_true", help="scrape with Accept-Encoding: gzip")
     ap.add_argument("--backend", default="auto")
+    ap.add_argument("--sample-threads", type=int, default=0, help="parallel per-GPU sampling threads")
+    ap.add_argument("--replicate", type=int, default=1,
+                    help="REHEARSAL ONLY: sample each physical GPU R times (sampler scaling on a 1-GPU box)")
     ap.add_argument("--allreduce-mb", type=int, default=256)
     ap.add_argument("--probe", action="store_true", help="also run the K1 probe kernel each tick")
     ap.add_argument("--out", default="")
@@ -105,10 +108,13 @@ def main() -> int:
 
         core = _core()
         if backend == "auto":
-            backend = "amdsmi" if has_gpu else f"mock:gpus={n},mode=load"
-        cfg = Config(backend=backend, devices=list(range(n)) if backend == "amdsmi" else [],
+            backend = "amdsmi" if has_gpu else f"mock:gpus={n * args.replicate},mode=load"
+            if has_gpu and args.replicate > 1:
+                backend = f"amdsmi:replicate={args.replicate}"
+        cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith("amdsmi") else [],
                      interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
-                     enable_probe=args.probe and has_gpu, log_level="warn")
+                     enable_probe=args.probe and has_gpu, log_level="warn",
+                     sample_threads=args.sample_threads)
         mon = GpuMonitor(cfg, control_plane=False).start()
         if mon.start_error:
             raise SystemExit(f"exporter backend failed: {mon.start_error}")
@@ -174,9 +180,12 @@ def main() -> int:
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / n / BASELINE_SAMPLES_PER_GPU, 3),
+            "vs_baseline": round(value / max(1, len(sm)) / BASELINE_SAMPLES_PER_GPU, 3),
             "dtype": "bf16",
-            "data": "synthetic" if backend == "amdsmi" else "synthetic (mock backend: no GPU visible)",
+            "data": ("synthetic" if backend == "amdsmi" else
+                     f"synthetic (REHEARSAL: {n} physical GPU(s) each sampled {args.replicate}x)"
+                     if backend.startswith("amdsmi:replicate") else "synthetic (mock backend: no GPU visible)"),
+            "sampled_devices": len(sm),
             "config": {
                 "model": "gpumon MI355X exporter (amdsmi backend) + synthetic bf16 MFMA/HBM HIP load",
                 "global_batch": n,
@@ -191,7 +200,7 @@ def main() -> int:
             "scrapes": len(lat),
             "scrape_errors": scrape_result.get("errors", 0),
             "scrape_body_kb": round(scrape_result.get("bytes", 0) / max(1, len(lat)) / 1024, 2),
-            "samples_per_sec_per_gpu": round(value / n, 4),
+            "samples_per_sec_per_gpu": round(value / max(1, len(sm)), 4),
             "ticks": ticks,
             "tick_mean_ms": round(tick_mean * 1e3, 4),
             "tick_p99_ms": round(mon.ex.sample_quantile(0.99) * 1e3, 4),

@@ -47,6 +47,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "gzip", &c.gzip);
   get(d, "compat_families", &c.compat_families);
   get(d, "extended_families", &c.extended_families);
+  get(d, "full_device_labels", &c.full_device_labels);
   get(d, "processes", &c.processes);
   get(d, "link_every", &c.link_every);
   get(d, "sample_threads", &c.sample_threads);
@@ -317,8 +318,14 @@ PYBIND11_MODULE(_core, m) {
              d["devices_ok"] = t.devices_ok;
              d["pod_rows"] = t.pod_rows;
              d["body_bytes"] = t.body_bytes;
+             d["t_sample"] = t.t_sample;
+             d["t_procs"] = t.t_procs;
+             d["t_attrib"] = t.t_attrib;
+             d["t_render"] = t.t_render;
+             d["t_gzip"] = t.t_gzip;
              return d;
            })
+      .def("phase_totals", &Exporter::phase_totals)
       .def("wait_for_seq",
            [](Exporter& e, uint64_t seq, double timeout_s) {
              py::gil_scoped_release nogil;

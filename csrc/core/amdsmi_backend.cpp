@@ -255,6 +255,20 @@ bool AmdSmiBackend::init(std::string* err) {
     caps_.emplace_back();
     proc_buf_.emplace_back(sizeof(amdsmi_proc_info_t) * 64);
   }
+  if (replicate_ > 1 && !devs_.empty()) {
+    const size_t real = devs_.size();
+    for (int r = 1; r < replicate_; ++r)
+      for (size_t k = 0; k < real; ++k) {
+        DeviceStatic d = devs_[k];
+        d.index = static_cast<int>(devs_.size());
+        d.gpu_id = std::to_string(d.index);
+        d.model += " (replica of hip " + std::to_string(devs_[k].hip_id) + ")";
+        handles_.push_back(handles_[k]);
+        devs_.push_back(std::move(d));
+        caps_.emplace_back();
+        proc_buf_.emplace_back(sizeof(amdsmi_proc_info_t) * 64);
+      }
+  }
   if (devs_.empty()) {
     if (err) *err = "amdsmi: no AMD GPUs found (after device filter)";
     return false;

@@ -123,8 +123,12 @@ class AmdSmiBackend : public Backend {
   bool supports_links() const override;
   void sample_links(int i, DeviceSample* out) override;
   std::string lib_version() const { return lib_version_; }
+  // Expose every physical device `r` times (distinct gpu_id labels). Only for measuring how the
+  // sampler scales with the GPU count on a box with fewer GPUs than a full 8x MI355X node.
+  void set_replicate(int r) { replicate_ = r < 1 ? 1 : r; }
 
  private:
+  int replicate_ = 1;
   std::string lib_path_;
   std::unique_ptr<SmiTable> t_;
   bool inited_ = false;

@@ -105,8 +105,12 @@ std::unique_ptr<Backend> make_backend_from_config(const ExporterConfig& cfg, std
   std::unique_ptr<Backend> b;
   if (starts_with(cfg.backend, "mock")) {
     b = std::make_unique<MockBackend>(parse_mock_spec(cfg.backend, cfg.mock));
-  } else if (cfg.backend == "amdsmi" || cfg.backend == "auto") {
-    b = std::make_unique<AmdSmiBackend>(cfg.amdsmi_lib);
+  } else if (starts_with(cfg.backend, "amdsmi") || cfg.backend == "auto") {
+    auto a = std::make_unique<AmdSmiBackend>(cfg.amdsmi_lib);
+    // "amdsmi:replicate=8": sample every real device 8 times (scaling rehearsal on small boxes)
+    size_t p = cfg.backend.find("replicate=");
+    if (p != std::string::npos) a->set_replicate(atoi(cfg.backend.c_str() + p + 10));
+    b = std::move(a);
   } else {
     if (err) *err = "unknown backend '" + cfg.backend + "' (amdsmi | mock[:k=v,...] | auto)";
     return nullptr;
@@ -232,15 +236,30 @@ void Exporter::sampler_loop() {
   }
 }
 
-void Exporter::sample_devices(std::vector<DeviceSample>* out) {
+void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
+                              double* procs_s) {
   int n = backend_->device_count();
   out->resize(n);
+  procs->assign(n, {});
   bool links_tick = backend_->supports_links() && cfg_.link_every > 0 &&
                     (ticks_.load() % static_cast<uint64_t>(cfg_.link_every) == 0);
+  std::atomic<int64_t> proc_ns{0};
+  // One task per device: metrics table, (links), process list. With a pool the devices run in
+  // parallel (amdsmi calls are per-device sysfs/ioctl I/O).
   auto one = [&](int i) {
     backend_->sample(i, &(*out)[i]);
     if (links_tick) backend_->sample_links(i, &(*out)[i]);
+    if (cfg_.processes && (*out)[i].ok) {
+      int64_t t = mono_ns();
+      backend_->processes(i, &(*procs)[i]);
+      proc_ns += mono_ns() - t;
+    }
   };
+  struct Acc {
+    std::atomic<int64_t>* p;
+    double* s;
+    ~Acc() { *s = p->load() * 1e-9; }
+  } acc{&proc_ns, procs_s};
   if (pool_ && n > 1) pool_->run(n, one);
   else
     for (int i = 0; i < n; ++i) one(i);
@@ -338,10 +357,11 @@ TickInfo Exporter::tick() {
       std::lock_guard<std::mutex> g(state_mu_);
       statics = statics_;
     }
-    sample_devices(&cur);
+    int64_t ta = mono_ns();
+    sample_devices(&cur, &procs, &info.t_procs);
     int n = static_cast<int>(cur.size());
+    info.t_sample = (mono_ns() - ta) * 1e-9;
     rates.resize(n);
-    procs.resize(n);
     proc_counts.assign(n, 0);
     std::vector<DeviceSample> prev;
     {
@@ -372,12 +392,11 @@ TickInfo Exporter::tick() {
       } else {
         info.devices_ok++;
       }
-      if (cfg_.processes && s.ok) {
-        backend_->processes(i, &procs[i]);
-        proc_counts[i] = procs[i].size();
-      }
+      proc_counts[i] = procs[i].size();
     }
+    int64_t tb = mono_ns();
     build_pod_rows(procs, cur, &rows);
+    info.t_attrib = (mono_ns() - tb) * 1e-9;
     info.devices = n;
   }
 
@@ -401,10 +420,20 @@ TickInfo Exporter::tick() {
   in.self = &self;
   in.compat_families = cfg_.compat_families;
   in.extended_families = cfg_.extended_families;
+  in.full_device_labels = cfg_.full_device_labels;
   auto snap = std::make_shared<Snapshot>();
   snap->body.reserve(64 * 1024);
+  int64_t tr = mono_ns();
   render_prometheus(in, &snap->body);
+  int64_t tz = mono_ns();
+  info.t_render = (tz - tr) * 1e-9;
   if (cfg_.gzip) gzip_compress(snap->body, &snap->body_gz, 1);
+  info.t_gzip = (mono_ns() - tz) * 1e-9;
+  phase_ns_[0] += static_cast<uint64_t>(info.t_sample * 1e9);
+  phase_ns_[1] += static_cast<uint64_t>(info.t_procs * 1e9);
+  phase_ns_[2] += static_cast<uint64_t>(info.t_attrib * 1e9);
+  phase_ns_[3] += static_cast<uint64_t>(info.t_render * 1e9);
+  phase_ns_[4] += static_cast<uint64_t>(info.t_gzip * 1e9);
   snap->wall_ns = wall_ns();
   std::string influx;
   if (!cfg_.influx_url.empty() && cfg_.influx_every > 0 &&

@@ -43,6 +43,7 @@ struct ExporterConfig {
   bool gzip = true;
   bool compat_families = true;
   bool extended_families = true;
+  bool full_device_labels = false;
   bool processes = true;
   int link_every = 30;                // ticks between amdsmi_get_link_metrics refreshes
   int sample_threads = 0;             // parallel device sampling; 0 = sequential
@@ -64,6 +65,8 @@ struct TickInfo {
   int devices_ok = 0;
   size_t pod_rows = 0;
   size_t body_bytes = 0;
+  // phase breakdown (seconds): device metrics, process lists, attribution, render, gzip
+  double t_sample = 0, t_procs = 0, t_attrib = 0, t_render = 0, t_gzip = 0;
 };
 
 class Exporter {
@@ -105,7 +108,8 @@ class Exporter {
   void influx_loop();
   bool ensure_backend();
   void handle_http(const HttpRequest& req, HttpResponse* resp);
-  void sample_devices(std::vector<DeviceSample>* out);
+  void sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
+                      double* procs_s);
   void build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
                       const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows);
 
@@ -153,6 +157,17 @@ class Exporter {
   std::mutex seq_mu_;
   std::condition_variable seq_cv_;
   std::atomic<uint64_t> ticks_{0}, samples_{0}, stale_{0}, overruns_{0};
+  std::atomic<uint64_t> phase_ns_[5] = {};  // sample, procs, attrib, render, gzip (cumulative)
+
+ public:
+  // Cumulative seconds per tick phase: sample, procs, attrib, render, gzip.
+  std::vector<double> phase_totals() const {
+    std::vector<double> v;
+    for (const auto& p : phase_ns_) v.push_back(p.load() * 1e-9);
+    return v;
+  }
+
+ private:
   std::atomic<int64_t> last_tick_wall_ns_{0}, last_tick_mono_ns_{0};
 
   // Influx pusher

@@ -173,8 +173,10 @@ void render_prometheus(const RenderInput& in, std::string* o) {
   const size_t n = std::min(st.size(), sm.size());
   std::vector<std::string> dl(n);
   for (size_t d = 0; d < n; ++d)
-    dl[d] = label_str({{"host", in.host}, {"gpu_id", st[d].gpu_id}, {"gpu_uuid", st[d].uuid},
-                       {"bdf", st[d].bdf}});
+    dl[d] = in.full_device_labels
+                ? label_str({{"host", in.host}, {"gpu_id", st[d].gpu_id}, {"gpu_uuid", st[d].uuid},
+                             {"bdf", st[d].bdf}})
+                : label_str({{"host", in.host}, {"gpu_id", st[d].gpu_id}});
   auto devf = [&](const char* name, const char* help, const char* type, auto get) {
     Family f(o, name, help, type);
     for (size_t d = 0; d < n; ++d)
@@ -217,17 +219,23 @@ void render_prometheus(const RenderInput& in, std::string* o) {
     }
     {
       Family f(o, "gpu_info", "Static GPU identity (value is always 1).", "gauge");
-      for (size_t d = 0; d < n; ++d)
-        f.add(dl[d],
-              {{"model", st[d].model},
+      for (size_t d = 0; d < n; ++d) {
+        Labels extra;
+        if (!in.full_device_labels) {
+          extra.emplace_back("gpu_uuid", st[d].uuid);
+          extra.emplace_back("bdf", st[d].bdf);
+        }
+        for (auto& kv : Labels{{"model", st[d].model},
                {"serial", st[d].serial},
                {"gfx_target", st[d].gfx_target},
                {"hip_id", std::to_string(st[d].hip_id)},
                {"drm_card", std::to_string(st[d].drm_card)},
                {"compute_partition", st[d].compute_partition},
                {"memory_partition", st[d].memory_partition},
-               {"driver_version", st[d].driver_version}},
-              1.0);
+               {"driver_version", st[d].driver_version}})
+          extra.push_back(std::move(kv));
+        f.add(dl[d], extra, 1.0);
+      }
     }
     devf("gpu_sample_fresh", "1 if the firmware metrics table advanced since the previous tick.",
          "gauge", [&](size_t d) { return sm[d].fresh ? 1.0 : 0.0; });

@@ -86,6 +86,9 @@ struct RenderInput {
   const SelfStats* self = nullptr;
   bool compat_families = true;      // node_gpu_* / pod_gpu_*
   bool extended_families = true;    // gpu_* MI355X extras
+  // false: device series carry only host + gpu_id (the reference's tags, gpu.py:137); uuid / bdf /
+  // model live once on gpu_info (join on gpu_id). true: uuid + bdf on every device series.
+  bool full_device_labels = false;
 };
 
 void render_prometheus(const RenderInput& in, std::string* out);

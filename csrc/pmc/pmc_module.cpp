@@ -127,7 +127,7 @@ void load_supported(Agent& A) {
     bool found = false;
     for (uint64_t d = 0; d < info.dimensions_count; ++d) {
       std::string dn = info.dimensions[d]->name;
-      if (dn == "XCC" || dn == "xcc") {
+      if (dn == "DIMENSION_XCC" || dn == "XCC") {  // ROCm 7.2 names it DIMENSION_XCC
         A.xcc_dim[id.handle] = info.dimensions[d]->id;
         found = true;
       }

@@ -22,9 +22,19 @@ def test_prometheus_text_is_valid_and_has_reference_families(mock_exporter):
         assert fam[name]["type"] == "gauge"
     # labels: host + gpu_id on every device series (reference tags host, gpu_id)
     for _, labels, _ in fam["node_gpu_gpu_util"]["samples"]:
+        assert set(labels) == {"host", "gpu_id"}  # the reference's tags (gpu.py:137)
         assert labels["host"] == "node-a"
         assert labels["gpu_id"] in {"0", "1", "2", "3"}
-        assert "gpu_uuid" in labels and "bdf" in labels
+    # identity is carried once per GPU on gpu_info (join on gpu_id)
+    for _, labels, _ in fam["gpu_info"]["samples"]:
+        assert labels["gpu_uuid"] and labels["bdf"] and labels["gfx_target"] == "gfx950"
+
+
+def test_full_device_labels_option(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1", full_device_labels=True)
+    fam = promtext.parse(ex.metrics_text())
+    _, labels, _ = fam["node_gpu_gpu_util"]["samples"][0]
+    assert set(labels) == {"host", "gpu_id", "gpu_uuid", "bdf"}
 
 
 def test_mem_fields_consistent(mock_exporter):
