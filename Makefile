@@ -61,12 +61,14 @@ build/obj/bindings/hip_module.o: csrc/bindings/hip_module.cpp $(HIP_HDR)
 $(HIPEXT): build/obj/hip/kernels.o build/obj/bindings/hip_module.o
 	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -shared -fPIC $^ -o $@
 
-asan: $(CORE_SRC) csrc/exporter_main.cpp
+asan: bin/gpumon-exporter-asan
+bin/gpumon-exporter-asan: $(CORE_SRC) $(CORE_HDR) csrc/exporter_main.cpp
 	@mkdir -p bin
 	$(CXX) -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer $(INC) \
 	  $(CORE_SRC) csrc/exporter_main.cpp -o bin/gpumon-exporter-asan $(LIBS)
 
-tsan: $(CORE_SRC) csrc/exporter_main.cpp
+tsan: bin/gpumon-exporter-tsan
+bin/gpumon-exporter-tsan: $(CORE_SRC) $(CORE_HDR) csrc/exporter_main.cpp
 	@mkdir -p bin
 	$(CXX) -O1 -g -std=c++17 -fsanitize=thread $(INC) \
 	  $(CORE_SRC) csrc/exporter_main.cpp -o bin/gpumon-exporter-tsan $(LIBS)

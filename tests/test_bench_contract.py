@@ -1,0 +1,60 @@
+"""bench.py driver contract on CPU: single process and 2-rank torch.distributed (gloo).
+
+The driver runs `python bench.py --gpus N --steps K --warmup W` (N=1) and, for N>1,
+`python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py`; rank 0
+prints exactly one JSON line with the BASELINE metric name.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def _check(d, n, steps, warmup):
+    assert REQUIRED <= set(d)
+    base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    assert d["n_gpus"] == n and d["steps"] == steps and d["warmup"] == warmup
+    assert d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert set(d["config"]) >= {"model", "global_batch", "seq_len", "parallelism"}
+    assert d["value"] > 0 and d["scrape_p99_ms"] > 0 and d["scrape_errors"] == 0
+    assert d["ticks"] == steps
+
+
+def test_bench_single_process():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--interval", "0.1"], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 1, 3, 1)
+    assert lines[0]["value"] == pytest.approx(10.0, rel=0.2)  # 1 device x 10 Hz
+
+
+@pytest.mark.slow
+def test_bench_two_ranks_gloo():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(29600 + os.getpid() % 300),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--interval", "0.1", "--allreduce-mb", "1"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    _check(lines[0], 2, 3, 1)
+    assert "all-reduce" in lines[0]["config"]["parallelism"]

@@ -1,0 +1,76 @@
+"""Host-side sanitizer runs of the native exporter (SURVEY.md §5 race detection): ASan+UBSan and
+TSan builds of bin/gpumon-exporter under concurrent scrapes while the sampler ticks at 100 Hz and
+snapshots are swapped. GPU sanitizers are not available on this pool; these cover the C++ core."""
+
+import os
+import signal
+import socket
+import subprocess
+import threading
+import time
+import urllib.request
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(binary, env_extra):
+    port = _free_port()
+    env = dict(os.environ, **env_extra)
+    p = subprocess.Popen([binary, "--backend", "mock:gpus=4", "--interval", "0.01", "--listen", f"127.0.0.1:{port}",
+                          "--sample-threads", "2", "--http-threads", "2", "--log-level", "error"],
+                         stderr=subprocess.PIPE, stdout=subprocess.DEVNULL, env=env, text=True)
+    try:
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            try:
+                urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=1).read()
+                break
+            except OSError:
+                time.sleep(0.1)
+        errors = []
+
+        def hammer():
+            for _ in range(60):
+                try:
+                    req = urllib.request.Request(f"http://127.0.0.1:{port}/metrics",
+                                                 headers={"Accept-Encoding": "gzip"})
+                    urllib.request.urlopen(req, timeout=5).read()
+                except Exception as e:  # noqa: BLE001
+                    errors.append(e)
+
+        ts = [threading.Thread(target=hammer) for _ in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errors, errors[:3]
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=60)
+    return p.returncode, err
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_exporter_under_concurrent_scrapes(target, binary, env):
+    r = subprocess.run(["make", "-C", ROOT, target], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rc, err = _run(os.path.join(ROOT, binary), env)
+    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
+           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    assert not bad, err[-4000:]
+    assert rc == 0, err[-2000:]
