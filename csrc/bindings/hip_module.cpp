@@ -24,10 +24,11 @@ PYBIND11_MODULE(_hip, m) {
     launch_mfma_burn(dev, P(a), P(b), static_cast<float*>(P(out)), blocks, iters, P(stream));
   }, py::arg("dev"), py::arg("a"), py::arg("b"), py::arg("out"), py::arg("blocks"), py::arg("iters"),
      py::arg("stream") = 0);
-  m.def("stream_copy", [](int dev, uintptr_t src, uintptr_t dst, size_t n16, int blocks, uintptr_t stream) {
-    launch_stream_copy(dev, P(src), P(dst), n16, blocks, P(stream));
+  m.def("stream_copy", [](int dev, uintptr_t src, uintptr_t dst, size_t n16, int blocks, uintptr_t stream,
+                          int unroll) {
+    launch_stream_copy(dev, P(src), P(dst), n16, blocks, P(stream), unroll);
   }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("n16"), py::arg("blocks") = 4096,
-     py::arg("stream") = 0);
+     py::arg("stream") = 0, py::arg("unroll") = 4);
   m.def("stream_triad", [](int dev, uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n, int blocks,
                            uintptr_t stream) {
     launch_stream_triad(dev, static_cast<const float*>(P(a)), static_cast<const float*>(P(b)),
@@ -54,8 +55,10 @@ PYBIND11_MODULE(_hip, m) {
         d["busy_s"] = s.busy_s;
         d["flops"] = s.flops;
         d["bytes"] = s.bytes;
-        d["tflops"] = s.busy_s > 0 ? s.flops / s.busy_s / 1e12 : 0.0;
-        d["tbps"] = s.busy_s > 0 ? s.bytes / s.busy_s / 1e12 : 0.0;
+        d["mfma_s"] = s.mfma_s;
+        d["hbm_s"] = s.hbm_s;
+        d["tflops"] = s.mfma_s > 0 ? s.flops / s.mfma_s / 1e12 : 0.0;  // rate while MFMA batches ran
+        d["tbps"] = s.hbm_s > 0 ? s.bytes / s.hbm_s / 1e12 : 0.0;      // rate while HBM batches ran
         return d;
       });
 

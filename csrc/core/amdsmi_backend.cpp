@@ -100,6 +100,17 @@ static inline double u32v(uint32_t x, double scale = 1.0) {
 static inline double u64v(uint64_t x, double scale = 1.0) {
   return x == ~0ull ? kNaN : static_cast<double>(x) * scale;
 }
+// Times one amdsmi call into the backend's per-call accounting (member-function scope only).
+#define SMI_TIMED(call_id, expr)                                                                  \
+  ([&]() {                                                                                        \
+    const int64_t t_start_ = mono_ns();                                                           \
+    const amdsmi_status_t s_ = (expr);                                                            \
+    record_call(call_id, mono_ns() - t_start_,                                                    \
+                s_ == AMDSMI_STATUS_SUCCESS || s_ == AMDSMI_STATUS_OUT_OF_RESOURCES ||             \
+                    s_ == AMDSMI_STATUS_NOT_SUPPORTED);                                           \
+    return s_;                                                                                    \
+  }())
+
 static inline bool ok16(uint16_t x) { return x != 0xFFFF; }
 static inline bool ok32(uint32_t x) { return x != 0xFFFFFFFFu; }
 static inline bool ok64(uint64_t x) { return x != ~0ull; }
@@ -298,7 +309,7 @@ void AmdSmiBackend::sample(int i, DeviceSample* out) {
 
   if (c.metrics && t_->amdsmi_get_gpu_metrics_info) {
     amdsmi_gpu_metrics_t m;
-    amdsmi_status_t st = t_->amdsmi_get_gpu_metrics_info(h, &m);
+    amdsmi_status_t st = SMI_TIMED(kCallMetrics, t_->amdsmi_get_gpu_metrics_info(h, &m));
     if (st == AMDSMI_STATUS_SUCCESS) {
       any = true;
       v[F_GFX_UTIL] = u16v(m.average_gfx_activity);
@@ -403,7 +414,7 @@ void AmdSmiBackend::sample(int i, DeviceSample* out) {
   // Fallbacks for devices without a metrics table.
   if (!c.metrics && c.activity && t_->amdsmi_get_gpu_activity) {
     amdsmi_engine_usage_t u{};
-    amdsmi_status_t st = t_->amdsmi_get_gpu_activity(h, &u);
+    amdsmi_status_t st = SMI_TIMED(kCallActivity, t_->amdsmi_get_gpu_activity(h, &u));
     if (st == AMDSMI_STATUS_SUCCESS) {
       any = true;
       v[F_GFX_UTIL] = u32v(u.gfx_activity);
@@ -418,7 +429,7 @@ void AmdSmiBackend::sample(int i, DeviceSample* out) {
   }
   if (!c.metrics && c.power && t_->amdsmi_get_power_info) {
     amdsmi_power_info_t p{};
-    amdsmi_status_t st = t_->amdsmi_get_power_info(h, &p);
+    amdsmi_status_t st = SMI_TIMED(kCallPower, t_->amdsmi_get_power_info(h, &p));
     if (st == AMDSMI_STATUS_SUCCESS) {
       v[F_POWER_CUR] = u32v(p.current_socket_power);
       v[F_POWER_AVG] = u32v(p.average_socket_power);
@@ -428,7 +439,7 @@ void AmdSmiBackend::sample(int i, DeviceSample* out) {
   }
   if (c.vram && t_->amdsmi_get_gpu_vram_usage) {
     amdsmi_vram_usage_t vu{};
-    amdsmi_status_t st = t_->amdsmi_get_gpu_vram_usage(h, &vu);
+    amdsmi_status_t st = SMI_TIMED(kCallVram, t_->amdsmi_get_gpu_vram_usage(h, &vu));
     if (st == AMDSMI_STATUS_SUCCESS) {
       any = true;
       v[F_VRAM_USED] = static_cast<double>(vu.vram_used) * 1048576.0;
@@ -452,7 +463,7 @@ bool AmdSmiBackend::processes(int i, std::vector<ProcSample>* out) {
     uint32_t cap = static_cast<uint32_t>(buf.size() / sizeof(amdsmi_proc_info_t));
     uint32_t n = cap;
     auto* list = reinterpret_cast<amdsmi_proc_info_t*>(buf.data());
-    amdsmi_status_t st = t_->amdsmi_get_gpu_process_list(handles_[i], &n, list);
+    amdsmi_status_t st = SMI_TIMED(kCallProcs, t_->amdsmi_get_gpu_process_list(handles_[i], &n, list));
     if (st == AMDSMI_STATUS_OUT_OF_RESOURCES) {
       buf.resize(sizeof(amdsmi_proc_info_t) * std::max<size_t>(n + 16, cap * 2));
       continue;
@@ -489,7 +500,7 @@ void AmdSmiBackend::sample_links(int i, DeviceSample* out) {
   if (!caps_[i].links || !t_->amdsmi_get_link_metrics) return;
   amdsmi_link_metrics_t lm;
   memset(&lm, 0, sizeof lm);
-  amdsmi_status_t st = t_->amdsmi_get_link_metrics(handles_[i], &lm);
+  amdsmi_status_t st = SMI_TIMED(kCallLinks, t_->amdsmi_get_link_metrics(handles_[i], &lm));
   if (st == AMDSMI_STATUS_NOT_SUPPORTED) {
     caps_[i].links = false;
     return;

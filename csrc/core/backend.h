@@ -37,7 +37,38 @@ class Backend {
   // Restrict to a subset of device hip_ids (empty = all). Applied at init().
   void set_device_filter(const std::vector<int>& ids) { filter_ = ids; }
 
+  // Per-call latency accounting (exported as gpumon_backend_call_* self-metrics).
+  enum Call { kCallMetrics = 0, kCallVram, kCallProcs, kCallLinks, kCallActivity, kCallPower, kCallCount };
+  static const char* call_name(int c) {
+    static const char* n[] = {"gpu_metrics", "vram_usage", "process_list", "link_metrics", "gpu_activity",
+                              "power_info"};
+    return c >= 0 && c < kCallCount ? n[c] : "?";
+  }
+  struct CallSnap {
+    std::string call;
+    uint64_t n = 0, errors = 0;
+    double seconds = 0;
+  };
+  std::vector<CallSnap> call_stats() const {
+    std::vector<CallSnap> v;
+    for (int c = 0; c < kCallCount; ++c) {
+      uint64_t n = calls_n_[c].load(std::memory_order_relaxed);
+      if (!n) continue;
+      v.push_back({call_name(c), n, calls_err_[c].load(std::memory_order_relaxed),
+                   calls_ns_[c].load(std::memory_order_relaxed) * 1e-9});
+    }
+    return v;
+  }
+
  protected:
+  void record_call(int c, int64_t ns, bool ok) {
+    calls_n_[c].fetch_add(1, std::memory_order_relaxed);
+    calls_ns_[c].fetch_add(static_cast<uint64_t>(ns > 0 ? ns : 0), std::memory_order_relaxed);
+    if (!ok) calls_err_[c].fetch_add(1, std::memory_order_relaxed);
+  }
+  std::atomic<uint64_t> calls_n_[kCallCount] = {};
+  std::atomic<uint64_t> calls_ns_[kCallCount] = {};
+  std::atomic<uint64_t> calls_err_[kCallCount] = {};
   std::vector<int> filter_;
   bool keep(int hip_id) const {
     if (filter_.empty()) return true;

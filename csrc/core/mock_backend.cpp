@@ -128,6 +128,7 @@ void MockBackend::sample(int i, DeviceSample* out) {
     out->errors = 1;
     out->last_error = "gpu_metrics: MOCK_INJECTED_FAILURE";
     out->sample_ns = mono_ns() - t0;
+    record_call(kCallMetrics, out->sample_ns, false);
     return;
   }
   double t = (out->host_mono_ns - t0_ns_) * 1e-9;
@@ -221,6 +222,7 @@ void MockBackend::sample(int i, DeviceSample* out) {
   }
   out->ok = true;
   out->sample_ns = mono_ns() - t0;
+  record_call(kCallMetrics, out->sample_ns, true);
 }
 
 bool MockBackend::processes(int i, std::vector<ProcSample>* out) {

@@ -606,6 +606,19 @@ void render_prometheus(const RenderInput& in, std::string* o) {
         f.add(hl, {{"result", "dropped"}}, static_cast<double>(s.influx_dropped));
       }
     }
+    {
+      Family f(o, "gpumon_backend_calls_total", "Device-library calls by kind.", "counter");
+      for (const auto& c : s.backend_calls) f.add(hl, {{"call", c.call}}, static_cast<double>(c.n));
+    }
+    {
+      Family f(o, "gpumon_backend_call_seconds_total", "Time spent in device-library calls by kind.",
+               "counter");
+      for (const auto& c : s.backend_calls) f.add(hl, {{"call", c.call}}, c.seconds);
+    }
+    {
+      Family f(o, "gpumon_backend_call_errors_total", "Failed device-library calls by kind.", "counter");
+      for (const auto& c : s.backend_calls) f.add(hl, {{"call", c.call}}, static_cast<double>(c.errors));
+    }
   }
 }
 

@@ -62,6 +62,12 @@ struct SelfStats {
   uint64_t pods_attributed = 0;
   uint64_t attribution_cache_hits = 0, attribution_cache_misses = 0;
   uint64_t influx_ok = 0, influx_fail = 0, influx_dropped = 0;
+  struct Call {
+    std::string call;
+    uint64_t n = 0, errors = 0;
+    double seconds = 0;
+  };
+  std::vector<Call> backend_calls;  // per backend call kind (amdsmi_get_gpu_metrics_info, ...)
   std::vector<uint64_t> device_errors;  // per device
 };
 

@@ -23,7 +23,7 @@ void launch_mfma_tile(int dev, const void* a, const void* b, float* c, int iters
 // Burn: `blocks` x 256 threads; each wave runs iters x 4 MFMAs; wave sums go to out[blocks*4].
 void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blocks, int iters, void* stream);
 // dst = src (n16 = number of 16-byte vectors)
-void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream);
+void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream, int unroll = 4);
 // c = a + s * b  (fp32, n elements, n % 4 == 0)
 void launch_stream_triad(int dev, const float* a, const float* b, float* c, float s, size_t n, int blocks,
                          void* stream);
@@ -34,6 +34,8 @@ struct LoadStats {
   double busy_s = 0;        // GPU time measured with events
   double flops = 0;         // MFMA FLOP issued
   double bytes = 0;         // HBM bytes moved (read + write)
+  double mfma_s = 0;        // GPU time of MFMA batches
+  double hbm_s = 0;         // GPU time of HBM-stream batches
 };
 
 class LoadGen {
@@ -65,6 +67,7 @@ class LoadGen {
   std::atomic<uint64_t> busy_ns_{0};
   std::atomic<uint64_t> flops_{0};
   std::atomic<uint64_t> bytes_moved_{0};
+  std::atomic<uint64_t> mfma_ns_{0}, hbm_ns_{0};
   std::string err_;
 };
 

@@ -111,6 +111,29 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(const i32x4* __restric
   }
 }
 
+// U independent 16-B loads in flight per lane before the stores (each k-slice of a 256*U-vector
+// chunk is one fully coalesced 4 KiB wave-group access); grid-stride over chunks.
+template <int U>
+__global__ void __launch_bounds__(256) stream_copy_unrolled_kernel(const i32x4* __restrict__ src,
+                                                                   i32x4* __restrict__ dst, size_t n) {
+  const size_t chunk = static_cast<size_t>(256) * U;
+  for (size_t base = static_cast<size_t>(blockIdx.x) * chunk; base < n; base += static_cast<size_t>(gridDim.x) * chunk) {
+    i32x4 v[U];
+    if (base + chunk <= n) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) v[k] = __builtin_nontemporal_load(src + base + k * 256 + threadIdx.x);
+#pragma unroll
+      for (int k = 0; k < U; ++k) __builtin_nontemporal_store(v[k], dst + base + k * 256 + threadIdx.x);
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const size_t i = base + k * 256 + threadIdx.x;
+        if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) stream_triad_kernel(const f32x4* __restrict__ a,
                                                            const f32x4* __restrict__ b,
                                                            f32x4* __restrict__ c, float s, size_t n4) {
@@ -177,10 +200,18 @@ void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blo
   check(hipGetLastError(), "mfma_burn_kernel");
 }
 
-void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream) {
+void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream, int unroll) {
   check(hipSetDevice(dev), "hipSetDevice");
-  hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     static_cast<const i32x4*>(src), static_cast<i32x4*>(dst), n16);
+  auto s = static_cast<hipStream_t>(stream);
+  auto in = static_cast<const i32x4*>(src);
+  auto out = static_cast<i32x4*>(dst);
+  switch (unroll) {
+    case 1: hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, s, in, out, n16); break;
+    case 2: hipLaunchKernelGGL(stream_copy_unrolled_kernel<2>, dim3(blocks), dim3(256), 0, s, in, out, n16); break;
+    case 4: hipLaunchKernelGGL(stream_copy_unrolled_kernel<4>, dim3(blocks), dim3(256), 0, s, in, out, n16); break;
+    case 8: hipLaunchKernelGGL(stream_copy_unrolled_kernel<8>, dim3(blocks), dim3(256), 0, s, in, out, n16); break;
+    default: throw std::invalid_argument("stream_copy: unroll must be 1, 2, 4 or 8");
+  }
   check(hipGetLastError(), "stream_copy_kernel");
 }
 
@@ -199,8 +230,8 @@ void launch_stream_triad(int dev, const float* a, const float* b, float* c, floa
 // ---------------------------------------------------------------------------------------------
 LoadGen::LoadGen(int dev, std::string kind, double duty, size_t hbm_bytes, int mfma_iters)
     : dev_(dev), kind_(std::move(kind)), duty_(std::clamp(duty, 0.01, 1.0)), bytes_(hbm_bytes), iters_(mfma_iters) {
-  if (kind_ != "mfma" && kind_ != "hbm" && kind_ != "mixed")
-    throw std::invalid_argument("LoadGen kind must be mfma | hbm | mixed");
+  if (kind_ != "mfma" && kind_ != "hbm" && kind_ != "mixed" && kind_ != "partial")
+    throw std::invalid_argument("LoadGen kind must be mfma | hbm | mixed | partial");
   bytes_ = std::max<size_t>(bytes_ / 16 * 16, 1 << 20);
 }
 
@@ -224,7 +255,7 @@ void LoadGen::start() {
   b_ = static_cast<char*>(a_) + 32 * 16 * 2;
   check(hipMemcpy(a_, h.data(), h.size() * 2, hipMemcpyHostToDevice), "hipMemcpy");
   check(hipMalloc(reinterpret_cast<void**>(&out_), 4096 * 4 * sizeof(float)), "hipMalloc");
-  if (kind_ != "mfma") {
+  if (kind_ == "hbm" || kind_ == "mixed") {
     check(hipMalloc(&src_, bytes_), "hipMalloc");
     check(hipMalloc(&dst_, bytes_), "hipMalloc");
     check(hipMemsetAsync(src_, 1, bytes_, s), "hipMemset");
@@ -242,14 +273,17 @@ void LoadGen::loop() {
     check(hipEventCreate(&e0), "hipEventCreate");
     check(hipEventCreate(&e1), "hipEventCreate");
     const int cus = device_cu_count(dev_);
-    const int burn_blocks = cus * 8;     // 8 waves/CU = 2 per SIMD
+    // 8 blocks x 4 waves requested per CU (residency then limited by VGPRs: ~7 waves/SIMD at 68 VGPRs)
+    const int burn_blocks = kind_ == "partial" ? cus / 4 : cus * 8;  // partial: ~1/4 of the CUs busy
     const int stream_blocks = cus * 16;  // >> 256 workgroups across all 8 XCDs
     bool flip = false;
     while (running_) {
+      // one kind per batch so the event time is attributed to exactly one kernel kind
+      const bool do_mfma = kind_ == "mfma" || kind_ == "partial" || (kind_ == "mixed" && !flip);
+      flip = !flip;
       check(hipEventRecord(e0, s), "hipEventRecord");
       double fl = 0, by = 0;
       for (int k = 0; k < 4; ++k) {
-        bool do_mfma = kind_ == "mfma" || (kind_ == "mixed" && !flip);
         if (do_mfma) {
           launch_mfma_burn(dev_, a_, b_, out_, burn_blocks, iters_, s);
           fl += static_cast<double>(burn_blocks) * 4 * 4 * iters_ * 32768.0;
@@ -257,7 +291,6 @@ void LoadGen::loop() {
           launch_stream_copy(dev_, src_, dst_, bytes_ / 16, stream_blocks, s);
           by += 2.0 * static_cast<double>(bytes_);
         }
-        flip = !flip;
         launches_++;
       }
       check(hipEventRecord(e1, s), "hipEventRecord");
@@ -265,6 +298,7 @@ void LoadGen::loop() {
       float ms = 0;
       check(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
       busy_ns_ += static_cast<uint64_t>(ms * 1e6);
+      (do_mfma ? mfma_ns_ : hbm_ns_) += static_cast<uint64_t>(ms * 1e6);
       flops_ += static_cast<uint64_t>(fl);
       bytes_moved_ += static_cast<uint64_t>(by);
       if (duty_ < 0.999) {
@@ -309,6 +343,8 @@ LoadStats LoadGen::stats() const {
   s.busy_s = busy_ns_ * 1e-9;
   s.flops = static_cast<double>(flops_.load());
   s.bytes = static_cast<double>(bytes_moved_.load());
+  s.mfma_s = mfma_ns_ * 1e-9;
+  s.hbm_s = hbm_ns_ * 1e-9;
   return s;
 }
 
