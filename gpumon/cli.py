@@ -59,6 +59,9 @@ def cmd_once(args) -> int:
     _setup_logging(cfg.log_level)
     with GpuMonitor(cfg) as mon:
         time.sleep(0.05)
+        for plugin in (mon.pmc, mon.probe):  # make sure device plugins contributed to this sample
+            if plugin is not None:
+                plugin.step()
         mon.tick()  # second tick: rates populated
         if args.format == "influx":
             sys.stdout.write(mon.ex.influx_text())

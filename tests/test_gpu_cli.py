@@ -1,0 +1,38 @@
+"""End-to-end CLI on a real MI355X with both device plugins enabled (fresh subprocess: PMC must
+register before HSA init): `gpumon once --enable-pmc --enable-probe-kernel`."""
+
+import os
+import subprocess
+import sys
+
+import pytest
+
+from gpumon.export import promtext
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_once_with_probe_and_pmc():
+    r = subprocess.run([sys.executable, "-m", "gpumon", "once", "--backend", "amdsmi", "--devices", "0",
+                        "--enable-pmc", "--enable-probe-kernel", "--log-level", "warn"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    fam = promtext.parse(r.stdout)
+    assert promtext.one(fam, "node_gpu_mem_total", gpu_id="0") > 250000
+    assert len(promtext.values(fam, "gpu_probe_xcd_clock_mhz", gpu_id="0")) == 8
+    assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
+    assert promtext.values(fam, "gpu_mfma_busy_percent", gpu_id="0")
+    assert promtext.values(fam, "gpu_occupancy_percent", gpu_id="0")
+    assert len(promtext.values(fam, "gpu_xcd_mfma_busy_percent", gpu_id="0")) == 8
+    assert promtext.one(fam, "gpumon_backend_calls_total", call="gpu_metrics") >= 2
+
+
+def test_native_binary_once():
+    exe = os.path.join(ROOT, "bin", "gpumon-exporter")
+    r = subprocess.run([exe, "--backend", "amdsmi", "--once", "--host", "box"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    fam = promtext.parse(r.stdout)
+    assert promtext.values(fam, "node_gpu_gpu_util", host="box")
+    assert len(promtext.values(fam, "gpu_xcd_busy_percent")) >= 8

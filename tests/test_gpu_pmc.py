@@ -25,4 +25,7 @@ def test_pmc_separates_idle_mfma_hbm():
     assert d["hbm"].get("mfma_busy", 0) < 5
     assert d["hbm"]["occupancy"] > 20
     assert d["mfma"]["gui_active"] > 90
+    # partial occupancy (burn on ~1/4 of the CUs): busy GPU, but MFMA pipes mostly idle
+    assert 5 < d["partial"]["mfma_busy"] < 0.6 * d["mfma"]["mfma_busy"], d["partial"]
+    assert len(d["mfma"].get("xcd_mfma_busy", [])) == 8
     print("pmc:", {k: d[k] for k in ("idle", "mfma", "hbm")})

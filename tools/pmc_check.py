@@ -24,7 +24,7 @@ def main():
     out["idle_raw"] = raw
     from gpumon.ops.load import SyntheticLoad
 
-    for kind in ("mfma", "hbm"):
+    for kind in ("mfma", "hbm", "partial"):
         with SyntheticLoad(0, kind) as load:
             time.sleep(1.0)
             raw = P.sample(0, counters, 0.2)
