@@ -74,9 +74,15 @@ class PmcRunner:
         self.errors = 0
         self.last: Dict[int, dict] = {}
         self._stop = threading.Event()
+        self._lock = threading.Lock()
         self._th = None
 
     def step(self) -> Dict[int, dict]:
+        # one counting context per agent may run at a time: serialise explicit + background calls
+        with self._lock:
+            return self._step()
+
+    def _step(self) -> Dict[int, dict]:
         res = {}
         for dev, ai in self.map.items():
             try:

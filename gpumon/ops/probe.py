@@ -47,10 +47,16 @@ class ProbeRunner:
         self.timeouts: Dict[int, int] = {i: 0 for i in self.probes}
         self.last: Dict[int, dict] = {}
         self._stop = threading.Event()
+        self._lock = threading.Lock()
         self._th = None
 
     def step(self) -> Dict[int, dict]:
-        """Launch (if the previous launch completed) and collect one round; returns results."""
+        """Launch (if the previous launch completed) and collect one round; returns results.
+        Serialised: the background thread and an explicit caller (``gpumon once``) may both call it."""
+        with self._lock:
+            return self._step()
+
+    def _step(self) -> Dict[int, dict]:
         for i, p in self.probes.items():
             if i not in self.pending:
                 slot = p.launch()
