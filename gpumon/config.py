@@ -65,7 +65,9 @@ class Config:
     enable_probe: bool = False
     probe_every: int = 1
     enable_pmc: bool = False
-    pmc_counters: List[str] = field(default_factory=lambda: ["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_WAVES", "SQ_BUSY_CYCLES"])
+    # the counters gpumon.ops.pmc.derive() needs (2 SQ + 2 GRBM slots: one counting pass on gfx950)
+    pmc_counters: List[str] = field(default_factory=lambda: ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES",
+                                                             "GRBM_GUI_ACTIVE", "GRBM_COUNT"])
     # rates calibration
     activity_acc_scale: float = 1.0
     xgmi_kb_bytes: float = 1024.0
