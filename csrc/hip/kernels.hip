@@ -275,7 +275,9 @@ void LoadGen::loop() {
     const int cus = device_cu_count(dev_);
     // 8 blocks x 4 waves requested per CU (residency then limited by VGPRs: ~7 waves/SIMD at 68 VGPRs)
     const int burn_blocks = kind_ == "partial" ? cus / 4 : cus * 8;  // partial: ~1/4 of the CUs busy
-    const int stream_blocks = cus * 16;  // >> 256 workgroups across all 8 XCDs
+    // 8192 workgroups x unroll 4: best of the interleaved sweep on MI355X (5.74 TB/s copy vs 4.79 for
+    // 4096 x 1; profiles/r1_kernels_and_pmc.md)
+    const int stream_blocks = cus * 32;
     bool flip = false;
     while (running_) {
       // one kind per batch so the event time is attributed to exactly one kernel kind
