@@ -1,5 +1,8 @@
 #include "exporter.h"
 
+#include <dirent.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -279,7 +282,17 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
   std::vector<std::tuple<std::string, std::string, std::string, int>> active;
   for (size_t d = 0; d < procs.size(); ++d) {
     double dev_util = d < samples.size() ? samples[d].v[F_GFX_UTIL] : kNaN;
+    // One row per (pid, device): duplicate entries (several KFD contexts of one process) are merged,
+    // a duplicate series would make Prometheus reject the whole scrape.
+    std::unordered_map<uint32_t, size_t> row_of_pid;
     for (const auto& p : procs[d]) {
+      auto dup = row_of_pid.find(p.pid);
+      if (dup != row_of_pid.end()) {
+        PodRow& r = (*rows)[dup->second];
+        r.used_memory_bytes += has(p.vram_bytes) ? p.vram_bytes : 0;
+        if (has(p.cu_occupancy)) r.cu_occupancy = has(r.cu_occupancy) ? r.cu_occupancy + p.cu_occupancy : p.cu_occupancy;
+        continue;
+      }
       alive.push_back(p.pid);
       ProcIdentity id = attr_->resolve(p.pid);
       // per-process gfx util from engine_usage.gfx ns deltas
@@ -311,6 +324,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       r.proc_gfx_util = util;
       r.cu_occupancy = p.cu_occupancy;
       active.emplace_back(r.pod_namespace, r.pod_name, r.container, r.dev);
+      row_of_pid[p.pid] = rows->size();
       rows->push_back(std::move(r));
     }
   }
@@ -332,6 +346,8 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
         break;
       }
     if (busy) continue;
+    // the same (pod, container, GPU) listed twice must still be one series
+    active.emplace_back(ns, pod, ctr, a.gpu_index);
     PodRow r;
     r.dev = a.gpu_index;
     r.idle = true;
@@ -616,6 +632,37 @@ std::string Exporter::render_influx_now() {
   return out;
 }
 
+// /proc/self based process collector (CPU, RSS, threads, fds, start time).
+static void read_process_stats(SelfStats* s) {
+  std::string st;
+  if (read_file("/proc/self/stat", &st, 4096)) {
+    size_t rp = st.rfind(')');
+    if (rp != std::string::npos) {
+      std::vector<std::string> f = split(std::string_view(st).substr(rp + 2), ' ');
+      // after ") ": [0]=state ... [11]=utime [12]=stime [17]=num_threads [19]=starttime [21]=rss pages
+      if (f.size() > 21) {
+        const double hz = static_cast<double>(sysconf(_SC_CLK_TCK));
+        const double page = static_cast<double>(sysconf(_SC_PAGESIZE));
+        s->cpu_seconds = (atof(f[11].c_str()) + atof(f[12].c_str())) / hz;
+        s->threads = atoi(f[17].c_str());
+        s->rss_bytes = atof(f[21].c_str()) * page;
+        std::string up;
+        if (read_file("/proc/uptime", &up, 256)) {
+          const double boot = wall_ns() * 1e-9 - atof(up.c_str());
+          s->start_time_s = boot + atof(f[19].c_str()) / hz;
+        }
+      }
+    }
+  }
+  if (DIR* d = opendir("/proc/self/fd")) {
+    int n = 0;
+    while (struct dirent* e = readdir(d))
+      if (e->d_name[0] != '.') ++n;
+    closedir(d);
+    s->open_fds = n - 1;  // minus the directory handle itself
+  }
+}
+
 SelfStats Exporter::self_stats() const {
   SelfStats s;
   s.version = cfg_.version;
@@ -641,6 +688,7 @@ SelfStats Exporter::self_stats() const {
   s.influx_dropped = influx_dropped_;
   if (backend_)
     for (const auto& c : backend_->call_stats()) s.backend_calls.push_back({c.call, c.n, c.errors, c.seconds});
+  read_process_stats(&s);
   {
     std::lock_guard<std::mutex> g(state_mu_);
     s.device_errors = dev_errors_;

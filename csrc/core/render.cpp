@@ -607,6 +607,26 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       }
     }
     {
+      Family f(o, "process_cpu_seconds_total", "Exporter user+system CPU time.", "counter");
+      if (s.cpu_seconds >= 0) f.add(hl, s.cpu_seconds);
+    }
+    {
+      Family f(o, "process_resident_memory_bytes", "Exporter resident memory.", "gauge");
+      if (s.rss_bytes >= 0) f.add(hl, s.rss_bytes);
+    }
+    {
+      Family f(o, "process_start_time_seconds", "Exporter start time (unix seconds).", "gauge");
+      if (s.start_time_s >= 0) f.add(hl, s.start_time_s);
+    }
+    {
+      Family f(o, "process_threads", "Exporter OS threads.", "gauge");
+      if (s.threads >= 0) f.add(hl, s.threads);
+    }
+    {
+      Family f(o, "process_open_fds", "Exporter open file descriptors.", "gauge");
+      if (s.open_fds >= 0) f.add(hl, s.open_fds);
+    }
+    {
       Family f(o, "gpumon_backend_calls_total", "Device-library calls by kind.", "counter");
       for (const auto& c : s.backend_calls) f.add(hl, {{"call", c.call}}, static_cast<double>(c.n));
     }

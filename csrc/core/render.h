@@ -68,6 +68,9 @@ struct SelfStats {
     double seconds = 0;
   };
   std::vector<Call> backend_calls;  // per backend call kind (amdsmi_get_gpu_metrics_info, ...)
+  // process collector (the reference forked ~4+2C+P subprocesses per cycle; this is the whole cost)
+  double cpu_seconds = -1, rss_bytes = -1, start_time_s = -1;
+  int threads = -1, open_fds = -1;
   std::vector<uint64_t> device_errors;  // per device
 };
 

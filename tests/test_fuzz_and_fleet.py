@@ -1,0 +1,89 @@
+"""Property tests of the renderers (hypothesis-generated label values and GPU/process sets) and a
+fleet test: several node-local exporters scraped by one scraper (the reference's only
+"distributed" mode: N independent DaemonSet pods, gpu_monitor.yaml:1-5; Prometheus does fan-in)."""
+
+import os
+
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from gpumon.export import promtext
+
+label_text = st.text(alphabet=st.characters(blacklist_categories=("Cs",), blacklist_characters="\x00"),
+                     min_size=1, max_size=40)
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(pod=label_text, ns=label_text, user=label_text, procname=label_text)
+def test_pod_labels_roundtrip_any_text(core, pod, ns, user, procname):
+    ex = core.Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0, "host": 'no"de\\1'})
+    ex.start()
+    try:
+        ex.mock_set_procs([{"pid": 1, "device": 0, "name": procname, "vram_bytes": 7 << 20}])
+        ex.set_allocations([{"pod_namespace": ns, "pod_name": pod, "container_name": "c", "gpu_index": 0,
+                             "user_name": user}])
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())  # must stay valid exposition for any input
+        idle = [l for _, l, _ in fam["pod_gpu_used_memory"]["samples"] if l["pid"] == "-"]
+        assert idle and idle[0]["podname"] == pod and idle[0]["namespace"] == ns and idle[0]["user_name"] == user
+        assert idle[0]["host"] == 'no"de\\1'
+        procs = [l for _, l, _ in fam["pod_gpu_used_memory"]["samples"] if l["pid"] == "1"]
+        assert procs and procs[0]["procressname"] == procname
+        # Influx lines: one line per row, no raw newlines leaking into a line
+        lines = ex.influx_text().split("\n")
+        assert sum(l.startswith("pod_gpu,") for l in lines) == 2
+    finally:
+        ex.stop()
+
+
+@settings(max_examples=25, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(gpus=st.integers(0, 16), procs=st.lists(st.tuples(st.integers(1, 10**6), st.integers(0, 15)), max_size=30),
+       unsupported=st.lists(st.sampled_from(["temp_hotspot", "power_cur", "vram_used", "xcd", "xgmi", "gfx_util"]),
+                            max_size=4))
+def test_any_device_and_process_set_renders_valid(core, gpus, procs, unsupported):
+    spec = f"mock:gpus={gpus}" + (f",unsupported={';'.join(unsupported)}" if unsupported else "")
+    ex = core.Exporter({"backend": spec, "serve_http": False, "interval_s": 0})
+    ex.start()
+    try:
+        ex.mock_set_procs([{"pid": p, "device": d} for p, d in procs])
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())
+        n = len(promtext.values(fam, "gpu_up"))
+        assert n == gpus
+        seen = {(p, d) for p, d in procs if d < gpus}
+        assert len(promtext.values(fam, "pod_gpu_used_memory_bytes")) == len(seen)
+    finally:
+        ex.stop()
+
+
+def test_fleet_of_exporters_one_scraper(core):
+    nodes = []
+    try:
+        for i in range(3):
+            ex = core.Exporter({"backend": f"mock:gpus={2 + i}", "listen_addr": "127.0.0.1", "port": 0,
+                                "interval_s": 0.05, "host": f"gpu-node-{i}", "http_threads": 1})
+            ex.start()
+            nodes.append(ex)
+        total = {}
+        for ex in nodes:
+            r = core.scrape_load("127.0.0.1", ex.port, "/metrics", n_requests=20, concurrency=2)
+            assert r["errors"] == 0
+            fam = promtext.parse(ex.metrics_text())
+            for _, labels, v in fam["gpumon_gpus"]["samples"]:
+                if labels["state"] == "total":
+                    total[labels["host"]] = v
+        assert total == {"gpu-node-0": 2, "gpu-node-1": 3, "gpu-node-2": 4}
+    finally:
+        for ex in nodes:
+            ex.stop()
+
+
+def test_metrics_doc_is_current():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools/gen_metrics_doc.py"), "--check"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, "docs/metrics.md is stale: run python tools/gen_metrics_doc.py"
