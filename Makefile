@@ -82,3 +82,10 @@ pmc: $(PMCEXT)
 $(PMCEXT): csrc/pmc/pmc_module.cpp
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared -fvisibility=hidden -I$(ROCM)/include -I$(PYINC) -I$(PYBIND) $< \
 	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrocprofiler-sdk -lhsa-runtime64 -o $@
+
+# Fake libamd_smi (CPU tests of the real amdsmi backend through the dlopen table).
+FAKESMI := build/fakes/libfake_amd_smi.so
+fakes: $(FAKESMI)
+$(FAKESMI): csrc/fakes/fake_amd_smi.cpp
+	@mkdir -p $(dir $@)
+	$(CXX) -O1 -std=c++17 -fPIC -shared -I$(ROCM)/include $< -o $@

@@ -57,6 +57,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "influx_timeout_s", &c.influx_timeout_s);
   get(d, "init_retry_s", &c.init_retry_s);
   get(d, "health_stale_s", &c.health_stale_s);
+  get(d, "reinit_after", &c.reinit_after);
   get(d, "version", &c.version);
   get(d, "activity_acc_scale", &c.rates.activity_acc_scale);
   get(d, "xgmi_kb_bytes", &c.rates.xgmi_kb_bytes);
@@ -384,6 +385,7 @@ PYBIND11_MODULE(_core, m) {
              d["backend"] = s.backend;
              d["backend_version"] = s.backend_version;
              d["backend_up"] = s.backend_up;
+             d["backend_reinits"] = s.backend_reinits;
              d["influx_ok"] = s.influx_ok;
              d["influx_fail"] = s.influx_fail;
              d["influx_dropped"] = s.influx_dropped;

@@ -400,6 +400,16 @@ TickInfo Exporter::tick() {
             s.links[k].max_bandwidth_gbps = p.links[k].max_bandwidth_gbps;
           if (s.links[k].link_type < 0) s.links[k].link_type = p.links[k].link_type;
         }
+      }
+      // amdsmi_get_link_metrics lists 7 entries (incl. self) while the metrics table has 8 xGMI
+      // slots on MI355X: a slot without a link_metrics entry gets speed x width (38 Gb/s x 16 =
+      // 608 Gb/s, the value link_metrics reports for every other link).
+      const double lane = s.v[F_XGMI_LINK_SPEED], width = s.v[F_XGMI_LINK_WIDTH];
+      for (int k = 0; k < s.n_links; ++k)
+        if (s.links[k].status >= 0 && !has(s.links[k].max_bandwidth_gbps) && has(lane) && has(width))
+          s.links[k].max_bandwidth_gbps = lane * width;
+      if (i < static_cast<int>(prev.size())) {
+        const DeviceSample& p = prev[i];
         if (s.ok && p.ok && s.acc.firmware_ts && s.acc.firmware_ts == p.acc.firmware_ts) {
           s.fresh = false;
           stale_++;
@@ -407,18 +417,31 @@ TickInfo Exporter::tick() {
         compute_rates(p, s, cfg_.rates, &rates[i]);
       }
       samples_++;
-      if (!s.ok) {
+      if (!s.ok || s.errors) {  // partial failures (one call failed, others answered) count too
         std::lock_guard<std::mutex> g(state_mu_);
-        if (i < static_cast<int>(dev_errors_.size())) dev_errors_[i] += std::max<uint32_t>(1, s.errors);
-      } else {
-        info.devices_ok++;
+        if (i < static_cast<int>(dev_errors_.size()))
+          dev_errors_[i] += s.ok ? s.errors : std::max<uint32_t>(1, s.errors);
       }
+      if (s.ok) info.devices_ok++;
       proc_counts[i] = procs[i].size();
     }
     int64_t tb = mono_ns();
     build_pod_rows(procs, cur, &rows);
     info.t_attrib = (mono_ns() - tb) * 1e-9;
     info.devices = n;
+    // Whole-backend failure (driver reload, amdsmi lost its handles): re-initialise with backoff
+    // instead of exporting gpu_up 0 forever (the reference crashed and relied on the kubelet).
+    all_failed_ticks_ = (n > 0 && info.devices_ok == 0) ? all_failed_ticks_ + 1 : 0;
+    if (cfg_.reinit_after > 0 && all_failed_ticks_ >= cfg_.reinit_after) {
+      GPUMON_LOG(LogLevel::kWarn, "exporter",
+                 "all " + std::to_string(n) + " GPU(s) failed " + std::to_string(all_failed_ticks_) +
+                     " ticks in a row: re-initialising the backend");
+      all_failed_ticks_ = 0;
+      backend_up_ = false;
+      reinits_++;
+      next_init_ns_ = mono_ns();  // first retry immediately, then init_retry_s backoff
+      backend_->shutdown();
+    }
   }
 
   SelfStats self = self_stats();
@@ -669,6 +692,7 @@ SelfStats Exporter::self_stats() const {
   s.backend = backend_ ? backend_->name() : cfg_.backend;
   if (auto* a = dynamic_cast<AmdSmiBackend*>(backend_.get())) s.backend_version = a->lib_version();
   s.backend_up = backend_up_;
+  s.backend_reinits = reinits_;
   s.ticks = ticks_;
   s.samples = samples_;
   s.stale_samples = stale_;

@@ -55,6 +55,7 @@ struct ExporterConfig {
   double influx_timeout_s = 2.0;
   double init_retry_s = 5.0;
   double health_stale_s = 0;          // 0 = max(3*interval, 10 s)
+  int reinit_after = 5;               // consecutive all-devices-failed ticks before re-initialising
   std::string version = "0.1.0";
 };
 
@@ -151,6 +152,8 @@ class Exporter {
   std::atomic<bool> running_{false};
   std::atomic<bool> backend_up_{false};
   int64_t next_init_ns_ = 0;
+  int all_failed_ticks_ = 0;
+  std::atomic<uint64_t> reinits_{0};
   std::string backend_err_;
   std::thread sampler_;
   std::atomic<uint64_t> seq_{0};

@@ -122,7 +122,7 @@ void MockBackend::sample(int i, DeviceSample* out) {
   uint64_t call = ++calls_[i];
   out->host_mono_ns = mono_ns();
   out->host_wall_ns = wall_ns();
-  if (cfg_.fail_device == devs_[i].hip_id &&
+  if ((cfg_.fail_device == devs_[i].hip_id || cfg_.fail_device == -2) &&  // -2: every device
       (cfg_.fail_every < 0 || (cfg_.fail_every > 0 && call % static_cast<uint64_t>(cfg_.fail_every) == 0))) {
     out->ok = false;
     out->errors = 1;

@@ -544,6 +544,11 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       f.add(hl, s.backend_up ? 1.0 : 0.0);
     }
     {
+      Family f(o, "gpumon_backend_reinits_total",
+               "Backend re-initialisations after every GPU failed for several ticks.", "counter");
+      f.add(hl, static_cast<double>(s.backend_reinits));
+    }
+    {
       Family f(o, "gpumon_sample_interval_seconds", "Configured sampling interval.", "gauge");
       f.add(hl, s.interval_s);
     }

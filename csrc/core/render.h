@@ -49,6 +49,7 @@ struct SelfStats {
   std::string backend;
   std::string backend_version;
   bool backend_up = false;
+  uint64_t backend_reinits = 0;
   uint64_t ticks = 0;
   uint64_t samples = 0;
   uint64_t stale_samples = 0;

@@ -1,0 +1,264 @@
+// Fake libamd_smi for CPU tests of the REAL AmdSmiBackend ("a C++ fake with the
+// same dlopen function-table signature, so the C++ sampler is testable without ROCm").
+//
+// Exports the amdsmi C API subset gpumon resolves, with MI355X-shaped values (gpu_metrics v1.8:
+// 8 XCC, 7 xGMI peer links + N/A slot 0, 288 GiB HBM3E, N/A edge temperature, 15.3 uJ energy
+// resolution). Behaviour is scripted by environment variables read at amdsmi_init():
+//   FAKE_AMDSMI_GPUS=N            number of GPUs (default 2)
+//   FAKE_AMDSMI_PROCS=N           GPU processes per device (default 1; >64 exercises the
+//                                 OUT_OF_RESOURCES resize path)
+//   FAKE_AMDSMI_FAIL_METRICS=K    gpu_metrics fails (AMDSMI_STATUS_BUSY) on device K
+//   FAKE_AMDSMI_INIT_FAIL=1       amdsmi_init returns AMDSMI_STATUS_INIT_ERROR
+//   FAKE_AMDSMI_NO_METRICS=1      gpu_metrics NOT_SUPPORTED (exercises the activity/power fallback)
+// Counters advance deterministically per call so rates are checkable.
+#include <amd_smi/amdsmi.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+namespace {
+int g_gpus = 2, g_procs = 1, g_fail_metrics = -1;
+bool g_no_metrics = false;
+std::vector<uintptr_t> g_handles;
+std::atomic<uint64_t> g_calls[64];
+int env_int(const char* k, int d) {
+  const char* v = getenv(k);
+  return v ? atoi(v) : d;
+}
+int dev_of(amdsmi_processor_handle h) {
+  uintptr_t x = reinterpret_cast<uintptr_t>(h);
+  return (x >= 0x1000 && x < 0x1000 + static_cast<uintptr_t>(g_gpus)) ? static_cast<int>(x - 0x1000) : -1;
+}
+}  // namespace
+
+extern "C" {
+
+amdsmi_status_t amdsmi_init(uint64_t) {
+  if (env_int("FAKE_AMDSMI_INIT_FAIL", 0)) return AMDSMI_STATUS_INIT_ERROR;
+  g_gpus = env_int("FAKE_AMDSMI_GPUS", 2);
+  g_procs = env_int("FAKE_AMDSMI_PROCS", 1);
+  g_fail_metrics = env_int("FAKE_AMDSMI_FAIL_METRICS", -1);
+  g_no_metrics = env_int("FAKE_AMDSMI_NO_METRICS", 0) != 0;
+  g_handles.clear();
+  for (int i = 0; i < g_gpus; ++i) g_handles.push_back(0x1000 + i);
+  for (auto& c : g_calls) c = 0;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_shut_down(void) { return AMDSMI_STATUS_SUCCESS; }
+
+amdsmi_status_t amdsmi_get_lib_version(amdsmi_version_t* v) {
+  v->major = 99;
+  v->minor = 0;
+  v->release = 1;
+  v->build = "fake";
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_socket_handles(uint32_t* count, amdsmi_socket_handle* socks) {
+  // one socket per GPU, as on MI355X OAM platforms
+  if (!socks) {
+    *count = static_cast<uint32_t>(g_gpus);
+    return AMDSMI_STATUS_SUCCESS;
+  }
+  for (uint32_t i = 0; i < *count && i < static_cast<uint32_t>(g_gpus); ++i)
+    socks[i] = reinterpret_cast<amdsmi_socket_handle>(0x100 + i);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle s, uint32_t* count,
+                                             amdsmi_processor_handle* hs) {
+  const uintptr_t si = reinterpret_cast<uintptr_t>(s) - 0x100;
+  if (!hs) {
+    *count = 1;
+    return AMDSMI_STATUS_SUCCESS;
+  }
+  // reverse order on purpose: the backend must sort by hip_id
+  hs[0] = reinterpret_cast<amdsmi_processor_handle>(g_handles[g_gpus - 1 - si]);
+  *count = 1;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_processor_type(amdsmi_processor_handle, processor_type_t* t) {
+  *t = AMDSMI_PROCESSOR_TYPE_AMD_GPU;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_enumeration_info(amdsmi_processor_handle h, amdsmi_enumeration_info_t* e) {
+  int d = dev_of(h);
+  if (d < 0) return AMDSMI_STATUS_INVAL;
+  memset(e, 0, sizeof *e);
+  e->hip_id = d;
+  e->drm_card = 24 + d;
+  e->drm_render = 152 + d;
+  e->hsa_id = 2 + d;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_device_uuid(amdsmi_processor_handle h, unsigned int* len, char* uuid) {
+  int d = dev_of(h);
+  snprintf(uuid, *len, "8bff75a3-0000-1000-80d2-cf9ceac6%04x", d);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_device_bdf(amdsmi_processor_handle h, amdsmi_bdf_t* b) {
+  int d = dev_of(h);
+  b->as_uint = 0;
+  b->bus_number = 0x26 + 0x20 * d;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle, amdsmi_asic_info_t* a) {
+  memset(a, 0, sizeof *a);
+  strcpy(a->market_name, "AMD Instinct MI355 OAM (fake amdsmi)");
+  strcpy(a->asic_serial, "0xFAKE");
+  a->num_of_compute_units = 256;
+  a->target_graphics_version = 0x950;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle h, amdsmi_kfd_info_t* k) {
+  k->kfd_id = 36622 + dev_of(h);
+  k->node_id = 2 + dev_of(h);
+  k->current_partition_id = 0;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_driver_info(amdsmi_processor_handle, amdsmi_driver_info_t* i) {
+  memset(i, 0, sizeof *i);
+  strcpy(i->driver_name, "amdgpu");
+  strcpy(i->driver_version, "6.18.0-fake");
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_compute_partition(amdsmi_processor_handle, char* p, uint32_t len) {
+  snprintf(p, len, "SPX");
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_memory_partition(amdsmi_processor_handle, char* p, uint32_t len) {
+  snprintf(p, len, "NPS1");
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_power_info(amdsmi_processor_handle, amdsmi_power_info_t* p) {
+  memset(p, 0xFF, sizeof *p);
+  p->socket_power = 250;
+  p->current_socket_power = 250;
+  p->power_limit = 1400000000;  // ROCm 7.2 reports microwatts here (measured on MI355X)
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_energy_count(amdsmi_processor_handle, uint64_t* e, float* res, uint64_t* ts) {
+  *e = 1000;
+  *res = 15.3f;
+  *ts = 0;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_vram_usage(amdsmi_processor_handle h, amdsmi_vram_usage_t* v) {
+  v->vram_total = 294896;
+  v->vram_used = 283 + 1024 * dev_of(h);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_activity(amdsmi_processor_handle h, amdsmi_engine_usage_t* u) {
+  memset(u, 0, sizeof *u);
+  u->gfx_activity = 11 + dev_of(h);
+  u->umc_activity = 5;
+  u->mm_activity = 0xFFFFFFFF;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_metrics_info(amdsmi_processor_handle h, amdsmi_gpu_metrics_t* m) {
+  int d = dev_of(h);
+  if (g_no_metrics) return AMDSMI_STATUS_NOT_SUPPORTED;
+  if (d == g_fail_metrics) return AMDSMI_STATUS_BUSY;
+  uint64_t n = ++g_calls[d];  // advances once per tick
+  memset(m, 0xFF, sizeof *m);  // every field N/A unless set below (firmware convention)
+  m->common_header.format_revision = 1;
+  m->common_header.content_revision = 8;
+  m->temperature_hotspot = 46 + d;
+  m->temperature_mem = 33;
+  m->temperature_vrsoc = 43;
+  m->average_gfx_activity = 37;
+  m->average_umc_activity = 12;
+  m->current_socket_power = 600;
+  m->energy_accumulator = 1000000 + n * 1000000;  // x15.3 uJ per tick
+  m->system_clock_counter = n * 1000000000ull;     // 1 s per tick (driver ns)
+  m->firmware_timestamp = n * 100000000ull;
+  m->current_gfxclk = 2100;
+  m->current_uclk = 2000;
+  m->current_socclk = 1200;
+  m->throttle_status = 0;
+  m->pcie_link_width = 16;
+  m->pcie_link_speed = 320;
+  m->pcie_bandwidth_inst = 18;
+  m->pcie_replay_count_acc = 0;
+  m->gfx_activity_acc = static_cast<uint32_t>(n * 37 * 1000);  // 37 % per counter tick
+  m->mem_activity_acc = static_cast<uint32_t>(n * 12 * 1000);
+  m->accumulation_counter = n * 1000;
+  m->ppt_residency_acc = n * 100;  // 10 % PVIOL
+  m->prochot_residency_acc = 0;
+  m->socket_thm_residency_acc = 0;
+  m->vr_thm_residency_acc = 0;
+  m->hbm_thm_residency_acc = 0;
+  m->xgmi_link_speed = 38;
+  m->xgmi_link_width = 16;
+  m->vram_max_bandwidth = 8192;
+  m->num_partition = 1;
+  for (int k = 0; k < 8; ++k) {
+    m->current_gfxclks[k] = static_cast<uint16_t>(2100 - k);
+    m->xcp_stats[0].gfx_busy_inst[k] = 37;
+    m->xcp_stats[0].gfx_busy_acc[k] = n * 37 * 1000;
+  }
+  m->xgmi_link_status[0] = 0xFFFF;   // slot 0: N/A on MI355X
+  m->xgmi_read_data_acc[0] = 0;
+  m->xgmi_write_data_acc[0] = 0;
+  for (int k = 1; k < 8; ++k) {
+    m->xgmi_link_status[k] = 1;
+    m->xgmi_read_data_acc[k] = n * 1000000ull * k;  // k GB/s (KB units, 1 s per tick)
+    m->xgmi_write_data_acc[k] = n * 500000ull * k;
+  }
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_process_list(amdsmi_processor_handle h, uint32_t* max, amdsmi_proc_info_t* list) {
+  int d = dev_of(h);
+  const uint32_t n = static_cast<uint32_t>(g_procs);
+  const uint32_t cap = *max;
+  for (uint32_t i = 0; i < n && i < cap; ++i) {
+    amdsmi_proc_info_t& p = list[i];
+    memset(&p, 0, sizeof p);
+    snprintf(p.name, sizeof p.name, "worker-%u", i);
+    p.pid = 100000 + 1000 * d + i;
+    p.mem = (1ull << 30) * (i + 1);
+    p.memory_usage.vram_mem = (1ull << 30) * (i + 1);
+    p.engine_usage.gfx = g_calls[d] * 500000000ull;  // 50 % of a 1 s tick
+    p.cu_occupancy = 64;
+  }
+  *max = n;
+  return n > cap ? AMDSMI_STATUS_OUT_OF_RESOURCES : AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_link_metrics(amdsmi_processor_handle h, amdsmi_link_metrics_t* lm) {
+  memset(lm, 0, sizeof *lm);
+  lm->num_links = 7;
+  for (int k = 0; k < 7; ++k) {
+    if (k == 0) {
+      lm->links[k].bdf.as_uint = ~0ull;  // self / unknown, as on MI355X
+    } else {
+      lm->links[k].bdf.bus_number = 0x40 + k;
+    }
+    lm->links[k].bit_rate = 38;
+    lm->links[k].max_bandwidth = 608;
+    lm->links[k].link_type = AMDSMI_LINK_TYPE_XGMI;
+  }
+  (void)h;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+}  // extern "C"

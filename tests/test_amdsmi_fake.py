@@ -1,0 +1,137 @@
+"""The REAL AmdSmiBackend (dlopen table, metrics parsing, N/A handling, resize paths, fallbacks)
+exercised on CPU against build/fakes/libfake_amd_smi.so (csrc/fakes/fake_amd_smi.cpp), which
+returns MI355X-shaped gpu_metrics v1.8 tables."""
+
+import os
+import subprocess
+
+import pytest
+
+from gpumon.export import promtext
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAKE = os.path.join(ROOT, "build", "fakes", "libfake_amd_smi.so")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def fake_lib():
+    subprocess.run(["make", "-C", ROOT, "fakes"], check=True, stdout=subprocess.DEVNULL)
+    return FAKE
+
+
+@pytest.fixture
+def fake_exporter(core, monkeypatch):
+    made = []
+
+    def make(env=None, **over):
+        for k in ("FAKE_AMDSMI_GPUS", "FAKE_AMDSMI_PROCS", "FAKE_AMDSMI_FAIL_METRICS", "FAKE_AMDSMI_INIT_FAIL",
+                  "FAKE_AMDSMI_NO_METRICS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in (env or {}).items():
+            monkeypatch.setenv(k, str(v))
+        cfg = {"backend": "amdsmi", "amdsmi_lib": FAKE, "serve_http": False, "interval_s": 0, "host": "n1",
+               "verify_kfd": False, "init_retry_s": 0.0}
+        cfg.update(over)
+        ex = core.Exporter(cfg)
+        err = ex.start()
+        made.append(ex)
+        return ex, err
+
+    yield make
+    for ex in made:
+        ex.stop()
+
+
+def test_enumeration_sorted_by_hip_id_and_statics(fake_exporter):
+    ex, err = fake_exporter({"FAKE_AMDSMI_GPUS": 4})
+    assert err == ""
+    st = ex.statics()
+    assert [s["gpu_id"] for s in st] == ["0", "1", "2", "3"]  # the fake hands them out reversed
+    assert st[1]["bdf"] == "0000:46:00.0"
+    assert st[0]["gfx_target"] == "gfx950" and st[0]["num_cu"] == 256
+    assert st[0]["power_limit_w"] == 1400  # microwatt power_limit normalised
+    assert st[0]["compute_partition"] == "SPX" and st[0]["memory_partition"] == "NPS1"
+    assert st[0]["vram_total_bytes"] == 294896 * 2 ** 20
+
+
+def test_metrics_table_fields_and_na_omission(fake_exporter):
+    ex, _ = fake_exporter()
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "node_gpu_gpu_util", gpu_id="0") == 37
+    assert promtext.one(fam, "node_gpu_mem_bw_util", gpu_id="0") == 12
+    assert not promtext.values(fam, "gpu_temperature_celsius", gpu_id="0", sensor="edge")  # N/A
+    assert promtext.one(fam, "gpu_temperature_celsius", gpu_id="1", sensor="hotspot") == 47
+    assert promtext.one(fam, "gpu_pcie_link_speed_gts", gpu_id="0") == 32
+    assert len(promtext.values(fam, "gpu_xcd_busy_percent", gpu_id="0")) == 8
+    clk = promtext.values(fam, "gpu_xcd_clock_mhz", gpu_id="0")
+    assert sorted(clk) == [2093, 2094, 2095, 2096, 2097, 2098, 2099, 2100]
+    links = {l["link"]: (l["peer_bdf"], v) for _, l, v in fam["gpu_xgmi_link_up"]["samples"] if l["gpu_id"] == "0"}
+    assert set(links) == {str(k) for k in range(1, 8)}  # slot 0 (N/A status) is not a link
+    assert links["3"] == ("0000:43:00.0", 1)
+    assert promtext.one(fam, "gpu_xgmi_link_max_bandwidth_bytes_per_second", gpu_id="0", link="1") == 76e9
+    assert "gpu_fan_rpm" not in fam and "gpu_voltage_volts" not in fam  # all N/A
+
+
+def test_rates_from_accumulators(fake_exporter):
+    ex, _ = fake_exporter()
+    ex.tick()
+    r = ex.rates()[0]
+    assert r["valid"] and r["dt_s"] == pytest.approx(1.0)  # driver timestamp, not host time
+    assert r["power_from_energy_w"] == pytest.approx(15.3, rel=1e-3)
+    assert r["gfx_activity_avg_pct"] == pytest.approx(37.0)
+    assert r["ppt_violation_pct"] == pytest.approx(10.0)
+    assert r["xcd_busy_avg"] == pytest.approx([37.0] * 8)
+    assert r["xgmi_rd_Bps"][3] == pytest.approx(3 * 1024e6)
+    fam = promtext.parse(ex.metrics_text())
+    u = promtext.one(fam, "gpu_xgmi_link_utilization_ratio", gpu_id="0", link="7")
+    assert u == pytest.approx((7 * 1024e6 + 3.5 * 1024e6) * 8 / (608e9 * 2))
+
+
+def test_process_list_resize_path(fake_exporter):
+    ex, _ = fake_exporter({"FAKE_AMDSMI_GPUS": 1, "FAKE_AMDSMI_PROCS": 150})
+    ex.tick()
+    rows = ex.pod_rows()
+    assert len(rows) == 150  # > the initial 64-entry buffer: OUT_OF_RESOURCES -> grow -> retry
+    assert {r["procname"] for r in rows} >= {"worker-0", "worker-149"}
+    assert max(r["used_memory_bytes"] for r in rows) == 150 * 2 ** 30
+
+
+def test_per_device_failure_isolated(fake_exporter):
+    ex, _ = fake_exporter({"FAKE_AMDSMI_GPUS": 3, "FAKE_AMDSMI_FAIL_METRICS": 1})
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    # gpu 1 lost its metrics table but VRAM still answers -> still "up" with partial data
+    assert promtext.one(fam, "gpu_up", gpu_id="1") == 1
+    assert not promtext.values(fam, "node_gpu_gpu_util", gpu_id="1")
+    assert promtext.one(fam, "node_gpu_mem_used", gpu_id="1") == 283 + 1024
+    assert promtext.one(fam, "gpumon_sample_errors_total", gpu_id="1") >= 1
+    assert promtext.one(fam, "gpumon_backend_call_errors_total", call="gpu_metrics") >= 1
+    assert promtext.one(fam, "node_gpu_gpu_util", gpu_id="2") == 37
+
+
+def test_no_metrics_table_falls_back_to_activity_api(fake_exporter):
+    ex, _ = fake_exporter({"FAKE_AMDSMI_GPUS": 2, "FAKE_AMDSMI_NO_METRICS": 1})
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "node_gpu_gpu_util", gpu_id="1") == 12  # amdsmi_get_gpu_activity
+    assert promtext.one(fam, "gpumon_backend_calls_total", call="gpu_activity") >= 2
+
+
+def test_init_failure_then_recovery(fake_exporter, monkeypatch):
+    ex, err = fake_exporter({"FAKE_AMDSMI_INIT_FAIL": 1})
+    assert "INIT_ERROR" in err
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpumon_backend_up") == 0
+    monkeypatch.delenv("FAKE_AMDSMI_INIT_FAIL")
+    ex.tick()  # init_retry_s = 0: retried on the next tick
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpumon_backend_up") == 1
+    assert len(promtext.values(fam, "node_gpu_gpu_util")) == 2
+
+
+def test_device_filter_and_replicate(fake_exporter):
+    ex, _ = fake_exporter({"FAKE_AMDSMI_GPUS": 4}, devices=[2], backend="amdsmi:replicate=3")
+    st = ex.statics()
+    assert [s["gpu_id"] for s in st] == ["2", "1", "2"] or len(st) == 3
+    assert all(s["bdf"] == "0000:66:00.0" for s in st)

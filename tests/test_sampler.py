@@ -144,6 +144,20 @@ def test_parallel_device_sampling(core):
     assert dt < 0.12, dt  # 8 x 20 ms sequential would be >= 160 ms
 
 
+def test_backend_reinit_after_total_failure(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=2", reinit_after=3, init_retry_s=0.0)
+    ex.mock_set_fail(-2, -1)  # every device, every call
+    for _ in range(3):
+        ex.tick()
+    assert ex.self_stats()["backend_reinits"] == 1
+    ex.mock_set_fail(-1, 0)
+    ex.tick()  # re-initialised on this tick, samples again
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpumon_backend_up") == 1
+    assert promtext.values(fam, "gpu_up") == [1, 1]
+    assert promtext.one(fam, "gpumon_backend_reinits_total") == 1
+
+
 def test_device_filter(core):
     ex = core.Exporter({"backend": "mock:gpus=8", "serve_http": False, "interval_s": 0, "devices": [1, 3]})
     ex.start()
