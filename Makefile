@@ -85,7 +85,11 @@ $(PMCEXT): csrc/pmc/pmc_module.cpp
 
 # Fake libamd_smi (CPU tests of the real amdsmi backend through the dlopen table).
 FAKESMI := build/fakes/libfake_amd_smi.so
-fakes: $(FAKESMI)
-$(FAKESMI): csrc/fakes/fake_amd_smi.cpp
+FAKERSMI := build/fakes/libfake_rocm_smi.so
+fakes: $(FAKESMI) $(FAKERSMI)
+$(FAKESMI): csrc/fakes/fake_amd_smi.cpp csrc/fakes/fake_metrics.h
+	@mkdir -p $(dir $@)
+	$(CXX) -O1 -std=c++17 -fPIC -shared -I$(ROCM)/include $< -o $@
+$(FAKERSMI): csrc/fakes/fake_rocm_smi.cpp csrc/fakes/fake_metrics.h
 	@mkdir -p $(dir $@)
 	$(CXX) -O1 -std=c++17 -fPIC -shared -I$(ROCM)/include $< -o $@

@@ -37,6 +37,7 @@ ExporterConfig config_from(const py::dict& d) {
   ExporterConfig c;
   get(d, "backend", &c.backend);
   get(d, "amdsmi_lib", &c.amdsmi_lib);
+  get(d, "rocm_smi_lib", &c.rocm_smi_lib);
   get(d, "devices", &c.devices);
   get(d, "interval_s", &c.interval_s);
   get(d, "serve_http", &c.serve_http);

@@ -175,6 +175,35 @@ class AmdSmiBackend : public Backend {
   std::vector<std::vector<char>> proc_buf_;  // reusable process-list buffers
 };
 
+// ---------------------------------------------------------------------------------------------
+// rocm_smi_lib fallback (dlopen'd librocm_smi64), same firmware table
+// ---------------------------------------------------------------------------------------------
+struct RsmiTable;
+
+class RocmSmiBackend : public Backend {
+ public:
+  explicit RocmSmiBackend(std::string lib_path = "");
+  ~RocmSmiBackend() override;
+  std::string name() const override { return "rocm_smi"; }
+  bool init(std::string* err) override;
+  void shutdown() override;
+  int device_count() const override { return static_cast<int>(devs_.size()); }
+  const DeviceStatic& static_info(int i) const override { return devs_[i]; }
+  void sample(int i, DeviceSample* out) override;
+  bool processes(int i, std::vector<ProcSample>* out) override;
+  std::string lib_version() const { return lib_version_; }
+
+ private:
+  std::string lib_path_;
+  std::unique_ptr<RsmiTable> t_;
+  bool inited_ = false;
+  bool metrics_ok_ = true;
+  std::vector<DeviceStatic> devs_;
+  std::vector<uint32_t> idx_;  // rsmi device index per exported device
+  std::string lib_version_;
+  double energy_res_uj_ = 15.3;
+};
+
 std::unique_ptr<Backend> make_backend(const std::string& spec, std::string* err);
 
 // Field-name registry (used by mock "unsupported" lists and tests).

@@ -114,8 +114,10 @@ std::unique_ptr<Backend> make_backend_from_config(const ExporterConfig& cfg, std
     size_t p = cfg.backend.find("replicate=");
     if (p != std::string::npos) a->set_replicate(atoi(cfg.backend.c_str() + p + 10));
     b = std::move(a);
+  } else if (cfg.backend == "rocm_smi") {
+    b = std::make_unique<RocmSmiBackend>(cfg.rocm_smi_lib);
   } else {
-    if (err) *err = "unknown backend '" + cfg.backend + "' (amdsmi | mock[:k=v,...] | auto)";
+    if (err) *err = "unknown backend '" + cfg.backend + "' (amdsmi | rocm_smi | mock[:k=v,...] | auto)";
     return nullptr;
   }
   b->set_device_filter(cfg.devices);
@@ -146,7 +148,21 @@ bool Exporter::ensure_backend() {
   next_init_ns_ = now + static_cast<int64_t>(cfg_.init_retry_s * 1e9);
   std::string err;
   if (!backend_) backend_ = make_backend_from_config(cfg_, &err);
-  if (!backend_ || !backend_->init(&err)) {
+  bool ok = backend_ && backend_->init(&err);
+  if (!ok && cfg_.backend == "auto" && backend_ && backend_->name() == "amdsmi") {
+    // auto: libamd_smi missing or failing -> rocm_smi_lib behind the same kind of dlopen table
+    auto fb = std::make_unique<RocmSmiBackend>(cfg_.rocm_smi_lib);
+    fb->set_device_filter(cfg_.devices);
+    std::string err2;
+    if (fb->init(&err2)) {
+      GPUMON_LOG(LogLevel::kWarn, "exporter", "amdsmi unavailable (" + err + "); using rocm_smi fallback");
+      backend_ = std::move(fb);
+      ok = true;
+    } else {
+      err += "; rocm_smi fallback: " + err2;
+    }
+  }
+  if (!ok) {
     if (err != backend_err_)
       GPUMON_LOG(LogLevel::kError, "exporter", "backend init failed: " + err);
     backend_err_ = err;
@@ -691,6 +707,7 @@ SelfStats Exporter::self_stats() const {
   s.version = cfg_.version;
   s.backend = backend_ ? backend_->name() : cfg_.backend;
   if (auto* a = dynamic_cast<AmdSmiBackend*>(backend_.get())) s.backend_version = a->lib_version();
+  if (auto* r = dynamic_cast<RocmSmiBackend*>(backend_.get())) s.backend_version = r->lib_version();
   s.backend_up = backend_up_;
   s.backend_reinits = reinits_;
   s.ticks = ticks_;

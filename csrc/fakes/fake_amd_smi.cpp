@@ -19,6 +19,8 @@
 #include <cstring>
 #include <vector>
 
+#include "fake_metrics.h"
+
 namespace {
 int g_gpus = 2, g_procs = 1, g_fail_metrics = -1;
 bool g_no_metrics = false;
@@ -177,52 +179,7 @@ amdsmi_status_t amdsmi_get_gpu_metrics_info(amdsmi_processor_handle h, amdsmi_gp
   int d = dev_of(h);
   if (g_no_metrics) return AMDSMI_STATUS_NOT_SUPPORTED;
   if (d == g_fail_metrics) return AMDSMI_STATUS_BUSY;
-  uint64_t n = ++g_calls[d];  // advances once per tick
-  memset(m, 0xFF, sizeof *m);  // every field N/A unless set below (firmware convention)
-  m->common_header.format_revision = 1;
-  m->common_header.content_revision = 8;
-  m->temperature_hotspot = 46 + d;
-  m->temperature_mem = 33;
-  m->temperature_vrsoc = 43;
-  m->average_gfx_activity = 37;
-  m->average_umc_activity = 12;
-  m->current_socket_power = 600;
-  m->energy_accumulator = 1000000 + n * 1000000;  // x15.3 uJ per tick
-  m->system_clock_counter = n * 1000000000ull;     // 1 s per tick (driver ns)
-  m->firmware_timestamp = n * 100000000ull;
-  m->current_gfxclk = 2100;
-  m->current_uclk = 2000;
-  m->current_socclk = 1200;
-  m->throttle_status = 0;
-  m->pcie_link_width = 16;
-  m->pcie_link_speed = 320;
-  m->pcie_bandwidth_inst = 18;
-  m->pcie_replay_count_acc = 0;
-  m->gfx_activity_acc = static_cast<uint32_t>(n * 37 * 1000);  // 37 % per counter tick
-  m->mem_activity_acc = static_cast<uint32_t>(n * 12 * 1000);
-  m->accumulation_counter = n * 1000;
-  m->ppt_residency_acc = n * 100;  // 10 % PVIOL
-  m->prochot_residency_acc = 0;
-  m->socket_thm_residency_acc = 0;
-  m->vr_thm_residency_acc = 0;
-  m->hbm_thm_residency_acc = 0;
-  m->xgmi_link_speed = 38;
-  m->xgmi_link_width = 16;
-  m->vram_max_bandwidth = 8192;
-  m->num_partition = 1;
-  for (int k = 0; k < 8; ++k) {
-    m->current_gfxclks[k] = static_cast<uint16_t>(2100 - k);
-    m->xcp_stats[0].gfx_busy_inst[k] = 37;
-    m->xcp_stats[0].gfx_busy_acc[k] = n * 37 * 1000;
-  }
-  m->xgmi_link_status[0] = 0xFFFF;   // slot 0: N/A on MI355X
-  m->xgmi_read_data_acc[0] = 0;
-  m->xgmi_write_data_acc[0] = 0;
-  for (int k = 1; k < 8; ++k) {
-    m->xgmi_link_status[k] = 1;
-    m->xgmi_read_data_acc[k] = n * 1000000ull * k;  // k GB/s (KB units, 1 s per tick)
-    m->xgmi_write_data_acc[k] = n * 500000ull * k;
-  }
+  fake::fill_metrics(m, d, ++g_calls[d]);  // advances once per tick
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -29,8 +29,9 @@ REFERENCE_DEFAULT_INFLUX = "http://10.0.4.235:9000/write?db=gpu_process"  # gpu.
 @dataclass
 class Config:
     # device backend
-    backend: str = "auto"                 # auto | amdsmi | mock[:k=v,...]
+    backend: str = "auto"                 # auto | amdsmi | rocm_smi | mock[:k=v,...]
     amdsmi_lib: str = ""
+    rocm_smi_lib: str = ""                # librocm_smi64 override (rocm_smi backend / auto fallback)
     devices: List[int] = field(default_factory=list)
     interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
     processes: bool = True
@@ -90,6 +91,7 @@ class Config:
         return {
             "backend": self.backend,
             "amdsmi_lib": self.amdsmi_lib,
+            "rocm_smi_lib": self.rocm_smi_lib,
             "devices": list(self.devices),
             "interval_s": float(self.interval),
             "processes": self.processes,
@@ -183,7 +185,8 @@ def load_yaml(path: str) -> Dict[str, Any]:
 def add_cli_args(p: argparse.ArgumentParser) -> None:
     d = Config()
     p.add_argument("--config", default=os.environ.get("GPUMON_CONFIG", ""), help="YAML config file")
-    p.add_argument("--backend", help=f"amdsmi | mock[:gpus=N,...] | auto (default {d.backend})")
+    p.add_argument("--backend", help=f"amdsmi | rocm_smi | mock[:gpus=N,...] | auto (default {d.backend}; "
+                   "auto = amdsmi, falling back to rocm_smi)")
     p.add_argument("--devices", help="comma-separated hip ids to monitor (default all)")
     p.add_argument("--interval", type=float, help=f"sampling interval seconds (default {d.interval})")
     p.add_argument("--listen", help=f"ADDR:PORT for /metrics (default {d.listen})")
