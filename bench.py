@@ -111,7 +111,7 @@ def main() -> int:
             backend = "amdsmi" if has_gpu else f"mock:gpus={n * args.replicate},mode=load"
             if has_gpu and args.replicate > 1:
                 backend = f"amdsmi:replicate={args.replicate}"
-        cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith("amdsmi") else [],
+        cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi")) else [],
                      interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
                      enable_probe=args.probe and has_gpu, log_level="warn",
                      sample_threads=args.sample_threads)
@@ -182,12 +182,12 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / max(1, len(sm)) / BASELINE_SAMPLES_PER_GPU, 3),
             "dtype": "bf16",
-            "data": ("synthetic" if backend == "amdsmi" else
+            "data": ("synthetic" if backend in ("amdsmi", "rocm_smi") else
                      f"synthetic (REHEARSAL: {n} physical GPU(s) each sampled {args.replicate}x)"
                      if backend.startswith("amdsmi:replicate") else "synthetic (mock backend: no GPU visible)"),
             "sampled_devices": len(sm),
             "config": {
-                "model": "gpumon MI355X exporter (amdsmi backend) + synthetic bf16 MFMA/HBM HIP load",
+                "model": f"gpumon MI355X exporter ({backend.split(':')[0]} backend) + synthetic bf16 MFMA/HBM HIP load",
                 "global_batch": n,
                 "seq_len": None,
                 "parallelism": f"node-local exporter over {n} GPU(s); one rank per GPU"

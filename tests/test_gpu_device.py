@@ -72,6 +72,37 @@ def test_amdsmi_static_and_sample_sane(core, torch_gpu):
         ex.stop()
 
 
+def test_rocm_smi_backend_agrees_with_amdsmi(core, torch_gpu):
+    """The rocm_smi_lib fallback reads the same firmware table: same device (matched by BDF),
+    same VRAM size, 8 XCDs, 7 up xGMI links, sane temperature."""
+    am = _exporter(core)
+    try:
+        ref = am.statics()[0]
+        am.tick()
+        ref_s = am.samples()[0]
+    finally:
+        am.stop()
+    rs = core.Exporter({"backend": "rocm_smi", "serve_http": False, "interval_s": 0.0, "host": "gpu-box"})
+    err = rs.start()
+    try:
+        assert err == "", err
+        st = rs.statics()
+        match = [i for i, s in enumerate(st) if s["bdf"].lower() == ref["bdf"].lower()]
+        assert match, ([s["bdf"] for s in st], ref["bdf"])
+        i = match[0]
+        assert st[i]["vram_total_bytes"] == pytest.approx(ref["vram_total_bytes"])
+        rs.tick()
+        sm = rs.samples()[i]
+        assert sm["ok"], sm["last_error"]
+        assert len(sm["xcd_busy"]) == 8
+        assert sum(1 for l in sm["links"] if l["status"] == 1) == 7
+        assert abs(sm["fields"]["temp_hotspot"] - ref_s["fields"]["temp_hotspot"]) < 10
+        print(f"\nrocm_smi: {len(st)} device(s), version {rs.self_stats()['backend_version']}, "
+              f"sample {sm['sample_ns'] / 1e3:.0f} us vs amdsmi {ref_s['sample_ns'] / 1e3:.0f} us")
+    finally:
+        rs.stop()
+
+
 def test_mfma_tile_matches_torch_fp32(H, torch_gpu):
     torch = torch_gpu
     g = torch.Generator(device="cpu").manual_seed(0)
