@@ -45,6 +45,22 @@ def _pct(xs, q):
     return xs[f] if f == c else xs[f] + (xs[c] - xs[f]) * (k - f)
 
 
+def _xgmi_summary(xgmi, xgmi_rates):
+    """Exporter-measured xGMI traffic over the timed ticks (mean per GPU), next to the all-reduce
+    expectation. The first tick's rate spans part of the warmup, so it is skipped."""
+    ticks = [t for t in xgmi_rates[1:] if t] or [t for t in xgmi_rates if t]
+    out = dict(xgmi or {})
+    if ticks:
+        tx = [sum(w for w, _ in t) / len(t) for t in ticks]
+        rx = [sum(r for _, r in t) / len(t) for t in ticks]
+        out["exporter_tx_GBps_per_gpu"] = round(sum(tx) / len(tx) / 1e9, 3)
+        out["exporter_rx_GBps_per_gpu"] = round(sum(rx) / len(rx) / 1e9, 3)
+        exp = out.get("expected_tx_GBps_per_gpu")
+        if exp:
+            out["exporter_vs_expected"] = round(out["exporter_tx_GBps_per_gpu"] / exp, 3)
+    return out or None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -143,18 +159,43 @@ def main() -> int:
     t0 = time.perf_counter()
     if scraper is not None:
         scraper.start()
+    xgmi_rates = []  # per tick: (sum of per-link write B/s, sum of read B/s) per sampled device
+    ar_events = []
     for step in range(args.steps):
         if rank == 0:
             if not mon.ex.wait_for_seq(seq0 + step + 1, args.interval * 5 + 10):
                 raise SystemExit("exporter tick timed out")
+            xgmi_rates.append([(sum(r.get("xgmi_wr_Bps") or [0.0]), sum(r.get("xgmi_rd_Bps") or [0.0]))
+                               for r in mon.ex.rates() if r.get("valid")])
         if ar_buf is not None:
-            dist.all_reduce(ar_buf)
+            if has_gpu:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
+                dist.all_reduce(ar_buf)
+                ev[1].record()
+                ar_events.append(ev)
+            else:
+                dist.all_reduce(ar_buf)
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # xGMI cross-check (N > 1): RCCL ring all-reduce bus bandwidth vs the exporter's own per-link
+    # xGMI counters. A ring all-reduce of S bytes moves 2(n-1)/n * S out of every GPU per call.
+    xgmi = None
+    if ar_buf is not None:
+        nbytes = ar_buf.numel() * ar_buf.element_size()
+        ar_ms = [a.elapsed_time(b) for a, b in ar_events] if ar_events else []
+        t = torch.tensor([sum(ar_ms) / len(ar_ms) if ar_ms else float("nan")], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ar_mean_s = float(t.item()) * 1e-3
+        xgmi = {"allreduce_mb": args.allreduce_mb, "allreduce_ms": round(ar_mean_s * 1e3, 3),
+                "allreduce_busbw_GBps": round(2 * (n - 1) / n * nbytes / ar_mean_s / 1e9, 2)
+                if ar_mean_s == ar_mean_s and ar_mean_s > 0 else None,
+                "expected_tx_GBps_per_gpu": round(2 * (n - 1) / n * nbytes * args.steps / elapsed / 1e9, 3)}
 
     result = None
     if rank == 0:
@@ -212,6 +253,7 @@ def main() -> int:
             "load_tbps": round(lstats.get("tbps", 0.0), 3) if lstats else None,
             "gfx_util_last": util,
             "procs_seen": len([r for r in rows if not r["idle"]]),
+            "xgmi": _xgmi_summary(xgmi, xgmi_rates),
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,
         }
         mon.stop()

@@ -58,3 +58,8 @@ def test_bench_two_ranks_gloo():
     assert len(lines) == 1, r.stdout  # rank 0 only
     _check(lines[0], 2, 3, 1)
     assert "all-reduce" in lines[0]["config"]["parallelism"]
+    x = lines[0]["xgmi"]
+    assert x["allreduce_mb"] == 1
+    # 2 ranks: a ring all-reduce moves (2(n-1)/n) * S = 1 MiB out of each rank per step
+    assert x["expected_tx_GBps_per_gpu"] > 0
+    assert "exporter_tx_GBps_per_gpu" in x and "exporter_vs_expected" in x
