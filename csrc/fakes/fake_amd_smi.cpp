@@ -10,6 +10,8 @@
 //   FAKE_AMDSMI_FAIL_METRICS=K    gpu_metrics fails (AMDSMI_STATUS_BUSY) on device K
 //   FAKE_AMDSMI_INIT_FAIL=1       amdsmi_init returns AMDSMI_STATUS_INIT_ERROR
 //   FAKE_AMDSMI_NO_METRICS=1      gpu_metrics NOT_SUPPORTED (exercises the activity/power fallback)
+//   FAKE_AMDSMI_CPX=1             CPX compute partitioning: every socket exposes 8 logical GPUs (one
+//                                 XCD each); partition k's busy counters live in xcp_stats[k]
 // Counters advance deterministically per call so rates are checkable.
 #include <amd_smi/amdsmi.h>
 
@@ -22,7 +24,7 @@
 #include "fake_metrics.h"
 
 namespace {
-int g_gpus = 2, g_procs = 1, g_fail_metrics = -1;
+int g_gpus = 2, g_procs = 1, g_fail_metrics = -1, g_parts = 1;
 bool g_no_metrics = false;
 std::vector<uintptr_t> g_handles;
 std::atomic<uint64_t> g_calls[64];
@@ -32,8 +34,10 @@ int env_int(const char* k, int d) {
 }
 int dev_of(amdsmi_processor_handle h) {
   uintptr_t x = reinterpret_cast<uintptr_t>(h);
-  return (x >= 0x1000 && x < 0x1000 + static_cast<uintptr_t>(g_gpus)) ? static_cast<int>(x - 0x1000) : -1;
+  return (x >= 0x1000 && x < 0x1000 + static_cast<uintptr_t>(g_gpus * g_parts)) ? static_cast<int>(x - 0x1000) : -1;
 }
+int part_of(int d) { return d % g_parts; }
+int sock_of(int d) { return d / g_parts; }
 }  // namespace
 
 extern "C" {
@@ -44,8 +48,9 @@ amdsmi_status_t amdsmi_init(uint64_t) {
   g_procs = env_int("FAKE_AMDSMI_PROCS", 1);
   g_fail_metrics = env_int("FAKE_AMDSMI_FAIL_METRICS", -1);
   g_no_metrics = env_int("FAKE_AMDSMI_NO_METRICS", 0) != 0;
+  g_parts = env_int("FAKE_AMDSMI_CPX", 0) ? 8 : 1;
   g_handles.clear();
-  for (int i = 0; i < g_gpus; ++i) g_handles.push_back(0x1000 + i);
+  for (int i = 0; i < g_gpus * g_parts; ++i) g_handles.push_back(0x1000 + i);
   for (auto& c : g_calls) c = 0;
   return AMDSMI_STATUS_SUCCESS;
 }
@@ -75,12 +80,14 @@ amdsmi_status_t amdsmi_get_processor_handles(amdsmi_socket_handle s, uint32_t* c
                                              amdsmi_processor_handle* hs) {
   const uintptr_t si = reinterpret_cast<uintptr_t>(s) - 0x100;
   if (!hs) {
-    *count = 1;
+    *count = static_cast<uint32_t>(g_parts);
     return AMDSMI_STATUS_SUCCESS;
   }
-  // reverse order on purpose: the backend must sort by hip_id
-  hs[0] = reinterpret_cast<amdsmi_processor_handle>(g_handles[g_gpus - 1 - si]);
-  *count = 1;
+  // reverse socket order on purpose: the backend must sort by hip_id
+  const int sock = g_gpus - 1 - static_cast<int>(si);
+  for (int k = 0; k < g_parts && k < static_cast<int>(*count); ++k)
+    hs[k] = reinterpret_cast<amdsmi_processor_handle>(g_handles[sock * g_parts + k]);
+  *count = static_cast<uint32_t>(g_parts);
   return AMDSMI_STATUS_SUCCESS;
 }
 
@@ -109,7 +116,8 @@ amdsmi_status_t amdsmi_get_gpu_device_uuid(amdsmi_processor_handle h, unsigned i
 amdsmi_status_t amdsmi_get_gpu_device_bdf(amdsmi_processor_handle h, amdsmi_bdf_t* b) {
   int d = dev_of(h);
   b->as_uint = 0;
-  b->bus_number = 0x26 + 0x20 * d;
+  b->bus_number = 0x26 + 0x20 * sock_of(d);
+  b->function_number = part_of(d);  // CPX partitions: one PCI function each
   return AMDSMI_STATUS_SUCCESS;
 }
 
@@ -125,7 +133,7 @@ amdsmi_status_t amdsmi_get_gpu_asic_info(amdsmi_processor_handle, amdsmi_asic_in
 amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle h, amdsmi_kfd_info_t* k) {
   k->kfd_id = 36622 + dev_of(h);
   k->node_id = 2 + dev_of(h);
-  k->current_partition_id = 0;
+  k->current_partition_id = static_cast<uint32_t>(part_of(dev_of(h)));
   return AMDSMI_STATUS_SUCCESS;
 }
 
@@ -137,7 +145,7 @@ amdsmi_status_t amdsmi_get_gpu_driver_info(amdsmi_processor_handle, amdsmi_drive
 }
 
 amdsmi_status_t amdsmi_get_gpu_compute_partition(amdsmi_processor_handle, char* p, uint32_t len) {
-  snprintf(p, len, "SPX");
+  snprintf(p, len, g_parts > 1 ? "CPX" : "SPX");
   return AMDSMI_STATUS_SUCCESS;
 }
 
@@ -179,7 +187,15 @@ amdsmi_status_t amdsmi_get_gpu_metrics_info(amdsmi_processor_handle h, amdsmi_gp
   int d = dev_of(h);
   if (g_no_metrics) return AMDSMI_STATUS_NOT_SUPPORTED;
   if (d == g_fail_metrics) return AMDSMI_STATUS_BUSY;
-  fake::fill_metrics(m, d, ++g_calls[d]);  // advances once per tick
+  const uint64_t n = ++g_calls[d];  // advances once per tick
+  fake::fill_metrics(m, sock_of(d), n);
+  if (g_parts > 1) {
+    // CPX: every logical GPU returns the socket table; XCP k holds partition k's single XCC
+    const int k = part_of(d);
+    memset(m->xcp_stats, 0xFF, sizeof m->xcp_stats);
+    m->xcp_stats[k].gfx_busy_inst[0] = static_cast<uint32_t>(10 * k + 5);
+    m->xcp_stats[k].gfx_busy_acc[0] = n * (10 * k + 5) * 1000;
+  }
   return AMDSMI_STATUS_SUCCESS;
 }
 

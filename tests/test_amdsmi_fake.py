@@ -135,3 +135,25 @@ def test_device_filter_and_replicate(fake_exporter):
     st = ex.statics()
     assert [s["gpu_id"] for s in st] == ["2", "1", "2"] or len(st) == 3
     assert all(s["bdf"] == "0000:66:00.0" for s in st)
+
+
+def test_cpx_partition_mode(fake_exporter):
+    """CPX: 8 logical GPUs per socket, each with ONE XCD whose counters live in
+    xcp_stats[partition_id] (SURVEY.md §7.3 hard part 2)."""
+    ex, err = fake_exporter({"FAKE_AMDSMI_GPUS": 2, "FAKE_AMDSMI_CPX": 1})
+    assert err == ""
+    st = ex.statics()
+    assert len(st) == 16
+    assert [s["gpu_id"] for s in st] == [str(i) for i in range(16)]
+    assert {s["compute_partition"] for s in st} == {"CPX"}
+    assert [s["partition_id"] for s in st[:8]] == list(range(8))
+    assert st[3]["bdf"] == "0000:26:00.3" and st[11]["bdf"] == "0000:46:00.3"
+    ex.tick()
+    ex.tick()
+    for i in (0, 3, 9):
+        sm = ex.samples()[i]
+        assert sm["xcd_busy"] == [10 * (i % 8) + 5]  # exactly one XCD, from its own XCP slot
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_xcd_busy_percent", gpu_id="3", xcd="0") == 35
+    assert promtext.one(fam, "gpu_xcd_busy_avg_percent", gpu_id="3", xcd="0") == pytest.approx(35)
+    assert len(promtext.values(fam, "gpu_xcd_busy_percent")) == 16
