@@ -12,6 +12,7 @@
 #include "../core/http_client.h"
 #include "../core/render.h"
 #include "../core/snapshot.h"
+#include "../core/trace.h"
 
 namespace py = pybind11;
 using namespace gpumon;
@@ -46,6 +47,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "http_threads", &c.http_threads);
   get(d, "host", &c.host);
   get(d, "gzip", &c.gzip);
+  get(d, "roctx", &c.roctx);
   get(d, "compat_families", &c.compat_families);
   get(d, "extended_families", &c.extended_families);
   get(d, "full_device_labels", &c.full_device_labels);
@@ -249,6 +251,10 @@ PYBIND11_MODULE(_core, m) {
     append_double(v, &o);
     return o;
   });
+  m.def("roctx_enable", &Roctx::enable, py::arg("on") = true,
+        "Load librocprofiler-sdk-roctx and bracket sampler phases with ROCTx ranges");
+  m.def("roctx_active", &Roctx::active);
+  m.def("roctx_ranges", &Roctx::ranges, "ROCTx ranges opened so far by this process");
   m.def("gzip", [](const std::string& s) {
     std::string o;
     if (!gzip_compress(s, &o)) throw std::runtime_error("gzip failed");

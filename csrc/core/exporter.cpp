@@ -6,10 +6,12 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstring>
 #include <functional>
 
 #include "common.h"
 #include "http_client.h"
+#include "trace.h"
 
 namespace gpumon {
 
@@ -189,6 +191,10 @@ bool Exporter::ensure_backend() {
 
 bool Exporter::start(std::string* err) {
   if (running_) return true;
+  const char* rx = getenv("GPUMON_ROCTX");
+  if (cfg_.roctx || (rx && *rx && strcmp(rx, "0") != 0)) {
+    if (!Roctx::enable(true)) GPUMON_LOG(LogLevel::kWarn, "exporter", "roctx requested but librocprofiler-sdk-roctx not found");
+  }
   if (!ensure_backend() && cfg_.backend != "auto" && !starts_with(cfg_.backend, "mock")) {
     // explicit amdsmi: keep running (retry with backoff) but report the error to the caller
     if (err) *err = backend_err_;
@@ -271,6 +277,7 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
   // One task per device: metrics table, (links), process list. With a pool the devices run in
   // parallel (amdsmi calls are per-device sysfs/ioctl I/O).
   auto one = [&](int i) {
+    TraceRange tr("gpumon.sample_dev");
     backend_->sample(i, &(*out)[i]);
     if (links_due(i)) backend_->sample_links(i, &(*out)[i]);
     if (cfg_.processes && (*out)[i].ok) {
@@ -380,6 +387,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
 
 TickInfo Exporter::tick() {
   std::lock_guard<std::mutex> tl(tick_mu_);
+  TraceRange trace_tick("gpumon.tick");
   TickInfo info;
   int64_t t0 = mono_ns();
   std::vector<DeviceSample> cur;
@@ -395,7 +403,10 @@ TickInfo Exporter::tick() {
       statics = statics_;
     }
     int64_t ta = mono_ns();
-    sample_devices(&cur, &procs, &info.t_procs);
+    {
+      TraceRange tr("gpumon.sample");
+      sample_devices(&cur, &procs, &info.t_procs);
+    }
     int n = static_cast<int>(cur.size());
     info.t_sample = (mono_ns() - ta) * 1e-9;
     rates.resize(n);
@@ -442,7 +453,10 @@ TickInfo Exporter::tick() {
       proc_counts[i] = procs[i].size();
     }
     int64_t tb = mono_ns();
-    build_pod_rows(procs, cur, &rows);
+    {
+      TraceRange tr("gpumon.attrib");
+      build_pod_rows(procs, cur, &rows);
+    }
     info.t_attrib = (mono_ns() - tb) * 1e-9;
     info.devices = n;
     // Whole-backend failure (driver reload, amdsmi lost its handles): re-initialise with backoff
@@ -484,10 +498,16 @@ TickInfo Exporter::tick() {
   auto snap = std::make_shared<Snapshot>();
   snap->body.reserve(64 * 1024);
   int64_t tr = mono_ns();
-  render_prometheus(in, &snap->body);
+  {
+    TraceRange trr("gpumon.render");
+    render_prometheus(in, &snap->body);
+  }
   int64_t tz = mono_ns();
   info.t_render = (tz - tr) * 1e-9;
-  if (cfg_.gzip) gzip_compress(snap->body, &snap->body_gz, 1);
+  if (cfg_.gzip) {
+    TraceRange trz("gpumon.gzip");
+    gzip_compress(snap->body, &snap->body_gz, 1);
+  }
   info.t_gzip = (mono_ns() - tz) * 1e-9;
   phase_ns_[0] += static_cast<uint64_t>(info.t_sample * 1e9);
   phase_ns_[1] += static_cast<uint64_t>(info.t_procs * 1e9);

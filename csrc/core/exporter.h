@@ -42,6 +42,7 @@ struct ExporterConfig {
   int http_threads = 2;
   std::string host = "no_name";       // NODE_NAME (reference fallback "no_name", gpu.py:23-24)
   bool gzip = true;
+  bool roctx = false;                 // ROCTx ranges around sampler phases (also GPUMON_ROCTX=1)
   bool compat_families = true;
   bool extended_families = true;
   bool full_device_labels = false;

@@ -66,6 +66,7 @@ class Config:
     enable_probe: bool = False
     probe_every: int = 1
     enable_pmc: bool = False
+    roctx: bool = False                   # ROCTx ranges around sampler phases (rocprofv3 --marker-trace)
     # the counters gpumon.ops.pmc.derive() needs (2 SQ + 2 GRBM slots: one counting pass on gfx950)
     pmc_counters: List[str] = field(default_factory=lambda: ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES",
                                                              "GRBM_GUI_ACTIVE", "GRBM_COUNT"])
@@ -102,6 +103,7 @@ class Config:
             "http_threads": int(self.http_threads),
             "host": self.resolved_host(),
             "gzip": self.gzip,
+            "roctx": self.roctx,
             "compat_families": self.compat_families,
             "extended_families": self.extended_families,
             "influx_url": self.influx_url,
@@ -204,6 +206,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--sample-threads", dest="sample_threads", type=int)
     p.add_argument("--enable-probe-kernel", dest="enable_probe", action="store_true", default=None)
     p.add_argument("--enable-pmc", dest="enable_pmc", action="store_true", default=None)
+    p.add_argument("--roctx", dest="roctx", action="store_true", default=None,
+                   help="bracket sampler phases with ROCTx ranges (view with rocprofv3 --marker-trace)")
     p.add_argument("--compat", action="store_true",
                    help="reference behaviour: opt-in label mlgpu=mlgpu and 10 s interval")
     p.add_argument("--log-level", dest="log_level")
