@@ -247,6 +247,9 @@ def main() -> int:
             "tick_p99_ms": round(mon.ex.sample_quantile(0.99) * 1e3, 4),
             "server_scrape_p99_ms": round(mon.ex.scrape_quantile(0.99) * 1e3, 4),
             "overruns": s1["overruns"] - s0["overruns"],
+            "backend_call_us": {k: round((v["seconds"] - s0["backend_calls"].get(k, {}).get("seconds", 0.0)) * 1e6
+                                         / max(1, v["n"] - s0["backend_calls"].get(k, {}).get("n", 0)), 1)
+                                for k, v in s1.get("backend_calls", {}).items()},
             "backend": backend,
             "load": args.load if has_gpu else "none",
             "load_tflops": round(lstats.get("tflops", 0.0), 1) if lstats else None,

@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include "../core/attribution.h"
+#include "../core/backend.h"
 #include "../core/common.h"
 #include "../core/exporter.h"
 #include "../core/http_client.h"
@@ -39,6 +40,8 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "backend", &c.backend);
   get(d, "amdsmi_lib", &c.amdsmi_lib);
   get(d, "rocm_smi_lib", &c.rocm_smi_lib);
+  get(d, "fast_path", &c.fast_path);
+  get(d, "sysfs_root", &c.sysfs_root);
   get(d, "devices", &c.devices);
   get(d, "interval_s", &c.interval_s);
   get(d, "serve_http", &c.serve_http);
@@ -251,6 +254,27 @@ PYBIND11_MODULE(_core, m) {
     append_double(v, &o);
     return o;
   });
+  m.def(
+      "amdsmi_compare_tables",
+      [](const std::string& lib, const std::string& sys_root, int dev) {
+        AmdSmiBackend b(lib);
+        b.set_fast_path(true, sys_root, "/proc");
+        std::string err;
+        py::dict r;
+        if (!b.init(&err)) {
+          r["error"] = err;
+          return r;
+        }
+        r["fast_path_devices"] = b.fast_path_devices();
+        r["fast_path_status"] = b.fast_path_status();
+        py::list rows;
+        for (const auto& [name, a, s] : b.compare_tables(dev, &err)) rows.append(py::make_tuple(name, a, s));
+        r["rows"] = rows;
+        r["error"] = err;
+        return r;
+      },
+      py::arg("lib") = "", py::arg("sys_root") = "/sys", py::arg("dev") = 0,
+      "libamd_smi vs sysfs-decoded gpu_metrics v1.8, field by field: (name, amdsmi, sysfs)");
   m.def("roctx_enable", &Roctx::enable, py::arg("on") = true,
         "Load librocprofiler-sdk-roctx and bracket sampler phases with ROCTx ranges");
   m.def("roctx_active", &Roctx::active);
@@ -393,6 +417,17 @@ PYBIND11_MODULE(_core, m) {
              d["backend_version"] = s.backend_version;
              d["backend_up"] = s.backend_up;
              d["backend_reinits"] = s.backend_reinits;
+             d["fast_path_devices"] = s.fast_path_devices;
+             d["fast_path_status"] = s.fast_path_status;
+             py::dict calls;
+             for (const auto& c : s.backend_calls) {
+               py::dict cd;
+               cd["n"] = c.n;
+               cd["errors"] = c.errors;
+               cd["seconds"] = c.seconds;
+               calls[py::str(c.call)] = cd;
+             }
+             d["backend_calls"] = calls;
              d["influx_ok"] = s.influx_ok;
              d["influx_fail"] = s.influx_fail;
              d["influx_dropped"] = s.influx_dropped;

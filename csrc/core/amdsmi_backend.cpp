@@ -10,6 +10,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 
@@ -17,6 +18,7 @@
 #include "common.h"
 #include "metrics_table.h"
 #include "smi_table.h"
+#include "sysfs_fast.h"
 
 namespace gpumon {
 
@@ -139,6 +141,8 @@ void AmdSmiBackend::shutdown() {
   handles_.clear();
   devs_.clear();
   caps_.clear();
+  fast_.clear();
+  kfd_ids_.clear();
 }
 
 bool AmdSmiBackend::init(std::string* err) {
@@ -225,9 +229,11 @@ bool AmdSmiBackend::init(std::string* err) {
         }
       }
     }
+    uint64_t kfd_id = 0;
     if (t_->amdsmi_get_gpu_kfd_info) {
       amdsmi_kfd_info_t ki{};
       if (t_->amdsmi_get_gpu_kfd_info(h, &ki) == AMDSMI_STATUS_SUCCESS) {
+        kfd_id = ok64(ki.kfd_id) ? ki.kfd_id : 0;
         d.kfd_node = ok32(ki.node_id) ? static_cast<int>(ki.node_id) : -1;
         d.partition_id = ok32(ki.current_partition_id) ? static_cast<int>(ki.current_partition_id) : 0;
       }
@@ -263,6 +269,7 @@ bool AmdSmiBackend::init(std::string* err) {
         d.vram_total_bytes = static_cast<double>(vu.vram_total) * 1048576.0;
     }
     handles_.push_back(h);
+    kfd_ids_.push_back(kfd_id);
     devs_.push_back(std::move(d));
     caps_.emplace_back();
     proc_buf_.emplace_back(sizeof(amdsmi_proc_info_t) * 64);
@@ -276,6 +283,7 @@ bool AmdSmiBackend::init(std::string* err) {
         d.gpu_id = std::to_string(d.index);
         d.model += " (replica of hip " + std::to_string(devs_[k].hip_id) + ")";
         handles_.push_back(handles_[k]);
+        kfd_ids_.push_back(kfd_ids_[k]);
         devs_.push_back(std::move(d));
         caps_.emplace_back();
         proc_buf_.emplace_back(sizeof(amdsmi_proc_info_t) * 64);
@@ -292,9 +300,168 @@ bool AmdSmiBackend::init(std::string* err) {
     if (t_->amdsmi_get_energy_count(handles_[0], &e, &res, &ts) == AMDSMI_STATUS_SUCCESS && res > 0)
       energy_res_uj_ = res;
   }
+  // Sysfs fast path: per device, only after its decoded table matches libamd_smi's.
+  fast_.clear();
+  fast_.resize(devs_.size());
+  fast_status_ = fast_path_ ? "" : "disabled by config";
+  if (fast_path_) {
+    int ok = 0;
+    for (size_t i = 0; i < devs_.size(); ++i) {
+      auto g = std::make_unique<SysfsGpu>();
+      std::string why;
+      if (devs_[i].bdf.empty() ||
+          !g->open(sys_root_, proc_root_, devs_[i].bdf, kfd_ids_[i], devs_[i].drm_render, &why)) {
+        fast_status_ = "gpu " + devs_[i].gpu_id + ": " + (why.empty() ? "no BDF" : why);
+        continue;
+      }
+      fast_[i] = std::move(g);
+      if (!validate_fast(static_cast<int>(i), &why)) {
+        fast_[i].reset();
+        fast_status_ = "gpu " + devs_[i].gpu_id + ": " + why;
+        continue;
+      }
+      ok++;
+    }
+    if (ok == static_cast<int>(devs_.size())) fast_status_ = "sysfs";
+    GPUMON_LOG(ok ? LogLevel::kInfo : LogLevel::kWarn, "amdsmi",
+               "sysfs fast path on " + std::to_string(ok) + "/" + std::to_string(devs_.size()) +
+                   " GPU(s)" + (ok == static_cast<int>(devs_.size()) ? "" : " (" + fast_status_ + ")"));
+  }
   GPUMON_LOG(LogLevel::kInfo, "amdsmi",
              "loaded " + t_->path + " version=" + lib_version_ + " gpus=" +
                  std::to_string(devs_.size()));
+  return true;
+}
+
+int AmdSmiBackend::fast_path_devices() const {
+  int n = 0;
+  for (const auto& f : fast_) n += f != nullptr;
+  return n;
+}
+
+namespace {
+double na16(uint16_t x) { return x == 0xFFFF ? kNaN : x; }
+double na32(uint32_t x) { return x == 0xFFFFFFFFu ? kNaN : x; }
+double na64(uint64_t x) { return x == ~0ull ? kNaN : static_cast<double>(x); }
+std::string fmtd(double v) {
+  char b[32];
+  snprintf(b, sizeof b, "%.6g", v);
+  return b;
+}
+}  // namespace
+
+std::vector<std::tuple<std::string, double, double>> AmdSmiBackend::compare_tables(int i, std::string* err) {
+  std::vector<std::tuple<std::string, double, double>> out;
+  if (i < 0 || i >= static_cast<int>(devs_.size())) {
+    if (err) *err = "no such device";
+    return out;
+  }
+  amdsmi_gpu_metrics_t a;
+  if (t_->amdsmi_get_gpu_metrics_info(handles_[i], &a) != AMDSMI_STATUS_SUCCESS) {
+    if (err) *err = "amdsmi_get_gpu_metrics_info failed";
+    return out;
+  }
+  SysfsGpu own;
+  SysfsGpu* g = fast_[i].get();
+  std::string why;
+  if (!g) {
+    if (!own.open(sys_root_, proc_root_, devs_[i].bdf, kfd_ids_[i], devs_[i].drm_render, &why)) {
+      if (err) *err = why;
+      return out;
+    }
+    g = &own;
+  }
+  kgm::V18 k;
+  if (!g->read_metrics(&k, &why)) {
+    if (err) *err = why;
+    return out;
+  }
+  amdsmi_gpu_metrics_t s;
+  kgm::to_smi(k, &s);
+#define CMP16(f) out.emplace_back(#f, na16(a.f), na16(s.f));
+#define CMP32(f) out.emplace_back(#f, na32(a.f), na32(s.f));
+#define CMP64(f) out.emplace_back(#f, na64(a.f), na64(s.f));
+  out.emplace_back("structure_size", a.common_header.structure_size, s.common_header.structure_size);
+  out.emplace_back("format_revision", a.common_header.format_revision, s.common_header.format_revision);
+  out.emplace_back("content_revision", a.common_header.content_revision, s.common_header.content_revision);
+  CMP16(temperature_edge) CMP16(temperature_hotspot) CMP16(temperature_mem) CMP16(temperature_vrgfx)
+  CMP16(temperature_vrsoc) CMP16(temperature_vrmem) CMP16(average_gfx_activity) CMP16(average_umc_activity)
+  CMP16(average_mm_activity) CMP16(average_socket_power) CMP16(current_socket_power)
+  CMP64(energy_accumulator) CMP64(system_clock_counter) CMP64(firmware_timestamp)
+  CMP16(average_gfxclk_frequency) CMP16(current_gfxclk) CMP16(current_socclk) CMP16(current_uclk)
+  CMP16(current_vclk0) CMP16(current_dclk0) CMP32(throttle_status) CMP64(indep_throttle_status)
+  CMP16(current_fan_speed) CMP16(pcie_link_width) CMP16(pcie_link_speed) CMP32(gfx_activity_acc)
+  CMP32(mem_activity_acc) CMP16(voltage_soc) CMP16(voltage_gfx) CMP16(voltage_mem) CMP32(gfxclk_lock_status)
+  CMP16(xgmi_link_width) CMP16(xgmi_link_speed) CMP64(pcie_bandwidth_acc) CMP64(pcie_bandwidth_inst)
+  CMP64(pcie_l0_to_recov_count_acc) CMP64(pcie_replay_count_acc) CMP64(pcie_replay_rover_count_acc)
+  CMP32(pcie_nak_sent_count_acc) CMP32(pcie_nak_rcvd_count_acc) CMP64(accumulation_counter)
+  CMP64(prochot_residency_acc) CMP64(ppt_residency_acc) CMP64(socket_thm_residency_acc)
+  CMP64(vr_thm_residency_acc) CMP64(hbm_thm_residency_acc) CMP16(num_partition)
+  CMP32(pcie_lc_perf_other_end_recovery) CMP64(vram_max_bandwidth)
+  for (int k2 = 0; k2 < AMDSMI_MAX_NUM_XGMI_LINKS; ++k2) {
+    const std::string n = "[" + std::to_string(k2) + "]";
+    out.emplace_back("xgmi_read_data_acc" + n, na64(a.xgmi_read_data_acc[k2]), na64(s.xgmi_read_data_acc[k2]));
+    out.emplace_back("xgmi_write_data_acc" + n, na64(a.xgmi_write_data_acc[k2]), na64(s.xgmi_write_data_acc[k2]));
+    out.emplace_back("xgmi_link_status" + n, na16(a.xgmi_link_status[k2]), na16(s.xgmi_link_status[k2]));
+  }
+  for (int k2 = 0; k2 < AMDSMI_MAX_NUM_GFX_CLKS; ++k2)
+    out.emplace_back("current_gfxclks[" + std::to_string(k2) + "]", na16(a.current_gfxclks[k2]),
+                     na16(s.current_gfxclks[k2]));
+  for (int k2 = 0; k2 < AMDSMI_MAX_NUM_CLKS; ++k2) {
+    const std::string n = "[" + std::to_string(k2) + "]";
+    out.emplace_back("current_socclks" + n, na16(a.current_socclks[k2]), na16(s.current_socclks[k2]));
+    out.emplace_back("current_vclk0s" + n, na16(a.current_vclk0s[k2]), na16(s.current_vclk0s[k2]));
+    out.emplace_back("current_dclk0s" + n, na16(a.current_dclk0s[k2]), na16(s.current_dclk0s[k2]));
+  }
+  for (int x = 0; x < AMDSMI_MAX_NUM_XCP; ++x)
+    for (int c = 0; c < AMDSMI_MAX_NUM_XCC; ++c) {
+      const std::string n = "xcp_stats[" + std::to_string(x) + "].";
+      const std::string ix = "[" + std::to_string(c) + "]";
+      out.emplace_back(n + "gfx_busy_inst" + ix, na32(a.xcp_stats[x].gfx_busy_inst[c]),
+                       na32(s.xcp_stats[x].gfx_busy_inst[c]));
+      out.emplace_back(n + "gfx_busy_acc" + ix, na64(a.xcp_stats[x].gfx_busy_acc[c]),
+                       na64(s.xcp_stats[x].gfx_busy_acc[c]));
+      out.emplace_back(n + "gfx_low_utilization_acc" + ix, na64(a.xcp_stats[x].gfx_low_utilization_acc[c]),
+                       na64(s.xcp_stats[x].gfx_low_utilization_acc[c]));
+    }
+#undef CMP16
+#undef CMP32
+#undef CMP64
+  return out;
+}
+
+// Stable fields that must agree between libamd_smi and the sysfs decode before the fast path is
+// trusted for a device (a mismatch means the kernel layout is not the one sysfs_fast.h knows).
+bool AmdSmiBackend::validate_fast(int i, std::string* why) {
+  std::string err;
+  auto rows = compare_tables(i, &err);
+  if (rows.empty()) {
+    *why = "validation read failed: " + err;
+    return false;
+  }
+  static const char* exact[] = {"format_revision", "content_revision", "pcie_link_width",
+                                "xgmi_link_width", "xgmi_link_speed", "num_partition", "vram_max_bandwidth",
+                                "xgmi_link_status[1]", "xgmi_link_status[7]"};
+  static const char* close[] = {"temperature_hotspot", "temperature_mem", "current_uclk"};
+  for (const auto& [name, a, s] : rows) {
+    const bool a_na = a != a, s_na = s != s;
+    for (const char* e : exact)
+      if (name == e && (a_na != s_na || (!a_na && a != s))) {
+        *why = "sysfs table disagrees with amdsmi on " + name + " (" + fmtd(a) + " vs " +
+               fmtd(s) + ")";
+        return false;
+      }
+    for (const char* c : close)
+      if (name == c && (a_na != s_na || (!a_na && std::fabs(a - s) > std::max(5.0, 0.1 * std::fabs(a))))) {
+        *why = "sysfs table disagrees with amdsmi on " + name + " (" + fmtd(a) + " vs " +
+               fmtd(s) + ")";
+        return false;
+      }
+    if (name == "firmware_timestamp" && !a_na && !s_na && (s < a || s - a > 1e10)) {
+      *why = "sysfs firmware_timestamp not after amdsmi's";
+      return false;
+    }
+  }
   return true;
 }
 
@@ -307,6 +474,36 @@ void AmdSmiBackend::sample(int i, DeviceSample* out) {
   Caps& c = caps_[i];
   auto& v = out->v;
   bool any = false;
+
+  // Fast path: the kernel files directly (52 us + 6 us instead of ~1.1 ms through libamd_smi).
+  if (SysfsGpu* g = i < static_cast<int>(fast_.size()) ? fast_[i].get() : nullptr) {
+    kgm::V18 k;
+    std::string why;
+    int64_t ts = mono_ns();
+    bool ok = g->read_metrics(&k, &why);
+    record_call(kCallMetrics, mono_ns() - ts, ok);
+    if (ok) {
+      amdsmi_gpu_metrics_t m;
+      kgm::to_smi(k, &m);
+      fill_from_gpu_metrics(m, devs_[i].partition_id, AMDSMI_MAX_NUM_XCP, devs_[i].power_limit_w,
+                            energy_res_uj_, out);
+      ts = mono_ns();
+      double used = kNaN, total = devs_[i].vram_total_bytes;
+      bool vok = g->read_vram(&used, &total);
+      record_call(kCallVram, mono_ns() - ts, vok);
+      if (vok) {
+        v[F_VRAM_USED] = used;
+        v[F_VRAM_TOTAL] = total;
+      }
+      double gtt = kNaN;
+      if (g->read_gtt(&gtt)) v[F_GTT_USED] = gtt;
+      out->ok = true;
+      out->sample_ns = mono_ns() - t0;
+      return;
+    }
+    out->errors++;
+    out->last_error = why;  // fall through to libamd_smi for this tick
+  }
 
   if (c.metrics && t_->amdsmi_get_gpu_metrics_info) {
     amdsmi_gpu_metrics_t m;
@@ -368,6 +565,12 @@ void AmdSmiBackend::sample(int i, DeviceSample* out) {
 
 bool AmdSmiBackend::processes(int i, std::vector<ProcSample>* out) {
   out->clear();
+  if (SysfsGpu* g = i < static_cast<int>(fast_.size()) ? fast_[i].get() : nullptr; g && g->have_kfd()) {
+    const int64_t ts = mono_ns();
+    const bool ok = g->processes(out);
+    record_call(kCallProcs, mono_ns() - ts, ok);
+    if (ok) return true;
+  }
   if (!caps_[i].procs || !t_->amdsmi_get_gpu_process_list) return false;
   auto& buf = proc_buf_[i];
   for (int attempt = 0; attempt < 3; ++attempt) {

@@ -12,6 +12,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "sample.h"
@@ -139,6 +140,7 @@ class MockBackend : public Backend {
 // amdsmi backend (dlopen'd libamd_smi)
 // ---------------------------------------------------------------------------------------------
 struct SmiTable;  // smi_table.h
+class SysfsGpu;   // sysfs_fast.h
 
 class AmdSmiBackend : public Backend {
  public:
@@ -157,9 +159,25 @@ class AmdSmiBackend : public Backend {
   // Expose every physical device `r` times (distinct gpu_id labels). Only for measuring how the
   // sampler scales with the GPU count on a box with fewer GPUs than a full 8x MI355X node.
   void set_replicate(int r) { replicate_ = r < 1 ? 1 : r; }
+  // Direct sysfs/KFD reads for the per-tick values (sysfs_fast.h); libamd_smi stays the source of
+  // enumeration, statics, links and the fallback. Applied at init().
+  void set_fast_path(bool on, std::string sys_root = "/sys", std::string proc_root = "/proc") {
+    fast_path_ = on;
+    sys_root_ = std::move(sys_root);
+    proc_root_ = std::move(proc_root);
+  }
+  int fast_path_devices() const;
+  const std::string& fast_path_status() const { return fast_status_; }
+  // Field-by-field libamd_smi vs sysfs-decoded firmware table of device i: (field, amdsmi, sysfs).
+  std::vector<std::tuple<std::string, double, double>> compare_tables(int i, std::string* err);
 
  private:
+  bool validate_fast(int i, std::string* why);
   int replicate_ = 1;
+  bool fast_path_ = true;
+  std::string sys_root_ = "/sys", proc_root_ = "/proc", fast_status_;
+  std::vector<std::unique_ptr<SysfsGpu>> fast_;
+  std::vector<uint64_t> kfd_ids_;
   std::string lib_path_;
   std::unique_ptr<SmiTable> t_;
   bool inited_ = false;

@@ -115,6 +115,7 @@ std::unique_ptr<Backend> make_backend_from_config(const ExporterConfig& cfg, std
     // "amdsmi:replicate=8": sample every real device 8 times (scaling rehearsal on small boxes)
     size_t p = cfg.backend.find("replicate=");
     if (p != std::string::npos) a->set_replicate(atoi(cfg.backend.c_str() + p + 10));
+    a->set_fast_path(cfg.fast_path, cfg.sysfs_root, cfg.attribution.procfs_root);
     b = std::move(a);
   } else if (cfg.backend == "rocm_smi") {
     b = std::make_unique<RocmSmiBackend>(cfg.rocm_smi_lib);
@@ -726,7 +727,11 @@ SelfStats Exporter::self_stats() const {
   SelfStats s;
   s.version = cfg_.version;
   s.backend = backend_ ? backend_->name() : cfg_.backend;
-  if (auto* a = dynamic_cast<AmdSmiBackend*>(backend_.get())) s.backend_version = a->lib_version();
+  if (auto* a = dynamic_cast<AmdSmiBackend*>(backend_.get())) {
+    s.backend_version = a->lib_version();
+    s.fast_path_devices = a->fast_path_devices();
+    s.fast_path_status = a->fast_path_status();
+  }
   if (auto* r = dynamic_cast<RocmSmiBackend*>(backend_.get())) s.backend_version = r->lib_version();
   s.backend_up = backend_up_;
   s.backend_reinits = reinits_;

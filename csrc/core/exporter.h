@@ -32,7 +32,9 @@ namespace gpumon {
 struct ExporterConfig {
   std::string backend = "auto";       // auto | amdsmi | mock
   std::string amdsmi_lib;
-  std::string rocm_smi_lib;  // librocm_smi64 path override (rocm_smi backend / auto fallback)
+  std::string rocm_smi_lib;
+  bool fast_path = true;              // amdsmi: per-tick reads straight from sysfs/KFD (sysfs_fast.h)
+  std::string sysfs_root = "/sys";  // librocm_smi64 path override (rocm_smi backend / auto fallback)
   MockConfig mock;
   std::vector<int> devices;           // hip_id filter; empty = all
   double interval_s = 1.0;            // <= 0: no sampler thread (ticks driven by tick())

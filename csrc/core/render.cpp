@@ -543,6 +543,11 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       Family f(o, "gpumon_backend_up", "1 if the device backend is initialised.", "gauge");
       f.add(hl, s.backend_up ? 1.0 : 0.0);
     }
+    if (s.fast_path_devices >= 0) {
+      Family f(o, "gpumon_fast_path_devices",
+               "GPUs whose per-tick values are read straight from sysfs/KFD instead of libamd_smi.", "gauge");
+      f.add(hl, static_cast<double>(s.fast_path_devices));
+    }
     {
       Family f(o, "gpumon_backend_reinits_total",
                "Backend re-initialisations after every GPU failed for several ticks.", "counter");

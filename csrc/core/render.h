@@ -49,6 +49,8 @@ struct SelfStats {
   std::string backend;
   std::string backend_version;
   bool backend_up = false;
+  int fast_path_devices = -1;        // amdsmi sysfs fast path (-1: not applicable)
+  std::string fast_path_status;
   uint64_t backend_reinits = 0;
   uint64_t ticks = 0;
   uint64_t samples = 0;

@@ -1,0 +1,210 @@
+// Direct sysfs/KFD fast path for the per-tick device reads.
+//
+// Measured on MI355X (tools/probe_sysfs.py, profiles/r1_sysfs_fast_path.md): going through
+// libamd_smi costs ~0.86 ms for amdsmi_get_gpu_metrics_info, ~0.23 ms for the VRAM query and
+// ~0.54 ms for the process list per device, while the underlying reads cost 52 us (pread of the
+// 3872-byte firmware table at /sys/bus/pci/devices/<bdf>/gpu_metrics), 6 us (mem_info_vram_used)
+// and ~20 us per process (/sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>). The sampler therefore
+// keeps libamd_smi for enumeration, statics, links and as the fallback, and reads the hot values
+// straight from the kernel through file descriptors held open across ticks.
+//
+// The firmware table is the kernel's `struct gpu_metrics_v1_8` (amdgpu, MI350/MI355X): header
+// {structure_size=3872, format 1, content 8}. It is decoded into the amdsmi/rsmi gpu_metrics
+// structs (same field names) so the exposition path (metrics_table.h) is shared. The fast path is
+// only enabled for a device after its decoded table agrees with libamd_smi's on the stable
+// fields (AmdSmiBackend::init), so a layout change in a future firmware/driver disables it
+// instead of exporting garbage.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "sample.h"
+
+namespace gpumon {
+namespace kgm {
+
+constexpr int kLinks = 8, kGfxClks = 8, kClks = 4, kXcp = 8, kXcc = 8, kJpeg = 40, kVcn = 4;
+
+struct Header {
+  uint16_t structure_size;
+  uint8_t format_revision;
+  uint8_t content_revision;
+};
+
+struct XcpV12 {  // amdgpu_xcp_metrics_v1_2
+  uint32_t gfx_busy_inst[kXcc];
+  uint16_t jpeg_busy[kJpeg];
+  uint16_t vcn_busy[kVcn];
+  uint64_t gfx_busy_acc[kXcc];
+  uint64_t gfx_below_host_limit_ppt_acc[kXcc];
+  uint64_t gfx_below_host_limit_thm_acc[kXcc];
+  uint64_t gfx_low_utilization_acc[kXcc];
+  uint64_t gfx_below_host_limit_total_acc[kXcc];
+};
+
+struct V18 {  // gpu_metrics_v1_8 (natural alignment, as the kernel declares it)
+  Header common_header;
+  uint16_t temperature_hotspot;
+  uint16_t temperature_mem;
+  uint16_t temperature_vrsoc;
+  uint16_t curr_socket_power;
+  uint16_t average_gfx_activity;
+  uint16_t average_umc_activity;
+  uint64_t mem_max_bandwidth;
+  uint64_t energy_accumulator;
+  uint64_t system_clock_counter;
+  uint32_t accumulation_counter;
+  uint32_t prochot_residency_acc;
+  uint32_t ppt_residency_acc;
+  uint32_t socket_thm_residency_acc;
+  uint32_t vr_thm_residency_acc;
+  uint32_t hbm_thm_residency_acc;
+  uint32_t gfxclk_lock_status;
+  uint16_t pcie_link_width;
+  uint16_t pcie_link_speed;
+  uint16_t xgmi_link_width;
+  uint16_t xgmi_link_speed;
+  uint32_t gfx_activity_acc;
+  uint32_t mem_activity_acc;
+  uint64_t pcie_bandwidth_acc;
+  uint64_t pcie_bandwidth_inst;
+  uint64_t pcie_l0_to_recov_count_acc;
+  uint64_t pcie_replay_count_acc;
+  uint64_t pcie_replay_rover_count_acc;
+  uint32_t pcie_nak_sent_count_acc;
+  uint32_t pcie_nak_rcvd_count_acc;
+  uint64_t xgmi_read_data_acc[kLinks];
+  uint64_t xgmi_write_data_acc[kLinks];
+  uint16_t xgmi_link_status[kLinks];
+  uint16_t padding;
+  uint64_t firmware_timestamp;
+  uint16_t current_gfxclk[kGfxClks];
+  uint16_t current_socclk[kClks];
+  uint16_t current_vclk0[kClks];
+  uint16_t current_dclk0[kClks];
+  uint16_t current_uclk;
+  uint16_t num_partition;
+  XcpV12 xcp_stats[kXcp];
+  uint32_t pcie_lc_perf_other_end_recovery;
+};
+
+static_assert(sizeof(XcpV12) == 440, "xcp_metrics_v1_2 layout");
+static_assert(offsetof(V18, xgmi_read_data_acc) == 136, "gpu_metrics_v1_8 layout");
+static_assert(offsetof(V18, firmware_timestamp) == 288, "gpu_metrics_v1_8 layout");
+static_assert(offsetof(V18, xcp_stats) == 344, "gpu_metrics_v1_8 layout");
+static_assert(sizeof(V18) == 3872, "gpu_metrics_v1_8 is 3872 bytes on MI355X");
+
+inline uint64_t w32(uint32_t x) { return x == 0xFFFFFFFFu ? ~0ull : x; }
+
+// Kernel v1.8 table -> amdsmi_gpu_metrics_t / rsmi_gpu_metrics_t (identical field names).
+// Fields the v1.8 table does not carry stay all-ones (= N/A, the firmware convention).
+template <typename M>
+void to_smi(const V18& k, M* m) {
+  memset(m, 0xFF, sizeof *m);
+  m->common_header.structure_size = k.common_header.structure_size;
+  m->common_header.format_revision = k.common_header.format_revision;
+  m->common_header.content_revision = k.common_header.content_revision;
+  m->temperature_hotspot = k.temperature_hotspot;
+  m->temperature_mem = k.temperature_mem;
+  m->temperature_vrsoc = k.temperature_vrsoc;
+  m->current_socket_power = k.curr_socket_power;
+  m->average_gfx_activity = k.average_gfx_activity;
+  m->average_umc_activity = k.average_umc_activity;
+  m->vram_max_bandwidth = k.mem_max_bandwidth;
+  m->energy_accumulator = k.energy_accumulator;
+  m->system_clock_counter = k.system_clock_counter;
+  m->accumulation_counter = w32(k.accumulation_counter);
+  m->prochot_residency_acc = w32(k.prochot_residency_acc);
+  m->ppt_residency_acc = w32(k.ppt_residency_acc);
+  m->socket_thm_residency_acc = w32(k.socket_thm_residency_acc);
+  m->vr_thm_residency_acc = w32(k.vr_thm_residency_acc);
+  m->hbm_thm_residency_acc = w32(k.hbm_thm_residency_acc);
+  m->gfxclk_lock_status = k.gfxclk_lock_status;
+  m->pcie_link_width = k.pcie_link_width;
+  m->pcie_link_speed = k.pcie_link_speed;
+  m->xgmi_link_width = k.xgmi_link_width;
+  m->xgmi_link_speed = k.xgmi_link_speed;
+  m->gfx_activity_acc = k.gfx_activity_acc;
+  m->mem_activity_acc = k.mem_activity_acc;
+  m->pcie_bandwidth_acc = k.pcie_bandwidth_acc;
+  m->pcie_bandwidth_inst = k.pcie_bandwidth_inst;
+  m->pcie_l0_to_recov_count_acc = k.pcie_l0_to_recov_count_acc;
+  m->pcie_replay_count_acc = k.pcie_replay_count_acc;
+  m->pcie_replay_rover_count_acc = k.pcie_replay_rover_count_acc;
+  m->pcie_nak_sent_count_acc = k.pcie_nak_sent_count_acc;
+  m->pcie_nak_rcvd_count_acc = k.pcie_nak_rcvd_count_acc;
+  for (int i = 0; i < kLinks; ++i) {
+    m->xgmi_read_data_acc[i] = k.xgmi_read_data_acc[i];
+    m->xgmi_write_data_acc[i] = k.xgmi_write_data_acc[i];
+    m->xgmi_link_status[i] = k.xgmi_link_status[i];
+  }
+  m->firmware_timestamp = k.firmware_timestamp;
+  for (int i = 0; i < kGfxClks; ++i) m->current_gfxclks[i] = k.current_gfxclk[i];
+  for (int i = 0; i < kClks; ++i) {
+    m->current_socclks[i] = k.current_socclk[i];
+    m->current_vclk0s[i] = k.current_vclk0[i];
+    m->current_dclk0s[i] = k.current_dclk0[i];
+  }
+  m->current_gfxclk = k.current_gfxclk[0];
+  m->current_socclk = k.current_socclk[0];
+  m->current_vclk0 = k.current_vclk0[0];
+  m->current_dclk0 = k.current_dclk0[0];
+  m->current_uclk = k.current_uclk;
+  m->num_partition = k.num_partition;
+  for (int x = 0; x < kXcp; ++x) {
+    const XcpV12& s = k.xcp_stats[x];
+    auto& d = m->xcp_stats[x];
+    for (int i = 0; i < kXcc; ++i) {
+      d.gfx_busy_inst[i] = s.gfx_busy_inst[i];
+      d.gfx_busy_acc[i] = s.gfx_busy_acc[i];
+      d.gfx_below_host_limit_ppt_acc[i] = s.gfx_below_host_limit_ppt_acc[i];
+      d.gfx_below_host_limit_thm_acc[i] = s.gfx_below_host_limit_thm_acc[i];
+      d.gfx_low_utilization_acc[i] = s.gfx_low_utilization_acc[i];
+      d.gfx_below_host_limit_total_acc[i] = s.gfx_below_host_limit_total_acc[i];
+    }
+    for (int i = 0; i < kJpeg; ++i) d.jpeg_busy[i] = s.jpeg_busy[i];
+    for (int i = 0; i < kVcn; ++i) d.vcn_busy[i] = s.vcn_busy[i];
+  }
+  m->pcie_lc_perf_other_end_recovery = k.pcie_lc_perf_other_end_recovery;
+}
+
+}  // namespace kgm
+
+// One device's kernel files, opened once and re-read with pread(…, 0) every tick.
+class SysfsGpu {
+ public:
+  SysfsGpu() = default;
+  ~SysfsGpu();
+  SysfsGpu(const SysfsGpu&) = delete;
+  SysfsGpu& operator=(const SysfsGpu&) = delete;
+
+  // sys_root: "/sys" (tests point it at a fake tree); proc_root: "/proc".
+  bool open(const std::string& sys_root, const std::string& proc_root, const std::string& bdf,
+            uint64_t kfd_gpu_id, int drm_render, std::string* why);
+  // Raw firmware table; false if the read failed or it is not a v1.8 table.
+  bool read_metrics(kgm::V18* out, std::string* why);
+  bool read_vram(double* used_bytes, double* total_bytes);
+  bool read_gtt(double* used_bytes);
+  // Compute processes with memory on this GPU (KFD), plus DRM fdinfo gfx engine time / memory.
+  bool processes(std::vector<ProcSample>* out);
+  bool have_kfd() const { return kfd_gpu_id_ != 0; }
+
+ private:
+  struct FdCache {
+    int64_t scanned_ns = 0;
+    std::vector<int> fds;  // this GPU's DRM render-node fds of the process
+  };
+  void fdinfo_usage(uint32_t pid, ProcSample* p);
+  std::string sys_root_, proc_root_, dev_dir_;
+  uint64_t kfd_gpu_id_ = 0;
+  std::string render_path_;  // "/dev/dri/renderD<minor>"
+  int fd_metrics_ = -1, fd_vram_used_ = -1, fd_vram_total_ = -1, fd_gtt_used_ = -1;
+  std::unordered_map<uint32_t, FdCache> fd_cache_;
+};
+
+}  // namespace gpumon

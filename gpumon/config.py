@@ -32,6 +32,8 @@ class Config:
     backend: str = "auto"                 # auto | amdsmi | rocm_smi | mock[:k=v,...]
     amdsmi_lib: str = ""
     rocm_smi_lib: str = ""                # librocm_smi64 override (rocm_smi backend / auto fallback)
+    fast_path: bool = True                # amdsmi: hot per-tick reads straight from sysfs/KFD
+    sysfs_root: str = "/sys"
     devices: List[int] = field(default_factory=list)
     interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
     processes: bool = True
@@ -93,6 +95,8 @@ class Config:
             "backend": self.backend,
             "amdsmi_lib": self.amdsmi_lib,
             "rocm_smi_lib": self.rocm_smi_lib,
+            "fast_path": self.fast_path,
+            "sysfs_root": self.sysfs_root,
             "devices": list(self.devices),
             "interval_s": float(self.interval),
             "processes": self.processes,
@@ -206,6 +210,9 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--sample-threads", dest="sample_threads", type=int)
     p.add_argument("--enable-probe-kernel", dest="enable_probe", action="store_true", default=None)
     p.add_argument("--enable-pmc", dest="enable_pmc", action="store_true", default=None)
+    p.add_argument("--no-fast-path", dest="fast_path", action="store_false", default=None,
+                   help="amdsmi: read every value through libamd_smi (disable the sysfs/KFD fast path)")
+    p.add_argument("--sysfs-root", dest="sysfs_root")
     p.add_argument("--roctx", dest="roctx", action="store_true", default=None,
                    help="bracket sampler phases with ROCTx ranges (view with rocprofv3 --marker-trace)")
     p.add_argument("--compat", action="store_true",

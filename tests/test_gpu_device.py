@@ -228,3 +228,23 @@ def test_smoke_entry():
     import __graft_entry__ as g
 
     g.smoke()
+
+
+def test_sysfs_fast_path_matches_amdsmi(core, torch_gpu):
+    """The kernel gpu_metrics v1.8 decode (sysfs_fast.h) agrees with libamd_smi on every
+    non-counter field of the MI355X table, and the exporter uses it."""
+    r = core.amdsmi_compare_tables("", "/sys", 0)
+    assert r["error"] == "", r
+    assert r["fast_path_devices"] >= 1, r["fast_path_status"]
+    counters = ("accumulator", "clock_counter", "timestamp", "_acc", "temperature", "power", "clk",
+                "activity", "busy_inst", "bandwidth_inst")
+    bad = [(n, a, s) for n, a, s in r["rows"]
+           if not ((a != a and s != s) or a == s) and not any(c in n for c in counters)]
+    assert not bad, bad
+    ex = _exporter(core)
+    try:
+        assert ex.self_stats()["fast_path_devices"] == 1
+        ex.tick()
+        assert ex.samples()[0]["ok"]
+    finally:
+        ex.stop()

@@ -1,0 +1,167 @@
+"""The amdsmi backend's sysfs/KFD fast path (csrc/core/sysfs_fast.*) on CPU.
+
+A fake sysfs tree holds a gpu_metrics v1.8 blob packed here with `struct` from the kernel layout
+(an encoding independent of the C++ struct), mem_info_* files and KFD proc entries; the fake
+libamd_smi supplies enumeration. Checks: the fast path engages only when the decoded table agrees
+with libamd_smi on the stable fields, the exported values then come from sysfs, KFD process rows
+carry fdinfo gfx time, and a layout/header mismatch falls back to libamd_smi.
+"""
+
+import os
+import struct
+import subprocess
+
+import pytest
+
+from gpumon.export import promtext
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAKE = os.path.join(ROOT, "build", "fakes", "libfake_amd_smi.so")
+NA16, NA32, NA64 = 0xFFFF, 0xFFFFFFFF, 0xFFFFFFFFFFFFFFFF
+
+
+def pack_v18(d=0, gfx=77, xgmi_width=16, revision=8, fw_ts=5_000_000_000, n=1):
+    """gpu_metrics_v1_8, little endian, natural alignment spelled out as explicit pad bytes."""
+    b = struct.pack("<HBB", 3872, 1, revision)
+    b += struct.pack("<6H", 46 + d, 33, 43, 600, gfx, 12)
+    b += struct.pack("<3Q", 8192, 1_000_000 + n * 1_000_000, n * 1_000_000_000)
+    b += struct.pack("<7I", n * 1000, 0, n * 100, 0, 0, 0, 0)
+    b += struct.pack("<4H", 16, 320, xgmi_width, 38)
+    b += struct.pack("<2I", n * gfx * 1000, n * 12 * 1000)
+    b += b"\0" * 4
+    b += struct.pack("<5Q", NA64, 18, 0, 0, 0)
+    b += struct.pack("<2I", 0, 0)
+    b += struct.pack("<8Q", *([0] + [n * 1_000_000 * k for k in range(1, 8)]))
+    b += struct.pack("<8Q", *([0] + [n * 500_000 * k for k in range(1, 8)]))
+    b += struct.pack("<8H", NA16, 1, 1, 1, 1, 1, 1, 1) + struct.pack("<H", 0)
+    b += b"\0" * 6
+    b += struct.pack("<Q", fw_ts)
+    b += struct.pack("<8H", *[2100 - k for k in range(8)])
+    b += struct.pack("<4H", 1200, NA16, NA16, NA16) + struct.pack("<4H", 29, NA16, NA16, NA16)
+    b += struct.pack("<4H", 22, NA16, NA16, NA16) + struct.pack("<2H", 2000, 1)
+    b += b"\0" * 4
+    for x in range(8):
+        busy = [gfx] * 8 if x == 0 else [NA32] * 8
+        acc = [n * gfx * 1000] * 8 if x == 0 else [NA64] * 8
+        b += struct.pack("<8I", *busy) + struct.pack("<40H", *([NA16] * 40)) + struct.pack("<4H", *([NA16] * 4))
+        b += struct.pack("<8Q", *acc) + struct.pack("<32Q", *([NA64] * 32))
+    b += struct.pack("<I", 0) + b"\0" * 4
+    assert len(b) == 3872
+    return b
+
+
+def make_tree(tmp, gpus=2, blob_kw=None, procs=((4242, 0),)):
+    sysr, procr = tmp / "sys", tmp / "proc"
+    for d in range(gpus):
+        dev = sysr / "bus" / "pci" / "devices" / f"0000:{0x26 + 0x20 * d:02x}:00.0"
+        dev.mkdir(parents=True)
+        (dev / "gpu_metrics").write_bytes(pack_v18(d=d, **(blob_kw or {})))
+        (dev / "mem_info_vram_used").write_text(f"{(123 + d) << 20}\n")
+        (dev / "mem_info_vram_total").write_text(f"{288 << 30}\n")
+        (dev / "mem_info_gtt_used").write_text(f"{7 << 20}\n")
+    for pid, d in procs:
+        kp = sysr / "class" / "kfd" / "kfd" / "proc" / str(pid)
+        (kp / f"stats_{36622 + d}").mkdir(parents=True)
+        (kp / f"vram_{36622 + d}").write_text(f"{2 << 30}\n")
+        (kp / f"stats_{36622 + d}" / "cu_occupancy").write_text("17\n")
+        fd, fdinfo = procr / str(pid) / "fd", procr / str(pid) / "fdinfo"
+        fd.mkdir(parents=True)
+        fdinfo.mkdir()
+        os.symlink(f"/dev/dri/renderD{152 + d}", fd / "5")
+        os.symlink(f"/dev/dri/renderD{152 + d}", fd / "6")  # dup() of the same DRM file
+        os.symlink("/dev/null", fd / "7")
+        for n in ("5", "6"):
+            (fdinfo / n).write_text("pos:\t0\nflags:\t02100002\ndrm-driver:\tamdgpu\ndrm-client-id:\t7\n"
+                                    "drm-engine-gfx:\t5000000 ns\ndrm-memory-vram:\t1048576 KiB\n"
+                                    "drm-memory-gtt:\t2048 KiB\n")
+    return sysr, procr
+
+
+@pytest.fixture(scope="module", autouse=True)
+def fake_lib():
+    subprocess.run(["make", "-C", ROOT, "fakes"], check=True, stdout=subprocess.DEVNULL)
+
+
+@pytest.fixture
+def exporter(core, monkeypatch):
+    made = []
+
+    def make(sysr, procr, **over):
+        for k in ("FAKE_AMDSMI_GPUS", "FAKE_AMDSMI_CPX", "FAKE_AMDSMI_NO_METRICS"):
+            monkeypatch.delenv(k, raising=False)
+        cfg = {"backend": "amdsmi", "amdsmi_lib": FAKE, "serve_http": False, "interval_s": 0, "host": "n1",
+               "verify_kfd": False, "init_retry_s": 0.0, "sysfs_root": str(sysr), "procfs_root": str(procr)}
+        cfg.update(over)
+        ex = core.Exporter(cfg)
+        assert ex.start() == ""
+        made.append(ex)
+        return ex
+
+    yield make
+    for ex in made:
+        ex.stop()
+
+
+def test_fast_path_engages_and_values_come_from_sysfs(exporter, tmp_path):
+    sysr, procr = make_tree(tmp_path)
+    ex = exporter(sysr, procr)
+    st = ex.self_stats()
+    assert st["fast_path_devices"] == 2 and st["fast_path_status"] == "sysfs"
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpumon_fast_path_devices") == 2
+    assert promtext.one(fam, "node_gpu_gpu_util", gpu_id="0") == 77  # the blob's value, not amdsmi's 37
+    assert promtext.one(fam, "node_gpu_mem_used", gpu_id="1") == 124
+    assert promtext.one(fam, "gpu_temperature_celsius", gpu_id="1", sensor="hotspot") == 47
+    assert promtext.one(fam, "gpu_gtt_used_bytes", gpu_id="0") == 7 << 20
+    assert promtext.values(fam, "gpu_xcd_busy_percent", gpu_id="0") == [77] * 8
+    assert promtext.one(fam, "gpu_clock_mhz", gpu_id="0", clock="soc") == 1200
+
+
+def test_kfd_processes_with_fdinfo(exporter, tmp_path):
+    sysr, procr = make_tree(tmp_path)
+    ex = exporter(sysr, procr)
+    ex.tick()
+    rows = [r for r in ex.pod_rows() if not r["idle"]]
+    assert [(r["dev"], r["pid"]) for r in rows] == [(0, "4242")]
+    r = rows[0]
+    assert r["used_memory_bytes"] == 1 << 30  # fdinfo drm-memory-vram (dup'ed fd counted once)
+    assert r["cu_occupancy"] == 17
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_process_count", gpu_id="0") == 1
+    assert promtext.one(fam, "gpu_process_count", gpu_id="1") == 0
+
+
+def test_layout_mismatch_falls_back_to_amdsmi(exporter, tmp_path):
+    sysr, procr = make_tree(tmp_path, blob_kw={"xgmi_width": 8})
+    ex = exporter(sysr, procr)
+    st = ex.self_stats()
+    assert st["fast_path_devices"] == 0
+    assert "xgmi_link_width" in st["fast_path_status"]
+    ex.tick()
+    assert promtext.one(promtext.parse(ex.metrics_text()), "node_gpu_gpu_util", gpu_id="0") == 37
+
+
+def test_unknown_table_revision_rejected(exporter, tmp_path):
+    sysr, procr = make_tree(tmp_path, blob_kw={"revision": 9})
+    ex = exporter(sysr, procr)
+    assert ex.self_stats()["fast_path_devices"] == 0
+
+
+def test_fast_path_can_be_disabled(exporter, tmp_path):
+    sysr, procr = make_tree(tmp_path)
+    ex = exporter(sysr, procr, fast_path=False)
+    assert ex.self_stats()["fast_path_devices"] == 0
+    ex.tick()
+    assert promtext.one(promtext.parse(ex.metrics_text()), "node_gpu_gpu_util", gpu_id="0") == 37
+
+
+def test_compare_tables_binding(core, tmp_path, monkeypatch):
+    monkeypatch.delenv("FAKE_AMDSMI_GPUS", raising=False)
+    sysr, _ = make_tree(tmp_path)
+    r = core.amdsmi_compare_tables(FAKE, str(sysr), 1)
+    assert r["error"] == ""
+    rows = {name: (a, s) for name, a, s in r["rows"]}
+    assert rows["temperature_hotspot"] == (47, 47)
+    assert rows["average_gfx_activity"] == (37, 77)
+    assert rows["xgmi_link_status[3]"] == (1, 1)
