@@ -243,6 +243,9 @@ bool RocmSmiBackend::processes(int i, std::vector<ProcSample>* out) {
   for (uint32_t k = 0; k < n && k < all.size(); ++k) {
     rsmi_process_info_t pi{};
     if (t_->rsmi_compute_process_info_by_device_get(all[k].process_id, idx_[i], &pi) != RSMI_STATUS_SUCCESS) continue;
+    // rocm_smi_lib answers SUCCESS for node-wide KFD processes that hold nothing on this GPU
+    // (seen on MI355X: 8 rows where libamd_smi lists 2); keep only those with memory here.
+    if (pi.vram_usage == 0) continue;
     ProcSample p;
     p.pid = pi.process_id;
     p.vram_bytes = static_cast<double>(pi.vram_usage);

@@ -1,7 +1,7 @@
 #!/bin/bash
 # rocm_smi fallback on hardware + full GPU test tier + 1-GPU bench.
 set -o pipefail
-out=gpurun_out/r4
+out=gpurun_out/${ROUND_TAG:-r4}
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 600 python -m pytest tests -m gpu -x -q -s > $out/pytest_gpu.txt 2>&1; rc=$?
