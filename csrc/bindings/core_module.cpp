@@ -59,6 +59,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "sample_threads", &c.sample_threads);
   get(d, "influx_url", &c.influx_url);
   get(d, "influx_extended", &c.influx_extended);
+  get(d, "influx_schema", &c.influx_schema);
   get(d, "influx_every", &c.influx_every);
   get(d, "influx_timeout_s", &c.influx_timeout_s);
   get(d, "init_retry_s", &c.init_retry_s);

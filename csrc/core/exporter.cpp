@@ -519,7 +519,7 @@ TickInfo Exporter::tick() {
   std::string influx;
   if (!cfg_.influx_url.empty() && cfg_.influx_every > 0 &&
       ticks_.load() % static_cast<uint64_t>(cfg_.influx_every) == 0) {
-    render_influx(in, snap->wall_ns, cfg_.influx_extended, &influx);
+    render_influx(in, snap->wall_ns, cfg_.influx_extended, &influx, cfg_.influx_schema);
   }
   {
     std::lock_guard<std::mutex> g(state_mu_);
@@ -688,7 +688,7 @@ std::string Exporter::render_influx_now() {
   in.samples = &sm;
   in.pod_rows = &rows;
   std::string out;
-  render_influx(in, wall_ns(), cfg_.influx_extended, &out);
+  render_influx(in, wall_ns(), cfg_.influx_extended, &out, cfg_.influx_schema);
   return out;
 }
 

@@ -55,6 +55,7 @@ struct ExporterConfig {
   RateConfig rates;
   std::string influx_url;             // INFLUXDB_URL; empty = push disabled
   bool influx_extended = false;
+  int influx_schema = 2019;           // 2019 (gpu.py layout) | 2018 (img/influxdb.png pod_gpu)
   int influx_every = 1;               // ticks per push
   double influx_timeout_s = 2.0;
   double init_retry_s = 5.0;

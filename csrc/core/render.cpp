@@ -655,7 +655,7 @@ void render_prometheus(const RenderInput& in, std::string* o) {
 // ---------------------------------------------------------------------------------------------
 // Influx line protocol (reference-compatible)
 // ---------------------------------------------------------------------------------------------
-void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::string* o) {
+void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::string* o, int schema) {
   const auto& st = *in.statics;
   const auto& sm = *in.samples;
   const size_t n = std::min(st.size(), sm.size());
@@ -724,6 +724,39 @@ void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::str
     }
   }
   if (!in.pod_rows) return;
+  if (schema == 2018) {
+    // The earlier pod_gpu layout still shown in the reference's img/influxdb.png (2018-08-06):
+    // columns containerid, gid, gpu, host, namespace, node, pid, pod, procressname, used_gpu (MiB).
+    // Idle allocation rows did not exist yet in that version, so they are not emitted here.
+    for (const auto& p : *in.pod_rows) {
+      if (p.idle) continue;
+      const std::string gid = p.dev < static_cast<int>(n) ? st[p.dev].gpu_id : "-";
+      o->append("pod_gpu,host=");
+      escape_influx_tag(in.host, o);
+      o->append(",namespace=");
+      escape_influx_tag(p.pod_namespace, o);
+      o->append(",gpu=");
+      escape_influx_tag(gid, o);
+      o->append(",containerid=");
+      escape_influx_tag(p.containerid, o);
+      o->append(" gid=");
+      o->append(gid == "-" ? "-1" : gid);
+      o->append(",node=\"");
+      escape_influx_field_str(in.host, o);
+      o->append("\",pid=\"");
+      escape_influx_field_str(p.pid, o);
+      o->append("\",pod=\"");
+      escape_influx_field_str(p.pod_name, o);
+      o->append("\",procressname=\"");
+      escape_influx_field_str(p.procname, o);
+      o->append("\",used_gpu=");
+      append_double(std::floor(p.used_memory_bytes / kMiB), o);
+      o->push_back(' ');
+      o->append(std::to_string(ts_ns));
+      o->push_back('\n');
+    }
+    return;
+  }
   for (const auto& p : *in.pod_rows) {
     const std::string gid = p.dev < static_cast<int>(n) ? st[p.dev].gpu_id : "-";
     // pod_gpu,host,namespace,gpu_id,containerid,pid_t,gpu_util_t,user_name_t  (gpu.py:207-208)

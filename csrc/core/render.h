@@ -105,7 +105,9 @@ struct RenderInput {
 
 void render_prometheus(const RenderInput& in, std::string* out);
 // Line protocol; one line per node_gpu / pod_gpu row (+ gpu_ext when extended), ns timestamps.
-void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::string* out);
+// schema: 2019 = the reference's current node_gpu/pod_gpu layout (gpu.py:136-143,206-216,240-250);
+// 2018 = the older pod_gpu layout of img/influxdb.png (node_gpu unchanged).
+void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::string* out, int schema = 2019);
 
 // Escapers (exposed for tests).
 void escape_label_value(const std::string& v, std::string* out);

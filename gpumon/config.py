@@ -49,6 +49,7 @@ class Config:
     # influx compat push
     influx_url: str = ""
     influx_extended: bool = False
+    influx_schema: int = 2019             # 2019 = gpu.py layout; 2018 = img/influxdb.png pod_gpu layout
     influx_every: int = 1
     # attribution
     procfs_root: str = "/proc"
@@ -112,6 +113,7 @@ class Config:
             "extended_families": self.extended_families,
             "influx_url": self.influx_url,
             "influx_extended": self.influx_extended,
+            "influx_schema": int(self.influx_schema),
             "influx_every": int(self.influx_every),
             "procfs_root": self.procfs_root,
             "opt_in": self.opt_in_label,
@@ -199,6 +201,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--host", help="node name label (default $NODE_NAME, then hostname)")
     p.add_argument("--influx-url", dest="influx_url", help="enable InfluxDB line-protocol push (default $INFLUXDB_URL)")
     p.add_argument("--influx-extended", dest="influx_extended", action="store_true", default=None)
+    p.add_argument("--influx-schema", dest="influx_schema", type=int, choices=[2018, 2019],
+                   help="pod_gpu line layout: 2019 (gpu.py, default) or 2018 (img/influxdb.png)")
     p.add_argument("--opt-in-label", dest="opt_in_label", help="only report pods with label KEY=VALUE")
     p.add_argument("--user-regex", dest="user_regex", help="regex on pod name; group 1 = user")
     p.add_argument("--user-label", dest="user_label", help="pod label holding the user name")

@@ -110,6 +110,21 @@ def test_influx_pod_gpu_line_matches_reference_layout(mock_exporter):
                     r"node=\"node-a\",user_name=\"-\",gpu_util=[\d.]+,used_memory=1024 \d{19}$", l), l
 
 
+def test_influx_2018_pod_gpu_layout(mock_exporter):
+    """img/influxdb.png: pod_gpu columns containerid, gid, gpu, host, namespace, node, pid, pod,
+    procressname, used_gpu (MiB)."""
+    import os
+
+    ex = mock_exporter(backend="mock:gpus=2", influx_schema=2018)
+    ex.mock_set_procs([{"pid": os.getpid(), "device": 1, "name": "python3", "vram_bytes": 15524 * 2 ** 20}])
+    ex.tick()
+    lines = [l for l in ex.influx_text().splitlines() if l.startswith("pod_gpu,")]
+    assert len(lines) == 1, lines
+    assert re.match(r"^pod_gpu,host=node-a,namespace=-,gpu=1,containerid=[-0-9a-f]+ gid=1,node=\"node-a\","
+                    r"pid=\"\d+\",pod=\"-\",procressname=\"python3\",used_gpu=15524 \d{19}$", lines[0]), lines[0]
+    assert sum(l.startswith("node_gpu,") for l in ex.influx_text().splitlines()) == 2  # node_gpu unchanged
+
+
 def test_no_nan_in_exposition(mock_exporter):
     ex = mock_exporter(backend="mock:gpus=3")
     ex.tick()
