@@ -25,11 +25,12 @@ static void on_signal(int) { g_stop = true; }
 
 static void usage() {
   fprintf(stderr,
-          "usage: gpumon-exporter [--backend amdsmi|mock[:k=v,..]] [--interval SEC] [--listen ADDR:PORT]\n"
-          "                       [--host NAME] [--devices 0,1,..] [--influx-url URL] [--influx-extended]\n"
+          "usage: gpumon-exporter [--backend auto|amdsmi|rocm_smi|mock[:k=v,..]] [--interval SEC]\n"
+          "                       [--listen ADDR:PORT] [--host NAME] [--devices 0,1,..] [--no-fast-path]\n"
+          "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--procfs /proc] [--no-processes] [--no-gzip] [--sample-threads N]\n"
-          "                       [--http-threads N] [--log-level debug|info|warn|error] [--once]\n"
+          "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx] [--once]\n"
           "env: NODE_NAME, INFLUXDB_URL, GPUMON_LISTEN, GPUMON_INTERVAL, GPUMON_BACKEND\n");
 }
 
@@ -59,6 +60,10 @@ int main(int argc, char** argv) {
         if (!s.empty()) cfg.devices.push_back(atoi(s.c_str()));
     } else if (a == "--influx-url") cfg.influx_url = next();
     else if (a == "--influx-extended") cfg.influx_extended = true;
+    else if (a == "--influx-schema") cfg.influx_schema = atoi(next().c_str());
+    else if (a == "--no-fast-path") cfg.fast_path = false;
+    else if (a == "--sysfs") cfg.sysfs_root = next();
+    else if (a == "--roctx") cfg.roctx = true;
     else if (a == "--opt-in-label") cfg.attribution.opt_in = next();
     else if (a == "--user-regex") cfg.attribution.user_regex = next();
     else if (a == "--user-label") cfg.attribution.user_label = next();
