@@ -526,5 +526,7 @@ PYBIND11_MODULE(_core, m) {
            })
       .def("mock_set_fail", [](Exporter& e, int dev, int every) { mock_of(e)->set_fail(dev, every); })
       .def("mock_set_hang_ms", [](Exporter& e, double ms) { mock_of(e)->set_hang_ms(ms); })
+      .def("mock_set_xgmi",
+           [](Exporter& e, int dev, int link, double gbps) { mock_of(e)->set_xgmi(dev, link, gbps); })
       .def("mock_calls", [](Exporter& e, int dev) { return mock_of(e)->calls(dev); });
 }

@@ -122,6 +122,9 @@ class MockBackend : public Backend {
   void set_procs(const std::vector<MockProc>& procs);
   void set_fail(int dev, int every);
   void set_hang_ms(double ms);
+  // Force link `link` of `dev` to carry `gbps` GB/s of reads (and half of it as writes);
+  // negative = back to the util-proportional default. For xGMI link-map tests.
+  void set_xgmi(int dev, int link, double gbps);
   uint64_t calls(int dev) const;
 
  private:
@@ -129,6 +132,7 @@ class MockBackend : public Backend {
   std::vector<DeviceStatic> devs_;
   mutable std::mutex mu_;
   std::vector<double> forced_util_;
+  std::vector<double> forced_xgmi_;  // per dev * kMaxLinks, GB/s (NaN = default)
   std::vector<uint64_t> calls_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
   std::map<std::pair<uint32_t, int>, uint64_t> proc_gfx_ns_;

@@ -67,6 +67,7 @@ bool MockBackend::init(std::string* err) {
   }
   size_t n = devs_.size();
   forced_util_.assign(n, kNaN);
+  forced_xgmi_.assign(n * kMaxLinks, kNaN);
   calls_.assign(n, 0);
   energy_.assign(n, 1000000);
   xgmi_rd_.assign(n * kMaxLinks, 0);
@@ -92,6 +93,13 @@ void MockBackend::set_fail(int dev, int every) {
   cfg_.fail_device = dev;
   cfg_.fail_every = every;
 }
+void MockBackend::set_xgmi(int dev, int link, double gbps) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (dev < 0 || link < 0 || link >= kMaxLinks) return;
+  const size_t k = static_cast<size_t>(dev) * kMaxLinks + link;
+  if (k < forced_xgmi_.size()) forced_xgmi_[k] = gbps < 0 ? kNaN : gbps;
+}
+
 void MockBackend::set_hang_ms(double ms) {
   std::lock_guard<std::mutex> g(mu_);
   cfg_.hang_ms = ms;
@@ -198,8 +206,9 @@ void MockBackend::sample(int i, DeviceSample* out) {
   a.n_links_acc = nl;
   for (int k = 0; k < nl; ++k) {
     if (k > 0) {
-      // ~util% of 64 GB/s per link, in KB
-      uint64_t kb = static_cast<uint64_t>(util / 100.0 * 64e6 * elapsed);
+      // ~util% of 64 GB/s per link, in KB (or the forced per-link rate)
+      const double forced = forced_xgmi_[i * kMaxLinks + k];
+      uint64_t kb = static_cast<uint64_t>((has(forced) ? forced : util / 100.0 * 64.0) * 1e6 * elapsed);
       xgmi_rd_[i * kMaxLinks + k] += kb;
       xgmi_wr_[i * kMaxLinks + k] += kb / 2;
     }

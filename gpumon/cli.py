@@ -7,6 +7,7 @@
     gpumon demo    [--gpus 8]                                                        mock node + fake kubelet
     gpumon probe   [--blocks 1024]                                                   run the K1 probe once
     gpumon load    [--kind mixed --seconds 10]                                       synthetic gfx950 load
+    gpumon xgmi    [--pairs 0:1,1:0 | --all-pairs] [--seconds 2]                     xGMI link-map validation
 
 Reference: the agent had no CLI, only ``python3 /gpu.py`` with env vars (Dockerfile:7,
 gpu.py:17-26); its display-table formatter (gpu.py:155-168) was dead code — ``gpumon top`` is
@@ -191,6 +192,39 @@ def cmd_load(args) -> int:
     return 0
 
 
+def cmd_xgmi(args) -> int:
+    """Peer-copy each (src, dst) pair and check that the exporter sees the traffic on the link it
+    attributes to dst (validation load for the per-link xGMI fields)."""
+    from ._native import core as _core
+    from .parallel.xgmi import validate_pair
+
+    import torch
+
+    n = torch.cuda.device_count()
+    if n < 2:
+        print(json.dumps({"skipped": f"needs >= 2 GPUs, found {n}"}))
+        return 0
+    if args.all_pairs:
+        pairs = [(a, b) for a in range(n) for b in range(n) if a != b]
+    else:
+        pairs = [tuple(int(x) for x in p.split(":")) for p in args.pairs.split(",")]
+    ex = _core().Exporter({"backend": args.backend, "devices": list(range(n)), "serve_http": False,
+                           "interval_s": args.interval, "link_every": 1, "processes": False})
+    err = ex.start()
+    if err:
+        print(err, file=sys.stderr)
+        return 1
+    ok = True
+    try:
+        for src, dst in pairs:
+            r = validate_pair(ex, src, dst, seconds=args.seconds, interval=args.interval)
+            ok &= r["peer_matches"]
+            print(json.dumps(r), flush=True)
+    finally:
+        ex.stop()
+    return 0 if ok else 1
+
+
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(prog="gpumon", description="MI355X Kubernetes GPU telemetry exporter")
     sub = p.add_subparsers(dest="cmd", required=True)
@@ -229,6 +263,13 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--duty", type=float, default=1.0)
     s.add_argument("--seconds", type=float, default=10.0)
     s.set_defaults(fn=cmd_load)
+    s = sub.add_parser("xgmi", help="validate the per-link xGMI counters with peer copies")
+    s.add_argument("--pairs", default="0:1")
+    s.add_argument("--all-pairs", action="store_true")
+    s.add_argument("--seconds", type=float, default=2.0)
+    s.add_argument("--interval", type=float, default=0.1)
+    s.add_argument("--backend", default="amdsmi")
+    s.set_defaults(fn=cmd_xgmi)
     return p
 
 

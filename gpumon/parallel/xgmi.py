@@ -61,3 +61,56 @@ def make_allreduce_buffer(nbytes: int, device) -> Optional[object]:
     import torch
 
     return torch.ones(max(1, nbytes // 2), dtype=torch.bfloat16, device=device)
+
+
+# ------------------------------------------------------------------------------------------------
+# Link-map validation: drive one peer copy at a time and see which link counter moves.
+# ------------------------------------------------------------------------------------------------
+def busiest_link(rates: dict, key: str = "xgmi_wr_Bps"):
+    """(link index, bytes/s) of the link carrying the most traffic in one device's rate dict."""
+    vals = rates.get(key) or []
+    if not vals:
+        return -1, 0.0
+    k = max(range(len(vals)), key=lambda i: vals[i])
+    return k, float(vals[k])
+
+
+def link_peer_bdf(sample: dict, link: int) -> str:
+    links = sample.get("links") or []
+    return links[link].get("peer_bdf", "") if 0 <= link < len(links) else ""
+
+
+def validate_pair(ex, src: int, dst: int, copier_factory=None, seconds: float = 2.0,
+                  interval: float = 0.1) -> dict:
+    """Copy src -> dst for ``seconds`` while the exporter ``ex`` samples both devices; report the
+    copy bandwidth, the link on ``src`` whose write counter moved most, the peer BDF the exporter
+    attributes to that link and whether it is ``dst``'s BDF."""
+    statics = {s["index"]: s for s in ex.statics()}
+    copier = (copier_factory or PeerCopier)(src, dst)
+    seq0 = ex.seq
+    ex.wait_for_seq(seq0 + 1, 10.0)
+    result = {"src": src, "dst": dst}
+    stop = time.perf_counter() + seconds
+    best = (-1, 0.0)
+    rx = (-1, 0.0)
+    bw = []
+    while time.perf_counter() < stop:
+        bw.append(copier.run(min(interval * 3, max(0.05, stop - time.perf_counter()))))
+        r = ex.rates()
+        if src < len(r) and r[src].get("valid"):
+            cand = busiest_link(r[src], "xgmi_wr_Bps")
+            if cand[1] > best[1]:
+                best = cand
+        if dst < len(r) and r[dst].get("valid"):
+            cand = busiest_link(r[dst], "xgmi_rd_Bps")
+            if cand[1] > rx[1]:
+                rx = cand
+    samples = ex.samples()
+    result["copy_GBps"] = round(sum(bw) / max(1, len(bw)) / 1e9, 2)
+    result["src_link"], result["src_link_tx_GBps"] = best[0], round(best[1] / 1e9, 2)
+    result["dst_link"], result["dst_link_rx_GBps"] = rx[0], round(rx[1] / 1e9, 2)
+    peer = link_peer_bdf(samples[src], best[0]) if src < len(samples) else ""
+    result["src_link_peer_bdf"] = peer
+    result["dst_bdf"] = statics.get(dst, {}).get("bdf", "")
+    result["peer_matches"] = bool(peer) and peer.lower() == result["dst_bdf"].lower()
+    return result
