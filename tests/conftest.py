@@ -9,6 +9,17 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def make_locked(target):
+    """`make <target>` serialised across pytest-xdist workers (a worker must never dlopen a fake
+    library another worker is relinking)."""
+    import fcntl
+
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", ROOT, target], check=True, stdout=subprocess.DEVNULL)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run on the GPU box with -m gpu)")
     config.addinivalue_line("markers", "slow: takes more than a few seconds")

@@ -7,6 +7,7 @@ import subprocess
 
 import pytest
 
+from conftest import make_locked
 from gpumon.export import promtext
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -15,7 +16,7 @@ FAKE = os.path.join(ROOT, "build", "fakes", "libfake_amd_smi.so")
 
 @pytest.fixture(scope="module", autouse=True)
 def fake_lib():
-    subprocess.run(["make", "-C", ROOT, "fakes"], check=True, stdout=subprocess.DEVNULL)
+    make_locked("fakes")
     return FAKE
 
 

@@ -8,6 +8,7 @@ import subprocess
 
 import pytest
 
+from conftest import make_locked
 from gpumon.export import promtext
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -20,7 +21,7 @@ ENV_KEYS = ("FAKE_RSMI_GPUS", "FAKE_RSMI_PROCS", "FAKE_RSMI_FAIL_METRICS", "FAKE
 
 @pytest.fixture(scope="module", autouse=True)
 def fake_libs():
-    subprocess.run(["make", "-C", ROOT, "fakes"], check=True, stdout=subprocess.DEVNULL)
+    make_locked("fakes")
 
 
 @pytest.fixture

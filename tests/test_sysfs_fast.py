@@ -13,6 +13,7 @@ import subprocess
 
 import pytest
 
+from conftest import make_locked
 from gpumon.export import promtext
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -79,7 +80,7 @@ def make_tree(tmp, gpus=2, blob_kw=None, procs=((4242, 0),)):
 
 @pytest.fixture(scope="module", autouse=True)
 def fake_lib():
-    subprocess.run(["make", "-C", ROOT, "fakes"], check=True, stdout=subprocess.DEVNULL)
+    make_locked("fakes")
 
 
 @pytest.fixture
