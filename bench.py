@@ -72,11 +72,13 @@ def main() -> int:
     ap.add_argument("--scrape-concurrency", type=int, default=2)
     ap.add_argument("--gzip", action="store_true", help="scrape with Accept-Encoding: gzip")
     ap.add_argument("--backend", default="auto")
-    ap.add_argument("--sample-threads", type=int, default=0, help="parallel per-GPU sampling threads")
+    ap.add_argument("--sample-threads", type=int, default=-1,
+                    help="parallel per-GPU sampling threads (-1 = auto: one per GPU, 0 = sequential)")
     ap.add_argument("--replicate", type=int, default=1,
                     help="REHEARSAL ONLY: sample each physical GPU R times (sampler scaling on a 1-GPU box)")
     ap.add_argument("--allreduce-mb", type=int, default=256)
     ap.add_argument("--probe", action="store_true", help="also run the K1 probe kernel each tick")
+    ap.add_argument("--no-fast-path", action="store_true", help="read every value through libamd_smi")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -129,7 +131,7 @@ def main() -> int:
                 backend = f"amdsmi:replicate={args.replicate}"
         cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi")) else [],
                      interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
-                     enable_probe=args.probe and has_gpu, log_level="warn",
+                     enable_probe=args.probe and has_gpu, log_level="warn", fast_path=not args.no_fast_path,
                      sample_threads=args.sample_threads)
         mon = GpuMonitor(cfg, control_plane=False).start()
         if mon.start_error:

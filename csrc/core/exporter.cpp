@@ -183,7 +183,12 @@ bool Exporter::ensure_backend() {
     dev_errors_.assign(st.size(), 0);
     proc_counts_.assign(st.size(), 0);
   }
-  if (cfg_.sample_threads > 0 && !pool_) pool_ = std::make_unique<Pool>(cfg_.sample_threads);
+  // auto: the per-device reads are independent (each waits on its own SMU/KFD), so sample them
+  // concurrently -- the caller thread takes one device, so n devices need n-1 workers.
+  const int nthreads = cfg_.sample_threads >= 0 ? cfg_.sample_threads
+                       : static_cast<int>(st.size()) >= 2 ? std::min<int>(static_cast<int>(st.size()), 8) - 1
+                                                          : 0;
+  if (nthreads > 0 && !pool_) pool_ = std::make_unique<Pool>(nthreads);
   backend_up_ = true;
   GPUMON_LOG(LogLevel::kInfo, "exporter",
              "backend " + backend_->name() + " up with " + std::to_string(st.size()) + " GPU(s)");

@@ -38,7 +38,7 @@ class Config:
     interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
     processes: bool = True
     link_every: int = 30
-    sample_threads: int = 0
+    sample_threads: int = -1              # -1 = auto (parallel per GPU when >= 2 GPUs)
     # exposition
     listen: str = "0.0.0.0:9400"
     http_threads: int = 2

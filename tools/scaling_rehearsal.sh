@@ -16,8 +16,10 @@ for hz in 1 10; do
     echo "done hz=$hz r=$r"
   done
 done
-timeout -k 10 150 python bench.py --steps 10 --warmup 2 --interval 1.0 --replicate 8 --sample-threads 8 \
-  --out $out/b_1hz_r8_par.json > $out/log_par.txt 2>&1 && cat $out/b_1hz_r8_par.json >> $out/results.jsonl
+timeout -k 10 150 python bench.py --steps 10 --warmup 2 --interval 1.0 --replicate 8 --sample-threads 0 \
+  --out $out/b_1hz_r8_seq.json > $out/log_seq.txt 2>&1 && cat $out/b_1hz_r8_seq.json >> $out/results.jsonl
+timeout -k 10 150 python bench.py --steps 10 --warmup 2 --interval 1.0 --no-fast-path \
+  --out $out/b_1hz_nofast.json > $out/log_nofast.txt 2>&1 && cat $out/b_1hz_nofast.json >> $out/results.jsonl
 timeout -k 10 150 python bench.py --steps 10 --warmup 2 --interval 1.0 --probe \
   --out $out/b_1hz_probe.json > $out/log_probe.txt 2>&1 && cat $out/b_1hz_probe.json >> $out/results.jsonl
 timeout -k 10 150 python bench.py --steps 10 --warmup 2 --interval 1.0 --load idle \
