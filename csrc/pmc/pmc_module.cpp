@@ -138,6 +138,72 @@ void load_supported(Agent& A) {
 
 }  // namespace
 
+// Resolve (and cache) the counter config for `counters` on `agent`; returns the record count.
+static size_t prepare(int agent, const std::vector<std::string>& counters, Agent** out) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (agent < 0 || agent >= static_cast<int>(g_agents.size())) throw std::out_of_range("agent");
+  Agent* A = g_agents[agent].get();
+  load_supported(*A);
+  auto it = A->profiles.find(counters);
+  if (it == A->profiles.end()) {
+    std::vector<rocprofiler_counter_id_t> ids;
+    size_t expect = 0;
+    for (const auto& c : counters) {
+      auto s = A->supported.find(c);
+      if (s == A->supported.end()) throw std::invalid_argument("counter not supported: " + c);
+      ids.push_back(s->second);
+      rocprofiler_counter_info_v1_t info{};
+      info.size = sizeof(info);
+      check(rocprofiler_query_counter_info(s->second, ROCPROFILER_COUNTER_INFO_VERSION_1, &info),
+            "query_counter_info");
+      expect += info.dimensions_instances_count;
+    }
+    rocprofiler_counter_config_id_t cfg{};
+    check(rocprofiler_create_counter_config(A->info.id, ids.data(), ids.size(), &cfg), "create_counter_config");
+    it = A->profiles.emplace(counters, std::make_pair(cfg, expect)).first;
+  }
+  A->active = it->second.first;
+  *out = A;
+  return it->second.second;
+}
+
+// Per counter: sum / max / count over all dimension instances, plus per-XCC sums.
+static py::dict reduce(const Agent& A, const std::vector<rocprofiler_counter_record_t>& recs) {
+  std::map<std::string, double> sum, mx;
+  std::map<std::string, uint64_t> cnt;
+  std::map<std::string, std::map<size_t, double>> by_xcc;
+  for (const auto& r : recs) {
+    rocprofiler_counter_id_t cid{};
+    rocprofiler_query_record_counter_id(r.id, &cid);
+    auto nm = A.id2name.find(cid.handle);
+    std::string name = nm == A.id2name.end() ? "UNKNOWN" : nm->second;
+    sum[name] += r.counter_value;
+    mx[name] = cnt[name] ? std::max(mx[name], r.counter_value) : r.counter_value;
+    cnt[name]++;
+    auto xd = A.xcc_dim.find(cid.handle);
+    if (xd != A.xcc_dim.end()) {
+      size_t pos = 0;
+      if (rocprofiler_query_record_dimension_position(r.id, xd->second, &pos) == ROCPROFILER_STATUS_SUCCESS)
+        by_xcc[name][pos] += r.counter_value;
+    }
+  }
+  py::dict out;
+  for (const auto& kv : sum) {
+    py::dict d;
+    d["sum"] = kv.second;
+    d["max"] = mx[kv.first];
+    d["n"] = cnt[kv.first];
+    std::vector<double> xs;
+    for (const auto& [pos, v] : by_xcc[kv.first]) {
+      if (xs.size() <= pos) xs.resize(pos + 1, 0.0);
+      xs[pos] = v;
+    }
+    d["by_xcc"] = xs;
+    out[py::str(kv.first)] = d;
+  }
+  return out;
+}
+
 PYBIND11_MODULE(_pmc, m) {
   m.doc() = "gpumon device-wide PMC sampling (rocprofiler-sdk device counting service)";
 
@@ -205,37 +271,9 @@ PYBIND11_MODULE(_pmc, m) {
   m.def(
       "sample",
       [](int agent, std::vector<std::string> counters, double window_s) {
-        std::vector<rocprofiler_counter_record_t> recs;
-        Agent* A;
-        size_t n = 0;
-        {
-          std::lock_guard<std::mutex> g(g_mu);
-          if (agent < 0 || agent >= static_cast<int>(g_agents.size())) throw std::out_of_range("agent");
-          A = g_agents[agent].get();
-          load_supported(*A);
-          auto it = A->profiles.find(counters);
-          if (it == A->profiles.end()) {
-            std::vector<rocprofiler_counter_id_t> ids;
-            size_t expect = 0;
-            for (const auto& c : counters) {
-              auto s = A->supported.find(c);
-              if (s == A->supported.end()) throw std::invalid_argument("counter not supported: " + c);
-              ids.push_back(s->second);
-              rocprofiler_counter_info_v1_t info{};
-              info.size = sizeof(info);
-              check(rocprofiler_query_counter_info(s->second, ROCPROFILER_COUNTER_INFO_VERSION_1, &info),
-                    "query_counter_info");
-              expect += info.dimensions_instances_count;
-            }
-            rocprofiler_counter_config_id_t cfg{};
-            check(rocprofiler_create_counter_config(A->info.id, ids.data(), ids.size(), &cfg),
-                  "create_counter_config");
-            it = A->profiles.emplace(counters, std::make_pair(cfg, expect)).first;
-          }
-          A->active = it->second.first;
-          n = it->second.second;
-        }
-        recs.resize(std::max<size_t>(n, 1));
+        Agent* A = nullptr;
+        size_t n = prepare(agent, counters, &A);
+        std::vector<rocprofiler_counter_record_t> recs(std::max<size_t>(n, 1));
         rocprofiler_status_t st;
         {
           py::gil_scoped_release nogil;
@@ -247,40 +285,48 @@ PYBIND11_MODULE(_pmc, m) {
           recs.resize(cnt);
         }
         check(st, "sample_device_counting_service");
-        // reduce: per counter sum / max / count, and per-XCC sums
-        std::map<std::string, double> sum, mx;
-        std::map<std::string, uint64_t> cnt;
-        std::map<std::string, std::map<size_t, double>> by_xcc;
-        for (const auto& r : recs) {
-          rocprofiler_counter_id_t cid{};
-          rocprofiler_query_record_counter_id(r.id, &cid);
-          auto nm = A->id2name.find(cid.handle);
-          std::string name = nm == A->id2name.end() ? "UNKNOWN" : nm->second;
-          sum[name] += r.counter_value;
-          mx[name] = cnt[name] ? std::max(mx[name], r.counter_value) : r.counter_value;
-          cnt[name]++;
-          auto xd = A->xcc_dim.find(cid.handle);
-          if (xd != A->xcc_dim.end()) {
-            size_t pos = 0;
-            if (rocprofiler_query_record_dimension_position(r.id, xd->second, &pos) == ROCPROFILER_STATUS_SUCCESS)
-              by_xcc[name][pos] += r.counter_value;
+        return reduce(*A, recs);
+      },
+      py::arg("agent"), py::arg("counters"), py::arg("window_s") = 0.1);
+
+  // Every listed agent counts over the SAME window: on an 8-GPU node one PMC step costs one
+  // window instead of eight back-to-back ones.
+  m.def(
+      "sample_many",
+      [](std::vector<int> agents, std::vector<std::string> counters, double window_s) {
+        std::vector<Agent*> As(agents.size(), nullptr);
+        std::vector<std::vector<rocprofiler_counter_record_t>> recs(agents.size());
+        for (size_t k = 0; k < agents.size(); ++k)
+          recs[k].resize(std::max<size_t>(prepare(agents[k], counters, &As[k]), 1));
+        std::vector<rocprofiler_status_t> st(agents.size(), ROCPROFILER_STATUS_SUCCESS);
+        {
+          py::gil_scoped_release nogil;
+          size_t started = 0;
+          for (; started < As.size(); ++started)
+            if (rocprofiler_start_context(As[started]->ctx) != ROCPROFILER_STATUS_SUCCESS) break;
+          if (started == As.size()) std::this_thread::sleep_for(std::chrono::duration<double>(window_s));
+          for (size_t k = 0; k < As.size(); ++k) {
+            if (k >= started) {
+              st[k] = ROCPROFILER_STATUS_ERROR;
+              continue;
+            }
+            size_t cnt = recs[k].size();
+            st[k] = rocprofiler_sample_device_counting_service(As[k]->ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE,
+                                                               recs[k].data(), &cnt);
+            recs[k].resize(cnt);
           }
+          for (size_t k = 0; k < started; ++k) rocprofiler_stop_context(As[k]->ctx);
         }
-        py::dict out;
-        for (const auto& kv : sum) {
-          py::dict d;
-          d["sum"] = kv.second;
-          d["max"] = mx[kv.first];
-          d["n"] = cnt[kv.first];
-          std::vector<double> xs;
-          for (const auto& [pos, v] : by_xcc[kv.first]) {
-            if (xs.size() <= pos) xs.resize(pos + 1, 0.0);
-            xs[pos] = v;
+        py::list out;
+        for (size_t k = 0; k < As.size(); ++k) {
+          if (st[k] != ROCPROFILER_STATUS_SUCCESS) {
+            out.append(py::none());
+            continue;
           }
-          d["by_xcc"] = xs;
-          out[py::str(kv.first)] = d;
+          out.append(reduce(*As[k], recs[k]));
         }
         return out;
       },
-      py::arg("agent"), py::arg("counters"), py::arg("window_s") = 0.1);
+      py::arg("agents"), py::arg("counters"), py::arg("window_s") = 0.1,
+      "sample() for several agents over one shared window; None for an agent that failed");
 }

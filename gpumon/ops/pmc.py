@@ -84,6 +84,23 @@ class PmcRunner:
 
     def _step(self) -> Dict[int, dict]:
         res = {}
+        if len(self.map) > 1 and hasattr(self.P, "sample_many"):
+            # all GPUs count over one shared window (8 GPUs: one 0.1 s window, not eight)
+            devs = list(self.map)
+            try:
+                raws = self.P.sample_many([self.map[d] for d in devs], self.counters, self.window_s)
+            except Exception as e:  # noqa: BLE001
+                raws = [None] * len(devs)
+                log.warning("pmc sample_many failed: %s", e)
+            for dev, raw in zip(devs, raws):
+                if raw is None:
+                    self.errors += 1
+                    continue
+                res[dev] = derive(raw, self.agents[self.map[dev]])
+                res[dev]["raw"] = raw
+            self.last.update(res)
+            self._export()
+            return res
         for dev, ai in self.map.items():
             try:
                 raw = self.P.sample(ai, self.counters, self.window_s)

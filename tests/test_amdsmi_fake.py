@@ -3,7 +3,6 @@ exercised on CPU against build/fakes/libfake_amd_smi.so (csrc/fakes/fake_amd_smi
 returns MI355X-shaped gpu_metrics v1.8 tables."""
 
 import os
-import subprocess
 
 import pytest
 

@@ -28,4 +28,5 @@ def test_pmc_separates_idle_mfma_hbm():
     # partial occupancy (burn on ~1/4 of the CUs): busy GPU, but MFMA pipes mostly idle
     assert 5 < d["partial"]["mfma_busy"] < 0.6 * d["mfma"]["mfma_busy"], d["partial"]
     assert len(d["mfma"].get("xcd_mfma_busy", [])) == 8
+    assert d["mfma_many"][0]["mfma_busy"] > 60, d["mfma_many"]  # sample_many agrees with sample
     print("pmc:", {k: d[k] for k in ("idle", "mfma", "hbm")})

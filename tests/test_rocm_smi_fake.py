@@ -4,7 +4,6 @@ the amdsmi fake, so the exposition must match field for field; plus the `auto` f
 failing libamd_smi to rocm_smi."""
 
 import os
-import subprocess
 
 import pytest
 

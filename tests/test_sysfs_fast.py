@@ -9,7 +9,6 @@ carry fdinfo gfx time, and a layout/header mismatch falls back to libamd_smi.
 
 import os
 import struct
-import subprocess
 
 import pytest
 

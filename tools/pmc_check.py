@@ -31,6 +31,9 @@ def main():
             out[kind] = derive(raw, agents[0])
             out[kind + "_raw"] = {k: {"sum": v["sum"], "max": v["max"], "n": v["n"]} for k, v in raw.items()}
             out[kind + "_load"] = load.stats()
+            if kind == "mfma":  # shared-window path used by PmcRunner on multi-GPU nodes
+                many = P.sample_many(list(range(len(agents))), counters, 0.2)
+                out["mfma_many"] = [derive(r, agents[i]) if r is not None else None for i, r in enumerate(many)]
     print(json.dumps(out, default=str))
 
 
