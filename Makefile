@@ -50,9 +50,12 @@ $(BIN): $(CORE_OBJ) build/obj/exporter_main.o
 
 # HIP kernels + their pybind11 wrapper in one hipcc-built extension (gfx950 only).
 HIPFLAGS  := --offload-arch=$(GPUMON_ARCH) -O3 -std=c++17 -fPIC -fvisibility=hidden -Icsrc
+# MFMA accumulators in VGPRs: with AGPR accumulators LLVM rotates the 4-register 16x16x32 chains
+# through v_accvgpr_read/write/mov inside the burn loop (checked with --cuda-device-only -S).
+KERNEL_FLAGS := -mllvm -amdgpu-mfma-vgpr-form
 build/obj/hip/kernels.o: csrc/hip/kernels.hip $(HIP_HDR)
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(KERNEL_FLAGS) -c $< -o $@
 
 build/obj/bindings/hip_module.o: csrc/bindings/hip_module.cpp $(HIP_HDR)
 	@mkdir -p $(dir $@)

@@ -20,10 +20,11 @@ PYBIND11_MODULE(_hip, m) {
   m.def("mfma_tile", [](int dev, uintptr_t a, uintptr_t b, uintptr_t c, int iters, uintptr_t stream) {
     launch_mfma_tile(dev, P(a), P(b), static_cast<float*>(P(c)), iters, P(stream));
   }, py::arg("dev"), py::arg("a"), py::arg("b"), py::arg("c"), py::arg("iters"), py::arg("stream") = 0);
-  m.def("mfma_burn", [](int dev, uintptr_t a, uintptr_t b, uintptr_t out, int blocks, int iters, uintptr_t stream) {
-    launch_mfma_burn(dev, P(a), P(b), static_cast<float*>(P(out)), blocks, iters, P(stream));
+  m.def("mfma_burn", [](int dev, uintptr_t a, uintptr_t b, uintptr_t out, int blocks, int iters, uintptr_t stream,
+                        int shape) {
+    launch_mfma_burn(dev, P(a), P(b), static_cast<float*>(P(out)), blocks, iters, P(stream), shape);
   }, py::arg("dev"), py::arg("a"), py::arg("b"), py::arg("out"), py::arg("blocks"), py::arg("iters"),
-     py::arg("stream") = 0);
+     py::arg("stream") = 0, py::arg("shape") = 32);
   m.def("stream_copy", [](int dev, uintptr_t src, uintptr_t dst, size_t n16, int blocks, uintptr_t stream,
                           int unroll) {
     launch_stream_copy(dev, P(src), P(dst), n16, blocks, P(stream), unroll);
@@ -37,8 +38,13 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("blocks") = 4096, py::arg("stream") = 0);
 
   py::class_<LoadGen>(m, "LoadGen")
-      .def(py::init<int, std::string, double, size_t, int>(), py::arg("dev"), py::arg("kind") = "mixed",
-           py::arg("duty") = 1.0, py::arg("hbm_bytes") = size_t(1) << 30, py::arg("mfma_iters") = 8192)
+      .def(py::init([](int dev, std::string kind, double duty, size_t hbm_bytes, int mfma_iters, int shape) {
+             auto g = std::make_unique<LoadGen>(dev, std::move(kind), duty, hbm_bytes, mfma_iters);
+             g->set_mfma_shape(shape);
+             return g;
+           }),
+           py::arg("dev"), py::arg("kind") = "mixed", py::arg("duty") = 1.0, py::arg("hbm_bytes") = size_t(1) << 30,
+           py::arg("mfma_iters") = 8192, py::arg("mfma_shape") = 32)
       .def("start", [](LoadGen& g) {
         py::gil_scoped_release nogil;
         g.start();

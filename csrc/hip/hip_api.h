@@ -21,7 +21,9 @@ int device_cu_count(int dev);
 // C[32x32] (fp32, row-major) = iters * A[32x16] @ B[16x32] (bf16, row-major), one wave.
 void launch_mfma_tile(int dev, const void* a, const void* b, float* c, int iters, void* stream);
 // Burn: `blocks` x 256 threads; each wave runs iters x 4 MFMAs; wave sums go to out[blocks*4].
-void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blocks, int iters, void* stream);
+// shape 32: v_mfma_f32_32x32x16_bf16 x4 accumulators; 16: v_mfma_f32_16x16x32_bf16 x8 (same FLOP/iter)
+void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blocks, int iters, void* stream,
+                      int shape = 32);
 // dst = src (n16 = number of 16-byte vectors)
 void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream, int unroll = 4);
 // c = a + s * b  (fp32, n elements, n % 4 == 0)
@@ -47,6 +49,8 @@ class LoadGen {
   void stop();
   LoadStats stats() const;
   bool running() const { return running_; }
+  void set_mfma_shape(int shape) { shape_ = shape; }  // 32 or 16 (launch_mfma_burn); before start()
+  int mfma_shape() const { return shape_; }
 
  private:
   void loop();
@@ -55,6 +59,7 @@ class LoadGen {
   double duty_;
   size_t bytes_;
   int iters_;
+  int shape_ = 32;
   void* stream_ = nullptr;
   void* a_ = nullptr;
   void* b_ = nullptr;

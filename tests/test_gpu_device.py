@@ -135,6 +135,35 @@ def test_mfma_burn_runs_and_is_deterministic(H, torch_gpu):
     assert torch.allclose(out1, torch.full_like(out1, ref), rtol=1e-3, atol=1e-2), (out1[:4], ref)
 
 
+def test_mfma_burn16_matches_fragment_reference(H, torch_gpu):
+    """16x16x32 burn: the 32x32x16 register fragments reinterpreted with the 16x16x32 mapping
+    (A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15], C col l&15 row 4(l>>4)+reg), fp32 reference."""
+    torch = torch_gpu
+    g = torch.Generator(device="cpu").manual_seed(3)
+    a = torch.randint(-3, 4, (32, 16), generator=g).to(torch.bfloat16)
+    b = torch.randint(-3, 4, (16, 32), generator=g).to(torch.bfloat16)
+    af, bf = a.float(), b.float()
+    A = torch.empty(16, 32)
+    B = torch.empty(32, 16)
+    for lane in range(64):
+        r, h = lane & 31, lane >> 5
+        av = [af[r, 8 * h + j] for j in range(8)]
+        bv = [bf[8 * h + j, r] for j in range(8)]
+        i, q = lane & 15, lane >> 4
+        for j in range(8):
+            A[i, 8 * q + j] = av[j]
+            B[8 * q + j, i] = bv[j]
+    C = A @ B
+    iters = 32
+    ref = 28.0 + 8 * iters * C[0:4, 0].sum().item()
+    out = torch.zeros(256 * 4, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    ad, bd = a.cuda(), b.cuda()
+    H.mfma_burn(0, ad.data_ptr(), bd.data_ptr(), out.data_ptr(), 256, iters, s, 16)
+    torch.cuda.synchronize()
+    assert torch.allclose(out, torch.full_like(out, ref)), (out[:4], ref)
+
+
 def test_stream_copy_and_triad_match_torch(H, torch_gpu):
     torch = torch_gpu
     n = (1 << 22) + 64
