@@ -99,35 +99,6 @@ __global__ void __launch_bounds__(256) mfma_burn_kernel(const __bf16* __restrict
   if (lane == 0) out[blockIdx.x * 4 + (threadIdx.x >> 6)] = s;
 }
 
-// Burn, 16x16x32 form: 8 accumulators x 16 cycles = the same 128 KFLOP per wave per iteration as
-// the 32x32x16 loop above, in the shape that holds a higher clock under load on random operands
-// (MI355X_MICROARCH.md DVFS item 7: ~1.15x FLOP/s). The register fragments loaded for the 32x32
-// form are reused as-is (a burn needs live operands, not a particular product); the 16x16x32
-// fragment mapping (A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15], C col l&15 row 4(l>>4)+reg) is what
-// the numerics test reproduces.
-__global__ void __launch_bounds__(256) mfma_burn16_kernel(const __bf16* __restrict__ a, const __bf16* __restrict__ b,
-                                                          float* __restrict__ out, int iters) {
-  const int lane = threadIdx.x & 63;
-  bf16x8 av, bv;
-  load_frags(a, b, lane, &av, &bv);
-  // named accumulators (an array of vectors made the compiler rotate AGPRs inside the loop)
-  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {1.f, 0.f, 0.f, 0.f}, c2 = {2.f, 0.f, 0.f, 0.f}, c3 = {3.f, 0.f, 0.f, 0.f};
-  f32x4 c4 = {4.f, 0.f, 0.f, 0.f}, c5 = {5.f, 0.f, 0.f, 0.f}, c6 = {6.f, 0.f, 0.f, 0.f}, c7 = {7.f, 0.f, 0.f, 0.f};
-  for (int i = 0; i < iters; ++i) {
-    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c0, 0, 0, 0);
-    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c1, 0, 0, 0);
-    c2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c2, 0, 0, 0);
-    c3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c3, 0, 0, 0);
-    c4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c4, 0, 0, 0);
-    c5 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c5, 0, 0, 0);
-    c6 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c6, 0, 0, 0);
-    c7 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c7, 0, 0, 0);
-  }
-  const f32x4 t = c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7;
-  const float s = t[0] + t[1] + t[2] + t[3];
-  if (lane == 0) out[blockIdx.x * 4 + (threadIdx.x >> 6)] = s;
-}
-
 // ============================================================================================
 // K2b: HBM stream. 16 B per lane, non-temporal (streamed once), grid-stride.
 // ============================================================================================
@@ -222,6 +193,9 @@ void launch_mfma_tile(int dev, const void* a, const void* b, float* c, int iters
   check(hipGetLastError(), "mfma_tile_kernel");
 }
 
+// burn16.hip (own TU, VGPR-form MFMA accumulators)
+void launch_mfma_burn16(const __bf16* a, const __bf16* b, float* out, int blocks, int iters, hipStream_t s);
+
 void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blocks, int iters, void* stream,
                       int shape) {
   check(hipSetDevice(dev), "hipSetDevice");
@@ -229,7 +203,7 @@ void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blo
   auto pa = static_cast<const __bf16*>(a);
   auto pb = static_cast<const __bf16*>(b);
   if (shape == 32) hipLaunchKernelGGL(mfma_burn_kernel, dim3(blocks), dim3(256), 0, s, pa, pb, out, iters);
-  else if (shape == 16) hipLaunchKernelGGL(mfma_burn16_kernel, dim3(blocks), dim3(256), 0, s, pa, pb, out, iters);
+  else if (shape == 16) launch_mfma_burn16(pa, pb, out, blocks, iters, s);
   else throw std::invalid_argument("mfma_burn: shape must be 32 (32x32x16) or 16 (16x16x32)");
   check(hipGetLastError(), "mfma_burn_kernel");
 }

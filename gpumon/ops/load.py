@@ -3,7 +3,9 @@
 ``SyntheticLoad(dev, kind)`` drives one GPU from a native C++ thread (no GIL) with back-to-back
 launches of the gfx950 kernels in ``csrc/hip/kernels.hip``:
 
-* ``mfma``  — bf16 ``v_mfma_f32_32x32x16_bf16`` burn, 2 waves per SIMD, 4 accumulators per wave;
+* ``mfma``  — bf16 MFMA burn: ``mfma_shape=16`` = ``v_mfma_f32_16x16x32_bf16`` x 8 chains per wave
+  (2.24 PFLOP/s sustained on MI355X, profiles/r1_kernels_and_pmc.md), ``32`` =
+  ``v_mfma_f32_32x32x16_bf16`` x 4 chains (1.76–2.0 PFLOP/s: the chip holds a lower clock on it);
 * ``hbm``   — 16 B/lane non-temporal copy over a ``hbm_bytes`` buffer pair (HBM3E bound);
 * ``mixed`` — alternating; ``duty`` < 1 inserts idle gaps (partial-utilisation validation).
 """
@@ -15,8 +17,8 @@ from .._native import hip
 
 class SyntheticLoad:
     def __init__(self, dev: int = 0, kind: str = "mixed", duty: float = 1.0, hbm_bytes: int = 1 << 30,
-                 mfma_iters: int = 8192):
-        self._g = hip().LoadGen(dev, kind, duty, hbm_bytes, mfma_iters)
+                 mfma_iters: int = 8192, mfma_shape: int = 16):
+        self._g = hip().LoadGen(dev, kind, duty, hbm_bytes, mfma_iters, mfma_shape)
         self.dev = dev
         self.kind = kind
 
