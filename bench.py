@@ -258,6 +258,9 @@ def main() -> int:
             "load_tbps": round(lstats.get("tbps", 0.0), 3) if lstats else None,
             "gfx_util_last": util,
             "procs_seen": len([r for r in rows if not r["idle"]]),
+            "proc_rows": [{"pid": r["pid"], "vram_gib": round(r["used_memory_bytes"] / 2 ** 30, 2),
+                           "cu_occupancy": r["cu_occupancy"], "gfx_util": r["proc_gfx_util"]}
+                          for r in rows if not r["idle"]][:8],
             "xgmi": _xgmi_summary(xgmi, xgmi_rates),
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,
         }
