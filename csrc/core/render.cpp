@@ -457,12 +457,27 @@ void render_prometheus(const RenderInput& in, std::string* o) {
     }
     {
       Family f(o, "pod_gpu_proc_gfx_util",
-               "Per-process GFX engine utilization in percent over the sampling interval.", "gauge");
+               "Per-process GFX engine utilization in percent over the sampling interval (DRM fdinfo "
+               "engine time: graphics/kernel-queue work; HIP compute on KFD user queues shows in "
+               "pod_gpu_proc_cu_occupancy_percent instead).",
+               "gauge");
       for (size_t r = 0; r < rows.size(); ++r) f.add(rl[r], rows[r].proc_gfx_util);
     }
     {
-      Family f(o, "pod_gpu_proc_cu_occupancy", "Compute units occupied by the process.", "gauge");
+      Family f(o, "pod_gpu_proc_cu_occupancy", "Compute units occupied by the process's waves (KFD).", "gauge");
       for (size_t r = 0; r < rows.size(); ++r) f.add(rl[r], rows[r].cu_occupancy);
+    }
+    {
+      // The per-process utilisation signal for HIP compute: CUs holding the process's waves / CUs
+      // on the device (256 on MI355X, measured 256 under the bf16 burn).
+      Family f(o, "pod_gpu_proc_cu_occupancy_percent",
+               "Share of the GPU's compute units occupied by the process's waves, in percent.", "gauge");
+      for (size_t r = 0; r < rows.size(); ++r) {
+        const int dev = rows[r].dev;
+        const int cus = dev >= 0 && dev < static_cast<int>(in.statics->size()) ? (*in.statics)[dev].num_cu : 0;
+        if (cus > 0 && has(rows[r].cu_occupancy))
+          f.add(rl[r], std::min(100.0, 100.0 * rows[r].cu_occupancy / cus));
+      }
     }
     // One series per (pod, container, gpu): the allocation view behind the reference dashboard's
     // "GPUs per user" and "allocated / in use" panels.

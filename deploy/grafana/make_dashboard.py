@@ -92,6 +92,11 @@ def build():
                         [(f'gpu_mfma_busy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} mfma"),
                          (f'gpu_occupancy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} occupancy")], 12, y, 12, 8))
     y += 8
+    panels.append(panel("Per-pod compute share (% of CUs holding the pod's waves)", "timeseries",
+                        [(f'sum by (host, gpu_id, namespace, podname) (pod_gpu_proc_cu_occupancy_percent{{{HOST}}})',
+                          "{{host}} gpu{{gpu_id}} {{namespace}}/{{podname}}")], 0, y, 24, 8,
+                        fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
+    y += 8
     panels.append(panel("Exporter: /metrics p99 and tick p99 (s)", "timeseries",
                         [(f'histogram_quantile(0.99, sum by (le, host) (rate(gpumon_scrape_duration_seconds_bucket{{{HOST}}}[5m])))',
                           "{{host}} scrape p99"),

@@ -77,6 +77,7 @@ def test_dashboard_queries_resolve_against_exposition(mock_exporter):
     dash = json.load(open(os.path.join(ROOT, "deploy/grafana/gpumon-dashboard.json")))
     ex = mock_exporter(backend="mock:gpus=2")
     ex.set_allocations([{"pod_namespace": "ml", "pod_name": "jupyter-e-0", "container_name": "c", "gpu_index": 0}])
+    ex.mock_set_procs([{"pid": os.getpid(), "device": 1, "name": "python3"}])
     ex.tick()
     fam = promtext.parse(ex.metrics_text())
     produced = set()
