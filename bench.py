@@ -113,7 +113,8 @@ def main() -> int:
         load = SyntheticLoad(dev=local_rank, kind=args.load, hbm_bytes=1 << 30).start()
     ar_buf = None
     if dist is not None and args.allreduce_mb > 0:
-        ar_buf = torch.ones(args.allreduce_mb * (1 << 20) // 2, dtype=torch.bfloat16, device=device)
+        # zeros: repeated in-place sums stay finite (ones would reach inf after ~40 steps on 8 ranks)
+        ar_buf = torch.zeros(args.allreduce_mb * (1 << 20) // 2, dtype=torch.bfloat16, device=device)
 
     # ---------------------------------------------------------------- rank 0: exporter + scraper
     mon = None
