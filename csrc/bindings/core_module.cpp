@@ -65,6 +65,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "init_retry_s", &c.init_retry_s);
   get(d, "health_stale_s", &c.health_stale_s);
   get(d, "reinit_after", &c.reinit_after);
+  get(d, "device_timeout_s", &c.device_timeout_s);
   get(d, "version", &c.version);
   get(d, "activity_acc_scale", &c.rates.activity_acc_scale);
   get(d, "xgmi_kb_bytes", &c.rates.xgmi_kb_bytes);
@@ -433,6 +434,7 @@ PYBIND11_MODULE(_core, m) {
              d["influx_fail"] = s.influx_fail;
              d["influx_dropped"] = s.influx_dropped;
              d["device_errors"] = s.device_errors;
+             d["device_timeouts"] = s.device_timeouts;
              d["sample_count"] = s.sample_hist.count;
              d["sample_sum_s"] = s.sample_hist.sum;
              d["attribution_cache_hits"] = s.attribution_cache_hits;
@@ -525,7 +527,8 @@ PYBIND11_MODULE(_core, m) {
              mock_of(e)->set_procs(v);
            })
       .def("mock_set_fail", [](Exporter& e, int dev, int every) { mock_of(e)->set_fail(dev, every); })
-      .def("mock_set_hang_ms", [](Exporter& e, double ms) { mock_of(e)->set_hang_ms(ms); })
+      .def("mock_set_hang_ms", [](Exporter& e, double ms, int dev) { mock_of(e)->set_hang_ms(ms, dev); },
+           py::arg("ms"), py::arg("dev") = -1)
       .def("mock_set_xgmi",
            [](Exporter& e, int dev, int link, double gbps) { mock_of(e)->set_xgmi(dev, link, gbps); })
       .def("mock_calls", [](Exporter& e, int dev) { return mock_of(e)->calls(dev); });

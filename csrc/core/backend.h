@@ -96,6 +96,7 @@ struct MockConfig {
   std::string mode = "wave";          // "wave" (sinusoid), "const", "idle", "load"
   double const_util = 50.0;
   double hang_ms = 0.0;               // sleep inside sample() (watchdog / latency tests)
+  int hang_device = -1;               // ... on this hip_id only (-1: every device)
   int fail_device = -1;               // device whose sample() fails ...
   int fail_every = 0;                 // ... every N calls (0 = never); -1 = always
   std::vector<std::string> unsupported;  // field names forced to NaN, e.g. "temp_edge"
@@ -121,7 +122,7 @@ class MockBackend : public Backend {
   void set_util(int dev, double pct);
   void set_procs(const std::vector<MockProc>& procs);
   void set_fail(int dev, int every);
-  void set_hang_ms(double ms);
+  void set_hang_ms(double ms, int dev = -1);  // dev -1: every device
   // Force link `link` of `dev` to carry `gbps` GB/s of reads (and half of it as writes);
   // negative = back to the util-proportional default. For xGMI link-map tests.
   void set_xgmi(int dev, int link, double gbps);

@@ -16,71 +16,135 @@
 namespace gpumon {
 
 // ---------------------------------------------------------------------------------------------
-// Small persistent fork-join pool for per-device sampling (amdsmi calls are per-device I/O).
+// Per-device sampling workers with a watchdog.
+//
+// Each GPU gets its own thread; a tick hands every idle worker a request and waits until all
+// answer or `device_timeout_s` passes. A device whose call has not returned by then (a hung
+// driver/SMU call) is exported as gpu_up 0 with gpumon_device_timeouts_total incremented, and is not
+// asked again until its call returns -- the other GPUs keep their 1 Hz cadence (the reference
+// stalled the whole node on any slow nvidia-smi, gpu.py:104-116). Workers only touch their own
+// heap state and the backend, so a worker stuck at shutdown can be detached safely (the backend is
+// then deliberately leaked instead of destroyed under it).
 // ---------------------------------------------------------------------------------------------
-struct Exporter::Pool {
-  explicit Pool(int n) {
-    for (int i = 0; i < n; ++i) th.emplace_back([this] { work(); });
-  }
-  ~Pool() {
-    {
-      std::lock_guard<std::mutex> g(mu);
-      quit = true;
-    }
-    cv.notify_all();
-    for (auto& t : th) t.join();
-  }
-  void run(int n, const std::function<void(int)>& fn) {
-    {
-      std::lock_guard<std::mutex> g(mu);
-      job = &fn;
-      total = n;
-      next = 0;
-      done = 0;
-      ++gen;
-    }
-    cv.notify_all();
-    // the caller participates
-    while (true) {
-      int i;
-      {
-        std::lock_guard<std::mutex> g(mu);
-        if (next >= total) break;
-        i = next++;
-      }
-      fn(i);
-      std::lock_guard<std::mutex> g(mu);
-      if (++done == total) done_cv.notify_all();
-    }
-    std::unique_lock<std::mutex> lk(mu);
-    done_cv.wait(lk, [&] { return done >= total; });
-    job = nullptr;
-  }
-  void work() {
-    uint64_t seen = 0;
-    while (true) {
-      std::unique_lock<std::mutex> lk(mu);
-      cv.wait(lk, [&] { return quit || (gen != seen && job && next < total); });
-      if (quit) return;
-      seen = gen;
-      while (job && next < total) {
-        int i = next++;
-        const auto* f = job;
-        lk.unlock();
-        (*f)(i);
-        lk.lock();
-        if (++done == total) done_cv.notify_all();
-      }
-    }
-  }
-  std::vector<std::thread> th;
+struct Exporter::DoneSignal {
   std::mutex mu;
-  std::condition_variable cv, done_cv;
-  const std::function<void(int)>* job = nullptr;
-  int total = 0, next = 0, done = 0;
-  uint64_t gen = 0;
-  bool quit = false;
+  std::condition_variable cv;
 };
+
+struct Exporter::DevWorker {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool quit = false;
+  bool pending = false;          // request posted, not yet picked up
+  bool busy = false;             // request in flight (posted or running)
+  uint64_t req = 0;              // tick id of the current request
+  std::atomic<uint64_t> done{0}; // tick id whose results are stored below
+  bool want_links = false, want_procs = false;
+  int64_t started_ns = 0;
+  DeviceSample sample;
+  std::vector<ProcSample> procs;
+  int64_t proc_ns = 0;
+  std::thread th;
+};
+
+static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_ptr<Exporter::DoneSignal> sig,
+                            Backend* backend, int i) {
+  while (true) {
+    uint64_t id;
+    bool links, procs;
+    {
+      std::unique_lock<std::mutex> lk(w->mu);
+      w->cv.wait(lk, [&] { return w->quit || w->pending; });
+      if (w->quit) return;
+      w->pending = false;
+      id = w->req;
+      links = w->want_links;
+      procs = w->want_procs;
+    }
+    DeviceSample s;
+    std::vector<ProcSample> p;
+    int64_t pns = 0;
+    {
+      TraceRange tr("gpumon.sample_dev");
+      backend->sample(i, &s);
+      if (links) backend->sample_links(i, &s);
+      if (procs && s.ok) {
+        const int64_t t = mono_ns();
+        backend->processes(i, &p);
+        pns = mono_ns() - t;
+      }
+    }
+    {
+      std::lock_guard<std::mutex> g(w->mu);
+      w->sample = std::move(s);
+      w->procs = std::move(p);
+      w->proc_ns = pns;
+      w->busy = false;
+      w->done.store(id, std::memory_order_release);
+      if (w->quit) {
+        std::lock_guard<std::mutex> g2(sig->mu);
+        sig->cv.notify_all();
+        return;
+      }
+    }
+    std::lock_guard<std::mutex> g(sig->mu);
+    sig->cv.notify_all();
+  }
+}
+
+void Exporter::start_workers(int n) {
+  stop_workers();
+  if (!done_sig_) done_sig_ = std::make_shared<DoneSignal>();
+  for (int i = 0; i < n; ++i) {
+    auto w = std::make_shared<DevWorker>();
+    w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i);
+    workers_.push_back(std::move(w));
+  }
+}
+
+// Returns false if a worker was stuck in a device call and had to be detached.
+bool Exporter::stop_workers() {
+  bool clean = true;
+  for (auto& w : workers_) {
+    bool busy;
+    {
+      std::lock_guard<std::mutex> g(w->mu);
+      w->quit = true;
+      busy = w->busy && !w->pending;
+    }
+    w->cv.notify_all();
+    if (busy) {
+      // give an in-flight call a moment to return before giving up on it
+      const int64_t until = mono_ns() + 200'000'000;
+      while (mono_ns() < until) {
+        {
+          std::lock_guard<std::mutex> g(w->mu);
+          if (!w->busy) break;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(5));
+      }
+      std::lock_guard<std::mutex> g(w->mu);
+      busy = w->busy;
+    }
+    if (busy) {
+      GPUMON_LOG(LogLevel::kError, "exporter", "device worker stuck in a backend call at shutdown: detaching it");
+      w->th.detach();
+      clean = false;
+    } else if (w->th.joinable()) {
+      w->th.join();
+    }
+  }
+  workers_.clear();
+  return clean;
+}
+
+bool Exporter::workers_busy() const {
+  for (const auto& w : workers_) {
+    std::lock_guard<std::mutex> g(w->mu);
+    if (w->busy) return true;
+  }
+  return false;
+}
 
 // ---------------------------------------------------------------------------------------------
 static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
@@ -99,6 +163,7 @@ static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
     else if (k == "fail_device") base.fail_device = atoi(v.c_str());
     else if (k == "fail_every") base.fail_every = atoi(v.c_str());
     else if (k == "hang_ms") base.hang_ms = atof(v.c_str());
+    else if (k == "hang_device") base.hang_device = atoi(v.c_str());
     else if (k == "seed") base.seed = strtoull(v.c_str(), nullptr, 10);
     else if (k == "firmware_hz") base.firmware_hz = atof(v.c_str());
     else if (k == "unsupported") base.unsupported = split(v, ';');
@@ -181,14 +246,12 @@ bool Exporter::ensure_backend() {
     cur_.assign(st.size(), DeviceSample{});
     rates_.assign(st.size(), DeviceRates{});
     dev_errors_.assign(st.size(), 0);
+    dev_timeouts_.assign(st.size(), 0);
     proc_counts_.assign(st.size(), 0);
   }
-  // auto: the per-device reads are independent (each waits on its own SMU/KFD), so sample them
-  // concurrently -- the caller thread takes one device, so n devices need n-1 workers.
-  const int nthreads = cfg_.sample_threads >= 0 ? cfg_.sample_threads
-                       : static_cast<int>(st.size()) >= 2 ? std::min<int>(static_cast<int>(st.size()), 8) - 1
-                                                          : 0;
-  if (nthreads > 0 && !pool_) pool_ = std::make_unique<Pool>(nthreads);
+  // One worker per GPU (parallel + watchdog) unless sequential sampling was asked for
+  // (sample_threads 0) or the watchdog is disabled (device_timeout_s <= 0).
+  if (cfg_.sample_threads != 0 && cfg_.device_timeout_s > 0) start_workers(static_cast<int>(st.size()));
   backend_up_ = true;
   GPUMON_LOG(LogLevel::kInfo, "exporter",
              "backend " + backend_->name() + " up with " + std::to_string(st.size()) + " GPU(s)");
@@ -239,7 +302,10 @@ void Exporter::stop() {
   if (pusher_.joinable()) pusher_.join();
   if (server_) server_->stop();
   server_.reset();
-  pool_.reset();
+  if (!stop_workers() && backend_) {
+    // a detached worker is still inside a backend call: never destroy the backend under it
+    (void)backend_.release();
+  }
   if (backend_) backend_->shutdown();
   backend_up_ = false;
 }
@@ -279,27 +345,74 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
   auto links_due = [&](int i) {
     return links_ok && (tk == 0 || (tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(cfg_.link_every) == 0);
   };
-  std::atomic<int64_t> proc_ns{0};
-  // One task per device: metrics table, (links), process list. With a pool the devices run in
-  // parallel (amdsmi calls are per-device sysfs/ioctl I/O).
-  auto one = [&](int i) {
-    TraceRange tr("gpumon.sample_dev");
-    backend_->sample(i, &(*out)[i]);
-    if (links_due(i)) backend_->sample_links(i, &(*out)[i]);
-    if (cfg_.processes && (*out)[i].ok) {
-      int64_t t = mono_ns();
-      backend_->processes(i, &(*procs)[i]);
-      proc_ns += mono_ns() - t;
+  int64_t proc_ns = 0;
+  if (static_cast<int>(workers_.size()) != n) {
+    // sequential: metrics table, (links), process list per device on the sampler thread
+    for (int i = 0; i < n; ++i) {
+      TraceRange tr("gpumon.sample_dev");
+      backend_->sample(i, &(*out)[i]);
+      if (links_due(i)) backend_->sample_links(i, &(*out)[i]);
+      if (cfg_.processes && (*out)[i].ok) {
+        const int64_t t = mono_ns();
+        backend_->processes(i, &(*procs)[i]);
+        proc_ns += mono_ns() - t;
+      }
     }
+    *procs_s = proc_ns * 1e-9;
+    return;
+  }
+  const uint64_t id = ++tick_id_;
+  const int64_t t0 = mono_ns();
+  std::vector<char> asked(n, 0);
+  for (int i = 0; i < n; ++i) {
+    DevWorker& w = *workers_[i];
+    std::lock_guard<std::mutex> g(w.mu);
+    if (w.busy) continue;  // still inside an earlier (hung) call
+    w.busy = w.pending = true;
+    w.req = id;
+    w.want_links = links_due(i);
+    w.want_procs = cfg_.processes;
+    w.started_ns = t0;
+    asked[i] = 1;
+    w.cv.notify_one();
+  }
+  const int64_t deadline = t0 + static_cast<int64_t>(cfg_.device_timeout_s * 1e9);
+  auto all_done = [&] {
+    for (int i = 0; i < n; ++i)
+      if (asked[i] && workers_[i]->done.load(std::memory_order_acquire) != id) return false;
+    return true;
   };
-  struct Acc {
-    std::atomic<int64_t>* p;
-    double* s;
-    ~Acc() { *s = p->load() * 1e-9; }
-  } acc{&proc_ns, procs_s};
-  if (pool_ && n > 1) pool_->run(n, one);
-  else
-    for (int i = 0; i < n; ++i) one(i);
+  {
+    // Waits in <= 20 ms system_clock slices checked against the monotonic deadline: a steady_clock
+    // wait_until compiles to pthread_cond_clockwait, which the toolchain's TSan does not intercept.
+    std::unique_lock<std::mutex> lk(done_sig_->mu);
+    while (!all_done()) {
+      const int64_t left = deadline - mono_ns();
+      if (left <= 0) break;
+      done_sig_->cv.wait_until(lk, std::chrono::system_clock::now() +
+                                       std::chrono::nanoseconds(std::min<int64_t>(left, 20'000'000)));
+    }
+  }
+  for (int i = 0; i < n; ++i) {
+    DevWorker& w = *workers_[i];
+    std::lock_guard<std::mutex> g(w.mu);
+    if (asked[i] && w.done.load(std::memory_order_acquire) == id) {
+      (*out)[i] = std::move(w.sample);
+      (*procs)[i] = std::move(w.procs);
+      proc_ns += w.proc_ns;
+      continue;
+    }
+    DeviceSample& s = (*out)[i];
+    s.reset();
+    s.host_mono_ns = mono_ns();
+    s.host_wall_ns = wall_ns();
+    s.ok = false;
+    s.errors = 1;
+    s.last_error = asked[i] ? "device call exceeded device_timeout_s" : "previous device call still running (hung)";
+    std::lock_guard<std::mutex> g2(state_mu_);
+    if (i < static_cast<int>(dev_timeouts_.size())) dev_timeouts_[i]++;
+  }
+  *procs_s = proc_ns * 1e-9;
 }
 
 void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
@@ -468,7 +581,10 @@ TickInfo Exporter::tick() {
     // Whole-backend failure (driver reload, amdsmi lost its handles): re-initialise with backoff
     // instead of exporting gpu_up 0 forever (the reference crashed and relied on the kubelet).
     all_failed_ticks_ = (n > 0 && info.devices_ok == 0) ? all_failed_ticks_ + 1 : 0;
-    if (cfg_.reinit_after > 0 && all_failed_ticks_ >= cfg_.reinit_after) {
+    if (cfg_.reinit_after > 0 && all_failed_ticks_ >= cfg_.reinit_after && workers_busy()) {
+      // a worker is still inside a (hung) backend call: shutting the backend down under it is
+      // unsafe; keep exporting gpu_up 0 until the call returns.
+    } else if (cfg_.reinit_after > 0 && all_failed_ticks_ >= cfg_.reinit_after) {
       GPUMON_LOG(LogLevel::kWarn, "exporter",
                  "all " + std::to_string(n) + " GPU(s) failed " + std::to_string(all_failed_ticks_) +
                      " ticks in a row: re-initialising the backend");
@@ -763,6 +879,7 @@ SelfStats Exporter::self_stats() const {
   {
     std::lock_guard<std::mutex> g(state_mu_);
     s.device_errors = dev_errors_;
+    s.device_timeouts = dev_timeouts_;
     s.pods_attributed = rows_.size();
   }
   return s;

@@ -61,6 +61,7 @@ struct ExporterConfig {
   double init_retry_s = 5.0;
   double health_stale_s = 0;          // 0 = max(3*interval, 10 s)
   int reinit_after = 5;               // consecutive all-devices-failed ticks before re-initialising
+  double device_timeout_s = 2.0;      // a device call still running after this is exported as hung
   std::string version = "0.1.0";
 };
 
@@ -77,6 +78,9 @@ struct TickInfo {
 
 class Exporter {
  public:
+  struct DevWorker;   // one sampling thread per GPU (exporter.cpp)
+  struct DoneSignal;
+
   explicit Exporter(ExporterConfig cfg);
   ~Exporter();
 
@@ -185,9 +189,14 @@ class Exporter {
   std::deque<std::string> push_q_;
   std::atomic<uint64_t> influx_ok_{0}, influx_fail_{0}, influx_dropped_{0};
 
-  // parallel sampling pool
-  struct Pool;
-  std::unique_ptr<Pool> pool_;
+  // per-device sampling workers + watchdog (exporter.cpp)
+  void start_workers(int n);
+  bool stop_workers();
+  bool workers_busy() const;
+  std::vector<std::shared_ptr<DevWorker>> workers_;
+  std::shared_ptr<DoneSignal> done_sig_;
+  uint64_t tick_id_ = 0;
+  std::vector<uint64_t> dev_timeouts_;  // guarded by state_mu_
 };
 
 // "auto": amdsmi if it initialises, else error (never silently mock on a GPU host);

@@ -100,9 +100,10 @@ void MockBackend::set_xgmi(int dev, int link, double gbps) {
   if (k < forced_xgmi_.size()) forced_xgmi_[k] = gbps < 0 ? kNaN : gbps;
 }
 
-void MockBackend::set_hang_ms(double ms) {
+void MockBackend::set_hang_ms(double ms, int dev) {
   std::lock_guard<std::mutex> g(mu_);
   cfg_.hang_ms = ms;
+  cfg_.hang_device = dev;
 }
 uint64_t MockBackend::calls(int dev) const {
   std::lock_guard<std::mutex> g(mu_);
@@ -123,7 +124,7 @@ void MockBackend::sample(int i, DeviceSample* out) {
   double hang;
   {
     std::lock_guard<std::mutex> g(mu_);
-    hang = cfg_.hang_ms;
+    hang = (cfg_.hang_device < 0 || cfg_.hang_device == devs_[i].hip_id) ? cfg_.hang_ms : 0.0;
   }
   if (hang > 0) std::this_thread::sleep_for(std::chrono::microseconds(static_cast<int64_t>(hang * 1000)));
   std::lock_guard<std::mutex> g(mu_);

@@ -601,6 +601,13 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       for (size_t d = 0; d < s.device_errors.size() && d < n; ++d)
         f.add(dl[d], static_cast<double>(s.device_errors[d]));
     }
+    {
+      Family f(o, "gpumon_device_timeouts_total",
+               "Ticks in which a GPU's backend call exceeded device_timeout_s (hung call; exported as gpu_up 0).",
+               "counter");
+      for (size_t d = 0; d < s.device_timeouts.size() && d < n; ++d)
+        f.add(dl[d], static_cast<double>(s.device_timeouts[d]));
+    }
     histogram(o, "gpumon_sample_duration_seconds",
               "Time to sample all GPUs, attribute processes and render one tick.", s.sample_hist, hl);
     histogram(o, "gpumon_scrape_duration_seconds",

@@ -75,6 +75,7 @@ struct SelfStats {
   double cpu_seconds = -1, rss_bytes = -1, start_time_s = -1;
   int threads = -1, open_fds = -1;
   std::vector<uint64_t> device_errors;  // per device
+  std::vector<uint64_t> device_timeouts;  // per device: hung calls caught by the watchdog
 };
 
 // Values supplied from outside the sampler (probe kernel, PMC device counting, plugins).

@@ -164,3 +164,53 @@ def test_device_filter(core):
     st = ex.statics()
     ex.stop()
     assert [s["gpu_id"] for s in st] == ["1", "3"]
+
+
+def test_hung_device_is_isolated_by_the_watchdog(core):
+    """A device whose backend call hangs is exported as gpu_up 0 after device_timeout_s while the
+    other GPUs keep their cadence; the hung call is not re-issued until it returns."""
+    ex = core.Exporter({"backend": "mock:gpus=3", "serve_http": False, "interval_s": 0,
+                        "device_timeout_s": 0.2})
+    ex.start()
+    try:
+        ex.mock_set_hang_ms(1500, 1)
+        t0 = time.monotonic()
+        info = ex.tick()
+        dt = time.monotonic() - t0
+        assert 0.15 < dt < 0.6, dt
+        assert info["devices_ok"] == 2
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpu_up", gpu_id="1") == 0
+        assert promtext.one(fam, "gpu_up", gpu_id="0") == 1
+        assert promtext.one(fam, "gpumon_device_timeouts_total", gpu_id="1") == 1
+        # the next tick does not wait for the still-running call at all
+        t0 = time.monotonic()
+        ex.tick()
+        assert time.monotonic() - t0 < 0.15
+        assert ex.self_stats()["device_timeouts"][1] == 2
+        ex.mock_set_hang_ms(0)
+        time.sleep(1.6)  # the hung call returns
+        ex.tick()
+        assert promtext.one(promtext.parse(ex.metrics_text()), "gpu_up", gpu_id="1") == 1
+    finally:
+        ex.mock_set_hang_ms(0)
+        ex.stop()
+
+
+def test_stop_with_a_hung_call_does_not_block(core):
+    ex = core.Exporter({"backend": "mock:gpus=2", "serve_http": False, "interval_s": 0,
+                        "device_timeout_s": 0.1})
+    ex.start()
+    ex.mock_set_hang_ms(3000, 0)
+    ex.tick()
+    t0 = time.monotonic()
+    ex.stop()  # the worker stuck in the call is detached, the backend is kept alive for it
+    assert time.monotonic() - t0 < 1.0
+
+
+def test_sequential_mode_has_no_workers(core):
+    ex = core.Exporter({"backend": "mock:gpus=2", "serve_http": False, "interval_s": 0, "sample_threads": 0})
+    ex.start()
+    info = ex.tick()
+    ex.stop()
+    assert info["devices_ok"] == 2
