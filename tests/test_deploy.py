@@ -110,3 +110,36 @@ def test_dockerfile_entrypoint():
     assert 'ENTRYPOINT ["python3", "-m", "gpumon", "serve"]' in txt
     assert "libltdl" not in txt.split("\n", 5)[-1] or "no vendored" in txt
     assert "EXPOSE 9400" in txt
+
+
+def test_alert_and_recording_rules_resolve(mock_exporter):
+    """Every series a PrometheusRule expression uses is produced by the exporter, and the label
+    values the alerts match on (sensor, kind, state) exist in a scrape."""
+    (rule,) = _docs("deploy/k8s/gpumon-alerts.yaml")
+    assert rule["apiVersion"] == "monitoring.coreos.com/v1" and rule["kind"] == "PrometheusRule"
+    ex = mock_exporter(backend="mock:gpus=2,mode=load")
+    ex.set_allocations([{"pod_namespace": "ml", "pod_name": "p-0", "container_name": "c", "gpu_index": 0}])
+    ex.mock_set_procs([{"pid": os.getpid(), "device": 1, "name": "python3"}])
+    ex.tick()
+    import time
+
+    time.sleep(0.05)
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    produced = {n for f, v in fam.items() for n in [f] + [s[0] for s in v["samples"]]}
+    words = {"sum", "by", "count", "rate", "increase", "avg", "max", "time", "host", "namespace", "podname",
+             "user_name"}
+    exprs = [r["expr"] for g in rule["spec"]["groups"] for r in g["rules"]]
+    assert len(exprs) >= 12
+    for e in exprs:
+        for name in re.findall(r"\b([a-z_][a-z0-9_]*)\s*[{(\[]", e) + re.findall(r"\b(gpu[a-z0-9_]*|pod_gpu[a-z0-9_]*|node_gpu[a-z0-9_]*)\b", e):
+            if name in words:
+                continue
+            assert name in produced, (e, name)
+    label_values = {(k, v) for f in fam.values() for _, labels, _ in f["samples"] for k, v in labels.items()}
+    for k, v in [("sensor", "hotspot"), ("sensor", "mem"), ("kind", "socket_thermal"), ("kind", "hbm_thermal"),
+                 ("kind", "vr_thermal"), ("state", "idle")]:
+        assert (k, v) in label_values, (k, v)
+    kust = _docs("deploy/k8s/kustomization.yaml")[0]
+    for r in kust["resources"]:
+        assert os.path.exists(os.path.join(ROOT, "deploy/k8s", r)), r

@@ -2,7 +2,7 @@
 # Burn shapes after splitting the 16x16x32 burn into its own VGPR-form TU; PMC on the default load;
 # GPU tests; 1 Hz bench.
 set -o pipefail
-out=gpurun_out/r10
+out=gpurun_out/${ROUND_TAG:-r10}
 mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 120 python3 tools/burn_shapes.py > $out/burn_shapes.json 2> $out/burn.err || exit 1
