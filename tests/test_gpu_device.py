@@ -277,3 +277,27 @@ def test_sysfs_fast_path_matches_amdsmi(core, torch_gpu):
         assert ex.samples()[0]["ok"]
     finally:
         ex.stop()
+
+
+def test_exported_activity_tracks_duty_cycle(core, torch_gpu):
+    """A 50 % duty bf16 burn must read ~50 % in gpu_gfx_activity_avg_percent (firmware accumulator
+    average over the tick interval) -- profiles/r1_duty_calibration.md: within 1.1 points."""
+    from gpumon.ops.load import SyntheticLoad
+
+    ex = _exporter(core)
+    try:
+        with SyntheticLoad(0, "mfma", duty=0.5, mfma_iters=2048) as load:
+            time.sleep(1.0)
+            ex.tick()
+            s0, t0 = load.stats(), time.monotonic()
+            acts = []
+            for _ in range(4):
+                time.sleep(0.5)
+                ex.tick()
+                acts.append(ex.rates()[0]["gfx_activity_avg_pct"])
+            busy = (load.stats()["busy_s"] - s0["busy_s"]) / (time.monotonic() - t0) * 100
+        got = sum(acts) / len(acts)
+        assert 30 < busy < 70, busy
+        assert abs(got - busy) < 8, (got, busy, acts)
+    finally:
+        ex.stop()
