@@ -1,0 +1,92 @@
+#!/usr/bin/env python3
+"""Soak test: the exporter at 10 Hz on the real GPU under the mixed MFMA/HBM load with a
+continuous scraper, for --minutes. Every 30 s: RSS, open fds, threads, ticks, overruns, errors,
+scrape p99 over the last window. A leak or a slow drift shows up as a trend. One progress line per
+window on stdout; the final JSON summary is the last line.
+"""
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def proc_stats():
+    rss = 0
+    with open("/proc/self/status") as f:
+        for l in f:
+            if l.startswith("VmRSS:"):
+                rss = int(l.split()[1]) * 1024
+    return {"rss_mb": round(rss / 2 ** 20, 1), "fds": len(os.listdir("/proc/self/fd")),
+            "threads": len(os.listdir("/proc/self/task"))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--minutes", type=float, default=10.0)
+    ap.add_argument("--interval", type=float, default=0.1)
+    ap.add_argument("--scrape-rate", type=float, default=50.0)
+    ap.add_argument("--backend", default="amdsmi")
+    ap.add_argument("--window", type=float, default=30.0)
+    a = ap.parse_args()
+
+    from gpumon import core as _core
+    from gpumon.config import Config
+    from gpumon.monitor import GpuMonitor
+
+    core = _core()
+    load = None
+    if a.backend.startswith("amdsmi"):
+        from gpumon.ops.load import SyntheticLoad
+
+        load = SyntheticLoad(0, "mixed").start()
+    cfg = Config(backend=a.backend, devices=[0] if a.backend.startswith("amdsmi") else [], interval=a.interval,
+                 listen="127.0.0.1:0", log_level="warn")
+    mon = GpuMonitor(cfg, control_plane=False).start()
+    windows = []
+    end = time.monotonic() + a.minutes * 60
+    base = proc_stats()
+    while time.monotonic() < end:
+        res = {}
+
+        def scrape():
+            res.update(core.scrape_load("127.0.0.1", mon.port, "/metrics", n_requests=0, duration_s=a.window,
+                                        concurrency=2, rate_hz=a.scrape_rate, keep_alive=True, gzip=True))
+
+        th = threading.Thread(target=scrape)
+        th.start()
+        th.join()
+        st = mon.ex.self_stats()
+        lat = sorted(res.get("latencies_s", []))
+        w = dict(proc_stats(), t_min=round((a.minutes * 60 - (end - time.monotonic())) / 60, 2),
+                 ticks=st["ticks"], overruns=st["overruns"], stale=st["stale_samples"],
+                 errors=sum(st.get("device_errors", [])), timeouts=sum(st.get("device_timeouts", [])),
+                 scrapes=len(lat), scrape_errors=res.get("errors", 0),
+                 scrape_p99_ms=round(lat[int(0.99 * (len(lat) - 1))] * 1e3, 3) if lat else None)
+        windows.append(w)
+        print(json.dumps(w), flush=True)
+    mon.stop()
+    if load:
+        lst = load.stats()
+        load.stop()
+    else:
+        lst = {}
+    first, last = windows[0], windows[-1]
+    summary = {"minutes": a.minutes, "interval_s": a.interval, "windows": len(windows),
+               "rss_mb_start": first["rss_mb"], "rss_mb_end": last["rss_mb"],
+               "rss_mb_growth_after_first_window": round(last["rss_mb"] - first["rss_mb"], 1),
+               "fds_start": first["fds"], "fds_end": last["fds"], "threads_end": last["threads"],
+               "ticks": last["ticks"], "overruns": last["overruns"], "device_errors": last["errors"],
+               "scrapes": sum(w["scrapes"] for w in windows), "scrape_errors": sum(w["scrape_errors"] for w in windows),
+               "scrape_p99_ms_max_window": max(w["scrape_p99_ms"] or 0 for w in windows),
+               "load_tflops": round(lst.get("tflops", 0.0), 1), "load_tbps": round(lst.get("tbps", 0.0), 3),
+               "baseline_before_start": base}
+    print(json.dumps(summary), flush=True)
+
+
+if __name__ == "__main__":
+    main()
