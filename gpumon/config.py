@@ -38,7 +38,11 @@ class Config:
     interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
     processes: bool = True
     link_every: int = 30
-    sample_threads: int = -1              # -1 = auto (parallel per GPU when >= 2 GPUs)
+    sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
+    device_timeout_s: float = 2.0         # a device call still running after this is exported as hung
+    reinit_after: int = 5                 # ticks with every GPU failing before the backend is re-initialised
+    init_retry_s: float = 5.0             # backoff between backend init attempts
+    health_stale_s: float = 0.0           # /healthz 503 after this long without a tick (0 = max(3*interval, 10 s))
     # exposition
     listen: str = "0.0.0.0:9400"
     http_threads: int = 2
@@ -103,6 +107,10 @@ class Config:
             "processes": self.processes,
             "link_every": int(self.link_every),
             "sample_threads": int(self.sample_threads),
+            "device_timeout_s": float(self.device_timeout_s),
+            "reinit_after": int(self.reinit_after),
+            "init_retry_s": float(self.init_retry_s),
+            "health_stale_s": float(self.health_stale_s),
             "listen_addr": self.listen_addr,
             "port": self.port,
             "http_threads": int(self.http_threads),
@@ -212,6 +220,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--no-processes", dest="processes", action="store_false", default=None)
     p.add_argument("--no-gzip", dest="gzip", action="store_false", default=None)
     p.add_argument("--sample-threads", dest="sample_threads", type=int)
+    p.add_argument("--device-timeout", dest="device_timeout_s", type=float,
+                   help="seconds before a device call is exported as hung (gpu_up 0)")
     p.add_argument("--enable-probe-kernel", dest="enable_probe", action="store_true", default=None)
     p.add_argument("--enable-pmc", dest="enable_pmc", action="store_true", default=None)
     p.add_argument("--no-fast-path", dest="fast_path", action="store_false", default=None,

@@ -87,3 +87,14 @@ def test_metrics_doc_is_current():
     r = subprocess.run([sys.executable, os.path.join(root, "tools/gen_metrics_doc.py"), "--check"],
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, "docs/metrics.md is stale: run python tools/gen_metrics_doc.py"
+
+
+def test_configuration_doc_is_current():
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("gen_config_doc", os.path.join(root, "tools/gen_config_doc.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    with open(os.path.join(root, "docs/configuration.md")) as fh:
+        assert fh.read() == mod.render(), "docs/configuration.md is stale: run python tools/gen_config_doc.py"
