@@ -31,6 +31,8 @@ UID = "1b4e28ba-2fa1-11d2-883f-0016d3cca427"
     # plain docker (no k8s)
     (f"0::/system.slice/docker-{CID}.scope\n", "docker", CID, "", ""),
     (f"13:name=systemd:/docker/{CID}\n", "docker", CID, "", ""),
+    # podman (rootful, systemd cgroup manager)
+    (f"0::/machine.slice/libpod-{CID}.scope/container\n", "podman", CID, "", ""),
 ])
 def test_parse_cgroup_formats(core, text, runtime, cid, uid, qos):
     r = core.parse_cgroup(text)
