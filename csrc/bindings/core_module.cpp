@@ -10,6 +10,7 @@
 #include "../core/backend.h"
 #include "../core/common.h"
 #include "../core/exporter.h"
+#include "../core/grpc_lite.h"
 #include "../core/http_client.h"
 #include "../core/render.h"
 #include "../core/snapshot.h"
@@ -66,6 +67,9 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "health_stale_s", &c.health_stale_s);
   get(d, "reinit_after", &c.reinit_after);
   get(d, "device_timeout_s", &c.device_timeout_s);
+  get(d, "pod_resources_socket", &c.pod_resources_socket);
+  get(d, "pod_resources_prefix", &c.pod_resources_prefix);
+  get(d, "pod_resources_refresh_s", &c.pod_resources_refresh_s);
   get(d, "version", &c.version);
   get(d, "activity_acc_scale", &c.rates.activity_acc_scale);
   get(d, "xgmi_kb_bytes", &c.rates.xgmi_kb_bytes);
@@ -277,6 +281,43 @@ PYBIND11_MODULE(_core, m) {
       },
       py::arg("lib") = "", py::arg("sys_root") = "/sys", py::arg("dev") = 0,
       "libamd_smi vs sysfs-decoded gpu_metrics v1.8, field by field: (name, amdsmi, sysfs)");
+  m.def(
+      "podresources_list",
+      [](const std::string& sock, const std::string& prefix, int timeout_ms) {
+        std::vector<PodDeviceRow> rows;
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = podresources_list(sock, prefix, &rows, &err, timeout_ms);
+        }
+        if (!ok) throw std::runtime_error(err);
+        py::list l;
+        for (const auto& r : rows) {
+          py::dict d;
+          d["namespace"] = r.pod_namespace;
+          d["pod"] = r.pod_name;
+          d["container"] = r.container_name;
+          d["resource"] = r.resource_name;
+          d["device_id"] = r.device_id;
+          l.append(d);
+        }
+        return l;
+      },
+      py::arg("socket"), py::arg("resource_prefix") = "amd.com/gpu", py::arg("timeout_ms") = 3000,
+      "kubelet PodResources List() through the native HTTP/2 client (grpc_lite.cpp)");
+  m.def(
+      "parse_list_pod_resources",
+      [](py::bytes b, const std::string& prefix) {
+        std::vector<PodDeviceRow> rows;
+        std::string s = b;
+        if (!parse_list_pod_resources(s, prefix, &rows)) throw std::runtime_error("malformed");
+        py::list l;
+        for (const auto& r : rows)
+          l.append(py::make_tuple(r.pod_namespace, r.pod_name, r.container_name, r.resource_name, r.device_id));
+        return l;
+      },
+      py::arg("data"), py::arg("resource_prefix") = "");
   m.def("roctx_enable", &Roctx::enable, py::arg("on") = true,
         "Load librocprofiler-sdk-roctx and bracket sampler phases with ROCTx ranges");
   m.def("roctx_active", &Roctx::active);

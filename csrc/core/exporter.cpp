@@ -10,6 +10,7 @@
 #include <functional>
 
 #include "common.h"
+#include "grpc_lite.h"
 #include "http_client.h"
 #include "trace.h"
 
@@ -291,6 +292,10 @@ bool Exporter::start(std::string* err) {
   tick();
   if (cfg_.interval_s > 0) sampler_ = std::thread([this] { sampler_loop(); });
   if (!cfg_.influx_url.empty()) pusher_ = std::thread([this] { influx_loop(); });
+  if (!cfg_.pod_resources_socket.empty()) {
+    podres_poll_once();  // allocations known before the first scrape
+    podres_ = std::thread([this] { podres_loop(); });
+  }
   return true;
 }
 
@@ -300,6 +305,8 @@ void Exporter::stop() {
   push_cv_.notify_all();
   if (sampler_.joinable()) sampler_.join();
   if (pusher_.joinable()) pusher_.join();
+  podres_cv_.notify_all();
+  if (podres_.joinable()) podres_.join();
   if (server_) server_->stop();
   server_.reset();
   if (!stop_workers() && backend_) {
@@ -883,6 +890,93 @@ SelfStats Exporter::self_stats() const {
     s.pods_attributed = rows_.size();
   }
   return s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Native PodResources poller (standalone binary): kubelet List() -> Allocation table.
+// ---------------------------------------------------------------------------------------------
+namespace {
+std::string lower(std::string s) {
+  for (auto& c : s) c = static_cast<char>(tolower(static_cast<unsigned char>(c)));
+  return s;
+}
+}  // namespace
+
+// Device-plugin device ID -> exporter device index (-1 unknown). The AMD device plugin uses PCI
+// addresses; UUIDs, hip ids and DRM node names are accepted too (gpumon/attribution/plane.py).
+int match_device_id(const std::string& raw, const std::vector<DeviceStatic>& st) {
+  const std::string d = lower(std::string(trim(raw)));
+  if (d.empty()) return -1;
+  for (const auto& s : st) {
+    const std::string bdf = lower(s.bdf);
+    if (!bdf.empty()) {
+      if (d == bdf) return s.index;
+      if (d.find(':') != std::string::npos && ends_with(bdf, d)) return s.index;  // without domain
+    }
+    const std::string uuid = lower(s.uuid);
+    if (!uuid.empty() && (d == uuid || d == "gpu-" + uuid)) return s.index;
+  }
+  for (const auto& s : st) {
+    const bool digits = std::all_of(d.begin(), d.end(), [](char c) { return c >= '0' && c <= '9'; });
+    if (digits && std::to_string(s.hip_id) == d) return s.index;
+    if (starts_with(d, "card") && d.substr(4) == std::to_string(s.drm_card)) return s.index;
+    if (starts_with(d, "renderd") && d.substr(7) == std::to_string(s.drm_render)) return s.index;
+  }
+  return -1;
+}
+
+bool Exporter::podres_poll_once() {
+  std::vector<PodDeviceRow> rows;
+  std::string err;
+  const int64_t t0 = mono_ns();
+  const bool ok = podresources_list(cfg_.pod_resources_socket, cfg_.pod_resources_prefix, &rows, &err, 3000);
+  const double dt = (mono_ns() - t0) * 1e-9;
+  std::vector<DeviceStatic> st;
+  {
+    std::lock_guard<std::mutex> g(state_mu_);
+    st = statics_;
+  }
+  size_t unknown = 0;
+  if (ok) {
+    std::vector<Allocation> allocs;
+    for (const auto& r : rows) {
+      const int idx = match_device_id(r.device_id, st);
+      if (idx < 0) {
+        unknown++;  // Q5: the reference emitted gpu_id=None for these (gpu.py:226)
+        continue;
+      }
+      Allocation a;
+      a.pod_namespace = r.pod_namespace;
+      a.pod_name = r.pod_name;
+      a.container_name = r.container_name;
+      a.gpu_index = idx;
+      allocs.push_back(std::move(a));
+    }
+    attr_->set_allocations(std::move(allocs));
+  } else {
+    GPUMON_LOG(LogLevel::kWarn, "podresources", "List() failed: " + err);
+  }
+  std::vector<ExtraSeries> ex;
+  ex.push_back({"gpumon_podresources_up", "1 if the last kubelet PodResources List() succeeded.", "gauge", -1, {},
+                ok ? 1.0 : 0.0});
+  ex.push_back({"gpumon_podresources_unknown_devices", "Allocated device IDs that match no local GPU.", "gauge",
+                -1, {}, static_cast<double>(unknown)});
+  ex.push_back({"gpumon_podresources_list_seconds", "Duration of the last PodResources List() call.", "gauge", -1,
+                {}, dt});
+  set_extra("podresources_native", std::move(ex));
+  return ok;
+}
+
+void Exporter::podres_loop() {
+  std::unique_lock<std::mutex> lk(podres_mu_);
+  while (running_) {
+    podres_cv_.wait_for(lk, std::chrono::duration<double>(std::max(0.5, cfg_.pod_resources_refresh_s)),
+                        [&] { return !running_.load(); });
+    if (!running_) break;
+    lk.unlock();
+    podres_poll_once();
+    lk.lock();
+  }
 }
 
 }  // namespace gpumon

@@ -62,6 +62,11 @@ struct ExporterConfig {
   double health_stale_s = 0;          // 0 = max(3*interval, 10 s)
   int reinit_after = 5;               // consecutive all-devices-failed ticks before re-initialising
   double device_timeout_s = 2.0;      // a device call still running after this is exported as hung
+  // Native kubelet PodResources poller (grpc_lite.cpp) for the standalone binary; the Python
+  // control plane (gpumon/attribution) leaves this empty and pushes allocations itself.
+  std::string pod_resources_socket;
+  std::string pod_resources_prefix = "amd.com/gpu";
+  double pod_resources_refresh_s = 10.0;
   std::string version = "0.1.0";
 };
 
@@ -116,6 +121,8 @@ class Exporter {
  private:
   void sampler_loop();
   void influx_loop();
+  void podres_loop();
+  bool podres_poll_once();
   bool ensure_backend();
   void handle_http(const HttpRequest& req, HttpResponse* resp);
   void sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
@@ -184,6 +191,9 @@ class Exporter {
 
   // Influx pusher
   std::thread pusher_;
+  std::thread podres_;
+  std::mutex podres_mu_;
+  std::condition_variable podres_cv_;
   std::mutex push_mu_;
   std::condition_variable push_cv_;
   std::deque<std::string> push_q_;
@@ -202,5 +212,8 @@ class Exporter {
 // "auto": amdsmi if it initialises, else error (never silently mock on a GPU host);
 // "mock" / "mock:gpus=8" etc.
 std::unique_ptr<Backend> make_backend_from_config(const ExporterConfig& cfg, std::string* err);
+
+// Device-plugin device ID (PCI address, UUID, hip id, cardN, renderDN) -> device index, -1 unknown.
+int match_device_id(const std::string& id, const std::vector<DeviceStatic>& statics);
 
 }  // namespace gpumon

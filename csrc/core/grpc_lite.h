@@ -1,0 +1,53 @@
+// Minimal unary gRPC client over HTTP/2 cleartext on a unix socket, plus a protobuf wire reader.
+//
+// Enough for the kubelet PodResources API (/var/lib/kubelet/pod-resources/kubelet.sock) so the
+// standalone native exporter (bin/gpumon-exporter) can attribute idle GPU allocations without the
+// Python control plane or a gRPC library. The reference got the same information by `docker exec`
+// into every opted-in container and running `nvidia-smi -L` there (gpu.py:220-253).
+//
+// HTTP/2 subset: prior-knowledge preface, SETTINGS (+ACK), PING ACK, one request stream with
+// HPACK literal (never-indexed, non-Huffman) request headers, a 16 MiB receive window so large
+// responses need no WINDOW_UPDATE round-trips, DATA reassembly, RST_STREAM/GOAWAY as errors.
+// Response headers are not decoded (HPACK/Huffman): a call succeeds iff a complete gRPC message
+// arrives on the stream before it ends.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace gpumon {
+
+// Unary call: `path` like "/v1.PodResourcesLister/List", `request` = serialized protobuf.
+bool grpc_unary_unix(const std::string& socket_path, const std::string& path, const std::string& request,
+                     std::string* response, std::string* err, int timeout_ms = 3000);
+
+// Protobuf wire-format reader (varint / length-delimited; fixed32/64 skipped).
+class PbReader {
+ public:
+  explicit PbReader(std::string_view b) : b_(b) {}
+  // Next field; false at end or on malformed input (then ok() is false).
+  bool next(uint32_t* field, uint32_t* wire);
+  bool varint(uint64_t* v);
+  bool bytes(std::string_view* v);
+  bool skip(uint32_t wire);
+  bool ok() const { return ok_; }
+
+ private:
+  std::string_view b_;
+  size_t p_ = 0;
+  bool ok_ = true;
+};
+
+// kubelet PodResources v1: every (pod, container, resource, device id) of `resource_prefix`
+// resources (e.g. "amd.com/gpu").
+struct PodDeviceRow {
+  std::string pod_namespace, pod_name, container_name, resource_name, device_id;
+};
+bool podresources_list(const std::string& socket_path, const std::string& resource_prefix,
+                       std::vector<PodDeviceRow>* out, std::string* err, int timeout_ms = 3000);
+bool parse_list_pod_resources(std::string_view msg, const std::string& resource_prefix,
+                              std::vector<PodDeviceRow>* out);
+
+}  // namespace gpumon

@@ -31,6 +31,7 @@ static void usage() {
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--procfs /proc] [--no-processes] [--no-gzip] [--sample-threads N]\n"
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx] [--once]\n"
+          "                       [--pod-resources SOCKET | --no-pod-resources]\n"
           "env: NODE_NAME, INFLUXDB_URL, GPUMON_LISTEN, GPUMON_INTERVAL, GPUMON_BACKEND\n");
 }
 
@@ -42,6 +43,8 @@ int main(int argc, char** argv) {
   if (const char* v = getenv("GPUMON_INTERVAL")) cfg.interval_s = atof(v);
   std::string listen = getenv("GPUMON_LISTEN") ? getenv("GPUMON_LISTEN") : "0.0.0.0:9400";
   bool once = false;
+  // kubelet PodResources: on by default when the socket is mounted (deploy/k8s DaemonSet)
+  std::string podres = "/var/lib/kubelet/pod-resources/kubelet.sock";
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -64,6 +67,8 @@ int main(int argc, char** argv) {
     else if (a == "--no-fast-path") cfg.fast_path = false;
     else if (a == "--sysfs") cfg.sysfs_root = next();
     else if (a == "--roctx") cfg.roctx = true;
+    else if (a == "--pod-resources") podres = next();
+    else if (a == "--no-pod-resources") podres = "";
     else if (a == "--opt-in-label") cfg.attribution.opt_in = next();
     else if (a == "--user-regex") cfg.attribution.user_regex = next();
     else if (a == "--user-label") cfg.attribution.user_label = next();
@@ -89,6 +94,7 @@ int main(int argc, char** argv) {
   cfg.listen_addr = colon == std::string::npos ? "0.0.0.0" : listen.substr(0, colon);
   cfg.port = atoi(colon == std::string::npos ? listen.c_str() : listen.c_str() + colon + 1);
   if (cfg.host.empty()) cfg.host = "no_name";
+  if (!podres.empty() && access(podres.c_str(), F_OK) == 0) cfg.pod_resources_socket = podres;
 
   if (once) {
     cfg.serve_http = false;
