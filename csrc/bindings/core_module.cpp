@@ -70,6 +70,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "pod_resources_socket", &c.pod_resources_socket);
   get(d, "pod_resources_prefix", &c.pod_resources_prefix);
   get(d, "pod_resources_refresh_s", &c.pod_resources_refresh_s);
+  get(d, "cri_socket", &c.cri_socket);
   get(d, "version", &c.version);
   get(d, "activity_acc_scale", &c.rates.activity_acc_scale);
   get(d, "xgmi_kb_bytes", &c.rates.xgmi_kb_bytes);
@@ -306,6 +307,41 @@ PYBIND11_MODULE(_core, m) {
       },
       py::arg("socket"), py::arg("resource_prefix") = "amd.com/gpu", py::arg("timeout_ms") = 3000,
       "kubelet PodResources List() through the native HTTP/2 client (grpc_lite.cpp)");
+  m.def(
+      "cri_list",
+      [](const std::string& sock, int timeout_ms) {
+        std::vector<CriContainer> cs;
+        std::vector<CriSandbox> sbs;
+        std::string err;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = cri_list(sock, &cs, &sbs, &err, timeout_ms);
+        }
+        if (!ok) throw std::runtime_error(err);
+        py::list lc, ls;
+        for (const auto& c : cs) {
+          py::dict d;
+          d["id"] = c.id;
+          d["sandbox_id"] = c.sandbox_id;
+          d["name"] = c.name;
+          d["labels"] = c.labels;
+          d["annotations"] = c.annotations;
+          lc.append(d);
+        }
+        for (const auto& s : sbs) {
+          py::dict d;
+          d["id"] = s.id;
+          d["name"] = s.name;
+          d["uid"] = s.uid;
+          d["namespace"] = s.pod_namespace;
+          d["labels"] = s.labels;
+          d["annotations"] = s.annotations;
+          ls.append(d);
+        }
+        return py::make_tuple(lc, ls);
+      },
+      py::arg("socket"), py::arg("timeout_ms") = 3000, "CRI ListContainers + ListPodSandbox via grpc_lite.cpp");
   m.def(
       "parse_list_pod_resources",
       [](py::bytes b, const std::string& prefix) {

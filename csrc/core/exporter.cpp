@@ -292,8 +292,10 @@ bool Exporter::start(std::string* err) {
   tick();
   if (cfg_.interval_s > 0) sampler_ = std::thread([this] { sampler_loop(); });
   if (!cfg_.influx_url.empty()) pusher_ = std::thread([this] { influx_loop(); });
-  if (!cfg_.pod_resources_socket.empty()) {
-    podres_poll_once();  // allocations known before the first scrape
+  if (!cfg_.pod_resources_socket.empty() || !cfg_.cri_socket.empty()) {
+    // metadata and allocations known before the first scrape
+    if (!cfg_.cri_socket.empty()) cri_poll_once();
+    if (!cfg_.pod_resources_socket.empty()) podres_poll_once();
     podres_ = std::thread([this] { podres_loop(); });
   }
   return true;
@@ -950,6 +952,16 @@ bool Exporter::podres_poll_once() {
       a.pod_name = r.pod_name;
       a.container_name = r.container_name;
       a.gpu_index = idx;
+      {
+        // enrich from CRI (container id, pod uid, labels for the opt-in gate and user label)
+        std::lock_guard<std::mutex> g(podres_mu_);
+        const auto it = native_meta_.find(r.pod_namespace + "/" + r.pod_name + "/" + r.container_name);
+        if (it != native_meta_.end()) {
+          a.container_id = it->second.container_id;
+          a.pod_uid = it->second.pod_uid;
+          a.labels = it->second.labels;
+        }
+      }
       allocs.push_back(std::move(a));
     }
     attr_->set_allocations(std::move(allocs));
@@ -974,9 +986,65 @@ void Exporter::podres_loop() {
                         [&] { return !running_.load(); });
     if (!running_) break;
     lk.unlock();
-    podres_poll_once();
+    if (!cfg_.cri_socket.empty()) cri_poll_once();
+    if (!cfg_.pod_resources_socket.empty()) podres_poll_once();
     lk.lock();
   }
+}
+
+// CRI containers + sandboxes -> ContainerMeta (same merge as gpumon/attribution/plane.py: pod
+// annotations < pod labels < container annotations < container labels).
+bool Exporter::cri_poll_once() {
+  std::vector<CriContainer> cs;
+  std::vector<CriSandbox> sbs;
+  std::string err;
+  const int64_t t0 = mono_ns();
+  const bool ok = cri_list(cfg_.cri_socket, &cs, &sbs, &err, 3000);
+  const double dt = (mono_ns() - t0) * 1e-9;
+  if (ok) {
+    std::unordered_map<std::string, const CriSandbox*> by_id;
+    for (const auto& s : sbs) by_id[s.id] = &s;
+    std::vector<ContainerMeta> metas;
+    metas.reserve(cs.size());
+    for (const auto& c : cs) {
+      const auto it = by_id.find(c.sandbox_id);
+      const CriSandbox* sb = it == by_id.end() ? nullptr : it->second;
+      ContainerMeta m;
+      m.container_id = c.id;
+      if (sb) {
+        m.labels.insert(sb->annotations.begin(), sb->annotations.end());
+        for (const auto& kv : sb->labels) m.labels[kv.first] = kv.second;
+      }
+      for (const auto& kv : c.annotations) m.labels[kv.first] = kv.second;
+      for (const auto& kv : c.labels) m.labels[kv.first] = kv.second;
+      auto lab = [&](const char* k, const std::string& dflt) {
+        const auto l = c.labels.find(k);
+        return l != c.labels.end() && !l->second.empty() ? l->second : dflt;
+      };
+      m.container_name = lab("io.kubernetes.container.name", c.name);
+      m.pod_name = lab("io.kubernetes.pod.name", sb ? sb->name : "");
+      m.pod_namespace = lab("io.kubernetes.pod.namespace", sb ? sb->pod_namespace : "");
+      m.pod_uid = lab("io.kubernetes.pod.uid", sb ? sb->uid : "");
+      metas.push_back(std::move(m));
+    }
+    {
+      std::lock_guard<std::mutex> g(podres_mu_);
+      native_meta_.clear();
+      for (const auto& m : metas)
+        native_meta_[m.pod_namespace + "/" + m.pod_name + "/" + m.container_name] = m;
+    }
+    attr_->set_container_meta(std::move(metas));
+  } else {
+    GPUMON_LOG(LogLevel::kWarn, "cri", "ListContainers/ListPodSandbox failed: " + err);
+  }
+  std::vector<ExtraSeries> ex;
+  ex.push_back({"gpumon_cri_up", "1 if the last CRI ListContainers/ListPodSandbox succeeded.", "gauge", -1, {},
+                ok ? 1.0 : 0.0});
+  ex.push_back({"gpumon_cri_containers", "Containers known from the CRI runtime.", "gauge", -1, {},
+                static_cast<double>(cs.size())});
+  ex.push_back({"gpumon_cri_list_seconds", "Duration of the last CRI listing.", "gauge", -1, {}, dt});
+  set_extra("cri_native", std::move(ex));
+  return ok;
 }
 
 }  // namespace gpumon

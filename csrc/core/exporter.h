@@ -32,9 +32,9 @@ namespace gpumon {
 struct ExporterConfig {
   std::string backend = "auto";       // auto | amdsmi | mock
   std::string amdsmi_lib;
-  std::string rocm_smi_lib;
+  std::string rocm_smi_lib;           // librocm_smi64 path override (rocm_smi backend / auto fallback)
   bool fast_path = true;              // amdsmi: per-tick reads straight from sysfs/KFD (sysfs_fast.h)
-  std::string sysfs_root = "/sys";  // librocm_smi64 path override (rocm_smi backend / auto fallback)
+  std::string sysfs_root = "/sys";
   MockConfig mock;
   std::vector<int> devices;           // hip_id filter; empty = all
   double interval_s = 1.0;            // <= 0: no sampler thread (ticks driven by tick())
@@ -67,6 +67,7 @@ struct ExporterConfig {
   std::string pod_resources_socket;
   std::string pod_resources_prefix = "amd.com/gpu";
   double pod_resources_refresh_s = 10.0;
+  std::string cri_socket;             // native CRI ListContainers/ListPodSandbox (same refresh)
   std::string version = "0.1.0";
 };
 
@@ -123,6 +124,7 @@ class Exporter {
   void influx_loop();
   void podres_loop();
   bool podres_poll_once();
+  bool cri_poll_once();
   bool ensure_backend();
   void handle_http(const HttpRequest& req, HttpResponse* resp);
   void sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
@@ -194,6 +196,7 @@ class Exporter {
   std::thread podres_;
   std::mutex podres_mu_;
   std::condition_variable podres_cv_;
+  std::unordered_map<std::string, ContainerMeta> native_meta_;  // "ns/pod/container" (guarded by podres_mu_)
   std::mutex push_mu_;
   std::condition_variable push_cv_;
   std::deque<std::string> push_q_;

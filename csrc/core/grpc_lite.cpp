@@ -353,4 +353,127 @@ bool podresources_list(const std::string& socket_path, const std::string& resour
   return true;
 }
 
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+bool parse_map_entry(std::string_view b, std::map<std::string, std::string>* m) {
+  PbReader r(b);
+  uint32_t f, w;
+  std::string k, v;
+  while (r.next(&f, &w)) {
+    std::string_view x;
+    if (w == 2 && (f == 1 || f == 2)) {
+      if (!r.bytes(&x)) return false;
+      (f == 1 ? k : v).assign(x);
+    } else if (!r.skip(w)) {
+      return false;
+    }
+  }
+  if (!r.ok()) return false;
+  (*m)[k] = v;
+  return true;
+}
+
+// name = field 1 of a nested metadata message (ContainerMetadata / PodSandboxMetadata); the
+// sandbox metadata also carries uid (2) and namespace (3).
+bool parse_metadata(std::string_view b, std::string* name, std::string* uid, std::string* ns) {
+  PbReader r(b);
+  uint32_t f, w;
+  while (r.next(&f, &w)) {
+    std::string_view x;
+    if (w == 2 && f >= 1 && f <= 3) {
+      if (!r.bytes(&x)) return false;
+      if (f == 1) name->assign(x);
+      else if (f == 2 && uid) uid->assign(x);
+      else if (f == 3 && ns) ns->assign(x);
+    } else if (!r.skip(w)) {
+      return false;
+    }
+  }
+  return r.ok();
+}
+
+}  // namespace
+
+bool parse_cri_containers(std::string_view msg, std::vector<CriContainer>* out) {
+  PbReader top(msg);
+  uint32_t f, w;
+  while (top.next(&f, &w)) {
+    if (f != 1 || w != 2) {
+      if (!top.skip(w)) return false;
+      continue;
+    }
+    std::string_view cb;
+    if (!top.bytes(&cb)) return false;
+    CriContainer c;
+    PbReader r(cb);
+    while (r.next(&f, &w)) {
+      std::string_view x;
+      if (w != 2 || (f != 1 && f != 2 && f != 3 && f != 8 && f != 9)) {
+        if (!r.skip(w)) return false;
+        continue;
+      }
+      if (!r.bytes(&x)) return false;
+      if (f == 1) c.id.assign(x);
+      else if (f == 2) c.sandbox_id.assign(x);
+      else if (f == 3 && !parse_metadata(x, &c.name, nullptr, nullptr)) return false;
+      else if (f == 8 && !parse_map_entry(x, &c.labels)) return false;
+      else if (f == 9 && !parse_map_entry(x, &c.annotations)) return false;
+    }
+    if (!r.ok()) return false;
+    out->push_back(std::move(c));
+  }
+  return top.ok();
+}
+
+bool parse_cri_sandboxes(std::string_view msg, std::vector<CriSandbox>* out) {
+  PbReader top(msg);
+  uint32_t f, w;
+  while (top.next(&f, &w)) {
+    if (f != 1 || w != 2) {
+      if (!top.skip(w)) return false;
+      continue;
+    }
+    std::string_view sb;
+    if (!top.bytes(&sb)) return false;
+    CriSandbox s;
+    PbReader r(sb);
+    while (r.next(&f, &w)) {
+      std::string_view x;
+      if (w != 2 || (f != 1 && f != 2 && f != 5 && f != 6)) {
+        if (!r.skip(w)) return false;
+        continue;
+      }
+      if (!r.bytes(&x)) return false;
+      if (f == 1) s.id.assign(x);
+      else if (f == 2 && !parse_metadata(x, &s.name, &s.uid, &s.pod_namespace)) return false;
+      else if (f == 5 && !parse_map_entry(x, &s.labels)) return false;
+      else if (f == 6 && !parse_map_entry(x, &s.annotations)) return false;
+    }
+    if (!r.ok()) return false;
+    out->push_back(std::move(s));
+  }
+  return top.ok();
+}
+
+bool cri_list(const std::string& socket_path, std::vector<CriContainer>* containers, std::vector<CriSandbox>* sandboxes,
+              std::string* err, int timeout_ms) {
+  containers->clear();
+  sandboxes->clear();
+  std::string resp;
+  if (!grpc_unary_unix(socket_path, "/runtime.v1.RuntimeService/ListContainers", "", &resp, err, timeout_ms))
+    return false;
+  if (!parse_cri_containers(resp, containers)) {
+    *err = "malformed ListContainersResponse";
+    return false;
+  }
+  if (!grpc_unary_unix(socket_path, "/runtime.v1.RuntimeService/ListPodSandbox", "", &resp, err, timeout_ms))
+    return false;
+  if (!parse_cri_sandboxes(resp, sandboxes)) {
+    *err = "malformed ListPodSandboxResponse";
+    return false;
+  }
+  return true;
+}
+
 }  // namespace gpumon

@@ -13,6 +13,7 @@
 #pragma once
 
 #include <cstdint>
+#include <map>
 #include <string>
 #include <string_view>
 #include <vector>
@@ -49,5 +50,21 @@ bool podresources_list(const std::string& socket_path, const std::string& resour
                        std::vector<PodDeviceRow>* out, std::string* err, int timeout_ms = 3000);
 bool parse_list_pod_resources(std::string_view msg, const std::string& resource_prefix,
                               std::vector<PodDeviceRow>* out);
+
+// CRI runtime.v1 RuntimeService ListContainers + ListPodSandbox (containerd / cri-o): container id
+// -> pod identity and labels (the reference read the same io.kubernetes.* labels with
+// `docker inspect`, gpu.py:86-88,184-195).
+struct CriContainer {
+  std::string id, sandbox_id, name;
+  std::map<std::string, std::string> labels, annotations;
+};
+struct CriSandbox {
+  std::string id, name, uid, pod_namespace;
+  std::map<std::string, std::string> labels, annotations;
+};
+bool parse_cri_containers(std::string_view msg, std::vector<CriContainer>* out);
+bool parse_cri_sandboxes(std::string_view msg, std::vector<CriSandbox>* out);
+bool cri_list(const std::string& socket_path, std::vector<CriContainer>* containers, std::vector<CriSandbox>* sandboxes,
+              std::string* err, int timeout_ms = 3000);
 
 }  // namespace gpumon

@@ -31,7 +31,7 @@ static void usage() {
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--procfs /proc] [--no-processes] [--no-gzip] [--sample-threads N]\n"
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx] [--once]\n"
-          "                       [--pod-resources SOCKET | --no-pod-resources]\n"
+          "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri]\n"
           "env: NODE_NAME, INFLUXDB_URL, GPUMON_LISTEN, GPUMON_INTERVAL, GPUMON_BACKEND\n");
 }
 
@@ -45,6 +45,7 @@ int main(int argc, char** argv) {
   bool once = false;
   // kubelet PodResources: on by default when the socket is mounted (deploy/k8s DaemonSet)
   std::string podres = "/var/lib/kubelet/pod-resources/kubelet.sock";
+  std::string cri;  // "" = first existing well-known runtime socket, "none" = off
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -69,6 +70,8 @@ int main(int argc, char** argv) {
     else if (a == "--roctx") cfg.roctx = true;
     else if (a == "--pod-resources") podres = next();
     else if (a == "--no-pod-resources") podres = "";
+    else if (a == "--cri") cri = next();
+    else if (a == "--no-cri") cri = "none";
     else if (a == "--opt-in-label") cfg.attribution.opt_in = next();
     else if (a == "--user-regex") cfg.attribution.user_regex = next();
     else if (a == "--user-label") cfg.attribution.user_label = next();
@@ -95,6 +98,15 @@ int main(int argc, char** argv) {
   cfg.port = atoi(colon == std::string::npos ? listen.c_str() : listen.c_str() + colon + 1);
   if (cfg.host.empty()) cfg.host = "no_name";
   if (!podres.empty() && access(podres.c_str(), F_OK) == 0) cfg.pod_resources_socket = podres;
+  if (cri.empty()) {
+    for (const char* c : {"/run/containerd/containerd.sock", "/var/run/crio/crio.sock", "/run/crio/crio.sock",
+                          "/var/run/cri-dockerd.sock"})
+      if (access(c, F_OK) == 0) {
+        cri = c;
+        break;
+      }
+  }
+  if (!cri.empty() && cri != "none") cfg.cri_socket = cri;
 
   if (once) {
     cfg.serve_http = false;

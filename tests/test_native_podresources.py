@@ -117,3 +117,60 @@ def test_parser_never_crashes_on_garbage(data):
         assert isinstance(rows, list)
     except RuntimeError:
         pass
+
+
+CID_A = "aa" * 32
+CID_B = "bb" * 32
+
+
+def _fake_proc(root, pid, cid):
+    d = root / str(pid)
+    d.mkdir(parents=True)
+    (d / "stat").write_text(f"{pid} (train) S 1 1 1 0 -1 0 0 0 0 0 0 0 0 0 20 0 1 0 777 0 0\n")
+    (d / "cgroup").write_text(f"0::/kubepods.slice/cri-containerd-{cid}.scope\n")
+
+
+def test_native_cri_client(core, tmp_path):
+    d = f"/tmp/gpumon-ncri-{os.getpid()}"
+    os.makedirs(d, exist_ok=True)
+    with FakeKubelet(cri_socket=f"{d}/cri.sock") as k:
+        k.pods = [FakePod("jupyter-q-0", "research", "uid-b", labels={"team": "q"},
+                          containers={"main": (CID_B, ["0000:25:00.0"])})]
+        cs, sbs = core.cri_list(k.cri_socket)
+    assert [c["id"] for c in cs] == [CID_B]
+    assert cs[0]["labels"]["io.kubernetes.pod.name"] == "jupyter-q-0"
+    assert sbs[0]["name"] == "jupyter-q-0" and sbs[0]["namespace"] == "research" and sbs[0]["uid"] == "uid-b"
+    assert sbs[0]["labels"]["team"] == "q"
+
+
+def test_native_control_plane_end_to_end(core, tmp_path):
+    """Same scenario as test_control_plane.test_plane_end_to_end, with no Python control plane:
+    the exporter's own CRI + PodResources pollers (what bin/gpumon-exporter runs)."""
+    d = f"/tmp/gpumon-nkl-{os.getpid()}"
+    os.makedirs(d, exist_ok=True)
+    with FakeKubelet(podres_socket=f"{d}/kubelet.sock", cri_socket=f"{d}/cri.sock") as k:
+        k.pods = [
+            FakePod("turing-gpu-notebook-alice-1-2", "ml", "uid-a", labels={"mlgpu": "mlgpu"},
+                    containers={"nb": (CID_A, ["0000:05:00.0"])}),
+            FakePod("jupyter-q-0", "research", "uid-b", containers={"main": (CID_B, ["0000:25:00.0"])}),
+        ]
+        _fake_proc(tmp_path, 1000, CID_A)
+        ex = core.Exporter({"backend": "mock:gpus=2", "serve_http": False, "interval_s": 0, "host": "n1",
+                            "procfs_root": str(tmp_path), "cri_socket": k.cri_socket,
+                            "pod_resources_socket": k.podres_socket})
+        ex.start()
+        try:
+            ex.mock_set_procs([{"pid": 1000, "device": 0, "name": "python", "vram_bytes": 5 << 30}])
+            ex.tick()
+            rows = {(r["podname"], r["idle"]): r for r in ex.pod_rows()}
+            active = rows[("turing-gpu-notebook-alice-1-2", False)]
+            assert (active["namespace"], active["container"], active["user_name"], active["containerid"],
+                    active["pid"]) == ("ml", "nb", "alice", CID_A[:12], "1000")
+            idle = rows[("jupyter-q-0", True)]
+            assert (idle["pid"], idle["user_name"], idle["dev"], idle["containerid"]) == ("-", "q", 1, CID_B[:12])
+            fam = promtext.parse(ex.metrics_text())
+            assert promtext.one(fam, "gpumon_cri_up") == 1 and promtext.one(fam, "gpumon_cri_containers") == 2
+            assert promtext.one(fam, "gpumon_podresources_up") == 1
+            assert promtext.one(fam, "gpumon_gpus", state="allocated_active") == 1
+        finally:
+            ex.stop()
