@@ -141,7 +141,7 @@ def test_parallel_device_sampling(core):
     dt = time.monotonic() - t0
     ex.stop()
     assert info["devices_ok"] == 8
-    assert dt < 0.12, dt  # 8 x 20 ms sequential would be >= 160 ms
+    assert dt < 0.15, dt  # 8 x 20 ms sequential would be >= 160 ms
 
 
 def test_backend_reinit_after_total_failure(mock_exporter):
@@ -186,7 +186,7 @@ def test_hung_device_is_isolated_by_the_watchdog(core):
         # the next tick does not wait for the still-running call at all
         t0 = time.monotonic()
         ex.tick()
-        assert time.monotonic() - t0 < 0.15
+        assert time.monotonic() - t0 < 0.5  # the hung call has 1.3 s left
         assert ex.self_stats()["device_timeouts"][1] == 2
         ex.mock_set_hang_ms(0)
         time.sleep(1.6)  # the hung call returns
