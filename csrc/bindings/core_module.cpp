@@ -187,6 +187,19 @@ py::dict rates_to_dict(const DeviceRates& r) {
     wr.append(num(r.xgmi_wr_Bps[k]));
   }
   d["xcd_busy_avg"] = xb;
+  if (r.has_xcd_limit) {
+    py::list lp, lt, la, lu;
+    for (int k = 0; k < r.n_xcd; ++k) {
+      lp.append(num(r.xcd_below_ppt_pct[k]));
+      lt.append(num(r.xcd_below_thm_pct[k]));
+      la.append(num(r.xcd_below_total_pct[k]));
+      lu.append(num(r.xcd_low_util_pct[k]));
+    }
+    d["xcd_below_ppt_pct"] = lp;
+    d["xcd_below_thm_pct"] = lt;
+    d["xcd_below_total_pct"] = la;
+    d["xcd_low_util_pct"] = lu;
+  }
   d["xgmi_rd_Bps"] = rd;
   d["xgmi_wr_Bps"] = wr;
   return d;

@@ -136,6 +136,7 @@ class MockBackend : public Backend {
   std::vector<double> forced_xgmi_;  // per dev * kMaxLinks, GB/s (NaN = default)
   std::vector<uint64_t> calls_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
+  std::vector<uint64_t> lim_acc_;  // per device x XCC x {ppt, thermal, any, low-util}
   std::map<std::pair<uint32_t, int>, uint64_t> proc_gfx_ns_;
   int64_t t0_ns_ = 0;
   std::vector<int64_t> last_ns_;

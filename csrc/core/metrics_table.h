@@ -107,6 +107,16 @@ void fill_from_gpu_metrics(const M& m, int partition_id, int max_xcp, double pow
     a.xcd_busy_acc[k] = ok64(xs.gfx_busy_acc[k]) ? xs.gfx_busy_acc[k] : 0;
     nx = k + 1;
   }
+  if (nx > 0 && ok64(xs.gfx_below_host_limit_total_acc[0])) {
+    a.has_xcd_limit_acc = true;
+    for (int k = 0; k < nx; ++k) {
+      a.xcd_below_ppt_acc[k] = ok64(xs.gfx_below_host_limit_ppt_acc[k]) ? xs.gfx_below_host_limit_ppt_acc[k] : 0;
+      a.xcd_below_thm_acc[k] = ok64(xs.gfx_below_host_limit_thm_acc[k]) ? xs.gfx_below_host_limit_thm_acc[k] : 0;
+      a.xcd_below_total_acc[k] =
+          ok64(xs.gfx_below_host_limit_total_acc[k]) ? xs.gfx_below_host_limit_total_acc[k] : 0;
+      a.xcd_low_util_acc[k] = ok64(xs.gfx_low_utilization_acc[k]) ? xs.gfx_low_utilization_acc[k] : 0;
+    }
+  }
   out->n_xcd = nx;
   a.n_xcd_acc = nx;
   // xGMI accumulators (KB) and link status. Slot 0 on MI355X is the (N/A) self slot.

@@ -73,6 +73,7 @@ bool MockBackend::init(std::string* err) {
   xgmi_rd_.assign(n * kMaxLinks, 0);
   xgmi_wr_.assign(n * kMaxLinks, 0);
   busy_acc_.assign(n * kMaxXcc, 0);
+  lim_acc_.assign(n * kMaxXcc * 4, 0);
   acc_counter_.assign(n, 0);
   gfx_act_acc_.assign(n, 0);
   t0_ns_ = mono_ns();
@@ -201,7 +202,20 @@ void MockBackend::sample(int i, DeviceSample* out) {
     busy_acc_[i * kMaxXcc + k] += static_cast<uint64_t>(xb * elapsed * 100000.0);
     a.xcd_busy_acc[k] = busy_acc_[i * kMaxXcc + k];
     out->gfxclks[k] = v[F_GFXCLK_CUR];
+    // residency counters (+1 per 10 us tick while true): PPT-limited above 90 % busy, low
+    // utilisation below 5 % (as measured on MI355X: idle = low-util + any)
+    const uint64_t ticks = static_cast<uint64_t>(elapsed * 100000.0);
+    uint64_t* L = &lim_acc_[(static_cast<size_t>(i) * kMaxXcc + k) * 4];
+    const bool ppt = xb > 90.0, low = xb < 5.0;
+    if (ppt) L[0] += ticks / 4;
+    if (low) L[3] += ticks;
+    L[2] += low ? ticks : (ppt ? ticks / 4 : 0);
+    a.xcd_below_ppt_acc[k] = L[0];
+    a.xcd_below_thm_acc[k] = L[1];
+    a.xcd_below_total_acc[k] = L[2];
+    a.xcd_low_util_acc[k] = L[3];
   }
+  a.has_xcd_limit_acc = nx > 0;
   int nl = std::min(cfg_.n_links + 1, kMaxLinks);  // slot 0 = self, as on MI355X
   out->n_links = nl;
   a.n_links_acc = nl;

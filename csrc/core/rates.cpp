@@ -63,6 +63,19 @@ void compute_rates(const DeviceSample& prev, const DeviceSample& cur, const Rate
                                  ? std::min(100.0, dx * cfg.activity_acc_scale / dacc)
                                  : kNaN;
     }
+    if (a.has_xcd_limit_acc && b.has_xcd_limit_acc) {
+      out->has_xcd_limit = true;
+      auto pct = [&](uint64_t x0, uint64_t x1) {
+        uint64_t d = 0;
+        return acc_delta(x0, x1, false, &d) ? std::min(100.0, 100.0 * static_cast<double>(d) / dacc) : kNaN;
+      };
+      for (int k = 0; k < nx; ++k) {
+        out->xcd_below_ppt_pct[k] = pct(a.xcd_below_ppt_acc[k], b.xcd_below_ppt_acc[k]);
+        out->xcd_below_thm_pct[k] = pct(a.xcd_below_thm_acc[k], b.xcd_below_thm_acc[k]);
+        out->xcd_below_total_pct[k] = pct(a.xcd_below_total_acc[k], b.xcd_below_total_acc[k]);
+        out->xcd_low_util_pct[k] = pct(a.xcd_low_util_acc[k], b.xcd_low_util_acc[k]);
+      }
+    }
   }
   int nl = std::min(a.n_links_acc, b.n_links_acc);
   out->n_links = nl;

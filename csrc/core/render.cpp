@@ -315,6 +315,32 @@ void render_prometheus(const RenderInput& in, std::string* o) {
             f.add(dl[d], {{"xcd", std::to_string(k)}}, r.xcd_busy_avg[k]);
       }
     }
+    {
+      // MI355X gpu_metrics v1.8 per-XCC residencies: is each XCD's clock being held down, and why?
+      Family f(o, "gpu_xcd_clock_below_limit_percent",
+               "Share of the interval each XCD's clock was held below the host limit, by reason "
+               "(ppt = power, thermal, any).",
+               "gauge");
+      for (size_t d = 0; d < n; ++d) {
+        const auto& r = rate(d);
+        if (!sm[d].ok || !r.valid || !r.has_xcd_limit) continue;
+        for (int k = 0; k < r.n_xcd; ++k) {
+          const std::string x = std::to_string(k);
+          f.add(dl[d], {{"xcd", x}, {"reason", "ppt"}}, r.xcd_below_ppt_pct[k]);
+          f.add(dl[d], {{"xcd", x}, {"reason", "thermal"}}, r.xcd_below_thm_pct[k]);
+          f.add(dl[d], {{"xcd", x}, {"reason", "any"}}, r.xcd_below_total_pct[k]);
+        }
+      }
+    }
+    {
+      Family f(o, "gpu_xcd_low_utilization_percent",
+               "Share of the interval each XCD spent in the firmware's low-utilisation state.", "gauge");
+      for (size_t d = 0; d < n; ++d) {
+        const auto& r = rate(d);
+        if (!sm[d].ok || !r.valid || !r.has_xcd_limit) continue;
+        for (int k = 0; k < r.n_xcd; ++k) f.add(dl[d], {{"xcd", std::to_string(k)}}, r.xcd_low_util_pct[k]);
+      }
+    }
     devf("gpu_throttle_status", "Firmware throttle status bitfield.", "gauge",
          [&](size_t d) { return sm[d].v[F_THROTTLE_STATUS]; });
     {

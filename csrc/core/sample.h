@@ -109,6 +109,11 @@ struct Accumulators {
   bool has_pcie_bw_acc = false;
   std::array<uint64_t, kMaxXcc> xcd_busy_acc{};
   int n_xcd_acc = 0;
+  // gpu_metrics v1.8 xcp_stats v1.2 per-XCC residency counters: +1 per accumulation tick while
+  // the XCC clock is held below the host limit by PPT / thermal / any reason, or the XCC is in
+  // low utilisation (measured on MI355X: idle 1.0/tick low-util + any; bf16 burn 0).
+  std::array<uint64_t, kMaxXcc> xcd_below_ppt_acc{}, xcd_below_thm_acc{}, xcd_below_total_acc{}, xcd_low_util_acc{};
+  bool has_xcd_limit_acc = false;
   std::array<uint64_t, kMaxLinks> xgmi_rd_kb{};
   std::array<uint64_t, kMaxLinks> xgmi_wr_kb{};
   int n_links_acc = 0;
@@ -185,6 +190,9 @@ struct DeviceRates {
   double mem_activity_avg_pct = kNaN;
   std::array<double, kMaxXcc> xcd_busy_avg{};
   int n_xcd = 0;
+  // % of the interval each XCC clock spent below the host limit (by reason) / in low utilisation
+  std::array<double, kMaxXcc> xcd_below_ppt_pct{}, xcd_below_thm_pct{}, xcd_below_total_pct{}, xcd_low_util_pct{};
+  bool has_xcd_limit = false;
   std::array<double, kMaxLinks> xgmi_rd_Bps{};
   std::array<double, kMaxLinks> xgmi_wr_Bps{};
   int n_links = 0;

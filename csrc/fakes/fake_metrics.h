@@ -47,6 +47,10 @@ void fill_metrics(M* m, int d, uint64_t n) {
     m->current_gfxclks[k] = static_cast<uint16_t>(2100 - k);
     m->xcp_stats[0].gfx_busy_inst[k] = 37;
     m->xcp_stats[0].gfx_busy_acc[k] = n * 37 * 1000;
+    m->xcp_stats[0].gfx_below_host_limit_ppt_acc[k] = n * 250;    // 25 % of the 1000 ticks per call
+    m->xcp_stats[0].gfx_below_host_limit_thm_acc[k] = 0;
+    m->xcp_stats[0].gfx_below_host_limit_total_acc[k] = n * 250;
+    m->xcp_stats[0].gfx_low_utilization_acc[k] = 0;
   }
   m->xgmi_link_status[0] = 0xFFFF;  // slot 0: N/A on MI355X
   m->xgmi_read_data_acc[0] = 0;
