@@ -301,3 +301,28 @@ def test_exported_activity_tracks_duty_cycle(core, torch_gpu):
         assert abs(got - busy) < 8, (got, busy, acts)
     finally:
         ex.stop()
+
+
+def test_xcd_limit_residencies_idle_vs_burn(core, torch_gpu):
+    """gpu_metrics v1.8 per-XCC residencies (profiles: +1 per accumulation tick): an idle GPU sits in
+    the low-utilisation state on every XCD; under the bf16 burn none of them is."""
+    from gpumon.ops.load import SyntheticLoad
+
+    ex = _exporter(core)
+    try:
+        ex.tick()
+        time.sleep(0.5)
+        ex.tick()
+        r = ex.rates()[0]
+        assert len(r["xcd_low_util_pct"]) == 8
+        assert min(r["xcd_low_util_pct"]) > 80, r["xcd_low_util_pct"]
+        with SyntheticLoad(0, "mfma"):
+            time.sleep(1.0)
+            ex.tick()
+            time.sleep(0.5)
+            ex.tick()
+            r = ex.rates()[0]
+        assert max(r["xcd_low_util_pct"]) < 20, r["xcd_low_util_pct"]
+        print("\nxcd limits under burn: ppt=%s any=%s" % (r["xcd_below_ppt_pct"], r["xcd_below_total_pct"]))
+    finally:
+        ex.stop()
