@@ -94,7 +94,11 @@ def build():
     y += 8
     panels.append(panel("Per-pod compute share (% of CUs holding the pod's waves)", "timeseries",
                         [(f'sum by (host, gpu_id, namespace, podname) (pod_gpu_proc_cu_occupancy_percent{{{HOST}}})',
-                          "{{host}} gpu{{gpu_id}} {{namespace}}/{{podname}}")], 0, y, 24, 8,
+                          "{{host}} gpu{{gpu_id}} {{namespace}}/{{podname}}")], 0, y, 12, 8,
+                        fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
+    panels.append(panel("XCD clock held below limit (% of time, by reason)", "timeseries",
+                        [(f'avg by (host, gpu_id, reason) (gpu_xcd_clock_below_limit_percent{{{HOST},reason!="any"}})',
+                          "{{host}} gpu{{gpu_id}} {{reason}}")], 12, y, 12, 8,
                         fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
     y += 8
     panels.append(panel("Exporter: /metrics p99 and tick p99 (s)", "timeseries",
