@@ -127,7 +127,7 @@ def test_alert_and_recording_rules_resolve(mock_exporter):
     ex.tick()
     fam = promtext.parse(ex.metrics_text())
     produced = {n for f, v in fam.items() for n in [f] + [s[0] for s in v["samples"]]}
-    words = {"sum", "by", "count", "rate", "increase", "avg", "max", "time", "host", "namespace", "podname",
+    words = {"sum", "by", "count", "rate", "increase", "avg", "max", "time", "host", "namespace", "podname", "gpu_id",
              "user_name"}
     exprs = [r["expr"] for g in rule["spec"]["groups"] for r in g["rules"]]
     assert len(exprs) >= 12
