@@ -65,6 +65,7 @@ class Config:
     procfs_env_fallback: bool = True
     include_host_processes: bool = True
     # control plane (k8s)
+    control_plane: str = "python"         # python (grpcio clients) | native (C++ grpc_lite pollers) | off
     cri_socket: str = ""                  # e.g. unix:///run/containerd/containerd.sock ; "" = autodetect
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     resource_names: List[str] = field(default_factory=lambda: ["amd.com/gpu"])
@@ -217,6 +218,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--procfs-root", dest="procfs_root")
     p.add_argument("--cri-socket", dest="cri_socket")
     p.add_argument("--pod-resources-socket", dest="pod_resources_socket")
+    p.add_argument("--control-plane", dest="control_plane", choices=["python", "native", "off"],
+                   help="who polls kubelet PodResources / CRI: python (grpcio) or native (C++, no grpcio)")
     p.add_argument("--no-processes", dest="processes", action="store_false", default=None)
     p.add_argument("--no-gzip", dest="gzip", action="store_false", default=None)
     p.add_argument("--sample-threads", dest="sample_threads", type=int)

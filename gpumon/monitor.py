@@ -13,6 +13,7 @@ on its own thread with per-GPU error isolation, and this object only wires the p
 from __future__ import annotations
 
 import logging
+import os
 from typing import Optional
 
 from ._native import core
@@ -23,16 +24,41 @@ log = logging.getLogger("gpumon")
 _LEVELS = {"debug": 0, "info": 1, "warn": 2, "warning": 2, "error": 3, "off": 4}
 
 
+# well-known CRI sockets (gpumon/attribution/clients.py DEFAULT_CRI_SOCKETS; kept here so the
+# native path needs no grpcio import)
+_CRI_SOCKETS = ("/run/containerd/containerd.sock", "/var/run/containerd/containerd.sock", "/var/run/crio/crio.sock",
+                "/run/crio/crio.sock", "/var/run/cri-dockerd.sock")
+
+
 class GpuMonitor:
     def __init__(self, cfg: Optional[Config] = None, control_plane: bool = True):
         self.cfg = cfg or Config()
         self._core = core()
         self._core.set_log_level(_LEVELS.get(self.cfg.log_level.lower(), 1))
-        self.ex = self._core.Exporter(self.cfg.to_core())
+        core_cfg = self.cfg.to_core()
+        mode = self.cfg.control_plane if control_plane else "off"
+        if mode == "python":
+            try:
+                import grpc  # noqa: F401
+            except ImportError:
+                log.warning("grpcio not importable: using the native CRI/PodResources pollers")
+                mode = "native"
+        if mode == "native":
+            # the exporter's own C++ pollers (csrc/core/grpc_lite.cpp) -- same as bin/gpumon-exporter
+            if os.path.exists(self.cfg.pod_resources_socket):
+                core_cfg["pod_resources_socket"] = self.cfg.pod_resources_socket
+            cri = self.cfg.cri_socket or next((p for p in _CRI_SOCKETS if os.path.exists(p)), "")
+            if cri:
+                core_cfg["cri_socket"] = cri[len("unix://"):] if cri.startswith("unix://") else cri
+            core_cfg["pod_resources_refresh_s"] = float(self.cfg.metadata_refresh)
+            if self.cfg.resource_names:
+                core_cfg["pod_resources_prefix"] = self.cfg.resource_names[0]
+        self.control_plane_mode = mode
+        self.ex = self._core.Exporter(core_cfg)
         self.plane = None
         self.probe = None
         self.pmc = None
-        self._want_plane = control_plane
+        self._want_plane = mode == "python"
         self.start_error = ""
 
     # ------------------------------------------------------------------ lifecycle

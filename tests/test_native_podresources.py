@@ -174,3 +174,22 @@ def test_native_control_plane_end_to_end(core, tmp_path):
             assert promtext.one(fam, "gpumon_gpus", state="allocated_active") == 1
         finally:
             ex.stop()
+
+
+def test_gpumon_monitor_native_mode(tmp_path):
+    """`gpumon serve --control-plane native`: the Python monitor hands the sockets to the C++
+    pollers instead of starting the grpcio control plane."""
+    from gpumon.config import Config
+    from gpumon.monitor import GpuMonitor
+
+    d = f"/tmp/gpumon-nm-{os.getpid()}"
+    os.makedirs(d, exist_ok=True)
+    with FakeKubelet(podres_socket=f"{d}/kubelet.sock", cri_socket=f"{d}/cri.sock") as k:
+        k.pods = [FakePod("jupyter-q-0", "research", "uid-b", containers={"main": (CID_B, ["0000:25:00.0"])})]
+        cfg = Config(backend="mock:gpus=2,mode=idle", interval=0, listen="127.0.0.1:0", control_plane="native",
+                     pod_resources_socket=k.podres_socket, cri_socket=k.cri_socket, log_level="warn")
+        with GpuMonitor(cfg) as mon:
+            assert mon.control_plane_mode == "native" and mon.plane is None
+            mon.ex.tick()
+            idle = [r for r in mon.ex.pod_rows() if r["idle"]]
+            assert [(r["podname"], r["dev"], r["containerid"]) for r in idle] == [("jupyter-q-0", 1, CID_B[:12])]
