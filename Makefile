@@ -2,6 +2,7 @@
 #   make            -> python extension gpumon/_core*.so + bin/gpumon-exporter + HIP library
 #   make core       -> C++ core only (no hipcc needed)
 #   make hip        -> gpumon/_hip*.so (HIP kernels: probe + synthetic load, gfx950)
+#   make plugins    -> lib/libgpumon_pmc.so + lib/libgpumon_probe.so (dlopen'd on-device plugins)
 #   make asan       -> bin/gpumon-exporter-asan (host-only sanitizers)
 # Everything builds IN-TREE so the .so files travel with the repo snapshot to the GPU box.
 
@@ -28,8 +29,8 @@ BIN       := bin/gpumon-exporter
 HIP_SRC   := $(wildcard csrc/hip/*.hip)
 HIP_HDR   := $(wildcard csrc/hip/*.h)
 
-.PHONY: all core hip pmc clean asan tsan
-all: core hip pmc
+.PHONY: all core hip pmc plugins clean asan tsan fakes
+all: core hip plugins pmc
 core: $(PYEXT) $(BIN)
 hip: $(HIPEXT)
 
@@ -82,19 +83,39 @@ bin/gpumon-exporter-tsan: $(CORE_SRC) $(CORE_HDR) csrc/exporter_main.cpp
 	  $(CORE_SRC) csrc/exporter_main.cpp -o bin/gpumon-exporter-tsan $(LIBS)
 
 clean:
-	rm -rf build bin gpumon/_core*.so gpumon/_hip*.so gpumon/_pmc*.so
+	rm -rf build bin lib gpumon/_core*.so gpumon/_hip*.so gpumon/_pmc*.so
 
-# rocprofiler-sdk device counting module (host-only C++; links the ROCm profiler + HSA runtime).
+# On-device plugins (csrc/plugins/ondevice_abi.h). The exporter binary and gpumon._core dlopen()
+# them from lib/ only when PMC / probe sampling is enabled, so neither links HIP or rocprofiler.
+PMCLIB   := lib/libgpumon_pmc.so
+PROBELIB := lib/libgpumon_probe.so
+plugins: $(PMCLIB) $(PROBELIB)
+$(PMCLIB): csrc/plugins/pmc_plugin.cpp csrc/plugins/ondevice_abi.h
+	@mkdir -p lib
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared -fvisibility=hidden -I$(ROCM)/include $< -Wl,-soname,libgpumon_pmc.so \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrocprofiler-sdk -lhsa-runtime64 -o $@
+build/obj/plugins/probe_plugin.o: csrc/plugins/probe_plugin.cpp csrc/plugins/ondevice_abi.h $(HIP_HDR)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(PROBELIB): build/obj/plugins/probe_plugin.o build/obj/hip/kernels.o build/obj/hip/burn16.o
+	@mkdir -p lib
+	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -shared -fPIC $^ -Wl,-soname,libgpumon_probe.so -o $@
+
+# gpumon._pmc: Python view of the PMC plugin (linked, rpath $ORIGIN/../lib).
 PMCEXT := gpumon/_pmc$(EXT)
 pmc: $(PMCEXT)
-$(PMCEXT): csrc/pmc/pmc_module.cpp
-	$(HIPCC) -O2 -std=c++17 -fPIC -shared -fvisibility=hidden -I$(ROCM)/include -I$(PYINC) -I$(PYBIND) $< \
-	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrocprofiler-sdk -lhsa-runtime64 -o $@
+$(PMCEXT): csrc/pmc/pmc_module.cpp csrc/plugins/ondevice_abi.h $(PMCLIB)
+	$(CXX) -O2 -std=c++17 -fPIC -shared -fvisibility=hidden -I$(PYINC) -I$(PYBIND) $< \
+	  -Llib -lgpumon_pmc -Wl,-rpath,'$$ORIGIN/../lib' -o $@
 
 # Fake libamd_smi (CPU tests of the real amdsmi backend through the dlopen table).
 FAKESMI := build/fakes/libfake_amd_smi.so
 FAKERSMI := build/fakes/libfake_rocm_smi.so
-fakes: $(FAKESMI) $(FAKERSMI)
+FAKEOND := build/fakes/ondevice/libgpumon_pmc.so build/fakes/ondevice/libgpumon_probe.so
+fakes: $(FAKESMI) $(FAKERSMI) $(FAKEOND)
+build/fakes/ondevice/%.so: csrc/fakes/fake_ondevice.cpp csrc/plugins/ondevice_abi.h
+	@mkdir -p $(dir $@)
+	$(CXX) -O1 -std=c++17 -fPIC -shared $< -o $@ -lpthread
 $(FAKESMI): csrc/fakes/fake_amd_smi.cpp csrc/fakes/fake_metrics.h
 	@mkdir -p $(dir $@)
 	$(CXX) -O1 -std=c++17 -fPIC -shared -I$(ROCM)/include $< -o $@

@@ -12,6 +12,7 @@
 #include "../core/exporter.h"
 #include "../core/grpc_lite.h"
 #include "../core/http_client.h"
+#include "../core/ondevice.h"
 #include "../core/render.h"
 #include "../core/snapshot.h"
 #include "../core/trace.h"
@@ -24,6 +25,21 @@ namespace {
 template <typename T>
 void get(const py::dict& d, const char* k, T* out) {
   if (d.contains(k) && !d[k].is_none()) *out = d[k].cast<T>();
+}
+
+OnDeviceConfig ondevice_from(const py::dict& d) {
+  OnDeviceConfig c;
+  get(d, "plugin_dir", &c.plugin_dir);
+  get(d, "pmc", &c.pmc);
+  get(d, "pmc_counters", &c.pmc_counters);
+  get(d, "pmc_every_s", &c.pmc_every_s);
+  get(d, "pmc_window_s", &c.pmc_window_s);
+  get(d, "probe", &c.probe);
+  get(d, "probe_every_s", &c.probe_every_s);
+  get(d, "probe_blocks", &c.probe_blocks);
+  get(d, "probe_spin_ticks", &c.probe_spin_ticks);
+  get(d, "probe_timeout_s", &c.probe_timeout_s);
+  return c;
 }
 
 MockProc mock_proc_from(const py::dict& d) {
@@ -622,4 +638,72 @@ PYBIND11_MODULE(_core, m) {
       .def("mock_set_xgmi",
            [](Exporter& e, int dev, int link, double gbps) { mock_of(e)->set_xgmi(dev, link, gbps); })
       .def("mock_calls", [](Exporter& e, int dev) { return mock_of(e)->calls(dev); });
+
+  // Native on-device samplers (csrc/core/ondevice.h): the same PMC / probe plugins the standalone
+  // binary dlopen()s, driven from C++ threads instead of the Python runners in gpumon/ops.
+  py::class_<OnDevice>(m, "OnDevice")
+      .def(py::init([](Exporter& e, const py::dict& cfg) { return new OnDevice(&e, ondevice_from(cfg)); }),
+           py::keep_alive<1, 2>())
+      .def("start",
+           [](OnDevice& o) {
+             std::string err;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = o.start(&err);
+             }
+             if (!ok) throw std::runtime_error("on-device samplers: " + err);
+           })
+      .def("stop",
+           [](OnDevice& o) {
+             py::gil_scoped_release nogil;
+             o.stop();
+           })
+      .def("step",
+           [](OnDevice& o) {
+             py::gil_scoped_release nogil;
+             return o.step();
+           })
+      .def("stats", [](const OnDevice& o) {
+        auto s = o.stats();
+        py::dict d;
+        d["pmc_samples"] = s.pmc_samples;
+        d["pmc_errors"] = s.pmc_errors;
+        d["probe_done"] = s.probe_done;
+        d["probe_timeouts"] = s.probe_timeouts;
+        d["pmc_agents"] = s.pmc_agents;
+        d["probe_devices"] = s.probe_devices;
+        return d;
+      });
+  m.def("default_plugin_dir", &default_plugin_dir);
+  m.def(
+      "pmc_derive",
+      [](const py::dict& raw, const py::dict& agent) {
+        std::map<std::string, PmcReduced> r;
+        for (auto kv : raw) {
+          py::dict v = kv.second.cast<py::dict>();
+          PmcReduced x;
+          get(v, "sum", &x.sum);
+          get(v, "max", &x.max);
+          get(v, "n", &x.n);
+          get(v, "by_xcc", &x.by_xcc);
+          r[kv.first.cast<std::string>()] = x;
+        }
+        PmcAgentInfo a;
+        get(agent, "cu_count", &a.cu_count);
+        get(agent, "simd_count", &a.simd_count);
+        get(agent, "num_xcc", &a.num_xcc);
+        get(agent, "max_waves_per_cu", &a.max_waves_per_cu);
+        PmcDerived d = pmc_derive(r, a);
+        py::dict out;
+        auto put = [&](const char* k, double v) {
+          if (v == v) out[k] = v;
+        };
+        put("mfma_busy", d.mfma_busy);
+        put("occupancy", d.occupancy);
+        put("gui_active", d.gui_active);
+        if (!d.xcd_mfma_busy.empty()) out["xcd_mfma_busy"] = d.xcd_mfma_busy;
+        return out;
+      },
+      "C++ twin of gpumon.ops.pmc.derive (used by the native samplers)");
 }

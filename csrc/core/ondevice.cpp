@@ -1,0 +1,409 @@
+// On-device samplers (PMC device counting + K1 probe) for the native exporter; see ondevice.h.
+#include "ondevice.h"
+
+#include <dlfcn.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "../plugins/ondevice_abi.h"
+#include "common.h"
+#include "exporter.h"
+
+namespace gpumon {
+
+// ---------------------------------------------------------------------------------------------
+// plugin loading
+
+struct OnDevice::Plugin {
+  void* h = nullptr;
+  std::string path;
+  // pmc
+  int (*pmc_abi)() = nullptr;
+  int (*pmc_init)(char*, size_t) = nullptr;
+  int (*pmc_agent)(int, gpumon_pmc_agent_t*) = nullptr;
+  int (*pmc_sample_many)(const int*, int, const char* const*, int, double, gpumon_pmc_value_t*, int32_t*, char*,
+                         size_t) = nullptr;
+  // probe
+  int (*probe_abi)() = nullptr;
+  int (*probe_count)() = nullptr;
+  gpumon_probe* (*probe_create)(int, int, int, int, char*, size_t) = nullptr;
+  int (*probe_launch)(gpumon_probe*) = nullptr;
+  int (*probe_wait)(gpumon_probe*, int, double, gpumon_probe_result_t*) = nullptr;
+  void (*probe_destroy)(gpumon_probe*) = nullptr;
+
+  // Plugins stay loaded for the life of the process: rocprofiler keeps the tool's callbacks and
+  // the HIP runtime keeps its threads, so dlclose() would leave dangling code pointers.
+  ~Plugin() = default;
+};
+
+namespace {
+
+template <class F>
+bool sym(void* h, const char* name, F* out, std::string* missing) {
+  *out = reinterpret_cast<F>(dlsym(h, name));
+  if (!*out) *missing += std::string(missing->empty() ? "" : ",") + name;
+  return *out != nullptr;
+}
+
+std::unique_ptr<OnDevice::Plugin> load_plugin(const std::string& dir, const char* file, bool pmc, std::string* err) {
+  auto p = std::make_unique<OnDevice::Plugin>();
+  p->path = dir + "/" + file;
+  // gpumon._pmc links the same file (rpath $ORIGIN/../lib); the loader matches it by inode, so a
+  // process using both holds ONE copy and one rocprofiler tool registration. RTLD_LOCAL keeps a
+  // fake plugin (tests) from interposing on a real one loaded later.
+  p->h = dlopen(p->path.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!p->h) {
+    *err = std::string("dlopen ") + p->path + ": " + dlerror();
+    return nullptr;
+  }
+  std::string missing;
+  if (pmc) {
+    sym(p->h, "gpumon_pmc_abi_version", &p->pmc_abi, &missing);
+    sym(p->h, "gpumon_pmc_init", &p->pmc_init, &missing);
+    sym(p->h, "gpumon_pmc_agent", &p->pmc_agent, &missing);
+    sym(p->h, "gpumon_pmc_sample_many", &p->pmc_sample_many, &missing);
+  } else {
+    sym(p->h, "gpumon_probe_abi_version", &p->probe_abi, &missing);
+    sym(p->h, "gpumon_probe_device_count", &p->probe_count, &missing);
+    sym(p->h, "gpumon_probe_create", &p->probe_create, &missing);
+    sym(p->h, "gpumon_probe_launch", &p->probe_launch, &missing);
+    sym(p->h, "gpumon_probe_wait", &p->probe_wait, &missing);
+    sym(p->h, "gpumon_probe_destroy", &p->probe_destroy, &missing);
+  }
+  if (!missing.empty()) {
+    *err = p->path + ": missing symbols " + missing;
+    return nullptr;
+  }
+  const int abi = pmc ? p->pmc_abi() : p->probe_abi();
+  if (abi != GPUMON_ONDEVICE_ABI) {
+    *err = p->path + ": plugin ABI " + std::to_string(abi) + " != " + std::to_string(GPUMON_ONDEVICE_ABI);
+    return nullptr;
+  }
+  return p;
+}
+
+ExtraSeries xs(const char* name, const char* help, int dev, double v, const char* type = "gauge") {
+  ExtraSeries s;
+  s.name = name;
+  s.help = help;
+  s.type = type;
+  s.dev = dev;
+  s.value = v;
+  return s;
+}
+
+}  // namespace
+
+std::string default_plugin_dir() {
+  if (const char* e = getenv("GPUMON_PLUGIN_DIR"); e && *e) return e;
+  Dl_info info{};
+  // The object holding this function: bin/gpumon-exporter or gpumon/_core*.so; both sit one level
+  // below the tree root, next to lib/.
+  if (dladdr(reinterpret_cast<void*>(&default_plugin_dir), &info) && info.dli_fname) {
+    std::string f = info.dli_fname;
+    if (f.find('/') == std::string::npos) {
+      char buf[4096];
+      ssize_t n = readlink("/proc/self/exe", buf, sizeof buf - 1);
+      if (n > 0) f.assign(buf, static_cast<size_t>(n));
+    }
+    auto slash = f.rfind('/');
+    std::string dir = slash == std::string::npos ? "." : f.substr(0, slash);
+    return dir + "/../lib";
+  }
+  return "lib";
+}
+
+// ---------------------------------------------------------------------------------------------
+// derivation (mirrors gpumon/ops/pmc.py derive())
+
+PmcDerived pmc_derive(const std::map<std::string, PmcReduced>& raw, const PmcAgentInfo& agent) {
+  PmcDerived d;
+  auto get = [&](const char* k) -> const PmcReduced* {
+    auto it = raw.find(k);
+    return it == raw.end() ? nullptr : &it->second;
+  };
+  const PmcReduced* gui_r = get("GRBM_GUI_ACTIVE");
+  const double gui = gui_r ? gui_r->max : 0.0;
+  const double simds = agent.simd_count ? agent.simd_count : agent.cu_count * 4.0;
+  const double cus = agent.cu_count;
+  const double waves = agent.max_waves_per_cu ? agent.max_waves_per_cu : 32.0;
+  if (gui > 0 && simds > 0) {
+    if (const PmcReduced* m = get("SQ_VALU_MFMA_BUSY_CYCLES")) {
+      d.mfma_busy = std::min(100.0, 100.0 * m->sum / (gui * simds));
+      if (m->by_xcc.size() > 1) {
+        const double per = simds / m->by_xcc.size();
+        for (double v : m->by_xcc) d.xcd_mfma_busy.push_back(std::min(100.0, 100.0 * v / (gui * per)));
+      }
+    }
+  }
+  if (gui > 0 && cus > 0)
+    if (const PmcReduced* w = get("SQ_WAVE_CYCLES")) d.occupancy = std::min(100.0, 400.0 * w->sum / gui / cus / waves);
+  if (const PmcReduced* c = get("GRBM_COUNT"); c && c->max > 0) d.gui_active = std::min(100.0, 100.0 * gui / c->max);
+  return d;
+}
+
+// ---------------------------------------------------------------------------------------------
+
+OnDevice::OnDevice(Exporter* ex, OnDeviceConfig cfg) : ex_(ex), cfg_(std::move(cfg)) {
+  cfg_.pmc_window_s = std::max(0.001, std::min(cfg_.pmc_window_s, cfg_.pmc_every_s * 0.5));
+  cfg_.probe_timeout_s = std::min(cfg_.probe_timeout_s, cfg_.probe_every_s);
+}
+
+OnDevice::~OnDevice() { stop(); }
+
+bool OnDevice::start(std::string* err) {
+  const std::string dir = cfg_.plugin_dir.empty() ? default_plugin_dir() : cfg_.plugin_dir;
+  char ebuf[512] = {0};
+  if (cfg_.pmc) {
+    pmc_lib_ = load_plugin(dir, "libgpumon_pmc.so", true, err);
+    if (!pmc_lib_) return false;
+    const int n = pmc_lib_->pmc_init(ebuf, sizeof ebuf);
+    if (n < 0) {
+      *err = std::string("pmc init: ") + ebuf;
+      pmc_lib_.reset();
+      return false;
+    }
+    gpumon_pmc_agent_t a{};
+    for (int i = 0; i < n && pmc_lib_->pmc_agent(i, &a) == 0; ++i) {
+      PmcAgentInfo ai;
+      ai.cu_count = a.cu_count;
+      ai.simd_count = a.simd_count;
+      ai.num_xcc = a.num_xcc;
+      ai.max_waves_per_cu = a.max_waves_per_cu;
+      ai.drm_render_minor = a.drm_render_minor;
+      agents_.push_back(ai);
+    }
+    map_pmc_agents();
+    GPUMON_LOG(LogLevel::kInfo, "ondevice",
+               "pmc plugin " + pmc_lib_->path + " agents=" + std::to_string(agents_.size()) +
+                   " mapped=" + std::to_string(pmc_map_.size()));
+  }
+  if (cfg_.probe) {
+    probe_lib_ = load_plugin(dir, "libgpumon_probe.so", false, err);
+    if (!probe_lib_) {
+      pmc_lib_.reset();
+      return false;
+    }
+    const int n_hip = probe_lib_->probe_count();
+    for (const auto& s : ex_->statics()) {
+      if (s.hip_id < 0 || s.hip_id >= n_hip) continue;
+      ProbeDev d;
+      d.dev = s.index;
+      d.handle = probe_lib_->probe_create(s.hip_id, cfg_.probe_blocks, 4, cfg_.probe_spin_ticks, ebuf, sizeof ebuf);
+      if (!d.handle) {
+        *err = std::string("probe create on hip device ") + std::to_string(s.hip_id) + ": " + ebuf;
+        for (auto& p : probes_) probe_lib_->probe_destroy(static_cast<gpumon_probe*>(p.handle));
+        probes_.clear();
+        return false;
+      }
+      probes_.push_back(std::move(d));
+    }
+    GPUMON_LOG(LogLevel::kInfo, "ondevice",
+               "probe plugin " + probe_lib_->path + " devices=" + std::to_string(probes_.size()));
+  }
+  running_ = true;
+  if (pmc_lib_) pmc_th_ = std::thread([this] { pmc_loop(); });
+  if (probe_lib_) probe_th_ = std::thread([this] { probe_loop(); });
+  return true;
+}
+
+void OnDevice::stop() {
+  if (running_.exchange(false)) {
+    wait_cv_.notify_all();
+  }
+  if (pmc_th_.joinable()) pmc_th_.join();
+  if (probe_th_.joinable()) probe_th_.join();
+  if (probe_lib_) {
+    std::lock_guard<std::mutex> g(probe_mu_);
+    gpumon_probe_result_t r{};
+    for (auto& p : probes_) {
+      // drain the in-flight launch before its pinned ring is freed
+      if (p.pending >= 0) probe_lib_->probe_wait(static_cast<gpumon_probe*>(p.handle), p.pending, 2.0, &r);
+      probe_lib_->probe_destroy(static_cast<gpumon_probe*>(p.handle));
+    }
+    probes_.clear();
+    ex_->set_extra("probe", {});
+  }
+  if (pmc_lib_) ex_->set_extra("pmc", {});
+}
+
+bool OnDevice::step() {
+  if (pmc_lib_) pmc_step();
+  if (probe_lib_) probe_step();
+  return pmc_lib_ || probe_lib_;
+}
+
+OnDevice::Stats OnDevice::stats() const {
+  Stats s;
+  s.pmc_samples = pmc_samples_;
+  s.pmc_errors = pmc_errors_;
+  s.probe_done = probe_done_;
+  s.probe_timeouts = probe_timeouts_;
+  s.pmc_agents = static_cast<int>(agents_.size());
+  s.probe_devices = static_cast<int>(probes_.size());
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// PMC
+
+void OnDevice::map_pmc_agents() {
+  pmc_map_.clear();
+  for (const auto& s : ex_->statics()) {
+    for (size_t ai = 0; ai < agents_.size(); ++ai) {
+      if ((s.drm_render >= 0 && s.drm_render == agents_[ai].drm_render_minor) ||
+          (s.drm_render < 0 && static_cast<int>(ai) == s.index)) {
+        pmc_map_[s.index] = static_cast<int>(ai);
+        break;
+      }
+    }
+  }
+}
+
+void OnDevice::pmc_step() {
+  std::lock_guard<std::mutex> g(pmc_mu_);
+  if (pmc_map_.empty()) map_pmc_agents();  // backend came up after start()
+  if (pmc_map_.empty()) return;
+  std::vector<int> devs, ags;
+  for (const auto& kv : pmc_map_) {
+    devs.push_back(kv.first);
+    ags.push_back(kv.second);
+  }
+  std::vector<const char*> names;
+  for (const auto& c : cfg_.pmc_counters) names.push_back(c.c_str());
+  std::vector<gpumon_pmc_value_t> vals(devs.size() * names.size());
+  std::vector<int32_t> ok(devs.size(), 0);
+  char ebuf[512] = {0};
+  // every GPU counts over ONE shared window (8 GPUs: one window, not eight)
+  const int rc = pmc_lib_->pmc_sample_many(ags.data(), static_cast<int>(ags.size()), names.data(),
+                                           static_cast<int>(names.size()), cfg_.pmc_window_s, vals.data(), ok.data(),
+                                           ebuf, sizeof ebuf);
+  if (rc != 0) {
+    pmc_errors_ += devs.size();
+    GPUMON_LOG(LogLevel::kWarn, "ondevice", std::string("pmc sample failed: ") + ebuf);
+  } else {
+    for (size_t k = 0; k < devs.size(); ++k) {
+      if (!ok[k]) {
+        pmc_errors_++;
+        continue;
+      }
+      std::map<std::string, PmcReduced> raw;
+      for (size_t c = 0; c < names.size(); ++c) {
+        const auto& v = vals[k * names.size() + c];
+        if (!v.ok) continue;
+        PmcReduced r;
+        r.sum = v.sum;
+        r.max = v.max;
+        r.n = v.n;
+        r.by_xcc.assign(v.by_xcc, v.by_xcc + std::max(0, std::min<int>(v.n_xcc, GPUMON_PMC_MAX_XCC)));
+        raw[cfg_.pmc_counters[c]] = std::move(r);
+      }
+      pmc_last_[devs[k]] = pmc_derive(raw, agents_[ags[k]]);
+      pmc_samples_++;
+    }
+  }
+  export_pmc();
+}
+
+void OnDevice::export_pmc() {
+  std::vector<ExtraSeries> out;
+  for (const auto& kv : pmc_last_) {
+    const int dev = kv.first;
+    const PmcDerived& d = kv.second;
+    if (!std::isnan(d.mfma_busy))
+      out.push_back(xs("gpu_mfma_busy_percent", "MFMA pipe busy % (rocprofiler device counting).", dev, d.mfma_busy));
+    for (size_t x = 0; x < d.xcd_mfma_busy.size(); ++x) {
+      out.push_back(xs("gpu_xcd_mfma_busy_percent", "MFMA pipe busy % per XCD.", dev, d.xcd_mfma_busy[x]));
+      out.back().labels.push_back({"xcd", std::to_string(x)});
+    }
+    if (!std::isnan(d.occupancy))
+      out.push_back(xs("gpu_occupancy_percent", "Resident waves / max waves % (rocprofiler device counting).", dev,
+                       d.occupancy));
+    if (!std::isnan(d.gui_active))
+      out.push_back(xs("gpu_gui_active_percent", "GRBM GUI active % of the counting window.", dev, d.gui_active));
+    out.push_back(xs("gpu_pmc_window_seconds", "PMC counting window per sample.", dev, cfg_.pmc_window_s));
+  }
+  out.push_back(xs("gpumon_pmc_errors_total", "Failed PMC samples.", -1, static_cast<double>(pmc_errors_.load()),
+                   "counter"));
+  ex_->set_extra("pmc", std::move(out));
+}
+
+void OnDevice::pmc_loop() {
+  while (running_) {
+    const int64_t t0 = mono_ns();
+    pmc_step();
+    const double left = cfg_.pmc_every_s - (mono_ns() - t0) * 1e-9;
+    std::unique_lock<std::mutex> lk(wait_mu_);
+    wait_cv_.wait_for(lk, std::chrono::duration<double>(std::max(0.0, left)), [this] { return !running_; });
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K1 probe
+
+void OnDevice::probe_step() {
+  std::lock_guard<std::mutex> g(probe_mu_);
+  for (auto& p : probes_)
+    if (p.pending < 0) p.pending = probe_lib_->probe_launch(static_cast<gpumon_probe*>(p.handle));
+  const int64_t deadline = mono_ns() + static_cast<int64_t>(cfg_.probe_timeout_s * 1e9);
+  for (auto& p : probes_) {
+    if (p.pending < 0) continue;
+    gpumon_probe_result_t r{};
+    const double left = std::max(0.0, (deadline - mono_ns()) * 1e-9);
+    if (probe_lib_->probe_wait(static_cast<gpumon_probe*>(p.handle), p.pending, left, &r) == 1) {
+      p.pending = -1;
+      p.have = true;
+      p.latency_s = r.host_latency_s;
+      p.span_s = r.gpu_span_s;
+      p.unique_cus = r.unique_cus;
+      p.xcc_blocks.assign(r.xcc_blocks, r.xcc_blocks + GPUMON_PROBE_MAX_XCC);
+      p.xcc_mhz.assign(r.xcc_clock_mhz, r.xcc_clock_mhz + GPUMON_PROBE_MAX_XCC);
+      probe_done_++;
+    } else {
+      p.timeouts++;
+      probe_timeouts_++;
+    }
+  }
+  export_probe();
+}
+
+void OnDevice::export_probe() {
+  std::vector<ExtraSeries> out;
+  for (const auto& p : probes_) {
+    out.push_back(xs("gpu_probe_pending", "1 if the last probe launch has not completed yet.", p.dev,
+                     p.pending >= 0 ? 1 : 0));
+    out.push_back(xs("gpu_probe_timeouts_total", "Probe polls that timed out (GPU saturated or hung).", p.dev,
+                     static_cast<double>(p.timeouts), "counter"));
+    if (!p.have) continue;
+    out.push_back(xs("gpu_probe_latency_seconds", "Probe host launch -> all workgroups arrived (pinned ring).", p.dev,
+                     p.latency_s));
+    out.push_back(xs("gpu_probe_kernel_span_seconds", "Probe first start -> last end on the GPU 100 MHz clock.", p.dev,
+                     p.span_s));
+    out.push_back(xs("gpu_probe_unique_cus", "Distinct compute units that ran probe workgroups.", p.dev, p.unique_cus));
+    for (size_t x = 0; x < p.xcc_blocks.size(); ++x) {
+      if (!p.xcc_blocks[x]) continue;
+      out.push_back(xs("gpu_probe_xcd_blocks", "Probe workgroups executed per XCD (liveness).", p.dev, p.xcc_blocks[x]));
+      out.back().labels.push_back({"xcd", std::to_string(x)});
+      out.push_back(xs("gpu_probe_xcd_clock_mhz", "Effective shader clock per XCD measured in-kernel.", p.dev,
+                       p.xcc_mhz[x]));
+      out.back().labels.push_back({"xcd", std::to_string(x)});
+    }
+  }
+  ex_->set_extra("probe", std::move(out));
+}
+
+void OnDevice::probe_loop() {
+  while (running_) {
+    const int64_t t0 = mono_ns();
+    probe_step();
+    const double left = cfg_.probe_every_s - (mono_ns() - t0) * 1e-9;
+    std::unique_lock<std::mutex> lk(wait_mu_);
+    wait_cv_.wait_for(lk, std::chrono::duration<double>(std::max(0.0, left)), [this] { return !running_; });
+  }
+}
+
+}  // namespace gpumon

@@ -1,0 +1,127 @@
+// On-device samplers of the native exporter: rocprofiler-sdk device counting (MFMA busy /
+// occupancy) and the K1 gfx950 probe microkernel, each in its own thread, publishing through
+// Exporter::set_extra() like every other out-of-band source.
+//
+// Neither is linked: both live in plugins (csrc/plugins/ondevice_abi.h) that this file dlopen()s
+// from <dir of this binary or .so>/../lib, or GPUMON_PLUGIN_DIR. The exporter binary therefore
+// runs on a node without HIP or rocprofiler-sdk and only loads them when --pmc / --probe ask — the
+// role the reference gives its vendored libltdl.so.7 (/root/reference/Dockerfile:4):
+// keep the agent independent of the host's tool-library ABI.
+//
+// Series and formulas match gpumon/ops/pmc.py and gpumon/ops/probe.py (the Python runners used by
+// `gpumon serve --enable-pmc/--enable-probe`), so dashboards see the same families from either path.
+#pragma once
+
+#include <atomic>
+#include <condition_variable>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "render.h"
+#include "sample.h"
+
+namespace gpumon {
+
+class Exporter;
+
+struct OnDeviceConfig {
+  std::string plugin_dir;   // "" = $GPUMON_PLUGIN_DIR or <dir of this object>/../lib
+  bool pmc = false;
+  std::vector<std::string> pmc_counters = {"SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE",
+                                           "GRBM_COUNT"};
+  double pmc_every_s = 1.0;
+  double pmc_window_s = 0.1;  // counting window per sample (capped at half the period)
+  bool probe = false;
+  double probe_every_s = 1.0;
+  int probe_blocks = 1024;    // one-wave workgroups per launch (>= 4 per CU spreads over all 8 XCDs)
+  int probe_spin_ticks = 200;
+  double probe_timeout_s = 0.5;
+};
+
+// Reduced counter values of one agent (sum / max over instances, per-XCC sums).
+struct PmcReduced {
+  double sum = 0, max = 0;
+  uint64_t n = 0;
+  std::vector<double> by_xcc;
+};
+
+struct PmcAgentInfo {
+  uint32_t cu_count = 0, simd_count = 0, num_xcc = 0, max_waves_per_cu = 0;
+  int drm_render_minor = -1;
+};
+
+// NaN = not derivable from the counters given.
+struct PmcDerived {
+  double mfma_busy = kNaN, occupancy = kNaN, gui_active = kNaN;
+  std::vector<double> xcd_mfma_busy;
+};
+
+// Pure (CPU-tested against gpumon.ops.pmc.derive): the gfx9xx formulas ROCm 7.2 falls back to on gfx950.
+PmcDerived pmc_derive(const std::map<std::string, PmcReduced>& raw, const PmcAgentInfo& agent);
+
+// Directory the plugins are looked up in (see OnDeviceConfig::plugin_dir).
+std::string default_plugin_dir();
+
+class OnDevice {
+ public:
+  OnDevice(Exporter* ex, OnDeviceConfig cfg);
+  ~OnDevice();
+  // Loads and initialises the enabled plugins (PMC before the probe: rocprofiler must register before
+  // the HIP runtime initialises HSA) and starts their threads. False + err when a requested plugin
+  // cannot be loaded; nothing is left running then.
+  bool start(std::string* err);
+  void stop();
+  // One synchronous step of each enabled sampler (tests, --once); returns false if none is enabled.
+  bool step();
+
+  struct Stats {
+    uint64_t pmc_samples = 0, pmc_errors = 0, probe_done = 0, probe_timeouts = 0;
+    int pmc_agents = 0, probe_devices = 0;
+  };
+  Stats stats() const;
+
+  struct Plugin;  // dlopen'd function table (ondevice.cpp)
+
+ private:
+  void pmc_loop();
+  void probe_loop();
+  void pmc_step();
+  void probe_step();
+  void map_pmc_agents();
+  void export_pmc();
+  void export_probe();
+
+  Exporter* ex_;
+  OnDeviceConfig cfg_;
+  std::unique_ptr<Plugin> pmc_lib_, probe_lib_;
+
+  std::mutex pmc_mu_, probe_mu_;
+  std::vector<PmcAgentInfo> agents_;
+  std::map<int, int> pmc_map_;  // exporter device index -> pmc agent index
+  std::map<int, PmcDerived> pmc_last_;
+
+  struct ProbeDev {
+    int dev = 0;
+    void* handle = nullptr;
+    int pending = -1;   // slot in flight, -1 none
+    uint64_t timeouts = 0;
+    bool have = false;
+    double latency_s = 0, span_s = 0;
+    int unique_cus = 0;
+    std::vector<int> xcc_blocks;
+    std::vector<double> xcc_mhz;
+  };
+  std::vector<ProbeDev> probes_;
+
+  std::atomic<bool> running_{false};
+  std::mutex wait_mu_;
+  std::condition_variable wait_cv_;
+  std::thread pmc_th_, probe_th_;
+  std::atomic<uint64_t> pmc_samples_{0}, pmc_errors_{0}, probe_done_{0}, probe_timeouts_{0};
+};
+
+}  // namespace gpumon

@@ -11,12 +11,14 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <thread>
 
 #include "core/common.h"
 #include "core/exporter.h"
+#include "core/ondevice.h"
 
 using namespace gpumon;
 
@@ -32,6 +34,8 @@ static void usage() {
           "                       [--procfs /proc] [--no-processes] [--no-gzip] [--sample-threads N]\n"
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx] [--once]\n"
           "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri]\n"
+          "                       [--pmc] [--pmc-counters A,B,..] [--pmc-window SEC] [--probe] [--probe-every N]\n"
+          "                       [--probe-blocks N] [--plugin-dir DIR]\n"
           "env: NODE_NAME, INFLUXDB_URL, GPUMON_LISTEN, GPUMON_INTERVAL, GPUMON_BACKEND\n");
 }
 
@@ -43,6 +47,8 @@ int main(int argc, char** argv) {
   if (const char* v = getenv("GPUMON_INTERVAL")) cfg.interval_s = atof(v);
   std::string listen = getenv("GPUMON_LISTEN") ? getenv("GPUMON_LISTEN") : "0.0.0.0:9400";
   bool once = false;
+  OnDeviceConfig od;
+  int probe_every = 1;
   // kubelet PodResources: on by default when the socket is mounted (deploy/k8s DaemonSet)
   std::string podres = "/var/lib/kubelet/pod-resources/kubelet.sock";
   std::string cri;  // "" = first existing well-known runtime socket, "none" = off
@@ -81,6 +87,13 @@ int main(int argc, char** argv) {
     else if (a == "--sample-threads") cfg.sample_threads = atoi(next().c_str());
     else if (a == "--http-threads") cfg.http_threads = atoi(next().c_str());
     else if (a == "--once") once = true;
+    else if (a == "--pmc") od.pmc = true;
+    else if (a == "--pmc-counters") od.pmc_counters = split(next(), ',');
+    else if (a == "--pmc-window") od.pmc_window_s = atof(next().c_str());
+    else if (a == "--probe") od.probe = true;
+    else if (a == "--probe-every") probe_every = std::max(1, atoi(next().c_str()));
+    else if (a == "--probe-blocks") od.probe_blocks = atoi(next().c_str());
+    else if (a == "--plugin-dir") od.plugin_dir = next();
     else if (a == "--log-level") {
       std::string l = next();
       g_log_level = l == "debug" ? 0 : l == "info" ? 1 : l == "warn" ? 2 : 3;
@@ -107,6 +120,10 @@ int main(int argc, char** argv) {
       }
   }
   if (!cri.empty() && cri != "none") cfg.cri_socket = cri;
+  // on-device samplers run at the sampler cadence (the probe every N ticks)
+  const double period = cfg.interval_s > 0 ? std::max(cfg.interval_s, 0.1) : 1.0;
+  od.pmc_every_s = period;
+  od.probe_every_s = period * probe_every;
 
   if (once) {
     cfg.serve_http = false;
@@ -117,7 +134,13 @@ int main(int argc, char** argv) {
       fprintf(stderr, "start failed: %s\n", err.c_str());
       return 1;
     }
-    e.tick();  // second tick so rates are populated
+    OnDevice ondev(&e, od);
+    if ((od.pmc || od.probe) && !ondev.start(&err)) {
+      fprintf(stderr, "on-device samplers: %s\n", err.c_str());
+      return 1;
+    }
+    ondev.step();
+    e.tick();  // second tick so rates are populated (and the on-device series are rendered)
     auto s = e.snapshot();
     fwrite(s->body.data(), 1, s->body.size(), stdout);
     e.stop();
@@ -134,10 +157,21 @@ int main(int argc, char** argv) {
     return 1;
   }
   if (!err.empty()) GPUMON_LOG(LogLevel::kWarn, "main", "backend not ready (retrying): " + err);
+  OnDevice ondev(&e, od);
+  if (od.pmc || od.probe) {
+    std::string oerr;
+    if (!ondev.start(&oerr)) {
+      // fail loudly: a DaemonSet asked for PMC / probe series and would otherwise silently lack them
+      fprintf(stderr, "on-device samplers: %s\n", oerr.c_str());
+      e.stop();
+      return 1;
+    }
+  }
   GPUMON_LOG(LogLevel::kInfo, "main",
              "serving http://" + cfg.listen_addr + ":" + std::to_string(e.port()) +
                  "/metrics host=" + cfg.host + " interval=" + std::to_string(cfg.interval_s) + "s");
   while (!g_stop) std::this_thread::sleep_for(std::chrono::milliseconds(200));
+  ondev.stop();
   e.stop();
   return 0;
 }

@@ -1,0 +1,162 @@
+// Fake on-device plugins (both C ABIs of csrc/plugins/ondevice_abi.h) for CPU tests of the native
+// PMC / probe samplers (csrc/core/ondevice.cpp) through the same dlopen path the exporter uses on a
+// GPU node. Built twice, as build/fakes/ondevice/libgpumon_pmc.so and libgpumon_probe.so.
+//
+// Scripted by environment:
+//   GPUMON_FAKE_AGENTS      GPU agents / HIP devices (default 1)
+//   GPUMON_FAKE_MFMA        MFMA busy fraction 0..1 (default 0.5), spread evenly over 8 XCCs
+//   GPUMON_FAKE_OCC         occupancy fraction 0..1 (default 0.25)
+//   GPUMON_FAKE_PMC_FAIL    "init" -> init fails; "sample" -> every sample reports not-ok
+//   GPUMON_FAKE_PROBE_HANG  1 -> launches never complete (timeouts path)
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <chrono>
+
+#include "../plugins/ondevice_abi.h"
+
+#define EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+int agents() {
+  const char* e = getenv("GPUMON_FAKE_AGENTS");
+  return e ? atoi(e) : 1;
+}
+double envd(const char* k, double d) {
+  const char* e = getenv(k);
+  return e ? atof(e) : d;
+}
+bool fail(const char* what) {
+  const char* e = getenv("GPUMON_FAKE_PMC_FAIL");
+  return e && strcmp(e, what) == 0;
+}
+constexpr uint32_t kCus = 256, kSimds = 1024, kXcc = 8, kWaves = 32;
+constexpr double kClock = 2.4e9;
+}  // namespace
+
+EXPORT int gpumon_pmc_abi_version(void) { return GPUMON_ONDEVICE_ABI; }
+
+EXPORT int gpumon_pmc_init(char* err, size_t errlen) {
+  if (fail("init")) {
+    snprintf(err, errlen, "fake: device counting unavailable");
+    return -1;
+  }
+  return agents();
+}
+
+EXPORT int gpumon_pmc_agent(int agent, gpumon_pmc_agent_t* out) {
+  if (agent < 0 || agent >= agents() || !out) return -1;
+  *out = gpumon_pmc_agent_t{};
+  out->node_id = 2 + agent;
+  out->logical_node_id = 1 + agent;
+  out->drm_render_minor = 128 + agent;
+  out->cu_count = kCus;
+  out->simd_count = kSimds;
+  out->num_xcc = kXcc;
+  out->max_waves_per_cu = kWaves;
+  snprintf(out->name, sizeof out->name, "gfx950");
+  snprintf(out->product_name, sizeof out->product_name, "fake MI355X");
+  return 0;
+}
+
+EXPORT size_t gpumon_pmc_supported(int, char* buf, size_t n) {
+  const char* s = "GRBM_COUNT\nGRBM_GUI_ACTIVE\nSQ_VALU_MFMA_BUSY_CYCLES\nSQ_WAVE_CYCLES\n";
+  if (buf && n) snprintf(buf, n, "%s", s);
+  return strlen(s) + 1;
+}
+
+EXPORT size_t gpumon_pmc_dimensions(int, const char*, char* buf, size_t n) {
+  const char* s = "DIMENSION_XCC:8\n";
+  if (buf && n) snprintf(buf, n, "%s", s);
+  return strlen(s) + 1;
+}
+
+EXPORT int gpumon_pmc_sample_many(const int* ags, int n_agents, const char* const* counters, int n_counters,
+                                  double window_s, gpumon_pmc_value_t* out, int32_t* ok, char* err, size_t errlen) {
+  for (int k = 0; k < n_agents; ++k)
+    if (ags[k] < 0 || ags[k] >= agents()) {
+      snprintf(err, errlen, "pmc agent index");
+      return -1;
+    }
+  std::this_thread::sleep_for(std::chrono::duration<double>(window_s));
+  const double gui = window_s * kClock;
+  for (int k = 0; k < n_agents; ++k) {
+    ok[k] = fail("sample") ? 0 : 1;
+    for (int c = 0; c < n_counters; ++c) {
+      gpumon_pmc_value_t& v = out[k * n_counters + c];
+      v = gpumon_pmc_value_t{};
+      if (!ok[k]) continue;
+      std::string name = counters[c];
+      double total = 0;
+      bool per_xcc = true;
+      if (name == "GRBM_GUI_ACTIVE" || name == "GRBM_COUNT") {
+        total = gui;
+        per_xcc = false;
+      } else if (name == "SQ_VALU_MFMA_BUSY_CYCLES") {
+        total = envd("GPUMON_FAKE_MFMA", 0.5) * gui * kSimds;
+      } else if (name == "SQ_WAVE_CYCLES") {
+        total = envd("GPUMON_FAKE_OCC", 0.25) * gui * kCus * kWaves / 4.0;
+      } else {
+        snprintf(err, errlen, "counter not supported: %s", name.c_str());
+        return -1;
+      }
+      v.ok = 1;
+      if (per_xcc) {
+        v.n = kXcc;
+        v.n_xcc = kXcc;
+        for (uint32_t x = 0; x < kXcc; ++x) v.by_xcc[x] = total / kXcc;
+        v.sum = total;
+        v.max = total / kXcc;
+      } else {
+        v.n = kXcc;  // GRBM is replicated per XCC: max is the device value
+        v.sum = total * kXcc;
+        v.max = total;
+      }
+    }
+  }
+  return 0;
+}
+
+// ---- probe ----------------------------------------------------------------------------------
+struct gpumon_probe {
+  int dev;
+  int blocks;
+  uint32_t seq;
+};
+
+EXPORT int gpumon_probe_abi_version(void) { return GPUMON_ONDEVICE_ABI; }
+EXPORT int gpumon_probe_device_count(void) { return agents(); }
+EXPORT size_t gpumon_probe_device_arch(int, char* buf, size_t n) {
+  if (buf && n) snprintf(buf, n, "gfx950:sramecc+:xnack-");
+  return 23;
+}
+EXPORT gpumon_probe* gpumon_probe_create(int dev, int blocks, int, int, char* err, size_t errlen) {
+  if (dev < 0 || dev >= agents()) {
+    snprintf(err, errlen, "fake: no hip device %d", dev);
+    return nullptr;
+  }
+  return new gpumon_probe{dev, blocks, 0};
+}
+EXPORT int gpumon_probe_launch(gpumon_probe* p) { return p ? static_cast<int>(p->seq++ % 4) : -1; }
+EXPORT int gpumon_probe_wait(gpumon_probe* p, int, double timeout_s, gpumon_probe_result_t* out) {
+  if (!p || !out) return 0;
+  if (getenv("GPUMON_FAKE_PROBE_HANG")) {
+    std::this_thread::sleep_for(std::chrono::duration<double>(timeout_s));
+    return 0;
+  }
+  *out = gpumon_probe_result_t{};
+  out->seq = p->seq;
+  out->blocks = p->blocks;
+  out->arrived = p->blocks;
+  out->host_latency_s = 25e-6;
+  out->gpu_span_s = 6e-6;
+  out->unique_cus = kCus;
+  for (uint32_t x = 0; x < kXcc; ++x) {
+    out->xcc_blocks[x] = p->blocks / kXcc;
+    out->xcc_clock_mhz[x] = 2400.0 - 10.0 * x;
+  }
+  return 1;
+}
+EXPORT void gpumon_probe_destroy(gpumon_probe* p) { delete p; }

@@ -60,9 +60,7 @@ def cmd_once(args) -> int:
     _setup_logging(cfg.log_level)
     with GpuMonitor(cfg) as mon:
         time.sleep(0.05)
-        for plugin in (mon.pmc, mon.probe):  # make sure device plugins contributed to this sample
-            if plugin is not None:
-                plugin.step()
+        mon.step_ondevice()  # make sure the PMC / probe samplers contributed to this sample
         mon.tick()  # second tick: rates populated
         if args.format == "influx":
             sys.stdout.write(mon.ex.influx_text())

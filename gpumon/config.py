@@ -74,6 +74,8 @@ class Config:
     enable_probe: bool = False
     probe_every: int = 1
     enable_pmc: bool = False
+    ondevice: str = "native"              # native (C++ samplers over lib/ plugins) | python (gpumon/ops runners)
+    plugin_dir: str = ""                  # "" = <tree>/lib or $GPUMON_PLUGIN_DIR
     roctx: bool = False                   # ROCTx ranges around sampler phases (rocprofv3 --marker-trace)
     # the counters gpumon.ops.pmc.derive() needs (2 SQ + 2 GRBM slots: one counting pass on gfx950)
     pmc_counters: List[str] = field(default_factory=lambda: ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES",
@@ -227,6 +229,9 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
                    help="seconds before a device call is exported as hung (gpu_up 0)")
     p.add_argument("--enable-probe-kernel", dest="enable_probe", action="store_true", default=None)
     p.add_argument("--enable-pmc", dest="enable_pmc", action="store_true", default=None)
+    p.add_argument("--ondevice", dest="ondevice", choices=["native", "python"],
+                   help="who drives the PMC / probe samplers: native (C++ threads over lib/ plugins) or python")
+    p.add_argument("--plugin-dir", dest="plugin_dir", help="directory holding libgpumon_pmc.so / libgpumon_probe.so")
     p.add_argument("--no-fast-path", dest="fast_path", action="store_false", default=None,
                    help="amdsmi: read every value through libamd_smi (disable the sysfs/KFD fast path)")
     p.add_argument("--sysfs-root", dest="sysfs_root")

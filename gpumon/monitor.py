@@ -58,6 +58,7 @@ class GpuMonitor:
         self.plane = None
         self.probe = None
         self.pmc = None
+        self.ondevice = None   # _core.OnDevice when cfg.ondevice == "native"
         self._want_plane = mode == "python"
         self.start_error = ""
 
@@ -72,19 +73,41 @@ class GpuMonitor:
             plane = ControlPlane(self.ex, self.cfg)
             if plane.enabled:
                 self.plane = plane.start()
+        if self.cfg.enable_pmc or self.cfg.enable_probe:
+            self._start_ondevice()
+        return self
+
+    def _start_ondevice(self) -> None:
+        period = max(self.cfg.interval, 0.1)
+        if self.cfg.ondevice == "native":
+            # C++ threads over the same plugins the standalone binary dlopen()s (csrc/core/ondevice.h);
+            # PMC initialises before the probe (rocprofiler must register before HIP brings HSA up).
+            self.ondevice = self._core.OnDevice(self.ex, {
+                "plugin_dir": self.cfg.plugin_dir, "pmc": bool(self.cfg.enable_pmc),
+                "pmc_counters": list(self.cfg.pmc_counters), "pmc_every_s": period,
+                "probe": bool(self.cfg.enable_probe), "probe_every_s": period * self.cfg.probe_every})
+            self.ondevice.start()
+            return
         # PMC first: rocprofiler must register before anything in this process initialises HSA/HIP.
         if self.cfg.enable_pmc:
             from .ops.pmc import PmcRunner
 
-            self.pmc = PmcRunner(self.ex, self.cfg.pmc_counters, every_s=max(self.cfg.interval, 0.1)).start()
+            self.pmc = PmcRunner(self.ex, self.cfg.pmc_counters, every_s=period).start()
         if self.cfg.enable_probe:
             from .ops.probe import ProbeRunner
 
-            self.probe = ProbeRunner(self.ex, every_s=max(self.cfg.interval, 0.1) * self.cfg.probe_every).start()
-        return self
+            self.probe = ProbeRunner(self.ex, every_s=period * self.cfg.probe_every).start()
+
+    def step_ondevice(self) -> None:
+        """One synchronous PMC / probe step (so a one-shot sample carries their series)."""
+        if self.ondevice is not None:
+            self.ondevice.step()
+        for plugin in (self.pmc, self.probe):
+            if plugin is not None:
+                plugin.step()
 
     def stop(self) -> None:
-        for p in (self.pmc, self.probe, self.plane):
+        for p in (self.ondevice, self.pmc, self.probe, self.plane):
             if p is not None:
                 try:
                     p.stop()

@@ -36,3 +36,43 @@ def test_native_binary_once():
     fam = promtext.parse(r.stdout)
     assert promtext.values(fam, "node_gpu_gpu_util", host="box")
     assert len(promtext.values(fam, "gpu_xcd_busy_percent")) >= 8
+
+
+def test_once_python_runners():
+    """The Python runners (gpumon/ops) over the same plugins: identical families."""
+    r = subprocess.run([sys.executable, "-m", "gpumon", "once", "--backend", "amdsmi", "--devices", "0",
+                        "--enable-pmc", "--enable-probe-kernel", "--ondevice", "python", "--log-level", "warn"],
+                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    fam = promtext.parse(r.stdout)
+    assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
+    assert promtext.values(fam, "gpu_mfma_busy_percent", gpu_id="0")
+
+
+def test_native_binary_pmc_probe_under_mfma_load():
+    """bin/gpumon-exporter --pmc --probe: the C++ samplers dlopen lib/libgpumon_{pmc,probe}.so (no
+    Python in the exporter process) and see a bf16 MFMA burn running in another process."""
+    exe = os.path.join(ROOT, "bin", "gpumon-exporter")
+    load = subprocess.Popen([sys.executable, "-m", "gpumon", "load", "--kind", "mfma", "--seconds", "15"],
+                            cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        import time
+
+        time.sleep(8)  # torch-free, but the HIP module load + first launches take a few seconds
+        assert load.poll() is None, load.stderr.read()[-2000:]
+        r = subprocess.run([exe, "--backend", "amdsmi", "--once", "--host", "box", "--pmc", "--probe",
+                            "--pmc-window", "0.2", "--log-level", "warn"], capture_output=True, text=True,
+                           timeout=120)
+    finally:
+        try:
+            load.wait(60)  # let the burn finish on its own (no kill mid-kernel)
+        except subprocess.TimeoutExpired:
+            load.kill()
+            load.wait(30)
+    assert r.returncode == 0, r.stderr[-2000:]
+    fam = promtext.parse(r.stdout)
+    assert promtext.one(fam, "gpu_mfma_busy_percent", gpu_id="0") > 50
+    assert len(promtext.values(fam, "gpu_xcd_mfma_busy_percent", gpu_id="0")) == 8
+    assert promtext.one(fam, "gpu_pmc_window_seconds", gpu_id="0") == pytest.approx(0.2)
+    assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
+    assert promtext.one(fam, "gpu_probe_unique_cus", gpu_id="0") > 200

@@ -1,0 +1,216 @@
+"""Native on-device samplers (csrc/core/ondevice.cpp) on CPU, through the same dlopen path the
+exporter uses on a GPU node, against the fake plugins of csrc/fakes/fake_ondevice.cpp.
+
+The real plugins (lib/libgpumon_pmc.so, lib/libgpumon_probe.so) are covered on the MI355X by
+tests/test_gpu_pmc.py and tests/test_gpu_cli.py."""
+
+import os
+import re
+import subprocess
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from conftest import ROOT, make_locked
+from gpumon.ops.pmc import derive
+
+FAKE_DIR = os.path.join(ROOT, "build", "fakes", "ondevice")
+BIN = os.path.join(ROOT, "bin", "gpumon-exporter")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def fakes():
+    make_locked("fakes")
+    make_locked("core")
+
+
+def _val(text, name, **labels):
+    for line in text.splitlines():
+        if not line.startswith(name + "{"):
+            continue
+        if all(f'{k}="{v}"' in line for k, v in labels.items()):
+            return float(line.rsplit(" ", 1)[1])
+    return None
+
+
+def _ondevice(core, ex, **over):
+    cfg = {"plugin_dir": FAKE_DIR, "pmc": True, "probe": True, "pmc_every_s": 0.2, "probe_every_s": 0.2,
+           "pmc_window_s": 0.01}
+    cfg.update(over)
+    return core.OnDevice(ex, cfg)
+
+
+# ---------------------------------------------------------------- derivation parity (C++ vs Python)
+AGENT = {"cu_count": 256, "simd_count": 1024, "max_waves_per_cu": 32, "num_xcc": 8}
+_pos = st.floats(min_value=0, max_value=1e12, allow_nan=False)
+
+
+@settings(max_examples=200, deadline=None)
+@given(gui=_pos, cnt=_pos, mfma=_pos, waves=_pos, nx=st.integers(0, 8), has=st.lists(st.booleans(), min_size=4,
+                                                                                     max_size=4))
+def test_pmc_derive_matches_python(gui, cnt, mfma, waves, nx, has):
+    raw = {}
+    if has[0]:
+        raw["GRBM_GUI_ACTIVE"] = {"sum": gui * 8, "max": gui, "n": 8, "by_xcc": []}
+    if has[1]:
+        raw["GRBM_COUNT"] = {"sum": cnt * 8, "max": cnt, "n": 8, "by_xcc": []}
+    if has[2]:
+        raw["SQ_VALU_MFMA_BUSY_CYCLES"] = {"sum": mfma, "max": mfma, "n": 8, "by_xcc": [mfma / nx] * nx if nx else []}
+    if has[3]:
+        raw["SQ_WAVE_CYCLES"] = {"sum": waves, "max": waves, "n": 8, "by_xcc": []}
+    from gpumon import core
+
+    py = derive(raw, AGENT)
+    cc = core().pmc_derive(raw, AGENT)
+    assert set(py) == set(cc)
+    for k in py:
+        assert cc[k] == pytest.approx(py[k], rel=1e-12)
+
+
+def test_default_plugin_dir_is_tree_lib(core, monkeypatch):
+    monkeypatch.delenv("GPUMON_PLUGIN_DIR", raising=False)
+    assert os.path.realpath(core.default_plugin_dir()) == os.path.join(os.path.realpath(ROOT), "lib")
+    monkeypatch.setenv("GPUMON_PLUGIN_DIR", "/elsewhere")
+    assert core.default_plugin_dir() == "/elsewhere"
+
+
+# ---------------------------------------------------------------- in-process (gpumon._core.OnDevice)
+def test_native_samplers_export_series(core, mock_exporter, monkeypatch):
+    monkeypatch.setenv("GPUMON_FAKE_AGENTS", "2")
+    monkeypatch.setenv("GPUMON_FAKE_MFMA", "0.75")
+    monkeypatch.setenv("GPUMON_FAKE_OCC", "0.5")
+    ex = mock_exporter()
+    od = _ondevice(core, ex)
+    od.start()
+    try:
+        assert od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        for g in ("0", "1"):
+            assert _val(m, "gpu_mfma_busy_percent", gpu_id=g) == pytest.approx(75.0)
+            assert _val(m, "gpu_occupancy_percent", gpu_id=g) == pytest.approx(50.0)
+            assert _val(m, "gpu_gui_active_percent", gpu_id=g) == pytest.approx(100.0)
+            assert _val(m, "gpu_pmc_window_seconds", gpu_id=g) == pytest.approx(0.01)
+            for x in range(8):
+                assert _val(m, "gpu_xcd_mfma_busy_percent", gpu_id=g, xcd=x) == pytest.approx(75.0)
+                assert _val(m, "gpu_probe_xcd_blocks", gpu_id=g, xcd=x) == 1024 / 8
+                assert _val(m, "gpu_probe_xcd_clock_mhz", gpu_id=g, xcd=x) == pytest.approx(2400 - 10 * x)
+            assert _val(m, "gpu_probe_unique_cus", gpu_id=g) == 256
+            assert _val(m, "gpu_probe_pending", gpu_id=g) == 0
+        assert "# TYPE gpumon_pmc_errors_total counter" in m
+        s = od.stats()
+        assert s["pmc_agents"] == 2 and s["probe_devices"] == 2 and s["pmc_samples"] >= 2 and s["probe_done"] >= 2
+    finally:
+        od.stop()
+    ex.tick()
+    m = ex.metrics_text()
+    assert "gpu_mfma_busy_percent" not in m and "gpu_probe_pending" not in m  # series withdrawn on stop
+
+
+def test_background_threads_keep_sampling(core, mock_exporter, monkeypatch):
+    import time
+
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, pmc_every_s=0.05, probe_every_s=0.05)
+    od.start()
+    try:
+        t0 = time.monotonic()
+        while time.monotonic() - t0 < 5 and (od.stats()["pmc_samples"] < 5 or od.stats()["probe_done"] < 5):
+            time.sleep(0.02)
+        s = od.stats()
+        assert s["pmc_samples"] >= 5 and s["probe_done"] >= 5 and s["pmc_errors"] == 0
+    finally:
+        t0 = time.monotonic()
+        od.stop()
+        assert time.monotonic() - t0 < 2  # the waits are interruptible
+
+
+def test_pmc_init_failure_fails_loudly(core, mock_exporter, monkeypatch):
+    monkeypatch.setenv("GPUMON_FAKE_PMC_FAIL", "init")
+    od = _ondevice(core, mock_exporter())
+    with pytest.raises(RuntimeError, match="device counting unavailable"):
+        od.start()
+
+
+def test_missing_plugin_fails_loudly(core, mock_exporter, tmp_path):
+    od = _ondevice(core, mock_exporter(), plugin_dir=str(tmp_path))
+    with pytest.raises(RuntimeError, match="dlopen .*libgpumon_pmc.so"):
+        od.start()
+
+
+def test_sample_failures_counted(core, mock_exporter, monkeypatch):
+    monkeypatch.setenv("GPUMON_FAKE_PMC_FAIL", "sample")
+    ex = mock_exporter()
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60)
+    od.start()
+    try:
+        od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        assert "gpu_mfma_busy_percent" not in m
+        assert re.search(r'^gpumon_pmc_errors_total\{host="node-a"\} [1-9]', m, re.M)  # node-level series
+        assert od.stats()["pmc_errors"] >= 1
+    finally:
+        od.stop()
+
+
+def test_probe_timeouts(core, mock_exporter, monkeypatch):
+    monkeypatch.setenv("GPUMON_FAKE_PROBE_HANG", "1")
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, pmc=False, probe_every_s=60, probe_timeout_s=0.01)
+    od.start()
+    try:
+        od.step()
+        od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        assert _val(m, "gpu_probe_timeouts_total", gpu_id="0") >= 2  # + the background thread's first step
+        assert _val(m, "gpu_probe_pending", gpu_id="0") == 1
+        assert "gpu_probe_latency_seconds" not in m
+    finally:
+        monkeypatch.delenv("GPUMON_FAKE_PROBE_HANG")
+        od.stop()
+
+
+# ---------------------------------------------------------------- standalone binary + Python CLI
+def _run_bin(*args, env=None):
+    e = dict(os.environ, GPUMON_FAKE_AGENTS="2")
+    e.update(env or {})
+    return subprocess.run([BIN, "--backend", "mock:gpus=2", "--once", "--no-pod-resources", "--no-cri", *args],
+                          capture_output=True, text=True, timeout=60, env=e)
+
+
+def test_binary_pmc_and_probe_flags():
+    r = _run_bin("--pmc", "--probe", "--plugin-dir", FAKE_DIR, env={"GPUMON_FAKE_MFMA": "0.25"})
+    assert r.returncode == 0, r.stderr
+    assert _val(r.stdout, "gpu_mfma_busy_percent", gpu_id="1") == pytest.approx(25.0)
+    assert _val(r.stdout, "gpu_probe_xcd_blocks", gpu_id="1", xcd="7") == 128
+
+
+def test_binary_plugin_dir_from_env():
+    r = _run_bin("--probe", env={"GPUMON_PLUGIN_DIR": FAKE_DIR})
+    assert r.returncode == 0, r.stderr
+    assert "gpu_probe_unique_cus" in r.stdout and "gpu_mfma_busy_percent" not in r.stdout
+
+
+def test_binary_missing_plugin_exits_nonzero(tmp_path):
+    r = _run_bin("--pmc", "--plugin-dir", str(tmp_path))
+    assert r.returncode == 1 and "libgpumon_pmc.so" in r.stderr
+
+
+def test_binary_without_flags_loads_no_plugin():
+    r = _run_bin(env={"GPUMON_PLUGIN_DIR": "/nonexistent"})
+    assert r.returncode == 0 and "gpu_probe" not in r.stdout
+
+
+def test_cli_once_native_ondevice(monkeypatch, capsys):
+    from gpumon import cli
+
+    monkeypatch.setenv("GPUMON_FAKE_AGENTS", "1")
+    rc = cli.main(["once", "--backend", "mock:gpus=1", "--enable-pmc", "--enable-probe-kernel",
+                   "--plugin-dir", FAKE_DIR, "--control-plane", "off"])
+    out = capsys.readouterr().out
+    assert rc == 0
+    assert _val(out, "gpu_mfma_busy_percent", gpu_id="0") == pytest.approx(50.0)
+    assert _val(out, "gpu_probe_unique_cus", gpu_id="0") == 256
