@@ -90,6 +90,7 @@ PYBIND11_MODULE(_hip, m) {
         d["xcc_blocks"] = r.xcc_blocks;
         d["xcc_clock_mhz"] = r.xcc_clock_mhz;
         d["unique_cus"] = r.unique_cus;
+        d["stale_records"] = r.stale_records;
         py::list recs;
         for (const auto& x : r.records)
           recs.append(py::make_tuple(x.xcc_id, x.hw_id, x.t0_real, x.t1_real, x.c0, x.c1, x.seq, x.block));

@@ -360,6 +360,7 @@ void OnDevice::probe_step() {
       p.latency_s = r.host_latency_s;
       p.span_s = r.gpu_span_s;
       p.unique_cus = r.unique_cus;
+      p.stale += static_cast<uint64_t>(std::max(0, r.stale_records));
       p.xcc_blocks.assign(r.xcc_blocks, r.xcc_blocks + GPUMON_PROBE_MAX_XCC);
       p.xcc_mhz.assign(r.xcc_clock_mhz, r.xcc_clock_mhz + GPUMON_PROBE_MAX_XCC);
       probe_done_++;
@@ -378,6 +379,8 @@ void OnDevice::export_probe() {
                      p.pending >= 0 ? 1 : 0));
     out.push_back(xs("gpu_probe_timeouts_total", "Probe polls that timed out (GPU saturated or hung).", p.dev,
                      static_cast<double>(p.timeouts), "counter"));
+    out.push_back(xs("gpu_probe_stale_records_total", "Probe records not visible when the arrival flag was.", p.dev,
+                     static_cast<double>(p.stale), "counter"));
     if (!p.have) continue;
     out.push_back(xs("gpu_probe_latency_seconds", "Probe host launch -> all workgroups arrived (pinned ring).", p.dev,
                      p.latency_s));

@@ -109,6 +109,7 @@ class OnDevice {
     void* handle = nullptr;
     int pending = -1;   // slot in flight, -1 none
     uint64_t timeouts = 0;
+    uint64_t stale = 0;     // records that had not landed when the arrival flag had
     bool have = false;
     double latency_s = 0, span_s = 0;
     int unique_cus = 0;

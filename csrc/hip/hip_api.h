@@ -89,6 +89,7 @@ struct ProbeResult {
   std::vector<int> xcc_blocks;  // blocks seen per XCC id (index 0..15)
   std::vector<double> xcc_clock_mhz;  // mean effective shader clock per XCC (0 if none)
   int unique_cus = 0;
+  int stale_records = 0;        // records whose seq never matched after the flag (should be 0)
   std::vector<ProbeRecord> records;
 };
 
@@ -108,6 +109,7 @@ class Probe {
   uint32_t* arrivals_ = nullptr;        // host pinned, one counter per slot
   ProbeRecord* ring_dev_ = nullptr;
   uint32_t* arrivals_dev_ = nullptr;
+  uint32_t* counters_dev_ = nullptr;   // device memory, one arrival counter per slot (self re-arming)
   std::vector<uint32_t> slot_seq_;
   std::vector<int64_t> slot_launch_ns_;
   uint32_t seq_ = 0;

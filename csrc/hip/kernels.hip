@@ -151,13 +151,22 @@ __global__ void __launch_bounds__(256) stream_triad_kernel(const f32x4* __restri
 }
 
 // ============================================================================================
-// K1: probe. One wave per workgroup; lane 0 does the work (stamps are wave-uniform SGPR reads).
-// Publication to the pinned host ring: plain stores -> vmcnt(0) drain -> system-scope release
-// fetch_add on the slot's arrival counter (the counter is what the host polls).
+// K1: probe. One wave per workgroup; the stamps are wave-uniform SGPR reads.
+//
+// Publication to the pinned host ring costs ONE host-memory store per wave plus ONE host flag per
+// launch. Each wave writes its 48-byte record as three 16-byte lane stores (one instruction,
+// coalesced into one transaction to fine-grained host memory), drains them (vmcnt(0)), then bumps
+// a per-slot counter in device memory at agent scope (an L2 atomic: no fabric round trip, no L2
+// writeback). The wave that takes the counter to `blocks` re-arms it and publishes the slot with a
+// single system-scope store of `blocks` to the host arrival word that the exporter polls.
+// The first version did a system-scope release fetch_add on the host word from every wave: 1024
+// serialised host atomics each preceded by an L2 writeback (buffer_wbl2), ~1.0 ms per launch on
+// MI355X (profiles/r1_probe_publication.md).
 // ============================================================================================
 __global__ void __launch_bounds__(64) probe_kernel(ProbeRecord* __restrict__ recs, uint32_t* arrivals,
-                                                   uint32_t seq, uint32_t spin_ticks) {
-  if (threadIdx.x != 0) return;
+                                                   uint32_t* counter, uint32_t seq, uint32_t spin_ticks,
+                                                   uint32_t blocks) {
+  const uint32_t lane = threadIdx.x;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const uint64_t c0 = __builtin_amdgcn_s_memtime();
   uint32_t xcc, hw;
@@ -170,17 +179,24 @@ __global__ void __launch_bounds__(64) probe_kernel(ProbeRecord* __restrict__ rec
     if (t1 - t0 >= spin_ticks) break;
   }
   const uint64_t c1 = __builtin_amdgcn_s_memtime();
-  ProbeRecord* r = recs + blockIdx.x;
-  r->xcc_id = xcc & 0xF;
-  r->hw_id = hw;
-  r->t0_real = t0;
-  r->t1_real = t1;
-  r->c0 = c0;
-  r->c1 = c1;
-  r->seq = seq;
-  r->block = blockIdx.x;
+  // ProbeRecord = 3 x 16 B: {xcc_id, hw_id, t0_real}, {t1_real, c0}, {c1, seq, block}
+  if (lane < 3) {
+    uint4 v;
+    if (lane == 0) v = make_uint4(xcc & 0xF, hw, static_cast<uint32_t>(t0), static_cast<uint32_t>(t0 >> 32));
+    else if (lane == 1)
+      v = make_uint4(static_cast<uint32_t>(t1), static_cast<uint32_t>(t1 >> 32), static_cast<uint32_t>(c0),
+                     static_cast<uint32_t>(c0 >> 32));
+    else v = make_uint4(static_cast<uint32_t>(c1), static_cast<uint32_t>(c1 >> 32), seq, blockIdx.x);
+    reinterpret_cast<uint4*>(recs + blockIdx.x)[lane] = v;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (lane == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == blocks - 1) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm the slot
+      __hip_atomic_store(arrivals, blocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // ============================================================================================
@@ -377,6 +393,9 @@ Probe::Probe(int dev, int blocks, int slots, int spin_ticks)
   memset(arrivals_, 0, sizeof(uint32_t) * slots_);
   check(hipHostGetDevicePointer(reinterpret_cast<void**>(&ring_dev_), ring_, 0), "hipHostGetDevicePointer");
   check(hipHostGetDevicePointer(reinterpret_cast<void**>(&arrivals_dev_), arrivals_, 0), "hipHostGetDevicePointer");
+  check(hipMalloc(reinterpret_cast<void**>(&counters_dev_), sizeof(uint32_t) * slots_), "hipMalloc(counters)");
+  check(hipMemsetAsync(counters_dev_, 0, sizeof(uint32_t) * slots_, s), "hipMemset(counters)");
+  check(hipStreamSynchronize(s), "hipStreamSynchronize");
   slot_seq_.assign(slots_, 0);
   slot_launch_ns_.assign(slots_, 0);
 }
@@ -389,6 +408,7 @@ Probe::~Probe() {
   }
   if (ring_) (void)hipHostFree(ring_);
   if (arrivals_) (void)hipHostFree(arrivals_);
+  if (counters_dev_) (void)hipFree(counters_dev_);
 }
 
 int Probe::launch() {
@@ -403,8 +423,8 @@ int Probe::launch() {
   check(hipSetDevice(dev_), "hipSetDevice");
   slot_launch_ns_[slot] = mono_ns();
   hipLaunchKernelGGL(probe_kernel, dim3(blocks_), dim3(64), 0, static_cast<hipStream_t>(stream_),
-                     ring_dev_ + static_cast<size_t>(slot) * blocks_, arrivals_dev_ + slot, seq,
-                     static_cast<uint32_t>(spin_));
+                     ring_dev_ + static_cast<size_t>(slot) * blocks_, arrivals_dev_ + slot, counters_dev_ + slot, seq,
+                     static_cast<uint32_t>(spin_), static_cast<uint32_t>(blocks_));
   check(hipGetLastError(), "probe_kernel");
   return slot;
 }
@@ -423,6 +443,19 @@ bool Probe::poll(int slot, ProbeResult* out) {
   out->complete = true;
   out->host_done_ns = mono_ns();
   const ProbeRecord* r = ring_ + static_cast<size_t>(slot) * blocks_;
+  // The flag is written after every wave drained its record stores; a record still in flight on
+  // another fabric path would show the previous seq. Re-read those briefly (bounded) and count what
+  // never landed.
+  std::vector<int> late;
+  for (int b = 0; b < blocks_; ++b)
+    if (__atomic_load_n(&r[b].seq, __ATOMIC_ACQUIRE) != out->seq) late.push_back(b);
+  for (int spin = 0; !late.empty() && spin < 1000; ++spin) {
+    std::this_thread::yield();
+    late.erase(std::remove_if(late.begin(), late.end(),
+                              [&](int b) { return __atomic_load_n(&r[b].seq, __ATOMIC_ACQUIRE) == out->seq; }),
+               late.end());
+  }
+  out->stale_records = static_cast<int>(late.size());
   out->records.assign(r, r + blocks_);
   out->xcc_blocks.assign(16, 0);
   std::vector<double> clk_sum(16, 0.0);

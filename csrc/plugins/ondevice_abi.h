@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define GPUMON_ONDEVICE_ABI 1
+#define GPUMON_ONDEVICE_ABI 2  // 2: gpumon_probe_result_t.stale_records
 #define GPUMON_PMC_MAX_XCC 16
 
 // ---- PMC (libgpumon_pmc.so) --------------------------------------------------------------------
@@ -70,6 +70,7 @@ typedef struct {
   double host_latency_s;   // host launch -> last arrival observed
   double gpu_span_s;       // max(end) - min(start) on the 100 MHz clock
   int32_t unique_cus;
+  int32_t stale_records;   // records not yet visible when the arrival flag was (expected 0)
   int32_t xcc_blocks[GPUMON_PROBE_MAX_XCC];
   double xcc_clock_mhz[GPUMON_PROBE_MAX_XCC];
 } gpumon_probe_result_t;

@@ -2,8 +2,9 @@
 pinned-ring-buffer results as ``gpu_probe_*`` series.
 
 Per tick and device: one launch of ``blocks`` one-wave workgroups on a private non-blocking stream;
-completion is detected by polling a host-pinned arrival counter written with system-scope release
-atomics by the kernel (no hipDeviceSynchronize, no stall of the workload). Exported:
+completion is detected by polling a host-pinned arrival word that the last wave writes once, after a
+device-memory (L2) arrival counter reaches ``blocks`` (no hipDeviceSynchronize, no stall of the
+workload; see csrc/hip/kernels.hip K1). Exported:
 
 * ``gpu_probe_xcd_blocks{xcd}``       — workgroups that ran on each XCD (per-XCD liveness)
 * ``gpu_probe_xcd_clock_mhz{xcd}``    — effective shader clock per XCD (Δs_memtime / Δs_memrealtime)
@@ -11,7 +12,7 @@ atomics by the kernel (no hipDeviceSynchronize, no stall of the workload). Expor
                                         workload is the contention signal)
 * ``gpu_probe_kernel_span_seconds``   — first start -> last end on the GPU's 100 MHz clock
 * ``gpu_probe_unique_cus``            — distinct (XCD, SE, CU) ids seen
-* ``gpu_probe_pending`` / ``gpu_probe_timeouts_total``
+* ``gpu_probe_pending`` / ``gpu_probe_timeouts_total`` / ``gpu_probe_stale_records_total``
 
 SQ/GRBM perf counters are not readable from shader code on CDNA4; MFMA-busy and occupancy come
 from :mod:`gpumon.ops.pmc` (rocprofiler-sdk device counting).
@@ -45,6 +46,7 @@ class ProbeRunner:
                 self.probes[s["index"]] = self._hip.Probe(hid, blocks, 4, spin_ticks)
         self.pending: Dict[int, int] = {}
         self.timeouts: Dict[int, int] = {i: 0 for i in self.probes}
+        self.stale: Dict[int, int] = {i: 0 for i in self.probes}
         self.last: Dict[int, dict] = {}
         self._stop = threading.Event()
         self._lock = threading.Lock()
@@ -71,6 +73,7 @@ class ProbeRunner:
             if r is not None:
                 out[i] = r
                 self.last[i] = r
+                self.stale[i] += r.get("stale_records", 0)
                 del self.pending[i]
             else:
                 self.timeouts[i] += 1
@@ -88,6 +91,8 @@ class ProbeRunner:
             add("gpu_probe_pending", "1 if the last probe launch has not completed yet.", i, 1 if i in self.pending else 0)
             add("gpu_probe_timeouts_total", "Probe polls that timed out (GPU saturated or hung).", i,
                 self.timeouts[i], typ="counter")
+            add("gpu_probe_stale_records_total", "Probe records not visible when the arrival flag was.", i,
+                self.stale[i], typ="counter")
             r = self.last.get(i)
             if not r:
                 continue
