@@ -90,6 +90,8 @@ PYBIND11_MODULE(_hip, m) {
         d["xcc_blocks"] = r.xcc_blocks;
         d["xcc_clock_mhz"] = r.xcc_clock_mhz;
         d["unique_cus"] = r.unique_cus;
+        d["xcc_wave_slot"] = r.xcc_wave_slot;
+        d["wave_slot_mean"] = r.wave_slot_mean;
         d["stale_records"] = r.stale_records;
         py::list recs;
         for (const auto& x : r.records)

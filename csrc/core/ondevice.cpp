@@ -363,6 +363,8 @@ void OnDevice::probe_step() {
       p.stale += static_cast<uint64_t>(std::max(0, r.stale_records));
       p.xcc_blocks.assign(r.xcc_blocks, r.xcc_blocks + GPUMON_PROBE_MAX_XCC);
       p.xcc_mhz.assign(r.xcc_clock_mhz, r.xcc_clock_mhz + GPUMON_PROBE_MAX_XCC);
+      p.xcc_slot.assign(r.xcc_wave_slot, r.xcc_wave_slot + GPUMON_PROBE_MAX_XCC);
+      p.slot_mean = r.wave_slot_mean;
       probe_done_++;
     } else {
       p.timeouts++;
@@ -371,6 +373,9 @@ void OnDevice::probe_step() {
   }
   export_probe();
 }
+
+constexpr const char* kSlotHelp =
+    "Mean lowest wave slot a probe wave got per SIMD (wave slots held by other work at probe launch).";
 
 void OnDevice::export_probe() {
   std::vector<ExtraSeries> out;
@@ -387,12 +392,15 @@ void OnDevice::export_probe() {
     out.push_back(xs("gpu_probe_kernel_span_seconds", "Probe first start -> last end on the GPU 100 MHz clock.", p.dev,
                      p.span_s));
     out.push_back(xs("gpu_probe_unique_cus", "Distinct compute units that ran probe workgroups.", p.dev, p.unique_cus));
+    out.push_back(xs("gpu_probe_wave_slot_mean", kSlotHelp, p.dev, p.slot_mean));
     for (size_t x = 0; x < p.xcc_blocks.size(); ++x) {
       if (!p.xcc_blocks[x]) continue;
       out.push_back(xs("gpu_probe_xcd_blocks", "Probe workgroups executed per XCD (liveness).", p.dev, p.xcc_blocks[x]));
       out.back().labels.push_back({"xcd", std::to_string(x)});
       out.push_back(xs("gpu_probe_xcd_clock_mhz", "Effective shader clock per XCD measured in-kernel.", p.dev,
                        p.xcc_mhz[x]));
+      out.back().labels.push_back({"xcd", std::to_string(x)});
+      out.push_back(xs("gpu_probe_xcd_wave_slot_mean", kSlotHelp, p.dev, p.xcc_slot[x]));
       out.back().labels.push_back({"xcd", std::to_string(x)});
     }
   }

@@ -115,6 +115,8 @@ class OnDevice {
     int unique_cus = 0;
     std::vector<int> xcc_blocks;
     std::vector<double> xcc_mhz;
+    std::vector<double> xcc_slot;
+    double slot_mean = 0;
   };
   std::vector<ProbeDev> probes_;
 

@@ -153,9 +153,11 @@ EXPORT int gpumon_probe_wait(gpumon_probe* p, int, double timeout_s, gpumon_prob
   out->host_latency_s = 25e-6;
   out->gpu_span_s = 6e-6;
   out->unique_cus = kCus;
+  out->wave_slot_mean = 1.75;
   for (uint32_t x = 0; x < kXcc; ++x) {
     out->xcc_blocks[x] = p->blocks / kXcc;
     out->xcc_clock_mhz[x] = 2400.0 - 10.0 * x;
+    out->xcc_wave_slot[x] = 0.5 * x;
   }
   return 1;
 }

@@ -89,6 +89,8 @@ struct ProbeResult {
   std::vector<int> xcc_blocks;  // blocks seen per XCC id (index 0..15)
   std::vector<double> xcc_clock_mhz;  // mean effective shader clock per XCC (0 if none)
   int unique_cus = 0;
+  std::vector<double> xcc_wave_slot;  // mean lowest HW_ID.WAVE_ID per SIMD, per XCC (resident-wave pressure)
+  double wave_slot_mean = 0;          // the same over every SIMD seen
   int stale_records = 0;        // records whose seq never matched after the flag (should be 0)
   std::vector<ProbeRecord> records;
 };

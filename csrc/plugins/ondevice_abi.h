@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define GPUMON_ONDEVICE_ABI 2  // 2: gpumon_probe_result_t.stale_records
+#define GPUMON_ONDEVICE_ABI 2  // 2: gpumon_probe_result_t.stale_records + xcc_wave_slot
 #define GPUMON_PMC_MAX_XCC 16
 
 // ---- PMC (libgpumon_pmc.so) --------------------------------------------------------------------
@@ -73,6 +73,10 @@ typedef struct {
   int32_t stale_records;   // records not yet visible when the arrival flag was (expected 0)
   int32_t xcc_blocks[GPUMON_PROBE_MAX_XCC];
   double xcc_clock_mhz[GPUMON_PROBE_MAX_XCC];
+  // Mean over the SIMDs a launch landed on of the lowest wave slot (HW_ID.WAVE_ID) a probe wave got
+  // there: the wave slots already held by other work at launch time (0 on an idle XCD).
+  double xcc_wave_slot[GPUMON_PROBE_MAX_XCC];
+  double wave_slot_mean;
 } gpumon_probe_result_t;
 
 int gpumon_probe_abi_version(void);

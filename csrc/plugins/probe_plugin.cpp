@@ -63,10 +63,12 @@ GPUMON_EXPORT int gpumon_probe_wait(gpumon_probe* h, int slot, double timeout_s,
   out->host_latency_s = (r.host_done_ns - r.host_launch_ns) * 1e-9;
   out->gpu_span_s = r.gpu_span_ticks * 1e-8;  // 100 MHz s_memrealtime
   out->unique_cus = r.unique_cus;
+  out->wave_slot_mean = r.wave_slot_mean;
   out->stale_records = r.stale_records;
   for (size_t x = 0; x < r.xcc_blocks.size() && x < GPUMON_PROBE_MAX_XCC; ++x) {
     out->xcc_blocks[x] = r.xcc_blocks[x];
     out->xcc_clock_mhz[x] = r.xcc_clock_mhz[x];
+    out->xcc_wave_slot[x] = x < r.xcc_wave_slot.size() ? r.xcc_wave_slot[x] : 0.0;
   }
   return 1;
 }

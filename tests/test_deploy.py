@@ -110,6 +110,8 @@ def test_dockerfile_entrypoint():
     assert 'ENTRYPOINT ["python3", "-m", "gpumon", "serve"]' in txt
     assert "libltdl" not in txt.split("\n", 5)[-1] or "no vendored" in txt
     assert "EXPOSE 9400" in txt
+    # the on-device plugins ship next to the package and the binary (csrc/core/ondevice.cpp lookup)
+    assert "COPY --from=build /src/lib /opt/gpumon/lib" in txt and "GPUMON_PLUGIN_DIR=/opt/gpumon/lib" in txt
 
 
 def test_alert_and_recording_rules_resolve(mock_exporter):

@@ -97,6 +97,8 @@ def test_native_samplers_export_series(core, mock_exporter, monkeypatch):
                 assert _val(m, "gpu_probe_xcd_blocks", gpu_id=g, xcd=x) == 1024 / 8
                 assert _val(m, "gpu_probe_xcd_clock_mhz", gpu_id=g, xcd=x) == pytest.approx(2400 - 10 * x)
             assert _val(m, "gpu_probe_unique_cus", gpu_id=g) == 256
+            assert _val(m, "gpu_probe_wave_slot_mean", gpu_id=g) == pytest.approx(1.75)
+            assert _val(m, "gpu_probe_xcd_wave_slot_mean", gpu_id=g, xcd=6) == pytest.approx(3.0)
             assert _val(m, "gpu_probe_pending", gpu_id=g) == 0
         assert "# TYPE gpumon_pmc_errors_total counter" in m
         s = od.stats()
