@@ -329,3 +329,26 @@ def test_xcd_limit_residencies_idle_vs_burn(core, torch_gpu):
               % (idle, r["xcd_low_util_pct"], r["xcd_below_ppt_pct"], r["xcd_below_total_pct"]))
     finally:
         ex.stop()
+
+
+def test_probe_wave_slots_track_partial_occupancy():
+    """K1 in-kernel resident-wave pressure vs rocprofiler occupancy (fresh process: PMC first).
+    profiles/r1_probe_wave_slots.md: persistent 1/4-SIMD load -> 0.25 slots = 3.1 % = the PMC's."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "wave_slot_check.py")], capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["idle"]["wave_slot_mean"] < 0.05
+    part = d["partial"]
+    assert 0.15 < part["wave_slot_mean"] < 0.4, part
+    slots_per_simd = d["max_waves_per_cu"] / 4  # 4 SIMDs per CU on CDNA4
+    assert abs(part["wave_slot_mean"] / slots_per_simd * 100 - part["pmc"]["occupancy"]) < 2.0, part
+    # saturated GPU: the probe queues behind the burn
+    idle_lat = sorted(d["idle"]["latency_ms"])[len(d["idle"]["latency_ms"]) // 2]
+    mfma_lat = sorted(d["mfma"]["latency_ms"])[len(d["mfma"]["latency_ms"]) // 2]
+    assert mfma_lat > 5 * idle_lat, (idle_lat, mfma_lat)
