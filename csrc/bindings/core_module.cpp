@@ -73,6 +73,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "full_device_labels", &c.full_device_labels);
   get(d, "processes", &c.processes);
   get(d, "link_every", &c.link_every);
+  get(d, "ras_every", &c.ras_every);
   get(d, "sample_threads", &c.sample_threads);
   get(d, "influx_url", &c.influx_url);
   get(d, "influx_extended", &c.influx_extended);
@@ -172,6 +173,26 @@ py::dict sample_to_dict(const DeviceSample& s) {
     links.append(l);
   }
   d["links"] = links;
+  if (s.ras.valid) {
+    py::dict r;
+    r["source"] = s.ras.source;
+    py::dict blocks;
+    for (const auto& c : s.ras.blocks) {
+      py::dict b;
+      b["ue"] = c.ue;
+      b["ce"] = c.ce;
+      if (c.has_de) b["de"] = c.de;
+      blocks[py::str(c.block)] = b;
+    }
+    r["blocks"] = blocks;
+    r["fatal"] = num(s.ras.fatal);
+    r["poison_created"] = num(s.ras.poison_created);
+    r["poison_consumed"] = num(s.ras.poison_consumed);
+    r["bad_pages"] = num(s.ras.bad_pages);
+    d["ras"] = r;
+  } else {
+    d["ras"] = py::none();
+  }
   py::dict a;
   a["energy"] = s.acc.energy;
   a["accumulation_counter"] = s.acc.accumulation_counter;
@@ -626,6 +647,13 @@ PYBIND11_MODULE(_core, m) {
              return e.attributor().derive_user(pod, m);
            })
       .def("mock_set_util", [](Exporter& e, int dev, double pct) { mock_of(e)->set_util(dev, pct); })
+      .def("mock_add_ecc",
+           [](Exporter& e, int dev, const std::string& block, uint64_t ue, uint64_t ce, uint64_t de) {
+             mock_of(e)->add_ecc(dev, block, ue, ce, de);
+           },
+           py::arg("dev"), py::arg("block"), py::arg("ue") = 0, py::arg("ce") = 0, py::arg("de") = 0)
+      .def("mock_set_ras_event",
+           [](Exporter& e, int dev, const std::string& ev, double v) { mock_of(e)->set_ras_event(dev, ev, v); })
       .def("mock_set_procs",
            [](Exporter& e, const py::list& procs) {
              std::vector<MockProc> v;

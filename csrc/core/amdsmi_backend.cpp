@@ -17,6 +17,7 @@
 #include "backend.h"
 #include "common.h"
 #include "metrics_table.h"
+#include "ras.h"
 #include "smi_table.h"
 #include "sysfs_fast.h"
 
@@ -631,6 +632,61 @@ void AmdSmiBackend::sample_links(int i, DeviceSample* out) {
     L.link_type = static_cast<int>(s.link_type);
   }
   if (n > out->n_links) out->n_links = n;
+}
+
+// RAS: the kernel's ras/ text files first (no library call, readable by a non-root exporter, every
+// block the driver tracks); per-block amdsmi_get_gpu_ecc_count where the directory is absent.
+void AmdSmiBackend::sample_ras(int i, DeviceSample* out) {
+  if (i < 0 || i >= static_cast<int>(devs_.size())) return;
+  Caps& c = caps_[i];
+  const int64_t t0 = mono_ns();
+  if (c.ras_sysfs) {
+    if (read_ras_sysfs(sys_root_, devs_[i].bdf, &out->ras)) {
+      record_call(kCallRas, mono_ns() - t0, true);
+      return;
+    }
+    c.ras_sysfs = false;  // no ras/ directory on this node: do not stat it every refresh
+  }
+  if (!t_->amdsmi_get_gpu_ecc_count || !c.ecc_blocks) return;
+  static const std::pair<amdsmi_gpu_block_t, const char*> kBlocks[] = {
+      {AMDSMI_GPU_BLOCK_UMC, "umc"},       {AMDSMI_GPU_BLOCK_SDMA, "sdma"},
+      {AMDSMI_GPU_BLOCK_GFX, "gfx"},       {AMDSMI_GPU_BLOCK_MMHUB, "mmhub"},
+      {AMDSMI_GPU_BLOCK_ATHUB, "athub"},   {AMDSMI_GPU_BLOCK_PCIE_BIF, "pcie_bif"},
+      {AMDSMI_GPU_BLOCK_HDP, "hdp"},       {AMDSMI_GPU_BLOCK_XGMI_WAFL, "xgmi_wafl"},
+      {AMDSMI_GPU_BLOCK_DF, "df"},         {AMDSMI_GPU_BLOCK_MCA, "mca"},
+      {AMDSMI_GPU_BLOCK_VCN, "vcn"},       {AMDSMI_GPU_BLOCK_JPEG, "jpeg"}};
+  RasSample r;
+  r.source = "amdsmi";
+  bool any_err = false;
+  for (const auto& b : kBlocks) {
+    if (!(c.ecc_blocks & static_cast<uint64_t>(b.first))) continue;
+    amdsmi_error_count_t ec;
+    memset(&ec, 0, sizeof ec);
+    const amdsmi_status_t st = t_->amdsmi_get_gpu_ecc_count(handles_[i], b.first, &ec);
+    if (st != AMDSMI_STATUS_SUCCESS) {
+      // a block that never answered has no counters on this ASIC (MI355X: 12 of 19 blocks): stop
+      // asking; a block that used to answer is a real error
+      if (c.ecc_seen & static_cast<uint64_t>(b.first)) any_err = true;
+      else c.ecc_blocks &= ~static_cast<uint64_t>(b.first);
+      continue;
+    }
+    c.ecc_seen |= static_cast<uint64_t>(b.first);
+    RasCount rc;
+    rc.block = b.second;
+    rc.ue = ec.uncorrectable_count;
+    rc.ce = ec.correctable_count;
+    rc.de = ec.deferred_count;
+    rc.has_de = true;
+    r.blocks.push_back(rc);
+  }
+  if (t_->amdsmi_get_gpu_bad_page_info) {
+    uint32_t np = 0;
+    if (t_->amdsmi_get_gpu_bad_page_info(handles_[i], &np, nullptr) == AMDSMI_STATUS_SUCCESS) r.bad_pages = np;
+  }
+  record_call(kCallRas, mono_ns() - t0, !any_err);
+  if (r.blocks.empty()) return;
+  r.valid = true;
+  out->ras = std::move(r);
 }
 
 }  // namespace gpumon

@@ -35,14 +35,17 @@ class Backend {
   // Optional: per-link metrics are expensive (~1 ms); sampled every `link_every` ticks.
   virtual bool supports_links() const { return false; }
   virtual void sample_links(int, DeviceSample*) {}
+  // Optional: RAS / ECC counters (ras.h), refreshed every `ras_every` ticks into out->ras.
+  virtual bool supports_ras() const { return false; }
+  virtual void sample_ras(int, DeviceSample*) {}
   // Restrict to a subset of device hip_ids (empty = all). Applied at init().
   void set_device_filter(const std::vector<int>& ids) { filter_ = ids; }
 
   // Per-call latency accounting (exported as gpumon_backend_call_* self-metrics).
-  enum Call { kCallMetrics = 0, kCallVram, kCallProcs, kCallLinks, kCallActivity, kCallPower, kCallCount };
+  enum Call { kCallMetrics = 0, kCallVram, kCallProcs, kCallLinks, kCallActivity, kCallPower, kCallRas, kCallCount };
   static const char* call_name(int c) {
     static const char* n[] = {"gpu_metrics", "vram_usage", "process_list", "link_metrics", "gpu_activity",
-                              "power_info"};
+                              "power_info", "ras"};
     return c >= 0 && c < kCallCount ? n[c] : "?";
   }
   struct CallSnap {
@@ -117,8 +120,14 @@ class MockBackend : public Backend {
   bool processes(int i, std::vector<ProcSample>* out) override;
   bool supports_links() const override { return true; }
   void sample_links(int i, DeviceSample* out) override;
+  bool supports_ras() const override { return true; }
+  void sample_ras(int i, DeviceSample* out) override;
 
   // Test controls (thread-safe).
+  // Add errors to a RAS block of `dev` (blocks: umc gfx sdma mmhub xgmi_wafl vcn jpeg); `event`
+  // counters: "fatal", "poison_created", "poison_consumed", "bad_pages" (set, not added).
+  void add_ecc(int dev, const std::string& block, uint64_t ue, uint64_t ce, uint64_t de);
+  void set_ras_event(int dev, const std::string& event, double value);
   void set_util(int dev, double pct);
   void set_procs(const std::vector<MockProc>& procs);
   void set_fail(int dev, int every);
@@ -137,6 +146,7 @@ class MockBackend : public Backend {
   std::vector<uint64_t> calls_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
   std::vector<uint64_t> lim_acc_;  // per device x XCC x {ppt, thermal, any, low-util}
+  std::vector<RasSample> ras_;     // per device (mock RAS state)
   std::map<std::pair<uint32_t, int>, uint64_t> proc_gfx_ns_;
   int64_t t0_ns_ = 0;
   std::vector<int64_t> last_ns_;
@@ -161,6 +171,8 @@ class AmdSmiBackend : public Backend {
   bool processes(int i, std::vector<ProcSample>* out) override;
   bool supports_links() const override;
   void sample_links(int i, DeviceSample* out) override;
+  bool supports_ras() const override { return true; }
+  void sample_ras(int i, DeviceSample* out) override;
   std::string lib_version() const { return lib_version_; }
   // Expose every physical device `r` times (distinct gpu_id labels). Only for measuring how the
   // sampler scales with the GPU count on a box with fewer GPUs than a full 8x MI355X node.
@@ -194,6 +206,9 @@ class AmdSmiBackend : public Backend {
   // Per device: calls that returned NOT_SUPPORTED are not retried.
   struct Caps {
     bool metrics = true, vram = true, activity = true, power = true, procs = true, links = true;
+    bool ras_sysfs = true;          // ras/ directory present (else amdsmi ECC calls)
+    uint64_t ecc_blocks = ~0ull;    // AMDSMI_GPU_BLOCK_* bits still worth asking for
+    uint64_t ecc_seen = 0;          // ... and those that answered at least once
   };
   std::vector<Caps> caps_;
   std::vector<std::vector<char>> proc_buf_;  // reusable process-list buffers
@@ -215,9 +230,13 @@ class RocmSmiBackend : public Backend {
   const DeviceStatic& static_info(int i) const override { return devs_[i]; }
   void sample(int i, DeviceSample* out) override;
   bool processes(int i, std::vector<ProcSample>* out) override;
+  bool supports_ras() const override { return true; }
+  void sample_ras(int i, DeviceSample* out) override;  // kernel ras/ sysfs files
   std::string lib_version() const { return lib_version_; }
+  void set_sys_root(std::string r) { sys_root_ = std::move(r); }
 
  private:
+  std::string sys_root_ = "/sys";
   std::string lib_path_;
   std::unique_ptr<RsmiTable> t_;
   bool inited_ = false;

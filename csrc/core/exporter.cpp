@@ -40,7 +40,7 @@ struct Exporter::DevWorker {
   bool busy = false;             // request in flight (posted or running)
   uint64_t req = 0;              // tick id of the current request
   std::atomic<uint64_t> done{0}; // tick id whose results are stored below
-  bool want_links = false, want_procs = false;
+  bool want_links = false, want_procs = false, want_ras = false;
   int64_t started_ns = 0;
   DeviceSample sample;
   std::vector<ProcSample> procs;
@@ -52,7 +52,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
                             Backend* backend, int i) {
   while (true) {
     uint64_t id;
-    bool links, procs;
+    bool links, procs, ras;
     {
       std::unique_lock<std::mutex> lk(w->mu);
       w->cv.wait(lk, [&] { return w->quit || w->pending; });
@@ -61,6 +61,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       id = w->req;
       links = w->want_links;
       procs = w->want_procs;
+      ras = w->want_ras;
     }
     DeviceSample s;
     std::vector<ProcSample> p;
@@ -69,6 +70,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       TraceRange tr("gpumon.sample_dev");
       backend->sample(i, &s);
       if (links) backend->sample_links(i, &s);
+      if (ras && s.ok) backend->sample_ras(i, &s);
       if (procs && s.ok) {
         const int64_t t = mono_ns();
         backend->processes(i, &p);
@@ -184,7 +186,9 @@ std::unique_ptr<Backend> make_backend_from_config(const ExporterConfig& cfg, std
     a->set_fast_path(cfg.fast_path, cfg.sysfs_root, cfg.attribution.procfs_root);
     b = std::move(a);
   } else if (cfg.backend == "rocm_smi") {
-    b = std::make_unique<RocmSmiBackend>(cfg.rocm_smi_lib);
+    auto r = std::make_unique<RocmSmiBackend>(cfg.rocm_smi_lib);
+    r->set_sys_root(cfg.sysfs_root);
+    b = std::move(r);
   } else {
     if (err) *err = "unknown backend '" + cfg.backend + "' (amdsmi | rocm_smi | mock[:k=v,...] | auto)";
     return nullptr;
@@ -222,6 +226,7 @@ bool Exporter::ensure_backend() {
     // auto: libamd_smi missing or failing -> rocm_smi_lib behind the same kind of dlopen table
     auto fb = std::make_unique<RocmSmiBackend>(cfg_.rocm_smi_lib);
     fb->set_device_filter(cfg_.devices);
+    fb->set_sys_root(cfg_.sysfs_root);
     std::string err2;
     if (fb->init(&err2)) {
       GPUMON_LOG(LogLevel::kWarn, "exporter", "amdsmi unavailable (" + err + "); using rocm_smi fallback");
@@ -354,6 +359,11 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
   auto links_due = [&](int i) {
     return links_ok && (tk == 0 || (tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(cfg_.link_every) == 0);
   };
+  // RAS text files (~0.3 ms per device) every `ras_every` ticks, staggered the same way.
+  const bool ras_ok = backend_->supports_ras() && cfg_.ras_every > 0;
+  auto ras_due = [&](int i) {
+    return ras_ok && (tk == 0 || (tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(cfg_.ras_every) == 0);
+  };
   int64_t proc_ns = 0;
   if (static_cast<int>(workers_.size()) != n) {
     // sequential: metrics table, (links), process list per device on the sampler thread
@@ -361,6 +371,7 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
       TraceRange tr("gpumon.sample_dev");
       backend_->sample(i, &(*out)[i]);
       if (links_due(i)) backend_->sample_links(i, &(*out)[i]);
+      if (ras_due(i) && (*out)[i].ok) backend_->sample_ras(i, &(*out)[i]);
       if (cfg_.processes && (*out)[i].ok) {
         const int64_t t = mono_ns();
         backend_->processes(i, &(*procs)[i]);
@@ -380,6 +391,7 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
     w.busy = w.pending = true;
     w.req = id;
     w.want_links = links_due(i);
+    w.want_ras = ras_due(i);
     w.want_procs = cfg_.processes;
     w.started_ns = t0;
     asked[i] = 1;
@@ -555,6 +567,7 @@ TickInfo Exporter::tick() {
             s.links[k].max_bandwidth_gbps = p.links[k].max_bandwidth_gbps;
           if (s.links[k].link_type < 0) s.links[k].link_type = p.links[k].link_type;
         }
+        if (!s.ras.valid && p.ras.valid && s.ok) s.ras = p.ras;  // between RAS refreshes
       }
       // amdsmi_get_link_metrics lists 7 entries (incl. self) while the metrics table has 8 xGMI
       // slots on MI355X: a slot without a link_metrics entry gets speed x width (38 Gb/s x 16 =

@@ -78,7 +78,55 @@ bool MockBackend::init(std::string* err) {
   gfx_act_acc_.assign(n, 0);
   t0_ns_ = mono_ns();
   last_ns_.assign(n, t0_ns_);
+  // RAS: the blocks MI355X publishes under ras/aca_* (measured), all clean
+  ras_.assign(n, RasSample{});
+  for (auto& r : ras_) {
+    r.valid = true;
+    r.source = "mock";
+    for (const char* b : {"gfx", "jpeg", "mmhub", "sdma", "umc", "vcn", "xgmi_wafl"}) {
+      RasCount c;
+      c.block = b;
+      c.has_de = true;
+      r.blocks.push_back(c);
+    }
+    r.fatal = r.poison_created = r.poison_consumed = r.bad_pages = 0;
+  }
   return true;
+}
+
+void MockBackend::sample_ras(int i, DeviceSample* out) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (i < 0 || i >= static_cast<int>(ras_.size())) return;
+  out->ras = ras_[i];
+}
+
+void MockBackend::add_ecc(int dev, const std::string& block, uint64_t ue, uint64_t ce, uint64_t de) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (dev < 0 || dev >= static_cast<int>(ras_.size())) return;
+  for (auto& c : ras_[dev].blocks)
+    if (c.block == block) {
+      c.ue += ue;
+      c.ce += ce;
+      c.de += de;
+      return;
+    }
+  RasCount c;
+  c.block = block;
+  c.ue = ue;
+  c.ce = ce;
+  c.de = de;
+  c.has_de = true;
+  ras_[dev].blocks.push_back(c);
+}
+
+void MockBackend::set_ras_event(int dev, const std::string& event, double value) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (dev < 0 || dev >= static_cast<int>(ras_.size())) return;
+  auto& r = ras_[dev];
+  if (event == "fatal") r.fatal = value;
+  else if (event == "poison_created") r.poison_created = value;
+  else if (event == "poison_consumed") r.poison_consumed = value;
+  else if (event == "bad_pages") r.bad_pages = value;
 }
 
 void MockBackend::set_util(int dev, double pct) {

@@ -383,6 +383,33 @@ void render_prometheus(const RenderInput& in, std::string* o) {
            double g = sm[d].v[F_VRAM_MAX_BW];
            return has(g) ? g * 1e9 : kNaN;
          });
+    // ---- RAS / ECC (ras.h; the reference exports no health data) ----
+    {
+      Family f(o, "gpu_ecc_errors_total",
+               "Accumulated RAS error count by block and type (uncorrectable / correctable / deferred).",
+               "counter");
+      for (size_t d = 0; d < n; ++d) {
+        if (!sm[d].ok || !sm[d].ras.valid) continue;
+        for (const auto& c : sm[d].ras.blocks) {
+          f.add(dl[d], {{"block", c.block}, {"type", "uncorrectable"}}, static_cast<double>(c.ue));
+          f.add(dl[d], {{"block", c.block}, {"type", "correctable"}}, static_cast<double>(c.ce));
+          if (c.has_de) f.add(dl[d], {{"block", c.block}, {"type", "deferred"}}, static_cast<double>(c.de));
+        }
+      }
+    }
+    {
+      Family f(o, "gpu_ras_events_total", "RAS events by kind (fatal error, poison creation / consumption).",
+               "counter");
+      for (size_t d = 0; d < n; ++d) {
+        const auto& r = sm[d].ras;
+        if (!sm[d].ok || !r.valid) continue;
+        f.add(dl[d], {{"event", "fatal"}}, r.fatal);
+        f.add(dl[d], {{"event", "poison_creation"}}, r.poison_created);
+        f.add(dl[d], {{"event", "poison_consumption"}}, r.poison_consumed);
+      }
+    }
+    devf("gpu_retired_pages", "VRAM pages in the bad-page table (retired or pending retirement).", "gauge",
+         [&](size_t d) { return sm[d].ras.valid ? sm[d].ras.bad_pages : kNaN; });
     // ---- xGMI (replaces the reference's absent NVLink fields) ----
     {
       Family fs(o, "gpu_xgmi_link_up", "xGMI link status (1 up, 0 down/disabled).", "gauge");

@@ -16,6 +16,7 @@
 #include "backend.h"
 #include "common.h"
 #include "metrics_table.h"
+#include "ras.h"
 
 namespace gpumon {
 
@@ -255,6 +256,13 @@ bool RocmSmiBackend::processes(int i, std::vector<ProcSample>* out) {
   }
   record_call(kCallProcs, mono_ns() - t0, true);
   return true;
+}
+
+void RocmSmiBackend::sample_ras(int i, DeviceSample* out) {
+  if (i < 0 || i >= static_cast<int>(devs_.size())) return;
+  const int64_t t0 = mono_ns();
+  const bool ok = read_ras_sysfs(sys_root_, devs_[i].bdf, &out->ras);
+  record_call(kCallRas, mono_ns() - t0, ok);
 }
 
 }  // namespace gpumon

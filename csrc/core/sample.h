@@ -129,6 +129,23 @@ struct LinkInfo {
   int status = -1;                   // 0 down, 1 up, 2 disabled
 };
 
+// RAS / ECC error counters of one device (refreshed every `ras_every` ticks; the reference has no
+// health data at all). Source: the kernel's ras/ sysfs files (aca_<block> on MI300/MI355X, or
+// <block>_err_count), else amdsmi_get_gpu_ecc_count per block.
+struct RasCount {
+  std::string block;       // umc, gfx, sdma, mmhub, xgmi_wafl, vcn, jpeg, ...
+  uint64_t ue = 0, ce = 0, de = 0;  // uncorrectable, correctable, deferred (accumulated)
+  bool has_de = false;
+};
+
+struct RasSample {
+  bool valid = false;
+  std::string source;      // "sysfs" | "amdsmi" | "mock"
+  std::vector<RasCount> blocks;
+  double fatal = kNaN, poison_created = kNaN, poison_consumed = kNaN;  // ras/event_state counts
+  double bad_pages = kNaN; // retired / pending VRAM pages (ras/gpu_vram_bad_pages entries)
+};
+
 struct DeviceSample {
   bool ok = false;                  // at least the primary metrics call succeeded
   bool fresh = true;                // firmware table advanced since last tick
@@ -143,6 +160,7 @@ struct DeviceSample {
   int n_links = 0;
   std::array<LinkInfo, kMaxLinks> links;
   Accumulators acc;
+  RasSample ras;                    // valid only on ticks that refreshed it (carried over otherwise)
   uint32_t errors = 0;              // failed calls this tick
   std::string last_error;
 
@@ -158,6 +176,7 @@ struct DeviceSample {
     n_links = 0;
     for (auto& l : links) l = LinkInfo{};
     acc = Accumulators{};
+    ras = RasSample{};
     errors = 0;
     last_error.clear();
   }

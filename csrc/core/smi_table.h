@@ -39,7 +39,9 @@ namespace gpumon {
   X(amdsmi_get_gpu_process_list)        \
   X(amdsmi_get_link_metrics)            \
   X(amdsmi_get_temp_metric)             \
-  X(amdsmi_get_clock_info)
+  X(amdsmi_get_clock_info)             \
+  X(amdsmi_get_gpu_ecc_count)          \
+  X(amdsmi_get_gpu_bad_page_info)
 
 struct SmiTable {
   void* dl = nullptr;

@@ -31,7 +31,7 @@ static void usage() {
           "                       [--listen ADDR:PORT] [--host NAME] [--devices 0,1,..] [--no-fast-path]\n"
           "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
-          "                       [--procfs /proc] [--no-processes] [--no-gzip] [--sample-threads N]\n"
+          "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--no-gzip] [--sample-threads N]\n"
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx] [--once]\n"
           "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri]\n"
           "                       [--pmc] [--pmc-counters A,B,..] [--pmc-window SEC] [--probe] [--probe-every N]\n"
@@ -83,6 +83,7 @@ int main(int argc, char** argv) {
     else if (a == "--user-label") cfg.attribution.user_label = next();
     else if (a == "--procfs") cfg.attribution.procfs_root = next();
     else if (a == "--no-processes") cfg.processes = false;
+    else if (a == "--ras-every") cfg.ras_every = atoi(next().c_str());
     else if (a == "--no-gzip") cfg.gzip = false;
     else if (a == "--sample-threads") cfg.sample_threads = atoi(next().c_str());
     else if (a == "--http-threads") cfg.http_threads = atoi(next().c_str());

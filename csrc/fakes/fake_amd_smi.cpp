@@ -12,6 +12,9 @@
 //   FAKE_AMDSMI_NO_METRICS=1      gpu_metrics NOT_SUPPORTED (exercises the activity/power fallback)
 //   FAKE_AMDSMI_CPX=1             CPX compute partitioning: every socket exposes 8 logical GPUs (one
 //                                 XCD each); partition k's busy counters live in xcp_stats[k]
+//   FAKE_AMDSMI_ECC_UMC_CE=N      correctable UMC errors on device 0 (other ECC blocks: 0; only UMC,
+//                                 SDMA, GFX, MMHUB, XGMI_WAFL answer, as measured on MI355X)
+//   FAKE_AMDSMI_BAD_PAGES=N       bad-page records on device 0
 // Counters advance deterministically per call so rates are checkable.
 #include <amd_smi/amdsmi.h>
 
@@ -231,6 +234,29 @@ amdsmi_status_t amdsmi_get_link_metrics(amdsmi_processor_handle h, amdsmi_link_m
     lm->links[k].link_type = AMDSMI_LINK_TYPE_XGMI;
   }
   (void)h;
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_ecc_count(amdsmi_processor_handle h, amdsmi_gpu_block_t block,
+                                         amdsmi_error_count_t* ec) {
+  const int d = dev_of(h);
+  if (d < 0 || !ec) return AMDSMI_STATUS_INVAL;
+  switch (block) {
+    case AMDSMI_GPU_BLOCK_UMC: case AMDSMI_GPU_BLOCK_SDMA: case AMDSMI_GPU_BLOCK_GFX:
+    case AMDSMI_GPU_BLOCK_MMHUB: case AMDSMI_GPU_BLOCK_XGMI_WAFL: break;
+    default: return AMDSMI_STATUS_API_FAILED;  // what libamd_smi answers for untracked blocks
+  }
+  memset(ec, 0, sizeof *ec);
+  if (d == 0 && block == AMDSMI_GPU_BLOCK_UMC) ec->correctable_count = env_int("FAKE_AMDSMI_ECC_UMC_CE", 0);
+  return AMDSMI_STATUS_SUCCESS;
+}
+
+amdsmi_status_t amdsmi_get_gpu_bad_page_info(amdsmi_processor_handle h, uint32_t* num_pages,
+                                             amdsmi_retired_page_record_t* info) {
+  const int d = dev_of(h);
+  if (d < 0 || !num_pages) return AMDSMI_STATUS_INVAL;
+  *num_pages = d == 0 ? env_int("FAKE_AMDSMI_BAD_PAGES", 0) : 0;
+  (void)info;
   return AMDSMI_STATUS_SUCCESS;
 }
 

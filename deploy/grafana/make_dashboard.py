@@ -101,6 +101,12 @@ def build():
                           "{{host}} gpu{{gpu_id}} {{reason}}")], 12, y, 12, 8,
                         fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
     y += 8
+    panels.append(panel("RAS: ECC errors by block (uncorrectable / correctable / deferred)", "table",
+                        [(f'sum by (host, gpu_id, block, type) (gpu_ecc_errors_total{{{HOST}}}) > 0', "")], 0, y, 12, 8))
+    panels.append(panel("RAS: retired HBM pages and poison / fatal events", "timeseries",
+                        [(f'gpu_retired_pages{{{HOST}}}', "{{host}} gpu{{gpu_id}} retired pages"),
+                         (f'gpu_ras_events_total{{{HOST}}} > 0', "{{host}} gpu{{gpu_id}} {{event}}")], 12, y, 12, 8))
+    y += 8
     panels.append(panel("Exporter: /metrics p99 and tick p99 (s)", "timeseries",
                         [(f'histogram_quantile(0.99, sum by (le, host) (rate(gpumon_scrape_duration_seconds_bucket{{{HOST}}}[5m])))',
                           "{{host}} scrape p99"),

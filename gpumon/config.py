@@ -38,6 +38,7 @@ class Config:
     interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
     processes: bool = True
     link_every: int = 30
+    ras_every: int = 5                    # ticks between RAS / ECC counter refreshes (0 = off)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
     device_timeout_s: float = 2.0         # a device call still running after this is exported as hung
     reinit_after: int = 5                 # ticks with every GPU failing before the backend is re-initialised
@@ -109,6 +110,7 @@ class Config:
             "interval_s": float(self.interval),
             "processes": self.processes,
             "link_every": int(self.link_every),
+            "ras_every": int(self.ras_every),
             "sample_threads": int(self.sample_threads),
             "device_timeout_s": float(self.device_timeout_s),
             "reinit_after": int(self.reinit_after),

@@ -129,8 +129,8 @@ def test_alert_and_recording_rules_resolve(mock_exporter):
     ex.tick()
     fam = promtext.parse(ex.metrics_text())
     produced = {n for f, v in fam.items() for n in [f] + [s[0] for s in v["samples"]]}
-    words = {"sum", "by", "count", "rate", "increase", "avg", "max", "time", "host", "namespace", "podname", "gpu_id",
-             "user_name"}
+    words = {"sum", "by", "count", "rate", "increase", "delta", "avg", "max", "time", "host", "namespace", "podname",
+             "gpu_id", "user_name"}
     exprs = [r["expr"] for g in rule["spec"]["groups"] for r in g["rules"]]
     assert len(exprs) >= 12
     for e in exprs:
@@ -140,7 +140,8 @@ def test_alert_and_recording_rules_resolve(mock_exporter):
             assert name in produced, (e, name)
     label_values = {(k, v) for f in fam.values() for _, labels, _ in f["samples"] for k, v in labels.items()}
     for k, v in [("sensor", "hotspot"), ("sensor", "mem"), ("kind", "socket_thermal"), ("kind", "hbm_thermal"),
-                 ("kind", "vr_thermal"), ("state", "idle")]:
+                 ("kind", "vr_thermal"), ("state", "idle"), ("type", "uncorrectable"), ("type", "correctable"),
+                 ("event", "poison_consumption"), ("event", "fatal")]:
         assert (k, v) in label_values, (k, v)
     kust = _docs("deploy/k8s/kustomization.yaml")[0]
     for r in kust["resources"]:

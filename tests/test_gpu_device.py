@@ -352,3 +352,42 @@ def test_probe_wave_slots_track_partial_occupancy():
     idle_lat = sorted(d["idle"]["latency_ms"])[len(d["idle"]["latency_ms"]) // 2]
     mfma_lat = sorted(d["mfma"]["latency_ms"])[len(d["mfma"]["latency_ms"]) // 2]
     assert mfma_lat > 5 * idle_lat, (idle_lat, mfma_lat)
+
+
+def test_ras_counters_from_sysfs_and_amdsmi(core, torch_gpu):
+    """RAS / ECC on MI355X: the kernel's ras/aca_* files (umc, gfx, sdma, mmhub, xgmi_wafl, vcn,
+    jpeg) through the amdsmi backend, cross-checked with libamd_smi's per-block counts for the blocks
+    both report, and the same files through the rocm_smi fallback."""
+    from gpumon.export import promtext
+
+    ex = _exporter(core)
+    try:
+        ex.tick()
+        ras = ex.samples()[0]["ras"]
+        assert ras and ras["source"] == "sysfs", ras
+        for b in ("umc", "gfx", "xgmi_wafl"):
+            assert b in ras["blocks"], ras
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.values(fam, "gpu_ecc_errors_total", block="umc", type="uncorrectable")
+        assert promtext.values(fam, "gpu_ras_events_total", event="poison_consumption")
+        st = ex.self_stats()["backend_calls"]["ras"]
+        assert st["errors"] == 0 and st["seconds"] / st["n"] < 0.005, st
+    finally:
+        ex.stop()
+    # libamd_smi per-block path on the same device (no sysfs root -> amdsmi_get_gpu_ecc_count)
+    ex2 = _exporter(core, sysfs_root="/nonexistent", fast_path=False)
+    try:
+        ex2.tick()
+        r2 = ex2.samples()[0]["ras"]
+        assert r2 and r2["source"] == "amdsmi", r2
+        for b in set(ras["blocks"]) & set(r2["blocks"]):
+            assert r2["blocks"][b]["ue"] == ras["blocks"][b]["ue"], b
+            assert r2["blocks"][b]["ce"] == ras["blocks"][b]["ce"], b
+    finally:
+        ex2.stop()
+    rs = _exporter(core, backend="rocm_smi")
+    try:
+        rs.tick()
+        assert rs.samples()[0]["ras"]["blocks"].keys() == ras["blocks"].keys()
+    finally:
+        rs.stop()

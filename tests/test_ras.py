@@ -1,0 +1,138 @@
+"""RAS / ECC counters (csrc/core/ras.cpp): the kernel's ras/ sysfs files (aca_<block> on MI355X,
+legacy <block>_err_count, event_state, gpu_vram_bad_pages), the per-block amdsmi fallback, the
+refresh cadence with carry-over, and the mock's fault injection. The on-box file layout was
+measured on MI355X (profiles/r1_ras.md)."""
+
+import os
+
+import pytest
+
+from conftest import make_locked
+from gpumon.export import promtext
+from test_sysfs_fast import FAKE, make_tree
+
+MI355X_EVENT_STATE = ("current seqno: 7\nFatal Error: count:1, last_seqno:3\n"
+                      "Poison Creation: count:2, last_seqno:5\nPoison Consumption: count:4, last_seqno:7\n")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def fakes():
+    make_locked("fakes")
+
+
+def _ras_dir(sysr, d=0):
+    r = sysr / "bus" / "pci" / "devices" / f"0000:{0x26 + 0x20 * d:02x}:00.0" / "ras"
+    r.mkdir(parents=True, exist_ok=True)
+    return r
+
+
+def _exporter(core, monkeypatch, sysr, procr, env=None, **over):
+    for k in ("FAKE_AMDSMI_GPUS", "FAKE_AMDSMI_CPX", "FAKE_AMDSMI_NO_METRICS", "FAKE_AMDSMI_ECC_UMC_CE",
+              "FAKE_AMDSMI_BAD_PAGES"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, str(v))
+    cfg = {"backend": "amdsmi", "amdsmi_lib": FAKE, "serve_http": False, "interval_s": 0, "host": "n1",
+           "verify_kfd": False, "init_retry_s": 0.0, "sysfs_root": str(sysr), "procfs_root": str(procr)}
+    cfg.update(over)
+    ex = core.Exporter(cfg)
+    assert ex.start() == ""
+    return ex
+
+
+def test_sysfs_aca_files(core, monkeypatch, tmp_path):
+    sysr, procr = make_tree(tmp_path)
+    r = _ras_dir(sysr)
+    (r / "aca_umc").write_text("ue: 1\nce: 12\nde: 3\n")
+    (r / "aca_gfx").write_text("ue: 0\nce: 5\nde: 0\n")
+    (r / "aca_xgmi_wafl").write_text("ue: 0\nce: 0\nde: 0\n")
+    (r / "umc_err_count").write_text("ue: 99\nce: 99\n")  # legacy duplicate: the ACA file wins
+    (r / "event_state").write_text(MI355X_EVENT_STATE)
+    (r / "gpu_vram_bad_pages").write_text("0x00001234 : 0x00001000 : R\n0x00005678 : 0x00001000 : P\n")
+    (r / "features").write_text("feature mask: 0x400fdbff\n")
+    ex = _exporter(core, monkeypatch, sysr, procr)
+    try:
+        ex.tick()
+        s = ex.samples()
+        assert s[0]["ras"]["source"] == "sysfs"
+        assert s[0]["ras"]["blocks"]["umc"] == {"ue": 1, "ce": 12, "de": 3}
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpu_ecc_errors_total", gpu_id="0", block="umc", type="uncorrectable") == 1
+        assert promtext.one(fam, "gpu_ecc_errors_total", gpu_id="0", block="umc", type="correctable") == 12
+        assert promtext.one(fam, "gpu_ecc_errors_total", gpu_id="0", block="umc", type="deferred") == 3
+        assert promtext.one(fam, "gpu_ecc_errors_total", gpu_id="0", block="gfx", type="correctable") == 5
+        assert promtext.one(fam, "gpu_ras_events_total", gpu_id="0", event="fatal") == 1
+        assert promtext.one(fam, "gpu_ras_events_total", gpu_id="0", event="poison_creation") == 2
+        assert promtext.one(fam, "gpu_ras_events_total", gpu_id="0", event="poison_consumption") == 4
+        assert promtext.one(fam, "gpu_retired_pages", gpu_id="0") == 2
+        # device 1 has no ras/ directory: amdsmi per-block fallback (5 blocks answer, as on MI355X)
+        assert s[1]["ras"]["source"] == "amdsmi"
+        assert sorted(s[1]["ras"]["blocks"]) == ["gfx", "mmhub", "sdma", "umc", "xgmi_wafl"]
+        assert "ras" in ex.self_stats()["backend_calls"]
+    finally:
+        ex.stop()
+
+
+def test_legacy_err_count_files_without_deferred(core, monkeypatch, tmp_path):
+    sysr, procr = make_tree(tmp_path, gpus=1)
+    r = _ras_dir(sysr)
+    (r / "umc_err_count").write_text("ue: 2\nce: 7\n")
+    (r / "sdma_err_count").write_text("ue: 0\nce: 1\n")
+    ex = _exporter(core, monkeypatch, sysr, procr, env={"FAKE_AMDSMI_GPUS": 1})
+    try:
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpu_ecc_errors_total", block="umc", type="uncorrectable") == 2
+        assert promtext.one(fam, "gpu_ecc_errors_total", block="sdma", type="correctable") == 1
+        assert not promtext.values(fam, "gpu_ecc_errors_total", type="deferred")
+        assert not promtext.values(fam, "gpu_ras_events_total")  # no event_state file
+    finally:
+        ex.stop()
+
+
+def test_amdsmi_fallback_counts_and_bad_pages(core, monkeypatch, tmp_path):
+    sysr, procr = make_tree(tmp_path, gpus=1)
+    ex = _exporter(core, monkeypatch, sysr, procr, env={"FAKE_AMDSMI_GPUS": 1, "FAKE_AMDSMI_ECC_UMC_CE": 6,
+                                                         "FAKE_AMDSMI_BAD_PAGES": 3})
+    try:
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpu_ecc_errors_total", block="umc", type="correctable") == 6
+        assert promtext.one(fam, "gpu_retired_pages", gpu_id="0") == 3
+        assert len(promtext.values(fam, "gpu_ecc_errors_total")) == 5 * 3
+        st = ex.self_stats()["backend_calls"]["ras"]
+        assert st["errors"] == 0  # the blocks MI355X does not track were dropped, not counted as errors
+    finally:
+        ex.stop()
+
+
+def test_refresh_cadence_and_carry_over(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=2", ras_every=3)
+    ex.mock_add_ecc(1, "umc", ue=0, ce=4)
+    seen = []
+    for _ in range(6):
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())
+        seen.append(promtext.values(fam, "gpu_ecc_errors_total", gpu_id="1", block="umc", type="correctable"))
+    # refreshed once within 3 ticks, then carried over on the ticks between refreshes (never missing)
+    first = next(i for i, v in enumerate(seen) if v == [4.0])
+    assert first < 3 and all(v == [4.0] for v in seen[first:]), seen
+    assert all(v in ([0.0], [4.0]) for v in seen)
+    ex.mock_add_ecc(0, "umc", ue=1)
+    ex.mock_set_ras_event(0, "poison_consumed", 2)
+    ex.mock_set_ras_event(0, "bad_pages", 9)
+    for _ in range(3):
+        ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_ecc_errors_total", gpu_id="0", block="umc", type="uncorrectable") == 1
+    assert promtext.one(fam, "gpu_ras_events_total", gpu_id="0", event="poison_consumption") == 2
+    assert promtext.one(fam, "gpu_retired_pages", gpu_id="0") == 9
+    assert promtext.one(fam, "gpu_ecc_errors_total", gpu_id="1", block="umc", type="correctable") == 4
+
+
+def test_ras_off(mock_exporter):
+    ex = mock_exporter(ras_every=0)
+    ex.tick()
+    ex.tick()
+    text = ex.metrics_text()
+    assert "gpu_ecc_errors_total" not in text and "gpu_retired_pages" not in text
