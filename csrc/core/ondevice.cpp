@@ -213,6 +213,7 @@ bool OnDevice::start(std::string* err) {
 
 void OnDevice::stop() {
   if (running_.exchange(false)) {
+    std::lock_guard<std::mutex> g(wait_mu_);  // no lost wake-up between the check and the wait
     wait_cv_.notify_all();
   }
   if (pmc_th_.joinable()) pmc_th_.join();
@@ -332,13 +333,24 @@ void OnDevice::export_pmc() {
   ex_->set_extra("pmc", std::move(out));
 }
 
+// Interruptible sleep to a monotonic deadline, in <= 20 ms system_clock slices: a steady_clock
+// wait compiles to pthread_cond_clockwait, which the toolchain's TSan does not intercept (it then
+// reports the waiting thread as still holding the mutex). Same idiom as Exporter::sample_devices.
+void OnDevice::sleep_until(int64_t deadline_ns) {
+  std::unique_lock<std::mutex> lk(wait_mu_);
+  while (running_) {
+    const int64_t left = deadline_ns - mono_ns();
+    if (left <= 0) return;
+    wait_cv_.wait_until(lk, std::chrono::system_clock::now() +
+                                std::chrono::nanoseconds(std::min<int64_t>(left, 20'000'000)));
+  }
+}
+
 void OnDevice::pmc_loop() {
   while (running_) {
     const int64_t t0 = mono_ns();
     pmc_step();
-    const double left = cfg_.pmc_every_s - (mono_ns() - t0) * 1e-9;
-    std::unique_lock<std::mutex> lk(wait_mu_);
-    wait_cv_.wait_for(lk, std::chrono::duration<double>(std::max(0.0, left)), [this] { return !running_; });
+    sleep_until(t0 + static_cast<int64_t>(cfg_.pmc_every_s * 1e9));
   }
 }
 
@@ -411,9 +423,7 @@ void OnDevice::probe_loop() {
   while (running_) {
     const int64_t t0 = mono_ns();
     probe_step();
-    const double left = cfg_.probe_every_s - (mono_ns() - t0) * 1e-9;
-    std::unique_lock<std::mutex> lk(wait_mu_);
-    wait_cv_.wait_for(lk, std::chrono::duration<double>(std::max(0.0, left)), [this] { return !running_; });
+    sleep_until(t0 + static_cast<int64_t>(cfg_.probe_every_s * 1e9));
   }
 }
 

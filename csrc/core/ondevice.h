@@ -94,6 +94,7 @@ class OnDevice {
   void map_pmc_agents();
   void export_pmc();
   void export_probe();
+  void sleep_until(int64_t deadline_ns);
 
   Exporter* ex_;
   OnDeviceConfig cfg_;

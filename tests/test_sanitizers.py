@@ -23,11 +23,11 @@ def _free_port():
     return p
 
 
-def _run(binary, env_extra):
+def _run(binary, env_extra, extra_args=()):
     port = _free_port()
     env = dict(os.environ, **env_extra)
     p = subprocess.Popen([binary, "--backend", "mock:gpus=4", "--interval", "0.01", "--listen", f"127.0.0.1:{port}",
-                          "--sample-threads", "2", "--http-threads", "2", "--log-level", "error"],
+                          "--sample-threads", "2", "--http-threads", "2", "--log-level", "error", *extra_args],
                          stderr=subprocess.PIPE, stdout=subprocess.DEVNULL, env=env, text=True)
     try:
         deadline = time.time() + 30
@@ -60,16 +60,23 @@ def _run(binary, env_extra):
     return p.returncode, err
 
 
+# the on-device sampler threads (csrc/core/ondevice.cpp) over the fake plugins, plus a RAS refresh
+# every tick: PMC / probe / RAS state crosses threads into set_extra() and the renderer
+ONDEVICE = ("--pmc", "--probe", "--plugin-dir", os.path.join(ROOT, "build", "fakes", "ondevice"), "--ras-every", "1")
+
+
 @pytest.mark.slow
+@pytest.mark.parametrize("extra", [(), ONDEVICE], ids=["core", "ondevice"])
 @pytest.mark.parametrize("target,binary,env", [
     ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
                                           "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
     ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
 ])
-def test_sanitized_exporter_under_concurrent_scrapes(target, binary, env):
-    r = subprocess.run(["make", "-C", ROOT, target], capture_output=True, text=True, timeout=600)
+def test_sanitized_exporter_under_concurrent_scrapes(target, binary, env, extra):
+    r = subprocess.run(["make", "-C", ROOT, target] + (["fakes"] if extra else []), capture_output=True, text=True,
+                       timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
-    rc, err = _run(os.path.join(ROOT, binary), env)
+    rc, err = _run(os.path.join(ROOT, binary), dict(env, GPUMON_FAKE_AGENTS="4"), extra)
     bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
            or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
     assert not bad, err[-4000:]
