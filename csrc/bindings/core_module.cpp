@@ -86,6 +86,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "device_timeout_s", &c.device_timeout_s);
   get(d, "pod_resources_socket", &c.pod_resources_socket);
   get(d, "pod_resources_prefix", &c.pod_resources_prefix);
+  get(d, "pod_resources_dra_drivers", &c.pod_resources_dra_drivers);
   get(d, "pod_resources_refresh_s", &c.pod_resources_refresh_s);
   get(d, "cri_socket", &c.cri_socket);
   get(d, "version", &c.version);
@@ -334,13 +335,13 @@ PYBIND11_MODULE(_core, m) {
       "libamd_smi vs sysfs-decoded gpu_metrics v1.8, field by field: (name, amdsmi, sysfs)");
   m.def(
       "podresources_list",
-      [](const std::string& sock, const std::string& prefix, int timeout_ms) {
+      [](const std::string& sock, const std::string& prefix, int timeout_ms, const std::vector<std::string>& dra) {
         std::vector<PodDeviceRow> rows;
         std::string err;
         bool ok;
         {
           py::gil_scoped_release nogil;
-          ok = podresources_list(sock, prefix, &rows, &err, timeout_ms);
+          ok = podresources_list(sock, prefix, &rows, &err, timeout_ms, dra);
         }
         if (!ok) throw std::runtime_error(err);
         py::list l;
@@ -356,6 +357,7 @@ PYBIND11_MODULE(_core, m) {
         return l;
       },
       py::arg("socket"), py::arg("resource_prefix") = "amd.com/gpu", py::arg("timeout_ms") = 3000,
+      py::arg("dra_drivers") = std::vector<std::string>{"gpu.amd.com"},
       "kubelet PodResources List() through the native HTTP/2 client (grpc_lite.cpp)");
   m.def(
       "cri_list",
@@ -394,16 +396,34 @@ PYBIND11_MODULE(_core, m) {
       py::arg("socket"), py::arg("timeout_ms") = 3000, "CRI ListContainers + ListPodSandbox via grpc_lite.cpp");
   m.def(
       "parse_list_pod_resources",
-      [](py::bytes b, const std::string& prefix) {
+      [](py::bytes b, const std::string& prefix, const std::vector<std::string>& dra) {
         std::vector<PodDeviceRow> rows;
         std::string s = b;
-        if (!parse_list_pod_resources(s, prefix, &rows)) throw std::runtime_error("malformed");
+        if (!parse_list_pod_resources(s, prefix, &rows, dra)) throw std::runtime_error("malformed");
         py::list l;
         for (const auto& r : rows)
           l.append(py::make_tuple(r.pod_namespace, r.pod_name, r.container_name, r.resource_name, r.device_id));
         return l;
       },
-      py::arg("data"), py::arg("resource_prefix") = "");
+      py::arg("data"), py::arg("resource_prefix") = "", py::arg("dra_drivers") = std::vector<std::string>{});
+  m.def(
+      "match_device_id",
+      [](const std::string& id, const py::list& statics) {
+        std::vector<DeviceStatic> st;
+        for (auto o : statics) {
+          py::dict d = o.cast<py::dict>();
+          DeviceStatic s;
+          get(d, "index", &s.index);
+          get(d, "hip_id", &s.hip_id);
+          get(d, "bdf", &s.bdf);
+          get(d, "uuid", &s.uuid);
+          get(d, "drm_card", &s.drm_card);
+          get(d, "drm_render", &s.drm_render);
+          st.push_back(s);
+        }
+        return match_device_id(id, st);
+      },
+      "C++ twin of gpumon.attribution.plane.match_device_id (the native PodResources poller's matcher)");
   m.def("roctx_enable", &Roctx::enable, py::arg("on") = true,
         "Load librocprofiler-sdk-roctx and bracket sampler phases with ROCTx ranges");
   m.def("roctx_active", &Roctx::active);

@@ -920,7 +920,21 @@ std::string lower(std::string s) {
 // Device-plugin device ID -> exporter device index (-1 unknown). The AMD device plugin uses PCI
 // addresses; UUIDs, hip ids and DRM node names are accepted too (gpumon/attribution/plane.py).
 int match_device_id(const std::string& raw, const std::vector<DeviceStatic>& st) {
-  const std::string d = lower(std::string(trim(raw)));
+  std::string d = lower(std::string(trim(raw)));
+  // DRA forms: CDI name "amd.com/gpu=gpu-0" (part after '='), "gpu-N" (hip id), dashed PCI address
+  // "gpu-0000-26-00-0" / "pci-0000-26-00-0" / "0000-26-00-0"
+  if (auto eq = d.find('='); eq != std::string::npos) d = d.substr(eq + 1);
+  {
+    std::string x = d;
+    if (starts_with(x, "gpu-") || starts_with(x, "pci-")) x = x.substr(4);
+    auto hex = [](char c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f'); };
+    if (x.size() == 12 && x[4] == '-' && x[7] == '-' && x[10] == '-' && x[11] >= '0' && x[11] <= '7' &&
+        std::all_of(x.begin(), x.begin() + 4, hex) && hex(x[5]) && hex(x[6]) && hex(x[8]) && hex(x[9]))
+      d = x.substr(0, 4) + ":" + x.substr(5, 2) + ":" + x.substr(8, 2) + "." + x.substr(11);
+    else if (starts_with(d, "gpu-") && d.size() > 4 &&
+             std::all_of(d.begin() + 4, d.end(), [](char c) { return c >= '0' && c <= '9'; }))
+      d = d.substr(4);
+  }
   if (d.empty()) return -1;
   for (const auto& s : st) {
     const std::string bdf = lower(s.bdf);
@@ -944,7 +958,8 @@ bool Exporter::podres_poll_once() {
   std::vector<PodDeviceRow> rows;
   std::string err;
   const int64_t t0 = mono_ns();
-  const bool ok = podresources_list(cfg_.pod_resources_socket, cfg_.pod_resources_prefix, &rows, &err, 3000);
+  const bool ok = podresources_list(cfg_.pod_resources_socket, cfg_.pod_resources_prefix, &rows, &err, 3000,
+                                    cfg_.pod_resources_dra_drivers);
   const double dt = (mono_ns() - t0) * 1e-9;
   std::vector<DeviceStatic> st;
   {

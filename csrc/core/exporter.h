@@ -67,6 +67,7 @@ struct ExporterConfig {
   // control plane (gpumon/attribution) leaves this empty and pushes allocations itself.
   std::string pod_resources_socket;
   std::string pod_resources_prefix = "amd.com/gpu";
+  std::vector<std::string> pod_resources_dra_drivers = {"gpu.amd.com"};  // DRA claim devices counted too
   double pod_resources_refresh_s = 10.0;
   std::string cri_socket;             // native CRI ListContainers/ListPodSandbox (same refresh)
   std::string version = "0.1.0";

@@ -5,6 +5,7 @@
 #include <sys/un.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstring>
 
@@ -275,10 +276,66 @@ bool PbReader::skip(uint32_t wire) {
   }
 }
 
+namespace {
+
+// DynamicResource{2 claim_name, 3 claim_namespace, 4 ClaimResource{1 CDIDevice{1 name}, 2 driver_name,
+// 4 device_name}} -> one row per claimed device of a wanted DRA driver.
+bool parse_dynamic_resource(std::string_view b, const std::vector<std::string>& drivers, const std::string& ns,
+                            const std::string& pod, const std::string& cname, std::vector<PodDeviceRow>* out) {
+  PbReader dr(b);
+  uint32_t f, w;
+  std::vector<std::string_view> claims;
+  while (dr.next(&f, &w)) {
+    std::string_view v;
+    if (w == 2 && f == 4) {
+      if (!dr.bytes(&v)) return false;
+      claims.push_back(v);
+    } else if (!dr.skip(w)) {
+      return false;
+    }
+  }
+  if (!dr.ok()) return false;
+  for (std::string_view cb : claims) {
+    PbReader c(cb);
+    std::string driver, device, cdi;
+    while (c.next(&f, &w)) {
+      std::string_view v;
+      if (w == 2 && (f == 1 || f == 2 || f == 4)) {
+        if (!c.bytes(&v)) return false;
+        if (f == 2) driver.assign(v);
+        else if (f == 4) device.assign(v);
+        else if (cdi.empty()) {  // CDIDevice{1 name}
+          PbReader cd(v);
+          uint32_t f2, w2;
+          while (cd.next(&f2, &w2)) {
+            std::string_view n;
+            if (w2 == 2 && f2 == 1) {
+              if (!cd.bytes(&n)) return false;
+              cdi.assign(n);
+            } else if (!cd.skip(w2)) {
+              return false;
+            }
+          }
+        }
+      } else if (!c.skip(w)) {
+        return false;
+      }
+    }
+    if (!c.ok()) return false;
+    if (std::find(drivers.begin(), drivers.end(), driver) == drivers.end()) continue;
+    const std::string& id = device.empty() ? cdi : device;
+    if (!id.empty()) out->push_back({ns, pod, cname, driver, id});
+  }
+  return true;
+}
+
+}  // namespace
+
 // ListPodResourcesResponse{1: PodResources{1 name, 2 namespace, 3 ContainerResources{1 name,
-// 2 ContainerDevices{1 resource_name, 2 device_ids}}}}  (k8s.io/kubelet podresources/v1 api.proto)
+// 2 ContainerDevices{1 resource_name, 2 device_ids}, 5 DynamicResource}}}  (k8s.io/kubelet
+// podresources/v1 api.proto)
 bool parse_list_pod_resources(std::string_view msg, const std::string& resource_prefix,
-                              std::vector<PodDeviceRow>* out) {
+                              std::vector<PodDeviceRow>* out, const std::vector<std::string>& dra_drivers) {
   PbReader top(msg);
   uint32_t f, w;
   while (top.next(&f, &w)) {
@@ -306,18 +363,21 @@ bool parse_list_pod_resources(std::string_view msg, const std::string& resource_
     for (std::string_view cb : containers) {
       PbReader c(cb);
       std::string cname;
-      std::vector<std::string_view> devs;
+      std::vector<std::string_view> devs, dyn;
       while (c.next(&f, &w)) {
         std::string_view v;
-        if (w == 2 && (f == 1 || f == 2)) {
+        if (w == 2 && (f == 1 || f == 2 || f == 5)) {
           if (!c.bytes(&v)) return false;
           if (f == 1) cname.assign(v);
-          else devs.push_back(v);
+          else if (f == 2) devs.push_back(v);
+          else dyn.push_back(v);
         } else if (!c.skip(w)) {
           return false;
         }
       }
       if (!c.ok()) return false;
+      for (std::string_view db : dyn)
+        if (!dra_drivers.empty() && !parse_dynamic_resource(db, dra_drivers, ns, name, cname, out)) return false;
       for (std::string_view db : devs) {
         PbReader d(db);
         std::string res;
@@ -342,11 +402,12 @@ bool parse_list_pod_resources(std::string_view msg, const std::string& resource_
 }
 
 bool podresources_list(const std::string& socket_path, const std::string& resource_prefix,
-                       std::vector<PodDeviceRow>* out, std::string* err, int timeout_ms) {
+                       std::vector<PodDeviceRow>* out, std::string* err, int timeout_ms,
+                       const std::vector<std::string>& dra_drivers) {
   std::string resp;
   out->clear();
   if (!grpc_unary_unix(socket_path, "/v1.PodResourcesLister/List", "", &resp, err, timeout_ms)) return false;
-  if (!parse_list_pod_resources(resp, resource_prefix, out)) {
+  if (!parse_list_pod_resources(resp, resource_prefix, out, dra_drivers)) {
     *err = "malformed ListPodResourcesResponse";
     return false;
   }

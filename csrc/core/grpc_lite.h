@@ -46,10 +46,14 @@ class PbReader {
 struct PodDeviceRow {
   std::string pod_namespace, pod_name, container_name, resource_name, device_id;
 };
+// Device-plugin rows whose resource starts with `resource_prefix`, plus DRA claim devices
+// (ContainerResources.dynamic_resources) of the drivers in `dra_drivers` (resource_name = driver,
+// device_id = its device name, else the first CDI device name).
 bool podresources_list(const std::string& socket_path, const std::string& resource_prefix,
-                       std::vector<PodDeviceRow>* out, std::string* err, int timeout_ms = 3000);
+                       std::vector<PodDeviceRow>* out, std::string* err, int timeout_ms = 3000,
+                       const std::vector<std::string>& dra_drivers = {});
 bool parse_list_pod_resources(std::string_view msg, const std::string& resource_prefix,
-                              std::vector<PodDeviceRow>* out);
+                              std::vector<PodDeviceRow>* out, const std::vector<std::string>& dra_drivers = {});
 
 // CRI runtime.v1 RuntimeService ListContainers + ListPodSandbox (containerd / cri-o): container id
 // -> pod identity and labels (the reference read the same io.kubernetes.* labels with

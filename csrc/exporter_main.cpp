@@ -34,6 +34,7 @@ static void usage() {
           "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--no-gzip] [--sample-threads N]\n"
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx] [--once]\n"
           "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri]\n"
+          "                       [--dra-drivers gpu.amd.com,..|none]\n"
           "                       [--pmc] [--pmc-counters A,B,..] [--pmc-window SEC] [--probe] [--probe-every N]\n"
           "                       [--probe-blocks N] [--plugin-dir DIR]\n"
           "env: NODE_NAME, INFLUXDB_URL, GPUMON_LISTEN, GPUMON_INTERVAL, GPUMON_BACKEND\n");
@@ -78,6 +79,13 @@ int main(int argc, char** argv) {
     else if (a == "--no-pod-resources") podres = "";
     else if (a == "--cri") cri = next();
     else if (a == "--no-cri") cri = "none";
+    else if (a == "--dra-drivers") {
+      const std::string v = next();
+      cfg.pod_resources_dra_drivers.clear();
+      if (v != "none")
+        for (const auto& d : split(v, ','))
+          if (!d.empty()) cfg.pod_resources_dra_drivers.push_back(d);
+    }
     else if (a == "--opt-in-label") cfg.attribution.opt_in = next();
     else if (a == "--user-regex") cfg.attribution.user_regex = next();
     else if (a == "--user-label") cfg.attribution.user_label = next();

@@ -44,8 +44,9 @@ class DeviceAllocation:
     pod_namespace: str
     pod_name: str
     container_name: str
-    resource_name: str
+    resource_name: str          # device-plugin resource, or the DRA driver name
     device_ids: List[str]
+    claim: str = ""             # DRA: "<claim namespace>/<claim name>"
 
 
 class PodResourcesClient:
@@ -59,7 +60,10 @@ class PodResourcesClient:
         self._alloc = _unary(self._ch, P.PODRESOURCES_ALLOCATABLE, P.AllocatableResourcesRequest,
                              P.AllocatableResourcesResponse)
 
-    def list(self, resource_names: Optional[List[str]] = None) -> List[DeviceAllocation]:
+    def list(self, resource_names: Optional[List[str]] = None,
+             dra_drivers: Optional[List[str]] = None) -> List[DeviceAllocation]:
+        """Device-plugin allocations of ``resource_names`` plus DRA claim devices whose driver is in
+        ``dra_drivers`` (device id = the driver's device name, else its first CDI device)."""
         resp = self._list(P.ListPodResourcesRequest(), timeout=self.timeout_s)
         out = []
         for pod in resp.pod_resources:
@@ -68,6 +72,16 @@ class PodResourcesClient:
                     if resource_names and d.resource_name not in resource_names:
                         continue
                     out.append(DeviceAllocation(pod.namespace, pod.name, c.name, d.resource_name, list(d.device_ids)))
+                if not dra_drivers:
+                    continue
+                for dr in c.dynamic_resources:
+                    for cr in dr.claim_resources:
+                        if cr.driver_name not in dra_drivers:
+                            continue
+                        dev = cr.device_name or (cr.cdi_devices[0].name if cr.cdi_devices else "")
+                        if dev:
+                            out.append(DeviceAllocation(pod.namespace, pod.name, c.name, cr.driver_name, [dev],
+                                                        claim=f"{dr.claim_namespace}/{dr.claim_name}"))
         return out
 
     def allocatable(self, resource_names: Optional[List[str]] = None) -> List[str]:

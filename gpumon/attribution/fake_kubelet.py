@@ -25,6 +25,8 @@ class FakePod:
     annotations: Dict[str, str] = field(default_factory=dict)
     # container name -> (container id, device ids)
     containers: Dict[str, tuple] = field(default_factory=dict)
+    # container name -> DRA claimed devices [(driver, device name, cdi name)] (one claim per container)
+    claims: Dict[str, List[tuple]] = field(default_factory=dict)
 
 
 class FakeKubelet:
@@ -48,6 +50,12 @@ class FakeKubelet:
                 c = pr.containers.add(name=cname)
                 if devs:
                     c.devices.add(resource_name=self.resource_name, device_ids=list(devs))
+                if p.claims.get(cname):
+                    dr = c.dynamic_resources.add(claim_name=f"{p.name}-{cname}-gpu", claim_namespace=p.namespace)
+                    for driver, dev, cdi in p.claims[cname]:
+                        cr = dr.claim_resources.add(driver_name=driver, pool_name="node-a", device_name=dev)
+                        if cdi:
+                            cr.cdi_devices.add(name=cdi)
         return r
 
     def _allocatable(self, req, ctx):

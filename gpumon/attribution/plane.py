@@ -13,6 +13,7 @@ Failures are isolated per source and exported as ``gpumon_control_plane_up{sourc
 from __future__ import annotations
 
 import logging
+import re
 import threading
 import time
 from typing import Dict, List, Optional
@@ -26,13 +27,26 @@ def normalize_id(s: str) -> str:
     return s.strip().lower()
 
 
+_DASHED_BDF = re.compile(r"^(?:gpu-|pci-)?([0-9a-f]{4})-([0-9a-f]{2})-([0-9a-f]{2})-([0-7])$")
+
+
 def match_device_id(dev_id: str, statics: List[dict]) -> int:
     """Map a device-plugin device ID to an exporter device index (-1 if unknown).
 
     Accepts PCI addresses with or without domain (AMD k8s-device-plugin uses the PCI bus id),
-    amdsmi UUIDs, HIP uuids (``GPU-...``), plain hip ids, ``cardN`` / ``renderDN``.
+    amdsmi UUIDs, HIP uuids (``GPU-...``), plain hip ids, ``cardN`` / ``renderDN``, and the DRA
+    forms: a CDI name (``amd.com/gpu=gpu-0``: the part after ``=``), ``gpu-N`` (hip id N) and
+    dashed PCI addresses (``gpu-0000-26-00-0`` / ``0000-26-00-0``). Same rules as the C++
+    ``match_device_id`` (csrc/core/exporter.cpp).
     """
     d = normalize_id(dev_id)
+    if "=" in d:
+        d = d.split("=", 1)[1]
+    m = _DASHED_BDF.match(d)
+    if m:
+        d = "%s:%s:%s.%s" % m.groups()
+    elif d.startswith("gpu-") and d[4:].isdigit():
+        d = d[4:]
     if not d:
         return -1
     for s in statics:
@@ -114,7 +128,7 @@ class ControlPlane:
             try:
                 statics = self.ex.statics()
                 unknown = 0
-                for a in self.podres.list(self.cfg.resource_names):
+                for a in self.podres.list(self.cfg.resource_names, self.cfg.dra_drivers):
                     meta = by_pod_container.get((a.pod_namespace, a.pod_name, a.container_name), {})
                     for did in a.device_ids:
                         idx = match_device_id(did, statics)

@@ -75,11 +75,28 @@ _msg(_pr, "ContainerMemory", [
     ("size", 2, F.TYPE_UINT64, OPT, None),
     ("topology", 3, MSG, OPT, ".v1.TopologyInfo"),
 ])
+# Dynamic Resource Allocation (k8s >= 1.27 kubelet; GPUs claimed through a DRA driver such as
+# gpu.amd.com instead of the amd.com/gpu device-plugin resource). class_name (1) is the 1.27-1.30
+# field, dropped later; decoding ignores it either way.
+_msg(_pr, "CDIDevice", [("name", 1, STR, OPT, None)])
+_msg(_pr, "ClaimResource", [
+    ("cdi_devices", 1, MSG, REP, ".v1.CDIDevice"),
+    ("driver_name", 2, STR, OPT, None),
+    ("pool_name", 3, STR, OPT, None),
+    ("device_name", 4, STR, OPT, None),
+])
+_msg(_pr, "DynamicResource", [
+    ("class_name", 1, STR, OPT, None),
+    ("claim_name", 2, STR, OPT, None),
+    ("claim_namespace", 3, STR, OPT, None),
+    ("claim_resources", 4, MSG, REP, ".v1.ClaimResource"),
+])
 _msg(_pr, "ContainerResources", [
     ("name", 1, STR, OPT, None),
     ("devices", 2, MSG, REP, ".v1.ContainerDevices"),
     ("cpu_ids", 3, I64, REP, None),
     ("memory", 4, MSG, REP, ".v1.ContainerMemory"),
+    ("dynamic_resources", 5, MSG, REP, ".v1.DynamicResource"),
 ])
 _msg(_pr, "PodResources", [
     ("name", 1, STR, OPT, None),

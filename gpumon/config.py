@@ -70,6 +70,8 @@ class Config:
     cri_socket: str = ""                  # e.g. unix:///run/containerd/containerd.sock ; "" = autodetect
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     resource_names: List[str] = field(default_factory=lambda: ["amd.com/gpu"])
+    # DRA drivers whose claimed devices count as GPU allocations (kubelet PodResources dynamic_resources)
+    dra_drivers: List[str] = field(default_factory=lambda: ["gpu.amd.com"])
     metadata_refresh: float = 10.0
     # on-device probe / PMC
     enable_probe: bool = False

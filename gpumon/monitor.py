@@ -53,6 +53,7 @@ class GpuMonitor:
             core_cfg["pod_resources_refresh_s"] = float(self.cfg.metadata_refresh)
             if self.cfg.resource_names:
                 core_cfg["pod_resources_prefix"] = self.cfg.resource_names[0]
+            core_cfg["pod_resources_dra_drivers"] = list(self.cfg.dra_drivers)
         self.control_plane_mode = mode
         self.ex = self._core.Exporter(core_cfg)
         self.plane = None
