@@ -102,6 +102,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "procfs_env_fallback", &a.procfs_env_fallback);
   get(d, "include_host_processes", &a.include_host_processes);
   get(d, "verify_kfd", &a.verify_kfd);
+  get(d, "label_allowlist", &a.label_allowlist);
   if (d.contains("mock") && !d["mock"].is_none()) {
     py::dict m = d["mock"].cast<py::dict>();
     get(m, "gpus", &c.mock.gpus);

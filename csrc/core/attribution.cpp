@@ -150,6 +150,19 @@ Attributor::Attributor(AttributionConfig cfg) : cfg_(std::move(cfg)) {
     opt_key_ = cfg_.opt_in.substr(0, eq);
     opt_val_ = eq == std::string::npos ? "" : cfg_.opt_in.substr(eq + 1);
   }
+  for (const auto& key : cfg_.label_allowlist) {
+    if (key.empty()) continue;
+    std::string name = "label_";
+    for (char c : key)
+      name.push_back((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') ? c : '_');
+    bool dup = false;
+    for (const auto& kv : allow_) dup = dup || kv.second == name;
+    if (dup) {  // "app.kubernetes.io/name" and "app_kubernetes_io_name" would collide: first one wins
+      GPUMON_LOG(LogLevel::kWarn, "attribution", "label allowlist: " + key + " collides with an earlier key");
+      continue;
+    }
+    allow_.emplace_back(key, name);
+  }
   by_cid_ = std::make_shared<std::unordered_map<std::string, ContainerMeta>>();
   by_pod_uid_ = std::make_shared<std::unordered_map<std::string, ContainerMeta>>();
 }
@@ -316,6 +329,7 @@ ProcIdentity Attributor::resolve(uint32_t pid) {
     id.container_name = m->container_name;
     labels = &m->labels;
     id.user_name = !m->user_name.empty() ? m->user_name : derive_user(id.pod_name, m->labels);
+    id.extra_labels = export_labels(m->labels);
   } else if (cg.found && cfg_.procfs_env_fallback) {
     if (!e->env_done) read_env_fallback(pid, e);
     if (!e->env_pod.empty()) {
@@ -332,6 +346,15 @@ ProcIdentity Attributor::resolve(uint32_t pid) {
   id.opted_in = opted_in(*labels);
   if (!cg.found && !cfg_.include_host_processes) id.opted_in = false;
   return id;
+}
+
+LabelPairs Attributor::export_labels(const std::map<std::string, std::string>& labels) const {
+  LabelPairs out;
+  for (const auto& [key, name] : allow_) {
+    auto it = labels.find(key);
+    if (it != labels.end() && !it->second.empty()) out.emplace_back(name, it->second);
+  }
+  return out;
 }
 
 void Attributor::gc(const std::vector<uint32_t>& alive) {

@@ -70,7 +70,12 @@ struct AttributionConfig {
   // an unrelated process: require /proc/<pid>/fd to hold /dev/kfd before trusting /proc/<pid>
   // (an unreadable fd dir is treated as "unknown", not as a mismatch).
   bool verify_kfd = true;
+  // Pod / container label keys copied onto the pod_gpu_* series as label_<key> (non [A-Za-z0-9_]
+  // characters -> '_'), like kube-state-metrics' --metric-labels-allowlist. Empty = none.
+  std::vector<std::string> label_allowlist;
 };
+
+using LabelPairs = std::vector<std::pair<std::string, std::string>>;
 
 struct ProcIdentity {
   bool valid = false;           // /proc/<pid> readable
@@ -87,6 +92,7 @@ struct ProcIdentity {
   std::string pod_uid;
   std::string user_name = "-";
   std::string source;           // meta | procfs | none
+  LabelPairs extra_labels;      // allowlisted pod labels (label_<key>, value)
 };
 
 class Attributor {
@@ -105,6 +111,8 @@ class Attributor {
   std::string derive_user(const std::string& pod_name,
                           const std::map<std::string, std::string>& labels) const;
   bool opted_in(const std::map<std::string, std::string>& labels) const;
+  // Allowlisted labels present in `labels`, as (prometheus label name, value) in allowlist order.
+  LabelPairs export_labels(const std::map<std::string, std::string>& labels) const;
   const AttributionConfig& config() const { return cfg_; }
 
   uint64_t cache_hits() const { return hits_; }
@@ -123,6 +131,7 @@ class Attributor {
   AttributionConfig cfg_;
   std::unique_ptr<std::regex> user_re_;
   std::string opt_key_, opt_val_;
+  std::vector<std::pair<std::string, std::string>> allow_;  // (label key, prometheus name)
   mutable std::mutex mu_;
   std::shared_ptr<const std::unordered_map<std::string, ContainerMeta>> by_cid_;
   std::shared_ptr<const std::unordered_map<std::string, ContainerMeta>> by_pod_uid_;

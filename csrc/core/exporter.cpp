@@ -482,6 +482,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       r.container = id.container_name.empty() ? "-" : id.container_name;
       r.containerid = id.container_id.empty() ? "-" : id.container_id.substr(0, 12);
       r.user_name = id.user_name;
+      r.extra_labels = std::move(id.extra_labels);
       r.used_memory_bytes = has(p.vram_bytes) ? p.vram_bytes : (has(p.mem_bytes) ? p.mem_bytes : 0);
       r.gpu_util = has(dev_util) ? dev_util : 0;
       r.proc_gfx_util = util;
@@ -519,6 +520,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
     r.container = ctr;
     r.containerid = a.container_id.empty() ? "-" : a.container_id.substr(0, 12);
     r.user_name = !a.user_name.empty() ? a.user_name : attr_->derive_user(pod, a.labels);
+    r.extra_labels = attr_->export_labels(a.labels);
     r.used_memory_bytes = 0;
     r.gpu_util = 0;
     rows->push_back(std::move(r));

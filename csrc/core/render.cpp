@@ -482,15 +482,17 @@ void render_prometheus(const RenderInput& in, std::string* o) {
     for (size_t r = 0; r < rows.size(); ++r) {
       const auto& p = rows[r];
       const DeviceStatic* s = p.dev < static_cast<int>(n) ? &st[p.dev] : nullptr;
-      rl[r] = label_str({{"host", in.host},
-                         {"namespace", p.pod_namespace},
-                         {"gpu_id", s ? s->gpu_id : "-"},
-                         {"containerid", p.containerid},
-                         {"pid", p.pid},
-                         {"user_name", p.user_name},
-                         {"procressname", p.procname},  // sic: reference field name (gpu.py:209)
-                         {"podname", p.pod_name},
-                         {"container", p.container}});
+      Labels l = {{"host", in.host},
+                  {"namespace", p.pod_namespace},
+                  {"gpu_id", s ? s->gpu_id : "-"},
+                  {"containerid", p.containerid},
+                  {"pid", p.pid},
+                  {"user_name", p.user_name},
+                  {"procressname", p.procname},  // sic: reference field name (gpu.py:209)
+                  {"podname", p.pod_name},
+                  {"container", p.container}};
+      for (const auto& kv : p.extra_labels) l.emplace_back(kv.first.c_str(), kv.second);
+      rl[r] = label_str(l);
     }
     if (in.compat_families) {
       Family fm(o, "pod_gpu_used_memory", "GPU memory used by the process in MiB (0 for idle rows).",
@@ -540,15 +542,16 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       struct Key {
         std::string ns, pod, container, cid, user;
         int dev;
+        std::vector<std::pair<std::string, std::string>> extra;
         bool operator<(const Key& o) const {
-          return std::tie(ns, pod, container, cid, user, dev) <
-                 std::tie(o.ns, o.pod, o.container, o.cid, o.user, o.dev);
+          return std::tie(ns, pod, container, cid, user, dev, extra) <
+                 std::tie(o.ns, o.pod, o.container, o.cid, o.user, o.dev, o.extra);
         }
       };
       std::map<Key, bool> alloc;  // -> active
       for (const auto& p : rows) {
         if (p.pod_name == "-" && p.containerid == "-") continue;  // host process
-        Key k{p.pod_namespace, p.pod_name, p.container, p.containerid, p.user_name, p.dev};
+        Key k{p.pod_namespace, p.pod_name, p.container, p.containerid, p.user_name, p.dev, p.extra_labels};
         alloc[k] = alloc[k] || !p.idle;
       }
       std::set<int> devs_alloc, devs_active;
@@ -557,15 +560,16 @@ void render_prometheus(const RenderInput& in, std::string* o) {
                  "1 per (pod, container, GPU) holding a GPU; state=active|idle.", "gauge");
         for (const auto& [k, active] : alloc) {
           const DeviceStatic* s = k.dev < static_cast<int>(n) ? &st[k.dev] : nullptr;
-          f.add(label_str({{"host", in.host},
-                           {"namespace", k.ns},
-                           {"podname", k.pod},
-                           {"container", k.container},
-                           {"containerid", k.cid},
-                           {"user_name", k.user},
-                           {"gpu_id", s ? s->gpu_id : "-"},
-                           {"state", active ? "active" : "idle"}}),
-                1.0);
+          Labels l = {{"host", in.host},
+                      {"namespace", k.ns},
+                      {"podname", k.pod},
+                      {"container", k.container},
+                      {"containerid", k.cid},
+                      {"user_name", k.user},
+                      {"gpu_id", s ? s->gpu_id : "-"},
+                      {"state", active ? "active" : "idle"}};
+          for (const auto& kv : k.extra) l.emplace_back(kv.first.c_str(), kv.second);
+          f.add(label_str(l), 1.0);
           devs_alloc.insert(k.dev);
           if (active) devs_active.insert(k.dev);
         }

@@ -34,6 +34,7 @@ struct PodRow {
   double gpu_util = 0;              // device-wide util (reference semantics, Q4)
   double proc_gfx_util = kNaN;      // true per-process util from engine_usage.gfx ns
   double cu_occupancy = kNaN;
+  std::vector<std::pair<std::string, std::string>> extra_labels;  // allowlisted pod labels (label_<key>)
 };
 
 // Histogram with fixed upper bounds (seconds).

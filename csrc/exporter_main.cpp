@@ -31,6 +31,7 @@ static void usage() {
           "                       [--listen ADDR:PORT] [--host NAME] [--devices 0,1,..] [--no-fast-path]\n"
           "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
+          "                       [--pod-labels KEY,KEY..]\n"
           "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--no-gzip] [--sample-threads N]\n"
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx] [--once]\n"
           "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri]\n"
@@ -88,6 +89,7 @@ int main(int argc, char** argv) {
     }
     else if (a == "--opt-in-label") cfg.attribution.opt_in = next();
     else if (a == "--user-regex") cfg.attribution.user_regex = next();
+    else if (a == "--pod-labels") cfg.attribution.label_allowlist = split(next(), ',');
     else if (a == "--user-label") cfg.attribution.user_label = next();
     else if (a == "--procfs") cfg.attribution.procfs_root = next();
     else if (a == "--no-processes") cfg.processes = false;

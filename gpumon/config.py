@@ -61,6 +61,8 @@ class Config:
     opt_in_label: str = ""
     user_label: str = ""
     user_regex: str = ""
+    # pod / container label keys copied onto pod_gpu_* series as label_<key> (kube-state-metrics style)
+    pod_label_allowlist: List[str] = field(default_factory=list)
     user_prefix: str = "turing-gpu-notebook-"
     compat_user_rule: bool = True
     procfs_env_fallback: bool = True
@@ -134,6 +136,7 @@ class Config:
             "opt_in": self.opt_in_label,
             "user_label": self.user_label,
             "user_regex": self.user_regex,
+            "label_allowlist": list(self.pod_label_allowlist),
             "user_prefix": self.user_prefix,
             "compat_user_rule": self.compat_user_rule,
             "procfs_env_fallback": self.procfs_env_fallback,
@@ -220,6 +223,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
                    help="pod_gpu line layout: 2019 (gpu.py, default) or 2018 (img/influxdb.png)")
     p.add_argument("--opt-in-label", dest="opt_in_label", help="only report pods with label KEY=VALUE")
     p.add_argument("--user-regex", dest="user_regex", help="regex on pod name; group 1 = user")
+    p.add_argument("--pod-labels", dest="pod_label_allowlist",
+                   help="comma-separated pod label keys exported on pod_gpu_* series as label_<key>")
     p.add_argument("--user-label", dest="user_label", help="pod label holding the user name")
     p.add_argument("--procfs-root", dest="procfs_root")
     p.add_argument("--cri-socket", dest="cri_socket")

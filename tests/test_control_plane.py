@@ -132,3 +132,28 @@ def test_cri_version_and_allocatable(kubelet):
     assert p.allocatable(["amd.com/gpu"]) == kubelet.allocatable
     c.close()
     p.close()
+
+
+def test_pod_label_allowlist_on_pod_gpu_series(kubelet, mock_exporter, tmp_path):
+    """Allowlisted pod labels (kube-state-metrics style) land on every pod_gpu_* series of the pod,
+    active and idle rows, as label_<sanitised key>; other labels do not."""
+    kubelet.pods = [
+        FakePod("train-a-0", "ml", "uid-a", labels={"team": "vision", "app.kubernetes.io/name": "trainer",
+                                                    "secret-ish": "no"},
+                containers={"nb": (CID_A, ["0000:05:00.0"])}),
+        FakePod("idle-b-0", "ml", "uid-b", labels={"team": "nlp"}, containers={"main": (CID_B, ["0000:25:00.0"])}),
+    ]
+    _fake_proc(tmp_path, 1000, CID_A)
+    ex = mock_exporter(backend="mock:gpus=2", procfs_root=str(tmp_path),
+                       label_allowlist=["team", "app.kubernetes.io/name", "missing"])
+    ex.mock_set_procs([{"pid": 1000, "device": 0, "name": "python", "vram_bytes": 5 << 30}])
+    plane = ControlPlane(ex, Config(cri_socket=kubelet.cri_socket, pod_resources_socket=kubelet.podres_socket))
+    plane.refresh_once()
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    (active,) = [s for s in fam["pod_gpu_used_memory_bytes"]["samples"] if s[1]["podname"] == "train-a-0"]
+    assert active[1]["label_team"] == "vision" and active[1]["label_app_kubernetes_io_name"] == "trainer"
+    assert "label_secret_ish" not in active[1] and "label_missing" not in active[1]
+    (idle,) = [s for s in fam["pod_gpu_allocated"]["samples"] if s[1]["podname"] == "idle-b-0"]
+    assert idle[1]["label_team"] == "nlp" and idle[1]["state"] == "idle"
+    plane.stop()
