@@ -26,10 +26,10 @@ PYBIND11_MODULE(_hip, m) {
   }, py::arg("dev"), py::arg("a"), py::arg("b"), py::arg("out"), py::arg("blocks"), py::arg("iters"),
      py::arg("stream") = 0, py::arg("shape") = 32);
   m.def("stream_copy", [](int dev, uintptr_t src, uintptr_t dst, size_t n16, int blocks, uintptr_t stream,
-                          int unroll) {
-    launch_stream_copy(dev, P(src), P(dst), n16, blocks, P(stream), unroll);
+                          int unroll, int policy, bool span) {
+    launch_stream_copy(dev, P(src), P(dst), n16, blocks, P(stream), unroll, policy, span);
   }, py::arg("dev"), py::arg("src"), py::arg("dst"), py::arg("n16"), py::arg("blocks") = 4096,
-     py::arg("stream") = 0, py::arg("unroll") = 4);
+     py::arg("stream") = 0, py::arg("unroll") = 4, py::arg("policy") = 0, py::arg("span") = false);
   m.def("stream_triad", [](int dev, uintptr_t a, uintptr_t b, uintptr_t c, float s, size_t n, int blocks,
                            uintptr_t stream) {
     launch_stream_triad(dev, static_cast<const float*>(P(a)), static_cast<const float*>(P(b)),

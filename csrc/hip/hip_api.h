@@ -25,7 +25,10 @@ void launch_mfma_tile(int dev, const void* a, const void* b, float* c, int iters
 void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blocks, int iters, void* stream,
                       int shape = 32);
 // dst = src (n16 = number of 16-byte vectors)
-void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream, int unroll = 4);
+// policy: 0 nt loads + nt stores, 1 plain, 2 plain loads + nt stores, 3 nt loads + plain stores;
+// span: each block copies one contiguous range instead of grid-striding
+void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream, int unroll = 4,
+                        int policy = 0, bool span = false);
 // c = a + s * b  (fp32, n elements, n % 4 == 0)
 void launch_stream_triad(int dev, const float* a, const float* b, float* c, float s, size_t n, int blocks,
                          void* stream);

@@ -112,9 +112,22 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(const i32x4* __restric
   }
 }
 
+// Cache policy of the streamed operands: bit 0 = non-temporal loads, bit 1 = non-temporal stores
+// (kStreamNtNt = both, the load generator's choice; the sweep in tools/hbm_sweep.py times all four).
+template <int POL>
+__device__ __forceinline__ i32x4 ld16(const i32x4* p) {
+  if constexpr (POL & 1) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int POL>
+__device__ __forceinline__ void st16(i32x4 v, i32x4* p) {
+  if constexpr (POL & 2) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // U independent 16-B loads in flight per lane before the stores (each k-slice of a 256*U-vector
 // chunk is one fully coalesced 4 KiB wave-group access); grid-stride over chunks.
-template <int U>
+template <int U, int POL>
 __global__ void __launch_bounds__(256) stream_copy_unrolled_kernel(const i32x4* __restrict__ src,
                                                                    i32x4* __restrict__ dst, size_t n) {
   const size_t chunk = static_cast<size_t>(256) * U;
@@ -122,14 +135,39 @@ __global__ void __launch_bounds__(256) stream_copy_unrolled_kernel(const i32x4* 
     i32x4 v[U];
     if (base + chunk <= n) {
 #pragma unroll
-      for (int k = 0; k < U; ++k) v[k] = __builtin_nontemporal_load(src + base + k * 256 + threadIdx.x);
+      for (int k = 0; k < U; ++k) v[k] = ld16<POL>(src + base + k * 256 + threadIdx.x);
 #pragma unroll
-      for (int k = 0; k < U; ++k) __builtin_nontemporal_store(v[k], dst + base + k * 256 + threadIdx.x);
+      for (int k = 0; k < U; ++k) st16<POL>(v[k], dst + base + k * 256 + threadIdx.x);
     } else {
 #pragma unroll
       for (int k = 0; k < U; ++k) {
         const size_t i = base + k * 256 + threadIdx.x;
-        if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+        if (i < n) st16<POL>(ld16<POL>(src + i), dst + i);
+      }
+    }
+  }
+}
+
+// Contiguous-span variant: block b copies [b*span, (b+1)*span) in U-vector chunks, so each CU walks
+// one long run of DRAM pages instead of hopping by gridDim*chunk.
+template <int U, int POL>
+__global__ void __launch_bounds__(256) stream_copy_span_kernel(const i32x4* __restrict__ src, i32x4* __restrict__ dst,
+                                                               size_t n, size_t span) {
+  const size_t chunk = static_cast<size_t>(256) * U;
+  const size_t lo = static_cast<size_t>(blockIdx.x) * span;
+  const size_t hi = lo + span < n ? lo + span : n;
+  for (size_t base = lo; base < hi; base += chunk) {
+    i32x4 v[U];
+    if (base + chunk <= hi) {
+#pragma unroll
+      for (int k = 0; k < U; ++k) v[k] = ld16<POL>(src + base + k * 256 + threadIdx.x);
+#pragma unroll
+      for (int k = 0; k < U; ++k) st16<POL>(v[k], dst + base + k * 256 + threadIdx.x);
+    } else {
+#pragma unroll
+      for (int k = 0; k < U; ++k) {
+        const size_t i = base + k * 256 + threadIdx.x;
+        if (i < hi) st16<POL>(ld16<POL>(src + i), dst + i);
       }
     }
   }
@@ -225,16 +263,45 @@ void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blo
   check(hipGetLastError(), "mfma_burn_kernel");
 }
 
-void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream, int unroll) {
+namespace {
+template <int U, int POL>
+void copy_launch(hipStream_t s, const i32x4* in, i32x4* out, size_t n16, int blocks, bool span) {
+  if (span) {
+    const size_t chunk = static_cast<size_t>(256) * U;
+    const size_t per = (n16 + blocks - 1) / blocks;
+    const size_t sp = (per + chunk - 1) / chunk * chunk;  // whole chunks per block
+    hipLaunchKernelGGL((stream_copy_span_kernel<U, POL>), dim3(blocks), dim3(256), 0, s, in, out, n16, sp);
+  } else {
+    hipLaunchKernelGGL((stream_copy_unrolled_kernel<U, POL>), dim3(blocks), dim3(256), 0, s, in, out, n16);
+  }
+}
+template <int U>
+void copy_policy(int policy, hipStream_t s, const i32x4* in, i32x4* out, size_t n16, int blocks, bool span) {
+  switch (policy) {
+    case 0: copy_launch<U, 3>(s, in, out, n16, blocks, span); break;  // nt loads + nt stores (default)
+    case 1: copy_launch<U, 0>(s, in, out, n16, blocks, span); break;  // plain / plain
+    case 2: copy_launch<U, 2>(s, in, out, n16, blocks, span); break;  // plain loads, nt stores
+    case 3: copy_launch<U, 1>(s, in, out, n16, blocks, span); break;  // nt loads, plain stores
+    default: throw std::invalid_argument("stream_copy: policy must be 0..3");
+  }
+}
+}  // namespace
+
+void launch_stream_copy(int dev, const void* src, void* dst, size_t n16, int blocks, void* stream, int unroll,
+                        int policy, bool span) {
   check(hipSetDevice(dev), "hipSetDevice");
+  if (blocks <= 0) throw std::invalid_argument("stream_copy: blocks must be > 0");
   auto s = static_cast<hipStream_t>(stream);
   auto in = static_cast<const i32x4*>(src);
   auto out = static_cast<i32x4*>(dst);
   switch (unroll) {
-    case 1: hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, s, in, out, n16); break;
-    case 2: hipLaunchKernelGGL(stream_copy_unrolled_kernel<2>, dim3(blocks), dim3(256), 0, s, in, out, n16); break;
-    case 4: hipLaunchKernelGGL(stream_copy_unrolled_kernel<4>, dim3(blocks), dim3(256), 0, s, in, out, n16); break;
-    case 8: hipLaunchKernelGGL(stream_copy_unrolled_kernel<8>, dim3(blocks), dim3(256), 0, s, in, out, n16); break;
+    case 1:
+      if (policy == 0 && !span) hipLaunchKernelGGL(stream_copy_kernel, dim3(blocks), dim3(256), 0, s, in, out, n16);
+      else copy_policy<1>(policy, s, in, out, n16, blocks, span);
+      break;
+    case 2: copy_policy<2>(policy, s, in, out, n16, blocks, span); break;
+    case 4: copy_policy<4>(policy, s, in, out, n16, blocks, span); break;
+    case 8: copy_policy<8>(policy, s, in, out, n16, blocks, span); break;
     default: throw std::invalid_argument("stream_copy: unroll must be 1, 2, 4 or 8");
   }
   check(hipGetLastError(), "stream_copy_kernel");
@@ -300,9 +367,12 @@ void LoadGen::loop() {
     const int cus = device_cu_count(dev_);
     // 8 blocks x 4 waves requested per CU (residency then limited by VGPRs: ~7 waves/SIMD at 68 VGPRs)
     const int burn_blocks = kind_ == "partial" ? cus / 4 : cus * 8;  // partial: ~1/4 of the CUs busy
-    // 8192 workgroups x unroll 4: best of the interleaved sweep on MI355X (5.74 TB/s copy vs 4.79 for
-    // 4096 x 1; profiles/r1_kernels_and_pmc.md)
-    const int stream_blocks = cus * 32;
+    // One 16-B vector per lane and one 4 KiB chunk per workgroup, the grid covering the buffer once
+    // (no grid-stride loop), nt loads + nt stores: 6.52 TB/s copy on MI355X vs 5.37-5.74 for the
+    // earlier 8192 x unroll-4 grid-stride form, 6.20 for PyTorch's elementwise kernel and 4.75 for
+    // hipMemcpy D2D in the same interleaved sweep (profiles/r1_hbm_stream.md)
+    const size_t n16 = bytes_ / 16;
+    const int stream_blocks = static_cast<int>((n16 + 255) / 256);
     bool flip = false;
     while (running_) {
       // one kind per batch so the event time is attributed to exactly one kernel kind
@@ -315,7 +385,7 @@ void LoadGen::loop() {
           launch_mfma_burn(dev_, a_, b_, out_, burn_blocks, iters_, s, shape_);
           fl += static_cast<double>(burn_blocks) * 4 * 4 * iters_ * 32768.0;
         } else {
-          launch_stream_copy(dev_, src_, dst_, bytes_ / 16, stream_blocks, s);
+          launch_stream_copy(dev_, src_, dst_, n16, stream_blocks, s, 1, 0, true);
           by += 2.0 * static_cast<double>(bytes_);
         }
         launches_++;
