@@ -6,7 +6,8 @@ launches of the gfx950 kernels in ``csrc/hip/kernels.hip``:
 * ``mfma``  — bf16 MFMA burn: ``mfma_shape=16`` = ``v_mfma_f32_16x16x32_bf16`` x 8 chains per wave
   (2.24 PFLOP/s sustained on MI355X, profiles/r1_kernels_and_pmc.md), ``32`` =
   ``v_mfma_f32_32x32x16_bf16`` x 4 chains (1.76–2.0 PFLOP/s: the chip holds a lower clock on it);
-* ``hbm``   — 16 B/lane non-temporal copy over a ``hbm_bytes`` buffer pair (HBM3E bound);
+* ``hbm``   — 16 B/lane non-temporal copy over a ``hbm_bytes`` buffer pair, one 4 KiB chunk per
+  workgroup (6.5 TB/s on MI355X, profiles/r1_hbm_stream.md);
 * ``mixed`` — alternating; ``duty`` < 1 inserts idle gaps (partial-utilisation validation).
 """
 
