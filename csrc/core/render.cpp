@@ -793,6 +793,16 @@ void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::str
         std::string key = "xcd" + std::to_string(k) + "_busy";
         field(key.c_str(), sm[d].xcd_busy[k]);
       }
+      if (sm[d].ras.valid) {  // RAS totals over every block (ras.h)
+        double ue = 0, ce = 0;
+        for (const auto& c : sm[d].ras.blocks) {
+          ue += static_cast<double>(c.ue);
+          ce += static_cast<double>(c.ce);
+        }
+        field("ecc_uncorrectable", ue);
+        field("ecc_correctable", ce);
+        field("retired_pages", sm[d].ras.bad_pages);
+      }
       if (!first) {
         o->push_back(' ');
         o->append(std::to_string(ts_ns));

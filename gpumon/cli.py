@@ -101,6 +101,8 @@ def render_top(statics, samples, rates, rows) -> str:
 
 
 def cmd_top(args) -> int:
+    if args.url:
+        return _top_remote(args)
     from .monitor import GpuMonitor
 
     cfg = from_args(args)
@@ -116,6 +118,28 @@ def cmd_top(args) -> int:
             sys.stdout.flush()
             n += 1
     return 0
+
+
+def _top_remote(args) -> int:
+    """Fleet view: read running exporters' /metrics instead of opening a GPU (export/fleet.py)."""
+    from .export import fleet
+
+    urls = [u if "://" in u else f"http://{u}" for u in args.url]
+    urls = [u if u.rstrip("/").endswith("/metrics") else u.rstrip("/") + "/metrics" for u in urls]
+    n, rc = 0, 0
+    while args.iterations <= 0 or n < args.iterations:
+        t0 = time.monotonic()
+        frames, errors = fleet.fetch(urls)
+        text = fleet.render(frames, errors)
+        if sys.stdout.isatty():
+            sys.stdout.write("\x1b[2J\x1b[H")
+        sys.stdout.write(text + "\n")
+        sys.stdout.flush()
+        rc = 1 if errors and not frames else 0
+        n += 1
+        if args.iterations <= 0 or n < args.iterations:
+            time.sleep(max(0.0, (args.interval or 1.0) - (time.monotonic() - t0)))
+    return rc
 
 
 def cmd_scrape(args) -> int:
@@ -233,9 +257,11 @@ def build_parser() -> argparse.ArgumentParser:
     add_cli_args(s)
     s.add_argument("--format", choices=["prom", "influx", "json"], default="prom")
     s.set_defaults(fn=cmd_once)
-    s = sub.add_parser("top", help="live console view")
+    s = sub.add_parser("top", help="live console view (local GPUs, or running exporters with --url)")
     add_cli_args(s)
     s.add_argument("--iterations", type=int, default=0)
+    s.add_argument("--url", action="append", default=[],
+                   help="exporter to read instead of the local GPUs (HOST:PORT or URL; repeat for a fleet view)")
     s.set_defaults(fn=cmd_top)
     s = sub.add_parser("scrape", help="measure /metrics latency")
     s.add_argument("url")

@@ -78,7 +78,7 @@ def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
     for fam in frames:
         for r in gpu_rows(fam):
             xcd = " ".join(f"{int(x):3d}" for x in r["xcd"][:8]) if r["xcd"] else "-"
-            vram = "-" if r["vram_used"] is None else f"{r['vram_used'] / 2**30:5.1f}/{(r['vram_total'] or 0) / 2**30:5.0f}"
+            vram = "-" if r["vram_used"] is None else f"{r['vram_used'] / 2**30:.1f}/{(r['vram_total'] or 0) / 2**30:.0f}"
             lines.append(f"{r['host'][:19]:<20}{r['gpu_id']:>4} {_f(r['up'], 2)} {_f(r['util'], 6)} {xcd:<32} "
                          f"{vram:>13} {_f(r['power'], 6)} {_f(r['hot'], 6)} {_f(r['gfx_mhz'], 8)} "
                          f"{_f(r['mfma'], 6, 1)} {_f(r['ecc_ue'], 7)}")

@@ -1,0 +1,60 @@
+"""Fleet view (gpumon/export/fleet.py, `gpumon top --url ...`): several running exporters read over
+HTTP, rendered as the reference's two Grafana views (per-card gauges, container table) in a
+terminal, without opening a GPU."""
+
+import os
+
+from gpumon import cli
+from gpumon.export import fleet, promtext
+
+
+def _node(mock_exporter, host, gpus=2):
+    ex = mock_exporter(backend=f"mock:gpus={gpus},mode=load", host=host, ras_every=1)
+    ex.set_allocations([{"pod_namespace": "ml", "pod_name": f"{host}-job-0", "container_name": "c", "gpu_index": 0}])
+    ex.mock_set_procs([{"pid": os.getpid(), "device": 1, "name": "python3", "vram_bytes": 3 << 30}])
+    ex.mock_add_ecc(1, "umc", ue=2)
+    ex.tick()
+    ex.tick()
+    return ex
+
+
+def test_gpu_and_pod_rows_from_an_exposition(mock_exporter):
+    ex = _node(mock_exporter, "node-a")
+    fam = promtext.parse(ex.metrics_text())
+    rows = fleet.gpu_rows(fam)
+    assert [(r["host"], r["gpu_id"]) for r in rows] == [("node-a", "0"), ("node-a", "1")]
+    r1 = rows[1]
+    assert r1["up"] == 1 and len(r1["xcd"]) == 8 and r1["vram_total"] > 280 * 2 ** 30
+    assert r1["ecc_ue"] == 2 and rows[0]["ecc_ue"] == 0
+    pods = fleet.pod_rows(fam)
+    assert {p["podname"] for p in pods} >= {"node-a-job-0"}
+    assert any(p["pid"] == str(os.getpid()) and p["used_memory_bytes"] == 3 << 30 for p in pods)
+
+
+def test_cli_top_over_two_exporters(mock_exporter, capsys):
+    a, b = _node(mock_exporter, "node-a"), _node(mock_exporter, "node-b", gpus=3)
+    rc = cli.main(["top", "--url", f"127.0.0.1:{a.port}", "--url", f"http://127.0.0.1:{b.port}/metrics",
+                   "--iterations", "1"])
+    out = capsys.readouterr().out
+    assert rc == 0
+    gpu_lines = [l for l in out.splitlines() if l.startswith("node-")]
+    assert sum(l.startswith("node-a") for l in gpu_lines) >= 2 + 2  # 2 GPUs + pod rows
+    assert "node-b-job-0" in out and "ECC-UE" in out
+    assert sum(1 for l in out.splitlines() if l.startswith("node-b") and "/288 " in l) == 3  # GPU rows
+
+
+def test_unreachable_exporter_is_reported(mock_exporter, capsys):
+    a = _node(mock_exporter, "node-a", gpus=1)
+    rc = cli.main(["top", "--url", f"127.0.0.1:{a.port}", "--url", "127.0.0.1:9", "--iterations", "1"])
+    out = capsys.readouterr().out
+    assert rc == 0 and "127.0.0.1:9/metrics:" in out
+    assert cli.main(["top", "--url", "127.0.0.1:9", "--iterations", "1"]) == 1
+
+
+def test_influx_extended_carries_ras_totals(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1", influx_extended=True, ras_every=1)
+    ex.mock_add_ecc(0, "umc", ue=1, ce=5)
+    ex.mock_add_ecc(0, "gfx", ce=2)
+    ex.tick()
+    (ext,) = [l for l in ex.influx_text().splitlines() if l.startswith("gpu_ext,")]
+    assert "ecc_uncorrectable=1" in ext and "ecc_correctable=7" in ext and "retired_pages=0" in ext
