@@ -727,7 +727,7 @@ PYBIND11_MODULE(_core, m) {
   m.def("default_plugin_dir", &default_plugin_dir);
   m.def(
       "pmc_derive",
-      [](const py::dict& raw, const py::dict& agent) {
+      [](const py::dict& raw, const py::dict& agent, double window_s) {
         std::map<std::string, PmcReduced> r;
         for (auto kv : raw) {
           py::dict v = kv.second.cast<py::dict>();
@@ -743,7 +743,7 @@ PYBIND11_MODULE(_core, m) {
         get(agent, "simd_count", &a.simd_count);
         get(agent, "num_xcc", &a.num_xcc);
         get(agent, "max_waves_per_cu", &a.max_waves_per_cu);
-        PmcDerived d = pmc_derive(r, a);
+        PmcDerived d = pmc_derive(r, a, window_s);
         py::dict out;
         auto put = [&](const char* k, double v) {
           if (v == v) out[k] = v;
@@ -752,7 +752,13 @@ PYBIND11_MODULE(_core, m) {
         put("occupancy", d.occupancy);
         put("gui_active", d.gui_active);
         if (!d.xcd_mfma_busy.empty()) out["xcd_mfma_busy"] = d.xcd_mfma_busy;
+        if (!d.mfma_tflops.empty()) {
+          py::dict tf;
+          for (const auto& [dt, v] : d.mfma_tflops) tf[py::str(dt)] = v;
+          out["mfma_tflops"] = tf;
+        }
         return out;
       },
+      py::arg("raw"), py::arg("agent"), py::arg("window_s") = 0.0,
       "C++ twin of gpumon.ops.pmc.derive (used by the native samplers)");
 }

@@ -594,6 +594,17 @@ TickInfo Exporter::tick() {
       }
       if (s.ok) info.devices_ok++;
       proc_counts[i] = procs[i].size();
+      // device-level spatial occupancy: CUs holding any process's waves (every process, opted in or not)
+      if (s.ok && cfg_.processes) {
+        double cu = 0;
+        bool any = false;
+        for (const auto& p : procs[i])
+          if (has(p.cu_occupancy)) {
+            cu += p.cu_occupancy;
+            any = true;
+          }
+        if (any || procs[i].empty()) s.v[F_CU_OCC] = cu;
+      }
     }
     int64_t tb = mono_ns();
     {

@@ -21,7 +21,8 @@ static const char* kFieldNames[F_COUNT] = {
     "vclk0_cur",     "dclk0_cur",      "throttle_status", "indep_throttle", "fan_rpm",
     "pcie_width",    "pcie_speed_gts", "pcie_bw_inst",   "pcie_replay",    "pcie_l0_recov",
     "pcie_nak_sent", "pcie_nak_rcvd",  "volt_soc",       "volt_gfx",       "volt_mem",
-    "xgmi_link_width", "xgmi_link_speed", "vram_max_bw", "num_partition",  "gfxclk_lock"};
+    "xgmi_link_width", "xgmi_link_speed", "vram_max_bw", "num_partition",  "gfxclk_lock",
+    "cu_occupancy"};
 
 int field_by_name(const std::string& name) {
   for (int i = 0; i < F_COUNT; ++i)

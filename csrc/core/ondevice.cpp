@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cctype>
 #include <cstring>
 
 #include "../plugins/ondevice_abi.h"
@@ -120,8 +121,17 @@ std::string default_plugin_dir() {
 // ---------------------------------------------------------------------------------------------
 // derivation (mirrors gpumon/ops/pmc.py derive())
 
-PmcDerived pmc_derive(const std::map<std::string, PmcReduced>& raw, const PmcAgentInfo& agent) {
+PmcDerived pmc_derive(const std::map<std::string, PmcReduced>& raw, const PmcAgentInfo& agent, double window_s) {
   PmcDerived d;
+  if (window_s > 0) {
+    static const std::string kMops = "SQ_INSTS_VALU_MFMA_MOPS_";
+    for (const auto& [name, v] : raw) {  // std::map: sorted by counter name
+      if (name.compare(0, kMops.size(), kMops) != 0) continue;
+      std::string dt = name.substr(kMops.size());
+      for (auto& c : dt) c = static_cast<char>(std::tolower(static_cast<unsigned char>(c)));
+      d.mfma_tflops.emplace_back(dt, 512.0 * v.sum / window_s / 1e12);
+    }
+  }
   auto get = [&](const char* k) -> const PmcReduced* {
     auto it = raw.find(k);
     return it == raw.end() ? nullptr : &it->second;
@@ -303,7 +313,7 @@ void OnDevice::pmc_step() {
         r.by_xcc.assign(v.by_xcc, v.by_xcc + std::max(0, std::min<int>(v.n_xcc, GPUMON_PMC_MAX_XCC)));
         raw[cfg_.pmc_counters[c]] = std::move(r);
       }
-      pmc_last_[devs[k]] = pmc_derive(raw, agents_[ags[k]]);
+      pmc_last_[devs[k]] = pmc_derive(raw, agents_[ags[k]], cfg_.pmc_window_s);
       pmc_samples_++;
     }
   }
@@ -320,6 +330,13 @@ void OnDevice::export_pmc() {
     for (size_t x = 0; x < d.xcd_mfma_busy.size(); ++x) {
       out.push_back(xs("gpu_xcd_mfma_busy_percent", "MFMA pipe busy % per XCD.", dev, d.xcd_mfma_busy[x]));
       out.back().labels.push_back({"xcd", std::to_string(x)});
+    }
+    for (const auto& [dt, tf] : d.mfma_tflops) {
+      out.push_back(xs("gpu_mfma_tflops",
+                       "Achieved MFMA throughput by operand type in TFLOP/s (512 x SQ_INSTS_VALU_MFMA_MOPS_<type> "
+                       "over the counting window; every process).",
+                       dev, tf));
+      out.back().labels.push_back({"dtype", dt});
     }
     if (!std::isnan(d.occupancy))
       out.push_back(xs("gpu_occupancy_percent", "Resident waves / max waves % (rocprofiler device counting).", dev,

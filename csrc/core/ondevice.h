@@ -31,8 +31,13 @@ class Exporter;
 struct OnDeviceConfig {
   std::string plugin_dir;   // "" = $GPUMON_PLUGIN_DIR or <dir of this object>/../lib
   bool pmc = false;
-  std::vector<std::string> pmc_counters = {"SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE",
-                                           "GRBM_COUNT"};
+  // MFMA busy + MFMA MOPS per operand type + GRBM: 8 SQ + 2 GRBM = one gfx950 counting pass. No
+  // per-wave SQ counters: they count only the profiling process's waves (gpumon/ops/pmc.py).
+  std::vector<std::string> pmc_counters = {
+      "SQ_VALU_MFMA_BUSY_CYCLES",    "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_VALU_MFMA_MOPS_F16",
+      "SQ_INSTS_VALU_MFMA_MOPS_F8",  "SQ_INSTS_VALU_MFMA_MOPS_F6F4", "SQ_INSTS_VALU_MFMA_MOPS_F32",
+      "SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_INSTS_VALU_MFMA_MOPS_I8",   "GRBM_GUI_ACTIVE",
+      "GRBM_COUNT"};
   double pmc_every_s = 1.0;
   double pmc_window_s = 0.1;  // counting window per sample (capped at half the period)
   bool probe = false;
@@ -58,10 +63,12 @@ struct PmcAgentInfo {
 struct PmcDerived {
   double mfma_busy = kNaN, occupancy = kNaN, gui_active = kNaN;
   std::vector<double> xcd_mfma_busy;
+  std::vector<std::pair<std::string, double>> mfma_tflops;  // (dtype lower-case, TFLOP/s), by name
 };
 
 // Pure (CPU-tested against gpumon.ops.pmc.derive): the gfx9xx formulas ROCm 7.2 falls back to on gfx950.
-PmcDerived pmc_derive(const std::map<std::string, PmcReduced>& raw, const PmcAgentInfo& agent);
+// window_s > 0 adds the MFMA TFLOP/s per operand type (512 FLOP per SQ_INSTS_VALU_MFMA_MOPS_* unit).
+PmcDerived pmc_derive(const std::map<std::string, PmcReduced>& raw, const PmcAgentInfo& agent, double window_s = 0);
 
 // Directory the plugins are looked up in (see OnDeviceConfig::plugin_dir).
 std::string default_plugin_dir();

@@ -383,6 +383,14 @@ void render_prometheus(const RenderInput& in, std::string* o) {
            double g = sm[d].v[F_VRAM_MAX_BW];
            return has(g) ? g * 1e9 : kNaN;
          });
+    devf("gpu_cu_occupancy_percent",
+         "Share of the GPU's compute units holding waves of any process, in percent (KFD cu_occupancy summed "
+         "over processes, capped at 100; the per-process split is pod_gpu_proc_cu_occupancy_percent).",
+         "gauge", [&](size_t d) {
+           const double cu = sm[d].v[F_CU_OCC];
+           const int n_cu = st[d].num_cu;
+           return has(cu) && n_cu > 0 ? std::min(100.0, 100.0 * cu / n_cu) : kNaN;
+         });
     // ---- RAS / ECC (ras.h; the reference exports no health data) ----
     {
       Family f(o, "gpu_ecc_errors_total",

@@ -91,6 +91,7 @@ enum Field : int {
   F_VRAM_MAX_BW,        // GB/s
   F_NUM_PARTITION,
   F_GFXCLK_LOCK,
+  F_CU_OCC,             // CUs holding waves, summed over the device's processes (KFD cu_occupancy)
   F_COUNT
 };
 

@@ -6,6 +6,7 @@
 //   GPUMON_FAKE_AGENTS      GPU agents / HIP devices (default 1)
 //   GPUMON_FAKE_MFMA        MFMA busy fraction 0..1 (default 0.5), spread evenly over 8 XCCs
 //   GPUMON_FAKE_OCC         occupancy fraction 0..1 (default 0.25)
+//   GPUMON_FAKE_TFLOPS      bf16 MFMA TFLOP/s (default 1000; f16 at a tenth, other types 0)
 //   GPUMON_FAKE_PMC_FAIL    "init" -> init fails; "sample" -> every sample reports not-ok
 //   GPUMON_FAKE_PROBE_HANG  1 -> launches never complete (timeouts path)
 #include <cstdio>
@@ -62,7 +63,10 @@ EXPORT int gpumon_pmc_agent(int agent, gpumon_pmc_agent_t* out) {
 }
 
 EXPORT size_t gpumon_pmc_supported(int, char* buf, size_t n) {
-  const char* s = "GRBM_COUNT\nGRBM_GUI_ACTIVE\nSQ_VALU_MFMA_BUSY_CYCLES\nSQ_WAVE_CYCLES\n";
+  const char* s =
+      "GRBM_COUNT\nGRBM_GUI_ACTIVE\nSQ_VALU_MFMA_BUSY_CYCLES\nSQ_WAVE_CYCLES\nSQ_INSTS_VALU_MFMA_MOPS_BF16\n"
+      "SQ_INSTS_VALU_MFMA_MOPS_F16\nSQ_INSTS_VALU_MFMA_MOPS_F8\nSQ_INSTS_VALU_MFMA_MOPS_F6F4\n"
+      "SQ_INSTS_VALU_MFMA_MOPS_F32\nSQ_INSTS_VALU_MFMA_MOPS_F64\nSQ_INSTS_VALU_MFMA_MOPS_I8\n";
   if (buf && n) snprintf(buf, n, "%s", s);
   return strlen(s) + 1;
 }
@@ -98,6 +102,10 @@ EXPORT int gpumon_pmc_sample_many(const int* ags, int n_agents, const char* cons
         total = envd("GPUMON_FAKE_MFMA", 0.5) * gui * kSimds;
       } else if (name == "SQ_WAVE_CYCLES") {
         total = envd("GPUMON_FAKE_OCC", 0.25) * gui * kCus * kWaves / 4.0;
+      } else if (name.rfind("SQ_INSTS_VALU_MFMA_MOPS_", 0) == 0) {
+        const double tf = envd("GPUMON_FAKE_TFLOPS", 1000.0);
+        const std::string dt = name.substr(24);
+        total = (dt == "BF16" ? tf : dt == "F16" ? tf / 10 : 0.0) * 1e12 * window_s / 512.0;
       } else {
         snprintf(err, errlen, "counter not supported: %s", name.c_str());
         return -1;

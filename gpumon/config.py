@@ -82,9 +82,13 @@ class Config:
     ondevice: str = "native"              # native (C++ samplers over lib/ plugins) | python (gpumon/ops runners)
     plugin_dir: str = ""                  # "" = <tree>/lib or $GPUMON_PLUGIN_DIR
     roctx: bool = False                   # ROCTx ranges around sampler phases (rocprofv3 --marker-trace)
-    # the counters gpumon.ops.pmc.derive() needs (2 SQ + 2 GRBM slots: one counting pass on gfx950)
-    pmc_counters: List[str] = field(default_factory=lambda: ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES",
-                                                             "GRBM_GUI_ACTIVE", "GRBM_COUNT"])
+    # the counters gpumon.ops.pmc.derive() needs (8 SQ + 2 GRBM slots: one counting pass on gfx950):
+    # MFMA busy + MFMA MOPS per operand type; no per-wave SQ counters (they count only the profiling
+    # process's own waves, profiles/r1_pmc_cross_process.md)
+    pmc_counters: List[str] = field(default_factory=lambda: (
+        ["SQ_VALU_MFMA_BUSY_CYCLES"] + ["SQ_INSTS_VALU_MFMA_MOPS_" + d for d in
+                                        ("BF16", "F16", "F8", "F6F4", "F32", "F64", "I8")]
+        + ["GRBM_GUI_ACTIVE", "GRBM_COUNT"]))
     # rates calibration
     activity_acc_scale: float = 1.0
     xgmi_kb_bytes: float = 1024.0

@@ -1,13 +1,21 @@
-"""Device-wide PMC sampling (rocprofiler-sdk device counting) -> MFMA busy / occupancy series.
+"""Device-wide PMC sampling (rocprofiler-sdk device counting) -> MFMA busy / throughput series.
 
 Exported per GPU (derived with the gfx9xx formulas ROCm 7.2 falls back to for gfx950, see
 MI355X_MICROARCH.md §rocprofv3 PMC slots):
 
 * ``gpu_mfma_busy_percent``      = 100 * sum(SQ_VALU_MFMA_BUSY_CYCLES) / (max(GRBM_GUI_ACTIVE) * SIMDs)
 * ``gpu_xcd_mfma_busy_percent``  = the same per XCC (when the counter carries an XCC dimension)
-* ``gpu_occupancy_percent``      = 400 * sum(SQ_WAVE_CYCLES) / max(GRBM_GUI_ACTIVE) / CUs / max_waves_per_cu
+* ``gpu_mfma_tflops{dtype}``     = 512 * sum(SQ_INSTS_VALU_MFMA_MOPS_<DTYPE>) / window / 1e12
+  (achieved matrix-core throughput per operand type: bf16, f16, f8, f6f4, f32, f64, i8)
 * ``gpu_gui_active_percent``     = 100 * max(GRBM_GUI_ACTIVE) / max(GRBM_COUNT)
 * ``gpu_pmc_window_seconds``     — counting window per sample (duty cycle = window / interval)
+* ``gpu_occupancy_percent``      = 400 * sum(SQ_WAVE_CYCLES) / max(GRBM_GUI_ACTIVE) / CUs / max_waves_per_cu,
+  only when SQ_WAVE_CYCLES is configured explicitly: on ROCm 7.2 device counting the per-wave SQ
+  counters (SQ_WAVES, SQ_WAVE_CYCLES, SQ_BUSY_CYCLES, SQ_LEVEL_WAVES, SQ_INSTS_*) count only the
+  waves of the profiling process, while the per-SIMD ones above (MFMA busy, MFMA MOPS) count every
+  process (measured on MI355X: profiles/r1_pmc_cross_process.md). An exporter never owns the
+  workload, so the default set has no wave counters; occupancy comes from KFD instead
+  (``gpu_cu_occupancy_percent``, ``pod_gpu_proc_cu_occupancy_percent``) and from the K1 probe.
 
 ``init()`` of the native module must run before anything initialises HSA/HIP in the process
 (rocprofiler_force_configure); :class:`gpumon.monitor.GpuMonitor` starts the PMC runner first.
@@ -22,8 +30,14 @@ import time
 from typing import Dict, List
 
 log = logging.getLogger("gpumon.pmc")
+TFLOPS_HELP = ("Achieved MFMA throughput by operand type in TFLOP/s (512 x SQ_INSTS_VALU_MFMA_MOPS_<type> over the "
+               "counting window; every process).")
 
-DEFAULT_COUNTERS = ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
+# 8 SQ + 2 GRBM: exactly one counting pass on gfx950 (8 SQ / 2 GRBM counter slots)
+MFMA_DTYPES = ["BF16", "F16", "F8", "F6F4", "F32", "F64", "I8"]
+DEFAULT_COUNTERS = (["SQ_VALU_MFMA_BUSY_CYCLES"] + ["SQ_INSTS_VALU_MFMA_MOPS_" + d for d in MFMA_DTYPES]
+                    + ["GRBM_GUI_ACTIVE", "GRBM_COUNT"])
+MOPS_FLOP = 512.0  # FLOP per SQ_INSTS_VALU_MFMA_MOPS_* unit
 
 
 def pmc_module():
@@ -33,9 +47,15 @@ def pmc_module():
         raise ImportError("gpumon._pmc is not built; run `make pmc`") from e
 
 
-def derive(raw: Dict[str, dict], agent: dict) -> Dict[str, object]:
-    """Turn reduced counter values into percentages (pure function, unit-tested on CPU)."""
+def derive(raw: Dict[str, dict], agent: dict, window_s: float = 0.0) -> Dict[str, object]:
+    """Turn reduced counter values into percentages / TFLOP/s (pure function, unit-tested on CPU;
+    C++ twin: gpumon._core.pmc_derive)."""
     out: Dict[str, object] = {}
+    if window_s > 0:
+        tf = {k[len("SQ_INSTS_VALU_MFMA_MOPS_"):].lower(): MOPS_FLOP * v["sum"] / window_s / 1e12
+              for k, v in raw.items() if k.startswith("SQ_INSTS_VALU_MFMA_MOPS_")}
+        if tf:
+            out["mfma_tflops"] = tf
     gui = raw.get("GRBM_GUI_ACTIVE", {}).get("max", 0.0)
     simds = agent.get("simd_count") or (agent.get("cu_count", 0) * 4)
     cus = agent.get("cu_count") or 0
@@ -96,7 +116,7 @@ class PmcRunner:
                 if raw is None:
                     self.errors += 1
                     continue
-                res[dev] = derive(raw, self.agents[self.map[dev]])
+                res[dev] = derive(raw, self.agents[self.map[dev]], self.window_s)
                 res[dev]["raw"] = raw
             self.last.update(res)
             self._export()
@@ -104,7 +124,7 @@ class PmcRunner:
         for dev, ai in self.map.items():
             try:
                 raw = self.P.sample(ai, self.counters, self.window_s)
-                res[dev] = derive(raw, self.agents[ai])
+                res[dev] = derive(raw, self.agents[ai], self.window_s)
                 res[dev]["raw"] = raw
             except Exception as e:  # noqa: BLE001
                 self.errors += 1
@@ -124,6 +144,8 @@ class PmcRunner:
                 add("gpu_mfma_busy_percent", "MFMA pipe busy % (rocprofiler device counting).", dev, d["mfma_busy"])
             for x, v in enumerate(d.get("xcd_mfma_busy", [])):
                 add("gpu_xcd_mfma_busy_percent", "MFMA pipe busy % per XCD.", dev, v, {"xcd": str(x)})
+            for dt, v in sorted(d.get("mfma_tflops", {}).items()):
+                add("gpu_mfma_tflops", TFLOPS_HELP, dev, v, {"dtype": dt})
             if "occupancy" in d:
                 add("gpu_occupancy_percent", "Resident waves / max waves % (rocprofiler device counting).", dev,
                     d["occupancy"])

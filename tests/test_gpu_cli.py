@@ -23,7 +23,9 @@ def test_once_with_probe_and_pmc():
     assert len(promtext.values(fam, "gpu_probe_xcd_clock_mhz", gpu_id="0")) == 8
     assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
     assert promtext.values(fam, "gpu_mfma_busy_percent", gpu_id="0")
-    assert promtext.values(fam, "gpu_occupancy_percent", gpu_id="0")
+    assert promtext.values(fam, "gpu_mfma_tflops", gpu_id="0", dtype="bf16")
+    assert not promtext.values(fam, "gpu_occupancy_percent")  # no per-wave counters by default
+    assert promtext.values(fam, "gpu_cu_occupancy_percent", gpu_id="0")
     assert len(promtext.values(fam, "gpu_xcd_mfma_busy_percent", gpu_id="0")) == 8
     assert promtext.one(fam, "gpumon_backend_calls_total", call="gpu_metrics") >= 2
 
@@ -72,6 +74,9 @@ def test_native_binary_pmc_probe_under_mfma_load():
     assert r.returncode == 0, r.stderr[-2000:]
     fam = promtext.parse(r.stdout)
     assert promtext.one(fam, "gpu_mfma_busy_percent", gpu_id="0") > 50
+    # the burn runs in ANOTHER process: the MOPS counters see it (per-wave SQ counters would not)
+    assert promtext.one(fam, "gpu_mfma_tflops", gpu_id="0", dtype="bf16") > 1000
+    assert promtext.one(fam, "gpu_cu_occupancy_percent", gpu_id="0") > 90  # KFD: every CU holds burn waves
     assert len(promtext.values(fam, "gpu_xcd_mfma_busy_percent", gpu_id="0")) == 8
     assert promtext.one(fam, "gpu_pmc_window_seconds", gpu_id="0") == pytest.approx(0.2)
     assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8

@@ -25,6 +25,11 @@ def test_pmc_separates_idle_mfma_hbm():
     assert d["hbm"].get("mfma_busy", 0) < 5
     assert d["hbm"]["occupancy"] > 20
     assert d["mfma"]["gui_active"] > 90
+    # achieved bf16 MFMA throughput from SQ_INSTS_VALU_MFMA_MOPS_BF16 (LoadGen reports ~2 PFLOP/s)
+    assert 1000 < d["mfma"]["mfma_tflops"]["bf16"] < 2600, d["mfma"]
+    assert d["idle"].get("mfma_tflops", {}).get("bf16", 0) < 5 and d["hbm"]["mfma_tflops"]["bf16"] < 5
+    tf_load = d["mfma_load"]["tflops"]
+    assert abs(d["mfma"]["mfma_tflops"]["bf16"] - tf_load) < 0.25 * tf_load, (d["mfma"], tf_load)
     # partial occupancy (burn on ~1/4 of the CUs): busy GPU, but MFMA pipes mostly idle
     assert 5 < d["partial"]["mfma_busy"] < 0.6 * d["mfma"]["mfma_busy"], d["partial"]
     assert len(d["mfma"].get("xcd_mfma_busy", [])) == 8

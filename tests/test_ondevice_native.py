@@ -47,9 +47,10 @@ _pos = st.floats(min_value=0, max_value=1e12, allow_nan=False)
 
 
 @settings(max_examples=200, deadline=None)
-@given(gui=_pos, cnt=_pos, mfma=_pos, waves=_pos, nx=st.integers(0, 8), has=st.lists(st.booleans(), min_size=4,
-                                                                                     max_size=4))
-def test_pmc_derive_matches_python(gui, cnt, mfma, waves, nx, has):
+@given(gui=_pos, cnt=_pos, mfma=_pos, waves=_pos, nx=st.integers(0, 8), has=st.lists(st.booleans(), min_size=5,
+                                                                                     max_size=5),
+       mops=_pos, window=st.sampled_from([0.0, 0.05, 0.1]))
+def test_pmc_derive_matches_python(gui, cnt, mfma, waves, nx, has, mops, window):
     raw = {}
     if has[0]:
         raw["GRBM_GUI_ACTIVE"] = {"sum": gui * 8, "max": gui, "n": 8, "by_xcc": []}
@@ -59,10 +60,13 @@ def test_pmc_derive_matches_python(gui, cnt, mfma, waves, nx, has):
         raw["SQ_VALU_MFMA_BUSY_CYCLES"] = {"sum": mfma, "max": mfma, "n": 8, "by_xcc": [mfma / nx] * nx if nx else []}
     if has[3]:
         raw["SQ_WAVE_CYCLES"] = {"sum": waves, "max": waves, "n": 8, "by_xcc": []}
+    if has[4]:
+        raw["SQ_INSTS_VALU_MFMA_MOPS_BF16"] = {"sum": mops, "max": mops, "n": 8, "by_xcc": []}
+        raw["SQ_INSTS_VALU_MFMA_MOPS_F6F4"] = {"sum": mops / 3, "max": mops, "n": 8, "by_xcc": []}
     from gpumon import core
 
-    py = derive(raw, AGENT)
-    cc = core().pmc_derive(raw, AGENT)
+    py = derive(raw, AGENT, window)
+    cc = core().pmc_derive(raw, AGENT, window)
     assert set(py) == set(cc)
     for k in py:
         assert cc[k] == pytest.approx(py[k], rel=1e-12)
@@ -80,6 +84,7 @@ def test_native_samplers_export_series(core, mock_exporter, monkeypatch):
     monkeypatch.setenv("GPUMON_FAKE_AGENTS", "2")
     monkeypatch.setenv("GPUMON_FAKE_MFMA", "0.75")
     monkeypatch.setenv("GPUMON_FAKE_OCC", "0.5")
+    monkeypatch.setenv("GPUMON_FAKE_TFLOPS", "2000")
     ex = mock_exporter()
     od = _ondevice(core, ex)
     od.start()
@@ -89,7 +94,10 @@ def test_native_samplers_export_series(core, mock_exporter, monkeypatch):
         m = ex.metrics_text()
         for g in ("0", "1"):
             assert _val(m, "gpu_mfma_busy_percent", gpu_id=g) == pytest.approx(75.0)
-            assert _val(m, "gpu_occupancy_percent", gpu_id=g) == pytest.approx(50.0)
+            assert _val(m, "gpu_mfma_tflops", gpu_id=g, dtype="bf16") == pytest.approx(2000.0)
+            assert _val(m, "gpu_mfma_tflops", gpu_id=g, dtype="f16") == pytest.approx(200.0)
+            assert _val(m, "gpu_mfma_tflops", gpu_id=g, dtype="f64") == 0
+            assert _val(m, "gpu_occupancy_percent", gpu_id=g) is None  # no wave counters by default
             assert _val(m, "gpu_gui_active_percent", gpu_id=g) == pytest.approx(100.0)
             assert _val(m, "gpu_pmc_window_seconds", gpu_id=g) == pytest.approx(0.01)
             for x in range(8):
@@ -108,6 +116,21 @@ def test_native_samplers_export_series(core, mock_exporter, monkeypatch):
     ex.tick()
     m = ex.metrics_text()
     assert "gpu_mfma_busy_percent" not in m and "gpu_probe_pending" not in m  # series withdrawn on stop
+
+
+def test_explicit_wave_counter_gives_occupancy(core, mock_exporter, monkeypatch):
+    monkeypatch.setenv("GPUMON_FAKE_OCC", "0.5")
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, probe=False, pmc_counters=["SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT"])
+    od.start()
+    try:
+        od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        assert _val(m, "gpu_occupancy_percent", gpu_id="0") == pytest.approx(50.0)
+        assert "gpu_mfma_tflops" not in m
+    finally:
+        od.stop()
 
 
 def test_background_threads_keep_sampling(core, mock_exporter, monkeypatch):

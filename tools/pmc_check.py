@@ -19,8 +19,17 @@ def main():
     agents = P.agents()
     out = {"agents": agents, "n": n}
     counters = DEFAULT_COUNTERS
+    # occupancy needs the per-wave SQ_WAVE_CYCLES, which counts only this process's waves: valid
+    # here because SyntheticLoad runs in-process (the exporter's default set leaves it out)
+    occ = ["SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
+
+    def measure():
+        d = derive(P.sample(0, counters, 0.2), agents[0], 0.2)
+        d["occupancy"] = derive(P.sample(0, occ, 0.2), agents[0]).get("occupancy", 0.0)
+        return d
+
     raw = P.sample(0, counters, 0.2)
-    out["idle"] = derive(raw, agents[0])
+    out["idle"] = measure()
     out["idle_raw"] = raw
     from gpumon.ops.load import SyntheticLoad
 
@@ -28,12 +37,12 @@ def main():
         with SyntheticLoad(0, kind) as load:
             time.sleep(1.0)
             raw = P.sample(0, counters, 0.2)
-            out[kind] = derive(raw, agents[0])
+            out[kind] = measure()
             out[kind + "_raw"] = {k: {"sum": v["sum"], "max": v["max"], "n": v["n"]} for k, v in raw.items()}
             out[kind + "_load"] = load.stats()
             if kind == "mfma":  # shared-window path used by PmcRunner on multi-GPU nodes
                 many = P.sample_many(list(range(len(agents))), counters, 0.2)
-                out["mfma_many"] = [derive(r, agents[i]) if r is not None else None for i, r in enumerate(many)]
+                out["mfma_many"] = [derive(r, agents[i], 0.2) if r is not None else None for i, r in enumerate(many)]
     print(json.dumps(out, default=str))
 
 
