@@ -88,9 +88,14 @@ def build():
     y += 8
     panels.append(panel("Probe: effective shader clock per XCD (MHz)", "timeseries",
                         [(f'gpu_probe_xcd_clock_mhz{{{HOST}}}', "{{host}} gpu{{gpu_id}} xcd{{xcd}}")], 0, y, 12, 8))
-    panels.append(panel("PMC: MFMA busy % / occupancy %", "timeseries",
-                        [(f'gpu_mfma_busy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} mfma"),
-                         (f'gpu_occupancy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} occupancy")], 12, y, 12, 8))
+    panels.append(panel("PMC: MFMA busy % / KFD CU occupancy %", "timeseries",
+                        [(f'gpu_mfma_busy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} mfma busy"),
+                         (f'gpu_cu_occupancy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} CUs occupied")], 12, y, 12, 8,
+                        fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
+    y += 8
+    panels.append(panel("PMC: achieved MFMA TFLOP/s by operand type", "timeseries",
+                        [(f'sum by (host, gpu_id, dtype) (gpu_mfma_tflops{{{HOST}}}) > 0',
+                          "{{host}} gpu{{gpu_id}} {{dtype}}")], 0, y, 24, 8))
     y += 8
     panels.append(panel("Per-pod compute share (% of CUs holding the pod's waves)", "timeseries",
                         [(f'sum by (host, gpu_id, namespace, podname) (pod_gpu_proc_cu_occupancy_percent{{{HOST}}})',
