@@ -339,7 +339,7 @@ void OnDevice::export_pmc() {
       out.back().labels.push_back({"dtype", dt});
     }
     if (!std::isnan(d.occupancy))
-      out.push_back(xs("gpu_occupancy_percent", "Resident waves / max waves % (rocprofiler device counting).", dev,
+      out.push_back(xs("gpu_occupancy_percent", "Resident waves / max waves % from SQ_WAVE_CYCLES (only when configured; counts the profiling process own waves).", dev,
                        d.occupancy));
     if (!std::isnan(d.gui_active))
       out.push_back(xs("gpu_gui_active_percent", "GRBM GUI active % of the counting window.", dev, d.gui_active));

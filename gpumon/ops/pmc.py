@@ -147,7 +147,7 @@ class PmcRunner:
             for dt, v in sorted(d.get("mfma_tflops", {}).items()):
                 add("gpu_mfma_tflops", TFLOPS_HELP, dev, v, {"dtype": dt})
             if "occupancy" in d:
-                add("gpu_occupancy_percent", "Resident waves / max waves % (rocprofiler device counting).", dev,
+                add("gpu_occupancy_percent", "Resident waves / max waves % from SQ_WAVE_CYCLES (only when configured; counts the profiling process own waves).", dev,
                     d["occupancy"])
             if "gui_active" in d:
                 add("gpu_gui_active_percent", "GRBM GUI active % of the counting window.", dev, d["gui_active"])
