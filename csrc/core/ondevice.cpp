@@ -166,6 +166,10 @@ OnDevice::OnDevice(Exporter* ex, OnDeviceConfig cfg) : ex_(ex), cfg_(std::move(c
 OnDevice::~OnDevice() { stop(); }
 
 bool OnDevice::start(std::string* err) {
+  if (stopped_) {
+    *err = "on-device samplers already stopped";
+    return false;
+  }
   const std::string dir = cfg_.plugin_dir.empty() ? default_plugin_dir() : cfg_.plugin_dir;
   char ebuf[512] = {0};
   if (cfg_.pmc) {
@@ -222,6 +226,9 @@ bool OnDevice::start(std::string* err) {
 }
 
 void OnDevice::stop() {
+  // idempotent: the destructor calls it again, possibly during interpreter teardown, and must not
+  // touch the exporter a second time
+  if (stopped_.exchange(true)) return;
   if (running_.exchange(false)) {
     std::lock_guard<std::mutex> g(wait_mu_);  // no lost wake-up between the check and the wait
     wait_cv_.notify_all();

@@ -129,6 +129,7 @@ class OnDevice {
   std::vector<ProbeDev> probes_;
 
   std::atomic<bool> running_{false};
+  std::atomic<bool> stopped_{false};
   std::mutex wait_mu_;
   std::condition_variable wait_cv_;
   std::thread pmc_th_, probe_th_;
