@@ -146,3 +146,21 @@ def test_alert_and_recording_rules_resolve(mock_exporter):
     kust = _docs("deploy/k8s/kustomization.yaml")[0]
     for r in kust["resources"]:
         assert os.path.exists(os.path.join(ROOT, "deploy/k8s", r)), r
+
+
+def test_validation_job_and_tools_image():
+    """The node-validation Job (reference Dockerfile2's debug-image role, made purpose-built) runs
+    tools that exist in the tree, on the tools image, with the DaemonSet's device access."""
+    (job,) = _docs("deploy/k8s/gpumon-validate-job.yaml")
+    assert job["apiVersion"] == "batch/v1" and job["kind"] == "Job"
+    spec = job["spec"]["template"]["spec"]
+    assert spec["restartPolicy"] == "Never" and spec["hostPID"] is True
+    (c,) = spec["containers"]
+    assert c["image"].startswith("gpumon-tools:")
+    script = c["args"][0]
+    for tool in re.findall(r"(tools/[a-z_]+\.py|bench\.py)", script):
+        assert os.path.exists(os.path.join(ROOT, tool)), tool
+    mounts = {m["mountPath"] for m in c["volumeMounts"]}
+    assert {"/sys", "/dev/kfd", "/dev/dri"} <= mounts
+    txt = open(os.path.join(ROOT, "deploy/Dockerfile.tools")).read()
+    assert "COPY tools /opt/gpumon/tools" in txt and "rocprofv3" in txt

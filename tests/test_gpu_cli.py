@@ -81,3 +81,39 @@ def test_native_binary_pmc_probe_under_mfma_load():
     assert promtext.one(fam, "gpu_pmc_window_seconds", gpu_id="0") == pytest.approx(0.2)
     assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
     assert promtext.one(fam, "gpu_probe_unique_cus", gpu_id="0") > 200
+
+
+def test_fleet_view_reads_the_native_exporter():
+    """`gpumon top --url` against bin/gpumon-exporter serving the real MI355X: the fleet view parses
+    the live exposition (per-card row with 8 XCD columns, 288 GiB, ECC column)."""
+    import socket
+    import time
+    import urllib.request
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    exe = os.path.join(ROOT, "bin", "gpumon-exporter")
+    p = subprocess.Popen([exe, "--backend", "amdsmi", "--interval", "0.2", "--listen", f"127.0.0.1:{port}",
+                          "--host", "box", "--log-level", "warn"], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    try:
+        deadline = time.time() + 60
+        while time.time() < deadline:
+            try:
+                urllib.request.urlopen(f"http://127.0.0.1:{port}/readyz", timeout=1).read()
+                break
+            except OSError:
+                time.sleep(0.2)
+        r = subprocess.run([sys.executable, "-m", "gpumon", "top", "--url", f"127.0.0.1:{port}", "--iterations", "1"],
+                           capture_output=True, text=True, timeout=60, cwd=ROOT)
+    finally:
+        p.terminate()
+        p.wait(30)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = [l for l in r.stdout.splitlines() if l.startswith("box ")]
+    assert rows, r.stdout
+    fields = rows[0].split()
+    assert fields[1] == "0" and fields[2] == "1"  # gpu_id 0, up
+    assert len(fields[4:12]) == 8 and all(f.isdigit() for f in fields[4:12])  # 8 XCD busy columns
+    assert "/288" in rows[0]
