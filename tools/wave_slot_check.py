@@ -36,7 +36,11 @@ def probe_stats(H, probe, n=8):
 
 
 def main():
-    from gpumon.ops.pmc import DEFAULT_COUNTERS, derive, pmc_module
+    from gpumon.ops.pmc import derive, pmc_module
+
+    # per-wave SQ_WAVE_CYCLES: valid here because the loads run in THIS process
+    # (profiles/r1_pmc_cross_process.md)
+    occ = ["SQ_WAVE_CYCLES", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "GRBM_COUNT"]
 
     P = pmc_module()
     P.init()
@@ -48,11 +52,11 @@ def main():
     probe = H.Probe(0, 1024, 4, 200)
     out = {"max_waves_per_cu": agent["max_waves_per_cu"], "simd_count": agent["simd_count"]}
     out["idle"] = probe_stats(H, probe)
-    out["idle"]["pmc"] = derive(P.sample(0, DEFAULT_COUNTERS, 0.2), agent)
+    out["idle"]["pmc"] = derive(P.sample(0, occ, 0.2), agent)
     for kind in ("mfma", "hbm", "partial"):
         with SyntheticLoad(0, kind):
             time.sleep(1.0)
-            pmc = derive(P.sample(0, DEFAULT_COUNTERS, 0.2), agent)
+            pmc = derive(P.sample(0, occ, 0.2), agent)
             out[kind] = probe_stats(H, probe)
             out[kind]["pmc"] = pmc
     print(json.dumps(out))
