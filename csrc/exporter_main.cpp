@@ -2,16 +2,17 @@
 //
 // Reference entrypoint: `python3 /gpu.py` (/root/reference/Dockerfile:7) reading NODE_NAME and
 // INFLUXDB_URL from the environment (gpu.py:19-26) and looping forever (gpu.py:258-263).
-// Same env names are honoured here; flags override. Attribution in this binary uses /proc
-// (cgroup -> container id; HOSTNAME / service-account namespace fallback). The Python CLI
-// (`gpumon serve`) adds CRI + kubelet PodResources metadata on top of the same core.
+// Configuration (csrc/core/options.h) uses the Python control plane's keys and precedence:
+// defaults < YAML file (--config / GPUMON_CONFIG, the DaemonSet's ConfigMap format) < environment
+// (NODE_NAME, INFLUXDB_URL, GPUMON_<KEY>) < flags. Attribution uses /proc plus the native kubelet
+// PodResources and CRI pollers; --pmc / --probe load the on-device plugins.
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
-#include <algorithm>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -19,41 +20,63 @@
 #include "core/common.h"
 #include "core/exporter.h"
 #include "core/ondevice.h"
+#include "core/options.h"
 
 using namespace gpumon;
+
+extern char** environ;
 
 static std::atomic<bool> g_stop{false};
 static void on_signal(int) { g_stop = true; }
 
 static void usage() {
   fprintf(stderr,
-          "usage: gpumon-exporter [--backend auto|amdsmi|rocm_smi|mock[:k=v,..]] [--interval SEC]\n"
+          "usage: gpumon-exporter [--config FILE] [--print-config] [--once]\n"
+          "                       [--backend auto|amdsmi|rocm_smi|mock[:k=v,..]] [--interval SEC]\n"
           "                       [--listen ADDR:PORT] [--host NAME] [--devices 0,1,..] [--no-fast-path]\n"
           "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--pod-labels KEY,KEY..]\n"
           "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--no-gzip] [--sample-threads N]\n"
-          "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx] [--once]\n"
+          "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx]\n"
           "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri]\n"
           "                       [--dra-drivers gpu.amd.com,..|none]\n"
           "                       [--pmc] [--pmc-counters A,B,..] [--pmc-window SEC] [--probe] [--probe-every N]\n"
           "                       [--probe-blocks N] [--plugin-dir DIR]\n"
-          "env: NODE_NAME, INFLUXDB_URL, GPUMON_LISTEN, GPUMON_INTERVAL, GPUMON_BACKEND\n");
+          "config keys: the gpumon.* keys of gpumon/config.py (docs/configuration.md), in the file, as\n"
+          "GPUMON_<KEY> in the environment, or as the flags above; NODE_NAME and INFLUXDB_URL as in the reference\n");
 }
 
 int main(int argc, char** argv) {
-  ExporterConfig cfg;
-  if (const char* v = getenv("NODE_NAME")) cfg.host = v;
-  if (const char* v = getenv("INFLUXDB_URL")) cfg.influx_url = v;
-  if (const char* v = getenv("GPUMON_BACKEND")) cfg.backend = v;
-  if (const char* v = getenv("GPUMON_INTERVAL")) cfg.interval_s = atof(v);
-  std::string listen = getenv("GPUMON_LISTEN") ? getenv("GPUMON_LISTEN") : "0.0.0.0:9400";
-  bool once = false;
-  OnDeviceConfig od;
-  int probe_every = 1;
-  // kubelet PodResources: on by default when the socket is mounted (deploy/k8s DaemonSet)
-  std::string podres = "/var/lib/kubelet/pod-resources/kubelet.sock";
-  std::string cri;  // "" = first existing well-known runtime socket, "none" = off
+  NativeOptions o;
+  std::string err;
+  // 1. config file: --config wins over GPUMON_CONFIG
+  std::string config = getenv("GPUMON_CONFIG") ? getenv("GPUMON_CONFIG") : "";
+  for (int i = 1; i + 1 < argc; ++i)
+    if (std::string(argv[i]) == "--config") config = argv[i + 1];
+  if (!config.empty()) {
+    std::vector<std::string> unknown;
+    if (!options_load_file(&o, config, &unknown, &err)) {
+      fprintf(stderr, "config: %s\n", err.c_str());
+      return 2;
+    }
+    for (const auto& k : unknown)
+      fprintf(stderr, "config: key '%s' is not used by the native exporter (ignored)\n", k.c_str());
+  }
+  // 2. environment
+  if (!options_apply_env(&o, environ, &err)) {
+    fprintf(stderr, "environment: %s\n", err.c_str());
+    return 2;
+  }
+  // 3. flags
+  bool once = false, print_config = false;
+  auto set = [&](const char* key, const std::string& v) {
+    std::string e;
+    if (options_set(&o, key, {v}, &e) < 0) {
+      fprintf(stderr, "%s\n", e.c_str());
+      exit(2);
+    }
+  };
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -63,52 +86,46 @@ int main(int argc, char** argv) {
       }
       return argv[++i];
     };
-    if (a == "--backend") cfg.backend = next();
-    else if (a == "--interval") cfg.interval_s = atof(next().c_str());
-    else if (a == "--listen") listen = next();
-    else if (a == "--host") cfg.host = next();
-    else if (a == "--devices") {
-      for (const auto& s : split(next(), ','))
-        if (!s.empty()) cfg.devices.push_back(atoi(s.c_str()));
-    } else if (a == "--influx-url") cfg.influx_url = next();
-    else if (a == "--influx-extended") cfg.influx_extended = true;
-    else if (a == "--influx-schema") cfg.influx_schema = atoi(next().c_str());
-    else if (a == "--no-fast-path") cfg.fast_path = false;
-    else if (a == "--sysfs") cfg.sysfs_root = next();
-    else if (a == "--roctx") cfg.roctx = true;
-    else if (a == "--pod-resources") podres = next();
-    else if (a == "--no-pod-resources") podres = "";
-    else if (a == "--cri") cri = next();
-    else if (a == "--no-cri") cri = "none";
+    if (a == "--config") next();
+    else if (a == "--print-config") print_config = true;
+    else if (a == "--once") once = true;
+    else if (a == "--backend") set("backend", next());
+    else if (a == "--interval") set("interval", next());
+    else if (a == "--listen") set("listen", next());
+    else if (a == "--host") set("host", next());
+    else if (a == "--devices") set("devices", next());
+    else if (a == "--influx-url") set("influx_url", next());
+    else if (a == "--influx-extended") set("influx_extended", "true");
+    else if (a == "--influx-schema") set("influx_schema", next());
+    else if (a == "--no-fast-path") set("fast_path", "false");
+    else if (a == "--sysfs") set("sysfs_root", next());
+    else if (a == "--roctx") set("roctx", "true");
+    else if (a == "--pod-resources") set("pod_resources_socket", next());
+    else if (a == "--no-pod-resources") set("pod_resources_socket", "");
+    else if (a == "--cri") set("cri_socket", next());
+    else if (a == "--no-cri") set("cri_socket", "none");
     else if (a == "--dra-drivers") {
       const std::string v = next();
-      cfg.pod_resources_dra_drivers.clear();
-      if (v != "none")
-        for (const auto& d : split(v, ','))
-          if (!d.empty()) cfg.pod_resources_dra_drivers.push_back(d);
-    }
-    else if (a == "--opt-in-label") cfg.attribution.opt_in = next();
-    else if (a == "--user-regex") cfg.attribution.user_regex = next();
-    else if (a == "--pod-labels") cfg.attribution.label_allowlist = split(next(), ',');
-    else if (a == "--user-label") cfg.attribution.user_label = next();
-    else if (a == "--procfs") cfg.attribution.procfs_root = next();
-    else if (a == "--no-processes") cfg.processes = false;
-    else if (a == "--ras-every") cfg.ras_every = atoi(next().c_str());
-    else if (a == "--no-gzip") cfg.gzip = false;
-    else if (a == "--sample-threads") cfg.sample_threads = atoi(next().c_str());
-    else if (a == "--http-threads") cfg.http_threads = atoi(next().c_str());
-    else if (a == "--once") once = true;
-    else if (a == "--pmc") od.pmc = true;
-    else if (a == "--pmc-counters") od.pmc_counters = split(next(), ',');
-    else if (a == "--pmc-window") od.pmc_window_s = atof(next().c_str());
-    else if (a == "--probe") od.probe = true;
-    else if (a == "--probe-every") probe_every = std::max(1, atoi(next().c_str()));
-    else if (a == "--probe-blocks") od.probe_blocks = atoi(next().c_str());
-    else if (a == "--plugin-dir") od.plugin_dir = next();
-    else if (a == "--log-level") {
-      std::string l = next();
-      g_log_level = l == "debug" ? 0 : l == "info" ? 1 : l == "warn" ? 2 : 3;
-    } else if (a == "-h" || a == "--help") {
+      set("dra_drivers", v == "none" ? "" : v);
+    } else if (a == "--opt-in-label") set("opt_in_label", next());
+    else if (a == "--user-regex") set("user_regex", next());
+    else if (a == "--user-label") set("user_label", next());
+    else if (a == "--pod-labels") set("pod_label_allowlist", next());
+    else if (a == "--procfs") set("procfs_root", next());
+    else if (a == "--no-processes") set("processes", "false");
+    else if (a == "--ras-every") set("ras_every", next());
+    else if (a == "--no-gzip") set("gzip", "false");
+    else if (a == "--sample-threads") set("sample_threads", next());
+    else if (a == "--http-threads") set("http_threads", next());
+    else if (a == "--log-level") set("log_level", next());
+    else if (a == "--pmc") set("enable_pmc", "true");
+    else if (a == "--pmc-counters") set("pmc_counters", next());
+    else if (a == "--pmc-window") o.od.pmc_window_s = atof(next().c_str());
+    else if (a == "--probe") set("enable_probe", "true");
+    else if (a == "--probe-every") set("probe_every", next());
+    else if (a == "--probe-blocks") o.od.probe_blocks = atoi(next().c_str());
+    else if (a == "--plugin-dir") set("plugin_dir", next());
+    else if (a == "-h" || a == "--help") {
       usage();
       return 0;
     } else {
@@ -117,30 +134,18 @@ int main(int argc, char** argv) {
       return 2;
     }
   }
-  size_t colon = listen.rfind(':');
-  cfg.listen_addr = colon == std::string::npos ? "0.0.0.0" : listen.substr(0, colon);
-  cfg.port = atoi(colon == std::string::npos ? listen.c_str() : listen.c_str() + colon + 1);
-  if (cfg.host.empty()) cfg.host = "no_name";
-  if (!podres.empty() && access(podres.c_str(), F_OK) == 0) cfg.pod_resources_socket = podres;
-  if (cri.empty()) {
-    for (const char* c : {"/run/containerd/containerd.sock", "/var/run/crio/crio.sock", "/run/crio/crio.sock",
-                          "/var/run/cri-dockerd.sock"})
-      if (access(c, F_OK) == 0) {
-        cri = c;
-        break;
-      }
+  if (print_config) {
+    printf("%s\n", options_json(o).c_str());
+    return 0;
   }
-  if (!cri.empty() && cri != "none") cfg.cri_socket = cri;
-  // on-device samplers run at the sampler cadence (the probe every N ticks)
-  const double period = cfg.interval_s > 0 ? std::max(cfg.interval_s, 0.1) : 1.0;
-  od.pmc_every_s = period;
-  od.probe_every_s = period * probe_every;
+  options_finalize(&o);
+  ExporterConfig& cfg = o.cfg;
+  const OnDeviceConfig& od = o.od;
 
   if (once) {
     cfg.serve_http = false;
     cfg.interval_s = 0;
     Exporter e(cfg);
-    std::string err;
     if (!e.start(&err)) {
       fprintf(stderr, "start failed: %s\n", err.c_str());
       return 1;
@@ -154,6 +159,7 @@ int main(int argc, char** argv) {
     e.tick();  // second tick so rates are populated (and the on-device series are rendered)
     auto s = e.snapshot();
     fwrite(s->body.data(), 1, s->body.size(), stdout);
+    ondev.stop();
     e.stop();
     return 0;
   }
@@ -162,7 +168,6 @@ int main(int argc, char** argv) {
   signal(SIGTERM, on_signal);
   signal(SIGPIPE, SIG_IGN);
   Exporter e(cfg);
-  std::string err;
   if (!e.start(&err)) {
     fprintf(stderr, "start failed: %s\n", err.c_str());
     return 1;

@@ -1,0 +1,144 @@
+"""bin/gpumon-exporter reads the same configuration as the Python control plane
+(csrc/core/options.cpp vs gpumon/config.py): the DaemonSet ConfigMap's YAML, GPUMON_<KEY> env,
+the reference's NODE_NAME / INFLUXDB_URL, flags last."""
+
+import dataclasses
+import json
+import os
+import subprocess
+
+import pytest
+import yaml
+
+from gpumon.config import Config, load_yaml
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "bin", "gpumon-exporter")
+CLEAN_ENV = {k: v for k, v in os.environ.items() if not k.startswith("GPUMON_") and k not in ("NODE_NAME", "INFLUXDB_URL")}
+
+
+def _print(*args, env=None):
+    e = dict(CLEAN_ENV, **(env or {}))
+    r = subprocess.run([BIN, *args, "--print-config"], capture_output=True, text=True, timeout=30, env=e)
+    return r
+
+
+def _py(path=None, env=None):
+    cfg = Config()
+    if path:
+        cfg.apply_dict(load_yaml(path))
+    cfg.apply_env(dict(env or {}))
+    return dataclasses.asdict(cfg)
+
+
+def _same(native, py):
+    for k, v in native.items():
+        if k == "host":
+            continue
+        assert k in py, k
+        pv = py[k]
+        if isinstance(v, float) or isinstance(pv, float):
+            assert float(v) == pytest.approx(float(pv)), k
+        else:
+            assert v == pv, (k, v, pv)
+
+
+def test_daemonset_configmap_parses_identically(tmp_path):
+    (cm,) = [d for d in yaml.safe_load_all(open(os.path.join(ROOT, "deploy/k8s/gpumon-daemonset.yaml")))
+             if d and d.get("kind") == "ConfigMap"]
+    p = tmp_path / "config.yaml"
+    p.write_text(cm["data"]["config.yaml"])
+    r = _print("--config", str(p))
+    assert r.returncode == 0, r.stderr
+    _same(json.loads(r.stdout), _py(str(p)))
+
+
+RICH = """\
+# every value form the ConfigMap format allows
+gpumon:
+  interval: 0.1                 # 10 Hz
+  listen: "127.0.0.1:9500"
+  devices: [0, 2, 5]
+  opt_in_label: 'mlgpu=mlgpu'
+  user_regex: "^jupyter-([a-z]+)-"
+  pod_label_allowlist:
+    - team
+    - app.kubernetes.io/name
+  resource_names: [amd.com/gpu, "amd.com/gpu-cpx"]
+  dra_drivers: []
+  enable_pmc: yes
+  enable_probe: true
+  probe_every: 5
+  pmc_counters: [SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE, GRBM_COUNT]
+  ras_every: 0
+  gzip: off
+  influx_url: http://influx:8086/write?db=k8s#not-a-comment
+  control_plane: native         # Python-only key: warned about, ignored
+"""
+
+
+def test_rich_file_env_and_flag_precedence(tmp_path):
+    p = tmp_path / "rich.yaml"
+    p.write_text(RICH)
+    r = _print("--config", str(p))
+    assert r.returncode == 0, r.stderr
+    n = json.loads(r.stdout)
+    _same(n, _py(str(p)))
+    assert n["devices"] == [0, 2, 5] and n["dra_drivers"] == [] and n["gzip"] is False
+    assert n["pod_label_allowlist"] == ["team", "app.kubernetes.io/name"]
+    assert n["influx_url"] == "http://influx:8086/write?db=k8s#not-a-comment"
+    assert "control_plane" in r.stderr  # the ignored key is named
+    # env over file, flags over env; the reference's env names
+    env = {"GPUMON_INTERVAL": "2.5", "GPUMON_DEVICES": "1,3", "NODE_NAME": "gpu-node-7",
+           "INFLUXDB_URL": "http://other/write", "GPUMON_FAKE_SOMETHING": "x"}
+    r = _print("--config", str(p), "--interval", "0.5", env=env)
+    assert r.returncode == 0, r.stderr
+    n = json.loads(r.stdout)
+    assert n["interval"] == 0.5 and n["devices"] == [1, 3] and n["host"] == "gpu-node-7"
+    assert n["influx_url"] == "http://other/write"
+    py = _py(str(p), env)
+    assert py["devices"] == [1, 3] and py["influx_url"] == "http://other/write" and py["host"] == "gpu-node-7"
+
+
+def test_config_env_var_names_the_file(tmp_path):
+    p = tmp_path / "c.yaml"
+    p.write_text("gpumon:\n  ras_every: 7\n")
+    r = _print(env={"GPUMON_CONFIG": str(p)})
+    assert r.returncode == 0 and json.loads(r.stdout)["ras_every"] == 7
+
+
+@pytest.mark.parametrize("text,msg", [
+    ("gpumon:\n  interval: fast\n", "interval: not a number"),
+    ("gpumon:\n  probe_every: 1.5\n", "probe_every: not an integer"),
+    ("gpumon:\n  gzip: maybe\n", "gzip: not a boolean"),
+    ("gpumon:\n  rates:\n    xgmi: 1\n", "line 3: nested mappings"),
+    ("gpumon:\n  interval: 1\n  interval: 2\n", "line 3: duplicate key"),
+    ("gpumon:\n  devices: [0, 1\n", "line 2: unterminated flow list"),
+    ("gpumon:\n  user_regex: \"abc\n", "unterminated"),
+    ("gpumon:\n  listen: {a: b}\n", "unsupported YAML construct"),
+    ("other: 1\n", None),  # no gpumon: mapping: flat file, unknown key -> warning only
+])
+def test_bad_files_fail_with_the_line(tmp_path, text, msg):
+    p = tmp_path / "bad.yaml"
+    p.write_text(text)
+    r = _print("--config", str(p))
+    if msg is None:
+        assert r.returncode == 0 and "'other'" in r.stderr
+    else:
+        assert r.returncode == 2 and msg in r.stderr, r.stderr
+
+
+def test_bad_env_value_is_fatal():
+    r = _print(env={"GPUMON_INTERVAL": "soon"})
+    assert r.returncode == 2 and "GPUMON_INTERVAL" in r.stderr
+
+
+def test_binary_serves_with_the_configmap(tmp_path):
+    """--once with a config file drives the sampler (mock backend from the file)."""
+    p = tmp_path / "c.yaml"
+    p.write_text("gpumon:\n  backend: 'mock:gpus=3'\n  pod_resources_socket: ''\n  cri_socket: none\n"
+                 "  host: from-file\n")
+    r = subprocess.run([BIN, "--config", str(p), "--once"], capture_output=True, text=True, timeout=60,
+                       env=CLEAN_ENV)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count('node_gpu_gpu_util{host="from-file"') == 3
