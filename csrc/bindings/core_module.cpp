@@ -13,6 +13,7 @@
 #include "../core/grpc_lite.h"
 #include "../core/http_client.h"
 #include "../core/ondevice.h"
+#include "../core/options.h"
 #include "../core/render.h"
 #include "../core/snapshot.h"
 #include "../core/trace.h"
@@ -725,6 +726,17 @@ PYBIND11_MODULE(_core, m) {
         return d;
       });
   m.def("default_plugin_dir", &default_plugin_dir);
+  m.def(
+      "parse_yaml_subset",
+      [](const std::string& text) {
+        YamlDoc doc;
+        std::string err;
+        if (!parse_yaml_subset(text, &doc, &err)) throw py::value_error(err);
+        py::dict d;
+        for (const auto& k : doc.order) d[py::str(k)] = doc.values[k];
+        return d;
+      },
+      "The native exporter's config-file parser (csrc/core/options.cpp): key -> list of strings");
   m.def(
       "pmc_derive",
       [](const py::dict& raw, const py::dict& agent, double window_s) {

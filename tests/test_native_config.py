@@ -142,3 +142,61 @@ def test_binary_serves_with_the_configmap(tmp_path):
                        env=CLEAN_ENV)
     assert r.returncode == 0, r.stderr
     assert r.stdout.count('node_gpu_gpu_util{host="from-file"') == 3
+
+
+# ---------------------------------------------------------------- parser vs PyYAML (property-based)
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+_word = st.text(alphabet="abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789_./-:=@ ", min_size=1,
+                max_size=20).filter(lambda s: s.strip() == s)
+_scalar = st.one_of(_word, st.integers(-10 ** 6, 10 ** 6), st.booleans(),
+                    st.floats(-1e6, 1e6, allow_nan=False).map(lambda f: round(f, 3)))
+_value = st.one_of(_scalar, st.lists(st.one_of(_word, st.integers(0, 999)), max_size=5))
+_doc = st.dictionaries(st.from_regex(r"[a-z][a-z0-9_]{0,11}", fullmatch=True), _value, max_size=8)
+
+
+def _as_text(v):
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    return str(v)
+
+
+def _dump_scalar(v):
+    t = yaml.safe_dump(v, width=10 ** 6)
+    return t[:-len("\n...\n")] if t.endswith("\n...\n") else t.rstrip("\n")
+
+
+def _dump(doc, flow_lists, wrap):
+    """Block mapping (the ConfigMap's shape) with lists in flow or block style, scalars exactly as
+    PyYAML would emit them (quoting included)."""
+    ind = "  " if wrap else ""
+    out = ["gpumon:"] if wrap else []
+    for k, v in doc.items():
+        if isinstance(v, list) and (flow_lists or not v):
+            out.append(f"{ind}{k}: " + yaml.safe_dump(v, default_flow_style=True, width=10 ** 6).strip())
+        elif isinstance(v, list):
+            out.append(f"{ind}{k}:")
+            out.extend(f"{ind}  - {_dump_scalar(x)}" for x in v)
+        else:
+            out.append(f"{ind}{k}: {_dump_scalar(v)}")
+    return "\n".join(out) + "\n"
+
+
+@settings(max_examples=300, deadline=None)
+@given(doc=_doc.filter(bool), flow=st.booleans(), wrap=st.booleans())
+def test_yaml_subset_agrees_with_pyyaml(doc, flow, wrap):
+    from gpumon import core
+
+    body = _dump(doc, flow, wrap)
+    got = core().parse_yaml_subset(body)
+    want = yaml.safe_load(body)
+    want = want.get("gpumon", want) if wrap else want
+    assert list(got) == list(want)
+    for k, v in want.items():
+        exp = [_as_text(x) for x in v] if isinstance(v, list) else [_as_text(v)]
+        g = got[k]
+        if isinstance(v, float):
+            assert float(g[0]) == pytest.approx(v)
+        else:
+            assert g == exp, (k, g, exp, body)
