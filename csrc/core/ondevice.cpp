@@ -202,22 +202,10 @@ bool OnDevice::start(std::string* err) {
       pmc_lib_.reset();
       return false;
     }
-    const int n_hip = probe_lib_->probe_count();
-    for (const auto& s : ex_->statics()) {
-      if (s.hip_id < 0 || s.hip_id >= n_hip) continue;
-      ProbeDev d;
-      d.dev = s.index;
-      d.handle = probe_lib_->probe_create(s.hip_id, cfg_.probe_blocks, 4, cfg_.probe_spin_ticks, ebuf, sizeof ebuf);
-      if (!d.handle) {
-        *err = std::string("probe create on hip device ") + std::to_string(s.hip_id) + ": " + ebuf;
-        for (auto& p : probes_) probe_lib_->probe_destroy(static_cast<gpumon_probe*>(p.handle));
-        probes_.clear();
-        return false;
-      }
-      probes_.push_back(std::move(d));
-    }
+    if (!create_probes(err)) return false;
     GPUMON_LOG(LogLevel::kInfo, "ondevice",
-               "probe plugin " + probe_lib_->path + " devices=" + std::to_string(probes_.size()));
+               "probe plugin " + probe_lib_->path + " devices=" + std::to_string(probes_.size()) +
+                   (probes_.empty() ? " (device list not known yet: created on the first step that has it)" : ""));
   }
   running_ = true;
   if (pmc_lib_) pmc_th_ = std::thread([this] { pmc_loop(); });
@@ -381,8 +369,35 @@ void OnDevice::pmc_loop() {
 // ---------------------------------------------------------------------------------------------
 // K1 probe
 
+// One probe per exported device with a HIP id. Called at start and, while the exporter's backend
+// has not come up yet (empty statics), again on later steps.
+bool OnDevice::create_probes(std::string* err) {
+  if (!probes_.empty()) return true;
+  char ebuf[512] = {0};
+  const int n_hip = probe_lib_->probe_count();
+  std::vector<ProbeDev> made;
+  for (const auto& s : ex_->statics()) {
+    if (s.hip_id < 0 || s.hip_id >= n_hip) continue;
+    ProbeDev d;
+    d.dev = s.index;
+    d.handle = probe_lib_->probe_create(s.hip_id, cfg_.probe_blocks, 4, cfg_.probe_spin_ticks, ebuf, sizeof ebuf);
+    if (!d.handle) {
+      *err = std::string("probe create on hip device ") + std::to_string(s.hip_id) + ": " + ebuf;
+      for (auto& p : made) probe_lib_->probe_destroy(static_cast<gpumon_probe*>(p.handle));
+      return false;
+    }
+    made.push_back(std::move(d));
+  }
+  probes_ = std::move(made);
+  return true;
+}
+
 void OnDevice::probe_step() {
   std::lock_guard<std::mutex> g(probe_mu_);
+  if (probes_.empty()) {
+    std::string err;
+    if (!create_probes(&err)) GPUMON_LOG(LogLevel::kWarn, "ondevice", err);
+  }
   for (auto& p : probes_)
     if (p.pending < 0) p.pending = probe_lib_->probe_launch(static_cast<gpumon_probe*>(p.handle));
   const int64_t deadline = mono_ns() + static_cast<int64_t>(cfg_.probe_timeout_s * 1e9);

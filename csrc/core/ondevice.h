@@ -99,6 +99,7 @@ class OnDevice {
   void pmc_step();
   void probe_step();
   void map_pmc_agents();
+  bool create_probes(std::string* err);
   void export_pmc();
   void export_probe();
   void sleep_until(int64_t deadline_ns);

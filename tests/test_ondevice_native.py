@@ -239,3 +239,30 @@ def test_cli_once_native_ondevice(monkeypatch, capsys):
     assert rc == 0
     assert _val(out, "gpu_mfma_busy_percent", gpu_id="0") == pytest.approx(50.0)
     assert _val(out, "gpu_probe_unique_cus", gpu_id="0") == 256
+
+
+def test_probe_created_once_backend_comes_up(core, monkeypatch):
+    """Backend down at start (no device list yet): the probe sampler starts with nothing to probe and
+    creates its probes on the first step after the exporter's backend initialises."""
+    make_locked("fakes")
+    fake = os.path.join(ROOT, "build", "fakes", "libfake_amd_smi.so")
+    monkeypatch.setenv("GPUMON_FAKE_AGENTS", "2")
+    monkeypatch.setenv("FAKE_AMDSMI_INIT_FAIL", "1")
+    ex = core.Exporter({"backend": "amdsmi", "amdsmi_lib": fake, "serve_http": False, "interval_s": 0,
+                        "init_retry_s": 0.0, "verify_kfd": False, "sysfs_root": "/nonexistent"})
+    assert ex.start() != ""  # backend not ready yet (retrying)
+    od = _ondevice(core, ex, pmc=False, probe_every_s=60)
+    od.start()
+    try:
+        od.step()
+        assert od.stats()["probe_devices"] == 0
+        monkeypatch.delenv("FAKE_AMDSMI_INIT_FAIL")
+        ex.tick()
+        assert len(ex.statics()) == 2
+        od.step()
+        ex.tick()
+        assert od.stats()["probe_devices"] == 2
+        assert _val(ex.metrics_text(), "gpu_probe_unique_cus", gpu_id="1") == 256
+    finally:
+        od.stop()
+        ex.stop()
