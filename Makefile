@@ -67,7 +67,11 @@ build/obj/bindings/hip_module.o: csrc/bindings/hip_module.cpp $(HIP_HDR)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -I$(PYINC) -I$(PYBIND) -c $< -o $@
 
-$(HIPEXT): build/obj/hip/kernels.o build/obj/hip/burn16.o build/obj/bindings/hip_module.o
+build/obj/hip/burn_dtypes.o: csrc/hip/burn_dtypes.hip $(HIP_HDR)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) $(BURN16_FLAGS) -c $< -o $@
+
+$(HIPEXT): build/obj/hip/kernels.o build/obj/hip/burn16.o build/obj/hip/burn_dtypes.o build/obj/bindings/hip_module.o
 	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -shared -fPIC $^ -o $@
 
 asan: bin/gpumon-exporter-asan
@@ -97,7 +101,7 @@ $(PMCLIB): csrc/plugins/pmc_plugin.cpp csrc/plugins/ondevice_abi.h
 build/obj/plugins/probe_plugin.o: csrc/plugins/probe_plugin.cpp csrc/plugins/ondevice_abi.h $(HIP_HDR)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-$(PROBELIB): build/obj/plugins/probe_plugin.o build/obj/hip/kernels.o build/obj/hip/burn16.o
+$(PROBELIB): build/obj/plugins/probe_plugin.o build/obj/hip/kernels.o build/obj/hip/burn16.o build/obj/hip/burn_dtypes.o
 	@mkdir -p lib
 	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -shared -fPIC $^ -Wl,-soname,libgpumon_probe.so -o $@
 

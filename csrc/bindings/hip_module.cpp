@@ -25,6 +25,11 @@ PYBIND11_MODULE(_hip, m) {
     launch_mfma_burn(dev, P(a), P(b), static_cast<float*>(P(out)), blocks, iters, P(stream), shape);
   }, py::arg("dev"), py::arg("a"), py::arg("b"), py::arg("out"), py::arg("blocks"), py::arg("iters"),
      py::arg("stream") = 0, py::arg("shape") = 32);
+  m.def("mfma_burn_dtype", [](int dev, const std::string& dtype, uintptr_t out, int blocks, int iters,
+                              uintptr_t stream) {
+    return launch_mfma_burn_dtype(dev, dtype, static_cast<float*>(P(out)), blocks, iters, P(stream));
+  }, py::arg("dev"), py::arg("dtype"), py::arg("out"), py::arg("blocks"), py::arg("iters"), py::arg("stream") = 0,
+     "MFMA burn of one matrix path (f16|fp8|f32|f64|i8|mxfp8|mxfp4); returns FLOP per launch");
   m.def("stream_copy", [](int dev, uintptr_t src, uintptr_t dst, size_t n16, int blocks, uintptr_t stream,
                           int unroll, int policy, bool span) {
     launch_stream_copy(dev, P(src), P(dst), n16, blocks, P(stream), unroll, policy, span);
@@ -38,13 +43,15 @@ PYBIND11_MODULE(_hip, m) {
      py::arg("blocks") = 4096, py::arg("stream") = 0);
 
   py::class_<LoadGen>(m, "LoadGen")
-      .def(py::init([](int dev, std::string kind, double duty, size_t hbm_bytes, int mfma_iters, int shape) {
+      .def(py::init([](int dev, std::string kind, double duty, size_t hbm_bytes, int mfma_iters, int shape,
+                       std::string dtype) {
              auto g = std::make_unique<LoadGen>(dev, std::move(kind), duty, hbm_bytes, mfma_iters);
              g->set_mfma_shape(shape);
+             g->set_mfma_dtype(std::move(dtype));
              return g;
            }),
            py::arg("dev"), py::arg("kind") = "mixed", py::arg("duty") = 1.0, py::arg("hbm_bytes") = size_t(1) << 30,
-           py::arg("mfma_iters") = 8192, py::arg("mfma_shape") = 32)
+           py::arg("mfma_iters") = 8192, py::arg("mfma_shape") = 32, py::arg("mfma_dtype") = "bf16")
       .def("start", [](LoadGen& g) {
         py::gil_scoped_release nogil;
         g.start();

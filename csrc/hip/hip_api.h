@@ -24,6 +24,9 @@ void launch_mfma_tile(int dev, const void* a, const void* b, float* c, int iters
 // shape 32: v_mfma_f32_32x32x16_bf16 x4 accumulators; 16: v_mfma_f32_16x16x32_bf16 x8 (same FLOP/iter)
 void launch_mfma_burn(int dev, const void* a, const void* b, float* out, int blocks, int iters, void* stream,
                       int shape = 32);
+// Burns of the other matrix paths (burn_dtypes.hip): dtype f16 | fp8 | f32 | f64 | i8 | mxfp8 | mxfp4.
+// Same geometry as the bf16 burn (256-thread workgroups, 8 chains/wave); returns FLOP per launch.
+double launch_mfma_burn_dtype(int dev, const std::string& dtype, float* out, int blocks, int iters, void* stream);
 // dst = src (n16 = number of 16-byte vectors)
 // policy: 0 nt loads + nt stores, 1 plain, 2 plain loads + nt stores, 3 nt loads + plain stores;
 // span: each block copies one contiguous range instead of grid-striding
@@ -53,6 +56,8 @@ class LoadGen {
   LoadStats stats() const;
   bool running() const { return running_; }
   void set_mfma_shape(int shape) { shape_ = shape; }  // 32 or 16 (launch_mfma_burn); before start()
+  // bf16 (the shape above) or a launch_mfma_burn_dtype path: f16 fp8 f32 f64 i8 mxfp8 mxfp4; before start()
+  void set_mfma_dtype(std::string dtype) { dtype_ = std::move(dtype); }
   int mfma_shape() const { return shape_; }
 
  private:
@@ -63,6 +68,7 @@ class LoadGen {
   size_t bytes_;
   int iters_;
   int shape_ = 32;
+  std::string dtype_ = "bf16";
   void* stream_ = nullptr;
   void* a_ = nullptr;
   void* b_ = nullptr;

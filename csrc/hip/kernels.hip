@@ -381,7 +381,9 @@ void LoadGen::loop() {
       check(hipEventRecord(e0, s), "hipEventRecord");
       double fl = 0, by = 0;
       for (int k = 0; k < 4; ++k) {
-        if (do_mfma) {
+        if (do_mfma && dtype_ != "bf16") {
+          fl += launch_mfma_burn_dtype(dev_, dtype_, out_, burn_blocks, iters_, s);
+        } else if (do_mfma) {
           launch_mfma_burn(dev_, a_, b_, out_, burn_blocks, iters_, s, shape_);
           fl += static_cast<double>(burn_blocks) * 4 * 4 * iters_ * 32768.0;
         } else {

@@ -208,7 +208,7 @@ def cmd_probe(args) -> int:
 def cmd_load(args) -> int:
     from .ops.load import SyntheticLoad
 
-    with SyntheticLoad(args.device, args.kind, duty=args.duty) as load:
+    with SyntheticLoad(args.device, args.kind, duty=args.duty, mfma_dtype=args.dtype) as load:
         time.sleep(args.seconds)
         print(json.dumps(load.stats()))
     return 0
@@ -286,6 +286,8 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--kind", choices=["mfma", "hbm", "mixed"], default="mixed")
     s.add_argument("--duty", type=float, default=1.0)
     s.add_argument("--seconds", type=float, default=10.0)
+    s.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8", "f32", "f64", "i8", "mxfp8", "mxfp4"],
+                   help="matrix path of the mfma burn")
     s.set_defaults(fn=cmd_load)
     s = sub.add_parser("xgmi", help="validate the per-link xGMI counters with peer copies")
     s.add_argument("--pairs", default="0:1")

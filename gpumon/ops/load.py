@@ -9,6 +9,10 @@ launches of the gfx950 kernels in ``csrc/hip/kernels.hip``:
 * ``hbm``   — 16 B/lane non-temporal copy over a ``hbm_bytes`` buffer pair, one 4 KiB chunk per
   workgroup (6.5 TB/s on MI355X, profiles/r1_hbm_stream.md);
 * ``mixed`` — alternating; ``duty`` < 1 inserts idle gaps (partial-utilisation validation).
+
+``mfma_dtype`` swaps the bf16 burn for another matrix path of the same geometry
+(``csrc/hip/burn_dtypes.hip``): ``f16``, ``fp8``, ``f32``, ``f64``, ``i8`` and the block-scaled
+``mxfp8`` / ``mxfp4`` (f8f6f4) instructions — one load per ``gpu_mfma_tflops{dtype}`` counter.
 """
 
 from __future__ import annotations
@@ -18,8 +22,8 @@ from .._native import hip
 
 class SyntheticLoad:
     def __init__(self, dev: int = 0, kind: str = "mixed", duty: float = 1.0, hbm_bytes: int = 1 << 30,
-                 mfma_iters: int = 8192, mfma_shape: int = 16):
-        self._g = hip().LoadGen(dev, kind, duty, hbm_bytes, mfma_iters, mfma_shape)
+                 mfma_iters: int = 8192, mfma_shape: int = 16, mfma_dtype: str = "bf16"):
+        self._g = hip().LoadGen(dev, kind, duty, hbm_bytes, mfma_iters, mfma_shape, mfma_dtype)
         self.dev = dev
         self.kind = kind
 

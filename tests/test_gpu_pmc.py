@@ -35,3 +35,19 @@ def test_pmc_separates_idle_mfma_hbm():
     assert len(d["mfma"].get("xcd_mfma_busy", [])) == 8
     assert d["mfma_many"][0]["mfma_busy"] > 60, d["mfma_many"]  # sample_many agrees with sample
     print("pmc:", {k: d[k] for k in ("idle", "mfma", "hbm")})
+
+
+def test_mfma_tflops_per_dtype_match_events():
+    """gpu_mfma_tflops{dtype}: each matrix path's burn lights exactly its own MOPS counter, at the
+    event-timed rate (profiles/r1_mfma_dtypes.md)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools/mfma_dtypes.py"), "fp8", "mxfp4", "i8", "f64"],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    want = {"fp8": "f8", "mxfp4": "f6f4", "i8": "i8", "f64": "f64"}
+    for dt, counter in want.items():
+        (got, tf), = d[dt]["pmc_tflops"].items()
+        assert got == counter, d[dt]
+        ev = d[dt]["event_tflops"]
+        assert abs(tf - ev) < 0.03 * ev, d[dt]
+    assert d["mxfp4"]["event_tflops"] > 3 * d["fp8"]["event_tflops"]  # the 4x-rate f8f6f4 path
