@@ -404,3 +404,17 @@ def test_ras_counters_from_sysfs_and_amdsmi(core, torch_gpu):
         assert rs.samples()[0]["ras"]["blocks"].keys() == ras["blocks"].keys()
     finally:
         rs.stop()
+
+
+def test_mfma_dtype_burns_run_and_agree_across_waves(H, torch_gpu):
+    """Every matrix-path burn (burn_dtypes.hip) runs, produces finite non-zero sums, and every wave
+    computes the same sum (same operands in every wave): catches a miscompiled or faulting path."""
+    torch = torch_gpu
+    s = torch.cuda.current_stream().cuda_stream
+    for dt in ("f16", "fp8", "mxfp8", "mxfp4", "i8", "f32", "f64"):
+        o = torch.zeros(8 * 4, device="cuda")
+        flop = H.mfma_burn_dtype(0, dt, o.data_ptr(), 8, 4, s)
+        torch.cuda.synchronize()
+        assert flop > 0
+        assert torch.isfinite(o).all() and (o != 0).all(), (dt, o)
+        assert torch.equal(o, o[:1].expand_as(o)), (dt, o)
