@@ -24,7 +24,8 @@ def main():
 
     res = {}
     for dt in sys.argv[1:] or ("bf16", "f16", "fp8", "mxfp8", "mxfp4", "i8", "f32", "f64"):
-        with SyntheticLoad(0, "mfma", mfma_dtype=dt, mfma_iters=2048) as load:
+        # long launches (7-30 ms): the host sync between 4-launch batches stays < 0.5 % of the window
+        with SyntheticLoad(0, "mfma", mfma_dtype=dt, mfma_iters=16384) as load:
             time.sleep(1.0)
             s0 = load.stats()
             raw = P.sample(0, DEFAULT_COUNTERS, 0.4)
