@@ -687,7 +687,10 @@ PYBIND11_MODULE(_core, m) {
            py::arg("ms"), py::arg("dev") = -1)
       .def("mock_set_xgmi",
            [](Exporter& e, int dev, int link, double gbps) { mock_of(e)->set_xgmi(dev, link, gbps); })
-      .def("mock_calls", [](Exporter& e, int dev) { return mock_of(e)->calls(dev); });
+      .def("mock_calls", [](Exporter& e, int dev) { return mock_of(e)->calls(dev); })
+      .def("mock_set_link_up",
+           [](Exporter& e, int dev, int link, bool up) { mock_of(e)->set_link_up(dev, link, up); })
+      .def("mock_link_calls", [](Exporter& e, int dev) { return mock_of(e)->link_calls(dev); });
 
   // Native on-device samplers (csrc/core/ondevice.h): the same PMC / probe plugins the standalone
   // binary dlopen()s, driven from C++ threads instead of the Python runners in gpumon/ops.

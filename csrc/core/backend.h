@@ -135,6 +135,8 @@ class MockBackend : public Backend {
   // Force link `link` of `dev` to carry `gbps` GB/s of reads (and half of it as writes);
   // negative = back to the util-proportional default. For xGMI link-map tests.
   void set_xgmi(int dev, int link, double gbps);
+  void set_link_up(int dev, int link, bool up);  // firmware link status (0 down) of one xGMI slot
+  uint64_t link_calls(int dev) const;            // sample_links() calls (link-metrics refreshes)
   uint64_t calls(int dev) const;
 
  private:
@@ -143,6 +145,8 @@ class MockBackend : public Backend {
   mutable std::mutex mu_;
   std::vector<double> forced_util_;
   std::vector<double> forced_xgmi_;  // per dev * kMaxLinks, GB/s (NaN = default)
+  std::vector<char> link_down_;      // per dev * kMaxLinks
+  std::vector<uint64_t> link_calls_;
   std::vector<uint64_t> calls_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
   std::vector<uint64_t> lim_acc_;  // per device x XCC x {ppt, thermal, any, low-util}

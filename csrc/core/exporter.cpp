@@ -352,12 +352,18 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
   int n = backend_->device_count();
   out->resize(n);
   procs->assign(n, {});
-  // Link metrics (~1 ms per device) are refreshed every `link_every` ticks, staggered so at most
-  // ceil(n / link_every) devices pay it in any one tick (keeps the tick p99 flat at 8 GPUs).
+  // Link metrics (~1.2 ms per device: peer BDF, lane rate, max bandwidth — static while the link
+  // state holds) are refreshed every `link_every` ticks, staggered so at most ceil(n / link_every)
+  // devices pay it in one tick, and on the tick after a device's per-link status (read every tick
+  // from the firmware table) changed. Per-tick link traffic and status never need this call.
   const uint64_t tk = ticks_.load();
   const bool links_ok = backend_->supports_links() && cfg_.link_every > 0;
+  force_links_.resize(n, 0);
   auto links_due = [&](int i) {
-    return links_ok && (tk == 0 || (tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(cfg_.link_every) == 0);
+    const bool forced = force_links_[i] != 0;
+    force_links_[i] = 0;
+    return links_ok &&
+           (forced || tk == 0 || (tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(cfg_.link_every) == 0);
   };
   // RAS text files (~0.3 ms per device) every `ras_every` ticks, staggered the same way.
   const bool ras_ok = backend_->supports_ras() && cfg_.ras_every > 0;
@@ -570,6 +576,12 @@ TickInfo Exporter::tick() {
           if (s.links[k].link_type < 0) s.links[k].link_type = p.links[k].link_type;
         }
         if (!s.ras.valid && p.ras.valid && s.ok) s.ras = p.ras;  // between RAS refreshes
+        if (s.ok && p.ok && i < static_cast<int>(force_links_.size()))
+          for (int k = 0; k < kMaxLinks; ++k)
+            if (s.links[k].status >= 0 && p.links[k].status >= 0 && s.links[k].status != p.links[k].status) {
+              force_links_[i] = 1;  // a link went up / down: re-read peer identity and bandwidth
+              break;
+            }
       }
       // amdsmi_get_link_metrics lists 7 entries (incl. self) while the metrics table has 8 xGMI
       // slots on MI355X: a slot without a link_metrics entry gets speed x width (38 Gb/s x 16 =

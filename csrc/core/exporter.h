@@ -49,7 +49,7 @@ struct ExporterConfig {
   bool extended_families = true;
   bool full_device_labels = false;
   bool processes = true;
-  int link_every = 30;                // ticks between amdsmi_get_link_metrics refreshes
+  int link_every = 600;               // ticks between amdsmi_get_link_metrics refreshes (+ on link state change)
   int ras_every = 5;                  // ticks between RAS / ECC counter refreshes (0 = off)
   int sample_threads = -1;            // parallel device sampling; 0 = sequential, -1 = auto (one per GPU, max 8)
   AttributionConfig attribution;
@@ -212,6 +212,7 @@ class Exporter {
   std::shared_ptr<DoneSignal> done_sig_;
   uint64_t tick_id_ = 0;
   std::vector<uint64_t> dev_timeouts_;  // guarded by state_mu_
+  std::vector<char> force_links_;       // per device: refresh link metrics next tick (tick_mu_)
 };
 
 // "auto": amdsmi if it initialises, else error (never silently mock on a GPU host);

@@ -69,6 +69,8 @@ bool MockBackend::init(std::string* err) {
   size_t n = devs_.size();
   forced_util_.assign(n, kNaN);
   forced_xgmi_.assign(n * kMaxLinks, kNaN);
+  link_down_.assign(n * kMaxLinks, 0);
+  link_calls_.assign(n, 0);
   calls_.assign(n, 0);
   energy_.assign(n, 1000000);
   xgmi_rd_.assign(n * kMaxLinks, 0);
@@ -154,6 +156,15 @@ void MockBackend::set_hang_ms(double ms, int dev) {
   std::lock_guard<std::mutex> g(mu_);
   cfg_.hang_ms = ms;
   cfg_.hang_device = dev;
+}
+void MockBackend::set_link_up(int dev, int link, bool up) {
+  std::lock_guard<std::mutex> g(mu_);
+  const size_t k = static_cast<size_t>(dev) * kMaxLinks + link;
+  if (dev >= 0 && link >= 0 && link < kMaxLinks && k < link_down_.size()) link_down_[k] = up ? 0 : 1;
+}
+uint64_t MockBackend::link_calls(int dev) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return dev >= 0 && dev < static_cast<int>(link_calls_.size()) ? link_calls_[dev] : 0;
 }
 uint64_t MockBackend::calls(int dev) const {
   std::lock_guard<std::mutex> g(mu_);
@@ -278,7 +289,7 @@ void MockBackend::sample(int i, DeviceSample* out) {
     }
     a.xgmi_rd_kb[k] = xgmi_rd_[i * kMaxLinks + k];
     a.xgmi_wr_kb[k] = xgmi_wr_[i * kMaxLinks + k];
-    out->links[k].status = k == 0 ? -1 : 1;
+    out->links[k].status = k == 0 ? -1 : (link_down_[i * kMaxLinks + k] ? 0 : 1);
     out->links[k].bit_rate_gbps = 38;
   }
   for (const auto& name : cfg_.unsupported) {
@@ -326,6 +337,7 @@ bool MockBackend::processes(int i, std::vector<ProcSample>* out) {
 
 void MockBackend::sample_links(int i, DeviceSample* out) {
   std::lock_guard<std::mutex> g(mu_);
+  if (i >= 0 && i < static_cast<int>(link_calls_.size())) link_calls_[i]++;
   int nl = std::min(cfg_.n_links + 1, kMaxLinks);
   for (int k = 0; k < nl; ++k) {
     auto& L = out->links[k];

@@ -37,7 +37,7 @@ class Config:
     devices: List[int] = field(default_factory=list)
     interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
     processes: bool = True
-    link_every: int = 30
+    link_every: int = 600                 # ticks between link-metrics refreshes (+ whenever a link's state changes)
     ras_every: int = 5                    # ticks between RAS / ECC counter refreshes (0 = off)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
     device_timeout_s: float = 2.0         # a device call still running after this is exported as hung

@@ -214,3 +214,24 @@ def test_sequential_mode_has_no_workers(core):
     info = ex.tick()
     ex.stop()
     assert info["devices_ok"] == 2
+
+
+def test_link_metrics_refresh_rarely_and_on_link_state_change(mock_exporter):
+    """amdsmi_get_link_metrics (~1.2 ms, static peer / bandwidth data) runs at start, every
+    link_every ticks, and on the tick after a link's per-tick firmware status changed."""
+    from gpumon.export import promtext
+
+    ex = mock_exporter(backend="mock:gpus=2", link_every=600)
+    for _ in range(3):
+        ex.tick()
+    base = [ex.mock_link_calls(0), ex.mock_link_calls(1)]
+    assert base == [1, 1]  # only the first tick
+    ex.mock_set_link_up(1, 3, False)
+    ex.tick()  # status change seen here ...
+    ex.tick()  # ... link metrics re-read here
+    assert [ex.mock_link_calls(0), ex.mock_link_calls(1)] == [1, 2]
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_xgmi_link_up", gpu_id="1", link="3") == 0
+    assert promtext.one(fam, "gpu_xgmi_link_up", gpu_id="0", link="3") == 1
+    ex.tick()
+    assert ex.mock_link_calls(1) == 2  # no further refresh while the state holds
