@@ -8,11 +8,15 @@
 namespace gpumon {
 
 Histogram::Histogram(std::vector<double> bounds)
-    : bounds_(std::move(bounds)), counts_(new std::atomic<uint64_t>[bounds_.size() + 1]) {
+    : bounds_(std::move(bounds)), counts_(new std::atomic<uint64_t>[bounds_.size() + 1]),
+      recent_(new std::atomic<float>[kRecent]) {
   for (size_t i = 0; i <= bounds_.size(); ++i) counts_[i].store(0);
+  for (size_t i = 0; i < kRecent; ++i) recent_[i].store(0.f);
 }
 
 void Histogram::observe(double s) {
+  const uint64_t slot = recent_n_.fetch_add(1, std::memory_order_relaxed);
+  recent_[slot % kRecent].store(static_cast<float>(s), std::memory_order_relaxed);
   size_t i = std::lower_bound(bounds_.begin(), bounds_.end(), s) - bounds_.begin();
   counts_[i].fetch_add(1, std::memory_order_relaxed);
   count_.fetch_add(1, std::memory_order_relaxed);
@@ -34,6 +38,16 @@ void Histogram::snapshot(std::vector<double>* bounds, std::vector<uint64_t>* cou
 }
 
 double Histogram::quantile(double q) const {
+  const uint64_t n = std::min<uint64_t>(recent_n_.load(std::memory_order_relaxed), kRecent);
+  if (!n) return NAN;
+  std::vector<float> v(n);
+  for (uint64_t k = 0; k < n; ++k) v[k] = recent_[k].load(std::memory_order_relaxed);
+  const size_t idx = std::min<size_t>(n - 1, static_cast<size_t>(std::ceil(q * n)) - (q > 0 ? 1 : 0));
+  std::nth_element(v.begin(), v.begin() + idx, v.end());
+  return v[idx];
+}
+
+double Histogram::bucket_quantile(double q) const {
   std::vector<uint64_t> c(bounds_.size() + 1);
   uint64_t total = 0;
   for (size_t i = 0; i <= bounds_.size(); ++i) total += (c[i] = counts_[i].load());
