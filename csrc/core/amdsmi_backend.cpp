@@ -331,6 +331,8 @@ bool AmdSmiBackend::init(std::string* err) {
   GPUMON_LOG(LogLevel::kInfo, "amdsmi",
              "loaded " + t_->path + " version=" + lib_version_ + " gpus=" +
                  std::to_string(devs_.size()));
+  ras_readers_.clear();
+  ras_readers_.resize(devs_.size());  // entry i is created and used by device i's worker only
   return true;
 }
 
@@ -636,18 +638,19 @@ void AmdSmiBackend::sample_links(int i, DeviceSample* out) {
 
 // RAS: the kernel's ras/ text files first (no library call, readable by a non-root exporter, every
 // block the driver tracks); per-block amdsmi_get_gpu_ecc_count where the directory is absent.
-void AmdSmiBackend::sample_ras(int i, DeviceSample* out) {
+void AmdSmiBackend::sample_ras(int i, DeviceSample* out, int slice, int nslices) {
   if (i < 0 || i >= static_cast<int>(devs_.size())) return;
   Caps& c = caps_[i];
   const int64_t t0 = mono_ns();
   if (c.ras_sysfs) {
-    if (read_ras_sysfs(sys_root_, devs_[i].bdf, &out->ras)) {
+    if (!ras_readers_[i]) ras_readers_[i] = std::make_unique<RasSysfsReader>(sys_root_, devs_[i].bdf);
+    if (ras_readers_[i]->read(slice, nslices, &out->ras)) {
       record_call(kCallRas, mono_ns() - t0, true);
       return;
     }
     c.ras_sysfs = false;  // no ras/ directory on this node: do not stat it every refresh
   }
-  if (!t_->amdsmi_get_gpu_ecc_count || !c.ecc_blocks) return;
+  if (slice != 0 || !t_->amdsmi_get_gpu_ecc_count || !c.ecc_blocks) return;  // one library pass per cycle
   static const std::pair<amdsmi_gpu_block_t, const char*> kBlocks[] = {
       {AMDSMI_GPU_BLOCK_UMC, "umc"},       {AMDSMI_GPU_BLOCK_SDMA, "sdma"},
       {AMDSMI_GPU_BLOCK_GFX, "gfx"},       {AMDSMI_GPU_BLOCK_MMHUB, "mmhub"},

@@ -18,6 +18,10 @@
 #include "sample.h"
 
 namespace gpumon {
+class RasSysfsReader;
+}
+
+namespace gpumon {
 
 class Backend {
  public:
@@ -35,9 +39,11 @@ class Backend {
   // Optional: per-link metrics are expensive (~1 ms); sampled every `link_every` ticks.
   virtual bool supports_links() const { return false; }
   virtual void sample_links(int, DeviceSample*) {}
-  // Optional: RAS / ECC counters (ras.h), refreshed every `ras_every` ticks into out->ras.
+  // Optional: RAS / ECC counters (ras.h) into out->ras. Called every tick with slice =
+  // (tick + device) % nslices, nslices = `ras_every`: a source that can refresh part of its
+  // counters (the sysfs files) reads that slice; others refresh everything on slice 0 only.
   virtual bool supports_ras() const { return false; }
-  virtual void sample_ras(int, DeviceSample*) {}
+  virtual void sample_ras(int, DeviceSample*, int /*slice*/ = 0, int /*nslices*/ = 1) {}
   // Restrict to a subset of device hip_ids (empty = all). Applied at init().
   void set_device_filter(const std::vector<int>& ids) { filter_ = ids; }
 
@@ -121,7 +127,7 @@ class MockBackend : public Backend {
   bool supports_links() const override { return true; }
   void sample_links(int i, DeviceSample* out) override;
   bool supports_ras() const override { return true; }
-  void sample_ras(int i, DeviceSample* out) override;
+  void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;
 
   // Test controls (thread-safe).
   // Add errors to a RAS block of `dev` (blocks: umc gfx sdma mmhub xgmi_wafl vcn jpeg); `event`
@@ -176,7 +182,7 @@ class AmdSmiBackend : public Backend {
   bool supports_links() const override;
   void sample_links(int i, DeviceSample* out) override;
   bool supports_ras() const override { return true; }
-  void sample_ras(int i, DeviceSample* out) override;
+  void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;
   std::string lib_version() const { return lib_version_; }
   // Expose every physical device `r` times (distinct gpu_id labels). Only for measuring how the
   // sampler scales with the GPU count on a box with fewer GPUs than a full 8x MI355X node.
@@ -215,6 +221,7 @@ class AmdSmiBackend : public Backend {
     uint64_t ecc_seen = 0;          // ... and those that answered at least once
   };
   std::vector<Caps> caps_;
+  std::vector<std::unique_ptr<RasSysfsReader>> ras_readers_;  // per device, created on first use
   std::vector<std::vector<char>> proc_buf_;  // reusable process-list buffers
 };
 
@@ -235,7 +242,7 @@ class RocmSmiBackend : public Backend {
   void sample(int i, DeviceSample* out) override;
   bool processes(int i, std::vector<ProcSample>* out) override;
   bool supports_ras() const override { return true; }
-  void sample_ras(int i, DeviceSample* out) override;  // kernel ras/ sysfs files
+  void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;  // kernel ras/ sysfs files
   std::string lib_version() const { return lib_version_; }
   void set_sys_root(std::string r) { sys_root_ = std::move(r); }
 
@@ -247,6 +254,7 @@ class RocmSmiBackend : public Backend {
   bool metrics_ok_ = true;
   std::vector<DeviceStatic> devs_;
   std::vector<uint32_t> idx_;  // rsmi device index per exported device
+  std::vector<std::unique_ptr<RasSysfsReader>> ras_readers_;
   std::string lib_version_;
   double energy_res_uj_ = 15.3;
 };

@@ -41,6 +41,7 @@ struct Exporter::DevWorker {
   uint64_t req = 0;              // tick id of the current request
   std::atomic<uint64_t> done{0}; // tick id whose results are stored below
   bool want_links = false, want_procs = false, want_ras = false;
+  int ras_slice = 0, ras_n = 1;
   int64_t started_ns = 0;
   DeviceSample sample;
   std::vector<ProcSample> procs;
@@ -53,6 +54,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
   while (true) {
     uint64_t id;
     bool links, procs, ras;
+    int ras_slice, ras_n;
     {
       std::unique_lock<std::mutex> lk(w->mu);
       w->cv.wait(lk, [&] { return w->quit || w->pending; });
@@ -62,6 +64,8 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       links = w->want_links;
       procs = w->want_procs;
       ras = w->want_ras;
+      ras_slice = w->ras_slice;
+      ras_n = w->ras_n;
     }
     DeviceSample s;
     std::vector<ProcSample> p;
@@ -70,7 +74,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       TraceRange tr("gpumon.sample_dev");
       backend->sample(i, &s);
       if (links) backend->sample_links(i, &s);
-      if (ras && s.ok) backend->sample_ras(i, &s);
+      if (ras && s.ok) backend->sample_ras(i, &s, ras_slice, ras_n);
       if (procs && s.ok) {
         const int64_t t = mono_ns();
         backend->processes(i, &p);
@@ -365,10 +369,13 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
     return links_ok &&
            (forced || tk == 0 || (tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(cfg_.link_every) == 0);
   };
-  // RAS text files (~0.3 ms per device) every `ras_every` ticks, staggered the same way.
+  // RAS: one full pass over the text files (0.25-0.5 ms per device) per `ras_every` ticks, read
+  // as one slice per tick (slice 0 of device i lands on the same staggered tick as before); the
+  // first tick reads everything.
   const bool ras_ok = backend_->supports_ras() && cfg_.ras_every > 0;
-  auto ras_due = [&](int i) {
-    return ras_ok && (tk == 0 || (tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(cfg_.ras_every) == 0);
+  const int ras_n = tk == 0 ? 1 : std::max(1, cfg_.ras_every);
+  auto ras_slice = [&](int i) {
+    return static_cast<int>((tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(ras_n));
   };
   int64_t proc_ns = 0;
   if (static_cast<int>(workers_.size()) != n) {
@@ -377,7 +384,7 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
       TraceRange tr("gpumon.sample_dev");
       backend_->sample(i, &(*out)[i]);
       if (links_due(i)) backend_->sample_links(i, &(*out)[i]);
-      if (ras_due(i) && (*out)[i].ok) backend_->sample_ras(i, &(*out)[i]);
+      if (ras_ok && (*out)[i].ok) backend_->sample_ras(i, &(*out)[i], ras_slice(i), ras_n);
       if (cfg_.processes && (*out)[i].ok) {
         const int64_t t = mono_ns();
         backend_->processes(i, &(*procs)[i]);
@@ -397,7 +404,9 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
     w.busy = w.pending = true;
     w.req = id;
     w.want_links = links_due(i);
-    w.want_ras = ras_due(i);
+    w.want_ras = ras_ok;
+    w.ras_slice = ras_slice(i);
+    w.ras_n = ras_n;
     w.want_procs = cfg_.processes;
     w.started_ns = t0;
     asked[i] = 1;

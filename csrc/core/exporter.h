@@ -50,7 +50,7 @@ struct ExporterConfig {
   bool full_device_labels = false;
   bool processes = true;
   int link_every = 600;               // ticks between amdsmi_get_link_metrics refreshes (+ on link state change)
-  int ras_every = 5;                  // ticks between RAS / ECC counter refreshes (0 = off)
+  int ras_every = 5;                  // ticks per full RAS / ECC pass, one slice of the files per tick (0 = off)
   int sample_threads = -1;            // parallel device sampling; 0 = sequential, -1 = auto (one per GPU, max 8)
   AttributionConfig attribution;
   RateConfig rates;

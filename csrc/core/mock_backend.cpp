@@ -97,7 +97,8 @@ bool MockBackend::init(std::string* err) {
   return true;
 }
 
-void MockBackend::sample_ras(int i, DeviceSample* out) {
+void MockBackend::sample_ras(int i, DeviceSample* out, int slice, int) {
+  if (slice != 0) return;  // whole refresh once per cycle (carried over between)
   std::lock_guard<std::mutex> g(mu_);
   if (i < 0 || i >= static_cast<int>(ras_.size())) return;
   out->ras = ras_[i];

@@ -53,36 +53,77 @@ int count_bad_pages(const std::string& text) {
   return n;
 }
 
-bool read_ras_sysfs(const std::string& sys_root, const std::string& bdf, RasSample* out) {
-  if (bdf.empty()) return false;
-  const std::string dir = sys_root + "/bus/pci/devices/" + bdf + "/ras";
-  DIR* d = opendir(dir.c_str());
+RasSysfsReader::RasSysfsReader(const std::string& sys_root, const std::string& bdf)
+    : dir_(bdf.empty() ? std::string() : sys_root + "/bus/pci/devices/" + bdf + "/ras") {}
+
+bool RasSysfsReader::list() {
+  listed_ = true;
+  files_.clear();
+  if (dir_.empty()) return false;
+  DIR* d = opendir(dir_.c_str());
   if (!d) return false;
-  std::vector<std::pair<std::string, std::string>> files;  // (block, file)
   while (dirent* e = readdir(d)) {
     const std::string f = e->d_name;
-    if (starts_with(f, "aca_")) files.emplace_back(f.substr(4), f);
-    else if (ends_with(f, "_err_count")) files.emplace_back(f.substr(0, f.size() - 10), f);
+    if (starts_with(f, "aca_")) files_.emplace_back(f.substr(4), f);
+    else if (ends_with(f, "_err_count")) files_.emplace_back(f.substr(0, f.size() - 10), f);
   }
   closedir(d);
-  if (files.empty()) return false;
-  std::sort(files.begin(), files.end());
+  // an ACA file and a legacy file for the same block: keep the ACA one (it carries deferred);
+  // "aca_x" sorts before "x_err_count" within a block once keyed by block name
+  std::sort(files_.begin(), files_.end(), [](const auto& a, const auto& b) {
+    if (a.first != b.first) return a.first < b.first;
+    return starts_with(a.second, "aca_") && !starts_with(b.second, "aca_");
+  });
+  files_.erase(std::unique(files_.begin(), files_.end(),
+                           [](const auto& a, const auto& b) { return a.first == b.first; }),
+               files_.end());
+  return !files_.empty();
+}
+
+bool RasSysfsReader::read(int slice, int nslices, RasSample* out) {
+  const bool full = !cur_.valid;
+  if (full && !list()) return false;
+  if (nslices < 1) nslices = 1;
+  auto mine = [&](size_t k) { return full || static_cast<int>(k % static_cast<size_t>(nslices)) == slice; };
   RasSample r;
   r.source = "sysfs";
   std::string text;
-  for (const auto& bf : files) {
-    // an ACA file and a legacy file for the same block: keep the ACA one (it carries deferred)
-    if (!r.blocks.empty() && r.blocks.back().block == bf.first) continue;
+  for (size_t k = 0; k < files_.size(); ++k) {
     RasCount c;
-    c.block = bf.first;
-    if (read_file(dir + "/" + bf.second, &text, 4096) && parse_err_count(text, &c)) r.blocks.push_back(c);
+    c.block = files_[k].first;
+    const RasCount* prev = nullptr;
+    for (const auto& p : cur_.blocks)
+      if (p.block == c.block) prev = &p;
+    if (mine(k)) {
+      if (read_file(dir_ + "/" + files_[k].second, &text, 4096) && parse_err_count(text, &c)) r.blocks.push_back(c);
+      else if (prev) r.blocks.push_back(*prev);  // transient read failure: keep the last count
+    } else if (prev) {
+      r.blocks.push_back(*prev);
+    }
   }
   if (r.blocks.empty()) return false;
-  if (read_file(dir + "/event_state", &text, 4096)) parse_event_state(text, &r);
-  if (read_file(dir + "/gpu_vram_bad_pages", &text, 1 << 20)) r.bad_pages = count_bad_pages(text);
+  const size_t ev = files_.size(), bp = files_.size() + 1;
+  if (mine(ev)) {
+    if (read_file(dir_ + "/event_state", &text, 4096)) parse_event_state(text, &r);
+  } else {
+    r.fatal = cur_.fatal;
+    r.poison_created = cur_.poison_created;
+    r.poison_consumed = cur_.poison_consumed;
+  }
+  if (mine(bp)) {
+    if (read_file(dir_ + "/gpu_vram_bad_pages", &text, 1 << 20)) r.bad_pages = count_bad_pages(text);
+  } else {
+    r.bad_pages = cur_.bad_pages;
+  }
   r.valid = true;
+  cur_ = r;
   *out = std::move(r);
   return true;
+}
+
+bool read_ras_sysfs(const std::string& sys_root, const std::string& bdf, RasSample* out) {
+  RasSysfsReader r(sys_root, bdf);
+  return r.read(0, 1, out);
 }
 
 }  // namespace gpumon

@@ -8,11 +8,13 @@
 //   <block>_err_count   "ue: N\nce: N\n"          (older ASICs / kernels)
 //   event_state         fatal-error and poison creation / consumption counters
 //   gpu_vram_bad_pages  one "0xPFN : 0xSIZE : R|P|F" line per retired / pending page
-// Files are world-readable (0444) and cost 10-130 us each, so a non-root exporter reads them every
-// `ras_every` ticks without libamd_smi.
+// Files are world-readable (0444) and cost 10-130 us each, so a non-root exporter reads them without
+// libamd_smi, one slice per tick (RasSysfsReader), a full pass every `ras_every` ticks.
 #pragma once
 
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "sample.h"
 
@@ -30,5 +32,25 @@ int count_bad_pages(const std::string& text);
 // Reads <sys_root>/bus/pci/devices/<bdf>/ras; false (out untouched) when the directory has no
 // error-count files (RAS disabled, VM guest, or no such device).
 bool read_ras_sysfs(const std::string& sys_root, const std::string& bdf, RasSample* out);
+
+// Incremental reader for one device. A full refresh costs 0.24 ms idle and ~0.5 ms under load on
+// MI355X (aca_gfx alone 0.13 ms: the driver queries firmware per file), which made every
+// `ras_every`-th tick the slowest. read(slice, nslices) re-reads only the files whose index is
+// slice (mod nslices) and merges them into the last reading, so a full pass is spread over
+// nslices ticks. The first call always reads everything.
+class RasSysfsReader {
+ public:
+  RasSysfsReader(const std::string& sys_root, const std::string& bdf);
+  // false (out untouched) when the directory has no error-count files.
+  bool read(int slice, int nslices, RasSample* out);
+  int items() const { return static_cast<int>(files_.size()) + 2; }  // + event_state, bad pages
+
+ private:
+  bool list();
+  std::string dir_;
+  bool listed_ = false;
+  std::vector<std::pair<std::string, std::string>> files_;  // (block, file), one per block
+  RasSample cur_;
+};
 
 }  // namespace gpumon

@@ -178,6 +178,8 @@ bool RocmSmiBackend::init(std::string* err) {
   }
   GPUMON_LOG(LogLevel::kInfo, "rocm_smi",
              "loaded " + t_->path + " version=" + lib_version_ + " gpus=" + std::to_string(devs_.size()));
+  ras_readers_.clear();
+  ras_readers_.resize(devs_.size());
   return true;
 }
 
@@ -258,10 +260,11 @@ bool RocmSmiBackend::processes(int i, std::vector<ProcSample>* out) {
   return true;
 }
 
-void RocmSmiBackend::sample_ras(int i, DeviceSample* out) {
+void RocmSmiBackend::sample_ras(int i, DeviceSample* out, int slice, int nslices) {
   if (i < 0 || i >= static_cast<int>(devs_.size())) return;
+  if (!ras_readers_[i]) ras_readers_[i] = std::make_unique<RasSysfsReader>(sys_root_, devs_[i].bdf);
   const int64_t t0 = mono_ns();
-  const bool ok = read_ras_sysfs(sys_root_, devs_[i].bdf, &out->ras);
+  const bool ok = ras_readers_[i]->read(slice, nslices, &out->ras);
   record_call(kCallRas, mono_ns() - t0, ok);
 }
 

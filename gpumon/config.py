@@ -38,7 +38,7 @@ class Config:
     interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
     processes: bool = True
     link_every: int = 600                 # ticks between link-metrics refreshes (+ whenever a link's state changes)
-    ras_every: int = 5                    # ticks between RAS / ECC counter refreshes (0 = off)
+    ras_every: int = 5                    # ticks per full RAS / ECC pass, one slice of the files per tick (0 = off)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
     device_timeout_s: float = 2.0         # a device call still running after this is exported as hung
     reinit_after: int = 5                 # ticks with every GPU failing before the backend is re-initialised

@@ -153,7 +153,10 @@ _word = st.text(alphabet="abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ01
 _scalar = st.one_of(_word, st.integers(-10 ** 6, 10 ** 6), st.booleans(),
                     st.floats(-1e6, 1e6, allow_nan=False).map(lambda f: round(f, 3)))
 _value = st.one_of(_scalar, st.lists(st.one_of(_word, st.integers(0, 999)), max_size=5))
-_doc = st.dictionaries(st.from_regex(r"[a-z][a-z0-9_]{0,11}", fullmatch=True), _value, max_size=8)
+# keys PyYAML (YAML 1.1) would resolve to a bool / null are not config keys: leave them out
+_YAML11_KEYWORDS = {"y", "n", "yes", "no", "on", "off", "true", "false", "null"}
+_doc = st.dictionaries(st.from_regex(r"[a-z][a-z0-9_]{0,11}", fullmatch=True).filter(lambda k: k not in _YAML11_KEYWORDS),
+                       _value, max_size=8)
 
 
 def _as_text(v):

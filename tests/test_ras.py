@@ -136,3 +136,37 @@ def test_ras_off(mock_exporter):
     ex.tick()
     text = ex.metrics_text()
     assert "gpu_ecc_errors_total" not in text and "gpu_retired_pages" not in text
+
+
+def test_sysfs_refresh_is_spread_over_ras_every_ticks(core, monkeypatch, tmp_path):
+    """A full pass over the ras/ files costs 0.25-0.5 ms on MI355X; each tick re-reads one slice
+    (file index mod ras_every) and keeps the rest from the last pass, so no tick pays for all of
+    them and every counter is at most ras_every ticks old."""
+    sysr, procr = make_tree(tmp_path, gpus=1)
+    r = _ras_dir(sysr)
+    (r / "aca_gfx").write_text("ue: 0\nce: 1\nde: 0\n")      # item 0
+    (r / "aca_umc").write_text("ue: 0\nce: 2\nde: 0\n")      # item 1
+    (r / "aca_xgmi_wafl").write_text("ue: 0\nce: 0\nde: 0\n")  # item 2
+    (r / "event_state").write_text(MI355X_EVENT_STATE)      # item 3
+    ex = _exporter(core, monkeypatch, sysr, procr, env={"FAKE_AMDSMI_GPUS": 1}, ras_every=3)
+
+    def ce():
+        b = ex.samples()[0]["ras"]["blocks"]
+        return b["gfx"]["ce"], b["umc"]["ce"], sorted(b)
+
+    try:
+        ex.tick()  # first tick: everything
+        assert ce() == (1, 2, ["gfx", "umc", "xgmi_wafl"])
+        (r / "aca_gfx").write_text("ue: 0\nce: 10\nde: 0\n")
+        (r / "aca_umc").write_text("ue: 0\nce: 20\nde: 0\n")
+        seen = []
+        for _ in range(3):
+            ex.tick()
+            seen.append(ce())
+        assert all(s[2] == ["gfx", "umc", "xgmi_wafl"] for s in seen)  # never a partial block set
+        assert seen[-1][:2] == (10, 20)  # both refreshed within ras_every ticks ...
+        assert any(s[:2] in ((10, 2), (1, 20)) for s in seen), seen  # ... on different ticks
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpu_ras_events_total", event="poison_consumption") == 4  # carried
+    finally:
+        ex.stop()
