@@ -50,6 +50,7 @@ MockProc mock_proc_from(const py::dict& d) {
   get(d, "name", &p.name);
   get(d, "vram_bytes", &p.vram_bytes);
   get(d, "gfx_share", &p.gfx_share);
+  get(d, "kfd_only", &p.kfd_only);
   return p;
 }
 
@@ -75,6 +76,8 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "processes", &c.processes);
   get(d, "link_every", &c.link_every);
   get(d, "ras_every", &c.ras_every);
+  get(d, "ras_slices", &c.ras_slices);
+  get(d, "occ_samples", &c.occ_samples);
   get(d, "sample_threads", &c.sample_threads);
   get(d, "influx_url", &c.influx_url);
   get(d, "influx_extended", &c.influx_extended);
@@ -260,6 +263,7 @@ py::dict row_to_dict(const PodRow& r) {
   d["gpu_util"] = r.gpu_util;
   d["proc_gfx_util"] = num(r.proc_gfx_util);
   d["cu_occupancy"] = num(r.cu_occupancy);
+  d["occ_samples"] = r.occ_samples;
   return d;
 }
 
@@ -277,6 +281,25 @@ MockBackend* mock_of(Exporter& e) {
 }
 
 }  // namespace
+
+static py::dict tick_to_dict(const TickInfo& t) {
+  py::dict d;
+  d["seq"] = t.seq;
+  d["duration_s"] = t.duration_s;
+  d["devices"] = t.devices;
+  d["devices_ok"] = t.devices_ok;
+  d["pod_rows"] = t.pod_rows;
+  d["body_bytes"] = t.body_bytes;
+  d["t_sample"] = t.t_sample;
+  d["t_procs"] = t.t_procs;
+  d["t_attrib"] = t.t_attrib;
+  d["t_render"] = t.t_render;
+  d["t_gzip"] = t.t_gzip;
+  d["link_refreshes"] = t.link_refreshes;
+  d["ras_reads"] = t.ras_reads;
+  d["ras_full"] = t.ras_full;
+  return d;
+}
 
 PYBIND11_MODULE(_core, m) {
   m.doc() = "gpumon C++ core (MI355X telemetry exporter)";
@@ -494,20 +517,15 @@ PYBIND11_MODULE(_core, m) {
                py::gil_scoped_release nogil;
                t = e.tick();
              }
-             py::dict d;
-             d["seq"] = t.seq;
-             d["duration_s"] = t.duration_s;
-             d["devices"] = t.devices;
-             d["devices_ok"] = t.devices_ok;
-             d["pod_rows"] = t.pod_rows;
-             d["body_bytes"] = t.body_bytes;
-             d["t_sample"] = t.t_sample;
-             d["t_procs"] = t.t_procs;
-             d["t_attrib"] = t.t_attrib;
-             d["t_render"] = t.t_render;
-             d["t_gzip"] = t.t_gzip;
-             return d;
+             return tick_to_dict(t);
            })
+      .def("tick_log",
+           [](const Exporter& e) {
+             py::list l;
+             for (const auto& t : e.tick_log()) l.append(tick_to_dict(t));
+             return l;
+           },
+           "the last 4096 ticks (TickInfo dicts, oldest first): per-tick phase times for tail attribution")
       .def("phase_totals", &Exporter::phase_totals)
       .def("wait_for_seq",
            [](Exporter& e, uint64_t seq, double timeout_s) {
@@ -560,6 +578,7 @@ PYBIND11_MODULE(_core, m) {
              d["ticks"] = s.ticks;
              d["samples"] = s.samples;
              d["stale_samples"] = s.stale_samples;
+             d["occupancy_reads"] = s.occupancy_reads;
              d["overruns"] = s.overruns;
              d["scrapes"] = s.scrapes;
              d["http_connections"] = s.http_connections;
@@ -690,7 +709,10 @@ PYBIND11_MODULE(_core, m) {
       .def("mock_calls", [](Exporter& e, int dev) { return mock_of(e)->calls(dev); })
       .def("mock_set_link_up",
            [](Exporter& e, int dev, int link, bool up) { mock_of(e)->set_link_up(dev, link, up); })
-      .def("mock_link_calls", [](Exporter& e, int dev) { return mock_of(e)->link_calls(dev); });
+      .def("mock_link_calls", [](Exporter& e, int dev) { return mock_of(e)->link_calls(dev); })
+      .def("mock_set_occ_series",
+           [](Exporter& e, int dev, const std::vector<double>& v) { mock_of(e)->set_occ_series(dev, v); })
+      .def("mock_occ_reads", [](Exporter& e, int dev) { return mock_of(e)->occ_reads(dev); });
 
   // Native on-device samplers (csrc/core/ondevice.h): the same PMC / probe plugins the standalone
   // binary dlopen()s, driven from C++ threads instead of the Python runners in gpumon/ops.

@@ -44,14 +44,16 @@ PYBIND11_MODULE(_hip, m) {
 
   py::class_<LoadGen>(m, "LoadGen")
       .def(py::init([](int dev, std::string kind, double duty, size_t hbm_bytes, int mfma_iters, int shape,
-                       std::string dtype) {
+                       std::string dtype, double period_s) {
              auto g = std::make_unique<LoadGen>(dev, std::move(kind), duty, hbm_bytes, mfma_iters);
              g->set_mfma_shape(shape);
              g->set_mfma_dtype(std::move(dtype));
+             g->set_period(period_s);
              return g;
            }),
            py::arg("dev"), py::arg("kind") = "mixed", py::arg("duty") = 1.0, py::arg("hbm_bytes") = size_t(1) << 30,
-           py::arg("mfma_iters") = 8192, py::arg("mfma_shape") = 32, py::arg("mfma_dtype") = "bf16")
+           py::arg("mfma_iters") = 8192, py::arg("mfma_shape") = 32, py::arg("mfma_dtype") = "bf16",
+           py::arg("period_s") = 0.0)
       .def("start", [](LoadGen& g) {
         py::gil_scoped_release nogil;
         g.start();
@@ -70,8 +72,35 @@ PYBIND11_MODULE(_hip, m) {
         d["bytes"] = s.bytes;
         d["mfma_s"] = s.mfma_s;
         d["hbm_s"] = s.hbm_s;
+        d["wall_s"] = s.wall_s;
         d["tflops"] = s.mfma_s > 0 ? s.flops / s.mfma_s / 1e12 : 0.0;  // rate while MFMA batches ran
         d["tbps"] = s.hbm_s > 0 ? s.bytes / s.hbm_s / 1e12 : 0.0;      // rate while HBM batches ran
+        d["tflops_wall"] = s.wall_s > 0 ? s.flops / s.wall_s / 1e12 : 0.0;  // averaged over wall time
+        d["tbps_wall"] = s.wall_s > 0 ? s.bytes / s.wall_s / 1e12 : 0.0;
+        return d;
+      });
+
+  py::class_<XgmiLoad>(m, "XgmiLoad")
+      .def(py::init<int, int, size_t, std::string, int>(), py::arg("src"), py::arg("dst"),
+           py::arg("nbytes") = size_t(256) << 20, py::arg("method") = "kernel", py::arg("blocks") = 512)
+      .def("start", [](XgmiLoad& g) {
+        py::gil_scoped_release nogil;
+        g.start();
+      })
+      .def("stop", [](XgmiLoad& g) {
+        py::gil_scoped_release nogil;
+        g.stop();
+      })
+      .def_property_readonly("running", &XgmiLoad::running)
+      .def("stats", [](XgmiLoad& g) {
+        XgmiStats s = g.stats();
+        py::dict d;
+        d["copies"] = s.copies;
+        d["bytes"] = s.bytes;
+        d["busy_s"] = s.busy_s;
+        d["wall_s"] = s.wall_s;
+        d["GBps"] = s.busy_s > 0 ? s.bytes / s.busy_s / 1e9 : 0.0;       // while copying
+        d["GBps_wall"] = s.wall_s > 0 ? s.bytes / s.wall_s / 1e9 : 0.0;  // averaged over wall time
         return d;
       });
 

@@ -611,6 +611,18 @@ bool AmdSmiBackend::processes(int i, std::vector<ProcSample>* out) {
   return false;
 }
 
+bool AmdSmiBackend::supports_occupancy(int i) const {
+  return i >= 0 && i < static_cast<int>(fast_.size()) && fast_[i] && fast_[i]->have_kfd();
+}
+
+void AmdSmiBackend::occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) {
+  if (!supports_occupancy(i)) {
+    out->assign(pids.size(), kNaN);
+    return;
+  }
+  fast_[i]->occupancy(pids, out);
+}
+
 bool AmdSmiBackend::supports_links() const { return t_ && t_->amdsmi_get_link_metrics; }
 
 void AmdSmiBackend::sample_links(int i, DeviceSample* out) {
@@ -645,7 +657,9 @@ void AmdSmiBackend::sample_ras(int i, DeviceSample* out, int slice, int nslices)
   if (c.ras_sysfs) {
     if (!ras_readers_[i]) ras_readers_[i] = std::make_unique<RasSysfsReader>(sys_root_, devs_[i].bdf);
     if (ras_readers_[i]->read(slice, nslices, &out->ras)) {
-      record_call(kCallRas, mono_ns() - t0, true);
+      // a due file that failed keeps its last value: report the call failed so a stuck file shows
+      // in gpumon_backend_call_errors_total{call="ras"} instead of freezing silently
+      record_call(kCallRas, mono_ns() - t0, out->ras.stale_items == 0);
       return;
     }
     c.ras_sysfs = false;  // no ras/ directory on this node: do not stat it every refresh

@@ -39,10 +39,17 @@ class Backend {
   // Optional: per-link metrics are expensive (~1 ms); sampled every `link_every` ticks.
   virtual bool supports_links() const { return false; }
   virtual void sample_links(int, DeviceSample*) {}
-  // Optional: RAS / ECC counters (ras.h) into out->ras. Called every tick with slice =
-  // (tick + device) % nslices, nslices = `ras_every`: a source that can refresh part of its
-  // counters (the sysfs files) reads that slice; others refresh everything on slice 0 only.
+  // Optional: RAS / ECC counters (ras.h) into out->ras. Called on the ticks where a RAS slice is due
+  // (Exporter::sample_devices: `ras_slices` consecutive ticks out of every `ras_every`) with slice
+  // in [0, nslices), nslices = `ras_slices`: a source that can refresh part of its counters (the
+  // sysfs files) reads that slice; others refresh everything on slice 0 only.
   virtual bool supports_ras() const { return false; }
+  // Optional: instantaneous KFD cu_occupancy of `pids` on device i (out[k] NaN = unreadable).
+  // Cheap (~27 us per process on MI355X): the device worker sub-samples it between ticks.
+  virtual bool supports_occupancy(int /*i*/) const { return false; }
+  virtual void occupancy(int, const std::vector<uint32_t>& pids, std::vector<double>* out) {
+    out->assign(pids.size(), kNaN);
+  }
   virtual void sample_ras(int, DeviceSample*, int /*slice*/ = 0, int /*nslices*/ = 1) {}
   // Restrict to a subset of device hip_ids (empty = all). Applied at init().
   void set_device_filter(const std::vector<int>& ids) { filter_ = ids; }
@@ -97,6 +104,7 @@ struct MockProc {
   std::string name = "python3";
   double vram_bytes = 1024.0 * 1024 * 1024;
   double gfx_share = 0.5;  // fraction of device busy time attributed to this process
+  bool kfd_only = false;   // HIP compute on KFD user queues: no DRM fdinfo engine time
 };
 
 struct MockConfig {
@@ -128,8 +136,14 @@ class MockBackend : public Backend {
   void sample_links(int i, DeviceSample* out) override;
   bool supports_ras() const override { return true; }
   void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;
+  bool supports_occupancy(int) const override { return true; }
+  void occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) override;
 
   // Test controls (thread-safe).
+  // Every cu_occupancy read of `dev` (process list and sub-samples alike) returns the next value of
+  // `values`, cycling; empty = back to the util-proportional default.
+  void set_occ_series(int dev, const std::vector<double>& values);
+  uint64_t occ_reads(int dev) const;
   // Add errors to a RAS block of `dev` (blocks: umc gfx sdma mmhub xgmi_wafl vcn jpeg); `event`
   // counters: "fatal", "poison_created", "poison_consumed", "bad_pages" (set, not added).
   void add_ecc(int dev, const std::string& block, uint64_t ue, uint64_t ce, uint64_t de);
@@ -150,6 +164,9 @@ class MockBackend : public Backend {
   std::vector<DeviceStatic> devs_;
   mutable std::mutex mu_;
   std::vector<double> forced_util_;
+  std::vector<std::vector<double>> occ_series_;  // per dev (set_occ_series)
+  std::vector<uint64_t> occ_reads_;               // per dev: cu_occupancy reads served
+  double occ_value(int i, const MockProc& p, double util);  // mu_ held
   std::vector<double> forced_xgmi_;  // per dev * kMaxLinks, GB/s (NaN = default)
   std::vector<char> link_down_;      // per dev * kMaxLinks
   std::vector<uint64_t> link_calls_;
@@ -183,6 +200,8 @@ class AmdSmiBackend : public Backend {
   void sample_links(int i, DeviceSample* out) override;
   bool supports_ras() const override { return true; }
   void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;
+  bool supports_occupancy(int i) const override;  // with the sysfs fast path (KFD files)
+  void occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) override;
   std::string lib_version() const { return lib_version_; }
   // Expose every physical device `r` times (distinct gpu_id labels). Only for measuring how the
   // sampler scales with the GPU count on a box with fewer GPUs than a full 8x MI355X node.
@@ -255,6 +274,7 @@ class RocmSmiBackend : public Backend {
   std::vector<DeviceStatic> devs_;
   std::vector<uint32_t> idx_;  // rsmi device index per exported device
   std::vector<std::unique_ptr<RasSysfsReader>> ras_readers_;
+  std::vector<char> ras_missing_;  // per device: no readable ras/ files (reset by init())
   std::string lib_version_;
   double energy_res_uj_ = 15.3;
 };

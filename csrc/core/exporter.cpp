@@ -49,16 +49,56 @@ struct Exporter::DevWorker {
   std::thread th;
 };
 
+// Between ticks the worker sub-samples the KFD cu_occupancy of the processes its device had at
+// the last tick, every occ_period_ns (interval / occ_samples): one read per tick is an instant
+// (4.6 % of reads under a saturating burn land between two kernels and return 0, profiles/
+// r2_kfd_occupancy.md); the tick's process rows carry the interval mean and the share of reads
+// that found the process's waves resident.
 static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_ptr<Exporter::DoneSignal> sig,
-                            Backend* backend, int i) {
+                            Backend* backend, int i, int64_t occ_period_ns,
+                            std::shared_ptr<std::atomic<uint64_t>> occ_reads) {
+  std::vector<uint32_t> occ_pids;                      // processes on this device at the last tick
+  std::vector<double> occ_sum;                         // per occ_pids entry
+  std::vector<int> occ_n, occ_busy;
+  std::vector<double> vals;
+  const bool occ_on = occ_period_ns > 0 && backend->supports_occupancy(i);
+  int64_t next_occ = 0;
   while (true) {
     uint64_t id;
     bool links, procs, ras;
     int ras_slice, ras_n;
     {
       std::unique_lock<std::mutex> lk(w->mu);
-      w->cv.wait(lk, [&] { return w->quit || w->pending; });
+      bool subsample = false;
+      while (!w->quit && !w->pending) {
+        if (!occ_on || occ_pids.empty()) {
+          w->cv.wait(lk);
+          continue;
+        }
+        const int64_t left = next_occ - mono_ns();
+        if (left <= 0) {
+          subsample = true;
+          break;
+        }
+        // system_clock slices checked against the monotonic deadline (TSan: see sample_devices)
+        w->cv.wait_until(lk, std::chrono::system_clock::now() +
+                                 std::chrono::nanoseconds(std::min<int64_t>(left, 20'000'000)));
+      }
       if (w->quit) return;
+      if (subsample) {
+        lk.unlock();
+        backend->occupancy(i, occ_pids, &vals);
+        for (size_t k = 0; k < occ_pids.size() && k < vals.size(); ++k)
+          if (has(vals[k])) {
+            occ_sum[k] += vals[k];
+            occ_n[k]++;
+            occ_busy[k] += vals[k] > 0 ? 1 : 0;
+          }
+        occ_reads->fetch_add(occ_pids.size(), std::memory_order_relaxed);
+        next_occ += occ_period_ns;
+        if (next_occ < mono_ns()) next_occ = mono_ns() + occ_period_ns;
+        continue;
+      }
       w->pending = false;
       id = w->req;
       links = w->want_links;
@@ -80,6 +120,32 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
         backend->processes(i, &p);
         pns = mono_ns() - t;
       }
+    }
+    // fold the interval's sub-samples into this tick's instantaneous reading
+    for (auto& ps : p) {
+      if (!has(ps.cu_occupancy)) continue;
+      double sum = ps.cu_occupancy;
+      int n = 1, busy = ps.cu_occupancy > 0 ? 1 : 0;
+      for (size_t k = 0; k < occ_pids.size(); ++k)
+        if (occ_pids[k] == ps.pid) {
+          sum += occ_sum[k];
+          n += occ_n[k];
+          busy += occ_busy[k];
+          break;
+        }
+      ps.cu_occupancy = sum / n;
+      ps.occ_samples = n;
+      ps.occ_busy = busy;
+    }
+    if (occ_on && procs) {
+      occ_pids.clear();
+      for (const auto& ps : p)
+        if (has(ps.cu_occupancy) && std::find(occ_pids.begin(), occ_pids.end(), ps.pid) == occ_pids.end())
+          occ_pids.push_back(ps.pid);
+      occ_sum.assign(occ_pids.size(), 0.0);
+      occ_n.assign(occ_pids.size(), 0);
+      occ_busy.assign(occ_pids.size(), 0);
+      next_occ = mono_ns() + occ_period_ns;
     }
     {
       std::lock_guard<std::mutex> g(w->mu);
@@ -104,7 +170,11 @@ void Exporter::start_workers(int n) {
   if (!done_sig_) done_sig_ = std::make_shared<DoneSignal>();
   for (int i = 0; i < n; ++i) {
     auto w = std::make_shared<DevWorker>();
-    w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i);
+    // sub-sample period: interval / occ_samples, no faster than 50 Hz; manual ticks: none
+    const int64_t occ_ns = cfg_.interval_s > 0 && cfg_.occ_samples > 1 && cfg_.processes
+                               ? std::max<int64_t>(20'000'000, static_cast<int64_t>(cfg_.interval_s * 1e9 / cfg_.occ_samples))
+                               : 0;
+    w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i, occ_ns, occ_reads_);
     workers_.push_back(std::move(w));
   }
 }
@@ -328,6 +398,14 @@ void Exporter::stop() {
   backend_up_ = false;
 }
 
+std::vector<TickInfo> Exporter::tick_log() const {
+  std::lock_guard<std::mutex> g(tick_log_mu_);
+  if (tick_log_.size() < kTickLog) return tick_log_;
+  std::vector<TickInfo> v(tick_log_.begin() + static_cast<std::ptrdiff_t>(tick_log_next_), tick_log_.end());
+  v.insert(v.end(), tick_log_.begin(), tick_log_.begin() + static_cast<std::ptrdiff_t>(tick_log_next_));
+  return v;
+}
+
 void Exporter::sampler_loop() {
   const int64_t period = static_cast<int64_t>(cfg_.interval_s * 1e9);
   int64_t next = mono_ns() + period;
@@ -352,7 +430,7 @@ void Exporter::sampler_loop() {
 }
 
 void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
-                              double* procs_s) {
+                              double* procs_s, TickInfo* info) {
   int n = backend_->device_count();
   out->resize(n);
   procs->assign(n, {});
@@ -363,20 +441,29 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
   const uint64_t tk = ticks_.load();
   const bool links_ok = backend_->supports_links() && cfg_.link_every > 0;
   force_links_.resize(n, 0);
+  links_read_.assign(n, 0);
   auto links_due = [&](int i) {
     const bool forced = force_links_[i] != 0;
     force_links_[i] = 0;
-    return links_ok &&
-           (forced || tk == 0 || (tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(cfg_.link_every) == 0);
+    const bool due =
+        links_ok && (forced || tk == 0 || (tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(cfg_.link_every) == 0);
+    links_read_[i] = due ? 1 : 0;
+    if (due) info->link_refreshes++;
+    return due;
   };
-  // RAS: one full pass over the text files (0.25-0.5 ms per device) per `ras_every` ticks, read
-  // as one slice per tick (slice 0 of device i lands on the same staggered tick as before); the
-  // first tick reads everything.
+  // RAS: one full pass over the files every `ras_every` ticks (staggered per device), read as
+  // `ras_slices` slices on consecutive ticks (1 = the whole pass on one tick: the fewest firmware
+  // query bursts; more slices flatten the pass's tick-time spike). The first tick reads everything.
   const bool ras_ok = backend_->supports_ras() && cfg_.ras_every > 0;
-  const int ras_n = tk == 0 ? 1 : std::max(1, cfg_.ras_every);
-  auto ras_slice = [&](int i) {
-    return static_cast<int>((tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(ras_n));
+  const int ras_period = std::max(1, cfg_.ras_every);
+  const int ras_n = tk == 0 ? 1 : std::clamp(cfg_.ras_slices, 1, ras_period);
+  auto ras_slice = [&](int i) {  // slice due for device i this tick, or -1
+    if (!ras_ok) return -1;
+    if (tk == 0) return 0;
+    const int ph = static_cast<int>((tk + static_cast<uint64_t>(i)) % static_cast<uint64_t>(ras_period));
+    return ph < ras_n ? ph : -1;
   };
+  info->ras_full = ras_ok && ras_n == 1;
   int64_t proc_ns = 0;
   if (static_cast<int>(workers_.size()) != n) {
     // sequential: metrics table, (links), process list per device on the sampler thread
@@ -384,11 +471,20 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
       TraceRange tr("gpumon.sample_dev");
       backend_->sample(i, &(*out)[i]);
       if (links_due(i)) backend_->sample_links(i, &(*out)[i]);
-      if (ras_ok && (*out)[i].ok) backend_->sample_ras(i, &(*out)[i], ras_slice(i), ras_n);
+      const int rs = ras_slice(i);
+      if (rs >= 0 && (*out)[i].ok) {
+        backend_->sample_ras(i, &(*out)[i], rs, ras_n);
+        info->ras_reads++;
+      }
       if (cfg_.processes && (*out)[i].ok) {
         const int64_t t = mono_ns();
         backend_->processes(i, &(*procs)[i]);
         proc_ns += mono_ns() - t;
+        for (auto& ps : (*procs)[i])
+          if (has(ps.cu_occupancy)) {
+            ps.occ_samples = 1;
+            ps.occ_busy = ps.cu_occupancy > 0 ? 1 : 0;
+          }
       }
     }
     *procs_s = proc_ns * 1e-9;
@@ -404,9 +500,10 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
     w.busy = w.pending = true;
     w.req = id;
     w.want_links = links_due(i);
-    w.want_ras = ras_ok;
     w.ras_slice = ras_slice(i);
+    w.want_ras = w.ras_slice >= 0;
     w.ras_n = ras_n;
+    if (w.want_ras) info->ras_reads++;
     w.want_procs = cfg_.processes;
     w.started_ns = t0;
     asked[i] = 1;
@@ -484,6 +581,10 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
           util = std::min(100.0, (p.gfx_ns - it->second.gfx_ns) * 100.0 / (now - it->second.t_ns));
         next_prev[k] = ProcPrev{p.gfx_ns, now, id.starttime};
       }
+      // HIP compute runs on KFD user queues, which DRM fdinfo engine time never sees: there the
+      // process's busy % is the share of the interval's cu_occupancy reads that found its waves
+      // resident (the per-process analogue of the device's gfx activity)
+      if (!has(util) && p.occ_samples > 0) util = 100.0 * p.occ_busy / p.occ_samples;
       if (!id.opted_in) continue;
       PodRow r;
       r.dev = static_cast<int>(d);
@@ -502,6 +603,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       r.gpu_util = has(dev_util) ? dev_util : 0;
       r.proc_gfx_util = util;
       r.cu_occupancy = p.cu_occupancy;
+      r.occ_samples = p.occ_samples;
       active.emplace_back(r.pod_namespace, r.pod_name, r.container, r.dev);
       row_of_pid[p.pid] = rows->size();
       rows->push_back(std::move(r));
@@ -562,7 +664,7 @@ TickInfo Exporter::tick() {
     int64_t ta = mono_ns();
     {
       TraceRange tr("gpumon.sample");
-      sample_devices(&cur, &procs, &info.t_procs);
+      sample_devices(&cur, &procs, &info.t_procs, &info);
     }
     int n = static_cast<int>(cur.size());
     info.t_sample = (mono_ns() - ta) * 1e-9;
@@ -577,20 +679,31 @@ TickInfo Exporter::tick() {
       DeviceSample& s = cur[i];
       if (i < static_cast<int>(prev.size())) {
         const DeviceSample& p = prev[i];
-        // keep link identity (peer bdf, max bw) between link refreshes
-        for (int k = 0; k < kMaxLinks; ++k) {
-          if (s.links[k].peer_bdf.empty()) s.links[k].peer_bdf = p.links[k].peer_bdf;
-          if (!has(s.links[k].max_bandwidth_gbps))
-            s.links[k].max_bandwidth_gbps = p.links[k].max_bandwidth_gbps;
-          if (s.links[k].link_type < 0) s.links[k].link_type = p.links[k].link_type;
-        }
+        // keep link identity (peer bdf, max bw) between link refreshes -- but not on a tick that
+        // re-read the links: an empty peer / unknown bandwidth then means the link lost them
+        const bool refreshed = i < static_cast<int>(links_read_.size()) && links_read_[i];
+        if (!refreshed)
+          for (int k = 0; k < kMaxLinks; ++k) {
+            if (s.links[k].peer_bdf.empty()) s.links[k].peer_bdf = p.links[k].peer_bdf;
+            if (!has(s.links[k].max_bandwidth_gbps))
+              s.links[k].max_bandwidth_gbps = p.links[k].max_bandwidth_gbps;
+            if (s.links[k].link_type < 0) s.links[k].link_type = p.links[k].link_type;
+          }
         if (!s.ras.valid && p.ras.valid && s.ok) s.ras = p.ras;  // between RAS refreshes
-        if (s.ok && p.ok && i < static_cast<int>(force_links_.size()))
-          for (int k = 0; k < kMaxLinks; ++k)
-            if (s.links[k].status >= 0 && p.links[k].status >= 0 && s.links[k].status != p.links[k].status) {
-              force_links_[i] = 1;  // a link went up / down: re-read peer identity and bandwidth
+      }
+      // A link's firmware status changed since the last SUCCESSFUL sample of this device (a failed
+      // tick in between must not hide the change): re-read peer identity and bandwidth next tick.
+      if (s.ok && i < static_cast<int>(force_links_.size())) {
+        if (static_cast<int>(link_status_.size()) < n) link_status_.resize(n);
+        auto& last = link_status_[i];
+        if (!last.empty())
+          for (int k = 0; k < kMaxLinks && k < static_cast<int>(last.size()); ++k)
+            if (s.links[k].status >= 0 && last[k] >= 0 && s.links[k].status != last[k]) {
+              force_links_[i] = 1;
               break;
             }
+        last.assign(kMaxLinks, -1);
+        for (int k = 0; k < kMaxLinks; ++k) last[k] = s.links[k].status;
       }
       // amdsmi_get_link_metrics lists 7 entries (incl. self) while the metrics table has 8 xGMI
       // slots on MI355X: a slot without a link_metrics entry gets speed x width (38 Gb/s x 16 =
@@ -719,6 +832,12 @@ TickInfo Exporter::tick() {
   info.duration_s = (mono_ns() - t0) * 1e-9;
   sample_hist_.observe(info.duration_s);
   info.seq = s;
+  {
+    std::lock_guard<std::mutex> g(tick_log_mu_);
+    if (tick_log_.size() < kTickLog) tick_log_.push_back(info);
+    else tick_log_[tick_log_next_] = info;
+    tick_log_next_ = (tick_log_next_ + 1) % kTickLog;
+  }
   {
     std::lock_guard<std::mutex> g(seq_mu_);
     seq_ = s;
@@ -915,6 +1034,7 @@ SelfStats Exporter::self_stats() const {
   s.ticks = ticks_;
   s.samples = samples_;
   s.stale_samples = stale_;
+  s.occupancy_reads = occ_reads_->load(std::memory_order_relaxed);
   s.overruns = overruns_;
   s.last_tick_wall_s = last_tick_wall_ns_.load() * 1e-9;
   s.interval_s = cfg_.interval_s;

@@ -50,8 +50,10 @@ struct ExporterConfig {
   bool full_device_labels = false;
   bool processes = true;
   int link_every = 600;               // ticks between amdsmi_get_link_metrics refreshes (+ on link state change)
-  int ras_every = 5;                  // ticks per full RAS / ECC pass, one slice of the files per tick (0 = off)
+  int ras_every = 5;                  // ticks per full RAS / ECC pass (0 = off)
+  int ras_slices = 1;                 // the pass read in this many slices on consecutive ticks (1..ras_every)
   int sample_threads = -1;            // parallel device sampling; 0 = sequential, -1 = auto (one per GPU, max 8)
+  int occ_samples = 10;               // KFD cu_occupancy reads per process per tick on the device workers (1 = the tick's own)
   AttributionConfig attribution;
   RateConfig rates;
   std::string influx_url;             // INFLUXDB_URL; empty = push disabled
@@ -82,6 +84,9 @@ struct TickInfo {
   size_t body_bytes = 0;
   // phase breakdown (seconds): device metrics, process lists, attribution, render, gzip
   double t_sample = 0, t_procs = 0, t_attrib = 0, t_render = 0, t_gzip = 0;
+  int link_refreshes = 0;   // devices whose link metrics were re-read this tick
+  int ras_reads = 0;        // devices that read a RAS slice this tick
+  bool ras_full = false;    // the RAS read covered every file (first tick / ras_slices = 1)
 };
 
 class Exporter {
@@ -120,6 +125,9 @@ class Exporter {
   const ExporterConfig& config() const { return cfg_; }
   double scrape_quantile(double q) const { return scrape_hist_.quantile(q); }
   double sample_quantile(double q) const { return sample_hist_.quantile(q); }
+  // The last kTickLog ticks' TickInfo, oldest first (tick-tail attribution: bench / introspection).
+  static constexpr size_t kTickLog = 4096;
+  std::vector<TickInfo> tick_log() const;
 
  private:
   void sampler_loop();
@@ -130,7 +138,7 @@ class Exporter {
   bool ensure_backend();
   void handle_http(const HttpRequest& req, HttpResponse* resp);
   void sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
-                      double* procs_s);
+                      double* procs_s, TickInfo* info);
   void build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
                       const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows);
 
@@ -140,6 +148,9 @@ class Exporter {
   std::unique_ptr<HttpServer> server_;
   SnapshotStore store_;
   Histogram sample_hist_;
+  mutable std::mutex tick_log_mu_;
+  std::vector<TickInfo> tick_log_;  // ring of kTickLog entries
+  size_t tick_log_next_ = 0;
   Histogram scrape_hist_;
 
   mutable std::mutex state_mu_;       // guards the "latest" introspection copies below
@@ -209,10 +220,14 @@ class Exporter {
   bool stop_workers();
   bool workers_busy() const;
   std::vector<std::shared_ptr<DevWorker>> workers_;
+  // cu_occupancy sub-sample reads by the workers (shared: a detached worker may outlive a restart)
+  std::shared_ptr<std::atomic<uint64_t>> occ_reads_ = std::make_shared<std::atomic<uint64_t>>(0);
   std::shared_ptr<DoneSignal> done_sig_;
   uint64_t tick_id_ = 0;
   std::vector<uint64_t> dev_timeouts_;  // guarded by state_mu_
   std::vector<char> force_links_;       // per device: refresh link metrics next tick (tick_mu_)
+  std::vector<char> links_read_;        // per device: link metrics were re-read this tick (tick_mu_)
+  std::vector<std::vector<int>> link_status_;  // per device: link status at its last ok sample (tick_mu_)
 };
 
 // "auto": amdsmi if it initialises, else error (never silently mock on a GPU host);

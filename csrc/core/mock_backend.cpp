@@ -329,11 +329,47 @@ bool MockBackend::processes(int i, std::vector<ProcSample>* out) {
     uint64_t& ns = proc_gfx_ns_[key];
     ns += static_cast<uint64_t>(util / 100.0 * p.gfx_share * 1e7);
     ps.gfx_ns = ns + static_cast<uint64_t>((mono_ns() - t0_ns_) * (util / 100.0) * p.gfx_share);
-    ps.has_gfx_ns = true;
-    ps.cu_occupancy = std::floor(256.0 * util / 100.0 * p.gfx_share);
+    ps.has_gfx_ns = !p.kfd_only;
+    ps.cu_occupancy = occ_value(i, p, util);
     out->push_back(std::move(ps));
   }
   return true;
+}
+
+double MockBackend::occ_value(int i, const MockProc& p, double util) {
+  if (static_cast<int>(occ_reads_.size()) <= i) occ_reads_.resize(devs_.size(), 0);
+  const uint64_t k = occ_reads_[i]++;
+  if (i < static_cast<int>(occ_series_.size()) && !occ_series_[i].empty())
+    return occ_series_[i][k % occ_series_[i].size()];
+  return std::floor(256.0 * util / 100.0 * p.gfx_share);
+}
+
+void MockBackend::occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) {
+  std::lock_guard<std::mutex> g(mu_);
+  out->assign(pids.size(), kNaN);
+  if (i < 0 || i >= static_cast<int>(devs_.size())) return;
+  const double util = has(forced_util_[i]) ? forced_util_[i]
+                                           : mock_util(cfg_, devs_[i].hip_id, (mono_ns() - t0_ns_) * 1e-9);
+  for (size_t k = 0; k < pids.size(); ++k)
+    for (const auto& p : cfg_.procs)
+      if (p.pid == pids[k] && p.device == devs_[i].hip_id) {
+        (*out)[k] = occ_value(i, p, util);
+        break;
+      }
+}
+
+void MockBackend::set_occ_series(int dev, const std::vector<double>& values) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (dev < 0 || dev >= static_cast<int>(devs_.size())) return;
+  if (static_cast<int>(occ_series_.size()) <= dev) occ_series_.resize(devs_.size());
+  occ_series_[dev] = values;
+  if (static_cast<int>(occ_reads_.size()) <= dev) occ_reads_.resize(devs_.size(), 0);
+  occ_reads_[dev] = 0;
+}
+
+uint64_t MockBackend::occ_reads(int dev) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return dev >= 0 && dev < static_cast<int>(occ_reads_.size()) ? occ_reads_[dev] : 0;
 }
 
 void MockBackend::sample_links(int i, DeviceSample* out) {
@@ -346,9 +382,10 @@ void MockBackend::sample_links(int i, DeviceSample* out) {
     char buf[32];
     int peer = (devs_[i].hip_id + k) % std::max(2, cfg_.gpus + 1);
     snprintf(buf, sizeof buf, "0000:%02x:00.0", 0x05 + 0x20 * peer);
-    L.peer_bdf = buf;
-    L.bit_rate_gbps = 38;
-    L.max_bandwidth_gbps = 608;
+    const bool down = link_down_[i * kMaxLinks + k] != 0;
+    L.peer_bdf = down ? "" : buf;  // a down link reports no peer (as amdsmi does)
+    L.bit_rate_gbps = down ? kNaN : 38;
+    L.max_bandwidth_gbps = down ? kNaN : 608;
     L.link_type = 2;
   }
   if (nl > out->n_links) out->n_links = nl;

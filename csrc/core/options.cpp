@@ -221,6 +221,8 @@ const std::map<std::string, Setter>& setters() {
       {"processes", bool_at([](NativeOptions* o) { return &o->cfg.processes; })},
       {"link_every", int_at([](NativeOptions* o) { return &o->cfg.link_every; })},
       {"ras_every", int_at([](NativeOptions* o) { return &o->cfg.ras_every; })},
+      {"ras_slices", int_at([](NativeOptions* o) { return &o->cfg.ras_slices; })},
+      {"occ_samples", int_at([](NativeOptions* o) { return &o->cfg.occ_samples; })},
       {"sample_threads", int_at([](NativeOptions* o) { return &o->cfg.sample_threads; })},
       {"device_timeout_s", dbl_at([](NativeOptions* o) { return &o->cfg.device_timeout_s; })},
       {"reinit_after", int_at([](NativeOptions* o) { return &o->cfg.reinit_after; })},
@@ -482,6 +484,8 @@ std::string options_json(const NativeOptions& o) {
   B("processes", c.processes);
   N("link_every", c.link_every);
   N("ras_every", c.ras_every);
+  N("ras_slices", c.ras_slices);
+  N("occ_samples", c.occ_samples);
   N("sample_threads", c.sample_threads);
   N("device_timeout_s", c.device_timeout_s);
   N("reinit_after", c.reinit_after);

@@ -62,9 +62,12 @@ bool RasSysfsReader::list() {
   if (dir_.empty()) return false;
   DIR* d = opendir(dir_.c_str());
   if (!d) return false;
+  has_events_ = has_bad_pages_ = false;
   while (dirent* e = readdir(d)) {
     const std::string f = e->d_name;
-    if (starts_with(f, "aca_")) files_.emplace_back(f.substr(4), f);
+    if (f == "event_state") has_events_ = true;
+    else if (f == "gpu_vram_bad_pages") has_bad_pages_ = true;
+    else if (starts_with(f, "aca_")) files_.emplace_back(f.substr(4), f);
     else if (ends_with(f, "_err_count")) files_.emplace_back(f.substr(0, f.size() - 10), f);
   }
   closedir(d);
@@ -88,6 +91,7 @@ bool RasSysfsReader::read(int slice, int nslices, RasSample* out) {
   RasSample r;
   r.source = "sysfs";
   std::string text;
+  int failed = 0;
   for (size_t k = 0; k < files_.size(); ++k) {
     RasCount c;
     c.block = files_[k].first;
@@ -95,27 +99,34 @@ bool RasSysfsReader::read(int slice, int nslices, RasSample* out) {
     for (const auto& p : cur_.blocks)
       if (p.block == c.block) prev = &p;
     if (mine(k)) {
-      if (read_file(dir_ + "/" + files_[k].second, &text, 4096) && parse_err_count(text, &c)) r.blocks.push_back(c);
-      else if (prev) r.blocks.push_back(*prev);  // transient read failure: keep the last count
+      if (read_file(dir_ + "/" + files_[k].second, &text, 4096) && parse_err_count(text, &c)) {
+        r.blocks.push_back(c);
+      } else {
+        failed++;
+        if (prev) r.blocks.push_back(*prev);  // transient read failure: keep the last count
+      }
     } else if (prev) {
       r.blocks.push_back(*prev);
     }
   }
   if (r.blocks.empty()) return false;
+  // event_state and bad pages: carried from the last reading when not due OR when the read fails
+  // (a failed read must not blank the fatal / poison / bad-page series for a cycle)
+  r.fatal = cur_.fatal;
+  r.poison_created = cur_.poison_created;
+  r.poison_consumed = cur_.poison_consumed;
+  r.bad_pages = cur_.bad_pages;
   const size_t ev = files_.size(), bp = files_.size() + 1;
-  if (mine(ev)) {
+  if (mine(ev) && has_events_) {
     if (read_file(dir_ + "/event_state", &text, 4096)) parse_event_state(text, &r);
-  } else {
-    r.fatal = cur_.fatal;
-    r.poison_created = cur_.poison_created;
-    r.poison_consumed = cur_.poison_consumed;
+    else failed++;
   }
-  if (mine(bp)) {
+  if (mine(bp) && has_bad_pages_) {
     if (read_file(dir_ + "/gpu_vram_bad_pages", &text, 1 << 20)) r.bad_pages = count_bad_pages(text);
-  } else {
-    r.bad_pages = cur_.bad_pages;
+    else failed++;
   }
   r.valid = true;
+  r.stale_items = failed;
   cur_ = r;
   *out = std::move(r);
   return true;

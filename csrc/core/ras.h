@@ -41,7 +41,8 @@ bool read_ras_sysfs(const std::string& sys_root, const std::string& bdf, RasSamp
 class RasSysfsReader {
  public:
   RasSysfsReader(const std::string& sys_root, const std::string& bdf);
-  // false (out untouched) when the directory has no error-count files.
+  // false (out untouched) when the directory has no error-count files. A due file that fails to
+  // read keeps its last value and counts in out->stale_items (the caller reports the call failed).
   bool read(int slice, int nslices, RasSample* out);
   int items() const { return static_cast<int>(files_.size()) + 2; }  // + event_state, bad pages
 
@@ -50,6 +51,7 @@ class RasSysfsReader {
   std::string dir_;
   bool listed_ = false;
   std::vector<std::pair<std::string, std::string>> files_;  // (block, file), one per block
+  bool has_events_ = false, has_bad_pages_ = false;         // listed at the last directory scan
   RasSample cur_;
 };
 

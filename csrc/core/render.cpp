@@ -384,8 +384,9 @@ void render_prometheus(const RenderInput& in, std::string* o) {
            return has(g) ? g * 1e9 : kNaN;
          });
     devf("gpu_cu_occupancy_percent",
-         "Share of the GPU's compute units holding waves of any process, in percent (KFD cu_occupancy summed "
-         "over processes, capped at 100; the per-process split is pod_gpu_proc_cu_occupancy_percent).",
+         "Resident waves of every process as a share of the GPU's wave slots, in percent (KFD cu_occupancy = "
+         "waves / max waves per CU, summed over processes, interval mean of occ_samples reads, capped at 100; "
+         "the per-process split is pod_gpu_proc_cu_occupancy_percent).",
          "gauge", [&](size_t d) {
            const double cu = sm[d].v[F_CU_OCC];
            const int n_cu = st[d].num_cu;
@@ -522,21 +523,26 @@ void render_prometheus(const RenderInput& in, std::string* o) {
     }
     {
       Family f(o, "pod_gpu_proc_gfx_util",
-               "Per-process GFX engine utilization in percent over the sampling interval (DRM fdinfo "
-               "engine time: graphics/kernel-queue work; HIP compute on KFD user queues shows in "
-               "pod_gpu_proc_cu_occupancy_percent instead).",
+               "Per-process GPU busy percent over the sampling interval: DRM fdinfo gfx engine time when the "
+               "process submits through the kernel (graphics); for HIP compute on KFD user queues, the share of "
+               "the interval's cu_occupancy reads that found the process's waves resident.",
                "gauge");
       for (size_t r = 0; r < rows.size(); ++r) f.add(rl[r], rows[r].proc_gfx_util);
     }
     {
-      Family f(o, "pod_gpu_proc_cu_occupancy", "Compute units occupied by the process's waves (KFD).", "gauge");
+      Family f(o, "pod_gpu_proc_cu_occupancy",
+               "The process's resident waves in CU-equivalents (KFD cu_occupancy = waves / max waves per CU; "
+               "interval mean of occ_samples reads).",
+               "gauge");
       for (size_t r = 0; r < rows.size(); ++r) f.add(rl[r], rows[r].cu_occupancy);
     }
     {
-      // The per-process utilisation signal for HIP compute: CUs holding the process's waves / CUs
-      // on the device (256 on MI355X, measured 256 under the bf16 burn).
+      // Per-process wave occupancy: the process's resident waves / the device's wave slots (KFD
+      // counts waves / max waves per CU; 243 of 256 on MI355X under the saturating bf16 burn,
+      // 7.7 under a 64-workgroup load, profiles/r2_kfd_occupancy.md).
       Family f(o, "pod_gpu_proc_cu_occupancy_percent",
-               "Share of the GPU's compute units occupied by the process's waves, in percent.", "gauge");
+               "The process's resident waves as a share of the GPU's wave slots, in percent (interval mean).",
+               "gauge");
       for (size_t r = 0; r < rows.size(); ++r) {
         const int dev = rows[r].dev;
         const int cus = dev >= 0 && dev < static_cast<int>(in.statics->size()) ? (*in.statics)[dev].num_cu : 0;
@@ -652,6 +658,12 @@ void render_prometheus(const RenderInput& in, std::string* o) {
                "Device samples whose firmware table had not advanced since the previous tick.",
                "counter");
       f.add(hl, static_cast<double>(s.stale_samples));
+    }
+    {
+      Family f(o, "gpumon_occupancy_reads_total",
+               "KFD cu_occupancy reads made between ticks by the device workers (occ_samples per tick).",
+               "counter");
+      f.add(hl, static_cast<double>(s.occupancy_reads));
     }
     {
       Family f(o, "gpumon_tick_overruns_total", "Ticks that took longer than the interval.",

@@ -34,6 +34,7 @@ struct PodRow {
   double gpu_util = 0;              // device-wide util (reference semantics, Q4)
   double proc_gfx_util = kNaN;      // true per-process util from engine_usage.gfx ns
   double cu_occupancy = kNaN;
+  int occ_samples = 0;  // cu_occupancy reads behind the interval mean
   std::vector<std::pair<std::string, std::string>> extra_labels;  // allowlisted pod labels (label_<key>)
 };
 
@@ -56,6 +57,7 @@ struct SelfStats {
   uint64_t ticks = 0;
   uint64_t samples = 0;
   uint64_t stale_samples = 0;
+  uint64_t occupancy_reads = 0;     // KFD cu_occupancy sub-sample reads by the device workers
   uint64_t overruns = 0;
   double last_tick_wall_s = 0;
   double interval_s = 1.0;

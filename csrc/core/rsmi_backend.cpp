@@ -180,6 +180,7 @@ bool RocmSmiBackend::init(std::string* err) {
              "loaded " + t_->path + " version=" + lib_version_ + " gpus=" + std::to_string(devs_.size()));
   ras_readers_.clear();
   ras_readers_.resize(devs_.size());
+  ras_missing_.assign(devs_.size(), 0);
   return true;
 }
 
@@ -262,10 +263,16 @@ bool RocmSmiBackend::processes(int i, std::vector<ProcSample>* out) {
 
 void RocmSmiBackend::sample_ras(int i, DeviceSample* out, int slice, int nslices) {
   if (i < 0 || i >= static_cast<int>(devs_.size())) return;
+  if (i < static_cast<int>(ras_missing_.size()) && ras_missing_[i]) return;  // no ras/ files on this node
   if (!ras_readers_[i]) ras_readers_[i] = std::make_unique<RasSysfsReader>(sys_root_, devs_[i].bdf);
   const int64_t t0 = mono_ns();
   const bool ok = ras_readers_[i]->read(slice, nslices, &out->ras);
-  record_call(kCallRas, mono_ns() - t0, ok);
+  if (!ok) {
+    // no error-count files (VM guest, RAS disabled) or none readable: stop re-listing the
+    // directory every tick (the amdsmi backend's caps.ras_sysfs does the same)
+    if (i < static_cast<int>(ras_missing_.size())) ras_missing_[i] = 1;
+  }
+  record_call(kCallRas, mono_ns() - t0, ok && out->ras.stale_items == 0);
 }
 
 }  // namespace gpumon

@@ -145,6 +145,7 @@ struct RasSample {
   std::vector<RasCount> blocks;
   double fatal = kNaN, poison_created = kNaN, poison_consumed = kNaN;  // ras/event_state counts
   double bad_pages = kNaN; // retired / pending VRAM pages (ras/gpu_vram_bad_pages entries)
+  int stale_items = 0;     // files due in this read that failed (their last values are carried)
 };
 
 struct DeviceSample {
@@ -193,7 +194,12 @@ struct ProcSample {
   double mem_bytes = kNaN;
   uint64_t gfx_ns = 0;          // accumulated gfx engine time
   bool has_gfx_ns = false;
+  // KFD stats_<gpu>/cu_occupancy: the process's resident waves / max waves per CU ("CU-equivalents
+  // of waves"; 256 = every wave slot of an MI355X held). Instantaneous when read once; the device
+  // worker also reads it `occ_samples - 1` more times between ticks and stores the interval mean.
   double cu_occupancy = kNaN;
+  int occ_samples = 0;          // reads behind cu_occupancy (0 = none)
+  int occ_busy = 0;             // of those, reads with waves resident (> 0): the process's busy share
 };
 
 // Derived per-device values computed from two consecutive samples.

@@ -189,6 +189,19 @@ void SysfsGpu::fdinfo_usage(uint32_t pid, ProcSample* p) {
   }
 }
 
+void SysfsGpu::occupancy(const std::vector<uint32_t>& pids, std::vector<double>* out) {
+  out->assign(pids.size(), kNaN);
+  if (!kfd_gpu_id_) return;
+  const std::string tail = "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy";
+  const std::string kdir = sys_root_ + "/class/kfd/kfd/proc/";
+  char b[64];
+  for (size_t k = 0; k < pids.size(); ++k) {
+    size_t n = 0;
+    if (read_small(kdir + std::to_string(pids[k]) + tail, b, sizeof b, &n))
+      (*out)[k] = static_cast<double>(strtoull(b, nullptr, 10));
+  }
+}
+
 bool SysfsGpu::processes(std::vector<ProcSample>* out) {
   out->clear();
   if (!kfd_gpu_id_) return false;

@@ -192,6 +192,8 @@ class SysfsGpu {
   bool read_gtt(double* used_bytes);
   // Compute processes with memory on this GPU (KFD), plus DRM fdinfo gfx engine time / memory.
   bool processes(std::vector<ProcSample>* out);
+  // Instantaneous KFD cu_occupancy of each pid on this GPU (NaN where the file is unreadable).
+  void occupancy(const std::vector<uint32_t>& pids, std::vector<double>* out);
   bool have_kfd() const { return kfd_gpu_id_ != 0; }
 
  private:

@@ -7,7 +7,10 @@
 //   GPUMON_FAKE_MFMA        MFMA busy fraction 0..1 (default 0.5), spread evenly over 8 XCCs
 //   GPUMON_FAKE_OCC         occupancy fraction 0..1 (default 0.25)
 //   GPUMON_FAKE_TFLOPS      bf16 MFMA TFLOP/s (default 1000; f16 at a tenth, other types 0)
-//   GPUMON_FAKE_PMC_FAIL    "init" -> init fails; "sample" -> every sample reports not-ok
+//   GPUMON_FAKE_PMC_FAIL    "init" -> init fails; "sample" -> every sample reports not-ok;
+//                           "start" -> continuous counting cannot start (counters held elsewhere)
+//   GPUMON_FAKE_PMC_READ    continuous reads: "cumulative" (default: values since the start) or
+//                           "reset" (values since the previous read)
 //   GPUMON_FAKE_PROBE_HANG  1 -> launches never complete (timeouts path)
 #include <cstdio>
 #include <cstdlib>
@@ -77,14 +80,10 @@ EXPORT size_t gpumon_pmc_dimensions(int, const char*, char* buf, size_t n) {
   return strlen(s) + 1;
 }
 
-EXPORT int gpumon_pmc_sample_many(const int* ags, int n_agents, const char* const* counters, int n_counters,
-                                  double window_s, gpumon_pmc_value_t* out, int32_t* ok, char* err, size_t errlen) {
-  for (int k = 0; k < n_agents; ++k)
-    if (ags[k] < 0 || ags[k] >= agents()) {
-      snprintf(err, errlen, "pmc agent index");
-      return -1;
-    }
-  std::this_thread::sleep_for(std::chrono::duration<double>(window_s));
+namespace {
+// Values of `counters` for a counting span of window_s seconds (both sampling modes use it).
+int fill(int n_agents, const char* const* counters, int n_counters, double window_s, gpumon_pmc_value_t* out,
+         int32_t* ok, char* err, size_t errlen) {
   const double gui = window_s * kClock;
   for (int k = 0; k < n_agents; ++k) {
     ok[k] = fail("sample") ? 0 : 1;
@@ -126,6 +125,50 @@ EXPORT int gpumon_pmc_sample_many(const int* ags, int n_agents, const char* cons
   }
   return 0;
 }
+
+bool g_running = false;
+std::chrono::steady_clock::time_point g_t0, g_last;
+}  // namespace
+
+EXPORT int gpumon_pmc_sample_many(const int* ags, int n_agents, const char* const* counters, int n_counters,
+                                  double window_s, gpumon_pmc_value_t* out, int32_t* ok, char* err, size_t errlen) {
+  for (int k = 0; k < n_agents; ++k)
+    if (ags[k] < 0 || ags[k] >= agents()) {
+      snprintf(err, errlen, "pmc agent index");
+      return -1;
+    }
+  g_running = false;
+  std::this_thread::sleep_for(std::chrono::duration<double>(window_s));
+  return fill(n_agents, counters, n_counters, window_s, out, ok, err, errlen);
+}
+
+EXPORT int gpumon_pmc_read_running(const int* ags, int n_agents, const char* const* counters, int n_counters,
+                                   gpumon_pmc_value_t* out, int32_t* ok, int32_t* started, char* err, size_t errlen) {
+  for (int k = 0; k < n_agents; ++k)
+    if (ags[k] < 0 || ags[k] >= agents()) {
+      snprintf(err, errlen, "pmc agent index");
+      return -1;
+    }
+  const auto now = std::chrono::steady_clock::now();
+  if (started) *started = 0;
+  if (!g_running) {
+    if (fail("start")) {
+      snprintf(err, errlen, "pmc read: start_context failed on agent %d (another profiler holds the device counters?)",
+               ags[0]);
+      return -1;
+    }
+    g_running = true;
+    g_t0 = g_last = now;
+    if (started) *started = 1;
+  }
+  const char* mode = getenv("GPUMON_FAKE_PMC_READ");
+  const bool reset = mode && strcmp(mode, "reset") == 0;
+  const double span = std::chrono::duration<double>(now - (reset ? g_last : g_t0)).count();
+  g_last = now;
+  return fill(n_agents, counters, n_counters, span, out, ok, err, errlen);
+}
+
+EXPORT void gpumon_pmc_stop_running(void) { g_running = false; }
 
 // ---- probe ----------------------------------------------------------------------------------
 struct gpumon_probe {

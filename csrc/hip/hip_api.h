@@ -44,11 +44,15 @@ struct LoadStats {
   double bytes = 0;         // HBM bytes moved (read + write)
   double mfma_s = 0;        // GPU time of MFMA batches
   double hbm_s = 0;         // GPU time of HBM-stream batches
+  double wall_s = 0;        // wall time since start() (rates over wall time = flops / wall_s)
 };
 
 class LoadGen {
  public:
-  // kind: "mfma" | "hbm" | "mixed" ; duty in (0, 1]: fraction of wall time the GPU is kept busy
+  // kind: "mfma" | "hbm" | "mixed" (alternating MFMA / HBM batches on one stream) | "concurrent"
+  // (MFMA burn and HBM stream on two streams at the same time: both pipes loaded at once, the
+  // power/thermal worst case) | "partial" (a quarter of the CUs burning);
+  // duty in (0, 1]: fraction of wall time the GPU is kept busy
   LoadGen(int dev, std::string kind, double duty, size_t hbm_bytes, int mfma_iters);
   ~LoadGen();
   void start();
@@ -59,29 +63,71 @@ class LoadGen {
   // bf16 (the shape above) or a launch_mfma_burn_dtype path: f16 fp8 f32 f64 i8 mxfp8 mxfp4; before start()
   void set_mfma_dtype(std::string dtype) { dtype_ = std::move(dtype); }
   int mfma_shape() const { return shape_; }
+  // > 0: duty cycle as long bursts, duty * period_s busy then (1 - duty) * period_s idle (step /
+  // communication phases), instead of an idle gap after every batch; before start()
+  void set_period(double period_s) { period_s_ = period_s; }
 
  private:
-  void loop();
+  void loop(bool alternate, bool mfma, void* stream);
   int dev_;
   std::string kind_;
   double duty_;
   size_t bytes_;
   int iters_;
   int shape_ = 32;
+  double period_s_ = 0;
   std::string dtype_ = "bf16";
   void* stream_ = nullptr;
+  void* stream2_ = nullptr;  // "concurrent": the HBM stream's own HIP stream
   void* a_ = nullptr;
   void* b_ = nullptr;
   float* out_ = nullptr;
   void* src_ = nullptr;
   void* dst_ = nullptr;
-  std::thread th_;
+  std::thread th_, th2_;
   std::atomic<bool> running_{false};
+  int64_t t_start_ns_ = 0;
   mutable std::atomic<uint64_t> launches_{0};
   std::atomic<uint64_t> busy_ns_{0};
   std::atomic<uint64_t> flops_{0};
   std::atomic<uint64_t> bytes_moved_{0};
   std::atomic<uint64_t> mfma_ns_{0}, hbm_ns_{0};
+  std::string err_;
+};
+
+// --- xGMI load: one GPU pushes to one peer (drives exactly the link between them) ---------------
+struct XgmiStats {
+  uint64_t copies = 0;
+  double bytes = 0;    // bytes that crossed the link
+  double busy_s = 0;   // event-timed GPU time of the copies
+  double wall_s = 0;   // since start()
+};
+
+class XgmiLoad {
+ public:
+  // method "kernel": a copy kernel on `src` reads local HBM and stores into `dst`'s memory through
+  //                  the peer mapping (the store stream crosses the src->dst xGMI link);
+  //        "dma":    hipMemcpyPeerAsync on a src-device stream.
+  XgmiLoad(int src, int dst, size_t bytes, std::string method, int blocks);
+  ~XgmiLoad();
+  void start();
+  void stop();
+  XgmiStats stats() const;
+  bool running() const { return running_; }
+
+ private:
+  void loop();
+  int src_, dst_;
+  size_t bytes_;
+  std::string method_;
+  int blocks_;
+  void* stream_ = nullptr;
+  void* sbuf_ = nullptr;  // on src
+  void* dbuf_ = nullptr;  // on dst
+  std::thread th_;
+  std::atomic<bool> running_{false};
+  int64_t t_start_ns_ = 0;
+  std::atomic<uint64_t> copies_{0}, bytes_moved_{0}, busy_ns_{0};
   std::string err_;
 };
 

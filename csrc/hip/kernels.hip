@@ -322,8 +322,8 @@ void launch_stream_triad(int dev, const float* a, const float* b, float* c, floa
 // ---------------------------------------------------------------------------------------------
 LoadGen::LoadGen(int dev, std::string kind, double duty, size_t hbm_bytes, int mfma_iters)
     : dev_(dev), kind_(std::move(kind)), duty_(std::clamp(duty, 0.01, 1.0)), bytes_(hbm_bytes), iters_(mfma_iters) {
-  if (kind_ != "mfma" && kind_ != "hbm" && kind_ != "mixed" && kind_ != "partial")
-    throw std::invalid_argument("LoadGen kind must be mfma | hbm | mixed | partial");
+  if (kind_ != "mfma" && kind_ != "hbm" && kind_ != "mixed" && kind_ != "partial" && kind_ != "concurrent")
+    throw std::invalid_argument("LoadGen kind must be mfma | hbm | mixed | concurrent | partial");
   bytes_ = std::max<size_t>(bytes_ / 16 * 16, 1 << 20);
 }
 
@@ -335,6 +335,11 @@ void LoadGen::start() {
   hipStream_t s;
   check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   stream_ = s;
+  if (kind_ == "concurrent") {
+    hipStream_t s2;
+    check(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking), "hipStreamCreate");
+    stream2_ = s2;
+  }
   // bf16 operand tile with non-trivial values (keeps the MFMA datapath toggling: realistic power)
   std::vector<uint16_t> h(32 * 16 + 16 * 32);
   for (size_t i = 0; i < h.size(); ++i) {
@@ -347,20 +352,27 @@ void LoadGen::start() {
   b_ = static_cast<char*>(a_) + 32 * 16 * 2;
   check(hipMemcpy(a_, h.data(), h.size() * 2, hipMemcpyHostToDevice), "hipMemcpy");
   check(hipMalloc(reinterpret_cast<void**>(&out_), 4096 * 4 * sizeof(float)), "hipMalloc");
-  if (kind_ == "hbm" || kind_ == "mixed") {
+  if (kind_ == "hbm" || kind_ == "mixed" || kind_ == "concurrent") {
     check(hipMalloc(&src_, bytes_), "hipMalloc");
     check(hipMalloc(&dst_, bytes_), "hipMalloc");
     check(hipMemsetAsync(src_, 1, bytes_, s), "hipMemset");
     check(hipStreamSynchronize(s), "hipStreamSynchronize");
   }
   running_ = true;
-  th_ = std::thread([this] { loop(); });
+  t_start_ns_ = mono_ns();
+  if (kind_ == "concurrent") {  // two host threads, two streams: both kernels resident at once
+    th_ = std::thread([this] { loop(false, true, stream_); });
+    th2_ = std::thread([this] { loop(false, false, stream2_); });
+  } else {
+    th_ = std::thread([this] { loop(kind_ == "mixed", kind_ != "hbm", stream_); });
+  }
 }
 
-void LoadGen::loop() {
+// alternate: flip MFMA / HBM per batch ("mixed"); otherwise `mfma` picks the one kernel kind.
+void LoadGen::loop(bool alternate, bool mfma, void* stream) {
   try {
     check(hipSetDevice(dev_), "hipSetDevice");
-    hipStream_t s = static_cast<hipStream_t>(stream_);
+    hipStream_t s = static_cast<hipStream_t>(stream);
     hipEvent_t e0, e1;
     check(hipEventCreate(&e0), "hipEventCreate");
     check(hipEventCreate(&e1), "hipEventCreate");
@@ -376,7 +388,7 @@ void LoadGen::loop() {
     bool flip = false;
     while (running_) {
       // one kind per batch so the event time is attributed to exactly one kernel kind
-      const bool do_mfma = kind_ == "mfma" || kind_ == "partial" || (kind_ == "mixed" && !flip);
+      const bool do_mfma = alternate ? !flip : mfma;
       flip = !flip;
       check(hipEventRecord(e0, s), "hipEventRecord");
       double fl = 0, by = 0;
@@ -400,7 +412,16 @@ void LoadGen::loop() {
       (do_mfma ? mfma_ns_ : hbm_ns_) += static_cast<uint64_t>(ms * 1e6);
       flops_ += static_cast<uint64_t>(fl);
       bytes_moved_ += static_cast<uint64_t>(by);
-      if (duty_ < 0.999) {
+      if (duty_ < 0.999 && period_s_ > 0) {
+        // burst pattern: busy until duty * period into the period, then idle to its end
+        const int64_t now = mono_ns();
+        const int64_t per = static_cast<int64_t>(period_s_ * 1e9);
+        const int64_t phase = (now - t_start_ns_) % per;
+        if (phase >= static_cast<int64_t>(duty_ * per)) {
+          const int64_t until_ns = now + (per - phase);
+          while (running_ && mono_ns() < until_ns) std::this_thread::sleep_for(std::chrono::microseconds(500));
+        }
+      } else if (duty_ < 0.999) {
         double idle_ms = ms * (1.0 / duty_ - 1.0);
         auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(static_cast<int64_t>(idle_ms * 1e3));
         while (running_ && std::chrono::steady_clock::now() < until)
@@ -416,16 +437,16 @@ void LoadGen::loop() {
 }
 
 void LoadGen::stop() {
-  if (th_.joinable()) {
-    running_ = false;
-    th_.join();
-  }
   running_ = false;
-  if (stream_) {
-    (void)hipSetDevice(dev_);
-    (void)hipStreamSynchronize(static_cast<hipStream_t>(stream_));
-    (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
-    stream_ = nullptr;
+  if (th_.joinable()) th_.join();
+  if (th2_.joinable()) th2_.join();
+  (void)hipSetDevice(dev_);
+  for (void** sp : {&stream_, &stream2_}) {
+    if (*sp) {
+      (void)hipStreamSynchronize(static_cast<hipStream_t>(*sp));
+      (void)hipStreamDestroy(static_cast<hipStream_t>(*sp));
+      *sp = nullptr;
+    }
   }
   if (a_) (void)hipFree(a_);
   if (out_) (void)hipFree(out_);
@@ -444,7 +465,104 @@ LoadStats LoadGen::stats() const {
   s.bytes = static_cast<double>(bytes_moved_.load());
   s.mfma_s = mfma_ns_ * 1e-9;
   s.hbm_s = hbm_ns_ * 1e-9;
+  s.wall_s = t_start_ns_ ? (mono_ns() - t_start_ns_) * 1e-9 : 0.0;
   return s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// XgmiLoad: src GPU pushes a buffer into dst GPU memory, back to back, on one src stream.
+// ---------------------------------------------------------------------------------------------
+XgmiLoad::XgmiLoad(int src, int dst, size_t bytes, std::string method, int blocks)
+    : src_(src), dst_(dst), bytes_(std::max<size_t>(bytes / 4096 * 4096, 1 << 20)), method_(std::move(method)),
+      blocks_(std::clamp(blocks, 1, 65535)) {
+  if (method_ != "kernel" && method_ != "dma") throw std::invalid_argument("XgmiLoad method must be kernel | dma");
+  if (src_ == dst_) throw std::invalid_argument("XgmiLoad: src and dst must differ");
+  const int n = device_count();
+  if (src_ < 0 || dst_ < 0 || src_ >= n || dst_ >= n) throw std::invalid_argument("XgmiLoad: device out of range");
+}
+
+XgmiLoad::~XgmiLoad() { stop(); }
+
+void XgmiLoad::start() {
+  if (running_) return;
+  int can = 0;
+  check(hipDeviceCanAccessPeer(&can, src_, dst_), "hipDeviceCanAccessPeer");
+  if (!can) throw std::runtime_error("XgmiLoad: device " + std::to_string(src_) + " cannot access peer " +
+                                     std::to_string(dst_));
+  check(hipSetDevice(dst_), "hipSetDevice");
+  check(hipMalloc(&dbuf_, bytes_), "hipMalloc(dst)");
+  check(hipSetDevice(src_), "hipSetDevice");
+  const hipError_t pe = hipDeviceEnablePeerAccess(dst_, 0);
+  if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) check(pe, "hipDeviceEnablePeerAccess");
+  (void)hipGetLastError();  // clear a sticky "already enabled"
+  hipStream_t s;
+  check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  stream_ = s;
+  check(hipMalloc(&sbuf_, bytes_), "hipMalloc(src)");
+  check(hipMemsetAsync(sbuf_, 3, bytes_, s), "hipMemset");
+  check(hipStreamSynchronize(s), "hipStreamSynchronize");
+  running_ = true;
+  t_start_ns_ = mono_ns();
+  th_ = std::thread([this] { loop(); });
+}
+
+void XgmiLoad::loop() {
+  try {
+    check(hipSetDevice(src_), "hipSetDevice");
+    hipStream_t s = static_cast<hipStream_t>(stream_);
+    hipEvent_t e0, e1;
+    check(hipEventCreate(&e0), "hipEventCreate");
+    check(hipEventCreate(&e1), "hipEventCreate");
+    while (running_) {
+      check(hipEventRecord(e0, s), "hipEventRecord");
+      for (int k = 0; k < 4; ++k) {
+        if (method_ == "dma") check(hipMemcpyPeerAsync(dbuf_, dst_, sbuf_, src_, bytes_, s), "hipMemcpyPeerAsync");
+        else launch_stream_copy(src_, sbuf_, dbuf_, bytes_ / 16, blocks_, s, 4, 1, false);  // plain ld / st
+      }
+      check(hipEventRecord(e1, s), "hipEventRecord");
+      check(hipEventSynchronize(e1), "hipEventSynchronize");
+      float ms = 0;
+      check(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
+      busy_ns_ += static_cast<uint64_t>(ms * 1e6);
+      copies_ += 4;
+      bytes_moved_ += 4 * static_cast<uint64_t>(bytes_);
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+  } catch (const std::exception& e) {
+    err_ = e.what();
+    running_ = false;
+  }
+}
+
+void XgmiLoad::stop() {
+  running_ = false;
+  if (th_.joinable()) th_.join();
+  if (stream_) {
+    (void)hipSetDevice(src_);
+    (void)hipStreamSynchronize(static_cast<hipStream_t>(stream_));
+    (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
+    stream_ = nullptr;
+  }
+  if (sbuf_) {
+    (void)hipSetDevice(src_);
+    (void)hipFree(sbuf_);
+  }
+  if (dbuf_) {
+    (void)hipSetDevice(dst_);
+    (void)hipFree(dbuf_);
+  }
+  sbuf_ = dbuf_ = nullptr;
+}
+
+XgmiStats XgmiLoad::stats() const {
+  if (!err_.empty()) throw std::runtime_error("XgmiLoad failed: " + err_);
+  XgmiStats st;
+  st.copies = copies_;
+  st.bytes = static_cast<double>(bytes_moved_.load());
+  st.busy_s = busy_ns_ * 1e-9;
+  st.wall_s = t_start_ns_ ? (mono_ns() - t_start_ns_) * 1e-9 : 0.0;
+  return st;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define GPUMON_ONDEVICE_ABI 2  // 2: gpumon_probe_result_t.stale_records + xcc_wave_slot
+#define GPUMON_ONDEVICE_ABI 3  // 2: gpumon_probe_result_t.stale_records + xcc_wave_slot; 3: continuous PMC reads
 #define GPUMON_PMC_MAX_XCC 16
 
 // ---- PMC (libgpumon_pmc.so) --------------------------------------------------------------------
@@ -58,6 +58,12 @@ size_t gpumon_pmc_dimensions(int agent, const char* counter, char* buf, size_t b
 // agent index; nothing was sampled).
 int gpumon_pmc_sample_many(const int* agents, int n_agents, const char* const* counters, int n_counters,
                            double window_s, gpumon_pmc_value_t* out, int32_t* ok, char* err, size_t errlen);
+// Continuous counting: the contexts stay started between calls, each call reads them without a
+// stop (no uncounted gap between reads). The first call, or one with a different request, (re)starts
+// them and sets *started = 1. A gpumon_pmc_sample_many call ends continuous counting.
+int gpumon_pmc_read_running(const int* agents, int n_agents, const char* const* counters, int n_counters,
+                            gpumon_pmc_value_t* out, int32_t* ok, int32_t* started, char* err, size_t errlen);
+void gpumon_pmc_stop_running(void);
 
 // ---- K1 probe (libgpumon_probe.so) -------------------------------------------------------------
 typedef struct gpumon_probe gpumon_probe;

@@ -53,6 +53,15 @@ std::string g_err;
 bool g_configured = false;
 bool g_hsa = false;
 
+// Continuous counting (gpumon_pmc_read_running): contexts left started between reads. Guarded by
+// g_sample, like every start/stop/read.
+struct Running {
+  std::vector<int> agents;
+  std::vector<std::string> counters;
+  bool on = false;
+};
+Running g_run;
+
 std::string st_str(rocprofiler_status_t s) { return rocprofiler_get_status_string(s); }
 
 void check(rocprofiler_status_t s, const char* what) {
@@ -198,6 +207,14 @@ void reduce(const Agent& A, const std::vector<rocprofiler_counter_record_t>& rec
   }
 }
 
+// caller holds g_sample
+void stop_running_locked() {
+  if (!g_run.on) return;
+  for (int a : g_run.agents)
+    if (a >= 0 && a < static_cast<int>(g_agents.size())) rocprofiler_stop_context(g_agents[a]->ctx);
+  g_run = Running{};
+}
+
 size_t copy_out(const std::string& s, char* buf, size_t n) {
   if (buf && n) snprintf(buf, n, "%s", s.c_str());
   return s.size() + 1;
@@ -289,6 +306,7 @@ GPUMON_EXPORT int gpumon_pmc_sample_many(const int* agents, int n_agents, const 
   }
   std::vector<std::string> names(counters, counters + n_counters);
   std::lock_guard<std::mutex> sg(g_sample);
+  stop_running_locked();  // a windowed sample owns the contexts: continuous counting ends here
   std::vector<Agent*> As(n_agents, nullptr);
   std::vector<std::vector<rocprofiler_counter_record_t>> recs(n_agents);
   try {
@@ -318,4 +336,65 @@ GPUMON_EXPORT int gpumon_pmc_sample_many(const int* agents, int n_agents, const 
       for (int c = 0; c < n_counters; ++c) out[static_cast<size_t>(k) * n_counters + c] = gpumon_pmc_value_t{};
   }
   return 0;
+}
+
+// Continuous counting: the first call starts the contexts of `agents` with `counters`; later calls
+// with the same request read them WITHOUT stopping, so no interval goes uncounted between reads.
+// A different request (agents or counters) restarts the contexts. Every read returns the service's
+// raw values for the running context; the caller works out the interval values (the service's
+// read semantics on MI355X are measured in profiles/r2_pmc_continuous.md). *started = 1 when this
+// call (re)started the contexts (its values cover only the instant since the start).
+GPUMON_EXPORT int gpumon_pmc_read_running(const int* agents, int n_agents, const char* const* counters,
+                                          int n_counters, gpumon_pmc_value_t* out, int32_t* ok, int32_t* started,
+                                          char* err, size_t errlen) {
+  if (n_agents <= 0 || n_counters <= 0 || !agents || !counters || !out || !ok) {
+    set_err(err, errlen, "pmc read: empty request");
+    return -1;
+  }
+  std::vector<int> ag(agents, agents + n_agents);
+  std::vector<std::string> names(counters, counters + n_counters);
+  std::lock_guard<std::mutex> sg(g_sample);
+  if (g_run.on && (g_run.agents != ag || g_run.counters != names)) stop_running_locked();
+  std::vector<Agent*> As(n_agents, nullptr);
+  std::vector<std::vector<rocprofiler_counter_record_t>> recs(n_agents);
+  try {
+    for (int k = 0; k < n_agents; ++k) recs[k].resize(std::max<size_t>(prepare(agents[k], names, &As[k]), 1));
+  } catch (const std::exception& e) {
+    set_err(err, errlen, e.what());
+    return -1;
+  }
+  if (started) *started = 0;
+  if (!g_run.on) {
+    int k = 0;
+    for (; k < n_agents; ++k)
+      if (rocprofiler_start_context(As[k]->ctx) != ROCPROFILER_STATUS_SUCCESS) break;
+    if (k < n_agents) {
+      for (int j = 0; j < k; ++j) rocprofiler_stop_context(As[j]->ctx);
+      set_err(err, errlen, "pmc read: start_context failed on agent " + std::to_string(agents[k]) +
+                               " (another profiler holds the device counters?)");
+      return -1;
+    }
+    g_run.agents = ag;
+    g_run.counters = names;
+    g_run.on = true;
+    if (started) *started = 1;
+  }
+  for (int k = 0; k < n_agents; ++k) {
+    ok[k] = 0;
+    size_t cnt = recs[k].size();
+    if (rocprofiler_sample_device_counting_service(As[k]->ctx, {}, ROCPROFILER_COUNTER_FLAG_NONE, recs[k].data(),
+                                                   &cnt) == ROCPROFILER_STATUS_SUCCESS) {
+      recs[k].resize(cnt);
+      ok[k] = 1;
+      reduce(*As[k], recs[k], names, out + static_cast<size_t>(k) * n_counters);
+    } else {
+      for (int c = 0; c < n_counters; ++c) out[static_cast<size_t>(k) * n_counters + c] = gpumon_pmc_value_t{};
+    }
+  }
+  return 0;
+}
+
+GPUMON_EXPORT void gpumon_pmc_stop_running(void) {
+  std::lock_guard<std::mutex> sg(g_sample);
+  stop_running_locked();
 }

@@ -67,6 +67,31 @@ py::list sample_many(const std::vector<int>& agents, const std::vector<std::stri
   return out;
 }
 
+py::dict read_running(const std::vector<int>& agents, const std::vector<std::string>& counters) {
+  std::vector<const char*> cn;
+  for (const auto& c : counters) cn.push_back(c.c_str());
+  std::vector<gpumon_pmc_value_t> vals(agents.size() * counters.size());
+  std::vector<int32_t> ok(agents.size(), 0);
+  int32_t started = 0;
+  char err[512] = {0};
+  int rc;
+  {
+    py::gil_scoped_release nogil;
+    rc = gpumon_pmc_read_running(agents.data(), static_cast<int>(agents.size()), cn.data(),
+                                 static_cast<int>(cn.size()), vals.data(), ok.data(), &started, err, sizeof err);
+  }
+  if (rc != 0) throw std::runtime_error(err);
+  py::list per;
+  for (size_t k = 0; k < agents.size(); ++k) {
+    if (!ok[k]) per.append(py::none());
+    else per.append(to_dict(counters, vals.data() + k * counters.size()));
+  }
+  py::dict d;
+  d["started"] = started != 0;
+  d["agents"] = per;
+  return d;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_pmc, m) {
@@ -128,6 +153,12 @@ PYBIND11_MODULE(_pmc, m) {
       },
       py::arg("agent"), py::arg("counters"), py::arg("window_s") = 0.1);
 
+  m.def("read_running", &read_running, py::arg("agents"), py::arg("counters"),
+        "continuous counting: read running contexts without stopping them ({'started', 'agents'})");
+  m.def("stop_running", []() {
+    py::gil_scoped_release nogil;
+    gpumon_pmc_stop_running();
+  });
   m.def("sample_many", &sample_many, py::arg("agents"), py::arg("counters"), py::arg("window_s") = 0.1,
         "sample() for several agents over one shared window; None for an agent that failed");
 }

@@ -208,7 +208,7 @@ def cmd_probe(args) -> int:
 def cmd_load(args) -> int:
     from .ops.load import SyntheticLoad
 
-    with SyntheticLoad(args.device, args.kind, duty=args.duty, mfma_dtype=args.dtype) as load:
+    with SyntheticLoad(args.device, args.kind, duty=args.duty, mfma_dtype=args.dtype, period_s=args.period) as load:
         time.sleep(args.seconds)
         print(json.dumps(load.stats()))
     return 0
@@ -283,8 +283,9 @@ def build_parser() -> argparse.ArgumentParser:
     s.set_defaults(fn=cmd_probe)
     s = sub.add_parser("load", help="synthetic gfx950 load")
     s.add_argument("--device", type=int, default=0)
-    s.add_argument("--kind", choices=["mfma", "hbm", "mixed"], default="mixed")
+    s.add_argument("--kind", choices=["mfma", "hbm", "mixed", "concurrent", "partial"], default="mixed")
     s.add_argument("--duty", type=float, default=1.0)
+    s.add_argument("--period", type=float, default=0.0, help="burst period in s (duty = busy fraction of it)")
     s.add_argument("--seconds", type=float, default=10.0)
     s.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8", "f32", "f64", "i8", "mxfp8", "mxfp4"],
                    help="matrix path of the mfma burn")

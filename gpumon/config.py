@@ -38,7 +38,9 @@ class Config:
     interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
     processes: bool = True
     link_every: int = 600                 # ticks between link-metrics refreshes (+ whenever a link's state changes)
-    ras_every: int = 5                    # ticks per full RAS / ECC pass, one slice of the files per tick (0 = off)
+    ras_every: int = 5                    # ticks per full RAS / ECC pass (0 = off)
+    ras_slices: int = 1                   # the pass read in this many slices on consecutive ticks (1..ras_every)
+    occ_samples: int = 10                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
     device_timeout_s: float = 2.0         # a device call still running after this is exported as hung
     reinit_after: int = 5                 # ticks with every GPU failing before the backend is re-initialised
@@ -119,6 +121,8 @@ class Config:
             "processes": self.processes,
             "link_every": int(self.link_every),
             "ras_every": int(self.ras_every),
+            "ras_slices": int(self.ras_slices),
+            "occ_samples": int(self.occ_samples),
             "sample_threads": int(self.sample_threads),
             "device_timeout_s": float(self.device_timeout_s),
             "reinit_after": int(self.reinit_after),

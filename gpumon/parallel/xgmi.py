@@ -35,26 +35,40 @@ def allreduce_busbw(nbytes: int, seconds: float, world: int) -> float:
 
 
 class PeerCopier:
-    def __init__(self, src_dev: int, dst_dev: int, nbytes: int = 1 << 30):
-        import torch
+    """One GPU pushing into one peer's memory, back to back, from a native thread (``_hip.XgmiLoad``:
+    a copy kernel on ``src`` whose stores cross the src->dst xGMI link, or ``method="dma"`` for
+    hipMemcpyPeerAsync). ``run(seconds)`` keeps it running and returns the bytes/s achieved over
+    that window; ``close()`` stops it."""
 
-        self.src = torch.empty(nbytes // 4, dtype=torch.float32, device=f"cuda:{src_dev}")
-        self.dst = torch.empty(nbytes // 4, dtype=torch.float32, device=f"cuda:{dst_dev}")
-        self.nbytes = nbytes
+    def __init__(self, src_dev: int, dst_dev: int, nbytes: int = 256 << 20, method: str = "kernel",
+                 blocks: int = 512):
+        from .._native import hip
+
+        self._g = hip().XgmiLoad(src_dev, dst_dev, nbytes, method, blocks)
+        self.src, self.dst, self.nbytes = src_dev, dst_dev, nbytes
+        self._started = False
+
+    def start(self) -> "PeerCopier":
+        if not self._started:
+            self._g.start()
+            self._started = True
+        return self
+
+    def stats(self) -> dict:
+        return self._g.stats()
 
     def run(self, seconds: float = 1.0) -> float:
-        """Copy repeatedly for ~``seconds``; returns achieved bytes/s."""
-        import torch
+        self.start()
+        s0 = self._g.stats()
+        time.sleep(seconds)
+        s1 = self._g.stats()
+        dt = s1["wall_s"] - s0["wall_s"]
+        return (s1["bytes"] - s0["bytes"]) / dt if dt > 0 else 0.0
 
-        t0 = time.perf_counter()
-        n = 0
-        while time.perf_counter() - t0 < seconds:
-            self.dst.copy_(self.src, non_blocking=True)
-            n += 1
-            if n % 8 == 0:
-                torch.cuda.synchronize(self.src.device)
-        torch.cuda.synchronize(self.src.device)
-        return n * self.nbytes / (time.perf_counter() - t0)
+    def close(self) -> None:
+        if self._started:
+            self._g.stop()
+            self._started = False
 
 
 def make_allreduce_buffer(nbytes: int, device) -> Optional[object]:
@@ -80,37 +94,63 @@ def link_peer_bdf(sample: dict, link: int) -> str:
     return links[link].get("peer_bdf", "") if 0 <= link < len(links) else ""
 
 
+def _median(xs):
+    xs = sorted(xs)
+    return xs[len(xs) // 2] if xs else 0.0
+
+
 def validate_pair(ex, src: int, dst: int, copier_factory=None, seconds: float = 2.0,
                   interval: float = 0.1) -> dict:
-    """Copy src -> dst for ``seconds`` while the exporter ``ex`` samples both devices; report the
-    copy bandwidth, the link on ``src`` whose write counter moved most, the peer BDF the exporter
-    attributes to that link and whether it is ``dst``'s BDF."""
+    """Copy src -> dst for ``seconds`` while the exporter ``ex`` samples both devices. Reports the
+    copy bandwidth, the link on ``src`` whose write counter moved most (the mode over the sampled
+    ticks), the median exporter rate on that link (``src_link_tx_GBps``) and its ratio to the copy
+    rate (``tx_vs_copy``), the same on the receiving side, the peer BDF the exporter attributes to
+    the src link and whether it is ``dst``'s BDF (``peer_matches``). The first tick after the
+    copy starts is skipped: its rate spans time before the copy."""
     statics = {s["index"]: s for s in ex.statics()}
     copier = (copier_factory or PeerCopier)(src, dst)
-    seq0 = ex.seq
-    ex.wait_for_seq(seq0 + 1, 10.0)
     result = {"src": src, "dst": dst}
-    stop = time.perf_counter() + seconds
-    best = (-1, 0.0)
-    rx = (-1, 0.0)
-    bw = []
-    while time.perf_counter() < stop:
-        bw.append(copier.run(min(interval * 3, max(0.05, stop - time.perf_counter()))))
-        r = ex.rates()
-        if src < len(r) and r[src].get("valid"):
-            cand = busiest_link(r[src], "xgmi_wr_Bps")
-            if cand[1] > best[1]:
-                best = cand
-        if dst < len(r) and r[dst].get("valid"):
-            cand = busiest_link(r[dst], "xgmi_rd_Bps")
-            if cand[1] > rx[1]:
-                rx = cand
+    bw, tx, rx = [], [], []  # per poll: copy B/s; (link, B/s) busiest on src write / dst read
+    try:
+        bw_first = copier.run(min(interval * 2, 1.0))  # ramp: the tick spanning the start is discarded
+        seq = ex.seq
+        ex.wait_for_seq(seq + 1, interval * 5 + 5.0)
+        stop = time.perf_counter() + seconds
+        while time.perf_counter() < stop:
+            bw.append(copier.run(min(interval * 2, max(0.05, stop - time.perf_counter()))))
+            r = ex.rates()
+            if src < len(r) and r[src].get("valid"):
+                tx.append(busiest_link(r[src], "xgmi_wr_Bps"))
+            if dst < len(r) and r[dst].get("valid"):
+                rx.append(busiest_link(r[dst], "xgmi_rd_Bps"))
+    finally:
+        close = getattr(copier, "close", None)
+        if close:
+            close()
     samples = ex.samples()
-    result["copy_GBps"] = round(sum(bw) / max(1, len(bw)) / 1e9, 2)
-    result["src_link"], result["src_link_tx_GBps"] = best[0], round(best[1] / 1e9, 2)
-    result["dst_link"], result["dst_link_rx_GBps"] = rx[0], round(rx[1] / 1e9, 2)
-    peer = link_peer_bdf(samples[src], best[0]) if src < len(samples) else ""
+
+    def mode_link(xs):
+        links = [k for k, v in xs if k >= 0 and v > 0]
+        if not links:
+            return -1, 0.0
+        k = max(set(links), key=links.count)
+        return k, _median([v for kk, v in xs if kk == k])
+
+    copy_bps = sum(bw) / len(bw) if bw else bw_first
+    result["copy_GBps"] = round(copy_bps / 1e9, 2)
+    (sl, sv), (dl, dv) = mode_link(tx), mode_link(rx)
+    result["src_link"], result["src_link_tx_GBps"] = sl, round(sv / 1e9, 2)
+    result["dst_link"], result["dst_link_rx_GBps"] = dl, round(dv / 1e9, 2)
+    result["tx_vs_copy"] = round(sv / copy_bps, 3) if copy_bps > 0 else None
+    result["rx_vs_copy"] = round(dv / copy_bps, 3) if copy_bps > 0 else None
+    peer = link_peer_bdf(samples[src], sl) if src < len(samples) else ""
     result["src_link_peer_bdf"] = peer
     result["dst_bdf"] = statics.get(dst, {}).get("bdf", "")
     result["peer_matches"] = bool(peer) and peer.lower() == result["dst_bdf"].lower()
     return result
+
+
+def rate_within(r: dict, tol: float = 0.15) -> bool:
+    """The exporter's per-link tx rate agrees with the copy's own rate within ``tol``."""
+    v = r.get("tx_vs_copy")
+    return v is not None and abs(v - 1.0) <= tol

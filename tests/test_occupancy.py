@@ -1,0 +1,71 @@
+"""Per-process compute utilisation for HIP workloads (KFD cu_occupancy sub-sampled by the device
+workers). The reference copies the DEVICE utilisation onto every process row
+(/root/reference/gpu.py:205); here each process row carries the interval mean of its
+own resident waves and the share of reads that found its waves resident (pod_gpu_proc_gfx_util
+for KFD compute, which DRM fdinfo engine time never sees). Hardware behaviour of the KFD file:
+profiles/r2_kfd_occupancy.md."""
+
+import time
+
+from gpumon.export import promtext
+
+
+def _wait_ticks(ex, n, timeout=10.0):
+    s0 = ex.seq
+    assert ex.wait_for_seq(s0 + n, timeout)
+
+
+def test_interval_mean_and_busy_share_from_subsamples(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", interval_s=0.2, occ_samples=10, sample_threads=-1,
+                       mock={"procs": [{"pid": 4242, "device": 0, "name": "train", "kfd_only": True}]})
+    ex.mock_set_occ_series(0, [200.0, 0.0])  # resident half of the reads
+    _wait_ticks(ex, 4)
+    row = next(r for r in ex.pod_rows() if r["pid"] == "4242")
+    assert row["occ_samples"] >= 5  # sub-samples between ticks + the tick's own read
+    assert 60 <= row["cu_occupancy"] <= 140, row  # mean of a 200 / 0 alternation
+    assert 25 <= row["proc_gfx_util"] <= 75, row  # share of reads with waves resident
+    assert ex.self_stats()["occupancy_reads"] > 0
+    fam = promtext.parse(ex.metrics_text())
+    pct = promtext.one(fam, "pod_gpu_proc_cu_occupancy_percent", pid="4242")
+    assert 20 <= pct <= 60  # of 256 CU-equivalents of wave slots
+
+
+def test_saturating_process_reads_near_full(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", interval_s=0.2, occ_samples=10, sample_threads=-1,
+                       mock={"procs": [{"pid": 7, "device": 0, "name": "burn", "kfd_only": True},
+                                       {"pid": 8, "device": 0, "name": "idle-holder", "kfd_only": True}]})
+    # two processes: pid 7 saturates (the reads alternate between the two pids' values)
+    ex.mock_set_occ_series(0, [243.0, 0.0])
+    _wait_ticks(ex, 4)
+    rows = {r["pid"]: r for r in ex.pod_rows()}
+    assert rows["7"]["proc_gfx_util"] > 90 and rows["7"]["cu_occupancy"] > 200, rows["7"]
+    assert rows["8"]["proc_gfx_util"] < 10 and rows["8"]["cu_occupancy"] < 30, rows["8"]
+
+
+def test_sequential_sampling_reports_the_instant(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0,
+                       mock={"procs": [{"pid": 9, "device": 0, "kfd_only": True}]})
+    ex.mock_set_occ_series(0, [128.0])
+    ex.tick()
+    row = next(r for r in ex.pod_rows() if r["pid"] == "9")
+    assert row["occ_samples"] == 1 and row["cu_occupancy"] == 128 and row["proc_gfx_util"] == 100
+
+
+def test_drm_engine_time_wins_when_present(mock_exporter):
+    """A process with DRM fdinfo gfx time (graphics / kernel queues) keeps that as its busy %."""
+    ex = mock_exporter(backend="mock:gpus=1,mode=load", sample_threads=0,
+                       mock={"procs": [{"pid": 11, "device": 0, "gfx_share": 0.5}]})
+    ex.mock_set_occ_series(0, [0.0])
+    ex.tick()
+    time.sleep(0.05)
+    ex.tick()
+    row = next(r for r in ex.pod_rows() if r["pid"] == "11")
+    assert row["proc_gfx_util"] > 0  # from engine-time deltas, not the (zero) occupancy reads
+
+
+def test_occ_samples_one_disables_subsampling(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", interval_s=0.1, occ_samples=1, sample_threads=-1,
+                       mock={"procs": [{"pid": 5, "device": 0, "kfd_only": True}]})
+    _wait_ticks(ex, 3)
+    assert ex.self_stats()["occupancy_reads"] == 0
+    assert all(r["occ_samples"] == 1 for r in ex.pod_rows() if r["pid"] == "5")

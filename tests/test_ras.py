@@ -138,17 +138,17 @@ def test_ras_off(mock_exporter):
     assert "gpu_ecc_errors_total" not in text and "gpu_retired_pages" not in text
 
 
-def test_sysfs_refresh_is_spread_over_ras_every_ticks(core, monkeypatch, tmp_path):
-    """A full pass over the ras/ files costs 0.25-0.5 ms on MI355X; each tick re-reads one slice
-    (file index mod ras_every) and keeps the rest from the last pass, so no tick pays for all of
-    them and every counter is at most ras_every ticks old."""
+def test_sysfs_refresh_can_be_spread_over_ras_slices_ticks(core, monkeypatch, tmp_path):
+    """A full pass over the ras/ files costs 0.25-0.5 ms on MI355X; with ras_slices = ras_every each
+    tick re-reads one slice (file index mod ras_slices) and keeps the rest from the last pass, so no
+    tick pays for all of them and every counter is at most ras_every ticks old."""
     sysr, procr = make_tree(tmp_path, gpus=1)
     r = _ras_dir(sysr)
     (r / "aca_gfx").write_text("ue: 0\nce: 1\nde: 0\n")      # item 0
     (r / "aca_umc").write_text("ue: 0\nce: 2\nde: 0\n")      # item 1
     (r / "aca_xgmi_wafl").write_text("ue: 0\nce: 0\nde: 0\n")  # item 2
     (r / "event_state").write_text(MI355X_EVENT_STATE)      # item 3
-    ex = _exporter(core, monkeypatch, sysr, procr, env={"FAKE_AMDSMI_GPUS": 1}, ras_every=3)
+    ex = _exporter(core, monkeypatch, sysr, procr, env={"FAKE_AMDSMI_GPUS": 1}, ras_every=3, ras_slices=3)
 
     def ce():
         b = ex.samples()[0]["ras"]["blocks"]
@@ -168,5 +168,46 @@ def test_sysfs_refresh_is_spread_over_ras_every_ticks(core, monkeypatch, tmp_pat
         assert any(s[:2] in ((10, 2), (1, 20)) for s in seen), seen  # ... on different ticks
         fam = promtext.parse(ex.metrics_text())
         assert promtext.one(fam, "gpu_ras_events_total", event="poison_consumption") == 4  # carried
+    finally:
+        ex.stop()
+
+
+def test_ras_pass_runs_on_one_tick_per_ras_every_by_default(mock_exporter):
+    """ras_slices = 1 (default): the whole pass on one tick out of every ras_every (one firmware
+    query burst per GPU per period), staggered across GPUs; ras_slices = N spreads it over N
+    consecutive ticks."""
+    ex = mock_exporter(backend="mock:gpus=2", ras_every=4)
+    for _ in range(9):
+        ex.tick()
+    log = ex.tick_log()
+    assert log[0]["ras_reads"] == 2 and log[0]["ras_full"]  # first tick: every GPU, everything
+    # ticks 1..8: each GPU reads once per 4 ticks, never both on the same tick (staggered)
+    assert [t["ras_reads"] for t in log[1:9]] == [0, 0, 1, 1, 0, 0, 1, 1]
+    ex2 = mock_exporter(backend="mock:gpus=1", ras_every=4, ras_slices=2)
+    for _ in range(9):
+        ex2.tick()
+    reads = [t["ras_reads"] for t in ex2.tick_log()[1:9]]
+    assert reads == [1, 0, 0, 1, 1, 0, 0, 1] and not ex2.tick_log()[1]["ras_full"]
+
+
+def test_failed_ras_read_keeps_last_values_and_is_reported(core, monkeypatch, tmp_path):
+    """A due file that fails to read keeps its last value (event_state, bad pages included: the
+    series never blank for a cycle) and the RAS call counts as failed, so a stuck file shows in
+    gpumon_backend_call_errors_total{call="ras"} instead of freezing silently."""
+    sysr, procr = make_tree(tmp_path, gpus=1)
+    r = _ras_dir(sysr)
+    (r / "aca_umc").write_text("ue: 0\nce: 2\nde: 0\n")
+    (r / "event_state").write_text(MI355X_EVENT_STATE)
+    ex = _exporter(core, monkeypatch, sysr, procr, env={"FAKE_AMDSMI_GPUS": 1}, ras_every=1)
+    try:
+        ex.tick()
+        assert ex.self_stats()["backend_calls"]["ras"]["errors"] == 0
+        (r / "event_state").unlink()
+        (r / "event_state").mkdir()  # unreadable as a file (root ignores permission bits)
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpu_ras_events_total", event="poison_consumption") == 4  # carried
+        assert promtext.one(fam, "gpu_ecc_errors_total", block="umc", type="correctable") == 2
+        assert ex.self_stats()["backend_calls"]["ras"]["errors"] == 1
     finally:
         ex.stop()

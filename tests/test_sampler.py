@@ -235,3 +235,50 @@ def test_link_metrics_refresh_rarely_and_on_link_state_change(mock_exporter):
     assert promtext.one(fam, "gpu_xgmi_link_up", gpu_id="0", link="3") == 1
     ex.tick()
     assert ex.mock_link_calls(1) == 2  # no further refresh while the state holds
+
+
+def test_link_refresh_drops_the_peer_of_a_link_that_went_down(mock_exporter):
+    """On a tick that re-read the link metrics, an empty peer / unknown bandwidth is the new truth
+    (the link lost them): it must not be papered over with the previous tick's identity."""
+    from gpumon.export import promtext
+
+    ex = mock_exporter(backend="mock:gpus=2", link_every=600)
+    ex.tick()
+    assert ex.samples()[1]["links"][3]["peer_bdf"]
+    ex.mock_set_link_up(1, 3, False)
+    ex.tick()  # status change seen
+    ex.tick()  # links re-read: link 3 has no peer now
+    assert ex.mock_link_calls(1) == 2
+    assert ex.samples()[1]["links"][3]["peer_bdf"] == ""
+    ex.tick()  # between refreshes the (empty) identity is carried, not resurrected
+    assert ex.samples()[1]["links"][3]["peer_bdf"] == ""
+    assert ex.samples()[1]["links"][2]["peer_bdf"]  # other links keep theirs
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_xgmi_link_up", gpu_id="1", link="3") == 0
+
+
+def test_link_change_across_a_failed_tick_still_forces_a_refresh(mock_exporter):
+    """The status is compared with the last SUCCESSFUL sample: a change that happens while the
+    device fails a tick is still caught when it answers again."""
+    ex = mock_exporter(backend="mock:gpus=1", link_every=600, sample_threads=0)
+    ex.tick()
+    assert ex.mock_link_calls(0) == 1
+    ex.mock_set_fail(0, 1)  # every call fails
+    ex.tick()
+    ex.mock_set_link_up(0, 2, False)
+    ex.mock_set_fail(0, 0)
+    ex.tick()  # ok again: status differs from the last ok sample -> refresh next tick
+    ex.tick()
+    assert ex.mock_link_calls(0) == 2
+
+
+def test_tick_log_records_phases_and_link_refreshes(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=3", link_every=2)
+    for _ in range(4):
+        ex.tick()
+    log = ex.tick_log()  # start()'s own tick + 4
+    assert [t["seq"] for t in log] == sorted(t["seq"] for t in log) and len(log) == 5
+    assert log[0]["link_refreshes"] == 3  # first tick: every device
+    assert [t["link_refreshes"] for t in log[1:]] == [1, 2, 1, 2]  # staggered over link_every
+    for t in log:
+        assert t["duration_s"] >= t["t_sample"] + t["t_attrib"] + t["t_render"] > 0
