@@ -21,7 +21,7 @@ LIBS      := -ldl -lpthread -lz
 
 CORE_SRC  := $(wildcard csrc/core/*.cpp)
 CORE_OBJ  := $(patsubst csrc/%.cpp,build/obj/%.o,$(CORE_SRC))
-CORE_HDR  := $(wildcard csrc/core/*.h)
+CORE_HDR  := $(wildcard csrc/core/*.h) csrc/plugins/ondevice_abi.h
 
 PYEXT     := gpumon/_core$(EXT)
 HIPEXT    := gpumon/_hip$(EXT)

@@ -1,22 +1,34 @@
 #!/usr/bin/env python3
 """Headline benchmark (BASELINE.json): p99 /metrics scrape latency + samples/sec/GPU at 1 Hz.
 
-    python bench.py [--gpus N --steps K --warmup W]                       # 1 GPU
+    python bench.py [--gpus N --steps K --warmup W]                       # 1 process, N GPUs
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W           # N GPUs, one rank each
 
 What one "step" is: one sampling period of the exporter (default 1 Hz, the BASELINE interval).
 Rank 0 runs the native exporter (amdsmi backend) over GPUs 0..N-1 and a client-side scraper that
-hits /metrics at --scrape-rate while every rank keeps its own GPU under a synthetic gfx950 HIP load
-(bf16 MFMA burn + HBM stream, csrc/hip/kernels.hip) and, for N > 1, runs one RCCL all-reduce per
-step (xGMI traffic). W warmup ticks, then exactly K ticks are timed between barriers +
+hits /metrics at --scrape-rate, while EVERY GPU runs a synthetic gfx950 HIP load (bf16 MFMA burn +
+HBM stream, csrc/hip/kernels.hip) and, for N > 1, xGMI traffic:
+
+* under torchrun (one rank per GPU) each rank loads its own GPU and all ranks run RCCL ring
+  all-reduces each step, as many as fill --xgmi-duty of the interval (calibrated before the timed
+  region): every GPU's links carry 2(N-1)/N x bytes per all-reduce;
+* in one process (``--gpus N`` without torchrun) the process loads all N GPUs and runs a native
+  peer-copy ring (GPU i pushes into GPU (i+1) mod N, ``_hip.XgmiLoad``): each GPU's tx equals its
+  copy rate.
+
+The exporter's own per-GPU xGMI counters are compared with that expectation
+(``xgmi.per_gpu[].tx_vs_expected``), and after the timed region rank 0 drives GPU 0 -> k for every
+peer k and checks that the link whose counter moves is the one the exporter maps to k's BDF
+(``xgmi.link_map``). W warmup ticks, then exactly K ticks are timed between barriers +
 torch.cuda.synchronize(); the MAX elapsed over ranks is used.
 
 Reported ``value`` = whole-node fresh device samples per second (K ticks x N GPUs / elapsed);
 ``vs_baseline`` = per-GPU rate / 0.077 samples/s/GPU, the reference's best observed rate
 (one node_gpu line per 13-19 s). The scrape-latency half of the headline metric is
 reported as ``scrape_p99_ms`` / ``scrape_p50_ms`` (client-side, keep-alive, like a Prometheus
-server). Without a GPU the exporter uses the mock backend and says so in ``data``.
+server). Tick quantiles are exact over the timed ticks (the exporter's tick log). Without a GPU
+the exporter uses the mock backend and says so in ``data``.
 """
 
 from __future__ import annotations
@@ -45,20 +57,52 @@ def _pct(xs, q):
     return xs[f] if f == c else xs[f] + (xs[c] - xs[f]) * (k - f)
 
 
-def _xgmi_summary(xgmi, xgmi_rates):
-    """Exporter-measured xGMI traffic over the timed ticks (mean per GPU), next to the all-reduce
-    expectation. The first tick's rate spans part of the warmup, so it is skipped."""
-    ticks = [t for t in xgmi_rates[1:] if t] or [t for t in xgmi_rates if t]
-    out = dict(xgmi or {})
-    if ticks:
-        tx = [sum(w for w, _ in t) / len(t) for t in ticks]
-        rx = [sum(r for _, r in t) / len(t) for t in ticks]
-        out["exporter_tx_GBps_per_gpu"] = round(sum(tx) / len(tx) / 1e9, 3)
-        out["exporter_rx_GBps_per_gpu"] = round(sum(rx) / len(rx) / 1e9, 3)
-        exp = out.get("expected_tx_GBps_per_gpu")
-        if exp:
-            out["exporter_vs_expected"] = round(out["exporter_tx_GBps_per_gpu"] / exp, 3)
-    return out or None
+def _r(x, nd=3):
+    return round(x, nd) if isinstance(x, float) and x == x else x
+
+
+def _per_gpu_xgmi(tick_rates, n, expected_tx, expected_rx):
+    """Exporter-measured xGMI tx / rx per GPU (sum over links, mean over the timed ticks; the first
+    tick's rate spans part of the warmup and is skipped) against the traffic the bench drove."""
+    ticks = tick_rates[1:] if len(tick_rates) > 1 else tick_rates
+    out = []
+    for d in range(n):
+        tx = [t[d][0] for t in ticks if d < len(t) and t[d] is not None]
+        rx = [t[d][1] for t in ticks if d < len(t) and t[d] is not None]
+        row = {"gpu": d,
+               "exporter_tx_GBps": _r(sum(tx) / len(tx) / 1e9) if tx else None,
+               "exporter_rx_GBps": _r(sum(rx) / len(rx) / 1e9) if rx else None,
+               "expected_tx_GBps": _r(expected_tx[d] / 1e9) if expected_tx else None,
+               "expected_rx_GBps": _r(expected_rx[d] / 1e9) if expected_rx else None}
+        if tx and expected_tx and expected_tx[d] > 0:
+            row["tx_vs_expected"] = _r(sum(tx) / len(tx) / expected_tx[d])
+        if rx and expected_rx and expected_rx[d] > 0:
+            row["rx_vs_expected"] = _r(sum(rx) / len(rx) / expected_rx[d])
+        out.append(row)
+    return out
+
+
+def _link_map_check(n, seconds):
+    """GPU 0 pushes into every peer in turn while a fresh 10 Hz exporter watches: the link whose
+    write counter moves must be the one the exporter attributes to that peer's BDF."""
+    from gpumon import core as _core
+    from gpumon.parallel.xgmi import rate_within, validate_pair
+
+    ex = _core().Exporter({"backend": "amdsmi", "devices": list(range(n)), "serve_http": False,
+                           "interval_s": 0.1, "link_every": 1, "processes": False, "log_level": "warn"})
+    err = ex.start()
+    if err:
+        return {"error": err}
+    rows = []
+    try:
+        for k in range(1, n):
+            r = validate_pair(ex, 0, k, seconds=seconds, interval=0.1)
+            r["rate_within_15pct"] = rate_within(r, 0.15)
+            rows.append(r)
+    finally:
+        ex.stop()
+    return {"pairs": rows, "peers_matched": sum(1 for r in rows if r["peer_matches"]), "peers": len(rows),
+            "rates_within_15pct": sum(1 for r in rows if r["rate_within_15pct"])}
 
 
 def main() -> int:
@@ -67,7 +111,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--interval", type=float, default=1.0, help="sampling interval (1.0 = BASELINE; 0.1 = 10 Hz stress)")
-    ap.add_argument("--load", default="mixed", choices=["mixed", "mfma", "hbm", "idle"])
+    ap.add_argument("--load", default="mixed", choices=["mixed", "concurrent", "mfma", "hbm", "idle"])
     ap.add_argument("--scrape-rate", type=float, default=20.0, help="aggregate /metrics requests per second")
     ap.add_argument("--scrape-concurrency", type=int, default=2)
     ap.add_argument("--gzip", action="store_true", help="scrape with Accept-Encoding: gzip")
@@ -76,7 +120,13 @@ def main() -> int:
                     help="parallel per-GPU sampling threads (-1 = auto: one per GPU, 0 = sequential)")
     ap.add_argument("--replicate", type=int, default=1,
                     help="REHEARSAL ONLY: sample each physical GPU R times (sampler scaling on a 1-GPU box)")
-    ap.add_argument("--allreduce-mb", type=int, default=256)
+    ap.add_argument("--allreduce-mb", type=int, default=256, help="torchrun: all-reduce message size")
+    ap.add_argument("--xgmi-duty", type=float, default=0.4,
+                    help="torchrun: fraction of each interval filled with all-reduces (0 = one per step)")
+    ap.add_argument("--xgmi-mb", type=int, default=256, help="single process: peer-copy ring buffer size")
+    ap.add_argument("--no-xgmi", action="store_true", help="no xGMI traffic for N > 1")
+    ap.add_argument("--link-check-s", type=float, default=0.6,
+                    help="N > 1: seconds per peer of the GPU 0 -> k link-map check after the timed region (0 = off)")
     ap.add_argument("--probe", action="store_true", help="also run the K1 probe kernel each tick")
     ap.add_argument("--no-fast-path", action="store_true", help="read every value through libamd_smi")
     ap.add_argument("--out", default="")
@@ -105,16 +155,28 @@ def main() -> int:
         if has_gpu:
             torch.cuda.synchronize()
 
-    # ---------------------------------------------------------------- per-rank synthetic load
-    load = None
+    # ---------------------------------------------------------------- synthetic load on every GPU
+    # torchrun: this rank's GPU; one process: all N GPUs (the node-level exporter watches them all)
+    my_devs = [local_rank] if world > 1 else list(range(n))
+    loads = []
     if has_gpu and args.load != "idle":
+        from gpumon import hip
         from gpumon.ops.load import SyntheticLoad
 
-        load = SyntheticLoad(dev=local_rank, kind=args.load, hbm_bytes=1 << 30).start()
+        if hip().device_count() < max(my_devs) + 1:
+            raise SystemExit(f"bench needs GPUs {my_devs}, HIP sees {hip().device_count()}")
+        loads = [SyntheticLoad(dev=d, kind=args.load, hbm_bytes=1 << 30).start() for d in my_devs]
+
+    xgmi_on = n > 1 and not args.no_xgmi
     ar_buf = None
-    if dist is not None and args.allreduce_mb > 0:
+    if dist is not None and xgmi_on and args.allreduce_mb > 0:
         # zeros: repeated in-place sums stay finite (ones would reach inf after ~40 steps on 8 ranks)
         ar_buf = torch.zeros(args.allreduce_mb * (1 << 20) // 2, dtype=torch.bfloat16, device=device)
+    copiers = []
+    if dist is None and has_gpu and xgmi_on:
+        from gpumon.parallel.xgmi import PeerCopier
+
+        copiers = [PeerCopier(i, (i + 1) % n, nbytes=args.xgmi_mb << 20).start() for i in range(n)]
 
     # ---------------------------------------------------------------- rank 0: exporter + scraper
     mon = None
@@ -143,6 +205,30 @@ def main() -> int:
         mon.wait_ticks(args.warmup, timeout_s=args.warmup * args.interval * 5 + 30)
 
     barrier()
+    # RCCL channel / buffer setup and the all-reduce calibration stay out of the timed region
+    reps = 1
+    ar_cal_ms = None
+    if ar_buf is not None:
+        for _ in range(3):
+            dist.all_reduce(ar_buf)
+        if has_gpu:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                dist.all_reduce(ar_buf)
+            e1.record()
+            e1.synchronize()
+            t = torch.tensor([e0.elapsed_time(e1) / 5], dtype=torch.float64, device=device)
+        else:
+            t0 = time.perf_counter()
+            for _ in range(5):
+                dist.all_reduce(ar_buf)
+            t = torch.tensor([(time.perf_counter() - t0) / 5 * 1e3], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)  # every rank derives the same count
+        ar_cal_ms = float(t.item())
+        if args.xgmi_duty > 0 and ar_cal_ms > 0:
+            reps = max(1, min(4000, int(args.xgmi_duty * args.interval * 1e3 / ar_cal_ms)))
+
     scrape_result = {}
     scraper = None
     if rank == 0:
@@ -157,52 +243,79 @@ def main() -> int:
         s0 = mon.ex.self_stats()
         seq0 = mon.ex.seq
 
-    if ar_buf is not None:  # RCCL channel/buffer setup stays out of the timed region
-        for _ in range(max(1, args.warmup)):
-            dist.all_reduce(ar_buf)
-
     # ---------------------------------------------------------------- timed region
     barrier()
+    c0 = [c.stats() for c in copiers]
+    l0 = [ld.stats() for ld in loads]
     t0 = time.perf_counter()
     if scraper is not None:
         scraper.start()
-    xgmi_rates = []  # per tick: (sum of per-link write B/s, sum of read B/s) per sampled device
+    tick_rates = []  # per tick, per sampled device: (sum of per-link write B/s, read B/s) or None
     ar_events = []
     for step in range(args.steps):
         if rank == 0:
             if not mon.ex.wait_for_seq(seq0 + step + 1, args.interval * 5 + 10):
                 raise SystemExit("exporter tick timed out")
-            xgmi_rates.append([(sum(r.get("xgmi_wr_Bps") or [0.0]), sum(r.get("xgmi_rd_Bps") or [0.0]))
-                               for r in mon.ex.rates() if r.get("valid")])
+            tick_rates.append([(sum(r.get("xgmi_wr_Bps") or [0.0]), sum(r.get("xgmi_rd_Bps") or [0.0]))
+                               if r.get("valid") else None for r in mon.ex.rates()])
         if ar_buf is not None:
             if has_gpu:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 ev[0].record()
-                dist.all_reduce(ar_buf)
+                for _ in range(reps):
+                    dist.all_reduce(ar_buf)
                 ev[1].record()
                 ar_events.append(ev)
             else:
-                dist.all_reduce(ar_buf)
+                for _ in range(reps):
+                    dist.all_reduce(ar_buf)
     barrier()
     elapsed = time.perf_counter() - t0
+    c1 = [c.stats() for c in copiers]
+    l1 = [ld.stats() for ld in loads]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # xGMI cross-check (N > 1): RCCL ring all-reduce bus bandwidth vs the exporter's own per-link
-    # xGMI counters. A ring all-reduce of S bytes moves 2(n-1)/n * S out of every GPU per call.
+    # ---------------------------------------------------------------- per-GPU load rates (every rank)
+    # event-timed TFLOP/s / TB/s over the timed region, gathered to rank 0 as one row per GPU
+    lrates = torch.zeros(n, 3, dtype=torch.float64, device=device)
+    for d, a, b in zip(my_devs, l0, l1):
+        dm, dh = b["mfma_s"] - a["mfma_s"], b["hbm_s"] - a["hbm_s"]
+        lrates[d, 0] = (b["flops"] - a["flops"]) / dm / 1e12 if dm > 0 else 0.0
+        lrates[d, 1] = (b["bytes"] - a["bytes"]) / dh / 1e12 if dh > 0 else 0.0
+        lrates[d, 2] = (b["busy_s"] - a["busy_s"]) / max(1e-9, b["wall_s"] - a["wall_s"])
+    if dist is not None:
+        dist.all_reduce(lrates)
+    lrates = lrates.cpu().tolist()
+
+    # ---------------------------------------------------------------- xGMI expectation
     xgmi = None
+    exp_tx = exp_rx = None
     if ar_buf is not None:
         nbytes = ar_buf.numel() * ar_buf.element_size()
-        ar_ms = [a.elapsed_time(b) for a, b in ar_events] if ar_events else []
+        ar_ms = [a.elapsed_time(b) / reps for a, b in ar_events] if ar_events else []
         t = torch.tensor([sum(ar_ms) / len(ar_ms) if ar_ms else float("nan")], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ar_mean_s = float(t.item()) * 1e-3
-        xgmi = {"allreduce_mb": args.allreduce_mb, "allreduce_ms": round(ar_mean_s * 1e3, 3),
+        per_gpu = 2 * (n - 1) / n * nbytes * reps * args.steps / elapsed  # B/s out of (and into) every GPU
+        exp_tx = exp_rx = [per_gpu] * n
+        xgmi = {"mode": "rccl_allreduce", "allreduce_mb": args.allreduce_mb, "allreduces_per_step": reps,
+                "calibration_ms": _r(ar_cal_ms),
+                "allreduce_ms": round(ar_mean_s * 1e3, 3) if ar_mean_s == ar_mean_s else None,
                 "allreduce_busbw_GBps": round(2 * (n - 1) / n * nbytes / ar_mean_s / 1e9, 2)
                 if ar_mean_s == ar_mean_s and ar_mean_s > 0 else None,
-                "expected_tx_GBps_per_gpu": round(2 * (n - 1) / n * nbytes * args.steps / elapsed / 1e9, 3)}
+                "expected_tx_GBps_per_gpu": round(per_gpu / 1e9, 3)}
+    elif copiers:
+        rates = [(b["bytes"] - a["bytes"]) / max(1e-9, b["wall_s"] - a["wall_s"]) for a, b in zip(c0, c1)]
+        exp_tx = rates
+        exp_rx = [rates[(d - 1) % n] for d in range(n)]
+        xgmi = {"mode": "peer_copy_ring", "copy_mb": args.xgmi_mb,
+                "copy_GBps": [round(r / 1e9, 2) for r in rates],
+                "expected_tx_GBps_per_gpu": round(sum(rates) / n / 1e9, 3)}
+    for c in copiers:
+        c.close()
 
     result = None
     if rank == 0:
@@ -212,12 +325,23 @@ def main() -> int:
         lat = scrape_result.get("latencies_s", [])
         samples = s1["samples"] - s0["samples"]
         ticks = mon.ex.seq - seq0
-        tick_mean = (s1["sample_sum_s"] - s0["sample_sum_s"]) / max(1, s1["sample_count"] - s0["sample_count"])
+        timed = [t for t in mon.ex.tick_log() if seq0 < t["seq"] <= seq0 + ticks]
+        tdur = [t["duration_s"] for t in timed]
+        slow = max(timed, key=lambda t: t["duration_s"]) if timed else None
         sm = mon.ex.samples()
         util = [x["fields"].get("gfx_util") for x in sm]
         rows = mon.ex.pod_rows()
         value = samples / elapsed
-        lstats = load.stats() if load is not None else {}
+        per_gpu = _per_gpu_xgmi(tick_rates, n, exp_tx, exp_rx) if xgmi is not None else None
+        if xgmi is not None:
+            tx = [r["exporter_tx_GBps"] for r in per_gpu if r["exporter_tx_GBps"] is not None]
+            rx = [r["exporter_rx_GBps"] for r in per_gpu if r["exporter_rx_GBps"] is not None]
+            xgmi["exporter_tx_GBps_per_gpu"] = round(sum(tx) / len(tx), 3) if tx else None
+            xgmi["exporter_rx_GBps_per_gpu"] = round(sum(rx) / len(rx), 3) if rx else None
+            if tx and xgmi.get("expected_tx_GBps_per_gpu"):
+                xgmi["exporter_vs_expected"] = round(xgmi["exporter_tx_GBps_per_gpu"]
+                                                     / xgmi["expected_tx_GBps_per_gpu"], 3)
+            xgmi["per_gpu"] = per_gpu
         result = {
             "metric": BASELINE_METRIC,
             "value": round(value, 4),
@@ -238,8 +362,11 @@ def main() -> int:
                 "model": f"gpumon MI355X exporter ({backend.split(':')[0]} backend) + synthetic bf16 MFMA/HBM HIP load",
                 "global_batch": n,
                 "seq_len": None,
-                "parallelism": f"node-local exporter over {n} GPU(s); one rank per GPU"
-                               + (", RCCL all-reduce per step" if ar_buf is not None else ""),
+                "parallelism": f"node-local exporter over {n} GPU(s); "
+                               + ("one rank per GPU" if world > 1 else "one process loading every GPU")
+                               + (f", {'RCCL' if has_gpu else 'gloo'} all-reduce x{reps} per step"
+                                  if ar_buf is not None else "")
+                               + (", peer-copy xGMI ring" if copiers else ""),
                 "interval_s": args.interval,
             },
             "scrape_p50_ms": round(_pct(lat, 0.50) * 1e3, 4),
@@ -250,28 +377,42 @@ def main() -> int:
             "scrape_body_kb": round(scrape_result.get("bytes", 0) / max(1, len(lat)) / 1024, 2),
             "samples_per_sec_per_gpu": round(value / max(1, len(sm)), 4),
             "ticks": ticks,
-            "tick_mean_ms": round(tick_mean * 1e3, 4),
-            "tick_p99_ms": round(mon.ex.sample_quantile(0.99) * 1e3, 4),
-            "server_scrape_p99_ms": round(mon.ex.scrape_quantile(0.99) * 1e3, 4),
+            "tick_mean_ms": round(sum(tdur) / len(tdur) * 1e3, 4) if tdur else None,
+            "tick_p50_ms": round(_pct(tdur, 0.50) * 1e3, 4) if tdur else None,
+            "tick_p99_ms": round(_pct(tdur, 0.99) * 1e3, 4) if tdur else None,
+            "tick_max_ms": round(max(tdur) * 1e3, 4) if tdur else None,
+            # what the slowest timed tick spent its time on (tick-tail attribution)
+            "slowest_tick": {k: (round(v * 1e3, 4) if k.startswith("t_") or k == "duration_s" else v)
+                             for k, v in slow.items() if k in ("seq", "duration_s", "t_sample", "t_procs", "t_attrib",
+                                                               "t_render", "t_gzip", "link_refreshes", "ras_reads",
+                                                               "ras_full")} if slow else None,
+            "tick_quantiles": "exact over the timed ticks (exporter tick log); times in ms",
+            "server_scrape_p99_ms_last4096": round(mon.ex.scrape_quantile(0.99) * 1e3, 4),
             "overruns": s1["overruns"] - s0["overruns"],
             "backend_call_us": {k: round((v["seconds"] - s0["backend_calls"].get(k, {}).get("seconds", 0.0)) * 1e6
                                          / max(1, v["n"] - s0["backend_calls"].get(k, {}).get("n", 0)), 1)
                                 for k, v in s1.get("backend_calls", {}).items()},
             "backend": backend,
             "load": args.load if has_gpu else "none",
-            "load_tflops": round(lstats.get("tflops", 0.0), 1) if lstats else None,
-            "load_tbps": round(lstats.get("tbps", 0.0), 3) if lstats else None,
+            "load_per_gpu": [{"gpu": d, "tflops": round(r[0], 1), "tbps": round(r[1], 3), "busy": round(r[2], 3)}
+                             for d, r in enumerate(lrates)] if has_gpu and loads else None,
+            "load_tflops": round(sum(r[0] for r in lrates), 1) if has_gpu and loads else None,
+            "load_tbps": round(sum(r[1] for r in lrates), 3) if has_gpu and loads else None,
             "gfx_util_last": util,
             "procs_seen": len([r for r in rows if not r["idle"]]),
-            "proc_rows": [{"pid": r["pid"], "vram_gib": round(r["used_memory_bytes"] / 2 ** 30, 2),
-                           "cu_occupancy": r["cu_occupancy"], "gfx_util": r["proc_gfx_util"]}
-                          for r in rows if not r["idle"]][:8],
-            "xgmi": _xgmi_summary(xgmi, xgmi_rates),
+            "proc_rows": [{"gpu": r["dev"], "pid": r["pid"], "vram_gib": round(r["used_memory_bytes"] / 2 ** 30, 2),
+                           "cu_occupancy": _r(r["cu_occupancy"], 1), "occ_samples": r["occ_samples"],
+                           "busy_pct": _r(r["proc_gfx_util"], 1)}
+                          for r in rows if not r["idle"]][:16],
+            "occupancy_reads": s1.get("occupancy_reads", 0) - s0.get("occupancy_reads", 0),
+            "xgmi": xgmi,
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,
         }
         mon.stop()
-    if load is not None:
-        load.stop()
+        if has_gpu and n > 1 and args.link_check_s > 0:
+            result["xgmi"] = dict(result["xgmi"] or {}, link_map=_link_map_check(n, args.link_check_s))
+    for ld in loads:
+        ld.stop()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

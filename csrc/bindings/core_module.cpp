@@ -11,6 +11,7 @@
 #include "../core/common.h"
 #include "../core/exporter.h"
 #include "../core/grpc_lite.h"
+#include "../core/hpack.h"
 #include "../core/http_client.h"
 #include "../core/ondevice.h"
 #include "../core/options.h"
@@ -35,6 +36,7 @@ OnDeviceConfig ondevice_from(const py::dict& d) {
   get(d, "pmc_counters", &c.pmc_counters);
   get(d, "pmc_every_s", &c.pmc_every_s);
   get(d, "pmc_window_s", &c.pmc_window_s);
+  get(d, "pmc_mode", &c.pmc_mode);
   get(d, "probe", &c.probe);
   get(d, "probe_every_s", &c.probe_every_s);
   get(d, "probe_blocks", &c.probe_blocks);
@@ -78,6 +80,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "ras_every", &c.ras_every);
   get(d, "ras_slices", &c.ras_slices);
   get(d, "occ_samples", &c.occ_samples);
+  get(d, "hide_empty_contexts", &c.hide_empty_contexts);
   get(d, "sample_threads", &c.sample_threads);
   get(d, "influx_url", &c.influx_url);
   get(d, "influx_extended", &c.influx_extended);
@@ -385,6 +388,56 @@ PYBIND11_MODULE(_core, m) {
       py::arg("dra_drivers") = std::vector<std::string>{"gpu.amd.com"},
       "kubelet PodResources List() through the native HTTP/2 client (grpc_lite.cpp)");
   m.def(
+      "grpc_call",
+      [](const std::string& sock, const std::string& path, py::bytes req, int timeout_ms) {
+        std::string resp, err;
+        GrpcStatus st;
+        bool ok;
+        const std::string r = req;
+        {
+          py::gil_scoped_release nogil;
+          ok = grpc_unary_unix(sock, path, r, &resp, &err, timeout_ms, &st);
+        }
+        py::dict d;
+        d["ok"] = ok;
+        d["response"] = py::bytes(resp);
+        d["error"] = err;
+        d["code"] = st.code;
+        d["code_name"] = st.code >= 0 ? std::string(grpc_code_name(st.code)) : std::string();
+        d["message"] = st.message;
+        d["http_status"] = st.http_status;
+        return d;
+      },
+      py::arg("socket"), py::arg("path"), py::arg("request") = py::bytes(""), py::arg("timeout_ms") = 3000,
+      "one unary call through grpc_lite.cpp with the server's decoded status");
+  m.def(
+      "hpack_decode",
+      [](const std::vector<py::bytes>& blocks, size_t table_size) {
+        HpackDecoder dec(table_size);
+        py::list out;
+        for (const auto& b : blocks) {
+          HeaderList h;
+          std::string err;
+          if (!dec.decode(std::string(b), &h, &err)) throw py::value_error(err);
+          py::list l;
+          for (const auto& [k, v] : h) l.append(py::make_tuple(k, v));
+          py::dict d;
+          d["headers"] = l;
+          d["table_size"] = dec.table_size();
+          d["table_entries"] = dec.table_entries();
+          out.append(d);
+        }
+        return out;
+      },
+      py::arg("blocks"), py::arg("table_size") = 4096,
+      "decode consecutive HPACK header blocks of one connection (hpack.cpp)");
+  m.def("hpack_huffman_encode", [](py::bytes s) { return py::bytes(hpack_huffman_encode(std::string(s))); });
+  m.def("hpack_huffman_decode", [](py::bytes b) {
+    std::string out;
+    if (!hpack_huffman_decode(std::string(b), &out)) throw py::value_error("invalid Huffman string");
+    return py::bytes(out);
+  });
+  m.def(
       "cri_list",
       [](const std::string& sock, int timeout_ms) {
         std::vector<CriContainer> cs;
@@ -579,6 +632,7 @@ PYBIND11_MODULE(_core, m) {
              d["samples"] = s.samples;
              d["stale_samples"] = s.stale_samples;
              d["occupancy_reads"] = s.occupancy_reads;
+             d["hidden_contexts"] = s.hidden_contexts;
              d["overruns"] = s.overruns;
              d["scrapes"] = s.scrapes;
              d["http_connections"] = s.http_connections;
@@ -744,6 +798,8 @@ PYBIND11_MODULE(_core, m) {
         py::dict d;
         d["pmc_samples"] = s.pmc_samples;
         d["pmc_errors"] = s.pmc_errors;
+        d["pmc_resets"] = s.pmc_resets;
+        d["pmc_continuous"] = s.pmc_continuous;
         d["probe_done"] = s.probe_done;
         d["probe_timeouts"] = s.probe_timeouts;
         d["pmc_agents"] = s.pmc_agents;

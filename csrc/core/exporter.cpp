@@ -551,6 +551,7 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
 void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
                               const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows) {
   rows->clear();
+  uint64_t hidden = 0;
   std::vector<uint32_t> alive;
   std::unordered_map<ProcKey, ProcPrev, ProcKeyHash> next_prev;
   // (ns, pod, container, dev) with an active process -> suppress the idle row for it
@@ -566,6 +567,14 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
         PodRow& r = (*rows)[dup->second];
         r.used_memory_bytes += has(p.vram_bytes) ? p.vram_bytes : 0;
         if (has(p.cu_occupancy)) r.cu_occupancy = has(r.cu_occupancy) ? r.cu_occupancy + p.cu_occupancy : p.cu_occupancy;
+        continue;
+      }
+      // A KFD context that holds no VRAM and never had a wave resident this interval (a runtime
+      // that only probed the device: rocminfo, amd-smi, an exporter's own HIP init) is not a GPU
+      // workload; rows for it read as phantom 0-MiB processes. Counted, not exported.
+      if (cfg_.hide_empty_contexts && !(p.vram_bytes > 0) && !(p.mem_bytes > 0) && !(p.cu_occupancy > 0) &&
+          p.occ_busy == 0) {
+        hidden++;
         continue;
       }
       alive.push_back(p.pid);
@@ -610,6 +619,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
     }
   }
   proc_prev_.swap(next_prev);
+  hidden_contexts_ = hidden;
   attr_->gc(alive);
   // Allocated-but-idle GPUs (reference gpu.py:220-253 via `docker exec nvidia-smi -L`; here the
   // kubelet PodResources allocation list pushed by the control plane).
@@ -1035,6 +1045,7 @@ SelfStats Exporter::self_stats() const {
   s.samples = samples_;
   s.stale_samples = stale_;
   s.occupancy_reads = occ_reads_->load(std::memory_order_relaxed);
+  s.hidden_contexts = hidden_contexts_.load();
   s.overruns = overruns_;
   s.last_tick_wall_s = last_tick_wall_ns_.load() * 1e-9;
   s.interval_s = cfg_.interval_s;
@@ -1112,8 +1123,9 @@ bool Exporter::podres_poll_once() {
   std::vector<PodDeviceRow> rows;
   std::string err;
   const int64_t t0 = mono_ns();
+  GrpcStatus gst;
   const bool ok = podresources_list(cfg_.pod_resources_socket, cfg_.pod_resources_prefix, &rows, &err, 3000,
-                                    cfg_.pod_resources_dra_drivers);
+                                    cfg_.pod_resources_dra_drivers, &gst);
   const double dt = (mono_ns() - t0) * 1e-9;
   std::vector<DeviceStatic> st;
   {
@@ -1157,6 +1169,10 @@ bool Exporter::podres_poll_once() {
                 -1, {}, static_cast<double>(unknown)});
   ex.push_back({"gpumon_podresources_list_seconds", "Duration of the last PodResources List() call.", "gauge", -1,
                 {}, dt});
+  ex.push_back({"gpumon_podresources_grpc_status",
+                "grpc-status of the last PodResources List() (0 OK, 7 PERMISSION_DENIED, 12 UNIMPLEMENTED, ...; "
+                "-1 = no status: transport failure).",
+                "gauge", -1, {}, static_cast<double>(gst.code)});
   set_extra("podresources_native", std::move(ex));
   return ok;
 }
@@ -1181,7 +1197,8 @@ bool Exporter::cri_poll_once() {
   std::vector<CriSandbox> sbs;
   std::string err;
   const int64_t t0 = mono_ns();
-  const bool ok = cri_list(cfg_.cri_socket, &cs, &sbs, &err, 3000);
+  GrpcStatus gst;
+  const bool ok = cri_list(cfg_.cri_socket, &cs, &sbs, &err, 3000, &gst);
   const double dt = (mono_ns() - t0) * 1e-9;
   if (ok) {
     std::unordered_map<std::string, const CriSandbox*> by_id;
@@ -1225,6 +1242,10 @@ bool Exporter::cri_poll_once() {
   ex.push_back({"gpumon_cri_containers", "Containers known from the CRI runtime.", "gauge", -1, {},
                 static_cast<double>(cs.size())});
   ex.push_back({"gpumon_cri_list_seconds", "Duration of the last CRI listing.", "gauge", -1, {}, dt});
+  ex.push_back({"gpumon_cri_grpc_status",
+                "grpc-status of the last CRI call (0 OK, 12 UNIMPLEMENTED after both runtime.v1 and v1alpha2, ...; "
+                "-1 = no status: transport failure).",
+                "gauge", -1, {}, static_cast<double>(gst.code)});
   set_extra("cri_native", std::move(ex));
   return ok;
 }

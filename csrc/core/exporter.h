@@ -54,6 +54,7 @@ struct ExporterConfig {
   int ras_slices = 1;                 // the pass read in this many slices on consecutive ticks (1..ras_every)
   int sample_threads = -1;            // parallel device sampling; 0 = sequential, -1 = auto (one per GPU, max 8)
   int occ_samples = 10;               // KFD cu_occupancy reads per process per tick on the device workers (1 = the tick's own)
+  bool hide_empty_contexts = true;    // no pod_gpu row for a process with a GPU context but no VRAM and no waves
   AttributionConfig attribution;
   RateConfig rates;
   std::string influx_url;             // INFLUXDB_URL; empty = push disabled
@@ -220,6 +221,7 @@ class Exporter {
   bool stop_workers();
   bool workers_busy() const;
   std::vector<std::shared_ptr<DevWorker>> workers_;
+  std::atomic<uint64_t> hidden_contexts_{0};  // empty GPU contexts left out of the last tick's rows
   // cu_occupancy sub-sample reads by the workers (shared: a detached worker may outlive a restart)
   std::shared_ptr<std::atomic<uint64_t>> occ_reads_ = std::make_shared<std::atomic<uint64_t>>(0);
   std::shared_ptr<DoneSignal> done_sig_;

@@ -8,14 +8,18 @@
 #include <algorithm>
 #include <cerrno>
 #include <cstring>
+#include <mutex>
 
 #include "common.h"
+#include "hpack.h"
 
 namespace gpumon {
 
 namespace {
 
-enum : uint8_t { kData = 0, kHeaders = 1, kRstStream = 3, kSettings = 4, kPing = 6, kGoaway = 7, kWindowUpdate = 8 };
+enum : uint8_t {
+  kData = 0, kHeaders = 1, kRstStream = 3, kSettings = 4, kPing = 6, kGoaway = 7, kWindowUpdate = 8, kContinuation = 9
+};
 enum : uint8_t { kEndStream = 0x1, kAck = 0x1, kEndHeaders = 0x4, kPadded = 0x8, kPriority = 0x20 };
 constexpr uint32_t kWindow = 16u << 20;
 
@@ -83,8 +87,39 @@ bool write_all(int fd, const std::string& b, int64_t deadline_ns) {
 
 }  // namespace
 
+const char* grpc_code_name(int code) {
+  static const char* const n[] = {"OK", "CANCELLED", "UNKNOWN", "INVALID_ARGUMENT", "DEADLINE_EXCEEDED",
+                                  "NOT_FOUND", "ALREADY_EXISTS", "PERMISSION_DENIED", "RESOURCE_EXHAUSTED",
+                                  "FAILED_PRECONDITION", "ABORTED", "OUT_OF_RANGE", "UNIMPLEMENTED", "INTERNAL",
+                                  "UNAVAILABLE", "DATA_LOSS", "UNAUTHENTICATED"};
+  return code >= 0 && code <= 16 ? n[code] : "UNKNOWN_CODE";
+}
+
+std::string grpc_percent_decode(std::string_view s) {
+  auto hex = [](char c) -> int {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  };
+  std::string o;
+  o.reserve(s.size());
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && hex(s[i + 1]) >= 0 && hex(s[i + 2]) >= 0) {
+      o.push_back(static_cast<char>(hex(s[i + 1]) * 16 + hex(s[i + 2])));
+      i += 2;
+    } else {
+      o.push_back(s[i]);
+    }
+  }
+  return o;
+}
+
 bool grpc_unary_unix(const std::string& socket_path, const std::string& path, const std::string& request,
-                     std::string* response, std::string* err, int timeout_ms) {
+                     std::string* response, std::string* err, int timeout_ms, GrpcStatus* status_out) {
+  GrpcStatus local;
+  GrpcStatus& st = status_out ? *status_out : local;
+  st = GrpcStatus{};
   const int64_t deadline = mono_ns() + static_cast<int64_t>(timeout_ms) * 1000000;
   std::string path_only = socket_path;
   if (path_only.rfind("unix://", 0) == 0) path_only = path_only.substr(7);
@@ -141,6 +176,26 @@ bool grpc_unary_unix(const std::string& socket_path, const std::string& path, co
 
   std::string in, body;
   bool ended = false;
+  HpackDecoder hpack;      // one per connection: the dynamic table spans header blocks
+  std::string hblock;      // header block being assembled (HEADERS + CONTINUATION)
+  bool in_block = false, block_ends_stream = false;
+  auto finish_block = [&]() -> bool {
+    HeaderList fields;
+    std::string herr;
+    if (!hpack.decode(hblock, &fields, &herr)) {
+      *err = herr;
+      return false;
+    }
+    for (const auto& [k, v] : fields) {
+      if (k == ":status") st.http_status = atoi(v.c_str());
+      else if (k == "grpc-status") st.code = atoi(v.c_str());
+      else if (k == "grpc-message") st.message = grpc_percent_decode(v);
+    }
+    hblock.clear();
+    in_block = false;
+    if (block_ends_stream) ended = true;
+    return true;
+  };
   while (!ended) {
     // parse complete frames
     while (in.size() >= 9) {
@@ -178,8 +233,34 @@ bool grpc_unary_unix(const std::string& socket_path, const std::string& path, co
         }
         body.append(pl.substr(start, pl.size() - start - pad));
         if (flags & kEndStream) ended = true;
-      } else if (type == kHeaders && stream == 1 && (flags & kEndStream)) {
-        ended = true;  // trailers (grpc-status); not decoded, success is judged by the body
+      } else if ((type == kHeaders || type == kContinuation) && stream == 1) {
+        // response headers, trailers, or a Trailers-Only error response
+        if ((type == kHeaders) == in_block) {
+          *err = "malformed header block sequence";
+          return false;
+        }
+        std::string_view frag = pl;
+        if (type == kHeaders) {
+          size_t pad = 0, start = 0;
+          if (flags & kPadded) {
+            if (frag.empty()) {
+              *err = "bad padded HEADERS";
+              return false;
+            }
+            pad = static_cast<uint8_t>(frag[0]);
+            start = 1;
+          }
+          if (flags & kPriority) start += 5;
+          if (start + pad > frag.size()) {
+            *err = "bad HEADERS padding";
+            return false;
+          }
+          frag = frag.substr(start, frag.size() - start - pad);
+          in_block = true;
+          block_ends_stream = flags & kEndStream;
+        }
+        hblock.append(frag);
+        if ((flags & kEndHeaders) && !finish_block()) return false;
       }
       if (!reply.empty() && !write_all(fd, reply, deadline)) {
         *err = "write failed";
@@ -212,8 +293,19 @@ bool grpc_unary_unix(const std::string& socket_path, const std::string& path, co
       return false;
     }
   }
+  if (st.http_status != 0 && st.http_status != 200) {
+    *err = "HTTP :status " + std::to_string(st.http_status) + (st.code >= 0 ? std::string(", grpc-status ") +
+           std::to_string(st.code) + " " + grpc_code_name(st.code) : std::string());
+    return false;
+  }
+  if (st.code > 0) {
+    *err = "grpc-status " + std::to_string(st.code) + " " + grpc_code_name(st.code) +
+           (st.message.empty() ? std::string() : ": " + st.message);
+    return false;
+  }
   if (body.size() < 5) {
-    *err = "no gRPC message in the response (server-side error status?)";
+    *err = st.code == 0 ? "grpc-status 0 OK without a response message"
+                        : "no gRPC message and no grpc-status in the response";
     return false;
   }
   const uint32_t mlen = (static_cast<uint8_t>(body[1]) << 24) | (static_cast<uint8_t>(body[2]) << 16) |
@@ -403,10 +495,10 @@ bool parse_list_pod_resources(std::string_view msg, const std::string& resource_
 
 bool podresources_list(const std::string& socket_path, const std::string& resource_prefix,
                        std::vector<PodDeviceRow>* out, std::string* err, int timeout_ms,
-                       const std::vector<std::string>& dra_drivers) {
+                       const std::vector<std::string>& dra_drivers, GrpcStatus* status) {
   std::string resp;
   out->clear();
-  if (!grpc_unary_unix(socket_path, "/v1.PodResourcesLister/List", "", &resp, err, timeout_ms)) return false;
+  if (!grpc_unary_unix(socket_path, "/v1.PodResourcesLister/List", "", &resp, err, timeout_ms, status)) return false;
   if (!parse_list_pod_resources(resp, resource_prefix, out, dra_drivers)) {
     *err = "malformed ListPodResourcesResponse";
     return false;
@@ -518,17 +610,38 @@ bool parse_cri_sandboxes(std::string_view msg, std::vector<CriSandbox>* out) {
 }
 
 bool cri_list(const std::string& socket_path, std::vector<CriContainer>* containers, std::vector<CriSandbox>* sandboxes,
-              std::string* err, int timeout_ms) {
+              std::string* err, int timeout_ms, GrpcStatus* status) {
   containers->clear();
   sandboxes->clear();
+  // runtime.v1 first; a runtime that answers UNIMPLEMENTED (containerd < 1.7, older cri-o) speaks
+  // runtime.v1alpha2, whose List* messages are wire-identical. The version that worked is remembered
+  // per socket.
+  static std::mutex mu;
+  static std::map<std::string, std::string> api_of;
+  std::string api;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = api_of.find(socket_path);
+    api = it == api_of.end() ? "runtime.v1" : it->second;
+  }
+  GrpcStatus local;
+  GrpcStatus& st = status ? *status : local;
   std::string resp;
-  if (!grpc_unary_unix(socket_path, "/runtime.v1.RuntimeService/ListContainers", "", &resp, err, timeout_ms))
-    return false;
+  if (!grpc_unary_unix(socket_path, "/" + api + ".RuntimeService/ListContainers", "", &resp, err, timeout_ms, &st)) {
+    if (st.code != 12 || api != "runtime.v1") return false;
+    api = "runtime.v1alpha2";
+    if (!grpc_unary_unix(socket_path, "/" + api + ".RuntimeService/ListContainers", "", &resp, err, timeout_ms, &st))
+      return false;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu);
+    api_of[socket_path] = api;
+  }
   if (!parse_cri_containers(resp, containers)) {
     *err = "malformed ListContainersResponse";
     return false;
   }
-  if (!grpc_unary_unix(socket_path, "/runtime.v1.RuntimeService/ListPodSandbox", "", &resp, err, timeout_ms))
+  if (!grpc_unary_unix(socket_path, "/" + api + ".RuntimeService/ListPodSandbox", "", &resp, err, timeout_ms, &st))
     return false;
   if (!parse_cri_sandboxes(resp, sandboxes)) {
     *err = "malformed ListPodSandboxResponse";

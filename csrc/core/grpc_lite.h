@@ -8,8 +8,9 @@
 // HTTP/2 subset: prior-knowledge preface, SETTINGS (+ACK), PING ACK, one request stream with
 // HPACK literal (never-indexed, non-Huffman) request headers, a 16 MiB receive window so large
 // responses need no WINDOW_UPDATE round-trips, DATA reassembly, RST_STREAM/GOAWAY as errors.
-// Response headers are not decoded (HPACK/Huffman): a call succeeds iff a complete gRPC message
-// arrives on the stream before it ends.
+// Response headers and trailers (HEADERS + CONTINUATION) are HPACK-decoded (hpack.h): the call's
+// :status, grpc-status and grpc-message decide success, so Unimplemented / PermissionDenied /
+// version skew from the kubelet or the runtime are reported as such.
 #pragma once
 
 #include <cstdint>
@@ -20,9 +21,21 @@
 
 namespace gpumon {
 
-// Unary call: `path` like "/v1.PodResourcesLister/List", `request` = serialized protobuf.
+// Outcome of a call as the server reported it.
+struct GrpcStatus {
+  int code = -1;          // grpc-status (0 OK ... 16 UNAUTHENTICATED); -1 = none received (transport failure)
+  std::string message;    // grpc-message, percent-decoded
+  int http_status = 0;    // :status of the response headers
+};
+const char* grpc_code_name(int code);  // "UNIMPLEMENTED", ... ("UNKNOWN_CODE" out of range)
+// "%XX" sequences of a grpc-message value decoded (gRPC over HTTP/2 spec).
+std::string grpc_percent_decode(std::string_view s);
+
+// Unary call: `path` like "/v1.PodResourcesLister/List", `request` = serialized protobuf. False
+// with `err` = "grpc-status 12 UNIMPLEMENTED: <message>" (or the transport failure) unless the
+// server answered OK with a message; `status` (optional) receives the server's verdict either way.
 bool grpc_unary_unix(const std::string& socket_path, const std::string& path, const std::string& request,
-                     std::string* response, std::string* err, int timeout_ms = 3000);
+                     std::string* response, std::string* err, int timeout_ms = 3000, GrpcStatus* status = nullptr);
 
 // Protobuf wire-format reader (varint / length-delimited; fixed32/64 skipped).
 class PbReader {
@@ -51,7 +64,7 @@ struct PodDeviceRow {
 // device_id = its device name, else the first CDI device name).
 bool podresources_list(const std::string& socket_path, const std::string& resource_prefix,
                        std::vector<PodDeviceRow>* out, std::string* err, int timeout_ms = 3000,
-                       const std::vector<std::string>& dra_drivers = {});
+                       const std::vector<std::string>& dra_drivers = {}, GrpcStatus* status = nullptr);
 bool parse_list_pod_resources(std::string_view msg, const std::string& resource_prefix,
                               std::vector<PodDeviceRow>* out, const std::vector<std::string>& dra_drivers = {});
 
@@ -69,6 +82,6 @@ struct CriSandbox {
 bool parse_cri_containers(std::string_view msg, std::vector<CriContainer>* out);
 bool parse_cri_sandboxes(std::string_view msg, std::vector<CriSandbox>* out);
 bool cri_list(const std::string& socket_path, std::vector<CriContainer>* containers, std::vector<CriSandbox>* sandboxes,
-              std::string* err, int timeout_ms = 3000);
+              std::string* err, int timeout_ms = 3000, GrpcStatus* status = nullptr);
 
 }  // namespace gpumon

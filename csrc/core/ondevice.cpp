@@ -5,6 +5,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstdlib>
 #include <cctype>
@@ -28,6 +29,10 @@ struct OnDevice::Plugin {
   int (*pmc_agent)(int, gpumon_pmc_agent_t*) = nullptr;
   int (*pmc_sample_many)(const int*, int, const char* const*, int, double, gpumon_pmc_value_t*, int32_t*, char*,
                          size_t) = nullptr;
+  // continuous counting (optional symbols)
+  int (*pmc_read_running)(const int*, int, const char* const*, int, gpumon_pmc_value_t*, int32_t*, int32_t*, char*,
+                          size_t) = nullptr;
+  void (*pmc_stop_running)() = nullptr;
   // probe
   int (*probe_abi)() = nullptr;
   int (*probe_count)() = nullptr;
@@ -67,6 +72,9 @@ std::unique_ptr<OnDevice::Plugin> load_plugin(const std::string& dir, const char
     sym(p->h, "gpumon_pmc_init", &p->pmc_init, &missing);
     sym(p->h, "gpumon_pmc_agent", &p->pmc_agent, &missing);
     sym(p->h, "gpumon_pmc_sample_many", &p->pmc_sample_many, &missing);
+    std::string optional;  // continuous counting: absent -> window mode
+    sym(p->h, "gpumon_pmc_read_running", &p->pmc_read_running, &optional);
+    sym(p->h, "gpumon_pmc_stop_running", &p->pmc_stop_running, &optional);
   } else {
     sym(p->h, "gpumon_probe_abi_version", &p->probe_abi, &missing);
     sym(p->h, "gpumon_probe_device_count", &p->probe_count, &missing);
@@ -160,6 +168,7 @@ PmcDerived pmc_derive(const std::map<std::string, PmcReduced>& raw, const PmcAge
 
 OnDevice::OnDevice(Exporter* ex, OnDeviceConfig cfg) : ex_(ex), cfg_(std::move(cfg)) {
   cfg_.pmc_window_s = std::max(0.001, std::min(cfg_.pmc_window_s, cfg_.pmc_every_s * 0.5));
+  cfg_.pmc_every_s = std::max(0.01, cfg_.pmc_every_s);
   cfg_.probe_timeout_s = std::min(cfg_.probe_timeout_s, cfg_.probe_every_s);
 }
 
@@ -192,9 +201,11 @@ bool OnDevice::start(std::string* err) {
       agents_.push_back(ai);
     }
     map_pmc_agents();
+    pmc_continuous_ = cfg_.pmc_mode != "window" && pmc_lib_->pmc_read_running && pmc_lib_->pmc_stop_running;
     GPUMON_LOG(LogLevel::kInfo, "ondevice",
                "pmc plugin " + pmc_lib_->path + " agents=" + std::to_string(agents_.size()) +
-                   " mapped=" + std::to_string(pmc_map_.size()));
+                   " mapped=" + std::to_string(pmc_map_.size()) +
+                   (pmc_continuous_ ? " mode=continuous" : " mode=window"));
   }
   if (cfg_.probe) {
     probe_lib_ = load_plugin(dir, "libgpumon_probe.so", false, err);
@@ -223,6 +234,7 @@ void OnDevice::stop() {
   }
   if (pmc_th_.joinable()) pmc_th_.join();
   if (probe_th_.joinable()) probe_th_.join();
+  if (pmc_lib_ && pmc_continuous_) pmc_lib_->pmc_stop_running();  // release the device counters
   if (probe_lib_) {
     std::lock_guard<std::mutex> g(probe_mu_);
     gpumon_probe_result_t r{};
@@ -238,7 +250,20 @@ void OnDevice::stop() {
 }
 
 bool OnDevice::step() {
-  if (pmc_lib_) pmc_step();
+  if (pmc_lib_) {
+    pmc_step();
+    // continuous mode: a first read only starts the counting; a synchronous step (tests, --once)
+    // must produce values, so read again after one window
+    bool empty;
+    {
+      std::lock_guard<std::mutex> g(pmc_mu_);
+      empty = pmc_continuous_ && pmc_last_.empty() && pmc_up_;
+    }
+    if (empty) {
+      std::this_thread::sleep_for(std::chrono::duration<double>(cfg_.pmc_window_s));
+      pmc_step();
+    }
+  }
   if (probe_lib_) probe_step();
   return pmc_lib_ || probe_lib_;
 }
@@ -247,6 +272,8 @@ OnDevice::Stats OnDevice::stats() const {
   Stats s;
   s.pmc_samples = pmc_samples_;
   s.pmc_errors = pmc_errors_;
+  s.pmc_resets = pmc_resets_;
+  s.pmc_continuous = pmc_continuous_;
   s.probe_done = probe_done_;
   s.probe_timeouts = probe_timeouts_;
   s.pmc_agents = static_cast<int>(agents_.size());
@@ -279,6 +306,47 @@ void OnDevice::pmc_step() {
     devs.push_back(kv.first);
     ags.push_back(kv.second);
   }
+  if (pmc_continuous_) pmc_step_continuous(devs, ags);
+  else pmc_step_window(devs, ags);
+  export_pmc();
+}
+
+namespace {
+PmcReduced to_reduced(const gpumon_pmc_value_t& v) {
+  PmcReduced r;
+  r.sum = v.sum;
+  r.max = v.max;
+  r.n = v.n;
+  r.by_xcc.assign(v.by_xcc, v.by_xcc + std::max(0, std::min<int>(v.n_xcc, GPUMON_PMC_MAX_XCC)));
+  return r;
+}
+}  // namespace
+
+// Wall-time MFMA utilisation: the active-cycle share times the share of WALL time the GPU was
+// active. GRBM_COUNT cannot give the latter -- the shader clock drops while idle (2.25 -> 1.58 GHz
+// in a 500 ms on / off burst on MI355X), so cycle shares over-weight busy time -- but the
+// firmware's gfx activity accumulator is wall-time based: the product tracks event-timed duty
+// loads within 3 points, bursts included (profiles/r2_pmc_continuous.md).
+void OnDevice::finish_derived(int dev, PmcDerived* d) {
+  double act = kNaN;
+  std::array<double, kMaxXcc> xcd_act{};
+  int n_xcd = 0;
+  const auto rates = ex_->rates();
+  if (dev >= 0 && dev < static_cast<int>(rates.size()) && rates[dev].valid) {
+    act = rates[dev].gfx_activity_avg_pct;
+    n_xcd = rates[dev].n_xcd;
+    xcd_act = rates[dev].xcd_busy_avg;
+  }
+  if (!has(act)) act = d->gui_active;  // no firmware activity: the cycle share is the best left
+  if (has(d->mfma_busy) && has(act)) d->mfma_util = std::min(100.0, d->mfma_busy * act / 100.0);
+  d->xcd_mfma_util.clear();
+  for (size_t x = 0; x < d->xcd_mfma_busy.size(); ++x) {
+    const double a = static_cast<int>(x) < n_xcd && has(xcd_act[x]) ? xcd_act[x] : act;
+    if (has(a)) d->xcd_mfma_util.push_back(std::min(100.0, d->xcd_mfma_busy[x] * a / 100.0));
+  }
+}
+
+void OnDevice::pmc_step_window(const std::vector<int>& devs, const std::vector<int>& ags) {
   std::vector<const char*> names;
   for (const auto& c : cfg_.pmc_counters) names.push_back(c.c_str());
   std::vector<gpumon_pmc_value_t> vals(devs.size() * names.size());
@@ -290,29 +358,94 @@ void OnDevice::pmc_step() {
                                            ebuf, sizeof ebuf);
   if (rc != 0) {
     pmc_errors_ += devs.size();
+    pmc_up_ = false;
     GPUMON_LOG(LogLevel::kWarn, "ondevice", std::string("pmc sample failed: ") + ebuf);
-  } else {
-    for (size_t k = 0; k < devs.size(); ++k) {
-      if (!ok[k]) {
-        pmc_errors_++;
-        continue;
-      }
-      std::map<std::string, PmcReduced> raw;
-      for (size_t c = 0; c < names.size(); ++c) {
-        const auto& v = vals[k * names.size() + c];
-        if (!v.ok) continue;
-        PmcReduced r;
-        r.sum = v.sum;
-        r.max = v.max;
-        r.n = v.n;
-        r.by_xcc.assign(v.by_xcc, v.by_xcc + std::max(0, std::min<int>(v.n_xcc, GPUMON_PMC_MAX_XCC)));
-        raw[cfg_.pmc_counters[c]] = std::move(r);
-      }
-      pmc_last_[devs[k]] = pmc_derive(raw, agents_[ags[k]], cfg_.pmc_window_s);
-      pmc_samples_++;
-    }
+    return;
   }
-  export_pmc();
+  pmc_up_ = true;
+  for (size_t k = 0; k < devs.size(); ++k) {
+    if (!ok[k]) {
+      pmc_errors_++;
+      continue;
+    }
+    std::map<std::string, PmcReduced> raw;
+    for (size_t c = 0; c < names.size(); ++c)
+      if (vals[k * names.size() + c].ok) raw[cfg_.pmc_counters[c]] = to_reduced(vals[k * names.size() + c]);
+    PmcDerived d = pmc_derive(raw, agents_[ags[k]], cfg_.pmc_window_s);
+    d.span_s = cfg_.pmc_window_s;
+    d.coverage = cfg_.pmc_window_s / cfg_.pmc_every_s;
+    finish_derived(devs[k], &d);
+    pmc_last_[devs[k]] = std::move(d);
+    pmc_samples_++;
+  }
+}
+
+void OnDevice::pmc_step_continuous(const std::vector<int>& devs, const std::vector<int>& ags) {
+  std::vector<const char*> names;
+  for (const auto& c : cfg_.pmc_counters) names.push_back(c.c_str());
+  std::vector<gpumon_pmc_value_t> vals(devs.size() * names.size());
+  std::vector<int32_t> ok(devs.size(), 0);
+  int32_t started = 0;
+  char ebuf[512] = {0};
+  const int rc = pmc_lib_->pmc_read_running(ags.data(), static_cast<int>(ags.size()), names.data(),
+                                            static_cast<int>(names.size()), vals.data(), ok.data(), &started, ebuf,
+                                            sizeof ebuf);
+  const int64_t now = mono_ns();
+  if (rc != 0) {
+    // contexts could not start / be read (another profiler holds the counters?): no values this
+    // step, the series withdrawn (never stale values), and the next step tries again from scratch
+    pmc_errors_ += devs.size();
+    if (pmc_up_) GPUMON_LOG(LogLevel::kWarn, "ondevice", std::string("pmc continuous read failed: ") + ebuf);
+    pmc_up_ = false;
+    pmc_prev_.clear();
+    pmc_last_.clear();
+    return;
+  }
+  pmc_up_ = true;
+  const double dt = pmc_prev_ns_ ? (now - pmc_prev_ns_) * 1e-9 : 0.0;
+  for (size_t k = 0; k < devs.size(); ++k) {
+    if (!ok[k]) {
+      pmc_errors_++;
+      pmc_prev_.erase(devs[k]);
+      pmc_last_.erase(devs[k]);
+      continue;
+    }
+    std::map<std::string, PmcReduced> cur;
+    for (size_t c = 0; c < names.size(); ++c)
+      if (vals[k * names.size() + c].ok) cur[cfg_.pmc_counters[c]] = to_reduced(vals[k * names.size() + c]);
+    auto prev_it = pmc_prev_.find(devs[k]);
+    if (!started && prev_it != pmc_prev_.end() && dt > 0) {
+      // counts are cumulative since the context start: the interval is the difference
+      std::map<std::string, PmcReduced> delta;
+      bool reset = false;
+      for (const auto& [name, v] : cur) {
+        auto p = prev_it->second.find(name);
+        if (p == prev_it->second.end()) continue;
+        PmcReduced d;
+        d.sum = v.sum - p->second.sum;
+        d.max = v.max - p->second.max;
+        d.n = v.n;
+        if (d.sum < 0 || d.max < 0) reset = true;  // restarted underneath us: drop this interval
+        d.by_xcc.resize(v.by_xcc.size());
+        for (size_t x = 0; x < v.by_xcc.size(); ++x)
+          d.by_xcc[x] = v.by_xcc[x] - (x < p->second.by_xcc.size() ? p->second.by_xcc[x] : 0.0);
+        delta[name] = std::move(d);
+      }
+      if (reset) {
+        pmc_resets_++;
+        pmc_last_.erase(devs[k]);
+      } else {
+        PmcDerived d = pmc_derive(delta, agents_[ags[k]], dt);
+        d.span_s = dt;
+        d.coverage = 1.0;
+        finish_derived(devs[k], &d);
+        pmc_last_[devs[k]] = std::move(d);
+        pmc_samples_++;
+      }
+    }
+    pmc_prev_[devs[k]] = std::move(cur);
+  }
+  pmc_prev_ns_ = now;
 }
 
 void OnDevice::export_pmc() {
@@ -320,16 +453,31 @@ void OnDevice::export_pmc() {
   for (const auto& kv : pmc_last_) {
     const int dev = kv.first;
     const PmcDerived& d = kv.second;
+    if (!std::isnan(d.mfma_util))
+      out.push_back(xs("gpu_mfma_util_percent",
+                       "MFMA pipes busy as a share of wall time, in percent: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE "
+                       "x SIMDs) x the firmware's wall-time gfx activity over the interval (every process).",
+                       dev, d.mfma_util));
+    for (size_t x = 0; x < d.xcd_mfma_util.size(); ++x) {
+      out.push_back(xs("gpu_xcd_mfma_util_percent", "MFMA pipes busy as a share of wall time per XCD, in percent.", dev,
+                       d.xcd_mfma_util[x]));
+      out.back().labels.push_back({"xcd", std::to_string(x)});
+    }
     if (!std::isnan(d.mfma_busy))
-      out.push_back(xs("gpu_mfma_busy_percent", "MFMA pipe busy % (rocprofiler device counting).", dev, d.mfma_busy));
+      out.push_back(xs("gpu_mfma_busy_active_percent",
+                       "MFMA pipes busy as a share of the GPU's ACTIVE cycles (GRBM_GUI_ACTIVE), in percent: how "
+                       "matrix-bound the work is while the GPU runs anything; wall-time utilisation is "
+                       "gpu_mfma_util_percent.",
+                       dev, d.mfma_busy));
     for (size_t x = 0; x < d.xcd_mfma_busy.size(); ++x) {
-      out.push_back(xs("gpu_xcd_mfma_busy_percent", "MFMA pipe busy % per XCD.", dev, d.xcd_mfma_busy[x]));
+      out.push_back(xs("gpu_xcd_mfma_busy_active_percent", "MFMA busy share of active cycles per XCD, in percent.",
+                       dev, d.xcd_mfma_busy[x]));
       out.back().labels.push_back({"xcd", std::to_string(x)});
     }
     for (const auto& [dt, tf] : d.mfma_tflops) {
       out.push_back(xs("gpu_mfma_tflops",
                        "Achieved MFMA throughput by operand type in TFLOP/s (512 x SQ_INSTS_VALU_MFMA_MOPS_<type> "
-                       "over the counting window; every process).",
+                       "over the counted interval; every process).",
                        dev, tf));
       out.back().labels.push_back({"dtype", dt});
     }
@@ -337,11 +485,26 @@ void OnDevice::export_pmc() {
       out.push_back(xs("gpu_occupancy_percent", "Resident waves / max waves % from SQ_WAVE_CYCLES (only when configured; counts the profiling process own waves).", dev,
                        d.occupancy));
     if (!std::isnan(d.gui_active))
-      out.push_back(xs("gpu_gui_active_percent", "GRBM GUI active % of the counting window.", dev, d.gui_active));
-    out.push_back(xs("gpu_pmc_window_seconds", "PMC counting window per sample.", dev, cfg_.pmc_window_s));
+      out.push_back(xs("gpu_gui_active_percent",
+                       "GRBM_GUI_ACTIVE / GRBM_COUNT in percent: a share of CYCLES (the clock drops while idle, so it "
+                       "reads above the wall-time activity for bursty loads).",
+                       dev, d.gui_active));
+    out.push_back(xs("gpu_pmc_window_seconds", "Counted time behind the last PMC sample.", dev, d.span_s));
+    if (!std::isnan(d.coverage))
+      out.push_back(xs("gpu_pmc_coverage_ratio",
+                       "Counted time / wall time between PMC samples (1 = continuous counting; window mode: "
+                       "window / period).",
+                       dev, std::min(1.0, d.coverage)));
   }
+  out.push_back(xs("gpumon_pmc_up", "1 if the last PMC step produced values (0: counters unavailable, e.g. held by "
+                                    "another profiler; the pmc series are withdrawn meanwhile).",
+                   -1, pmc_up_ ? 1.0 : 0.0));
   out.push_back(xs("gpumon_pmc_errors_total", "Failed PMC samples.", -1, static_cast<double>(pmc_errors_.load()),
                    "counter"));
+  out.push_back(xs("gpumon_pmc_resets_total",
+                   "Continuous-counting intervals dropped because the counts went backwards (contexts restarted "
+                   "underneath the exporter).",
+                   -1, static_cast<double>(pmc_resets_.load()), "counter"));
   ex_->set_extra("pmc", std::move(out));
 }
 

@@ -39,7 +39,12 @@ struct OnDeviceConfig {
       "SQ_INSTS_VALU_MFMA_MOPS_F64", "SQ_INSTS_VALU_MFMA_MOPS_I8",   "GRBM_GUI_ACTIVE",
       "GRBM_COUNT"};
   double pmc_every_s = 1.0;
-  double pmc_window_s = 0.1;  // counting window per sample (capped at half the period)
+  // "continuous": the counting contexts run all the time and every step reads them without a stop
+  // (cumulative counts, measured on MI355X: profiles/r2_pmc_continuous.md), so 100 % of each
+  // interval is counted; "window": start -> pmc_window_s -> read -> stop per step (the r1 sampler:
+  // aliases bursts longer than the window). Continuous falls back to window when the plugin lacks it.
+  std::string pmc_mode = "continuous";
+  double pmc_window_s = 0.1;  // window mode: counting window per sample (capped at half the period)
   bool probe = false;
   double probe_every_s = 1.0;
   int probe_blocks = 1024;    // one-wave workgroups per launch (>= 4 per CU spreads over all 8 XCDs)
@@ -61,8 +66,13 @@ struct PmcAgentInfo {
 
 // NaN = not derivable from the counters given.
 struct PmcDerived {
-  double mfma_busy = kNaN, occupancy = kNaN, gui_active = kNaN;
-  std::vector<double> xcd_mfma_busy;
+  // mfma_busy: MFMA busy cycles as a share of the GPU's ACTIVE cycles (GRBM_GUI_ACTIVE x SIMDs);
+  // mfma_util: the same as a share of WALL time (x the firmware's wall-time gfx activity, set by
+  // OnDevice); gui_active: active cycles / all cycles (GRBM_COUNT slows while idle: a cycle share).
+  double mfma_busy = kNaN, mfma_util = kNaN, occupancy = kNaN, gui_active = kNaN;
+  std::vector<double> xcd_mfma_busy, xcd_mfma_util;
+  double span_s = 0;      // counted time behind this sample
+  double coverage = kNaN; // counted time / wall time since the previous sample
   std::vector<std::pair<std::string, double>> mfma_tflops;  // (dtype lower-case, TFLOP/s), by name
 };
 
@@ -86,8 +96,9 @@ class OnDevice {
   bool step();
 
   struct Stats {
-    uint64_t pmc_samples = 0, pmc_errors = 0, probe_done = 0, probe_timeouts = 0;
+    uint64_t pmc_samples = 0, pmc_errors = 0, pmc_resets = 0, probe_done = 0, probe_timeouts = 0;
     int pmc_agents = 0, probe_devices = 0;
+    bool pmc_continuous = false;
   };
   Stats stats() const;
 
@@ -97,6 +108,9 @@ class OnDevice {
   void pmc_loop();
   void probe_loop();
   void pmc_step();
+  void pmc_step_window(const std::vector<int>& devs, const std::vector<int>& ags);
+  void pmc_step_continuous(const std::vector<int>& devs, const std::vector<int>& ags);
+  void finish_derived(int dev, PmcDerived* d);
   void probe_step();
   void map_pmc_agents();
   bool create_probes(std::string* err);
@@ -112,6 +126,12 @@ class OnDevice {
   std::vector<PmcAgentInfo> agents_;
   std::map<int, int> pmc_map_;  // exporter device index -> pmc agent index
   std::map<int, PmcDerived> pmc_last_;
+  // continuous mode: the previous read per device and when it was taken
+  std::map<int, std::map<std::string, PmcReduced>> pmc_prev_;
+  int64_t pmc_prev_ns_ = 0;
+  bool pmc_continuous_ = false;
+  int64_t pmc_last_ok_ns_ = 0;  // last step that produced values (window or continuous)
+  bool pmc_up_ = false;
 
   struct ProbeDev {
     int dev = 0;
@@ -134,7 +154,7 @@ class OnDevice {
   std::mutex wait_mu_;
   std::condition_variable wait_cv_;
   std::thread pmc_th_, probe_th_;
-  std::atomic<uint64_t> pmc_samples_{0}, pmc_errors_{0}, probe_done_{0}, probe_timeouts_{0};
+  std::atomic<uint64_t> pmc_samples_{0}, pmc_errors_{0}, pmc_resets_{0}, probe_done_{0}, probe_timeouts_{0};
 };
 
 }  // namespace gpumon

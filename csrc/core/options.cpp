@@ -223,6 +223,7 @@ const std::map<std::string, Setter>& setters() {
       {"ras_every", int_at([](NativeOptions* o) { return &o->cfg.ras_every; })},
       {"ras_slices", int_at([](NativeOptions* o) { return &o->cfg.ras_slices; })},
       {"occ_samples", int_at([](NativeOptions* o) { return &o->cfg.occ_samples; })},
+      {"hide_empty_contexts", bool_at([](NativeOptions* o) { return &o->cfg.hide_empty_contexts; })},
       {"sample_threads", int_at([](NativeOptions* o) { return &o->cfg.sample_threads; })},
       {"device_timeout_s", dbl_at([](NativeOptions* o) { return &o->cfg.device_timeout_s; })},
       {"reinit_after", int_at([](NativeOptions* o) { return &o->cfg.reinit_after; })},
@@ -260,6 +261,7 @@ const std::map<std::string, Setter>& setters() {
       {"probe_every", int_at([](NativeOptions* o) { return &o->probe_every; })},
       {"enable_pmc", bool_at([](NativeOptions* o) { return &o->od.pmc; })},
       {"pmc_counters", list_at([](NativeOptions* o) { return &o->od.pmc_counters; })},
+      {"pmc_mode", str_at([](NativeOptions* o) { return &o->od.pmc_mode; })},
       {"plugin_dir", str_at([](NativeOptions* o) { return &o->od.plugin_dir; })},
       {"activity_acc_scale", dbl_at([](NativeOptions* o) { return &o->cfg.rates.activity_acc_scale; })},
       {"xgmi_kb_bytes", dbl_at([](NativeOptions* o) { return &o->cfg.rates.xgmi_kb_bytes; })},
@@ -486,6 +488,7 @@ std::string options_json(const NativeOptions& o) {
   N("ras_every", c.ras_every);
   N("ras_slices", c.ras_slices);
   N("occ_samples", c.occ_samples);
+  B("hide_empty_contexts", c.hide_empty_contexts);
   N("sample_threads", c.sample_threads);
   N("device_timeout_s", c.device_timeout_s);
   N("reinit_after", c.reinit_after);
@@ -520,6 +523,7 @@ std::string options_json(const NativeOptions& o) {
   N("probe_every", o.probe_every);
   B("enable_pmc", o.od.pmc);
   L("pmc_counters", o.od.pmc_counters);
+  S("pmc_mode", o.od.pmc_mode);
   S("plugin_dir", o.od.plugin_dir);
   N("activity_acc_scale", c.rates.activity_acc_scale);
   N("xgmi_kb_bytes", c.rates.xgmi_kb_bytes);

@@ -660,6 +660,13 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       f.add(hl, static_cast<double>(s.stale_samples));
     }
     {
+      Family f(o, "gpumon_hidden_gpu_contexts",
+               "Processes with a GPU context but no VRAM and no resident waves in the last tick, left out of the "
+               "pod_gpu rows (hide_empty_contexts).",
+               "gauge");
+      f.add(hl, static_cast<double>(s.hidden_contexts));
+    }
+    {
       Family f(o, "gpumon_occupancy_reads_total",
                "KFD cu_occupancy reads made between ticks by the device workers (occ_samples per tick).",
                "counter");

@@ -41,7 +41,7 @@ static void usage() {
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx]\n"
           "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri]\n"
           "                       [--dra-drivers gpu.amd.com,..|none]\n"
-          "                       [--pmc] [--pmc-counters A,B,..] [--pmc-window SEC] [--probe] [--probe-every N]\n"
+          "                       [--pmc] [--pmc-counters A,B,..] [--pmc-mode continuous|window] [--pmc-window SEC] [--probe] [--probe-every N]\n"
           "                       [--probe-blocks N] [--plugin-dir DIR]\n"
           "config keys: the gpumon.* keys of gpumon/config.py (docs/configuration.md), in the file, as\n"
           "GPUMON_<KEY> in the environment, or as the flags above; NODE_NAME and INFLUXDB_URL as in the reference\n");
@@ -122,6 +122,7 @@ int main(int argc, char** argv) {
     else if (a == "--pmc") set("enable_pmc", "true");
     else if (a == "--pmc-counters") set("pmc_counters", next());
     else if (a == "--pmc-window") o.od.pmc_window_s = atof(next().c_str());
+    else if (a == "--pmc-mode") set("pmc_mode", next());
     else if (a == "--probe") set("enable_probe", "true");
     else if (a == "--probe-every") set("probe_every", next());
     else if (a == "--probe-blocks") o.od.probe_blocks = atoi(next().c_str());

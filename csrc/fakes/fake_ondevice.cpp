@@ -11,6 +11,8 @@
 //                           "start" -> continuous counting cannot start (counters held elsewhere)
 //   GPUMON_FAKE_PMC_READ    continuous reads: "cumulative" (default: values since the start) or
 //                           "reset" (values since the previous read)
+//   GPUMON_FAKE_PMC_RESTART every Nth continuous read the counts restart from 0 without the
+//                           started flag (another tool restarted the contexts underneath)
 //   GPUMON_FAKE_PROBE_HANG  1 -> launches never complete (timeouts path)
 #include <cstdio>
 #include <cstdlib>
@@ -161,6 +163,9 @@ EXPORT int gpumon_pmc_read_running(const int* ags, int n_agents, const char* con
     g_t0 = g_last = now;
     if (started) *started = 1;
   }
+  static int reads = 0;
+  const int restart = static_cast<int>(envd("GPUMON_FAKE_PMC_RESTART", 0));
+  if (restart > 0 && ++reads % restart == 0) g_t0 = now - std::chrono::milliseconds(1);
   const char* mode = getenv("GPUMON_FAKE_PMC_READ");
   const bool reset = mode && strcmp(mode, "reset") == 0;
   const double span = std::chrono::duration<double>(now - (reset ? g_last : g_t0)).count();

@@ -88,9 +88,9 @@ def build():
     y += 8
     panels.append(panel("Probe: effective shader clock per XCD (MHz)", "timeseries",
                         [(f'gpu_probe_xcd_clock_mhz{{{HOST}}}', "{{host}} gpu{{gpu_id}} xcd{{xcd}}")], 0, y, 12, 8))
-    panels.append(panel("PMC: MFMA busy % / KFD CU occupancy %", "timeseries",
-                        [(f'gpu_mfma_busy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} mfma busy"),
-                         (f'gpu_cu_occupancy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} CUs occupied")], 12, y, 12, 8,
+    panels.append(panel("PMC: MFMA utilisation % of wall time / KFD wave occupancy %", "timeseries",
+                        [(f'gpu_mfma_util_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} mfma util"),
+                         (f'gpu_cu_occupancy_percent{{{HOST}}}', "{{host}} gpu{{gpu_id}} wave slots held")], 12, y, 12, 8,
                         fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
     y += 8
     panels.append(panel("PMC: achieved MFMA TFLOP/s by operand type", "timeseries",

@@ -30,7 +30,8 @@ class FakePod:
 
 
 class FakeKubelet:
-    def __init__(self, podres_socket: str = "", cri_socket: str = "", resource_name: str = "amd.com/gpu"):
+    def __init__(self, podres_socket: str = "", cri_socket: str = "", resource_name: str = "amd.com/gpu",
+                 cri_api: str = "runtime.v1"):
         self.podres_socket = podres_socket
         self.cri_socket = cri_socket
         self.resource_name = resource_name
@@ -38,11 +39,16 @@ class FakeKubelet:
         self.allocatable: List[str] = []
         self.calls = {"list": 0, "containers": 0, "sandboxes": 0}
         self.fail_cri = False
+        # (grpc.StatusCode, message) the PodResources List() answers with instead of a response
+        self.podres_error = None
+        self.cri_api = cri_api  # "runtime.v1" | "runtime.v1alpha2" (containerd < 1.7)
         self._servers = []
 
     # ---------------------------------------------------------------- handlers
     def _list(self, req, ctx):
         self.calls["list"] += 1
+        if self.podres_error is not None:
+            ctx.abort(*self.podres_error)
         r = P.ListPodResourcesResponse()
         for p in self.pods:
             pr = r.pod_resources.add(name=p.name, namespace=p.namespace)
@@ -115,7 +121,7 @@ class FakeKubelet:
             self._servers.append(s)
         if self.cri_socket:
             s = grpc.server(futures.ThreadPoolExecutor(max_workers=2))
-            s.add_generic_rpc_handlers((grpc.method_handlers_generic_handler("runtime.v1.RuntimeService", {
+            s.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(f"{self.cri_api}.RuntimeService", {
                 "Version": h(self._version, P.VersionRequest, P.VersionResponse),
                 "ListContainers": h(self._containers, P.ListContainersRequest, P.ListContainersResponse),
                 "ListPodSandbox": h(self._sandboxes, P.ListPodSandboxRequest, P.ListPodSandboxResponse),

@@ -40,6 +40,7 @@ class Config:
     link_every: int = 600                 # ticks between link-metrics refreshes (+ whenever a link's state changes)
     ras_every: int = 5                    # ticks per full RAS / ECC pass (0 = off)
     ras_slices: int = 1                   # the pass read in this many slices on consecutive ticks (1..ras_every)
+    hide_empty_contexts: bool = True      # no pod_gpu row for a GPU context with no VRAM and no waves
     occ_samples: int = 10                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
     device_timeout_s: float = 2.0         # a device call still running after this is exported as hung
@@ -70,7 +71,7 @@ class Config:
     procfs_env_fallback: bool = True
     include_host_processes: bool = True
     # control plane (k8s)
-    control_plane: str = "python"         # python (grpcio clients) | native (C++ grpc_lite pollers) | off
+    control_plane: str = "native"         # native (C++ grpc_lite pollers: production) | python (grpcio clients: test oracle) | off
     cri_socket: str = ""                  # e.g. unix:///run/containerd/containerd.sock ; "" = autodetect
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     resource_names: List[str] = field(default_factory=lambda: ["amd.com/gpu"])
@@ -87,6 +88,9 @@ class Config:
     # the counters gpumon.ops.pmc.derive() needs (8 SQ + 2 GRBM slots: one counting pass on gfx950):
     # MFMA busy + MFMA MOPS per operand type; no per-wave SQ counters (they count only the profiling
     # process's own waves, profiles/r1_pmc_cross_process.md)
+    # continuous: counting contexts run all the time, read without a stop (100 % coverage);
+    # window: start -> pmc_window -> stop per period (the r1 sampler)
+    pmc_mode: str = "continuous"
     pmc_counters: List[str] = field(default_factory=lambda: (
         ["SQ_VALU_MFMA_BUSY_CYCLES"] + ["SQ_INSTS_VALU_MFMA_MOPS_" + d for d in
                                         ("BF16", "F16", "F8", "F6F4", "F32", "F64", "I8")]
@@ -123,6 +127,7 @@ class Config:
             "ras_every": int(self.ras_every),
             "ras_slices": int(self.ras_slices),
             "occ_samples": int(self.occ_samples),
+            "hide_empty_contexts": bool(self.hide_empty_contexts),
             "sample_threads": int(self.sample_threads),
             "device_timeout_s": float(self.device_timeout_s),
             "reinit_after": int(self.reinit_after),

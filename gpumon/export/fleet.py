@@ -35,7 +35,7 @@ def gpu_rows(fam: dict) -> List[dict]:
     hot = _per_gpu(fam, "gpu_temperature_celsius", sensor="hotspot")
     gfx = _per_gpu(fam, "gpu_clock_mhz", clock="gfx")
     up = _per_gpu(fam, "gpu_up")
-    mfma = _per_gpu(fam, "gpu_mfma_busy_percent")
+    mfma = _per_gpu(fam, "gpu_mfma_util_percent")
     xcd: Dict[Key, Dict[int, float]] = defaultdict(dict)
     for n, labels, v in fam.get("gpu_xcd_busy_percent", {"samples": []})["samples"]:
         xcd[(labels.get("host", "?"), labels.get("gpu_id", "?"))][int(labels.get("xcd", 0))] = v

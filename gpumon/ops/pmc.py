@@ -3,8 +3,12 @@
 Exported per GPU (derived with the gfx9xx formulas ROCm 7.2 falls back to for gfx950, see
 MI355X_MICROARCH.md §rocprofv3 PMC slots):
 
-* ``gpu_mfma_busy_percent``      = 100 * sum(SQ_VALU_MFMA_BUSY_CYCLES) / (max(GRBM_GUI_ACTIVE) * SIMDs)
-* ``gpu_xcd_mfma_busy_percent``  = the same per XCC (when the counter carries an XCC dimension)
+* ``gpu_mfma_busy_active_percent``     = 100 * sum(SQ_VALU_MFMA_BUSY_CYCLES) / (max(GRBM_GUI_ACTIVE) * SIMDs)
+* ``gpu_xcd_mfma_busy_active_percent`` = the same per XCC (when the counter carries an XCC dimension)
+
+This runner (windowed counting, no wall-time MFMA utilisation) is the TEST ORACLE for the
+production path, the native samplers of csrc/core/ondevice.cpp (continuous counting,
+``gpu_mfma_util_percent``); `gpumon serve` uses the native one unless ``--ondevice python``.
 * ``gpu_mfma_tflops{dtype}``     = 512 * sum(SQ_INSTS_VALU_MFMA_MOPS_<DTYPE>) / window / 1e12
   (achieved matrix-core throughput per operand type: bf16, f16, f8, f6f4, f32, f64, i8)
 * ``gpu_gui_active_percent``     = 100 * max(GRBM_GUI_ACTIVE) / max(GRBM_COUNT)
@@ -141,9 +145,11 @@ class PmcRunner:
 
         for dev, d in self.last.items():
             if "mfma_busy" in d:
-                add("gpu_mfma_busy_percent", "MFMA pipe busy % (rocprofiler device counting).", dev, d["mfma_busy"])
+                add("gpu_mfma_busy_active_percent", "MFMA busy share of active cycles (windowed, Python oracle).",
+                    dev, d["mfma_busy"])
             for x, v in enumerate(d.get("xcd_mfma_busy", [])):
-                add("gpu_xcd_mfma_busy_percent", "MFMA pipe busy % per XCD.", dev, v, {"xcd": str(x)})
+                add("gpu_xcd_mfma_busy_active_percent", "MFMA busy share of active cycles per XCD.", dev, v,
+                    {"xcd": str(x)})
             for dt, v in sorted(d.get("mfma_tflops", {}).items()):
                 add("gpu_mfma_tflops", TFLOPS_HELP, dev, v, {"dtype": dt})
             if "occupancy" in d:

@@ -63,6 +63,8 @@ def _plugin_metric_names():
     for f in os.listdir(os.path.join(ROOT, "gpumon/ops")):
         if f.endswith(".py"):
             names |= set(re.findall(r'"(gpu_[a-z0-9_]+)"', open(os.path.join(ROOT, "gpumon/ops", f)).read()))
+    # the production on-device samplers (native)
+    names |= set(re.findall(r'"(gpu_[a-z0-9_]+)"', open(os.path.join(ROOT, "csrc/core/ondevice.cpp")).read()))
     return names
 
 

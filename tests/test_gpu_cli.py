@@ -22,11 +22,12 @@ def test_once_with_probe_and_pmc():
     assert promtext.one(fam, "node_gpu_mem_total", gpu_id="0") > 250000
     assert len(promtext.values(fam, "gpu_probe_xcd_clock_mhz", gpu_id="0")) == 8
     assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
-    assert promtext.values(fam, "gpu_mfma_busy_percent", gpu_id="0")
+    assert promtext.values(fam, "gpu_mfma_util_percent", gpu_id="0")
+    assert promtext.values(fam, "gpu_mfma_busy_active_percent", gpu_id="0")
     assert promtext.values(fam, "gpu_mfma_tflops", gpu_id="0", dtype="bf16")
     assert not promtext.values(fam, "gpu_occupancy_percent")  # no per-wave counters by default
     assert promtext.values(fam, "gpu_cu_occupancy_percent", gpu_id="0")
-    assert len(promtext.values(fam, "gpu_xcd_mfma_busy_percent", gpu_id="0")) == 8
+    assert len(promtext.values(fam, "gpu_xcd_mfma_busy_active_percent", gpu_id="0")) == 8
     assert promtext.one(fam, "gpumon_backend_calls_total", call="gpu_metrics") >= 2
 
 
@@ -48,7 +49,7 @@ def test_once_python_runners():
     assert r.returncode == 0, r.stderr[-3000:]
     fam = promtext.parse(r.stdout)
     assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
-    assert promtext.values(fam, "gpu_mfma_busy_percent", gpu_id="0")
+    assert promtext.values(fam, "gpu_mfma_busy_active_percent", gpu_id="0")
 
 
 def test_native_binary_pmc_probe_under_mfma_load():
@@ -65,6 +66,9 @@ def test_native_binary_pmc_probe_under_mfma_load():
         r = subprocess.run([exe, "--backend", "amdsmi", "--once", "--host", "box", "--pmc", "--probe",
                             "--pmc-window", "0.2", "--log-level", "warn"], capture_output=True, text=True,
                            timeout=120)
+        rw = subprocess.run([exe, "--backend", "amdsmi", "--once", "--host", "box", "--pmc", "--pmc-mode", "window",
+                             "--pmc-window", "0.2", "--log-level", "warn"], capture_output=True, text=True,
+                            timeout=120)
     finally:
         try:
             load.wait(60)  # let the burn finish on its own (no kill mid-kernel)
@@ -73,12 +77,18 @@ def test_native_binary_pmc_probe_under_mfma_load():
             load.wait(30)
     assert r.returncode == 0, r.stderr[-2000:]
     fam = promtext.parse(r.stdout)
-    assert promtext.one(fam, "gpu_mfma_busy_percent", gpu_id="0") > 50
+    assert promtext.one(fam, "gpu_mfma_busy_active_percent", gpu_id="0") > 50
+    assert promtext.one(fam, "gpu_mfma_util_percent", gpu_id="0") > 50  # the burn runs all the time
+    assert promtext.one(fam, "gpu_pmc_coverage_ratio", gpu_id="0") == 1  # continuous counting
     # the burn runs in ANOTHER process: the MOPS counters see it (per-wave SQ counters would not)
     assert promtext.one(fam, "gpu_mfma_tflops", gpu_id="0", dtype="bf16") > 1000
     assert promtext.one(fam, "gpu_cu_occupancy_percent", gpu_id="0") > 90  # KFD: every CU holds burn waves
-    assert len(promtext.values(fam, "gpu_xcd_mfma_busy_percent", gpu_id="0")) == 8
-    assert promtext.one(fam, "gpu_pmc_window_seconds", gpu_id="0") == pytest.approx(0.2)
+    assert len(promtext.values(fam, "gpu_xcd_mfma_util_percent", gpu_id="0")) == 8
+    assert promtext.one(fam, "gpu_pmc_window_seconds", gpu_id="0") == pytest.approx(0.2, rel=0.5)
+    assert rw.returncode == 0, rw.stderr[-2000:]
+    famw = promtext.parse(rw.stdout)  # the windowed sampler still works on hardware
+    assert promtext.one(famw, "gpu_mfma_busy_active_percent", gpu_id="0") > 50
+    assert promtext.one(famw, "gpu_pmc_window_seconds", gpu_id="0") == pytest.approx(0.2)
     assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
     assert promtext.one(fam, "gpu_probe_unique_cus", gpu_id="0") > 200
 

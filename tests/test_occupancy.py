@@ -69,3 +69,21 @@ def test_occ_samples_one_disables_subsampling(mock_exporter):
     _wait_ticks(ex, 3)
     assert ex.self_stats()["occupancy_reads"] == 0
     assert all(r["occ_samples"] == 1 for r in ex.pod_rows() if r["pid"] == "5")
+
+
+def test_empty_contexts_are_hidden_but_counted(mock_exporter):
+    """A process with a GPU context but no VRAM and no waves (a runtime that only probed the device)
+    is not a workload: no pod_gpu row (BENCH_r01 showed such a 0-MiB pid), counted instead."""
+    procs = [{"pid": 21, "device": 0, "name": "train", "kfd_only": True},
+             {"pid": 22, "device": 0, "name": "rocminfo", "kfd_only": True, "vram_bytes": 0}]
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0, mock={"procs": procs})
+    ex.mock_set_occ_series(0, [100.0, 0.0])  # pid 21 reads 100, pid 22 reads 0
+    ex.tick()
+    assert [r["pid"] for r in ex.pod_rows() if not r["idle"]] == ["21"]
+    assert ex.self_stats()["hidden_contexts"] == 1
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpumon_hidden_gpu_contexts") == 1
+    ex2 = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0, mock={"procs": procs},
+                        hide_empty_contexts=False)
+    ex2.tick()
+    assert sorted(r["pid"] for r in ex2.pod_rows() if not r["idle"]) == ["21", "22"]

@@ -36,7 +36,7 @@ def _val(text, name, **labels):
 
 def _ondevice(core, ex, **over):
     cfg = {"plugin_dir": FAKE_DIR, "pmc": True, "probe": True, "pmc_every_s": 0.2, "probe_every_s": 0.2,
-           "pmc_window_s": 0.01}
+           "pmc_window_s": 0.01, "pmc_mode": "window"}
     cfg.update(over)
     return core.OnDevice(ex, cfg)
 
@@ -93,7 +93,9 @@ def test_native_samplers_export_series(core, mock_exporter, monkeypatch):
         ex.tick()
         m = ex.metrics_text()
         for g in ("0", "1"):
-            assert _val(m, "gpu_mfma_busy_percent", gpu_id=g) == pytest.approx(75.0)
+            assert _val(m, "gpu_mfma_busy_active_percent", gpu_id=g) == pytest.approx(75.0)
+            assert 0 < _val(m, "gpu_mfma_util_percent", gpu_id=g) <= 75.0  # x wall-time activity
+            assert _val(m, "gpu_pmc_coverage_ratio", gpu_id=g) == pytest.approx(0.01 / 0.2)
             assert _val(m, "gpu_mfma_tflops", gpu_id=g, dtype="bf16") == pytest.approx(2000.0)
             assert _val(m, "gpu_mfma_tflops", gpu_id=g, dtype="f16") == pytest.approx(200.0)
             assert _val(m, "gpu_mfma_tflops", gpu_id=g, dtype="f64") == 0
@@ -101,7 +103,7 @@ def test_native_samplers_export_series(core, mock_exporter, monkeypatch):
             assert _val(m, "gpu_gui_active_percent", gpu_id=g) == pytest.approx(100.0)
             assert _val(m, "gpu_pmc_window_seconds", gpu_id=g) == pytest.approx(0.01)
             for x in range(8):
-                assert _val(m, "gpu_xcd_mfma_busy_percent", gpu_id=g, xcd=x) == pytest.approx(75.0)
+                assert _val(m, "gpu_xcd_mfma_busy_active_percent", gpu_id=g, xcd=x) == pytest.approx(75.0)
                 assert _val(m, "gpu_probe_xcd_blocks", gpu_id=g, xcd=x) == 1024 / 8
                 assert _val(m, "gpu_probe_xcd_clock_mhz", gpu_id=g, xcd=x) == pytest.approx(2400 - 10 * x)
             assert _val(m, "gpu_probe_unique_cus", gpu_id=g) == 256
@@ -115,7 +117,7 @@ def test_native_samplers_export_series(core, mock_exporter, monkeypatch):
         od.stop()
     ex.tick()
     m = ex.metrics_text()
-    assert "gpu_mfma_busy_percent" not in m and "gpu_probe_pending" not in m  # series withdrawn on stop
+    assert "gpu_mfma_util_percent" not in m and "gpu_probe_pending" not in m  # series withdrawn on stop
 
 
 def test_explicit_wave_counter_gives_occupancy(core, mock_exporter, monkeypatch):
@@ -173,7 +175,7 @@ def test_sample_failures_counted(core, mock_exporter, monkeypatch):
         od.step()
         ex.tick()
         m = ex.metrics_text()
-        assert "gpu_mfma_busy_percent" not in m
+        assert "gpu_mfma_util_percent" not in m
         assert re.search(r'^gpumon_pmc_errors_total\{host="node-a"\} [1-9]', m, re.M)  # node-level series
         assert od.stats()["pmc_errors"] >= 1
     finally:
@@ -209,14 +211,15 @@ def _run_bin(*args, env=None):
 def test_binary_pmc_and_probe_flags():
     r = _run_bin("--pmc", "--probe", "--plugin-dir", FAKE_DIR, env={"GPUMON_FAKE_MFMA": "0.25"})
     assert r.returncode == 0, r.stderr
-    assert _val(r.stdout, "gpu_mfma_busy_percent", gpu_id="1") == pytest.approx(25.0)
+    assert _val(r.stdout, "gpu_mfma_busy_active_percent", gpu_id="1") == pytest.approx(25.0)
+    assert _val(r.stdout, "gpu_pmc_coverage_ratio", gpu_id="1") == 1  # continuous by default
     assert _val(r.stdout, "gpu_probe_xcd_blocks", gpu_id="1", xcd="7") == 128
 
 
 def test_binary_plugin_dir_from_env():
     r = _run_bin("--probe", env={"GPUMON_PLUGIN_DIR": FAKE_DIR})
     assert r.returncode == 0, r.stderr
-    assert "gpu_probe_unique_cus" in r.stdout and "gpu_mfma_busy_percent" not in r.stdout
+    assert "gpu_probe_unique_cus" in r.stdout and "gpu_mfma_util_percent" not in r.stdout
 
 
 def test_binary_missing_plugin_exits_nonzero(tmp_path):
@@ -237,7 +240,7 @@ def test_cli_once_native_ondevice(monkeypatch, capsys):
                    "--plugin-dir", FAKE_DIR, "--control-plane", "off"])
     out = capsys.readouterr().out
     assert rc == 0
-    assert _val(out, "gpu_mfma_busy_percent", gpu_id="0") == pytest.approx(50.0)
+    assert _val(out, "gpu_mfma_busy_active_percent", gpu_id="0") == pytest.approx(50.0)
     assert _val(out, "gpu_probe_unique_cus", gpu_id="0") == 256
 
 
@@ -266,3 +269,77 @@ def test_probe_created_once_backend_comes_up(core, monkeypatch):
     finally:
         od.stop()
         ex.stop()
+
+
+# ---------------------------------------------------------------- continuous counting
+def test_continuous_counting_covers_every_interval(core, mock_exporter, monkeypatch):
+    """Contexts stay started; each step reads the cumulative counts and exports the difference
+    since the previous read: the counted span is the whole interval (coverage 1)."""
+    import time
+
+    monkeypatch.setenv("GPUMON_FAKE_MFMA", "0.6")
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
+    od.start()
+    try:
+        od.step()  # starts the contexts and reads again after one window
+        time.sleep(0.15)
+        od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        assert _val(m, "gpu_mfma_busy_active_percent", gpu_id="0") == pytest.approx(60.0)
+        assert _val(m, "gpu_pmc_coverage_ratio", gpu_id="0") == 1
+        assert 0.14 <= _val(m, "gpu_pmc_window_seconds", gpu_id="0") <= 0.5  # the whole gap between reads
+        assert _val(m, "gpu_mfma_tflops", gpu_id="0", dtype="bf16") == pytest.approx(1000.0, rel=0.05)
+        assert _val(m, "gpumon_pmc_up") == 1
+        assert od.stats()["pmc_continuous"] and od.stats()["pmc_errors"] == 0
+    finally:
+        od.stop()
+
+
+def test_continuous_counters_held_elsewhere(core, mock_exporter, monkeypatch):
+    """Another profiler holds the device counters: no values (never stale ones), pmc_up 0, errors
+    counted, and counting resumes once the counters are free again."""
+    import time
+
+    monkeypatch.setenv("GPUMON_FAKE_PMC_FAIL", "start")
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
+    od.start()
+    try:
+        od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        assert _val(m, "gpumon_pmc_up") == 0 and "gpu_mfma_util_percent" not in m
+        assert od.stats()["pmc_errors"] >= 1
+        monkeypatch.delenv("GPUMON_FAKE_PMC_FAIL")
+        od.step()
+        time.sleep(0.05)
+        od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        assert _val(m, "gpumon_pmc_up") == 1 and _val(m, "gpu_mfma_busy_active_percent", gpu_id="0") > 0
+    finally:
+        od.stop()
+
+
+def test_continuous_restart_underneath_drops_the_interval(core, mock_exporter, monkeypatch):
+    """Counts going backwards (contexts restarted by someone else) must not export a negative or
+    garbage interval: it is dropped and counted in gpumon_pmc_resets_total."""
+    import time
+
+    monkeypatch.setenv("GPUMON_FAKE_PMC_RESTART", "3")
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
+    od.start()
+    try:
+        for _ in range(7):
+            od.step()
+            time.sleep(0.03)
+            ex.tick()
+            v = _val(ex.metrics_text(), "gpu_mfma_busy_active_percent", gpu_id="0")
+            assert v is None or 0 <= v <= 100
+        assert od.stats()["pmc_resets"] >= 1
+        assert _val(ex.metrics_text(), "gpumon_pmc_resets_total") >= 1
+    finally:
+        od.stop()

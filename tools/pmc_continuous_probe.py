@@ -68,8 +68,30 @@ def main() -> int:
     def interval_values(seq):
         res = []
         for a, b in zip(seq, seq[1:]):
-            res.append({c: (b[c] - a[c]) if cumulative else b[c] for c in COUNTERS if c in a and c in b})
+            iv = {c: (b[c] - a[c]) if cumulative else b[c] for c in COUNTERS if c in a and c in b}
+            iv["dt"] = b["t"] - a["t"]
+            iv["gfx_act"] = b.get("gfx_act")
+            iv["gfxclk"] = b.get("gfxclk")
+            res.append(iv)
         return res
+
+    # firmware-side view of the same intervals: amdsmi gfx activity accumulator (wall-time busy %)
+    # and the average gfx clock, from the exporter ticked at each continuous read
+    from gpumon import core as _core
+
+    ex = _core().Exporter({"backend": "amdsmi", "devices": [0], "serve_http": False, "interval_s": 0.0,
+                           "processes": False, "ras_every": 0})
+    ex_err = ex.start()
+    if ex_err:
+        log("exporter:", ex_err)
+
+    def fw():
+        if ex_err:
+            return {}
+        ex.tick()
+        r = ex.rates()[0]
+        f = ex.samples()[0]["fields"]
+        return {"gfx_act": r.get("gfx_activity_avg_pct"), "gfxclk": f.get("gfxclk_avg") or f.get("gfxclk_cur")}
 
     # ---- 2. accuracy per pattern
     patterns = [("full", 1.0, 0.0), ("duty25", 0.25, 0.0), ("duty50", 0.5, 0.0), ("duty75", 0.75, 0.0),
@@ -84,11 +106,11 @@ def main() -> int:
         seq = []
         for _ in range(int(secs) + 1):
             r = _pmc.read_running([0], COUNTERS)
-            seq.append({"t": time.perf_counter(), **vals(r["agents"][0] or {})})
+            seq.append({"t": time.perf_counter(), **vals(r["agents"][0] or {}), **fw()})
             time.sleep(1.0)
         _pmc.stop_running()
-        cont = []
-        for iv in interval_values(seq):
+        cont, raw = [], interval_values(seq)
+        for iv in raw:
             if iv.get("GRBM_COUNT"):
                 cont.append(100.0 * iv["SQ_VALU_MFMA_BUSY_CYCLES"] / (iv["GRBM_COUNT"] * simds))
         # (b) windowed: 0.2 s window per second (the r1 sampler)
@@ -107,14 +129,20 @@ def main() -> int:
                "cont_mean": statistics.fmean(cont) if cont else None,
                "cont_sd": statistics.pstdev(cont) if len(cont) > 1 else None, "cont": cont,
                "win_mean": statistics.fmean(win) if win else None,
-               "win_sd": statistics.pstdev(win) if len(win) > 1 else None, "win": win}
+               "win_sd": statistics.pstdev(win) if len(win) > 1 else None, "win": win, "raw": raw}
         if name == "full":
             full_busy = row["cont_mean"]
         if full_busy and busy_frac is not None:
             row["expected"] = full_busy * busy_frac
         out["patterns"].append(row)
         log(json.dumps({k: (round(v, 2) if isinstance(v, float) else v) for k, v in row.items()
-                        if k not in ("cont", "win")}))
+                        if k not in ("cont", "win", "raw")}))
+        if raw:
+            iv = raw[len(raw) // 2]
+            log("   raw:", {k: (round(v / 1e6, 2) if isinstance(v, (int, float)) and v and v > 1e5 else v)
+                            for k, v in iv.items()})
+    if not ex_err:
+        ex.stop()
     print(json.dumps(out, indent=1))
     return 0
 
