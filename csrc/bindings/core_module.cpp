@@ -79,6 +79,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "link_every", &c.link_every);
   get(d, "ras_every", &c.ras_every);
   get(d, "ras_slices", &c.ras_slices);
+  get(d, "ras_async", &c.ras_async);
   get(d, "occ_samples", &c.occ_samples);
   get(d, "hide_empty_contexts", &c.hide_empty_contexts);
   get(d, "sample_threads", &c.sample_threads);

@@ -41,6 +41,7 @@ struct Exporter::DevWorker {
   uint64_t req = 0;              // tick id of the current request
   std::atomic<uint64_t> done{0}; // tick id whose results are stored below
   bool want_links = false, want_procs = false, want_ras = false;
+  bool ras_async = false;        // read the RAS slice AFTER publishing this tick (applied next tick)
   int ras_slice = 0, ras_n = 1;
   int64_t started_ns = 0;
   DeviceSample sample;
@@ -63,9 +64,14 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
   std::vector<double> vals;
   const bool occ_on = occ_period_ns > 0 && backend->supports_occupancy(i);
   int64_t next_occ = 0;
+  // RAS refreshes read off the tick's critical path: the worker reads the slice right after it
+  // published the tick (the files cost 0.25-0.5 ms under load: the slowest tick of every RAS pass,
+  // profiles/r2_bench.md) and the next tick carries the result.
+  RasSample ras_ready;
+  bool have_ras_ready = false;
   while (true) {
     uint64_t id;
-    bool links, procs, ras;
+    bool links, procs, ras, ras_async;
     int ras_slice, ras_n;
     {
       std::unique_lock<std::mutex> lk(w->mu);
@@ -104,6 +110,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       links = w->want_links;
       procs = w->want_procs;
       ras = w->want_ras;
+      ras_async = w->ras_async;
       ras_slice = w->ras_slice;
       ras_n = w->ras_n;
     }
@@ -114,13 +121,18 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       TraceRange tr("gpumon.sample_dev");
       backend->sample(i, &s);
       if (links) backend->sample_links(i, &s);
-      if (ras && s.ok) backend->sample_ras(i, &s, ras_slice, ras_n);
+      if (have_ras_ready && s.ok) {
+        s.ras = std::move(ras_ready);
+        have_ras_ready = false;
+      }
+      if (ras && !ras_async && s.ok) backend->sample_ras(i, &s, ras_slice, ras_n);
       if (procs && s.ok) {
         const int64_t t = mono_ns();
         backend->processes(i, &p);
         pns = mono_ns() - t;
       }
     }
+    const bool ok_for_ras = s.ok;
     // fold the interval's sub-samples into this tick's instantaneous reading
     for (auto& ps : p) {
       if (!has(ps.cu_occupancy)) continue;
@@ -160,8 +172,19 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
         return;
       }
     }
-    std::lock_guard<std::mutex> g(sig->mu);
-    sig->cv.notify_all();
+    {
+      std::lock_guard<std::mutex> g(sig->mu);
+      sig->cv.notify_all();
+    }
+    if (ras && ras_async && ok_for_ras) {
+      TraceRange tr("gpumon.ras_async");
+      DeviceSample scratch;
+      backend->sample_ras(i, &scratch, ras_slice, ras_n);
+      if (scratch.ras.valid) {
+        ras_ready = std::move(scratch.ras);
+        have_ras_ready = true;
+      }
+    }
   }
 }
 
@@ -502,6 +525,7 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
     w.want_links = links_due(i);
     w.ras_slice = ras_slice(i);
     w.want_ras = w.ras_slice >= 0;
+    w.ras_async = cfg_.ras_async && tk > 0;  // the first tick reads synchronously (complete first scrape)
     w.ras_n = ras_n;
     if (w.want_ras) info->ras_reads++;
     w.want_procs = cfg_.processes;

@@ -52,6 +52,7 @@ struct ExporterConfig {
   int link_every = 600;               // ticks between amdsmi_get_link_metrics refreshes (+ on link state change)
   int ras_every = 5;                  // ticks per full RAS / ECC pass (0 = off)
   int ras_slices = 1;                 // the pass read in this many slices on consecutive ticks (1..ras_every)
+  bool ras_async = true;              // device workers read RAS after publishing a tick (next tick carries it)
   int sample_threads = -1;            // parallel device sampling; 0 = sequential, -1 = auto (one per GPU, max 8)
   int occ_samples = 10;               // KFD cu_occupancy reads per process per tick on the device workers (1 = the tick's own)
   bool hide_empty_contexts = true;    // no pod_gpu row for a process with a GPU context but no VRAM and no waves

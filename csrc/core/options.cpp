@@ -222,6 +222,7 @@ const std::map<std::string, Setter>& setters() {
       {"link_every", int_at([](NativeOptions* o) { return &o->cfg.link_every; })},
       {"ras_every", int_at([](NativeOptions* o) { return &o->cfg.ras_every; })},
       {"ras_slices", int_at([](NativeOptions* o) { return &o->cfg.ras_slices; })},
+      {"ras_async", bool_at([](NativeOptions* o) { return &o->cfg.ras_async; })},
       {"occ_samples", int_at([](NativeOptions* o) { return &o->cfg.occ_samples; })},
       {"hide_empty_contexts", bool_at([](NativeOptions* o) { return &o->cfg.hide_empty_contexts; })},
       {"sample_threads", int_at([](NativeOptions* o) { return &o->cfg.sample_threads; })},
@@ -487,6 +488,7 @@ std::string options_json(const NativeOptions& o) {
   N("link_every", c.link_every);
   N("ras_every", c.ras_every);
   N("ras_slices", c.ras_slices);
+  B("ras_async", c.ras_async);
   N("occ_samples", c.occ_samples);
   B("hide_empty_contexts", c.hide_empty_contexts);
   N("sample_threads", c.sample_threads);

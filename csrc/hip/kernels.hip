@@ -377,8 +377,10 @@ void LoadGen::loop(bool alternate, bool mfma, void* stream) {
     check(hipEventCreate(&e0), "hipEventCreate");
     check(hipEventCreate(&e1), "hipEventCreate");
     const int cus = device_cu_count(dev_);
-    // 8 blocks x 4 waves requested per CU (residency then limited by VGPRs: ~7 waves/SIMD at 68 VGPRs)
-    const int burn_blocks = kind_ == "partial" ? cus / 4 : cus * 8;  // partial: ~1/4 of the CUs busy
+    // 8 blocks x 4 waves requested per CU (residency then limited by VGPRs: ~7 waves/SIMD at 68 VGPRs);
+    // partial: ~1/4 of the CUs busy; concurrent: 4 waves per SIMD, leaving wave slots for the HBM
+    // stream's workgroups (with every slot held by the burn the stream got 0.03 TB/s)
+    const int burn_blocks = kind_ == "partial" ? cus / 4 : kind_ == "concurrent" ? cus * 4 : cus * 8;
     // One 16-B vector per lane and one 4 KiB chunk per workgroup, the grid covering the buffer once
     // (no grid-stride loop), nt loads + nt stores: 6.52 TB/s copy on MI355X vs 5.37-5.74 for the
     // earlier 8192 x unroll-4 grid-stride form, 6.20 for PyTorch's elementwise kernel and 4.75 for

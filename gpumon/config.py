@@ -40,6 +40,7 @@ class Config:
     link_every: int = 600                 # ticks between link-metrics refreshes (+ whenever a link's state changes)
     ras_every: int = 5                    # ticks per full RAS / ECC pass (0 = off)
     ras_slices: int = 1                   # the pass read in this many slices on consecutive ticks (1..ras_every)
+    ras_async: bool = True                # device workers read RAS after publishing a tick (next tick carries it)
     hide_empty_contexts: bool = True      # no pod_gpu row for a GPU context with no VRAM and no waves
     occ_samples: int = 10                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
@@ -126,6 +127,7 @@ class Config:
             "link_every": int(self.link_every),
             "ras_every": int(self.ras_every),
             "ras_slices": int(self.ras_slices),
+            "ras_async": bool(self.ras_async),
             "occ_samples": int(self.occ_samples),
             "hide_empty_contexts": bool(self.hide_empty_contexts),
             "sample_threads": int(self.sample_threads),

@@ -56,5 +56,6 @@ def test_influx_extended_carries_ras_totals(mock_exporter):
     ex.mock_add_ecc(0, "umc", ue=1, ce=5)
     ex.mock_add_ecc(0, "gfx", ce=2)
     ex.tick()
+    ex.tick()  # the RAS read runs after a tick is published; the next tick carries it (ras_async)
     (ext,) = [l for l in ex.influx_text().splitlines() if l.startswith("gpu_ext,")]
     assert "ecc_uncorrectable=1" in ext and "ecc_correctable=7" in ext and "retired_pages=0" in ext

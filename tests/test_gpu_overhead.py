@@ -1,0 +1,18 @@
+"""What the exporter costs the workload it watches, on the MI355X (gpumon/ops/tenant.py;
+profiles/r2_tenant_overhead.md). The reference intruded on tenants with `docker exec` into their
+containers every cycle (/root/reference/gpu.py:221); here the exporter is a separate process and
+the tenant's event-timed MFMA throughput must not move by more than 1 % at the default 1 Hz."""
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_default_exporter_costs_the_tenant_under_one_percent():
+    from gpumon.ops.tenant import measure
+
+    r = measure(kinds=("mfma",), conditions=("none", "1hz"), reps=2, window_s=4.0, settle_s=1.5)
+    k = r["kinds"]["mfma"]
+    assert k["none"]["median"] > 1500, k  # the burn really ran (TFLOP/s)
+    assert k["1hz"]["scrapes"] >= 6 and k["1hz"]["scrape_errors"] == 0, k
+    assert k["1hz"]["slowdown_pct"] <= 1.0, k

@@ -121,7 +121,7 @@ def test_refresh_cadence_and_carry_over(mock_exporter):
     ex.mock_add_ecc(0, "umc", ue=1)
     ex.mock_set_ras_event(0, "poison_consumed", 2)
     ex.mock_set_ras_event(0, "bad_pages", 9)
-    for _ in range(3):
+    for _ in range(4):  # read within ras_every ticks, exported on the tick after (ras_async)
         ex.tick()
     fam = promtext.parse(ex.metrics_text())
     assert promtext.one(fam, "gpu_ecc_errors_total", gpu_id="0", block="umc", type="uncorrectable") == 1
@@ -160,11 +160,11 @@ def test_sysfs_refresh_can_be_spread_over_ras_slices_ticks(core, monkeypatch, tm
         (r / "aca_gfx").write_text("ue: 0\nce: 10\nde: 0\n")
         (r / "aca_umc").write_text("ue: 0\nce: 20\nde: 0\n")
         seen = []
-        for _ in range(3):
+        for _ in range(4):
             ex.tick()
             seen.append(ce())
         assert all(s[2] == ["gfx", "umc", "xgmi_wafl"] for s in seen)  # never a partial block set
-        assert seen[-1][:2] == (10, 20)  # both refreshed within ras_every ticks ...
+        assert seen[-1][:2] == (10, 20)  # both read within ras_every ticks (exported the tick after) ...
         assert any(s[:2] in ((10, 2), (1, 20)) for s in seen), seen  # ... on different ticks
         fam = promtext.parse(ex.metrics_text())
         assert promtext.one(fam, "gpu_ras_events_total", event="poison_consumption") == 4  # carried
@@ -211,3 +211,21 @@ def test_failed_ras_read_keeps_last_values_and_is_reported(core, monkeypatch, tm
         assert ex.self_stats()["backend_calls"]["ras"]["errors"] == 1
     finally:
         ex.stop()
+
+
+def test_async_ras_is_off_the_tick_path(mock_exporter):
+    """ras_async (default): the device worker reads the RAS slice after publishing the tick, so
+    the RAS tick costs no more than the others and its values arrive on the next tick."""
+    ex = mock_exporter(backend="mock:gpus=1", ras_every=1)
+    ex.mock_add_ecc(0, "umc", ue=2)
+    ex.tick()  # reads (asynchronously) the new count
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_ecc_errors_total", block="umc", type="uncorrectable") == 0  # not yet
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_ecc_errors_total", block="umc", type="uncorrectable") == 2
+    sync = mock_exporter(backend="mock:gpus=1", ras_every=1, ras_async=False)
+    sync.mock_add_ecc(0, "umc", ue=3)
+    sync.tick()
+    fam = promtext.parse(sync.metrics_text())
+    assert promtext.one(fam, "gpu_ecc_errors_total", block="umc", type="uncorrectable") == 3
