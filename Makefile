@@ -21,7 +21,7 @@ LIBS      := -ldl -lpthread -lz
 
 CORE_SRC  := $(wildcard csrc/core/*.cpp)
 CORE_OBJ  := $(patsubst csrc/%.cpp,build/obj/%.o,$(CORE_SRC))
-CORE_HDR  := $(wildcard csrc/core/*.h) csrc/plugins/ondevice_abi.h
+CORE_HDR  := $(wildcard csrc/core/*.h) csrc/plugins/ondevice_abi.h csrc/plugins/pmc_helper_proto.h
 
 PYEXT     := gpumon/_core$(EXT)
 HIPEXT    := gpumon/_hip$(EXT)
@@ -93,7 +93,12 @@ clean:
 # them from lib/ only when PMC / probe sampling is enabled, so neither links HIP or rocprofiler.
 PMCLIB   := lib/libgpumon_pmc.so
 PROBELIB := lib/libgpumon_probe.so
-plugins: $(PMCLIB) $(PROBELIB)
+PMCHELPER := lib/gpumon-pmc-helper
+plugins: $(PMCLIB) $(PROBELIB) $(PMCHELPER)
+# The process that owns the device counting contexts (csrc/plugins/pmc_helper_proto.h): frozen by
+# the exporter between reads, because rocprofiler-sdk leaves an HSA thread polling.
+$(PMCHELPER): csrc/plugins/pmc_helper_main.cpp csrc/plugins/pmc_helper_proto.h csrc/plugins/ondevice_abi.h $(PMCLIB)
+	$(CXX) -O2 -std=c++17 $< -Llib -lgpumon_pmc -Wl,-rpath,'$$ORIGIN' -o $@
 $(PMCLIB): csrc/plugins/pmc_plugin.cpp csrc/plugins/ondevice_abi.h
 	@mkdir -p lib
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared -fvisibility=hidden -I$(ROCM)/include $< -Wl,-soname,libgpumon_pmc.so \
@@ -115,8 +120,12 @@ $(PMCEXT): csrc/pmc/pmc_module.cpp csrc/plugins/ondevice_abi.h $(PMCLIB)
 # Fake libamd_smi (CPU tests of the real amdsmi backend through the dlopen table).
 FAKESMI := build/fakes/libfake_amd_smi.so
 FAKERSMI := build/fakes/libfake_rocm_smi.so
-FAKEOND := build/fakes/ondevice/libgpumon_pmc.so build/fakes/ondevice/libgpumon_probe.so
+FAKEOND := build/fakes/ondevice/libgpumon_pmc.so build/fakes/ondevice/libgpumon_probe.so \
+           build/fakes/ondevice/gpumon-pmc-helper
 fakes: $(FAKESMI) $(FAKERSMI) $(FAKEOND)
+build/fakes/ondevice/gpumon-pmc-helper: csrc/plugins/pmc_helper_main.cpp csrc/plugins/pmc_helper_proto.h \
+                                        build/fakes/ondevice/libgpumon_pmc.so
+	$(CXX) -O1 -std=c++17 $< -Lbuild/fakes/ondevice -lgpumon_pmc -Wl,-rpath,'$$ORIGIN' -o $@
 build/fakes/ondevice/%.so: csrc/fakes/fake_ondevice.cpp csrc/plugins/ondevice_abi.h
 	@mkdir -p $(dir $@)
 	$(CXX) -O1 -std=c++17 -fPIC -shared $< -o $@ -lpthread

@@ -410,7 +410,12 @@ def main() -> int:
         }
         mon.stop()
         if has_gpu and n > 1 and args.link_check_s > 0:
-            result["xgmi"] = dict(result["xgmi"] or {}, link_map=_link_map_check(n, args.link_check_s))
+            # validation evidence, never a reason to lose the measured line
+            try:
+                lm = _link_map_check(n, args.link_check_s)
+            except Exception as e:  # noqa: BLE001
+                lm = {"error": f"{type(e).__name__}: {e}"}
+            result["xgmi"] = dict(result["xgmi"] or {}, link_map=lm)
     for ld in loads:
         ld.stop()
     if dist is not None:

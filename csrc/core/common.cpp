@@ -1,5 +1,7 @@
 #include "common.h"
 
+#include <pthread.h>
+
 #include <fcntl.h>
 #include <unistd.h>
 
@@ -8,6 +10,8 @@
 #include <mutex>
 
 namespace gpumon {
+
+void set_thread_name(const std::string& name) { pthread_setname_np(pthread_self(), name.substr(0, 15).c_str()); }
 
 std::atomic<int> g_log_level{static_cast<int>(LogLevel::kInfo)};
 

@@ -34,6 +34,10 @@ extern std::atomic<int> g_log_level;
 
 void log_line(LogLevel lvl, const char* component, const std::string& msg);
 
+// Names the calling thread (<= 15 chars) so per-thread CPU is attributable in /proc/<pid>/task,
+// top -H and perf (tools/thread_cpu.py).
+void set_thread_name(const std::string& name);
+
 #define GPUMON_LOG(lvl, comp, msg)                                              \
   do {                                                                          \
     if (static_cast<int>(lvl) >= ::gpumon::g_log_level.load(std::memory_order_relaxed)) \

@@ -58,6 +58,7 @@ struct Exporter::DevWorker {
 static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_ptr<Exporter::DoneSignal> sig,
                             Backend* backend, int i, int64_t occ_period_ns,
                             std::shared_ptr<std::atomic<uint64_t>> occ_reads) {
+  set_thread_name("gpumon-dev" + std::to_string(i));
   std::vector<uint32_t> occ_pids;                      // processes on this device at the last tick
   std::vector<double> occ_sum;                         // per occ_pids entry
   std::vector<int> occ_n, occ_busy;
@@ -392,13 +393,22 @@ bool Exporter::start(std::string* err) {
   running_ = true;
   // First tick synchronously so /metrics is ready as soon as start() returns.
   tick();
-  if (cfg_.interval_s > 0) sampler_ = std::thread([this] { sampler_loop(); });
-  if (!cfg_.influx_url.empty()) pusher_ = std::thread([this] { influx_loop(); });
+  if (cfg_.interval_s > 0) sampler_ = std::thread([this] {
+    set_thread_name("gpumon-sampler");
+    sampler_loop();
+  });
+  if (!cfg_.influx_url.empty()) pusher_ = std::thread([this] {
+    set_thread_name("gpumon-influx");
+    influx_loop();
+  });
   if (!cfg_.pod_resources_socket.empty() || !cfg_.cri_socket.empty()) {
     // metadata and allocations known before the first scrape
     if (!cfg_.cri_socket.empty()) cri_poll_once();
     if (!cfg_.pod_resources_socket.empty()) podres_poll_once();
-    podres_ = std::thread([this] { podres_loop(); });
+    podres_ = std::thread([this] {
+      set_thread_name("gpumon-k8s");
+      podres_loop();
+    });
   }
   return true;
 }

@@ -179,7 +179,10 @@ bool HttpServer::start(std::string* err) {
   running_ = true;
   for (auto& L : loops_) {
     Loop* p = L.get();
-    p->th = std::thread([this, p] { run(p); });
+    p->th = std::thread([this, p] {
+      set_thread_name("gpumon-http");
+      run(p);
+    });
   }
   return true;
 }

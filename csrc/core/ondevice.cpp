@@ -2,9 +2,15 @@
 #include "ondevice.h"
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <poll.h>
+#include <signal.h>
+#include <spawn.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <array>
 #include <cmath>
 #include <cstdlib>
@@ -12,8 +18,11 @@
 #include <cstring>
 
 #include "../plugins/ondevice_abi.h"
+#include "../plugins/pmc_helper_proto.h"
 #include "common.h"
 #include "exporter.h"
+
+extern char** environ;
 
 namespace gpumon {
 
@@ -93,6 +102,198 @@ std::unique_ptr<OnDevice::Plugin> load_plugin(const std::string& dir, const char
     return nullptr;
   }
   return p;
+}
+
+// ---------------------------------------------------------------------------------------------
+// PMC helper process (pmc_helper_proto.h): the device counting contexts live in
+// <plugin dir>/gpumon-pmc-helper, which this process freezes (SIGSTOP) between requests. The
+// functions below have the plugin ABI's signatures, so OnDevice drives the helper through the same
+// function table as an in-process plugin. One helper per process.
+struct HelperProc {
+  std::mutex mu;
+  pid_t pid = -1;
+  int to = -1, from = -1;  // request pipe (write end), response pipe (read end)
+  bool frozen = false;
+  std::string path;
+};
+HelperProc g_helper;
+
+bool io_full(int fd, void* p, size_t n, bool wr, int64_t deadline_ns) {
+  auto* b = static_cast<char*>(p);
+  while (n) {
+    pollfd pf{fd, static_cast<short>(wr ? POLLOUT : POLLIN), 0};
+    const int64_t left_ms = (deadline_ns - mono_ns()) / 1000000;
+    if (left_ms <= 0 || ::poll(&pf, 1, static_cast<int>(left_ms)) <= 0) return false;
+    const ssize_t r = wr ? ::write(fd, b, n) : ::read(fd, b, n);
+    if (r < 0 && (errno == EINTR || errno == EAGAIN)) continue;
+    if (r <= 0) return false;
+    b += r;
+    n -= static_cast<size_t>(r);
+  }
+  return true;
+}
+
+void helper_kill_locked() {
+  if (g_helper.pid > 0) {
+    ::kill(g_helper.pid, SIGKILL);  // frozen or hung: SIGKILL works on a stopped process
+    int st = 0;
+    ::waitpid(g_helper.pid, &st, 0);
+  }
+  if (g_helper.to >= 0) ::close(g_helper.to);
+  if (g_helper.from >= 0) ::close(g_helper.from);
+  g_helper.pid = -1;
+  g_helper.to = g_helper.from = -1;
+  g_helper.frozen = false;
+}
+
+bool helper_spawn(const std::string& path, std::string* err) {
+  std::lock_guard<std::mutex> g(g_helper.mu);
+  if (g_helper.pid > 0) return true;
+  if (::access(path.c_str(), X_OK) != 0) {
+    *err = "pmc helper " + path + " not found / not executable";
+    return false;
+  }
+  int req[2], resp[2];
+  if (::pipe2(req, O_CLOEXEC) != 0) {
+    *err = std::string("pipe: ") + strerror(errno);
+    return false;
+  }
+  if (::pipe2(resp, O_CLOEXEC) != 0) {
+    ::close(req[0]);
+    ::close(req[1]);
+    *err = std::string("pipe: ") + strerror(errno);
+    return false;
+  }
+  posix_spawn_file_actions_t fa;
+  posix_spawn_file_actions_init(&fa);
+  posix_spawn_file_actions_adddup2(&fa, req[0], 0);
+  posix_spawn_file_actions_adddup2(&fa, resp[1], 1);
+  char* argv[] = {const_cast<char*>(path.c_str()), nullptr};
+  pid_t pid = -1;
+  const int rc = posix_spawn(&pid, path.c_str(), &fa, nullptr, argv, environ);
+  posix_spawn_file_actions_destroy(&fa);
+  ::close(req[0]);
+  ::close(resp[1]);
+  if (rc != 0) {
+    ::close(req[1]);
+    ::close(resp[0]);
+    *err = "posix_spawn " + path + ": " + strerror(rc);
+    return false;
+  }
+  g_helper.pid = pid;
+  g_helper.to = req[1];
+  g_helper.from = resp[0];
+  g_helper.frozen = false;
+  g_helper.path = path;
+  return true;
+}
+
+// One request / response; the helper runs only for the duration of the call.
+int helper_call(uint32_t op, const int* agents, int n_agents, const char* const* counters, int n_counters,
+                double window_s, std::vector<char>* payload, int32_t* started, std::string* err) {
+  std::lock_guard<std::mutex> g(g_helper.mu);
+  if (g_helper.pid <= 0) {
+    *err = "pmc helper not running";
+    return -1;
+  }
+  if (g_helper.frozen) {
+    ::kill(g_helper.pid, SIGCONT);
+    g_helper.frozen = false;
+  }
+  std::string names;
+  for (int c = 0; c < n_counters; ++c) names += std::string(counters[c]) + "\n";
+  gpumon_pmc_req_t q{GPUMON_PMC_PROTO_MAGIC, op, static_cast<uint32_t>(std::max(0, n_agents)),
+                     static_cast<uint32_t>(names.size()), window_s};
+  // init brings HSA + rocprofiler up (seconds on a fresh node); a read takes milliseconds
+  const int64_t deadline = mono_ns() + static_cast<int64_t>((op == GPUMON_PMC_OP_INIT ? 60.0 : 10.0 + window_s) * 1e9);
+  gpumon_pmc_resp_t h{};
+  std::string e;
+  bool ok = io_full(g_helper.to, &q, sizeof q, true, deadline) &&
+            (n_agents <= 0 || io_full(g_helper.to, const_cast<int*>(agents), sizeof(int) * n_agents, true, deadline)) &&
+            (names.empty() || io_full(g_helper.to, &names[0], names.size(), true, deadline)) &&
+            io_full(g_helper.from, &h, sizeof h, false, deadline) && h.magic == GPUMON_PMC_PROTO_MAGIC;
+  if (ok && h.err_len) {
+    e.resize(h.err_len);
+    ok = io_full(g_helper.from, &e[0], e.size(), false, deadline);
+  }
+  if (ok) {
+    payload->resize(h.payload_len);
+    ok = h.payload_len == 0 || io_full(g_helper.from, payload->data(), payload->size(), false, deadline);
+  }
+  if (!ok) {
+    *err = "pmc helper " + g_helper.path + " died or timed out";
+    helper_kill_locked();  // the next start spawns a fresh one
+    return -1;
+  }
+  if (op != GPUMON_PMC_OP_QUIT && ::kill(g_helper.pid, SIGSTOP) == 0) g_helper.frozen = true;
+  if (started) *started = h.started;
+  *err = e;
+  return h.rc;
+}
+
+int h_abi() { return GPUMON_ONDEVICE_ABI; }
+int h_init(char* err, size_t n) {
+  std::vector<char> p;
+  std::string e;
+  const int rc = helper_call(GPUMON_PMC_OP_INIT, nullptr, 0, nullptr, 0, 0, &p, nullptr, &e);
+  if (rc < 0 && err && n) snprintf(err, n, "%s", e.c_str());
+  return rc;
+}
+int h_agent(int agent, gpumon_pmc_agent_t* out) {
+  std::vector<char> p;
+  std::string e;
+  if (helper_call(GPUMON_PMC_OP_AGENT, &agent, 1, nullptr, 0, 0, &p, nullptr, &e) != 0 ||
+      p.size() != sizeof(gpumon_pmc_agent_t))
+    return -1;
+  memcpy(out, p.data(), sizeof *out);
+  return 0;
+}
+int h_values(uint32_t op, const int* agents, int n_agents, const char* const* counters, int n_counters,
+             double window_s, gpumon_pmc_value_t* out, int32_t* ok, int32_t* started, char* err, size_t errlen) {
+  std::vector<char> p;
+  std::string e;
+  const int rc = helper_call(op, agents, n_agents, counters, n_counters, window_s, &p, started, &e);
+  const size_t nv = static_cast<size_t>(n_agents) * n_counters;
+  if (rc != 0 || p.size() != nv * sizeof(gpumon_pmc_value_t) + n_agents * sizeof(int32_t)) {
+    if (err && errlen) snprintf(err, errlen, "%s", e.empty() ? "pmc helper: bad response" : e.c_str());
+    return rc != 0 ? rc : -1;
+  }
+  memcpy(out, p.data(), nv * sizeof(gpumon_pmc_value_t));
+  memcpy(ok, p.data() + nv * sizeof(gpumon_pmc_value_t), n_agents * sizeof(int32_t));
+  return 0;
+}
+int h_sample_many(const int* a, int na, const char* const* c, int nc, double w, gpumon_pmc_value_t* out, int32_t* ok,
+                  char* err, size_t errlen) {
+  return h_values(GPUMON_PMC_OP_SAMPLE_MANY, a, na, c, nc, w, out, ok, nullptr, err, errlen);
+}
+int h_read_running(const int* a, int na, const char* const* c, int nc, gpumon_pmc_value_t* out, int32_t* ok,
+                   int32_t* started, char* err, size_t errlen) {
+  return h_values(GPUMON_PMC_OP_READ_RUNNING, a, na, c, nc, 0, out, ok, started, err, errlen);
+}
+void h_stop_running() {
+  std::vector<char> p;
+  std::string e;
+  helper_call(GPUMON_PMC_OP_STOP_RUNNING, nullptr, 0, nullptr, 0, 0, &p, nullptr, &e);
+}
+
+void helper_shutdown() {
+  {
+    std::vector<char> p;
+    std::string e;
+    helper_call(GPUMON_PMC_OP_QUIT, nullptr, 0, nullptr, 0, 0, &p, nullptr, &e);
+  }
+  std::lock_guard<std::mutex> g(g_helper.mu);
+  if (g_helper.pid > 0) {
+    const int64_t until = mono_ns() + 2'000'000'000;
+    int st = 0;
+    while (mono_ns() < until && ::waitpid(g_helper.pid, &st, WNOHANG) == 0)
+      std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    if (::waitpid(g_helper.pid, &st, WNOHANG) == 0) helper_kill_locked();
+    else {
+      g_helper.pid = -1;
+      helper_kill_locked();  // closes the pipes
+    }
+  }
 }
 
 ExtraSeries xs(const char* name, const char* help, int dev, double v, const char* type = "gauge") {
@@ -182,12 +383,27 @@ bool OnDevice::start(std::string* err) {
   const std::string dir = cfg_.plugin_dir.empty() ? default_plugin_dir() : cfg_.plugin_dir;
   char ebuf[512] = {0};
   if (cfg_.pmc) {
-    pmc_lib_ = load_plugin(dir, "libgpumon_pmc.so", true, err);
+    if (cfg_.pmc_isolate) {
+      // counting contexts in a helper process frozen between reads (pmc_helper_proto.h)
+      if (!helper_spawn(dir + "/gpumon-pmc-helper", err)) return false;
+      pmc_lib_ = std::make_unique<Plugin>();
+      pmc_lib_->path = dir + "/gpumon-pmc-helper";
+      pmc_lib_->pmc_abi = &h_abi;
+      pmc_lib_->pmc_init = &h_init;
+      pmc_lib_->pmc_agent = &h_agent;
+      pmc_lib_->pmc_sample_many = &h_sample_many;
+      pmc_lib_->pmc_read_running = &h_read_running;
+      pmc_lib_->pmc_stop_running = &h_stop_running;
+      pmc_helper_ = true;
+    } else {
+      pmc_lib_ = load_plugin(dir, "libgpumon_pmc.so", true, err);
+    }
     if (!pmc_lib_) return false;
     const int n = pmc_lib_->pmc_init(ebuf, sizeof ebuf);
     if (n < 0) {
       *err = std::string("pmc init: ") + ebuf;
       pmc_lib_.reset();
+      if (pmc_helper_) helper_shutdown();
       return false;
     }
     gpumon_pmc_agent_t a{};
@@ -219,8 +435,14 @@ bool OnDevice::start(std::string* err) {
                    (probes_.empty() ? " (device list not known yet: created on the first step that has it)" : ""));
   }
   running_ = true;
-  if (pmc_lib_) pmc_th_ = std::thread([this] { pmc_loop(); });
-  if (probe_lib_) probe_th_ = std::thread([this] { probe_loop(); });
+  if (pmc_lib_) pmc_th_ = std::thread([this] {
+    set_thread_name("gpumon-pmc");
+    pmc_loop();
+  });
+  if (probe_lib_) probe_th_ = std::thread([this] {
+    set_thread_name("gpumon-probe");
+    probe_loop();
+  });
   return true;
 }
 
@@ -235,6 +457,7 @@ void OnDevice::stop() {
   if (pmc_th_.joinable()) pmc_th_.join();
   if (probe_th_.joinable()) probe_th_.join();
   if (pmc_lib_ && pmc_continuous_) pmc_lib_->pmc_stop_running();  // release the device counters
+  if (pmc_helper_) helper_shutdown();
   if (probe_lib_) {
     std::lock_guard<std::mutex> g(probe_mu_);
     gpumon_probe_result_t r{};
@@ -589,7 +812,9 @@ void OnDevice::probe_step() {
 }
 
 constexpr const char* kSlotHelp =
-    "Mean lowest wave slot a probe wave got per SIMD (wave slots held by other work at probe launch).";
+    "Mean lowest wave slot a probe wave got per SIMD: wave slots held by other work at probe launch. Exact "
+    "only for PERSISTENT partial loads; short kernels free their slots between launches and read far low (a "
+    "saturating burn reads ~1 of 8). For occupancy use gpu_cu_occupancy_percent (KFD, interval mean).";
 
 void OnDevice::export_probe() {
   std::vector<ExtraSeries> out;

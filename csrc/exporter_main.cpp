@@ -144,17 +144,21 @@ int main(int argc, char** argv) {
   ExporterConfig& cfg = o.cfg;
   const OnDeviceConfig& od = o.od;
 
+  // The on-device samplers start BEFORE the backend: the PMC helper process is spawned while
+  // nothing in this process has touched the GPU yet, and the samplers pick the devices up once the
+  // backend lists them (OnDevice maps agents / creates probes on its first steps).
   if (once) {
     cfg.serve_http = false;
     cfg.interval_s = 0;
     Exporter e(cfg);
-    if (!e.start(&err)) {
-      fprintf(stderr, "start failed: %s\n", err.c_str());
-      return 1;
-    }
     OnDevice ondev(&e, od);
     if ((od.pmc || od.probe) && !ondev.start(&err)) {
       fprintf(stderr, "on-device samplers: %s\n", err.c_str());
+      return 1;
+    }
+    if (!e.start(&err)) {
+      fprintf(stderr, "start failed: %s\n", err.c_str());
+      ondev.stop();
       return 1;
     }
     ondev.step();
@@ -170,21 +174,21 @@ int main(int argc, char** argv) {
   signal(SIGTERM, on_signal);
   signal(SIGPIPE, SIG_IGN);
   Exporter e(cfg);
-  if (!e.start(&err)) {
-    fprintf(stderr, "start failed: %s\n", err.c_str());
-    return 1;
-  }
-  if (!err.empty()) GPUMON_LOG(LogLevel::kWarn, "main", "backend not ready (retrying): " + err);
   OnDevice ondev(&e, od);
   if (od.pmc || od.probe) {
     std::string oerr;
     if (!ondev.start(&oerr)) {
       // fail loudly: a DaemonSet asked for PMC / probe series and would otherwise silently lack them
       fprintf(stderr, "on-device samplers: %s\n", oerr.c_str());
-      e.stop();
       return 1;
     }
   }
+  if (!e.start(&err)) {
+    fprintf(stderr, "start failed: %s\n", err.c_str());
+    ondev.stop();
+    return 1;
+  }
+  if (!err.empty()) GPUMON_LOG(LogLevel::kWarn, "main", "backend not ready (retrying): " + err);
   GPUMON_LOG(LogLevel::kInfo, "main",
              "serving http://" + cfg.listen_addr + ":" + std::to_string(e.port()) +
                  "/metrics host=" + cfg.host + " interval=" + std::to_string(cfg.interval_s) + "s");

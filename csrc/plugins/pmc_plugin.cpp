@@ -15,11 +15,15 @@
 // C ABI in ondevice_abi.h; users: bin/gpumon-exporter and gpumon._core (csrc/core/ondevice.cpp,
 // dlopen) and the gpumon._pmc Python module (csrc/pmc/pmc_module.cpp, linked).
 #include <hsa/hsa.h>
+#include <rocprofiler-sdk/internal_threading.h>
 #include <rocprofiler-sdk/registration.h>
 #include <rocprofiler-sdk/rocprofiler.h>
 
+#include <dirent.h>
+
 #include <algorithm>
 #include <chrono>
+#include <set>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -64,12 +68,55 @@ Running g_run;
 
 std::string st_str(rocprofiler_status_t s) { return rocprofiler_get_status_string(s); }
 
+// Threads the runtimes create for us get names saying which step created them ("pmc-hsa-0",
+// "pmc-ctx-1", ...): per-thread CPU of the exporter is then attributable (tools/thread_cpu.py).
+std::set<int> task_ids() {
+  std::set<int> s;
+  if (DIR* d = opendir("/proc/self/task")) {
+    while (dirent* e = readdir(d))
+      if (e->d_name[0] >= '0' && e->d_name[0] <= '9') s.insert(atoi(e->d_name));
+    closedir(d);
+  }
+  return s;
+}
+
+void name_new_threads(const std::set<int>& before, const char* step) {
+  int k = 0;
+  for (int t : task_ids()) {
+    if (before.count(t)) continue;
+    char path[64], name[16], cur[32] = {0};
+    snprintf(path, sizeof path, "/proc/self/task/%d/comm", t);
+    if (FILE* f = fopen(path, "r")) {  // already named (an inner step named it): keep
+      const bool named = fgets(cur, sizeof cur, f) && strncmp(cur, "pmc-", 4) == 0;
+      fclose(f);
+      if (named) continue;
+    }
+    snprintf(name, sizeof name, "pmc-%s-%d", step, k++);
+    if (FILE* f = fopen(path, "w")) {
+      fputs(name, f);
+      fclose(f);
+    }
+  }
+}
+
 void check(rocprofiler_status_t s, const char* what) {
   if (s != ROCPROFILER_STATUS_SUCCESS) throw std::runtime_error(std::string(what) + ": " + st_str(s));
 }
 
 void set_err(char* err, size_t n, const std::string& m) {
   if (err && n) snprintf(err, n, "%s", m.c_str());
+}
+
+// Threads rocprofiler-sdk creates internally for a runtime library are named "pmc-rp<lib>-N" (see
+// name_new_threads): the creating library of every runtime thread in the exporter is then known.
+std::set<int> g_rp_before;
+const char* lib_tag(rocprofiler_runtime_library_t lib) {
+  switch (lib) {
+    case ROCPROFILER_LIBRARY: return "rprof";
+    case ROCPROFILER_HSA_LIBRARY: return "rphsa";
+    case ROCPROFILER_HIP_LIBRARY: return "rphip";
+    default: return "rpoth";
+  }
 }
 
 int tool_init(rocprofiler_client_finalize_t, void*) {
@@ -87,10 +134,18 @@ int tool_init(rocprofiler_client_finalize_t, void*) {
               },
               sizeof(rocprofiler_agent_v0_t), &agents),
           "query_available_agents");
+    const char* dbg = getenv("GPUMON_PMC_DEBUG_INIT");  // diagnosis of runtime threads (tools/thread_cpu.py)
+    const bool no_ctx = dbg && strcmp(dbg, "no-contexts") == 0;
+    const bool no_svc = dbg && strcmp(dbg, "no-service") == 0;
     for (const auto& a : agents) {
+      if (no_ctx) break;
       auto A = std::make_unique<Agent>();
       A->info = a;
       check(rocprofiler_create_context(&A->ctx), "create_context");
+      if (no_svc) {
+        g_agents.push_back(std::move(A));
+        continue;
+      }
       check(rocprofiler_configure_device_counting_service(
                 A->ctx, rocprofiler_buffer_id_t{0}, a.id,
                 [](rocprofiler_context_id_t ctx, rocprofiler_agent_id_t, rocprofiler_device_counting_agent_cb_t set,
@@ -113,6 +168,13 @@ void tool_fini(void*) {}
 
 rocprofiler_tool_configure_result_t* configure(uint32_t, const char*, uint32_t, rocprofiler_client_id_t* id) {
   id->name = "gpumon-pmc";
+  rocprofiler_at_internal_thread_create(
+      [](rocprofiler_runtime_library_t, void*) { g_rp_before = task_ids(); },
+      [](rocprofiler_runtime_library_t lib, void*) { name_new_threads(g_rp_before, lib_tag(lib)); },
+      static_cast<int>(ROCPROFILER_LIBRARY | ROCPROFILER_HSA_LIBRARY | ROCPROFILER_HIP_LIBRARY |
+                       ROCPROFILER_MARKER_LIBRARY | ROCPROFILER_RCCL_LIBRARY),
+      nullptr);
+
   static rocprofiler_tool_configure_result_t cfg{sizeof(rocprofiler_tool_configure_result_t), &tool_init,
                                                  &tool_fini, nullptr};
   return &cfg;
@@ -227,7 +289,9 @@ GPUMON_EXPORT int gpumon_pmc_abi_version(void) { return GPUMON_ONDEVICE_ABI; }
 GPUMON_EXPORT int gpumon_pmc_init(char* err, size_t errlen) {
   std::lock_guard<std::mutex> g(g_mu);
   if (!g_configured) {
+    const auto before = task_ids();
     rocprofiler_status_t s = rocprofiler_force_configure(&configure);
+    name_new_threads(before, "cfg");
     if (s != ROCPROFILER_STATUS_SUCCESS) {
       set_err(err, errlen, "rocprofiler_force_configure: " + st_str(s) +
                                " (HSA already initialised in this process? init must run first)");
@@ -240,7 +304,10 @@ GPUMON_EXPORT int gpumon_pmc_init(char* err, size_t errlen) {
     return -1;
   }
   if (!g_hsa) {
-    if (hsa_init() != HSA_STATUS_SUCCESS) {
+    const auto before = task_ids();
+    const hsa_status_t hs = hsa_init();
+    name_new_threads(before, "hsa");
+    if (hs != HSA_STATUS_SUCCESS) {
       set_err(err, errlen, "hsa_init failed");
       return -1;
     }
@@ -316,8 +383,10 @@ GPUMON_EXPORT int gpumon_pmc_sample_many(const int* agents, int n_agents, const 
     return -1;
   }
   int started = 0;
+  const auto before = task_ids();
   for (; started < n_agents; ++started)
     if (rocprofiler_start_context(As[started]->ctx) != ROCPROFILER_STATUS_SUCCESS) break;
+  name_new_threads(before, "ctx");
   if (started == n_agents) std::this_thread::sleep_for(std::chrono::duration<double>(window_s));
   for (int k = 0; k < n_agents; ++k) {
     ok[k] = 0;
@@ -365,9 +434,11 @@ GPUMON_EXPORT int gpumon_pmc_read_running(const int* agents, int n_agents, const
   }
   if (started) *started = 0;
   if (!g_run.on) {
+    const auto before = task_ids();
     int k = 0;
     for (; k < n_agents; ++k)
       if (rocprofiler_start_context(As[k]->ctx) != ROCPROFILER_STATUS_SUCCESS) break;
+    name_new_threads(before, "ctx");
     if (k < n_agents) {
       for (int j = 0; j < k; ++j) rocprofiler_stop_context(As[j]->ctx);
       set_err(err, errlen, "pmc read: start_context failed on agent " + std::to_string(agents[k]) +

@@ -65,6 +65,10 @@ class GpuMonitor:
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "GpuMonitor":
+        # on-device samplers first: the PMC helper process is spawned before anything in this
+        # process touches the GPU; the samplers pick the devices up once the backend lists them
+        if self.cfg.enable_pmc or self.cfg.enable_probe:
+            self._start_ondevice()
         self.start_error = self.ex.start()
         if self.start_error:
             log.warning("backend not ready yet (will retry): %s", self.start_error)
@@ -74,8 +78,6 @@ class GpuMonitor:
             plane = ControlPlane(self.ex, self.cfg)
             if plane.enabled:
                 self.plane = plane.start()
-        if self.cfg.enable_pmc or self.cfg.enable_probe:
-            self._start_ondevice()
         return self
 
     def _start_ondevice(self) -> None:
@@ -86,6 +88,7 @@ class GpuMonitor:
             self.ondevice = self._core.OnDevice(self.ex, {
                 "plugin_dir": self.cfg.plugin_dir, "pmc": bool(self.cfg.enable_pmc),
                 "pmc_counters": list(self.cfg.pmc_counters), "pmc_every_s": period, "pmc_mode": self.cfg.pmc_mode,
+                "pmc_isolate": self.cfg.pmc_isolate,
                 "probe": bool(self.cfg.enable_probe), "probe_every_s": period * self.cfg.probe_every})
             self.ondevice.start()
             return

@@ -1,6 +1,10 @@
 """K1 probe runner: launches the gfx950 probe microkernel on every monitored GPU and exports its
 pinned-ring-buffer results as ``gpu_probe_*`` series.
 
+This Python runner is the TEST ORACLE of the production path, the native sampler in
+csrc/core/ondevice.cpp (same plugin, same series); `gpumon serve` uses the native one unless
+``--ondevice python``.
+
 Per tick and device: one launch of ``blocks`` one-wave workgroups on a private non-blocking stream;
 completion is detected by polling a host-pinned arrival word that the last wave writes once, after a
 device-memory (L2) arrival counter reaches ``blocks`` (no hipDeviceSynchronize, no stall of the

@@ -418,3 +418,91 @@ def test_mfma_dtype_burns_run_and_agree_across_waves(H, torch_gpu):
         assert flop > 0
         assert torch.isfinite(o).all() and (o != 0).all(), (dt, o)
         assert torch.equal(o, o[:1].expand_as(o)), (dt, o)
+
+
+def _burn_closed_form(dt, iters):
+    """Exact value every wave of a burn_dtypes.hip burn writes: lane 0's four accumulator rows
+    (C rows 0..3, column 0 of the 16x16 tile) summed over the 8 chains, each chain = iters x (A.B).
+    Operand layout of the 16x16xK instructions: lane l holds A[l % 16][K/4 * (l / 16) + j] and
+    B[K/4 * (l / 16) + j][l % 16]; the burns' operand constants are fixed per lane (burn_dtypes.hip)."""
+    import numpy as np
+
+    rows = range(4)
+    if dt == "f16":
+        v = [float(np.float16(np.float32(0.5) + np.float32(0.001) * np.float32(m))) for m in range(8)]
+        per_row = [0.25 * 4 * sum(v) for _ in rows]  # (lane + j) & 7 covers 0..7 in every 8-k group
+    elif dt == "fp8":  # e4m3 (OCP): 0x38 = 1.0, 0x39 = 1.125 (byte 0 of odd lanes), B = 0x30 = 0.5
+        per_row = [0.5 * (32 + (4 * 0.125 if r % 2 else 0)) for r in rows]
+    elif dt == "i8":  # byte 0 of odd lanes = 2 (else 1), B = 2
+        per_row = [2 * (64 + (4 if r % 2 else 0)) for r in rows]
+    elif dt == "mxfp8":  # 8 dwords per lane, byte 0 of dword j = 1.125 when (lane + j) is odd: 4 of 8
+        per_row = [0.5 * (128 + 4 * 4 * 0.125) for r in rows]
+    elif dt == "mxfp4":  # e2m1: 0x2 = 1.0, 0x3 = 1.5 (nibble 0 of dword j, (lane + j) odd: 2 of the 4 used)
+        per_row = [0.5 * (128 + 4 * 2 * 0.5) for r in rows]
+    elif dt == "f32":
+        per_row = [0.5 * sum(float(np.float32(1.0) + np.float32(r + 16 * k) * np.float32(1e-3)) for k in range(4))
+                   for r in rows]
+    elif dt == "f64":
+        per_row = [0.5 * sum(1.0 + (r + 16 * k) * 1e-3 for k in range(4)) for r in rows]
+    return 8 * iters * sum(per_row)
+
+
+def test_mfma_dtype_burns_match_closed_form(H, torch_gpu):
+    """Numerics of every matrix path the load generator and gpu_mfma_tflops{dtype} cover: each
+    wave's output equals the closed-form fp64 / integer value of its fixed operands (exact for the
+    integer and narrow-float paths, fp32 / fp64 rounding tolerances otherwise)."""
+    torch = torch_gpu
+    s = torch.cuda.current_stream().cuda_stream
+    for iters in (4, 16):
+        for dt in ("f16", "fp8", "mxfp8", "mxfp4", "i8", "f32", "f64"):
+            o = torch.zeros(8 * 4, device="cuda")
+            H.mfma_burn_dtype(0, dt, o.data_ptr(), 8, iters, s)
+            torch.cuda.synchronize()
+            want = _burn_closed_form(dt, iters)
+            got = o.double().cpu()
+            tol = {"f32": 2e-6, "f64": 1e-7}.get(dt, 0.0)  # outputs are fp32 (the f64 path too)
+            assert torch.allclose(got, torch.full_like(got, want), rtol=tol, atol=0.0), (dt, iters, got[:4], want)
+
+
+def test_concurrent_load_runs_both_pipes_at_once(torch_gpu):
+    """kind="concurrent": the MFMA burn and the HBM stream on two streams at the same time (the
+    power / thermal worst case), both rates over wall time clearly non-zero (the alternating "mixed"
+    load never runs them together)."""
+    from gpumon.ops.load import SyntheticLoad
+
+    with SyntheticLoad(0, "concurrent") as ld:
+        time.sleep(3.0)
+        st = ld.stats()
+    assert st["tflops_wall"] > 500 and st["tbps_wall"] > 2.0, st
+    assert st["busy_s"] > 1.8 * st["wall_s"] * 0.8, st  # two streams busy ~all the time
+
+
+def test_burst_load_keeps_its_duty(torch_gpu):
+    """period_s: 150 ms on / 150 ms off bursts (the step / communication pattern the continuous PMC
+    counting is validated against) keep the requested busy fraction."""
+    from gpumon.ops.load import SyntheticLoad
+
+    with SyntheticLoad(0, "mfma", duty=0.5, period_s=0.3) as ld:
+        time.sleep(3.0)
+        st = ld.stats()
+    assert 0.45 <= st["busy_s"] / st["wall_s"] <= 0.62, st
+
+
+def test_xgmi_max_bandwidth_fill_in_matches_link_metrics(core, torch_gpu):
+    """The exporter fills a link slot that amdsmi_get_link_metrics does not list with lane speed x
+    width (exporter.cpp). On MI355X every listed peer link must report exactly that product, so the
+    fill-in cannot disagree with the library for the slot it covers."""
+    ex = _exporter(core, link_every=1)
+    try:
+        ex.tick()
+        sm = ex.samples()[0]
+        f = sm["fields"]
+        lane, width = f["xgmi_link_speed"], f["xgmi_link_width"]
+        assert lane and width, f
+        up = [l for l in sm["links"] if l["status"] == 1]
+        assert len(up) == 7
+        for l in up:
+            assert l["bit_rate_gbps"], l  # set only by amdsmi_get_link_metrics: the library listed it
+            assert l["max_bandwidth_gbps"] == pytest.approx(lane * width), (l, lane, width)
+    finally:
+        ex.stop()

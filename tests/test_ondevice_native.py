@@ -161,7 +161,7 @@ def test_pmc_init_failure_fails_loudly(core, mock_exporter, monkeypatch):
 
 
 def test_missing_plugin_fails_loudly(core, mock_exporter, tmp_path):
-    od = _ondevice(core, mock_exporter(), plugin_dir=str(tmp_path))
+    od = _ondevice(core, mock_exporter(), plugin_dir=str(tmp_path), pmc_isolate=False)
     with pytest.raises(RuntimeError, match="dlopen .*libgpumon_pmc.so"):
         od.start()
 
@@ -169,7 +169,7 @@ def test_missing_plugin_fails_loudly(core, mock_exporter, tmp_path):
 def test_sample_failures_counted(core, mock_exporter, monkeypatch):
     monkeypatch.setenv("GPUMON_FAKE_PMC_FAIL", "sample")
     ex = mock_exporter()
-    od = _ondevice(core, ex, probe=False, pmc_every_s=60)
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_isolate=False)
     od.start()
     try:
         od.step()
@@ -224,7 +224,7 @@ def test_binary_plugin_dir_from_env():
 
 def test_binary_missing_plugin_exits_nonzero(tmp_path):
     r = _run_bin("--pmc", "--plugin-dir", str(tmp_path))
-    assert r.returncode == 1 and "libgpumon_pmc.so" in r.stderr
+    assert r.returncode == 1 and "gpumon-pmc-helper" in r.stderr
 
 
 def test_binary_without_flags_loads_no_plugin():
@@ -304,7 +304,7 @@ def test_continuous_counters_held_elsewhere(core, mock_exporter, monkeypatch):
 
     monkeypatch.setenv("GPUMON_FAKE_PMC_FAIL", "start")
     ex = mock_exporter(backend="mock:gpus=1")
-    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous", pmc_isolate=False)
     od.start()
     try:
         od.step()
@@ -343,3 +343,90 @@ def test_continuous_restart_underneath_drops_the_interval(core, mock_exporter, m
         assert _val(ex.metrics_text(), "gpumon_pmc_resets_total") >= 1
     finally:
         od.stop()
+
+
+# ---------------------------------------------------------------- helper process (pmc_isolate)
+def _helper_pids():
+    out = []
+    for p in os.listdir("/proc"):
+        if p.isdigit():
+            try:
+                if open(f"/proc/{p}/comm").read().strip() == "gpumon-pmc-help" and \
+                        int(open(f"/proc/{p}/stat").read().rsplit(")", 1)[1].split()[1]) == os.getpid():
+                    out.append(int(p))
+            except (OSError, ValueError, IndexError):
+                pass
+    return out
+
+
+def _state(pid):
+    return open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()[0]
+
+
+def test_isolated_pmc_runs_in_a_frozen_helper(core, mock_exporter, monkeypatch):
+    """pmc_isolate (default): the counting contexts live in a child process that is stopped
+    (SIGSTOP, state T) between requests and answers correctly when resumed; stop() ends it."""
+    import time
+
+    monkeypatch.setenv("GPUMON_FAKE_MFMA", "0.4")
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
+    od.start()
+    try:
+        pids = _helper_pids()
+        assert len(pids) == 1
+        od.step()
+        time.sleep(0.05)
+        od.step()
+        assert _state(pids[0]) == "T"  # frozen between reads
+        ex.tick()
+        m = ex.metrics_text()
+        assert _val(m, "gpu_mfma_busy_active_percent", gpu_id="0") == pytest.approx(40.0)
+        assert _val(m, "gpu_pmc_coverage_ratio", gpu_id="0") == 1
+    finally:
+        od.stop()
+    time.sleep(0.1)
+    assert _helper_pids() == []  # reaped
+
+
+def test_isolated_pmc_window_mode_and_errors(core, mock_exporter, monkeypatch):
+    monkeypatch.setenv("GPUMON_FAKE_PMC_FAIL", "sample")
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="window")
+    od.start()
+    try:
+        od.step()
+        assert od.stats()["pmc_errors"] >= 1
+        ex.tick()
+        assert "gpu_mfma_util_percent" not in ex.metrics_text()
+    finally:
+        od.stop()
+
+
+def test_isolated_pmc_helper_death_is_survived(core, mock_exporter):
+    """A helper that dies (OOM-killed, crashed) turns into PMC errors, never a hang or a crash of
+    the exporter."""
+    import signal
+
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
+    od.start()
+    try:
+        od.step()
+        (pid,) = _helper_pids()
+        os.kill(pid, signal.SIGKILL)
+        od.step()
+        assert od.stats()["pmc_errors"] >= 1
+        ex.tick()
+        assert _val(ex.metrics_text(), "gpumon_pmc_up") == 0
+    finally:
+        od.stop()
+
+
+def test_isolated_pmc_missing_helper_fails_loudly(core, mock_exporter, tmp_path):
+    import shutil
+
+    shutil.copy(os.path.join(FAKE_DIR, "libgpumon_pmc.so"), tmp_path)
+    od = _ondevice(core, mock_exporter(), probe=False, plugin_dir=str(tmp_path))
+    with pytest.raises(RuntimeError, match="gpumon-pmc-helper"):
+        od.start()

@@ -20,3 +20,12 @@ def test_full_mfma():
 def test_idle_and_missing():
     assert derive({"GRBM_GUI_ACTIVE": {"max": 0.0}}, AGENT) == {}
     assert derive({}, AGENT) == {}
+
+
+def test_config_pmc_counters_cover_derivations():
+    """The default counter set (one gfx950 counting pass) holds every counter derive() uses."""
+    from gpumon.config import Config
+    from gpumon.ops.pmc import DEFAULT_COUNTERS
+
+    assert set(DEFAULT_COUNTERS) <= set(Config().pmc_counters)
+    assert Config().pmc_mode == "continuous"
