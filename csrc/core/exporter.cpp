@@ -70,6 +70,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
   // profiles/r2_bench.md) and the next tick carries the result.
   RasSample ras_ready;
   bool have_ras_ready = false;
+  uint64_t jitter = 0x9E3779B97F4A7C15ull * static_cast<uint64_t>(i + 1);  // per-worker LCG state
   while (true) {
     uint64_t id;
     bool links, procs, ras, ras_async;
@@ -102,7 +103,11 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
             occ_busy[k] += vals[k] > 0 ? 1 : 0;
           }
         occ_reads->fetch_add(occ_pids.size(), std::memory_order_relaxed);
-        next_occ += occ_period_ns;
+        // jittered spacing (0.5-1.5 periods, same mean): fixed-period reads phase-lock to a
+        // periodic workload (host-synchronised batches) and keep hitting -- or missing -- its gaps
+        jitter = jitter * 6364136223846793005ull + 1442695040888963407ull;
+        const double u = static_cast<double>(jitter >> 11) * (1.0 / 9007199254740992.0);
+        next_occ += static_cast<int64_t>(occ_period_ns * (0.5 + u));
         if (next_occ < mono_ns()) next_occ = mono_ns() + occ_period_ns;
         continue;
       }

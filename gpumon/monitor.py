@@ -65,11 +65,15 @@ class GpuMonitor:
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "GpuMonitor":
-        # on-device samplers first: the PMC helper process is spawned before anything in this
-        # process touches the GPU; the samplers pick the devices up once the backend lists them
-        if self.cfg.enable_pmc or self.cfg.enable_probe:
+        # native on-device samplers first: the PMC helper process is spawned before anything in
+        # this process touches the GPU; the samplers pick the devices up once the backend lists
+        # them. The Python runners (test oracle) need the device list, so they start after.
+        ondevice = self.cfg.enable_pmc or self.cfg.enable_probe
+        if ondevice and self.cfg.ondevice == "native":
             self._start_ondevice()
         self.start_error = self.ex.start()
+        if ondevice and self.cfg.ondevice != "native":
+            self._start_ondevice()
         if self.start_error:
             log.warning("backend not ready yet (will retry): %s", self.start_error)
         if self._want_plane:

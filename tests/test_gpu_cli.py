@@ -127,3 +127,47 @@ def test_fleet_view_reads_the_native_exporter():
     assert fields[1] == "0" and fields[2] == "1"  # gpu_id 0, up
     assert len(fields[4:12]) == 8 and all(f.isdigit() for f in fields[4:12])  # 8 XCD busy columns
     assert "/288" in rows[0]
+
+
+def test_native_exporter_reports_a_separate_tenant_process():
+    """The deployment shape: bin/gpumon-exporter in one process, the HIP workload in another. The
+    workload's pod_gpu row carries its VRAM, its wave occupancy (interval mean of the sub-sampled
+    KFD cu_occupancy) and its busy share -- per-process numbers, not the device util copied to
+    every row as the reference did (/root/reference/gpu.py:205)."""
+    import socket
+    import time
+    import urllib.request
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    load = subprocess.Popen([sys.executable, "-m", "gpumon", "load", "--kind", "mfma", "--seconds", "14"],
+                            cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    exe = os.path.join(ROOT, "bin", "gpumon-exporter")
+    ex = subprocess.Popen([exe, "--backend", "amdsmi", "--interval", "0.5", "--listen", f"127.0.0.1:{port}",
+                           "--log-level", "warn", "--no-pod-resources", "--no-cri"],
+                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    try:
+        time.sleep(9)
+        assert load.poll() is None, load.stderr.read()[-2000:]
+        assert ex.poll() is None, ex.stderr.read()[-2000:]
+        with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
+            fam = promtext.parse(r.read().decode())
+    finally:
+        ex.terminate()
+        ex.wait(20)
+        try:
+            load.wait(60)
+        except subprocess.TimeoutExpired:
+            load.kill()
+            load.wait(30)
+    occ = {l["pid"]: v for _, l, v in fam["pod_gpu_proc_cu_occupancy_percent"]["samples"]}
+    busy = {l["pid"]: v for _, l, v in fam["pod_gpu_proc_gfx_util"]["samples"]}
+    # the burn process holds every wave slot except in the gaps between its host-synchronised
+    # batches (~5 % of the time); 10 reads per tick estimate that share
+    hot = [p for p, v in occ.items() if v > 60]
+    assert len(hot) == 1, (occ, busy)
+    assert busy[hot[0]] > 60, (occ, busy)
+    assert promtext.one(fam, "gpu_cu_occupancy_percent", gpu_id="0") > 60
+    assert promtext.one(fam, "gpumon_occupancy_reads_total") > 0

@@ -443,7 +443,9 @@ def _burn_closed_form(dt, iters):
         per_row = [0.5 * sum(float(np.float32(1.0) + np.float32(r + 16 * k) * np.float32(1e-3)) for k in range(4))
                    for r in rows]
     elif dt == "f64":
-        per_row = [0.5 * sum(1.0 + (r + 16 * k) * 1e-3 for k in range(4)) for r in rows]
+        # v_mfma_f64_16x16x4_f64 lays its result out differently: accumulator register j of lane l
+        # holds row 4 * j + l / 16 (measured: lane 0 = rows 0, 4, 8, 12), not 4 * (l / 16) + j
+        per_row = [0.5 * sum(1.0 + (r + 16 * k) * 1e-3 for k in range(4)) for r in (0, 4, 8, 12)]
     return 8 * iters * sum(per_row)
 
 

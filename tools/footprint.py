@@ -38,6 +38,30 @@ def _port():
     return p
 
 
+def _children(pid):
+    out = []
+    for p in os.listdir("/proc"):
+        if p.isdigit():
+            try:
+                if int(open(f"/proc/{p}/stat").read().rsplit(")", 1)[1].split()[1]) == pid:
+                    out.append(int(p))
+            except (OSError, ValueError, IndexError):
+                pass
+    return out
+
+
+def _proc_tree(pid):
+    """_proc summed over pid and its child processes (the PMC helper): the container's footprint."""
+    rss, hwm, cpu = _proc(pid)
+    for c in _children(pid):
+        try:
+            r, h, u = _proc(c)
+        except OSError:
+            continue
+        rss, hwm, cpu = rss + r, hwm + h, cpu + u
+    return rss, hwm, cpu
+
+
 def _proc(pid):
     """(rss bytes, peak rss bytes, cpu seconds) of pid and its threads."""
     rss = hwm = 0
@@ -85,14 +109,14 @@ def main() -> int:
     for name, d in procs.items():
         if d["p"].poll() is not None:
             raise SystemExit(f"{name} exited: {d['p'].stderr.read()[-1500:]}")
-        d["cpu0"] = _proc(d["p"].pid)[2]
+        d["cpu0"] = _proc_tree(d["p"].pid)[2]
     t0 = time.time()
     last_scrape = 0.0
     last_log = t0
     while time.time() - t0 < args.seconds:
         now = time.time()
         for name, d in procs.items():
-            rss, hwm, cpu = _proc(d["p"].pid)
+            rss, hwm, cpu = _proc_tree(d["p"].pid)
             d["rss"].append(rss)
             d["hwm"] = hwm
             d["cpu1"] = cpu

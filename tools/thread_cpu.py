@@ -78,6 +78,21 @@ def main() -> int:
         time.sleep(8)
         if ex.poll() is not None:
             raise SystemExit(ex.stderr.read()[-2000:])
+        def kids():
+            out = []
+            for p in os.listdir("/proc"):  # the PMC helper (pmc_isolate): its CPU counts for the pod too
+                if p.isdigit():
+                    try:
+                        if int(open(f"/proc/{p}/stat").read().rsplit(")", 1)[1].split()[1]) == ex.pid:
+                            out.append(int(p))
+                    except (OSError, ValueError, IndexError):
+                        pass
+            return out
+
+        def kid_cpu(k):
+            return sum(v[1] for v in threads(k).values())
+
+        k0 = {k: kid_cpu(k) for k in kids()}
         t0, a0 = time.time(), threads(ex.pid)
         time.sleep(a.seconds)
         t1, a1 = time.time(), threads(ex.pid)
@@ -140,7 +155,9 @@ def main() -> int:
             for k in ("voluntary_ctxt_switches", "nonvoluntary_ctxt_switches"):
                 if k in st0 and k in st1:
                     rows[0][k + "_per_s"] = int(st1[k]) - int(st0[k])
-        print(json.dumps({"flags": flags, "env": a.env, "threads": len(rows), "rss_mb": rss_mb(ex.pid),
+        child_rows = [{"pid": k, "rss_mb": rss_mb(k), "state": open(f"/proc/{k}/stat").read().rsplit(")", 1)[1].split()[0],
+                       "cpu_pct": round(100 * (kid_cpu(k) - c0k) / dt, 2)} for k, c0k in k0.items()]
+        print(json.dumps({"flags": flags, "env": a.env, "threads": len(rows), "children": child_rows, "rss_mb": rss_mb(ex.pid),
                           "rss_by_mapping": rss_by_mapping(ex.pid),
                           "total_cpu_pct": round(sum(r["cpu_pct"] for r in rows), 2), "top": rows[:8]}), flush=True)
     finally:
