@@ -21,7 +21,7 @@ LIBS      := -ldl -lpthread -lz
 
 CORE_SRC  := $(wildcard csrc/core/*.cpp)
 CORE_OBJ  := $(patsubst csrc/%.cpp,build/obj/%.o,$(CORE_SRC))
-CORE_HDR  := $(wildcard csrc/core/*.h) csrc/plugins/ondevice_abi.h csrc/plugins/pmc_helper_proto.h
+CORE_HDR  := $(wildcard csrc/core/*.h) csrc/plugins/ondevice_abi.h csrc/plugins/ondevice_helper_proto.h
 
 PYEXT     := gpumon/_core$(EXT)
 HIPEXT    := gpumon/_hip$(EXT)
@@ -74,17 +74,27 @@ build/obj/hip/burn_dtypes.o: csrc/hip/burn_dtypes.hip $(HIP_HDR)
 $(HIPEXT): build/obj/hip/kernels.o build/obj/hip/burn16.o build/obj/hip/burn_dtypes.o build/obj/bindings/hip_module.o
 	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -shared -fPIC $^ -o $@
 
+# Sanitizer builds, one object per source so `make -j` compiles them in parallel.
+ASAN_FLAGS := -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer
+TSAN_FLAGS := -O1 -g -std=c++17 -fsanitize=thread
+ASAN_OBJ := $(patsubst csrc/%.cpp,build/asan/%.o,$(CORE_SRC) csrc/exporter_main.cpp)
+TSAN_OBJ := $(patsubst csrc/%.cpp,build/tsan/%.o,$(CORE_SRC) csrc/exporter_main.cpp)
+build/asan/%.o: csrc/%.cpp $(CORE_HDR)
+	@mkdir -p $(dir $@)
+	$(CXX) $(ASAN_FLAGS) $(INC) -c $< -o $@
+build/tsan/%.o: csrc/%.cpp $(CORE_HDR)
+	@mkdir -p $(dir $@)
+	$(CXX) $(TSAN_FLAGS) $(INC) -c $< -o $@
+
 asan: bin/gpumon-exporter-asan
-bin/gpumon-exporter-asan: $(CORE_SRC) $(CORE_HDR) csrc/exporter_main.cpp
+bin/gpumon-exporter-asan: $(ASAN_OBJ)
 	@mkdir -p bin
-	$(CXX) -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer $(INC) \
-	  $(CORE_SRC) csrc/exporter_main.cpp -o bin/gpumon-exporter-asan $(LIBS)
+	$(CXX) -fsanitize=address,undefined $^ -o $@ $(LIBS)
 
 tsan: bin/gpumon-exporter-tsan
-bin/gpumon-exporter-tsan: $(CORE_SRC) $(CORE_HDR) csrc/exporter_main.cpp
+bin/gpumon-exporter-tsan: $(TSAN_OBJ)
 	@mkdir -p bin
-	$(CXX) -O1 -g -std=c++17 -fsanitize=thread $(INC) \
-	  $(CORE_SRC) csrc/exporter_main.cpp -o bin/gpumon-exporter-tsan $(LIBS)
+	$(CXX) -fsanitize=thread $^ -o $@ $(LIBS)
 
 clean:
 	rm -rf build bin lib gpumon/_core*.so gpumon/_hip*.so gpumon/_pmc*.so
@@ -93,12 +103,12 @@ clean:
 # them from lib/ only when PMC / probe sampling is enabled, so neither links HIP or rocprofiler.
 PMCLIB   := lib/libgpumon_pmc.so
 PROBELIB := lib/libgpumon_probe.so
-PMCHELPER := lib/gpumon-pmc-helper
-plugins: $(PMCLIB) $(PROBELIB) $(PMCHELPER)
-# The process that owns the device counting contexts (csrc/plugins/pmc_helper_proto.h): frozen by
-# the exporter between reads, because rocprofiler-sdk leaves an HSA thread polling.
-$(PMCHELPER): csrc/plugins/pmc_helper_main.cpp csrc/plugins/pmc_helper_proto.h csrc/plugins/ondevice_abi.h $(PMCLIB)
-	$(CXX) -O2 -std=c++17 $< -Llib -lgpumon_pmc -Wl,-rpath,'$$ORIGIN' -o $@
+ONDHELPER := lib/gpumon-ondevice-helper
+plugins: $(PMCLIB) $(PROBELIB) $(ONDHELPER)
+# The process that runs the on-device samplers' GPU-runtime side (device counting contexts + K1
+# probe, csrc/plugins/ondevice_helper_proto.h), frozen by the exporter between requests.
+$(ONDHELPER): csrc/plugins/ondevice_helper_main.cpp csrc/plugins/ondevice_helper_proto.h csrc/plugins/ondevice_abi.h $(PMCLIB)
+	$(CXX) -O2 -std=c++17 $< -Llib -lgpumon_pmc -ldl -Wl,-rpath,'$$ORIGIN' -o $@
 $(PMCLIB): csrc/plugins/pmc_plugin.cpp csrc/plugins/ondevice_abi.h
 	@mkdir -p lib
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared -fvisibility=hidden -I$(ROCM)/include $< -Wl,-soname,libgpumon_pmc.so \
@@ -121,11 +131,11 @@ $(PMCEXT): csrc/pmc/pmc_module.cpp csrc/plugins/ondevice_abi.h $(PMCLIB)
 FAKESMI := build/fakes/libfake_amd_smi.so
 FAKERSMI := build/fakes/libfake_rocm_smi.so
 FAKEOND := build/fakes/ondevice/libgpumon_pmc.so build/fakes/ondevice/libgpumon_probe.so \
-           build/fakes/ondevice/gpumon-pmc-helper
+           build/fakes/ondevice/gpumon-ondevice-helper
 fakes: $(FAKESMI) $(FAKERSMI) $(FAKEOND)
-build/fakes/ondevice/gpumon-pmc-helper: csrc/plugins/pmc_helper_main.cpp csrc/plugins/pmc_helper_proto.h \
+build/fakes/ondevice/gpumon-ondevice-helper: csrc/plugins/ondevice_helper_main.cpp csrc/plugins/ondevice_helper_proto.h \
                                         build/fakes/ondevice/libgpumon_pmc.so
-	$(CXX) -O1 -std=c++17 $< -Lbuild/fakes/ondevice -lgpumon_pmc -Wl,-rpath,'$$ORIGIN' -o $@
+	$(CXX) -O1 -std=c++17 $< -Lbuild/fakes/ondevice -lgpumon_pmc -ldl -Wl,-rpath,'$$ORIGIN' -o $@
 build/fakes/ondevice/%.so: csrc/fakes/fake_ondevice.cpp csrc/plugins/ondevice_abi.h
 	@mkdir -p $(dir $@)
 	$(CXX) -O1 -std=c++17 -fPIC -shared $< -o $@ -lpthread

@@ -37,7 +37,7 @@ OnDeviceConfig ondevice_from(const py::dict& d) {
   get(d, "pmc_every_s", &c.pmc_every_s);
   get(d, "pmc_window_s", &c.pmc_window_s);
   get(d, "pmc_mode", &c.pmc_mode);
-  get(d, "pmc_isolate", &c.pmc_isolate);
+  get(d, "ondevice_isolate", &c.ondevice_isolate);
   get(d, "probe", &c.probe);
   get(d, "probe_every_s", &c.probe_every_s);
   get(d, "probe_blocks", &c.probe_blocks);

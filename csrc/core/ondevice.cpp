@@ -18,7 +18,7 @@
 #include <cstring>
 
 #include "../plugins/ondevice_abi.h"
-#include "../plugins/pmc_helper_proto.h"
+#include "../plugins/ondevice_helper_proto.h"
 #include "common.h"
 #include "exporter.h"
 
@@ -105,8 +105,8 @@ std::unique_ptr<OnDevice::Plugin> load_plugin(const std::string& dir, const char
 }
 
 // ---------------------------------------------------------------------------------------------
-// PMC helper process (pmc_helper_proto.h): the device counting contexts live in
-// <plugin dir>/gpumon-pmc-helper, which this process freezes (SIGSTOP) between requests. The
+// PMC helper process (ondevice_helper_proto.h): the device counting contexts live in
+// <plugin dir>/gpumon-ondevice-helper, which this process freezes (SIGSTOP) between requests. The
 // functions below have the plugin ABI's signatures, so OnDevice drives the helper through the same
 // function table as an in-process plugin. One helper per process.
 struct HelperProc {
@@ -276,6 +276,48 @@ void h_stop_running() {
   helper_call(GPUMON_PMC_OP_STOP_RUNNING, nullptr, 0, nullptr, 0, 0, &p, nullptr, &e);
 }
 
+// K1 probe through the helper: a handle is the helper's probe id + 1 disguised as the pointer type
+int h_probe_count() {
+  std::vector<char> p;
+  std::string e;
+  const int rc = helper_call(GPUMON_PROBE_OP_COUNT, nullptr, 0, nullptr, 0, 0, &p, nullptr, &e);
+  if (rc < 0) GPUMON_LOG(LogLevel::kWarn, "ondevice", "probe device count (helper): " + e);
+  return rc < 0 ? 0 : rc;
+}
+gpumon_probe* h_probe_create(int dev, int blocks, int slots, int spin, char* err, size_t errlen) {
+  const int a[4] = {dev, blocks, slots, spin};
+  std::vector<char> p;
+  std::string e;
+  const int rc = helper_call(GPUMON_PROBE_OP_CREATE, a, 4, nullptr, 0, 0, &p, nullptr, &e);
+  if (rc < 0) {
+    if (err && errlen) snprintf(err, errlen, "%s", e.c_str());
+    return nullptr;
+  }
+  return reinterpret_cast<gpumon_probe*>(static_cast<intptr_t>(rc) + 1);
+}
+int h_probe_id(gpumon_probe* h) { return static_cast<int>(reinterpret_cast<intptr_t>(h) - 1); }
+int h_probe_launch(gpumon_probe* h) {
+  const int a[1] = {h_probe_id(h)};
+  std::vector<char> p;
+  std::string e;
+  return helper_call(GPUMON_PROBE_OP_LAUNCH, a, 1, nullptr, 0, 0, &p, nullptr, &e);
+}
+int h_probe_wait(gpumon_probe* h, int slot, double timeout_s, gpumon_probe_result_t* out) {
+  const int a[2] = {h_probe_id(h), slot};
+  std::vector<char> p;
+  std::string e;
+  const int rc = helper_call(GPUMON_PROBE_OP_WAIT, a, 2, nullptr, 0, timeout_s, &p, nullptr, &e);
+  if (rc != 1 || p.size() != sizeof *out) return 0;
+  memcpy(out, p.data(), sizeof *out);
+  return 1;
+}
+void h_probe_destroy(gpumon_probe* h) {
+  const int a[1] = {h_probe_id(h)};
+  std::vector<char> p;
+  std::string e;
+  helper_call(GPUMON_PROBE_OP_DESTROY, a, 1, nullptr, 0, 0, &p, nullptr, &e);
+}
+
 void helper_shutdown() {
   {
     std::vector<char> p;
@@ -382,19 +424,22 @@ bool OnDevice::start(std::string* err) {
   }
   const std::string dir = cfg_.plugin_dir.empty() ? default_plugin_dir() : cfg_.plugin_dir;
   char ebuf[512] = {0};
+  if (cfg_.ondevice_isolate && (cfg_.pmc || cfg_.probe)) {
+    // device counting contexts and the probe in one helper process, frozen between requests
+    // (ondevice_helper_proto.h): this process never loads HIP, HSA or rocprofiler-sdk
+    if (!helper_spawn(dir + "/gpumon-ondevice-helper", err)) return false;
+    helper_ = true;
+  }
   if (cfg_.pmc) {
-    if (cfg_.pmc_isolate) {
-      // counting contexts in a helper process frozen between reads (pmc_helper_proto.h)
-      if (!helper_spawn(dir + "/gpumon-pmc-helper", err)) return false;
+    if (cfg_.ondevice_isolate) {
       pmc_lib_ = std::make_unique<Plugin>();
-      pmc_lib_->path = dir + "/gpumon-pmc-helper";
+      pmc_lib_->path = dir + "/gpumon-ondevice-helper";
       pmc_lib_->pmc_abi = &h_abi;
       pmc_lib_->pmc_init = &h_init;
       pmc_lib_->pmc_agent = &h_agent;
       pmc_lib_->pmc_sample_many = &h_sample_many;
       pmc_lib_->pmc_read_running = &h_read_running;
       pmc_lib_->pmc_stop_running = &h_stop_running;
-      pmc_helper_ = true;
     } else {
       pmc_lib_ = load_plugin(dir, "libgpumon_pmc.so", true, err);
     }
@@ -403,7 +448,7 @@ bool OnDevice::start(std::string* err) {
     if (n < 0) {
       *err = std::string("pmc init: ") + ebuf;
       pmc_lib_.reset();
-      if (pmc_helper_) helper_shutdown();
+      if (helper_) helper_shutdown();
       return false;
     }
     gpumon_pmc_agent_t a{};
@@ -424,12 +469,27 @@ bool OnDevice::start(std::string* err) {
                    (pmc_continuous_ ? " mode=continuous" : " mode=window"));
   }
   if (cfg_.probe) {
-    probe_lib_ = load_plugin(dir, "libgpumon_probe.so", false, err);
+    if (cfg_.ondevice_isolate) {
+      probe_lib_ = std::make_unique<Plugin>();
+      probe_lib_->path = dir + "/gpumon-ondevice-helper";
+      probe_lib_->probe_abi = &h_abi;
+      probe_lib_->probe_count = &h_probe_count;
+      probe_lib_->probe_create = &h_probe_create;
+      probe_lib_->probe_launch = &h_probe_launch;
+      probe_lib_->probe_wait = &h_probe_wait;
+      probe_lib_->probe_destroy = &h_probe_destroy;
+    } else {
+      probe_lib_ = load_plugin(dir, "libgpumon_probe.so", false, err);
+    }
     if (!probe_lib_) {
       pmc_lib_.reset();
+      if (helper_) helper_shutdown();
       return false;
     }
-    if (!create_probes(err)) return false;
+    if (!create_probes(err)) {
+      if (helper_) helper_shutdown();
+      return false;
+    }
     GPUMON_LOG(LogLevel::kInfo, "ondevice",
                "probe plugin " + probe_lib_->path + " devices=" + std::to_string(probes_.size()) +
                    (probes_.empty() ? " (device list not known yet: created on the first step that has it)" : ""));
@@ -457,7 +517,6 @@ void OnDevice::stop() {
   if (pmc_th_.joinable()) pmc_th_.join();
   if (probe_th_.joinable()) probe_th_.join();
   if (pmc_lib_ && pmc_continuous_) pmc_lib_->pmc_stop_running();  // release the device counters
-  if (pmc_helper_) helper_shutdown();
   if (probe_lib_) {
     std::lock_guard<std::mutex> g(probe_mu_);
     gpumon_probe_result_t r{};
@@ -469,6 +528,7 @@ void OnDevice::stop() {
     probes_.clear();
     ex_->set_extra("probe", {});
   }
+  if (helper_) helper_shutdown();  // after the probes' rings are drained and freed
   if (pmc_lib_) ex_->set_extra("pmc", {});
 }
 

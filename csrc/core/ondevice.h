@@ -44,10 +44,11 @@ struct OnDeviceConfig {
   // interval is counted; "window": start -> pmc_window_s -> read -> stop per step (the r1 sampler:
   // aliases bursts longer than the window). Continuous falls back to window when the plugin lacks it.
   std::string pmc_mode = "continuous";
-  // true: the counting contexts live in <plugin dir>/gpumon-pmc-helper, a child process frozen
-  // between reads (rocprofiler-sdk leaves an HSA thread polling a full core in the process that
-  // owns them); false: libgpumon_pmc.so in this process (tools that already run HIP / HSA).
-  bool pmc_isolate = true;
+  // true: the device counting contexts and the K1 probe run in <plugin dir>/gpumon-ondevice-helper,
+  // a child process frozen between requests (rocprofiler-sdk leaves an HSA thread polling a full
+  // core in the process that owns the contexts; this process then never loads a GPU runtime);
+  // false: the plugins in this process (tools that already run HIP / HSA).
+  bool ondevice_isolate = true;
   double pmc_window_s = 0.1;  // window mode: counting window per sample (capped at half the period)
   bool probe = false;
   double probe_every_s = 1.0;
@@ -134,7 +135,7 @@ class OnDevice {
   std::map<int, std::map<std::string, PmcReduced>> pmc_prev_;
   int64_t pmc_prev_ns_ = 0;
   bool pmc_continuous_ = false;
-  bool pmc_helper_ = false;     // pmc_lib_ is the helper-process client
+  bool helper_ = false;         // pmc_lib_ / probe_lib_ are clients of the helper process
   int64_t pmc_last_ok_ns_ = 0;  // last step that produced values (window or continuous)
   bool pmc_up_ = false;
 

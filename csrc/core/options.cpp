@@ -263,7 +263,7 @@ const std::map<std::string, Setter>& setters() {
       {"enable_pmc", bool_at([](NativeOptions* o) { return &o->od.pmc; })},
       {"pmc_counters", list_at([](NativeOptions* o) { return &o->od.pmc_counters; })},
       {"pmc_mode", str_at([](NativeOptions* o) { return &o->od.pmc_mode; })},
-      {"pmc_isolate", bool_at([](NativeOptions* o) { return &o->od.pmc_isolate; })},
+      {"ondevice_isolate", bool_at([](NativeOptions* o) { return &o->od.ondevice_isolate; })},
       {"plugin_dir", str_at([](NativeOptions* o) { return &o->od.plugin_dir; })},
       {"activity_acc_scale", dbl_at([](NativeOptions* o) { return &o->cfg.rates.activity_acc_scale; })},
       {"xgmi_kb_bytes", dbl_at([](NativeOptions* o) { return &o->cfg.rates.xgmi_kb_bytes; })},
@@ -527,7 +527,7 @@ std::string options_json(const NativeOptions& o) {
   B("enable_pmc", o.od.pmc);
   L("pmc_counters", o.od.pmc_counters);
   S("pmc_mode", o.od.pmc_mode);
-  B("pmc_isolate", o.od.pmc_isolate);
+  B("ondevice_isolate", o.od.ondevice_isolate);
   S("plugin_dir", o.od.plugin_dir);
   N("activity_acc_scale", c.rates.activity_acc_scale);
   N("xgmi_kb_bytes", c.rates.xgmi_kb_bytes);

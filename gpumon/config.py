@@ -94,7 +94,7 @@ class Config:
     pmc_mode: str = "continuous"
     # the counting contexts in a helper process frozen between reads (rocprofiler-sdk leaves an HSA
     # thread polling a full core in the process that owns them, profiles/r2_footprint.md)
-    pmc_isolate: bool = True
+    ondevice_isolate: bool = True
     pmc_counters: List[str] = field(default_factory=lambda: (
         ["SQ_VALU_MFMA_BUSY_CYCLES"] + ["SQ_INSTS_VALU_MFMA_MOPS_" + d for d in
                                         ("BF16", "F16", "F8", "F6F4", "F32", "F64", "I8")]

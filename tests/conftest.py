@@ -9,15 +9,18 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-def make_locked(target):
-    """`make <target>` serialised across pytest-xdist workers (a worker must never dlopen a fake
-    library another worker is relinking)."""
+def make_locked(*targets, jobs=1, timeout=900):
+    """`make <targets>` serialised across pytest-xdist workers (a worker must never dlopen a fake
+    library another worker is relinking, and two workers must not write the same object)."""
     import fcntl
 
     os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
     with open(os.path.join(ROOT, "build", ".make.lock"), "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
-        subprocess.run(["make", "-C", ROOT, target], check=True, stdout=subprocess.DEVNULL)
+        r = subprocess.run(["make", "-C", ROOT, f"-j{jobs}", *targets], capture_output=True, text=True,
+                           timeout=timeout)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return r
 
 
 def pytest_configure(config):

@@ -78,7 +78,9 @@ def test_asan_build_survives_raw_fuzz():
     import time
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run(["make", "-C", root, "asan"], capture_output=True, text=True, timeout=900)
+    from conftest import make_locked
+
+    r = make_locked("asan", jobs=8)
     assert r.returncode == 0, r.stderr[-2000:]
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -161,7 +161,7 @@ def test_pmc_init_failure_fails_loudly(core, mock_exporter, monkeypatch):
 
 
 def test_missing_plugin_fails_loudly(core, mock_exporter, tmp_path):
-    od = _ondevice(core, mock_exporter(), plugin_dir=str(tmp_path), pmc_isolate=False)
+    od = _ondevice(core, mock_exporter(), plugin_dir=str(tmp_path), ondevice_isolate=False)
     with pytest.raises(RuntimeError, match="dlopen .*libgpumon_pmc.so"):
         od.start()
 
@@ -169,7 +169,7 @@ def test_missing_plugin_fails_loudly(core, mock_exporter, tmp_path):
 def test_sample_failures_counted(core, mock_exporter, monkeypatch):
     monkeypatch.setenv("GPUMON_FAKE_PMC_FAIL", "sample")
     ex = mock_exporter()
-    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_isolate=False)
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, ondevice_isolate=False)
     od.start()
     try:
         od.step()
@@ -224,7 +224,7 @@ def test_binary_plugin_dir_from_env():
 
 def test_binary_missing_plugin_exits_nonzero(tmp_path):
     r = _run_bin("--pmc", "--plugin-dir", str(tmp_path))
-    assert r.returncode == 1 and "gpumon-pmc-helper" in r.stderr
+    assert r.returncode == 1 and "gpumon-ondevice-helper" in r.stderr
 
 
 def test_binary_without_flags_loads_no_plugin():
@@ -304,7 +304,7 @@ def test_continuous_counters_held_elsewhere(core, mock_exporter, monkeypatch):
 
     monkeypatch.setenv("GPUMON_FAKE_PMC_FAIL", "start")
     ex = mock_exporter(backend="mock:gpus=1")
-    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous", pmc_isolate=False)
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous", ondevice_isolate=False)
     od.start()
     try:
         od.step()
@@ -345,13 +345,13 @@ def test_continuous_restart_underneath_drops_the_interval(core, mock_exporter, m
         od.stop()
 
 
-# ---------------------------------------------------------------- helper process (pmc_isolate)
+# ---------------------------------------------------------------- helper process (ondevice_isolate)
 def _helper_pids():
     out = []
     for p in os.listdir("/proc"):
         if p.isdigit():
             try:
-                if open(f"/proc/{p}/comm").read().strip() == "gpumon-pmc-help" and \
+                if open(f"/proc/{p}/comm").read().strip() == "gpumon-ondevice" and \
                         int(open(f"/proc/{p}/stat").read().rsplit(")", 1)[1].split()[1]) == os.getpid():
                     out.append(int(p))
             except (OSError, ValueError, IndexError):
@@ -364,7 +364,7 @@ def _state(pid):
 
 
 def test_isolated_pmc_runs_in_a_frozen_helper(core, mock_exporter, monkeypatch):
-    """pmc_isolate (default): the counting contexts live in a child process that is stopped
+    """ondevice_isolate (default): the counting contexts live in a child process that is stopped
     (SIGSTOP, state T) between requests and answers correctly when resumed; stop() ends it."""
     import time
 
@@ -428,5 +428,39 @@ def test_isolated_pmc_missing_helper_fails_loudly(core, mock_exporter, tmp_path)
 
     shutil.copy(os.path.join(FAKE_DIR, "libgpumon_pmc.so"), tmp_path)
     od = _ondevice(core, mock_exporter(), probe=False, plugin_dir=str(tmp_path))
-    with pytest.raises(RuntimeError, match="gpumon-pmc-helper"):
+    with pytest.raises(RuntimeError, match="gpumon-ondevice-helper"):
         od.start()
+
+
+def test_isolated_probe_runs_in_the_helper(core, mock_exporter, monkeypatch):
+    """ondevice_isolate: the K1 probe is created, launched and waited on through the same helper
+    process as the counting contexts, so this process never maps the probe library (and with it
+    the HIP runtime); a killed helper turns into probe timeouts, not a hang."""
+    import signal
+    import time
+
+    monkeypatch.setenv("GPUMON_FAKE_AGENTS", "2")
+    ex = mock_exporter(backend="mock:gpus=2")
+    od = _ondevice(core, ex, probe_every_s=60, pmc_every_s=60, probe_timeout_s=0.5)
+    od.start()
+    try:
+        assert len(_helper_pids()) == 1  # one helper for both samplers
+        od.step()
+        time.sleep(0.05)
+        od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        for g in ("0", "1"):
+            assert _val(m, "gpu_probe_latency_seconds", gpu_id=g) is not None
+        maps = open("/proc/self/maps").read()
+        assert "libgpumon_probe.so" not in maps and "libgpumon_pmc.so" not in maps
+        (pid,) = _helper_pids()
+        assert _state(pid) == "T"
+        os.kill(pid, signal.SIGKILL)
+        t0 = time.monotonic()
+        od.step()
+        assert time.monotonic() - t0 < 5
+        ex.tick()
+        assert _val(ex.metrics_text(), "gpumon_pmc_up") == 0
+    finally:
+        od.stop()

@@ -73,8 +73,9 @@ ONDEVICE = ("--pmc", "--probe", "--plugin-dir", os.path.join(ROOT, "build", "fak
     ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
 ])
 def test_sanitized_exporter_under_concurrent_scrapes(target, binary, env, extra):
-    r = subprocess.run(["make", "-C", ROOT, target] + (["fakes"] if extra else []), capture_output=True, text=True,
-                       timeout=600)
+    from conftest import make_locked
+
+    r = make_locked(target, *(["fakes"] if extra else []), jobs=8)
     assert r.returncode == 0, r.stderr[-2000:]
     rc, err = _run(os.path.join(ROOT, binary), dict(env, GPUMON_FAKE_AGENTS="4"), extra)
     bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l

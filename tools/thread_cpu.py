@@ -80,7 +80,7 @@ def main() -> int:
             raise SystemExit(ex.stderr.read()[-2000:])
         def kids():
             out = []
-            for p in os.listdir("/proc"):  # the PMC helper (pmc_isolate): its CPU counts for the pod too
+            for p in os.listdir("/proc"):  # the PMC helper (ondevice_isolate): its CPU counts for the pod too
                 if p.isdigit():
                     try:
                         if int(open(f"/proc/{p}/stat").read().rsplit(")", 1)[1].split()[1]) == ex.pid:
