@@ -49,6 +49,9 @@ struct OnDevice::Plugin {
   int (*probe_launch)(gpumon_probe*) = nullptr;
   int (*probe_wait)(gpumon_probe*, int, double, gpumon_probe_result_t*) = nullptr;
   void (*probe_destroy)(gpumon_probe*) = nullptr;
+  // optional: launch where pending[k] < 0, then wait for every pending launch, in one call
+  // (the helper process: one awake period, so the host-observed latency is the GPU's, not IPC's)
+  bool (*probe_cycle)(gpumon_probe* const*, int, double, int*, int*, gpumon_probe_result_t*) = nullptr;
 
   // Plugins stay loaded for the life of the process: rocprofiler keeps the tool's callbacks and
   // the HIP runtime keeps its threads, so dlclose() would leave dangling code pointers.
@@ -318,6 +321,30 @@ void h_probe_destroy(gpumon_probe* h) {
   helper_call(GPUMON_PROBE_OP_DESTROY, a, 1, nullptr, 0, 0, &p, nullptr, &e);
 }
 
+bool h_probe_cycle(gpumon_probe* const* hs, int n, double timeout_s, int* pending, int* got,
+                   gpumon_probe_result_t* out) {
+  std::vector<int> a(2 * static_cast<size_t>(n));
+  for (int k = 0; k < n; ++k) {
+    a[2 * k] = h_probe_id(hs[k]);
+    a[2 * k + 1] = pending[k];
+  }
+  std::vector<char> p;
+  std::string e;
+  const int rc = helper_call(GPUMON_PROBE_OP_CYCLE, a.data(), 2 * n, nullptr, 0, timeout_s, &p, nullptr, &e);
+  if (rc != n || p.size() != n * sizeof(gpumon_probe_cycle_t)) {
+    for (int k = 0; k < n; ++k) got[k] = 0;  // pending unknown: keep the caller's (a later wait times out)
+    return false;
+  }
+  for (int k = 0; k < n; ++k) {
+    gpumon_probe_cycle_t c;
+    memcpy(&c, p.data() + k * sizeof c, sizeof c);
+    pending[k] = c.pending;
+    got[k] = c.got;
+    if (c.got) out[k] = c.result;
+  }
+  return true;
+}
+
 void helper_shutdown() {
   {
     std::vector<char> p;
@@ -478,6 +505,7 @@ bool OnDevice::start(std::string* err) {
       probe_lib_->probe_launch = &h_probe_launch;
       probe_lib_->probe_wait = &h_probe_wait;
       probe_lib_->probe_destroy = &h_probe_destroy;
+      probe_lib_->probe_cycle = &h_probe_cycle;
     } else {
       probe_lib_ = load_plugin(dir, "libgpumon_probe.so", false, err);
     }
@@ -844,14 +872,37 @@ void OnDevice::probe_step() {
     std::string err;
     if (!create_probes(&err)) GPUMON_LOG(LogLevel::kWarn, "ondevice", err);
   }
-  for (auto& p : probes_)
-    if (p.pending < 0) p.pending = probe_lib_->probe_launch(static_cast<gpumon_probe*>(p.handle));
-  const int64_t deadline = mono_ns() + static_cast<int64_t>(cfg_.probe_timeout_s * 1e9);
-  for (auto& p : probes_) {
-    if (p.pending < 0) continue;
-    gpumon_probe_result_t r{};
-    const double left = std::max(0.0, (deadline - mono_ns()) * 1e-9);
-    if (probe_lib_->probe_wait(static_cast<gpumon_probe*>(p.handle), p.pending, left, &r) == 1) {
+  const int n = static_cast<int>(probes_.size());
+  std::vector<int> got(n, 0);
+  std::vector<gpumon_probe_result_t> res(n);
+  bool failed = false;  // the helper did not answer: every probe's step is lost
+  if (probe_lib_->probe_cycle) {
+    std::vector<gpumon_probe*> hs(n);
+    std::vector<int> pend(n);
+    for (int k = 0; k < n; ++k) {
+      hs[k] = static_cast<gpumon_probe*>(probes_[k].handle);
+      pend[k] = probes_[k].pending;
+    }
+    if (probe_lib_->probe_cycle(hs.data(), n, cfg_.probe_timeout_s, pend.data(), got.data(), res.data()))
+      for (int k = 0; k < n; ++k) probes_[k].pending = pend[k];
+    else
+      failed = true;
+  } else {
+    for (auto& p : probes_)
+      if (p.pending < 0) p.pending = probe_lib_->probe_launch(static_cast<gpumon_probe*>(p.handle));
+    const int64_t deadline = mono_ns() + static_cast<int64_t>(cfg_.probe_timeout_s * 1e9);
+    for (int k = 0; k < n; ++k) {
+      auto& p = probes_[k];
+      if (p.pending < 0) continue;
+      const double left = std::max(0.0, (deadline - mono_ns()) * 1e-9);
+      got[k] = probe_lib_->probe_wait(static_cast<gpumon_probe*>(p.handle), p.pending, left, &res[k]) == 1;
+      if (got[k]) p.pending = -1;
+    }
+  }
+  for (int k = 0; k < n; ++k) {
+    auto& p = probes_[k];
+    const gpumon_probe_result_t& r = res[k];
+    if (got[k]) {
       p.pending = -1;
       p.have = true;
       p.latency_s = r.host_latency_s;
@@ -863,7 +914,7 @@ void OnDevice::probe_step() {
       p.xcc_slot.assign(r.xcc_wave_slot, r.xcc_wave_slot + GPUMON_PROBE_MAX_XCC);
       p.slot_mean = r.wave_slot_mean;
       probe_done_++;
-    } else {
+    } else if (p.pending >= 0 || failed) {
       p.timeouts++;
       probe_timeouts_++;
     }

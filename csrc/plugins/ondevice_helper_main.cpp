@@ -9,6 +9,9 @@
 #include <sys/prctl.h>
 #include <unistd.h>
 
+#include <time.h>
+
+#include <algorithm>
 #include <cerrno>
 #include <csignal>
 #include <cstdio>
@@ -98,9 +101,16 @@ bool probe_lib(std::string* err) {
   return true;
 }
 
-gpumon_probe* probe_handle(const std::vector<int>& a) {
-  if (a.empty() || a[0] < 0 || a[0] >= static_cast<int>(g_probe.handles.size())) return nullptr;
-  return g_probe.handles[a[0]];
+gpumon_probe* probe_handle_at(int id) {
+  if (id < 0 || id >= static_cast<int>(g_probe.handles.size())) return nullptr;
+  return g_probe.handles[id];
+}
+gpumon_probe* probe_handle(const std::vector<int>& a) { return a.empty() ? nullptr : probe_handle_at(a[0]); }
+
+double now_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
 }
 
 }  // namespace
@@ -197,6 +207,27 @@ int main() {
         gpumon_probe_result_t r{};
         const int got = p && agents.size() >= 2 ? g_probe.wait(p, agents[1], q.window_s, &r) : 0;
         ok = reply(got, 0, "", got == 1 ? &r : nullptr, got == 1 ? sizeof r : 0);
+        break;
+      }
+      case GPUMON_PROBE_OP_CYCLE: {
+        const size_t n = agents.size() / 2;
+        std::vector<gpumon_probe_cycle_t> res(n);
+        for (size_t k = 0; k < n; ++k) {
+          res[k].pending = agents[2 * k + 1];
+          res[k].got = 0;
+          gpumon_probe* p = probe_handle_at(agents[2 * k]);
+          if (p && res[k].pending < 0) res[k].pending = g_probe.launch(p);
+        }
+        const double t_end = now_s() + q.window_s;
+        for (size_t k = 0; k < n; ++k) {
+          gpumon_probe* p = probe_handle_at(agents[2 * k]);
+          if (!p || res[k].pending < 0) continue;
+          if (g_probe.wait(p, res[k].pending, std::max(0.0, t_end - now_s()), &res[k].result) == 1) {
+            res[k].got = 1;
+            res[k].pending = -1;
+          }
+        }
+        ok = reply(static_cast<int>(n), 0, "", res.data(), res.size() * sizeof(gpumon_probe_cycle_t));
         break;
       }
       case GPUMON_PROBE_OP_DESTROY: {

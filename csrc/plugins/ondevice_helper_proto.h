@@ -32,7 +32,17 @@ enum gpumon_pmc_op : uint32_t {
   GPUMON_PROBE_OP_LAUNCH = 12,     // agents = {handle} -> rc = slot (-1: every slot in flight)
   GPUMON_PROBE_OP_WAIT = 13,       // agents = {handle, slot}, window_s = timeout -> rc 1 + gpumon_probe_result_t | 0
   GPUMON_PROBE_OP_DESTROY = 14,    // agents = {handle}
+  // one sampler step in one request: agents = {handle, pending slot (-1: launch now)} per probe,
+  // window_s = timeout -> rc = n, payload gpumon_probe_cycle_t[n]. Launch and completion are seen
+  // within one awake period, so host_latency_s never includes the time the helper was stopped.
+  GPUMON_PROBE_OP_CYCLE = 15,
 };
+
+typedef struct {
+  int32_t pending;  // slot still in flight after the step (-1: completed or nothing launched)
+  int32_t got;      // 1: `result` holds the completed launch
+  gpumon_probe_result_t result;
+} gpumon_probe_cycle_t;
 
 // request: header, int32 agents[n_agents], char counters[counters_len] ('\n'-separated)
 typedef struct {
@@ -47,6 +57,7 @@ typedef struct {
 //   AGENT: gpumon_pmc_agent_t
 //   SAMPLE_MANY / READ_RUNNING: gpumon_pmc_value_t[n_agents * n_counters], int32 ok[n_agents]
 //   PROBE_WAIT (rc 1): gpumon_probe_result_t
+//   PROBE_CYCLE: gpumon_probe_cycle_t[n]
 typedef struct {
   uint32_t magic;
   int32_t rc;

@@ -452,8 +452,6 @@ def test_isolated_probe_runs_in_the_helper(core, mock_exporter, monkeypatch):
         m = ex.metrics_text()
         for g in ("0", "1"):
             assert _val(m, "gpu_probe_latency_seconds", gpu_id=g) is not None
-        maps = open("/proc/self/maps").read()
-        assert "libgpumon_probe.so" not in maps and "libgpumon_pmc.so" not in maps
         (pid,) = _helper_pids()
         assert _state(pid) == "T"
         os.kill(pid, signal.SIGKILL)
@@ -464,3 +462,30 @@ def test_isolated_probe_runs_in_the_helper(core, mock_exporter, monkeypatch):
         assert _val(ex.metrics_text(), "gpumon_pmc_up") == 0
     finally:
         od.stop()
+
+
+def test_isolated_exporter_maps_no_plugin():
+    """The deployed shape: bin/gpumon-exporter with --pmc --probe maps neither plugin (nor, on a GPU
+    node, the runtimes behind them); its one child, the helper, maps both."""
+    import time
+
+    e = dict(os.environ, GPUMON_FAKE_AGENTS="2")
+    p = subprocess.Popen([BIN, "--backend", "mock:gpus=2", "--listen", "127.0.0.1:0", "--interval", "0.1",
+                          "--no-pod-resources", "--no-cri", "--pmc", "--probe", "--plugin-dir", FAKE_DIR,
+                          "--log-level", "error"], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=e, text=True)
+    try:
+        kids = []
+        for _ in range(50):
+            time.sleep(0.1)
+            kids = [int(k) for k in open(f"/proc/{p.pid}/task/{p.pid}/children").read().split()]
+            if kids:
+                break
+        assert p.poll() is None and len(kids) == 1
+        time.sleep(0.5)
+        maps = open(f"/proc/{p.pid}/maps").read()
+        assert "libgpumon_probe.so" not in maps and "libgpumon_pmc.so" not in maps
+        helper = open(f"/proc/{kids[0]}/maps").read()
+        assert "libgpumon_probe.so" in helper and "libgpumon_pmc.so" in helper
+    finally:
+        p.terminate()
+        p.wait(20)
