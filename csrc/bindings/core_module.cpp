@@ -300,6 +300,8 @@ static py::dict tick_to_dict(const TickInfo& t) {
   d["t_attrib"] = t.t_attrib;
   d["t_render"] = t.t_render;
   d["t_gzip"] = t.t_gzip;
+  d["t_wake"] = t.t_wake;
+  d["t_device"] = t.t_device;
   d["link_refreshes"] = t.link_refreshes;
   d["ras_reads"] = t.ras_reads;
   d["ras_full"] = t.ras_full;

@@ -79,13 +79,17 @@ struct ExporterConfig {
 
 struct TickInfo {
   uint64_t seq = 0;
-  double duration_s = 0;
+  double duration_s = 0;  // tick start -> text snapshot published (sample-to-export latency)
   int devices = 0;
   int devices_ok = 0;
   size_t pod_rows = 0;
   size_t body_bytes = 0;
-  // phase breakdown (seconds): device metrics, process lists, attribution, render, gzip
+  // phase breakdown (seconds): device metrics, process lists, attribution, render; gzip runs after
+  // the text snapshot is published (not in duration_s)
   double t_sample = 0, t_procs = 0, t_attrib = 0, t_render = 0, t_gzip = 0;
+  // inside t_sample (parallel workers, max over devices): post -> worker picked the request up,
+  // and the worker's device calls (metrics table, links, RAS, process list)
+  double t_wake = 0, t_device = 0;
   int link_refreshes = 0;   // devices whose link metrics were re-read this tick
   int ras_reads = 0;        // devices that read a RAS slice this tick
   bool ras_full = false;    // the RAS read covered every file (first tick / ras_slices = 1)

@@ -695,7 +695,7 @@ void render_prometheus(const RenderInput& in, std::string* o) {
         f.add(dl[d], static_cast<double>(s.device_timeouts[d]));
     }
     histogram(o, "gpumon_sample_duration_seconds",
-              "Time to sample all GPUs, attribute processes and render one tick.", s.sample_hist, hl);
+              "Time to sample all GPUs, attribute processes, render and publish one tick (gzip follows the publish).", s.sample_hist, hl);
     histogram(o, "gpumon_scrape_duration_seconds",
               "Server-side /metrics latency (request parsed -> response written).", s.scrape_hist, hl);
     {
