@@ -153,7 +153,7 @@ bool helper_spawn(const std::string& path, std::string* err) {
   std::lock_guard<std::mutex> g(g_helper.mu);
   if (g_helper.pid > 0) return true;
   if (::access(path.c_str(), X_OK) != 0) {
-    *err = "pmc helper " + path + " not found / not executable";
+    *err = "on-device helper " + path + " not found / not executable";
     return false;
   }
   int req[2], resp[2];
@@ -196,7 +196,7 @@ int helper_call(uint32_t op, const int* agents, int n_agents, const char* const*
                 double window_s, std::vector<char>* payload, int32_t* started, std::string* err) {
   std::lock_guard<std::mutex> g(g_helper.mu);
   if (g_helper.pid <= 0) {
-    *err = "pmc helper not running";
+    *err = "on-device helper not running";
     return -1;
   }
   if (g_helper.frozen) {
@@ -224,7 +224,7 @@ int helper_call(uint32_t op, const int* agents, int n_agents, const char* const*
     ok = h.payload_len == 0 || io_full(g_helper.from, payload->data(), payload->size(), false, deadline);
   }
   if (!ok) {
-    *err = "pmc helper " + g_helper.path + " died or timed out";
+    *err = "on-device helper " + g_helper.path + " died or timed out";
     helper_kill_locked();  // the next start spawns a fresh one
     return -1;
   }
@@ -258,7 +258,7 @@ int h_values(uint32_t op, const int* agents, int n_agents, const char* const* co
   const int rc = helper_call(op, agents, n_agents, counters, n_counters, window_s, &p, started, &e);
   const size_t nv = static_cast<size_t>(n_agents) * n_counters;
   if (rc != 0 || p.size() != nv * sizeof(gpumon_pmc_value_t) + n_agents * sizeof(int32_t)) {
-    if (err && errlen) snprintf(err, errlen, "%s", e.empty() ? "pmc helper: bad response" : e.c_str());
+    if (err && errlen) snprintf(err, errlen, "%s", e.empty() ? "on-device helper: bad response" : e.c_str());
     return rc != 0 ? rc : -1;
   }
   memcpy(out, p.data(), nv * sizeof(gpumon_pmc_value_t));
