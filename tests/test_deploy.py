@@ -185,3 +185,41 @@ def test_ondevice_overlay_enables_pmc_and_sizes_limits():
     mib = int(res["limits"]["memory"].rstrip("Mi"))
     req = int(res["requests"]["memory"].rstrip("Mi"))
     assert 636 * 1.2 <= req <= mib  # 0.64 GB measured with PMC + probe, all of it in the helper
+
+
+def _json_patch(doc, ops):
+    """The add / replace subset of RFC 6902 that the overlays use (kustomize applies the real one)."""
+    import copy
+
+    doc = copy.deepcopy(doc)
+    for op in ops:
+        keys = [k.replace("~1", "/").replace("~0", "~") for k in op["path"].lstrip("/").split("/")]
+        parent = doc
+        for k in keys[:-1]:
+            parent = parent[int(k)] if isinstance(parent, list) else parent[k]
+        last = keys[-1]
+        if isinstance(parent, list):
+            if op["op"] == "add":
+                parent.insert(len(parent) if last == "-" else int(last), op["value"])
+            else:
+                parent[int(last)] = op["value"]
+        else:
+            assert op["op"] == "add" or last in parent, op["path"]
+            parent[last] = op["value"]
+    return doc
+
+
+def test_ondevice_overlay_patches_apply_to_the_base_daemonset():
+    """Every DaemonSet op of the overlay resolves against the base manifest, and every volume mount
+    of the patched pod names a volume (the helper's runtimes get a writable /tmp under the base's
+    read-only root filesystem)."""
+    (k,) = _docs("deploy/k8s/overlays/ondevice/kustomization.yaml")
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"])
+    out = _json_patch(ds, ops)
+    pod = out["spec"]["template"]["spec"]
+    vols = {v["name"] for v in pod["volumes"]}
+    c = pod["containers"][0]
+    assert all(m["name"] in vols for m in c["volumeMounts"])
+    assert any(m["mountPath"] == "/tmp" for m in c["volumeMounts"]) and c["securityContext"]["readOnlyRootFilesystem"]
+    assert c["resources"]["limits"]["memory"] == "1024Mi"
