@@ -18,6 +18,7 @@
 #include "../core/render.h"
 #include "../core/snapshot.h"
 #include "../core/trace.h"
+#include "../core/sysfs_fast.h"
 
 namespace py = pybind11;
 using namespace gpumon;
@@ -510,6 +511,15 @@ PYBIND11_MODULE(_core, m) {
         "Load librocprofiler-sdk-roctx and bracket sampler phases with ROCTx ranges");
   m.def("roctx_active", &Roctx::active);
   m.def("roctx_ranges", &Roctx::ranges, "ROCTx ranges opened so far by this process");
+  m.def(
+      "fd_table_stats",
+      [] {
+        py::dict d;
+        d["scans"] = gpumon::DrmFdTables::get().scans();
+        d["entries"] = gpumon::DrmFdTables::get().size();
+        return d;
+      },
+      "node-wide /proc/<pid>/fd scan cache of the sysfs fast path (scans so far, cached processes)");
   m.def("gzip", [](const std::string& s) {
     std::string o;
     if (!gzip_compress(s, &o)) throw std::runtime_error("gzip failed");

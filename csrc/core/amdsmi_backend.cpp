@@ -611,6 +611,10 @@ bool AmdSmiBackend::processes(int i, std::vector<ProcSample>* out) {
   return false;
 }
 
+void AmdSmiBackend::maintain(int i) {
+  if (i >= 0 && i < static_cast<int>(fast_.size()) && fast_[i]) fast_[i]->maintain();
+}
+
 bool AmdSmiBackend::supports_occupancy(int i) const {
   return i >= 0 && i < static_cast<int>(fast_.size()) && fast_[i] && fast_[i]->have_kfd();
 }

@@ -51,6 +51,9 @@ class Backend {
     out->assign(pids.size(), kNaN);
   }
   virtual void sample_ras(int, DeviceSample*, int /*slice*/ = 0, int /*nslices*/ = 1) {}
+  // Upkeep that must stay off the tick's critical path (the device worker calls it after it
+  // published the tick's sample): e.g. refreshing cached /proc fd tables.
+  virtual void maintain(int /*i*/) {}
   // Restrict to a subset of device hip_ids (empty = all). Applied at init().
   void set_device_filter(const std::vector<int>& ids) { filter_ = ids; }
 
@@ -201,6 +204,7 @@ class AmdSmiBackend : public Backend {
   bool supports_ras() const override { return true; }
   void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;
   bool supports_occupancy(int i) const override;  // with the sysfs fast path (KFD files)
+  void maintain(int i) override;                   // fast path: due /proc fd-table refreshes
   void occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) override;
   std::string lib_version() const { return lib_version_; }
   // Expose every physical device `r` times (distinct gpu_id labels). Only for measuring how the

@@ -196,6 +196,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
         have_ras_ready = true;
       }
     }
+    if (procs) backend->maintain(i);
   }
 }
 
@@ -533,6 +534,7 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
     }
     *procs_s = proc_ns * 1e-9;
     info->t_device = (mono_ns() - t_seq0) * 1e-9;
+    seq_maintain_ = cfg_.processes;  // tick() runs the upkeep after it published
     return;
   }
   const uint64_t id = ++tick_id_;
@@ -908,6 +910,10 @@ TickInfo Exporter::tick() {
     seq_ = s;
   }
   seq_cv_.notify_all();
+  if (seq_maintain_) {  // sequential sampling: no device worker to do it after the publish
+    seq_maintain_ = false;
+    for (int i = 0; i < backend_->device_count(); ++i) backend_->maintain(i);
+  }
   if (!influx.empty()) {
     std::lock_guard<std::mutex> g(push_mu_);
     last_influx_ = influx;

@@ -226,6 +226,7 @@ class Exporter {
   bool stop_workers();
   bool workers_busy() const;
   std::vector<std::shared_ptr<DevWorker>> workers_;
+  bool seq_maintain_ = false;  // sequential tick: run Backend::maintain after the publish
   std::atomic<uint64_t> hidden_contexts_{0};  // empty GPU contexts left out of the last tick's rows
   // cu_occupancy sub-sample reads by the workers (shared: a detached worker may outlive a restart)
   std::shared_ptr<std::atomic<uint64_t>> occ_reads_ = std::make_shared<std::atomic<uint64_t>>(0);

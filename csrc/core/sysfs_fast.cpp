@@ -126,37 +126,117 @@ bool SysfsGpu::read_gtt(double* used) {
   return true;
 }
 
+DrmFdTables& DrmFdTables::get() {
+  static DrmFdTables t;
+  return t;
+}
+
+void DrmFdTables::scan(const std::string& pdir, std::vector<std::pair<int, std::string>>* fds) {
+  fds->clear();
+  DIR* d = opendir((pdir + "/fd").c_str());
+  if (!d) return;
+  char target[256];
+  while (dirent* e = readdir(d)) {
+    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+    ssize_t n = readlink((pdir + "/fd/" + e->d_name).c_str(), target, sizeof target - 1);
+    if (n <= 0) continue;
+    target[n] = 0;
+    if (!strncmp(target, "/dev/dri/", 9)) fds->emplace_back(atoi(e->d_name), target);
+  }
+  closedir(d);
+}
+
+void DrmFdTables::fds_for(const std::string& pdir, const std::string& render, std::vector<int>* out) {
+  out->clear();
+  const int64_t now = mono_ns();
+  std::unique_lock<std::mutex> lk(mu_);
+  auto it = m_.find(pdir);
+  if (it == m_.end()) {
+    // first sight: scan now (this tick), outside the lock, once: another GPU's worker that needs
+    // the same process meanwhile waits for this scan instead of repeating it
+    m_[pdir].scanning = true;
+    lk.unlock();
+    std::vector<std::pair<int, std::string>> fds;
+    scan(pdir, &fds);
+    scans_++;
+    lk.lock();
+    Entry& e = m_[pdir];
+    e.fds = std::move(fds);
+    e.scanned_ns = e.used_ns = now;
+    e.scanning = false;
+    cv_.notify_all();
+    it = m_.find(pdir);
+  } else {
+    cv_.wait(lk, [&] {
+      it = m_.find(pdir);
+      return it == m_.end() || !it->second.scanning;
+    });
+    if (it == m_.end()) return;
+  }
+  Entry& e = it->second;
+  e.used_ns = now;
+  if (now - e.scanned_ns > 10'000'000'000ll) e.want = true;  // refreshed off the tick
+  for (const auto& [fd, target] : e.fds)
+    if (target == render) out->push_back(fd);
+}
+
+void DrmFdTables::invalidate(const std::string& pdir) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = m_.find(pdir);
+  if (it != m_.end()) it->second.want = true;
+}
+
+int DrmFdTables::refresh_due(int max_scans) {
+  const int64_t now = mono_ns();
+  std::vector<std::string> due;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (auto it = m_.begin(); it != m_.end();) {
+      if (!it->second.scanning && now - it->second.used_ns > 60'000'000'000ll) {  // unlisted for 60 s
+        it = m_.erase(it);
+        continue;
+      }
+      if (it->second.want && static_cast<int>(due.size()) < max_scans) {
+        it->second.want = false;  // claimed: another worker's maintain() skips it
+        due.push_back(it->first);
+      }
+      ++it;
+    }
+  }
+  for (const auto& pdir : due) {
+    std::vector<std::pair<int, std::string>> fds;
+    scan(pdir, &fds);
+    scans_++;
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = m_.find(pdir);
+    if (it == m_.end()) continue;
+    it->second.fds = std::move(fds);
+    it->second.scanned_ns = mono_ns();
+  }
+  return static_cast<int>(due.size());
+}
+
+size_t DrmFdTables::size() {
+  std::lock_guard<std::mutex> g(mu_);
+  return m_.size();
+}
+
+void SysfsGpu::maintain() { DrmFdTables::get().refresh_due(64); }
+
 void SysfsGpu::fdinfo_usage(uint32_t pid, ProcSample* p) {
   if (render_path_.empty()) return;
   const std::string base = proc_root_ + "/" + std::to_string(pid);
-  const int64_t now = mono_ns();
-  FdCache& c = fd_cache_[pid];
-  // The set of DRM fds of a process is stable; rescan the fd table every 10 s only.
-  if (c.scanned_ns == 0 || now - c.scanned_ns > 10'000'000'000ll) {
-    c.fds.clear();
-    c.scanned_ns = now;
-    DIR* d = opendir((base + "/fd").c_str());
-    if (d) {
-      char target[256];
-      while (dirent* e = readdir(d)) {
-        if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
-        ssize_t n = readlink((base + "/fd/" + e->d_name).c_str(), target, sizeof target - 1);
-        if (n <= 0) continue;
-        target[n] = 0;
-        if (render_path_ == target) c.fds.push_back(atoi(e->d_name));
-      }
-      closedir(d);
-    }
-  }
-  if (c.fds.empty()) return;
+  std::vector<int> fds;
+  DrmFdTables::get().fds_for(base, render_path_, &fds);
+  if (fds.empty()) return;
   uint64_t gfx = 0, vram = 0, gtt = 0, cpu = 0;
   bool any = false, have_vram = false;
   std::vector<uint64_t> clients;
   char text[4096];
-  for (int fd : c.fds) {
+  for (int fd : fds) {
     size_t n = 0;
     if (!read_small(base + "/fdinfo/" + std::to_string(fd), text, sizeof text, &n)) {
-      c.scanned_ns = 0;  // fd closed: rescan next tick
+      DrmFdTables::get().invalidate(base);  // fd closed: rescan off the tick
       continue;
     }
     uint64_t cid = 0;
@@ -210,7 +290,6 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out) {
   if (!d) return false;
   const std::string vram_name = "/vram_" + std::to_string(kfd_gpu_id_);
   const std::string occ_name = "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy";
-  std::vector<uint32_t> seen;
   char b[64];
   while (dirent* e = readdir(d)) {
     if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
@@ -224,16 +303,9 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out) {
     p.vram_bytes = p.mem_bytes;
     if (read_small(pdir + occ_name, b, sizeof b, &n)) p.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
     fdinfo_usage(pid, &p);
-    seen.push_back(pid);
     out->push_back(std::move(p));
   }
   closedir(d);
-  // forget fd tables of processes that left this GPU
-  for (auto it = fd_cache_.begin(); it != fd_cache_.end();) {
-    bool alive = false;
-    for (uint32_t s : seen) alive |= (s == it->first);
-    it = alive ? std::next(it) : fd_cache_.erase(it);
-  }
   return true;
 }
 

@@ -18,7 +18,10 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <atomic>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -195,18 +198,44 @@ class SysfsGpu {
   // Instantaneous KFD cu_occupancy of each pid on this GPU (NaN where the file is unreadable).
   void occupancy(const std::vector<uint32_t>& pids, std::vector<double>* out);
   bool have_kfd() const { return kfd_gpu_id_ != 0; }
+  // Off-tick upkeep (device worker, after it published): refreshes due /proc/<pid>/fd scans.
+  void maintain();
 
  private:
-  struct FdCache {
-    int64_t scanned_ns = 0;
-    std::vector<int> fds;  // this GPU's DRM render-node fds of the process
-  };
   void fdinfo_usage(uint32_t pid, ProcSample* p);
   std::string sys_root_, proc_root_, dev_dir_;
   uint64_t kfd_gpu_id_ = 0;
   std::string render_path_;  // "/dev/dri/renderD<minor>"
   int fd_metrics_ = -1, fd_vram_used_ = -1, fd_vram_total_ = -1, fd_gtt_used_ = -1;
-  std::unordered_map<uint32_t, FdCache> fd_cache_;
+};
+
+// Node-wide DRM fd tables of GPU processes. /proc/<pid>/fd lists every open file of a process
+// (thousands for a data-loading trainer), so readdir + readlink over it is the one per-process read
+// whose cost grows with the workload. One scan serves every GPU (each keeps the fds that point at
+// its own render node); a process is scanned on the tick it first appears, and the 10 s refreshes
+// (or the rescan after an fd vanished) run off the tick from SysfsGpu::maintain().
+class DrmFdTables {
+ public:
+  static DrmFdTables& get();
+  // fds of the process (pdir = <proc_root>/<pid>) that point at `render`
+  void fds_for(const std::string& pdir, const std::string& render, std::vector<int>* out);
+  void invalidate(const std::string& pdir);  // an fd vanished: rescan at the next maintain()
+  int refresh_due(int max_scans);            // scans done
+  uint64_t scans() const { return scans_.load(); }
+  size_t size();
+
+ private:
+  struct Entry {
+    int64_t scanned_ns = 0, used_ns = 0;
+    bool want = false;
+    bool scanning = false;  // first scan in flight (fds_for waits for it)
+    std::vector<std::pair<int, std::string>> fds;  // (fd, /dev/dri/... target)
+  };
+  static void scan(const std::string& pdir, std::vector<std::pair<int, std::string>>* fds);
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::unordered_map<std::string, Entry> m_;
+  std::atomic<uint64_t> scans_{0};
 };
 
 }  // namespace gpumon

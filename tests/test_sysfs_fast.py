@@ -65,12 +65,14 @@ def make_tree(tmp, gpus=2, blob_kw=None, procs=((4242, 0),)):
         (kp / f"vram_{36622 + d}").write_text(f"{2 << 30}\n")
         (kp / f"stats_{36622 + d}" / "cu_occupancy").write_text("17\n")
         fd, fdinfo = procr / str(pid) / "fd", procr / str(pid) / "fdinfo"
-        fd.mkdir(parents=True)
-        fdinfo.mkdir()
-        os.symlink(f"/dev/dri/renderD{152 + d}", fd / "5")
-        os.symlink(f"/dev/dri/renderD{152 + d}", fd / "6")  # dup() of the same DRM file
-        os.symlink("/dev/null", fd / "7")
-        for n in ("5", "6"):
+        fd.mkdir(parents=True, exist_ok=True)
+        fdinfo.mkdir(exist_ok=True)
+        a, b = str(5 + 10 * d), str(6 + 10 * d)
+        os.symlink(f"/dev/dri/renderD{152 + d}", fd / a)
+        os.symlink(f"/dev/dri/renderD{152 + d}", fd / b)  # dup() of the same DRM file
+        if not (fd / "7").is_symlink():
+            os.symlink("/dev/null", fd / "7")
+        for n in (a, b):
             (fdinfo / n).write_text("pos:\t0\nflags:\t02100002\ndrm-driver:\tamdgpu\ndrm-client-id:\t7\n"
                                     "drm-engine-gfx:\t5000000 ns\ndrm-memory-vram:\t1048576 KiB\n"
                                     "drm-memory-gtt:\t2048 KiB\n")
@@ -165,3 +167,37 @@ def test_compare_tables_binding(core, tmp_path, monkeypatch):
     assert rows["temperature_hotspot"] == (47, 47)
     assert rows["average_gfx_activity"] == (37, 77)
     assert rows["xgmi_link_status[3]"] == (1, 1)
+
+
+def test_fd_tables_are_shared_across_gpus_and_refreshed_off_tick(exporter, tmp_path, core):
+    """A process on both GPUs has its /proc/<pid>/fd table scanned once per node, not once per
+    GPU; a vanished fd makes the next tick's upkeep (after the publish) rescan it, and the tick
+    after that reads the new fd."""
+    sysr, procr = make_tree(tmp_path, procs=((4242, 0), (4242, 1)))
+    s0 = core.fd_table_stats()["scans"]
+    ex = exporter(sysr, procr, sample_threads=2, interval_s=0)  # start() runs the first tick
+    ex.tick()
+    rows = sorted((r["dev"], r["used_memory_bytes"]) for r in ex.pod_rows() if not r["idle"])
+    assert rows == [(0, 1 << 30), (1, 1 << 30)]
+    assert core.fd_table_stats()["scans"] - s0 == 1  # one scan served both GPUs
+    ex.tick()
+    assert core.fd_table_stats()["scans"] - s0 == 1  # cached
+    # the process closes fd 5 and opens fd 9 on GPU 0's render node
+    fd, fdinfo = procr / "4242" / "fd", procr / "4242" / "fdinfo"
+    text = (fdinfo / "5").read_text().replace("1048576 KiB", "2097152 KiB")
+    (fd / "5").unlink()
+    (fdinfo / "5").unlink()
+    (fd / "6").unlink()
+    (fdinfo / "6").unlink()
+    os.symlink("/dev/dri/renderD152", fd / "9")
+    (fdinfo / "9").write_text(text)
+    ex.tick()  # fdinfo/5 is gone: invalidated, rescanned by a worker after this tick's publish
+    import time
+
+    deadline = time.time() + 5
+    while core.fd_table_stats()["scans"] - s0 < 2 and time.time() < deadline:
+        time.sleep(0.01)
+    assert core.fd_table_stats()["scans"] - s0 == 2
+    ex.tick()  # the worker finished its upkeep before taking this tick
+    rows = dict((r["dev"], r["used_memory_bytes"]) for r in ex.pod_rows() if not r["idle"])
+    assert rows[0] == 2 << 30
