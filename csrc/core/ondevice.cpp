@@ -207,8 +207,10 @@ int helper_call(uint32_t op, const int* agents, int n_agents, const char* const*
   for (int c = 0; c < n_counters; ++c) names += std::string(counters[c]) + "\n";
   gpumon_pmc_req_t q{GPUMON_PMC_PROTO_MAGIC, op, static_cast<uint32_t>(std::max(0, n_agents)),
                      static_cast<uint32_t>(names.size()), window_s};
-  // init brings HSA + rocprofiler up (seconds on a fresh node); a read takes milliseconds
-  const int64_t deadline = mono_ns() + static_cast<int64_t>((op == GPUMON_PMC_OP_INIT ? 60.0 : 10.0 + window_s) * 1e9);
+  // init brings HSA + rocprofiler up, and the first probe op HIP (seconds on a fresh node, more
+  // while the runtime pages in); a read or a probe cycle takes milliseconds plus its own window
+  const bool slow = op == GPUMON_PMC_OP_INIT || op == GPUMON_PROBE_OP_COUNT || op == GPUMON_PROBE_OP_CREATE;
+  const int64_t deadline = mono_ns() + static_cast<int64_t>((slow ? 60.0 : 10.0 + window_s) * 1e9);
   gpumon_pmc_resp_t h{};
   std::string e;
   bool ok = io_full(g_helper.to, &q, sizeof q, true, deadline) &&
