@@ -4,7 +4,6 @@ fleet test: several node-local exporters scraped by one scraper (the reference's
 
 import os
 
-import pytest
 from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 

@@ -8,7 +8,6 @@ import sys
 
 import pytest
 
-from gpumon.ops.pmc import derive
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

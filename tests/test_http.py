@@ -10,7 +10,6 @@ import http.client
 import socket
 import threading
 
-import pytest
 
 from gpumon.export import promtext
 

@@ -3,7 +3,6 @@
 sysfs table twice, 1 s apart, idle and under the bf16 burn, and print delta / delta(accumulation_counter)
 for gfx_busy_acc, gfx_below_host_limit_{ppt,thm,total}_acc and gfx_low_utilization_acc."""
 
-import glob
 import json
 import os
 import struct
