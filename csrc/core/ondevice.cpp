@@ -16,6 +16,10 @@
 #include <cstdlib>
 #include <cctype>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 
 #include "../plugins/ondevice_abi.h"
 #include "../plugins/ondevice_helper_proto.h"
@@ -149,6 +153,42 @@ void helper_kill_locked() {
   g_helper.frozen = false;
 }
 
+// PR_SET_PDEATHSIG (the helper's tie to the exporter) fires when the THREAD that spawned it exits,
+// not the process: spawns run on one thread that lives as long as the process, whichever thread
+// called start() (a Python caller's worker thread may come and go).
+int spawn_on_keeper(const std::function<int()>& job) {
+  struct Keeper {
+    std::mutex mu;
+    std::condition_variable cv;
+    const std::function<int()>* job = nullptr;
+    int rc = 0;
+    bool done = false;
+  };
+  static Keeper* k = [] {
+    auto* kp = new Keeper;  // never freed: the detached thread may still wait on it at exit
+    std::thread([kp] {
+      set_thread_name("gpumon-spawner");
+      std::unique_lock<std::mutex> lk(kp->mu);
+      for (;;) {
+        kp->cv.wait(lk, [kp] { return kp->job != nullptr; });
+        kp->rc = (*kp->job)();
+        kp->job = nullptr;
+        kp->done = true;
+        kp->cv.notify_all();
+      }
+    }).detach();
+    return kp;
+  }();
+  static std::mutex one;  // one spawn at a time
+  std::lock_guard<std::mutex> g(one);
+  std::unique_lock<std::mutex> lk(k->mu);
+  k->done = false;
+  k->job = &job;
+  k->cv.notify_all();
+  k->cv.wait(lk, [] { return k->done; });
+  return k->rc;
+}
+
 bool helper_spawn(const std::string& path, std::string* err) {
   std::lock_guard<std::mutex> g(g_helper.mu);
   if (g_helper.pid > 0) return true;
@@ -173,7 +213,7 @@ bool helper_spawn(const std::string& path, std::string* err) {
   posix_spawn_file_actions_adddup2(&fa, resp[1], 1);
   char* argv[] = {const_cast<char*>(path.c_str()), nullptr};
   pid_t pid = -1;
-  const int rc = posix_spawn(&pid, path.c_str(), &fa, nullptr, argv, environ);
+  const int rc = spawn_on_keeper([&] { return posix_spawn(&pid, path.c_str(), &fa, nullptr, argv, environ); });
   posix_spawn_file_actions_destroy(&fa);
   ::close(req[0]);
   ::close(resp[1]);

@@ -477,7 +477,8 @@ def test_isolated_exporter_maps_no_plugin():
         kids = []
         for _ in range(50):
             time.sleep(0.1)
-            kids = [int(k) for k in open(f"/proc/{p.pid}/task/{p.pid}/children").read().split()]
+            kids = [int(k) for t in os.listdir(f"/proc/{p.pid}/task")  # any thread may be the parent
+                    for k in open(f"/proc/{p.pid}/task/{t}/children").read().split()]
             if kids:
                 break
         assert p.poll() is None and len(kids) == 1
@@ -489,3 +490,28 @@ def test_isolated_exporter_maps_no_plugin():
     finally:
         p.terminate()
         p.wait(20)
+
+
+def test_helper_outlives_the_thread_that_started_it(core, mock_exporter, monkeypatch):
+    """PR_SET_PDEATHSIG follows the spawning THREAD: the helper is spawned from a process-lifetime
+    thread, so starting the samplers from a short-lived thread does not kill it when that ends."""
+    import threading
+    import time
+
+    monkeypatch.setenv("GPUMON_FAKE_MFMA", "0.3")
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
+    t = threading.Thread(target=od.start)
+    t.start()
+    t.join()
+    try:
+        time.sleep(0.2)
+        assert len(_helper_pids()) == 1
+        od.step()
+        time.sleep(0.05)
+        od.step()
+        assert od.stats()["pmc_errors"] == 0
+        ex.tick()
+        assert _val(ex.metrics_text(), "gpu_mfma_busy_active_percent", gpu_id="0") == pytest.approx(30.0)
+    finally:
+        od.stop()
