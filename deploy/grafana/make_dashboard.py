@@ -106,6 +106,17 @@ def build():
                           "{{host}} gpu{{gpu_id}} {{reason}}")], 12, y, 12, 8,
                         fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
     y += 8
+    # Q4 fixed: the reference copied device utilisation onto every process row (gpu.py:205)
+    panels.append(panel("Per-process GPU busy % (share of the interval with the process's waves resident)",
+                        "timeseries",
+                        [(f'max by (host, gpu_id, namespace, podname, pid) (pod_gpu_proc_gfx_util{{{HOST}}})',
+                          "{{host}} gpu{{gpu_id}} {{namespace}}/{{podname}} pid {{pid}}")], 0, y, 12, 8,
+                        fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
+    panels.append(panel("On-device samplers: PMC up / counter resets (tenant profilers)", "timeseries",
+                        [(f'gpumon_pmc_up{{{HOST}}}', "{{host}} pmc up"),
+                         (f'increase(gpumon_pmc_resets_total{{{HOST}}}[5m])', "{{host}} resets / 5m")],
+                        12, y, 12, 8))
+    y += 8
     panels.append(panel("RAS: ECC errors by block (uncorrectable / correctable / deferred)", "table",
                         [(f'sum by (host, gpu_id, block, type) (gpu_ecc_errors_total{{{HOST}}}) > 0', "")], 0, y, 12, 8))
     panels.append(panel("RAS: retired HBM pages and poison / fatal events", "timeseries",

@@ -64,7 +64,7 @@ def _plugin_metric_names():
         if f.endswith(".py"):
             names |= set(re.findall(r'"(gpu_[a-z0-9_]+)"', open(os.path.join(ROOT, "gpumon/ops", f)).read()))
     # the production on-device samplers (native)
-    names |= set(re.findall(r'"(gpu_[a-z0-9_]+)"', open(os.path.join(ROOT, "csrc/core/ondevice.cpp")).read()))
+    names |= set(re.findall(r'"((?:gpu|gpumon)_[a-z0-9_]+)"', open(os.path.join(ROOT, "csrc/core/ondevice.cpp")).read()))
     return names
 
 
@@ -88,7 +88,7 @@ def test_dashboard_queries_resolve_against_exposition(mock_exporter):
         for n, _, _ in v["samples"]:
             produced.add(n)
     plugins = _plugin_metric_names()
-    words = {"sum", "by", "count", "rate", "max", "histogram_quantile", "le", "host", "user_name", "link",
+    words = {"sum", "by", "count", "rate", "increase", "max", "histogram_quantile", "le", "host", "user_name", "link",
              "gpu_id", "state", "m", "s"}
     missing = []
     titles = []
