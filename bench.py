@@ -271,6 +271,9 @@ def main() -> int:
                     dist.all_reduce(ar_buf)
     barrier()
     elapsed = time.perf_counter() - t0
+    if rank == 0:  # the exporter's counters at the end of the timed region (not after the reductions)
+        s1 = mon.ex.self_stats()
+        seq1 = mon.ex.seq
     c1 = [c.stats() for c in copiers]
     l1 = [ld.stats() for ld in loads]
     if dist is not None:
@@ -319,12 +322,11 @@ def main() -> int:
 
     result = None
     if rank == 0:
-        s1 = mon.ex.self_stats()
         if scraper is not None:
             scraper.join(timeout=args.interval * 5 + 30)
         lat = scrape_result.get("latencies_s", [])
         samples = s1["samples"] - s0["samples"]
-        ticks = mon.ex.seq - seq0
+        ticks = seq1 - seq0
         timed = [t for t in mon.ex.tick_log() if seq0 < t["seq"] <= seq0 + ticks]
         tdur = [t["duration_s"] for t in timed]
         slow = max(timed, key=lambda t: t["duration_s"]) if timed else None

@@ -39,6 +39,7 @@ OnDeviceConfig ondevice_from(const py::dict& d) {
   get(d, "pmc_window_s", &c.pmc_window_s);
   get(d, "pmc_mode", &c.pmc_mode);
   get(d, "ondevice_isolate", &c.ondevice_isolate);
+  get(d, "helper_retry_s", &c.helper_retry_s);
   get(d, "probe", &c.probe);
   get(d, "probe_every_s", &c.probe_every_s);
   get(d, "probe_blocks", &c.probe_blocks);
@@ -814,6 +815,7 @@ PYBIND11_MODULE(_core, m) {
         d["pmc_errors"] = s.pmc_errors;
         d["pmc_resets"] = s.pmc_resets;
         d["pmc_continuous"] = s.pmc_continuous;
+        d["helper_restarts"] = s.helper_restarts;
         d["probe_done"] = s.probe_done;
         d["probe_timeouts"] = s.probe_timeouts;
         d["pmc_agents"] = s.pmc_agents;

@@ -231,6 +231,11 @@ bool helper_spawn(const std::string& path, std::string* err) {
   return true;
 }
 
+bool helper_alive() {
+  std::lock_guard<std::mutex> g(g_helper.mu);
+  return g_helper.pid > 0;
+}
+
 // One request / response; the helper runs only for the duration of the call.
 int helper_call(uint32_t op, const int* agents, int n_agents, const char* const* counters, int n_counters,
                 double window_s, std::vector<char>* payload, int32_t* started, std::string* err) {
@@ -496,7 +501,8 @@ bool OnDevice::start(std::string* err) {
   if (cfg_.ondevice_isolate && (cfg_.pmc || cfg_.probe)) {
     // device counting contexts and the probe in one helper process, frozen between requests
     // (ondevice_helper_proto.h): this process never loads HIP, HSA or rocprofiler-sdk
-    if (!helper_spawn(dir + "/gpumon-ondevice-helper", err)) return false;
+    helper_path_ = dir + "/gpumon-ondevice-helper";
+    if (!helper_spawn(helper_path_, err)) return false;
     helper_ = true;
   }
   if (cfg_.pmc) {
@@ -564,6 +570,7 @@ bool OnDevice::start(std::string* err) {
                "probe plugin " + probe_lib_->path + " devices=" + std::to_string(probes_.size()) +
                    (probes_.empty() ? " (device list not known yet: created on the first step that has it)" : ""));
   }
+  if (helper_) export_helper();
   running_ = true;
   if (pmc_lib_) pmc_th_ = std::thread([this] {
     set_thread_name("gpumon-pmc");
@@ -598,7 +605,10 @@ void OnDevice::stop() {
     probes_.clear();
     ex_->set_extra("probe", {});
   }
-  if (helper_) helper_shutdown();  // after the probes' rings are drained and freed
+  if (helper_) {
+    helper_shutdown();  // after the probes' rings are drained and freed
+    ex_->set_extra("ondevice_helper", {});
+  }
   if (pmc_lib_) ex_->set_extra("pmc", {});
 }
 
@@ -631,7 +641,44 @@ OnDevice::Stats OnDevice::stats() const {
   s.probe_timeouts = probe_timeouts_;
   s.pmc_agents = static_cast<int>(agents_.size());
   s.probe_devices = static_cast<int>(probes_.size());
+  s.helper_restarts = helper_restarts_;
   return s;
+}
+
+bool OnDevice::helper_check() {
+  if (!helper_) return true;
+  std::lock_guard<std::mutex> g(recover_mu_);
+  if (helper_alive()) return true;
+  const int64_t now = mono_ns();
+  if (now < next_respawn_ns_) return false;
+  next_respawn_ns_ = now + static_cast<int64_t>(std::max(0.0, cfg_.helper_retry_s) * 1e9);
+  std::string err;
+  if (!helper_spawn(helper_path_, &err)) {
+    GPUMON_LOG(LogLevel::kWarn, "ondevice", "on-device helper respawn failed: " + err);
+    return false;
+  }
+  if (pmc_lib_) {  // rocprofiler must register before anything brings HSA up in the new helper
+    char ebuf[512] = {0};
+    if (pmc_lib_->pmc_init(ebuf, sizeof ebuf) < 0) {
+      GPUMON_LOG(LogLevel::kWarn, "ondevice", std::string("on-device helper respawned, pmc init failed: ") + ebuf);
+      helper_shutdown();
+      return false;
+    }
+  }
+  helper_gen_++;  // probe handles of the dead helper are void; the probe sampler recreates them
+  helper_restarts_++;
+  GPUMON_LOG(LogLevel::kWarn, "ondevice",
+             "on-device helper was gone: respawned " + helper_path_ + " (restart " +
+                 std::to_string(helper_restarts_.load()) + ")");
+  export_helper();
+  return true;
+}
+
+void OnDevice::export_helper() {
+  ex_->set_extra("ondevice_helper",
+                 {xs("gpumon_ondevice_helper_restarts_total",
+                     "Times the on-device helper process (PMC contexts + K1 probe) was found dead and respawned.",
+                     -1, static_cast<double>(helper_restarts_.load()), "counter")});
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -652,6 +699,14 @@ void OnDevice::map_pmc_agents() {
 
 void OnDevice::pmc_step() {
   std::lock_guard<std::mutex> g(pmc_mu_);
+  if (!helper_check()) {  // helper gone, respawn not due yet: no values, series withdrawn
+    pmc_errors_++;
+    pmc_up_ = false;
+    pmc_prev_.clear();
+    pmc_last_.clear();
+    export_pmc();
+    return;
+  }
   if (pmc_map_.empty()) map_pmc_agents();  // backend came up after start()
   if (pmc_map_.empty()) return;
   std::vector<int> devs, ags;
@@ -910,6 +965,16 @@ bool OnDevice::create_probes(std::string* err) {
 
 void OnDevice::probe_step() {
   std::lock_guard<std::mutex> g(probe_mu_);
+  if (!helper_check()) {
+    for (auto& p : probes_) p.timeouts++, probe_timeouts_++;
+    export_probe();
+    return;
+  }
+  if (helper_ && helper_gen_.load() != probe_gen_seen_) {
+    // a respawned helper: the old handles named probes in the dead process (nothing to free here)
+    probes_.clear();
+    probe_gen_seen_ = helper_gen_.load();
+  }
   if (probes_.empty()) {
     std::string err;
     if (!create_probes(&err)) GPUMON_LOG(LogLevel::kWarn, "ondevice", err);

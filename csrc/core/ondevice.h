@@ -49,6 +49,7 @@ struct OnDeviceConfig {
   // core in the process that owns the contexts; this process then never loads a GPU runtime);
   // false: the plugins in this process (tools that already run HIP / HSA).
   bool ondevice_isolate = true;
+  double helper_retry_s = 10.0;  // a dead helper is respawned at most this often
   double pmc_window_s = 0.1;  // window mode: counting window per sample (capped at half the period)
   bool probe = false;
   double probe_every_s = 1.0;
@@ -102,6 +103,7 @@ class OnDevice {
 
   struct Stats {
     uint64_t pmc_samples = 0, pmc_errors = 0, pmc_resets = 0, probe_done = 0, probe_timeouts = 0;
+    uint64_t helper_restarts = 0;
     int pmc_agents = 0, probe_devices = 0;
     bool pmc_continuous = false;
   };
@@ -122,6 +124,10 @@ class OnDevice {
   void export_pmc();
   void export_probe();
   void sleep_until(int64_t deadline_ns);
+  // ondevice_isolate: true when the helper is up; a dead helper (crashed, OOM-killed) is respawned
+  // and re-initialised here, at most once per helper_retry_s, by whichever sampler notices first
+  bool helper_check();
+  void export_helper();
 
   Exporter* ex_;
   OnDeviceConfig cfg_;
@@ -136,6 +142,11 @@ class OnDevice {
   int64_t pmc_prev_ns_ = 0;
   bool pmc_continuous_ = false;
   bool helper_ = false;         // pmc_lib_ / probe_lib_ are clients of the helper process
+  std::string helper_path_;
+  std::mutex recover_mu_;       // helper respawn + PMC re-init (before any probe op on a new helper)
+  int64_t next_respawn_ns_ = 0;
+  std::atomic<uint64_t> helper_gen_{0}, helper_restarts_{0};
+  uint64_t probe_gen_seen_ = 0;  // helper generation the probe handles belong to
   int64_t pmc_last_ok_ns_ = 0;  // last step that produced values (window or continuous)
   bool pmc_up_ = false;
 

@@ -29,7 +29,8 @@ def _check(d, n, steps, warmup):
     assert d["higher_is_better"] is True and d["scaling"] == "weak"
     assert set(d["config"]) >= {"model", "global_batch", "seq_len", "parallelism"}
     assert d["value"] > 0 and d["scrape_p99_ms"] > 0 and d["scrape_errors"] == 0
-    assert d["ticks"] == steps
+    # K waited-for ticks; at a 0.1 s interval the closing barrier (CPU all-reduces) can span another
+    assert steps <= d["ticks"] <= steps + 2
 
 
 def test_bench_single_process():

@@ -515,3 +515,42 @@ def test_helper_outlives_the_thread_that_started_it(core, mock_exporter, monkeyp
         assert _val(ex.metrics_text(), "gpu_mfma_busy_active_percent", gpu_id="0") == pytest.approx(30.0)
     finally:
         od.stop()
+
+
+def test_dead_helper_is_respawned_and_samplers_recover(core, mock_exporter, monkeypatch):
+    """A helper that dies (OOM-killed, crashed) is respawned by the next sampler step once
+    helper_retry_s has passed: PMC is re-initialised first (rocprofiler before HSA), the probes are
+    recreated, values come back and gpumon_ondevice_helper_restarts_total counts it."""
+    import signal
+    import time
+
+    monkeypatch.setenv("GPUMON_FAKE_MFMA", "0.5")
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, pmc_every_s=60, probe_every_s=60, pmc_mode="continuous", helper_retry_s=0.2)
+    od.start()
+    try:
+        od.step()
+        (pid,) = _helper_pids()
+        os.kill(pid, signal.SIGKILL)
+        od.step()  # the dead helper is noticed: errors, series withdrawn
+        ex.tick()
+        m = ex.metrics_text()
+        assert _val(m, "gpumon_pmc_up") == 0
+        time.sleep(0.3)
+        od.step()  # respawn + PMC init; the first continuous read only starts the new contexts
+        time.sleep(0.05)
+        od.step()
+        st = od.stats()
+        assert st["helper_restarts"] == 1
+        (pid2,) = _helper_pids()
+        assert pid2 != pid
+        ex.tick()
+        m = ex.metrics_text()
+        assert _val(m, "gpumon_pmc_up") == 1
+        assert _val(m, "gpu_mfma_busy_active_percent", gpu_id="0") == pytest.approx(50.0)
+        assert _val(m, "gpu_probe_latency_seconds", gpu_id="0") is not None
+        assert _val(m, "gpumon_ondevice_helper_restarts_total") == 1
+    finally:
+        od.stop()
+    time.sleep(0.1)
+    assert _helper_pids() == []
