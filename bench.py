@@ -17,6 +17,10 @@ HBM stream, csrc/hip/kernels.hip) and, for N > 1, xGMI traffic:
   peer-copy ring (GPU i pushes into GPU (i+1) mod N, ``_hip.XgmiLoad``): each GPU's tx equals its
   copy rate.
 
+Before any synthetic load starts, rank 0 runs the same scrape load for --idle-s seconds (untimed):
+``scrape_idle`` holds that idle reference (scrape p50 / p99, tick cost), so every run reports the
+BASELINE's "idle and under load" pair at its GPU count.
+
 The exporter's own per-GPU xGMI counters are compared with that expectation
 (``xgmi.per_gpu[].tx_vs_expected``), and after the timed region rank 0 drives GPU 0 -> k for every
 peer k and checks that the link whose counter moves is the one the exporter maps to k's BDF
@@ -128,6 +132,8 @@ def main() -> int:
     ap.add_argument("--link-check-s", type=float, default=0.6,
                     help="N > 1: seconds per peer of the GPU 0 -> k link-map check after the timed region (0 = off)")
     ap.add_argument("--probe", action="store_true", help="also run the K1 probe kernel each tick")
+    ap.add_argument("--idle-s", type=float, default=5.0,
+                    help="untimed idle reference before the load starts: scrape p50/p99 + tick cost (0 = off)")
     ap.add_argument("--no-fast-path", action="store_true", help="read every value through libamd_smi")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
@@ -155,29 +161,6 @@ def main() -> int:
         if has_gpu:
             torch.cuda.synchronize()
 
-    # ---------------------------------------------------------------- synthetic load on every GPU
-    # torchrun: this rank's GPU; one process: all N GPUs (the node-level exporter watches them all)
-    my_devs = [local_rank] if world > 1 else list(range(n))
-    loads = []
-    if has_gpu and args.load != "idle":
-        from gpumon import hip
-        from gpumon.ops.load import SyntheticLoad
-
-        if hip().device_count() < max(my_devs) + 1:
-            raise SystemExit(f"bench needs GPUs {my_devs}, HIP sees {hip().device_count()}")
-        loads = [SyntheticLoad(dev=d, kind=args.load, hbm_bytes=1 << 30).start() for d in my_devs]
-
-    xgmi_on = n > 1 and not args.no_xgmi
-    ar_buf = None
-    if dist is not None and xgmi_on and args.allreduce_mb > 0:
-        # zeros: repeated in-place sums stay finite (ones would reach inf after ~40 steps on 8 ranks)
-        ar_buf = torch.zeros(args.allreduce_mb * (1 << 20) // 2, dtype=torch.bfloat16, device=device)
-    copiers = []
-    if dist is None and has_gpu and xgmi_on:
-        from gpumon.parallel.xgmi import PeerCopier
-
-        copiers = [PeerCopier(i, (i + 1) % n, nbytes=args.xgmi_mb << 20).start() for i in range(n)]
-
     # ---------------------------------------------------------------- rank 0: exporter + scraper
     mon = None
     core = None
@@ -202,8 +185,52 @@ def main() -> int:
         st = mon.ex.statics()
         if len(st) < n:
             raise SystemExit(f"exporter sees {len(st)} GPU(s), bench needs {n}")
-        mon.wait_ticks(args.warmup, timeout_s=args.warmup * args.interval * 5 + 30)
 
+    # ---------------------------------------------------------------- idle reference (untimed)
+    # the same scrape load against the same exporter before any synthetic load starts: the
+    # BASELINE asks for scrape p99 idle and under load at every GPU count
+    idle = None
+    if rank == 0 and args.idle_s > 0:
+        mon.wait_ticks(1, timeout_s=args.interval * 5 + 30)
+        q0 = mon.ex.seq
+        r = core.scrape_load("127.0.0.1", mon.port, "/metrics", n_requests=0, duration_s=args.idle_s,
+                             concurrency=args.scrape_concurrency, rate_hz=args.scrape_rate, keep_alive=True,
+                             gzip=args.gzip)
+        q1 = mon.ex.seq
+        it = [t["duration_s"] for t in mon.ex.tick_log() if q0 < t["seq"] <= q1]
+        lat = r.get("latencies_s", [])
+        idle = {"seconds": args.idle_s, "scrapes": len(lat), "scrape_errors": r.get("errors", 0),
+                "scrape_p50_ms": round(_pct(lat, 0.50) * 1e3, 4) if lat else None,
+                "scrape_p99_ms": round(_pct(lat, 0.99) * 1e3, 4) if lat else None,
+                "ticks": len(it), "tick_mean_ms": round(sum(it) / len(it) * 1e3, 4) if it else None,
+                "tick_max_ms": round(max(it) * 1e3, 4) if it else None}
+    barrier()
+
+    # ---------------------------------------------------------------- synthetic load on every GPU
+    # torchrun: this rank's GPU; one process: all N GPUs (the node-level exporter watches them all)
+    my_devs = [local_rank] if world > 1 else list(range(n))
+    loads = []
+    if has_gpu and args.load != "idle":
+        from gpumon import hip
+        from gpumon.ops.load import SyntheticLoad
+
+        if hip().device_count() < max(my_devs) + 1:
+            raise SystemExit(f"bench needs GPUs {my_devs}, HIP sees {hip().device_count()}")
+        loads = [SyntheticLoad(dev=d, kind=args.load, hbm_bytes=1 << 30).start() for d in my_devs]
+
+    xgmi_on = n > 1 and not args.no_xgmi
+    ar_buf = None
+    if dist is not None and xgmi_on and args.allreduce_mb > 0:
+        # zeros: repeated in-place sums stay finite (ones would reach inf after ~40 steps on 8 ranks)
+        ar_buf = torch.zeros(args.allreduce_mb * (1 << 20) // 2, dtype=torch.bfloat16, device=device)
+    copiers = []
+    if dist is None and has_gpu and xgmi_on:
+        from gpumon.parallel.xgmi import PeerCopier
+
+        copiers = [PeerCopier(i, (i + 1) % n, nbytes=args.xgmi_mb << 20).start() for i in range(n)]
+
+    if rank == 0:
+        mon.wait_ticks(args.warmup, timeout_s=args.warmup * args.interval * 5 + 30)
     barrier()
     # RCCL channel / buffer setup and the all-reduce calibration stay out of the timed region
     reps = 1
@@ -371,6 +398,7 @@ def main() -> int:
                                + (", peer-copy xGMI ring" if copiers else ""),
                 "interval_s": args.interval,
             },
+            "scrape_idle": idle,  # same scrape load, before any synthetic load (untimed)
             "scrape_p50_ms": round(_pct(lat, 0.50) * 1e3, 4),
             "scrape_p99_ms": round(_pct(lat, 0.99) * 1e3, 4),
             "scrape_max_ms": round(max(lat) * 1e3, 4) if lat else None,

@@ -36,12 +36,15 @@ def _check(d, n, steps, warmup):
 def test_bench_single_process():
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--interval", "0.1"], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+                        "--interval", "0.1", "--idle-s", "1"], capture_output=True, text=True, timeout=240, env=env,
+                       cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
     _check(lines[0], 1, 3, 1)
     assert lines[0]["value"] == pytest.approx(10.0, rel=0.2)  # 1 device x 10 Hz
+    idle = lines[0]["scrape_idle"]  # untimed idle reference before the load
+    assert idle["scrapes"] > 5 and idle["scrape_errors"] == 0 and idle["scrape_p99_ms"] > 0 and idle["ticks"] >= 5
 
 
 @pytest.mark.slow
@@ -52,7 +55,7 @@ def test_bench_two_ranks_gloo():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(29600 + os.getpid() % 300),
                         os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
-                        "--interval", "0.1", "--allreduce-mb", "1"],
+                        "--interval", "0.1", "--allreduce-mb", "1", "--idle-s", "1"],
                        capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
