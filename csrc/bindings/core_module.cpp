@@ -86,6 +86,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "occ_samples", &c.occ_samples);
   get(d, "hide_empty_contexts", &c.hide_empty_contexts);
   get(d, "sample_threads", &c.sample_threads);
+  get(d, "rt_priority", &c.rt_priority);
   get(d, "influx_url", &c.influx_url);
   get(d, "influx_extended", &c.influx_extended);
   get(d, "influx_schema", &c.influx_schema);
@@ -304,6 +305,7 @@ static py::dict tick_to_dict(const TickInfo& t) {
   d["t_gzip"] = t.t_gzip;
   d["t_wake"] = t.t_wake;
   d["t_device"] = t.t_device;
+  d["t_late"] = t.t_late;
   d["link_refreshes"] = t.link_refreshes;
   d["ras_reads"] = t.ras_reads;
   d["ras_full"] = t.ras_full;
@@ -648,6 +650,7 @@ PYBIND11_MODULE(_core, m) {
              d["stale_samples"] = s.stale_samples;
              d["occupancy_reads"] = s.occupancy_reads;
              d["hidden_contexts"] = s.hidden_contexts;
+             d["rt_threads"] = s.rt_threads;
              d["overruns"] = s.overruns;
              d["scrapes"] = s.scrapes;
              d["http_connections"] = s.http_connections;

@@ -1,5 +1,8 @@
 #include "exporter.h"
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <dirent.h>
 #include <unistd.h>
 
@@ -56,10 +59,37 @@ struct Exporter::DevWorker {
 // (4.6 % of reads under a saturating burn land between two kernels and return 0, profiles/
 // r2_kfd_occupancy.md); the tick's process rows carry the interval mean and the share of reads
 // that found the process's waves resident.
+// SCHED_FIFO for the calling thread (rt_priority); counted in `rt` while the thread lives.
+static bool apply_rt(int prio, const std::string& who, std::atomic<int>* rt) {
+  if (prio <= 0) return false;
+  sched_param sp{};
+  sp.sched_priority = std::clamp(prio, 1, 99);
+  const int rc = pthread_setschedparam(pthread_self(), SCHED_FIFO, &sp);
+  if (rc != 0) {
+    static std::atomic<bool> warned{false};
+    if (!warned.exchange(true))
+      GPUMON_LOG(LogLevel::kWarn, "exporter",
+                 "rt_priority " + std::to_string(prio) + " for " + who + ": " + strerror(rc) +
+                     " (needs CAP_SYS_NICE); sampling threads keep normal scheduling");
+    return false;
+  }
+  rt->fetch_add(1);
+  return true;
+}
+
 static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_ptr<Exporter::DoneSignal> sig,
                             Backend* backend, int i, int64_t occ_period_ns,
-                            std::shared_ptr<std::atomic<uint64_t>> occ_reads) {
+                            std::shared_ptr<std::atomic<uint64_t>> occ_reads, int rt_prio,
+                            std::shared_ptr<std::atomic<int>> rt_threads) {
   set_thread_name("gpumon-dev" + std::to_string(i));
+  const bool rt = apply_rt(rt_prio, "device worker", rt_threads.get());
+  struct RtCount {  // the gauge counts live threads
+    bool on;
+    std::atomic<int>* n;
+    ~RtCount() {
+      if (on) n->fetch_sub(1);
+    }
+  } rt_count{rt, rt_threads.get()};
   std::vector<uint32_t> occ_pids;                      // processes on this device at the last tick
   std::vector<double> occ_sum;                         // per occ_pids entry
   std::vector<int> occ_n, occ_busy;
@@ -209,7 +239,8 @@ void Exporter::start_workers(int n) {
     const int64_t occ_ns = cfg_.interval_s > 0 && cfg_.occ_samples > 1 && cfg_.processes
                                ? std::max<int64_t>(20'000'000, static_cast<int64_t>(cfg_.interval_s * 1e9 / cfg_.occ_samples))
                                : 0;
-    w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i, occ_ns, occ_reads_);
+    w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i, occ_ns, occ_reads_, cfg_.rt_priority,
+                        rt_threads_);
     workers_.push_back(std::move(w));
   }
 }
@@ -451,6 +482,7 @@ std::vector<TickInfo> Exporter::tick_log() const {
 }
 
 void Exporter::sampler_loop() {
+  const bool rt = apply_rt(cfg_.rt_priority, "sampler", rt_threads_.get());
   const int64_t period = static_cast<int64_t>(cfg_.interval_s * 1e9);
   int64_t next = mono_ns() + period;
   while (running_) {
@@ -461,7 +493,9 @@ void Exporter::sampler_loop() {
       std::this_thread::sleep_for(std::chrono::nanoseconds(std::min<int64_t>(left, 50000000)));
       continue;
     }
+    tick_deadline_ns_ = next;
     tick();
+    tick_deadline_ns_ = 0;
     next += period;
     int64_t after = mono_ns();
     if (after > next) {
@@ -471,6 +505,7 @@ void Exporter::sampler_loop() {
       next += missed * period;
     }
   }
+  if (rt) rt_threads_->fetch_sub(1);
 }
 
 void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
@@ -709,6 +744,7 @@ TickInfo Exporter::tick() {
   TraceRange trace_tick("gpumon.tick");
   TickInfo info;
   int64_t t0 = mono_ns();
+  if (const int64_t dl = tick_deadline_ns_.load(); dl > 0) info.t_late = std::max<int64_t>(0, t0 - dl) * 1e-9;
   std::vector<DeviceSample> cur;
   std::vector<DeviceRates> rates;
   std::vector<std::vector<ProcSample>> procs;
@@ -1107,6 +1143,7 @@ SelfStats Exporter::self_stats() const {
   s.stale_samples = stale_;
   s.occupancy_reads = occ_reads_->load(std::memory_order_relaxed);
   s.hidden_contexts = hidden_contexts_.load();
+  s.rt_threads = rt_threads_->load();
   s.overruns = overruns_;
   s.last_tick_wall_s = last_tick_wall_ns_.load() * 1e-9;
   s.interval_s = cfg_.interval_s;

@@ -54,6 +54,12 @@ struct ExporterConfig {
   int ras_slices = 1;                 // the pass read in this many slices on consecutive ticks (1..ras_every)
   bool ras_async = true;              // device workers read RAS after publishing a tick (next tick carries it)
   int sample_threads = -1;            // parallel device sampling; 0 = sequential, -1 = auto (one per GPU, max 8)
+  // SCHED_FIFO priority (1-99) for the sampler and device-worker threads, 0 = normal scheduling.
+  // They do bounded work per tick (no request-driven work: the HTTP threads stay normal, so a
+  // scrape flood cannot starve the node), and on a node whose CPUs are saturated by data loaders
+  // it keeps the tick on its deadline. Needs CAP_SYS_NICE (the privileged DaemonSet has it);
+  // without it the threads stay normal and gpumon_sampler_rt_threads says so.
+  int rt_priority = 0;
   int occ_samples = 10;               // KFD cu_occupancy reads per process per tick on the device workers (1 = the tick's own)
   bool hide_empty_contexts = true;    // no pod_gpu row for a process with a GPU context but no VRAM and no waves
   AttributionConfig attribution;
@@ -90,6 +96,7 @@ struct TickInfo {
   // inside t_sample (parallel workers, max over devices): post -> worker picked the request up,
   // and the worker's device calls (metrics table, links, RAS, process list)
   double t_wake = 0, t_device = 0;
+  double t_late = 0;  // how late the tick started after its deadline (scheduled ticks only)
   int link_refreshes = 0;   // devices whose link metrics were re-read this tick
   int ras_reads = 0;        // devices that read a RAS slice this tick
   bool ras_full = false;    // the RAS read covered every file (first tick / ras_slices = 1)
@@ -230,6 +237,8 @@ class Exporter {
   std::atomic<uint64_t> hidden_contexts_{0};  // empty GPU contexts left out of the last tick's rows
   // cu_occupancy sub-sample reads by the workers (shared: a detached worker may outlive a restart)
   std::shared_ptr<std::atomic<uint64_t>> occ_reads_ = std::make_shared<std::atomic<uint64_t>>(0);
+  std::shared_ptr<std::atomic<int>> rt_threads_ = std::make_shared<std::atomic<int>>(0);  // SCHED_FIFO now
+  std::atomic<int64_t> tick_deadline_ns_{0};  // deadline of the tick the sampler loop is running
   std::shared_ptr<DoneSignal> done_sig_;
   uint64_t tick_id_ = 0;
   std::vector<uint64_t> dev_timeouts_;  // guarded by state_mu_

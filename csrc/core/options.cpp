@@ -226,6 +226,7 @@ const std::map<std::string, Setter>& setters() {
       {"occ_samples", int_at([](NativeOptions* o) { return &o->cfg.occ_samples; })},
       {"hide_empty_contexts", bool_at([](NativeOptions* o) { return &o->cfg.hide_empty_contexts; })},
       {"sample_threads", int_at([](NativeOptions* o) { return &o->cfg.sample_threads; })},
+      {"rt_priority", int_at([](NativeOptions* o) { return &o->cfg.rt_priority; })},
       {"device_timeout_s", dbl_at([](NativeOptions* o) { return &o->cfg.device_timeout_s; })},
       {"reinit_after", int_at([](NativeOptions* o) { return &o->cfg.reinit_after; })},
       {"init_retry_s", dbl_at([](NativeOptions* o) { return &o->cfg.init_retry_s; })},
@@ -493,6 +494,7 @@ std::string options_json(const NativeOptions& o) {
   N("occ_samples", c.occ_samples);
   B("hide_empty_contexts", c.hide_empty_contexts);
   N("sample_threads", c.sample_threads);
+  N("rt_priority", c.rt_priority);
   N("device_timeout_s", c.device_timeout_s);
   N("reinit_after", c.reinit_after);
   N("init_retry_s", c.init_retry_s);

@@ -667,6 +667,11 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       f.add(hl, static_cast<double>(s.hidden_contexts));
     }
     {
+      Family f(o, "gpumon_sampler_rt_threads",
+               "Sampler and device-worker threads running SCHED_FIFO (rt_priority > 0 and CAP_SYS_NICE).", "gauge");
+      f.add(hl, static_cast<double>(s.rt_threads));
+    }
+    {
       Family f(o, "gpumon_occupancy_reads_total",
                "KFD cu_occupancy reads made between ticks by the device workers (occ_samples per tick).",
                "counter");

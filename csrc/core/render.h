@@ -59,6 +59,7 @@ struct SelfStats {
   uint64_t stale_samples = 0;
   uint64_t occupancy_reads = 0;     // KFD cu_occupancy sub-sample reads by the device workers
   uint64_t hidden_contexts = 0;     // GPU contexts without VRAM or waves left out of pod_gpu rows
+  int rt_threads = 0;               // sampler / device-worker threads running SCHED_FIFO (rt_priority)
   uint64_t overruns = 0;
   double last_tick_wall_s = 0;
   double interval_s = 1.0;

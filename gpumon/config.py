@@ -44,6 +44,7 @@ class Config:
     hide_empty_contexts: bool = True      # no pod_gpu row for a GPU context with no VRAM and no waves
     occ_samples: int = 10                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
+    rt_priority: int = 0                  # SCHED_FIFO priority of the sampler + device workers (needs CAP_SYS_NICE)
     device_timeout_s: float = 2.0         # a device call still running after this is exported as hung
     reinit_after: int = 5                 # ticks with every GPU failing before the backend is re-initialised
     init_retry_s: float = 5.0             # backoff between backend init attempts
@@ -134,6 +135,7 @@ class Config:
             "occ_samples": int(self.occ_samples),
             "hide_empty_contexts": bool(self.hide_empty_contexts),
             "sample_threads": int(self.sample_threads),
+            "rt_priority": int(self.rt_priority),
             "device_timeout_s": float(self.device_timeout_s),
             "reinit_after": int(self.reinit_after),
             "init_retry_s": float(self.init_retry_s),

@@ -282,3 +282,35 @@ def test_tick_log_records_phases_and_link_refreshes(mock_exporter):
     assert [t["link_refreshes"] for t in log[1:]] == [1, 2, 1, 2]  # staggered over link_every
     for t in log:
         assert t["duration_s"] >= t["t_sample"] + t["t_attrib"] + t["t_render"] > 0
+
+
+def test_rt_priority_for_sampler_and_device_workers(core):
+    """rt_priority: the sampler and the device workers run SCHED_FIFO when the process may (root /
+    CAP_SYS_NICE: gpumon_sampler_rt_threads = workers + 1), and keep normal scheduling otherwise;
+    the HTTP threads never do. Ticks flow either way."""
+    import os
+    import time
+
+    ex = core.Exporter({"backend": "mock:gpus=2", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0.05,
+                        "rt_priority": 1, "http_threads": 1})
+    assert ex.start() == ""
+    try:
+        time.sleep(0.4)
+        n = ex.self_stats()["rt_threads"]
+        assert n in (0, 3)
+        pols = {}
+        for t in os.listdir("/proc/self/task"):
+            try:
+                s = open(f"/proc/self/task/{t}/stat").read()
+            except OSError:
+                continue
+            name = s[s.index("(") + 1:s.rindex(")")]
+            pols.setdefault(name, set()).add(int(s.rsplit(")", 1)[1].split()[38]))  # field 41: policy
+        if n == 3:
+            assert pols["gpumon-dev0"] == {1} and pols["gpumon-dev1"] == {1}  # SCHED_FIFO
+            assert all(p == {0} for k, p in pols.items() if k.startswith("gpumon-http"))
+        assert ex.self_stats()["ticks"] >= 5
+        assert "gpumon_sampler_rt_threads" in ex.metrics_text()
+    finally:
+        ex.stop()
+    assert ex.self_stats()["rt_threads"] == 0
