@@ -135,6 +135,8 @@ def main() -> int:
     ap.add_argument("--idle-s", type=float, default=5.0,
                     help="untimed idle reference before the load starts: scrape p50/p99 + tick cost (0 = off)")
     ap.add_argument("--no-fast-path", action="store_true", help="read every value through libamd_smi")
+    ap.add_argument("--rt-priority", type=int, default=1,
+                    help="the DaemonSet's rt_priority (SCHED_FIFO sampler; stays normal without CAP_SYS_NICE)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -178,7 +180,7 @@ def main() -> int:
         cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi")) else [],
                      interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
                      enable_probe=args.probe and has_gpu, log_level="warn", fast_path=not args.no_fast_path,
-                     sample_threads=args.sample_threads)
+                     sample_threads=args.sample_threads, rt_priority=args.rt_priority)
         mon = GpuMonitor(cfg, control_plane=False).start()
         if mon.start_error:
             raise SystemExit(f"exporter backend failed: {mon.start_error}")
@@ -423,6 +425,7 @@ def main() -> int:
             "tick_quantiles": "exact over the timed ticks (exporter tick log); times in ms",
             "server_scrape_p99_ms_last4096": round(mon.ex.scrape_quantile(0.99) * 1e3, 4),
             "overruns": s1["overruns"] - s0["overruns"],
+            "sampler_rt_threads": s1.get("rt_threads", 0),
             "backend_call_us": {k: round((v["seconds"] - s0["backend_calls"].get(k, {}).get("seconds", 0.0)) * 1e6
                                          / max(1, v["n"] - s0["backend_calls"].get(k, {}).get("n", 0)), 1)
                                 for k, v in s1.get("backend_calls", {}).items()},
