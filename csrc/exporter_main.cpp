@@ -37,7 +37,7 @@ static void usage() {
           "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--pod-labels KEY,KEY..]\n"
-          "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--ras-slices N] [--no-gzip] [--sample-threads N]\n"
+          "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--ras-slices N] [--no-gzip] [--sample-threads N] [--rt-priority N]\n"
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx]\n"
           "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri]\n"
           "                       [--dra-drivers gpu.amd.com,..|none]\n"
@@ -117,6 +117,7 @@ int main(int argc, char** argv) {
     else if (a == "--ras-slices") set("ras_slices", next());
     else if (a == "--no-gzip") set("gzip", "false");
     else if (a == "--sample-threads") set("sample_threads", next());
+    else if (a == "--rt-priority") set("rt_priority", next());
     else if (a == "--http-threads") set("http_threads", next());
     else if (a == "--log-level") set("log_level", next());
     else if (a == "--pmc") set("enable_pmc", "true");

@@ -254,6 +254,7 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--no-processes", dest="processes", action="store_false", default=None)
     p.add_argument("--no-gzip", dest="gzip", action="store_false", default=None)
     p.add_argument("--sample-threads", dest="sample_threads", type=int)
+    p.add_argument("--rt-priority", dest="rt_priority", type=int)
     p.add_argument("--device-timeout", dest="device_timeout_s", type=float,
                    help="seconds before a device call is exported as hung (gpu_up 0)")
     p.add_argument("--enable-probe-kernel", dest="enable_probe", action="store_true", default=None)

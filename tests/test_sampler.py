@@ -309,6 +309,9 @@ def test_rt_priority_for_sampler_and_device_workers(core):
         if n == 3:
             assert pols["gpumon-dev0"] == {1} and pols["gpumon-dev1"] == {1}  # SCHED_FIFO
             assert all(p == {0} for k, p in pols.items() if k.startswith("gpumon-http"))
+        deadline = time.time() + 5
+        while ex.self_stats()["ticks"] < 5 and time.time() < deadline:
+            time.sleep(0.05)
         assert ex.self_stats()["ticks"] >= 5
         assert "gpumon_sampler_rt_threads" in ex.metrics_text()
     finally:
