@@ -74,7 +74,7 @@ def cmd_once(args) -> int:
 
 
 def _fmt(v, w, p=0):
-    if v is None:
+    if v is None or v != v:  # None or NaN (not measured)
         return "-".rjust(w)
     return f"{v:{w}.{p}f}"
 
@@ -92,11 +92,14 @@ def render_top(statics, samples, rates, rows) -> str:
         lines.append(f"{st['gpu_id']:>3} {_fmt(f['gfx_util'], 6)} {xcd:<32} {used:8.0f}/{tot:8.0f} "
                      f"{_fmt(f['power_cur'], 6)} {_fmt(f['temp_hotspot'], 6)} {_fmt(f['gfxclk_cur'], 8)}")
     lines.append("")
-    lines.append(f"{'CONTAINER':<13}{'POD':<32}{'NAMESPACE':<14}{'USER':<10}{'PID':>8} {'GPU':>3} {'MEM MiB':>9} {'UTIL%':>6}  PROCESS")
+    # BUSY%: share of the interval with the process's waves resident (KFD; the reference copied the
+    # device's utilisation onto every process, gpu.py:205); CUs: mean CU-equivalents its waves held
+    lines.append(f"{'CONTAINER':<13}{'POD':<32}{'NAMESPACE':<14}{'USER':<10}{'PID':>8} {'GPU':>3} {'MEM MiB':>9} "
+                 f"{'BUSY%':>6} {'CUs':>6}  PROCESS")
     for r in rows:
         lines.append(f"{r['containerid'][:12]:<13}{r['podname'][:31]:<32}{r['namespace'][:13]:<14}{r['user_name'][:9]:<10}"
                      f"{r['pid']:>8} {r['dev']:>3} {r['used_memory_bytes'] / 1048576:9.0f} "
-                     f"{_fmt(r['proc_gfx_util'], 6, 1)}  {r['procname'][:30]}")
+                     f"{_fmt(r['proc_gfx_util'], 6, 1)} {_fmt(r.get('cu_occupancy'), 6, 1)}  {r['procname'][:30]}")
     return "\n".join(lines)
 
 
