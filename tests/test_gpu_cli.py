@@ -144,6 +144,10 @@ def test_native_exporter_reports_a_separate_tenant_process():
     s.close()
     load = subprocess.Popen([sys.executable, "-m", "gpumon", "load", "--kind", "mfma", "--seconds", "14"],
                             cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    # a second tenant that holds 3 GiB of VRAM and runs nothing
+    idle = subprocess.Popen([sys.executable, "-c", "import time, torch; x = torch.ones(3 << 28, device='cuda:0'); "
+                             "torch.cuda.synchronize(); time.sleep(16)"], cwd=ROOT, stdout=subprocess.DEVNULL,
+                            stderr=subprocess.PIPE, text=True)
     exe = os.path.join(ROOT, "bin", "gpumon-exporter")
     ex = subprocess.Popen([exe, "--backend", "amdsmi", "--interval", "0.5", "--listen", f"127.0.0.1:{port}",
                            "--log-level", "warn", "--no-pod-resources", "--no-cri"],
@@ -157,13 +161,19 @@ def test_native_exporter_reports_a_separate_tenant_process():
     finally:
         ex.terminate()
         ex.wait(20)
-        try:
-            load.wait(60)
-        except subprocess.TimeoutExpired:
-            load.kill()
-            load.wait(30)
+        for p in (load, idle):
+            try:
+                p.wait(60)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait(30)
     occ = {l["pid"]: v for _, l, v in fam["pod_gpu_proc_cu_occupancy_percent"]["samples"]}
     busy = {l["pid"]: v for _, l, v in fam["pod_gpu_proc_gfx_util"]["samples"]}
+    mem = {l["pid"]: v for _, l, v in fam["pod_gpu_used_memory"]["samples"]}  # MiB
+    # the idle tenant: its row is exported (it holds VRAM) with ~0 waves and ~0 busy
+    quiet = [p for p, v in mem.items() if v >= 3000 and occ.get(p, 1e9) < 2]
+    assert len(quiet) == 1, (mem, occ, busy)
+    assert busy[quiet[0]] < 5, (mem, occ, busy)
     # the burn process holds every wave slot except in the gaps between its host-synchronised
     # batches (~5 % of the time); 10 reads per tick estimate that share
     hot = [p for p, v in occ.items() if v > 60]
