@@ -272,6 +272,7 @@ py::dict row_to_dict(const PodRow& r) {
   d["proc_gfx_util"] = num(r.proc_gfx_util);
   d["cu_occupancy"] = num(r.cu_occupancy);
   d["occ_samples"] = r.occ_samples;
+  d["mfma_util"] = num(r.mfma_util);
   return d;
 }
 
@@ -784,7 +785,9 @@ PYBIND11_MODULE(_core, m) {
       .def("mock_link_calls", [](Exporter& e, int dev) { return mock_of(e)->link_calls(dev); })
       .def("mock_set_occ_series",
            [](Exporter& e, int dev, const std::vector<double>& v) { mock_of(e)->set_occ_series(dev, v); })
-      .def("mock_occ_reads", [](Exporter& e, int dev) { return mock_of(e)->occ_reads(dev); });
+      .def("mock_occ_reads", [](Exporter& e, int dev) { return mock_of(e)->occ_reads(dev); })
+      .def("set_device_mfma_util", &Exporter::set_device_mfma_util,
+           "per-device wall-time MFMA utilisation (what the PMC sampler publishes)");
 
   // Native on-device samplers (csrc/core/ondevice.h): the same PMC / probe plugins the standalone
   // binary dlopen()s, driven from C++ threads instead of the Python runners in gpumon/ops.

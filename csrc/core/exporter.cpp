@@ -633,9 +633,29 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
   *procs_s = proc_ns * 1e-9;
 }
 
+void Exporter::set_device_mfma_util(std::map<int, double> v) {
+  std::lock_guard<std::mutex> g(extra_mu_);
+  mfma_util_ = std::move(v);
+}
+
 void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
                               const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows) {
   rows->clear();
+  // Exclusive use: the one process of a device whose waves were resident this interval (every
+  // process counts, opted in or not). Its row carries the device's MFMA utilisation.
+  std::map<int, double> mfma;
+  {
+    std::lock_guard<std::mutex> g(extra_mu_);
+    mfma = mfma_util_;
+  }
+  std::vector<uint32_t> sole(procs.size(), 0);
+  for (size_t d = 0; d < procs.size(); ++d) {
+    std::vector<uint32_t> active;  // distinct pids (one process may hold several KFD contexts)
+    for (const auto& p : procs[d])
+      if ((p.occ_busy > 0 || p.cu_occupancy > 0) && std::find(active.begin(), active.end(), p.pid) == active.end())
+        active.push_back(p.pid);
+    if (active.size() == 1) sole[d] = active[0];
+  }
   uint64_t hidden = 0;
   std::vector<uint32_t> alive;
   std::unordered_map<ProcKey, ProcPrev, ProcKeyHash> next_prev;
@@ -698,6 +718,8 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       r.proc_gfx_util = util;
       r.cu_occupancy = p.cu_occupancy;
       r.occ_samples = p.occ_samples;
+      if (sole[d] == p.pid)
+        if (auto m = mfma.find(static_cast<int>(d)); m != mfma.end()) r.mfma_util = m->second;
       active.emplace_back(r.pod_namespace, r.pod_name, r.container, r.dev);
       row_of_pid[p.pid] = rows->size();
       rows->push_back(std::move(r));

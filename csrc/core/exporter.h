@@ -126,6 +126,9 @@ class Exporter {
   void set_container_meta(std::vector<ContainerMeta> metas) { attr_->set_container_meta(std::move(metas)); }
   void set_allocations(std::vector<Allocation> a) { attr_->set_allocations(std::move(a)); }
   void set_extra(const std::string& source, std::vector<ExtraSeries> series);
+  // Latest wall-time MFMA utilisation per device index from the PMC sampler (empty map: none);
+  // attributed to a pod_gpu row when that process used the GPU alone (pod_gpu_mfma_util_percent).
+  void set_device_mfma_util(std::map<int, double> v);
   Attributor& attributor() { return *attr_; }
 
   // Introspection.
@@ -234,6 +237,7 @@ class Exporter {
   bool workers_busy() const;
   std::vector<std::shared_ptr<DevWorker>> workers_;
   bool seq_maintain_ = false;  // sequential tick: run Backend::maintain after the publish
+  std::map<int, double> mfma_util_;  // set_device_mfma_util (guarded by extra_mu_)
   std::atomic<uint64_t> hidden_contexts_{0};  // empty GPU contexts left out of the last tick's rows
   // cu_occupancy sub-sample reads by the workers (shared: a detached worker may outlive a restart)
   std::shared_ptr<std::atomic<uint64_t>> occ_reads_ = std::make_shared<std::atomic<uint64_t>>(0);

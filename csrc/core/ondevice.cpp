@@ -609,7 +609,10 @@ void OnDevice::stop() {
     helper_shutdown();  // after the probes' rings are drained and freed
     ex_->set_extra("ondevice_helper", {});
   }
-  if (pmc_lib_) ex_->set_extra("pmc", {});
+  if (pmc_lib_) {
+    ex_->set_extra("pmc", {});
+    ex_->set_device_mfma_util({});
+  }
 }
 
 bool OnDevice::step() {
@@ -858,6 +861,10 @@ void OnDevice::pmc_step_continuous(const std::vector<int>& devs, const std::vect
 
 void OnDevice::export_pmc() {
   std::vector<ExtraSeries> out;
+  std::map<int, double> mfma;  // for pod_gpu_mfma_util_percent (exclusive use)
+  for (const auto& kv : pmc_last_)
+    if (!std::isnan(kv.second.mfma_util)) mfma[kv.first] = kv.second.mfma_util;
+  ex_->set_device_mfma_util(std::move(mfma));
   for (const auto& kv : pmc_last_) {
     const int dev = kv.first;
     const PmcDerived& d = kv.second;

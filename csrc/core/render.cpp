@@ -517,6 +517,15 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       for (size_t r = 0; r < rows.size(); ++r) fu.add(rl[r], rows[r].gpu_util);
     }
     {
+      Family f(o, "pod_gpu_mfma_util_percent",
+               "Wall-time MFMA (matrix core) utilisation of the GPU while this process was the only one with "
+               "waves resident in the interval (exclusive use): the device's gpu_mfma_util_percent. Absent when "
+               "the GPU was shared or PMC counting is off.",
+               "gauge");
+      for (size_t r = 0; r < rows.size(); ++r)
+        if (has(rows[r].mfma_util)) f.add(rl[r], rows[r].mfma_util);
+    }
+    {
       Family f(o, "pod_gpu_used_memory_bytes", "GPU memory (VRAM) used by the process in bytes.",
                "gauge");
       for (size_t r = 0; r < rows.size(); ++r) f.add(rl[r], rows[r].used_memory_bytes);

@@ -10,13 +10,17 @@ if ROOT not in sys.path:
 
 
 def make_locked(*targets, jobs=1, timeout=900):
-    """`make <targets>` serialised across pytest-xdist workers (a worker must never dlopen a fake
-    library another worker is relinking, and two workers must not write the same object)."""
+    """`make <targets>` serialised across pytest-xdist workers per target (a worker must never dlopen
+    a fake library another worker is relinking, and two workers must not write the same object).
+    One lock per target, taken in sorted order: a long sanitizer build does not hold up the fakes."""
+    import contextlib
     import fcntl
 
     os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
-    with open(os.path.join(ROOT, "build", ".make.lock"), "w") as lk:
-        fcntl.flock(lk, fcntl.LOCK_EX)
+    with contextlib.ExitStack() as stack:
+        for t in sorted(set(targets)):
+            lk = stack.enter_context(open(os.path.join(ROOT, "build", f".make-{t}.lock"), "w"))
+            fcntl.flock(lk, fcntl.LOCK_EX)
         r = subprocess.run(["make", "-C", ROOT, f"-j{jobs}", *targets], capture_output=True, text=True,
                            timeout=timeout)
     assert r.returncode == 0, r.stderr[-2000:]

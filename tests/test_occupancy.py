@@ -87,3 +87,28 @@ def test_empty_contexts_are_hidden_but_counted(mock_exporter):
                         hide_empty_contexts=False)
     ex2.tick()
     assert sorted(r["pid"] for r in ex2.pod_rows() if not r["idle"]) == ["21", "22"]
+
+
+def test_mfma_util_attributed_to_the_sole_active_process(mock_exporter):
+    """pod_gpu_mfma_util_percent: the device's MFMA utilisation on the row of the one process whose
+    waves were resident this interval (exclusive use, the usual k8s allocation); a process holding
+    VRAM without waves does not make the GPU shared; two active processes do, and the series is
+    left out rather than guessed."""
+    procs = [{"pid": 7, "device": 0, "name": "train", "kfd_only": True},
+             {"pid": 8, "device": 0, "name": "idle-holder", "kfd_only": True}]
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0, mock={"procs": procs})
+    ex.set_device_mfma_util({0: 42.5})
+    ex.mock_set_occ_series(0, [200.0, 0.0])  # pid 7 has waves, pid 8 none
+    ex.tick()
+    rows = {r["pid"]: r for r in ex.pod_rows() if not r["idle"]}
+    assert rows["7"]["mfma_util"] == 42.5 and rows["8"]["mfma_util"] is None
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "pod_gpu_mfma_util_percent", pid="7") == 42.5
+    assert not promtext.values(fam, "pod_gpu_mfma_util_percent", pid="8")
+    ex.mock_set_occ_series(0, [200.0, 50.0])  # both active: shared GPU
+    ex.tick()
+    assert not promtext.values(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent")
+    ex.set_device_mfma_util({})  # PMC off / withdrawn
+    ex.mock_set_occ_series(0, [200.0, 0.0])
+    ex.tick()
+    assert not promtext.values(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent")

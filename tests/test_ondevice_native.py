@@ -554,3 +554,31 @@ def test_dead_helper_is_respawned_and_samplers_recover(core, mock_exporter, monk
         od.stop()
     time.sleep(0.1)
     assert _helper_pids() == []
+
+
+def test_pmc_mfma_util_lands_on_the_exclusive_process_row(core, mock_exporter, monkeypatch):
+    """The PMC sampler publishes each device's wall-time MFMA utilisation to the exporter; the one
+    process with waves on that GPU gets it as pod_gpu_mfma_util_percent."""
+    import time
+
+    monkeypatch.setenv("GPUMON_FAKE_MFMA", "0.6")
+    ex = mock_exporter(backend="mock:gpus=1,mode=load", sample_threads=0,
+                       mock={"procs": [{"pid": 31, "device": 0, "name": "train", "kfd_only": True}]})
+    ex.mock_set_occ_series(0, [180.0])
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
+    od.start()
+    try:
+        od.step()
+        time.sleep(0.05)
+        od.step()
+        ex.tick()
+        time.sleep(0.05)
+        ex.tick()
+        m = ex.metrics_text()
+        dev = _val(m, "gpu_mfma_util_percent", gpu_id="0")
+        assert dev is not None and dev > 0
+        assert _val(m, "pod_gpu_mfma_util_percent", pid="31") == pytest.approx(dev)
+    finally:
+        od.stop()
+    ex.tick()
+    assert _val(ex.metrics_text(), "pod_gpu_mfma_util_percent", pid="31") is None  # withdrawn with PMC
