@@ -112,11 +112,15 @@ def build():
                         [(f'max by (host, gpu_id, namespace, podname, pid) (pod_gpu_proc_gfx_util{{{HOST}}})',
                           "{{host}} gpu{{gpu_id}} {{namespace}}/{{podname}} pid {{pid}}")], 0, y, 12, 8,
                         fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
+    panels.append(panel("Per-pod MFMA utilisation % (GPUs a pod uses alone; PMC)", "timeseries",
+                        [(f'max by (host, gpu_id, namespace, podname) (pod_gpu_mfma_util_percent{{{HOST}}})',
+                          "{{host}} gpu{{gpu_id}} {{namespace}}/{{podname}}")], 0, y + 8, 12, 8,
+                        fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
     panels.append(panel("On-device samplers: PMC up / counter resets (tenant profilers)", "timeseries",
                         [(f'gpumon_pmc_up{{{HOST}}}', "{{host}} pmc up"),
                          (f'increase(gpumon_pmc_resets_total{{{HOST}}}[5m])', "{{host}} resets / 5m")],
                         12, y, 12, 8))
-    y += 8
+    y += 16
     panels.append(panel("RAS: ECC errors by block (uncorrectable / correctable / deferred)", "table",
                         [(f'sum by (host, gpu_id, block, type) (gpu_ecc_errors_total{{{HOST}}}) > 0', "")], 0, y, 12, 8))
     panels.append(panel("RAS: retired HBM pages and poison / fatal events", "timeseries",
