@@ -80,6 +80,8 @@ def test_dashboard_queries_resolve_against_exposition(mock_exporter):
     ex = mock_exporter(backend="mock:gpus=2")
     ex.set_allocations([{"pod_namespace": "ml", "pod_name": "jupyter-e-0", "container_name": "c", "gpu_index": 0}])
     ex.mock_set_procs([{"pid": os.getpid(), "device": 1, "name": "python3"}])
+    ex.mock_set_occ_series(1, [100.0])
+    ex.set_device_mfma_util({1: 50.0})  # what the PMC sampler publishes (pod_gpu_mfma_util_percent)
     ex.tick()
     fam = promtext.parse(ex.metrics_text())
     produced = set()
