@@ -236,6 +236,37 @@ bool helper_alive() {
   return g_helper.pid > 0;
 }
 
+// The helper's CPU seconds and resident bytes from /proc (it is part of the pod's footprint: the
+// exporter's own process_* series do not include it). False when it is not running.
+bool helper_usage(double* cpu_s, double* rss_bytes) {
+  pid_t pid;
+  {
+    std::lock_guard<std::mutex> g(g_helper.mu);
+    pid = g_helper.pid;
+  }
+  if (pid <= 0) return false;
+  char buf[1024];
+  FILE* f = fopen(("/proc/" + std::to_string(pid) + "/stat").c_str(), "r");
+  if (!f) return false;
+  const size_t n = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  const char* p = strrchr(buf, ')');
+  if (!p) return false;
+  // fields after "(comm)": state(3) ... utime(14) stime(15) ... rss(24, pages)
+  unsigned long long v[22] = {0};
+  int k = 0;
+  for (const char* q = p + 2; *q && k < 22; ++k) {
+    while (*q == ' ') ++q;
+    if (k > 0) v[k] = strtoull(q, nullptr, 10);
+    while (*q && *q != ' ') ++q;
+  }
+  const double hz = static_cast<double>(sysconf(_SC_CLK_TCK));
+  *cpu_s = (v[11] + v[12]) / hz;  // utime, stime
+  *rss_bytes = static_cast<double>(v[21]) * static_cast<double>(sysconf(_SC_PAGESIZE));
+  return true;
+}
+
 // One request / response; the helper runs only for the duration of the call.
 int helper_call(uint32_t op, const int* agents, int n_agents, const char* const* counters, int n_counters,
                 double window_s, std::vector<char>* payload, int32_t* started, std::string* err) {
@@ -678,10 +709,20 @@ bool OnDevice::helper_check() {
 }
 
 void OnDevice::export_helper() {
-  ex_->set_extra("ondevice_helper",
-                 {xs("gpumon_ondevice_helper_restarts_total",
-                     "Times the on-device helper process (PMC contexts + K1 probe) was found dead and respawned.",
-                     -1, static_cast<double>(helper_restarts_.load()), "counter")});
+  std::vector<ExtraSeries> out = {
+      xs("gpumon_ondevice_helper_restarts_total",
+         "Times the on-device helper process (PMC contexts + K1 probe) was found dead and respawned.", -1,
+         static_cast<double>(helper_restarts_.load()), "counter")};
+  double cpu = 0, rss = 0;
+  if (helper_usage(&cpu, &rss)) {
+    out.push_back(xs("gpumon_ondevice_helper_cpu_seconds_total",
+                     "CPU time of the on-device helper process (part of the pod's footprint; process_* "
+                     "series cover the exporter process only).",
+                     -1, cpu, "counter"));
+    out.push_back(xs("gpumon_ondevice_helper_resident_memory_bytes",
+                     "Resident memory of the on-device helper process (its GPU runtimes).", -1, rss));
+  }
+  ex_->set_extra("ondevice_helper", std::move(out));
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -702,6 +743,7 @@ void OnDevice::map_pmc_agents() {
 
 void OnDevice::pmc_step() {
   std::lock_guard<std::mutex> g(pmc_mu_);
+  if (helper_) export_helper();
   if (!helper_check()) {  // helper gone, respawn not due yet: no values, series withdrawn
     pmc_errors_++;
     pmc_up_ = false;
@@ -972,6 +1014,7 @@ bool OnDevice::create_probes(std::string* err) {
 
 void OnDevice::probe_step() {
   std::lock_guard<std::mutex> g(probe_mu_);
+  if (helper_ && !pmc_lib_) export_helper();  // the PMC step refreshes it when both run
   if (!helper_check()) {
     for (auto& p : probes_) p.timeouts++, probe_timeouts_++;
     export_probe();

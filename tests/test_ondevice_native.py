@@ -381,6 +381,8 @@ def test_isolated_pmc_runs_in_a_frozen_helper(core, mock_exporter, monkeypatch):
         assert _state(pids[0]) == "T"  # frozen between reads
         ex.tick()
         m = ex.metrics_text()
+        assert _val(m, "gpumon_ondevice_helper_resident_memory_bytes") > 1 << 20  # the pod's footprint
+        assert _val(m, "gpumon_ondevice_helper_cpu_seconds_total") >= 0
         assert _val(m, "gpu_mfma_busy_active_percent", gpu_id="0") == pytest.approx(40.0)
         assert _val(m, "gpu_pmc_coverage_ratio", gpu_id="0") == 1
     finally:
