@@ -118,7 +118,9 @@ def build():
                         fieldConfig={"defaults": {"unit": "percent", "min": 0, "max": 100}, "overrides": []}))
     panels.append(panel("On-device samplers: PMC up / counter resets (tenant profilers)", "timeseries",
                         [(f'gpumon_pmc_up{{{HOST}}}', "{{host}} pmc up"),
-                         (f'increase(gpumon_pmc_resets_total{{{HOST}}}[5m])', "{{host}} resets / 5m")],
+                         (f'increase(gpumon_pmc_resets_total{{{HOST}}}[5m])', "{{host}} resets / 5m"),
+                         (f'increase(gpumon_ondevice_helper_restarts_total{{{HOST}}}[1h])', "{{host}} helper restarts / 1h"),
+                         (f'rate(gpumon_ondevice_helper_cpu_seconds_total{{{HOST}}}[5m])', "{{host}} helper CPU (cores)")],
                         12, y, 12, 8))
     y += 16
     panels.append(panel("RAS: ECC errors by block (uncorrectable / correctable / deferred)", "table",
