@@ -133,6 +133,7 @@ def test_alert_and_recording_rules_resolve(mock_exporter):
     ex.tick()
     fam = promtext.parse(ex.metrics_text())
     produced = {n for f, v in fam.items() for n in [f] + [s[0] for s in v["samples"]]}
+    produced |= _plugin_metric_names()  # the on-device samplers' series (PMC, probe, helper)
     words = {"sum", "by", "count", "rate", "increase", "delta", "avg", "max", "time", "host", "namespace", "podname",
              "gpu_id", "user_name"}
     exprs = [r["expr"] for g in rule["spec"]["groups"] for r in g["rules"]]
