@@ -925,6 +925,17 @@ void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::str
     append_double(p.idle ? 0.0 : p.gpu_util, o);
     o->append(",used_memory=");
     append_double(std::floor(p.used_memory_bytes / kMiB), o);
+    if (extended && !p.idle) {  // per-process fields the reference could not measure (Q4)
+      auto extra = [&](const char* k, double x) {
+        if (!has(x)) return;
+        o->push_back(',');
+        o->append(k).push_back('=');
+        append_double(x, o);
+      };
+      extra("proc_gfx_util", p.proc_gfx_util);
+      extra("cu_occupancy", p.cu_occupancy);
+      extra("mfma_util", p.mfma_util);
+    }
     o->push_back(' ');
     o->append(std::to_string(ts_ns));
     o->push_back('\n');

@@ -132,3 +132,23 @@ def test_no_nan_in_exposition(mock_exporter):
     for f in fam.values():
         for _, _, v in f["samples"]:
             assert not math.isnan(v)
+
+
+def test_influx_extended_pod_gpu_carries_per_process_fields(mock_exporter):
+    """influx_extended: the reference pod_gpu line plus the per-process numbers it could not measure
+    (busy share, CU-equivalents of waves, MFMA utilisation on an exclusive GPU); the plain schema
+    stays byte-for-byte the reference's."""
+    import os
+
+    procs = [{"pid": os.getpid(), "device": 0, "name": "train", "vram_bytes": 2 ** 30, "kfd_only": True}]
+    plain = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0, mock={"procs": procs})
+    ext = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0, influx_extended=True,
+                        mock={"procs": procs})
+    for ex in (plain, ext):
+        ex.mock_set_occ_series(0, [128.0])
+        ex.set_device_mfma_util({0: 61.5})
+        ex.tick()
+    (lp,) = [l for l in plain.influx_text().splitlines() if l.startswith("pod_gpu,")]
+    (le,) = [l for l in ext.influx_text().splitlines() if l.startswith("pod_gpu,")]
+    assert "proc_gfx_util" not in lp and "mfma_util" not in lp
+    assert re.search(r",used_memory=1024,proc_gfx_util=100,cu_occupancy=128,mfma_util=61\.5 \d{19}$", le), le
