@@ -359,8 +359,17 @@ def _helper_pids():
     return out
 
 
-def _state(pid):
-    return open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()[0]
+def _state(pid, want=None, timeout=2.0):
+    """The process state letter; with `want`, polls until it shows (SIGSTOP is delivered
+    asynchronously, a loaded CPU may not have stopped the helper yet when kill() returns)."""
+    import time
+
+    deadline = time.time() + timeout
+    while True:
+        st = open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()[0]
+        if want is None or st == want or time.time() > deadline:
+            return st
+        time.sleep(0.01)
 
 
 def test_isolated_pmc_runs_in_a_frozen_helper(core, mock_exporter, monkeypatch):
@@ -378,7 +387,7 @@ def test_isolated_pmc_runs_in_a_frozen_helper(core, mock_exporter, monkeypatch):
         od.step()
         time.sleep(0.05)
         od.step()
-        assert _state(pids[0]) == "T"  # frozen between reads
+        assert _state(pids[0], "T") == "T"  # frozen between reads
         ex.tick()
         m = ex.metrics_text()
         assert _val(m, "gpumon_ondevice_helper_resident_memory_bytes") > 1 << 20  # the pod's footprint
@@ -455,7 +464,7 @@ def test_isolated_probe_runs_in_the_helper(core, mock_exporter, monkeypatch):
         for g in ("0", "1"):
             assert _val(m, "gpu_probe_latency_seconds", gpu_id=g) is not None
         (pid,) = _helper_pids()
-        assert _state(pid) == "T"
+        assert _state(pid, "T") == "T"
         os.kill(pid, signal.SIGKILL)
         t0 = time.monotonic()
         od.step()
