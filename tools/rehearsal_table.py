@@ -14,8 +14,8 @@ NOTES = [""] * 8 + ["--sample-threads 0 (sequential)", "--no-fast-path (libamd_s
 def main(path="gpurun_out/scaling/results.jsonl"):
     rows = [json.loads(l) for l in open(path) if l.strip().startswith("{")]
     print("| interval | sampled GPUs | note | samples/s | scrape p50 ms | scrape p99 ms | scrape max ms "
-          "| tick mean ms | tick p99 ms (hist) | overruns | gpu_metrics us | process list us | body KB |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+          "| idle scrape p99 ms | tick mean ms | tick p99 ms | overruns | gpu_metrics us | process list us | body KB |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
     for i, d in enumerate(rows):
         notes = [NOTES[i]] if i < len(NOTES) and NOTES[i] else []
         if "mock" in d.get("data", ""):
@@ -23,7 +23,8 @@ def main(path="gpurun_out/scaling/results.jsonl"):
         calls = d.get("backend_call_us", {})
         cfg = d.get("config", {})
         print(f"| {cfg.get('interval_s')} s | {d.get('sampled_devices')} | {', '.join(notes)} | {d['value']} "
-              f"| {d['scrape_p50_ms']} | {d['scrape_p99_ms']} | {d['scrape_max_ms']} | {d['tick_mean_ms']} "
+              f"| {d['scrape_p50_ms']} | {d['scrape_p99_ms']} | {d['scrape_max_ms']} "
+              f"| {(d.get('scrape_idle') or {}).get('scrape_p99_ms', '')} | {d['tick_mean_ms']} "
               f"| {d['tick_p99_ms']} | {d['overruns']} | {calls.get('gpu_metrics', '')} "
               f"| {calls.get('process_list', '')} | {d['scrape_body_kb']} |")
 
