@@ -415,13 +415,13 @@ def main() -> int:
             "tick_max_ms": round(max(tdur) * 1e3, 4) if tdur else None,
             # what the slowest timed tick spent its time on (tick-tail attribution)
             "slowest_tick": {k: (round(v * 1e3, 4) if k.startswith("t_") or k == "duration_s" else v)
-                             for k, v in slow.items() if k in ("seq", "duration_s", "t_sample", "t_wake", "t_device",
+                             for k, v in slow.items() if k in ("seq", "duration_s", "t_late", "t_sample", "t_wake", "t_device",
                                                                "t_procs", "t_attrib", "t_render", "t_gzip",
                                                                "link_refreshes", "ras_reads", "ras_full")} if slow else None,
             # mean phase times over the timed ticks (ms): where a typical tick goes
             "tick_phases_mean_ms": {k: round(sum(t[k] for t in timed) / len(timed) * 1e3, 4)
-                                    for k in ("t_sample", "t_wake", "t_device", "t_procs", "t_attrib", "t_render",
-                                              "t_gzip")} if timed else None,
+                                    for k in ("t_late", "t_sample", "t_wake", "t_device", "t_procs", "t_attrib",
+                                              "t_render", "t_gzip")} if timed else None,
             "tick_quantiles": "exact over the timed ticks (exporter tick log); times in ms",
             "server_scrape_p99_ms_last4096": round(mon.ex.scrape_quantile(0.99) * 1e3, 4),
             "overruns": s1["overruns"] - s0["overruns"],
