@@ -55,14 +55,18 @@ def _ppid(p):
         return -1
 
 
-def _measure(flags, seconds=10.0):
+def _measure(flags, seconds=10.0, python=False):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    ex = subprocess.Popen([os.path.join(ROOT, "bin", "gpumon-exporter"), "--backend", "amdsmi", "--listen",
-                           f"127.0.0.1:{port}", "--log-level", "warn", "--no-pod-resources", "--no-cri", *flags],
-                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    if python:  # the DaemonSet's entrypoint (deploy/Dockerfile): python3 -m gpumon serve
+        cmd = [sys.executable, "-m", "gpumon", "serve", "--backend", "amdsmi", "--listen", f"127.0.0.1:{port}",
+               "--log-level", "warn", "--control-plane", "off", *flags]
+    else:
+        cmd = [os.path.join(ROOT, "bin", "gpumon-exporter"), "--backend", "amdsmi", "--listen", f"127.0.0.1:{port}",
+               "--log-level", "warn", "--no-pod-resources", "--no-cri", *flags]
+    ex = subprocess.Popen(cmd, cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     try:
         time.sleep(8)  # start-up (HSA / rocprofiler init) is not steady state
         assert ex.poll() is None, ex.stderr.read()[-2000:]
@@ -89,16 +93,19 @@ def load():
     p.wait(60)
 
 
-def test_default_exporter_within_daemonset_limits(load):
+@pytest.mark.parametrize("python", [False, True], ids=["native", "serve"])
+def test_default_exporter_within_daemonset_limits(load, python):
     cpu_req, mem_lim = _limits("deploy/k8s/gpumon-daemonset.yaml")
-    mcores, rss = _measure(["--interval", "1"])
+    mcores, rss = _measure(["--interval", "1"], python=python)
     print(f"\ndefault: {mcores:.1f} millicores, {rss:.1f} MiB (request {cpu_req}m, limit {mem_lim} MiB)")
     assert mcores < cpu_req and rss < mem_lim / 4
 
 
-def test_ondevice_exporter_within_overlay_limits(load):
+@pytest.mark.parametrize("python", [False, True], ids=["native", "serve"])
+def test_ondevice_exporter_within_overlay_limits(load, python):
     cpu_req, mem_lim = _limits("deploy/k8s/overlays/ondevice/kustomization.yaml", patched=True)
-    mcores, rss = _measure(["--interval", "1", "--pmc", "--probe"])
+    flags = ["--interval", "1"] + (["--enable-pmc", "--enable-probe-kernel"] if python else ["--pmc", "--probe"])
+    mcores, rss = _measure(flags, python=python)
     print(f"\non-device: {mcores:.1f} millicores, {rss:.1f} MiB (request {cpu_req}m, limit {mem_lim} MiB)")
     assert mcores < cpu_req  # the PMC helper's polling runtime thread is frozen between reads
     assert rss < mem_lim
