@@ -187,7 +187,8 @@ def test_ondevice_overlay_enables_pmc_and_sizes_limits():
     res = yaml.safe_load(res_patch["patch"])[0]["value"]
     mib = int(res["limits"]["memory"].rstrip("Mi"))
     req = int(res["requests"]["memory"].rstrip("Mi"))
-    assert 636 * 1.2 <= req <= mib  # 0.64 GB measured with PMC + probe, all of it in the helper
+    assert 636 * 1.2 <= req <= mib  # 0.64 GB measured with PMC + probe on 1 GPU, all of it in the helper
+    assert mib >= 300 + 8 * 350  # device counting init: +0.35 GB with the GPU visible, assumed per GPU
 
 
 def _json_patch(doc, ops):
@@ -225,4 +226,4 @@ def test_ondevice_overlay_patches_apply_to_the_base_daemonset():
     c = pod["containers"][0]
     assert all(m["name"] in vols for m in c["volumeMounts"])
     assert any(m["mountPath"] == "/tmp" for m in c["volumeMounts"]) and c["securityContext"]["readOnlyRootFilesystem"]
-    assert c["resources"]["limits"]["memory"] == "1024Mi"
+    assert c["resources"]["limits"]["memory"] == "3584Mi"
