@@ -186,9 +186,9 @@ def test_ondevice_overlay_enables_pmc_and_sizes_limits():
     res_patch = next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")
     res = yaml.safe_load(res_patch["patch"])[0]["value"]
     mib = int(res["limits"]["memory"].rstrip("Mi"))
-    req = int(res["requests"]["memory"].rstrip("Mi"))
+    req = int(res["requests"]["memory"][:-2]) * (1024 if res["requests"]["memory"].endswith("Gi") else 1)
     assert 636 * 1.2 <= req <= mib  # 0.64 GB measured with PMC + probe on 1 GPU, all of it in the helper
-    assert mib >= 300 + 8 * 350  # device counting init: +0.35 GB with the GPU visible, assumed per GPU
+    assert req >= 300 + 8 * 360 and mib >= req  # device counting service: +0.36 GB per configured GPU agent
 
 
 def _json_patch(doc, ops):
