@@ -226,4 +226,4 @@ def test_ondevice_overlay_patches_apply_to_the_base_daemonset():
     c = pod["containers"][0]
     assert all(m["name"] in vols for m in c["volumeMounts"])
     assert any(m["mountPath"] == "/tmp" for m in c["volumeMounts"]) and c["securityContext"]["readOnlyRootFilesystem"]
-    assert c["resources"]["limits"]["memory"] == "3584Mi"
+    assert c["resources"]["limits"]["memory"] == "4096Mi"
