@@ -535,6 +535,7 @@ bool OnDevice::start(std::string* err) {
     helper_path_ = dir + "/gpumon-ondevice-helper";
     if (!helper_spawn(helper_path_, err)) return false;
     helper_ = true;
+    helper_spawned_ns_ = mono_ns();
   }
   if (cfg_.pmc) {
     if (cfg_.ondevice_isolate) {
@@ -685,7 +686,13 @@ bool OnDevice::helper_check() {
   if (helper_alive()) return true;
   const int64_t now = mono_ns();
   if (now < next_respawn_ns_) return false;
-  next_respawn_ns_ = now + static_cast<int64_t>(std::max(0.0, cfg_.helper_retry_s) * 1e9);
+  // a helper that keeps dying soon after its start (OOM-killed under a tight memory limit, a
+  // broken driver) is retried with exponential backoff: helper_retry_s x 2^streak, at most 64x;
+  // one that ran for 10 minutes resets the streak
+  if (helper_spawned_ns_ && now - helper_spawned_ns_ > 600'000'000'000ll) respawn_streak_ = 0;
+  const double backoff = std::max(0.0, cfg_.helper_retry_s) * static_cast<double>(1 << std::min(respawn_streak_, 6));
+  next_respawn_ns_ = now + static_cast<int64_t>(backoff * 1e9);
+  respawn_streak_++;
   std::string err;
   if (!helper_spawn(helper_path_, &err)) {
     GPUMON_LOG(LogLevel::kWarn, "ondevice", "on-device helper respawn failed: " + err);
@@ -699,6 +706,7 @@ bool OnDevice::helper_check() {
       return false;
     }
   }
+  helper_spawned_ns_ = mono_ns();
   helper_gen_++;  // probe handles of the dead helper are void; the probe sampler recreates them
   helper_restarts_++;
   GPUMON_LOG(LogLevel::kWarn, "ondevice",

@@ -145,6 +145,8 @@ class OnDevice {
   std::string helper_path_;
   std::mutex recover_mu_;       // helper respawn + PMC re-init (before any probe op on a new helper)
   int64_t next_respawn_ns_ = 0;
+  int64_t helper_spawned_ns_ = 0;  // when the current helper was (re)spawned
+  int respawn_streak_ = 0;          // respawns of helpers that died within 10 minutes (backoff)
   std::atomic<uint64_t> helper_gen_{0}, helper_restarts_{0};
   uint64_t probe_gen_seen_ = 0;  // helper generation the probe handles belong to
   int64_t pmc_last_ok_ns_ = 0;  // last step that produced values (window or continuous)

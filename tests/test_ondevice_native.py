@@ -593,3 +593,32 @@ def test_pmc_mfma_util_lands_on_the_exclusive_process_row(core, mock_exporter, m
         od.stop()
     ex.tick()
     assert _val(ex.metrics_text(), "pod_gpu_mfma_util_percent", pid="31") is None  # withdrawn with PMC
+
+
+def test_helper_that_keeps_dying_backs_off(core, mock_exporter):
+    """A helper killed again right after each respawn (e.g. OOM under a tight limit) is retried
+    after helper_retry_s, then 2x, 4x ... that long, not in a tight loop."""
+    import signal
+    import time
+
+    ex = mock_exporter(backend="mock:gpus=1")
+    od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous", helper_retry_s=0.2)
+    od.start()
+    try:
+        respawn_at = []
+        t0 = time.monotonic()
+        od.step()
+        for _ in range(3):
+            n = od.stats()["helper_restarts"]
+            (pid,) = _helper_pids()
+            os.kill(pid, signal.SIGKILL)
+            while od.stats()["helper_restarts"] == n:
+                assert time.monotonic() - t0 < 10
+                time.sleep(0.02)
+                od.step()
+            respawn_at.append(time.monotonic())
+        gaps = [b - a for a, b in zip(respawn_at, respawn_at[1:])]
+        # respawn 1 is immediate; the next ones wait 0.2 s x 2^streak after the previous attempt
+        assert 0.15 <= gaps[0] < 0.6 and gaps[1] >= 0.35 and gaps[1] > gaps[0], gaps
+    finally:
+        od.stop()
