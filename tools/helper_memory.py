@@ -21,19 +21,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def smaps(pid, top=12):
     agg, cur, tot = {}, None, {"Rss": 0, "Anonymous": 0, "Shared_Clean": 0, "Private_Dirty": 0}
+    blocks = []  # individual anonymous mappings >= 8 MB resident (size, rss) in MB
+    size = 0
     for line in open(f"/proc/{pid}/smaps"):
         parts = line.split()
         if not parts:
             continue
         if "-" in parts[0] and not parts[0].endswith(":"):
             cur = parts[5] if len(parts) >= 6 else "[anon]"
+            lo, hi = (int(x, 16) for x in parts[0].split("-"))
+            size = (hi - lo) >> 20
         elif parts[0].rstrip(":") in tot:
             kb = int(parts[1])
             tot[parts[0].rstrip(":")] += kb
             if parts[0] == "Rss:":
                 agg[cur] = agg.get(cur, 0) + kb
+                if cur == "[anon]" and kb >= 8 << 10:
+                    blocks.append((size, round(kb / 1024, 1)))
     return ({k: round(v / 1024, 1) for k, v in tot.items()},
-            [(k, round(v / 1024, 1)) for k, v in sorted(agg.items(), key=lambda kv: -kv[1])[:top]])
+            [(k, round(v / 1024, 1)) for k, v in sorted(agg.items(), key=lambda kv: -kv[1])[:top]],
+            sorted(blocks, key=lambda b: -b[1]))
 
 
 def main() -> int:
@@ -54,8 +61,8 @@ def main() -> int:
                 open(f"/proc/{p}/stat").read().rsplit(")", 1)[1].split()[1] == str(ex.pid)]
         out = {"flags": flags, "env": a.env}
         for k in kids:
-            tot, top = smaps(k)
-            out[f"helper_{k}"] = {"totals_mb": tot, "top_mappings_mb": top,
+            tot, top, blocks = smaps(k)
+            out[f"helper_{k}"] = {"totals_mb": tot, "top_mappings_mb": top, "anon_blocks_mb": blocks,
                                   "threads": len(os.listdir(f"/proc/{k}/task"))}
         print(json.dumps(out, indent=1))
     finally:
