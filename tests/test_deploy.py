@@ -188,7 +188,7 @@ def test_ondevice_overlay_enables_pmc_and_sizes_limits():
     mib = int(res["limits"]["memory"].rstrip("Mi"))
     req = int(res["requests"]["memory"][:-2]) * (1024 if res["requests"]["memory"].endswith("Gi") else 1)
     assert 636 * 1.2 <= req <= mib  # 0.64 GB measured with PMC + probe on 1 GPU, all of it in the helper
-    assert req >= 300 + 8 * 360 and mib >= req  # device counting service: +0.36 GB per configured GPU agent
+    assert req >= 110 + 8 * 520 and mib >= req  # three 173 MB HSA queue blocks per GPU (profiles/r2_footprint.md)
 
 
 def _json_patch(doc, ops):
@@ -226,4 +226,4 @@ def test_ondevice_overlay_patches_apply_to_the_base_daemonset():
     c = pod["containers"][0]
     assert all(m["name"] in vols for m in c["volumeMounts"])
     assert any(m["mountPath"] == "/tmp" for m in c["volumeMounts"]) and c["securityContext"]["readOnlyRootFilesystem"]
-    assert c["resources"]["limits"]["memory"] == "4096Mi"
+    assert c["resources"]["limits"]["memory"] == "5120Mi"
