@@ -291,6 +291,7 @@ def test_rt_priority_for_sampler_and_device_workers(core):
     import os
     import time
 
+    before = set(os.listdir("/proc/self/task"))  # threads of other exporters in this process stay out
     ex = core.Exporter({"backend": "mock:gpus=2", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0.05,
                         "rt_priority": 1, "http_threads": 1})
     assert ex.start() == ""
@@ -299,7 +300,7 @@ def test_rt_priority_for_sampler_and_device_workers(core):
         n = ex.self_stats()["rt_threads"]
         assert n in (0, 3)
         pols = {}
-        for t in os.listdir("/proc/self/task"):
+        for t in set(os.listdir("/proc/self/task")) - before:
             try:
                 s = open(f"/proc/self/task/{t}/stat").read()
             except OSError:
