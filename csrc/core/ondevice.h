@@ -8,8 +8,18 @@
 // role the reference gives its vendored libltdl.so.7 (/root/reference/Dockerfile:4):
 // keep the agent independent of the host's tool-library ABI.
 //
-// Series and formulas match gpumon/ops/pmc.py and gpumon/ops/probe.py (the Python runners used by
-// `gpumon serve --enable-pmc/--enable-probe`), so dashboards see the same families from either path.
+// Production placement (ondevice_isolate, the default): both plugins run in ONE child process,
+// lib/gpumon-ondevice-helper, driven over a pipe pair (csrc/plugins/ondevice_helper_proto.h) and
+// SIGSTOPped between requests. rocprofiler-sdk's device counting leaves an HSA thread polling a
+// full core in the process that owns it; a frozen process polls nothing, the counters keep
+// counting, and this process never maps HIP, HSA or rocprofiler-sdk. A probe step is one request
+// (launch + wait in one awake period), a dead helper is respawned with backoff (PMC re-initialised
+// before any probe op: rocprofiler must register before HSA comes up), and the helper's CPU and
+// RSS are exported because they are part of the pod's footprint (profiles/r2_footprint.md).
+//
+// Series and formulas match gpumon/ops/pmc.py and gpumon/ops/probe.py (the Python test oracles,
+// `gpumon serve --ondevice python`), so dashboards see the same families from either path. The PMC
+// sampler also publishes each GPU's MFMA utilisation to the exporter for pod_gpu_mfma_util_percent.
 #pragma once
 
 #include <atomic>
