@@ -372,6 +372,10 @@ def main() -> int:
             if tx and xgmi.get("expected_tx_GBps_per_gpu"):
                 xgmi["exporter_vs_expected"] = round(xgmi["exporter_tx_GBps_per_gpu"]
                                                      / xgmi["expected_tx_GBps_per_gpu"], 3)
+            if rx and xgmi.get("expected_tx_GBps_per_gpu"):  # a ring moves as much in as out
+                # RCCL may push (writes: tx) or pull (reads: rx); the receive side is reported too
+                xgmi["exporter_rx_vs_expected"] = round(xgmi["exporter_rx_GBps_per_gpu"]
+                                                        / xgmi["expected_tx_GBps_per_gpu"], 3)
             xgmi["per_gpu"] = per_gpu
         result = {
             "metric": BASELINE_METRIC,
