@@ -221,11 +221,10 @@ def cmd_xgmi(args) -> int:
     """Peer-copy each (src, dst) pair and check that the exporter sees the traffic on the link it
     attributes to dst (validation load for the per-link xGMI fields)."""
     from ._native import core as _core
+    from ._native import hip
     from .parallel.xgmi import validate_pair
 
-    import torch
-
-    n = torch.cuda.device_count()
+    n = hip().device_count()  # the peer copies run on the native HIP path (no torch needed)
     if n < 2:
         print(json.dumps({"skipped": f"needs >= 2 GPUs, found {n}"}))
         return 0
