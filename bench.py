@@ -145,9 +145,19 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     n = max(1, args.gpus if world == 1 else world)
 
-    import torch
+    try:
+        import torch
+    except ImportError:  # a lean image (the exporter's + tools): one process, the native HIP path only
+        torch = None
+        if world > 1:
+            raise SystemExit("bench.py under torchrun needs PyTorch (torch.distributed over RCCL)")
 
-    has_gpu = torch.cuda.is_available()
+    if torch is not None:
+        has_gpu = torch.cuda.is_available()
+    else:
+        from gpumon import hip as _hip_rt
+
+        has_gpu = _hip_rt().device_count() > 0
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -155,12 +165,12 @@ def main() -> int:
         if has_gpu:
             torch.cuda.set_device(local_rank)
         dist.init_process_group(backend="nccl" if has_gpu else "gloo")
-    device = torch.device(f"cuda:{local_rank}") if has_gpu else torch.device("cpu")
+    device = (torch.device(f"cuda:{local_rank}") if has_gpu else torch.device("cpu")) if torch is not None else None
 
     def barrier():
         if dist is not None:
             dist.barrier()
-        if has_gpu:
+        if has_gpu and torch is not None:
             torch.cuda.synchronize()
 
     # ---------------------------------------------------------------- rank 0: exporter + scraper
@@ -312,15 +322,16 @@ def main() -> int:
 
     # ---------------------------------------------------------------- per-GPU load rates (every rank)
     # event-timed TFLOP/s / TB/s over the timed region, gathered to rank 0 as one row per GPU
-    lrates = torch.zeros(n, 3, dtype=torch.float64, device=device)
+    lrates = [[0.0, 0.0, 0.0] for _ in range(n)]
     for d, a, b in zip(my_devs, l0, l1):
         dm, dh = b["mfma_s"] - a["mfma_s"], b["hbm_s"] - a["hbm_s"]
-        lrates[d, 0] = (b["flops"] - a["flops"]) / dm / 1e12 if dm > 0 else 0.0
-        lrates[d, 1] = (b["bytes"] - a["bytes"]) / dh / 1e12 if dh > 0 else 0.0
-        lrates[d, 2] = (b["busy_s"] - a["busy_s"]) / max(1e-9, b["wall_s"] - a["wall_s"])
+        lrates[d][0] = (b["flops"] - a["flops"]) / dm / 1e12 if dm > 0 else 0.0
+        lrates[d][1] = (b["bytes"] - a["bytes"]) / dh / 1e12 if dh > 0 else 0.0
+        lrates[d][2] = (b["busy_s"] - a["busy_s"]) / max(1e-9, b["wall_s"] - a["wall_s"])
     if dist is not None:
-        dist.all_reduce(lrates)
-    lrates = lrates.cpu().tolist()
+        t = torch.tensor(lrates, dtype=torch.float64, device=device)
+        dist.all_reduce(t)
+        lrates = t.cpu().tolist()
 
     # ---------------------------------------------------------------- xGMI expectation
     xgmi = None

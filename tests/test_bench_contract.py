@@ -67,3 +67,15 @@ def test_bench_two_ranks_gloo():
     # 2 ranks: a ring all-reduce moves (2(n-1)/n) * S = 1 MiB out of each rank per step
     assert x["expected_tx_GBps_per_gpu"] > 0
     assert "exporter_tx_GBps_per_gpu" in x and "exporter_vs_expected" in x
+
+
+def test_bench_runs_without_torch():
+    """A lean image (the exporter's plus the tools) has no PyTorch: the single-process bench still
+    runs, on the native HIP path for the GPU check and loads."""
+    code = ("import sys, runpy; sys.modules['torch'] = None; sys.argv = ['bench.py', '--steps', '2', '--warmup', '1', "
+            "'--interval', '0.1', '--idle-s', '0.5']; runpy.run_path('bench.py', run_name='__main__')")
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (line,) = _json_lines(r.stdout)
+    _check(line, 1, 2, 1)
