@@ -8,6 +8,7 @@
     gpumon probe   [--blocks 1024]                                                   run the K1 probe once
     gpumon load    [--kind mixed --seconds 10]                                       synthetic gfx950 load
     gpumon xgmi    [--pairs 0:1,1:0 | --all-pairs] [--seconds 2]                     xGMI link-map validation
+    gpumon doctor  [serve flags] [--ondevice-check] [--format text|json]              node prerequisites check
 
 Reference: the agent had no CLI, only ``python3 /gpu.py`` with env vars (Dockerfile:7,
 gpu.py:17-26); its display-table formatter (gpu.py:155-168) was dead code — ``gpumon top`` is
@@ -71,6 +72,16 @@ def cmd_once(args) -> int:
         else:
             sys.stdout.write(mon.metrics())
     return 0
+
+
+def cmd_doctor(args) -> int:
+    from . import doctor
+
+    cfg = from_args(args)
+    if not args.log_level:
+        cfg.log_level = "error"  # the report is the output
+    _setup_logging(cfg.log_level)
+    return doctor.main(args, cfg)
 
 
 def _fmt(v, w, p=0):
@@ -292,6 +303,12 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "fp8", "f32", "f64", "i8", "mxfp8", "mxfp4"],
                    help="matrix path of the mfma burn")
     s.set_defaults(fn=cmd_load)
+    s = sub.add_parser("doctor", help="check what this node gives the exporter (backend, sysfs, KFD, hostPID, "
+                                      "kubelet / CRI sockets, RAS, rt_priority, on-device plugins)")
+    add_cli_args(s)
+    s.add_argument("--ondevice-check", action="store_true", help="also run the PMC and probe samplers once")
+    s.add_argument("--format", choices=["text", "json"], default="text")
+    s.set_defaults(fn=cmd_doctor)
     s = sub.add_parser("xgmi", help="validate the per-link xGMI counters with peer copies")
     s.add_argument("--pairs", default="0:1")
     s.add_argument("--all-pairs", action="store_true")

@@ -1,0 +1,166 @@
+"""``gpumon doctor``: does this node give the exporter what it needs? (operations runbook)
+
+The reference's only self-check was ``commandexists('docker') and commandexists('nvidia-smi')``
+at start-up (/root/reference/gpu.py:28-33,260), printing "Command(s) not found" and exiting.
+This runs the exporter's own code paths once and reports, per requirement of
+docs/operations.md ("What the DaemonSet needs on an MI355X node"), whether it is met and what is
+lost when it is not:
+
+    gpumon doctor [serve flags] [--ondevice-check] [--format text|json]
+
+Exit status 1 when a required check fails (no device backend), 0 otherwise; warnings name the
+series that will be missing.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import re
+import sys
+import time
+
+OK, WARN, FAIL, SKIP = "ok", "warn", "fail", "skip"
+
+
+def _gauge(text: str, name: str):
+    m = re.search(rf"^{name}(?:{{[^}}]*}})? (\S+)$", text, re.M)
+    return float(m.group(1)) if m else None
+
+
+def _rt_permitted() -> tuple:
+    """Whether this process may run SCHED_FIFO threads (rt_priority); restores the policy."""
+    if not hasattr(os, "sched_setscheduler"):
+        return SKIP, "no sched_setscheduler on this platform"
+    old = os.sched_getscheduler(0), os.sched_getparam(0)
+    try:
+        os.sched_setscheduler(0, os.SCHED_FIFO, os.sched_param(1))
+    except PermissionError:
+        return WARN, "SCHED_FIFO not permitted (no CAP_SYS_NICE): rt_priority falls back to normal scheduling"
+    except OSError as e:
+        return WARN, f"SCHED_FIFO: {e}"
+    finally:
+        try:
+            os.sched_setscheduler(0, old[0], old[1])
+        except OSError:
+            pass
+    return OK, "SCHED_FIFO permitted: rt_priority keeps ticks on their deadline"
+
+
+def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
+    """[(check, status, detail)] for the node this runs on, with the exporter configured as `cfg`."""
+    from .monitor import GpuMonitor
+
+    out = []
+    cfg.interval = 0
+    cfg.listen = "127.0.0.1:0"
+    cfg.enable_pmc = cfg.enable_probe = False  # the on-device check below runs them explicitly
+    mon = GpuMonitor(cfg).start()
+    try:
+        st = mon.ex.self_stats()
+        if mon.start_error or not st.get("backend_up"):
+            out.append(("device backend", FAIL, mon.start_error or "backend down"))
+            return out
+        statics = mon.ex.statics()
+        archs = sorted({s.get("gfx_target", "?") for s in statics})
+        out.append(("device backend", OK, f"{st.get('backend')} {st.get('backend_version', '')}".strip()
+                     + f": {len(statics)} GPU(s), {', '.join(archs)}"))
+        if any(a != "gfx950" for a in archs):
+            out.append(("gfx950", WARN, f"targets {archs}: the probe / load kernels are built for gfx950 only"))
+        fp = st.get("fast_path_devices", 0)
+        if fp < 0:
+            out.append(("sysfs fast path", SKIP, f"not applicable to the {st.get('backend')} backend"))
+        else:
+            out.append(("sysfs fast path", OK if fp == len(statics) else WARN,
+                        f"{fp}/{len(statics)} GPU(s) ({st.get('fast_path_status', '')})"
+                        + ("" if fp == len(statics) else ": the rest goes through libamd_smi (about 2x the tick time)")))
+        kfd = "/sys/class/kfd/kfd/proc"
+        out.append(("KFD process table", OK if os.access(kfd, os.R_OK) else WARN,
+                    f"{kfd} readable" if os.access(kfd, os.R_OK)
+                    else f"{kfd} not readable: no per-process rows (pod_gpu_*), no occupancy / busy %"))
+        try:
+            init = open("/proc/1/comm").read().strip()
+        except OSError:
+            init = "?"
+        host_pid = init in ("systemd", "init")
+        out.append(("host PID namespace", OK if host_pid else WARN,
+                    f"PID 1 is {init}" + ("" if host_pid else ": not the host's PID namespace; KFD reports host "
+                                          "PIDs, so pod attribution needs hostPID: true")))
+        ras = [s for s in statics if s.get("bdf") and os.path.isdir(f"/sys/bus/pci/devices/{s['bdf']}/ras")]
+        out.append(("RAS / ECC files", OK if ras else WARN,
+                    f"ras/ readable on {len(ras)}/{len(statics)} GPU(s)" if ras
+                    else "no ras/ directory: ECC from libamd_smi per block, no poison / fatal events"))
+        # control plane: the native pollers run at start; give them a moment to report
+        deadline = time.time() + wait_s
+        text = mon.metrics()
+        while time.time() < deadline and (_gauge(text, "gpumon_podresources_up") is None
+                                          or _gauge(text, "gpumon_cri_up") is None):
+            time.sleep(0.2)
+            mon.tick()
+            text = mon.metrics()
+        for name, series, sock, lost in (
+                ("kubelet PodResources", "gpumon_podresources", cfg.pod_resources_socket,
+                 "no idle-allocation rows, no allocated / in-use GPU counts"),
+                ("CRI runtime", "gpumon_cri", cfg.cri_socket or "(autodetect)",
+                 "pod names from /proc fallbacks only (HOSTNAME, service-account namespace)")):
+            up = _gauge(text, f"{series}_up")
+            code = _gauge(text, f"{series}_grpc_status")
+            if up is None:
+                out.append((name, SKIP, f"{sock}: not polled (control plane off or no socket)"))
+            elif up >= 1:
+                out.append((name, OK, f"{sock}: answering"))
+            else:
+                out.append((name, WARN, f"{sock}: down (grpc-status {code if code is not None else '-'}): {lost}"))
+        out.append(("rt_priority",) + _rt_permitted())
+        # on-device samplers: the helper and plugins must exist; --ondevice-check runs them once
+        from ._native import core as _core
+
+        core = _core()
+        plugin_dir = cfg.plugin_dir or os.environ.get("GPUMON_PLUGIN_DIR") or os.path.join(
+            os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "lib")
+        files = ["gpumon-ondevice-helper", "libgpumon_pmc.so", "libgpumon_probe.so"]
+        missing = [f for f in files if not os.path.exists(os.path.join(plugin_dir, f))]
+        out.append(("on-device plugins", OK if not missing else WARN,
+                    f"{plugin_dir}: " + ("helper + PMC + probe present" if not missing
+                                         else f"missing {', '.join(missing)}: enable_pmc / enable_probe will refuse "
+                                              "to start")))
+        if ondevice_check and not missing:
+            od = core.OnDevice(mon.ex, {"plugin_dir": plugin_dir, "pmc": True, "probe": True, "pmc_every_s": 60.0,
+                                        "probe_every_s": 60.0, "pmc_mode": "continuous", "ondevice_isolate": True})
+            try:
+                od.start()
+                od.step()
+                time.sleep(0.2)
+                od.step()
+                s = od.stats()
+                mon.tick()
+                text = mon.metrics()
+                pmc_up = _gauge(text, "gpumon_pmc_up")
+                out.append(("PMC device counting", OK if pmc_up == 1 else WARN,
+                            f"{s['pmc_agents']} agent(s), pmc_up {pmc_up}, errors {s['pmc_errors']}"
+                            + ("" if pmc_up == 1 else ": another profiler may hold the counters")))
+                out.append(("K1 probe", OK if s["probe_done"] > 0 else WARN,
+                            f"{s['probe_devices']} device(s), {s['probe_done']} completed, "
+                            f"{s['probe_timeouts']} timeouts"))
+                rss = _gauge(text, "gpumon_ondevice_helper_resident_memory_bytes")
+                if rss:
+                    out.append(("on-device helper memory", OK,
+                                f"{rss / 2 ** 20:.0f} MiB resident (size the pod's memory limit for it)"))
+            except RuntimeError as e:
+                out.append(("on-device samplers", FAIL, str(e)))
+            finally:
+                od.stop()
+    finally:
+        mon.stop()
+    return out
+
+
+def main(args, cfg) -> int:
+    checks = run(cfg, ondevice_check=args.ondevice_check)
+    if args.format == "json":
+        json.dump([{"check": c, "status": s, "detail": d} for c, s, d in checks], sys.stdout, indent=1)
+        sys.stdout.write("\n")
+    else:
+        for c, s, d in checks:
+            sys.stdout.write(f"[{s.upper():>4}] {c:<24} {d}\n")
+    return 1 if any(s == FAIL for _, s, _ in checks) else 0

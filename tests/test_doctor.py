@@ -1,0 +1,72 @@
+"""`gpumon doctor` (gpumon/doctor.py): the node-prerequisite report, against the mock backend and
+the fake kubelet. The reference's only self-check was commandexists('docker'/'nvidia-smi')
+(/root/reference/gpu.py:28-33,260)."""
+
+import json
+import os
+import subprocess
+import sys
+
+import grpc
+
+from gpumon.attribution.fake_kubelet import FakeKubelet
+from gpumon.config import Config
+from gpumon import doctor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _by_name(checks):
+    return {c: (s, d) for c, s, d in checks}
+
+
+def test_doctor_reports_sockets_and_plugins():
+    d = f"/tmp/gpumon-doc-{os.getpid()}"
+    os.makedirs(d, exist_ok=True)
+    with FakeKubelet(podres_socket=f"{d}/kubelet.sock", cri_socket=f"{d}/cri.sock") as k:
+        cfg = Config(backend="mock:gpus=2", control_plane="native", pod_resources_socket=k.podres_socket,
+                     cri_socket=k.cri_socket, log_level="error")
+        checks = _by_name(doctor.run(cfg, wait_s=5))
+    assert checks["device backend"][0] == "ok" and "2 GPU(s)" in checks["device backend"][1]
+    assert checks["kubelet PodResources"][0] == "ok" and checks["CRI runtime"][0] == "ok"
+    assert checks["sysfs fast path"][0] == "skip"  # mock backend
+    assert checks["on-device plugins"][0] == "ok"
+    assert checks["rt_priority"][0] in ("ok", "warn")
+
+
+def test_doctor_names_the_grpc_status_of_a_refusing_kubelet():
+    d = f"/tmp/gpumon-doc2-{os.getpid()}"
+    os.makedirs(d, exist_ok=True)
+    with FakeKubelet(podres_socket=f"{d}/kubelet.sock") as k:
+        k.podres_error = (grpc.StatusCode.PERMISSION_DENIED, "socket is root-only")
+        cfg = Config(backend="mock:gpus=1", control_plane="native", pod_resources_socket=k.podres_socket,
+                     cri_socket="", log_level="error")
+        checks = _by_name(doctor.run(cfg, wait_s=5))
+    s, detail = checks["kubelet PodResources"]
+    assert s == "warn" and "grpc-status 7" in detail and "idle-allocation" in detail
+
+
+def test_doctor_cli_json_and_exit_status():
+    r = subprocess.run([sys.executable, "-m", "gpumon", "doctor", "--backend", "mock:gpus=1", "--format", "json",
+                        "--control-plane", "off"], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = json.loads(r.stdout)
+    assert rows[0]["check"] == "device backend" and rows[0]["status"] == "ok"
+    # a backend that cannot come up is the one failing (exit 1) check
+    r = subprocess.run([sys.executable, "-m", "gpumon", "doctor", "--backend", "rocm_smi", "--format", "json",
+                        "--control-plane", "off"], capture_output=True, text=True, timeout=120, cwd=ROOT,
+                       env=dict(os.environ, LD_LIBRARY_PATH="/nonexistent"))
+    rows = json.loads(r.stdout)
+    assert r.returncode == 1 and rows[0]["status"] == "fail", (r.returncode, rows)
+
+
+def test_doctor_runs_the_ondevice_samplers_once():
+    from conftest import make_locked
+
+    make_locked("fakes")
+    cfg = Config(backend="mock:gpus=1", control_plane="off", log_level="error",
+                 plugin_dir=os.path.join(ROOT, "build", "fakes", "ondevice"))
+    checks = _by_name(doctor.run(cfg, ondevice_check=True, wait_s=0.5))
+    assert checks["PMC device counting"][0] == "ok", checks
+    assert checks["K1 probe"][0] == "ok", checks
+    assert checks["on-device helper memory"][0] == "ok"
