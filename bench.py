@@ -184,16 +184,19 @@ def main() -> int:
 
         core = _core()
         if backend == "auto":
-            backend = "amdsmi" if has_gpu else f"mock:gpus={n * args.replicate},mode=load"
+            # auto = libamd_smi with the sysfs fast path, rocm_smi_lib if libamd_smi cannot initialise
+            backend = "auto" if has_gpu else f"mock:gpus={n * args.replicate},mode=load"
             if has_gpu and args.replicate > 1:
                 backend = f"amdsmi:replicate={args.replicate}"
-        cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi")) else [],
+        cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi", "auto")) else [],
                      interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
                      enable_probe=args.probe and has_gpu, log_level="warn", fast_path=not args.no_fast_path,
                      sample_threads=args.sample_threads, rt_priority=args.rt_priority)
         mon = GpuMonitor(cfg, control_plane=False).start()
         if mon.start_error:
             raise SystemExit(f"exporter backend failed: {mon.start_error}")
+        if backend == "auto":
+            backend = mon.ex.self_stats().get("backend") or backend  # the one that came up
         st = mon.ex.statics()
         if len(st) < n:
             raise SystemExit(f"exporter sees {len(st)} GPU(s), bench needs {n}")
