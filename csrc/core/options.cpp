@@ -265,6 +265,7 @@ const std::map<std::string, Setter>& setters() {
       {"pmc_counters", list_at([](NativeOptions* o) { return &o->od.pmc_counters; })},
       {"pmc_mode", str_at([](NativeOptions* o) { return &o->od.pmc_mode; })},
       {"ondevice_isolate", bool_at([](NativeOptions* o) { return &o->od.ondevice_isolate; })},
+      {"helper_retry", dbl_at([](NativeOptions* o) { return &o->od.helper_retry_s; })},
       {"plugin_dir", str_at([](NativeOptions* o) { return &o->od.plugin_dir; })},
       {"activity_acc_scale", dbl_at([](NativeOptions* o) { return &o->cfg.rates.activity_acc_scale; })},
       {"xgmi_kb_bytes", dbl_at([](NativeOptions* o) { return &o->cfg.rates.xgmi_kb_bytes; })},
@@ -530,6 +531,7 @@ std::string options_json(const NativeOptions& o) {
   L("pmc_counters", o.od.pmc_counters);
   S("pmc_mode", o.od.pmc_mode);
   B("ondevice_isolate", o.od.ondevice_isolate);
+  N("helper_retry", o.od.helper_retry_s);
   S("plugin_dir", o.od.plugin_dir);
   N("activity_acc_scale", c.rates.activity_acc_scale);
   N("xgmi_kb_bytes", c.rates.xgmi_kb_bytes);

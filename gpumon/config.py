@@ -96,6 +96,7 @@ class Config:
     # the counting contexts in a helper process frozen between reads (rocprofiler-sdk leaves an HSA
     # thread polling a full core in the process that owns them, profiles/r2_footprint.md)
     ondevice_isolate: bool = True
+    helper_retry: float = 10.0            # seconds before a dead helper is respawned (doubling while it keeps dying)
     pmc_counters: List[str] = field(default_factory=lambda: (
         ["SQ_VALU_MFMA_BUSY_CYCLES"] + ["SQ_INSTS_VALU_MFMA_MOPS_" + d for d in
                                         ("BF16", "F16", "F8", "F6F4", "F32", "F64", "I8")]

@@ -92,7 +92,7 @@ class GpuMonitor:
             self.ondevice = self._core.OnDevice(self.ex, {
                 "plugin_dir": self.cfg.plugin_dir, "pmc": bool(self.cfg.enable_pmc),
                 "pmc_counters": list(self.cfg.pmc_counters), "pmc_every_s": period, "pmc_mode": self.cfg.pmc_mode,
-                "ondevice_isolate": self.cfg.ondevice_isolate,
+                "ondevice_isolate": self.cfg.ondevice_isolate, "helper_retry_s": float(self.cfg.helper_retry),
                 "probe": bool(self.cfg.enable_probe), "probe_every_s": period * self.cfg.probe_every})
             self.ondevice.start()
             return

@@ -3,6 +3,7 @@ TSan builds of bin/gpumon-exporter under concurrent scrapes while the sampler ti
 snapshots are swapped. GPU sanitizers are not available on this pool; these cover the C++ core."""
 
 import os
+import re
 import signal
 import socket
 import subprocess
@@ -82,3 +83,60 @@ def test_sanitized_exporter_under_concurrent_scrapes(target, binary, env, extra)
            or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
     assert not bad, err[-4000:]
     assert rc == 0, err[-2000:]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_exporter_survives_helper_kills(target, binary, env):
+    """The on-device helper SIGKILLed three times while the PMC and probe threads both use it: the
+    respawn path (one sampler respawns, the other waits on it; PMC re-init before probe ops) runs
+    under ASan/UBSan and TSan without a report, and the exporter keeps serving."""
+    from conftest import make_locked
+
+    make_locked(target, "fakes", jobs=8)
+    port = _free_port()
+    e = dict(os.environ, GPUMON_FAKE_AGENTS="2", **env)
+    p = subprocess.Popen([os.path.join(ROOT, binary), "--backend", "mock:gpus=2", "--interval", "0.02", "--listen",
+                          f"127.0.0.1:{port}", "--log-level", "error", "--pmc", "--probe", "--probe-every", "1",
+                          "--plugin-dir", os.path.join(ROOT, "build", "fakes", "ondevice")],
+                         stderr=subprocess.PIPE, stdout=subprocess.DEVNULL, env=dict(e, GPUMON_HELPER_RETRY="0.05"),
+                         text=True)
+    try:
+        def helpers():
+            out = []
+            for q in os.listdir("/proc"):
+                if q.isdigit():
+                    try:
+                        if open(f"/proc/{q}/comm").read().strip() == "gpumon-ondevice" and \
+                                int(open(f"/proc/{q}/stat").read().rsplit(")", 1)[1].split()[1]) == p.pid:
+                            out.append(int(q))
+                    except (OSError, ValueError, IndexError):
+                        pass
+            return out
+
+        deadline = time.time() + 60
+        kills = 0
+        while kills < 3 and time.time() < deadline:
+            hs = helpers()
+            if hs:
+                os.kill(hs[0], signal.SIGKILL)
+                kills += 1
+                time.sleep(0.3)
+            else:
+                time.sleep(0.05)
+        assert kills == 3
+        time.sleep(1.0)
+        assert p.poll() is None
+        body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+        restarts = float(re.search(r"^gpumon_ondevice_helper_restarts_total\{[^}]*\} (\S+)$", body, re.M).group(1))
+        assert restarts >= 2, restarts
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=60)
+    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
+           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    assert not bad, err[-4000:]
