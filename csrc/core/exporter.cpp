@@ -1088,6 +1088,14 @@ std::vector<DeviceSample> Exporter::samples() const {
   std::lock_guard<std::mutex> g(state_mu_);
   return cur_;
 }
+std::vector<int> Exporter::xcd_counts() const {
+  std::lock_guard<std::mutex> g(state_mu_);
+  std::vector<int> out;
+  out.reserve(cur_.size());
+  for (const auto& s : cur_) out.push_back(s.n_xcd);
+  return out;
+}
+
 std::vector<DeviceRates> Exporter::rates() const {
   std::lock_guard<std::mutex> g(state_mu_);
   return rates_;

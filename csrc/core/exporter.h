@@ -134,6 +134,7 @@ class Exporter {
   // Introspection.
   std::vector<DeviceStatic> statics() const;
   std::vector<DeviceSample> samples() const;
+  std::vector<int> xcd_counts() const;  // XCDs per device in the last sample (gpu_metrics xcp_stats)
   std::vector<DeviceRates> rates() const;
   std::vector<PodRow> pod_rows() const;
   SelfStats self_stats() const;

@@ -1094,6 +1094,7 @@ constexpr const char* kSlotHelp =
 
 void OnDevice::export_probe() {
   std::vector<ExtraSeries> out;
+  const std::vector<int> xcds = ex_->xcd_counts();
   for (const auto& p : probes_) {
     out.push_back(xs("gpu_probe_pending", "1 if the last probe launch has not completed yet.", p.dev,
                      p.pending >= 0 ? 1 : 0));
@@ -1108,9 +1109,18 @@ void OnDevice::export_probe() {
                      p.span_s));
     out.push_back(xs("gpu_probe_unique_cus", "Distinct compute units that ran probe workgroups.", p.dev, p.unique_cus));
     out.push_back(xs("gpu_probe_wave_slot_mean", kSlotHelp, p.dev, p.slot_mean));
+    // XCD liveness: every XCD the device has gets a gpu_probe_xcd_blocks sample, 0 when none of
+    // the probe's workgroups ran there (an alertable value instead of a vanished series)
+    const int n_xcd = p.dev < static_cast<int>(xcds.size()) ? xcds[p.dev] : 0;
     for (size_t x = 0; x < p.xcc_blocks.size(); ++x) {
-      if (!p.xcc_blocks[x]) continue;
-      out.push_back(xs("gpu_probe_xcd_blocks", "Probe workgroups executed per XCD (liveness).", p.dev, p.xcc_blocks[x]));
+      if (!p.xcc_blocks[x]) {
+        if (static_cast<int>(x) < n_xcd) {
+          out.push_back(xs("gpu_probe_xcd_blocks", "Probe workgroups executed per XCD (liveness: 0 = the XCD ran none of them).", p.dev, 0.0));
+          out.back().labels.push_back({"xcd", std::to_string(x)});
+        }
+        continue;
+      }
+      out.push_back(xs("gpu_probe_xcd_blocks", "Probe workgroups executed per XCD (liveness: 0 = the XCD ran none of them).", p.dev, p.xcc_blocks[x]));
       out.back().labels.push_back({"xcd", std::to_string(x)});
       out.push_back(xs("gpu_probe_xcd_clock_mhz", "Effective shader clock per XCD measured in-kernel.", p.dev,
                        p.xcc_mhz[x]));

@@ -14,6 +14,7 @@
 //   GPUMON_FAKE_PMC_RESTART every Nth continuous read the counts restart from 0 without the
 //                           started flag (another tool restarted the contexts underneath)
 //   GPUMON_FAKE_PROBE_HANG  1 -> launches never complete (timeouts path)
+//   GPUMON_FAKE_DEAD_XCD    N -> no probe workgroup runs on XCD N (liveness path)
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -210,8 +211,9 @@ EXPORT int gpumon_probe_wait(gpumon_probe* p, int, double timeout_s, gpumon_prob
   out->gpu_span_s = 6e-6;
   out->unique_cus = kCus;
   out->wave_slot_mean = 1.75;
+  const char* dead = getenv("GPUMON_FAKE_DEAD_XCD");
   for (uint32_t x = 0; x < kXcc; ++x) {
-    out->xcc_blocks[x] = p->blocks / kXcc;
+    out->xcc_blocks[x] = dead && static_cast<uint32_t>(atoi(dead)) == x ? 0 : p->blocks / kXcc;
     out->xcc_clock_mhz[x] = 2400.0 - 10.0 * x;
     out->xcc_wave_slot[x] = 0.5 * x;
   }

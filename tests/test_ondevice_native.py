@@ -622,3 +622,21 @@ def test_helper_that_keeps_dying_backs_off(core, mock_exporter):
         assert 0.15 <= gaps[0] < 0.6 and gaps[1] >= 0.35 and gaps[1] > gaps[0], gaps
     finally:
         od.stop()
+
+
+def test_silent_xcd_is_exported_as_zero_blocks(core, mock_exporter, monkeypatch):
+    """K1 liveness: an XCD that ran none of the probe's workgroups reads 0 in gpu_probe_xcd_blocks
+    (an alertable value), instead of its series disappearing."""
+    monkeypatch.setenv("GPUMON_FAKE_DEAD_XCD", "3")
+    ex = mock_exporter(backend="mock:gpus=1,n_xcd=8")
+    ex.tick()
+    od = _ondevice(core, ex, pmc=False, probe_every_s=60)
+    od.start()
+    try:
+        od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        blocks = {x: _val(m, "gpu_probe_xcd_blocks", gpu_id="0", xcd=str(x)) for x in range(8)}
+        assert blocks[3] == 0 and all(v > 0 for x, v in blocks.items() if x != 3), blocks
+    finally:
+        od.stop()
