@@ -65,6 +65,26 @@ def _r(x, nd=3):
     return round(x, nd) if isinstance(x, float) and x == x else x
 
 
+def _exporter_cpu_s():
+    """CPU seconds of the exporter's own threads in this process (named gpumon-*: sampler, device
+    workers, HTTP loops, pollers); the bench's loads, scraper and torch threads are not counted."""
+    hz = os.sysconf("SC_CLK_TCK")
+    total = 0.0
+    for t in os.listdir("/proc/self/task"):
+        try:
+            s = open(f"/proc/self/task/{t}/stat").read()
+            if not s[s.index("(") + 1:s.rindex(")")].startswith("gpumon-"):
+                continue
+            try:  # nanoseconds on the CPU (schedstat), else clock ticks
+                total += int(open(f"/proc/self/task/{t}/schedstat").read().split()[0]) * 1e-9
+            except (OSError, ValueError, IndexError):
+                f = s.rsplit(")", 1)[1].split()
+                total += (int(f[11]) + int(f[12])) / hz
+        except OSError:
+            continue
+    return total
+
+
 def _per_gpu_xgmi(tick_rates, n, expected_tx, expected_rx):
     """Exporter-measured xGMI tx / rx per GPU (sum over links, mean over the timed ticks; the first
     tick's rate spans part of the warmup and is skipped) against the traffic the bench drove."""
@@ -284,6 +304,7 @@ def main() -> int:
         scraper = threading.Thread(target=_scrape, daemon=True)
         s0 = mon.ex.self_stats()
         seq0 = mon.ex.seq
+        cpu0 = _exporter_cpu_s()
 
     # ---------------------------------------------------------------- timed region
     barrier()
@@ -316,6 +337,7 @@ def main() -> int:
     if rank == 0:  # the exporter's counters at the end of the timed region (not after the reductions)
         s1 = mon.ex.self_stats()
         seq1 = mon.ex.seq
+        cpu1 = _exporter_cpu_s()
     c1 = [c.stats() for c in copiers]
     l1 = [ld.stats() for ld in loads]
     if dist is not None:
@@ -444,6 +466,8 @@ def main() -> int:
             "server_scrape_p99_ms_last4096": round(mon.ex.scrape_quantile(0.99) * 1e3, 4),
             "overruns": s1["overruns"] - s0["overruns"],
             "sampler_rt_threads": s1.get("rt_threads", 0),
+            # the exporter's own threads over the timed region, serving the scrape load too (1/100 s ticks)
+            "exporter_cpu_millicores": round(1000.0 * (cpu1 - cpu0) / elapsed, 2),
             "backend_call_us": {k: round((v["seconds"] - s0["backend_calls"].get(k, {}).get("seconds", 0.0)) * 1e6
                                          / max(1, v["n"] - s0["backend_calls"].get(k, {}).get("n", 0)), 1)
                                 for k, v in s1.get("backend_calls", {}).items()},
