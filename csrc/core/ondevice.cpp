@@ -211,9 +211,21 @@ bool helper_spawn(const std::string& path, std::string* err) {
   posix_spawn_file_actions_init(&fa);
   posix_spawn_file_actions_adddup2(&fa, req[0], 0);
   posix_spawn_file_actions_adddup2(&fa, resp[1], 1);
+  // a clean signal state for the child: the exporter may block SIGTERM / SIGINT for its own
+  // signal handling, and a signal mask survives exec
+  posix_spawnattr_t sa;
+  posix_spawnattr_init(&sa);
+  sigset_t none, dflt;
+  sigemptyset(&none);
+  sigemptyset(&dflt);
+  for (int s : {SIGTERM, SIGINT, SIGHUP, SIGPIPE}) sigaddset(&dflt, s);
+  posix_spawnattr_setsigmask(&sa, &none);
+  posix_spawnattr_setsigdefault(&sa, &dflt);
+  posix_spawnattr_setflags(&sa, POSIX_SPAWN_SETSIGMASK | POSIX_SPAWN_SETSIGDEF);
   char* argv[] = {const_cast<char*>(path.c_str()), nullptr};
   pid_t pid = -1;
-  const int rc = spawn_on_keeper([&] { return posix_spawn(&pid, path.c_str(), &fa, nullptr, argv, environ); });
+  const int rc = spawn_on_keeper([&] { return posix_spawn(&pid, path.c_str(), &fa, &sa, argv, environ); });
+  posix_spawnattr_destroy(&sa);
   posix_spawn_file_actions_destroy(&fa);
   ::close(req[0]);
   ::close(resp[1]);

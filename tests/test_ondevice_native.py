@@ -640,3 +640,28 @@ def test_silent_xcd_is_exported_as_zero_blocks(core, mock_exporter, monkeypatch)
         assert blocks[3] == 0 and all(v > 0 for x, v in blocks.items() if x != 3), blocks
     finally:
         od.stop()
+
+
+def test_helper_starts_with_a_clean_signal_mask():
+    """The exporter binary blocks SIGTERM / SIGINT for its own handling; a signal mask survives
+    exec, so the helper is spawned with an empty mask and default dispositions."""
+    import time
+
+    e = dict(os.environ, GPUMON_FAKE_AGENTS="1")
+    p = subprocess.Popen([BIN, "--backend", "mock:gpus=1", "--listen", "127.0.0.1:0", "--interval", "0.2",
+                          "--no-pod-resources", "--no-cri", "--pmc", "--plugin-dir", FAKE_DIR, "--log-level", "error"],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=e, text=True)
+    try:
+        kids = []
+        for _ in range(50):
+            time.sleep(0.1)
+            kids = [int(k) for t in os.listdir(f"/proc/{p.pid}/task")
+                    for k in open(f"/proc/{p.pid}/task/{t}/children").read().split()]
+            if kids:
+                break
+        assert len(kids) == 1
+        status = dict(l.split(":", 1) for l in open(f"/proc/{kids[0]}/status") if ":" in l)
+        assert int(status["SigBlk"].strip(), 16) == 0, status["SigBlk"]
+    finally:
+        p.terminate()
+        p.wait(20)
