@@ -304,7 +304,8 @@ int helper_call(uint32_t op, const int* agents, int n_agents, const char* const*
   bool ok = io_full(g_helper.to, &q, sizeof q, true, deadline) &&
             (n_agents <= 0 || io_full(g_helper.to, const_cast<int*>(agents), sizeof(int) * n_agents, true, deadline)) &&
             (names.empty() || io_full(g_helper.to, &names[0], names.size(), true, deadline)) &&
-            io_full(g_helper.from, &h, sizeof h, false, deadline) && h.magic == GPUMON_PMC_PROTO_MAGIC;
+            io_full(g_helper.from, &h, sizeof h, false, deadline) && h.magic == GPUMON_PMC_PROTO_MAGIC &&
+            h.err_len <= (64u << 10) && h.payload_len <= (16u << 20);  // a corrupt header is a dead helper
   if (ok && h.err_len) {
     e.resize(h.err_len);
     ok = io_full(g_helper.from, &e[0], e.size(), false, deadline);
