@@ -123,6 +123,7 @@ int main() {
   for (;;) {
     gpumon_pmc_req_t q;
     if (!read_full(0, &q, sizeof q) || q.magic != GPUMON_PMC_PROTO_MAGIC) return 0;
+    if (q.n_agents > 4096 || q.counters_len > (64u << 10)) return 0;  // corrupt request: exit
     std::vector<int> agents(q.n_agents);
     std::string counters(q.counters_len, '\0');
     if ((q.n_agents && !read_full(0, agents.data(), agents.size() * sizeof(int))) ||
