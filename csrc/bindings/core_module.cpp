@@ -9,6 +9,7 @@
 #include "../core/attribution.h"
 #include "../core/backend.h"
 #include "../core/common.h"
+#include "../core/docker_lite.h"
 #include "../core/exporter.h"
 #include "../core/grpc_lite.h"
 #include "../core/hpack.h"
@@ -101,6 +102,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "pod_resources_dra_drivers", &c.pod_resources_dra_drivers);
   get(d, "pod_resources_refresh_s", &c.pod_resources_refresh_s);
   get(d, "cri_socket", &c.cri_socket);
+  get(d, "docker_socket", &c.docker_socket);
   get(d, "version", &c.version);
   get(d, "activity_acc_scale", &c.rates.activity_acc_scale);
   get(d, "xgmi_kb_bytes", &c.rates.xgmi_kb_bytes);
@@ -446,6 +448,51 @@ PYBIND11_MODULE(_core, m) {
     if (!hpack_huffman_decode(std::string(b), &out)) throw py::value_error("invalid Huffman string");
     return py::bytes(out);
   });
+  auto docker_rows = [](const std::vector<DockerContainer>& cs) {
+    py::list l;
+    for (const auto& c : cs) {
+      py::dict d;
+      d["id"] = c.id;
+      d["name"] = c.name;
+      d["state"] = c.state;
+      d["labels"] = c.labels;
+      l.append(d);
+    }
+    return l;
+  };
+  m.def(
+      "docker_parse_containers",
+      [docker_rows](py::bytes b) {
+        std::vector<DockerContainer> cs;
+        std::string err;
+        if (!docker_parse_containers(std::string(b), &cs, &err)) throw py::value_error(err);
+        return docker_rows(cs);
+      },
+      py::arg("json"), "parse a Docker Engine GET /containers/json body (docker_lite.cpp)");
+  m.def(
+      "http1_parse_response",
+      [](py::bytes raw) {
+        int status = -1;
+        std::string body, err;
+        if (!http1_parse_response(std::string(raw), &status, &body, &err)) throw py::value_error(err);
+        return py::make_tuple(status, py::bytes(body));
+      },
+      py::arg("raw"));
+  m.def(
+      "docker_list",
+      [docker_rows](const std::string& sock, int timeout_ms) {
+        std::vector<DockerContainer> cs;
+        std::string err;
+        int status = -1;
+        bool ok;
+        {
+          py::gil_scoped_release nogil;
+          ok = docker_list(sock, &cs, &err, timeout_ms, &status);
+        }
+        if (!ok) throw std::runtime_error(err);
+        return docker_rows(cs);
+      },
+      py::arg("socket"), py::arg("timeout_ms") = 3000, "Docker Engine GET /containers/json via docker_lite.cpp");
   m.def(
       "cri_list",
       [](const std::string& sock, int timeout_ms) {

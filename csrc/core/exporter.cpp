@@ -11,8 +11,10 @@
 #include <cmath>
 #include <cstring>
 #include <functional>
+#include <unordered_set>
 
 #include "common.h"
+#include "docker_lite.h"
 #include "grpc_lite.h"
 #include "http_client.h"
 #include "trace.h"
@@ -443,9 +445,10 @@ bool Exporter::start(std::string* err) {
     set_thread_name("gpumon-influx");
     influx_loop();
   });
-  if (!cfg_.pod_resources_socket.empty() || !cfg_.cri_socket.empty()) {
+  if (!cfg_.pod_resources_socket.empty() || !cfg_.cri_socket.empty() || !cfg_.docker_socket.empty()) {
     // metadata and allocations known before the first scrape
     if (!cfg_.cri_socket.empty()) cri_poll_once();
+    if (!cfg_.docker_socket.empty()) docker_poll_once();
     if (!cfg_.pod_resources_socket.empty()) podres_poll_once();
     podres_ = std::thread([this] {
       set_thread_name("gpumon-k8s");
@@ -1313,6 +1316,7 @@ void Exporter::podres_loop() {
     if (!running_) break;
     lk.unlock();
     if (!cfg_.cri_socket.empty()) cri_poll_once();
+    if (!cfg_.docker_socket.empty()) docker_poll_once();
     if (!cfg_.pod_resources_socket.empty()) podres_poll_once();
     lk.lock();
   }
@@ -1355,12 +1359,10 @@ bool Exporter::cri_poll_once() {
       metas.push_back(std::move(m));
     }
     {
-      std::lock_guard<std::mutex> g(podres_mu_);
-      native_meta_.clear();
-      for (const auto& m : metas)
-        native_meta_[m.pod_namespace + "/" + m.pod_name + "/" + m.container_name] = m;
+      std::lock_guard<std::mutex> g(meta_mu_);
+      cri_metas_ = std::move(metas);
     }
-    attr_->set_container_meta(std::move(metas));
+    publish_container_meta();
   } else {
     GPUMON_LOG(LogLevel::kWarn, "cri", "ListContainers/ListPodSandbox failed: " + err);
   }
@@ -1375,6 +1377,76 @@ bool Exporter::cri_poll_once() {
                 "-1 = no status: transport failure).",
                 "gauge", -1, {}, static_cast<double>(gst.code)});
   set_extra("cri_native", std::move(ex));
+  return ok;
+}
+
+// CRI metadata first; Docker listings add the containers no CRI runtime reported (plain-Docker
+// nodes, or dockershim-era nodes where both are configured). Empty pod names (non-k8s containers)
+// never enter the PodResources join.
+void Exporter::publish_container_meta() {
+  std::vector<ContainerMeta> all;
+  {
+    std::lock_guard<std::mutex> g(meta_mu_);
+    all = cri_metas_;
+    std::unordered_set<std::string> seen;
+    for (const auto& m : all) seen.insert(m.container_id);
+    for (const auto& m : docker_metas_)
+      if (seen.insert(m.container_id).second) all.push_back(m);
+  }
+  {
+    std::lock_guard<std::mutex> g(podres_mu_);
+    native_meta_.clear();
+    for (const auto& m : all)
+      if (!m.pod_name.empty()) native_meta_[m.pod_namespace + "/" + m.pod_name + "/" + m.container_name] = m;
+  }
+  attr_->set_container_meta(std::move(all));
+}
+
+// Docker Engine GET /containers/json -> ContainerMeta. The reference's `docker inspect` read the
+// same Config.Labels (/root/reference/gpu.py:86-88,184-195): io.kubernetes.* on dockershim-managed
+// containers, user labels (e.g. the `mlgpu` opt-in) on any container.
+bool Exporter::docker_poll_once() {
+  std::vector<DockerContainer> cs;
+  std::string err;
+  int http = -1;
+  const int64_t t0 = mono_ns();
+  const bool ok = docker_list(cfg_.docker_socket, &cs, &err, 3000, &http);
+  const double dt = (mono_ns() - t0) * 1e-9;
+  if (ok) {
+    std::vector<ContainerMeta> metas;
+    metas.reserve(cs.size());
+    for (auto& c : cs) {
+      ContainerMeta m;
+      m.container_id = c.id;
+      auto lab = [&](const char* k, const std::string& dflt) {
+        const auto l = c.labels.find(k);
+        return l != c.labels.end() && !l->second.empty() ? l->second : dflt;
+      };
+      m.container_name = lab("io.kubernetes.container.name", c.name);
+      m.pod_name = lab("io.kubernetes.pod.name", "");
+      m.pod_namespace = lab("io.kubernetes.pod.namespace", "");
+      m.pod_uid = lab("io.kubernetes.pod.uid", "");
+      m.labels = std::move(c.labels);
+      metas.push_back(std::move(m));
+    }
+    {
+      std::lock_guard<std::mutex> g(meta_mu_);
+      docker_metas_ = std::move(metas);
+    }
+    publish_container_meta();
+  } else {
+    GPUMON_LOG(LogLevel::kWarn, "docker", "GET /containers/json failed: " + err);
+  }
+  std::vector<ExtraSeries> ex;
+  ex.push_back({"gpumon_docker_up", "1 if the last Docker Engine GET /containers/json succeeded.", "gauge", -1, {},
+                ok ? 1.0 : 0.0});
+  ex.push_back({"gpumon_docker_containers", "Containers known from the Docker Engine API.", "gauge", -1, {},
+                static_cast<double>(cs.size())});
+  ex.push_back({"gpumon_docker_list_seconds", "Duration of the last Docker Engine listing.", "gauge", -1, {}, dt});
+  ex.push_back({"gpumon_docker_http_status",
+                "HTTP status of the last Docker Engine listing (-1 = transport failure).", "gauge", -1, {},
+                static_cast<double>(http)});
+  set_extra("docker_native", std::move(ex));
   return ok;
 }
 

@@ -80,6 +80,9 @@ struct ExporterConfig {
   std::vector<std::string> pod_resources_dra_drivers = {"gpu.amd.com"};  // DRA claim devices counted too
   double pod_resources_refresh_s = 10.0;
   std::string cri_socket;             // native CRI ListContainers/ListPodSandbox (same refresh)
+  // Docker Engine GET /containers/json (docker_lite.cpp) for plain-Docker nodes: opt-in only (the
+  // socket is root-equivalent), same refresh; merged under the CRI metadata by container id
+  std::string docker_socket;
   std::string version = "0.1.0";
 };
 
@@ -152,6 +155,8 @@ class Exporter {
   void podres_loop();
   bool podres_poll_once();
   bool cri_poll_once();
+  bool docker_poll_once();
+  void publish_container_meta();  // CRI U Docker metadata -> attribution + native_meta_
   bool ensure_backend();
   void handle_http(const HttpRequest& req, HttpResponse* resp);
   void sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
@@ -227,6 +232,8 @@ class Exporter {
   std::mutex podres_mu_;
   std::condition_variable podres_cv_;
   std::unordered_map<std::string, ContainerMeta> native_meta_;  // "ns/pod/container" (guarded by podres_mu_)
+  std::mutex meta_mu_;
+  std::vector<ContainerMeta> cri_metas_, docker_metas_;  // last successful listing of each (meta_mu_)
   std::mutex push_mu_;
   std::condition_variable push_cv_;
   std::deque<std::string> push_q_;

@@ -255,6 +255,7 @@ const std::map<std::string, Setter>& setters() {
        bool_at([](NativeOptions* o) { return &o->cfg.attribution.include_host_processes; })},
       {"verify_kfd", bool_at([](NativeOptions* o) { return &o->cfg.attribution.verify_kfd; })},
       {"cri_socket", str(&NativeOptions::cri_socket)},
+      {"docker_socket", str_at([](NativeOptions* o) { return &o->cfg.docker_socket; })},
       {"pod_resources_socket", str(&NativeOptions::pod_resources_socket)},
       {"resource_names", list_at([](NativeOptions* o) { return &o->resource_names; })},
       {"dra_drivers", list_at([](NativeOptions* o) { return &o->cfg.pod_resources_dra_drivers; })},
@@ -432,7 +433,7 @@ void options_finalize(NativeOptions* o) {
   if (starts_with(cri, "unix://")) cri = cri.substr(7);
   if (cri.empty()) {
     for (const char* s : {"/run/containerd/containerd.sock", "/var/run/crio/crio.sock", "/run/crio/crio.sock",
-                          "/var/run/cri-dockerd.sock"})
+                          "/var/run/cri-dockerd.sock", "/var/run/dockershim.sock"})
       if (access(s, F_OK) == 0) {
         cri = s;
         break;
@@ -521,6 +522,7 @@ std::string options_json(const NativeOptions& o) {
   B("procfs_env_fallback", c.attribution.procfs_env_fallback);
   B("include_host_processes", c.attribution.include_host_processes);
   S("cri_socket", o.cri_socket);
+  S("docker_socket", c.docker_socket);
   S("pod_resources_socket", o.pod_resources_socket);
   L("resource_names", o.resource_names);
   L("dra_drivers", c.pod_resources_dra_drivers);

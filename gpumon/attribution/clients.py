@@ -25,6 +25,7 @@ DEFAULT_CRI_SOCKETS = (
     "/var/run/crio/crio.sock",
     "/run/cri-dockerd.sock",
     "/var/run/cri-dockerd.sock",
+    "/var/run/dockershim.sock",  # kubelet <= 1.23 with the docker runtime (dockershim serves CRI)
 )
 
 

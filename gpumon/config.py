@@ -76,6 +76,7 @@ class Config:
     control_plane: str = "native"         # native (C++ grpc_lite pollers: production) | python (grpcio clients: test oracle) | off
     cri_socket: str = ""                  # e.g. unix:///run/containerd/containerd.sock ; "" = autodetect
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
+    docker_socket: str = ""               # plain-Docker nodes (native plane): Docker Engine container names + labels; opt-in, e.g. /var/run/docker.sock
     resource_names: List[str] = field(default_factory=lambda: ["amd.com/gpu"])
     # DRA drivers whose claimed devices count as GPU allocations (kubelet PodResources dynamic_resources)
     dra_drivers: List[str] = field(default_factory=lambda: ["gpu.amd.com"])
@@ -249,6 +250,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--user-label", dest="user_label", help="pod label holding the user name")
     p.add_argument("--procfs-root", dest="procfs_root")
     p.add_argument("--cri-socket", dest="cri_socket")
+    p.add_argument("--docker-socket", dest="docker_socket",
+                   help="plain-Docker nodes: read container names/labels from the Docker Engine API (opt-in)")
     p.add_argument("--pod-resources-socket", dest="pod_resources_socket")
     p.add_argument("--control-plane", dest="control_plane", choices=["python", "native", "off"],
                    help="who polls kubelet PodResources / CRI: python (grpcio) or native (C++, no grpcio)")

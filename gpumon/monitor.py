@@ -27,7 +27,7 @@ _LEVELS = {"debug": 0, "info": 1, "warn": 2, "warning": 2, "error": 3, "off": 4}
 # well-known CRI sockets (gpumon/attribution/clients.py DEFAULT_CRI_SOCKETS; kept here so the
 # native path needs no grpcio import)
 _CRI_SOCKETS = ("/run/containerd/containerd.sock", "/var/run/containerd/containerd.sock", "/var/run/crio/crio.sock",
-                "/run/crio/crio.sock", "/var/run/cri-dockerd.sock")
+                "/run/crio/crio.sock", "/var/run/cri-dockerd.sock", "/var/run/dockershim.sock")
 
 
 class GpuMonitor:
@@ -50,6 +50,9 @@ class GpuMonitor:
             cri = self.cfg.cri_socket or next((p for p in _CRI_SOCKETS if os.path.exists(p)), "")
             if cri:
                 core_cfg["cri_socket"] = cri[len("unix://"):] if cri.startswith("unix://") else cri
+            if self.cfg.docker_socket:  # opt-in: never autodetected (root-equivalent socket)
+                d = self.cfg.docker_socket
+                core_cfg["docker_socket"] = d[len("unix://"):] if d.startswith("unix://") else d
             core_cfg["pod_resources_refresh_s"] = float(self.cfg.metadata_refresh)
             if self.cfg.resource_names:
                 core_cfg["pod_resources_prefix"] = self.cfg.resource_names[0]

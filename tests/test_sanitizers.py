@@ -24,8 +24,9 @@ def _free_port():
     return p
 
 
-def _run(binary, env_extra, extra_args=()):
+def _run(binary, env_extra, extra_args=(), min_s=0.0):
     port = _free_port()
+    t_start = time.time()
     env = dict(os.environ, **env_extra)
     p = subprocess.Popen([binary, "--backend", "mock:gpus=4", "--interval", "0.01", "--listen", f"127.0.0.1:{port}",
                           "--sample-threads", "2", "--http-threads", "2", "--log-level", "error", *extra_args],
@@ -55,6 +56,7 @@ def _run(binary, env_extra, extra_args=()):
         for t in ts:
             t.join()
         assert not errors, errors[:3]
+        time.sleep(max(0.0, t_start + min_s - time.time()))  # background pollers get their refreshes
     finally:
         p.send_signal(signal.SIGTERM)
         _, err = p.communicate(timeout=60)
@@ -140,3 +142,49 @@ def test_sanitized_exporter_survives_helper_kills(target, binary, env):
     bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
            or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
     assert not bad, err[-4000:]
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_docker_poller_on_mutated_listings(target, binary, env):
+    """The Docker Engine poller (csrc/core/docker_lite.cpp) refreshing every 0.5 s against a fake
+    daemon whose every answer is a random mutation of a realistic listing (truncations, byte flips,
+    duplicated spans) while scrapes run: no ASan/UBSan/TSan report and the exporter keeps serving."""
+    import json
+    import random
+
+    from conftest import make_locked
+    from test_docker import CID_K8S, CID_PLAIN, K8S_LABELS, FakeDocker, _container
+
+    make_locked(target, jobs=8)
+    good = json.dumps([_container(CID_K8S, "k8s_nb", K8S_LABELS),
+                       _container(CID_PLAIN, "b\u00f6b", {"mlgpu": "mlgpu", "emoji": "\U0001F600"})]).encode()
+    rng = random.Random(7)
+    served = []
+
+    def mutate():
+        b = bytearray(good)
+        for _ in range(rng.randint(0, 6)):
+            op, i = rng.randrange(3), rng.randrange(len(b))
+            if op == 0:
+                b[i] = rng.randrange(256)
+            elif op == 1:
+                del b[i:i + rng.randint(1, 40)]
+            else:
+                b[i:i] = b[i:i + rng.randint(1, 40)]
+        served.append(len(b))
+        return bytes(b)
+
+    sock = f"/tmp/gpumon-docker-san-{target}-{os.getpid()}.sock"
+    with FakeDocker(sock, mutate):
+        rc, err = _run(os.path.join(ROOT, binary), dict(env, GPUMON_METADATA_REFRESH="0.5"), ("--docker", sock),
+                       min_s=4.0)
+    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
+           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    assert not bad, err[-4000:]
+    assert rc == 0, err[-2000:]
+    assert len(served) >= 4, served
