@@ -227,3 +227,26 @@ def test_ondevice_overlay_patches_apply_to_the_base_daemonset():
     assert all(m["name"] in vols for m in c["volumeMounts"])
     assert any(m["mountPath"] == "/tmp" for m in c["volumeMounts"]) and c["securityContext"]["readOnlyRootFilesystem"]
     assert c["resources"]["limits"]["memory"] == "5120Mi"
+
+
+def test_docker_overlay_mounts_the_socket_and_sets_docker_socket():
+    """Plain-Docker nodes (the reference's runtime, gpu_monitor.yaml:24-28): the opt-in overlay
+    mounts the Docker socket where its config points the native Docker poller, and the base stays
+    without it."""
+    from gpumon.config import Config
+
+    (k,) = _docs("deploy/k8s/overlays/docker/kustomization.yaml")
+    assert k["resources"] == ["../../"]
+    cfg_patch = next(p for p in k["patches"] if p["target"]["kind"] == "ConfigMap")
+    c = Config().apply_dict(yaml.safe_load(yaml.safe_load(cfg_patch["patch"])[0]["value"])["gpumon"])
+    assert c.docker_socket == "/var/run/docker.sock" and c.control_plane == "native"
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"])
+    pod = _json_patch(ds, ops)["spec"]["template"]["spec"]
+    vols = {v["name"]: v for v in pod["volumes"]}
+    mounts = {m["mountPath"]: m for m in pod["containers"][0]["volumeMounts"]}
+    assert all(m["name"] in vols for m in mounts.values())
+    m = mounts[c.docker_socket]
+    assert m["readOnly"] and vols[m["name"]]["hostPath"] == {"path": "/var/run/docker.sock", "type": "Socket"}
+    base = ds["spec"]["template"]["spec"]["containers"][0]["volumeMounts"]
+    assert all("docker" not in x["mountPath"] for x in base)
