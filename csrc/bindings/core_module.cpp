@@ -471,13 +471,13 @@ PYBIND11_MODULE(_core, m) {
       py::arg("json"), "parse a Docker Engine GET /containers/json body (docker_lite.cpp)");
   m.def(
       "http1_parse_response",
-      [](py::bytes raw) {
+      [](py::bytes raw, bool eof) {
         int status = -1;
         std::string body, err;
-        if (!http1_parse_response(std::string(raw), &status, &body, &err)) throw py::value_error(err);
+        if (!http1_parse_response(std::string(raw), &status, &body, &err, eof)) throw py::value_error(err);
         return py::make_tuple(status, py::bytes(body));
       },
-      py::arg("raw"));
+      py::arg("raw"), py::arg("eof") = true);
   m.def(
       "docker_list",
       [docker_rows](const std::string& sock, int timeout_ms) {

@@ -317,7 +317,7 @@ bool docker_parse_containers(const std::string& json, std::vector<DockerContaine
   }
 }
 
-bool http1_parse_response(const std::string& raw, int* status, std::string* body, std::string* err) {
+bool http1_parse_response(const std::string& raw, int* status, std::string* body, std::string* err, bool eof) {
   const size_t hdr_end = raw.find("\r\n\r\n");
   if (hdr_end == std::string::npos) {
     *err = "truncated HTTP response header";
@@ -390,7 +390,11 @@ bool http1_parse_response(const std::string& raw, int* status, std::string* body
     body->assign(raw, b, static_cast<size_t>(content_length));
     return true;
   }
-  body->assign(raw, b, std::string::npos);  // delimited by connection close
+  if (!eof) {
+    *err = "body delimited by connection close: incomplete until EOF";
+    return false;
+  }
+  body->assign(raw, b, std::string::npos);
   return true;
 }
 
@@ -457,7 +461,9 @@ bool docker_list(const std::string& socket_path, std::vector<DockerContainer>* o
       return false;
     }
   }
-  std::string raw;
+  std::string raw, body;
+  int st = -1;
+  bool framed = false;  // a complete Content-Length / chunked response arrived before EOF
   char buf[65536];
   for (;;) {
     const ssize_t r = ::recv(fd, buf, sizeof buf, 0);
@@ -466,6 +472,12 @@ bool docker_list(const std::string& socket_path, std::vector<DockerContainer>* o
       if (raw.size() > kMaxResponse) {
         *err = "response too large";
         return false;
+      }
+      // a daemon that keeps the connection open despite HTTP/1.0 still ends the read here
+      std::string e;
+      if (raw.find("\r\n\r\n") != std::string::npos && http1_parse_response(raw, &st, &body, &e, false)) {
+        framed = true;
+        break;
       }
       continue;
     }
@@ -481,9 +493,7 @@ bool docker_list(const std::string& socket_path, std::vector<DockerContainer>* o
     *err = std::string("read: ") + strerror(errno);
     return false;
   }
-  std::string body;
-  int st = -1;
-  if (!http1_parse_response(raw, &st, &body, err)) return false;
+  if (!framed && !http1_parse_response(raw, &st, &body, err, true)) return false;
   status = st;
   if (st != 200) {
     *err = "GET /containers/json: HTTP " + std::to_string(st) + (body.empty() ? "" : ": " + body.substr(0, 200));

@@ -30,8 +30,10 @@ struct DockerContainer {
 bool docker_parse_containers(const std::string& json, std::vector<DockerContainer>* out, std::string* err);
 
 // Splits a raw HTTP/1.x response (status line, headers, body delimited by Content-Length,
-// chunked transfer coding, or connection close) into status + body.
-bool http1_parse_response(const std::string& raw, int* status, std::string* body, std::string* err);
+// chunked transfer coding, or connection close) into status + body. `eof`: the peer has closed
+// the connection; without it a close-delimited body is reported incomplete (false).
+bool http1_parse_response(const std::string& raw, int* status, std::string* body, std::string* err,
+                          bool eof = true);
 
 // GET /containers/json on `socket_path` (optionally "unix://"-prefixed). *http_status receives the
 // HTTP status (-1: transport failure).

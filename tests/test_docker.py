@@ -94,6 +94,9 @@ def test_http1_response_framing(core):
     ch = b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n5\r\n[{\"Id\r\n9\r\n\": \"ab\"}]\r\n0\r\n\r\n"
     assert core.http1_parse_response(ch) == (200, body)
     assert core.http1_parse_response(b"HTTP/1.0 404 Not Found\r\n\r\nnope") == (404, b"nope")
+    assert core.http1_parse_response(cl, eof=False) == (200, body)  # framed: complete before EOF
+    with pytest.raises(ValueError, match="incomplete"):  # close-delimited: only complete at EOF
+        core.http1_parse_response(b"HTTP/1.0 200 OK\r\n\r\n[]", eof=False)
     for bad in (b"HTTP/1.1 200 OK\r\n", b"garbage\r\n\r\n", b"HTTP/1.1 200 OK\r\nContent-Length: 99\r\n\r\nshort",
                 b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n"):
         with pytest.raises(ValueError):
@@ -104,11 +107,14 @@ class FakeDocker:
     """Docker Engine API subset on a unix socket: GET /containers/json (others 404). `containers`
     is a listing, or a callable returning the raw body of each response."""
 
-    def __init__(self, path, containers, status=200, chunked=False):
+    def __init__(self, path, containers, status=200, chunked=False, keep_open=False):
         self.path, self.containers, self.status, self.chunked, self.requests = path, containers, status, chunked, []
         outer = self
 
         class H(BaseHTTPRequestHandler):
+            # keep_open: an HTTP/1.1 handler that keeps the connection after answering, even to 1.0
+            protocol_version = "HTTP/1.1" if keep_open else "HTTP/1.0"
+
             def do_GET(self):  # noqa: N802
                 outer.requests.append((self.command, self.path, self.request_version))
                 if self.path != "/containers/json":
@@ -160,11 +166,15 @@ def _sock(tag):
     return f"/tmp/gpumon-docker-{tag}-{os.getpid()}.sock"
 
 
-@pytest.mark.parametrize("chunked", [False, True])
-def test_native_docker_list(core, chunked):
+@pytest.mark.parametrize("chunked,keep_open", [(False, False), (True, False), (False, True), (True, True)])
+def test_native_docker_list(core, chunked, keep_open):
+    import time
+
     cs = [_container(CID_K8S, "k8s_nb", K8S_LABELS), _container(CID_PLAIN, "bench", {"mlgpu": "mlgpu"})]
-    with FakeDocker(_sock(f"l{int(chunked)}"), cs, chunked=chunked) as d:
-        got = core.docker_list(d.path)
+    with FakeDocker(_sock(f"l{int(chunked)}{int(keep_open)}"), cs, chunked=chunked, keep_open=keep_open) as d:
+        t0 = time.monotonic()
+        got = core.docker_list(d.path, timeout_ms=3000)
+        assert time.monotonic() - t0 < 1.0  # a framed response ends the read, not the timeout
     assert [(c["id"], c["name"]) for c in got] == [(CID_K8S, "k8s_nb"), (CID_PLAIN, "bench")]
     assert d.requests == [("GET", "/containers/json", "HTTP/1.0")]  # the one read-only request
 
