@@ -98,19 +98,22 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
             time.sleep(0.2)
             mon.tick()
             text = mon.metrics()
-        for name, series, sock, lost in (
+        for name, series, sock, lost, status in (
                 ("kubelet PodResources", "gpumon_podresources", cfg.pod_resources_socket,
-                 "no idle-allocation rows, no allocated / in-use GPU counts"),
+                 "no idle-allocation rows, no allocated / in-use GPU counts", "grpc_status"),
                 ("CRI runtime", "gpumon_cri", cfg.cri_socket or "(autodetect)",
-                 "pod names from /proc fallbacks only (HOSTNAME, service-account namespace)")):
+                 "pod names from /proc fallbacks only (HOSTNAME, service-account namespace)", "grpc_status"),
+                ("Docker Engine", "gpumon_docker", cfg.docker_socket or "(off: docker_socket not set)",
+                 "container names / labels from CRI or /proc fallbacks only", "http_status")):
             up = _gauge(text, f"{series}_up")
-            code = _gauge(text, f"{series}_grpc_status")
+            code = _gauge(text, f"{series}_{status}")
             if up is None:
                 out.append((name, SKIP, f"{sock}: not polled (control plane off or no socket)"))
             elif up >= 1:
                 out.append((name, OK, f"{sock}: answering"))
             else:
-                out.append((name, WARN, f"{sock}: down (grpc-status {code if code is not None else '-'}): {lost}"))
+                code_s = "-" if code is None else int(code)
+                out.append((name, WARN, f"{sock}: down ({status.replace('_', '-')} {code_s}): {lost}"))
         out.append(("rt_priority",) + _rt_permitted())
         # on-device samplers: the helper and plugins must exist; --ondevice-check runs them once
         from ._native import core as _core

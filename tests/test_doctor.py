@@ -70,3 +70,22 @@ def test_doctor_runs_the_ondevice_samplers_once():
     assert checks["PMC device counting"][0] == "ok", checks
     assert checks["K1 probe"][0] == "ok", checks
     assert checks["on-device helper memory"][0] == "ok"
+
+
+def test_doctor_checks_the_docker_socket_when_configured():
+    from test_docker import CID_PLAIN, FakeDocker, _container
+
+    sock = f"/tmp/gpumon-doc3-{os.getpid()}.sock"
+    with FakeDocker(sock, [_container(CID_PLAIN, "bench", {})]):
+        cfg = Config(backend="mock:gpus=1", control_plane="native", pod_resources_socket="", cri_socket="",
+                     docker_socket=sock, log_level="error")
+        s, detail = _by_name(doctor.run(cfg, wait_s=1))["Docker Engine"]
+    assert s == "ok" and sock in detail
+    with FakeDocker(sock, [], status=403):
+        cfg = Config(backend="mock:gpus=1", control_plane="native", pod_resources_socket="", cri_socket="",
+                     docker_socket=sock, log_level="error")
+        s, detail = _by_name(doctor.run(cfg, wait_s=1))["Docker Engine"]
+    assert s == "warn" and "http-status 403" in detail
+    s, _ = _by_name(doctor.run(Config(backend="mock:gpus=1", control_plane="native", pod_resources_socket="",
+                                      cri_socket="", log_level="error"), wait_s=1))["Docker Engine"]
+    assert s == "skip"  # never autodetected
