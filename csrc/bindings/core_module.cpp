@@ -93,6 +93,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "influx_schema", &c.influx_schema);
   get(d, "influx_every", &c.influx_every);
   get(d, "influx_timeout_s", &c.influx_timeout_s);
+  get(d, "influx_token", &c.influx_token);
   get(d, "init_retry_s", &c.init_retry_s);
   get(d, "health_stale_s", &c.health_stale_s);
   get(d, "reinit_after", &c.reinit_after);
@@ -595,6 +596,17 @@ PYBIND11_MODULE(_core, m) {
       py::arg("host"), py::arg("port"), py::arg("path") = "/metrics", py::arg("n_requests") = 100,
       py::arg("duration_s") = 0.0, py::arg("concurrency") = 1, py::arg("rate_hz") = 0.0,
       py::arg("keep_alive") = true, py::arg("gzip") = false);
+  m.def("parse_url", [](const std::string& url) {
+    const Url u = parse_url(url);
+    py::dict d;
+    d["ok"] = u.ok;
+    d["host"] = u.host;
+    d["port"] = u.port;
+    d["path"] = u.path;
+    d["auth_header"] = u.auth_header;
+    return d;
+  });
+  m.def("redact_url", &redact_url);
   m.def(
       "http_request",
       [](const std::string& method, const std::string& url, const std::string& body,

@@ -998,10 +998,13 @@ bool Exporter::wait_for_seq(uint64_t want, double timeout_s) {
 void Exporter::influx_loop() {
   Url u = parse_url(cfg_.influx_url);
   if (!u.ok) {
-    GPUMON_LOG(LogLevel::kError, "influx", "unsupported INFLUXDB_URL " + cfg_.influx_url);
+    GPUMON_LOG(LogLevel::kError, "influx", "unsupported INFLUXDB_URL " + redact_url(cfg_.influx_url));
     return;
   }
   HttpClient client(cfg_.influx_timeout_s);
+  const std::string headers = "Content-Type: text/plain; charset=utf-8\r\n" +
+                              (!cfg_.influx_token.empty() ? "Authorization: Token " + cfg_.influx_token + "\r\n"
+                                                          : u.auth_header);
   while (running_) {
     std::string body;
     {
@@ -1013,7 +1016,7 @@ void Exporter::influx_loop() {
       push_q_.pop_front();
     }
     std::string err, resp;
-    int st = client.request("POST", u, body, "Content-Type: text/plain; charset=utf-8\r\n", &resp, &err);
+    int st = client.request("POST", u, body, headers, &resp, &err);
     if (st >= 200 && st < 300) {
       influx_ok_++;
     } else {

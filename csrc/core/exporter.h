@@ -69,6 +69,9 @@ struct ExporterConfig {
   int influx_schema = 2019;           // 2019 (gpu.py layout) | 2018 (img/influxdb.png pod_gpu)
   int influx_every = 1;               // ticks per push
   double influx_timeout_s = 2.0;
+  // InfluxDB 2.x / 3.x token ("Authorization: Token ..."); 1.x credentials go in the URL
+  // (user:password@host) and become Basic auth. Set it from a Secret (INFLUXDB_TOKEN).
+  std::string influx_token;
   double init_retry_s = 5.0;
   double health_stale_s = 0;          // 0 = max(3*interval, 10 s)
   int reinit_after = 5;               // consecutive all-devices-failed ticks before re-initialising

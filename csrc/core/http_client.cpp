@@ -16,23 +16,93 @@
 
 namespace gpumon {
 
+std::string base64_encode(const std::string& in) {
+  static const char* k = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  std::string out;
+  out.reserve((in.size() + 2) / 3 * 4);
+  size_t i = 0;
+  for (; i + 2 < in.size(); i += 3) {
+    const uint32_t v = (static_cast<uint8_t>(in[i]) << 16) | (static_cast<uint8_t>(in[i + 1]) << 8) |
+                       static_cast<uint8_t>(in[i + 2]);
+    out += k[v >> 18];
+    out += k[(v >> 12) & 63];
+    out += k[(v >> 6) & 63];
+    out += k[v & 63];
+  }
+  if (i < in.size()) {
+    const uint32_t v = (static_cast<uint8_t>(in[i]) << 16) |
+                       (i + 1 < in.size() ? static_cast<uint8_t>(in[i + 1]) << 8 : 0);
+    out += k[v >> 18];
+    out += k[(v >> 12) & 63];
+    out += i + 1 < in.size() ? k[(v >> 6) & 63] : '=';
+    out += '=';
+  }
+  return out;
+}
+
+namespace {
+
+std::string pct_decode(const std::string& s) {
+  std::string out;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '%' && i + 2 < s.size() && isxdigit(static_cast<unsigned char>(s[i + 1])) &&
+        isxdigit(static_cast<unsigned char>(s[i + 2]))) {
+      out += static_cast<char>(strtol(s.substr(i + 1, 2).c_str(), nullptr, 16));
+      i += 2;
+    } else {
+      out += s[i];
+    }
+  }
+  return out;
+}
+
+}  // namespace
+
 Url parse_url(const std::string& url) {
   Url u;
   std::string s = url;
   if (starts_with(s, "http://")) s = s.substr(7);
   else if (s.find("://") != std::string::npos) return u;  // https etc. unsupported
-  size_t slash = s.find('/');
+  size_t slash = s.find_first_of("/?");
   std::string hp = slash == std::string::npos ? s : s.substr(0, slash);
   u.path = slash == std::string::npos ? "/" : s.substr(slash);
-  size_t colon = hp.rfind(':');
-  if (colon != std::string::npos) {
-    u.host = hp.substr(0, colon);
-    u.port = atoi(hp.c_str() + colon + 1);
-  } else {
-    u.host = hp;
+  if (u.path[0] == '?') u.path = "/" + u.path;
+  const size_t at = hp.rfind('@');
+  if (at != std::string::npos) {
+    u.auth_header = "Authorization: Basic " + base64_encode(pct_decode(hp.substr(0, at))) + "\r\n";
+    hp = hp.substr(at + 1);
   }
-  u.ok = !u.host.empty() && u.port > 0;
+  std::string port;
+  if (!hp.empty() && hp[0] == '[') {  // [v6]:port
+    const size_t rb = hp.find(']');
+    if (rb == std::string::npos) return u;
+    u.host = hp.substr(1, rb - 1);
+    if (rb + 1 < hp.size()) {
+      if (hp[rb + 1] != ':') return u;
+      port = hp.substr(rb + 2);
+    }
+  } else {
+    const size_t colon = hp.rfind(':');
+    u.host = colon == std::string::npos ? hp : hp.substr(0, colon);
+    if (colon != std::string::npos) port = hp.substr(colon + 1);
+  }
+  if (!port.empty()) {
+    if (port.find_first_not_of("0123456789") != std::string::npos || port.size() > 5) return u;
+    u.port = atoi(port.c_str());
+  }
+  u.ok = !u.host.empty() && u.port > 0 && u.port < 65536;
   return u;
+}
+
+std::string redact_url(const std::string& url) {
+  const size_t scheme = url.find("://");
+  const size_t start = scheme == std::string::npos ? 0 : scheme + 3;
+  const size_t end = url.find_first_of("/?", start);
+  const size_t at = url.rfind('@', end == std::string::npos ? std::string::npos : end);
+  if (at == std::string::npos || at < start) return url;
+  const size_t colon = url.find(':', start);
+  if (colon == std::string::npos || colon > at) return url;  // user without a password
+  return url.substr(0, colon + 1) + "***" + url.substr(at);
 }
 
 HttpClient::~HttpClient() { close_conn(); }

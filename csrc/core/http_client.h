@@ -14,12 +14,18 @@
 namespace gpumon {
 
 struct Url {
-  std::string host;
+  std::string host;         // IPv6 literals without the brackets
   int port = 80;
   std::string path = "/";   // including ?query
+  std::string auth_header;  // "Authorization: Basic ...\r\n" from user:password@ (InfluxDB 1.x auth)
   bool ok = false;
 };
+// http://[user[:password]@]host[:port][/path?query]; host may be a [v6] literal. https and other
+// schemes are rejected (ok = false).
 Url parse_url(const std::string& url);
+// The URL with any password replaced by "***" (for logs and --print-config).
+std::string redact_url(const std::string& url);
+std::string base64_encode(const std::string& in);
 
 class HttpClient {
  public:

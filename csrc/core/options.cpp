@@ -11,6 +11,7 @@
 #include <sstream>
 
 #include "common.h"
+#include "http_client.h"
 
 namespace gpumon {
 
@@ -240,6 +241,7 @@ const std::map<std::string, Setter>& setters() {
       {"extended_families", bool_at([](NativeOptions* o) { return &o->cfg.extended_families; })},
       {"full_device_labels", bool_at([](NativeOptions* o) { return &o->cfg.full_device_labels; })},
       {"influx_url", str_at([](NativeOptions* o) { return &o->cfg.influx_url; })},
+      {"influx_token", str_at([](NativeOptions* o) { return &o->cfg.influx_token; })},
       {"influx_extended", bool_at([](NativeOptions* o) { return &o->cfg.influx_extended; })},
       {"influx_schema", int_at([](NativeOptions* o) { return &o->cfg.influx_schema; })},
       {"influx_every", int_at([](NativeOptions* o) { return &o->cfg.influx_every; })},
@@ -401,6 +403,7 @@ bool options_apply_env(NativeOptions* o, char** envp, std::string* err) {
     const std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
     if (k == "NODE_NAME" && !v.empty()) o->cfg.host = v;
     else if (k == "INFLUXDB_URL" && !v.empty()) o->cfg.influx_url = v;
+    else if (k == "INFLUXDB_TOKEN" && !v.empty()) o->cfg.influx_token = v;
   }
   for (char** p = envp; p && *p; ++p) {
     const std::string kv = *p;
@@ -508,7 +511,8 @@ std::string options_json(const NativeOptions& o) {
   B("roctx", c.roctx);
   B("compat_families", c.compat_families);
   B("extended_families", c.extended_families);
-  S("influx_url", c.influx_url);
+  S("influx_url", redact_url(c.influx_url));
+  S("influx_token", c.influx_token.empty() ? "" : "***");
   B("influx_extended", c.influx_extended);
   N("influx_schema", c.influx_schema);
   N("influx_every", c.influx_every);

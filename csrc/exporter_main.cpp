@@ -95,6 +95,7 @@ int main(int argc, char** argv) {
     else if (a == "--host") set("host", next());
     else if (a == "--devices") set("devices", next());
     else if (a == "--influx-url") set("influx_url", next());
+    else if (a == "--influx-token") set("influx_token", next());
     else if (a == "--influx-extended") set("influx_extended", "true");
     else if (a == "--influx-schema") set("influx_schema", next());
     else if (a == "--no-fast-path") set("fast_path", "false");

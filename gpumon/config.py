@@ -58,6 +58,7 @@ class Config:
     extended_families: bool = True
     # influx compat push
     influx_url: str = ""
+    influx_token: str = ""                # InfluxDB 2.x/3.x API token (env INFLUXDB_TOKEN, from a Secret); 1.x: user:password@ in the URL
     influx_extended: bool = False
     influx_schema: int = 2019             # 2019 = gpu.py layout; 2018 = img/influxdb.png pod_gpu layout
     influx_every: int = 1
@@ -151,6 +152,7 @@ class Config:
             "compat_families": self.compat_families,
             "extended_families": self.extended_families,
             "influx_url": self.influx_url,
+            "influx_token": self.influx_token,
             "influx_extended": self.influx_extended,
             "influx_schema": int(self.influx_schema),
             "influx_every": int(self.influx_every),
@@ -184,6 +186,8 @@ class Config:
             self.host = env["NODE_NAME"]
         if env.get("INFLUXDB_URL"):
             self.influx_url = env["INFLUXDB_URL"]
+        if env.get("INFLUXDB_TOKEN"):
+            self.influx_token = env["INFLUXDB_TOKEN"]
         names = {f.name: f for f in dataclasses.fields(self)}
         for k, v in env.items():
             if k.startswith("GPUMON_") and k != "GPUMON_CONFIG" and k != "GPUMON_AMDSMI_LIB":

@@ -3,6 +3,8 @@ compat push (reference: one requests.post per line, gpu.py:145,218,252; here one
 tick over keep-alive, received by a local HTTP sink)."""
 
 import argparse
+import base64
+import os
 import http.server
 import threading
 import time
@@ -125,3 +127,73 @@ def test_influx_unreachable_does_not_block_sampling(core):
         ex.stop()
     assert st["ticks"] >= 10  # sampler kept its cadence
     assert st["influx_fail"] + st["influx_dropped"] >= 1
+
+
+def test_url_parsing_auth_and_v6(core):
+    u = core.parse_url("http://influx:8086/write?db=k8s")
+    assert (u["ok"], u["host"], u["port"], u["path"], u["auth_header"]) == (True, "influx", 8086, "/write?db=k8s", "")
+    u = core.parse_url("http://gpumon:p%40ss:w@influx.monitoring:8086/write?db=k8s")
+    assert u["host"] == "influx.monitoring" and u["path"] == "/write?db=k8s"
+    assert u["auth_header"] == "Authorization: Basic " + base64.b64encode(b"gpumon:p@ss:w").decode() + "\r\n"
+    u = core.parse_url("http://[fd00::1]:8086/api/v2/write?org=o&bucket=b")
+    assert (u["ok"], u["host"], u["port"], u["path"]) == (True, "fd00::1", 8086, "/api/v2/write?org=o&bucket=b")
+    assert core.parse_url("http://influx?db=x")["path"] == "/?db=x" and core.parse_url("http://influx")["port"] == 80
+    for bad in ("https://influx:8086/write", "http://:8086/", "http://influx:99999/", "http://influx:80x/",
+                "http://[fd00::1/", "http://[fd00::1]x/"):
+        assert not core.parse_url(bad)["ok"], bad
+    for b in ("", "f", "fo", "foo", "foob", "fooba", "u:\u00e9\u00fc"):  # padding cases, non-ASCII
+        h = core.parse_url(f"http://{b}@h/")["auth_header"]
+        assert h == "Authorization: Basic " + base64.b64encode(b.encode()).decode() + "\r\n", b
+    assert core.redact_url("http://u:secret@h:1/write?db=x") == "http://u:***@h:1/write?db=x"
+    assert core.redact_url("http://u@h/write") == "http://u@h/write"
+    assert core.redact_url("http://h/write?u=a@b") == "http://h/write?u=a@b"
+
+
+class _AuthSink(_Sink):
+    auth = []
+
+    def do_POST(self):  # noqa: N802
+        _AuthSink.auth.append(self.headers.get("Authorization"))
+        super().do_POST()
+
+
+@pytest.mark.parametrize("mode", ["basic", "token"])
+def test_influx_push_authenticates(core, mode):
+    """InfluxDB with auth on: 1.x credentials from the URL as Basic auth, 2.x/3.x API token from
+    influx_token (env INFLUXDB_TOKEN). The reference posted without credentials (gpu.py:145)."""
+    _AuthSink.auth, _Sink.bodies = [], []
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _AuthSink)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    port = srv.server_address[1]
+    cfg = {"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0.05, "host": "n"}
+    if mode == "basic":
+        cfg["influx_url"] = f"http://gpumon:s3cret@127.0.0.1:{port}/write?db=k8s"
+        want = "Basic " + base64.b64encode(b"gpumon:s3cret").decode()
+    else:
+        cfg.update(influx_url=f"http://127.0.0.1:{port}/api/v2/write?org=o&bucket=gpu", influx_token="tok-123")
+        want = "Token tok-123"
+    ex = core.Exporter(cfg)
+    ex.start()
+    try:
+        deadline = time.time() + 5
+        while time.time() < deadline and len(_AuthSink.auth) < 2:
+            time.sleep(0.02)
+    finally:
+        ex.stop()
+        srv.shutdown()
+    assert _AuthSink.auth[:2] == [want, want]
+
+
+def test_influx_credentials_never_printed(tmp_path):
+    import json
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, INFLUXDB_URL="http://u:pw123@influx:8086/write?db=k8s", INFLUXDB_TOKEN="tok-456")
+    r = subprocess.run([os.path.join(root, "bin/gpumon-exporter"), "--print-config"], capture_output=True,
+                       text=True, timeout=30, env=env, check=True)
+    assert "pw123" not in r.stdout and "tok-456" not in r.stdout
+    d = json.loads(r.stdout)
+    assert d["influx_url"] == "http://u:***@influx:8086/write?db=k8s" and d["influx_token"] == "***"
+    c = Config().apply_env({"INFLUXDB_TOKEN": "tok-456"})
+    assert c.influx_token == "tok-456" and c.to_core()["influx_token"] == "tok-456"
