@@ -1,0 +1,28 @@
+"""The exporter's PMC-derived throughput against a real PyTorch workload on the MI355X
+(tools/torch_workload_check.py): torch bf16 GEMMs and fp8 _scaled_mm (hipBLASLt kernels, not this
+repo's burns) in a tenant process, counted by the deployed exporter (bin/gpumon-exporter --pmc)
+from another process. profiles/r2_torch_workload.md: within 0.1 % on MI355X."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_exported_tflops_match_a_torch_gemm_tenant():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "torch_workload_check.py"), "--seconds", "6",
+                        "--dtypes", "bf16,fp8"], capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    runs = json.loads(r.stdout.strip().splitlines()[-1])["runs"]
+    bf16 = runs["bf16"]
+    assert bf16["tenant_tflops_event_timed"] > 800 and bf16["ticks_inside"] >= 3, runs
+    assert abs(bf16["exported_vs_tenant"] - 1.0) <= 0.05, runs
+    assert bf16["exported_mfma_util_median"] > 30, runs
+    assert bf16["exported_proc_busy_median"] > 60, runs  # KFD: the GEMM tenant's waves resident
+    if "error" not in runs["fp8"]:  # fp8 _scaled_mm needs a torch build with gfx950 fp8 GEMMs
+        assert abs(runs["fp8"]["exported_vs_tenant"] - 1.0) <= 0.05, runs
