@@ -57,6 +57,8 @@ class GpuMonitor:
             if self.cfg.resource_names:
                 core_cfg["pod_resources_prefix"] = self.cfg.resource_names[0]
             core_cfg["pod_resources_dra_drivers"] = list(self.cfg.dra_drivers)
+        if self.cfg.docker_socket and mode != "native":
+            log.warning("docker_socket is read by the native control plane only; control_plane=%s ignores it", mode)
         self.control_plane_mode = mode
         self.ex = self._core.Exporter(core_cfg)
         self.plane = None
