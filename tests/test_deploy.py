@@ -118,6 +118,31 @@ def test_dockerfile_entrypoint():
     assert "COPY --from=build /src/lib /opt/gpumon/lib" in txt and "GPUMON_PLUGIN_DIR=/opt/gpumon/lib" in txt
 
 
+def _control_plane_metric_names():
+    """Series of the native metadata pollers, from an exporter pointed at the fake kubelet (CRI +
+    PodResources) and a fake Docker daemon."""
+    from gpumon import core
+    from gpumon.attribution.fake_kubelet import FakeKubelet
+    from test_docker import FakeDocker
+
+    d = f"/tmp/gpumon-alerts-{os.getpid()}"
+    os.makedirs(d, exist_ok=True)
+    with FakeKubelet(podres_socket=f"{d}/kubelet.sock", cri_socket=f"{d}/cri.sock") as k, \
+            FakeDocker(f"{d}/docker.sock", []) as dk:
+        ex = core().Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0,
+                              "cri_socket": k.cri_socket, "pod_resources_socket": k.podres_socket,
+                              "docker_socket": dk.path})
+        ex.start()
+        try:
+            ex.tick()
+            fam = promtext.parse(ex.metrics_text())
+        finally:
+            ex.stop()
+    names = {n for n in fam if n.startswith(("gpumon_cri", "gpumon_podresources", "gpumon_docker"))}
+    assert {"gpumon_cri_up", "gpumon_podresources_up", "gpumon_docker_up"} <= names, names
+    return names
+
+
 def test_alert_and_recording_rules_resolve(mock_exporter):
     """Every series a PrometheusRule expression uses is produced by the exporter, and the label
     values the alerts match on (sensor, kind, state) exist in a scrape."""
@@ -134,6 +159,7 @@ def test_alert_and_recording_rules_resolve(mock_exporter):
     fam = promtext.parse(ex.metrics_text())
     produced = {n for f, v in fam.items() for n in [f] + [s[0] for s in v["samples"]]}
     produced |= _plugin_metric_names()  # the on-device samplers' series (PMC, probe, helper)
+    produced |= _control_plane_metric_names()  # CRI / PodResources / Docker pollers
     words = {"sum", "by", "count", "rate", "increase", "delta", "avg", "max", "time", "host", "namespace", "podname",
              "gpu_id", "user_name"}
     exprs = [r["expr"] for g in rule["spec"]["groups"] for r in g["rules"]]
