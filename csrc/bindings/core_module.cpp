@@ -86,6 +86,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "ras_async", &c.ras_async);
   get(d, "occ_samples", &c.occ_samples);
   get(d, "hide_empty_contexts", &c.hide_empty_contexts);
+  get(d, "mfma_exclusive_window_s", &c.mfma_exclusive_window_s);
   get(d, "sample_threads", &c.sample_threads);
   get(d, "rt_priority", &c.rt_priority);
   get(d, "influx_url", &c.influx_url);

@@ -651,13 +651,26 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
     std::lock_guard<std::mutex> g(extra_mu_);
     mfma = mfma_util_;
   }
+  // A process whose waves showed up in none of this tick's reads may still share the device (a
+  // 10 %-resident tenant escapes 10 reads a third of the time): the device counts as exclusive only
+  // when no other pid was seen within the last 5 ticks and mfma_exclusive_window_s.
   std::vector<uint32_t> sole(procs.size(), 0);
+  const uint64_t tick_no = ++pod_rows_built_;
+  const int64_t now_ns = mono_ns();
+  const int64_t window_ns = static_cast<int64_t>(std::max(0.0, cfg_.mfma_exclusive_window_s) * 1e9);
+  if (last_active_.size() < procs.size()) last_active_.resize(procs.size());
   for (size_t d = 0; d < procs.size(); ++d) {
+    auto& seen = last_active_[d];
     std::vector<uint32_t> active;  // distinct pids (one process may hold several KFD contexts)
     for (const auto& p : procs[d])
       if ((p.occ_busy > 0 || p.cu_occupancy > 0) && std::find(active.begin(), active.end(), p.pid) == active.end())
         active.push_back(p.pid);
-    if (active.size() == 1) sole[d] = active[0];
+    for (uint32_t pid : active) seen[pid] = {tick_no, now_ns};
+    for (auto it = seen.begin(); it != seen.end();) {  // forget pids past both windows
+      if (tick_no - it->second.first >= 5 && now_ns - it->second.second >= window_ns) it = seen.erase(it);
+      else ++it;
+    }
+    if (active.size() == 1 && seen.size() == 1) sole[d] = active[0];
   }
   uint64_t hidden = 0;
   std::vector<uint32_t> alive;

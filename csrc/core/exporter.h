@@ -62,6 +62,10 @@ struct ExporterConfig {
   int rt_priority = 0;
   int occ_samples = 10;               // KFD cu_occupancy reads per process per tick on the device workers (1 = the tick's own)
   bool hide_empty_contexts = true;    // no pod_gpu row for a process with a GPU context but no VRAM and no waves
+  // pod_gpu_mfma_util_percent needs exclusive use: no OTHER process's waves seen on the device in
+  // the last 5 ticks nor in the last mfma_exclusive_window_s seconds (a tenant resident 10 % of the
+  // time escapes one tick's 10 occupancy reads a third of the time; profiles/r2_torch_workload.md)
+  double mfma_exclusive_window_s = 5.0;
   AttributionConfig attribution;
   RateConfig rates;
   std::string influx_url;             // INFLUXDB_URL; empty = push disabled
@@ -235,6 +239,9 @@ class Exporter {
   std::mutex podres_mu_;
   std::condition_variable podres_cv_;
   std::unordered_map<std::string, ContainerMeta> native_meta_;  // "ns/pod/container" (guarded by podres_mu_)
+  // per device: pid -> (tick, mono ns) its waves were last seen resident (sampler thread only)
+  std::vector<std::unordered_map<uint32_t, std::pair<uint64_t, int64_t>>> last_active_;
+  uint64_t pod_rows_built_ = 0;
   std::mutex meta_mu_;
   std::vector<ContainerMeta> cri_metas_, docker_metas_;  // last successful listing of each (meta_mu_)
   std::mutex push_mu_;

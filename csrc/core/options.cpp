@@ -226,6 +226,7 @@ const std::map<std::string, Setter>& setters() {
       {"ras_async", bool_at([](NativeOptions* o) { return &o->cfg.ras_async; })},
       {"occ_samples", int_at([](NativeOptions* o) { return &o->cfg.occ_samples; })},
       {"hide_empty_contexts", bool_at([](NativeOptions* o) { return &o->cfg.hide_empty_contexts; })},
+      {"mfma_exclusive_window_s", dbl_at([](NativeOptions* o) { return &o->cfg.mfma_exclusive_window_s; })},
       {"sample_threads", int_at([](NativeOptions* o) { return &o->cfg.sample_threads; })},
       {"rt_priority", int_at([](NativeOptions* o) { return &o->cfg.rt_priority; })},
       {"device_timeout_s", dbl_at([](NativeOptions* o) { return &o->cfg.device_timeout_s; })},
@@ -498,6 +499,7 @@ std::string options_json(const NativeOptions& o) {
   B("ras_async", c.ras_async);
   N("occ_samples", c.occ_samples);
   B("hide_empty_contexts", c.hide_empty_contexts);
+  N("mfma_exclusive_window_s", c.mfma_exclusive_window_s);
   N("sample_threads", c.sample_threads);
   N("rt_priority", c.rt_priority);
   N("device_timeout_s", c.device_timeout_s);

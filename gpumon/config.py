@@ -42,6 +42,7 @@ class Config:
     ras_slices: int = 1                   # the pass read in this many slices on consecutive ticks (1..ras_every)
     ras_async: bool = True                # device workers read RAS after publishing a tick (next tick carries it)
     hide_empty_contexts: bool = True      # no pod_gpu row for a GPU context with no VRAM and no waves
+    mfma_exclusive_window_s: float = 5.0  # pod MFMA util only when no other process had waves in the last 5 ticks and this many seconds
     occ_samples: int = 10                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
     rt_priority: int = 0                  # SCHED_FIFO priority of the sampler + device workers (needs CAP_SYS_NICE)
@@ -137,6 +138,7 @@ class Config:
             "ras_async": bool(self.ras_async),
             "occ_samples": int(self.occ_samples),
             "hide_empty_contexts": bool(self.hide_empty_contexts),
+            "mfma_exclusive_window_s": float(self.mfma_exclusive_window_s),
             "sample_threads": int(self.sample_threads),
             "rt_priority": int(self.rt_priority),
             "device_timeout_s": float(self.device_timeout_s),

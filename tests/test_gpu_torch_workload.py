@@ -26,3 +26,18 @@ def test_exported_tflops_match_a_torch_gemm_tenant():
     assert bf16["exported_proc_busy_median"] > 60, runs  # KFD: the GEMM tenant's waves resident
     if "error" not in runs["fp8"]:  # fp8 _scaled_mm needs a torch build with gfx950 fp8 GEMMs
         assert abs(runs["fp8"]["exported_vs_tenant"] - 1.0) <= 0.05, runs
+
+
+def test_shared_gpu_two_torch_tenants():
+    """Two bf16 GEMM tenants on one GPU at once (the reference dashboard's "(共享)" shared column):
+    the exported device TFLOP/s equals the sum of both tenants' FLOPs over wall time, each tenant
+    gets its own busy share, and no pod row claims the device's MFMA utilisation."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "torch_workload_check.py"), "--shared",
+                        "--seconds", "10"], capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    s = json.loads(r.stdout.strip().splitlines()[-1])["shared"]
+    assert "error" not in s and s["ticks_inside"] >= 4, s
+    assert abs(s["exported_vs_sum"] - 1.0) <= 0.05, s
+    big, small = s["rows_median"]
+    assert big["busy"] > small["busy"] > 0 and big["busy"] + small["busy"] <= 110, s
+    assert s["pod_mfma_util_rows_max"] == 0, s

@@ -108,7 +108,32 @@ def test_mfma_util_attributed_to_the_sole_active_process(mock_exporter):
     ex.mock_set_occ_series(0, [200.0, 50.0])  # both active: shared GPU
     ex.tick()
     assert not promtext.values(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent")
+    ex.mock_set_occ_series(0, [200.0, 0.0])  # pid 8 missed by one tick's reads: still shared
+    ex.tick()
+    assert not promtext.values(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent")
     ex.set_device_mfma_util({})  # PMC off / withdrawn
     ex.mock_set_occ_series(0, [200.0, 0.0])
     ex.tick()
     assert not promtext.values(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent")
+
+
+def test_mfma_util_exclusive_again_after_the_window(mock_exporter):
+    """A device stays shared for 5 ticks and mfma_exclusive_window_s after the second process's
+    waves were last seen (an intermittent tenant is not missed by one tick's reads), then the
+    remaining process's row carries the device's MFMA utilisation again."""
+    import time
+
+    procs = [{"pid": 7, "device": 0, "name": "train", "kfd_only": True},
+             {"pid": 8, "device": 0, "name": "bursty", "kfd_only": True}]
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0, mock={"procs": procs},
+                       mfma_exclusive_window_s=0.3)
+    ex.set_device_mfma_util({0: 42.5})
+    ex.mock_set_occ_series(0, [200.0, 50.0])
+    ex.tick()
+    ex.mock_set_occ_series(0, [200.0, 0.0])
+    for _ in range(5):  # within 5 ticks: shared
+        ex.tick()
+        assert not promtext.values(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent")
+    time.sleep(0.35)  # past the time window too
+    ex.tick()
+    assert promtext.one(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent", pid="7") == 42.5

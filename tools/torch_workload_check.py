@@ -9,6 +9,12 @@ The reference had no compute-side signal at all: device util copied onto every p
 (/root/reference/gpu.py:205).
 
     python tools/torch_workload_check.py [--seconds 8] [--dtypes bf16,f16,fp8] > out.json
+    python tools/torch_workload_check.py --shared [--seconds 10] > out.json
+
+--shared: two bf16 GEMM tenants (8192^3 and 4096^3) on the same GPU at once, the reference
+dashboard's "(共享)" shared-GPU case. The exported device TFLOP/s must equal the sum of the two
+tenants' FLOPs over wall time; each tenant gets its own row (busy %, CU-equivalents), and
+pod_gpu_mfma_util_percent is absent (the device's MFMA util is not one pod's when shared).
 """
 
 import argparse
@@ -54,7 +60,7 @@ while time.time() - t0 < seconds:
     flops += 2.0 * n ** 3 * batch
     batches += 1
 t1 = time.time()
-print(json.dumps({"dtype": dtype, "n": n, "t0": t0, "t1": t1, "batches": batches,
+print(json.dumps({"dtype": dtype, "n": n, "t0": t0, "t1": t1, "batches": batches, "flops": flops,
                   "tflops": flops / (busy_ms * 1e-3) / 1e12, "busy": busy_ms * 1e-3 / (t1 - t0)}), flush=True)
 """
 
@@ -65,6 +71,47 @@ def _port():
         return s.getsockname()[1]
 
 
+def _shared(port, seconds):
+    from gpumon.export import promtext
+
+    sizes = (8192, 4096)
+    ts = [subprocess.Popen([sys.executable, "-c", TENANT, "bf16", str(seconds), str(n)], stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, text=True) for n in sizes]
+    ticks = []
+    deadline = time.time() + seconds + 60
+    while any(t.poll() is None for t in ts) and time.time() < deadline:
+        fam = promtext.parse(urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode())
+        busy = {l["pid"]: v for _, l, v in fam.get("pod_gpu_proc_gfx_util", {}).get("samples", [])}
+        cu = {l["pid"]: v for _, l, v in fam.get("pod_gpu_proc_cu_occupancy", {}).get("samples", [])}
+        mem = {l["pid"]: v for _, l, v in fam.get("pod_gpu_used_memory", {}).get("samples", [])}
+        ticks.append({"t": time.time(),
+                      "tflops": (promtext.values(fam, "gpu_mfma_tflops", gpu_id="0", dtype="bf16") or [None])[0],
+                      "pod_mfma_util_rows": len(promtext.values(fam, "pod_gpu_mfma_util_percent", gpu_id="0")),
+                      "rows": sorted(({"busy": busy.get(p), "cu": cu.get(p), "mib": mem.get(p)} for p in busy),
+                                     key=lambda r: -(r["mib"] or 0))})
+        time.sleep(1.0)
+    res = []
+    for t in ts:
+        so, se = t.communicate(timeout=120)
+        if t.returncode != 0:
+            return {"error": se.strip().splitlines()[-1] if se.strip() else f"rc {t.returncode}"}
+        res.append(json.loads(so.strip().splitlines()[-1]))
+    t0, t1 = max(r["t0"] for r in res) + 2.0, min(r["t1"] for r in res)
+    inside = [k for k in ticks if t0 <= k["t"] <= t1]
+    wall = [r["flops"] / (r["t1"] - r["t0"]) / 1e12 for r in res]
+    tf = [k["tflops"] for k in inside if k["tflops"] is not None]
+    rows = [k["rows"] for k in inside if len(k["rows"]) >= 2]
+    return {"tenants": [{"n": r["n"], "wall_tflops": round(w, 1), "busy": round(r["busy"], 3)}
+                        for r, w in zip(res, wall)],
+            "tenants_sum_wall_tflops": round(sum(wall), 1), "ticks_inside": len(inside),
+            "exported_tflops_median": round(statistics.median(tf), 1) if tf else None,
+            "exported_vs_sum": round(statistics.median(tf) / sum(wall), 4) if tf else None,
+            "rows_median": [{"busy": statistics.median([r[i]["busy"] for r in rows if r[i]["busy"] is not None] or [0]),
+                             "cu": round(statistics.median([r[i]["cu"] for r in rows if r[i]["cu"] is not None] or [0]), 1)}
+                            for i in range(2)] if rows else None,
+            "pod_mfma_util_rows_max": max((k["pod_mfma_util_rows"] for k in inside), default=None)}
+
+
 def main() -> int:
     from gpumon.export import promtext
 
@@ -72,6 +119,7 @@ def main() -> int:
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--dtypes", default="bf16,f16,fp8")
     ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--shared", action="store_true", help="two concurrent bf16 tenants on one GPU")
     args = ap.parse_args()
 
     port = _port()
@@ -83,7 +131,10 @@ def main() -> int:
         time.sleep(3)
         if ex.poll() is not None:
             raise SystemExit("exporter exited: " + ex.stderr.read()[-2000:])
-        for dtype in args.dtypes.split(","):
+        if args.shared:
+            out["shared"] = _shared(port, args.seconds)
+            print("shared", out["shared"], file=sys.stderr)
+        for dtype in ([] if args.shared else args.dtypes.split(",")):
             tenant = subprocess.Popen([sys.executable, "-c", TENANT, dtype, str(args.seconds), str(args.n)],
                                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
             ticks = []
