@@ -519,8 +519,9 @@ void render_prometheus(const RenderInput& in, std::string* o) {
     {
       Family f(o, "pod_gpu_mfma_util_percent",
                "Wall-time MFMA (matrix core) utilisation of the GPU while this process was the only one with "
-               "waves resident in the interval (exclusive use): the device's gpu_mfma_util_percent. Absent when "
-               "the GPU was shared or PMC counting is off.",
+               "waves resident (exclusive use: no other process's waves in the last 5 ticks and "
+               "mfma_exclusive_window_s): the device's gpu_mfma_util_percent. Absent when the GPU was shared or "
+               "PMC counting is off.",
                "gauge");
       for (size_t r = 0; r < rows.size(); ++r)
         if (has(rows[r].mfma_util)) f.add(rl[r], rows[r].mfma_util);
