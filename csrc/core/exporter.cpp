@@ -659,6 +659,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
   const int64_t now_ns = mono_ns();
   const int64_t window_ns = static_cast<int64_t>(std::max(0.0, cfg_.mfma_exclusive_window_s) * 1e9);
   if (last_active_.size() < procs.size()) last_active_.resize(procs.size());
+  std::vector<ExtraSeries> sharing;
   for (size_t d = 0; d < procs.size(); ++d) {
     auto& seen = last_active_[d];
     std::vector<uint32_t> active;  // distinct pids (one process may hold several KFD contexts)
@@ -671,7 +672,17 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       else ++it;
     }
     if (active.size() == 1 && seen.size() == 1) sole[d] = active[0];
+    // the sharing state itself (the reference dashboard's "shared" / "exclusive" columns): only
+    // where residency is observable (a process with occupancy reads, or no process at all)
+    const bool observable = procs[d].empty() || std::any_of(procs[d].begin(), procs[d].end(),
+                                                            [](const ProcSample& p) { return p.occ_samples > 0; });
+    if (observable)
+      sharing.push_back({"gpu_active_processes",
+                         "Distinct processes whose waves were resident on the GPU within the exclusivity window (5 "
+                         "ticks and mfma_exclusive_window_s; KFD occupancy reads): 0 idle, 1 exclusive, >1 shared.",
+                         "gauge", static_cast<int>(d), {}, static_cast<double>(seen.size())});
   }
+  set_extra("sharing", std::move(sharing));
   uint64_t hidden = 0;
   std::vector<uint32_t> alive;
   std::unordered_map<ProcKey, ProcPrev, ProcKeyHash> next_prev;

@@ -122,6 +122,10 @@ def build():
                          (f'increase(gpumon_ondevice_helper_restarts_total{{{HOST}}}[1h])', "{{host}} helper restarts / 1h"),
                          (f'rate(gpumon_ondevice_helper_cpu_seconds_total{{{HOST}}}[5m])', "{{host}} helper CPU (cores)")],
                         12, y, 12, 8))
+    # the reference dashboard titled node columns "(共享)" shared / "(独占)" exclusive by hand
+    panels.append(panel("共享 / 独占: processes with waves resident per GPU (1 exclusive, >1 shared)", "timeseries",
+                        [(f'gpu_active_processes{{{HOST}}}', "{{host}} gpu{{gpu_id}}")], 12, y + 8, 12, 8,
+                        fieldConfig={"defaults": {"min": 0, "decimals": 0}, "overrides": []}))
     y += 16
     panels.append(panel("RAS: ECC errors by block (uncorrectable / correctable / deferred)", "table",
                         [(f'sum by (host, gpu_id, block, type) (gpu_ecc_errors_total{{{HOST}}}) > 0', "")], 0, y, 12, 8))

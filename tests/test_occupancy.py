@@ -134,6 +134,9 @@ def test_mfma_util_exclusive_again_after_the_window(mock_exporter):
     for _ in range(5):  # within 5 ticks: shared
         ex.tick()
         assert not promtext.values(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent")
+    assert promtext.one(promtext.parse(ex.metrics_text()), "gpu_active_processes", gpu_id="0") == 2  # shared
     time.sleep(0.35)  # past the time window too
     ex.tick()
-    assert promtext.one(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent", pid="7") == 42.5
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "pod_gpu_mfma_util_percent", pid="7") == 42.5
+    assert promtext.one(fam, "gpu_active_processes", gpu_id="0") == 1  # exclusive
