@@ -24,6 +24,7 @@ def test_exported_tflops_match_a_torch_gemm_tenant():
     assert abs(bf16["exported_vs_tenant"] - 1.0) <= 0.05, runs
     assert bf16["exported_mfma_util_median"] > 30, runs
     assert bf16["exported_proc_busy_median"] > 60, runs  # KFD: the GEMM tenant's waves resident
+    assert all(a == 1 for a in bf16["active_processes"]), runs  # exclusive
     if "error" not in runs["fp8"]:  # fp8 _scaled_mm needs a torch build with gfx950 fp8 GEMMs
         assert abs(runs["fp8"]["exported_vs_tenant"] - 1.0) <= 0.05, runs
 
@@ -41,3 +42,4 @@ def test_shared_gpu_two_torch_tenants():
     big, small = s["rows_median"]
     assert big["busy"] > small["busy"] > 0 and big["busy"] + small["busy"] <= 110, s
     assert s["pod_mfma_util_rows_max"] == 0, s
+    assert all(a == 2 for a in s["active_processes"]), s  # shared

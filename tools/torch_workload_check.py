@@ -87,6 +87,7 @@ def _shared(port, seconds):
         ticks.append({"t": time.time(),
                       "tflops": (promtext.values(fam, "gpu_mfma_tflops", gpu_id="0", dtype="bf16") or [None])[0],
                       "pod_mfma_util_rows": len(promtext.values(fam, "pod_gpu_mfma_util_percent", gpu_id="0")),
+                      "active": (promtext.values(fam, "gpu_active_processes", gpu_id="0") or [None])[0],
                       "rows": sorted(({"busy": busy.get(p), "cu": cu.get(p), "mib": mem.get(p)} for p in busy),
                                      key=lambda r: -(r["mib"] or 0))})
         time.sleep(1.0)
@@ -109,7 +110,8 @@ def _shared(port, seconds):
             "rows_median": [{"busy": statistics.median([r[i]["busy"] for r in rows if r[i]["busy"] is not None] or [0]),
                              "cu": round(statistics.median([r[i]["cu"] for r in rows if r[i]["cu"] is not None] or [0]), 1)}
                             for i in range(2)] if rows else None,
-            "pod_mfma_util_rows_max": max((k["pod_mfma_util_rows"] for k in inside), default=None)}
+            "pod_mfma_util_rows_max": max((k["pod_mfma_util_rows"] for k in inside), default=None),
+            "active_processes": [k["active"] for k in inside]}
 
 
 def main() -> int:
@@ -152,6 +154,7 @@ def main() -> int:
                                          if k.get("gpu_id") == "0"},
                               "mfma_util": (promtext.values(fam, "gpu_mfma_util_percent", gpu_id="0") or [None])[0],
                               "proc_busy": rows[0][2] if rows else None,
+                              "active": (promtext.values(fam, "gpu_active_processes", gpu_id="0") or [None])[0],
                               "proc_cu": occ[0][2] if occ else None})
                 time.sleep(1.0)
             so, se = tenant.communicate(timeout=120)
@@ -172,7 +175,8 @@ def main() -> int:
                  "exported_tflops_median": round(statistics.median(exp_tf), 1) if exp_tf else None,
                  "exported_mfma_util_median": round(statistics.median(util), 1) if util else None,
                  "exported_proc_busy_median": round(statistics.median(busy), 1) if busy else None,
-                 "exported_proc_cu_median": round(statistics.median(cu), 1) if cu else None}
+                 "exported_proc_cu_median": round(statistics.median(cu), 1) if cu else None,
+                 "active_processes": [k["active"] for k in inside]}
             if r["exported_tflops_median"]:
                 # the tenant's rate is over its GPU-busy time; the exporter's over wall time
                 r["exported_vs_tenant"] = round(r["exported_tflops_median"] / (t["tflops"] * t["busy"]), 4)
