@@ -36,6 +36,7 @@ def gpu_rows(fam: dict) -> List[dict]:
     gfx = _per_gpu(fam, "gpu_clock_mhz", clock="gfx")
     up = _per_gpu(fam, "gpu_up")
     mfma = _per_gpu(fam, "gpu_mfma_util_percent")
+    active = _per_gpu(fam, "gpu_active_processes")
     xcd: Dict[Key, Dict[int, float]] = defaultdict(dict)
     for n, labels, v in fam.get("gpu_xcd_busy_percent", {"samples": []})["samples"]:
         xcd[(labels.get("host", "?"), labels.get("gpu_id", "?"))][int(labels.get("xcd", 0))] = v
@@ -50,7 +51,7 @@ def gpu_rows(fam: dict) -> List[dict]:
                      "xcd": [xcd[k][i] for i in sorted(xcd[k])] if k in xcd else [],
                      "vram_used": used.get(k), "vram_total": total.get(k), "power": power.get(k),
                      "hot": hot.get(k), "gfx_mhz": gfx.get(k), "ecc_ue": ue.get(k) if k in ue else None,
-                     "mfma": mfma.get(k)})
+                     "mfma": mfma.get(k), "procs": active.get(k)})
     return rows
 
 
@@ -73,7 +74,7 @@ def _f(v: Optional[float], w: int, p: int = 0) -> str:
 def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
     """Text tables for parsed expositions (one per node)."""
     lines = [f"{'HOST':<20}{'GPU':>4} {'UP':>2} {'UTIL%':>6} {'XCD busy% (0-7)':<32} {'VRAM GiB':>13} "
-             f"{'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8} {'MFMA%':>6} {'ECC-UE':>7}"]
+             f"{'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8} {'MFMA%':>6} {'ECC-UE':>7} {'PROCS':>5}"]
     pods = []
     for fam in frames:
         for r in gpu_rows(fam):
@@ -81,7 +82,7 @@ def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
             vram = "-" if r["vram_used"] is None else f"{r['vram_used'] / 2**30:.1f}/{(r['vram_total'] or 0) / 2**30:.0f}"
             lines.append(f"{r['host'][:19]:<20}{r['gpu_id']:>4} {_f(r['up'], 2)} {_f(r['util'], 6)} {xcd:<32} "
                          f"{vram:>13} {_f(r['power'], 6)} {_f(r['hot'], 6)} {_f(r['gfx_mhz'], 8)} "
-                         f"{_f(r['mfma'], 6, 1)} {_f(r['ecc_ue'], 7)}")
+                         f"{_f(r['mfma'], 6, 1)} {_f(r['ecc_ue'], 7)} {_f(r['procs'], 5)}")
         pods.extend(pod_rows(fam))
     for url, err in (errors or {}).items():
         lines.append(f"{url}: {err}")

@@ -40,6 +40,11 @@ def test_cli_top_over_two_exporters(mock_exporter, capsys):
     gpu_lines = [l for l in out.splitlines() if l.startswith("node-")]
     assert sum(l.startswith("node-a") for l in gpu_lines) >= 2 + 2  # 2 GPUs + pod rows
     assert "node-b-job-0" in out and "ECC-UE" in out
+    # PROCS (gpu_active_processes): node-a's GPU 1 runs this process in the mock -> 1 (exclusive)
+    hdr = next(l for l in out.splitlines() if l.startswith("HOST"))
+    assert hdr.rstrip().endswith("PROCS")
+    a1 = next(l for l in gpu_lines if l.split()[:2] == ["node-a", "1"])
+    assert a1.split()[-1] == "1", a1
     assert sum(1 for l in out.splitlines() if l.startswith("node-b") and "/288 " in l) == 3  # GPU rows
 
 
