@@ -7,6 +7,7 @@
 #include <unistd.h>
 
 #include <atomic>
+#include <cctype>
 #include <cerrno>
 #include <cstring>
 #include <strings.h>
