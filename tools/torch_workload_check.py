@@ -88,8 +88,10 @@ def _shared(port, seconds):
                       "tflops": (promtext.values(fam, "gpu_mfma_tflops", gpu_id="0", dtype="bf16") or [None])[0],
                       "pod_mfma_util_rows": len(promtext.values(fam, "pod_gpu_mfma_util_percent", gpu_id="0")),
                       "active": (promtext.values(fam, "gpu_active_processes", gpu_id="0") or [None])[0],
+                      # KFD reports host PIDs (not the tenants' pids inside a PID namespace): rows
+                      # ranked by busy share, the bigger tenant first
                       "rows": sorted(({"busy": busy.get(p), "cu": cu.get(p), "mib": mem.get(p)} for p in busy),
-                                     key=lambda r: -(r["mib"] or 0))})
+                                     key=lambda r: -(r["busy"] or 0))})
         time.sleep(1.0)
     res = []
     for t in ts:
