@@ -889,6 +889,7 @@ PYBIND11_MODULE(_core, m) {
         return d;
       });
   m.def("default_plugin_dir", &default_plugin_dir);
+  m.def("ondevice_helper_pid", &ondevice_helper_pid, "pid of the running on-device helper (0: none)");
   m.def(
       "parse_yaml_subset",
       [](const std::string& text) {

@@ -17,6 +17,7 @@
 #include "docker_lite.h"
 #include "grpc_lite.h"
 #include "http_client.h"
+#include "ondevice.h"
 #include "trace.h"
 
 namespace gpumon {
@@ -655,6 +656,11 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
   // 10 %-resident tenant escapes 10 reads a third of the time): the device counts as exclusive only
   // when no other pid was seen within the last 5 ticks and mfma_exclusive_window_s.
   std::vector<uint32_t> sole(procs.size(), 0);
+  // The exporter's own on-device helper holds a GPU context on every device (PMC counter buffers)
+  // and, with --probe, runs the K1 probe's waves: it is neither a workload row nor a sharer.
+  const int helper_pid = ondevice_helper_pid();
+  auto is_helper = [&](uint32_t pid) { return helper_pid > 0 && pid == static_cast<uint32_t>(helper_pid); };
+  uint64_t helper_rows = 0;
   const uint64_t tick_no = ++pod_rows_built_;
   const int64_t now_ns = mono_ns();
   const int64_t window_ns = static_cast<int64_t>(std::max(0.0, cfg_.mfma_exclusive_window_s) * 1e9);
@@ -664,7 +670,8 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
     auto& seen = last_active_[d];
     std::vector<uint32_t> active;  // distinct pids (one process may hold several KFD contexts)
     for (const auto& p : procs[d])
-      if ((p.occ_busy > 0 || p.cu_occupancy > 0) && std::find(active.begin(), active.end(), p.pid) == active.end())
+      if ((p.occ_busy > 0 || p.cu_occupancy > 0) && !is_helper(p.pid) &&
+          std::find(active.begin(), active.end(), p.pid) == active.end())
         active.push_back(p.pid);
     for (uint32_t pid : active) seen[pid] = {tick_no, now_ns};
     for (auto it = seen.begin(); it != seen.end();) {  // forget pids past both windows
@@ -682,6 +689,13 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
                          "ticks and mfma_exclusive_window_s; KFD occupancy reads): 0 idle, 1 exclusive, >1 shared.",
                          "gauge", static_cast<int>(d), {}, static_cast<double>(seen.size())});
   }
+  for (const auto& dev_procs : procs)
+    for (const auto& p : dev_procs) helper_rows += is_helper(p.pid) ? 1 : 0;
+  if (helper_pid > 0)
+    sharing.push_back({"gpumon_ondevice_helper_gpu_contexts",
+                     "GPU contexts of the exporter's own on-device helper (PMC counting / K1 probe), left out of "
+                     "pod_gpu rows and gpu_active_processes.",
+                     "gauge", -1, {}, static_cast<double>(helper_rows)});
   set_extra("sharing", std::move(sharing));
   uint64_t hidden = 0;
   std::vector<uint32_t> alive;
@@ -694,6 +708,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
     // a duplicate series would make Prometheus reject the whole scrape.
     std::unordered_map<uint32_t, size_t> row_of_pid;
     for (const auto& p : procs[d]) {
+      if (is_helper(p.pid)) continue;  // counted in gpumon_ondevice_helper_gpu_contexts
       auto dup = row_of_pid.find(p.pid);
       if (dup != row_of_pid.end()) {
         PodRow& r = (*rows)[dup->second];

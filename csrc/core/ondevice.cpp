@@ -468,6 +468,11 @@ ExtraSeries xs(const char* name, const char* help, int dev, double v, const char
 
 }  // namespace
 
+int ondevice_helper_pid() {
+  std::lock_guard<std::mutex> g(g_helper.mu);
+  return g_helper.pid;
+}
+
 std::string default_plugin_dir() {
   if (const char* e = getenv("GPUMON_PLUGIN_DIR"); e && *e) return e;
   Dl_info info{};

@@ -186,4 +186,8 @@ class OnDevice {
   std::atomic<uint64_t> pmc_samples_{0}, pmc_errors_{0}, pmc_resets_{0}, probe_done_{0}, probe_timeouts_{0};
 };
 
+// pid of the on-device helper process this exporter spawned (0: none running). Its GPU context
+// (PMC counting buffers, the K1 probe's waves) is the exporter's own, not a workload's.
+int ondevice_helper_pid();
+
 }  // namespace gpumon

@@ -665,3 +665,30 @@ def test_helper_starts_with_a_clean_signal_mask():
     finally:
         p.terminate()
         p.wait(20)
+
+
+def test_own_helper_is_not_a_workload_or_a_sharer(core, mock_exporter, monkeypatch):
+    """The exporter's on-device helper holds a GPU context on every device and (with --probe) runs
+    the K1 probe's waves. Its KFD process entry must not become a pod_gpu row, count toward
+    gpu_active_processes, or make an exclusively used GPU look shared (which would withdraw the
+    tenant's pod_gpu_mfma_util_percent)."""
+    monkeypatch.setenv("GPUMON_FAKE_AGENTS", "1")
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0)
+    od = _ondevice(core, ex, ondevice_isolate=True)
+    od.start()
+    try:
+        assert od.step()
+        helper = core.ondevice_helper_pid()
+        assert helper > 0
+        ex.mock_set_procs([{"pid": 4242, "device": 0, "name": "train", "kfd_only": True},
+                           {"pid": helper, "device": 0, "name": "gpumon-ondevice", "kfd_only": True}])
+        ex.mock_set_occ_series(0, [200.0, 8.0])  # both have waves resident (the helper: the probe)
+        ex.set_device_mfma_util({0: 61.0})
+        ex.tick()
+        rows = [r for r in ex.pod_rows() if not r["idle"]]
+        assert [r["pid"] for r in rows] == ["4242"] and rows[0]["mfma_util"] is not None
+        m = ex.metrics_text()
+        assert _val(m, "gpu_active_processes", gpu_id="0") == 1
+        assert "gpumon_ondevice_helper_gpu_contexts" in m and f'pid="{helper}"' not in m
+    finally:
+        od.stop()
