@@ -560,6 +560,40 @@ PYBIND11_MODULE(_core, m) {
         return match_device_id(id, st);
       },
       "C++ twin of gpumon.attribution.plane.match_device_id (the native PodResources poller's matcher)");
+  m.def(
+      "docker_parse_inspect",
+      [](py::bytes b) {
+        DockerInspect di;
+        std::string err;
+        if (!docker_parse_inspect(std::string(b), &di, &err)) throw py::value_error(err);
+        py::dict d;
+        d["id"] = di.id;
+        d["devices"] = di.devices;
+        d["env"] = di.env;
+        return d;
+      },
+      py::arg("json"));
+  m.def(
+      "docker_container_gpus",
+      [](const std::vector<std::string>& devices, const std::vector<std::string>& env, const py::list& statics) {
+        std::vector<DeviceStatic> st;
+        for (auto o : statics) {
+          py::dict d = o.cast<py::dict>();
+          DeviceStatic s;
+          get(d, "index", &s.index);
+          get(d, "hip_id", &s.hip_id);
+          get(d, "bdf", &s.bdf);
+          get(d, "uuid", &s.uuid);
+          get(d, "drm_card", &s.drm_card);
+          get(d, "drm_render", &s.drm_render);
+          st.push_back(s);
+        }
+        DockerInspect di;
+        di.devices = devices;
+        di.env = env;
+        return Exporter::docker_container_gpus(di, st);
+      },
+      py::arg("devices"), py::arg("env"), py::arg("statics"));
   m.def("roctx_enable", &Roctx::enable, py::arg("on") = true,
         "Load librocprofiler-sdk-roctx and bracket sampler phases with ROCTx ranges");
   m.def("roctx_active", &Roctx::active);

@@ -188,6 +188,39 @@ class JsonReader {
     }
   }
 
+  // {"k": v, ...}: on_member(key) must consume the value (null -> no members)
+  template <typename F>
+  bool members(F on_member) {
+    if (null()) return true;
+    if (!eat('{')) return false;
+    if (peek('}')) return ++p_, true;
+    for (;;) {
+      std::string k;
+      if (!string(&k) || !eat(':') || !on_member(k)) return false;
+      if (peek(',')) {
+        ++p_;
+        continue;
+      }
+      return eat('}');
+    }
+  }
+
+  // [v, ...]: on_elem() must consume each element (null -> none)
+  template <typename F>
+  bool elements(F on_elem) {
+    if (null()) return true;
+    if (!eat('[')) return false;
+    if (peek(']')) return ++p_, true;
+    for (;;) {
+      if (!on_elem()) return false;
+      if (peek(',')) {
+        ++p_;
+        continue;
+      }
+      return eat(']');
+    }
+  }
+
   bool null() {
     ws();
     if (e_ - p_ >= 4 && memcmp(p_, "null", 4) == 0) {
@@ -319,6 +352,37 @@ bool docker_parse_containers(const std::string& json, std::vector<DockerContaine
   }
 }
 
+bool docker_parse_inspect(const std::string& json, DockerInspect* out, std::string* err) {
+  *out = DockerInspect{};
+  JsonReader r(json);
+  const bool ok = r.members([&](const std::string& k) {
+    if (k == "Id" && r.peek('"')) return r.string(&out->id);
+    if (k == "Config")
+      return r.members([&](const std::string& ck) { return ck == "Env" ? r.string_array(&out->env) : r.skip(2); });
+    if (k == "HostConfig")
+      return r.members([&](const std::string& hk) {
+        if (hk != "Devices") return r.skip(2);
+        return r.elements([&]() {
+          return r.members([&](const std::string& dk) {
+            if (dk == "PathOnHost" && r.peek('"')) {
+              std::string path;
+              if (!r.string(&path)) return false;
+              out->devices.push_back(std::move(path));
+              return true;
+            }
+            return r.skip(4);
+          });
+        });
+      });
+    return r.skip(1);
+  });
+  if (!ok || !r.at_end()) {
+    *err = r.ok() ? "malformed container inspect" : r.error();
+    return false;
+  }
+  return true;
+}
+
 bool http1_parse_response(const std::string& raw, int* status, std::string* body, std::string* err, bool eof) {
   const size_t hdr_end = raw.find("\r\n\r\n");
   if (hdr_end == std::string::npos) {
@@ -400,12 +464,13 @@ bool http1_parse_response(const std::string& raw, int* status, std::string* body
   return true;
 }
 
-bool docker_list(const std::string& socket_path, std::vector<DockerContainer>* out, std::string* err, int timeout_ms,
-                 int* http_status) {
-  int local_status;
-  int& status = http_status ? *http_status : local_status;
+namespace {
+
+// One HTTP/1.0 GET on the daemon's unix socket: *status (-1 transport failure) and the body.
+bool docker_get(const std::string& socket_path, const std::string& target, std::string* body_out, int* status_out,
+                std::string* err, int timeout_ms) {
+  int& status = *status_out;
   status = -1;
-  out->clear();
   const int64_t deadline = mono_ns() + static_cast<int64_t>(timeout_ms) * 1000000;
   std::string path = socket_path;
   if (path.rfind("unix://", 0) == 0) path = path.substr(7);
@@ -448,7 +513,7 @@ bool docker_list(const std::string& socket_path, std::vector<DockerContainer>* o
     }
   }
   // HTTP/1.0: the daemon answers with Content-Length or closes the connection (no chunking)
-  const std::string req = "GET /containers/json HTTP/1.0\r\nHost: docker\r\nUser-Agent: gpumon\r\n\r\n";
+  const std::string req = "GET " + target + " HTTP/1.0\r\nHost: docker\r\nUser-Agent: gpumon\r\n\r\n";
   for (size_t off = 0; off < req.size();) {
     const ssize_t w = ::send(fd, req.data() + off, req.size() - off, MSG_NOSIGNAL);
     if (w > 0) {
@@ -498,10 +563,37 @@ bool docker_list(const std::string& socket_path, std::vector<DockerContainer>* o
   if (!framed && !http1_parse_response(raw, &st, &body, err, true)) return false;
   status = st;
   if (st != 200) {
-    *err = "GET /containers/json: HTTP " + std::to_string(st) + (body.empty() ? "" : ": " + body.substr(0, 200));
+    *err = "GET " + target + ": HTTP " + std::to_string(st) + (body.empty() ? "" : ": " + body.substr(0, 200));
     return false;
   }
-  return docker_parse_containers(body, out, err);
+  *body_out = std::move(body);
+  return true;
+}
+
+}  // namespace
+
+bool docker_list(const std::string& socket_path, std::vector<DockerContainer>* out, std::string* err, int timeout_ms,
+                 int* http_status) {
+  int local_status;
+  out->clear();
+  std::string body;
+  return docker_get(socket_path, "/containers/json", &body, http_status ? http_status : &local_status, err,
+                    timeout_ms) &&
+         docker_parse_containers(body, out, err);
+}
+
+bool docker_inspect(const std::string& socket_path, const std::string& id, DockerInspect* out, std::string* err,
+                    int timeout_ms, int* http_status) {
+  int local_status;
+  int& status = http_status ? *http_status : local_status;
+  status = -1;
+  if (id.empty() || id.size() > 128 || id.find_first_not_of("0123456789abcdef") != std::string::npos) {
+    *err = "container id must be hex";
+    return false;
+  }
+  std::string body;
+  return docker_get(socket_path, "/containers/" + id + "/json", &body, &status, err, timeout_ms) &&
+         docker_parse_inspect(body, out, err);
 }
 
 }  // namespace gpumon

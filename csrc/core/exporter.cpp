@@ -1331,7 +1331,11 @@ bool Exporter::podres_poll_once() {
       }
       allocs.push_back(std::move(a));
     }
-    attr_->set_allocations(std::move(allocs));
+    {
+      std::lock_guard<std::mutex> g(meta_mu_);
+      podres_allocs_ = std::move(allocs);
+    }
+    publish_allocations();
   } else {
     GPUMON_LOG(LogLevel::kWarn, "podresources", "List() failed: " + err);
   }
@@ -1453,6 +1457,7 @@ bool Exporter::docker_poll_once() {
   int http = -1;
   const int64_t t0 = mono_ns();
   const bool ok = docker_list(cfg_.docker_socket, &cs, &err, 3000, &http);
+  uint64_t inspect_errors = 0;
   const double dt = (mono_ns() - t0) * 1e-9;
   if (ok) {
     std::vector<ContainerMeta> metas;
@@ -1471,11 +1476,55 @@ bool Exporter::docker_poll_once() {
       m.labels = std::move(c.labels);
       metas.push_back(std::move(m));
     }
+    // which GPUs each container holds: one inspect per container the first time it is seen
+    std::vector<DeviceStatic> st;
+    {
+      std::lock_guard<std::mutex> g(state_mu_);
+      st = statics_;
+    }
+    std::unordered_map<std::string, std::vector<int>> gpus;
+    int inspected = 0;
+    for (const auto& m : metas) {
+      auto it = docker_gpus_.find(m.container_id);
+      if (it != docker_gpus_.end()) {
+        gpus.emplace(it->first, it->second);
+        continue;
+      }
+      if (inspected >= 64) continue;  // bounded per refresh; the rest next time
+      DockerInspect di;
+      std::string ierr;
+      ++inspected;
+      if (docker_inspect(cfg_.docker_socket, m.container_id, &di, &ierr, 3000)) {
+        gpus.emplace(m.container_id, docker_container_gpus(di, st));
+      } else {
+        inspect_errors++;
+        GPUMON_LOG(LogLevel::kDebug, "docker", "inspect " + m.container_id.substr(0, 12) + ": " + ierr);
+      }
+    }
+    std::vector<Allocation> allocs;
+    for (const auto& m : metas) {
+      const auto it = gpus.find(m.container_id);
+      if (it == gpus.end()) continue;
+      for (int idx : it->second) {
+        Allocation a;
+        a.pod_namespace = m.pod_namespace;
+        a.pod_name = m.pod_name;
+        a.container_name = m.container_name;
+        a.container_id = m.container_id;
+        a.pod_uid = m.pod_uid;
+        a.labels = m.labels;
+        a.gpu_index = idx;
+        allocs.push_back(std::move(a));
+      }
+    }
+    docker_gpus_.swap(gpus);  // forgets containers that are gone
     {
       std::lock_guard<std::mutex> g(meta_mu_);
       docker_metas_ = std::move(metas);
+      docker_allocs_ = std::move(allocs);
     }
     publish_container_meta();
+    publish_allocations();
   } else {
     GPUMON_LOG(LogLevel::kWarn, "docker", "GET /containers/json failed: " + err);
   }
@@ -1485,11 +1534,66 @@ bool Exporter::docker_poll_once() {
   ex.push_back({"gpumon_docker_containers", "Containers known from the Docker Engine API.", "gauge", -1, {},
                 static_cast<double>(cs.size())});
   ex.push_back({"gpumon_docker_list_seconds", "Duration of the last Docker Engine listing.", "gauge", -1, {}, dt});
+  ex.push_back({"gpumon_docker_inspect_errors", "Container inspects that failed in the last Docker refresh.", "gauge",
+                -1, {}, static_cast<double>(inspect_errors)});
   ex.push_back({"gpumon_docker_http_status",
                 "HTTP status of the last Docker Engine listing (-1 = transport failure).", "gauge", -1, {},
                 static_cast<double>(http)});
   set_extra("docker_native", std::move(ex));
   return ok;
+}
+
+void Exporter::publish_allocations() {
+  std::vector<Allocation> all;
+  {
+    std::lock_guard<std::mutex> g(meta_mu_);
+    all = podres_allocs_;
+    all.insert(all.end(), docker_allocs_.begin(), docker_allocs_.end());
+  }
+  attr_->set_allocations(std::move(all));  // a (pod, container, GPU) listed by both is one idle row
+}
+
+std::vector<int> Exporter::docker_container_gpus(const DockerInspect& in, const std::vector<DeviceStatic>& st) {
+  std::vector<int> out;
+  auto add = [&](int i) {
+    if (i >= 0 && i < static_cast<int>(st.size()) && std::find(out.begin(), out.end(), i) == out.end())
+      out.push_back(i);
+  };
+  auto all = [&] {
+    for (int i = 0; i < static_cast<int>(st.size()); ++i) add(i);
+  };
+  for (const auto& path : in.devices) {
+    std::string p = path;
+    while (p.size() > 1 && p.back() == '/') p.pop_back();
+    if (p == "/dev/dri") {
+      all();
+    } else if (starts_with(p, "/dev/dri/renderD") || starts_with(p, "/dev/dri/card")) {
+      const bool render = starts_with(p, "/dev/dri/renderD");
+      const std::string num = p.substr(render ? 16 : 13);
+      if (num.empty() || num.find_first_not_of("0123456789") != std::string::npos) continue;
+      const int n = atoi(num.c_str());
+      for (size_t i = 0; i < st.size(); ++i)
+        if ((render ? st[i].drm_render : st[i].drm_card) == n) add(static_cast<int>(i));
+    }
+  }
+  for (const auto& kv : in.env) {
+    if (!starts_with(kv, "AMD_VISIBLE_DEVICES=")) continue;
+    const std::string v = kv.substr(20);
+    if (v == "all") {
+      all();
+      continue;
+    }
+    for (size_t p = 0; p <= v.size();) {
+      size_t e = v.find(',', p);
+      if (e == std::string::npos) e = v.size();
+      const std::string tok = v.substr(p, e - p);
+      if (!tok.empty() && tok.find_first_not_of("0123456789") == std::string::npos) add(atoi(tok.c_str()));
+      else if (!tok.empty()) add(match_device_id(tok, st));
+      p = e + 1;
+    }
+  }
+  std::sort(out.begin(), out.end());
+  return out;
 }
 
 }  // namespace gpumon

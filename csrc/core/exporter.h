@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "attribution.h"
+#include "docker_lite.h"
 #include "backend.h"
 #include "http_server.h"
 #include "rates.h"
@@ -164,6 +165,12 @@ class Exporter {
   bool cri_poll_once();
   bool docker_poll_once();
   void publish_container_meta();  // CRI U Docker metadata -> attribution + native_meta_
+ public:
+  // GPU indices a Docker container holds: /dev/dri/renderD<N> / card<N> device mappings, all of
+  // /dev/dri, or AMD_VISIBLE_DEVICES (indices, UUIDs, BDFs or "all") in its environment.
+  static std::vector<int> docker_container_gpus(const DockerInspect& in, const std::vector<DeviceStatic>& st);
+
+ private:
   bool ensure_backend();
   void handle_http(const HttpRequest& req, HttpResponse* resp);
   void sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
@@ -244,6 +251,12 @@ class Exporter {
   uint64_t pod_rows_built_ = 0;
   std::mutex meta_mu_;
   std::vector<ContainerMeta> cri_metas_, docker_metas_;  // last successful listing of each (meta_mu_)
+  // GPU allocations: kubelet PodResources and, on Docker nodes, the GPU devices / AMD_VISIBLE_DEVICES
+  // of each running container (docker inspect, cached per container id: a container's devices are
+  // fixed at creation) -- published together (meta_mu_)
+  std::vector<Allocation> podres_allocs_, docker_allocs_;
+  std::unordered_map<std::string, std::vector<int>> docker_gpus_;  // container id -> GPU indices
+  void publish_allocations();
   std::mutex push_mu_;
   std::condition_variable push_cv_;
   std::deque<std::string> push_q_;

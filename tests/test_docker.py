@@ -107,8 +107,9 @@ class FakeDocker:
     """Docker Engine API subset on a unix socket: GET /containers/json (others 404). `containers`
     is a listing, or a callable returning the raw body of each response."""
 
-    def __init__(self, path, containers, status=200, chunked=False, keep_open=False):
+    def __init__(self, path, containers, status=200, chunked=False, keep_open=False, inspect=None):
         self.path, self.containers, self.status, self.chunked, self.requests = path, containers, status, chunked, []
+        self.inspect = inspect or {}  # container id -> GET /containers/{id}/json object
         outer = self
 
         class H(BaseHTTPRequestHandler):
@@ -117,6 +118,15 @@ class FakeDocker:
 
             def do_GET(self):  # noqa: N802
                 outer.requests.append((self.command, self.path, self.request_version))
+                parts = self.path.split("/")
+                if len(parts) == 4 and parts[1] == "containers" and parts[3] == "json" and parts[2] in outer.inspect:
+                    body = json.dumps(outer.inspect[parts[2]]).encode()
+                    self.send_response(200)
+                    self.send_header("Content-Type", "application/json")
+                    self.send_header("Content-Length", str(len(body)))
+                    self.end_headers()
+                    self.wfile.write(body)
+                    return
                 if self.path != "/containers/json":
                     self.send_error(404)
                     return
@@ -226,7 +236,8 @@ def test_exporter_attributes_docker_containers(core, tmp_path):
             assert promtext.one(fam, "gpumon_docker_http_status") == 200
         finally:
             ex.stop()
-    assert d.requests and all(r == ("GET", "/containers/json", "HTTP/1.0") for r in d.requests)
+    assert d.requests and all(r[0] == "GET" and r[2] == "HTTP/1.0" for r in d.requests)
+    assert {r[1] for r in d.requests} <= {"/containers/json"} | {f"/containers/{c}/json" for c in (CID_K8S, CID_PLAIN, CID_OTHER)}
 
 
 def test_exporter_reports_a_failing_docker_daemon(core, tmp_path):
@@ -256,3 +267,72 @@ def test_docker_socket_is_never_autodetected():
     r = subprocess.run([binary, "--docker", "/run/docker.sock", "--print-config"], capture_output=True, text=True,
                        timeout=30, check=True)
     assert json.loads(r.stdout)["docker_socket"] == "/run/docker.sock"
+
+
+def _inspect(cid, devices=(), env=()):
+    return {"Id": cid, "Created": "2026-10-17T00:00:00Z", "Path": "python", "Args": ["train.py"],
+            "State": {"Status": "running", "Pid": 4242},
+            "Config": {"Hostname": "x", "Env": list(env) + ["PATH=/usr/bin"], "Labels": {"a": "b"},
+                       "Cmd": ["python"], "Volumes": None},
+            "HostConfig": {"Binds": None, "Privileged": False,
+                           "Devices": [{"PathOnHost": p, "PathInContainer": p, "CgroupPermissions": "rwm"}
+                                       for p in devices],
+                           "DeviceRequests": None, "Ulimits": [{"Name": "memlock", "Soft": -1, "Hard": -1}]},
+            "Mounts": [], "NetworkSettings": {"Ports": {}}}
+
+
+def test_parse_inspect(core):
+    d = core.docker_parse_inspect(json.dumps(_inspect(CID_PLAIN, ["/dev/kfd", "/dev/dri/renderD129"],
+                                                      ["AMD_VISIBLE_DEVICES=1"])).encode())
+    assert d["id"] == CID_PLAIN and d["devices"] == ["/dev/kfd", "/dev/dri/renderD129"]
+    assert "AMD_VISIBLE_DEVICES=1" in d["env"]
+    d = core.docker_parse_inspect(b'{"Id": "ab", "Config": null, "HostConfig": {"Devices": null}}')
+    assert d["devices"] == [] and d["env"] == []
+    for bad in (b"[]", b'{"HostConfig": {"Devices": [{"PathOnHost": 1}]', b'{"Config": {"Env": [1,}}'):
+        with pytest.raises(ValueError):
+            core.docker_parse_inspect(bad)
+
+
+def test_container_gpus_mapping(core):
+    st = [{"index": i, "drm_card": i, "drm_render": 128 + i, "bdf": f"0000:{0x05 + 0x20 * i:02x}:00.0",
+           "uuid": f"uuid-{i}"} for i in range(4)]
+    g = core.docker_container_gpus
+    assert g(["/dev/kfd", "/dev/dri/renderD130"], [], st) == [2]
+    assert g(["/dev/dri/card1", "/dev/dri/renderD129"], [], st) == [1]
+    assert g(["/dev/dri/"], [], st) == [0, 1, 2, 3]  # the whole directory
+    assert g(["/dev/kfd"], [], st) == []  # KFD alone names no GPU
+    assert g([], ["AMD_VISIBLE_DEVICES=all"], st) == [0, 1, 2, 3]
+    assert g([], ["AMD_VISIBLE_DEVICES=3,0,9"], st) == [0, 3]  # 9: no such GPU
+    assert g([], ["AMD_VISIBLE_DEVICES=uuid-2,0000:25:00.0"], st) == [1, 2]
+    assert g(["/dev/dri/renderD999", "/dev/dri/renderDx"], ["OTHER=1"], st) == []
+
+
+def test_exporter_idle_rows_for_docker_gpu_containers(core, tmp_path):
+    """The reference found allocated-but-idle GPUs by running `nvidia-smi -L` inside every opted-in
+    container (gpu.py:220-253, docker exec). On a Docker node the exporter reads which GPUs each
+    container was given (device mappings or AMD_VISIBLE_DEVICES, one inspect per new container) and
+    emits the idle rows for those without a GPU process."""
+    _fake_proc(tmp_path, 2000, f"0::/system.slice/docker-{CID_PLAIN}.scope")
+    cs = [_container(CID_PLAIN, "busy", {"mlgpu": "mlgpu"}),
+          _container(CID_OTHER, "waiting", {"mlgpu": "mlgpu"}),
+          _container(CID_K8S, "k8s_nb", K8S_LABELS)]
+    insp = {CID_PLAIN: _inspect(CID_PLAIN, ["/dev/kfd", "/dev/dri/renderD128"]),
+            CID_OTHER: _inspect(CID_OTHER, ["/dev/kfd"], ["AMD_VISIBLE_DEVICES=1"]),
+            CID_K8S: _inspect(CID_K8S, [])}
+    with FakeDocker(_sock("a"), cs, inspect=insp) as d:
+        ex = core.Exporter({"backend": "mock:gpus=2", "serve_http": False, "interval_s": 0, "host": "n1",
+                            "procfs_root": str(tmp_path), "docker_socket": d.path, "opt_in": "mlgpu=mlgpu"})
+        ex.start()
+        try:
+            ex.mock_set_procs([{"pid": 2000, "device": 0, "name": "bench", "vram_bytes": 1 << 30}])
+            ex.tick()
+            rows = sorted((r["dev"], r["idle"], r["container"], r["containerid"]) for r in ex.pod_rows())
+            assert rows == [(0, False, "busy", CID_PLAIN[:12]), (1, True, "waiting", CID_OTHER[:12])], rows
+            fam = promtext.parse(ex.metrics_text())
+            assert promtext.one(fam, "gpumon_gpus", state="allocated") == 2
+            assert promtext.one(fam, "gpumon_gpus", state="allocated_idle") == 1
+            assert promtext.one(fam, "gpumon_docker_inspect_errors") == 0
+        finally:
+            ex.stop()
+    inspects = [r[1] for r in d.requests if r[1] != "/containers/json"]
+    assert sorted(inspects) == sorted(f"/containers/{c}/json" for c in insp)  # once per container
