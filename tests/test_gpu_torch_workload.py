@@ -42,4 +42,7 @@ def test_shared_gpu_two_torch_tenants():
     big, small = s["rows_median"]
     assert big["busy"] > small["busy"] > 0 and big["busy"] + small["busy"] <= 110, s
     assert s["pod_mfma_util_rows_max"] == 0, s
-    assert all(a == 2 for a in s["active_processes"]), s  # shared
+    # shared: 2 on every tick (a tenant resident 10 % of the time can escape 5 ticks' reads with
+    # p ~ 0.5 %, so one tick may read 1)
+    act = s["active_processes"]
+    assert all(a in (1, 2) for a in act) and sum(a == 2 for a in act) >= len(act) - 1, s
