@@ -1482,12 +1482,14 @@ bool Exporter::docker_poll_once() {
       std::lock_guard<std::mutex> g(state_mu_);
       st = statics_;
     }
+    std::unordered_map<std::string, DockerInspect> seen;
     std::unordered_map<std::string, std::vector<int>> gpus;
     int inspected = 0;
     for (const auto& m : metas) {
-      auto it = docker_gpus_.find(m.container_id);
-      if (it != docker_gpus_.end()) {
-        gpus.emplace(it->first, it->second);
+      auto it = docker_inspects_.find(m.container_id);
+      if (it != docker_inspects_.end()) {
+        gpus.emplace(m.container_id, docker_container_gpus(it->second, st));
+        seen.emplace(m.container_id, std::move(it->second));
         continue;
       }
       if (inspected >= 64) continue;  // bounded per refresh; the rest next time
@@ -1496,6 +1498,7 @@ bool Exporter::docker_poll_once() {
       ++inspected;
       if (docker_inspect(cfg_.docker_socket, m.container_id, &di, &ierr, 3000)) {
         gpus.emplace(m.container_id, docker_container_gpus(di, st));
+        seen.emplace(m.container_id, std::move(di));
       } else {
         inspect_errors++;
         GPUMON_LOG(LogLevel::kDebug, "docker", "inspect " + m.container_id.substr(0, 12) + ": " + ierr);
@@ -1517,7 +1520,7 @@ bool Exporter::docker_poll_once() {
         allocs.push_back(std::move(a));
       }
     }
-    docker_gpus_.swap(gpus);  // forgets containers that are gone
+    docker_inspects_.swap(seen);  // forgets containers that are gone
     {
       std::lock_guard<std::mutex> g(meta_mu_);
       docker_metas_ = std::move(metas);

@@ -255,7 +255,9 @@ class Exporter {
   // of each running container (docker inspect, cached per container id: a container's devices are
   // fixed at creation) -- published together (meta_mu_)
   std::vector<Allocation> podres_allocs_, docker_allocs_;
-  std::unordered_map<std::string, std::vector<int>> docker_gpus_;  // container id -> GPU indices
+  // container id -> its inspect (devices + env); mapped to GPU indices on every refresh, so a
+  // container seen before the backend listed its GPUs is still resolved later
+  std::unordered_map<std::string, DockerInspect> docker_inspects_;
   void publish_allocations();
   std::mutex push_mu_;
   std::condition_variable push_cv_;
