@@ -159,6 +159,8 @@ class FakeDocker:
         class S(socketserver.ThreadingMixIn, socketserver.UnixStreamServer):
             daemon_threads = True
 
+        if os.path.exists(path):  # left behind by a killed run
+            os.unlink(path)
         self.srv = S(path, H)
         self.t = threading.Thread(target=self.srv.serve_forever, daemon=True)
 
