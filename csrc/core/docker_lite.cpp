@@ -531,6 +531,8 @@ bool docker_get(const std::string& socket_path, const std::string& target, std::
   std::string raw, body;
   int st = -1;
   bool framed = false;  // a complete Content-Length / chunked response arrived before EOF
+  size_t hdr_end = std::string::npos, want = 0;
+  bool chunked = false;
   char buf[65536];
   for (;;) {
     const ssize_t r = ::recv(fd, buf, sizeof buf, 0);
@@ -540,9 +542,21 @@ bool docker_get(const std::string& socket_path, const std::string& target, std::
         *err = "response too large";
         return false;
       }
-      // a daemon that keeps the connection open despite HTTP/1.0 still ends the read here
+      // a daemon that keeps the connection open despite HTTP/1.0 still ends the read here. The full
+      // parse runs only once the bytes could hold a complete framed response (Content-Length
+      // reached, or the chunked terminator just arrived), so a large listing is not re-parsed per read.
+      if (hdr_end == std::string::npos && (hdr_end = raw.find("\r\n\r\n")) != std::string::npos) {
+        std::string h = raw.substr(0, hdr_end);
+        for (auto& c : h) c = static_cast<char>(tolower(static_cast<unsigned char>(c)));
+        const size_t cl = h.find("\r\ncontent-length:");
+        if (cl != std::string::npos) want = hdr_end + 4 + strtoull(h.c_str() + cl + 17, nullptr, 10);
+        chunked = h.find("\r\ntransfer-encoding:") != std::string::npos && h.find("chunked") != std::string::npos;
+      }
+      const bool maybe_complete = hdr_end != std::string::npos &&
+                                  ((want && raw.size() >= want) ||
+                                   (chunked && raw.size() >= 5 && raw.compare(raw.size() - 5, 5, "0\r\n\r\n") == 0));
       std::string e;
-      if (raw.find("\r\n\r\n") != std::string::npos && http1_parse_response(raw, &st, &body, &e, false)) {
+      if (maybe_complete && http1_parse_response(raw, &st, &body, &e, false)) {
         framed = true;
         break;
       }
