@@ -1041,6 +1041,10 @@ void Exporter::influx_loop() {
     return;
   }
   HttpClient client(cfg_.influx_timeout_s);
+  if (cfg_.influx_token.find_first_of("\r\n") != std::string::npos) {  // would inject headers
+    GPUMON_LOG(LogLevel::kError, "influx", "influx_token contains a line break: push disabled");
+    return;
+  }
   const std::string headers = "Content-Type: text/plain; charset=utf-8\r\n" +
                               (!cfg_.influx_token.empty() ? "Authorization: Token " + cfg_.influx_token + "\r\n"
                                                           : u.auth_header);

@@ -197,3 +197,17 @@ def test_influx_credentials_never_printed(tmp_path):
     assert d["influx_url"] == "http://u:***@influx:8086/write?db=k8s" and d["influx_token"] == "***"
     c = Config().apply_env({"INFLUXDB_TOKEN": "tok-456"})
     assert c.influx_token == "tok-456" and c.to_core()["influx_token"] == "tok-456"
+
+
+def test_influx_token_with_a_line_break_disables_the_push(core):
+    """A token is copied into a request header: CR/LF in it would inject headers, so the pusher
+    refuses to start (the sampler keeps running)."""
+    ex = core.Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0.02,
+                        "influx_url": "http://127.0.0.1:9/write", "influx_token": "tok\r\nX-Evil: 1"})
+    ex.start()
+    try:
+        time.sleep(0.3)
+        st = ex.self_stats()
+    finally:
+        ex.stop()
+    assert st["ticks"] >= 5 and st["influx_ok"] == 0 and st["influx_fail"] == 0
