@@ -627,6 +627,10 @@ void AmdSmiBackend::occupancy(int i, const std::vector<uint32_t>& pids, std::vec
   fast_[i]->occupancy(pids, out);
 }
 
+bool AmdSmiBackend::occupancy_scan(int i, std::vector<OccRead>* out) {
+  return supports_occupancy(i) && fast_[i]->occupancy_scan(out);
+}
+
 bool AmdSmiBackend::supports_links() const { return t_ && t_->amdsmi_get_link_metrics; }
 
 void AmdSmiBackend::sample_links(int i, DeviceSample* out) {

@@ -50,6 +50,10 @@ class Backend {
   virtual void occupancy(int, const std::vector<uint32_t>& pids, std::vector<double>* out) {
     out->assign(pids.size(), kNaN);
   }
+  // Optional: cu_occupancy + VRAM of EVERY process on device i right now, newly started ones
+  // included (the device worker's sub-samples; false = unsupported, use occupancy() on the pids of
+  // the last tick instead).
+  virtual bool occupancy_scan(int, std::vector<OccRead>*) { return false; }
   virtual void sample_ras(int, DeviceSample*, int /*slice*/ = 0, int /*nslices*/ = 1) {}
   // Upkeep that must stay off the tick's critical path (the device worker calls it after it
   // published the tick's sample): e.g. refreshing cached /proc fd tables.
@@ -124,6 +128,7 @@ struct MockConfig {
   int n_xcd = 8;
   int n_links = 7;
   double firmware_hz = 50.0;          // how fast the fake firmware table advances
+  bool occupancy = true;              // KFD cu_occupancy readable (false: a node without the file)
 };
 
 class MockBackend : public Backend {
@@ -139,8 +144,9 @@ class MockBackend : public Backend {
   void sample_links(int i, DeviceSample* out) override;
   bool supports_ras() const override { return true; }
   void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;
-  bool supports_occupancy(int) const override { return true; }
+  bool supports_occupancy(int) const override { return cfg_.occupancy; }
   void occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) override;
+  bool occupancy_scan(int i, std::vector<OccRead>* out) override;
 
   // Test controls (thread-safe).
   // Every cu_occupancy read of `dev` (process list and sub-samples alike) returns the next value of
@@ -206,6 +212,7 @@ class AmdSmiBackend : public Backend {
   bool supports_occupancy(int i) const override;  // with the sysfs fast path (KFD files)
   void maintain(int i) override;                   // fast path: due /proc fd-table refreshes
   void occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) override;
+  bool occupancy_scan(int i, std::vector<OccRead>* out) override;
   std::string lib_version() const { return lib_version_; }
   // Expose every physical device `r` times (distinct gpu_id labels). Only for measuring how the
   // sampler scales with the GPU count on a box with fewer GPUs than a full 8x MI355X node.

@@ -18,6 +18,7 @@
 #include <string>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "attribution.h"
@@ -61,11 +62,12 @@ struct ExporterConfig {
   // it keeps the tick on its deadline. Needs CAP_SYS_NICE (the privileged DaemonSet has it);
   // without it the threads stay normal and gpumon_sampler_rt_threads says so.
   int rt_priority = 0;
-  int occ_samples = 10;               // KFD cu_occupancy reads per process per tick on the device workers (1 = the tick's own)
+  int occ_samples = 20;               // KFD cu_occupancy reads per process per tick on the device workers (1 = the tick's own)
   bool hide_empty_contexts = true;    // no pod_gpu row for a process with a GPU context but no VRAM and no waves
   // pod_gpu_mfma_util_percent needs exclusive use: no OTHER process's waves seen on the device in
-  // the last 5 ticks nor in the last mfma_exclusive_window_s seconds (a tenant resident 10 % of the
-  // time escapes one tick's 10 occupancy reads a third of the time; profiles/r2_torch_workload.md)
+  // the last 5 ticks nor in the last mfma_exclusive_window_s seconds, and no other process that
+  // arrived (VRAM held) within that window (a tenant resident 10 % of the time escapes one tick's
+  // 20 occupancy reads 12 % of the time, a 5 s window's 100 reads 0.003 %)
   double mfma_exclusive_window_s = 5.0;
   AttributionConfig attribution;
   RateConfig rates;
@@ -248,6 +250,8 @@ class Exporter {
   std::unordered_map<std::string, ContainerMeta> native_meta_;  // "ns/pod/container" (guarded by podres_mu_)
   // per device: pid -> (tick, mono ns) its waves were last seen resident (sampler thread only)
   std::vector<std::unordered_map<uint32_t, std::pair<uint64_t, int64_t>>> last_active_;
+  std::vector<std::unordered_set<uint32_t>> present_;  // per device: non-helper pids listed at the last tick
+  std::vector<std::string> sharing_source_;            // per device: what gpu_active_processes counted
   uint64_t pod_rows_built_ = 0;
   std::mutex meta_mu_;
   std::vector<ContainerMeta> cri_metas_, docker_metas_;  // last successful listing of each (meta_mu_)

@@ -330,7 +330,7 @@ bool MockBackend::processes(int i, std::vector<ProcSample>* out) {
     ns += static_cast<uint64_t>(util / 100.0 * p.gfx_share * 1e7);
     ps.gfx_ns = ns + static_cast<uint64_t>((mono_ns() - t0_ns_) * (util / 100.0) * p.gfx_share);
     ps.has_gfx_ns = !p.kfd_only;
-    ps.cu_occupancy = occ_value(i, p, util);
+    if (cfg_.occupancy) ps.cu_occupancy = occ_value(i, p, util);
     out->push_back(std::move(ps));
   }
   return true;
@@ -356,6 +356,23 @@ void MockBackend::occupancy(int i, const std::vector<uint32_t>& pids, std::vecto
         (*out)[k] = occ_value(i, p, util);
         break;
       }
+}
+
+bool MockBackend::occupancy_scan(int i, std::vector<OccRead>* out) {
+  std::lock_guard<std::mutex> g(mu_);
+  out->clear();
+  if (!cfg_.occupancy || i < 0 || i >= static_cast<int>(devs_.size())) return false;
+  const double util = has(forced_util_[i]) ? forced_util_[i]
+                                           : mock_util(cfg_, devs_[i].hip_id, (mono_ns() - t0_ns_) * 1e-9);
+  for (const auto& p : cfg_.procs)
+    if (p.device == devs_[i].hip_id) {
+      OccRead r;
+      r.pid = p.pid;
+      r.vram_bytes = p.vram_bytes;
+      r.cu_occupancy = occ_value(i, p, util);
+      out->push_back(r);
+    }
+  return true;
 }
 
 void MockBackend::set_occ_series(int dev, const std::vector<double>& values) {

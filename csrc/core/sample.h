@@ -202,6 +202,14 @@ struct ProcSample {
   int occ_busy = 0;             // of those, reads with waves resident (> 0): the process's busy share
 };
 
+// One between-ticks KFD read of a process on a device (Backend::occupancy_scan): lists processes
+// that arrived since the last tick too, so a new tenant is sub-sampled from its first interval.
+struct OccRead {
+  uint32_t pid = 0;
+  double cu_occupancy = kNaN;
+  double vram_bytes = kNaN;
+};
+
 // Derived per-device values computed from two consecutive samples.
 struct DeviceRates {
   bool valid = false;

@@ -4,6 +4,7 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "common.h"
@@ -216,6 +217,22 @@ int DrmFdTables::refresh_due(int max_scans) {
   return static_cast<int>(due.size());
 }
 
+void DrmFdTables::retain(const std::string& proc_root, const std::vector<uint32_t>& kfd_pids) {
+  const std::string prefix = proc_root + "/";
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto it = m_.begin(); it != m_.end();) {
+    const std::string& pdir = it->first;
+    if (!it->second.scanning && pdir.compare(0, prefix.size(), prefix) == 0) {
+      const uint32_t pid = static_cast<uint32_t>(strtoul(pdir.c_str() + prefix.size(), nullptr, 10));
+      if (!std::binary_search(kfd_pids.begin(), kfd_pids.end(), pid)) {
+        it = m_.erase(it);
+        continue;
+      }
+    }
+    ++it;
+  }
+}
+
 size_t DrmFdTables::size() {
   std::lock_guard<std::mutex> g(mu_);
   return m_.size();
@@ -291,9 +308,11 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out) {
   const std::string vram_name = "/vram_" + std::to_string(kfd_gpu_id_);
   const std::string occ_name = "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy";
   char b[64];
+  std::vector<uint32_t> listed;  // every KFD process of the node (any GPU)
   while (dirent* e = readdir(d)) {
     if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
     const uint32_t pid = static_cast<uint32_t>(strtoul(e->d_name, nullptr, 10));
+    listed.push_back(pid);
     const std::string pdir = kdir + "/" + e->d_name;
     size_t n = 0;
     if (!read_small(pdir + vram_name, b, sizeof b, &n)) continue;  // process not on this GPU
@@ -304,6 +323,32 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out) {
     if (read_small(pdir + occ_name, b, sizeof b, &n)) p.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
     fdinfo_usage(pid, &p);
     out->push_back(std::move(p));
+  }
+  closedir(d);
+  std::sort(listed.begin(), listed.end());
+  DrmFdTables::get().retain(proc_root_, listed);
+  return true;
+}
+
+bool SysfsGpu::occupancy_scan(std::vector<OccRead>* out) {
+  out->clear();
+  if (!kfd_gpu_id_) return false;
+  const std::string kdir = sys_root_ + "/class/kfd/kfd/proc/";
+  DIR* d = opendir(kdir.c_str());
+  if (!d) return false;
+  const std::string occ_name = "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy";
+  const std::string vram_name = "/vram_" + std::to_string(kfd_gpu_id_);
+  char b[64];
+  while (dirent* e = readdir(d)) {
+    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+    const std::string pdir = kdir + e->d_name;
+    size_t n = 0;
+    if (!read_small(pdir + vram_name, b, sizeof b, &n)) continue;  // not on this GPU
+    OccRead r;
+    r.pid = static_cast<uint32_t>(strtoul(e->d_name, nullptr, 10));
+    r.vram_bytes = static_cast<double>(strtoull(b, nullptr, 10));
+    if (read_small(pdir + occ_name, b, sizeof b, &n)) r.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
+    out->push_back(r);
   }
   closedir(d);
   return true;

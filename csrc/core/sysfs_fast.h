@@ -197,6 +197,9 @@ class SysfsGpu {
   bool processes(std::vector<ProcSample>* out);
   // Instantaneous KFD cu_occupancy of each pid on this GPU (NaN where the file is unreadable).
   void occupancy(const std::vector<uint32_t>& pids, std::vector<double>* out);
+  // Every KFD process on this GPU with its cu_occupancy and VRAM (no fdinfo): the between-ticks
+  // sub-sample, which also sees processes started since the last tick.
+  bool occupancy_scan(std::vector<OccRead>* out);
   bool have_kfd() const { return kfd_gpu_id_ != 0; }
   // Off-tick upkeep (device worker, after it published): refreshes due /proc/<pid>/fd scans.
   void maintain();
@@ -221,6 +224,9 @@ class DrmFdTables {
   void fds_for(const std::string& pdir, const std::string& render, std::vector<int>* out);
   void invalidate(const std::string& pdir);  // an fd vanished: rescan at the next maintain()
   int refresh_due(int max_scans);            // scans done
+  // Drop the tables of processes under `proc_root` that are no longer in the node's KFD process
+  // list (`kfd_pids`, sorted): a reused pid must not be read at the old process's fd numbers.
+  void retain(const std::string& proc_root, const std::vector<uint32_t>& kfd_pids);
   uint64_t scans() const { return scans_.load(); }
   size_t size();
 

@@ -43,7 +43,7 @@ class Config:
     ras_async: bool = True                # device workers read RAS after publishing a tick (next tick carries it)
     hide_empty_contexts: bool = True      # no pod_gpu row for a GPU context with no VRAM and no waves
     mfma_exclusive_window_s: float = 5.0  # pod MFMA util only when no other process had waves in the last 5 ticks and this many seconds
-    occ_samples: int = 10                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
+    occ_samples: int = 20                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
     rt_priority: int = 0                  # SCHED_FIFO priority of the sampler + device workers (needs CAP_SYS_NICE)
     device_timeout_s: float = 2.0         # a device call still running after this is exported as hung

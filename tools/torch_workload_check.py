@@ -11,7 +11,7 @@ The reference had no compute-side signal at all: device util copied onto every p
     python tools/torch_workload_check.py [--seconds 8] [--dtypes bf16,f16,fp8] > out.json
     python tools/torch_workload_check.py --shared [--seconds 10] > out.json
 
---shared: two bf16 GEMM tenants (8192^3 and 4096^3) on the same GPU at once, the reference
+--shared: two bf16 GEMM tenants (8192^3, then 4096^3 4 s later) on the same GPU, the reference
 dashboard's "(共享)" shared-GPU case. The exported device TFLOP/s must equal the sum of the two
 tenants' FLOPs over wall time; each tenant gets its own row (busy %, CU-equivalents), and
 pod_gpu_mfma_util_percent is absent (the device's MFMA util is not one pod's when shared).
@@ -75,11 +75,19 @@ def _shared(port, seconds):
     from gpumon.export import promtext
 
     sizes = (8192, 4096)
-    ts = [subprocess.Popen([sys.executable, "-c", TENANT, "bf16", str(seconds), str(n)], stdout=subprocess.PIPE,
-                           stderr=subprocess.PIPE, text=True) for n in sizes]
+    # staggered: the big tenant first, the small (~10 % resident) one `stagger` s later -- the
+    # arrival the exporter must not miss (GPUTEST_r02: one tick read 1 active process and gave the
+    # big tenant's row the device MFMA util while the small one already held VRAM)
+    stagger = 4.0
+    spawn = lambda n, secs: subprocess.Popen([sys.executable, "-c", TENANT, "bf16", str(secs), str(n)],
+                                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    ts = [spawn(sizes[0], seconds + stagger)]
+    t_second = time.time() + stagger
     ticks = []
-    deadline = time.time() + seconds + 60
+    deadline = time.time() + seconds + stagger + 60
     while any(t.poll() is None for t in ts) and time.time() < deadline:
+        if len(ts) == 1 and time.time() >= t_second:
+            ts.append(spawn(sizes[1], seconds))
         fam = promtext.parse(urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode())
         busy = {l["pid"]: v for _, l, v in fam.get("pod_gpu_proc_gfx_util", {}).get("samples", [])}
         cu = {l["pid"]: v for _, l, v in fam.get("pod_gpu_proc_cu_occupancy", {}).get("samples", [])}
@@ -88,11 +96,12 @@ def _shared(port, seconds):
                       "tflops": (promtext.values(fam, "gpu_mfma_tflops", gpu_id="0", dtype="bf16") or [None])[0],
                       "pod_mfma_util_rows": len(promtext.values(fam, "pod_gpu_mfma_util_percent", gpu_id="0")),
                       "active": (promtext.values(fam, "gpu_active_processes", gpu_id="0") or [None])[0],
+                      "vram_rows": sum(1 for v in mem.values() if v > 0),
                       # KFD reports host PIDs (not the tenants' pids inside a PID namespace): rows
                       # ranked by busy share, the bigger tenant first
                       "rows": sorted(({"busy": busy.get(p), "cu": cu.get(p), "mib": mem.get(p)} for p in busy),
                                      key=lambda r: -(r["busy"] or 0))})
-        time.sleep(1.0)
+        time.sleep(0.5)
     res = []
     for t in ts:
         so, se = t.communicate(timeout=120)
@@ -113,6 +122,10 @@ def _shared(port, seconds):
                              "cu": round(statistics.median([r[i]["cu"] for r in rows if r[i]["cu"] is not None] or [0]), 1)}
                             for i in range(2)] if rows else None,
             "pod_mfma_util_rows_max": max((k["pod_mfma_util_rows"] for k in inside), default=None),
+            # every scrape (not only those inside the timed window) with two tenants holding VRAM
+            "scrapes_two_vram_tenants": sum(1 for k in ticks if k["vram_rows"] >= 2),
+            "pod_mfma_rows_while_two_vram_tenants": sum(k["pod_mfma_util_rows"] for k in ticks if k["vram_rows"] >= 2),
+            "pod_mfma_rows_single_tenant": sum(k["pod_mfma_util_rows"] for k in ticks if k["vram_rows"] == 1),
             "active_processes": [k["active"] for k in inside]}
 
 
