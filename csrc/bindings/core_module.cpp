@@ -877,6 +877,8 @@ PYBIND11_MODULE(_core, m) {
       .def("mock_set_link_up",
            [](Exporter& e, int dev, int link, bool up) { mock_of(e)->set_link_up(dev, link, up); })
       .def("mock_link_calls", [](Exporter& e, int dev) { return mock_of(e)->link_calls(dev); })
+      .def("mock_set_link_fail",
+           [](Exporter& e, int dev, bool fail) { mock_of(e)->set_link_fail(dev, fail); })
       .def("mock_set_occ_series",
            [](Exporter& e, int dev, const std::vector<double>& v) { mock_of(e)->set_occ_series(dev, v); })
       .def("mock_occ_reads", [](Exporter& e, int dev) { return mock_of(e)->occ_reads(dev); })

@@ -333,6 +333,7 @@ bool AmdSmiBackend::init(std::string* err) {
                  std::to_string(devs_.size()));
   ras_readers_.clear();
   ras_readers_.resize(devs_.size());  // entry i is created and used by device i's worker only
+  ras_retry_.assign(devs_.size(), RasRetry{});
   return true;
 }
 
@@ -642,18 +643,28 @@ void AmdSmiBackend::sample_links(int i, DeviceSample* out) {
     caps_[i].links = false;
     return;
   }
-  if (st != AMDSMI_STATUS_SUCCESS) return;
-  int n = std::min<int>(static_cast<int>(lm.num_links), kMaxLinks);
-  for (int k = 0; k < n; ++k) {
-    auto& L = out->links[k];
-    const auto& s = lm.links[k];
-    L.peer_bdf = s.bdf.as_uint == ~0ull ? "" : bdf_str(s.bdf);
-    if (L.peer_bdf.rfind("ffffffffffff", 0) == 0) L.peer_bdf.clear();
-    L.bit_rate_gbps = ok32(s.bit_rate) ? s.bit_rate : kNaN;
-    L.max_bandwidth_gbps = ok32(s.max_bandwidth) ? s.max_bandwidth : kNaN;
-    L.link_type = static_cast<int>(s.link_type);
+  if (st != AMDSMI_STATUS_SUCCESS) {
+    out->links_read = -1;
+    return;
   }
-  if (n > out->n_links) out->n_links = n;
+  // Raw entries only: which gpu_metrics slot an entry describes is decided by the exporter from
+  // the two sources' accumulators (xgmi_map.cpp), not by position.
+  const int n = std::min<int>(static_cast<int>(lm.num_links), AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK);
+  out->link_entries.clear();
+  for (int k = 0; k < n; ++k) {
+    const auto& s = lm.links[k];
+    LinkEntry e;
+    e.peer_bdf = s.bdf.as_uint == ~0ull ? "" : bdf_str(s.bdf);
+    if (e.peer_bdf.rfind("ffffffffffff", 0) == 0) e.peer_bdf.clear();
+    e.bit_rate_gbps = ok32(s.bit_rate) ? s.bit_rate : kNaN;
+    e.max_bandwidth_gbps = ok32(s.max_bandwidth) ? s.max_bandwidth : kNaN;
+    e.link_type = static_cast<int>(s.link_type);
+    e.has_acc = ok64(s.read) && ok64(s.write);
+    e.read_kb = e.has_acc ? s.read : 0;
+    e.write_kb = e.has_acc ? s.write : 0;
+    out->link_entries.push_back(std::move(e));
+  }
+  out->links_read = 1;
 }
 
 // RAS: the kernel's ras/ text files first (no library call, readable by a non-root exporter, every
@@ -664,13 +675,23 @@ void AmdSmiBackend::sample_ras(int i, DeviceSample* out, int slice, int nslices)
   const int64_t t0 = mono_ns();
   if (c.ras_sysfs) {
     if (!ras_readers_[i]) ras_readers_[i] = std::make_unique<RasSysfsReader>(sys_root_, devs_[i].bdf);
+    if (static_cast<int>(ras_retry_.size()) < static_cast<int>(devs_.size())) ras_retry_.resize(devs_.size());
+    if (!ras_retry_[i].due()) return;  // backing off after a transient failure
     if (ras_readers_[i]->read(slice, nslices, &out->ras)) {
+      ras_retry_[i].ok();
       // a due file that failed keeps its last value: report the call failed so a stuck file shows
       // in gpumon_backend_call_errors_total{call="ras"} instead of freezing silently
       record_call(kCallRas, mono_ns() - t0, out->ras.stale_items == 0);
       return;
     }
-    c.ras_sysfs = false;  // no ras/ directory on this node: do not stat it every refresh
+    if (!ras_readers_[i]->missing()) {
+      // files listed but none readable this time (empty cache on the first pass): a transient
+      // failure must not switch ECC monitoring off for good
+      ras_retry_[i].failed();
+      record_call(kCallRas, mono_ns() - t0, false);
+      return;
+    }
+    c.ras_sysfs = false;  // no ras/ error-count files on this node: do not stat it every refresh
   }
   if (slice != 0 || !t_->amdsmi_get_gpu_ecc_count || !c.ecc_blocks) return;  // one library pass per cycle
   static const std::pair<amdsmi_gpu_block_t, const char*> kBlocks[] = {

@@ -15,11 +15,8 @@
 #include <tuple>
 #include <vector>
 
+#include "ras.h"
 #include "sample.h"
-
-namespace gpumon {
-class RasSysfsReader;
-}
 
 namespace gpumon {
 
@@ -129,6 +126,8 @@ struct MockConfig {
   int n_links = 7;
   double firmware_hz = 50.0;          // how fast the fake firmware table advances
   bool occupancy = true;              // KFD cu_occupancy readable (false: a node without the file)
+  std::string link_order = "index";   // link-metrics entry order: index | reverse | rotate
+  bool link_offset = false;           // entry counters with another origin than the table's (delta pairing only)
 };
 
 class MockBackend : public Backend {
@@ -166,6 +165,7 @@ class MockBackend : public Backend {
   void set_xgmi(int dev, int link, double gbps);
   void set_link_up(int dev, int link, bool up);  // firmware link status (0 down) of one xGMI slot
   uint64_t link_calls(int dev) const;            // sample_links() calls (link-metrics refreshes)
+  void set_link_fail(int dev, bool fail);        // link-metrics reads of `dev` fail (links_read -1)
   uint64_t calls(int dev) const;
 
  private:
@@ -179,6 +179,7 @@ class MockBackend : public Backend {
   std::vector<double> forced_xgmi_;  // per dev * kMaxLinks, GB/s (NaN = default)
   std::vector<char> link_down_;      // per dev * kMaxLinks
   std::vector<uint64_t> link_calls_;
+  std::vector<char> link_fail_;
   std::vector<uint64_t> calls_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
   std::vector<uint64_t> lim_acc_;  // per device x XCC x {ppt, thermal, any, low-util}
@@ -252,6 +253,7 @@ class AmdSmiBackend : public Backend {
   };
   std::vector<Caps> caps_;
   std::vector<std::unique_ptr<RasSysfsReader>> ras_readers_;  // per device, created on first use
+  std::vector<RasRetry> ras_retry_;                           // per device: transient-failure backoff
   std::vector<std::vector<char>> proc_buf_;  // reusable process-list buffers
 };
 
@@ -285,7 +287,8 @@ class RocmSmiBackend : public Backend {
   std::vector<DeviceStatic> devs_;
   std::vector<uint32_t> idx_;  // rsmi device index per exported device
   std::vector<std::unique_ptr<RasSysfsReader>> ras_readers_;
-  std::vector<char> ras_missing_;  // per device: no readable ras/ files (reset by init())
+  std::vector<char> ras_missing_;  // per device: no ras/ error-count files (reset by init())
+  std::vector<RasRetry> ras_retry_;  // per device: backoff after transient read failures
   std::string lib_version_;
   double energy_res_uj_ = 15.3;
 };

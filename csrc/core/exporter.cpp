@@ -19,6 +19,7 @@
 #include "http_client.h"
 #include "ondevice.h"
 #include "trace.h"
+#include "xgmi_map.h"
 
 namespace gpumon {
 
@@ -335,6 +336,8 @@ static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
     else if (k == "seed") base.seed = strtoull(v.c_str(), nullptr, 10);
     else if (k == "firmware_hz") base.firmware_hz = atof(v.c_str());
     else if (k == "occupancy") base.occupancy = atoi(v.c_str()) != 0;
+    else if (k == "link_order") base.link_order = v;
+    else if (k == "link_offset") base.link_offset = atoi(v.c_str()) != 0;
     else if (k == "unsupported") base.unsupported = split(v, ';');
   }
   return base;
@@ -415,6 +418,7 @@ bool Exporter::ensure_backend() {
     std::lock_guard<std::mutex> g(state_mu_);
     statics_ = st;
     prev_.assign(st.size(), DeviceSample{});
+    xgmi_maps_.assign(st.size(), XgmiSlotMap{});
     cur_.assign(st.size(), DeviceSample{});
     rates_.assign(st.size(), DeviceRates{});
     dev_errors_.assign(st.size(), 0);
@@ -891,11 +895,23 @@ TickInfo Exporter::tick() {
     }
     for (int i = 0; i < n; ++i) {
       DeviceSample& s = cur[i];
+      // A link refresh counts only if the device answered AND the link-metrics read succeeded: a
+      // timed-out or failed refresh keeps carrying the last identity and is retried next tick
+      // (one failed refresh tick used to drop peer labels for up to link_every ticks).
+      const bool asked_links = i < static_cast<int>(links_read_.size()) && links_read_[i];
+      const bool refreshed = asked_links && s.ok && s.links_read == 1;
+      if (asked_links && !refreshed && (!s.ok || s.links_read < 0) && i < static_cast<int>(force_links_.size()))
+        force_links_[i] = 1;
+      if (refreshed) {
+        // pair link-metrics entries with table slots by their accumulators, then label the slots
+        if (static_cast<int>(xgmi_maps_.size()) < n) xgmi_maps_.resize(n);
+        xgmi_maps_[i].update(s);
+        xgmi_maps_[i].apply(s.link_entries, &s);
+      }
       if (i < static_cast<int>(prev.size())) {
         const DeviceSample& p = prev[i];
         // keep link identity (peer bdf, max bw) between link refreshes -- but not on a tick that
         // re-read the links: an empty peer / unknown bandwidth then means the link lost them
-        const bool refreshed = i < static_cast<int>(links_read_.size()) && links_read_[i];
         if (!refreshed)
           for (int k = 0; k < kMaxLinks; ++k) {
             if (s.links[k].peer_bdf.empty()) s.links[k].peer_bdf = p.links[k].peer_bdf;
@@ -919,9 +935,9 @@ TickInfo Exporter::tick() {
         last.assign(kMaxLinks, -1);
         for (int k = 0; k < kMaxLinks; ++k) last[k] = s.links[k].status;
       }
-      // amdsmi_get_link_metrics lists 7 entries (incl. self) while the metrics table has 8 xGMI
-      // slots on MI355X: a slot without a link_metrics entry gets speed x width (38 Gb/s x 16 =
-      // 608 Gb/s, the value link_metrics reports for every other link).
+      // amdsmi_get_link_metrics lists 7 entries while the metrics table has 8 xGMI slots on
+      // MI355X: a slot no link_metrics entry describes gets speed x width (38 Gb/s x 16 = 608 Gb/s,
+      // the value link_metrics reports for every other link).
       const double lane = s.v[F_XGMI_LINK_SPEED], width = s.v[F_XGMI_LINK_WIDTH];
       for (int k = 0; k < s.n_links; ++k)
         if (s.links[k].status >= 0 && !has(s.links[k].max_bandwidth_gbps) && has(lane) && has(width))
@@ -953,6 +969,27 @@ TickInfo Exporter::tick() {
           }
         if (any || procs[i].empty()) s.v[F_CU_OCC] = cu;
       }
+    }
+    {
+      // how far the xGMI peer labels rest on traffic evidence (xgmi_map.h)
+      std::vector<ExtraSeries> xm;
+      for (int i = 0; i < n && i < static_cast<int>(xgmi_maps_.size()); ++i) {
+        const XgmiSlotMap& m = xgmi_maps_[i];
+        if (m.empty()) continue;
+        xm.push_back({"gpumon_xgmi_slot_map_mismatch",
+                      "xGMI link-metrics entries whose peer was paired by traffic with a gpu_metrics slot other "
+                      "than the entry's position (positional pairing would mislabel these peers).",
+                      "gauge", i, {}, static_cast<double>(m.mismatched())});
+        xm.push_back({"gpumon_xgmi_slot_map_verified",
+                      "xGMI link-metrics entries with a peer whose gpu_metrics slot was confirmed by matching "
+                      "accumulators (absolute or per-interval deltas).",
+                      "gauge", i, {}, static_cast<double>(m.verified())});
+        xm.push_back({"gpumon_xgmi_slot_map_unverified",
+                      "xGMI link-metrics entries with a peer whose slot no traffic has confirmed yet (idle or "
+                      "evenly loaded links): their peer label is positional or withheld.",
+                      "gauge", i, {}, static_cast<double>(m.unverified())});
+      }
+      set_extra("xgmi_map", std::move(xm));
     }
     int64_t tb = mono_ns();
     {

@@ -28,6 +28,7 @@
 #include "rates.h"
 #include "render.h"
 #include "snapshot.h"
+#include "xgmi_map.h"
 
 namespace gpumon {
 
@@ -250,6 +251,7 @@ class Exporter {
   std::unordered_map<std::string, ContainerMeta> native_meta_;  // "ns/pod/container" (guarded by podres_mu_)
   // per device: pid -> (tick, mono ns) its waves were last seen resident (sampler thread only)
   std::vector<std::unordered_map<uint32_t, std::pair<uint64_t, int64_t>>> last_active_;
+  std::vector<XgmiSlotMap> xgmi_maps_;                 // per device: link-metrics entry -> table slot
   std::vector<std::unordered_set<uint32_t>> present_;  // per device: non-helper pids listed at the last tick
   std::vector<std::string> sharing_source_;            // per device: what gpu_active_processes counted
   uint64_t pod_rows_built_ = 0;

@@ -4,6 +4,7 @@
 // lets the whole pipeline (sampler -> attribution -> render -> HTTP) run and be tested on a CPU
 // box: BASELINE config #1 "mock backend, 1 fake GPU, Prometheus /metrics on CPU".
 // Values follow MI355X shapes: 288 GiB HBM3E, 8 XCDs, 7 xGMI peer links, 1400 W limit.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <thread>
@@ -71,6 +72,7 @@ bool MockBackend::init(std::string* err) {
   forced_xgmi_.assign(n * kMaxLinks, kNaN);
   link_down_.assign(n * kMaxLinks, 0);
   link_calls_.assign(n, 0);
+  link_fail_.assign(n, 0);
   calls_.assign(n, 0);
   energy_.assign(n, 1000000);
   xgmi_rd_.assign(n * kMaxLinks, 0);
@@ -392,20 +394,44 @@ uint64_t MockBackend::occ_reads(int dev) const {
 void MockBackend::sample_links(int i, DeviceSample* out) {
   std::lock_guard<std::mutex> g(mu_);
   if (i >= 0 && i < static_cast<int>(link_calls_.size())) link_calls_[i]++;
-  int nl = std::min(cfg_.n_links + 1, kMaxLinks);
+  if (i >= 0 && i < static_cast<int>(link_fail_.size()) && link_fail_[i]) {
+    out->links_read = -1;  // injected link-metrics failure
+    return;
+  }
+  // one link-metrics entry per table slot (slot 0 = self: no peer), each with the slot's own
+  // accumulators; cfg_.link_order scrambles their order like a library that does not list them in
+  // table-slot order, cfg_.link_offset gives them another counter origin
+  const int nl = std::min(cfg_.n_links + 1, kMaxLinks);
+  std::vector<LinkEntry> es;
   for (int k = 0; k < nl; ++k) {
-    auto& L = out->links[k];
-    if (k == 0) continue;
+    LinkEntry e;
+    if (k == 0) {
+      es.push_back(std::move(e));
+      continue;
+    }
     char buf[32];
     int peer = (devs_[i].hip_id + k) % std::max(2, cfg_.gpus + 1);
     snprintf(buf, sizeof buf, "0000:%02x:00.0", 0x05 + 0x20 * peer);
     const bool down = link_down_[i * kMaxLinks + k] != 0;
-    L.peer_bdf = down ? "" : buf;  // a down link reports no peer (as amdsmi does)
-    L.bit_rate_gbps = down ? kNaN : 38;
-    L.max_bandwidth_gbps = down ? kNaN : 608;
-    L.link_type = 2;
+    e.peer_bdf = down ? "" : buf;  // a down link reports no peer (as amdsmi does)
+    e.bit_rate_gbps = down ? kNaN : 38;
+    e.max_bandwidth_gbps = down ? kNaN : 608;
+    e.link_type = 2;
+    e.has_acc = true;
+    const uint64_t off = cfg_.link_offset ? 1000000000ull * static_cast<uint64_t>(k) : 0;
+    e.read_kb = xgmi_rd_[i * kMaxLinks + k] + off;
+    e.write_kb = xgmi_wr_[i * kMaxLinks + k] + off;
+    es.push_back(std::move(e));
   }
-  if (nl > out->n_links) out->n_links = nl;
+  if (cfg_.link_order == "reverse") std::reverse(es.begin(), es.end());
+  else if (cfg_.link_order == "rotate" && !es.empty()) std::rotate(es.begin(), es.begin() + 1, es.end());
+  out->link_entries = std::move(es);
+  out->links_read = 1;
+}
+
+void MockBackend::set_link_fail(int dev, bool fail) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (dev >= 0 && dev < static_cast<int>(link_fail_.size())) link_fail_[dev] = fail ? 1 : 0;
 }
 
 }  // namespace gpumon

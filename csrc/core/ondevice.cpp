@@ -222,7 +222,10 @@ bool helper_spawn(const std::string& path, std::string* err) {
   posix_spawnattr_setsigmask(&sa, &none);
   posix_spawnattr_setsigdefault(&sa, &dflt);
   posix_spawnattr_setflags(&sa, POSIX_SPAWN_SETSIGMASK | POSIX_SPAWN_SETSIGDEF);
-  char* argv[] = {const_cast<char*>(path.c_str()), nullptr};
+  // the helper checks its parent against this pid, not against 1: the exporter may itself be
+  // PID 1 (ENTRYPOINT without hostPID), and an orphan under hostPID goes to a subreaper, not 1
+  std::string parent = "--parent-pid=" + std::to_string(::getpid());
+  char* argv[] = {const_cast<char*>(path.c_str()), const_cast<char*>(parent.c_str()), nullptr};
   pid_t pid = -1;
   const int rc = spawn_on_keeper([&] { return posix_spawn(&pid, path.c_str(), &fa, &sa, argv, environ); });
   posix_spawnattr_destroy(&sa);

@@ -12,6 +12,7 @@
 // libamd_smi, one slice per tick (RasSysfsReader), a full pass every `ras_every` ticks.
 #pragma once
 
+#include <algorithm>
 #include <string>
 #include <utility>
 #include <vector>
@@ -45,6 +46,9 @@ class RasSysfsReader {
   // read keeps its last value and counts in out->stale_items (the caller reports the call failed).
   bool read(int slice, int nslices, RasSample* out);
   int items() const { return static_cast<int>(files_.size()) + 2; }  // + event_state, bad pages
+  // The last directory scan found no error-count files (RAS off, VM guest, no such device): the
+  // only reason to stop reading. A false read() with files listed is transient (retry with backoff).
+  bool missing() const { return listed_ && files_.empty(); }
 
  private:
   bool list();
@@ -53,6 +57,23 @@ class RasSysfsReader {
   std::vector<std::pair<std::string, std::string>> files_;  // (block, file), one per block
   bool has_events_ = false, has_bad_pages_ = false;         // listed at the last directory scan
   RasSample cur_;
+};
+
+// Backoff after transient RAS read failures: skip 1, 3, 7, ... up to 63 refreshes, reset on success.
+struct RasRetry {
+  int fails = 0, skip = 0;
+  bool due() {
+    if (skip > 0) {
+      --skip;
+      return false;
+    }
+    return true;
+  }
+  void failed() {
+    ++fails;
+    skip = (1 << std::min(fails, 6)) - 1;
+  }
+  void ok() { fails = skip = 0; }
 };
 
 }  // namespace gpumon

@@ -180,6 +180,7 @@ bool RocmSmiBackend::init(std::string* err) {
              "loaded " + t_->path + " version=" + lib_version_ + " gpus=" + std::to_string(devs_.size()));
   ras_readers_.clear();
   ras_readers_.resize(devs_.size());
+  ras_retry_.assign(devs_.size(), RasRetry{});
   ras_missing_.assign(devs_.size(), 0);
   return true;
 }
@@ -265,12 +266,17 @@ void RocmSmiBackend::sample_ras(int i, DeviceSample* out, int slice, int nslices
   if (i < 0 || i >= static_cast<int>(devs_.size())) return;
   if (i < static_cast<int>(ras_missing_.size()) && ras_missing_[i]) return;  // no ras/ files on this node
   if (!ras_readers_[i]) ras_readers_[i] = std::make_unique<RasSysfsReader>(sys_root_, devs_[i].bdf);
+  if (static_cast<int>(ras_retry_.size()) < static_cast<int>(devs_.size())) ras_retry_.resize(devs_.size());
+  if (!ras_retry_[i].due()) return;  // backing off after a transient failure
   const int64_t t0 = mono_ns();
   const bool ok = ras_readers_[i]->read(slice, nslices, &out->ras);
-  if (!ok) {
-    // no error-count files (VM guest, RAS disabled) or none readable: stop re-listing the
-    // directory every tick (the amdsmi backend's caps.ras_sysfs does the same)
+  if (ok) {
+    ras_retry_[i].ok();
+  } else if (ras_readers_[i]->missing()) {
+    // no error-count files (VM guest, RAS disabled): stop re-listing the directory every tick
     if (i < static_cast<int>(ras_missing_.size())) ras_missing_[i] = 1;
+  } else {
+    ras_retry_[i].failed();  // files listed but none readable this time: retry with backoff
   }
   record_call(kCallRas, mono_ns() - t0, ok && out->ras.stale_items == 0);
 }

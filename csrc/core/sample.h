@@ -130,6 +130,19 @@ struct LinkInfo {
   int status = -1;                   // 0 down, 1 up, 2 disabled
 };
 
+// One entry of amdsmi_get_link_metrics (amdsmi.h amdsmi_link_metrics_t.links[]): peer identity
+// and per-link read / write KB in the same struct. Its ORDER is not the gpu_metrics table's xGMI
+// slot order (7 entries vs 8 slots on MI355X), so the exporter pairs entries with slots by their
+// accumulators (xgmi_map.h) before the identity lands on a slot's LinkInfo.
+struct LinkEntry {
+  std::string peer_bdf;              // "" = self / unknown
+  uint64_t read_kb = 0, write_kb = 0;
+  bool has_acc = false;
+  double bit_rate_gbps = kNaN;
+  double max_bandwidth_gbps = kNaN;
+  int link_type = -1;
+};
+
 // RAS / ECC error counters of one device (refreshed every `ras_every` ticks; the reference has no
 // health data at all). Source: the kernel's ras/ sysfs files (aca_<block> on MI300/MI355X, or
 // <block>_err_count), else amdsmi_get_gpu_ecc_count per block.
@@ -161,6 +174,8 @@ struct DeviceSample {
   int n_xcd = 0;
   int n_links = 0;
   std::array<LinkInfo, kMaxLinks> links;
+  std::vector<LinkEntry> link_entries;  // raw link-metrics entries, on a link-refresh tick only
+  int links_read = 0;                   // this tick's link-metrics read: 1 ok, -1 failed, 0 not made
   Accumulators acc;
   RasSample ras;                    // valid only on ticks that refreshed it (carried over otherwise)
   uint32_t errors = 0;              // failed calls this tick
@@ -177,6 +192,8 @@ struct DeviceSample {
     n_xcd = 0;
     n_links = 0;
     for (auto& l : links) l = LinkInfo{};
+    link_entries.clear();
+    links_read = 0;
     acc = Accumulators{};
     ras = RasSample{};
     errors = 0;

@@ -15,6 +15,9 @@
 //   FAKE_AMDSMI_ECC_UMC_CE=N      correctable UMC errors on device 0 (other ECC blocks: 0; only UMC,
 //                                 SDMA, GFX, MMHUB, XGMI_WAFL answer, as measured on MI355X)
 //   FAKE_AMDSMI_BAD_PAGES=N       bad-page records on device 0
+//   FAKE_AMDSMI_LINK_SLOTS=a,b,.. the gpu_metrics xGMI slot each amdsmi_get_link_metrics entry
+//                                 describes, in entry order (0 = self: no peer). Default
+//                                 0,1,2,3,4,5,6: 7 entries, positional, slot 7 undescribed
 // Counters advance deterministically per call so rates are checkable.
 #include <amd_smi/amdsmi.h>
 
@@ -28,6 +31,7 @@
 
 namespace {
 int g_gpus = 2, g_procs = 1, g_fail_metrics = -1, g_parts = 1;
+std::vector<int> g_link_slots;
 bool g_no_metrics = false;
 std::vector<uintptr_t> g_handles;
 std::atomic<uint64_t> g_calls[64];
@@ -52,6 +56,17 @@ amdsmi_status_t amdsmi_init(uint64_t) {
   g_fail_metrics = env_int("FAKE_AMDSMI_FAIL_METRICS", -1);
   g_no_metrics = env_int("FAKE_AMDSMI_NO_METRICS", 0) != 0;
   g_parts = env_int("FAKE_AMDSMI_CPX", 0) ? 8 : 1;
+  g_link_slots = {0, 1, 2, 3, 4, 5, 6};
+  if (const char* ls = getenv("FAKE_AMDSMI_LINK_SLOTS")) {
+    g_link_slots.clear();
+    for (const char* p = ls; *p;) {
+      char* end = nullptr;
+      const long v = strtol(p, &end, 10);
+      if (end == p) break;
+      g_link_slots.push_back(static_cast<int>(v));
+      p = *end == ',' ? end + 1 : end;
+    }
+  }
   g_handles.clear();
   for (int i = 0; i < g_gpus * g_parts; ++i) g_handles.push_back(0x1000 + i);
   for (auto& c : g_calls) c = 0;
@@ -221,19 +236,25 @@ amdsmi_status_t amdsmi_get_gpu_process_list(amdsmi_processor_handle h, uint32_t*
 }
 
 amdsmi_status_t amdsmi_get_link_metrics(amdsmi_processor_handle h, amdsmi_link_metrics_t* lm) {
+  const int d = dev_of(h);
+  if (d < 0) return AMDSMI_STATUS_INVAL;
   memset(lm, 0, sizeof *lm);
-  lm->num_links = 7;
-  for (int k = 0; k < 7; ++k) {
+  const uint64_t n = g_calls[d];  // the table this tick's gpu_metrics call returned
+  lm->num_links = static_cast<uint32_t>(g_link_slots.size());
+  for (size_t j = 0; j < g_link_slots.size(); ++j) {
+    const int k = g_link_slots[j];  // slot k of the table: k GB/s read, k/2 GB/s write (fake_metrics.h)
+    auto& L = lm->links[j];
     if (k == 0) {
-      lm->links[k].bdf.as_uint = ~0ull;  // self / unknown, as on MI355X
+      L.bdf.as_uint = ~0ull;  // self / unknown, as on MI355X
     } else {
-      lm->links[k].bdf.bus_number = 0x40 + k;
+      L.bdf.bus_number = 0x40 + k;
+      L.read = n * 1000000ull * k;
+      L.write = n * 500000ull * k;
     }
-    lm->links[k].bit_rate = 38;
-    lm->links[k].max_bandwidth = 608;
-    lm->links[k].link_type = AMDSMI_LINK_TYPE_XGMI;
+    L.bit_rate = 38;
+    L.max_bandwidth = 608;
+    L.link_type = AMDSMI_LINK_TYPE_XGMI;
   }
-  (void)h;
   return AMDSMI_STATUS_SUCCESS;
 }
 

@@ -15,6 +15,7 @@
 #include <cerrno>
 #include <csignal>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -115,9 +116,14 @@ double now_s() {
 
 }  // namespace
 
-int main() {
+int main(int argc, char** argv) {
   prctl(PR_SET_PDEATHSIG, SIGKILL);
-  if (getppid() == 1) return 0;  // parent already gone
+  // Parent already gone before PDEATHSIG was armed: the exporter passes its pid (a getppid() == 1
+  // test is always true when the exporter is PID 1 itself, and misses reparenting to a subreaper).
+  long parent = 0;
+  for (int i = 1; i < argc; ++i)
+    if (!strncmp(argv[i], "--parent-pid=", 13)) parent = strtol(argv[i] + 13, nullptr, 10);
+  if (parent > 0 ? getppid() != static_cast<pid_t>(parent) : getppid() == 1) return 0;
   signal(SIGPIPE, SIG_IGN);
   char err[512];
   for (;;) {

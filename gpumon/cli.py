@@ -26,7 +26,7 @@ import sys
 import threading
 import time
 
-from .config import Config, add_cli_args, from_args
+from .config import Config, add_cli_args, from_args, redact_url
 
 
 def _setup_logging(level: str):
@@ -42,7 +42,7 @@ def cmd_serve(args) -> int:
     mon = GpuMonitor(cfg).start()
     log = logging.getLogger("gpumon")
     log.info("serving %s backend=%s host=%s interval=%.3fs influx=%s control_plane=%s", mon.url, cfg.backend,
-             cfg.resolved_host(), cfg.interval, cfg.influx_url or "-", bool(mon.plane))
+             cfg.resolved_host(), cfg.interval, redact_url(cfg.influx_url) or "-", bool(mon.plane))
     stop = threading.Event()
     for s in (signal.SIGINT, signal.SIGTERM):
         signal.signal(s, lambda *_: stop.set())

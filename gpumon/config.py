@@ -199,6 +199,22 @@ class Config:
         return self
 
 
+def redact_url(url: str) -> str:
+    """`user:password@` userinfo with the password masked (same rule as the native redact_url in
+    csrc/core/http_client.cpp): INFLUXDB_URL may carry 1.x credentials and is logged at startup."""
+    scheme = url.find("://")
+    start = 0 if scheme < 0 else scheme + 3
+    ends = [i for i in (url.find("/", start), url.find("?", start)) if i >= 0]
+    end = min(ends) if ends else len(url)
+    at = url.rfind("@", 0, end + 1 if ends else len(url))
+    if at < start:
+        return url
+    colon = url.find(":", start)
+    if colon < 0 or colon > at:
+        return url
+    return url[:colon + 1] + "***" + url[at:]
+
+
 def _version() -> str:
     from . import __version__
 

@@ -149,6 +149,37 @@ def test_url_parsing_auth_and_v6(core):
     assert core.redact_url("http://h/write?u=a@b") == "http://h/write?u=a@b"
 
 
+def test_python_redact_matches_native(core):
+    from gpumon.config import redact_url
+
+    for u in ("http://u:secret@h:1/write?db=x", "http://u@h/write", "http://h/write?u=a@b", "", "h:1",
+              "http://u:p@ss@h/write", "http://u:pw@h?db=x", "u:pw@h", "http://u:pw@[fd00::1]:8086/write",
+              "http://h:8086/write?db=x", "http://a:b@h/x/y@z"):
+        assert redact_url(u) == core.redact_url(u), u
+
+
+def test_serve_never_logs_the_influx_password(tmp_path):
+    """`gpumon serve` (the image's ENTRYPOINT) logged INFLUXDB_URL in full at INFO, so
+    1.x credentials in the URL reached the pod logs. Both the Python startup line and the native
+    exporter's logs must show the password masked."""
+    import signal
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, INFLUXDB_URL="http://gpumon:s3cr3tPW@127.0.0.1:1/write?db=k8s", PYTHONPATH=root)
+    p = subprocess.Popen([sys.executable, "-m", "gpumon", "serve", "--backend", "mock:gpus=1", "--listen",
+                          "127.0.0.1:0", "--interval", "0.2", "--control-plane", "off", "--log-level", "debug"],
+                         cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    time.sleep(3.0)
+    p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=30)
+    text = out + err
+    assert "serving" in text, text[-2000:]
+    assert "s3cr3tPW" not in text, text[-2000:]
+    assert "gpumon:***@127.0.0.1" in text, text[-2000:]
+
+
 class _AuthSink(_Sink):
     auth = []
 

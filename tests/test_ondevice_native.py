@@ -692,3 +692,21 @@ def test_own_helper_is_not_a_workload_or_a_sharer(core, mock_exporter, monkeypat
         assert "gpumon_ondevice_helper_gpu_contexts" in m and f'pid="{helper}"' not in m
     finally:
         od.stop()
+
+
+def test_helper_checks_its_parent_by_pid():
+    """the helper used `getppid() == 1` as "parent already gone" -- always true when the
+    exporter is PID 1 itself (ENTRYPOINT without hostPID), so PMC and probe never started there. The
+    exporter now passes its pid; the helper exits only if its parent is not that process."""
+    import time
+
+    helper = os.path.join(FAKE_DIR, "gpumon-ondevice-helper")
+    gone = subprocess.Popen([helper, "--parent-pid=1"], stdin=subprocess.PIPE, stdout=subprocess.PIPE)
+    assert gone.wait(10) == 0  # its parent (this process) is not pid 1's stand-in: already gone
+    alive = subprocess.Popen([helper, f"--parent-pid={os.getpid()}"], stdin=subprocess.PIPE, stdout=subprocess.PIPE)
+    try:
+        time.sleep(0.5)
+        assert alive.poll() is None  # parent matches: serves requests
+    finally:
+        alive.stdin.close()  # EOF on the request pipe: clean exit
+        assert alive.wait(10) == 0

@@ -229,3 +229,47 @@ def test_async_ras_is_off_the_tick_path(mock_exporter):
     sync.tick()
     fam = promtext.parse(sync.metrics_text())
     assert promtext.one(fam, "gpu_ecc_errors_total", block="umc", type="uncorrectable") == 3
+
+
+@pytest.mark.parametrize("backend", ["amdsmi", "rocm_smi"])
+def test_transient_first_read_failure_does_not_switch_ras_off(core, monkeypatch, tmp_path, backend):
+    """a first pass whose listed files could not be read (empty cache, a file briefly
+    unreadable) latched the device's sysfs RAS off until re-init -- the amdsmi backend then fell
+    back to library ECC calls for good, the rocm_smi one stopped reading RAS at all. Only a
+    directory without error-count files may do that; a transient failure is retried with backoff."""
+    from test_rocm_smi_fake import FAKE_RSMI
+
+    sysr, procr = make_tree(tmp_path, gpus=1)
+    r = _ras_dir(sysr)
+    (r / "aca_umc").mkdir()  # listed, but reading it fails (EISDIR) on the first pass
+    over = {"ras_every": 1, "ras_async": False}
+    if backend == "rocm_smi":
+        over.update(backend="rocm_smi", rocm_smi_lib=FAKE_RSMI)
+    ex = _exporter(core, monkeypatch, sysr, procr, env={"FAKE_AMDSMI_GPUS": 1, "FAKE_RSMI_GPUS": 1}, **over)
+    try:
+        ex.tick()
+        assert ex.self_stats()["backend_calls"]["ras"]["errors"] >= 1
+        (r / "aca_umc").rmdir()
+        (r / "aca_umc").write_text("ue: 0\nce: 9\nde: 0\n")
+        for _ in range(3):  # one pass skipped (backoff), then read again
+            ex.tick()
+        s = ex.samples()[0]["ras"]
+        assert s["source"] == "sysfs" and s["blocks"]["umc"]["ce"] == 9, s
+    finally:
+        ex.stop()
+
+
+def test_ras_retry_backoff_is_bounded(core, monkeypatch, tmp_path):
+    """Files that stay unreadable are retried ever more rarely (skip 1, 3, 7, ... 63 passes)."""
+    sysr, procr = make_tree(tmp_path, gpus=1)
+    r = _ras_dir(sysr)
+    (r / "aca_umc").mkdir()
+    ex = _exporter(core, monkeypatch, sysr, procr, env={"FAKE_AMDSMI_GPUS": 1}, ras_every=1, ras_async=False)
+    try:
+        for _ in range(40):
+            ex.tick()
+        st = ex.self_stats()["backend_calls"]["ras"]
+        assert 3 <= st["n"] <= 6, st  # passes at ticks 0, 2, 6, 14, 30 -- not 40
+        assert (ex.samples()[0]["ras"] or {}).get("source") != "amdsmi"  # never latched to the fallback
+    finally:
+        ex.stop()
