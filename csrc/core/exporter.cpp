@@ -820,7 +820,11 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       r.occ_samples = p.occ_samples;
       if (sole[d] == p.pid)
         if (auto m = mfma.find(static_cast<int>(d)); m != mfma.end()) r.mfma_util = m->second;
-      active.emplace_back(r.pod_namespace, r.pod_name, r.container, r.dev);
+      // only a process attributed to a pod or container can stand in for its idle allocation row
+      // (an unattributed host process reads "-" / "-" and must not swallow the allocation of a pod
+      // whose name was unknown, also "-")
+      if (r.pod_name != "-" || r.containerid != "-")
+        active.emplace_back(r.pod_namespace, r.pod_name, r.container, r.dev);
       row_of_pid[p.pid] = rows->size();
       rows->push_back(std::move(r));
     }
