@@ -649,7 +649,11 @@ void AmdSmiBackend::sample_links(int i, DeviceSample* out) {
   }
   // Raw entries only: which gpu_metrics slot an entry describes is decided by the exporter from
   // the two sources' accumulators (xgmi_map.cpp), not by position.
-  const int n = std::min<int>(static_cast<int>(lm.num_links), AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK);
+  // Measured on MI355X (ROCm 7.2, profiles/r3_xgmi_link_metrics.md): num_links reads 7 while the
+  // library fills 8 entries -- self (bdf all-ones) plus the 7 peers -- so trusting num_links drops
+  // the last peer. Entries past num_links that the library filled (non-zero bdf / rate) count too.
+  int n = std::min<int>(static_cast<int>(lm.num_links), AMDSMI_MAX_NUM_XGMI_PHYSICAL_LINK);
+  while (n < AMDSMI_MAX_NUM_XGMI_LINKS && (lm.links[n].bdf.as_uint != 0 || lm.links[n].bit_rate != 0)) ++n;
   out->link_entries.clear();
   for (int k = 0; k < n; ++k) {
     const auto& s = lm.links[k];

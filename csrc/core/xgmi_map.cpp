@@ -44,8 +44,24 @@ void XgmiSlotMap::update(const DeviceSample& s) {
   std::vector<int> match(n, -1);
   for (size_t j = 0; j < n; ++j) {
     if (!has_peer_[j] || !e[j].has_acc) continue;
-    // 1. absolute counters (same instant, same accumulators if the library reads the table)
+    // 1. absolute counters: libamd_smi fills the entries from the same firmware table (measured on
+    // MI355X: every entry equals its slot to the KB), so one slot with IDENTICAL counters pairs it
+    // (idle links keep their counts between the two reads); else one slot within the traffic the
+    // link can move between the reads
     int found = -1, count = 0;
+    if (e[j].read_kb + e[j].write_kb > 0) {
+      for (int k = 0; k < nslots; ++k)
+        if (slot_ok(k) && e[j].read_kb == a.xgmi_rd_kb[k] && e[j].write_kb == a.xgmi_wr_kb[k]) {
+          found = k;
+          ++count;
+        }
+      if (count == 1) {
+        match[j] = found;
+        continue;
+      }
+    }
+    found = -1;
+    count = 0;
     for (int k = 0; k < nslots; ++k)
       if (slot_ok(k) && close_abs(e[j].read_kb, a.xgmi_rd_kb[k]) && close_abs(e[j].write_kb, a.xgmi_wr_kb[k])) {
         found = k;

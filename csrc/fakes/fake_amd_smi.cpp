@@ -17,10 +17,14 @@
 //   FAKE_AMDSMI_BAD_PAGES=N       bad-page records on device 0
 //   FAKE_AMDSMI_LINK_SLOTS=a,b,.. the gpu_metrics xGMI slot each amdsmi_get_link_metrics entry
 //                                 describes, in entry order (0 = self: no peer). Default
-//                                 0,1,2,3,4,5,6: 7 entries, positional, slot 7 undescribed
+//                                 0,1,2,3,4,5,6,7: what ROCm 7.2 returns on MI355X (self + 7 peers,
+//                                 positional, counters equal to the table's)
+//   FAKE_AMDSMI_LINK_NUM=N        num_links reported (default: entries - 1, i.e. 7 for 8 entries,
+//                                 as measured: the count leaves out the self entry it fills)
 // Counters advance deterministically per call so rates are checkable.
 #include <amd_smi/amdsmi.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -32,6 +36,7 @@
 namespace {
 int g_gpus = 2, g_procs = 1, g_fail_metrics = -1, g_parts = 1;
 std::vector<int> g_link_slots;
+int g_link_num = -1;
 bool g_no_metrics = false;
 std::vector<uintptr_t> g_handles;
 std::atomic<uint64_t> g_calls[64];
@@ -56,7 +61,8 @@ amdsmi_status_t amdsmi_init(uint64_t) {
   g_fail_metrics = env_int("FAKE_AMDSMI_FAIL_METRICS", -1);
   g_no_metrics = env_int("FAKE_AMDSMI_NO_METRICS", 0) != 0;
   g_parts = env_int("FAKE_AMDSMI_CPX", 0) ? 8 : 1;
-  g_link_slots = {0, 1, 2, 3, 4, 5, 6};
+  g_link_slots = {0, 1, 2, 3, 4, 5, 6, 7};
+  g_link_num = env_int("FAKE_AMDSMI_LINK_NUM", -1);
   if (const char* ls = getenv("FAKE_AMDSMI_LINK_SLOTS")) {
     g_link_slots.clear();
     for (const char* p = ls; *p;) {
@@ -240,7 +246,7 @@ amdsmi_status_t amdsmi_get_link_metrics(amdsmi_processor_handle h, amdsmi_link_m
   if (d < 0) return AMDSMI_STATUS_INVAL;
   memset(lm, 0, sizeof *lm);
   const uint64_t n = g_calls[d];  // the table this tick's gpu_metrics call returned
-  lm->num_links = static_cast<uint32_t>(g_link_slots.size());
+  lm->num_links = static_cast<uint32_t>(g_link_num >= 0 ? g_link_num : std::max<int>(0, g_link_slots.size() - 1));
   for (size_t j = 0; j < g_link_slots.size(); ++j) {
     const int k = g_link_slots[j];  // slot k of the table: k GB/s read, k/2 GB/s write (fake_metrics.h)
     auto& L = lm->links[j];

@@ -7,8 +7,9 @@ DaemonSet deployment, NODE_NAME / INFLUXDB_URL configuration) re-designed for AM
   Influx renderers, epoll HTTP server).  Built in-tree by ``make`` / ``__graft_entry__.build()``.
 * ``gpumon._hip``   — hand-written gfx950 HIP kernels: on-device probe (per-XCD clock, dispatch
   latency, pinned ring buffer) and synthetic MFMA / HBM load generators.
-* ``gpumon.attribution`` — CRI + kubelet PodResources control plane (pod/namespace/user labels,
-  allocated-but-idle GPUs).
+  The core also holds the k8s control plane: CRI + kubelet PodResources (+ opt-in Docker) pollers
+  for pod / namespace / user labels and allocated-but-idle GPUs (csrc/core/grpc_lite.cpp).
+* ``gpumon.monitor`` / ``gpumon.cli`` — config, ``gpumon serve|once|top|doctor|...``.
 * ``gpumon.parallel`` — RCCL/xGMI load generators used to validate the per-link xGMI counters.
 """
 

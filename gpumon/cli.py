@@ -4,7 +4,6 @@
     gpumon once    [--format prom|influx|json]                                       one sample to stdout
     gpumon top     [--interval 1]                                                    live console table
     gpumon scrape  URL [-n 1000] [-c 4]                                              scrape-latency probe
-    gpumon demo    [--gpus 8]                                                        mock node + fake kubelet
     gpumon probe   [--blocks 1024]                                                   run the K1 probe once
     gpumon load    [--kind mixed --seconds 10]                                       synthetic gfx950 load
     gpumon xgmi    [--pairs 0:1,1:0 | --all-pairs] [--seconds 2]                     xGMI link-map validation
@@ -175,35 +174,6 @@ def cmd_scrape(args) -> int:
     return 0 if r["errors"] == 0 else 1
 
 
-def cmd_demo(args) -> int:
-    """Mock node with a fake kubelet/CRI: the full pod_gpu path without a cluster."""
-    import tempfile
-
-    from .attribution.fake_kubelet import FakeKubelet, FakePod
-    from .monitor import GpuMonitor
-
-    d = tempfile.mkdtemp(prefix="gpumon-demo-")
-    k = FakeKubelet(podres_socket=f"{d}/kubelet.sock", cri_socket=f"{d}/cri.sock").start()
-    cid = "%064x" % 0xC0FFEE
-    k.pods = [FakePod("turing-gpu-notebook-alice-5d8f-x1", "ml", "uid-alice", labels={"mlgpu": "mlgpu"},
-                      containers={"notebook": (cid, ["0000:05:00.0"])}),
-              FakePod("jupyter-q-0", "research", "uid-q", containers={"main": ("%064x" % 0xBEEF, ["0000:25:00.0"])})]
-    cfg = Config(backend=f"mock:gpus={args.gpus}", listen=args.listen, interval=args.interval,
-                 cri_socket=k.cri_socket, pod_resources_socket=k.podres_socket, metadata_refresh=2.0)
-    mon = GpuMonitor(cfg).start()
-    mon.ex.mock_set_procs([{"pid": os.getpid(), "device": 0, "name": "python train.py", "vram_bytes": 12 << 30}])
-    print(f"demo exporter at {mon.url} (fake kubelet in {d}); Ctrl-C to stop", flush=True)
-    stop = threading.Event()
-    for s in (signal.SIGINT, signal.SIGTERM):
-        signal.signal(s, lambda *_: stop.set())
-    end = time.time() + args.seconds if args.seconds > 0 else float("inf")
-    while not stop.wait(0.5) and time.time() < end:
-        pass
-    mon.stop()
-    k.stop()
-    return 0
-
-
 def cmd_probe(args) -> int:
     from ._native import hip
 
@@ -283,12 +253,6 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--gzip", action="store_true")
     s.add_argument("--no-keepalive", action="store_true")
     s.set_defaults(fn=cmd_scrape)
-    s = sub.add_parser("demo", help="mock node + fake kubelet")
-    s.add_argument("--gpus", type=int, default=8)
-    s.add_argument("--listen", default="127.0.0.1:9400")
-    s.add_argument("--interval", type=float, default=1.0)
-    s.add_argument("--seconds", type=float, default=0)
-    s.set_defaults(fn=cmd_demo)
     s = sub.add_parser("probe", help="run the gfx950 probe kernel once")
     s.add_argument("--device", type=int, default=0)
     s.add_argument("--blocks", type=int, default=1024)

@@ -75,7 +75,7 @@ class Config:
     procfs_env_fallback: bool = True
     include_host_processes: bool = True
     # control plane (k8s)
-    control_plane: str = "native"         # native (C++ grpc_lite pollers: production) | python (grpcio clients: test oracle) | off
+    control_plane: str = "native"         # native (C++ grpc_lite CRI / PodResources / Docker pollers) | off
     cri_socket: str = ""                  # e.g. unix:///run/containerd/containerd.sock ; "" = autodetect
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     docker_socket: str = ""               # plain-Docker nodes (native plane): Docker Engine container names + labels; opt-in, e.g. /var/run/docker.sock
@@ -87,10 +87,9 @@ class Config:
     enable_probe: bool = False
     probe_every: int = 1
     enable_pmc: bool = False
-    ondevice: str = "native"              # native (C++ samplers over lib/ plugins) | python (gpumon/ops runners)
     plugin_dir: str = ""                  # "" = <tree>/lib or $GPUMON_PLUGIN_DIR
     roctx: bool = False                   # ROCTx ranges around sampler phases (rocprofv3 --marker-trace)
-    # the counters gpumon.ops.pmc.derive() needs (8 SQ + 2 GRBM slots: one counting pass on gfx950):
+    # the counters the PMC derivation needs (csrc/core/ondevice.cpp; 8 SQ + 2 GRBM slots: one counting pass on gfx950):
     # MFMA busy + MFMA MOPS per operand type; no per-wave SQ counters (they count only the profiling
     # process's own waves, profiles/r1_pmc_cross_process.md)
     # continuous: counting contexts run all the time, read without a stop (100 % coverage);
@@ -177,6 +176,8 @@ class Config:
         names = {f.name: f for f in dataclasses.fields(self)}
         for k, v in (d or {}).items():
             key = k.replace("-", "_")
+            if key in _RETIRED:
+                continue  # accepted, no effect (see _RETIRED)
             if key not in names:
                 raise ValueError(f"unknown config key: {k}")
             setattr(self, key, _coerce(names[key], v))
@@ -197,6 +198,11 @@ class Config:
                 if key in names:
                     setattr(self, key, _coerce(names[key], v))
         return self
+
+
+# Keys of earlier releases that selected the Python test oracles (now under tests/oracles, not
+# shipped): a config file that still names them keeps working, with the native path.
+_RETIRED = {"ondevice"}
 
 
 def redact_url(url: str) -> str:
@@ -275,8 +281,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--docker-socket", dest="docker_socket",
                    help="plain-Docker nodes: read container names/labels from the Docker Engine API (opt-in)")
     p.add_argument("--pod-resources-socket", dest="pod_resources_socket")
-    p.add_argument("--control-plane", dest="control_plane", choices=["python", "native", "off"],
-                   help="who polls kubelet PodResources / CRI: python (grpcio) or native (C++, no grpcio)")
+    p.add_argument("--control-plane", dest="control_plane", choices=["native", "off"],
+                   help="kubelet PodResources / CRI / Docker metadata pollers: native (C++) or off")
     p.add_argument("--no-processes", dest="processes", action="store_false", default=None)
     p.add_argument("--no-gzip", dest="gzip", action="store_false", default=None)
     p.add_argument("--sample-threads", dest="sample_threads", type=int)
@@ -285,8 +291,6 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
                    help="seconds before a device call is exported as hung (gpu_up 0)")
     p.add_argument("--enable-probe-kernel", dest="enable_probe", action="store_true", default=None)
     p.add_argument("--enable-pmc", dest="enable_pmc", action="store_true", default=None)
-    p.add_argument("--ondevice", dest="ondevice", choices=["native", "python"],
-                   help="who drives the PMC / probe samplers: native (C++ threads over lib/ plugins) or python")
     p.add_argument("--plugin-dir", dest="plugin_dir", help="directory holding libgpumon_pmc.so / libgpumon_probe.so")
     p.add_argument("--no-fast-path", dest="fast_path", action="store_false", default=None,
                    help="amdsmi: read every value through libamd_smi (disable the sysfs/KFD fast path)")

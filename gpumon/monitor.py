@@ -24,8 +24,7 @@ log = logging.getLogger("gpumon")
 _LEVELS = {"debug": 0, "info": 1, "warn": 2, "warning": 2, "error": 3, "off": 4}
 
 
-# well-known CRI sockets (gpumon/attribution/clients.py DEFAULT_CRI_SOCKETS; kept here so the
-# native path needs no grpcio import)
+# well-known CRI sockets (the native pollers take the first that exists)
 _CRI_SOCKETS = ("/run/containerd/containerd.sock", "/var/run/containerd/containerd.sock", "/var/run/crio/crio.sock",
                 "/run/crio/crio.sock", "/var/run/cri-dockerd.sock", "/var/run/dockershim.sock")
 
@@ -37,12 +36,11 @@ class GpuMonitor:
         self._core.set_log_level(_LEVELS.get(self.cfg.log_level.lower(), 1))
         core_cfg = self.cfg.to_core()
         mode = self.cfg.control_plane if control_plane else "off"
-        if mode == "python":
-            try:
-                import grpc  # noqa: F401
-            except ImportError:
-                log.warning("grpcio not importable: using the native CRI/PodResources pollers")
-                mode = "native"
+        if mode not in ("native", "off"):
+            # control_plane: python selected the grpcio test oracle of earlier releases (now under
+            # tests/oracles, not shipped): the native pollers do the same work
+            log.warning("control_plane=%s is not available in the exporter: using native", mode)
+            mode = "native"
         if mode == "native":
             # the exporter's own C++ pollers (csrc/core/grpc_lite.cpp) -- same as bin/gpumon-exporter
             if os.path.exists(self.cfg.pod_resources_socket):
@@ -57,70 +55,41 @@ class GpuMonitor:
             if self.cfg.resource_names:
                 core_cfg["pod_resources_prefix"] = self.cfg.resource_names[0]
             core_cfg["pod_resources_dra_drivers"] = list(self.cfg.dra_drivers)
-        if self.cfg.docker_socket and mode != "native":
-            log.warning("docker_socket is read by the native control plane only; control_plane=%s ignores it", mode)
         self.control_plane_mode = mode
         self.ex = self._core.Exporter(core_cfg)
-        self.plane = None
-        self.probe = None
-        self.pmc = None
-        self.ondevice = None   # _core.OnDevice when cfg.ondevice == "native"
-        self._want_plane = mode == "python"
+        self.plane = None      # kept for callers that check it: the control plane is in the core
+        self.ondevice = None   # _core.OnDevice: PMC / probe samplers
         self.start_error = ""
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "GpuMonitor":
-        # native on-device samplers first: the PMC helper process is spawned before anything in
-        # this process touches the GPU; the samplers pick the devices up once the backend lists
-        # them. The Python runners (test oracle) need the device list, so they start after.
-        ondevice = self.cfg.enable_pmc or self.cfg.enable_probe
-        if ondevice and self.cfg.ondevice == "native":
+        # the on-device samplers first: the PMC helper process is spawned before anything in this
+        # process touches the GPU; the samplers pick the devices up once the backend lists them
+        if self.cfg.enable_pmc or self.cfg.enable_probe:
             self._start_ondevice()
         self.start_error = self.ex.start()
-        if ondevice and self.cfg.ondevice != "native":
-            self._start_ondevice()
         if self.start_error:
             log.warning("backend not ready yet (will retry): %s", self.start_error)
-        if self._want_plane:
-            from .attribution.plane import ControlPlane
-
-            plane = ControlPlane(self.ex, self.cfg)
-            if plane.enabled:
-                self.plane = plane.start()
         return self
 
     def _start_ondevice(self) -> None:
         period = max(self.cfg.interval, 0.1)
-        if self.cfg.ondevice == "native":
-            # C++ threads over the same plugins the standalone binary dlopen()s (csrc/core/ondevice.h);
-            # PMC initialises before the probe (rocprofiler must register before HIP brings HSA up).
-            self.ondevice = self._core.OnDevice(self.ex, {
-                "plugin_dir": self.cfg.plugin_dir, "pmc": bool(self.cfg.enable_pmc),
-                "pmc_counters": list(self.cfg.pmc_counters), "pmc_every_s": period, "pmc_mode": self.cfg.pmc_mode,
-                "ondevice_isolate": self.cfg.ondevice_isolate, "helper_retry_s": float(self.cfg.helper_retry),
-                "probe": bool(self.cfg.enable_probe), "probe_every_s": period * self.cfg.probe_every})
-            self.ondevice.start()
-            return
-        # PMC first: rocprofiler must register before anything in this process initialises HSA/HIP.
-        if self.cfg.enable_pmc:
-            from .ops.pmc import PmcRunner
-
-            self.pmc = PmcRunner(self.ex, self.cfg.pmc_counters, every_s=period).start()
-        if self.cfg.enable_probe:
-            from .ops.probe import ProbeRunner
-
-            self.probe = ProbeRunner(self.ex, every_s=period * self.cfg.probe_every).start()
+        # C++ threads over the same plugins the standalone binary dlopen()s (csrc/core/ondevice.h);
+        # PMC initialises before the probe (rocprofiler must register before HIP brings HSA up).
+        self.ondevice = self._core.OnDevice(self.ex, {
+            "plugin_dir": self.cfg.plugin_dir, "pmc": bool(self.cfg.enable_pmc),
+            "pmc_counters": list(self.cfg.pmc_counters), "pmc_every_s": period, "pmc_mode": self.cfg.pmc_mode,
+            "ondevice_isolate": self.cfg.ondevice_isolate, "helper_retry_s": float(self.cfg.helper_retry),
+            "probe": bool(self.cfg.enable_probe), "probe_every_s": period * self.cfg.probe_every})
+        self.ondevice.start()
 
     def step_ondevice(self) -> None:
         """One synchronous PMC / probe step (so a one-shot sample carries their series)."""
         if self.ondevice is not None:
             self.ondevice.step()
-        for plugin in (self.pmc, self.probe):
-            if plugin is not None:
-                plugin.step()
 
     def stop(self) -> None:
-        for p in (self.ondevice, self.pmc, self.probe, self.plane):
+        for p in (self.ondevice,):
             if p is not None:
                 try:
                     p.stop()

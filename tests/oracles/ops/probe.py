@@ -32,7 +32,7 @@ import threading
 import time
 from typing import Dict, List
 
-from .._native import hip
+from gpumon._native import hip
 
 log = logging.getLogger("gpumon.probe")
 SLOT_HELP = "Mean lowest wave slot a probe wave got per SIMD (wave slots held by other work at probe launch)."

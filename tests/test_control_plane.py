@@ -10,8 +10,8 @@ import time
 
 import pytest
 
-from gpumon.attribution.fake_kubelet import FakeKubelet, FakePod
-from gpumon.attribution.plane import ControlPlane, match_device_id
+from oracles.attribution.fake_kubelet import FakeKubelet, FakePod
+from oracles.attribution.plane import ControlPlane, match_device_id
 from gpumon.config import Config
 from gpumon.export import promtext
 
@@ -123,7 +123,7 @@ def test_plane_background_refresh(kubelet, mock_exporter, tmp_path):
 
 
 def test_cri_version_and_allocatable(kubelet):
-    from gpumon.attribution.clients import CRIClient, PodResourcesClient
+    from oracles.attribution.clients import CRIClient, PodResourcesClient
 
     kubelet.allocatable = ["0000:05:00.0", "0000:25:00.0"]
     c = CRIClient(kubelet.cri_socket)

@@ -122,7 +122,7 @@ def _control_plane_metric_names():
     """Series of the native metadata pollers, from an exporter pointed at the fake kubelet (CRI +
     PodResources) and a fake Docker daemon."""
     from gpumon import core
-    from gpumon.attribution.fake_kubelet import FakeKubelet
+    from oracles.attribution.fake_kubelet import FakeKubelet
     from test_docker import FakeDocker
 
     d = f"/tmp/gpumon-alerts-{os.getpid()}"

@@ -9,7 +9,7 @@ import sys
 
 import grpc
 
-from gpumon.attribution.fake_kubelet import FakeKubelet
+from oracles.attribution.fake_kubelet import FakeKubelet
 from gpumon.config import Config
 from gpumon import doctor
 

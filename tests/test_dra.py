@@ -4,15 +4,15 @@ ContainerDevices. Both control planes (Python grpcio client and the native grpc_
 them into allocations, and both device matchers accept the DRA id forms (CDI names, ``gpu-N``,
 dashed PCI addresses). The AMD DRA driver's exact device naming is not pinned by any fixture in the
 reference (which predates DRA): parity unpinned; the accepted forms are documented in
-gpumon/attribution/plane.py."""
+tests/oracles/attribution/plane.py."""
 
 import os
 
 import pytest
 
-from gpumon.attribution import proto as P
-from gpumon.attribution.fake_kubelet import FakeKubelet, FakePod
-from gpumon.attribution.plane import match_device_id
+from oracles.attribution import proto as P
+from oracles.attribution.fake_kubelet import FakeKubelet, FakePod
+from oracles.attribution.plane import match_device_id
 from gpumon.export import promtext
 
 STATICS = [{"index": i, "hip_id": i, "bdf": f"0000:{0x05 + 0x20 * i:02x}:00.0", "uuid": f"u{i}", "drm_card": i,
@@ -58,7 +58,7 @@ def kubelet(tmp_path):
 
 
 def test_python_client_lists_dra_claims(kubelet):
-    from gpumon.attribution.clients import PodResourcesClient
+    from oracles.attribution.clients import PodResourcesClient
 
     sock, _ = kubelet
     cl = PodResourcesClient(sock)
@@ -92,8 +92,8 @@ def test_native_poller_counts_dra_allocations(core, kubelet):
 
 
 def test_python_plane_counts_dra_allocations(kubelet, mock_exporter):
-    from gpumon.attribution.clients import PodResourcesClient
-    from gpumon.attribution.plane import ControlPlane
+    from oracles.attribution.clients import PodResourcesClient
+    from oracles.attribution.plane import ControlPlane
     from gpumon.config import Config
 
     sock, _ = kubelet

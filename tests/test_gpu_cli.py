@@ -1,6 +1,7 @@
 """End-to-end CLI on a real MI355X with both device plugins enabled (fresh subprocess: PMC must
 register before HSA init): `gpumon once --enable-pmc --enable-probe-kernel`."""
 
+import json
 import os
 import subprocess
 import sys
@@ -41,15 +42,33 @@ def test_native_binary_once():
     assert len(promtext.values(fam, "gpu_xcd_busy_percent")) >= 8
 
 
+ORACLE_RUNNERS = r"""
+import json, os, sys
+sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
+from gpumon import core
+from gpumon.export import promtext
+from oracles.ops.pmc import PmcRunner      # PMC first: rocprofiler registers before HIP comes up
+from oracles.ops.probe import ProbeRunner
+ex = core().Exporter({"backend": "amdsmi", "devices": [0], "serve_http": False, "interval_s": 0})
+assert ex.start() == ""  # amdsmi does not bring HSA up: the PMC runner still registers first
+pmc = PmcRunner(ex, every_s=60.0)
+probe = ProbeRunner(ex, every_s=60.0)
+pmc.step(); probe.step(); ex.tick()
+fam = promtext.parse(ex.metrics_text())
+print(json.dumps({"xcd_blocks": promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0"),
+                  "mfma_busy": promtext.values(fam, "gpu_mfma_busy_active_percent", gpu_id="0")}))
+probe.stop(); pmc.stop(); ex.stop()
+"""
+
+
 def test_once_python_runners():
-    """The Python runners (gpumon/ops) over the same plugins: identical families."""
-    r = subprocess.run([sys.executable, "-m", "gpumon", "once", "--backend", "amdsmi", "--devices", "0",
-                        "--enable-pmc", "--enable-probe-kernel", "--ondevice", "python", "--log-level", "warn"],
-                       capture_output=True, text=True, timeout=240, cwd=ROOT)
+    """The Python oracle runners (tests/oracles/ops, not shipped) over the same plugins the native
+    samplers use: the same families."""
+    r = subprocess.run([sys.executable, "-c", ORACLE_RUNNERS], capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
-    fam = promtext.parse(r.stdout)
-    assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
-    assert promtext.values(fam, "gpu_mfma_busy_active_percent", gpu_id="0")
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert len(out["xcd_blocks"]) == 8, out
+    assert out["mfma_busy"], out
 
 
 def test_native_binary_pmc_probe_under_mfma_load():

@@ -508,3 +508,29 @@ def test_xgmi_max_bandwidth_fill_in_matches_link_metrics(core, torch_gpu):
             assert l["max_bandwidth_gbps"] == pytest.approx(lane * width), (l, lane, width)
     finally:
         ex.stop()
+
+
+def test_xgmi_peer_labels_complete_and_paired_by_counters(core, torch_gpu):
+    """MI355X, ROCm 7.2: amdsmi_get_link_metrics reports num_links 7 but fills 8 entries (self + the
+    7 peers; profiles/r3_xgmi_link_metrics.md), so all 7 up links carry a distinct peer BDF that is
+    not the device's own. Entries are paired with table slots by their counters (xgmi_map.cpp): on
+    this ROCm the library reads the same table in the same order, so no pairing may contradict the
+    position, and every peer entry is either confirmed by its counters or counted as unverified."""
+    from gpumon.export import promtext
+
+    ex = _exporter(core, link_every=1)
+    try:
+        ex.tick()
+        ex.tick()
+        sm = ex.samples()[0]
+        own = ex.statics()[0]["bdf"]
+        up = [l for l in sm["links"] if l["status"] == 1]
+        peers = [l["peer_bdf"] for l in up]
+        assert len(up) == 7 and all(peers) and len(set(peers)) == 7 and own not in peers, sm["links"]
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpumon_xgmi_slot_map_mismatch", gpu_id="0") == 0
+        v = promtext.one(fam, "gpumon_xgmi_slot_map_verified", gpu_id="0")
+        u = promtext.one(fam, "gpumon_xgmi_slot_map_unverified", gpu_id="0")
+        assert v + u == 7, (v, u)
+    finally:
+        ex.stop()

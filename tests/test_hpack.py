@@ -89,7 +89,7 @@ def test_malformed_blocks_are_errors(core):
 # ------------------------------------------------------------------------------------ gRPC status
 @pytest.fixture
 def kubelet():
-    from gpumon.attribution.fake_kubelet import FakeKubelet
+    from oracles.attribution.fake_kubelet import FakeKubelet
 
     d = tempfile.mkdtemp(prefix="gpumon-kl-")
     k = FakeKubelet(podres_socket=os.path.join(d, "kubelet.sock"), cri_socket=os.path.join(d, "cri.sock"))
@@ -147,7 +147,7 @@ def test_exporter_exports_the_status(core, kubelet):
 
 
 def test_cri_falls_back_to_v1alpha2(core):
-    from gpumon.attribution.fake_kubelet import FakeKubelet, FakePod
+    from oracles.attribution.fake_kubelet import FakeKubelet, FakePod
 
     d = tempfile.mkdtemp(prefix="gpumon-cri-")
     k = FakeKubelet(cri_socket=os.path.join(d, "cri.sock"), cri_api="runtime.v1alpha2")

@@ -9,7 +9,7 @@ import urllib.request
 
 import pytest
 
-from gpumon.attribution.fake_kubelet import FakeKubelet, FakePod
+from oracles.attribution.fake_kubelet import FakeKubelet, FakePod
 from gpumon.export import promtext
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -42,7 +42,7 @@ def test_client_errors_are_reported(core, tmp_path):
 
 
 def test_parser_matches_python_protobuf(core):
-    from gpumon.attribution import proto as P
+    from oracles.attribution import proto as P
 
     r = P.ListPodResourcesResponse()
     pr = r.pod_resources.add(name="p", namespace="n")

@@ -13,7 +13,7 @@ from hypothesis import given, settings
 from hypothesis import strategies as st
 
 from conftest import ROOT, make_locked
-from gpumon.ops.pmc import derive
+from oracles.ops.pmc import derive
 
 FAKE_DIR = os.path.join(ROOT, "build", "fakes", "ondevice")
 BIN = os.path.join(ROOT, "bin", "gpumon-exporter")

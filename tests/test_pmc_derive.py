@@ -2,7 +2,7 @@
 
 import pytest
 
-from gpumon.ops.pmc import derive
+from oracles.ops.pmc import derive
 
 AGENT = {"cu_count": 256, "simd_count": 1024, "max_waves_per_cu": 32}
 
@@ -25,7 +25,7 @@ def test_idle_and_missing():
 def test_config_pmc_counters_cover_derivations():
     """The default counter set (one gfx950 counting pass) holds every counter derive() uses."""
     from gpumon.config import Config
-    from gpumon.ops.pmc import DEFAULT_COUNTERS
+    from oracles.ops.pmc import DEFAULT_COUNTERS
 
     assert set(DEFAULT_COUNTERS) <= set(Config().pmc_counters)
     assert Config().pmc_mode == "continuous"

@@ -1,0 +1,39 @@
+#!/bin/bash
+# What the default exporter still exports WITHOUT access to /dev/kfd and /dev/dri -- the situation
+# of an unprivileged DaemonSet pod (drop `privileged: true`). A user + mount
+# namespace hides both device nodes (tmpfs over /dev/dri, /dev/null over /dev/kfd) from one run of
+# bin/gpumon-exporter --once; a second run with the devices is the reference. A torch tenant keeps
+# a KFD process on the GPU meanwhile, so the process rows are compared too.
+#
+#   tools/no_device_check.sh [OUTDIR]      (on the GPU box; writes OUTDIR/{with_dev,no_dev}.prom, summary.json)
+set -o pipefail
+out=${1:-gpurun_out/nodev}
+mkdir -p "$out"
+ARGS="--backend amdsmi --once --no-pod-resources --no-cri --log-level warn"
+python -c "import torch,time; x=torch.randn(8192,8192,device='cuda'); t=time.time()
+while time.time()-t<25: y=x@x; torch.cuda.synchronize()" > "$out/tenant.log" 2>&1 &
+tenant=$!
+sleep 12
+timeout -k 5 60 ./bin/gpumon-exporter $ARGS > "$out/with_dev.prom" 2> "$out/with_dev.err"
+rc1=$?
+timeout -k 5 60 unshare -Urm sh -c "mount -t tmpfs tmpfs /dev/dri && mount --bind /dev/null /dev/kfd && ls -la /dev/dri /dev/kfd >&2 && ./bin/gpumon-exporter $ARGS" \
+  > "$out/no_dev.prom" 2> "$out/no_dev.err"
+rc2=$?
+wait $tenant
+python - "$out" "$rc1" "$rc2" <<'EOF'
+import json, sys
+sys.path.insert(0, ".")
+from gpumon.export import promtext
+out, rc1, rc2 = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+a = promtext.parse(open(f"{out}/with_dev.prom").read())
+b = promtext.parse(open(f"{out}/no_dev.prom").read())
+count = lambda f: {k: len(v["samples"]) for k, v in f.items()}
+ca, cb = count(a), count(b)
+res = {"rc_with_dev": rc1, "rc_no_dev": rc2, "families_with_dev": len(ca), "families_no_dev": len(cb),
+       "missing_without_dev": sorted(k for k in ca if k not in cb),
+       "fewer_samples_without_dev": {k: [ca[k], cb[k]] for k in ca if k in cb and cb[k] < ca[k]},
+       "pod_rows": [len(a.get("pod_gpu_used_memory", {}).get("samples", [])),
+                    len(b.get("pod_gpu_used_memory", {}).get("samples", []))]}
+json.dump(res, open(f"{out}/summary.json", "w"), indent=1)
+print(json.dumps(res))
+EOF

@@ -9,10 +9,12 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))  # oracles
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))  # oracles
 
 
 def main():
-    from gpumon.ops.pmc import DEFAULT_COUNTERS, derive, pmc_module
+    from oracles.ops.pmc import DEFAULT_COUNTERS, derive, pmc_module
 
     P = pmc_module()
     n = P.init()

@@ -14,6 +14,8 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))  # oracles
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))  # oracles
 
 
 def scan(P, names, window):
@@ -28,7 +30,7 @@ def scan(P, names, window):
 
 
 def main():
-    from gpumon.ops.pmc import pmc_module
+    from oracles.ops.pmc import pmc_module
 
     P = pmc_module()
     P.init()

@@ -81,6 +81,10 @@ def _shared(port, seconds):
     stagger = 4.0
     spawn = lambda n, secs: subprocess.Popen([sys.executable, "-c", TENANT, "bf16", str(secs), str(n)],
                                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    # processes already holding the GPU (the test runner itself when earlier tests used torch): not
+    # tenants -- they make the GPU look shared only for their arrival window (5 ticks / 5 s)
+    fam0 = promtext.parse(urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode())
+    background = {l["pid"] for _, l, _ in fam0.get("pod_gpu_used_memory", {}).get("samples", [])}
     ts = [spawn(sizes[0], seconds + stagger)]
     t_second = time.time() + stagger
     ticks = []
@@ -96,10 +100,11 @@ def _shared(port, seconds):
                       "tflops": (promtext.values(fam, "gpu_mfma_tflops", gpu_id="0", dtype="bf16") or [None])[0],
                       "pod_mfma_util_rows": len(promtext.values(fam, "pod_gpu_mfma_util_percent", gpu_id="0")),
                       "active": (promtext.values(fam, "gpu_active_processes", gpu_id="0") or [None])[0],
-                      "vram_rows": sum(1 for v in mem.values() if v > 0),
+                      "vram_rows": sum(1 for p, v in mem.items() if v > 0 and p not in background),
                       # KFD reports host PIDs (not the tenants' pids inside a PID namespace): rows
                       # ranked by busy share, the bigger tenant first
-                      "rows": sorted(({"busy": busy.get(p), "cu": cu.get(p), "mib": mem.get(p)} for p in busy),
+                      "rows": sorted(({"busy": busy.get(p), "cu": cu.get(p), "mib": mem.get(p)} for p in busy
+                                      if p not in background),
                                      key=lambda r: -(r["busy"] or 0))})
         time.sleep(0.5)
     res = []
@@ -121,6 +126,7 @@ def _shared(port, seconds):
             "rows_median": [{"busy": statistics.median([r[i]["busy"] for r in rows if r[i]["busy"] is not None] or [0]),
                              "cu": round(statistics.median([r[i]["cu"] for r in rows if r[i]["cu"] is not None] or [0]), 1)}
                             for i in range(2)] if rows else None,
+            "background_pids": sorted(background),
             "pod_mfma_util_rows_max": max((k["pod_mfma_util_rows"] for k in inside), default=None),
             # every scrape (not only those inside the timed window) with two tenants holding VRAM
             "scrapes_two_vram_tenants": sum(1 for k in ticks if k["vram_rows"] >= 2),

@@ -13,6 +13,8 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))  # oracles
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))  # oracles
 
 
 def probe_stats(H, probe, n=8):
@@ -36,7 +38,7 @@ def probe_stats(H, probe, n=8):
 
 
 def main():
-    from gpumon.ops.pmc import derive, pmc_module
+    from oracles.ops.pmc import derive, pmc_module
 
     # per-wave SQ_WAVE_CYCLES: valid here because the loads run in THIS process
     # (profiles/r1_pmc_cross_process.md)
