@@ -30,8 +30,9 @@ torch.cuda.synchronize(); the MAX elapsed over ranks is used.
 Reported ``value`` = whole-node fresh device samples per second (K ticks x N GPUs / elapsed);
 ``vs_baseline`` = per-GPU rate / 0.077 samples/s/GPU, the reference's best observed rate
 (one node_gpu line per 13-19 s). The scrape-latency half of the headline metric is
-reported as ``scrape_p99_ms`` / ``scrape_p50_ms`` (client-side, keep-alive, like a Prometheus
-server). Tick quantiles are exact over the timed ticks (the exporter's tick log). Without a GPU
+reported as ``scrape_p99_ms`` / ``scrape_p999_ms`` / ``scrape_p50_ms`` (client-side, keep-alive,
+like a Prometheus server, 200 req/s so a 10-tick run holds >= 2000 scrapes) and
+``server_scrape_p99_ms`` (the exporter's own service time of the same requests, exact). Tick quantiles are exact over the timed ticks (the exporter's tick log). Without a GPU
 the exporter uses the mock backend and says so in ``data``.
 """
 
@@ -136,7 +137,9 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--interval", type=float, default=1.0, help="sampling interval (1.0 = BASELINE; 0.1 = 10 Hz stress)")
     ap.add_argument("--load", default="mixed", choices=["mixed", "concurrent", "mfma", "hbm", "idle"])
-    ap.add_argument("--scrape-rate", type=float, default=20.0, help="aggregate /metrics requests per second")
+    ap.add_argument("--scrape-rate", type=float, default=200.0,
+                    help="aggregate /metrics requests per second (200: >= 2000 timed scrapes in a 10 s run, "
+                         "so p99 / p99.9 rest on >= 20 / 2 samples above them)")
     ap.add_argument("--scrape-concurrency", type=int, default=2)
     ap.add_argument("--gzip", action="store_true", help="scrape with Accept-Encoding: gzip")
     ap.add_argument("--backend", default="auto")
@@ -152,14 +155,17 @@ def main() -> int:
     ap.add_argument("--link-check-s", type=float, default=0.6,
                     help="N > 1: seconds per peer of the GPU 0 -> k link-map check after the timed region (0 = off)")
     ap.add_argument("--probe", action="store_true", help="also run the K1 probe kernel each tick")
-    ap.add_argument("--idle-s", type=float, default=5.0,
-                    help="untimed idle reference before the load starts: scrape p50/p99 + tick cost (0 = off)")
+    ap.add_argument("--idle-s", type=float, default=-1.0,
+                    help="untimed idle reference before the load starts: scrape p50/p99 + tick cost "
+                         "(-1 = as long as the timed region: the same scrape count; 0 = off)")
     ap.add_argument("--no-fast-path", action="store_true", help="read every value through libamd_smi")
     ap.add_argument("--rt-priority", type=int, default=1,
                     help="the DaemonSet's rt_priority (SCHED_FIFO sampler; stays normal without CAP_SYS_NICE)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
+    if args.idle_s < 0:
+        args.idle_s = max(5.0, args.steps * args.interval)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -228,15 +234,20 @@ def main() -> int:
     if rank == 0 and args.idle_s > 0:
         mon.wait_ticks(1, timeout_s=args.interval * 5 + 30)
         q0 = mon.ex.seq
+        n0 = mon.ex.scrape_count()
         r = core.scrape_load("127.0.0.1", mon.port, "/metrics", n_requests=0, duration_s=args.idle_s,
                              concurrency=args.scrape_concurrency, rate_hz=args.scrape_rate, keep_alive=True,
                              gzip=args.gzip)
         q1 = mon.ex.seq
         it = [t["duration_s"] for t in mon.ex.tick_log() if q0 < t["seq"] <= q1]
         lat = r.get("latencies_s", [])
+        srv = list(mon.ex.scrape_durations_since(n0))
         idle = {"seconds": args.idle_s, "scrapes": len(lat), "scrape_errors": r.get("errors", 0),
                 "scrape_p50_ms": round(_pct(lat, 0.50) * 1e3, 4) if lat else None,
                 "scrape_p99_ms": round(_pct(lat, 0.99) * 1e3, 4) if lat else None,
+                "scrape_p999_ms": round(_pct(lat, 0.999) * 1e3, 4) if lat else None,
+                "server_scrape_p99_ms": round(_pct(srv, 0.99) * 1e3, 4) if srv else None,
+                "server_scrape_p999_ms": round(_pct(srv, 0.999) * 1e3, 4) if srv else None,
                 "ticks": len(it), "tick_mean_ms": round(sum(it) / len(it) * 1e3, 4) if it else None,
                 "tick_max_ms": round(max(it) * 1e3, 4) if it else None}
     barrier()
@@ -302,6 +313,7 @@ def main() -> int:
                                                   rate_hz=args.scrape_rate, keep_alive=True, gzip=args.gzip))
 
         scraper = threading.Thread(target=_scrape, daemon=True)
+        n_scr0 = mon.ex.scrape_count()
         s0 = mon.ex.self_stats()
         seq0 = mon.ex.seq
         cpu0 = _exporter_cpu_s()
@@ -390,6 +402,7 @@ def main() -> int:
         if scraper is not None:
             scraper.join(timeout=args.interval * 5 + 30)
         lat = scrape_result.get("latencies_s", [])
+        srv = list(mon.ex.scrape_durations_since(n_scr0))  # server-side, the same scrapes
         samples = s1["samples"] - s0["samples"]
         ticks = seq1 - seq0
         timed = [t for t in mon.ex.tick_log() if seq0 < t["seq"] <= seq0 + ticks]
@@ -424,6 +437,9 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / max(1, len(sm)) / BASELINE_SAMPLES_PER_GPU, 3),
+            "value_note": ("value = fresh device samples/s over the timed ticks: fixed by the sampling "
+                           "interval (1/interval per GPU) unless ticks overrun; the measured speed is "
+                           "scrape_p99_ms / scrape_p999_ms (client), server_scrape_p99_ms and tick_*_ms"),
             "dtype": "bf16",
             "data": ("synthetic" if backend in ("amdsmi", "rocm_smi") else
                      f"synthetic (REHEARSAL: {n} physical GPU(s) each sampled {args.replicate}x)"
@@ -443,8 +459,16 @@ def main() -> int:
             "scrape_idle": idle,  # same scrape load, before any synthetic load (untimed)
             "scrape_p50_ms": round(_pct(lat, 0.50) * 1e3, 4),
             "scrape_p99_ms": round(_pct(lat, 0.99) * 1e3, 4),
+            "scrape_p999_ms": round(_pct(lat, 0.999) * 1e3, 4),
             "scrape_max_ms": round(max(lat) * 1e3, 4) if lat else None,
             "scrapes": len(lat),
+            "scrape_rate_hz": args.scrape_rate,
+            # the exporter's own service time of the same requests (request parsed -> response
+            # written), exact: client minus server = loopback + client scheduling
+            "server_scrape_p50_ms": round(_pct(srv, 0.50) * 1e3, 4) if srv else None,
+            "server_scrape_p99_ms": round(_pct(srv, 0.99) * 1e3, 4) if srv else None,
+            "server_scrape_p999_ms": round(_pct(srv, 0.999) * 1e3, 4) if srv else None,
+            "server_scrapes": len(srv),
             "scrape_errors": scrape_result.get("errors", 0),
             "scrape_body_kb": round(scrape_result.get("bytes", 0) / max(1, len(lat)) / 1024, 2),
             "samples_per_sec_per_gpu": round(value / max(1, len(sm)), 4),
@@ -463,7 +487,6 @@ def main() -> int:
                                     for k in ("t_late", "t_sample", "t_wake", "t_device", "t_procs", "t_attrib",
                                               "t_render", "t_gzip")} if timed else None,
             "tick_quantiles": "exact over the timed ticks (exporter tick log); times in ms",
-            "server_scrape_p99_ms_last4096": round(mon.ex.scrape_quantile(0.99) * 1e3, 4),
             "overruns": s1["overruns"] - s0["overruns"],
             "sampler_rt_threads": s1.get("rt_threads", 0),
             # the exporter's own threads over the timed region, serving the scrape load too (1/100 s ticks)

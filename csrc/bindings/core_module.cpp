@@ -607,6 +607,8 @@ PYBIND11_MODULE(_core, m) {
         return d;
       },
       "node-wide /proc/<pid>/fd scan cache of the sysfs fast path (scans so far, cached processes)");
+  m.def("fd_table_clear", [] { gpumon::DrmFdTables::get().clear(); },
+        "drop every cached fd table (tests: entries of an earlier test's fake /proc tree)");
   m.def("gzip", [](const std::string& s) {
     std::string o;
     if (!gzip_compress(s, &o)) throw std::runtime_error("gzip failed");
@@ -777,6 +779,9 @@ PYBIND11_MODULE(_core, m) {
              return d;
            })
       .def("scrape_quantile", &Exporter::scrape_quantile)
+      .def("scrape_count", &Exporter::scrape_count, "/metrics requests served so far")
+      .def("scrape_durations_since", &Exporter::scrape_durations_since, py::arg("from"),
+           "server-side service times (s) of the /metrics requests numbered >= from (last 16384)")
       .def("sample_quantile", &Exporter::sample_quantile)
       .def("set_container_meta",
            [](Exporter& e, const py::list& metas) {

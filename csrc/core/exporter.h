@@ -155,6 +155,9 @@ class Exporter {
   Backend* backend() { return backend_.get(); }
   const ExporterConfig& config() const { return cfg_; }
   double scrape_quantile(double q) const { return scrape_hist_.quantile(q); }
+  // server-side /metrics service times, exact, from scrape number `from` on (scrape_count() first)
+  uint64_t scrape_count() const { return scrape_hist_.observed(); }
+  std::vector<float> scrape_durations_since(uint64_t from) const { return scrape_hist_.since(from, nullptr); }
   double sample_quantile(double q) const { return sample_hist_.quantile(q); }
   // The last kTickLog ticks' TickInfo, oldest first (tick-tail attribution: bench / introspection).
   static constexpr size_t kTickLog = 4096;

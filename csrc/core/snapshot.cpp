@@ -47,6 +47,16 @@ double Histogram::quantile(double q) const {
   return v[idx];
 }
 
+std::vector<float> Histogram::since(uint64_t from, uint64_t* end) const {
+  const uint64_t n = recent_n_.load(std::memory_order_acquire);
+  if (end) *end = n;
+  const uint64_t lo = std::max<uint64_t>(from, n > kRecent ? n - kRecent : 0);
+  std::vector<float> v;
+  v.reserve(n > lo ? n - lo : 0);
+  for (uint64_t k = lo; k < n; ++k) v.push_back(recent_[k % kRecent].load(std::memory_order_relaxed));
+  return v;
+}
+
 double Histogram::bucket_quantile(double q) const {
   std::vector<uint64_t> c(bounds_.size() + 1);
   uint64_t total = 0;

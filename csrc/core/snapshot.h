@@ -51,7 +51,12 @@ class Histogram {
   // Bucket-interpolated estimate over every observation (what histogram_quantile() would say).
   double bucket_quantile(double q) const;
 
-  static constexpr size_t kRecent = 4096;
+  // Observations with index >= `from` (0-based, in arrival order) still held by the ring, and the
+  // index one past the newest: an exact window quantile for a caller that noted observed() first.
+  std::vector<float> since(uint64_t from, uint64_t* end) const;
+  uint64_t observed() const { return recent_n_.load(std::memory_order_relaxed); }
+
+  static constexpr size_t kRecent = 16384;
 
  private:
   std::vector<double> bounds_;

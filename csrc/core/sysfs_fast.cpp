@@ -233,6 +233,14 @@ void DrmFdTables::retain(const std::string& proc_root, const std::vector<uint32_
   }
 }
 
+void DrmFdTables::clear() {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto it = m_.begin(); it != m_.end();) {
+    if (it->second.scanning) ++it;
+    else it = m_.erase(it);
+  }
+}
+
 size_t DrmFdTables::size() {
   std::lock_guard<std::mutex> g(mu_);
   return m_.size();

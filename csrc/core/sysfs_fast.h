@@ -227,6 +227,7 @@ class DrmFdTables {
   // Drop the tables of processes under `proc_root` that are no longer in the node's KFD process
   // list (`kfd_pids`, sorted): a reused pid must not be read at the old process's fd numbers.
   void retain(const std::string& proc_root, const std::vector<uint32_t>& kfd_pids);
+  void clear();  // drop every entry not being scanned right now
   uint64_t scans() const { return scans_.load(); }
   size_t size();
 

@@ -174,6 +174,7 @@ def test_fd_tables_are_shared_across_gpus_and_refreshed_off_tick(exporter, tmp_p
     GPU; a vanished fd makes the next tick's upkeep (after the publish) rescan it, and the tick
     after that reads the new fd."""
     sysr, procr = make_tree(tmp_path, procs=((4242, 0), (4242, 1)))
+    core.fd_table_clear()  # the cache is node-wide: an earlier test's due rescans would count here
     s0 = core.fd_table_stats()["scans"]
     ex = exporter(sysr, procr, sample_threads=2, interval_s=0)  # start() runs the first tick
     ex.tick()
@@ -201,3 +202,38 @@ def test_fd_tables_are_shared_across_gpus_and_refreshed_off_tick(exporter, tmp_p
     ex.tick()  # the worker finished its upkeep before taking this tick
     rows = dict((r["dev"], r["used_memory_bytes"]) for r in ex.pod_rows() if not r["idle"])
     assert rows[0] == 2 << 30
+
+
+def test_reused_pid_is_not_read_at_the_old_fd_numbers(exporter, tmp_path, core):
+    """the node-wide fd-table cache was keyed by /proc/<pid> only and kept an entry 60 s
+    after last use, so a pid reused within that time was read at the old process's fd numbers
+    until a read failed or the 10 s refresh. An entry now goes as soon as its pid leaves the KFD
+    process list; the new process is scanned afresh."""
+    import shutil
+
+    sysr, procr = make_tree(tmp_path, gpus=1)
+    core.fd_table_clear()
+    ex = exporter(sysr, procr, sample_threads=0)
+    ex.tick()
+    row = next(r for r in ex.pod_rows() if r["pid"] == "4242")
+    assert row["used_memory_bytes"] == 1 << 30  # fdinfo VRAM (fds 5, 6)
+    # the process exits: gone from KFD and /proc
+    kp = sysr / "class" / "kfd" / "kfd" / "proc" / "4242"
+    shutil.rmtree(kp)
+    shutil.rmtree(procr / "4242")
+    ex.tick()
+    assert not [r for r in ex.pod_rows() if r["pid"] == "4242"]
+    assert core.fd_table_stats()["entries"] == 0  # dropped with the pid, not kept for 60 s
+    # a new process gets pid 4242 again, with its DRM file at another fd number
+    (kp / "stats_36622").mkdir(parents=True)
+    (kp / "vram_36622").write_text(f"{2 << 30}\n")
+    (kp / "stats_36622" / "cu_occupancy").write_text("0\n")
+    fd, fdinfo = procr / "4242" / "fd", procr / "4242" / "fdinfo"
+    fd.mkdir(parents=True)
+    fdinfo.mkdir()
+    os.symlink("/dev/dri/renderD152", fd / "11")
+    (fdinfo / "11").write_text("drm-driver:\tamdgpu\ndrm-client-id:\t9\ndrm-engine-gfx:\t1 ns\n"
+                               "drm-memory-vram:\t3145728 KiB\n")
+    ex.tick()
+    row = next(r for r in ex.pod_rows() if r["pid"] == "4242")
+    assert row["used_memory_bytes"] == 3 << 30, row  # the new process's fd 11, not the old fds
