@@ -105,6 +105,8 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "pod_resources_refresh_s", &c.pod_resources_refresh_s);
   get(d, "cri_socket", &c.cri_socket);
   get(d, "docker_socket", &c.docker_socket);
+  get(d, "pod_log_root", &c.pod_log_root);
+  get(d, "device_checkpoint", &c.device_checkpoint);
   get(d, "version", &c.version);
   get(d, "activity_acc_scale", &c.rates.activity_acc_scale);
   get(d, "xgmi_kb_bytes", &c.rates.xgmi_kb_bytes);

@@ -17,6 +17,7 @@
 #include "docker_lite.h"
 #include "grpc_lite.h"
 #include "http_client.h"
+#include "kubelet_files.h"
 #include "ondevice.h"
 #include "trace.h"
 #include "xgmi_map.h"
@@ -473,10 +474,12 @@ bool Exporter::start(std::string* err) {
     set_thread_name("gpumon-influx");
     influx_loop();
   });
-  if (!cfg_.pod_resources_socket.empty() || !cfg_.cri_socket.empty() || !cfg_.docker_socket.empty()) {
+  if (!cfg_.pod_resources_socket.empty() || !cfg_.cri_socket.empty() || !cfg_.docker_socket.empty() ||
+      !cfg_.pod_log_root.empty() || !cfg_.device_checkpoint.empty()) {
     // metadata and allocations known before the first scrape
     if (!cfg_.cri_socket.empty()) cri_poll_once();
     if (!cfg_.docker_socket.empty()) docker_poll_once();
+    if (!cfg_.pod_log_root.empty() || !cfg_.device_checkpoint.empty()) files_poll_once();
     if (!cfg_.pod_resources_socket.empty()) podres_poll_once();
     podres_ = std::thread([this] {
       set_thread_name("gpumon-k8s");
@@ -1462,6 +1465,7 @@ void Exporter::podres_loop() {
     lk.unlock();
     if (!cfg_.cri_socket.empty()) cri_poll_once();
     if (!cfg_.docker_socket.empty()) docker_poll_once();
+    if (!cfg_.pod_log_root.empty() || !cfg_.device_checkpoint.empty()) files_poll_once();
     if (!cfg_.pod_resources_socket.empty()) podres_poll_once();
     lk.lock();
   }
@@ -1536,6 +1540,8 @@ void Exporter::publish_container_meta() {
     std::unordered_set<std::string> seen;
     for (const auto& m : all) seen.insert(m.container_id);
     for (const auto& m : docker_metas_)
+      if (seen.insert(m.container_id).second) all.push_back(m);
+    for (const auto& m : files_metas_)
       if (seen.insert(m.container_id).second) all.push_back(m);
   }
   {
@@ -1645,12 +1651,95 @@ bool Exporter::docker_poll_once() {
   return ok;
 }
 
+// Kubelet-written files (kubelet_files.h): the log tree names every container on the node; the
+// device-plugin checkpoint lists the GPUs each (pod uid, container) was given. A checkpoint entry
+// of a pod without a log directory (gone from the node) is dropped.
+bool Exporter::files_poll_once() {
+  std::vector<ContainerMeta> metas;
+  std::string err;
+  bool logs_ok = false, ckpt_ok = false;
+  if (!cfg_.pod_log_root.empty()) {
+    logs_ok = kubelet_log_metadata(cfg_.pod_log_root, &metas, &err);
+    if (!logs_ok) GPUMON_LOG(LogLevel::kWarn, "kubelet-files", "pod log tree: " + err);
+  }
+  std::vector<Allocation> allocs;
+  size_t unknown = 0;
+  if (!cfg_.device_checkpoint.empty()) {
+    std::vector<CheckpointEntry> entries;
+    std::string cerr;
+    ckpt_ok = device_checkpoint_read(cfg_.device_checkpoint, &entries, &cerr);
+    if (!ckpt_ok) GPUMON_LOG(LogLevel::kWarn, "kubelet-files", "device checkpoint: " + cerr);
+    std::vector<DeviceStatic> st;
+    {
+      std::lock_guard<std::mutex> g(state_mu_);
+      st = statics_;
+    }
+    std::unordered_map<std::string, const ContainerMeta*> by_uid_ctr;
+    std::unordered_map<std::string, const ContainerMeta*> by_uid;
+    for (const auto& m : metas)
+      if (!m.pod_uid.empty()) {
+        by_uid_ctr[m.pod_uid + "/" + m.container_name] = &m;
+        by_uid.emplace(m.pod_uid, &m);
+      }
+    for (const auto& c : entries) {
+      if (!starts_with(c.resource, cfg_.pod_resources_prefix)) continue;
+      const auto pod = by_uid.find(c.pod_uid);
+      if (pod == by_uid.end()) continue;  // not (or no longer) on this node
+      const auto ctr = by_uid_ctr.find(c.pod_uid + "/" + c.container_name);
+      for (const auto& id : c.device_ids) {
+        const int idx = match_device_id(id, st);
+        if (idx < 0) {
+          unknown++;
+          continue;
+        }
+        Allocation a;
+        a.pod_namespace = pod->second->pod_namespace;
+        a.pod_name = pod->second->pod_name;
+        a.pod_uid = c.pod_uid;
+        a.container_name = c.container_name;
+        if (ctr != by_uid_ctr.end()) a.container_id = ctr->second->container_id;
+        a.gpu_index = idx;
+        allocs.push_back(std::move(a));
+      }
+    }
+  }
+  const size_t n_metas = metas.size();
+  {
+    std::lock_guard<std::mutex> g(meta_mu_);
+    if (logs_ok || cfg_.pod_log_root.empty()) files_metas_ = std::move(metas);
+    if (ckpt_ok || cfg_.device_checkpoint.empty()) files_allocs_ = std::move(allocs);
+  }
+  publish_container_meta();
+  publish_allocations();
+  std::vector<ExtraSeries> ex;
+  if (!cfg_.pod_log_root.empty()) {
+    ex.push_back({"gpumon_kubelet_files_up",
+                  "1 if the last read of a kubelet-written metadata file succeeded (pod_logs: the /var/log "
+                  "containers/ + pods/ trees; device_checkpoint: the device-plugin checkpoint).",
+                  "gauge", -1, {{"source", "pod_logs"}}, logs_ok ? 1.0 : 0.0});
+    ex.push_back({"gpumon_kubelet_files_containers", "Containers named by the kubelet's log tree.", "gauge", -1, {},
+                  static_cast<double>(n_metas)});
+  }
+  if (!cfg_.device_checkpoint.empty()) {
+    ex.push_back({"gpumon_kubelet_files_up",
+                  "1 if the last read of a kubelet-written metadata file succeeded (pod_logs: the /var/log "
+                  "containers/ + pods/ trees; device_checkpoint: the device-plugin checkpoint).",
+                  "gauge", -1, {{"source", "device_checkpoint"}}, ckpt_ok ? 1.0 : 0.0});
+    ex.push_back({"gpumon_kubelet_files_unknown_devices", "Checkpointed device IDs that match no local GPU.", "gauge",
+                  -1, {}, static_cast<double>(unknown)});
+  }
+  set_extra("kubelet_files", std::move(ex));
+  return logs_ok || ckpt_ok;
+}
+
 void Exporter::publish_allocations() {
   std::vector<Allocation> all;
   {
     std::lock_guard<std::mutex> g(meta_mu_);
     all = podres_allocs_;
     all.insert(all.end(), docker_allocs_.begin(), docker_allocs_.end());
+    // the device checkpoint says what the kubelet's PodResources says: only when that is not polled
+    if (cfg_.pod_resources_socket.empty()) all.insert(all.end(), files_allocs_.begin(), files_allocs_.end());
   }
   attr_->set_allocations(std::move(all));  // a (pod, container, GPU) listed by both is one idle row
 }

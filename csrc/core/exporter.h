@@ -94,6 +94,11 @@ struct ExporterConfig {
   // Docker Engine GET /containers/json (docker_lite.cpp) for plain-Docker nodes: opt-in only (the
   // socket is root-equivalent), same refresh; merged under the CRI metadata by container id
   std::string docker_socket;
+  // Socket-free pod metadata for a non-root exporter (kubelet_files.h), same refresh: the kubelet's
+  // log tree (containers/ + pods/ under this root, e.g. "/var/log") and its device-plugin
+  // checkpoint (allocations); "" = off. Lowest priority: CRI / Docker metadata wins per container.
+  std::string pod_log_root;
+  std::string device_checkpoint;
   std::string version = "0.1.0";
 };
 
@@ -170,6 +175,7 @@ class Exporter {
   bool podres_poll_once();
   bool cri_poll_once();
   bool docker_poll_once();
+  bool files_poll_once();  // kubelet log tree + device checkpoint (kubelet_files.h)
   void publish_container_meta();  // CRI U Docker metadata -> attribution + native_meta_
  public:
   // GPU indices a Docker container holds: /dev/dri/renderD<N> / card<N> device mappings, all of
@@ -259,11 +265,11 @@ class Exporter {
   std::vector<std::string> sharing_source_;            // per device: what gpu_active_processes counted
   uint64_t pod_rows_built_ = 0;
   std::mutex meta_mu_;
-  std::vector<ContainerMeta> cri_metas_, docker_metas_;  // last successful listing of each (meta_mu_)
+  std::vector<ContainerMeta> cri_metas_, docker_metas_, files_metas_;  // last successful listing of each (meta_mu_)
   // GPU allocations: kubelet PodResources and, on Docker nodes, the GPU devices / AMD_VISIBLE_DEVICES
   // of each running container (docker inspect, cached per container id: a container's devices are
   // fixed at creation) -- published together (meta_mu_)
-  std::vector<Allocation> podres_allocs_, docker_allocs_;
+  std::vector<Allocation> podres_allocs_, docker_allocs_, files_allocs_;
   // container id -> its inspect (devices + env); mapped to GPU indices on every refresh, so a
   // container seen before the backend listed its GPUs is still resolved later
   std::unordered_map<std::string, DockerInspect> docker_inspects_;

@@ -259,6 +259,8 @@ const std::map<std::string, Setter>& setters() {
       {"verify_kfd", bool_at([](NativeOptions* o) { return &o->cfg.attribution.verify_kfd; })},
       {"cri_socket", str(&NativeOptions::cri_socket)},
       {"docker_socket", str_at([](NativeOptions* o) { return &o->cfg.docker_socket; })},
+      {"pod_log_root", str_at([](NativeOptions* o) { return &o->cfg.pod_log_root; })},
+      {"device_checkpoint", str_at([](NativeOptions* o) { return &o->cfg.device_checkpoint; })},
       {"pod_resources_socket", str(&NativeOptions::pod_resources_socket)},
       {"resource_names", list_at([](NativeOptions* o) { return &o->resource_names; })},
       {"dra_drivers", list_at([](NativeOptions* o) { return &o->cfg.pod_resources_dra_drivers; })},
@@ -529,6 +531,8 @@ std::string options_json(const NativeOptions& o) {
   B("include_host_processes", c.attribution.include_host_processes);
   S("cri_socket", o.cri_socket);
   S("docker_socket", c.docker_socket);
+  S("pod_log_root", c.pod_log_root);
+  S("device_checkpoint", c.device_checkpoint);
   S("pod_resources_socket", o.pod_resources_socket);
   L("resource_names", o.resource_names);
   L("dra_drivers", c.pod_resources_dra_drivers);

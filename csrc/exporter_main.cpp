@@ -40,6 +40,7 @@ static void usage() {
           "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--ras-slices N] [--no-gzip] [--sample-threads N] [--rt-priority N]\n"
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx]\n"
           "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri] [--docker SOCKET]\n"
+          "                       [--pod-logs /var/log] [--device-checkpoint FILE]\n"
           "                       [--dra-drivers gpu.amd.com,..|none]\n"
           "                       [--pmc] [--pmc-counters A,B,..] [--pmc-mode continuous|window] [--pmc-window SEC] [--probe] [--probe-every N]\n"
           "                       [--probe-blocks N] [--plugin-dir DIR]\n"
@@ -106,6 +107,8 @@ int main(int argc, char** argv) {
     else if (a == "--cri") set("cri_socket", next());
     else if (a == "--no-cri") set("cri_socket", "none");
     else if (a == "--docker") set("docker_socket", next());
+    else if (a == "--pod-logs") set("pod_log_root", next());
+    else if (a == "--device-checkpoint") set("device_checkpoint", next());
     else if (a == "--dra-drivers") {
       const std::string v = next();
       set("dra_drivers", v == "none" ? "" : v);

@@ -79,6 +79,10 @@ class Config:
     cri_socket: str = ""                  # e.g. unix:///run/containerd/containerd.sock ; "" = autodetect
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     docker_socket: str = ""               # plain-Docker nodes (native plane): Docker Engine container names + labels; opt-in, e.g. /var/run/docker.sock
+    # socket-free metadata for a non-root exporter (csrc/core/kubelet_files.h): the kubelet's log tree
+    # (containers/ + pods/ under this root) and device-plugin checkpoint; "" = off
+    pod_log_root: str = ""                # e.g. /var/log
+    device_checkpoint: str = ""           # e.g. /var/lib/kubelet/device-plugins/kubelet_internal_checkpoint
     resource_names: List[str] = field(default_factory=lambda: ["amd.com/gpu"])
     # DRA drivers whose claimed devices count as GPU allocations (kubelet PodResources dynamic_resources)
     dra_drivers: List[str] = field(default_factory=lambda: ["gpu.amd.com"])
@@ -281,6 +285,10 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--docker-socket", dest="docker_socket",
                    help="plain-Docker nodes: read container names/labels from the Docker Engine API (opt-in)")
     p.add_argument("--pod-resources-socket", dest="pod_resources_socket")
+    p.add_argument("--pod-log-root", dest="pod_log_root",
+                   help="non-root metadata: the kubelet's log tree (containers/ + pods/), e.g. /var/log")
+    p.add_argument("--device-checkpoint", dest="device_checkpoint",
+                   help="GPU allocations from the kubelet's device-plugin checkpoint file (root-readable)")
     p.add_argument("--control-plane", dest="control_plane", choices=["native", "off"],
                    help="kubelet PodResources / CRI / Docker metadata pollers: native (C++) or off")
     p.add_argument("--no-processes", dest="processes", action="store_false", default=None)

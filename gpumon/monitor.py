@@ -51,6 +51,10 @@ class GpuMonitor:
             if self.cfg.docker_socket:  # opt-in: never autodetected (root-equivalent socket)
                 d = self.cfg.docker_socket
                 core_cfg["docker_socket"] = d[len("unix://"):] if d.startswith("unix://") else d
+            if self.cfg.pod_log_root:
+                core_cfg["pod_log_root"] = self.cfg.pod_log_root
+            if self.cfg.device_checkpoint:
+                core_cfg["device_checkpoint"] = self.cfg.device_checkpoint
             core_cfg["pod_resources_refresh_s"] = float(self.cfg.metadata_refresh)
             if self.cfg.resource_names:
                 core_cfg["pod_resources_prefix"] = self.cfg.resource_names[0]

@@ -276,3 +276,37 @@ def test_docker_overlay_mounts_the_socket_and_sets_docker_socket():
     assert m["readOnly"] and vols[m["name"]]["hostPath"] == {"path": "/var/run/docker.sock", "type": "Socket"}
     base = ds["spec"]["template"]["spec"]["containers"][0]["volumeMounts"]
     assert all("docker" not in x["mountPath"] for x in base)
+
+
+def test_serve_imports_no_oracle_or_grpc():
+    """the image's `gpumon serve` (ENTRYPOINT) must not import grpcio / protobuf or
+    the Python test oracles -- they live under tests/oracles and are not in the image. The package
+    itself no longer contains them."""
+    import importlib.util
+    import subprocess
+    import sys
+
+    for mod in ("gpumon.attribution", "gpumon.ops.pmc", "gpumon.ops.probe"):
+        assert importlib.util.find_spec(mod.rsplit(".", 1)[0]) is None or importlib.util.find_spec(mod) is None, mod
+    code = r"""
+import json, os, signal, sys, threading
+from gpumon import cli
+threading.Timer(2.0, lambda: os.kill(os.getpid(), signal.SIGTERM)).start()
+rc = cli.main(["serve", "--backend", "mock:gpus=1", "--listen", "127.0.0.1:0", "--interval", "0.2",
+               "--log-level", "error"])
+bad = sorted(m for m in sys.modules if m.split(".")[0] in ("grpc", "oracles") or m.startswith("google.protobuf")
+             or m.startswith(("gpumon.attribution", "gpumon.ops.pmc", "gpumon.ops.probe")))
+print(json.dumps({"rc": rc, "bad": bad}))
+"""
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out == {"rc": 0, "bad": []}, out
+
+
+def test_dockerfile_installs_no_grpc():
+    text = open(os.path.join(ROOT, "deploy", "Dockerfile")).read()
+    installs = [l for l in text.splitlines() if "pip3 install" in l]
+    assert installs and not any("grpc" in l or "protobuf" in l for l in installs), installs
+    assert "tests" not in " ".join(l for l in text.splitlines() if l.startswith("COPY")), "oracles stay out of the image"

@@ -1,0 +1,145 @@
+"""Socket-free pod metadata for a non-root exporter (csrc/core/kubelet_files.cpp):
+container id -> pod / namespace / container from the kubelet's /var/log/containers symlink names,
+pod uid from /var/log/pods, and GPU allocations (idle rows) from the device-plugin checkpoint.
+The reference needed the root-equivalent docker.sock for the same data
+(/root/reference/gpu.py:86-103,177; gpu_monitor.yaml:24-28)."""
+
+import json
+import os
+
+from gpumon.export import promtext
+
+CID_A = "a" * 63 + "1"
+CID_B = "b" * 63 + "2"
+UID_A = "1f0c6a8e-5d1b-4c53-9f8e-0000000000a1"
+UID_B = "2e1d7b9f-6e2c-4d64-8a9f-0000000000b2"
+
+
+def _fake_proc(root, pid, cgroup_line):
+    d = root / str(pid)
+    d.mkdir(parents=True)
+    (d / "stat").write_text(f"{pid} (python) S 1 1 1 0 -1 0 0 0 0 0 0 0 0 0 20 0 1 0 777 0 0\n")
+    (d / "cgroup").write_text(cgroup_line + "\n")
+
+
+def _log_tree(root):
+    pods, ctrs = root / "pods", root / "containers"
+    for ns, pod, uid, ctr, cid in (("ml", "turing-gpu-notebook-alice-5d8f-x1", UID_A, "notebook", CID_A),
+                                   ("research", "jupyter-q-0", UID_B, "main", CID_B)):
+        (pods / f"{ns}_{pod}_{uid}" / ctr).mkdir(parents=True)
+        ctrs.mkdir(exist_ok=True)
+        os.symlink(f"/var/log/pods/{ns}_{pod}_{uid}/{ctr}/0.log", ctrs / f"{pod}_{ns}_{ctr}-{cid}.log")
+    (ctrs / "not-a-kubelet-log.txt").write_text("")  # ignored
+
+
+def _checkpoint(path, v1=False):
+    def ids(x):
+        return x if v1 else {"0": x}
+
+    entries = [
+        {"PodUID": UID_A, "ContainerName": "notebook", "ResourceName": "amd.com/gpu",
+         "DeviceIDs": ids(["0000:05:00.0"]), "AllocResp": "Cg=="},
+        {"PodUID": UID_B, "ContainerName": "main", "ResourceName": "amd.com/gpu",
+         "DeviceIDs": ids(["0000:25:00.0"]), "AllocResp": "Cg=="},
+        {"PodUID": UID_B, "ContainerName": "main", "ResourceName": "example.com/nic",
+         "DeviceIDs": ids(["eth9"]), "AllocResp": ""},
+        {"PodUID": "gone-pod-uid", "ContainerName": "c", "ResourceName": "amd.com/gpu",
+         "DeviceIDs": ids(["0000:45:00.0"]), "AllocResp": ""},  # pod no longer on the node
+    ]
+    body = {"Data": {"PodDeviceEntries": entries, "RegisteredDevices": {"amd.com/gpu": ["0000:05:00.0"]}},
+            "Checksum": 1234567}
+    path.write_text(json.dumps(body))
+
+
+def test_pod_metadata_and_idle_rows_without_any_socket(core, tmp_path):
+    proc = tmp_path / "proc"
+    _fake_proc(proc, 2000, f"0::/kubepods.slice/kubepods-pod{UID_A.replace('-', '_')}.slice/"
+                           f"cri-containerd-{CID_A}.scope")
+    logs = tmp_path / "log"
+    _log_tree(logs)
+    ckpt = tmp_path / "kubelet_internal_checkpoint"
+    _checkpoint(ckpt)
+    ex = core.Exporter({"backend": "mock:gpus=3", "serve_http": False, "interval_s": 0, "host": "n1",
+                        "procfs_root": str(proc), "pod_log_root": str(logs), "device_checkpoint": str(ckpt)})
+    assert ex.start() == ""
+    try:
+        ex.mock_set_procs([{"pid": 2000, "device": 0, "name": "python train.py", "vram_bytes": 5 << 30}])
+        ex.tick()
+        rows = {(r["dev"], r["idle"]): r for r in ex.pod_rows()}
+        busy = rows[(0, False)]
+        assert (busy["namespace"], busy["podname"], busy["container"], busy["containerid"]) == \
+            ("ml", "turing-gpu-notebook-alice-5d8f-x1", "notebook", CID_A[:12])
+        assert busy["user_name"] == "alice"  # the reference's user rule on the pod name (gpu.py:196-199)
+        idle = rows[(1, True)]  # jupyter-q-0 holds GPU 1 (0000:25:00.0) and runs nothing on it
+        assert (idle["namespace"], idle["podname"], idle["container"], idle["containerid"]) == \
+            ("research", "jupyter-q-0", "main", CID_B[:12])
+        assert (0, True) not in rows  # the allocation of GPU 0 is in use: no idle row
+        assert not [r for r in ex.pod_rows() if r["dev"] == 2]  # the departed pod's GPU
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpumon_kubelet_files_up", source="pod_logs") == 1
+        assert promtext.one(fam, "gpumon_kubelet_files_up", source="device_checkpoint") == 1
+        assert promtext.one(fam, "gpumon_kubelet_files_containers") == 2
+    finally:
+        ex.stop()
+
+
+def test_checkpoint_v1_list_form_and_unreadable_files(core, tmp_path):
+    """Older kubelets checkpoint DeviceIDs as a plain list; an unreadable or malformed file reports
+    gpumon_kubelet_files_up 0 and keeps the exporter running."""
+    logs = tmp_path / "log"
+    _log_tree(logs)
+    ckpt = tmp_path / "ckpt"
+    _checkpoint(ckpt, v1=True)
+    ex = core.Exporter({"backend": "mock:gpus=2", "serve_http": False, "interval_s": 0, "host": "n1",
+                        "procfs_root": str(tmp_path / "proc"), "pod_log_root": str(logs),
+                        "device_checkpoint": str(ckpt)})
+    assert ex.start() == ""
+    try:
+        ex.tick()
+        idle = sorted((r["dev"], r["podname"]) for r in ex.pod_rows() if r["idle"])
+        assert idle == [(0, "turing-gpu-notebook-alice-5d8f-x1"), (1, "jupyter-q-0")]
+    finally:
+        ex.stop()
+    ckpt.write_text('{"Data": {"PodDeviceEntries": [{"PodUID": ')  # truncated
+    ex = core.Exporter({"backend": "mock:gpus=2", "serve_http": False, "interval_s": 0, "host": "n1",
+                        "pod_log_root": str(tmp_path / "nope"), "device_checkpoint": str(ckpt)})
+    assert ex.start() == ""
+    try:
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpumon_kubelet_files_up", source="pod_logs") == 0
+        assert promtext.one(fam, "gpumon_kubelet_files_up", source="device_checkpoint") == 0
+        assert not [r for r in ex.pod_rows() if r["idle"]]
+    finally:
+        ex.stop()
+
+
+def test_cri_metadata_wins_over_the_log_tree(core, tmp_path):
+    """The files are the lowest-priority source: a container the CRI runtime (or Docker) reports
+    keeps that metadata (labels included); the log tree only fills containers nobody else named."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracles.attribution.fake_kubelet import FakeKubelet, FakePod
+
+    proc = tmp_path / "proc"
+    _fake_proc(proc, 2000, f"0::/kubepods.slice/cri-containerd-{CID_A}.scope")
+    _fake_proc(proc, 3000, f"0::/kubepods.slice/cri-containerd-{CID_B}.scope")
+    logs = tmp_path / "log"
+    _log_tree(logs)
+    with FakeKubelet(podres_socket=str(tmp_path / "pr.sock"), cri_socket=str(tmp_path / "cri.sock")) as k:
+        k.pods = [FakePod("renamed-by-cri-0", "ml", UID_A, labels={"team": "x"},
+                          containers={"notebook": (CID_A, ["0000:05:00.0"])})]
+        ex = core.Exporter({"backend": "mock:gpus=2", "serve_http": False, "interval_s": 0, "host": "n1",
+                            "procfs_root": str(proc), "pod_log_root": str(logs), "cri_socket": k.cri_socket,
+                            "label_allowlist": ["team"]})
+        assert ex.start() == ""
+        try:
+            ex.mock_set_procs([{"pid": 2000, "device": 0, "vram_bytes": 1 << 30},
+                               {"pid": 3000, "device": 1, "vram_bytes": 1 << 30}])
+            ex.tick()
+            by_pid = {r["pid"]: r for r in ex.pod_rows() if not r["idle"]}
+            assert by_pid["2000"]["podname"] == "renamed-by-cri-0"  # CRI
+            assert by_pid["3000"]["podname"] == "jupyter-q-0"  # the log tree fills the gap
+        finally:
+            ex.stop()
