@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
@@ -573,8 +574,12 @@ XgmiStats XgmiLoad::stats() const {
 Probe::Probe(int dev, int blocks, int slots, int spin_ticks)
     : dev_(dev), blocks_(std::max(1, blocks)), slots_(std::max(1, slots)), spin_(std::max(1, spin_ticks)) {
   check(hipSetDevice(dev_), "hipSetDevice");
-  hipStream_t s;
-  check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  // Every HIP stream is a hardware queue, and on MI355X each queue pins a ~173 MB host context-save
+  // area (profiles/r2_footprint.md). GPUMON_PROBE_STREAM=null runs the probe on the device's null
+  // stream instead of a stream of its own (the helper issues nothing else through HIP).
+  hipStream_t s = nullptr;
+  const char* mode = getenv("GPUMON_PROBE_STREAM");
+  if (!(mode && !strcmp(mode, "null"))) check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
   stream_ = s;
   const size_t rb = sizeof(ProbeRecord) * static_cast<size_t>(blocks_) * slots_;
   check(hipHostMalloc(reinterpret_cast<void**>(&ring_), rb, hipHostMallocMapped | hipHostMallocCoherent),

@@ -5,7 +5,10 @@ The reference intrudes on tenants: ``docker exec`` into the workload container e
 stalls; :func:`measure` puts a number on that.
 
 The TENANT is the K2 load running in this process (one ``SyntheticLoad`` per kind, event-timed
-FLOP/s or bytes/s). The EXPORTER is ``bin/gpumon-exporter`` started as a separate process per
+FLOP/s or bytes/s), or -- kinds ``gemm`` / ``gemm_shared`` -- PyTorch processes running hipBLASLt
+bf16 GEMMs back to back (library kernels, not this repo's burns): ``gemm`` one 8192^3 tenant,
+event-timed; ``gemm_shared`` an 8192^3 and a 4096^3 tenant on the same GPU, their summed FLOPs
+over wall time (the shared-GPU case). The EXPORTER is ``bin/gpumon-exporter`` started as a separate process per
 condition (the deployment shape: a DaemonSet pod next to the workload pods), scraped once per
 second like a Prometheus server would. Conditions are interleaved (A B C D A B C D ...) so clock
 and thermal drift land on every condition alike; each window's tenant rate is the event-timed
@@ -74,6 +77,85 @@ class _Exporter:
         return (err or "")[-400:]
 
 
+GEMM_TENANT = r"""
+import sys, time, torch
+n = int(sys.argv[1])
+a = torch.randn(n, n, device="cuda:0", dtype=torch.bfloat16)
+b = torch.randn(n, n, device="cuda:0", dtype=torch.bfloat16)
+for _ in range(10):
+    a @ b
+torch.cuda.synchronize()
+print("ready", flush=True)
+batch = max(1, int(8 * (8192 / n) ** 3))  # ~7 ms of GEMMs per event pair at any size
+while True:
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(batch):
+        a @ b
+    e1.record()
+    e1.synchronize()
+    print(time.time(), 2.0 * n ** 3 * batch, e0.elapsed_time(e1), flush=True)
+"""
+
+
+class GemmTenants:
+    """PyTorch hipBLASLt bf16 GEMM tenants in their own processes; stats() mirrors LoadGen.stats()
+    for _rate(): cumulative FLOPs and either the event-timed GPU seconds (one tenant) or the wall
+    seconds since start (several tenants: their combined throughput over wall time)."""
+
+    def __init__(self, sizes=(8192,), device: int = 0):
+        import sys
+        import threading
+
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(device))
+        self.procs = [subprocess.Popen([sys.executable, "-c", GEMM_TENANT, str(n)], stdout=subprocess.PIPE,
+                                       stderr=subprocess.PIPE, text=True, env=env) for n in sizes]
+        self.flops = 0.0
+        self.gpu_s = 0.0
+        self.lock = threading.Lock()
+        self.ready = 0
+        self.t0 = None
+        self.threads = [threading.Thread(target=self._read, args=(p,), daemon=True) for p in self.procs]
+        for t in self.threads:
+            t.start()
+
+    def _read(self, p):
+        for line in p.stdout:
+            if line.startswith("ready"):
+                with self.lock:
+                    self.ready += 1
+                continue
+            _, fl, ms = line.split()
+            with self.lock:
+                self.flops += float(fl)
+                self.gpu_s += float(ms) * 1e-3
+
+    def wait_ready(self, timeout_s: float = 240.0) -> None:
+        deadline = time.time() + timeout_s
+        while self.ready < len(self.procs):
+            if any(p.poll() is not None for p in self.procs) or time.time() > deadline:
+                errs = " | ".join((p.stderr.read() or "")[-300:] for p in self.procs if p.poll() is not None)
+                raise RuntimeError(f"GEMM tenant did not start: {errs}")
+            time.sleep(0.1)
+        self.t0 = time.perf_counter()
+
+    def stats(self) -> dict:
+        with self.lock:
+            wall = time.perf_counter() - (self.t0 or time.perf_counter())
+            # one tenant: event-timed (GPU-busy) seconds; several: wall seconds
+            return {"flops": self.flops, "mfma_s": self.gpu_s if len(self.procs) == 1 else wall}
+
+    def __enter__(self):
+        self.wait_ready()
+        return self
+
+    def __exit__(self, *exc):
+        for p in self.procs:
+            p.kill()
+        for p in self.procs:
+            p.wait(30)
+
+
 def _rate(kind: str, s0: dict, s1: dict) -> float:
     """Event-timed tenant rate between two LoadGen stats: TFLOP/s (mfma) or TB/s (hbm)."""
     if kind == "hbm":
@@ -93,7 +175,9 @@ def measure(kinds=("mfma", "hbm"), conditions=tuple(CONDITIONS), reps: int = 3, 
     for kind in kinds:
         res = {c: [] for c in conditions}
         extra = {c: {"scrapes": 0, "scrape_errors": 0} for c in conditions}
-        with SyntheticLoad(device, kind) as load:
+        tenant = (GemmTenants((8192,), device) if kind == "gemm" else
+                  GemmTenants((8192, 4096), device) if kind == "gemm_shared" else SyntheticLoad(device, kind))
+        with tenant as load:
             time.sleep(settle_s * 2)  # clocks / power settle under the load first
             for r in range(reps):
                 for c in conditions:

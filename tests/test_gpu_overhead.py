@@ -16,3 +16,15 @@ def test_default_exporter_costs_the_tenant_under_one_percent():
     assert k["none"]["median"] > 1500, k  # the burn really ran (TFLOP/s)
     assert k["1hz"]["scrapes"] >= 6 and k["1hz"]["scrape_errors"] == 0, k
     assert k["1hz"]["slowdown_pct"] <= 1.0, k
+
+
+def test_default_exporter_costs_a_hipblaslt_gemm_tenant_under_one_percent():
+    """the same bound on a library GEMM tenant (PyTorch bf16 8192^3 GEMMs through
+    hipBLASLt in its own process), not only on this repo's burn kernel."""
+    from gpumon.ops.tenant import measure
+
+    r = measure(kinds=("gemm",), conditions=("none", "1hz"), reps=3, window_s=3.0, settle_s=1.0)
+    k = r["kinds"]["gemm"]
+    assert k["none"]["median"] > 800, k  # hipBLASLt bf16 really ran (TFLOP/s, event-timed)
+    assert k["1hz"]["scrape_errors"] == 0, k
+    assert k["1hz"]["slowdown_pct"] <= 1.0, k
