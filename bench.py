@@ -62,6 +62,18 @@ def _pct(xs, q):
     return xs[f] if f == c else xs[f] + (xs[c] - xs[f]) * (k - f)
 
 
+def _ci(xs, q, n_boot=200, seed=1):
+    """95 % bootstrap interval of the q-quantile (ms): how much a p99 over this many samples can
+    move from resampling alone."""
+    import random
+
+    if len(xs) < 20:
+        return None
+    rnd = random.Random(seed)
+    est = sorted(_pct([rnd.choice(xs) for _ in xs], q) for _ in range(n_boot))
+    return [round(est[int(0.025 * n_boot)] * 1e3, 4), round(est[int(0.975 * n_boot) - 1] * 1e3, 4)]
+
+
 def _r(x, nd=3):
     return round(x, nd) if isinstance(x, float) and x == x else x
 
@@ -246,6 +258,7 @@ def main() -> int:
                 "scrape_p50_ms": round(_pct(lat, 0.50) * 1e3, 4) if lat else None,
                 "scrape_p99_ms": round(_pct(lat, 0.99) * 1e3, 4) if lat else None,
                 "scrape_p999_ms": round(_pct(lat, 0.999) * 1e3, 4) if lat else None,
+                "scrape_p99_ci95_ms": _ci(lat, 0.99),
                 "server_scrape_p99_ms": round(_pct(srv, 0.99) * 1e3, 4) if srv else None,
                 "server_scrape_p999_ms": round(_pct(srv, 0.999) * 1e3, 4) if srv else None,
                 "ticks": len(it), "tick_mean_ms": round(sum(it) / len(it) * 1e3, 4) if it else None,
@@ -460,6 +473,7 @@ def main() -> int:
             "scrape_p50_ms": round(_pct(lat, 0.50) * 1e3, 4),
             "scrape_p99_ms": round(_pct(lat, 0.99) * 1e3, 4),
             "scrape_p999_ms": round(_pct(lat, 0.999) * 1e3, 4),
+            "scrape_p99_ci95_ms": _ci(lat, 0.99),
             "scrape_max_ms": round(max(lat) * 1e3, 4) if lat else None,
             "scrapes": len(lat),
             "scrape_rate_hz": args.scrape_rate,
