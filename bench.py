@@ -425,6 +425,13 @@ def main() -> int:
         util = [x["fields"].get("gfx_util") for x in sm]
         rows = mon.ex.pod_rows()
         value = samples / elapsed
+        from gpumon.export import promtext
+
+        fam = promtext.parse(mon.metrics())
+        slot_map = {}  # xGMI link-metrics entry -> table slot pairing (csrc/core/xgmi_map.cpp)
+        for what in ("verified", "unverified", "mismatch"):
+            for _, lab, v in fam.get(f"gpumon_xgmi_slot_map_{what}", {}).get("samples", []):
+                slot_map.setdefault(lab.get("gpu_id"), {})[what] = int(v)
         per_gpu = _per_gpu_xgmi(tick_rates, n, exp_tx, exp_rx) if xgmi is not None else None
         if xgmi is not None:
             tx = [r["exporter_tx_GBps"] for r in per_gpu if r["exporter_tx_GBps"] is not None]
@@ -522,6 +529,7 @@ def main() -> int:
                           for r in rows if not r["idle"]][:16],
             "occupancy_reads": s1.get("occupancy_reads", 0) - s0.get("occupancy_reads", 0),
             "xgmi": xgmi,
+            "xgmi_slot_map": slot_map or None,
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,
         }
         mon.stop()

@@ -76,7 +76,7 @@ class Config:
     include_host_processes: bool = True
     # control plane (k8s)
     control_plane: str = "native"         # native (C++ grpc_lite CRI / PodResources / Docker pollers) | off
-    cri_socket: str = ""                  # e.g. unix:///run/containerd/containerd.sock ; "" = autodetect
+    cri_socket: str = ""                  # e.g. unix:///run/containerd/containerd.sock ; "" = autodetect ; none = off
     pod_resources_socket: str = "/var/lib/kubelet/pod-resources/kubelet.sock"
     docker_socket: str = ""               # plain-Docker nodes (native plane): Docker Engine container names + labels; opt-in, e.g. /var/run/docker.sock
     # socket-free metadata for a non-root exporter (csrc/core/kubelet_files.h): the kubelet's log tree

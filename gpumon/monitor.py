@@ -43,10 +43,11 @@ class GpuMonitor:
             mode = "native"
         if mode == "native":
             # the exporter's own C++ pollers (csrc/core/grpc_lite.cpp) -- same as bin/gpumon-exporter
-            if os.path.exists(self.cfg.pod_resources_socket):
+            if self.cfg.pod_resources_socket not in ("", "none") and os.path.exists(self.cfg.pod_resources_socket):
                 core_cfg["pod_resources_socket"] = self.cfg.pod_resources_socket
+            # "" = autodetect, "none" = no CRI source (same rule as the native binary's options)
             cri = self.cfg.cri_socket or next((p for p in _CRI_SOCKETS if os.path.exists(p)), "")
-            if cri:
+            if cri and cri != "none":
                 core_cfg["cri_socket"] = cri[len("unix://"):] if cri.startswith("unix://") else cri
             if self.cfg.docker_socket:  # opt-in: never autodetected (root-equivalent socket)
                 d = self.cfg.docker_socket

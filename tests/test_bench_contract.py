@@ -45,6 +45,13 @@ def test_bench_single_process():
     assert lines[0]["value"] == pytest.approx(10.0, rel=0.2)  # 1 device x 10 Hz
     idle = lines[0]["scrape_idle"]  # untimed idle reference before the load
     assert idle["scrapes"] > 5 and idle["scrape_errors"] == 0 and idle["scrape_p99_ms"] > 0 and idle["ticks"] >= 5
+    d = lines[0]
+    # tail statistics worth quoting -- p99.9, the exporter's own service time of the
+    # same requests (exact, server side), and what `value` measures
+    assert d["scrape_p999_ms"] >= d["scrape_p99_ms"] > 0 and d["scrape_rate_hz"] >= 100
+    assert d["server_scrapes"] == d["scrapes"] and 0 < d["server_scrape_p99_ms"] <= d["scrape_max_ms"]
+    assert "interval" in d["value_note"]
+    assert idle["server_scrape_p99_ms"] > 0 and idle["scrape_p999_ms"] >= idle["scrape_p99_ms"]
 
 
 @pytest.mark.slow
