@@ -29,8 +29,8 @@ BIN       := bin/gpumon-exporter
 HIP_SRC   := $(wildcard csrc/hip/*.hip)
 HIP_HDR   := $(wildcard csrc/hip/*.h)
 
-.PHONY: all core hip pmc plugins clean asan tsan fakes
-all: core hip plugins pmc
+.PHONY: all core hip pmc plugins clean asan tsan fakes nodev
+all: core hip plugins pmc nodev
 core: $(PYEXT) $(BIN)
 hip: $(HIPEXT)
 
@@ -95,6 +95,14 @@ tsan: bin/gpumon-exporter-tsan
 bin/gpumon-exporter-tsan: $(TSAN_OBJ)
 	@mkdir -p bin
 	$(CXX) -fsanitize=thread $^ -o $@ $(LIBS)
+
+# Test tool: the exporter with /dev/kfd and /dev/dri opens refused (csrc/testtools/nodev_interpose.cpp,
+# tools/no_device_check.sh): what an unprivileged pod without device access still exports.
+nodev: bin/gpumon-exporter-nodev
+bin/gpumon-exporter-nodev: $(CORE_OBJ) build/obj/exporter_main.o csrc/testtools/nodev_interpose.cpp
+	@mkdir -p bin build/obj/testtools
+	$(CXX) $(CXXFLAGS) -c csrc/testtools/nodev_interpose.cpp -o build/obj/testtools/nodev_interpose.o
+	$(CXX) -rdynamic -o $@ $(CORE_OBJ) build/obj/exporter_main.o build/obj/testtools/nodev_interpose.o $(LIBS)
 
 clean:
 	rm -rf build bin lib gpumon/_core*.so gpumon/_hip*.so gpumon/_pmc*.so

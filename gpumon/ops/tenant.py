@@ -86,7 +86,7 @@ for _ in range(10):
     a @ b
 torch.cuda.synchronize()
 print("ready", flush=True)
-batch = max(1, int(8 * (8192 / n) ** 3))  # ~7 ms of GEMMs per event pair at any size
+batch = max(1, int(2 * (8192 / n) ** 3))  # ~1.6 ms of GEMMs per event pair at any size
 while True:
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()

@@ -1,9 +1,11 @@
 #!/bin/bash
 # What the default exporter still exports WITHOUT access to /dev/kfd and /dev/dri -- the situation
-# of an unprivileged DaemonSet pod (drop `privileged: true`). A user + mount
-# namespace hides both device nodes (tmpfs over /dev/dri, /dev/null over /dev/kfd) from one run of
-# bin/gpumon-exporter --once; a second run with the devices is the reference. A torch tenant keeps
-# a KFD process on the GPU meanwhile, so the process rows are compared too.
+# of an unprivileged DaemonSet pod (drop `privileged: true`): the device cgroup
+# refuses the hostPath device nodes. bin/gpumon-exporter-nodev (`make nodev`) is the exporter with
+# every open of /dev/kfd and /dev/dri/* refused with EPERM (csrc/testtools/nodev_interpose.cpp,
+# interposed on libamd_smi / libdrm / hsakmt); bin/gpumon-exporter is the reference run. A torch
+# tenant keeps a KFD process on the GPU meanwhile, so the process rows are compared too.
+# (A user + mount namespace that hides the nodes is not available on the gpurun boxes.)
 #
 #   tools/no_device_check.sh [OUTDIR]      (on the GPU box; writes OUTDIR/{with_dev,no_dev}.prom, summary.json)
 set -o pipefail
@@ -16,9 +18,15 @@ tenant=$!
 sleep 12
 timeout -k 5 60 ./bin/gpumon-exporter $ARGS > "$out/with_dev.prom" 2> "$out/with_dev.err"
 rc1=$?
-timeout -k 5 60 unshare -Urm sh -c "mount -t tmpfs tmpfs /dev/dri && mount --bind /dev/null /dev/kfd && ls -la /dev/dri /dev/kfd >&2 && ./bin/gpumon-exporter $ARGS" \
-  > "$out/no_dev.prom" 2> "$out/no_dev.err"
+timeout -k 5 60 ./bin/gpumon-exporter-nodev $ARGS > "$out/no_dev.prom" 2> "$out/no_dev.err"
 rc2=$?
+# which device nodes a running default exporter keeps open (complementary evidence)
+./bin/gpumon-exporter --backend amdsmi --interval 0.5 --listen 127.0.0.1:0 --no-pod-resources --no-cri \
+  --log-level warn > /dev/null 2>&1 &
+ex=$!
+sleep 4
+ls -l /proc/$ex/fd 2>/dev/null | grep -o '/dev/[a-z/A-Z0-9]*' | sort | uniq -c > "$out/open_device_nodes.txt" || true
+kill $ex; wait $ex 2>/dev/null
 wait $tenant
 python - "$out" "$rc1" "$rc2" <<'EOF'
 import json, sys
