@@ -161,7 +161,7 @@ def test_alert_and_recording_rules_resolve(mock_exporter):
     produced |= _plugin_metric_names()  # the on-device samplers' series (PMC, probe, helper)
     produced |= _control_plane_metric_names()  # CRI / PodResources / Docker pollers
     words = {"sum", "by", "count", "rate", "increase", "delta", "avg", "max", "time", "host", "namespace", "podname",
-             "gpu_id", "user_name"}
+             "gpu_id", "user_name", "on"}
     exprs = [r["expr"] for g in rule["spec"]["groups"] for r in g["rules"]]
     assert len(exprs) >= 12
     for e in exprs:
