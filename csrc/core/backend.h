@@ -52,6 +52,9 @@ class Backend {
   // the last tick instead).
   virtual bool occupancy_scan(int, std::vector<OccRead>*) { return false; }
   virtual void sample_ras(int, DeviceSample*, int /*slice*/ = 0, int /*nslices*/ = 1) {}
+  // May processes(i) run on another thread while sample(i) runs (the device worker then overlaps
+  // the process list with the firmware-table read)? Only where both read independent files.
+  virtual bool concurrent_processes(int /*i*/) const { return false; }
   // Upkeep that must stay off the tick's critical path (the device worker calls it after it
   // published the tick's sample): e.g. refreshing cached /proc fd tables.
   virtual void maintain(int /*i*/) {}
@@ -144,6 +147,7 @@ class MockBackend : public Backend {
   bool supports_ras() const override { return true; }
   void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;
   bool supports_occupancy(int) const override { return cfg_.occupancy; }
+  bool concurrent_processes(int) const override { return true; }  // every call holds mu_
   void occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) override;
   bool occupancy_scan(int i, std::vector<OccRead>* out) override;
 
@@ -211,6 +215,8 @@ class AmdSmiBackend : public Backend {
   bool supports_ras() const override { return true; }
   void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;
   bool supports_occupancy(int i) const override;  // with the sysfs fast path (KFD files)
+  // sysfs fast path: the table pread and the KFD / fdinfo reads share no state
+  bool concurrent_processes(int i) const override { return supports_occupancy(i); }
   void maintain(int i) override;                   // fast path: due /proc fd-table refreshes
   void occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) override;
   bool occupancy_scan(int i, std::vector<OccRead>* out) override;

@@ -106,6 +106,53 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
   // 10 %-resident arrival otherwise had one read in its first interval).
   bool scan_ok = occ_on;
   int64_t next_occ = 0;
+  // The process list (KFD + fdinfo reads, ~0.1 ms) runs on a second thread while this one reads
+  // the firmware table (~0.2 ms, mostly the SMU fetch): the device's part of a tick becomes the
+  // longer of the two instead of their sum. Only where the backend allows it (sysfs fast path).
+  struct ProcJob {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool want = false, done = false, quit = false;
+    std::vector<ProcSample> out;
+    int64_t ns = 0;
+  };
+  std::shared_ptr<ProcJob> job;
+  std::thread proc_thread;
+  if (backend->concurrent_processes(i)) {
+    job = std::make_shared<ProcJob>();
+    proc_thread = std::thread([job, backend, i] {
+      set_thread_name("gpumon-proc" + std::to_string(i));
+      std::unique_lock<std::mutex> lk(job->mu);
+      for (;;) {
+        job->cv.wait(lk, [&] { return job->want || job->quit; });
+        if (job->quit) return;
+        job->want = false;
+        lk.unlock();
+        std::vector<ProcSample> p;
+        const int64_t t = mono_ns();
+        backend->processes(i, &p);
+        const int64_t ns = mono_ns() - t;
+        lk.lock();
+        job->out = std::move(p);
+        job->ns = ns;
+        job->done = true;
+        job->cv.notify_all();
+      }
+    });
+  }
+  struct ProcJoin {  // every return path: stop and join the process-list thread
+    std::shared_ptr<ProcJob>& job;
+    std::thread& th;
+    ~ProcJoin() {
+      if (!job) return;
+      {
+        std::lock_guard<std::mutex> g(job->mu);
+        job->quit = true;
+      }
+      job->cv.notify_all();
+      if (th.joinable()) th.join();
+    }
+  } proc_join{job, proc_thread};
   // RAS refreshes read off the tick's critical path: the worker reads the slice right after it
   // published the tick (the files cost 0.25-0.5 ms under load: the slowest tick of every RAS pass,
   // profiles/r2_bench.md) and the next tick carries the result.
@@ -185,6 +232,13 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
     const int64_t t_dev0 = mono_ns();
     {
       TraceRange tr("gpumon.sample_dev");
+      const bool overlap = procs && job;
+      if (overlap) {
+        std::lock_guard<std::mutex> g(job->mu);
+        job->want = true;
+        job->done = false;
+      }
+      if (overlap) job->cv.notify_all();
       backend->sample(i, &s);
       if (links) backend->sample_links(i, &s);
       if (have_ras_ready && s.ok) {
@@ -192,7 +246,15 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
         have_ras_ready = false;
       }
       if (ras && !ras_async && s.ok) backend->sample_ras(i, &s, ras_slice, ras_n);
-      if (procs && s.ok) {
+      if (overlap) {
+        std::unique_lock<std::mutex> lk(job->mu);
+        job->cv.wait(lk, [&] { return job->done; });
+        if (s.ok) {
+          p = std::move(job->out);
+          pns = job->ns;
+        }
+        job->out.clear();
+      } else if (procs && s.ok) {
         const int64_t t = mono_ns();
         backend->processes(i, &p);
         pns = mono_ns() - t;
