@@ -310,3 +310,83 @@ def test_dockerfile_installs_no_grpc():
     installs = [l for l in text.splitlines() if "pip3 install" in l]
     assert installs and not any("grpc" in l or "protobuf" in l for l in installs), installs
     assert "tests" not in " ".join(l for l in text.splitlines() if l.startswith("COPY")), "oracles stay out of the image"
+
+
+def test_base_pod_is_unprivileged():
+    """the base DaemonSet runs unprivileged -- no privileged flag, no privilege
+    escalation, every capability dropped except the two with a named use, and no device node
+    mounted (the default exporter opens none: profiles/r3_no_device.md). The reference pod had
+    root-equivalent docker.sock access (/root/reference/gpu_monitor.yaml:24-28,38-44)."""
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    pod = ds["spec"]["template"]["spec"]
+    (c,) = pod["containers"]
+    sc = c["securityContext"]
+    assert sc.get("privileged", False) is False and sc["allowPrivilegeEscalation"] is False
+    assert sc["readOnlyRootFilesystem"] is True and sc["seccompProfile"]["type"] == "RuntimeDefault"
+    assert sc["capabilities"]["drop"] == ["ALL"]
+    assert set(sc["capabilities"].get("add", [])) <= {"SYS_PTRACE", "SYS_NICE"}
+    assert not pod.get("hostNetwork") and not pod.get("hostIPC")
+    mounts = {m["mountPath"] for m in c["volumeMounts"]}
+    assert not any(m.startswith("/dev") for m in mounts), mounts
+    assert all(not v.get("hostPath", {}).get("path", "").startswith("/dev") for v in pod["volumes"])
+    assert {"/var/log/pods", "/var/log/containers"} <= mounts  # socket-free metadata
+    assert all(m.get("readOnly") for m in c["volumeMounts"])  # the exporter writes nothing on the host
+
+
+def test_elevated_rights_only_in_the_ondevice_overlay():
+    """PMC device counting and the K1 probe open /dev/kfd: only the ondevice overlay is privileged
+    and mounts the device nodes; the docker overlay adds its socket and nothing else."""
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+
+    def patched(overlay):
+        (k,) = _docs(f"deploy/k8s/overlays/{overlay}/kustomization.yaml")
+        ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"])
+        return _json_patch(ds, ops)["spec"]["template"]["spec"]
+
+    pod = patched("ondevice")
+    c = pod["containers"][0]
+    assert c["securityContext"]["privileged"] is True
+    assert {"/dev/kfd", "/dev/dri"} <= {m["mountPath"] for m in c["volumeMounts"]}
+    vols = {v["name"] for v in pod["volumes"]}
+    assert all(m["name"] in vols for m in c["volumeMounts"])
+    pod = patched("docker")
+    assert pod["containers"][0]["securityContext"].get("privileged", False) is False
+
+
+def test_nonroot_overlay():
+    """A strictly non-root pod: no capabilities, runAsNonRoot, no kubelet / CRI socket (they accept
+    root only), pod metadata from the kubelet's log tree (csrc/core/kubelet_files.h)."""
+    from gpumon.config import Config
+
+    (k,) = _docs("deploy/k8s/overlays/nonroot/kustomization.yaml")
+    assert k["resources"] == ["../../"]
+    cfg_patch = next(p for p in k["patches"] if p["target"]["kind"] == "ConfigMap")
+    c = Config().apply_dict(yaml.safe_load(yaml.safe_load(cfg_patch["patch"])[0]["value"])["gpumon"])
+    assert c.pod_log_root == "/var/log" and c.cri_socket == "none" and c.pod_resources_socket == ""
+    assert c.rt_priority == 0
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"])
+    ctr = _json_patch(ds, ops)["spec"]["template"]["spec"]["containers"][0]
+    sc = ctr["securityContext"]
+    assert sc["runAsNonRoot"] is True and sc["runAsUser"] != 0 and sc["capabilities"] == {"drop": ["ALL"]}
+    assert sc["allowPrivilegeEscalation"] is False and not sc.get("privileged")
+    assert {"/var/log/pods", "/var/log/containers"} <= {m["mountPath"] for m in ctr["volumeMounts"]}
+
+
+def test_overlay_configs_are_valid_for_the_native_binary(tmp_path):
+    """Every overlay's ConfigMap is accepted by bin/gpumon-exporter --config (the Python-free
+    entrypoint reads the same keys)."""
+    import subprocess
+
+    from conftest import make_locked
+
+    make_locked("core")
+    for overlay in ("ondevice", "docker", "nonroot"):
+        (k,) = _docs(f"deploy/k8s/overlays/{overlay}/kustomization.yaml")
+        value = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "ConfigMap")["patch"])[0]["value"]
+        f = tmp_path / f"{overlay}.yaml"
+        f.write_text(value)
+        r = subprocess.run([os.path.join(ROOT, "bin", "gpumon-exporter"), "--config", str(f), "--print-config"],
+                           capture_output=True, text=True, timeout=30)
+        assert r.returncode == 0, (overlay, r.stderr[-1000:])
+        assert "unknown" not in r.stderr.lower(), (overlay, r.stderr[-1000:])
