@@ -114,6 +114,18 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
             else:
                 code_s = "-" if code is None else int(code)
                 out.append((name, WARN, f"{sock}: down ({status.replace('_', '-')} {code_s}): {lost}"))
+        # socket-free metadata (non-root deployments): the kubelet's log tree / device checkpoint
+        for name, src, path, lost in (
+                ("kubelet log tree", "pod_logs", cfg.pod_log_root,
+                 "containers the CRI source does not name stay at their /proc fallbacks"),
+                ("device-plugin checkpoint", "device_checkpoint", cfg.device_checkpoint,
+                 "no idle-allocation rows without PodResources (the file is root 0600 by default)")):
+            if not path:
+                out.append((name, SKIP, f"off ({src.replace('pod_logs', 'pod_log_root')} not set)"))
+                continue
+            m = re.search(r'^gpumon_kubelet_files_up\{[^}]*source="' + src + r'"[^}]*\} (\S+)$', text, re.M)
+            up = float(m.group(1)) if m else None
+            out.append((name, OK if up == 1 else WARN, f"{path}: readable" if up == 1 else f"{path}: unreadable: {lost}"))
         out.append(("rt_priority",) + _rt_permitted())
         # on-device samplers: the helper and plugins must exist; --ondevice-check runs them once
         from ._native import core as _core

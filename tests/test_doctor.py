@@ -89,3 +89,19 @@ def test_doctor_checks_the_docker_socket_when_configured():
     s, _ = _by_name(doctor.run(Config(backend="mock:gpus=1", control_plane="native", pod_resources_socket="",
                                       cri_socket="", log_level="error"), wait_s=1))["Docker Engine"]
     assert s == "skip"  # never autodetected
+
+
+def test_doctor_checks_the_kubelet_files_when_configured(tmp_path):
+    """Non-root deployments name pods from the kubelet's log tree: the doctor says whether it (and
+    the device-plugin checkpoint) could be read."""
+    (tmp_path / "log" / "pods").mkdir(parents=True)
+    (tmp_path / "log" / "containers").mkdir()
+    cfg = Config(backend="mock:gpus=1", control_plane="native", pod_resources_socket="", cri_socket="none",
+                 pod_log_root=str(tmp_path / "log"), device_checkpoint=str(tmp_path / "missing"), log_level="error")
+    checks = _by_name(doctor.run(cfg, wait_s=1))
+    assert checks["kubelet log tree"][0] == "ok", checks["kubelet log tree"]
+    assert checks["device-plugin checkpoint"][0] == "warn" and "unreadable" in checks["device-plugin checkpoint"][1]
+    cfg = Config(backend="mock:gpus=1", control_plane="native", pod_resources_socket="", cri_socket="none",
+                 log_level="error")
+    checks = _by_name(doctor.run(cfg, wait_s=1))
+    assert checks["kubelet log tree"][0] == "skip"
