@@ -20,6 +20,7 @@
 #include "../core/snapshot.h"
 #include "../core/trace.h"
 #include "../core/sysfs_fast.h"
+#include "../core/xgmi_map.h"
 
 namespace py = pybind11;
 using namespace gpumon;
@@ -661,6 +662,42 @@ PYBIND11_MODULE(_core, m) {
       },
       py::arg("method"), py::arg("url"), py::arg("body") = "", py::arg("headers") = "",
       py::arg("timeout_s") = 5.0);
+
+  // xGMI link-metrics entry -> gpu_metrics slot pairing (xgmi_map.h), for direct unit tests.
+  py::class_<XgmiSlotMap>(m, "XgmiSlotMap")
+      .def(py::init<>())
+      .def(
+          "update",
+          [](XgmiSlotMap& mp, const py::list& entries, const std::vector<uint64_t>& rd, const std::vector<uint64_t>& wr,
+             const std::vector<int>& status) {
+            DeviceSample s;
+            s.acc.valid = true;
+            s.acc.n_links_acc = static_cast<int>(std::min<size_t>(rd.size(), kMaxLinks));
+            for (int k = 0; k < s.acc.n_links_acc; ++k) {
+              s.acc.xgmi_rd_kb[k] = rd[k];
+              s.acc.xgmi_wr_kb[k] = k < static_cast<int>(wr.size()) ? wr[k] : 0;
+              s.links[k].status = k < static_cast<int>(status.size()) ? status[k] : 1;
+            }
+            for (auto e : entries) {
+              auto d = e.cast<py::dict>();
+              LinkEntry le;
+              le.peer_bdf = d.contains("bdf") ? d["bdf"].cast<std::string>() : "";
+              le.read_kb = d.contains("read") ? d["read"].cast<uint64_t>() : 0;
+              le.write_kb = d.contains("write") ? d["write"].cast<uint64_t>() : 0;
+              le.has_acc = !d.contains("has_acc") || d["has_acc"].cast<bool>();
+              s.link_entries.push_back(le);
+            }
+            mp.update(s);
+            std::vector<int> slots;
+            for (size_t j = 0; j < s.link_entries.size(); ++j) slots.push_back(mp.slot_of(j));
+            return slots;
+          },
+          py::arg("entries"), py::arg("rd"), py::arg("wr"), py::arg("status"),
+          "one link refresh: entries [{bdf, read, write}], the table slots' read / write KB and status; "
+          "returns the slot paired with each entry (-1 = none)")
+      .def_property_readonly("verified", &XgmiSlotMap::verified)
+      .def_property_readonly("unverified", &XgmiSlotMap::unverified)
+      .def_property_readonly("mismatched", &XgmiSlotMap::mismatched);
 
   py::class_<Exporter>(m, "Exporter")
       .def(py::init([](const py::dict& cfg) { return new Exporter(config_from(cfg)); }))

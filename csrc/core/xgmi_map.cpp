@@ -91,18 +91,23 @@ void XgmiSlotMap::update(const DeviceSample& s) {
   for (size_t j = 0; j < n; ++j)
     for (size_t m = j + 1; m < n; ++m)
       if (match[j] >= 0 && match[j] == match[m]) match[j] = match[m] = -2;
-  std::vector<char> claimed(kMaxLinks, 0);
   for (size_t j = 0; j < n; ++j)
     if (match[j] >= 0) {
       slot_[j] = match[j];
       verified_[j] = 1;
-      claimed[match[j]] = 1;
     } else if (match[j] == -2) {
       verified_[j] = 0;
     }
-  // an unpaired entry whose slot a paired one took: its peer is withheld, not guessed
+  // Slots held by verified entries (this refresh or an earlier one; this refresh's evidence wins
+  // over an older pairing of the same slot). An unverified entry on such a slot, or a verified one
+  // that lost its slot to newer evidence, has its peer withheld, not guessed.
+  std::vector<int> owner(kMaxLinks, -1);
   for (size_t j = 0; j < n; ++j)
-    if (match[j] < 0 && slot_[j] >= 0 && claimed[slot_[j]]) {
+    if (match[j] >= 0) owner[match[j]] = static_cast<int>(j);
+  for (size_t j = 0; j < n; ++j)
+    if (verified_[j] && match[j] < 0 && slot_[j] >= 0 && owner[slot_[j]] < 0) owner[slot_[j]] = static_cast<int>(j);
+  for (size_t j = 0; j < n; ++j)
+    if (slot_[j] >= 0 && owner[slot_[j]] >= 0 && owner[slot_[j]] != static_cast<int>(j)) {
       slot_[j] = -1;
       verified_[j] = 0;
     }

@@ -160,3 +160,73 @@ def test_real_backend_pairs_a_permuted_library_order(core, monkeypatch):
             assert _self_metric(ex, "gpumon_xgmi_slot_map_verified", 0) == len(listed)
         finally:
             ex.stop()
+
+
+# ------------------------------------------------------------- the pairing itself (XgmiSlotMap)
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+def _entries(perm, rd, wr):
+    # entry j describes table slot perm[j] (0 = self: no peer, no counters)
+    return [{"bdf": "" if k == 0 else "0000:%02x:00.0" % (0x40 + k), "read": rd[k] if k else 0,
+             "write": wr[k] if k else 0} for k in perm]
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(perm=st.permutations(list(range(8))),
+       rd=st.lists(st.integers(0, 10**12), min_size=8, max_size=8),
+       wr=st.lists(st.integers(0, 10**12), min_size=8, max_size=8))
+def test_pairing_is_never_wrong_and_never_doubles_a_slot(core, perm, rd, wr):
+    _check_pairing(core, perm, rd, wr)
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(perm=st.permutations(list(range(8))),
+       rd=st.lists(st.sampled_from([0, 10**9, 2 * 10**9]), min_size=8, max_size=8),
+       wr=st.lists(st.sampled_from([0, 10**9]), min_size=8, max_size=8))
+def test_pairing_with_many_identical_counters(core, perm, rd, wr):
+    """Idle or evenly loaded links (many slots with the same counters): ambiguous entries stay
+    unpaired; the ones that are unique still pair right."""
+    _check_pairing(core, perm, rd, wr)
+
+
+def _check_pairing(core, perm, rd, wr):
+    """Any entry order, any counters: a paired entry sits on the slot it describes; no slot carries
+    two entries; an entry whose counters match exactly one slot's is paired."""
+    status = [-1] + [1] * 7
+    m = core.XgmiSlotMap()
+    slots = m.update(_entries(perm, rd, wr), rd, wr, status)
+    used = [s for s in slots if s >= 0]
+    assert len(used) == len(set(used))
+    for j, k in enumerate(perm):
+        if k == 0:
+            continue
+        same = [q for q in range(1, 8) if abs(rd[q] - rd[k]) <= 65536 + max(rd[q], rd[k]) // 10000
+                and abs(wr[q] - wr[k]) <= 65536 + max(wr[q], wr[k]) // 10000]
+        exact = [q for q in range(1, 8) if rd[q] == rd[k] and wr[q] == wr[k]]
+        if len(exact) == 1 and rd[k] + wr[k] > 0 or len(same) == 1:
+            assert slots[j] == k, (perm, slots)  # identified
+        assert slots[j] in (k, -1) or j == slots[j], (perm, slots)  # paired right, withheld, or positional
+
+
+def test_deltas_pair_when_origins_differ_and_older_pairings_yield_to_newer(core):
+    status = [-1] + [1] * 7
+    rd0 = [0] + [10**9 * k for k in range(1, 8)]
+    wr0 = [0] + [5 * 10**8 * k for k in range(1, 8)]
+    perm = [0, 3, 1, 2, 7, 6, 5, 4]
+    off = 7 * 10**11  # entry counters with another origin: never equal to the table's
+
+    def ents(rd, wr):
+        return [{"bdf": "" if k == 0 else f"p{k}", "read": rd[k] + off if k else 0, "write": wr[k] + off if k else 0}
+                for k in perm]
+
+    m = core.XgmiSlotMap()
+    assert m.update(ents(rd0, wr0), rd0, wr0, status) == list(range(8))  # nothing to go on: positional
+    assert m.verified == 0 and m.unverified == 7
+    rd1 = [r + 10**6 * (3 * k + 1) for k, r in enumerate(rd0)]  # distinct traffic per link (KB)
+    wr1 = [w + 10**6 * (2 * k + 5) for k, w in enumerate(wr0)]
+    slots = m.update(ents(rd1, wr1), rd1, wr1, status)
+    assert slots[1:] == perm[1:] and m.verified == 7 and m.mismatched == 7  # none sits at its position
+    # idle afterwards: the pairing holds
+    assert m.update(ents(rd1, wr1), rd1, wr1, status)[1:] == perm[1:]
