@@ -105,6 +105,11 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
   // a tenant that started since the last tick is read from then on, not from the next tick (a
   // 10 %-resident arrival otherwise had one read in its first interval).
   bool scan_ok = occ_on;
+  // Every 4th sub-sample lists the directory (new tenants show up within 4 periods, 0.2 s at 1 Hz);
+  // the others re-read the known pids only: a node-wide KFD listing per GPU per sub-sample would
+  // cost P opens each time on a node with P GPU processes.
+  constexpr int kScanEvery = 4;
+  uint64_t n_sub = 0;
   int64_t next_occ = 0;
   // The process list (KFD + fdinfo reads, ~0.1 ms) runs on a second thread while this one reads
   // the firmware table (~0.2 ms, mostly the SMU fetch): the device's part of a tick becomes the
@@ -183,8 +188,9 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       if (w->quit) return;
       if (subsample) {
         lk.unlock();
-        if (scan_ok) scan_ok = backend->occupancy_scan(i, &scan);
-        if (scan_ok) {
+        const bool scan_turn = scan_ok && (n_sub++ % kScanEvery == 0);
+        if (scan_turn) scan_ok = backend->occupancy_scan(i, &scan);
+        if (scan_turn && scan_ok) {
           vals.assign(occ_pids.size(), kNaN);
           for (const OccRead& r : scan) {
             size_t k = std::find(occ_pids.begin(), occ_pids.end(), r.pid) - occ_pids.begin();
