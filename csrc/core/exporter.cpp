@@ -804,7 +804,10 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       if ((waves || arrived || (!observable && holds)) && std::find(active.begin(), active.end(), p.pid) == active.end())
         active.push_back(p.pid);
     }
-    present.swap(listed);
+    // A tick whose device sample failed has no process list: it must not make every process look
+    // like a new arrival on the next good tick, so the last list is kept.
+    const bool listed_ok = d >= samples.size() || samples[d].ok;
+    if (listed_ok) present.swap(listed);
     for (uint32_t pid : active) seen[pid] = {tick_no, now_ns};
     for (auto it = seen.begin(); it != seen.end();) {  // forget pids past both windows
       if (tick_no - it->second.first >= 5 && now_ns - it->second.second >= window_ns) it = seen.erase(it);

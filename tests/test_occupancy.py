@@ -232,3 +232,23 @@ def test_sharing_from_allocations_without_process_list(mock_exporter):
     fam = promtext.parse(ex.metrics_text())
     assert promtext.one(fam, "gpu_active_processes", gpu_id="0", source="allocations") == 2
     assert promtext.one(fam, "gpu_active_processes", gpu_id="1", source="allocations") == 0
+
+
+def test_a_failed_tick_does_not_turn_every_process_into_an_arrival(mock_exporter):
+    """A device whose sample fails for a tick lists no processes; the next good tick must not see
+    the same processes as new arrivals (which would make an exclusive GPU look shared for 5 s)."""
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0, mfma_exclusive_window_s=0.0,
+                       mock={"procs": [{"pid": 7, "device": 0, "name": "train", "kfd_only": True},
+                                       {"pid": 8, "device": 0, "name": "idle-holder", "kfd_only": True}]})
+    ex.set_device_mfma_util({0: 42.5})
+    ex.mock_set_occ_series(0, [200.0, 0.0])
+    for _ in range(6):  # past pid 8's arrival window
+        ex.tick()
+    assert promtext.one(promtext.parse(ex.metrics_text()), "pod_gpu_mfma_util_percent", pid="7") == 42.5
+    ex.mock_set_fail(0, -1)  # every call fails
+    ex.tick()
+    ex.mock_set_fail(0, 0)
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_active_processes", gpu_id="0") == 1
+    assert promtext.one(fam, "pod_gpu_mfma_util_percent", pid="7") == 42.5
