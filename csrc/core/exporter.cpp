@@ -284,7 +284,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       ps.occ_samples = n;
       ps.occ_busy = busy;
     }
-    if (occ_on && procs) {
+    if (occ_on && procs && ok_for_ras) {  // a failed tick listed nothing: keep sub-sampling the known pids
       occ_pids.clear();
       for (const auto& ps : p)
         if (has(ps.cu_occupancy) && std::find(occ_pids.begin(), occ_pids.end(), ps.pid) == occ_pids.end())
