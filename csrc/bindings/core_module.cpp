@@ -14,6 +14,7 @@
 #include "../core/grpc_lite.h"
 #include "../core/hpack.h"
 #include "../core/http_client.h"
+#include "../core/kubelet_files.h"
 #include "../core/ondevice.h"
 #include "../core/options.h"
 #include "../core/render.h"
@@ -474,6 +475,34 @@ PYBIND11_MODULE(_core, m) {
         return docker_rows(cs);
       },
       py::arg("json"), "parse a Docker Engine GET /containers/json body (docker_lite.cpp)");
+  m.def(
+      "device_checkpoint_parse",
+      [](py::bytes b) {
+        std::vector<CheckpointEntry> es;
+        std::string err;
+        if (!device_checkpoint_parse(std::string(b), &es, &err)) throw py::value_error(err);
+        py::list out;
+        for (const auto& e : es) {
+          py::dict d;
+          d["pod_uid"] = py::bytes(e.pod_uid);
+          d["container"] = py::bytes(e.container_name);
+          d["resource"] = py::bytes(e.resource);
+          py::list ids;
+          for (const auto& x : e.device_ids) ids.append(py::bytes(x));
+          d["device_ids"] = ids;
+          out.append(d);
+        }
+        return out;
+      },
+      py::arg("json"), "parse the kubelet device-plugin checkpoint (kubelet_files.cpp)");
+  m.def(
+      "container_log_name",
+      [](const std::string& name) -> py::object {
+        std::string pod, ns, ctr, id;
+        if (!parse_container_log_name(name, &pod, &ns, &ctr, &id)) return py::none();
+        return py::make_tuple(pod, ns, ctr, id);
+      },
+      py::arg("name"), "split /var/log/containers/<pod>_<ns>_<container>-<id>.log (kubelet_files.cpp)");
   m.def(
       "http1_parse_response",
       [](py::bytes raw, bool eof) {

@@ -143,3 +143,48 @@ def test_cri_metadata_wins_over_the_log_tree(core, tmp_path):
             assert by_pid["3000"]["podname"] == "jupyter-q-0"  # the log tree fills the gap
         finally:
             ex.stop()
+
+
+# ------------------------------------------------------------------ parsers (hypothesis)
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+_text = st.text(alphabet=st.characters(blacklist_categories=("Cs",)), max_size=20)
+_entry = st.fixed_dictionaries(
+    {"PodUID": _text.filter(bool), "ContainerName": _text, "ResourceName": _text,
+     "DeviceIDs": st.one_of(st.lists(_text, max_size=3), st.dictionaries(st.sampled_from(["-1", "0", "1"]),
+                                                                         st.lists(_text, max_size=3), max_size=2)),
+     "AllocResp": _text},
+    optional={"Extra": st.one_of(st.integers(), st.none(), st.lists(st.integers(), max_size=2))})
+
+
+@settings(max_examples=200, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(entries=st.lists(_entry, max_size=5), extra=st.dictionaries(st.sampled_from(["RegisteredDevices", "X"]),
+                                                                    st.integers(), max_size=2))
+def test_checkpoint_parser_matches_python_json(core, entries, extra):
+    body = json.dumps({"Data": {"PodDeviceEntries": entries, **extra}, "Checksum": 12345})
+    got = core.device_checkpoint_parse(body.encode())
+    want = []
+    for e in entries:
+        ids = e["DeviceIDs"] if isinstance(e["DeviceIDs"], list) else [x for v in e["DeviceIDs"].values() for x in v]
+        want.append({"pod_uid": e["PodUID"].encode(), "container": e["ContainerName"].encode(),
+                     "resource": e["ResourceName"].encode(), "device_ids": [x.encode() for x in ids]})
+    assert got == want
+
+
+@settings(max_examples=300, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(raw=st.binary(max_size=200))
+def test_checkpoint_parser_rejects_garbage_without_crashing(core, raw):
+    try:
+        core.device_checkpoint_parse(raw)
+    except ValueError:
+        pass
+
+
+def test_container_log_names(core):
+    cid = "0123456789abcdef" * 4
+    assert core.container_log_name(f"my-pod-7f9_team-a_my-ctr-2-{cid}.log") == ("my-pod-7f9", "team-a", "my-ctr-2", cid)
+    assert core.container_log_name(f"p.0_ns_c-{cid}.log") == ("p.0", "ns", "c", cid)
+    for bad in (f"p_ns_c-{cid}.txt", f"p_ns_c-{cid[:-1]}.log", f"p_ns_x_c-{cid}.log", f"_ns_c-{cid}.log",
+                f"p__c-{cid}.log", f"p_ns_-{cid}.log", "p_ns_c.log", f"p_ns_c-{cid.upper()}.log"):
+        assert core.container_log_name(bad) is None, bad
