@@ -571,7 +571,7 @@ bool AmdSmiBackend::processes(int i, std::vector<ProcSample>* out) {
   out->clear();
   if (SysfsGpu* g = i < static_cast<int>(fast_.size()) ? fast_[i].get() : nullptr; g && g->have_kfd()) {
     const int64_t ts = mono_ns();
-    const bool ok = g->processes(out);
+    const bool ok = g->processes(out, tick_occupancy_.load(std::memory_order_relaxed));
     record_call(kCallProcs, mono_ns() - ts, ok);
     if (ok) return true;
   }

@@ -52,6 +52,9 @@ class Backend {
   // the last tick instead).
   virtual bool occupancy_scan(int, std::vector<OccRead>*) { return false; }
   virtual void sample_ras(int, DeviceSample*, int /*slice*/ = 0, int /*nslices*/ = 1) {}
+  // The device workers sub-sample cu_occupancy between ticks (occupancy_scan / occupancy): the
+  // process list at the tick may then skip its own occupancy read (cu_occupancy left NaN).
+  virtual void set_tick_occupancy(bool /*on*/) {}
   // May processes(i) run on another thread while sample(i) runs (the device worker then overlaps
   // the process list with the firmware-table read)? Only where both read independent files.
   virtual bool concurrent_processes(int /*i*/) const { return false; }
@@ -217,6 +220,7 @@ class AmdSmiBackend : public Backend {
   bool supports_occupancy(int i) const override;  // with the sysfs fast path (KFD files)
   // sysfs fast path: the table pread and the KFD / fdinfo reads share no state
   bool concurrent_processes(int i) const override { return supports_occupancy(i); }
+  void set_tick_occupancy(bool on) override { tick_occupancy_ = on; }
   void maintain(int i) override;                   // fast path: due /proc fd-table refreshes
   void occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) override;
   bool occupancy_scan(int i, std::vector<OccRead>* out) override;
@@ -240,6 +244,7 @@ class AmdSmiBackend : public Backend {
   bool validate_fast(int i, std::string* why);
   int replicate_ = 1;
   bool fast_path_ = true;
+  std::atomic<bool> tick_occupancy_{true};
   std::string sys_root_ = "/sys", proc_root_ = "/proc", fast_status_;
   std::vector<std::unique_ptr<SysfsGpu>> fast_;
   std::vector<uint64_t> kfd_ids_;

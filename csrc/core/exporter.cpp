@@ -268,11 +268,12 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
     }
     const bool ok_for_ras = s.ok;
     const int64_t dev_ns = mono_ns() - t_dev0;
-    // fold the interval's sub-samples into this tick's instantaneous reading
+    // fold the interval's sub-samples into this tick's reading (with sub-sampling on, the tick's
+    // process list skips its own cu_occupancy read: Exporter::start_workers, set_tick_occupancy)
     for (auto& ps : p) {
-      if (!has(ps.cu_occupancy)) continue;
-      double sum = ps.cu_occupancy;
-      int n = 1, busy = ps.cu_occupancy > 0 ? 1 : 0;
+      if (!has(ps.cu_occupancy) && !occ_on) continue;
+      double sum = has(ps.cu_occupancy) ? ps.cu_occupancy : 0.0;
+      int n = has(ps.cu_occupancy) ? 1 : 0, busy = ps.cu_occupancy > 0 ? 1 : 0;
       for (size_t k = 0; k < occ_pids.size(); ++k)
         if (occ_pids[k] == ps.pid) {
           sum += occ_sum[k];
@@ -280,15 +281,14 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
           busy += occ_busy[k];
           break;
         }
-      ps.cu_occupancy = sum / n;
+      ps.cu_occupancy = n > 0 ? sum / n : kNaN;
       ps.occ_samples = n;
       ps.occ_busy = busy;
     }
     if (occ_on && procs && ok_for_ras) {  // a failed tick listed nothing: keep sub-sampling the known pids
       occ_pids.clear();
       for (const auto& ps : p)
-        if (has(ps.cu_occupancy) && std::find(occ_pids.begin(), occ_pids.end(), ps.pid) == occ_pids.end())
-          occ_pids.push_back(ps.pid);
+        if (std::find(occ_pids.begin(), occ_pids.end(), ps.pid) == occ_pids.end()) occ_pids.push_back(ps.pid);
       occ_sum.assign(occ_pids.size(), 0.0);
       occ_n.assign(occ_pids.size(), 0);
       occ_busy.assign(occ_pids.size(), 0);
@@ -334,6 +334,9 @@ void Exporter::start_workers(int n) {
     const int64_t occ_ns = cfg_.interval_s > 0 && cfg_.occ_samples > 1 && cfg_.processes
                                ? std::max<int64_t>(20'000'000, static_cast<int64_t>(cfg_.interval_s * 1e9 / cfg_.occ_samples))
                                : 0;
+    // the workers' sub-samples stand in for the tick's own cu_occupancy read (the costliest
+    // per-process file: ~27 us, a KFD walk over the process's queues)
+    if (i == 0) backend_->set_tick_occupancy(occ_ns == 0 || !backend_->supports_occupancy(i));
     w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i, occ_ns, occ_reads_, cfg_.rt_priority,
                         rt_threads_);
     workers_.push_back(std::move(w));
@@ -791,8 +794,11 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
     }
     auto& seen = last_active_[d];
     auto& present = present_[d];
+    // residency is observable where occupancy can be read (also on a tick where no read has landed
+    // yet for anyone: the first tick after start, a process that just arrived)
     const bool observable = std::any_of(procs[d].begin(), procs[d].end(),
-                                        [](const ProcSample& p) { return p.occ_samples > 0; });
+                                        [](const ProcSample& p) { return p.occ_samples > 0; }) ||
+                            (backend_ && backend_->supports_occupancy(static_cast<int>(d)));
     std::vector<uint32_t> active;  // distinct pids (one process may hold several KFD contexts)
     std::unordered_set<uint32_t> listed;
     for (const auto& p : procs[d]) {

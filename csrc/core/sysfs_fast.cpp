@@ -307,7 +307,7 @@ void SysfsGpu::occupancy(const std::vector<uint32_t>& pids, std::vector<double>*
   }
 }
 
-bool SysfsGpu::processes(std::vector<ProcSample>* out) {
+bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
   out->clear();
   if (!kfd_gpu_id_) return false;
   const std::string kdir = sys_root_ + "/class/kfd/kfd/proc";
@@ -328,7 +328,8 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out) {
     p.pid = pid;
     p.mem_bytes = static_cast<double>(strtoull(b, nullptr, 10));
     p.vram_bytes = p.mem_bytes;
-    if (read_small(pdir + occ_name, b, sizeof b, &n)) p.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
+    if (read_occupancy && read_small(pdir + occ_name, b, sizeof b, &n))
+      p.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
     fdinfo_usage(pid, &p);
     out->push_back(std::move(p));
   }

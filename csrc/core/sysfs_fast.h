@@ -194,7 +194,9 @@ class SysfsGpu {
   bool read_vram(double* used_bytes, double* total_bytes);
   bool read_gtt(double* used_bytes);
   // Compute processes with memory on this GPU (KFD), plus DRM fdinfo gfx engine time / memory.
-  bool processes(std::vector<ProcSample>* out);
+  // read_occupancy false: leave cu_occupancy NaN (the device worker sub-samples it between ticks,
+  // and the KFD read is the costliest per-process file: it walks the process's queues).
+  bool processes(std::vector<ProcSample>* out, bool read_occupancy = true);
   // Instantaneous KFD cu_occupancy of each pid on this GPU (NaN where the file is unreadable).
   void occupancy(const std::vector<uint32_t>& pids, std::vector<double>* out);
   // Every KFD process on this GPU with its cu_occupancy and VRAM (no fdinfo): the between-ticks
