@@ -591,7 +591,7 @@ PYBIND11_MODULE(_core, m) {
         }
         return match_device_id(id, st);
       },
-      "C++ twin of gpumon.attribution.plane.match_device_id (the native PodResources poller's matcher)");
+      "C++ twin of tests/oracles/attribution/plane.py match_device_id (the native PodResources poller's matcher)");
   m.def(
       "docker_parse_inspect",
       [](py::bytes b) {
@@ -1045,5 +1045,5 @@ PYBIND11_MODULE(_core, m) {
         return out;
       },
       py::arg("raw"), py::arg("agent"), py::arg("window_s") = 0.0,
-      "C++ twin of gpumon.ops.pmc.derive (used by the native samplers)");
+      "C++ twin of tests/oracles/ops/pmc.py derive (used by the native samplers)");
 }

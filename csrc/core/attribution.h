@@ -12,7 +12,7 @@
 //                     name without '-' yields "-" instead of crashing (Q2); a regex or a pod label
 //                     may override.
 // Container/pod metadata (the docker-inspect equivalent) is pushed in by the control plane
-// (gpumon/attribution: CRI ListContainers / ListPodSandbox, kubelet PodResources). When no table
+// (tests/oracles/attribution, the Python oracle: CRI ListContainers / ListPodSandbox, kubelet PodResources). When no table
 // entry exists, an optional procfs fallback reads HOSTNAME and the service-account namespace of
 // the process itself.
 #pragma once

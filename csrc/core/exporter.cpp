@@ -1435,7 +1435,7 @@ std::string lower(std::string s) {
 }  // namespace
 
 // Device-plugin device ID -> exporter device index (-1 unknown). The AMD device plugin uses PCI
-// addresses; UUIDs, hip ids and DRM node names are accepted too (gpumon/attribution/plane.py).
+// addresses; UUIDs, hip ids and DRM node names are accepted too (tests/oracles/attribution/plane.py).
 int match_device_id(const std::string& raw, const std::vector<DeviceStatic>& st) {
   std::string d = lower(std::string(trim(raw)));
   // DRA forms: CDI name "amd.com/gpu=gpu-0" (part after '='), "gpu-N" (hip id), dashed PCI address
@@ -1548,7 +1548,7 @@ void Exporter::podres_loop() {
   }
 }
 
-// CRI containers + sandboxes -> ContainerMeta (same merge as gpumon/attribution/plane.py: pod
+// CRI containers + sandboxes -> ContainerMeta (same merge as tests/oracles/attribution/plane.py: pod
 // annotations < pod labels < container annotations < container labels).
 bool Exporter::cri_poll_once() {
   std::vector<CriContainer> cs;

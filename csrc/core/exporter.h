@@ -85,7 +85,7 @@ struct ExporterConfig {
   int reinit_after = 5;               // consecutive all-devices-failed ticks before re-initialising
   double device_timeout_s = 2.0;      // a device call still running after this is exported as hung
   // Native kubelet PodResources poller (grpc_lite.cpp) for the standalone binary; the Python
-  // control plane (gpumon/attribution) leaves this empty and pushes allocations itself.
+  // control plane oracle (tests/oracles/attribution) leaves this empty and pushes allocations itself.
   std::string pod_resources_socket;
   std::string pod_resources_prefix = "amd.com/gpu";
   std::vector<std::string> pod_resources_dra_drivers = {"gpu.amd.com"};  // DRA claim devices counted too

@@ -496,7 +496,7 @@ std::string default_plugin_dir() {
 }
 
 // ---------------------------------------------------------------------------------------------
-// derivation (mirrors gpumon/ops/pmc.py derive())
+// derivation (mirrors tests/oracles/ops/pmc.py derive())
 
 PmcDerived pmc_derive(const std::map<std::string, PmcReduced>& raw, const PmcAgentInfo& agent, double window_s) {
   PmcDerived d;

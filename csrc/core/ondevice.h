@@ -17,8 +17,8 @@
 // before any probe op: rocprofiler must register before HSA comes up), and the helper's CPU and
 // RSS are exported because they are part of the pod's footprint (profiles/r2_footprint.md).
 //
-// Series and formulas match gpumon/ops/pmc.py and gpumon/ops/probe.py (the Python test oracles,
-// `gpumon serve --ondevice python`), so dashboards see the same families from either path. The PMC
+// Series and formulas match tests/oracles/ops/pmc.py and tests/oracles/ops/probe.py (the Python test oracles
+// under tests/oracles, not shipped), so dashboards see the same families from either path. The PMC
 // sampler also publishes each GPU's MFMA utilisation to the exporter for pod_gpu_mfma_util_percent.
 #pragma once
 
@@ -42,7 +42,7 @@ struct OnDeviceConfig {
   std::string plugin_dir;   // "" = $GPUMON_PLUGIN_DIR or <dir of this object>/../lib
   bool pmc = false;
   // MFMA busy + MFMA MOPS per operand type + GRBM: 8 SQ + 2 GRBM = one gfx950 counting pass. No
-  // per-wave SQ counters: they count only the profiling process's waves (gpumon/ops/pmc.py).
+  // per-wave SQ counters: they count only the profiling process's waves (tests/oracles/ops/pmc.py).
   std::vector<std::string> pmc_counters = {
       "SQ_VALU_MFMA_BUSY_CYCLES",    "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_INSTS_VALU_MFMA_MOPS_F16",
       "SQ_INSTS_VALU_MFMA_MOPS_F8",  "SQ_INSTS_VALU_MFMA_MOPS_F6F4", "SQ_INSTS_VALU_MFMA_MOPS_F32",
@@ -92,7 +92,7 @@ struct PmcDerived {
   std::vector<std::pair<std::string, double>> mfma_tflops;  // (dtype lower-case, TFLOP/s), by name
 };
 
-// Pure (CPU-tested against gpumon.ops.pmc.derive): the gfx9xx formulas ROCm 7.2 falls back to on gfx950.
+// Pure (CPU-tested against tests/oracles/ops/pmc.py derive): the gfx9xx formulas ROCm 7.2 falls back to on gfx950.
 // window_s > 0 adds the MFMA TFLOP/s per operand type (512 FLOP per SQ_INSTS_VALU_MFMA_MOPS_* unit).
 PmcDerived pmc_derive(const std::map<std::string, PmcReduced>& raw, const PmcAgentInfo& agent, double window_s = 0);
 

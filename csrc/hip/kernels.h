@@ -8,7 +8,7 @@
 //               hipDeviceSynchronize (no host-side stall, no interference with the workload's
 //               streams). SQ/GRBM perf counters are not readable from shader code on CDNA4 (they
 //               are privileged MMIO programmed by the driver); MFMA-busy / occupancy come from
-//               rocprofiler-sdk device counting (gpumon/ops/pmc.py), the probe supplies the
+//               rocprofiler-sdk device counting (tests/oracles/ops/pmc.py), the probe supplies the
 //               per-XCD liveness, clock and dispatch-latency signals.
 //   K2 load   — synthetic loads that validate the exporter under known conditions:
 //               bf16 MFMA burn (v_mfma_f32_32x32x16_bf16, 4 independent accumulators per wave,
