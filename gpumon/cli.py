@@ -89,10 +89,14 @@ def _fmt(v, w, p=0):
     return f"{v:{w}.{p}f}"
 
 
-def render_top(statics, samples, rates, rows) -> str:
-    """Console table (the reference's unused displayfmt columns, gpu.py:156-168, plus MI355X fields)."""
+def render_top(statics, samples, rates, rows, active=None) -> str:
+    """Console table (the reference's unused displayfmt columns, gpu.py:156-168, plus MI355X fields).
+    `active`: gpu_id -> gpu_active_processes (the sharing state)."""
+    from .export.fleet import sharing_label
+
     lines = []
-    hdr = f"{'GPU':>3} {'UTIL%':>6} {'XCD busy% (0-7)':<32} {'VRAM MiB':>17} {'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8}"
+    hdr = (f"{'GPU':>3} {'UTIL%':>6} {'XCD busy% (0-7)':<32} {'VRAM MiB':>17} {'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8}"
+           f" {'SHARING':>10}")
     lines.append(hdr)
     for st, sm, rt in zip(statics, samples, rates):
         f = sm["fields"]
@@ -100,7 +104,8 @@ def render_top(statics, samples, rates, rows) -> str:
         used = (f["vram_used"] or 0) / 1048576
         tot = (f["vram_total"] or 0) / 1048576
         lines.append(f"{st['gpu_id']:>3} {_fmt(f['gfx_util'], 6)} {xcd:<32} {used:8.0f}/{tot:8.0f} "
-                     f"{_fmt(f['power_cur'], 6)} {_fmt(f['temp_hotspot'], 6)} {_fmt(f['gfxclk_cur'], 8)}")
+                     f"{_fmt(f['power_cur'], 6)} {_fmt(f['temp_hotspot'], 6)} {_fmt(f['gfxclk_cur'], 8)}"
+                     f" {sharing_label((active or {}).get(str(st['gpu_id']))):>10}")
     lines.append("")
     # BUSY%: share of the interval with the process's waves resident (KFD; the reference copied the
     # device's utilisation onto every process, gpu.py:205); CUs: mean CU-equivalents its waves held
@@ -124,7 +129,11 @@ def cmd_top(args) -> int:
         n = 0
         while args.iterations <= 0 or n < args.iterations:
             mon.wait_ticks(1, timeout_s=cfg.interval * 5 + 5)
-            text = render_top(mon.ex.statics(), mon.ex.samples(), mon.ex.rates(), mon.ex.pod_rows())
+            from .export import promtext
+
+            fam = promtext.parse(mon.metrics())
+            active = {l["gpu_id"]: v for _, l, v in fam.get("gpu_active_processes", {}).get("samples", [])}
+            text = render_top(mon.ex.statics(), mon.ex.samples(), mon.ex.rates(), mon.ex.pod_rows(), active)
             if sys.stdout.isatty():
                 sys.stdout.write("\x1b[2J\x1b[H")
             sys.stdout.write(text + "\n")

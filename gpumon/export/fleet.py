@@ -71,10 +71,17 @@ def _f(v: Optional[float], w: int, p: int = 0) -> str:
     return "-".rjust(w) if v is None else f"{v:{w}.{p}f}"
 
 
+def sharing_label(n: Optional[float]) -> str:
+    """The sharing state from `gpu_active_processes` (idle / one process / shared by N)."""
+    if n is None:
+        return "-"
+    return "idle" if n < 1 else ("exclusive" if n < 2 else f"shared:{int(n)}")
+
+
 def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
     """Text tables for parsed expositions (one per node)."""
     lines = [f"{'HOST':<20}{'GPU':>4} {'UP':>2} {'UTIL%':>6} {'XCD busy% (0-7)':<32} {'VRAM GiB':>13} "
-             f"{'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8} {'MFMA%':>6} {'ECC-UE':>7} {'PROCS':>5}"]
+             f"{'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8} {'MFMA%':>6} {'ECC-UE':>7} {'SHARING':>10}"]
     pods = []
     for fam in frames:
         for r in gpu_rows(fam):
@@ -82,7 +89,7 @@ def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
             vram = "-" if r["vram_used"] is None else f"{r['vram_used'] / 2**30:.1f}/{(r['vram_total'] or 0) / 2**30:.0f}"
             lines.append(f"{r['host'][:19]:<20}{r['gpu_id']:>4} {_f(r['up'], 2)} {_f(r['util'], 6)} {xcd:<32} "
                          f"{vram:>13} {_f(r['power'], 6)} {_f(r['hot'], 6)} {_f(r['gfx_mhz'], 8)} "
-                         f"{_f(r['mfma'], 6, 1)} {_f(r['ecc_ue'], 7)} {_f(r['procs'], 5)}")
+                         f"{_f(r['mfma'], 6, 1)} {_f(r['ecc_ue'], 7)} {sharing_label(r['procs']):>10}")
         pods.extend(pod_rows(fam))
     for url, err in (errors or {}).items():
         lines.append(f"{url}: {err}")

@@ -40,11 +40,13 @@ def test_cli_top_over_two_exporters(mock_exporter, capsys):
     gpu_lines = [l for l in out.splitlines() if l.startswith("node-")]
     assert sum(l.startswith("node-a") for l in gpu_lines) >= 2 + 2  # 2 GPUs + pod rows
     assert "node-b-job-0" in out and "ECC-UE" in out
-    # PROCS (gpu_active_processes): node-a's GPU 1 runs this process in the mock -> 1 (exclusive)
+    # SHARING (gpu_active_processes): node-a's GPU 1 runs this process in the mock -> exclusive
     hdr = next(l for l in out.splitlines() if l.startswith("HOST"))
-    assert hdr.rstrip().endswith("PROCS")
+    assert hdr.rstrip().endswith("SHARING")
     a1 = next(l for l in gpu_lines if l.split()[:2] == ["node-a", "1"])
-    assert a1.split()[-1] == "1", a1
+    assert a1.split()[-1] == "exclusive", a1
+    assert fleet.sharing_label(None) == "-" and fleet.sharing_label(0) == "idle"
+    assert fleet.sharing_label(3.0) == "shared:3"
     assert sum(1 for l in out.splitlines() if l.startswith("node-b") and "/288 " in l) == 3  # GPU rows
 
 
