@@ -151,6 +151,9 @@ bool HttpClient::connect_to(const Url& u, std::string* err) {
   return true;
 }
 
+// Largest Content-Length accepted: the client sizes its buffer from it before reading.
+constexpr long kMaxBodyBytes = 256L << 20;
+
 static bool send_all(int fd, const char* p, size_t n) {
   while (n) {
     ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
@@ -212,15 +215,23 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
       pos = e + 2;
     }
     std::string rb = in.substr(hdr_end + 4);
+    if (clen > kMaxBodyBytes) {
+      close_conn();
+      *err = "response body of " + std::to_string(clen) + " bytes refused";
+      return -1;
+    }
     if (clen >= 0) {
-      while (static_cast<long>(rb.size()) < clen) {
-        ssize_t r = recv(fd_, buf, sizeof buf, 0);
+      // the body lands in place: one buffer of the announced length, no 16 KB staging copies
+      size_t got = std::min(rb.size(), static_cast<size_t>(clen));
+      rb.resize(static_cast<size_t>(clen));
+      while (got < static_cast<size_t>(clen)) {
+        ssize_t r = recv(fd_, &rb[got], static_cast<size_t>(clen) - got, 0);
         if (r <= 0) {
           close_conn();
           *err = "short body";
           return -1;
         }
-        rb.append(buf, static_cast<size_t>(r));
+        got += static_cast<size_t>(r);
       }
     } else if (status != 204 && status != 304) {
       // no length: read to EOF

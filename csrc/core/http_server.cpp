@@ -24,6 +24,7 @@ namespace {
 constexpr size_t kMaxHeader = 16 * 1024;
 constexpr int64_t kIdleTimeoutNs = 60LL * 1000000000LL;
 constexpr size_t kMaxConnsPerLoop = 4096;
+constexpr int kSndBuf = 1 << 20;
 
 const char* status_text(int s) {
   switch (s) {
@@ -269,6 +270,7 @@ void HttpServer::run(Loop* L) {
       long used = parse_request(c.in, &req);
       if (used == 0) return true;
       HttpResponse resp;
+      const int64_t t_req = mono_ns();  // service time = handler + response write
       if (used < 0) {
         resp.status = used == -2 ? 431 : 400;
         resp.inline_body = status_text(resp.status);
@@ -282,7 +284,7 @@ void HttpServer::run(Loop* L) {
         handler_(req, &resp);
       }
       requests_.fetch_add(1, std::memory_order_relaxed);
-      c.req_ns = mono_ns();
+      c.req_ns = t_req;
       c.path = req.path;
       c.in.erase(0, static_cast<size_t>(used));
       const char* body = resp.data;
@@ -335,6 +337,11 @@ void HttpServer::run(Loop* L) {
           }
           int one = 1;
           setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+          // room for a whole exposition in the socket: a node's identity body is 100-200 KB
+          // (8 GPUs), over the default initial send buffer, and every EAGAIN costs the
+          // response an epoll round trip through the client's reads
+          int sndbuf = kSndBuf;
+          setsockopt(cfd, SOL_SOCKET, SO_SNDBUF, &sndbuf, sizeof sndbuf);
           Conn c;
           c.fd = cfd;
           c.last_ns = now;

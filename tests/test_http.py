@@ -171,3 +171,36 @@ def test_port_conflict_reports_error(core):
             assert "bind" in str(e)
     finally:
         a.stop()
+
+
+def test_client_refuses_huge_content_length_and_reads_bodies_whole(core):
+    """The native client sizes its buffer from Content-Length (csrc/core/http_client.cpp): an
+    announced body over 256 MiB is refused before any allocation; a short body is an error."""
+    import socket
+    import threading
+
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(4)
+    port = srv.getsockname()[1]
+    answers = [b"HTTP/1.1 200 OK\r\nContent-Length: 1000000000000\r\n\r\nabc",
+               b"HTTP/1.1 200 OK\r\nContent-Length: 10\r\nConnection: close\r\n\r\nabc",
+               b"HTTP/1.1 200 OK\r\nContent-Length: 300000\r\nConnection: close\r\n\r\n" + b"x" * 300000]
+
+    def serve():
+        for a in answers:
+            c, _ = srv.accept()
+            c.recv(4096)
+            c.sendall(a)
+            c.close()
+
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    st, body, err = core.http_request("GET", f"http://127.0.0.1:{port}/", "", "", 5.0)
+    assert st != 200 and "refused" in err
+    st, body, err = core.http_request("GET", f"http://127.0.0.1:{port}/", "", "", 5.0)
+    assert st != 200 and "short body" in err
+    st, body, err = core.http_request("GET", f"http://127.0.0.1:{port}/", "", "", 5.0)
+    assert st == 200 and body == b"x" * 300000
+    t.join(5)
+    srv.close()
