@@ -173,6 +173,9 @@ def main() -> int:
     ap.add_argument("--no-fast-path", action="store_true", help="read every value through libamd_smi")
     ap.add_argument("--rt-priority", type=int, default=1,
                     help="the DaemonSet's rt_priority (SCHED_FIFO sampler; stays normal without CAP_SYS_NICE)")
+    ap.add_argument("--dist", action="store_true",
+                    help="initialise torch.distributed (RCCL) even with one rank: rehearses the torchrun path "
+                         "(process group, barriers, MAX over ranks) on a 1-GPU box")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -197,9 +200,11 @@ def main() -> int:
 
         has_gpu = _hip_rt().device_count() > 0
     dist = None
-    if world > 1:
+    if world > 1 or (args.dist and torch is not None):
         import torch.distributed as dist
 
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29517"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)  # --dist without a launcher
         if has_gpu:
             torch.cuda.set_device(local_rank)
         dist.init_process_group(backend="nccl" if has_gpu else "gloo")
