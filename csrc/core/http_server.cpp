@@ -10,7 +10,9 @@
 #include <sys/uio.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
+#include <cstdlib>
 #include <cstring>
 #include <strings.h>
 #include <unordered_map>
@@ -24,7 +26,7 @@ namespace {
 constexpr size_t kMaxHeader = 16 * 1024;
 constexpr int64_t kIdleTimeoutNs = 60LL * 1000000000LL;
 constexpr size_t kMaxConnsPerLoop = 4096;
-constexpr int kSndBuf = 1 << 20;
+constexpr int kSndBuf = 1 << 20;  // GPUMON_HTTP_SNDBUF overrides (bytes; 0 = the kernel's autotuning)
 
 const char* status_text(int s) {
   switch (s) {
@@ -133,6 +135,8 @@ HttpServer::~HttpServer() { stop(); }
 
 bool HttpServer::start(std::string* err) {
   if (running_) return true;
+  sndbuf_ = kSndBuf;
+  if (const char* e = getenv("GPUMON_HTTP_SNDBUF")) sndbuf_ = std::max(0, atoi(e));
   for (int t = 0; t < nthreads_; ++t) {
     auto L = std::make_unique<Loop>();
     L->lfd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
@@ -340,8 +344,7 @@ void HttpServer::run(Loop* L) {
           // room for a whole exposition in the socket: a node's identity body is 100-200 KB
           // (8 GPUs), over the default initial send buffer, and every EAGAIN costs the
           // response an epoll round trip through the client's reads
-          int sndbuf = kSndBuf;
-          setsockopt(cfd, SOL_SOCKET, SO_SNDBUF, &sndbuf, sizeof sndbuf);
+          if (sndbuf_ > 0) setsockopt(cfd, SOL_SOCKET, SO_SNDBUF, &sndbuf_, sizeof sndbuf_);
           Conn c;
           c.fd = cfd;
           c.last_ns = now;

@@ -52,6 +52,7 @@ class HttpServer {
   std::string addr_;
   int port_;
   int nthreads_;
+  int sndbuf_ = 0;  // SO_SNDBUF for accepted connections (0: kernel default)
   Handler handler_;
   Observer observer_;
   std::vector<std::unique_ptr<Loop>> loops_;

@@ -72,7 +72,9 @@ def _f(v: Optional[float], w: int, p: int = 0) -> str:
 
 
 def sharing_label(n: Optional[float]) -> str:
-    """The sharing state from `gpu_active_processes` (idle / one process / shared by N)."""
+    """The sharing state from `gpu_active_processes` (idle / one process / shared by N): the
+    reference's gauge board marked its node columns "(共享)" shared / "(独占)" exclusive
+    (/root/reference/img/grafana.png)."""
     if n is None:
         return "-"
     return "idle" if n < 1 else ("exclusive" if n < 2 else f"shared:{int(n)}")
