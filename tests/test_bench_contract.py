@@ -33,11 +33,14 @@ def _check(d, n, steps, warmup):
     assert steps <= d["ticks"] <= steps + 2
 
 
-def test_bench_single_process():
-    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+@pytest.mark.parametrize("dist", [False, True], ids=["plain", "dist"])
+def test_bench_single_process(dist):
+    """`--dist`: the torchrun code path (process group, barriers, MAX over ranks) with one rank."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(29600 + os.getpid() % 1000))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--interval", "0.1", "--idle-s", "1"], capture_output=True, text=True, timeout=240, env=env,
-                       cwd=ROOT)
+                        "--interval", "0.1", "--idle-s", "1"] + (["--dist"] if dist else []),
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
