@@ -146,6 +146,7 @@ def test_fleet_view_reads_the_native_exporter():
     assert fields[1] == "0" and fields[2] == "1"  # gpu_id 0, up
     assert len(fields[4:12]) == 8 and all(f.isdigit() for f in fields[4:12])  # 8 XCD busy columns
     assert "/288" in rows[0]
+    assert fields[-1] in ("idle", "exclusive") or fields[-1].startswith("shared:")  # SHARING column
 
 
 def test_native_exporter_reports_a_separate_tenant_process():
