@@ -389,9 +389,10 @@ bool Exporter::workers_busy() const {
 
 // ---------------------------------------------------------------------------------------------
 static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
-  // "mock" or "mock:gpus=8,mode=load,n_xcd=8,fail_device=1,fail_every=3,hang_ms=5,unsupported=a;b"
+  // "mock" or "mock:gpus=8,mode=load,n_xcd=8,fail_device=1,fail_every=3,hang_ms=5,unsupported=a;b,procs=2"
   size_t colon = spec.find(':');
   if (colon == std::string::npos) return base;
+  int procs_per_gpu = 0;
   for (const auto& kv : split(spec.substr(colon + 1), ',')) {
     size_t eq = kv.find('=');
     if (eq == std::string::npos) continue;
@@ -411,7 +412,22 @@ static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
     else if (k == "link_order") base.link_order = v;
     else if (k == "link_offset") base.link_offset = atoi(v.c_str()) != 0;
     else if (k == "unsupported") base.unsupported = split(v, ';');
+    else if (k == "procs") procs_per_gpu = std::max(0, atoi(v.c_str()));
   }
+  // procs=N: N processes on every GPU (the exporter's own pid first, so one attributes; the rest
+  // are pids that do not exist), half of them KFD-only -- sharing, occupancy sub-samples and the
+  // process-list thread from the command line (sanitizer runs)
+  for (int d = 0; d < base.gpus; ++d)
+    for (int k = 0; k < procs_per_gpu; ++k) {
+      MockProc p;
+      p.pid = k == 0 ? static_cast<uint32_t>(getpid()) : static_cast<uint32_t>(3900000 + d * 100 + k);
+      p.device = d;
+      p.name = "mock-tenant-" + std::to_string(k);
+      p.vram_bytes = static_cast<double>(1 + k) * (1ull << 30);
+      p.gfx_share = 1.0 / procs_per_gpu;
+      p.kfd_only = k % 2 == 1;
+      base.procs.push_back(p);
+    }
   return base;
 }
 

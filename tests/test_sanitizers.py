@@ -188,3 +188,36 @@ def test_sanitized_docker_poller_on_mutated_listings(target, binary, env):
     assert not bad, err[-4000:]
     assert rc == 0, err[-2000:]
     assert len(served) >= 4, served
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_sharing_subsamples_and_link_map(target, binary, env, tmp_path):
+    """The round-3 threads and state: three processes per GPU (sharing state, arrivals), the device
+    workers' between-tick KFD scans racing the per-device process-list threads, the xGMI slot map
+    refreshed every tick over a rotated entry order, and the kubelet-files poller (log tree and a
+    device-plugin checkpoint) -- under ASan/UBSan and TSan while scrapes run."""
+    import json
+
+    from conftest import make_locked
+
+    make_locked(target, jobs=8)
+    logs = tmp_path / "log"
+    (logs / "pods" / "ns_p-0_uid-1" / "c").mkdir(parents=True)
+    (logs / "containers").mkdir()
+    os.symlink("/var/log/pods/ns_p-0_uid-1/c/0.log", logs / "containers" / f"p-0_ns_c-{'a' * 64}.log")
+    ckpt = tmp_path / "ckpt"
+    ckpt.write_text(json.dumps({"Data": {"PodDeviceEntries": [
+        {"PodUID": "uid-1", "ContainerName": "c", "ResourceName": "amd.com/gpu", "DeviceIDs": {"0": ["x"]},
+         "AllocResp": ""}]}, "Checksum": 1}))
+    rc, err = _run(os.path.join(ROOT, binary), dict(env, GPUMON_LINK_EVERY="1", GPUMON_OCC_SAMPLES="20"),
+                   ("--backend", "mock:gpus=4,procs=3,link_order=rotate", "--interval", "0.1",
+                    "--pod-logs", str(logs), "--device-checkpoint", str(ckpt)), min_s=3.0)
+    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
+           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    assert not bad, err[-4000:]
+    assert rc == 0, err[-2000:]
