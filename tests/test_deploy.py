@@ -8,6 +8,7 @@ import json
 import os
 import re
 
+import pytest
 import yaml
 
 from gpumon.export import promtext
@@ -381,7 +382,7 @@ def test_overlay_configs_are_valid_for_the_native_binary(tmp_path):
     from conftest import make_locked
 
     make_locked("core")
-    for overlay in ("ondevice", "docker", "nonroot"):
+    for overlay in ("ondevice", "docker", "nonroot", "stress"):
         (k,) = _docs(f"deploy/k8s/overlays/{overlay}/kustomization.yaml")
         value = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "ConfigMap")["patch"])[0]["value"]
         f = tmp_path / f"{overlay}.yaml"
@@ -390,3 +391,30 @@ def test_overlay_configs_are_valid_for_the_native_binary(tmp_path):
                            capture_output=True, text=True, timeout=30)
         assert r.returncode == 0, (overlay, r.stderr[-1000:])
         assert "unknown" not in r.stderr.lower(), (overlay, r.stderr[-1000:])
+
+
+def test_stress_overlay_is_10hz_end_to_end():
+    """BASELINE.json's stress config (10 Hz sampling, Prometheus scraping at 10 Hz): the overlay
+    sets both, and its CPU request covers the measured 8-device 10 Hz cost (87 millicores at 200
+    scrapes/s, profiles/r3_churn.md)."""
+    from gpumon.config import Config
+
+    (k,) = _docs("deploy/k8s/overlays/stress/kustomization.yaml")
+    assert k["resources"] == ["../../"]
+    cfg_patch = next(p for p in k["patches"] if p["target"]["kind"] == "ConfigMap")
+    c = Config().apply_dict(yaml.safe_load(yaml.safe_load(cfg_patch["patch"])[0]["value"])["gpumon"])
+    assert c.interval == pytest.approx(0.1)
+    base = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "ConfigMap")
+    b = Config().apply_dict(yaml.safe_load(base["data"]["config.yaml"])["gpumon"])
+    for key in ("pod_resources_socket", "cri_socket", "pod_log_root", "rt_priority", "control_plane",
+                "enable_pmc", "enable_probe"):
+        assert getattr(c, key) == getattr(b, key), key  # only the rate differs from the base
+    sm = _docs("deploy/k8s/gpumon-servicemonitor.yaml")[0]
+    ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "ServiceMonitor")["patch"])
+    ep = _json_patch(sm, ops)["spec"]["endpoints"][0]
+    assert ep["interval"] == "100ms" and ep["scrapeTimeout"] == "90ms"
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"])
+    ctr = _json_patch(ds, ops)["spec"]["template"]["spec"]["containers"][0]
+    assert int(ctr["resources"]["requests"]["cpu"].rstrip("m")) >= 87
+    assert not ctr["securityContext"].get("privileged")
