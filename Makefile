@@ -30,7 +30,7 @@ HIP_SRC   := $(wildcard csrc/hip/*.hip)
 HIP_HDR   := $(wildcard csrc/hip/*.h)
 
 .PHONY: all core hip pmc plugins clean asan tsan fakes nodev
-all: core hip plugins pmc nodev
+all: core hip plugins pmc nodev snapshot
 core: $(PYEXT) $(BIN)
 hip: $(HIPEXT)
 
@@ -103,6 +103,12 @@ bin/gpumon-exporter-nodev: $(CORE_OBJ) build/obj/exporter_main.o csrc/testtools/
 	@mkdir -p bin build/obj/testtools
 	$(CXX) $(CXXFLAGS) -c csrc/testtools/nodev_interpose.cpp -o build/obj/testtools/nodev_interpose.o
 	$(CXX) -rdynamic -o $@ $(CORE_OBJ) build/obj/exporter_main.o build/obj/testtools/nodev_interpose.o $(LIBS)
+
+# Experiment tool: can a shader read the SQ's perf-snapshot registers (tools/perf_snapshot_probe.hip)?
+snapshot: bin/perf_snapshot_probe
+bin/perf_snapshot_probe: tools/perf_snapshot_probe.hip
+	@mkdir -p bin
+	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -O2 $< -o $@
 
 clean:
 	rm -rf build bin lib gpumon/_core*.so gpumon/_hip*.so gpumon/_pmc*.so

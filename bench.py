@@ -78,6 +78,16 @@ def _r(x, nd=3):
     return round(x, nd) if isinstance(x, float) and x == x else x
 
 
+def _server_durations(ex, n0, want, wait_s=1.0):
+    """The exporter's own service times of the scrapes since count n0. The server logs a scrape
+    after its response is written, so the client can hold the last response a moment before the
+    server has logged it: wait (bounded) until the server has as many as the client counted."""
+    t_end = time.monotonic() + wait_s
+    while ex.scrape_count() - n0 < want and time.monotonic() < t_end:
+        time.sleep(0.002)
+    return list(ex.scrape_durations_since(n0))
+
+
 def _exporter_cpu_s():
     """CPU seconds of the exporter's own threads in this process (named gpumon-*: sampler, device
     workers, HTTP loops, pollers); the bench's loads, scraper and torch threads are not counted."""
@@ -258,7 +268,7 @@ def main() -> int:
         q1 = mon.ex.seq
         it = [t["duration_s"] for t in mon.ex.tick_log() if q0 < t["seq"] <= q1]
         lat = r.get("latencies_s", [])
-        srv = list(mon.ex.scrape_durations_since(n0))
+        srv = _server_durations(mon.ex, n0, len(lat))
         idle = {"seconds": args.idle_s, "scrapes": len(lat), "scrape_errors": r.get("errors", 0),
                 "scrape_p50_ms": round(_pct(lat, 0.50) * 1e3, 4) if lat else None,
                 "scrape_p99_ms": round(_pct(lat, 0.99) * 1e3, 4) if lat else None,
@@ -420,7 +430,7 @@ def main() -> int:
         if scraper is not None:
             scraper.join(timeout=args.interval * 5 + 30)
         lat = scrape_result.get("latencies_s", [])
-        srv = list(mon.ex.scrape_durations_since(n_scr0))  # server-side, the same scrapes
+        srv = _server_durations(mon.ex, n_scr0, len(lat))  # server-side, the same scrapes
         samples = s1["samples"] - s0["samples"]
         ticks = seq1 - seq0
         timed = [t for t in mon.ex.tick_log() if seq0 < t["seq"] <= seq0 + ticks]

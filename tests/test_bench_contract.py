@@ -52,7 +52,9 @@ def test_bench_single_process(dist):
     # tail statistics worth quoting -- p99.9, the exporter's own service time of the
     # same requests (exact, server side), and what `value` measures
     assert d["scrape_p999_ms"] >= d["scrape_p99_ms"] > 0 and d["scrape_rate_hz"] >= 100
-    assert d["server_scrapes"] == d["scrapes"] and 0 < d["server_scrape_p99_ms"] <= d["scrape_max_ms"]
+    # the server stamps a scrape's end after its write returns: a thread preempted right there (a
+    # busy CPU box) logs a little more than the client saw, so the bound carries a 5 ms allowance
+    assert d["server_scrapes"] == d["scrapes"] and 0 < d["server_scrape_p99_ms"] <= d["scrape_max_ms"] + 5.0
     assert "interval" in d["value_note"]
     assert idle["server_scrape_p99_ms"] > 0 and idle["scrape_p999_ms"] >= idle["scrape_p99_ms"]
 
