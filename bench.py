@@ -25,7 +25,9 @@ The exporter's own per-GPU xGMI counters are compared with that expectation
 (``xgmi.per_gpu[].tx_vs_expected``), and after the timed region rank 0 drives GPU 0 -> k for every
 peer k and checks that the link whose counter moves is the one the exporter maps to k's BDF
 (``xgmi.link_map``). W warmup ticks, then exactly K ticks are timed between barriers +
-torch.cuda.synchronize(); the MAX elapsed over ranks is used.
+torch.cuda.synchronize(); the MAX elapsed over ranks is used. The timed region starts right after
+a tick and each step's xGMI traffic runs inside its own interval, so K steps span K intervals at
+every N.
 
 Reported ``value`` = whole-node fresh device samples per second (K ticks x N GPUs / elapsed);
 ``vs_baseline`` = per-GPU rate / 0.077 samples/s/GPU, the reference's best observed rate
@@ -333,6 +335,13 @@ def main() -> int:
     scrape_result = {}
     scraper = None
     if rank == 0:
+        # Start the timed region right after a tick: the K timed ticks then close K whole intervals
+        # (t0 + I, ..., t0 + K*I), whatever the calibration above took. Each step's all-reduces run
+        # INSIDE its interval, before the tick that closes it, so the region ends at tick K -- not
+        # a random phase of an interval plus the last step's reductions past it (the elapsed time
+        # then moved by up to -0.6 / +0.4 intervals with the phase, i.e. +-4-6 % of a 10-step
+        # samples/s, at N > 1 only).
+        mon.wait_ticks(1, timeout_s=args.interval * 5 + 30)
         duration = args.steps * args.interval
 
         def _scrape():
@@ -356,11 +365,7 @@ def main() -> int:
     tick_rates = []  # per tick, per sampled device: (sum of per-link write B/s, read B/s) or None
     ar_events = []
     for step in range(args.steps):
-        if rank == 0:
-            if not mon.ex.wait_for_seq(seq0 + step + 1, args.interval * 5 + 10):
-                raise SystemExit("exporter tick timed out")
-            tick_rates.append([(sum(r.get("xgmi_wr_Bps") or [0.0]), sum(r.get("xgmi_rd_Bps") or [0.0]))
-                               if r.get("valid") else None for r in mon.ex.rates()])
+        # one step = one sampling interval: this interval's xGMI traffic, then the tick closing it
         if ar_buf is not None:
             if has_gpu:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -372,6 +377,11 @@ def main() -> int:
             else:
                 for _ in range(reps):
                     dist.all_reduce(ar_buf)
+        if rank == 0:
+            if not mon.ex.wait_for_seq(seq0 + step + 1, args.interval * 5 + 10):
+                raise SystemExit("exporter tick timed out")
+            tick_rates.append([(sum(r.get("xgmi_wr_Bps") or [0.0]), sum(r.get("xgmi_rd_Bps") or [0.0]))
+                               if r.get("valid") else None for r in mon.ex.rates()])
     barrier()
     elapsed = time.perf_counter() - t0
     if rank == 0:  # the exporter's counters at the end of the timed region (not after the reductions)

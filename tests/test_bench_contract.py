@@ -79,6 +79,10 @@ def test_bench_two_ranks_gloo():
     # 2 ranks: a ring all-reduce moves (2(n-1)/n) * S = 1 MiB out of each rank per step
     assert x["expected_tx_GBps_per_gpu"] > 0
     assert "exporter_tx_GBps_per_gpu" in x and "exporter_vs_expected" in x
+    # the timed region starts on a tick and each step's all-reduces run inside its interval: K
+    # steps span K intervals, so the whole-node rate is N / interval (was ~0.9x with the last
+    # step's reductions past the last tick and a random start phase)
+    assert lines[0]["value"] == pytest.approx(2 / 0.1, rel=0.12)
 
 
 def test_bench_runs_without_torch():
