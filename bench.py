@@ -565,17 +565,17 @@ def main() -> int:
             except Exception as e:  # noqa: BLE001
                 lm = {"error": f"{type(e).__name__}: {e}"}
             result["xgmi"] = dict(result["xgmi"] or {}, link_map=lm)
-    for ld in loads:
-        ld.stop()
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
-    if result is not None:
+    if result is not None:  # the line is out before the teardown collectives can stall on a peer
         line = json.dumps(result)
         print(line, flush=True)
         if args.out:
             with open(args.out, "w") as fh:
                 fh.write(line + "\n")
+    for ld in loads:
+        ld.stop()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
     return 0
 
 
