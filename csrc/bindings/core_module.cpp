@@ -81,6 +81,8 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "compat_families", &c.compat_families);
   get(d, "extended_families", &c.extended_families);
   get(d, "full_device_labels", &c.full_device_labels);
+  get(d, "metrics_include", &c.metrics_include);
+  get(d, "metrics_exclude", &c.metrics_exclude);
   get(d, "processes", &c.processes);
   get(d, "link_every", &c.link_every);
   get(d, "ras_every", &c.ras_every);

@@ -1137,8 +1137,10 @@ TickInfo Exporter::tick() {
   in.compat_families = cfg_.compat_families;
   in.extended_families = cfg_.extended_families;
   in.full_device_labels = cfg_.full_device_labels;
+  in.metrics_include = &cfg_.metrics_include;
+  in.metrics_exclude = &cfg_.metrics_exclude;
   auto snap = std::make_shared<Snapshot>();
-  snap->body.reserve(64 * 1024);
+  snap->body.reserve(std::max<size_t>(64 * 1024, last_body_bytes_ + last_body_bytes_ / 8));  // 8 GPUs: ~130 KB
   int64_t tr = mono_ns();
   {
     TraceRange trr("gpumon.render");
@@ -1163,6 +1165,7 @@ TickInfo Exporter::tick() {
   }
   info.pod_rows = rows.size();
   info.body_bytes = snap->body.size();
+  last_body_bytes_ = snap->body.size();
   uint64_t s = seq_.load() + 1;
   snap->seq = s;
   // Publish the text body first (the tick's data is exported from here on), then gzip it and

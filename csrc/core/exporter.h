@@ -51,6 +51,10 @@ struct ExporterConfig {
   bool compat_families = true;
   bool extended_families = true;
   bool full_device_labels = false;
+  // Prometheus family filter, shell globs on the family name (e.g. "gpu_xcd_*"): with an include
+  // list only matching families are served, then exclude drops matching ones. The Influx push is
+  // not filtered (its measurements are the reference's fixed layout).
+  std::vector<std::string> metrics_include, metrics_exclude;
   bool processes = true;
   int link_every = 600;               // ticks between amdsmi_get_link_metrics refreshes (+ on link state change)
   int ras_every = 5;                  // ticks per full RAS / ECC pass (0 = off)
@@ -239,6 +243,7 @@ class Exporter {
   std::mutex seq_mu_;
   std::condition_variable seq_cv_;
   std::atomic<uint64_t> ticks_{0}, samples_{0}, stale_{0}, overruns_{0};
+  size_t last_body_bytes_ = 0;  // tick thread only: sizes the next render buffer
   std::atomic<uint64_t> phase_ns_[5] = {};  // sample, procs, attrib, render, gzip (cumulative)
 
  public:

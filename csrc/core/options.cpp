@@ -241,6 +241,8 @@ const std::map<std::string, Setter>& setters() {
       {"compat_families", bool_at([](NativeOptions* o) { return &o->cfg.compat_families; })},
       {"extended_families", bool_at([](NativeOptions* o) { return &o->cfg.extended_families; })},
       {"full_device_labels", bool_at([](NativeOptions* o) { return &o->cfg.full_device_labels; })},
+      {"metrics_include", list_at([](NativeOptions* o) { return &o->cfg.metrics_include; })},
+      {"metrics_exclude", list_at([](NativeOptions* o) { return &o->cfg.metrics_exclude; })},
       {"influx_url", str_at([](NativeOptions* o) { return &o->cfg.influx_url; })},
       {"influx_token", str_at([](NativeOptions* o) { return &o->cfg.influx_token; })},
       {"influx_extended", bool_at([](NativeOptions* o) { return &o->cfg.influx_extended; })},
@@ -515,6 +517,8 @@ std::string options_json(const NativeOptions& o) {
   B("roctx", c.roctx);
   B("compat_families", c.compat_families);
   B("extended_families", c.extended_families);
+  L("metrics_include", c.metrics_include);
+  L("metrics_exclude", c.metrics_exclude);
   S("influx_url", redact_url(c.influx_url));
   S("influx_token", c.influx_token.empty() ? "" : "***");
   B("influx_extended", c.influx_extended);

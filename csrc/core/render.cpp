@@ -1,5 +1,7 @@
 #include "render.h"
 
+#include <fnmatch.h>
+
 #include <charconv>
 #include <cmath>
 #include <cstring>
@@ -69,26 +71,43 @@ void escape_influx_field_str(const std::string& v, std::string* out) {
   }
 }
 
+bool family_selected(const RenderInput& in, const char* name) {
+  auto any = [name](const std::vector<std::string>* globs) {
+    for (const auto& g : *globs)
+      if (fnmatch(g.c_str(), name, 0) == 0) return true;
+    return false;
+  };
+  if (in.metrics_include && !in.metrics_include->empty() && !any(in.metrics_include)) return false;
+  return !(in.metrics_exclude && !in.metrics_exclude->empty() && any(in.metrics_exclude));
+}
+
 namespace {
 
 using Labels = std::vector<std::pair<const char*, std::string>>;
 
-// A metric family whose header is dropped again if no sample line follows it.
+// The input being rendered on this thread: every family checks the filter against it.
+thread_local const RenderInput* t_render_in = nullptr;
+
+bool selected(const char* name) { return !t_render_in || family_selected(*t_render_in, name); }
+
+// A metric family whose header is dropped again if no sample line follows it; a family the
+// filter deselects writes nothing at all.
 class Family {
  public:
   Family(std::string* o, const char* name, const char* help, const char* type)
-      : o_(o), name_(name), mark_(o->size()) {
+      : o_(o), name_(name), mark_(o->size()), on_(selected(name)) {
+    if (!on_) return;
     o_->append("# HELP ").append(name).push_back(' ');
     o_->append(help).push_back('\n');
     o_->append("# TYPE ").append(name).push_back(' ');
     o_->append(type).push_back('\n');
   }
   ~Family() {
-    if (!any_) o_->resize(mark_);
+    if (on_ && !any_) o_->resize(mark_);
   }
   // base: preformatted `k="v",...` (may be empty); extra: additional label pairs.
   void add(const std::string& base, const Labels& extra, double v, const char* suffix = nullptr) {
-    if (std::isnan(v)) return;
+    if (!on_ || std::isnan(v)) return;
     any_ = true;
     o_->append(name_);
     if (suffix) o_->append(suffix);
@@ -115,6 +134,7 @@ class Family {
   std::string* o_;
   const char* name_;
   size_t mark_;
+  bool on_;
   bool any_ = false;
 };
 
@@ -133,6 +153,7 @@ std::string label_str(const Labels& l) {
 
 void histogram(std::string* o, const char* name, const char* help, const HistSnapshot& h,
                const std::string& base) {
+  if (!selected(name)) return;
   o->append("# HELP ").append(name).append(" ").append(help).append("\n");
   o->append("# TYPE ").append(name).append(" histogram\n");
   uint64_t cum = 0;
@@ -168,6 +189,10 @@ const double kMiB = 1048576.0;
 }  // namespace
 
 void render_prometheus(const RenderInput& in, std::string* o) {
+  struct Scope {  // the filter applies to this call only (renders may nest on no other path)
+    explicit Scope(const RenderInput* in) { t_render_in = in; }
+    ~Scope() { t_render_in = nullptr; }
+  } scope(&in);
   const auto& st = *in.statics;
   const auto& sm = *in.samples;
   const size_t n = std::min(st.size(), sm.size());

@@ -110,7 +110,13 @@ struct RenderInput {
   // false: device series carry only host + gpu_id (the reference's tags, gpu.py:137); uuid / bdf /
   // model live once on gpu_info (join on gpu_id). true: uuid + bdf on every device series.
   bool full_device_labels = false;
+  // family filter (ExporterConfig::metrics_include / metrics_exclude); null or empty = no filter
+  const std::vector<std::string>* metrics_include = nullptr;
+  const std::vector<std::string>* metrics_exclude = nullptr;
 };
+
+// Whether render_prometheus emits family `name` under the input's include / exclude globs.
+bool family_selected(const RenderInput& in, const char* name);
 
 void render_prometheus(const RenderInput& in, std::string* out);
 // Line protocol; one line per node_gpu / pod_gpu row (+ gpu_ext when extended), ns timestamps.

@@ -57,6 +57,8 @@ class Config:
     gzip: bool = True
     compat_families: bool = True
     extended_families: bool = True
+    metrics_include: List[str] = field(default_factory=list)  # serve only families matching these globs (e.g. node_gpu_*)
+    metrics_exclude: List[str] = field(default_factory=list)  # drop families matching these globs (e.g. gpu_xcd_*); Influx unfiltered
     # influx compat push
     influx_url: str = ""
     influx_token: str = ""                # InfluxDB 2.x/3.x API token (env INFLUXDB_TOKEN, from a Secret); 1.x: user:password@ in the URL
@@ -156,6 +158,8 @@ class Config:
             "roctx": self.roctx,
             "compat_families": self.compat_families,
             "extended_families": self.extended_families,
+            "metrics_include": list(self.metrics_include),
+            "metrics_exclude": list(self.metrics_exclude),
             "influx_url": self.influx_url,
             "influx_token": self.influx_token,
             "influx_extended": self.influx_extended,
@@ -293,6 +297,10 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
                    help="kubelet PodResources / CRI / Docker metadata pollers: native (C++) or off")
     p.add_argument("--no-processes", dest="processes", action="store_false", default=None)
     p.add_argument("--no-gzip", dest="gzip", action="store_false", default=None)
+    p.add_argument("--metrics-include", dest="metrics_include",
+                   help="comma-separated globs: serve only these metric families (e.g. 'node_gpu_*,pod_gpu_*')")
+    p.add_argument("--metrics-exclude", dest="metrics_exclude",
+                   help="comma-separated globs: metric families left out of /metrics (e.g. 'gpu_xcd_*')")
     p.add_argument("--sample-threads", dest="sample_threads", type=int)
     p.add_argument("--rt-priority", dest="rt_priority", type=int)
     p.add_argument("--device-timeout", dest="device_timeout_s", type=float,

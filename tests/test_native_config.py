@@ -203,3 +203,19 @@ def test_yaml_subset_agrees_with_pyyaml(doc, flow, wrap):
             assert float(g[0]) == pytest.approx(v)
         else:
             assert g == exp, (k, g, exp, body)
+
+
+def test_metric_filter_keys_parse_identically(tmp_path):
+    """metrics_include / metrics_exclude: YAML block list, env, and the binary's flag."""
+    p = tmp_path / "filter.yaml"
+    p.write_text("gpumon:\n  metrics_exclude:\n    - 'gpu_xcd_*'\n    - gpu_probe_*\n  metrics_include: [node_gpu_*, 'gpu_*']\n")
+    r = _print("--config", str(p))
+    assert r.returncode == 0, r.stderr
+    n = json.loads(r.stdout)
+    assert n["metrics_exclude"] == ["gpu_xcd_*", "gpu_probe_*"] and n["metrics_include"] == ["node_gpu_*", "gpu_*"]
+    _same(n, _py(str(p)))
+    env = {"GPUMON_METRICS_EXCLUDE": "pod_gpu_*,gpumon_*"}
+    n = json.loads(_print("--config", str(p), env=env).stdout)
+    assert n["metrics_exclude"] == ["pod_gpu_*", "gpumon_*"] == _py(str(p), env)["metrics_exclude"]
+    n = json.loads(_print("--metrics-exclude", "gpu_xcd_*").stdout)
+    assert n["metrics_exclude"] == ["gpu_xcd_*"] and n["metrics_include"] == []

@@ -152,3 +152,25 @@ def test_influx_extended_pod_gpu_carries_per_process_fields(mock_exporter):
     (le,) = [l for l in ext.influx_text().splitlines() if l.startswith("pod_gpu,")]
     assert "proc_gfx_util" not in lp and "mfma_util" not in lp
     assert re.search(r",used_memory=1024,proc_gfx_util=100,cu_occupancy=128,mfma_util=61\.5 \d{19}$", le), le
+
+
+def test_metric_family_filter(mock_exporter):
+    """metrics_include / metrics_exclude (shell globs on family names): a deselected family writes
+    no HELP / TYPE / sample line; the rest of the body is unchanged."""
+    full = promtext.parse(mock_exporter(backend="mock:gpus=2").metrics_text())
+    ex = mock_exporter(backend="mock:gpus=2", metrics_exclude=["gpu_xcd_*", "gpumon_scrape_duration_seconds"])
+    text = ex.metrics_text()
+    fam = promtext.parse(text)
+    assert "gpu_xcd_busy_percent" in full and "gpumon_scrape_duration_seconds" in full
+    assert not [n for n in fam if n.startswith("gpu_xcd_")]
+    assert "gpumon_scrape_duration_seconds" not in text  # histogram: no _bucket / _sum / _count
+    assert set(full) - set(fam) == {n for n in full if n.startswith("gpu_xcd_")} | {"gpumon_scrape_duration_seconds"}
+    assert fam["node_gpu_gpu_util"]["samples"] == full["node_gpu_gpu_util"]["samples"]
+    # include first, then exclude
+    ex = mock_exporter(backend="mock:gpus=2", metrics_include=["node_gpu_*", "gpu_up"],
+                       metrics_exclude=["node_gpu_mem_bw_util"])
+    fam = promtext.parse(ex.metrics_text())
+    assert set(fam) == {n for n in full if n.startswith("node_gpu_") and n != "node_gpu_mem_bw_util"} | {"gpu_up"}
+    # the Influx sink keeps the reference's fixed layout
+    ex = mock_exporter(backend="mock:gpus=1", metrics_include=["gpu_up"])
+    assert any(l.startswith("node_gpu,") for l in ex.influx_text().splitlines())
