@@ -104,8 +104,12 @@ bin/gpumon-exporter-nodev: $(CORE_OBJ) build/obj/exporter_main.o csrc/testtools/
 	$(CXX) $(CXXFLAGS) -c csrc/testtools/nodev_interpose.cpp -o build/obj/testtools/nodev_interpose.o
 	$(CXX) -rdynamic -o $@ $(CORE_OBJ) build/obj/exporter_main.o build/obj/testtools/nodev_interpose.o $(LIBS)
 
-# Experiment tool: can a shader read the SQ's perf-snapshot registers (tools/perf_snapshot_probe.hip)?
-snapshot: bin/perf_snapshot_probe
+# Experiment tools: can a shader read the SQ's perf-snapshot registers (tools/perf_snapshot_probe.hip)?
+# Which raw-HSA step pins the per-queue host blocks (tools/hsa_stages.cpp)?
+snapshot: bin/perf_snapshot_probe bin/hsa_stages
+bin/hsa_stages: tools/hsa_stages.cpp
+	@mkdir -p bin
+	$(CXX) -O2 -std=c++17 -Wall -I$(ROCM)/include $< -L$(ROCM)/lib -lhsa-runtime64 -Wl,-rpath,$(ROCM)/lib -o $@
 bin/perf_snapshot_probe: tools/perf_snapshot_probe.hip
 	@mkdir -p bin
 	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -O2 $< -o $@
@@ -127,12 +131,23 @@ $(PMCLIB): csrc/plugins/pmc_plugin.cpp csrc/plugins/ondevice_abi.h
 	@mkdir -p lib
 	$(HIPCC) -O2 -std=c++17 -fPIC -shared -fvisibility=hidden -I$(ROCM)/include $< -Wl,-soname,libgpumon_pmc.so \
 	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lrocprofiler-sdk -lhsa-runtime64 -o $@
-build/obj/plugins/probe_plugin.o: csrc/plugins/probe_plugin.cpp csrc/plugins/ondevice_abi.h $(HIP_HDR)
+build/obj/plugins/probe_plugin.o: csrc/plugins/probe_plugin.cpp csrc/plugins/ondevice_abi.h csrc/plugins/probe_hsa.h $(HIP_HDR)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
-$(PROBELIB): build/obj/plugins/probe_plugin.o build/obj/hip/kernels.o build/obj/hip/burn16.o build/obj/hip/burn_dtypes.o
+# The K1 probe as an unbundled gfx950 code object, embedded (.incbin) in the raw-HSA launch path.
+PROBECO := build/obj/hip/probe_$(GPUMON_ARCH).hsaco
+$(PROBECO): csrc/hip/probe_co.hip $(HIP_HDR)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(GPUMON_ARCH) --offload-device-only --no-gpu-bundle-output -O3 -std=c++17 -Icsrc $< -o $@
+build/obj/plugins/probe_hsa.o: csrc/plugins/probe_hsa.cpp csrc/plugins/probe_hsa.h $(HIP_HDR) $(PROBECO)
+	@mkdir -p $(dir $@)
+	$(CXX) -O2 -std=c++17 -fPIC -fvisibility=hidden -Wall -Wextra -I$(ROCM)/include \
+	  -DGPUMON_PROBE_HSACO='"$(abspath $(PROBECO))"' -c $< -o $@
+$(PROBELIB): build/obj/plugins/probe_plugin.o build/obj/plugins/probe_hsa.o build/obj/hip/kernels.o build/obj/hip/burn16.o \
+             build/obj/hip/burn_dtypes.o
 	@mkdir -p lib
-	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -shared -fPIC $^ -Wl,-soname,libgpumon_probe.so -o $@
+	$(HIPCC) --offload-arch=$(GPUMON_ARCH) -shared -fPIC $^ -Wl,-soname,libgpumon_probe.so \
+	  -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lhsa-runtime64 -o $@
 
 # gpumon._pmc: Python view of the PMC plugin (linked, rpath $ORIGIN/../lib).
 PMCEXT := gpumon/_pmc$(EXT)

@@ -156,8 +156,11 @@ int main(int argc, char** argv) {
   // nothing in this process has touched the GPU yet, and the samplers pick the devices up once the
   // backend lists them (OnDevice maps agents / creates probes on its first steps).
   if (once) {
+    // One sample to stdout, over a short live interval (<= 0.5 s): the device workers sub-sample
+    // KFD occupancy through it (an interval mean, not one instantaneous read that can land between
+    // a tenant's kernels), rates span it, and the on-device step lands before its closing tick.
     cfg.serve_http = false;
-    cfg.interval_s = 0;
+    cfg.interval_s = std::min(cfg.interval_s > 0 ? cfg.interval_s : 0.5, 0.5);
     Exporter e(cfg);
     OnDevice ondev(&e, od);
     if ((od.pmc || od.probe) && !ondev.start(&err)) {
@@ -169,8 +172,11 @@ int main(int argc, char** argv) {
       ondev.stop();
       return 1;
     }
+    if (!err.empty()) fprintf(stderr, "backend not ready: %s\n", err.c_str());
     ondev.step();
-    e.tick();  // second tick so rates are populated (and the on-device series are rendered)
+    // the tick after the step renders its series; the one after that spans a whole interval
+    // that started after the step
+    e.wait_for_seq(e.seq() + 2, 30.0 + 4 * cfg.interval_s);
     auto s = e.snapshot();
     fwrite(s->body.data(), 1, s->body.size(), stdout);
     ondev.stop();

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "probe_collect.h"
 
 namespace gpumon_hip {
 
@@ -132,24 +133,6 @@ class XgmiLoad {
 };
 
 // --- K1 probe: pinned ring buffer ----------------------------------------------------------------
-struct ProbeResult {
-  bool complete = false;
-  uint32_t seq = 0;
-  int blocks = 0;
-  int arrived = 0;
-  int64_t host_launch_ns = 0;   // CLOCK_MONOTONIC before the launch call
-  int64_t host_done_ns = 0;     // when the host observed the last arrival
-  uint64_t gpu_span_ticks = 0;  // max(t1) - min(t0), 100 MHz ticks
-  uint64_t gpu_first_start = 0; // min(t0) in ticks
-  std::vector<int> xcc_blocks;  // blocks seen per XCC id (index 0..15)
-  std::vector<double> xcc_clock_mhz;  // mean effective shader clock per XCC (0 if none)
-  int unique_cus = 0;
-  std::vector<double> xcc_wave_slot;  // mean lowest HW_ID.WAVE_ID per SIMD, per XCC (resident-wave pressure)
-  double wave_slot_mean = 0;          // the same over every SIMD seen
-  int stale_records = 0;        // records whose seq never matched after the flag (should be 0)
-  std::vector<ProbeRecord> records;
-};
-
 class Probe {
  public:
   Probe(int dev, int blocks, int slots, int spin_ticks);

@@ -12,6 +12,7 @@
 #include <tuple>
 
 #include "hip_api.h"
+#include "probe_kernel.h"
 
 namespace gpumon_hip {
 
@@ -206,37 +207,7 @@ __global__ void __launch_bounds__(256) stream_triad_kernel(const f32x4* __restri
 __global__ void __launch_bounds__(64) probe_kernel(ProbeRecord* __restrict__ recs, uint32_t* arrivals,
                                                    uint32_t* counter, uint32_t seq, uint32_t spin_ticks,
                                                    uint32_t blocks) {
-  const uint32_t lane = threadIdx.x;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  const uint64_t c0 = __builtin_amdgcn_s_memtime();
-  uint32_t xcc, hw;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-  uint64_t t1 = t0;
-  // Bounded spin on the constant 100 MHz clock: exit condition reached by every wave.
-  for (int guard = 0; guard < (1 << 20); ++guard) {
-    t1 = __builtin_amdgcn_s_memrealtime();
-    if (t1 - t0 >= spin_ticks) break;
-  }
-  const uint64_t c1 = __builtin_amdgcn_s_memtime();
-  // ProbeRecord = 3 x 16 B: {xcc_id, hw_id, t0_real}, {t1_real, c0}, {c1, seq, block}
-  if (lane < 3) {
-    uint4 v;
-    if (lane == 0) v = make_uint4(xcc & 0xF, hw, static_cast<uint32_t>(t0), static_cast<uint32_t>(t0 >> 32));
-    else if (lane == 1)
-      v = make_uint4(static_cast<uint32_t>(t1), static_cast<uint32_t>(t1 >> 32), static_cast<uint32_t>(c0),
-                     static_cast<uint32_t>(c0 >> 32));
-    else v = make_uint4(static_cast<uint32_t>(c1), static_cast<uint32_t>(c1 >> 32), seq, blockIdx.x);
-    reinterpret_cast<uint4*>(recs + blockIdx.x)[lane] = v;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == blocks - 1) {
-      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm the slot
-      __hip_atomic_store(arrivals, blocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
+  probe_body(recs, arrivals, counter, seq, spin_ticks, blocks);  // probe_kernel.h (shared with the HSA path)
 }
 
 // ============================================================================================
@@ -640,64 +611,7 @@ bool Probe::poll(int slot, ProbeResult* out) {
   }
   out->complete = true;
   out->host_done_ns = mono_ns();
-  const ProbeRecord* r = ring_ + static_cast<size_t>(slot) * blocks_;
-  // The flag is written after every wave drained its record stores; a record still in flight on
-  // another fabric path would show the previous seq. Re-read those briefly (bounded) and count what
-  // never landed.
-  std::vector<int> late;
-  for (int b = 0; b < blocks_; ++b)
-    if (__atomic_load_n(&r[b].seq, __ATOMIC_ACQUIRE) != out->seq) late.push_back(b);
-  for (int spin = 0; !late.empty() && spin < 1000; ++spin) {
-    std::this_thread::yield();
-    late.erase(std::remove_if(late.begin(), late.end(),
-                              [&](int b) { return __atomic_load_n(&r[b].seq, __ATOMIC_ACQUIRE) == out->seq; }),
-               late.end());
-  }
-  out->stale_records = static_cast<int>(late.size());
-  out->records.assign(r, r + blocks_);
-  out->xcc_blocks.assign(16, 0);
-  std::vector<double> clk_sum(16, 0.0);
-  uint64_t tmin = ~0ull, tmax = 0;
-  std::set<std::tuple<uint32_t, uint32_t>> cus;
-  for (const auto& x : out->records) {
-    if (x.seq != out->seq) continue;  // torn / stale record (should not happen after the counter)
-    const uint32_t xc = x.xcc_id & 0xF;
-    out->xcc_blocks[xc]++;
-    const uint64_t dt = x.t1_real - x.t0_real;
-    if (dt) clk_sum[xc] += static_cast<double>(x.c1 - x.c0) / static_cast<double>(dt) * 100.0;  // MHz
-    tmin = std::min(tmin, x.t0_real);
-    tmax = std::max(tmax, x.t1_real);
-    // CU identity inside an XCC: HW_ID bits [15:8] = cu_id | sh_id | se_id
-    cus.insert({xc, (x.hw_id >> 8) & 0xFF});
-  }
-  // Resident-wave pressure: the SPI hands a new wave the lowest free slot of its SIMD, so the lowest
-  // WAVE_ID a probe wave got on a SIMD counts the slots other work held there at launch.
-  std::map<uint32_t, uint32_t> simd_min;  // (xcc, se, sh, cu, simd) -> lowest wave slot
-  for (const auto& x : out->records) {
-    if (x.seq != out->seq) continue;
-    const uint32_t key = ((x.xcc_id & 0xF) << 16) | (((x.hw_id >> 8) & 0xFF) << 2) | ((x.hw_id >> 4) & 0x3);
-    const uint32_t slot = x.hw_id & 0xF;
-    auto it = simd_min.find(key);
-    if (it == simd_min.end()) simd_min.emplace(key, slot);
-    else it->second = std::min(it->second, slot);
-  }
-  std::vector<double> ws_sum(16, 0.0), ws_n(16, 0.0);
-  double all = 0;
-  for (const auto& kv : simd_min) {
-    ws_sum[kv.first >> 16] += kv.second;
-    ws_n[kv.first >> 16] += 1;
-    all += kv.second;
-  }
-  out->xcc_wave_slot.assign(16, 0.0);
-  for (int k = 0; k < 16; ++k)
-    if (ws_n[k] > 0) out->xcc_wave_slot[k] = ws_sum[k] / ws_n[k];
-  out->wave_slot_mean = simd_min.empty() ? 0.0 : all / simd_min.size();
-  out->xcc_clock_mhz.assign(16, 0.0);
-  for (int k = 0; k < 16; ++k)
-    if (out->xcc_blocks[k]) out->xcc_clock_mhz[k] = clk_sum[k] / out->xcc_blocks[k];
-  out->gpu_first_start = tmin;
-  out->gpu_span_ticks = tmax > tmin ? tmax - tmin : 0;
-  out->unique_cus = static_cast<int>(cus.size());
+  probe_collect(ring_ + static_cast<size_t>(slot) * blocks_, blocks_, out);
   return true;
 }
 

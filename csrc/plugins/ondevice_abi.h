@@ -1,7 +1,8 @@
 // C ABI of the two on-device plugins the exporter dlopen()s at run time:
 //
 //   lib/libgpumon_pmc.so    rocprofiler-sdk device counting (SQ/GRBM PMCs, whole GPU, host thread)
-//   lib/libgpumon_probe.so  the K1 gfx950 probe microkernel + its pinned ring buffer (HIP runtime)
+//   lib/libgpumon_probe.so  the K1 gfx950 probe microkernel + its pinned ring buffer (raw HSA / AQL;
+//                           HIP with GPUMON_PROBE_RUNTIME=hip)
 //
 // Why plugins: bin/gpumon-exporter links neither HIP nor rocprofiler-sdk, so the same binary runs
 // on a node without them and only pays for them when --pmc / --probe ask (the SURVEY N1 role: the
