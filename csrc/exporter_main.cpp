@@ -161,6 +161,9 @@ int main(int argc, char** argv) {
     // a tenant's kernels), rates span it, and the on-device step lands before its closing tick.
     cfg.serve_http = false;
     cfg.interval_s = std::min(cfg.interval_s > 0 ? cfg.interval_s : 0.5, 0.5);
+    // the on-device values printed are the synchronous step's (PMC over --pmc-window): the
+    // samplers' own loops must not read again inside the short interval
+    o.od.pmc_every_s = o.od.probe_every_s = 3600.0;
     Exporter e(cfg);
     OnDevice ondev(&e, od);
     if ((od.pmc || od.probe) && !ondev.start(&err)) {
