@@ -1273,6 +1273,63 @@ bool Exporter::healthy() const {
   return last != 0 && (mono_ns() - last) * 1e-9 < stale;
 }
 
+namespace {
+
+std::string url_decode(const std::string& s) {
+  std::string o;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] == '+') {
+      o.push_back(' ');
+    } else if (s[i] == '%' && i + 2 < s.size() && isxdigit(static_cast<unsigned char>(s[i + 1])) &&
+               isxdigit(static_cast<unsigned char>(s[i + 2]))) {
+      o.push_back(static_cast<char>(std::stoi(s.substr(i + 1, 2), nullptr, 16)));
+      i += 2;
+    } else {
+      o.push_back(s[i]);
+    }
+  }
+  return o;
+}
+
+// include=a,b&exclude=c (each repeatable): the family globs of a per-request filter
+bool parse_filter_query(const std::string& q, std::vector<std::string>* inc, std::vector<std::string>* exc) {
+  bool any = false;
+  for (const auto& kv : split(q, '&')) {
+    const size_t eq = kv.find('=');
+    if (eq == std::string::npos) continue;
+    const std::string k = url_decode(kv.substr(0, eq));
+    std::vector<std::string>* dst = k == "include" ? inc : k == "exclude" ? exc : nullptr;
+    if (!dst) continue;
+    any = true;
+    for (const auto& g : split(url_decode(kv.substr(eq + 1)), ','))
+      if (!g.empty()) dst->push_back(g);
+  }
+  return any;
+}
+
+}  // namespace
+
+std::shared_ptr<const Exporter::Filtered> Exporter::filtered(const Snapshot& s, const std::string& query, bool gzip) {
+  {
+    std::lock_guard<std::mutex> g(filter_mu_);
+    if (filter_seq_ != s.seq) {
+      filter_cache_.clear();
+      filter_seq_ = s.seq;
+    }
+    auto it = filter_cache_.find(query);
+    if (it != filter_cache_.end() && (!gzip || !it->second->body_gz.empty())) return it->second;
+  }
+  std::vector<std::string> inc, exc;
+  parse_filter_query(query, &inc, &exc);
+  auto f = std::make_shared<Filtered>();
+  filter_exposition(s.body, inc, exc, &f->body);
+  if (gzip) gzip_compress(f->body, &f->body_gz, 1);
+  std::lock_guard<std::mutex> g(filter_mu_);
+  if (filter_seq_ == s.seq && (filter_cache_.size() < kFilterCache || filter_cache_.count(query)))
+    filter_cache_[query] = f;
+  return f;
+}
+
 void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
   if (req.path == "/metrics") {
     auto s = store_.get();
@@ -1282,6 +1339,21 @@ void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
       return;
     }
     resp->content_type = "text/plain; version=0.0.4; charset=utf-8";
+    std::vector<std::string> inc, exc;
+    if (!req.query.empty() && parse_filter_query(req.query, &inc, &exc)) {
+      // per-request family filter (e.g. a fast Prometheus job for node_gpu_* only)
+      auto f = filtered(*s, req.query, req.accept_gzip && cfg_.gzip);
+      if (req.accept_gzip && !f->body_gz.empty()) {
+        resp->extra_headers = "Content-Encoding: gzip\r\n";
+        resp->data = f->body_gz.data();
+        resp->len = f->body_gz.size();
+      } else {
+        resp->data = f->body.data();
+        resp->len = f->body.size();
+      }
+      resp->owner = f;
+      return;
+    }
     if (req.accept_gzip && !s->body_gz.empty()) {
       resp->extra_headers = "Content-Encoding: gzip\r\n";
       resp->data = s->body_gz.data();

@@ -199,6 +199,16 @@ class Exporter {
   std::unique_ptr<Attributor> attr_;
   std::unique_ptr<HttpServer> server_;
   SnapshotStore store_;
+  // /metrics?include=&exclude= bodies of the current snapshot, by query (filtered once per tick and
+  // query, at most kFilterCache queries; the next snapshot starts an empty cache)
+  struct Filtered {
+    std::string body, body_gz;
+  };
+  static constexpr size_t kFilterCache = 16;
+  std::mutex filter_mu_;
+  uint64_t filter_seq_ = 0;
+  std::map<std::string, std::shared_ptr<const Filtered>> filter_cache_;
+  std::shared_ptr<const Filtered> filtered(const Snapshot& s, const std::string& query, bool gzip);
   Histogram sample_hist_;
   mutable std::mutex tick_log_mu_;
   std::vector<TickInfo> tick_log_;  // ring of kTickLog entries

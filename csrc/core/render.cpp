@@ -71,14 +71,43 @@ void escape_influx_field_str(const std::string& v, std::string* out) {
   }
 }
 
-bool family_selected(const RenderInput& in, const char* name) {
-  auto any = [name](const std::vector<std::string>* globs) {
-    for (const auto& g : *globs)
+bool family_matches(const std::vector<std::string>& include, const std::vector<std::string>& exclude,
+                    const char* name) {
+  auto any = [name](const std::vector<std::string>& globs) {
+    for (const auto& g : globs)
       if (fnmatch(g.c_str(), name, 0) == 0) return true;
     return false;
   };
-  if (in.metrics_include && !in.metrics_include->empty() && !any(in.metrics_include)) return false;
-  return !(in.metrics_exclude && !in.metrics_exclude->empty() && any(in.metrics_exclude));
+  if (!include.empty() && !any(include)) return false;
+  return exclude.empty() || !any(exclude);
+}
+
+bool family_selected(const RenderInput& in, const char* name) {
+  static const std::vector<std::string> kNone;
+  return family_matches(in.metrics_include ? *in.metrics_include : kNone,
+                        in.metrics_exclude ? *in.metrics_exclude : kNone, name);
+}
+
+void filter_exposition(const std::string& body, const std::vector<std::string>& include,
+                       const std::vector<std::string>& exclude, std::string* out) {
+  out->clear();
+  out->reserve(body.size());
+  bool keep = true;
+  std::string name;
+  size_t pos = 0;
+  while (pos < body.size()) {
+    size_t eol = body.find('\n', pos);
+    const size_t end = eol == std::string::npos ? body.size() : eol + 1;
+    if (body.compare(pos, 7, "# HELP ") == 0) {
+      const size_t a = pos + 7;
+      size_t b = a;
+      while (b < end && body[b] != ' ' && body[b] != '\n') ++b;
+      name.assign(body, a, b - a);
+      keep = family_matches(include, exclude, name.c_str());
+    }
+    if (keep) out->append(body, pos, end - pos);
+    pos = end;
+  }
 }
 
 namespace {

@@ -117,6 +117,15 @@ struct RenderInput {
 
 // Whether render_prometheus emits family `name` under the input's include / exclude globs.
 bool family_selected(const RenderInput& in, const char* name);
+// The same rule on plain lists: with a non-empty include list only matching names pass, then
+// exclude drops matching ones (shell globs).
+bool family_matches(const std::vector<std::string>& include, const std::vector<std::string>& exclude,
+                    const char* name);
+// Filters a rendered exposition by family: every line from a family's "# HELP" up to the next one
+// (its TYPE line and samples, histogram _bucket/_sum/_count included) is kept or dropped as a unit.
+// Sample lines before any HELP are kept. Used for per-request filters (/metrics?include=&exclude=).
+void filter_exposition(const std::string& body, const std::vector<std::string>& include,
+                       const std::vector<std::string>& exclude, std::string* out);
 
 void render_prometheus(const RenderInput& in, std::string* out);
 // Line protocol; one line per node_gpu / pod_gpu row (+ gpu_ext when extended), ns timestamps.

@@ -204,3 +204,26 @@ def test_client_refuses_huge_content_length_and_reads_bodies_whole(core):
     assert st == 200 and body == b"x" * 300000
     t.join(5)
     srv.close()
+
+
+def test_per_request_family_filter(mock_exporter):
+    """/metrics?include=&exclude= (shell globs, comma-separated, repeatable, percent-decoded): the
+    same families the config filter would keep, cut from the current snapshot, gzip included; other
+    query parameters leave the body untouched."""
+    ex = mock_exporter(backend="mock:gpus=2")
+    ex.tick()
+    full = promtext.parse(ex.metrics_text())
+    st, _, body = _get(ex.port, "/metrics?exclude=gpu_xcd_*,gpumon_scrape_duration_seconds")
+    fam = promtext.parse(body.decode())
+    assert st == 200
+    assert set(fam) == set(full) - {n for n in full if n.startswith("gpu_xcd_")} - {"gpumon_scrape_duration_seconds"}
+    assert "gpumon_scrape_duration_seconds_bucket" not in body.decode()  # histogram lines go with it
+    st, h, body = _get(ex.port, "/metrics?include=node_gpu_%2A&include=gpu_up&exclude=node_gpu_mem_bw_util",
+                       {"Accept-Encoding": "gzip"})
+    assert st == 200 and h.get("Content-Encoding") == "gzip"
+    fam = promtext.parse(gzip.decompress(body).decode())
+    assert set(fam) == {n for n in full if n.startswith("node_gpu_") and n != "node_gpu_mem_bw_util"} | {"gpu_up"}
+    for _ in range(3):  # cached per snapshot: repeated requests agree
+        assert promtext.parse(_get(ex.port, "/metrics?include=gpu_up")[2].decode()).keys() == {"gpu_up"}
+    st, _, body = _get(ex.port, "/metrics?foo=bar")
+    assert st == 200 and set(promtext.parse(body.decode())) >= set(full) - {"gpumon_scrape_duration_seconds"}
