@@ -41,16 +41,18 @@ def _run(binary, env_extra, extra_args=(), min_s=0.0):
                 time.sleep(0.1)
         errors = []
 
-        def hammer():
+        def hammer(query):
             for _ in range(60):
                 try:
-                    req = urllib.request.Request(f"http://127.0.0.1:{port}/metrics",
+                    req = urllib.request.Request(f"http://127.0.0.1:{port}/metrics{query}",
                                                  headers={"Accept-Encoding": "gzip"})
                     urllib.request.urlopen(req, timeout=5).read()
                 except Exception as e:  # noqa: BLE001
                     errors.append(e)
 
-        ts = [threading.Thread(target=hammer) for _ in range(4)]
+        # plain scrapes and per-request family filters (the per-snapshot filter cache) side by side
+        ts = [threading.Thread(target=hammer, args=(q,))
+              for q in ("", "", "?exclude=gpu_xcd_*", "?include=node_gpu_*,gpu_up")]
         for t in ts:
             t.start()
         for t in ts:
