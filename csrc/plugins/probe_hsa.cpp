@@ -98,19 +98,14 @@ hsa_amd_memory_pool_t find_pool(hsa_agent_t agent, uint32_t want) {
   return q.pool;
 }
 
-// AQL dispatch header: kernel dispatch, barrier bit so slots retire in order, system-scope release
-// (the records and the arrival flag land in host memory the exporter reads). Acquire scope: system
-// by default (the kernargs are host-written); GPUMON_PROBE_ACQUIRE=agent for the A/B measurement.
-uint16_t header() {
-  static const uint16_t h = [] {
-    const char* a = getenv("GPUMON_PROBE_ACQUIRE");
-    const int acq = (a && !strcmp(a, "agent")) ? HSA_FENCE_SCOPE_AGENT : HSA_FENCE_SCOPE_SYSTEM;
-    return static_cast<uint16_t>((HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
-                                 (1 << HSA_PACKET_HEADER_BARRIER) | (acq << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
-                                 (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE));
-  }();
-  return h;
-}
+// AQL dispatch header: kernel dispatch, barrier bit so slots retire in order, system-scope acquire
+// (invalidates the L2 lines of the coarse-grained host kernargs written since the last launch of
+// the slot) and system-scope release (the records and the arrival flag land in host memory). An
+// agent-scope acquire measured the same on fine-grained kernargs but would not cover coarse ones.
+constexpr uint16_t kHeader = (HSA_PACKET_TYPE_KERNEL_DISPATCH << HSA_PACKET_HEADER_TYPE) |
+                             (1 << HSA_PACKET_HEADER_BARRIER) |
+                             (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCACQUIRE_FENCE_SCOPE) |
+                             (HSA_FENCE_SCOPE_SYSTEM << HSA_PACKET_HEADER_SCRELEASE_FENCE_SCOPE);
 
 struct Kernel {
   uint64_t object = 0;
@@ -188,7 +183,7 @@ struct HsaProbe::Impl {
     pkt->reserved2 = 0;
     pkt->completion_signal = done[sig_index];
     const uint32_t setup = 1u << HSA_KERNEL_DISPATCH_PACKET_SETUP_DIMENSIONS;  // 1-D grid
-    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), header() | (setup << 16), __ATOMIC_RELEASE);
+    __atomic_store_n(reinterpret_cast<uint32_t*>(pkt), kHeader | (setup << 16), __ATOMIC_RELEASE);
     hsa_signal_store_screlease(queue->doorbell_signal, static_cast<hsa_signal_value_t>(idx));
   }
 
@@ -238,7 +233,25 @@ HsaProbe::HsaProbe(int gpu, int blocks, int slots, int spin_ticks)
     sym("gpumon_probe_reset.kd", &d_->reset, 12);
     // memory
     const hsa_amd_memory_pool_t host_fine = find_pool(a.cpu, HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED);
-    const hsa_amd_memory_pool_t kernarg = find_pool(a.cpu, HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT);
+    // Kernargs: every probe wave reads its 36-byte block. From the kernarg pool (fine-grained,
+    // not cached in L2) those reads cross to host memory from every CU: a 32 us kernel with a
+    // 28 us wave spread on MI355X. From coarse-grained system memory the first read per XCD fills
+    // its L2 (the dispatch's system-scope acquire invalidates it before each launch): 16 us and
+    // 6.6 us, as on the HIP path (profiles/r3_probe_hsa.md). GPUMON_PROBE_KERNARG=kernarg selects
+    // the kernarg pool; without a coarse-grained system pool it is used anyway.
+    hsa_amd_memory_pool_t kernarg{};
+    {
+      const char* k = getenv("GPUMON_PROBE_KERNARG");
+      bool coarse = !(k && !strcmp(k, "kernarg"));
+      if (coarse) {
+        try {
+          kernarg = find_pool(a.cpu, HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED);
+        } catch (const std::exception&) {
+          coarse = false;
+        }
+      }
+      if (!coarse) kernarg = find_pool(a.cpu, HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_KERNARG_INIT);
+    }
     const hsa_amd_memory_pool_t vram = find_pool(d_->gpu, HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED);
     const size_t ring_bytes = sizeof(gpumon_hip::ProbeRecord) * static_cast<size_t>(blocks_) * slots_;
     auto host_alloc = [&](hsa_amd_memory_pool_t pool, size_t bytes, void** p, const char* what) {

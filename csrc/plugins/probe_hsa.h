@@ -11,7 +11,8 @@
 // Memory: ring + arrival flags in fine-grained system memory (the CPU agent's fine-grained pool,
 // made accessible to the GPU), the self re-arming per-slot counters in the GPU's coarse-grained
 // VRAM pool (zeroed once by gpumon_probe_reset on the same queue: a copy engine or blit kernel
-// would bring up another queue), one kernarg block and one completion signal per slot.
+// would bring up another queue), one kernarg block per slot in coarse-grained system memory (cached
+// in L2 after the first read per XCD) and one completion signal per slot.
 #pragma once
 
 #include <cstdint>

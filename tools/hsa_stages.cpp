@@ -83,6 +83,24 @@ int main(int argc, char** argv) {
     fprintf(stderr, "no GPU agent\n");
     return 1;
   }
+  // the memory pools of both agents (segment / global flags / size), for the kernarg placement
+  for (int ai = 0; ai < 2; ++ai)
+    hsa_amd_agent_iterate_memory_pools(
+        agents[ai],
+        [](hsa_amd_memory_pool_t pool, void* d) {
+          hsa_amd_segment_t seg;
+          uint32_t flags = 0;
+          size_t size = 0;
+          bool alloc = false;
+          hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+          hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+          hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_SIZE, &size);
+          hsa_amd_memory_pool_get_info(pool, HSA_AMD_MEMORY_POOL_INFO_RUNTIME_ALLOC_ALLOWED, &alloc);
+          printf("{\"pool_of\": \"%s\", \"segment\": %d, \"global_flags\": %u, \"size_gb\": %.1f, \"alloc\": %d}\n",
+                 *static_cast<int*>(d) == 0 ? "gpu" : "cpu", static_cast<int>(seg), flags, size / 1e9, alloc ? 1 : 0);
+          return HSA_STATUS_SUCCESS;
+        },
+        &ai);
   hsa_code_object_reader_t rd;
   hsa_executable_t exe;
   CK(hsa_code_object_reader_create_from_memory(bytes.data(), bytes.size(), &rd));
