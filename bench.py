@@ -166,6 +166,8 @@ def main() -> int:
                          "so p99 / p99.9 rest on >= 20 / 2 samples above them)")
     ap.add_argument("--scrape-concurrency", type=int, default=2)
     ap.add_argument("--gzip", action="store_true", help="scrape with Accept-Encoding: gzip")
+    ap.add_argument("--scrape-path", default="/metrics",
+                    help="request target, e.g. '/metrics?include=node_gpu_*,pod_gpu_*' (a per-request family filter)")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--sample-threads", type=int, default=-1,
                     help="parallel per-GPU sampling threads (-1 = auto: one per GPU, 0 = sequential)")
@@ -264,7 +266,7 @@ def main() -> int:
         mon.wait_ticks(1, timeout_s=args.interval * 5 + 30)
         q0 = mon.ex.seq
         n0 = mon.ex.scrape_count()
-        r = core.scrape_load("127.0.0.1", mon.port, "/metrics", n_requests=0, duration_s=args.idle_s,
+        r = core.scrape_load("127.0.0.1", mon.port, args.scrape_path, n_requests=0, duration_s=args.idle_s,
                              concurrency=args.scrape_concurrency, rate_hz=args.scrape_rate, keep_alive=True,
                              gzip=args.gzip)
         q1 = mon.ex.seq
@@ -345,7 +347,7 @@ def main() -> int:
         duration = args.steps * args.interval
 
         def _scrape():
-            scrape_result.update(core.scrape_load("127.0.0.1", mon.port, "/metrics", n_requests=0,
+            scrape_result.update(core.scrape_load("127.0.0.1", mon.port, args.scrape_path, n_requests=0,
                                                   duration_s=duration, concurrency=args.scrape_concurrency,
                                                   rate_hz=args.scrape_rate, keep_alive=True, gzip=args.gzip))
 
@@ -509,6 +511,7 @@ def main() -> int:
             "scrape_max_ms": round(max(lat) * 1e3, 4) if lat else None,
             "scrapes": len(lat),
             "scrape_rate_hz": args.scrape_rate,
+            "scrape_path": args.scrape_path,
             # the exporter's own service time of the same requests (request parsed -> response
             # written), exact: client minus server = loopback + client scheduling
             "server_scrape_p50_ms": round(_pct(srv, 0.50) * 1e3, 4) if srv else None,
