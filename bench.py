@@ -154,6 +154,45 @@ def _link_map_check(n, seconds):
             "rates_within_15pct": sum(1 for r in rows if r["rate_within_15pct"])}
 
 
+def _capacity(backend, n, args, has_gpu):
+    """Sampler capacity (untimed, after the timed region, load still running): a second exporter on
+    the same devices at --capacity-interval (1 ms) for --capacity-s seconds. `value` is fixed by the
+    configured interval; this is how fast the sampler can go: ticks/s, samples/s/GPU, the share of
+    them that carried a new firmware table (gpu_metrics timestamp moved), overruns, tick quantiles."""
+    from gpumon.config import Config
+    from gpumon.monitor import GpuMonitor
+
+    cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi", "auto")) else [],
+                 interval=args.capacity_interval, listen="127.0.0.1:0", http_threads=1, host="bench-node",
+                 log_level="warn", fast_path=not args.no_fast_path, sample_threads=args.sample_threads,
+                 rt_priority=args.rt_priority)
+    mon = GpuMonitor(cfg, control_plane=False).start()
+    try:
+        if mon.start_error:
+            return {"error": mon.start_error}
+        mon.wait_ticks(20, timeout_s=30)  # first-tick setup (fd tables, link / RAS passes) stays out
+        s0, q0, t0 = mon.ex.self_stats(), mon.ex.seq, time.perf_counter()
+        time.sleep(args.capacity_s)
+        s1, q1, t1 = mon.ex.self_stats(), mon.ex.seq, time.perf_counter()
+        durs = [t["duration_s"] for t in mon.ex.tick_log() if q0 < t["seq"] <= q1]
+    finally:
+        mon.stop()
+    dt = t1 - t0
+    devs = max(1, len(s1.get("device_errors") or [0]))
+    samples = s1["samples"] - s0["samples"]
+    stale = s1.get("stale_samples", 0) - s0.get("stale_samples", 0)
+    return {"interval_ms": args.capacity_interval * 1e3, "seconds": round(dt, 3), "devices": devs,
+            "ticks_per_s": round((q1 - q0) / dt, 1),
+            "samples_per_sec_per_gpu": round(samples / dt / devs, 1),
+            # a sample whose firmware table timestamp did not move since the last tick is stale: the
+            # fresh rate is bounded by how often the SMU rewrites gpu_metrics, not by the exporter
+            "fresh_samples_per_sec_per_gpu": round((samples - stale) / dt / devs, 1) if has_gpu else None,
+            "overruns": s1["overruns"] - s0["overruns"],
+            "tick_p50_ms": round(_pct(durs, 0.50) * 1e3, 4) if durs else None,
+            "tick_p99_ms": round(_pct(durs, 0.99) * 1e3, 4) if durs else None,
+            "ticks_logged": len(durs)}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -190,6 +229,10 @@ def main() -> int:
     ap.add_argument("--dist", action="store_true",
                     help="initialise torch.distributed (RCCL) even with one rank: rehearses the torchrun path "
                          "(process group, barriers, MAX over ranks) on a 1-GPU box")
+    ap.add_argument("--capacity-s", type=float, default=2.0,
+                    help="untimed sampler-capacity run after the timed region (seconds; 0 = off)")
+    ap.add_argument("--capacity-interval", type=float, default=0.001,
+                    help="sampling interval of the capacity run (seconds)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -568,6 +611,11 @@ def main() -> int:
             except Exception as e:  # noqa: BLE001
                 lm = {"error": f"{type(e).__name__}: {e}"}
             result["xgmi"] = dict(result["xgmi"] or {}, link_map=lm)
+        if args.capacity_s > 0:
+            try:
+                result["capacity"] = _capacity(backend, n, args, has_gpu)
+            except Exception as e:  # noqa: BLE001
+                result["capacity"] = {"error": f"{type(e).__name__}: {e}"}
     if result is not None:  # the line is out before the teardown collectives can stall on a peer
         line = json.dumps(result)
         print(line, flush=True)

@@ -57,6 +57,10 @@ def test_bench_single_process(dist):
     assert d["server_scrapes"] == d["scrapes"] and 0 < d["server_scrape_p99_ms"] <= d["scrape_max_ms"] + 5.0
     assert "interval" in d["value_note"]
     assert idle["server_scrape_p99_ms"] > 0 and idle["scrape_p999_ms"] >= idle["scrape_p99_ms"]
+    # sampler capacity: a 1 ms-interval exporter after the timed region goes far past 1/interval
+    cap = d["capacity"]
+    assert "error" not in cap, cap
+    assert cap["interval_ms"] == 1.0 and cap["ticks_logged"] > 0 and cap["samples_per_sec_per_gpu"] > 100
 
 
 @pytest.mark.slow
