@@ -188,6 +188,11 @@ def _capacity(backend, n, args, has_gpu):
             # fresh rate is bounded by how often the SMU rewrites gpu_metrics, not by the exporter
             "fresh_samples_per_sec_per_gpu": round((samples - stale) / dt / devs, 1) if has_gpu else None,
             "overruns": s1["overruns"] - s0["overruns"],
+            # an overrun tick makes the sampler skip to the next interval boundary (deadline-based):
+            # the back-to-back bound of the sample -> export path is 1 / the mean tick (the
+            # post-publish gzip and maintenance run on the sampler thread too, outside the tick)
+            "tick_bound_hz": round(len(durs) / sum(durs), 1) if durs else None,
+            "tick_mean_ms": round(sum(durs) / len(durs) * 1e3, 4) if durs else None,
             "tick_p50_ms": round(_pct(durs, 0.50) * 1e3, 4) if durs else None,
             "tick_p99_ms": round(_pct(durs, 0.99) * 1e3, 4) if durs else None,
             "ticks_logged": len(durs)}
