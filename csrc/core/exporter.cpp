@@ -550,6 +550,11 @@ bool Exporter::start(std::string* err) {
       return false;
     }
   }
+  if (cfg_.interval_s > 0 && cfg_.interval_s < 0.02 && !starts_with(cfg_.backend, "mock"))
+    GPUMON_LOG(LogLevel::kWarn, "exporter",
+               "interval " + std::to_string(cfg_.interval_s * 1e3) +
+                   " ms is below the firmware's gpu_metrics refresh (20 ms on MI355X): faster samples repeat the "
+                   "last table (gpumon_stale_samples_total)");
   running_ = true;
   // First tick synchronously so /metrics is ready as soon as start() returns.
   tick();
