@@ -994,9 +994,11 @@ TickInfo Exporter::tick() {
     rates.resize(n);
     proc_counts.assign(n, 0);
     std::vector<DeviceSample> prev;
+    std::vector<DeviceRates> prev_rates;
     {
       std::lock_guard<std::mutex> g(state_mu_);
       prev = cur_;  // the previous tick's samples
+      prev_rates = rates_;
     }
     for (int i = 0; i < n; ++i) {
       DeviceSample& s = cur[i];
@@ -1053,7 +1055,12 @@ TickInfo Exporter::tick() {
           s.fresh = false;
           stale_++;
         }
-        compute_rates(p, s, cfg_.rates, &rates[i]);
+        // A repeated table (sampling faster than the firmware refresh) holds no new window: it
+        // keeps the rates of the last one instead of reporting zero power / traffic over it.
+        if (!s.fresh && i < static_cast<int>(prev_rates.size()))
+          rates[i] = prev_rates[i];
+        else
+          compute_rates(p, s, cfg_.rates, &rates[i]);
       }
       samples_++;
       if (!s.ok || s.errors) {  // partial failures (one call failed, others answered) count too

@@ -79,7 +79,7 @@ bool MockBackend::init(std::string* err) {
   xgmi_wr_.assign(n * kMaxLinks, 0);
   busy_acc_.assign(n * kMaxXcc, 0);
   lim_acc_.assign(n * kMaxXcc * 4, 0);
-  acc_counter_.assign(n, 0);
+  acc_counter_.assign(n, 100000);  // 1 s of firmware uptime: a live counter is never 0
   gfx_act_acc_.assign(n, 0);
   t0_ns_ = mono_ns();
   last_ns_.assign(n, t0_ns_);
@@ -235,14 +235,16 @@ void MockBackend::sample(int i, DeviceSample* out) {
   v[F_NUM_PARTITION] = 1;
   v[F_THROTTLE_STATUS] = 0;
 
-  // Advance accumulators by elapsed time since the previous sample of this device.
+  // Accumulators advance with the firmware's table time, in quanta of 1/firmware_hz (as on
+  // hardware: a read between two firmware refreshes returns the same accumulators), while the
+  // driver stamps system_clock_counter at the read itself.
   Accumulators& a = out->acc;
   a.valid = true;
   int64_t now = out->host_mono_ns;
-  double elapsed = std::max(0.0, (now - last_ns_[i]) * 1e-9);
-  last_ns_[i] = now;
-  // firmware time advances in quanta of 1/firmware_hz
   uint64_t fw_tick = static_cast<uint64_t>(t * cfg_.firmware_hz);
+  const int64_t fw_ns = t0_ns_ + static_cast<int64_t>(fw_tick / std::max(1e-3, cfg_.firmware_hz) * 1e9);
+  double elapsed = std::max(0.0, (fw_ns - last_ns_[i]) * 1e-9);
+  last_ns_[i] = std::max(last_ns_[i], fw_ns);
   a.firmware_ts = (fw_tick + 1) * static_cast<uint64_t>(1e8 / std::max(1e-3, cfg_.firmware_hz));
   a.system_clock_ns = static_cast<uint64_t>(now);
   energy_[i] += static_cast<uint64_t>(power * elapsed / 15.3e-6);

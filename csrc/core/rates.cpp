@@ -21,12 +21,21 @@ void compute_rates(const DeviceSample& prev, const DeviceSample& cur, const Rate
   if (!prev.ok || !cur.ok || !prev.acc.valid || !cur.acc.valid) return;
   const Accumulators& a = prev.acc;
   const Accumulators& b = cur.acc;
-  // Time base: driver-attached ns timestamp of the table when both reads have one, else host.
-  double dt = 0;
+  // Time base. The accumulators move only when the firmware rewrites its table (every 20 ms on
+  // MI355X, profiles/r3_capacity.md), while system_clock_counter is stamped by the driver at each
+  // read: a read-time dt is off by up to one firmware period per interval (+-2 % at 1 Hz, +-20 %
+  // at 10 Hz). The firmware's own timestamp (10 ns units) spans exactly the accumulated window;
+  // it is used when it advanced and agrees with the read-time dt to within a factor of two.
+  double dt_read = 0;
   if (a.system_clock_ns && b.system_clock_ns && b.system_clock_ns > a.system_clock_ns)
-    dt = (b.system_clock_ns - a.system_clock_ns) * 1e-9;
+    dt_read = (b.system_clock_ns - a.system_clock_ns) * 1e-9;
   else if (cur.host_mono_ns > prev.host_mono_ns)
-    dt = (cur.host_mono_ns - prev.host_mono_ns) * 1e-9;
+    dt_read = (cur.host_mono_ns - prev.host_mono_ns) * 1e-9;
+  double dt = dt_read;
+  if (a.firmware_ts && b.firmware_ts > a.firmware_ts) {
+    const double dt_fw = (b.firmware_ts - a.firmware_ts) * 1e-8;
+    if (dt_read <= 0 || (dt_fw >= 0.5 * dt_read - 0.05 && dt_fw <= 2.0 * dt_read + 0.05)) dt = dt_fw;
+  }
   if (dt <= 0) return;
   out->valid = true;
   out->dt_s = dt;

@@ -7,6 +7,7 @@ probes, resources or ports and mounted the host docker socket; these tests pin t
 import json
 import os
 import re
+import time
 
 import pytest
 import yaml
@@ -83,6 +84,7 @@ def test_dashboard_queries_resolve_against_exposition(mock_exporter):
     ex.mock_set_procs([{"pid": os.getpid(), "device": 1, "name": "python3"}])
     ex.mock_set_occ_series(1, [100.0])
     ex.set_device_mfma_util({1: 50.0})  # what the PMC sampler publishes (pod_gpu_mfma_util_percent)
+    time.sleep(0.05)  # past one firmware refresh (20 ms): interval rates need a new table
     ex.tick()
     fam = promtext.parse(ex.metrics_text())
     produced = set()

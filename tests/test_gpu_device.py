@@ -72,6 +72,34 @@ def test_amdsmi_static_and_sample_sane(core, torch_gpu):
         ex.stop()
 
 
+def test_firmware_timestamp_is_the_rate_time_base(core, torch_gpu):
+    """gpu_metrics' firmware_timestamp counts 10 ns and advances only when the SMU rewrites the
+    table (every 20 ms on MI355X), while system_clock_counter is stamped by the driver at each read.
+    Rates divide by the firmware delta (csrc/core/rates.cpp), so its unit is pinned here against the
+    driver clock over ~1 s, and a back-to-back read returns the same table (stale, rates kept)."""
+    ex = _exporter(core)
+    try:
+        ex.tick()
+        a = ex.samples()[0]["acc"]
+        time.sleep(1.0)
+        ex.tick()
+        b = ex.samples()[0]["acc"]
+        d_fw = (b["firmware_ts"] - a["firmware_ts"]) * 1e-8
+        d_sys = (b["system_clock_ns"] - a["system_clock_ns"]) * 1e-9
+        assert d_sys > 0.9 and d_fw == pytest.approx(d_sys, abs=0.045)  # within two firmware periods
+        r = ex.rates()[0]
+        assert r["valid"] and r["dt_s"] == pytest.approx(d_fw, rel=1e-9)
+        assert 50 < r["power_from_energy_w"] < 1500
+        p = r["power_from_energy_w"]
+        ex.tick()  # back to back, well inside one firmware period: most often the same table
+        s = ex.samples()[0]
+        if not s["fresh"]:
+            assert s["acc"]["firmware_ts"] == b["firmware_ts"]
+            assert ex.rates()[0]["power_from_energy_w"] == pytest.approx(p)
+    finally:
+        ex.stop()
+
+
 def test_rocm_smi_backend_agrees_with_amdsmi(core, torch_gpu):
     """The rocm_smi_lib fallback reads the same firmware table: same device (matched by BDF),
     same VRAM size, 8 XCDs, 7 up xGMI links, sane temperature."""

@@ -73,6 +73,27 @@ def test_intermittent_failure_recovers(mock_exporter):
     assert oks.count(True) == 3 and oks.count(False) == 3
 
 
+def test_rates_span_the_firmware_window_and_survive_a_repeated_table(mock_exporter):
+    """The accumulators move only when the firmware rewrites its table (50 Hz on MI355X,
+    profiles/r3_capacity.md); the driver stamps system_clock_counter at each read. Rates divide by
+    the firmware timestamp's delta (whole refresh periods here), and a repeated table keeps the last
+    window's rates instead of reporting 0 W over it."""
+    ex = mock_exporter(backend="mock:gpus=1,mode=load,firmware_hz=20")  # a 50 ms firmware period
+    time.sleep(0.13)
+    ex.tick()
+    r = ex.rates()[0]
+    assert r["valid"]
+    periods = r["dt_s"] / 0.05
+    assert periods == pytest.approx(round(periods), abs=1e-6) and round(periods) >= 2  # not the host's 0.13 s
+    assert r["power_from_energy_w"] == pytest.approx(ex.samples()[0]["fields"]["power_cur"], rel=1e-3)
+    ex.tick()  # back to back: the same table
+    assert not ex.samples()[0]["fresh"]
+    r2 = ex.rates()[0]
+    assert r2["valid"] and r2["power_from_energy_w"] == pytest.approx(r["power_from_energy_w"])
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_power_interval_watts") == pytest.approx(r["power_from_energy_w"], rel=1e-6)
+
+
 def test_stale_firmware_table_detected(mock_exporter):
     ex = mock_exporter(backend="mock:gpus=1,firmware_hz=0.5")
     ex.tick()
