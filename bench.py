@@ -165,7 +165,7 @@ def _capacity(backend, n, args, has_gpu):
     cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi", "auto")) else [],
                  interval=args.capacity_interval, listen="127.0.0.1:0", http_threads=1, host="bench-node",
                  log_level="warn", fast_path=not args.no_fast_path, sample_threads=args.sample_threads,
-                 rt_priority=args.rt_priority)
+                 rt_priority=args.rt_priority, prewarm_ms=args.prewarm_ms)
     mon = GpuMonitor(cfg, control_plane=False).start()
     try:
         if mon.start_error:
@@ -234,6 +234,8 @@ def main() -> int:
     ap.add_argument("--dist", action="store_true",
                     help="initialise torch.distributed (RCCL) even with one rank: rehearses the torchrun path "
                          "(process group, barriers, MAX over ranks) on a 1-GPU box")
+    ap.add_argument("--prewarm-ms", type=float, default=3.0,
+                    help="device workers warm the firmware-table path this long before each tick (0 = off)")
     ap.add_argument("--capacity-s", type=float, default=2.0,
                     help="untimed sampler-capacity run after the timed region (seconds; 0 = off)")
     ap.add_argument("--capacity-interval", type=float, default=0.001,
@@ -296,7 +298,7 @@ def main() -> int:
         cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi", "auto")) else [],
                      interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
                      enable_probe=args.probe and has_gpu, log_level="warn", fast_path=not args.no_fast_path,
-                     sample_threads=args.sample_threads, rt_priority=args.rt_priority)
+                     sample_threads=args.sample_threads, rt_priority=args.rt_priority, prewarm_ms=args.prewarm_ms)
         mon = GpuMonitor(cfg, control_plane=False).start()
         if mon.start_error:
             raise SystemExit(f"exporter backend failed: {mon.start_error}")
@@ -586,6 +588,7 @@ def main() -> int:
             "tick_quantiles": "exact over the timed ticks (exporter tick log); times in ms",
             "overruns": s1["overruns"] - s0["overruns"],
             "sampler_rt_threads": s1.get("rt_threads", 0),
+            "prewarm_ms": args.prewarm_ms,
             # the exporter's own threads over the timed region, serving the scrape load too (1/100 s ticks)
             "exporter_cpu_millicores": round(1000.0 * (cpu1 - cpu0) / elapsed, 2),
             "backend_call_us": {k: round((v["seconds"] - s0["backend_calls"].get(k, {}).get("seconds", 0.0)) * 1e6

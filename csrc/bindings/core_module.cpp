@@ -89,6 +89,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "ras_slices", &c.ras_slices);
   get(d, "ras_async", &c.ras_async);
   get(d, "occ_samples", &c.occ_samples);
+  get(d, "prewarm_ms", &c.prewarm_ms);
   get(d, "hide_empty_contexts", &c.hide_empty_contexts);
   get(d, "mfma_exclusive_window_s", &c.mfma_exclusive_window_s);
   get(d, "sample_threads", &c.sample_threads);
@@ -949,6 +950,7 @@ PYBIND11_MODULE(_core, m) {
       .def("mock_set_xgmi",
            [](Exporter& e, int dev, int link, double gbps) { mock_of(e)->set_xgmi(dev, link, gbps); })
       .def("mock_calls", [](Exporter& e, int dev) { return mock_of(e)->calls(dev); })
+      .def("mock_prewarms", [](Exporter& e, int dev) { return mock_of(e)->prewarms(dev); })
       .def("mock_set_link_up",
            [](Exporter& e, int dev, int link, bool up) { mock_of(e)->set_link_up(dev, link, up); })
       .def("mock_link_calls", [](Exporter& e, int dev) { return mock_of(e)->link_calls(dev); })

@@ -616,6 +616,10 @@ void AmdSmiBackend::maintain(int i) {
   if (i >= 0 && i < static_cast<int>(fast_.size()) && fast_[i]) fast_[i]->maintain();
 }
 
+bool AmdSmiBackend::prewarm(int i) {
+  return i >= 0 && i < static_cast<int>(fast_.size()) && fast_[i] && fast_[i]->prewarm();
+}
+
 bool AmdSmiBackend::supports_occupancy(int i) const {
   return i >= 0 && i < static_cast<int>(fast_.size()) && fast_[i] && fast_[i]->have_kfd();
 }

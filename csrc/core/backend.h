@@ -61,6 +61,11 @@ class Backend {
   // Upkeep that must stay off the tick's critical path (the device worker calls it after it
   // published the tick's sample): e.g. refreshing cached /proc fd tables.
   virtual void maintain(int /*i*/) {}
+  // Wake the device's firmware-table path a few ms before a tick (the device worker calls it at
+  // deadline - prewarm_ms): on MI355X a gpu_metrics fetch costs ~50 us when the SMU served one
+  // within ~5 ms and 150-300 us after a longer gap; spinning the CPU instead does not help
+  // (profiles/r3_capacity.md). Returns false where the backend has nothing to warm.
+  virtual bool prewarm(int /*i*/) { return false; }
   // Restrict to a subset of device hip_ids (empty = all). Applied at init().
   void set_device_filter(const std::vector<int>& ids) { filter_ = ids; }
 
@@ -174,6 +179,8 @@ class MockBackend : public Backend {
   uint64_t link_calls(int dev) const;            // sample_links() calls (link-metrics refreshes)
   void set_link_fail(int dev, bool fail);        // link-metrics reads of `dev` fail (links_read -1)
   uint64_t calls(int dev) const;
+  bool prewarm(int i) override;
+  uint64_t prewarms(int dev) const;  // prewarm() calls
 
  private:
   MockConfig cfg_;
@@ -187,7 +194,7 @@ class MockBackend : public Backend {
   std::vector<char> link_down_;      // per dev * kMaxLinks
   std::vector<uint64_t> link_calls_;
   std::vector<char> link_fail_;
-  std::vector<uint64_t> calls_;
+  std::vector<uint64_t> calls_, prewarms_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
   std::vector<uint64_t> lim_acc_;  // per device x XCC x {ppt, thermal, any, low-util}
   std::vector<RasSample> ras_;     // per device (mock RAS state)
@@ -222,6 +229,7 @@ class AmdSmiBackend : public Backend {
   bool concurrent_processes(int i) const override { return supports_occupancy(i); }
   void set_tick_occupancy(bool on) override { tick_occupancy_ = on; }
   void maintain(int i) override;                   // fast path: due /proc fd-table refreshes
+  bool prewarm(int i) override;                    // fast path: one throwaway gpu_metrics pread
   void occupancy(int i, const std::vector<uint32_t>& pids, std::vector<double>* out) override;
   bool occupancy_scan(int i, std::vector<OccRead>* out) override;
   std::string lib_version() const { return lib_version_; }

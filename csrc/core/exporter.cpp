@@ -85,7 +85,8 @@ static bool apply_rt(int prio, const std::string& who, std::atomic<int>* rt) {
 static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_ptr<Exporter::DoneSignal> sig,
                             Backend* backend, int i, int64_t occ_period_ns,
                             std::shared_ptr<std::atomic<uint64_t>> occ_reads, int rt_prio,
-                            std::shared_ptr<std::atomic<int>> rt_threads) {
+                            std::shared_ptr<std::atomic<int>> rt_threads,
+                            std::shared_ptr<std::atomic<int64_t>> next_tick, int64_t prewarm_ns) {
   set_thread_name("gpumon-dev" + std::to_string(i));
   const bool rt = apply_rt(rt_prio, "device worker", rt_threads.get());
   struct RtCount {  // the gauge counts live threads
@@ -111,6 +112,10 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
   constexpr int kScanEvery = 4;
   uint64_t n_sub = 0;
   int64_t next_occ = 0;
+  // Prewarm: one throwaway firmware-table read prewarm_ns before each tick's deadline, so the
+  // tick's own read finds the SMU's fetch path awake (~50 us instead of 150-300 us after a long
+  // gap, profiles/r3_capacity.md). Once per deadline; skipped when the deadline is already close.
+  int64_t warmed_for = 0;
   // The process list (KFD + fdinfo reads, ~0.1 ms) runs on a second thread while this one reads
   // the firmware table (~0.2 ms, mostly the SMU fetch): the device's part of a tick becomes the
   // longer of the two instead of their sum. Only where the backend allows it (sysfs fast path).
@@ -170,22 +175,46 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
     int ras_slice, ras_n;
     {
       std::unique_lock<std::mutex> lk(w->mu);
-      bool subsample = false;
+      bool subsample = false, warm = false;
       while (!w->quit && !w->pending) {
-        if (!occ_on || (occ_pids.empty() && !scan_ok)) {
+        const int64_t now = mono_ns();
+        int64_t wake = INT64_MAX;
+        if (prewarm_ns > 0) {
+          const int64_t nt = next_tick->load(std::memory_order_acquire);
+          if (nt > 0 && nt != warmed_for) {
+            if (now >= nt - prewarm_ns) {
+              warmed_for = nt;
+              if (now < nt - prewarm_ns / 4) {  // not when the tick is about to sample anyway
+                warm = true;
+                break;
+              }
+            } else {
+              wake = nt - prewarm_ns;
+            }
+          }
+        }
+        if (occ_on && !(occ_pids.empty() && !scan_ok)) {
+          if (next_occ <= now) {
+            subsample = true;
+            break;
+          }
+          wake = std::min(wake, next_occ);
+        }
+        if (wake == INT64_MAX) {
           w->cv.wait(lk);
           continue;
         }
-        const int64_t left = next_occ - mono_ns();
-        if (left <= 0) {
-          subsample = true;
-          break;
-        }
         // system_clock slices checked against the monotonic deadline (TSan: see sample_devices)
         w->cv.wait_until(lk, std::chrono::system_clock::now() +
-                                 std::chrono::nanoseconds(std::min<int64_t>(left, 20'000'000)));
+                                 std::chrono::nanoseconds(std::min<int64_t>(wake - now, 20'000'000)));
       }
       if (w->quit) return;
+      if (warm) {
+        lk.unlock();
+        TraceRange tr("gpumon.prewarm");
+        backend->prewarm(i);
+        continue;
+      }
       if (subsample) {
         lk.unlock();
         const bool scan_turn = scan_ok && (n_sub++ % kScanEvery == 0);
@@ -337,8 +366,12 @@ void Exporter::start_workers(int n) {
     // the workers' sub-samples stand in for the tick's own cu_occupancy read (the costliest
     // per-process file: ~27 us, a KFD walk over the process's queues)
     if (i == 0) backend_->set_tick_occupancy(occ_ns == 0 || !backend_->supports_occupancy(i));
+    // prewarm only where ticks are far enough apart for the fetch path to cool (>= 10 ms gaps)
+    const int64_t prewarm_ns = cfg_.interval_s >= 0.02 && cfg_.prewarm_ms > 0
+                                   ? static_cast<int64_t>(std::min(cfg_.prewarm_ms, cfg_.interval_s * 250.0) * 1e6)
+                                   : 0;
     w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i, occ_ns, occ_reads_, cfg_.rt_priority,
-                        rt_threads_);
+                        rt_threads_, next_tick_ns_, prewarm_ns);
     workers_.push_back(std::move(w));
   }
 }
@@ -611,6 +644,7 @@ void Exporter::sampler_loop() {
   const bool rt = apply_rt(cfg_.rt_priority, "sampler", rt_threads_.get());
   const int64_t period = static_cast<int64_t>(cfg_.interval_s * 1e9);
   int64_t next = mono_ns() + period;
+  next_tick_ns_->store(next, std::memory_order_release);
   while (running_) {
     int64_t now = mono_ns();
     if (now < next) {
@@ -620,6 +654,7 @@ void Exporter::sampler_loop() {
       continue;
     }
     tick_deadline_ns_ = next;
+    next_tick_ns_->store(next + period, std::memory_order_release);
     tick();
     tick_deadline_ns_ = 0;
     next += period;
@@ -629,8 +664,10 @@ void Exporter::sampler_loop() {
       int64_t missed = (after - next) / period + 1;
       overruns_ += static_cast<uint64_t>(missed);
       next += missed * period;
+      next_tick_ns_->store(next, std::memory_order_release);
     }
   }
+  next_tick_ns_->store(0, std::memory_order_release);
   if (rt) rt_threads_->fetch_sub(1);
 }
 

@@ -67,6 +67,7 @@ struct ExporterConfig {
   // it keeps the tick on its deadline. Needs CAP_SYS_NICE (the privileged DaemonSet has it);
   // without it the threads stay normal and gpumon_sampler_rt_threads says so.
   int rt_priority = 0;
+  double prewarm_ms = 3.0;            // device workers warm the firmware-table path this long before each tick (0 = off)
   int occ_samples = 20;               // KFD cu_occupancy reads per process per tick on the device workers (1 = the tick's own)
   bool hide_empty_contexts = true;    // no pod_gpu row for a process with a GPU context but no VRAM and no waves
   // pod_gpu_mfma_util_percent needs exclusive use: no OTHER process's waves seen on the device in
@@ -306,6 +307,9 @@ class Exporter {
   std::shared_ptr<std::atomic<uint64_t>> occ_reads_ = std::make_shared<std::atomic<uint64_t>>(0);
   std::shared_ptr<std::atomic<int>> rt_threads_ = std::make_shared<std::atomic<int>>(0);  // SCHED_FIFO now
   std::atomic<int64_t> tick_deadline_ns_{0};  // deadline of the tick the sampler loop is running
+  // deadline of the sampler's next tick (0: none scheduled), set before the current tick runs so a
+  // device worker that finished its part already sees it: the workers' prewarm clock
+  std::shared_ptr<std::atomic<int64_t>> next_tick_ns_ = std::make_shared<std::atomic<int64_t>>(0);
   std::shared_ptr<DoneSignal> done_sig_;
   uint64_t tick_id_ = 0;
   std::vector<uint64_t> dev_timeouts_;  // guarded by state_mu_

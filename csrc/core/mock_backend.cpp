@@ -74,6 +74,7 @@ bool MockBackend::init(std::string* err) {
   link_calls_.assign(n, 0);
   link_fail_.assign(n, 0);
   calls_.assign(n, 0);
+  prewarms_.assign(n, 0);
   energy_.assign(n, 1000000);
   xgmi_rd_.assign(n * kMaxLinks, 0);
   xgmi_wr_.assign(n * kMaxLinks, 0);
@@ -168,6 +169,16 @@ void MockBackend::set_link_up(int dev, int link, bool up) {
 uint64_t MockBackend::link_calls(int dev) const {
   std::lock_guard<std::mutex> g(mu_);
   return dev >= 0 && dev < static_cast<int>(link_calls_.size()) ? link_calls_[dev] : 0;
+}
+bool MockBackend::prewarm(int i) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (i < 0 || i >= static_cast<int>(prewarms_.size())) return false;
+  prewarms_[i]++;
+  return true;
+}
+uint64_t MockBackend::prewarms(int dev) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return dev >= 0 && dev < static_cast<int>(prewarms_.size()) ? prewarms_[dev] : 0;
 }
 uint64_t MockBackend::calls(int dev) const {
   std::lock_guard<std::mutex> g(mu_);

@@ -225,6 +225,7 @@ const std::map<std::string, Setter>& setters() {
       {"ras_slices", int_at([](NativeOptions* o) { return &o->cfg.ras_slices; })},
       {"ras_async", bool_at([](NativeOptions* o) { return &o->cfg.ras_async; })},
       {"occ_samples", int_at([](NativeOptions* o) { return &o->cfg.occ_samples; })},
+      {"prewarm_ms", dbl_at([](NativeOptions* o) { return &o->cfg.prewarm_ms; })},
       {"hide_empty_contexts", bool_at([](NativeOptions* o) { return &o->cfg.hide_empty_contexts; })},
       {"mfma_exclusive_window_s", dbl_at([](NativeOptions* o) { return &o->cfg.mfma_exclusive_window_s; })},
       {"sample_threads", int_at([](NativeOptions* o) { return &o->cfg.sample_threads; })},
@@ -502,6 +503,7 @@ std::string options_json(const NativeOptions& o) {
   N("ras_slices", c.ras_slices);
   B("ras_async", c.ras_async);
   N("occ_samples", c.occ_samples);
+  N("prewarm_ms", c.prewarm_ms);
   B("hide_empty_contexts", c.hide_empty_contexts);
   N("mfma_exclusive_window_s", c.mfma_exclusive_window_s);
   N("sample_threads", c.sample_threads);

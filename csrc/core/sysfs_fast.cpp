@@ -92,6 +92,11 @@ bool SysfsGpu::open(const std::string& sys_root, const std::string& proc_root, c
   return true;
 }
 
+bool SysfsGpu::prewarm() {
+  alignas(8) unsigned char buf[4096];
+  return fd_metrics_ >= 0 && pread_all(fd_metrics_, buf, sizeof buf) > 0;
+}
+
 bool SysfsGpu::read_metrics(kgm::V18* out, std::string* why) {
   alignas(8) unsigned char buf[4096];
   ssize_t n = pread_all(fd_metrics_, buf, sizeof buf);

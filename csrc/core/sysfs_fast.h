@@ -205,6 +205,8 @@ class SysfsGpu {
   bool have_kfd() const { return kfd_gpu_id_ != 0; }
   // Off-tick upkeep (device worker, after it published): refreshes due /proc/<pid>/fd scans.
   void maintain();
+  // One gpu_metrics read whose table is discarded: leaves the SMU's fetch path warm for the tick.
+  bool prewarm();
 
  private:
   void fdinfo_usage(uint32_t pid, ProcSample* p);

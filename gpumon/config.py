@@ -44,6 +44,7 @@ class Config:
     hide_empty_contexts: bool = True      # no pod_gpu row for a GPU context with no VRAM and no waves
     mfma_exclusive_window_s: float = 5.0  # pod MFMA util only when no other process had waves in the last 5 ticks and this many seconds
     occ_samples: int = 20                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
+    prewarm_ms: float = 3.0               # device workers wake the firmware-table path this long before each tick (0 = off)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
     rt_priority: int = 0                  # SCHED_FIFO priority of the sampler + device workers (needs CAP_SYS_NICE)
     device_timeout_s: float = 2.0         # a device call still running after this is exported as hung
@@ -142,6 +143,7 @@ class Config:
             "ras_slices": int(self.ras_slices),
             "ras_async": bool(self.ras_async),
             "occ_samples": int(self.occ_samples),
+            "prewarm_ms": float(self.prewarm_ms),
             "hide_empty_contexts": bool(self.hide_empty_contexts),
             "mfma_exclusive_window_s": float(self.mfma_exclusive_window_s),
             "sample_threads": int(self.sample_threads),

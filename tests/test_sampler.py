@@ -339,3 +339,19 @@ def test_rt_priority_for_sampler_and_device_workers(core):
     finally:
         ex.stop()
     assert ex.self_stats()["rt_threads"] == 0
+
+
+def test_device_workers_prewarm_once_per_tick(mock_exporter):
+    """prewarm_ms: each device worker issues one throwaway firmware-table read that long before
+    every tick's deadline (the SMU fetch is ~3x cheaper warm, profiles/r3_capacity.md); none with
+    prewarm off, and none at intervals under 20 ms where the fetch path never cools."""
+    ex = mock_exporter(backend="mock:gpus=2,mode=idle", interval_s=0.1, prewarm_ms=20.0, sample_threads=-1)
+    time.sleep(0.7)
+    ticks = ex.self_stats()["ticks"]
+    for d in (0, 1):
+        w = ex.mock_prewarms(d)
+        assert ticks - 3 <= w <= ticks + 1, (d, w, ticks)
+    off = mock_exporter(backend="mock:gpus=1,mode=idle", interval_s=0.1, prewarm_ms=0.0, sample_threads=-1)
+    fast = mock_exporter(backend="mock:gpus=1,mode=idle", interval_s=0.01, prewarm_ms=3.0, sample_threads=-1)
+    time.sleep(0.5)
+    assert off.mock_prewarms(0) == 0 and fast.mock_prewarms(0) == 0
