@@ -306,6 +306,9 @@ class Exporter {
   // cu_occupancy sub-sample reads by the workers (shared: a detached worker may outlive a restart)
   std::shared_ptr<std::atomic<uint64_t>> occ_reads_ = std::make_shared<std::atomic<uint64_t>>(0);
   std::shared_ptr<std::atomic<int>> rt_threads_ = std::make_shared<std::atomic<int>>(0);  // SCHED_FIFO now
+  mutable std::mutex proc_stats_mu_;  // /proc/self figures, refreshed after each tick's publish
+  mutable SelfStats proc_stats_;
+  mutable bool proc_stats_valid_ = false;
   std::atomic<int64_t> tick_deadline_ns_{0};  // deadline of the tick the sampler loop is running
   // deadline of the sampler's next tick (0: none scheduled), set before the current tick runs so a
   // device worker that finished its part already sees it: the workers' prewarm clock

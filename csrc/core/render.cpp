@@ -35,6 +35,17 @@ void append_double(double v, std::string* out) {
 }
 
 void escape_label_value(const std::string& v, std::string* out) {
+  // fast path: most values (ids, BDFs, sensor names, pod names) need no escaping
+  bool plain = true;
+  for (char c : v)
+    if (c == '\\' || c == '"' || c == '\n') {
+      plain = false;
+      break;
+    }
+  if (plain) {
+    out->append(v);
+    return;
+  }
   for (char c : v) {
     switch (c) {
       case '\\': out->append("\\\\"); break;
