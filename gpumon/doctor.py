@@ -47,11 +47,61 @@ def _rt_permitted() -> tuple:
     return OK, "SCHED_FIFO permitted: rt_priority keeps ticks on their deadline"
 
 
+def firmware_table_check(path: str, interval_s: float, prewarm_ms: float, seconds: float = 0.25) -> tuple:
+    """(status, detail) for one GPU's gpu_metrics file: how often the SMU rewrites it (a new
+    firmware_timestamp, v1.8 offset 288; the driver stamps system_clock at every read, so raw bytes
+    always differ) against the sampling interval, and what a read costs cold (after 100 ms) vs 3 ms
+    after another read -- the gain prewarm_ms buys (profiles/r3_capacity.md)."""
+    import struct
+
+    try:
+        fd = os.open(path, os.O_RDONLY)
+    except OSError as e:
+        return WARN, f"{path}: {e.strerror}"
+    try:
+        b = os.pread(fd, 65536, 0)
+        if len(b) < 296 or (b[2], b[3]) != (1, 8):
+            return SKIP, f"gpu_metrics v{b[2] if len(b) > 2 else '?'}.{b[3] if len(b) > 3 else '?'}: cadence not decoded"
+        last, seen, t_end = struct.unpack_from("<Q", b, 288)[0], 0, time.perf_counter() + seconds
+        first_t = last_t = None
+        while time.perf_counter() < t_end:
+            fw = struct.unpack_from("<Q", os.pread(fd, 65536, 0), 288)[0]
+            if fw != last:
+                last, seen = fw, seen + 1
+                last_t = time.perf_counter()
+                first_t = first_t or last_t
+        period = (last_t - first_t) / (seen - 1) if seen > 1 else None
+
+        def read_after(gap_s, prefetch):
+            lat = []
+            for _ in range(5):
+                time.sleep(gap_s)
+                if prefetch:
+                    os.pread(fd, 65536, 0)
+                    time.sleep(0.003)
+                t0 = time.perf_counter()
+                os.pread(fd, 65536, 0)
+                lat.append(time.perf_counter() - t0)
+            return sorted(lat)[2] * 1e6
+
+        cold, warm = read_after(0.1, False), read_after(0.1, True)
+    finally:
+        os.close(fd)
+    if period is None:
+        return WARN, f"the firmware table did not advance in {seconds:.2f} s"
+    detail = (f"rewritten every {period * 1e3:.1f} ms ({1 / period:.0f} Hz); a read costs {cold:.0f} us cold, "
+              f"{warm:.0f} us 3 ms after another (prewarm_ms {prewarm_ms:g})")
+    if 0 < interval_s < period * 0.95:
+        return WARN, detail + f": interval {interval_s * 1e3:g} ms is shorter, so some samples repeat a table"
+    return OK, detail
+
+
 def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
     """[(check, status, detail)] for the node this runs on, with the exporter configured as `cfg`."""
     from .monitor import GpuMonitor
 
     out = []
+    interval_s = cfg.interval  # as configured (the checks below tick by hand)
     cfg.interval = 0
     cfg.listen = "127.0.0.1:0"
     cfg.enable_pmc = cfg.enable_probe = False  # the on-device check below runs them explicitly
@@ -74,6 +124,11 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
             out.append(("sysfs fast path", OK if fp == len(statics) else WARN,
                         f"{fp}/{len(statics)} GPU(s) ({st.get('fast_path_status', '')})"
                         + ("" if fp == len(statics) else ": the rest goes through libamd_smi (about 2x the tick time)")))
+        if statics and statics[0].get("bdf") and os.path.exists(f"/sys/bus/pci/devices/{statics[0]['bdf']}/gpu_metrics"):
+            out.append(("firmware table",) + firmware_table_check(
+                f"/sys/bus/pci/devices/{statics[0]['bdf']}/gpu_metrics", interval_s, cfg.prewarm_ms))
+        else:
+            out.append(("firmware table", SKIP, "no gpu_metrics file for the first GPU"))
         kfd = "/sys/class/kfd/kfd/proc"
         out.append(("KFD process table", OK if os.access(kfd, os.R_OK) else WARN,
                     f"{kfd} readable" if os.access(kfd, os.R_OK)

@@ -105,3 +105,50 @@ def test_doctor_checks_the_kubelet_files_when_configured(tmp_path):
                  log_level="error")
     checks = _by_name(doctor.run(cfg, wait_s=1))
     assert checks["kubelet log tree"][0] == "skip"
+
+
+def _fake_gpu_metrics(path, period_s, stop):
+    """A v1.8-shaped table file whose firmware_timestamp (offset 288) a thread bumps every period."""
+    import struct
+    import threading
+
+    buf = bytearray(3872)
+    struct.pack_into("<HBB", buf, 0, 3872, 1, 8)
+    path.write_bytes(bytes(buf))
+
+    def bump():
+        fw = 1
+        with open(path, "r+b") as fh:
+            while not stop.is_set():
+                fw += int(period_s * 1e8)
+                fh.seek(288)
+                fh.write(struct.pack("<Q", fw))
+                fh.flush()
+                stop.wait(period_s)
+
+    t = threading.Thread(target=bump, daemon=True)
+    t.start()
+    return t
+
+
+def test_doctor_firmware_table_cadence_against_the_interval(tmp_path):
+    """The SMU rewrites gpu_metrics every 20 ms on MI355X: doctor reports the period it measures and
+    warns when the configured interval is shorter (those samples repeat a table)."""
+    import re
+    import threading
+
+    from gpumon.doctor import OK, WARN, firmware_table_check
+
+    stop = threading.Event()
+    f = tmp_path / "gpu_metrics"
+    t = _fake_gpu_metrics(f, 0.02, stop)
+    try:
+        st, detail = firmware_table_check(str(f), 1.0, 3.0, seconds=0.3)
+        assert st == OK, detail
+        period = float(re.search(r"every ([0-9.]+) ms", detail).group(1))
+        assert 15 <= period <= 35, detail
+        st, detail = firmware_table_check(str(f), 0.005, 3.0, seconds=0.3)
+        assert st == WARN and "interval 5 ms is shorter" in detail, detail
+    finally:
+        stop.set()
+        t.join()

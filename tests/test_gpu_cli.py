@@ -203,3 +203,20 @@ def test_native_exporter_reports_a_separate_tenant_process():
     assert busy[hot[0]] > 60, (occ, busy)
     assert promtext.one(fam, "gpu_cu_occupancy_percent", gpu_id="0") > 60
     assert promtext.one(fam, "gpumon_occupancy_reads_total") > 0
+
+
+def test_doctor_on_mi355x_reports_the_firmware_cadence():
+    """gpumon doctor on the box: backend up, sysfs fast path, and the firmware table rewritten every
+    ~20 ms (profiles/r3_capacity.md) with a cheaper read after a prewarm."""
+    import re
+
+    r = subprocess.run([sys.executable, "-m", "gpumon", "doctor", "--backend", "amdsmi", "--devices", "0",
+                        "--format", "json"], capture_output=True, text=True, timeout=180, cwd=ROOT)
+    checks = {c["check"]: c for c in json.loads(r.stdout)}
+    assert checks["device backend"]["status"] == "ok", checks
+    fw = checks["firmware table"]
+    assert fw["status"] == "ok", fw
+    period = float(re.search(r"every ([0-9.]+) ms", fw["detail"]).group(1))
+    assert 15 <= period <= 25, fw
+    cold, warm = map(float, re.search(r"costs ([0-9.]+) us cold, ([0-9.]+) us", fw["detail"]).groups())
+    assert warm < cold, fw
