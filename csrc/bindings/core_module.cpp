@@ -642,6 +642,8 @@ PYBIND11_MODULE(_core, m) {
         return d;
       },
       "node-wide /proc/<pid>/fd scan cache of the sysfs fast path (scans so far, cached processes)");
+  m.def("fd_table_scans_of", [](const std::string& pdir) { return gpumon::DrmFdTables::get().scans_of(pdir); },
+        py::arg("pdir"), "scans of one /proc/<pid> entry of the fd-table cache (0 when not cached)");
   m.def("fd_table_clear", [] { gpumon::DrmFdTables::get().clear(); },
         "drop every cached fd table (tests: entries of an earlier test's fake /proc tree)");
   m.def("gzip", [](const std::string& s) {

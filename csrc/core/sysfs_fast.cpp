@@ -167,6 +167,7 @@ void DrmFdTables::fds_for(const std::string& pdir, const std::string& render, st
     scans_++;
     lk.lock();
     Entry& e = m_[pdir];
+    e.scans++;
     e.fds = std::move(fds);
     e.scanned_ns = e.used_ns = now;
     e.scanning = false;
@@ -216,6 +217,7 @@ int DrmFdTables::refresh_due(int max_scans) {
     std::lock_guard<std::mutex> g(mu_);
     auto it = m_.find(pdir);
     if (it == m_.end()) continue;
+    it->second.scans++;
     it->second.fds = std::move(fds);
     it->second.scanned_ns = mono_ns();
   }
@@ -236,6 +238,12 @@ void DrmFdTables::retain(const std::string& proc_root, const std::vector<uint32_
     }
     ++it;
   }
+}
+
+uint32_t DrmFdTables::scans_of(const std::string& pdir) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = m_.find(pdir);
+  return it == m_.end() ? 0 : it->second.scans;
 }
 
 void DrmFdTables::clear() {

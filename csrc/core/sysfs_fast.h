@@ -233,6 +233,7 @@ class DrmFdTables {
   void retain(const std::string& proc_root, const std::vector<uint32_t>& kfd_pids);
   void clear();  // drop every entry not being scanned right now
   uint64_t scans() const { return scans_.load(); }
+  uint32_t scans_of(const std::string& pdir);  // 0 when not cached
   size_t size();
 
  private:
@@ -240,6 +241,7 @@ class DrmFdTables {
     int64_t scanned_ns = 0, used_ns = 0;
     bool want = false;
     bool scanning = false;  // first scan in flight (fds_for waits for it)
+    uint32_t scans = 0;     // scans of this entry (tests: counts unaffected by other processes' entries)
     std::vector<std::pair<int, std::string>> fds;  // (fd, /dev/dri/... target)
   };
   static void scan(const std::string& pdir, std::vector<std::pair<int, std::string>>* fds);

@@ -175,14 +175,18 @@ def test_fd_tables_are_shared_across_gpus_and_refreshed_off_tick(exporter, tmp_p
     after that reads the new fd."""
     sysr, procr = make_tree(tmp_path, procs=((4242, 0), (4242, 1)))
     core.fd_table_clear()  # the cache is node-wide: an earlier test's due rescans would count here
-    s0 = core.fd_table_stats()["scans"]
+    pdir = str(procr / "4242")  # counted per entry: scans of other processes' tables do not count here
+
+    def scans():
+        return core.fd_table_scans_of(pdir)
+
     ex = exporter(sysr, procr, sample_threads=2, interval_s=0)  # start() runs the first tick
     ex.tick()
     rows = sorted((r["dev"], r["used_memory_bytes"]) for r in ex.pod_rows() if not r["idle"])
     assert rows == [(0, 1 << 30), (1, 1 << 30)]
-    assert core.fd_table_stats()["scans"] - s0 == 1  # one scan served both GPUs
+    assert scans() == 1  # one scan served both GPUs
     ex.tick()
-    assert core.fd_table_stats()["scans"] - s0 == 1  # cached
+    assert scans() == 1  # cached
     # the process closes fd 5 and opens fd 9 on GPU 0's render node
     fd, fdinfo = procr / "4242" / "fd", procr / "4242" / "fdinfo"
     text = (fdinfo / "5").read_text().replace("1048576 KiB", "2097152 KiB")
@@ -196,9 +200,9 @@ def test_fd_tables_are_shared_across_gpus_and_refreshed_off_tick(exporter, tmp_p
     import time
 
     deadline = time.time() + 5
-    while core.fd_table_stats()["scans"] - s0 < 2 and time.time() < deadline:
+    while scans() < 2 and time.time() < deadline:
         time.sleep(0.01)
-    assert core.fd_table_stats()["scans"] - s0 == 2
+    assert scans() == 2
     ex.tick()  # the worker finished its upkeep before taking this tick
     rows = dict((r["dev"], r["used_memory_bytes"]) for r in ex.pod_rows() if not r["idle"])
     assert rows[0] == 2 << 30
