@@ -617,7 +617,13 @@ void AmdSmiBackend::maintain(int i) {
 }
 
 bool AmdSmiBackend::prewarm(int i) {
-  return i >= 0 && i < static_cast<int>(fast_.size()) && fast_[i] && fast_[i]->prewarm();
+  if (i < 0 || i >= static_cast<int>(handles_.size())) return false;
+  if (i < static_cast<int>(fast_.size()) && fast_[i]) return fast_[i]->prewarm();
+  // without the fast path the tick's table read goes through libamd_smi (the same sysfs file
+  // underneath): warm it the same way, result discarded
+  if (!t_ || !t_->amdsmi_get_gpu_metrics_info || !caps_[i].metrics) return false;
+  amdsmi_gpu_metrics_t m;
+  return t_->amdsmi_get_gpu_metrics_info(handles_[i], &m) == AMDSMI_STATUS_SUCCESS;
 }
 
 bool AmdSmiBackend::supports_occupancy(int i) const {
