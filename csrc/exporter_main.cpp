@@ -37,7 +37,7 @@ static void usage() {
           "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--pod-labels KEY,KEY..]\n"
-          "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--ras-slices N] [--no-gzip] [--metrics-include GLOBS] [--metrics-exclude GLOBS] [--sample-threads N] [--rt-priority N]\n"
+          "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--ras-slices N] [--no-gzip] [--metrics-include GLOBS] [--metrics-exclude GLOBS] [--sample-threads N] [--rt-priority N] [--prewarm-ms MS]\n"
           "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx]\n"
           "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri] [--docker SOCKET]\n"
           "                       [--pod-logs /var/log] [--device-checkpoint FILE]\n"
@@ -125,6 +125,7 @@ int main(int argc, char** argv) {
     else if (a == "--metrics-exclude") set("metrics_exclude", next());
     else if (a == "--sample-threads") set("sample_threads", next());
     else if (a == "--rt-priority") set("rt_priority", next());
+    else if (a == "--prewarm-ms") set("prewarm_ms", next());
     else if (a == "--http-threads") set("http_threads", next());
     else if (a == "--log-level") set("log_level", next());
     else if (a == "--pmc") set("enable_pmc", "true");

@@ -305,6 +305,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
                    help="comma-separated globs: metric families left out of /metrics (e.g. 'gpu_xcd_*')")
     p.add_argument("--sample-threads", dest="sample_threads", type=int)
     p.add_argument("--rt-priority", dest="rt_priority", type=int)
+    p.add_argument("--prewarm-ms", dest="prewarm_ms", type=float,
+                   help="device workers warm the firmware-table read this long before each tick (0 = off)")
     p.add_argument("--device-timeout", dest="device_timeout_s", type=float,
                    help="seconds before a device call is exported as hung (gpu_up 0)")
     p.add_argument("--enable-probe-kernel", dest="enable_probe", action="store_true", default=None)

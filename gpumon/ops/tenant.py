@@ -32,6 +32,7 @@ CONDITIONS = {
     "none": None,
     "1hz": ["--interval", "1"],
     "10hz": ["--interval", "0.1"],
+    "10hz_noprewarm": ["--interval", "0.1", "--prewarm-ms", "0"],  # prewarm's own share of the cost
     "10hz_pmc_probe": ["--interval", "0.1", "--pmc", "--probe"],
 }
 
