@@ -369,7 +369,8 @@ void Exporter::start_workers(int n) {
     // the workers' sub-samples stand in for the tick's own cu_occupancy read (the costliest
     // per-process file: ~27 us, a KFD walk over the process's queues)
     if (i == 0) backend_->set_tick_occupancy(occ_ns == 0 || !backend_->supports_occupancy(i));
-    // prewarm only where ticks are far enough apart for the fetch path to cool (>= 10 ms gaps)
+    // prewarm only at intervals >= 20 ms: a read within ~5 ms of the last one is warm already, and
+    // the lead is capped at a quarter of the interval
     const int64_t prewarm_ns = cfg_.interval_s >= 0.02 && cfg_.prewarm_ms > 0
                                    ? static_cast<int64_t>(std::min(cfg_.prewarm_ms, cfg_.interval_s * 250.0) * 1e6)
                                    : 0;
@@ -646,8 +647,8 @@ std::vector<TickInfo> Exporter::tick_log() const {
 void Exporter::sampler_loop() {
   const bool rt = apply_rt(cfg_.rt_priority, "sampler", rt_threads_.get());
   // 1 us timer slack instead of the default 50 us: the tick starts on its deadline (t_late was
-  // 70-90 us on MI355X boxes, profiles/r3_capacity.md); the sampler wakes once per tick, so the
-  // extra precision costs nothing
+  // 70-90 us on MI355X boxes, profiles/r3_capacity.md); the sampler only sleeps in <= 50 ms
+  // slices between ticks, so the extra precision costs nothing measurable
   prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
   const int64_t period = static_cast<int64_t>(cfg_.interval_s * 1e9);
   int64_t next = mono_ns() + period;
