@@ -4,6 +4,10 @@
 #   make hip        -> gpumon/_hip*.so (HIP kernels: probe + synthetic load, gfx950)
 #   make plugins    -> lib/libgpumon_pmc.so + lib/libgpumon_probe.so (dlopen'd on-device plugins)
 #   make asan       -> bin/gpumon-exporter-asan (host-only sanitizers)
+#   make tools      -> test / experiment binaries (nodev, perf_snapshot_probe, hsa_stages); not in `all`
+# `all` is the product only: deploy/Dockerfile's build stage copies Makefile, csrc and gpumon and
+# runs `make all` -- nothing under tools/ or tests/ may become a prerequisite of it
+# (tests/test_deploy.py::test_image_build_stage_makes_all_from_its_copy_set).
 # Everything builds IN-TREE so the .so files travel with the repo snapshot to the GPU box.
 
 PY        ?= python3
@@ -29,8 +33,9 @@ BIN       := bin/gpumon-exporter
 HIP_SRC   := $(wildcard csrc/hip/*.hip)
 HIP_HDR   := $(wildcard csrc/hip/*.h)
 
-.PHONY: all core hip pmc plugins clean asan tsan fakes nodev
-all: core hip plugins pmc nodev snapshot
+.PHONY: all core hip pmc plugins clean asan tsan fakes nodev snapshot tools
+all: core hip plugins pmc
+tools: nodev snapshot
 core: $(PYEXT) $(BIN)
 hip: $(HIPEXT)
 

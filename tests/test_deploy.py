@@ -121,6 +121,97 @@ def test_dockerfile_entrypoint():
     assert "COPY --from=build /src/lib /opt/gpumon/lib" in txt and "GPUMON_PLUGIN_DIR=/opt/gpumon/lib" in txt
 
 
+def _build_stage_copies(dockerfile):
+    """(sources, dest) of every COPY in the Dockerfile's first (build) stage, in order. Only the
+    plain `COPY src... dest` form (no --from, no heredocs) may appear there."""
+    copies, stage = [], 0
+    for line in open(dockerfile).read().splitlines():
+        words = line.split()
+        if not words:
+            continue
+        if words[0] == "FROM":
+            stage += 1
+            if stage > 1:
+                break
+        elif words[0] == "COPY" and stage == 1:
+            assert not any(w.startswith("--") for w in words[1:]), line
+            copies.append((words[1:-1], words[-1]))
+    assert copies, "no COPY in the build stage"
+    return copies
+
+
+def _stage_tree(copies, dst):
+    """What `docker build` would see: each COPY source from a clean checkout (tracked files only,
+    so in-tree build outputs such as gpumon/_core*.so do not hide a missing rule)."""
+    import shutil
+    import subprocess
+
+    tracked = None
+    if os.path.isdir(os.path.join(ROOT, ".git")):
+        out = subprocess.run(["git", "-C", ROOT, "ls-files"], capture_output=True, text=True, check=True).stdout
+        tracked = set(out.split())
+    for srcs, dest in copies:
+        for s in srcs:
+            target = os.path.normpath(os.path.join(dst, dest if not dest.endswith("/") and len(srcs) == 1
+                                                   and dest not in ("./", ".") else os.path.join(dest, s)))
+            src = os.path.join(ROOT, s)
+            if os.path.isdir(src):
+                for base, _, files in os.walk(src):
+                    for f in files:
+                        rel = os.path.relpath(os.path.join(base, f), ROOT)
+                        if tracked is not None and rel not in tracked:
+                            continue
+                        if tracked is None and (f.endswith((".so", ".o", ".pyc")) or "__pycache__" in rel):
+                            continue
+                        out = os.path.join(target, os.path.relpath(os.path.join(base, f), src))
+                        os.makedirs(os.path.dirname(out), exist_ok=True)
+                        shutil.copy2(os.path.join(base, f), out)
+            else:
+                os.makedirs(os.path.dirname(target), exist_ok=True)
+                shutil.copy2(src, target)
+
+
+def _make_targets(dockerfile):
+    m = re.search(r"^RUN make\b(.*)$", open(dockerfile).read(), re.M)
+    assert m, "the build stage runs make"
+    return [w for w in m.group(1).split() if not w.startswith("-")]
+
+
+def test_image_build_stage_makes_all_from_its_copy_set(tmp_path):
+    """deploy/Dockerfile's build stage must build from exactly the files it
+    COPYs. `make -n all` over that set resolves every prerequisite (a rule that needs tools/ or
+    tests/ fails here), and `make core` really compiles there. Reference: its image builds from the
+    two files it ADDs (/root/reference/Dockerfile:1-7)."""
+    import subprocess
+
+    df = os.path.join(ROOT, "deploy", "Dockerfile")
+    copies = _build_stage_copies(df)
+    _stage_tree(copies, str(tmp_path))
+    assert sorted(os.listdir(tmp_path)) == ["Makefile", "csrc", "gpumon"], sorted(os.listdir(tmp_path))
+    targets = _make_targets(df)
+    assert targets == ["all", "GPUMON_ARCH=gfx950"], targets
+    r = subprocess.run(["make", "-C", str(tmp_path), "-n", *targets], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "tools/" not in r.stdout and "tests/" not in r.stdout
+    r = subprocess.run(["make", "-C", str(tmp_path), "-j8", "core"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert os.path.exists(tmp_path / "bin" / "gpumon-exporter")
+
+
+def test_copy_set_check_catches_an_outside_prerequisite(tmp_path):
+    """The check above is not vacuous: the same COPY set with `all` depending on a tools/ target
+    (round 3's `snapshot`) fails `make -n all`."""
+    import subprocess
+
+    _stage_tree(_build_stage_copies(os.path.join(ROOT, "deploy", "Dockerfile")), str(tmp_path))
+    mk = (tmp_path / "Makefile").read_text()
+    mk = re.sub(r"^all:(.*)$", r"all:\1 bin/perf_snapshot_probe", mk, count=1, flags=re.M)
+    (tmp_path / "Makefile").write_text(mk)
+    r = subprocess.run(["make", "-C", str(tmp_path), "-n", "all", "GPUMON_ARCH=gfx950"], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "tools/perf_snapshot_probe.hip" in r.stderr, (r.returncode, r.stderr[-500:])
+
+
 def _control_plane_metric_names():
     """Series of the native metadata pollers, from an exporter pointed at the fake kubelet (CRI +
     PodResources) and a fake Docker daemon."""

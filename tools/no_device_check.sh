@@ -11,6 +11,8 @@
 set -o pipefail
 out=${1:-gpurun_out/nodev}
 mkdir -p "$out"
+# a test tool, not part of `make all`: build it on the CPU side first (`make tools`)
+[ -x ./bin/gpumon-exporter-nodev ] || { echo "bin/gpumon-exporter-nodev missing: run 'make tools' first" >&2; exit 2; }
 ARGS="--backend amdsmi --once --no-pod-resources --no-cri --log-level warn"
 python -c "import torch,time; x=torch.randn(8192,8192,device='cuda'); t=time.time()
 while time.time()-t<25: y=x@x; torch.cuda.synchronize()" > "$out/tenant.log" 2>&1 &
