@@ -6,8 +6,10 @@
         --master-port P bench.py --gpus N --steps K --warmup W           # N GPUs, one rank each
 
 What one "step" is: one sampling period of the exporter (default 1 Hz, the BASELINE interval).
-Rank 0 runs the native exporter (amdsmi backend) over GPUs 0..N-1 and a client-side scraper that
-hits /metrics at --scrape-rate, while EVERY GPU runs a synthetic gfx950 HIP load (bf16 MFMA burn +
+Rank 0 runs the native exporter (amdsmi backend) over exactly the GPUs the job loads (each HIP
+ordinal paired with the exporter device of the same PCI BDF, gpumon/parallel/devmap.py, printed as
+``devices``; the run fails if a loaded GPU reads under 50 % gfx_util, ``device_check``) and a
+client-side scraper that hits /metrics at --scrape-rate, while EVERY GPU runs a synthetic gfx950 HIP load (bf16 MFMA burn +
 HBM stream, csrc/hip/kernels.hip) and, for N > 1, xGMI traffic:
 
 * under torchrun (one rank per GPU) each rank loads its own GPU and all ranks run RCCL ring
@@ -110,15 +112,18 @@ def _exporter_cpu_s():
     return total
 
 
-def _per_gpu_xgmi(tick_rates, n, expected_tx, expected_rx):
+def _per_gpu_xgmi(tick_rates, rows, expected_tx, expected_rx):
     """Exporter-measured xGMI tx / rx per GPU (sum over links, mean over the timed ticks; the first
-    tick's rate spans part of the warmup and is skipped) against the traffic the bench drove."""
+    tick's rate spans part of the warmup and is skipped) against the traffic the bench drove.
+    ``rows`` pair each loaded HIP ordinal with its exporter device (gpumon/parallel/devmap.py); the
+    expectations are indexed by ordinal, the exporter's rates by device index."""
     ticks = tick_rates[1:] if len(tick_rates) > 1 else tick_rates
     out = []
-    for d in range(n):
-        tx = [t[d][0] for t in ticks if d < len(t) and t[d] is not None]
-        rx = [t[d][1] for t in ticks if d < len(t) and t[d] is not None]
-        row = {"gpu": d,
+    for m in rows:
+        d, i = m["hip_ordinal"], m["index"]
+        tx = [t[i][0] for t in ticks if i < len(t) and t[i] is not None]
+        rx = [t[i][1] for t in ticks if i < len(t) and t[i] is not None]
+        row = {"gpu": d, "gpu_id": m["gpu_id"],
                "exporter_tx_GBps": _r(sum(tx) / len(tx) / 1e9) if tx else None,
                "exporter_rx_GBps": _r(sum(rx) / len(rx) / 1e9) if rx else None,
                "expected_tx_GBps": _r(expected_tx[d] / 1e9) if expected_tx else None,
@@ -131,21 +136,25 @@ def _per_gpu_xgmi(tick_rates, n, expected_tx, expected_rx):
     return out
 
 
-def _link_map_check(n, seconds):
-    """GPU 0 pushes into every peer in turn while a fresh 10 Hz exporter watches: the link whose
-    write counter moves must be the one the exporter attributes to that peer's BDF."""
+def _link_map_check(ord_bdfs, seconds):
+    """HIP ordinal 0 pushes into every peer in turn while a fresh 10 Hz exporter watches: the link
+    whose write counter moves must be the one the exporter attributes to that peer's BDF."""
     from gpumon import core as _core
+    from gpumon.parallel.devmap import index_of, match
     from gpumon.parallel.xgmi import rate_within, validate_pair
 
-    ex = _core().Exporter({"backend": "amdsmi", "devices": list(range(n)), "serve_http": False,
-                           "interval_s": 0.1, "link_every": 1, "processes": False, "log_level": "warn"})
+    n = len(ord_bdfs)
+    ex = _core().Exporter({"backend": "amdsmi", "devices": [ord_bdfs[k] for k in sorted(ord_bdfs)],
+                           "serve_http": False, "interval_s": 0.1, "link_every": 1, "processes": False,
+                           "log_level": "warn"})
     err = ex.start()
     if err:
         return {"error": err}
     rows = []
     try:
+        idx = index_of(match(ord_bdfs, ex.statics()))
         for k in range(1, n):
-            r = validate_pair(ex, 0, k, seconds=seconds, interval=0.1)
+            r = validate_pair(ex, 0, k, seconds=seconds, interval=0.1, index_of=idx)
             r["rate_within_15pct"] = rate_within(r, 0.15)
             rows.append(r)
     finally:
@@ -154,7 +163,7 @@ def _link_map_check(n, seconds):
             "rates_within_15pct": sum(1 for r in rows if r["rate_within_15pct"])}
 
 
-def _capacity(backend, n, args, has_gpu):
+def _capacity(backend, devices, args, has_gpu):
     """Sampler capacity (untimed, after the timed region, load still running): a second exporter on
     the same devices at --capacity-interval (1 ms) for --capacity-s seconds. `value` is fixed by the
     configured interval; this is how fast the sampler can go: ticks/s, samples/s/GPU, the share of
@@ -162,7 +171,7 @@ def _capacity(backend, n, args, has_gpu):
     from gpumon.config import Config
     from gpumon.monitor import GpuMonitor
 
-    cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi", "auto")) else [],
+    cfg = Config(backend=backend, devices=devices,
                  interval=args.capacity_interval, listen="127.0.0.1:0", http_threads=1, host="bench-node",
                  log_level="warn", fast_path=not args.no_fast_path, sample_threads=args.sample_threads,
                  rt_priority=args.rt_priority, prewarm_ms=args.prewarm_ms)
@@ -196,6 +205,26 @@ def _capacity(backend, n, args, has_gpu):
             "tick_p50_ms": round(_pct(durs, 0.50) * 1e3, 4) if durs else None,
             "tick_p99_ms": round(_pct(durs, 0.99) * 1e3, 4) if durs else None,
             "ticks_logged": len(durs)}
+
+
+GFX_UTIL_FLOOR = 50.0  # % : a GPU the bench loads must read at least this busy in the exporter
+
+
+def _device_check(rows, tick_util, loaded):
+    """Each loaded GPU's exporter gfx_util, mean over the timed ticks (the first one spans the
+    warmup and is skipped). A loaded GPU that reads under GFX_UTIL_FLOOR means the exporter is
+    watching some other GPU: the check fails, and bench.py exits non-zero after its line."""
+    ticks = tick_util[1:] if len(tick_util) > 1 else tick_util
+    per = []
+    for r in rows:
+        xs = [t[r["index"]] for t in ticks if r["index"] < len(t) and isinstance(t[r["index"]], (int, float))
+              and t[r["index"]] == t[r["index"]]]
+        per.append({"hip_ordinal": r["hip_ordinal"], "gpu_id": r["gpu_id"],
+                    "gfx_util_mean": round(sum(xs) / len(xs), 1) if xs else None})
+    if not loaded:
+        return {"ok": True, "checked": False, "reason": "no synthetic load", "per_gpu": per}
+    bad = [p for p in per if p["gfx_util_mean"] is None or p["gfx_util_mean"] < GFX_UTIL_FLOOR]
+    return {"ok": not bad, "checked": True, "floor_pct": GFX_UTIL_FLOOR, "per_gpu": per}
 
 
 def main() -> int:
@@ -274,6 +303,21 @@ def main() -> int:
         dist.init_process_group(backend="nccl" if has_gpu else "gloo")
     device = (torch.device(f"cuda:{local_rank}") if has_gpu else torch.device("cpu")) if torch is not None else None
 
+    # torchrun: this rank's GPU; one process: all N GPUs (the node-level exporter watches them all)
+    my_devs = [local_rank] if world > 1 else list(range(n))
+    # HIP ordinal -> PCI BDF of every GPU the job loads, gathered to rank 0: the exporter samples
+    # exactly those GPUs, named by BDF, since its gpu_id (libamd_smi hip_id) is node-wide and a
+    # HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES subset renumbers the ordinals (devmap.py)
+    ord_bdfs = {}
+    if has_gpu:
+        from gpumon.parallel.devmap import hip_bdfs
+
+        ord_bdfs = hip_bdfs(my_devs)
+        if dist is not None:
+            allb = [None] * world
+            dist.all_gather_object(allb, ord_bdfs)
+            ord_bdfs = {int(k): v for d in allb for k, v in d.items()}
+
     def barrier():
         if dist is not None:
             dist.barrier()
@@ -295,7 +339,9 @@ def main() -> int:
             backend = "auto" if has_gpu else f"mock:gpus={n * args.replicate},mode=load"
             if has_gpu and args.replicate > 1:
                 backend = f"amdsmi:replicate={args.replicate}"
-        cfg = Config(backend=backend, devices=list(range(n)) if backend.startswith(("amdsmi", "rocm_smi", "auto")) else [],
+        real = backend.startswith(("amdsmi", "rocm_smi", "auto"))
+        sampled = [ord_bdfs[k] for k in sorted(ord_bdfs)] if real and ord_bdfs else []
+        cfg = Config(backend=backend, devices=sampled,
                      interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
                      enable_probe=args.probe and has_gpu, log_level="warn", fast_path=not args.no_fast_path,
                      sample_threads=args.sample_threads, rt_priority=args.rt_priority, prewarm_ms=args.prewarm_ms)
@@ -307,6 +353,13 @@ def main() -> int:
         st = mon.ex.statics()
         if len(st) < n:
             raise SystemExit(f"exporter sees {len(st)} GPU(s), bench needs {n}")
+        from gpumon.parallel.devmap import DeviceMapError, match, positional
+
+        try:  # every loaded ordinal paired with the exporter device of the same BDF, or stop here
+            dev_rows = (match(ord_bdfs, st, replicas=args.replicate > 1) if real and ord_bdfs
+                        else positional(n, st))
+        except DeviceMapError as e:
+            raise SystemExit(f"bench: loaded GPUs and sampled GPUs disagree: {e}")
 
     # ---------------------------------------------------------------- idle reference (untimed)
     # the same scrape load against the same exporter before any synthetic load starts: the
@@ -335,8 +388,6 @@ def main() -> int:
     barrier()
 
     # ---------------------------------------------------------------- synthetic load on every GPU
-    # torchrun: this rank's GPU; one process: all N GPUs (the node-level exporter watches them all)
-    my_devs = [local_rank] if world > 1 else list(range(n))
     loads = []
     if has_gpu and args.load != "idle":
         from gpumon import hip
@@ -415,6 +466,7 @@ def main() -> int:
     if scraper is not None:
         scraper.start()
     tick_rates = []  # per tick, per sampled device: (sum of per-link write B/s, read B/s) or None
+    tick_util = []   # per tick, per sampled device: the exporter's gfx_util (%)
     ar_events = []
     for step in range(args.steps):
         # one step = one sampling interval: this interval's xGMI traffic, then the tick closing it
@@ -434,6 +486,7 @@ def main() -> int:
                 raise SystemExit("exporter tick timed out")
             tick_rates.append([(sum(r.get("xgmi_wr_Bps") or [0.0]), sum(r.get("xgmi_rd_Bps") or [0.0]))
                                if r.get("valid") else None for r in mon.ex.rates()])
+            tick_util.append([x["fields"].get("gfx_util") for x in mon.ex.samples()])
     barrier()
     elapsed = time.perf_counter() - t0
     if rank == 0:  # the exporter's counters at the end of the timed region (not after the reductions)
@@ -494,6 +547,8 @@ def main() -> int:
         lat = scrape_result.get("latencies_s", [])
         srv = _server_durations(mon.ex, n_scr0, len(lat))  # server-side, the same scrapes
         samples = s1["samples"] - s0["samples"]
+        stale = s1.get("stale_samples", 0) - s0.get("stale_samples", 0)
+        fresh = samples - stale  # a repeated firmware table is no new sample of the device
         ticks = seq1 - seq0
         timed = [t for t in mon.ex.tick_log() if seq0 < t["seq"] <= seq0 + ticks]
         tdur = [t["duration_s"] for t in timed]
@@ -501,15 +556,17 @@ def main() -> int:
         sm = mon.ex.samples()
         util = [x["fields"].get("gfx_util") for x in sm]
         rows = mon.ex.pod_rows()
-        value = samples / elapsed
+        value = fresh / elapsed
+        check = _device_check(dev_rows, tick_util, loaded=bool(loads) and args.load != "idle")
         from gpumon.export import promtext
 
+        gid = {r["hip_ordinal"]: r["gpu_id"] for r in dev_rows}
         fam = promtext.parse(mon.metrics())
         slot_map = {}  # xGMI link-metrics entry -> table slot pairing (csrc/core/xgmi_map.cpp)
         for what in ("verified", "unverified", "mismatch"):
             for _, lab, v in fam.get(f"gpumon_xgmi_slot_map_{what}", {}).get("samples", []):
                 slot_map.setdefault(lab.get("gpu_id"), {})[what] = int(v)
-        per_gpu = _per_gpu_xgmi(tick_rates, n, exp_tx, exp_rx) if xgmi is not None else None
+        per_gpu = _per_gpu_xgmi(tick_rates, dev_rows, exp_tx, exp_rx) if xgmi is not None else None
         if xgmi is not None:
             tx = [r["exporter_tx_GBps"] for r in per_gpu if r["exporter_tx_GBps"] is not None]
             rx = [r["exporter_rx_GBps"] for r in per_gpu if r["exporter_rx_GBps"] is not None]
@@ -534,14 +591,21 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / max(1, len(sm)) / BASELINE_SAMPLES_PER_GPU, 3),
-            "value_note": ("value = fresh device samples/s over the timed ticks: fixed by the sampling "
-                           "interval (1/interval per GPU) unless ticks overrun; the measured speed is "
-                           "scrape_p99_ms / scrape_p999_ms (client), server_scrape_p99_ms and tick_*_ms"),
+            "value_note": ("value = fresh device samples/s over the timed ticks (samples whose firmware table "
+                           "advanced; repeats of the last table are not counted): fixed by the sampling "
+                           "interval (1/interval per GPU) unless ticks overrun or the interval beats the SMU's "
+                           "refresh; the measured speed is scrape_p99_ms / scrape_p999_ms (client), "
+                           "server_scrape_p99_ms and tick_*_ms"),
+            "samples_total": samples,
+            "stale_samples": stale,
             "dtype": "bf16",
             "data": ("synthetic" if backend in ("amdsmi", "rocm_smi") else
                      f"synthetic (REHEARSAL: {n} physical GPU(s) each sampled {args.replicate}x)"
                      if backend.startswith("amdsmi:replicate") else "synthetic (mock backend: no GPU visible)"),
             "sampled_devices": len(sm),
+            # each loaded HIP ordinal and the exporter device sampled for it (same PCI BDF)
+            "devices": [{k: r[k] for k in ("hip_ordinal", "bdf", "gpu_id")} for r in dev_rows],
+            "device_check": check,
             "config": {
                 "model": f"gpumon MI355X exporter ({backend.split(':')[0]} backend) + synthetic bf16 MFMA/HBM HIP load",
                 "global_batch": n,
@@ -596,7 +660,8 @@ def main() -> int:
                                 for k, v in s1.get("backend_calls", {}).items()},
             "backend": backend,
             "load": args.load if has_gpu else "none",
-            "load_per_gpu": [{"gpu": d, "tflops": round(r[0], 1), "tbps": round(r[1], 3), "busy": round(r[2], 3)}
+            "load_per_gpu": [{"gpu": d, "gpu_id": gid.get(d), "tflops": round(r[0], 1), "tbps": round(r[1], 3),
+                              "busy": round(r[2], 3)}
                              for d, r in enumerate(lrates)] if has_gpu and loads else None,
             "load_tflops": round(sum(r[0] for r in lrates), 1) if has_gpu and loads else None,
             "load_tbps": round(sum(r[1] for r in lrates), 3) if has_gpu and loads else None,
@@ -615,13 +680,13 @@ def main() -> int:
         if has_gpu and n > 1 and args.link_check_s > 0:
             # validation evidence, never a reason to lose the measured line
             try:
-                lm = _link_map_check(n, args.link_check_s)
+                lm = _link_map_check(ord_bdfs, args.link_check_s)
             except Exception as e:  # noqa: BLE001
                 lm = {"error": f"{type(e).__name__}: {e}"}
             result["xgmi"] = dict(result["xgmi"] or {}, link_map=lm)
         if args.capacity_s > 0:
             try:
-                result["capacity"] = _capacity(backend, n, args, has_gpu)
+                result["capacity"] = _capacity(backend, sampled, args, has_gpu)
             except Exception as e:  # noqa: BLE001
                 result["capacity"] = {"error": f"{type(e).__name__}: {e}"}
     if result is not None:  # the line is out before the teardown collectives can stall on a peer
@@ -635,6 +700,9 @@ def main() -> int:
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if result is not None and not result["device_check"]["ok"]:
+        print(f"bench: FAILED device check: {json.dumps(result['device_check'])}", file=sys.stderr, flush=True)
+        return 1
     return 0
 
 

@@ -69,7 +69,8 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "rocm_smi_lib", &c.rocm_smi_lib);
   get(d, "fast_path", &c.fast_path);
   get(d, "sysfs_root", &c.sysfs_root);
-  get(d, "devices", &c.devices);
+  if (d.contains("devices") && !d["devices"].is_none())  // hip ids (int or str) and / or PCI BDFs
+    for (auto x : d["devices"]) c.devices.push_back(py::str(x).cast<std::string>());
   get(d, "interval_s", &c.interval_s);
   get(d, "serve_http", &c.serve_http);
   get(d, "listen_addr", &c.listen_addr);
@@ -90,6 +91,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "ras_async", &c.ras_async);
   get(d, "occ_samples", &c.occ_samples);
   get(d, "prewarm_ms", &c.prewarm_ms);
+  get(d, "stale_hold_s", &c.stale_hold_s);
   get(d, "hide_empty_contexts", &c.hide_empty_contexts);
   get(d, "mfma_exclusive_window_s", &c.mfma_exclusive_window_s);
   get(d, "sample_threads", &c.sample_threads);
@@ -818,6 +820,7 @@ PYBIND11_MODULE(_core, m) {
              d["ticks"] = s.ticks;
              d["samples"] = s.samples;
              d["stale_samples"] = s.stale_samples;
+             d["frozen_samples"] = s.frozen_samples;
              d["occupancy_reads"] = s.occupancy_reads;
              d["hidden_contexts"] = s.hidden_contexts;
              d["rt_threads"] = s.rt_threads;
@@ -958,6 +961,8 @@ PYBIND11_MODULE(_core, m) {
       .def("mock_link_calls", [](Exporter& e, int dev) { return mock_of(e)->link_calls(dev); })
       .def("mock_set_link_fail",
            [](Exporter& e, int dev, bool fail) { mock_of(e)->set_link_fail(dev, fail); })
+      .def("mock_set_firmware_frozen",
+           [](Exporter& e, int dev, bool frozen) { mock_of(e)->set_firmware_frozen(dev, frozen); })
       .def("mock_set_occ_series",
            [](Exporter& e, int dev, const std::vector<double>& v) { mock_of(e)->set_occ_series(dev, v); })
       .def("mock_occ_reads", [](Exporter& e, int dev) { return mock_of(e)->occ_reads(dev); })

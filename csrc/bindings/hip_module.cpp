@@ -16,6 +16,7 @@ PYBIND11_MODULE(_hip, m) {
   m.def("device_count", &device_count);
   m.def("device_arch", &device_arch);
   m.def("device_cu_count", &device_cu_count);
+  m.def("device_pci_bus_id", &device_pci_bus_id);
 
   m.def("mfma_tile", [](int dev, uintptr_t a, uintptr_t b, uintptr_t c, int iters, uintptr_t stream) {
     launch_mfma_tile(dev, P(a), P(b), static_cast<float*>(P(c)), iters, P(stream));

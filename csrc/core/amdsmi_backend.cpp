@@ -196,8 +196,14 @@ bool AmdSmiBackend::init(std::string* err) {
   std::sort(found.begin(), found.end(),
             [](const auto& a, const auto& b) { return a.first < b.first; });
   for (auto& [hip, h] : found) {
-    if (!keep(hip)) continue;
+    std::string bdf;
+    if (t_->amdsmi_get_gpu_device_bdf) {
+      amdsmi_bdf_t b{};
+      if (t_->amdsmi_get_gpu_device_bdf(h, &b) == AMDSMI_STATUS_SUCCESS) bdf = bdf_str(b);
+    }
+    if (!keep(hip, bdf)) continue;
     DeviceStatic d;
+    d.bdf = bdf;
     d.index = static_cast<int>(devs_.size());
     d.hip_id = hip;
     d.gpu_id = std::to_string(hip);
@@ -212,10 +218,6 @@ bool AmdSmiBackend::init(std::string* err) {
       char uuid[AMDSMI_MAX_STRING_LENGTH] = {0};
       unsigned int len = sizeof uuid;
       if (t_->amdsmi_get_gpu_device_uuid(h, &len, uuid) == AMDSMI_STATUS_SUCCESS) d.uuid = uuid;
-    }
-    if (t_->amdsmi_get_gpu_device_bdf) {
-      amdsmi_bdf_t b{};
-      if (t_->amdsmi_get_gpu_device_bdf(h, &b) == AMDSMI_STATUS_SUCCESS) d.bdf = bdf_str(b);
     }
     if (t_->amdsmi_get_gpu_asic_info) {
       amdsmi_asic_info_t ai{};

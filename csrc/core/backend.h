@@ -8,6 +8,7 @@
 #pragma once
 
 #include <atomic>
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -15,6 +16,7 @@
 #include <tuple>
 #include <vector>
 
+#include "common.h"
 #include "ras.h"
 #include "sample.h"
 
@@ -66,8 +68,26 @@ class Backend {
   // within ~5 ms and 150-300 us after a longer gap; spinning the CPU instead does not help
   // (profiles/r3_capacity.md). Returns false where the backend has nothing to warm.
   virtual bool prewarm(int /*i*/) { return false; }
-  // Restrict to a subset of device hip_ids (empty = all). Applied at init().
-  void set_device_filter(const std::vector<int>& ids) { filter_ = ids; }
+  // Restrict to a subset of devices (empty = all). Applied at init(). An entry is a hip_id ("3")
+  // or a PCI BDF ("0000:75:00.0", domain optional): a process that sees its GPUs through
+  // HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES numbers them 0..n-1, while libamd_smi's hip_id is
+  // the node-wide index, so callers that loaded HIP ordinals name them by BDF
+  // (hipDeviceGetPCIBusId, gpumon/parallel/devmap.py). Unparseable entries match nothing.
+  void set_device_filter(const std::vector<std::string>& ids) {
+    filter_ids_.clear();
+    filter_bdfs_.clear();
+    for (const auto& s : ids) {
+      std::string b = normalize_bdf(s);
+      if (!b.empty()) {
+        filter_bdfs_.push_back(b);
+        continue;
+      }
+      char* end = nullptr;
+      long v = strtol(s.c_str(), &end, 10);
+      filter_ids_.push_back(end && end != s.c_str() && *end == 0 && v >= 0 ? static_cast<int>(v) : -1);
+    }
+  }
+  bool has_device_filter() const { return !filter_ids_.empty() || !filter_bdfs_.empty(); }
 
   // Per-call latency accounting (exported as gpumon_backend_call_* self-metrics).
   enum Call { kCallMetrics = 0, kCallVram, kCallProcs, kCallLinks, kCallActivity, kCallPower, kCallRas, kCallCount };
@@ -101,11 +121,17 @@ class Backend {
   std::atomic<uint64_t> calls_n_[kCallCount] = {};
   std::atomic<uint64_t> calls_ns_[kCallCount] = {};
   std::atomic<uint64_t> calls_err_[kCallCount] = {};
-  std::vector<int> filter_;
-  bool keep(int hip_id) const {
-    if (filter_.empty()) return true;
-    for (int x : filter_)
+  std::vector<int> filter_ids_;
+  std::vector<std::string> filter_bdfs_;  // normalize_bdf form
+  bool keep(int hip_id, const std::string& bdf) const {
+    if (!has_device_filter()) return true;
+    for (int x : filter_ids_)
       if (x == hip_id) return true;
+    if (!bdf.empty()) {
+      std::string b = normalize_bdf(bdf);
+      for (const auto& x : filter_bdfs_)
+        if (x == b) return true;
+    }
     return false;
   }
 };
@@ -139,6 +165,8 @@ struct MockConfig {
   bool occupancy = true;              // KFD cu_occupancy readable (false: a node without the file)
   std::string link_order = "index";   // link-metrics entry order: index | reverse | rotate
   bool link_offset = false;           // entry counters with another origin than the table's (delta pairing only)
+  bool full = false;                  // every scalar field filled (fan, voltages, ... that MI355X leaves N/A):
+                                      // the metric reference lists the families a full table produces
 };
 
 class MockBackend : public Backend {
@@ -178,6 +206,8 @@ class MockBackend : public Backend {
   void set_link_up(int dev, int link, bool up);  // firmware link status (0 down) of one xGMI slot
   uint64_t link_calls(int dev) const;            // sample_links() calls (link-metrics refreshes)
   void set_link_fail(int dev, bool fail);        // link-metrics reads of `dev` fail (links_read -1)
+  // The fake SMU of `dev` stops refreshing its table (firmware timestamp and accumulators hold) / resumes.
+  void set_firmware_frozen(int dev, bool frozen);
   uint64_t calls(int dev) const;
   bool prewarm(int i) override;
   uint64_t prewarms(int dev) const;  // prewarm() calls
@@ -194,6 +224,7 @@ class MockBackend : public Backend {
   std::vector<char> link_down_;      // per dev * kMaxLinks
   std::vector<uint64_t> link_calls_;
   std::vector<char> link_fail_;
+  std::vector<int64_t> frozen_tick_;  // per dev: firmware tick the fake SMU is stuck at (-1 = running)
   std::vector<uint64_t> calls_, prewarms_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
   std::vector<uint64_t> lim_acc_;  // per device x XCC x {ppt, thermal, any, low-util}

@@ -1,3 +1,4 @@
+#include <algorithm>
 #include "common.h"
 
 #include <pthread.h>
@@ -59,6 +60,24 @@ bool starts_with(std::string_view s, std::string_view p) {
 
 bool ends_with(std::string_view s, std::string_view p) {
   return s.size() >= p.size() && s.compare(s.size() - p.size(), p.size(), p) == 0;
+}
+
+std::string normalize_bdf(std::string_view s) {
+  s = trim(s);
+  unsigned dom = 0, bus = 0, dev = 0, fn = 0;
+  int used = 0;
+  std::string z(s);
+  if (std::count(z.begin(), z.end(), ':') == 2) {
+    if (sscanf(z.c_str(), "%x:%x:%x.%x%n", &dom, &bus, &dev, &fn, &used) != 4) return "";
+  } else if (std::count(z.begin(), z.end(), ':') == 1) {
+    if (sscanf(z.c_str(), "%x:%x.%x%n", &bus, &dev, &fn, &used) != 3) return "";
+  } else {
+    return "";
+  }
+  if (used != static_cast<int>(z.size()) || dom > 0xffff || bus > 0xff || dev > 0x1f || fn > 7) return "";
+  char b[32];
+  snprintf(b, sizeof b, "%04x:%02x:%02x.%x", dom, bus, dev, fn);
+  return b;
 }
 
 bool read_file(const std::string& path, std::string* out, size_t max_bytes) {

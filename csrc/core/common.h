@@ -50,6 +50,10 @@ std::string_view trim(std::string_view s);
 bool starts_with(std::string_view s, std::string_view p);
 bool ends_with(std::string_view s, std::string_view p);
 
+// Canonical PCI address "dddd:bb:dd.f", lower case; a missing domain is 0000 ("75:00.0" ->
+// "0000:75:00.0"). "" if `s` is not a BDF. hipDeviceGetPCIBusId, libamd_smi and sysfs agree on it.
+std::string normalize_bdf(std::string_view s);
+
 // Reads a whole (small) file; returns false if it cannot be opened.
 bool read_file(const std::string& path, std::string* out, size_t max_bytes = 1 << 20);
 

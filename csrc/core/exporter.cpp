@@ -448,6 +448,7 @@ static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
     else if (k == "occupancy") base.occupancy = atoi(v.c_str()) != 0;
     else if (k == "link_order") base.link_order = v;
     else if (k == "link_offset") base.link_offset = atoi(v.c_str()) != 0;
+    else if (k == "full") base.full = atoi(v.c_str()) != 0;
     else if (k == "unsupported") base.unsupported = split(v, ';');
     else if (k == "procs") procs_per_gpu = std::max(0, atoi(v.c_str()));
   }
@@ -1094,6 +1095,7 @@ TickInfo Exporter::tick() {
       for (int k = 0; k < s.n_links; ++k)
         if (s.links[k].status >= 0 && !has(s.links[k].max_bandwidth_gbps) && has(lane) && has(width))
           s.links[k].max_bandwidth_gbps = lane * width;
+      if (static_cast<int>(last_fresh_ns_.size()) != n) last_fresh_ns_.assign(n, 0);
       if (i < static_cast<int>(prev.size())) {
         const DeviceSample& p = prev[i];
         if (s.ok && p.ok && s.acc.firmware_ts && s.acc.firmware_ts == p.acc.firmware_ts) {
@@ -1101,12 +1103,21 @@ TickInfo Exporter::tick() {
           stale_++;
         }
         // A repeated table (sampling faster than the firmware refresh) holds no new window: it
-        // keeps the rates of the last one instead of reporting zero power / traffic over it.
-        if (!s.fresh && i < static_cast<int>(prev_rates.size()))
+        // keeps the rates of the last one instead of reporting zero power / traffic over it --
+        // but only while the table is younger than stale_hold_s. An older repeat means the SMU
+        // stopped refreshing (hang, reset): the rates go invalid and gpu_metrics_table_frozen is 1
+        // rather than exporting the last power / activity / xGMI rates forever.
+        const bool young = last_fresh_ns_[i] > 0 && s.host_mono_ns - last_fresh_ns_[i] <= cfg_.stale_hold_s * 1e9;
+        if (!s.fresh && young && i < static_cast<int>(prev_rates.size())) {
           rates[i] = prev_rates[i];
-        else
+        } else if (!s.fresh) {
+          rates[i] = DeviceRates{};
+          frozen_++;
+        } else {
           compute_rates(p, s, cfg_.rates, &rates[i]);
+        }
       }
+      if (s.ok && s.fresh && s.acc.firmware_ts) last_fresh_ns_[i] = s.host_mono_ns;
       samples_++;
       if (!s.ok || s.errors) {  // partial failures (one call failed, others answered) count too
         std::lock_guard<std::mutex> g(state_mu_);
@@ -1147,6 +1158,23 @@ TickInfo Exporter::tick() {
                       "gauge", i, {}, static_cast<double>(m.unverified())});
       }
       set_extra("xgmi_map", std::move(xm));
+      // firmware-table freshness: how long since each table last advanced (host clock)
+      std::vector<ExtraSeries> fz;
+      for (int i = 0; i < n && i < static_cast<int>(last_fresh_ns_.size()); ++i) {
+        const DeviceSample& s = cur[i];
+        if (!s.ok || !s.acc.firmware_ts || last_fresh_ns_[i] <= 0) continue;
+        const double age = std::max<int64_t>(0, s.host_mono_ns - last_fresh_ns_[i]) * 1e-9;
+        fz.push_back({"gpu_metrics_table_age_seconds",
+                      "Host seconds since the device's firmware metrics table (gpu_metrics) last advanced: 0 "
+                      "on a fresh read; grows while the SMU serves the same table.",
+                      "gauge", i, {}, age});
+        fz.push_back({"gpu_metrics_table_frozen",
+                      "1 while the firmware metrics table has not advanced for longer than stale_hold_s: "
+                      "interval rates (power from energy, activity, xGMI) are withheld, instantaneous "
+                      "values are the frozen table's.",
+                      "gauge", i, {}, !s.fresh && age > cfg_.stale_hold_s ? 1.0 : 0.0});
+      }
+      set_extra("table_age", std::move(fz));
     }
     int64_t tb = mono_ns();
     {
@@ -1550,6 +1578,7 @@ SelfStats Exporter::self_stats() const {
   s.ticks = ticks_;
   s.samples = samples_;
   s.stale_samples = stale_;
+  s.frozen_samples = frozen_;
   s.occupancy_reads = occ_reads_->load(std::memory_order_relaxed);
   s.hidden_contexts = hidden_contexts_.load();
   s.rt_threads = rt_threads_->load();

@@ -39,7 +39,7 @@ struct ExporterConfig {
   bool fast_path = true;              // amdsmi: per-tick reads straight from sysfs/KFD (sysfs_fast.h)
   std::string sysfs_root = "/sys";
   MockConfig mock;
-  std::vector<int> devices;           // hip_id filter; empty = all
+  std::vector<std::string> devices;   // hip_ids ("3") and / or PCI BDFs; empty = all (Backend::set_device_filter)
   double interval_s = 1.0;            // <= 0: no sampler thread (ticks driven by tick())
   bool serve_http = true;
   std::string listen_addr = "0.0.0.0";
@@ -68,6 +68,10 @@ struct ExporterConfig {
   // without it the threads stay normal and gpumon_sampler_rt_threads says so.
   int rt_priority = 0;
   double prewarm_ms = 3.0;            // device workers warm the firmware-table path this long before each tick (0 = off)
+  // A repeated firmware table (same firmware timestamp) keeps the last rates only while the table
+  // is at most this old (host time since it last advanced): sampling faster than the SMU's ~20 ms
+  // refresh repeats tables; at 1 Hz a repeat means the SMU stopped, and the rates go invalid.
+  double stale_hold_s = 0.1;
   int occ_samples = 20;               // KFD cu_occupancy reads per process per tick on the device workers (1 = the tick's own)
   bool hide_empty_contexts = true;    // no pod_gpu row for a process with a GPU context but no VRAM and no waves
   // pod_gpu_mfma_util_percent needs exclusive use: no OTHER process's waves seen on the device in
@@ -254,6 +258,8 @@ class Exporter {
   std::mutex seq_mu_;
   std::condition_variable seq_cv_;
   std::atomic<uint64_t> ticks_{0}, samples_{0}, stale_{0}, overruns_{0};
+  std::atomic<uint64_t> frozen_{0};      // samples whose repeated table was older than stale_hold_s
+  std::vector<int64_t> last_fresh_ns_;   // per device: host time the firmware table last advanced (tick_mu_)
   size_t last_body_bytes_ = 0;  // tick thread only: sizes the next render buffer
   std::atomic<uint64_t> phase_ns_[5] = {};  // sample, procs, attrib, render, gzip (cumulative)
 

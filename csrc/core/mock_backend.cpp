@@ -42,17 +42,17 @@ bool MockBackend::init(std::string* err) {
   }
   devs_.clear();
   for (int i = 0; i < cfg_.gpus; ++i) {
-    if (!keep(i)) continue;
+    char buf[64];
+    snprintf(buf, sizeof buf, "0000:%02x:%02x.0", 0x05 + 0x20 * (i % 8), i / 8);  // 8 buses, then devices
+    if (!keep(i, buf)) continue;
     DeviceStatic d;
+    d.bdf = buf;
     d.index = static_cast<int>(devs_.size());
     d.hip_id = i;
     d.gpu_id = std::to_string(i);
-    char buf[64];
     snprintf(buf, sizeof buf, "mock-%04x-0000-1000-80d2-%012llx", 0x75a3 + i,
              static_cast<unsigned long long>(cfg_.seed * 1000 + i));
     d.uuid = buf;
-    snprintf(buf, sizeof buf, "0000:%02x:00.0", 0x05 + 0x20 * i);
-    d.bdf = buf;
     d.model = "AMD Instinct MI355 OAM (mock)";
     d.serial = "MOCK" + std::to_string(i);
     d.gfx_target = "gfx950";
@@ -73,6 +73,7 @@ bool MockBackend::init(std::string* err) {
   link_down_.assign(n * kMaxLinks, 0);
   link_calls_.assign(n, 0);
   link_fail_.assign(n, 0);
+  frozen_tick_.assign(n, -1);
   calls_.assign(n, 0);
   prewarms_.assign(n, 0);
   energy_.assign(n, 1000000);
@@ -253,6 +254,7 @@ void MockBackend::sample(int i, DeviceSample* out) {
   a.valid = true;
   int64_t now = out->host_mono_ns;
   uint64_t fw_tick = static_cast<uint64_t>(t * cfg_.firmware_hz);
+  if (frozen_tick_[i] >= 0) fw_tick = static_cast<uint64_t>(frozen_tick_[i]);
   const int64_t fw_ns = t0_ns_ + static_cast<int64_t>(fw_tick / std::max(1e-3, cfg_.firmware_hz) * 1e9);
   double elapsed = std::max(0.0, (fw_ns - last_ns_[i]) * 1e-9);
   last_ns_[i] = std::max(last_ns_[i], fw_ns);
@@ -308,6 +310,9 @@ void MockBackend::sample(int i, DeviceSample* out) {
     out->links[k].status = k == 0 ? -1 : (link_down_[i * kMaxLinks + k] ? 0 : 1);
     out->links[k].bit_rate_gbps = 38;
   }
+  if (cfg_.full)  // fields a real MI355X table leaves N/A get a neutral value
+    for (int f = 0; f < F_COUNT; ++f)
+      if (!has(v[f])) v[f] = 0.0;
   for (const auto& name : cfg_.unsupported) {
     int f = field_by_name(name);
     if (f >= 0) v[f] = kNaN;
@@ -440,6 +445,13 @@ void MockBackend::sample_links(int i, DeviceSample* out) {
   else if (cfg_.link_order == "rotate" && !es.empty()) std::rotate(es.begin(), es.begin() + 1, es.end());
   out->link_entries = std::move(es);
   out->links_read = 1;
+}
+
+void MockBackend::set_firmware_frozen(int dev, bool frozen) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (dev < 0 || dev >= static_cast<int>(frozen_tick_.size())) return;
+  const double t = (mono_ns() - t0_ns_) * 1e-9;
+  frozen_tick_[dev] = frozen ? static_cast<int64_t>(t * cfg_.firmware_hz) : -1;
 }
 
 void MockBackend::set_link_fail(int dev, bool fail) {

@@ -209,11 +209,18 @@ const std::map<std::string, Setter>& setters() {
       {"sysfs_root", str_at([](NativeOptions* o) { return &o->cfg.sysfs_root; })},
       {"devices",
        [](NativeOptions* o, const std::vector<std::string>& v, std::string* e) {
-         std::vector<int> ids;
+         std::vector<std::string> ids;
          for (const auto& s : as_list(v)) {
            int x;
-           if (!to_int(s, &x, e)) return false;
-           ids.push_back(x);
+           std::string b = normalize_bdf(s);
+           if (!b.empty()) {
+             ids.push_back(b);
+           } else if (to_int(s, &x, e) && x >= 0) {
+             ids.push_back(std::to_string(x));
+           } else {
+             if (e) *e = "devices: '" + s + "' is neither a hip id nor a PCI BDF";
+             return false;
+           }
          }
          o->cfg.devices = ids;
          return true;
@@ -226,6 +233,7 @@ const std::map<std::string, Setter>& setters() {
       {"ras_async", bool_at([](NativeOptions* o) { return &o->cfg.ras_async; })},
       {"occ_samples", int_at([](NativeOptions* o) { return &o->cfg.occ_samples; })},
       {"prewarm_ms", dbl_at([](NativeOptions* o) { return &o->cfg.prewarm_ms; })},
+      {"stale_hold_s", dbl_at([](NativeOptions* o) { return &o->cfg.stale_hold_s; })},
       {"hide_empty_contexts", bool_at([](NativeOptions* o) { return &o->cfg.hide_empty_contexts; })},
       {"mfma_exclusive_window_s", dbl_at([](NativeOptions* o) { return &o->cfg.mfma_exclusive_window_s; })},
       {"sample_threads", int_at([](NativeOptions* o) { return &o->cfg.sample_threads; })},
@@ -492,10 +500,7 @@ std::string options_json(const NativeOptions& o) {
   S("backend", c.backend);
   B("fast_path", c.fast_path);
   S("sysfs_root", c.sysfs_root);
-  key("devices");
-  s += "[";
-  for (size_t i = 0; i < c.devices.size(); ++i) s += (i ? ", " : "") + std::to_string(c.devices[i]);
-  s += "]";
+  L("devices", c.devices);
   N("interval", c.interval_s);
   B("processes", c.processes);
   N("link_every", c.link_every);
@@ -504,6 +509,7 @@ std::string options_json(const NativeOptions& o) {
   B("ras_async", c.ras_async);
   N("occ_samples", c.occ_samples);
   N("prewarm_ms", c.prewarm_ms);
+  N("stale_hold_s", c.stale_hold_s);
   B("hide_empty_contexts", c.hide_empty_contexts);
   N("mfma_exclusive_window_s", c.mfma_exclusive_window_s);
   N("sample_threads", c.sample_threads);

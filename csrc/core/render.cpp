@@ -735,6 +735,13 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       f.add(hl, static_cast<double>(s.stale_samples));
     }
     {
+      Family f(o, "gpumon_frozen_samples_total",
+               "Stale device samples whose table had not advanced for longer than stale_hold_s: the SMU stopped "
+               "refreshing it, and the interval rates were withheld.",
+               "counter");
+      f.add(hl, static_cast<double>(s.frozen_samples));
+    }
+    {
       Family f(o, "gpumon_hidden_gpu_contexts",
                "Processes with a GPU context but no VRAM and no resident waves in the last tick, left out of the "
                "pod_gpu rows (hide_empty_contexts).",

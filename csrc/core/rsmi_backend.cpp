@@ -123,24 +123,28 @@ bool RocmSmiBackend::init(std::string* err) {
   uint32_t n = 0;
   t_->rsmi_num_monitor_devices(&n);
   for (uint32_t i = 0; i < n; ++i) {
-    if (!keep(static_cast<int>(i))) continue;
-    DeviceStatic d;
-    d.index = static_cast<int>(devs_.size());
-    d.hip_id = static_cast<int>(i);  // rsmi enumeration follows the KFD node order
-    d.gpu_id = std::to_string(i);
     char buf[256] = {0};
-    if (t_->rsmi_dev_name_get && t_->rsmi_dev_name_get(i, buf, sizeof buf) == RSMI_STATUS_SUCCESS) d.model = buf;
-    memset(buf, 0, sizeof buf);
-    if (t_->rsmi_dev_serial_number_get && t_->rsmi_dev_serial_number_get(i, buf, sizeof buf) == RSMI_STATUS_SUCCESS)
-      d.serial = buf;
     uint64_t bdf = 0;
+    std::string bdf_s;
     if (t_->rsmi_dev_pci_id_get && t_->rsmi_dev_pci_id_get(i, &bdf) == RSMI_STATUS_SUCCESS) {
       // rsmi BDFID: domain[63:32] bus[15:8] device[7:3] function[2:0]
       snprintf(buf, sizeof buf, "%04llx:%02llx:%02llx.%llx", static_cast<unsigned long long>(bdf >> 32),
                static_cast<unsigned long long>((bdf >> 8) & 0xFF), static_cast<unsigned long long>((bdf >> 3) & 0x1F),
                static_cast<unsigned long long>(bdf & 0x7));
-      d.bdf = buf;
+      bdf_s = buf;
     }
+    // rsmi's index is the hip_id: its enumeration follows the KFD node order, as HIP's does
+    if (!keep(static_cast<int>(i), bdf_s)) continue;
+    DeviceStatic d;
+    d.index = static_cast<int>(devs_.size());
+    d.hip_id = static_cast<int>(i);
+    d.gpu_id = std::to_string(i);
+    d.bdf = bdf_s;
+    memset(buf, 0, sizeof buf);
+    if (t_->rsmi_dev_name_get && t_->rsmi_dev_name_get(i, buf, sizeof buf) == RSMI_STATUS_SUCCESS) d.model = buf;
+    memset(buf, 0, sizeof buf);
+    if (t_->rsmi_dev_serial_number_get && t_->rsmi_dev_serial_number_get(i, buf, sizeof buf) == RSMI_STATUS_SUCCESS)
+      d.serial = buf;
     uint64_t uid = 0;
     if (t_->rsmi_dev_unique_id_get && t_->rsmi_dev_unique_id_get(i, &uid) == RSMI_STATUS_SUCCESS) {
       snprintf(buf, sizeof buf, "%016llx", static_cast<unsigned long long>(uid));

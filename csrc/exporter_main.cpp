@@ -33,7 +33,7 @@ static void usage() {
   fprintf(stderr,
           "usage: gpumon-exporter [--config FILE] [--print-config] [--once]\n"
           "                       [--backend auto|amdsmi|rocm_smi|mock[:k=v,..]] [--interval SEC]\n"
-          "                       [--listen ADDR:PORT] [--host NAME] [--devices 0,1,..] [--no-fast-path]\n"
+          "                       [--listen ADDR:PORT] [--host NAME] [--devices 0,1|BDF,..] [--no-fast-path]\n"
           "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--pod-labels KEY,KEY..]\n"

@@ -17,6 +17,10 @@ void check(int err, const char* what);  // throws std::runtime_error on a HIP er
 int device_count();
 std::string device_arch(int dev);
 int device_cu_count(int dev);
+// PCI address of a HIP ordinal ("0000:75:00.0", hipDeviceGetPCIBusId): how a process that sees a
+// subset of the node (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES) names its GPUs to the exporter,
+// whose hip_id is node-wide (gpumon/parallel/devmap.py).
+std::string device_pci_bus_id(int dev);
 
 // --- numerics-testable launches on caller-provided device pointers / streams -------------------
 // C[32x32] (fp32, row-major) = iters * A[32x16] @ B[16x32] (bf16, row-major), one wave.

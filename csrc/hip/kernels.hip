@@ -44,6 +44,12 @@ std::string device_arch(int dev) {
   return p.gcnArchName;
 }
 
+std::string device_pci_bus_id(int dev) {
+  char buf[64] = {0};
+  check(hipDeviceGetPCIBusId(buf, sizeof buf, dev), "hipDeviceGetPCIBusId");
+  return buf;
+}
+
 int device_cu_count(int dev) {
   hipDeviceProp_t p;
   check(hipGetDeviceProperties(&p, dev), "hipGetDeviceProperties");

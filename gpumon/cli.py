@@ -222,7 +222,10 @@ def cmd_xgmi(args) -> int:
         pairs = [(a, b) for a in range(n) for b in range(n) if a != b]
     else:
         pairs = [tuple(int(x) for x in p.split(":")) for p in args.pairs.split(",")]
-    ex = _core().Exporter({"backend": args.backend, "devices": list(range(n)), "serve_http": False,
+    from .parallel.devmap import hip_bdfs, index_of, match
+
+    bdfs = hip_bdfs(range(n))  # the exporter samples these GPUs, named by PCI address (devmap.py)
+    ex = _core().Exporter({"backend": args.backend, "devices": [bdfs[k] for k in range(n)], "serve_http": False,
                            "interval_s": args.interval, "link_every": 1, "processes": False})
     err = ex.start()
     if err:
@@ -230,8 +233,9 @@ def cmd_xgmi(args) -> int:
         return 1
     ok = True
     try:
+        idx = index_of(match(bdfs, ex.statics()))
         for src, dst in pairs:
-            r = validate_pair(ex, src, dst, seconds=args.seconds, interval=args.interval)
+            r = validate_pair(ex, src, dst, seconds=args.seconds, interval=args.interval, index_of=idx)
             ok &= r["peer_matches"]
             print(json.dumps(r), flush=True)
     finally:

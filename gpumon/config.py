@@ -34,7 +34,7 @@ class Config:
     rocm_smi_lib: str = ""                # librocm_smi64 override (rocm_smi backend / auto fallback)
     fast_path: bool = True                # amdsmi: hot per-tick reads straight from sysfs/KFD
     sysfs_root: str = "/sys"
-    devices: List[int] = field(default_factory=list)
+    devices: List[str] = field(default_factory=list)  # hip ids ("3") and / or PCI BDFs ("0000:75:00.0")
     interval: float = 1.0                 # seconds; 0.1 = 10 Hz stress config
     processes: bool = True
     link_every: int = 600                 # ticks between link-metrics refreshes (+ whenever a link's state changes)
@@ -45,6 +45,7 @@ class Config:
     mfma_exclusive_window_s: float = 5.0  # pod MFMA util only when no other process had waves in the last 5 ticks and this many seconds
     occ_samples: int = 20                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
     prewarm_ms: float = 3.0               # device workers wake the firmware-table path this long before each tick (0 = off)
+    stale_hold_s: float = 0.1             # a repeated firmware table keeps the last rates only while it is this old (then: invalid)
     sample_threads: int = -1              # -1 = one worker per GPU (parallel + watchdog); 0 = sequential
     rt_priority: int = 0                  # SCHED_FIFO priority of the sampler + device workers (needs CAP_SYS_NICE)
     device_timeout_s: float = 2.0         # a device call still running after this is exported as hung
@@ -135,7 +136,7 @@ class Config:
             "rocm_smi_lib": self.rocm_smi_lib,
             "fast_path": self.fast_path,
             "sysfs_root": self.sysfs_root,
-            "devices": list(self.devices),
+            "devices": [str(x) for x in self.devices],
             "interval_s": float(self.interval),
             "processes": self.processes,
             "link_every": int(self.link_every),
@@ -144,6 +145,7 @@ class Config:
             "ras_async": bool(self.ras_async),
             "occ_samples": int(self.occ_samples),
             "prewarm_ms": float(self.prewarm_ms),
+            "stale_hold_s": float(self.stale_hold_s),
             "hide_empty_contexts": bool(self.hide_empty_contexts),
             "mfma_exclusive_window_s": float(self.mfma_exclusive_window_s),
             "sample_threads": int(self.sample_threads),
@@ -273,7 +275,7 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--config", default=os.environ.get("GPUMON_CONFIG", ""), help="YAML config file")
     p.add_argument("--backend", help=f"amdsmi | rocm_smi | mock[:gpus=N,...] | auto (default {d.backend}; "
                    "auto = amdsmi, falling back to rocm_smi)")
-    p.add_argument("--devices", help="comma-separated hip ids to monitor (default all)")
+    p.add_argument("--devices", help="comma-separated hip ids and / or PCI BDFs to monitor (default all)")
     p.add_argument("--interval", type=float, help=f"sampling interval seconds (default {d.interval})")
     p.add_argument("--listen", help=f"ADDR:PORT for /metrics (default {d.listen})")
     p.add_argument("--host", help="node name label (default $NODE_NAME, then hostname)")

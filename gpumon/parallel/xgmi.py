@@ -12,7 +12,7 @@ Neither is used by the exporter itself; they are validation load only.
 from __future__ import annotations
 
 import time
-from typing import Optional
+from typing import Dict, Optional
 
 
 def allreduce_step(buf, group=None) -> float:
@@ -100,16 +100,30 @@ def _median(xs):
 
 
 def validate_pair(ex, src: int, dst: int, copier_factory=None, seconds: float = 2.0,
-                  interval: float = 0.1) -> dict:
+                  interval: float = 0.1, index_of: Optional[Dict[int, int]] = None) -> dict:
     """Copy src -> dst for ``seconds`` while the exporter ``ex`` samples both devices. Reports the
     copy bandwidth, the link on ``src`` whose write counter moved most (the mode over the sampled
     ticks), the median exporter rate on that link (``src_link_tx_GBps``) and its ratio to the copy
     rate (``tx_vs_copy``), the same on the receiving side, the peer BDF the exporter attributes to
     the src link and whether it is ``dst``'s BDF (``peer_matches``). The first tick after the
-    copy starts is skipped: its rate spans time before the copy."""
+    copy starts is skipped: its rate spans time before the copy.
+
+    ``src`` / ``dst`` are HIP ordinals (what the copier loads). ``index_of`` maps them to the
+    exporter's device indices; by default they are paired by PCI BDF (gpumon/parallel/devmap.py)
+    when the real copier runs, and taken as equal for an injected ``copier_factory`` (mock)."""
+    if index_of is None:
+        if copier_factory is None:
+            from .devmap import exporter_rows
+            from .devmap import index_of as _index_of
+
+            index_of = _index_of(exporter_rows(ex, sorted({src, dst})))
+        else:
+            index_of = {src: src, dst: dst}
+    si, di = index_of[src], index_of[dst]
     statics = {s["index"]: s for s in ex.statics()}
     copier = (copier_factory or PeerCopier)(src, dst)
-    result = {"src": src, "dst": dst}
+    result = {"src": src, "dst": dst, "src_gpu_id": statics.get(si, {}).get("gpu_id"),
+              "dst_gpu_id": statics.get(di, {}).get("gpu_id")}
     bw, tx, rx = [], [], []  # per poll: copy B/s; (link, B/s) busiest on src write / dst read
     try:
         bw_first = copier.run(min(interval * 2, 1.0))  # ramp: the tick spanning the start is discarded
@@ -119,10 +133,10 @@ def validate_pair(ex, src: int, dst: int, copier_factory=None, seconds: float = 
         while time.perf_counter() < stop:
             bw.append(copier.run(min(interval * 2, max(0.05, stop - time.perf_counter()))))
             r = ex.rates()
-            if src < len(r) and r[src].get("valid"):
-                tx.append(busiest_link(r[src], "xgmi_wr_Bps"))
-            if dst < len(r) and r[dst].get("valid"):
-                rx.append(busiest_link(r[dst], "xgmi_rd_Bps"))
+            if si < len(r) and r[si].get("valid"):
+                tx.append(busiest_link(r[si], "xgmi_wr_Bps"))
+            if di < len(r) and r[di].get("valid"):
+                rx.append(busiest_link(r[di], "xgmi_rd_Bps"))
     finally:
         close = getattr(copier, "close", None)
         if close:
@@ -143,9 +157,9 @@ def validate_pair(ex, src: int, dst: int, copier_factory=None, seconds: float = 
     result["dst_link"], result["dst_link_rx_GBps"] = dl, round(dv / 1e9, 2)
     result["tx_vs_copy"] = round(sv / copy_bps, 3) if copy_bps > 0 else None
     result["rx_vs_copy"] = round(dv / copy_bps, 3) if copy_bps > 0 else None
-    peer = link_peer_bdf(samples[src], sl) if src < len(samples) else ""
+    peer = link_peer_bdf(samples[si], sl) if si < len(samples) else ""
     result["src_link_peer_bdf"] = peer
-    result["dst_bdf"] = statics.get(dst, {}).get("bdf", "")
+    result["dst_bdf"] = statics.get(di, {}).get("bdf", "")
     result["peer_matches"] = bool(peer) and peer.lower() == result["dst_bdf"].lower()
     return result
 

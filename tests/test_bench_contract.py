@@ -99,3 +99,44 @@ def test_bench_runs_without_torch():
     assert r.returncode == 0, r.stderr[-2000:]
     (line,) = _json_lines(r.stdout)
     _check(line, 1, 2, 1)
+
+
+def test_value_counts_fresh_samples_only():
+    """`value` is fresh device samples/s. A mock SMU refreshing at 50 Hz sampled
+    every 5 ms repeats most tables: value stays near 50 per GPU while the exporter took ~200 samples/s,
+    and both counts are in the line."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "200", "--warmup", "2",
+                        "--interval", "0.005", "--idle-s", "0", "--capacity-s", "0", "--scrape-rate", "50",
+                        "--backend", "mock:gpus=1,mode=load,firmware_hz=50"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (d,) = _json_lines(r.stdout)
+    assert d["value"] <= 50 * 1.15, d["value"]
+    assert d["samples_total"] >= 3 * d["value"] * d["ms_per_step"] * d["steps"] / 1e3
+    assert d["stale_samples"] == d["samples_total"] - round(d["value"] * d["ms_per_step"] * d["steps"] / 1e3)
+    assert d["devices"] == [{"hip_ordinal": 0, "bdf": "0000:05:00.0", "gpu_id": "0"}]
+    assert d["device_check"]["ok"]
+
+
+@pytest.mark.slow
+def test_bench_eight_ranks_exact_scale_command():
+    """the driver's SCALE command shape at N=8 (torchrun, one rank per GPU, no extra
+    flags) over gloo + the mock backend: one line from rank 0 with 8 sampled devices, each HIP
+    ordinal paired with a distinct device, and the whole-node rate N / interval."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(29000 + os.getpid() % 400),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    _check(d, 8, 3, 1)
+    assert d["sampled_devices"] == 8 and d["config"]["interval_s"] == 1.0
+    assert [x["hip_ordinal"] for x in d["devices"]] == list(range(8))
+    assert len({x["gpu_id"] for x in d["devices"]}) == 8 and d["device_check"]["ok"]
+    assert d["value"] == pytest.approx(8.0, rel=0.05)

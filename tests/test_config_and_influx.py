@@ -45,7 +45,7 @@ def test_yaml_env_flag_precedence(tmp_path):
     y = tmp_path / "c.yaml"
     y.write_text("gpumon:\n  interval: 5\n  listen: 0.0.0.0:9000\n  devices: [0, 2]\n  opt_in_label: a=b\n")
     c = _ns(["--config", str(y)], env={})
-    assert (c.interval, c.listen, c.devices, c.opt_in_label) == (5.0, "0.0.0.0:9000", [0, 2], "a=b")
+    assert (c.interval, c.listen, c.devices, c.opt_in_label) == (5.0, "0.0.0.0:9000", ["0", "2"], "a=b")
     c = _ns(["--config", str(y)], env={"GPUMON_INTERVAL": "2"})
     assert c.interval == 2.0
     c = _ns(["--config", str(y), "--interval", "0.1"], env={"GPUMON_INTERVAL": "2"})

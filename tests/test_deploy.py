@@ -212,29 +212,21 @@ def test_copy_set_check_catches_an_outside_prerequisite(tmp_path):
     assert r.returncode != 0 and "tools/perf_snapshot_probe.hip" in r.stderr, (r.returncode, r.stderr[-500:])
 
 
-def _control_plane_metric_names():
-    """Series of the native metadata pollers, from an exporter pointed at the fake kubelet (CRI +
-    PodResources) and a fake Docker daemon."""
-    from gpumon import core
-    from oracles.attribution.fake_kubelet import FakeKubelet
-    from test_docker import FakeDocker
+def _product_families():
+    """Every family the native exporter emits in the metric reference's configurations (mock with
+    full tables, CRI / PodResources / Docker / kubelet-files pollers, Influx push, on-device samplers
+    through the helper, the amdsmi backend): tools/gen_metrics_doc.py collect()."""
+    import importlib.util
 
-    d = f"/tmp/gpumon-alerts-{os.getpid()}"
-    os.makedirs(d, exist_ok=True)
-    with FakeKubelet(podres_socket=f"{d}/kubelet.sock", cri_socket=f"{d}/cri.sock") as k, \
-            FakeDocker(f"{d}/docker.sock", []) as dk:
-        ex = core().Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0,
-                              "cri_socket": k.cri_socket, "pod_resources_socket": k.podres_socket,
-                              "docker_socket": dk.path})
-        ex.start()
-        try:
-            ex.tick()
-            fam = promtext.parse(ex.metrics_text())
-        finally:
-            ex.stop()
-    names = {n for n in fam if n.startswith(("gpumon_cri", "gpumon_podresources", "gpumon_docker"))}
-    assert {"gpumon_cri_up", "gpumon_podresources_up", "gpumon_docker_up"} <= names, names
-    return names
+    from conftest import make_locked
+
+    make_locked("fakes")
+    spec = importlib.util.spec_from_file_location("gen_metrics_doc", os.path.join(ROOT, "tools", "gen_metrics_doc.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    fams = mod.collect()
+    assert {"gpumon_cri_up", "gpumon_podresources_up", "gpumon_docker_up", "gpumon_kubelet_files_up"} <= set(fams)
+    return set(fams)
 
 
 def test_alert_and_recording_rules_resolve(mock_exporter):
@@ -252,8 +244,7 @@ def test_alert_and_recording_rules_resolve(mock_exporter):
     ex.tick()
     fam = promtext.parse(ex.metrics_text())
     produced = {n for f, v in fam.items() for n in [f] + [s[0] for s in v["samples"]]}
-    produced |= _plugin_metric_names()  # the on-device samplers' series (PMC, probe, helper)
-    produced |= _control_plane_metric_names()  # CRI / PodResources / Docker pollers
+    produced |= _product_families()  # on-device samplers, metadata pollers, Influx push, amdsmi backend
     words = {"sum", "by", "count", "rate", "increase", "delta", "avg", "max", "time", "host", "namespace", "podname",
              "gpu_id", "user_name", "on"}
     exprs = [r["expr"] for g in rule["spec"]["groups"] for r in g["rules"]]

@@ -91,6 +91,36 @@ def test_metrics_doc_is_current():
     assert r.returncode == 0, "docs/metrics.md is stale: run python tools/gen_metrics_doc.py"
 
 
+# String literals in csrc/ that look like family names but are not: label keys, libamd_smi call
+# names (gpumon_backend_call_* labels), a sysfs file name, and the on-device plugins' dlsym'd ABI
+# symbols (csrc/plugins/ondevice_abi.h).
+NOT_FAMILIES = {"gpu_id", "gpu_uuid", "gpu_metrics", "gpu_activity", "gpu_vram_bad_pages"}
+NOT_FAMILY_PREFIXES = ("gpumon_pmc_abi", "gpumon_pmc_agent", "gpumon_pmc_init", "gpumon_pmc_read_running",
+                       "gpumon_pmc_sample_many", "gpumon_pmc_stop_running", "gpumon_probe_abi", "gpumon_probe_create",
+                       "gpumon_probe_destroy", "gpumon_probe_device_count", "gpumon_probe_launch", "gpumon_probe_wait")
+
+
+def test_metrics_doc_matches_the_product():
+    """docs/metrics.md lists exactly what the native exporter emits. Each row's
+    family is a literal in the C++ sources (nothing harvested from test oracles), and each
+    family-shaped literal in csrc/core and csrc/plugins is a row, unless it is a declared
+    non-family string."""
+    import glob
+    import re
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    doc = open(os.path.join(root, "docs", "metrics.md")).read()
+    rows = set(re.findall(r"^\| `([a-z0-9_]+)` \|", doc, re.M))
+    src = ""
+    for f in glob.glob(os.path.join(root, "csrc", "core", "*.cpp")) + glob.glob(os.path.join(root, "csrc", "plugins", "*.cpp")):
+        src += open(f).read()
+    literals = set(re.findall(r'"((?:gpu|gpumon|node_gpu|pod_gpu|process)_[a-z0-9_]+)"', src))
+    assert rows and rows <= literals, sorted(rows - literals)
+    families = {x for x in literals if x not in NOT_FAMILIES and not x.startswith(NOT_FAMILY_PREFIXES)}
+    assert families <= rows, sorted(families - rows)
+    assert not any(x in rows for x in ("gpumon_control_plane_up", "gpumon_control_plane_refresh_seconds"))
+
+
 def test_configuration_doc_is_current():
     import importlib.util
 

@@ -45,6 +45,21 @@ def test_device_is_gfx950(H):
     assert H.device_cu_count(0) == 256
 
 
+def test_hip_ordinal_and_exporter_agree_on_the_bdf(core, H):
+    """HIP ordinal 0's hipDeviceGetPCIBusId names the device libamd_smi samples when
+    the exporter is filtered by that BDF (gpumon/parallel/devmap.py): the pairing bench.py uses."""
+    from gpumon.parallel.devmap import hip_bdfs, match
+
+    b = hip_bdfs([0])
+    ex = _exporter(core, devices=[b[0]])
+    try:
+        (row,) = match(b, ex.statics())
+    finally:
+        ex.stop()
+    assert row["bdf"] == b[0] and row["index"] == 0, (row, b)
+    print(f"\nHIP ordinal 0 -> {b[0]} -> exporter gpu_id {row['gpu_id']}")
+
+
 def test_amdsmi_static_and_sample_sane(core, torch_gpu):
     ex = _exporter(core)
     try:

@@ -41,19 +41,22 @@ needs2 = pytest.mark.skipif(N < 2, reason=f"needs >= 2 GPUs (found {N})")
 @needs2
 def test_every_peer_link_maps_to_its_bdf_and_rate():
     from gpumon import core
+    from gpumon.parallel.devmap import hip_bdfs, index_of, match
     from gpumon.parallel.xgmi import rate_within, validate_pair
 
     n = min(N, 8)
-    ex = core().Exporter({"backend": "amdsmi", "devices": list(range(n)), "serve_http": False,
+    bdfs = hip_bdfs(range(n))  # HIP ordinal -> PCI address: the exporter samples exactly these
+    ex = core().Exporter({"backend": "amdsmi", "devices": [bdfs[k] for k in range(n)], "serve_http": False,
                           "interval_s": 0.1, "link_every": 1, "processes": False})
     assert ex.start() == ""
     bad = []
     try:
+        idx = index_of(match(bdfs, ex.statics()))
         for src in range(n):
             for dst in range(n):
                 if src == dst:
                     continue
-                r = validate_pair(ex, src, dst, seconds=0.6, interval=0.1)
+                r = validate_pair(ex, src, dst, seconds=0.6, interval=0.1, index_of=idx)
                 if not (r["peer_matches"] and rate_within(r, 0.15)):
                     bad.append(r)
     finally:
@@ -73,6 +76,7 @@ def test_single_process_bench_loads_every_gpu_and_sees_the_copy_ring():
     d = _bench([sys.executable, "bench.py", "--gpus", str(n), "--steps", "5", "--warmup", "2",
                 "--interval", "0.5", "--link-check-s", "0"], 400)
     assert d["sampled_devices"] == n and d["scrape_errors"] == 0
+    assert sorted(r["hip_ordinal"] for r in d["devices"]) == list(range(n)) and d["device_check"]["ok"], d["devices"]
     assert all(g["tflops"] > 500 for g in d["load_per_gpu"]), d["load_per_gpu"]
     x = d["xgmi"]
     assert x["mode"] == "peer_copy_ring"

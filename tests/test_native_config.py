@@ -84,7 +84,7 @@ def test_rich_file_env_and_flag_precedence(tmp_path):
     assert r.returncode == 0, r.stderr
     n = json.loads(r.stdout)
     _same(n, _py(str(p)))
-    assert n["devices"] == [0, 2, 5] and n["dra_drivers"] == [] and n["gzip"] is False
+    assert n["devices"] == ["0", "2", "5"] and n["dra_drivers"] == [] and n["gzip"] is False
     assert n["pod_label_allowlist"] == ["team", "app.kubernetes.io/name"]
     assert n["influx_url"] == "http://influx:8086/write?db=k8s#not-a-comment"
     assert "control_plane" in r.stderr  # the ignored key is named
@@ -94,10 +94,10 @@ def test_rich_file_env_and_flag_precedence(tmp_path):
     r = _print("--config", str(p), "--interval", "0.5", env=env)
     assert r.returncode == 0, r.stderr
     n = json.loads(r.stdout)
-    assert n["interval"] == 0.5 and n["devices"] == [1, 3] and n["host"] == "gpu-node-7"
+    assert n["interval"] == 0.5 and n["devices"] == ["1", "3"] and n["host"] == "gpu-node-7"
     assert n["influx_url"] == "http://other/write"
     py = _py(str(p), env)
-    assert py["devices"] == [1, 3] and py["influx_url"] == "http://other/write" and py["host"] == "gpu-node-7"
+    assert py["devices"] == ["1", "3"] and py["influx_url"] == "http://other/write" and py["host"] == "gpu-node-7"
 
 
 def test_config_env_var_names_the_file(tmp_path):

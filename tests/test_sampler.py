@@ -103,6 +103,42 @@ def test_stale_firmware_table_detected(mock_exporter):
     assert promtext.one(fam, "gpumon_stale_samples_total") >= 1
 
 
+def test_frozen_firmware_table_withholds_rates(mock_exporter):
+    """an SMU that stops refreshing gpu_metrics (same firmware timestamp tick after tick)
+    must not keep exporting the last window's power / activity / xGMI rates forever. Repeats are
+    held only while the table is younger than stale_hold_s; then the rates go invalid and
+    gpu_metrics_table_frozen is 1 -- on that GPU only -- until the table moves again."""
+    ex = mock_exporter(backend="mock:gpus=2,mode=load,firmware_hz=50", stale_hold_s=0.1)
+    time.sleep(0.05)
+    ex.tick()
+    time.sleep(0.05)
+    ex.tick()
+    assert all(r["valid"] for r in ex.rates())
+    ex.mock_set_firmware_frozen(0, True)
+    time.sleep(0.05)
+    ex.tick()  # the repeat is young (<= 0.1 s since the table last moved): the last rates are held
+    assert not ex.samples()[0]["fresh"] and ex.rates()[0]["valid"]
+    for _ in range(3):  # 1 Hz-like gaps: a repeat of a table this old means the SMU stopped
+        time.sleep(0.06)
+        ex.tick()
+    r = ex.rates()
+    assert not r[0]["valid"] and r[1]["valid"]
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_metrics_table_frozen", gpu_id="0") == 1
+    assert promtext.one(fam, "gpu_metrics_table_frozen", gpu_id="1") == 0
+    assert promtext.one(fam, "gpu_metrics_table_age_seconds", gpu_id="0") > 0.1
+    assert promtext.one(fam, "gpu_metrics_table_age_seconds", gpu_id="1") == 0
+    assert not promtext.values(fam, "gpu_power_interval_watts", gpu_id="0")  # withheld, not frozen at a value
+    assert promtext.values(fam, "gpu_power_interval_watts", gpu_id="1")
+    assert promtext.one(fam, "gpumon_frozen_samples_total") >= 2
+    ex.mock_set_firmware_frozen(0, False)
+    time.sleep(0.05)
+    ex.tick()
+    assert ex.rates()[0]["valid"]
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_metrics_table_frozen", gpu_id="0") == 0
+
+
 def test_health_goes_503_when_sampler_stalls(core):
     import http.client
 
@@ -185,6 +221,18 @@ def test_device_filter(core):
     st = ex.statics()
     ex.stop()
     assert [s["gpu_id"] for s in st] == ["1", "3"]
+
+
+def test_device_filter_by_bdf(core):
+    """Devices named by PCI address (what a HIP process under HIP_VISIBLE_DEVICES knows), any
+    case, domain optional, mixed with hip ids; an entry that matches nothing selects nothing."""
+    ex = core.Exporter({"backend": "mock:gpus=8", "serve_http": False, "interval_s": 0,
+                        "devices": ["0000:65:00.0", "A5:00.0", 7, "0000:99:00.0"]})
+    ex.start()
+    st = ex.statics()
+    ex.stop()
+    assert [(s["gpu_id"], s["bdf"]) for s in st] == [("3", "0000:65:00.0"), ("5", "0000:a5:00.0"),
+                                                    ("7", "0000:e5:00.0")]
 
 
 def test_hung_device_is_isolated_by_the_watchdog(core):
