@@ -330,6 +330,8 @@ PYBIND11_MODULE(_core, m) {
   m.doc() = "gpumon C++ core (MI355X telemetry exporter)";
 
   m.def("set_log_level", [](int lvl) { g_log_level.store(lvl); });
+  m.def("glob_match", [](const std::string& glob, const std::string& name) { return glob_match(glob.c_str(), name.c_str()); },
+        py::arg("glob"), py::arg("name"), "the family-filter glob rule (render.h)");
   m.def("parse_cgroup", [](const std::string& text) {
     CgroupInfo c = parse_cgroup(text);
     py::dict d;

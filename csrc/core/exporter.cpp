@@ -1383,8 +1383,19 @@ std::string url_decode(const std::string& s) {
   return o;
 }
 
-// include=a,b&exclude=c (each repeatable): the family globs of a per-request filter
-bool parse_filter_query(const std::string& q, std::vector<std::string>* inc, std::vector<std::string>* exc) {
+// Bounds on a per-request filter: the globs come from any client that can reach the port, and a
+// filter runs on an HTTP loop thread. Matching is O(glob x name) (glob_match), so these keep one
+// request's work to ~32 globs x 128 chars x ~150 family names.
+constexpr size_t kMaxFilterQuery = 8192, kMaxFilterGlobs = 32, kMaxGlobLen = 128;
+
+// include=a,b&exclude=c (each repeatable): the family globs of a per-request filter.
+// 1 = a filter, 0 = no filter keys, -1 = over the bounds above (*err says which).
+int parse_filter_query(const std::string& q, std::vector<std::string>* inc, std::vector<std::string>* exc,
+                       std::string* err) {
+  if (q.size() > kMaxFilterQuery) {
+    *err = "query longer than " + std::to_string(kMaxFilterQuery) + " bytes";
+    return -1;
+  }
   bool any = false;
   for (const auto& kv : split(q, '&')) {
     const size_t eq = kv.find('=');
@@ -1393,10 +1404,20 @@ bool parse_filter_query(const std::string& q, std::vector<std::string>* inc, std
     std::vector<std::string>* dst = k == "include" ? inc : k == "exclude" ? exc : nullptr;
     if (!dst) continue;
     any = true;
-    for (const auto& g : split(url_decode(kv.substr(eq + 1)), ','))
-      if (!g.empty()) dst->push_back(g);
+    for (const auto& g : split(url_decode(kv.substr(eq + 1)), ',')) {
+      if (g.empty()) continue;
+      if (g.size() > kMaxGlobLen) {
+        *err = "glob longer than " + std::to_string(kMaxGlobLen) + " bytes";
+        return -1;
+      }
+      dst->push_back(g);
+      if (inc->size() + exc->size() > kMaxFilterGlobs) {
+        *err = "more than " + std::to_string(kMaxFilterGlobs) + " globs";
+        return -1;
+      }
+    }
   }
-  return any;
+  return any ? 1 : 0;
 }
 
 }  // namespace
@@ -1412,7 +1433,8 @@ std::shared_ptr<const Exporter::Filtered> Exporter::filtered(const Snapshot& s, 
     if (it != filter_cache_.end() && (!gzip || !it->second->body_gz.empty())) return it->second;
   }
   std::vector<std::string> inc, exc;
-  parse_filter_query(query, &inc, &exc);
+  std::string err;
+  parse_filter_query(query, &inc, &exc, &err);  // handle_http validated it
   auto f = std::make_shared<Filtered>();
   filter_exposition(s.body, inc, exc, &f->body);
   if (gzip) gzip_compress(f->body, &f->body_gz, 1);
@@ -1432,7 +1454,14 @@ void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
     }
     resp->content_type = "text/plain; version=0.0.4; charset=utf-8";
     std::vector<std::string> inc, exc;
-    if (!req.query.empty() && parse_filter_query(req.query, &inc, &exc)) {
+    std::string err;
+    const int fq = req.query.empty() ? 0 : parse_filter_query(req.query, &inc, &exc, &err);
+    if (fq < 0) {
+      resp->status = 400;
+      resp->inline_body = "bad family filter: " + err + "\n";
+      return;
+    }
+    if (fq > 0) {
       // per-request family filter (e.g. a fast Prometheus job for node_gpu_* only)
       auto f = filtered(*s, req.query, req.accept_gzip && cfg_.gzip);
       if (req.accept_gzip && !f->body_gz.empty()) {

@@ -1,6 +1,5 @@
 #include "render.h"
 
-#include <fnmatch.h>
 
 #include <charconv>
 #include <cmath>
@@ -82,11 +81,76 @@ void escape_influx_field_str(const std::string& v, std::string* out) {
   }
 }
 
+namespace {
+// One pattern element at p against character c: advances *next past the element; false when c does
+// not match. A malformed class ('[' without ']') matches a literal '['.
+bool glob_one(const char* p, char c, const char** next) {
+  if (*p == '?') {
+    *next = p + 1;
+    return true;
+  }
+  if (*p == '[') {
+    const char* q = p + 1;
+    const bool neg = *q == '!' || *q == '^';
+    if (neg) ++q;
+    bool hit = false;
+    const char* first = q;
+    while (*q && (*q != ']' || q == first)) {
+      if (q[1] == '-' && q[2] && q[2] != ']') {
+        if (static_cast<unsigned char>(c) >= static_cast<unsigned char>(q[0]) &&
+            static_cast<unsigned char>(c) <= static_cast<unsigned char>(q[2]))
+          hit = true;
+        q += 3;
+      } else {
+        if (*q == c) hit = true;
+        ++q;
+      }
+    }
+    if (*q == ']') {
+      *next = q + 1;
+      return hit != neg;
+    }
+    *next = p + 1;  // no closing ']': literal
+    return c == '[';
+  }
+  if (*p == '\\' && p[1]) {
+    *next = p + 2;
+    return p[1] == c;
+  }
+  *next = p + 1;
+  return *p == c;
+}
+}  // namespace
+
+bool glob_match(const char* p, const char* s) {
+  const char* star = nullptr;  // pattern position after the last '*'
+  const char* mark = nullptr;  // name position that '*' is currently absorbing up to
+  while (*s) {
+    const char* next = nullptr;
+    if (*p == '*') {
+      while (*p == '*') ++p;
+      star = p;
+      mark = s;
+      continue;
+    }
+    if (*p && glob_one(p, *s, &next)) {
+      p = next;
+      ++s;
+      continue;
+    }
+    if (!star) return false;
+    p = star;  // let the last '*' absorb one more character and retry
+    s = ++mark;
+  }
+  while (*p == '*') ++p;
+  return *p == 0;
+}
+
 bool family_matches(const std::vector<std::string>& include, const std::vector<std::string>& exclude,
                     const char* name) {
   auto any = [name](const std::vector<std::string>& globs) {
     for (const auto& g : globs)
-      if (fnmatch(g.c_str(), name, 0) == 0) return true;
+      if (glob_match(g.c_str(), name)) return true;
     return false;
   };
   if (!include.empty() && !any(include)) return false;

@@ -118,8 +118,12 @@ struct RenderInput {
 
 // Whether render_prometheus emits family `name` under the input's include / exclude globs.
 bool family_selected(const RenderInput& in, const char* name);
+// Shell glob: '*', '?', '[abc]' / '[a-z]' / '[!x]' classes, '\\' escapes. Time O(|glob| x |name|)
+// (one backtrack point: the last '*'), never exponential -- request globs reach it from the
+// network, and glibc fnmatch recurses per '*' (ADVICE r3).
+bool glob_match(const char* glob, const char* name);
 // The same rule on plain lists: with a non-empty include list only matching names pass, then
-// exclude drops matching ones (shell globs).
+// exclude drops matching ones (glob_match).
 bool family_matches(const std::vector<std::string>& include, const std::vector<std::string>& exclude,
                     const char* name);
 // Filters a rendered exposition by family: every line from a family's "# HELP" up to the next one

@@ -227,3 +227,43 @@ def test_per_request_family_filter(mock_exporter):
         assert promtext.parse(_get(ex.port, "/metrics?include=gpu_up")[2].decode()).keys() == {"gpu_up"}
     st, _, body = _get(ex.port, "/metrics?foo=bar")
     assert st == 200 and set(promtext.parse(body.decode())) >= set(full) - {"gpumon_scrape_duration_seconds"}
+
+
+def test_glob_match_agrees_with_fnmatch(core):
+    """The native family-filter glob (render.cpp glob_match) follows shell-glob rules: same answers
+    as Python's fnmatchcase on '*', '?' and bracket classes, over random patterns and names."""
+    import fnmatch
+    import random
+
+    rnd = random.Random(4)
+    alphabet = "ab_"
+    atoms = ["*", "?", "a", "b", "_", "[ab]", "[!a]", "[a-b]", "**"]
+    names = ["".join(rnd.choice(alphabet) for _ in range(rnd.randint(0, 8))) for _ in range(60)]
+    names += ["gpu_xcd_busy_percent", "node_gpu_gpu_util", "gpumon_scrape_duration_seconds"]
+    pats = ["".join(rnd.choice(atoms) for _ in range(rnd.randint(0, 6))) for _ in range(300)]
+    pats += ["gpu_xcd_*", "node_gpu_*", "*_seconds", "gpu_?cd_*", "[gn]*_util", "*"]
+    bad = [(p, n) for p in pats for n in names if core.glob_match(p, n) != fnmatch.fnmatchcase(n, p)]
+    assert not bad, bad[:10]
+
+
+def test_pathological_filter_is_fast_and_oversized_filters_are_refused(mock_exporter):
+    """a '*a*a*a...*b' glob made glibc fnmatch backtrack exponentially on the HTTP loop.
+    The native matcher is linear in the name per star position; the longest allowed glob against
+    every family stays in milliseconds, and over-long / too many globs get a 400."""
+    import time
+
+    ex = mock_exporter(backend="mock:gpus=8")
+    ex.tick()
+    glob = ("*a" * 63) + "*b"  # 128 bytes, the per-glob limit
+    q = "include=" + ",".join([glob] * 32)  # 32 globs, the count limit ('*' needs no escaping)
+    t0 = time.perf_counter()
+    st, _, body = _get(ex.port, "/metrics?" + q)
+    assert st == 200 and time.perf_counter() - t0 < 1.0
+    st, _, body = _get(ex.port, "/metrics?include=" + "a" * 129)
+    assert st == 400 and b"glob longer than 128" in body
+    st, _, body = _get(ex.port, "/metrics?include=" + ",".join(["x*"] * 33))
+    assert st == 400 and b"more than 32 globs" in body
+    st, _, body = _get(ex.port, "/metrics?exclude=" + "x," * 4100)
+    assert st == 400 and b"query longer than" in body
+    st, _, _ = _get(ex.port, "/metrics?include=gpu_up")  # the loop is still serving
+    assert st == 200
