@@ -824,6 +824,7 @@ PYBIND11_MODULE(_core, m) {
              d["stale_samples"] = s.stale_samples;
              d["frozen_samples"] = s.frozen_samples;
              d["occupancy_reads"] = s.occupancy_reads;
+             d["occupancy_scan_failures"] = s.occupancy_scan_failures;
              d["hidden_contexts"] = s.hidden_contexts;
              d["rt_threads"] = s.rt_threads;
              d["overruns"] = s.overruns;
@@ -963,6 +964,7 @@ PYBIND11_MODULE(_core, m) {
       .def("mock_link_calls", [](Exporter& e, int dev) { return mock_of(e)->link_calls(dev); })
       .def("mock_set_link_fail",
            [](Exporter& e, int dev, bool fail) { mock_of(e)->set_link_fail(dev, fail); })
+      .def("mock_fail_scans", [](Exporter& e, int dev, int n) { mock_of(e)->fail_scans(dev, n); })
       .def("mock_set_firmware_frozen",
            [](Exporter& e, int dev, bool frozen) { mock_of(e)->set_firmware_frozen(dev, frozen); })
       .def("mock_set_occ_series",

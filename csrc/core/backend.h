@@ -208,6 +208,8 @@ class MockBackend : public Backend {
   void set_link_fail(int dev, bool fail);        // link-metrics reads of `dev` fail (links_read -1)
   // The fake SMU of `dev` stops refreshing its table (firmware timestamp and accumulators hold) / resumes.
   void set_firmware_frozen(int dev, bool frozen);
+  // The next `n` occupancy_scan() calls of `dev` fail as a transient error would (occupancy stays supported).
+  void fail_scans(int dev, int n);
   uint64_t calls(int dev) const;
   bool prewarm(int i) override;
   uint64_t prewarms(int dev) const;  // prewarm() calls
@@ -224,7 +226,8 @@ class MockBackend : public Backend {
   std::vector<char> link_down_;      // per dev * kMaxLinks
   std::vector<uint64_t> link_calls_;
   std::vector<char> link_fail_;
-  std::vector<int64_t> frozen_tick_;  // per dev: firmware tick the fake SMU is stuck at (-1 = running)
+  std::vector<int64_t> frozen_tick_;
+  std::vector<int> scan_fail_;       // per dev: occupancy scans still to fail  // per dev: firmware tick the fake SMU is stuck at (-1 = running)
   std::vector<uint64_t> calls_, prewarms_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
   std::vector<uint64_t> lim_acc_;  // per device x XCC x {ppt, thermal, any, low-util}

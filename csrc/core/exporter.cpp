@@ -87,7 +87,8 @@ static void read_process_stats(SelfStats* s);  // /proc/self figures (defined be
 
 static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_ptr<Exporter::DoneSignal> sig,
                             Backend* backend, int i, int64_t occ_period_ns,
-                            std::shared_ptr<std::atomic<uint64_t>> occ_reads, int rt_prio,
+                            std::shared_ptr<std::atomic<uint64_t>> occ_reads,
+                            std::shared_ptr<std::atomic<uint64_t>> scan_failures, int rt_prio,
                             std::shared_ptr<std::atomic<int>> rt_threads,
                             std::shared_ptr<std::atomic<int64_t>> next_tick, int64_t prewarm_ns) {
   set_thread_name("gpumon-dev" + std::to_string(i));
@@ -109,6 +110,10 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
   // a tenant that started since the last tick is read from then on, not from the next tick (a
   // 10 %-resident arrival otherwise had one read in its first interval).
   bool scan_ok = occ_on;
+  // A failed listing (a transient opendir / read error) is retried with a backoff (1 s doubling to
+  // 60 s), not latched off for the worker's life; only a backend that stopped supporting the read
+  // ends the scans. In between, the known pids are re-read as before.
+  int64_t scan_retry_at = 0, scan_backoff_ns = 1'000'000'000;
   // Every 4th sub-sample lists the directory (new tenants show up within 4 periods, 0.2 s at 1 Hz);
   // the others re-read the known pids only: a node-wide KFD listing per GPU per sub-sample would
   // cost P opens each time on a node with P GPU processes.
@@ -220,9 +225,21 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       }
       if (subsample) {
         lk.unlock();
-        const bool scan_turn = scan_ok && (n_sub++ % kScanEvery == 0);
-        if (scan_turn) scan_ok = backend->occupancy_scan(i, &scan);
-        if (scan_turn && scan_ok) {
+        const bool scan_turn = scan_ok && (n_sub++ % kScanEvery == 0) && mono_ns() >= scan_retry_at;
+        bool scanned = false;
+        if (scan_turn) {
+          scanned = backend->occupancy_scan(i, &scan);
+          scan_failures->fetch_add(scanned ? 0 : 1, std::memory_order_relaxed);
+          if (scanned) {
+            scan_backoff_ns = 1'000'000'000;
+          } else if (!backend->supports_occupancy(i)) {
+            scan_ok = false;
+          } else {
+            scan_retry_at = mono_ns() + scan_backoff_ns;
+            scan_backoff_ns = std::min<int64_t>(scan_backoff_ns * 2, 60'000'000'000);
+          }
+        }
+        if (scanned) {
           vals.assign(occ_pids.size(), kNaN);
           for (const OccRead& r : scan) {
             size_t k = std::find(occ_pids.begin(), occ_pids.end(), r.pid) - occ_pids.begin();
@@ -374,7 +391,8 @@ void Exporter::start_workers(int n) {
     const int64_t prewarm_ns = cfg_.interval_s >= 0.02 && cfg_.prewarm_ms > 0
                                    ? static_cast<int64_t>(std::min(cfg_.prewarm_ms, cfg_.interval_s * 250.0) * 1e6)
                                    : 0;
-    w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i, occ_ns, occ_reads_, cfg_.rt_priority,
+    w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i, occ_ns, occ_reads_, scan_failures_,
+                        cfg_.rt_priority,
                         rt_threads_, next_tick_ns_, prewarm_ns);
     workers_.push_back(std::move(w));
   }
@@ -1609,6 +1627,7 @@ SelfStats Exporter::self_stats() const {
   s.stale_samples = stale_;
   s.frozen_samples = frozen_;
   s.occupancy_reads = occ_reads_->load(std::memory_order_relaxed);
+  s.occupancy_scan_failures = scan_failures_->load(std::memory_order_relaxed);
   s.hidden_contexts = hidden_contexts_.load();
   s.rt_threads = rt_threads_->load();
   s.overruns = overruns_;

@@ -311,6 +311,7 @@ class Exporter {
   std::atomic<uint64_t> hidden_contexts_{0};  // empty GPU contexts left out of the last tick's rows
   // cu_occupancy sub-sample reads by the workers (shared: a detached worker may outlive a restart)
   std::shared_ptr<std::atomic<uint64_t>> occ_reads_ = std::make_shared<std::atomic<uint64_t>>(0);
+  std::shared_ptr<std::atomic<uint64_t>> scan_failures_ = std::make_shared<std::atomic<uint64_t>>(0);
   std::shared_ptr<std::atomic<int>> rt_threads_ = std::make_shared<std::atomic<int>>(0);  // SCHED_FIFO now
   mutable std::mutex proc_stats_mu_;  // /proc/self figures, refreshed after each tick's publish
   mutable SelfStats proc_stats_;

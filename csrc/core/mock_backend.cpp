@@ -74,6 +74,7 @@ bool MockBackend::init(std::string* err) {
   link_calls_.assign(n, 0);
   link_fail_.assign(n, 0);
   frozen_tick_.assign(n, -1);
+  scan_fail_.assign(n, 0);
   calls_.assign(n, 0);
   prewarms_.assign(n, 0);
   energy_.assign(n, 1000000);
@@ -382,6 +383,10 @@ bool MockBackend::occupancy_scan(int i, std::vector<OccRead>* out) {
   std::lock_guard<std::mutex> g(mu_);
   out->clear();
   if (!cfg_.occupancy || i < 0 || i >= static_cast<int>(devs_.size())) return false;
+  if (scan_fail_[i] > 0) {
+    --scan_fail_[i];
+    return false;
+  }
   const double util = has(forced_util_[i]) ? forced_util_[i]
                                            : mock_util(cfg_, devs_[i].hip_id, (mono_ns() - t0_ns_) * 1e-9);
   for (const auto& p : cfg_.procs)
@@ -445,6 +450,11 @@ void MockBackend::sample_links(int i, DeviceSample* out) {
   else if (cfg_.link_order == "rotate" && !es.empty()) std::rotate(es.begin(), es.begin() + 1, es.end());
   out->link_entries = std::move(es);
   out->links_read = 1;
+}
+
+void MockBackend::fail_scans(int dev, int n) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (dev >= 0 && dev < static_cast<int>(scan_fail_.size())) scan_fail_[dev] = n;
 }
 
 void MockBackend::set_firmware_frozen(int dev, bool frozen) {

@@ -824,6 +824,13 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       f.add(hl, static_cast<double>(s.occupancy_reads));
     }
     {
+      Family f(o, "gpumon_occupancy_scan_failures_total",
+               "Device-worker KFD process listings that failed (retried after 1 s, doubling to 60 s; the known "
+               "pids are re-read meanwhile).",
+               "counter");
+      f.add(hl, static_cast<double>(s.occupancy_scan_failures));
+    }
+    {
       Family f(o, "gpumon_tick_overruns_total", "Ticks that took longer than the interval.",
                "counter");
       f.add(hl, static_cast<double>(s.overruns));

@@ -198,6 +198,35 @@ def test_arrival_between_ticks_is_subsampled(mock_exporter):
     assert row["occ_samples"] >= 2, row
 
 
+def test_a_failed_process_listing_is_retried_not_latched_off(mock_exporter):
+    """one failed between-tick listing (a transient opendir error) used to end the scans
+    for the worker's life, so later arrivals were again read from their first tick only. Now the
+    listing is retried after a backoff (1 s first) and a tenant arriving after that is sub-sampled
+    between ticks as before; the failures are counted."""
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", interval_s=0.2, occ_samples=10, sample_threads=-1,
+                       mock={"procs": [{"pid": 7, "device": 0, "name": "train", "kfd_only": True}]})
+    ex.mock_set_occ_series(0, [100.0])
+    ex.mock_fail_scans(0, 2)
+    _wait_ticks(ex, 2)
+    deadline = time.time() + 5
+    while ex.self_stats()["occupancy_scan_failures"] < 1 and time.time() < deadline:
+        time.sleep(0.01)
+    assert ex.self_stats()["occupancy_scan_failures"] >= 1
+    time.sleep(3.5)  # past the backoff (1 s, then 2 s if the retry failed too)
+    ex.mock_set_procs([{"pid": 7, "device": 0, "name": "train", "kfd_only": True},
+                       {"pid": 9, "device": 0, "name": "newcomer", "kfd_only": True}])
+    deadline = time.time() + 10
+    row = None
+    while time.time() < deadline:
+        rows = {r["pid"]: r for r in ex.pod_rows() if not r["idle"]}
+        if "9" in rows:
+            row = rows["9"]
+            break
+        time.sleep(0.01)
+    assert row is not None and row["occ_samples"] >= 2, row
+    assert promtext.one(promtext.parse(ex.metrics_text()), "gpumon_occupancy_scan_failures_total") == 2
+
+
 def test_sharing_falls_back_to_vram_holders_without_occupancy(mock_exporter):
     """where KFD cu_occupancy is unreadable, gpu_active_processes counts the processes
     holding VRAM (source="vram") instead of going blank, and a sole VRAM holder is exclusive."""
