@@ -257,9 +257,14 @@ def main() -> int:
     ap.add_argument("--idle-s", type=float, default=-1.0,
                     help="untimed idle reference before the load starts: scrape p50/p99 + tick cost "
                          "(-1 = as long as the timed region: the same scrape count; 0 = off)")
+    ap.add_argument("--idle-spinners", type=int, default=0,
+                    help="DIAGNOSTIC: SCHED_IDLE busy loops during the idle reference (they take no CPU from "
+                         "runnable threads but keep CPUs out of idle states: isolates wake-from-idle latency)")
     ap.add_argument("--no-fast-path", action="store_true", help="read every value through libamd_smi")
     ap.add_argument("--rt-priority", type=int, default=1,
                     help="the DaemonSet's rt_priority (SCHED_FIFO sampler; stays normal without CAP_SYS_NICE)")
+    ap.add_argument("--http-rt-priority", type=int, default=1,
+                    help="the DaemonSet's http_rt_priority (SCHED_FIFO HTTP loops; normal without CAP_SYS_NICE)")
     ap.add_argument("--dist", action="store_true",
                     help="initialise torch.distributed (RCCL) even with one rank: rehearses the torchrun path "
                          "(process group, barriers, MAX over ranks) on a 1-GPU box")
@@ -343,6 +348,7 @@ def main() -> int:
         sampled = [ord_bdfs[k] for k in sorted(ord_bdfs)] if real and ord_bdfs else []
         cfg = Config(backend=backend, devices=sampled,
                      interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
+                     http_rt_priority=args.http_rt_priority,
                      enable_probe=args.probe and has_gpu, log_level="warn", fast_path=not args.no_fast_path,
                      sample_threads=args.sample_threads, rt_priority=args.rt_priority, prewarm_ms=args.prewarm_ms)
         mon = GpuMonitor(cfg, control_plane=False).start()
@@ -367,11 +373,23 @@ def main() -> int:
     idle = None
     if rank == 0 and args.idle_s > 0:
         mon.wait_ticks(1, timeout_s=args.interval * 5 + 30)
+        spin = []
+        if args.idle_spinners > 0:
+            import subprocess
+
+            code = "import os; os.sched_setscheduler(0, os.SCHED_IDLE, os.sched_param(0))\nwhile True: pass"
+            spin = [subprocess.Popen([sys.executable, "-c", code]) for _ in range(args.idle_spinners)]
+            time.sleep(1.0)
         q0 = mon.ex.seq
         n0 = mon.ex.scrape_count()
-        r = core.scrape_load("127.0.0.1", mon.port, args.scrape_path, n_requests=0, duration_s=args.idle_s,
-                             concurrency=args.scrape_concurrency, rate_hz=args.scrape_rate, keep_alive=True,
-                             gzip=args.gzip)
+        try:
+            r = core.scrape_load("127.0.0.1", mon.port, args.scrape_path, n_requests=0, duration_s=args.idle_s,
+                                 concurrency=args.scrape_concurrency, rate_hz=args.scrape_rate, keep_alive=True,
+                                 gzip=args.gzip)
+        finally:
+            for p in spin:
+                p.kill()
+                p.wait()
         q1 = mon.ex.seq
         it = [t["duration_s"] for t in mon.ex.tick_log() if q0 < t["seq"] <= q1]
         lat = r.get("latencies_s", [])
@@ -384,7 +402,8 @@ def main() -> int:
                 "server_scrape_p99_ms": round(_pct(srv, 0.99) * 1e3, 4) if srv else None,
                 "server_scrape_p999_ms": round(_pct(srv, 0.999) * 1e3, 4) if srv else None,
                 "ticks": len(it), "tick_mean_ms": round(sum(it) / len(it) * 1e3, 4) if it else None,
-                "tick_max_ms": round(max(it) * 1e3, 4) if it else None}
+                "tick_max_ms": round(max(it) * 1e3, 4) if it else None,
+                "idle_spinners": args.idle_spinners}
     barrier()
 
     # ---------------------------------------------------------------- synthetic load on every GPU
@@ -652,6 +671,7 @@ def main() -> int:
             "tick_quantiles": "exact over the timed ticks (exporter tick log); times in ms",
             "overruns": s1["overruns"] - s0["overruns"],
             "sampler_rt_threads": s1.get("rt_threads", 0),
+            "http_rt_loops": s1.get("http_rt_loops"),
             "prewarm_ms": args.prewarm_ms,
             # the exporter's own threads over the timed region, serving the scrape load too (1/100 s ticks)
             "exporter_cpu_millicores": round(1000.0 * (cpu1 - cpu0) / elapsed, 2),

@@ -76,6 +76,8 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "listen_addr", &c.listen_addr);
   get(d, "port", &c.port);
   get(d, "http_threads", &c.http_threads);
+  get(d, "http_rt_priority", &c.http_rt_priority);
+  get(d, "http_rt_budget", &c.http_rt_budget);
   get(d, "host", &c.host);
   get(d, "gzip", &c.gzip);
   get(d, "roctx", &c.roctx);
@@ -825,6 +827,8 @@ PYBIND11_MODULE(_core, m) {
              d["frozen_samples"] = s.frozen_samples;
              d["occupancy_reads"] = s.occupancy_reads;
              d["occupancy_scan_failures"] = s.occupancy_scan_failures;
+             d["http_rt_loops"] = s.http_rt_loops;
+             d["http_rt_demotions"] = s.http_rt_demotions;
              d["hidden_contexts"] = s.hidden_contexts;
              d["rt_threads"] = s.rt_threads;
              d["overruns"] = s.overruns;

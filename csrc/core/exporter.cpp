@@ -599,6 +599,7 @@ bool Exporter::start(std::string* err) {
         [this](const std::string& path, double s) {
           if (path == "/metrics") scrape_hist_.observe(s);
         });
+    server_->set_rt(cfg_.http_rt_priority, cfg_.http_rt_budget);
     std::string e;
     if (!server_->start(&e)) {
       if (err) *err = e;
@@ -1630,6 +1631,10 @@ SelfStats Exporter::self_stats() const {
   s.occupancy_scan_failures = scan_failures_->load(std::memory_order_relaxed);
   s.hidden_contexts = hidden_contexts_.load();
   s.rt_threads = rt_threads_->load();
+  if (cfg_.http_rt_priority > 0 && server_) {
+    s.http_rt_loops = server_->rt_loops();
+    s.http_rt_demotions = static_cast<int64_t>(server_->rt_demotions());
+  }
   s.overruns = overruns_;
   s.last_tick_wall_s = last_tick_wall_ns_.load() * 1e-9;
   s.interval_s = cfg_.interval_s;

@@ -45,6 +45,8 @@ struct ExporterConfig {
   std::string listen_addr = "0.0.0.0";
   int port = 9400;
   int http_threads = 2;
+  int http_rt_priority = 0;           // SCHED_FIFO HTTP loops (needs CAP_SYS_NICE; 0 = normal scheduling)
+  double http_rt_budget = 0.2;        // ... at most this share of a CPU per loop per 100 ms window, then demoted
   std::string host = "no_name";       // NODE_NAME (reference fallback "no_name", gpu.py:23-24)
   bool gzip = true;
   bool roctx = false;                 // ROCTx ranges around sampler phases (also GPUMON_ROCTX=1)

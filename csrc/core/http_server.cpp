@@ -4,6 +4,8 @@
 #include <fcntl.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
@@ -15,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <strings.h>
+#include <ctime>
 #include <unordered_map>
 
 #include "common.h"
@@ -210,9 +213,35 @@ void HttpServer::stop() {
   loops_.clear();
 }
 
+namespace {
+int64_t thread_cpu_ns() {
+  timespec ts{};
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
+}
+bool set_fifo(int prio) {
+  sched_param sp{};
+  sp.sched_priority = prio;
+  return pthread_setschedparam(pthread_self(), prio > 0 ? SCHED_FIFO : SCHED_OTHER, &sp) == 0;
+}
+}  // namespace
+
 void HttpServer::run(Loop* L) {
   epoll_event evs[256];
   int64_t last_sweep = mono_ns();
+  // http_rt_priority: FIFO while this loop's CPU time in the current 100 ms window stays under
+  // rt_budget_ x 100 ms; demoted to SCHED_OTHER for the rest of the window otherwise.
+  constexpr int64_t kRtWindowNs = 100'000'000;
+  const int prio = std::clamp(rt_prio_, 0, 99);
+  bool fifo = prio > 0 && set_fifo(prio);
+  if (prio > 0 && !fifo)
+    GPUMON_LOG(LogLevel::kWarn, "http",
+               "http_rt_priority " + std::to_string(prio) + ": " + strerror(errno) +
+                   " (needs CAP_SYS_NICE); HTTP loops keep normal scheduling");
+  const bool rt_on = fifo;
+  if (fifo) rt_loops_.fetch_add(1);
+  int64_t win_start = mono_ns(), win_cpu0 = thread_cpu_ns();
+  const int64_t budget_ns = static_cast<int64_t>(std::clamp(rt_budget_, 0.01, 1.0) * kRtWindowNs);
   auto close_conn = [&](int fd) {
     epoll_ctl(L->ep, EPOLL_CTL_DEL, fd, nullptr);
     close(fd);
@@ -326,8 +355,24 @@ void HttpServer::run(Loop* L) {
   };
 
   while (running_.load(std::memory_order_relaxed)) {
-    int n = epoll_wait(L->ep, evs, 256, 1000);
+    int n = epoll_wait(L->ep, evs, 256, rt_on ? 100 : 1000);
     int64_t now = mono_ns();
+    if (rt_on) {
+      if (now - win_start >= kRtWindowNs) {  // new window: back to FIFO
+        win_start = now;
+        win_cpu0 = thread_cpu_ns();
+        if (!fifo && set_fifo(prio)) {
+          fifo = true;
+          rt_loops_.fetch_add(1);
+        }
+      } else if (fifo && thread_cpu_ns() - win_cpu0 > budget_ns) {  // budget spent: yield the CPU
+        if (set_fifo(0)) {
+          fifo = false;
+          rt_loops_.fetch_sub(1);
+          rt_demotions_.fetch_add(1, std::memory_order_relaxed);
+        }
+      }
+    }
     for (int i = 0; i < n; ++i) {
       int fd = evs[i].data.fd;
       if (fd == L->wake) continue;
@@ -407,6 +452,7 @@ void HttpServer::run(Loop* L) {
       for (int fd : idle) close_conn(fd);
     }
   }
+  if (fifo) rt_loops_.fetch_sub(1);
 }
 
 }  // namespace gpumon

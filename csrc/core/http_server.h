@@ -40,6 +40,16 @@ class HttpServer {
 
   HttpServer(std::string addr, int port, int threads, Handler h, Observer obs);
   ~HttpServer();
+  // Opt-in SCHED_FIFO for the event loops (http_rt_priority; needs CAP_SYS_NICE): a scrape is then
+  // served as soon as it arrives on a CPU-saturated node. Each loop may spend at most
+  // `budget` of one CPU per 100 ms window at that priority; past it the loop drops to normal
+  // scheduling until the window ends, so a request flood cannot monopolise a core. Before start().
+  void set_rt(int prio, double budget) {
+    rt_prio_ = prio;
+    rt_budget_ = budget;
+  }
+  int rt_loops() const { return rt_loops_.load(); }           // loops running at SCHED_FIFO now
+  uint64_t rt_demotions() const { return rt_demotions_.load(); }  // budget exhaustions
   bool start(std::string* err);
   void stop();
   int port() const { return port_; }
@@ -59,6 +69,10 @@ class HttpServer {
   std::atomic<bool> running_{false};
   std::atomic<uint64_t> conns_{0};
   std::atomic<uint64_t> requests_{0};
+  int rt_prio_ = 0;
+  double rt_budget_ = 0.2;
+  std::atomic<int> rt_loops_{0};
+  std::atomic<uint64_t> rt_demotions_{0};
 };
 
 }  // namespace gpumon

@@ -244,6 +244,8 @@ const std::map<std::string, Setter>& setters() {
       {"health_stale_s", dbl_at([](NativeOptions* o) { return &o->cfg.health_stale_s; })},
       {"listen", str(&NativeOptions::listen)},
       {"http_threads", int_at([](NativeOptions* o) { return &o->cfg.http_threads; })},
+      {"http_rt_priority", int_at([](NativeOptions* o) { return &o->cfg.http_rt_priority; })},
+      {"http_rt_budget", dbl_at([](NativeOptions* o) { return &o->cfg.http_rt_budget; })},
       {"host", str_at([](NativeOptions* o) { return &o->cfg.host; })},
       {"gzip", bool_at([](NativeOptions* o) { return &o->cfg.gzip; })},
       {"roctx", bool_at([](NativeOptions* o) { return &o->cfg.roctx; })},
@@ -520,6 +522,8 @@ std::string options_json(const NativeOptions& o) {
   N("health_stale_s", c.health_stale_s);
   S("listen", o.listen);
   N("http_threads", c.http_threads);
+  N("http_rt_priority", c.http_rt_priority);
+  N("http_rt_budget", c.http_rt_budget);
   S("host", c.host);
   B("gzip", c.gzip);
   B("roctx", c.roctx);

@@ -817,6 +817,22 @@ void render_prometheus(const RenderInput& in, std::string* o) {
                "Sampler and device-worker threads running SCHED_FIFO (rt_priority > 0 and CAP_SYS_NICE).", "gauge");
       f.add(hl, static_cast<double>(s.rt_threads));
     }
+    if (s.http_rt_loops >= 0) {
+      {
+        Family f(o, "gpumon_http_rt_loops",
+                 "HTTP event loops running SCHED_FIFO right now (http_rt_priority; a loop past its CPU budget "
+                 "runs at normal priority until its 100 ms window ends).",
+                 "gauge");
+        f.add(hl, static_cast<double>(s.http_rt_loops));
+      }
+      {
+        Family f(o, "gpumon_http_rt_demotions_total",
+                 "Times an SCHED_FIFO HTTP loop used its CPU budget (http_rt_budget per 100 ms) and dropped to "
+                 "normal scheduling for the rest of the window: a request flood.",
+                 "counter");
+        f.add(hl, static_cast<double>(s.http_rt_demotions));
+      }
+    }
     {
       Family f(o, "gpumon_occupancy_reads_total",
                "KFD cu_occupancy reads made between ticks by the device workers (occ_samples per tick).",

@@ -125,6 +125,7 @@ int main(int argc, char** argv) {
     else if (a == "--metrics-exclude") set("metrics_exclude", next());
     else if (a == "--sample-threads") set("sample_threads", next());
     else if (a == "--rt-priority") set("rt_priority", next());
+    else if (a == "--http-rt-priority") set("http_rt_priority", next());
     else if (a == "--prewarm-ms") set("prewarm_ms", next());
     else if (a == "--http-threads") set("http_threads", next());
     else if (a == "--log-level") set("log_level", next());

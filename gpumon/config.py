@@ -55,6 +55,8 @@ class Config:
     # exposition
     listen: str = "0.0.0.0:9400"
     http_threads: int = 2
+    http_rt_priority: int = 0             # SCHED_FIFO HTTP loops (CAP_SYS_NICE), each capped at http_rt_budget of a CPU
+    http_rt_budget: float = 0.2           # share of a CPU per 100 ms an RT HTTP loop may use before it is demoted
     host: str = ""
     gzip: bool = True
     compat_families: bool = True
@@ -157,6 +159,8 @@ class Config:
             "listen_addr": self.listen_addr,
             "port": self.port,
             "http_threads": int(self.http_threads),
+            "http_rt_priority": int(self.http_rt_priority),
+            "http_rt_budget": float(self.http_rt_budget),
             "host": self.resolved_host(),
             "gzip": self.gzip,
             "roctx": self.roctx,
@@ -307,6 +311,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
                    help="comma-separated globs: metric families left out of /metrics (e.g. 'gpu_xcd_*')")
     p.add_argument("--sample-threads", dest="sample_threads", type=int)
     p.add_argument("--rt-priority", dest="rt_priority", type=int)
+    p.add_argument("--http-rt-priority", dest="http_rt_priority", type=int,
+                   help="SCHED_FIFO priority of the HTTP loops (0 = normal; needs CAP_SYS_NICE)")
     p.add_argument("--prewarm-ms", dest="prewarm_ms", type=float,
                    help="device workers warm the firmware-table read this long before each tick (0 = off)")
     p.add_argument("--device-timeout", dest="device_timeout_s", type=float,

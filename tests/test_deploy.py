@@ -448,7 +448,7 @@ def test_nonroot_overlay():
     cfg_patch = next(p for p in k["patches"] if p["target"]["kind"] == "ConfigMap")
     c = Config().apply_dict(yaml.safe_load(yaml.safe_load(cfg_patch["patch"])[0]["value"])["gpumon"])
     assert c.pod_log_root == "/var/log" and c.cri_socket == "none" and c.pod_resources_socket == ""
-    assert c.rt_priority == 0
+    assert c.rt_priority == 0 and c.http_rt_priority == 0
     ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
     ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"])
     ctr = _json_patch(ds, ops)["spec"]["template"]["spec"]["containers"][0]
@@ -490,7 +490,7 @@ def test_stress_overlay_is_10hz_end_to_end():
     assert c.interval == pytest.approx(0.1)
     base = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "ConfigMap")
     b = Config().apply_dict(yaml.safe_load(base["data"]["config.yaml"])["gpumon"])
-    for key in ("pod_resources_socket", "cri_socket", "pod_log_root", "rt_priority", "control_plane",
+    for key in ("pod_resources_socket", "cri_socket", "pod_log_root", "rt_priority", "http_rt_priority", "control_plane",
                 "enable_pmc", "enable_probe"):
         assert getattr(c, key) == getattr(b, key), key  # only the rate differs from the base
     sm = _docs("deploy/k8s/gpumon-servicemonitor.yaml")[0]

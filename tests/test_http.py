@@ -267,3 +267,32 @@ def test_pathological_filter_is_fast_and_oversized_filters_are_refused(mock_expo
     assert st == 400 and b"query longer than" in body
     st, _, _ = _get(ex.port, "/metrics?include=gpu_up")  # the loop is still serving
     assert st == 200
+
+
+def test_http_rt_loops_are_budget_capped(core):
+    """http_rt_priority: the HTTP loops run SCHED_FIFO (where CAP_SYS_NICE allows), and under an
+    unthrottled flood each loop drops to normal scheduling once it used its budget of the 100 ms
+    window (profiles/r4_scrape_contention.md), so the flood cannot hold a CPU at RT priority."""
+    import os
+
+    ex = core.Exporter({"backend": "mock:gpus=2", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0.1,
+                        "http_threads": 2, "http_rt_priority": 1, "http_rt_budget": 0.05})
+    assert ex.start() == ""
+    try:
+        ex.wait_for_seq(1, 10)
+        st = ex.self_stats()
+        try:
+            os.sched_setscheduler(0, os.SCHED_FIFO, os.sched_param(1))
+            os.sched_setscheduler(0, os.SCHED_OTHER, os.sched_param(0))
+        except PermissionError:
+            assert st["http_rt_loops"] == 0  # no CAP_SYS_NICE: normal scheduling, said so
+            return
+        assert st["http_rt_loops"] == 2 and st["http_rt_demotions"] == 0
+        r = core.scrape_load("127.0.0.1", ex.port, "/metrics", n_requests=0, duration_s=1.5, concurrency=4,
+                             rate_hz=0.0, keep_alive=True, gzip=False)
+        assert r["errors"] == 0 and len(r["latencies_s"]) > 100
+        assert ex.self_stats()["http_rt_demotions"] > 0
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpumon_http_rt_demotions_total") > 0
+    finally:
+        ex.stop()

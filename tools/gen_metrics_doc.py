@@ -12,6 +12,7 @@ Configurations (all native, no Python oracle):
 * influx     -- the batched Influx push against a local sink;
 * pmc/probe/helper -- the on-device samplers through the fake plugins, in the helper process
                 (csrc/fakes/fake_ondevice.cpp; `make fakes`);
+* http_rt_priority -- SCHED_FIFO HTTP loops (their self-metrics);
 * amdsmi     -- the libamd_smi backend over the fake library (backend-specific self-metrics).
 """
 
@@ -133,6 +134,13 @@ def collect():
             finally:
                 ex.stop()
     srv.shutdown()
+    # HTTP loops at SCHED_FIFO (http_rt_priority): their self-metrics
+    ex = c.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                     "host": "node", "http_rt_priority": 1})
+    if ex.start() == "":
+        ex.tick()
+        add(_families(ex), "http_rt_priority")
+    ex.stop()
     # backend-specific self-metrics: the libamd_smi backend over the fake library
     os.environ.setdefault("FAKE_AMDSMI_GPUS", "1")
     ex = c.Exporter({"backend": "amdsmi", "amdsmi_lib": os.path.join(ROOT, "build", "fakes", "libfake_amd_smi.so"),
