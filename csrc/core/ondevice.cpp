@@ -751,6 +751,16 @@ void OnDevice::export_helper() {
     out.push_back(xs("gpumon_ondevice_helper_resident_memory_bytes",
                      "Resident memory of the on-device helper process (its GPU runtimes).", -1, rss));
   }
+  // What the enabled samplers should hold (profiles/r3_helper_memory.md, r3_probe_hsa.md): 0.11 GB
+  // of runtime plus one fully resident 173 MB context-save block per hardware queue per GPU --
+  // device counting alone brings up 2 queues per GPU, the K1 probe alone 2, both together 3 (the
+  // runtime's copy queue is shared). The memory alert compares the helper's RSS with this.
+  const int blocks = cfg_.pmc && cfg_.probe ? 3 : (cfg_.pmc || cfg_.probe) ? 2 : 0;
+  const double gpus = static_cast<double>(ex_->statics().size());
+  out.push_back(xs("gpumon_ondevice_helper_memory_model_bytes",
+                   "Expected resident memory of the on-device helper for the enabled samplers: 0.11 GB + 173 MB "
+                   "per hardware queue per GPU (PMC 2 queues, probe 2, both 3).",
+                   -1, 110e6 + gpus * blocks * 173e6));
   ex_->set_extra("ondevice_helper", std::move(out));
 }
 
