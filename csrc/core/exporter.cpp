@@ -1980,7 +1980,9 @@ bool Exporter::docker_poll_once() {
 
 // Kubelet-written files (kubelet_files.h): the log tree names every container on the node; the
 // device-plugin checkpoint lists the GPUs each (pod uid, container) was given. A checkpoint entry
-// of a pod without a log directory (gone from the node) is dropped.
+// of a pod without a log directory (gone from the node) is dropped, and so is one whose container
+// has no live process (a Completed / Failed pod the kubelet has not deleted: its checkpoint entry
+// and log directory stay until then) -- where the process scan can tell.
 bool Exporter::files_poll_once() {
   std::vector<ContainerMeta> metas;
   std::string err;
@@ -2030,6 +2032,19 @@ bool Exporter::files_poll_once() {
       }
     }
   }
+  size_t exited = 0;
+  if (std::any_of(allocs.begin(), allocs.end(), [](const Allocation& a) { return !a.container_id.empty(); })) {
+    std::unordered_set<std::string> running;
+    if (running_container_ids(cfg_.attribution.procfs_root, &running)) {
+      const size_t before = allocs.size();
+      allocs.erase(std::remove_if(allocs.begin(), allocs.end(),
+                                  [&](const Allocation& a) {
+                                    return !a.container_id.empty() && !running.count(a.container_id);
+                                  }),
+                   allocs.end());
+      exited = before - allocs.size();
+    }
+  }
   const size_t n_metas = metas.size();
   {
     std::lock_guard<std::mutex> g(meta_mu_);
@@ -2054,6 +2069,10 @@ bool Exporter::files_poll_once() {
                   "gauge", -1, {{"source", "device_checkpoint"}}, ckpt_ok ? 1.0 : 0.0});
     ex.push_back({"gpumon_kubelet_files_unknown_devices", "Checkpointed device IDs that match no local GPU.", "gauge",
                   -1, {}, static_cast<double>(unknown)});
+    ex.push_back({"gpumon_kubelet_files_exited_allocations",
+                  "Checkpointed GPU allocations left out because their container has no live process (a finished "
+                  "pod the kubelet has not deleted yet).",
+                  "gauge", -1, {}, static_cast<double>(exited)});
   }
   set_extra("kubelet_files", std::move(ex));
   return logs_ok || ckpt_ok;

@@ -72,6 +72,25 @@ bool parse_pod_log_dir(const std::string& name, std::string* ns, std::string* po
   return pod->find('_') == std::string::npos;
 }
 
+bool running_container_ids(const std::string& procfs_root, std::unordered_set<std::string>* out) {
+  out->clear();
+  DIR* d = opendir(procfs_root.c_str());
+  if (!d) return false;
+  std::string text, self;
+  if (read_file(procfs_root + "/self/cgroup", &text, 65536)) self = parse_cgroup(text).container_id;
+  while (struct dirent* ent = readdir(d)) {
+    const char* n = ent->d_name;
+    if (*n < '1' || *n > '9') continue;  // pids only
+    if (!read_file(procfs_root + "/" + n + "/cgroup", &text, 65536)) continue;  // exited meanwhile
+    CgroupInfo cg = parse_cgroup(text);
+    if (cg.found) out->insert(std::move(cg.container_id));
+  }
+  closedir(d);
+  for (const auto& id : *out)
+    if (id != self) return true;
+  return false;
+}
+
 bool kubelet_log_metadata(const std::string& log_root, std::vector<ContainerMeta>* out, std::string* err) {
   out->clear();
   std::vector<std::string> pods, ctrs;

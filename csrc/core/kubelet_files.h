@@ -20,6 +20,7 @@
 
 #include <map>
 #include <string>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -46,5 +47,12 @@ struct CheckpointEntry {
 // "ResourceName", "DeviceIDs": {"<numa>": [ids]} (v2) or [ids] (v1), "AllocResp"}], ...}, "Checksum"}.
 bool device_checkpoint_parse(const std::string& json, std::vector<CheckpointEntry>* out, std::string* err);
 bool device_checkpoint_read(const std::string& path, std::vector<CheckpointEntry>* out, std::string* err);
+
+// Container ids that have at least one live process: /proc/<pid>/cgroup of every process
+// (parse_cgroup). The checkpoint keeps entries of pods that finished but were not deleted (the
+// kubelet prunes them at its next Allocate), and their containers have no process left. False when
+// the scan cannot tell: procfs unreadable, or no container other than the reader's own is visible
+// (not in the host PID namespace).
+bool running_container_ids(const std::string& procfs_root, std::unordered_set<std::string>* out);
 
 }  // namespace gpumon

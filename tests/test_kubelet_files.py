@@ -55,6 +55,9 @@ def test_pod_metadata_and_idle_rows_without_any_socket(core, tmp_path):
     proc = tmp_path / "proc"
     _fake_proc(proc, 2000, f"0::/kubepods.slice/kubepods-pod{UID_A.replace('-', '_')}.slice/"
                            f"cri-containerd-{CID_A}.scope")
+    # jupyter-q-0 is running (a process in its container), just not on a GPU
+    _fake_proc(proc, 2001, f"0::/kubepods.slice/kubepods-pod{UID_B.replace('-', '_')}.slice/"
+                           f"cri-containerd-{CID_B}.scope")
     logs = tmp_path / "log"
     _log_tree(logs)
     ckpt = tmp_path / "kubelet_internal_checkpoint"
@@ -79,6 +82,30 @@ def test_pod_metadata_and_idle_rows_without_any_socket(core, tmp_path):
         assert promtext.one(fam, "gpumon_kubelet_files_up", source="pod_logs") == 1
         assert promtext.one(fam, "gpumon_kubelet_files_up", source="device_checkpoint") == 1
         assert promtext.one(fam, "gpumon_kubelet_files_containers") == 2
+    finally:
+        ex.stop()
+
+
+def test_checkpoint_entry_of_a_finished_pod_is_not_an_idle_row(core, tmp_path):
+    """the checkpoint keeps a Completed pod's entry (and the log tree its directory) until
+    the pod is deleted. Its container has no live process, so it is no idle allocation: dropped
+    and counted. A running pod's idle allocation stays."""
+    proc = tmp_path / "proc"
+    _fake_proc(proc, 2000, f"0::/kubepods.slice/kubepods-pod{UID_A.replace('-', '_')}.slice/"
+                           f"cri-containerd-{CID_A}.scope")  # notebook pod: running (no GPU process)
+    logs = tmp_path / "log"
+    _log_tree(logs)  # jupyter-q-0 (CID_B) has its log dir and symlink, but no process: it completed
+    ckpt = tmp_path / "ckpt"
+    _checkpoint(ckpt)
+    ex = core.Exporter({"backend": "mock:gpus=3", "serve_http": False, "interval_s": 0, "host": "n1",
+                        "procfs_root": str(proc), "pod_log_root": str(logs), "device_checkpoint": str(ckpt)})
+    assert ex.start() == ""
+    try:
+        ex.tick()
+        idle = sorted((r["dev"], r["podname"]) for r in ex.pod_rows() if r["idle"])
+        assert idle == [(0, "turing-gpu-notebook-alice-5d8f-x1")]
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpumon_kubelet_files_exited_allocations") == 1
     finally:
         ex.stop()
 
