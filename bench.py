@@ -260,6 +260,9 @@ def main() -> int:
     ap.add_argument("--idle-spinners", type=int, default=0,
                     help="DIAGNOSTIC: SCHED_IDLE busy loops during the idle reference (they take no CPU from "
                          "runnable threads but keep CPUs out of idle states: isolates wake-from-idle latency)")
+    ap.add_argument("--pin-cpus", type=int, default=0,
+                    help="DIAGNOSTIC: run the whole bench (exporter, scraper, loads, spinners) on the first N CPUs "
+                         "of its allowed set, so --idle-spinners can keep exactly those CPUs out of idle")
     ap.add_argument("--no-fast-path", action="store_true", help="read every value through libamd_smi")
     ap.add_argument("--rt-priority", type=int, default=1,
                     help="the DaemonSet's rt_priority (SCHED_FIFO sampler; stays normal without CAP_SYS_NICE)")
@@ -279,6 +282,8 @@ def main() -> int:
 
     if args.idle_s < 0:
         args.idle_s = max(5.0, args.steps * args.interval)
+    if args.pin_cpus > 0:  # before any thread exists: every thread and child inherits the mask
+        os.sched_setaffinity(0, sorted(os.sched_getaffinity(0))[:args.pin_cpus])
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -403,7 +408,8 @@ def main() -> int:
                 "server_scrape_p999_ms": round(_pct(srv, 0.999) * 1e3, 4) if srv else None,
                 "ticks": len(it), "tick_mean_ms": round(sum(it) / len(it) * 1e3, 4) if it else None,
                 "tick_max_ms": round(max(it) * 1e3, 4) if it else None,
-                "idle_spinners": args.idle_spinners}
+                "idle_spinners": args.idle_spinners,
+                "pinned_cpus": sorted(os.sched_getaffinity(0)) if args.pin_cpus > 0 else None}
     barrier()
 
     # ---------------------------------------------------------------- synthetic load on every GPU

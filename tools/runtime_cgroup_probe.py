@@ -57,7 +57,7 @@ def main():
             deadline = time.time() + 10
             while time.time() < deadline:
                 ex.tick()
-                rows = [r for r in ex.pod_rows() if r.get("pid") == tenant.pid]
+                rows = [r for r in ex.pod_rows() if str(r.get("pid")) == str(tenant.pid)]
                 if rows:
                     break
                 time.sleep(0.2)
@@ -84,8 +84,8 @@ def main():
             "uid": os.getuid(),
             "resolved": resolved,
             "parsed_without_kfd_check": parsed,
-            "tenant_rows": [{k: r.get(k) for k in ("dev", "pid", "idle", "container_id", "podname", "namespace",
-                                                   "procressname", "used_memory_bytes")} for r in rows],
+            "tenant_rows": [{k: r.get(k) for k in ("dev", "pid", "idle", "containerid", "podname", "namespace",
+                                                   "procressname", "used_memory_bytes", "source")} for r in rows],
         }
         res["cgroup_namespaced_root"] = any(l.endswith("::/") for l in res["self_cgroup"])
     finally:
