@@ -219,10 +219,11 @@ int64_t thread_cpu_ns() {
   clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
   return static_cast<int64_t>(ts.tv_sec) * 1000000000LL + ts.tv_nsec;
 }
-bool set_fifo(int prio) {
+// 0 or the error number (pthread_setschedparam returns it; errno is not set)
+int set_fifo(int prio) {
   sched_param sp{};
   sp.sched_priority = prio;
-  return pthread_setschedparam(pthread_self(), prio > 0 ? SCHED_FIFO : SCHED_OTHER, &sp) == 0;
+  return pthread_setschedparam(pthread_self(), prio > 0 ? SCHED_FIFO : SCHED_OTHER, &sp);
 }
 }  // namespace
 
@@ -233,10 +234,11 @@ void HttpServer::run(Loop* L) {
   // rt_budget_ x 100 ms; demoted to SCHED_OTHER for the rest of the window otherwise.
   constexpr int64_t kRtWindowNs = 100'000'000;
   const int prio = std::clamp(rt_prio_, 0, 99);
-  bool fifo = prio > 0 && set_fifo(prio);
+  const int rc = prio > 0 ? set_fifo(prio) : 0;
+  bool fifo = prio > 0 && rc == 0;
   if (prio > 0 && !fifo)
     GPUMON_LOG(LogLevel::kWarn, "http",
-               "http_rt_priority " + std::to_string(prio) + ": " + strerror(errno) +
+               "http_rt_priority " + std::to_string(prio) + ": " + strerror(rc) +
                    " (needs CAP_SYS_NICE); HTTP loops keep normal scheduling");
   const bool rt_on = fifo;
   if (fifo) rt_loops_.fetch_add(1);
@@ -361,12 +363,12 @@ void HttpServer::run(Loop* L) {
       if (now - win_start >= kRtWindowNs) {  // new window: back to FIFO
         win_start = now;
         win_cpu0 = thread_cpu_ns();
-        if (!fifo && set_fifo(prio)) {
+        if (!fifo && set_fifo(prio) == 0) {
           fifo = true;
           rt_loops_.fetch_add(1);
         }
       } else if (fifo && thread_cpu_ns() - win_cpu0 > budget_ns) {  // budget spent: yield the CPU
-        if (set_fifo(0)) {
+        if (set_fifo(0) == 0) {
           fifo = false;
           rt_loops_.fetch_sub(1);
           rt_demotions_.fetch_add(1, std::memory_order_relaxed);

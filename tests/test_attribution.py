@@ -43,6 +43,26 @@ def test_parse_cgroup_formats(core, text, runtime, cid, uid, qos):
     assert r["qos"] == qos
 
 
+# What /proc/<pid>/cgroup says on a real container runtime (gpurun call r4a, tools/runtime_cgroup_probe.py,
+# profiles/r4_runtime_attribution.md; the 32-hex id replaced): a cgroup v2 host whose runtime puts each
+# container in /<manager>/<32-hex id> -- the exporter, and a torch tenant holding /dev/kfd, share it;
+# the box's init sits in /<manager>/core. And what a DaemonSet pod with a private cgroup namespace
+# reads for another pod's process: a path relative to its own namespace root ("/../..").
+BOX_ID = "5e1f" * 8
+
+
+@pytest.mark.parametrize("text,found,runtime,cid,uid,qos", [
+    (f"0::/process_api/{BOX_ID}\n", True, "cgroupfs", BOX_ID, "", ""),
+    ("0::/process_api/core\n", False, "", "", "", ""),
+    (f"0::/../../kubepods-besteffort-pod{UID.replace('-', '_')}.slice/cri-containerd-{CID}.scope\n",
+     True, "containerd", CID, UID, "besteffort"),
+    (f"0::/../kubepods/burstable/pod{UID}/{CID}\n", True, "cgroupfs", CID, UID, "burstable"),
+])
+def test_parse_cgroup_observed_and_namespaced(core, text, found, runtime, cid, uid, qos):
+    r = core.parse_cgroup(text)
+    assert (r["found"], r["runtime"], r["container_id"], r["pod_uid"], r["qos"]) == (found, runtime, cid, uid, qos)
+
+
 def test_parse_cgroup_host_process(core):
     r = core.parse_cgroup("0::/user.slice/user-1000.slice/session-3.scope\n")
     assert not r["found"] and r["container_id"] == ""

@@ -13,3 +13,25 @@ for i in 1 2; do
     --out $out/pin8_spin_$i.json > $out/pin8_spin_$i.log 2>&1 || exit 1
   echo round_$i ok
 done
+# the deployed configs on the hardware: the DaemonSet ConfigMap and each overlay's config through
+# the Python-free entry point (--once), sockets / log tree absent on the box
+python - $out <<'PY'
+import sys, yaml
+out = sys.argv[1]
+docs = [d for d in yaml.safe_load_all(open("deploy/k8s/gpumon-daemonset.yaml")) if d]
+cm = next(d for d in docs if d["kind"] == "ConfigMap")
+open(f"{out}/cm_base.yaml", "w").write(cm["data"]["config.yaml"])
+for ov in ("pmc", "ondevice", "stress", "nonroot"):
+    k = yaml.safe_load(open(f"deploy/k8s/overlays/{ov}/kustomization.yaml"))
+    p = next(p for p in k["patches"] if p["target"]["kind"] == "ConfigMap")
+    open(f"{out}/cm_{ov}.yaml", "w").write(yaml.safe_load(p["patch"])[0]["value"])
+PY
+for c in base pmc ondevice stress nonroot; do
+  timeout -k 10 90 ./bin/gpumon-exporter --config $out/cm_$c.yaml --once > $out/cm_$c.prom 2> $out/cm_$c.err || exit 1
+  echo "cm_$c families=$(grep -c '^# TYPE' $out/cm_$c.prom)"
+done
+# per-kernel time of the driver-shape bench
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o r4b -- python3 bench.py --steps 5 --warmup 1 \
+  --capacity-s 0 --idle-s 2 > $out/prof.log 2>&1 || exit 1
+echo prof_ok
