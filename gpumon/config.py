@@ -138,7 +138,7 @@ class Config:
             "rocm_smi_lib": self.rocm_smi_lib,
             "fast_path": self.fast_path,
             "sysfs_root": self.sysfs_root,
-            "devices": [str(x) for x in self.devices],
+            "devices": _device_ids(self.devices),
             "interval_s": float(self.interval),
             "processes": self.processes,
             "link_every": int(self.link_every),
@@ -235,6 +235,24 @@ def redact_url(url: str) -> str:
     if colon < 0 or colon > at:
         return url
     return url[:colon + 1] + "***" + url[at:]
+
+
+def _device_ids(devices) -> List[str]:
+    """`devices` entries as the native filter takes them: a hip id ("3") or a PCI BDF; anything else
+    is a configuration error here (the native parser refuses it the same way, csrc/core/options.cpp)."""
+    from .parallel.devmap import normalize_bdf
+
+    out = []
+    for x in devices:
+        s = str(x).strip()
+        b = normalize_bdf(s)
+        if b:
+            out.append(b)
+        elif s.isdigit():
+            out.append(str(int(s)))
+        else:
+            raise ValueError(f"devices: {x!r} is neither a hip id nor a PCI BDF")
+    return out
 
 
 def _version() -> str:

@@ -242,3 +242,14 @@ def test_influx_token_with_a_line_break_disables_the_push(core):
     finally:
         ex.stop()
     assert st["ticks"] >= 5 and st["influx_ok"] == 0 and st["influx_fail"] == 0
+
+
+def test_devices_accept_hip_ids_and_bdfs_and_refuse_the_rest():
+    """`devices` takes hip ids and PCI BDFs (loaders name GPUs by BDF); the core
+    gets them normalised, and a token that is neither is a configuration error, as in the binary."""
+    from gpumon.config import Config
+
+    assert Config(devices=[0, "75:00.0", "0000:E5:00.0"]).to_core()["devices"] == ["0", "0000:75:00.0", "0000:e5:00.0"]
+    assert Config().apply_dict({"devices": "1, 0000:25:00.0"}).to_core()["devices"] == ["1", "0000:25:00.0"]
+    with pytest.raises(ValueError, match="neither a hip id nor a PCI BDF"):
+        Config(devices=["gpu3"]).to_core()
