@@ -1014,6 +1014,7 @@ PYBIND11_MODULE(_core, m) {
         d["probe_timeouts"] = s.probe_timeouts;
         d["pmc_agents"] = s.pmc_agents;
         d["probe_devices"] = s.probe_devices;
+        d["probe_by_bdf"] = s.probe_by_bdf;
         return d;
       });
   m.def("default_plugin_dir", &default_plugin_dir);

@@ -53,6 +53,7 @@ struct OnDevice::Plugin {
   int (*probe_launch)(gpumon_probe*) = nullptr;
   int (*probe_wait)(gpumon_probe*, int, double, gpumon_probe_result_t*) = nullptr;
   void (*probe_destroy)(gpumon_probe*) = nullptr;
+  size_t (*probe_pci)(int, char*, size_t) = nullptr;  // optional: HIP ordinal -> PCI address
   // optional: launch where pending[k] < 0, then wait for every pending launch, in one call
   // (the helper process: one awake period, so the host-observed latency is the GPU's, not IPC's)
   bool (*probe_cycle)(gpumon_probe* const*, int, double, int*, int*, gpumon_probe_result_t*) = nullptr;
@@ -98,6 +99,8 @@ std::unique_ptr<OnDevice::Plugin> load_plugin(const std::string& dir, const char
     sym(p->h, "gpumon_probe_launch", &p->probe_launch, &missing);
     sym(p->h, "gpumon_probe_wait", &p->probe_wait, &missing);
     sym(p->h, "gpumon_probe_destroy", &p->probe_destroy, &missing);
+    std::string optional;  // absent -> devices paired by hip_id
+    sym(p->h, "gpumon_probe_device_pci", &p->probe_pci, &optional);
   }
   if (!missing.empty()) {
     *err = p->path + ": missing symbols " + missing;
@@ -408,6 +411,17 @@ int h_probe_wait(gpumon_probe* h, int slot, double timeout_s, gpumon_probe_resul
   memcpy(out, p.data(), sizeof *out);
   return 1;
 }
+size_t h_probe_pci(int dev, char* buf, size_t len) {
+  const int a[1] = {dev};
+  std::vector<char> p;
+  std::string e;
+  const int rc = helper_call(GPUMON_PROBE_OP_PCI, a, 1, nullptr, 0, 0, &p, nullptr, &e);
+  if (rc <= 0 || p.empty() || !buf || !len) return 0;
+  const size_t n = std::min(p.size(), len - 1);
+  memcpy(buf, p.data(), n);
+  buf[n] = 0;
+  return n + 1;
+}
 void h_probe_destroy(gpumon_probe* h) {
   const int a[1] = {h_probe_id(h)};
   std::vector<char> p;
@@ -607,6 +621,7 @@ bool OnDevice::start(std::string* err) {
       probe_lib_->probe_wait = &h_probe_wait;
       probe_lib_->probe_destroy = &h_probe_destroy;
       probe_lib_->probe_cycle = &h_probe_cycle;
+      probe_lib_->probe_pci = &h_probe_pci;
     } else {
       probe_lib_ = load_plugin(dir, "libgpumon_probe.so", false, err);
     }
@@ -697,6 +712,7 @@ OnDevice::Stats OnDevice::stats() const {
   s.probe_timeouts = probe_timeouts_;
   s.pmc_agents = static_cast<int>(agents_.size());
   s.probe_devices = static_cast<int>(probes_.size());
+  s.probe_by_bdf = probe_by_bdf_;
   s.helper_restarts = helper_restarts_;
   return s;
 }
@@ -1028,20 +1044,39 @@ void OnDevice::pmc_loop() {
 // ---------------------------------------------------------------------------------------------
 // K1 probe
 
-// One probe per exported device with a HIP id. Called at start and, while the exporter's backend
-// has not come up yet (empty statics), again on later steps.
+// One probe per exported device that the probe's runtime can see. Called at start and, while the
+// exporter's backend has not come up yet (empty statics), again on later steps. Devices are paired
+// with the runtime's HIP ordinals by PCI address where the plugin reports it: the exporter's
+// hip_id is node-wide, the ordinals follow HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES of the
+// process (gpumon/parallel/devmap.py does the same for the bench). Without it, by hip_id.
 bool OnDevice::create_probes(std::string* err) {
   if (!probes_.empty()) return true;
   char ebuf[512] = {0};
   const int n_hip = probe_lib_->probe_count();
+  std::map<std::string, int> ordinal_of;  // normalised BDF -> HIP ordinal
+  if (probe_lib_->probe_pci)
+    for (int o = 0; o < n_hip; ++o) {
+      char b[64] = {0};
+      if (probe_lib_->probe_pci(o, b, sizeof b) > 0) {
+        const std::string nb = normalize_bdf(b);
+        if (!nb.empty()) ordinal_of[nb] = o;
+      }
+    }
+  probe_by_bdf_ = !ordinal_of.empty();
   std::vector<ProbeDev> made;
   for (const auto& s : ex_->statics()) {
-    if (s.hip_id < 0 || s.hip_id >= n_hip) continue;
+    int ord = s.hip_id;
+    if (probe_by_bdf_) {
+      const auto it = ordinal_of.find(normalize_bdf(s.bdf));
+      if (it == ordinal_of.end()) continue;  // a GPU the probe's runtime does not see
+      ord = it->second;
+    }
+    if (ord < 0 || ord >= n_hip) continue;
     ProbeDev d;
     d.dev = s.index;
-    d.handle = probe_lib_->probe_create(s.hip_id, cfg_.probe_blocks, 4, cfg_.probe_spin_ticks, ebuf, sizeof ebuf);
+    d.handle = probe_lib_->probe_create(ord, cfg_.probe_blocks, 4, cfg_.probe_spin_ticks, ebuf, sizeof ebuf);
     if (!d.handle) {
-      *err = std::string("probe create on hip device ") + std::to_string(s.hip_id) + ": " + ebuf;
+      *err = std::string("probe create on hip device ") + std::to_string(ord) + ": " + ebuf;
       for (auto& p : made) probe_lib_->probe_destroy(static_cast<gpumon_probe*>(p.handle));
       return false;
     }

@@ -115,6 +115,7 @@ class OnDevice {
     uint64_t pmc_samples = 0, pmc_errors = 0, pmc_resets = 0, probe_done = 0, probe_timeouts = 0;
     uint64_t helper_restarts = 0;
     int pmc_agents = 0, probe_devices = 0;
+    bool probe_by_bdf = false;
     bool pmc_continuous = false;
   };
   Stats stats() const;
@@ -177,6 +178,7 @@ class OnDevice {
     double slot_mean = 0;
   };
   std::vector<ProbeDev> probes_;
+  bool probe_by_bdf_ = false;  // probes paired with exporter devices by PCI address (else hip_id)
 
   std::atomic<bool> running_{false};
   std::atomic<bool> stopped_{false};

@@ -185,6 +185,25 @@ struct gpumon_probe {
 
 EXPORT int gpumon_probe_abi_version(void) { return GPUMON_ONDEVICE_ABI; }
 EXPORT int gpumon_probe_device_count(void) { return agents(); }
+// PCI address per HIP ordinal from GPUMON_FAKE_PCI ("0000:65:00.0,0000:a5:00.0": a
+// HIP_VISIBLE_DEVICES-style subset of the mock's GPUs); unset = unknown, the exporter pairs by hip_id
+EXPORT size_t gpumon_probe_device_pci(int dev, char* buf, size_t n) {
+  const char* v = getenv("GPUMON_FAKE_PCI");
+  if (!v || dev < 0 || dev >= agents()) return 0;
+  char b[32];
+  const char* p = v;
+  for (int k = 0; k < dev && p; ++k) {
+    p = strchr(p, ',');
+    if (p) ++p;
+  }
+  if (!p || !*p) return 0;
+  const size_t len = strcspn(p, ",");
+  if (len >= sizeof b) return 0;
+  memcpy(b, p, len);
+  b[len] = 0;
+  if (buf && n) snprintf(buf, n, "%s", b);
+  return strlen(b) + 1;
+}
 EXPORT size_t gpumon_probe_device_arch(int, char* buf, size_t n) {
   if (buf && n) snprintf(buf, n, "gfx950:sramecc+:xnack-");
   return 23;

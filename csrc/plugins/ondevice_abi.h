@@ -90,6 +90,10 @@ int gpumon_probe_abi_version(void);
 int gpumon_probe_device_count(void);
 // Arch string of a HIP device ("gfx950:sramecc+:xnack-"), bytes needed incl. NUL.
 size_t gpumon_probe_device_arch(int hip_dev, char* buf, size_t buflen);
+// Optional: PCI address of a HIP device ("0000:75:00.0"), bytes needed incl. NUL (0: unknown). The
+// exporter pairs its devices with the helper's HIP ordinals by it: the helper's ordinals follow
+// HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES, the exporter's hip_id does not.
+size_t gpumon_probe_device_pci(int hip_dev, char* buf, size_t buflen);
 gpumon_probe* gpumon_probe_create(int hip_dev, int blocks, int slots, int spin_ticks, char* err, size_t errlen);
 int gpumon_probe_launch(gpumon_probe* p);  // slot >= 0, or -1 when every slot is still in flight
 // 1 = complete (result filled), 0 = not yet (after waiting up to timeout_s; 0 = just poll)

@@ -63,6 +63,7 @@ struct ProbeLib {
   int (*launch)(gpumon_probe*) = nullptr;
   int (*wait)(gpumon_probe*, int, double, gpumon_probe_result_t*) = nullptr;
   void (*destroy)(gpumon_probe*) = nullptr;
+  size_t (*pci)(int, char*, size_t) = nullptr;  // optional
   std::vector<gpumon_probe*> handles;  // handle id = index
 };
 ProbeLib g_probe;
@@ -90,6 +91,7 @@ bool probe_lib(std::string* err) {
   g_probe.launch = reinterpret_cast<int (*)(gpumon_probe*)>(dlsym(h, "gpumon_probe_launch"));
   g_probe.wait = reinterpret_cast<int (*)(gpumon_probe*, int, double, gpumon_probe_result_t*)>(dlsym(h, "gpumon_probe_wait"));
   g_probe.destroy = reinterpret_cast<void (*)(gpumon_probe*)>(dlsym(h, "gpumon_probe_destroy"));
+  g_probe.pci = reinterpret_cast<size_t (*)(int, char*, size_t)>(dlsym(h, "gpumon_probe_device_pci"));
   if (!abi || !g_probe.count || !g_probe.create || !g_probe.launch || !g_probe.wait || !g_probe.destroy) {
     *err = path + ": missing symbols";
     return false;
@@ -187,6 +189,17 @@ int main(int argc, char** argv) {
       case GPUMON_PROBE_OP_COUNT: {
         std::string e;
         ok = probe_lib(&e) ? reply(g_probe.count(), 0, "", nullptr, 0) : reply(-1, 0, e, nullptr, 0);
+        break;
+      }
+      case GPUMON_PROBE_OP_PCI: {
+        std::string e;
+        char b[64] = {0};
+        if (agents.empty() || !probe_lib(&e)) {
+          ok = reply(-1, 0, e.empty() ? "bad probe pci request" : e, nullptr, 0);
+          break;
+        }
+        const size_t len = g_probe.pci ? g_probe.pci(agents[0], b, sizeof b) : 0;
+        ok = len > 0 ? reply(static_cast<int>(strlen(b)), 0, "", b, strlen(b)) : reply(0, 0, "", nullptr, 0);
         break;
       }
       case GPUMON_PROBE_OP_CREATE: {

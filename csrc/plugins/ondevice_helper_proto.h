@@ -36,6 +36,7 @@ enum gpumon_pmc_op : uint32_t {
   // window_s = timeout -> rc = n, payload gpumon_probe_cycle_t[n]. Launch and completion are seen
   // within one awake period, so host_latency_s never includes the time the helper was stopped.
   GPUMON_PROBE_OP_CYCLE = 15,
+  GPUMON_PROBE_OP_PCI = 16,        // agents = {hip_dev} -> rc = bytes, payload = "dddd:bb:dd.f" (rc 0: unknown)
 };
 
 typedef struct {

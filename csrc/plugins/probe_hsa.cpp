@@ -116,6 +116,21 @@ struct Kernel {
 
 int gpu_count() { return agents().up ? static_cast<int>(agents().gpus.size()) : 0; }
 
+std::string gpu_pci(int index) {
+  const Agents& a = agents();
+  if (!a.up || index < 0 || index >= static_cast<int>(a.gpus.size())) return "";
+  uint32_t bdf = 0, domain = 0;
+  if (hsa_agent_get_info(a.gpus[index], static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_BDFID), &bdf) !=
+      HSA_STATUS_SUCCESS)
+    return "";
+  if (hsa_agent_get_info(a.gpus[index], static_cast<hsa_agent_info_t>(HSA_AMD_AGENT_INFO_DOMAIN), &domain) !=
+      HSA_STATUS_SUCCESS)
+    domain = 0;
+  char buf[32];  // BDFID: bus[15:8] device[7:3] function[2:0]
+  snprintf(buf, sizeof buf, "%04x:%02x:%02x.%x", domain & 0xffff, (bdf >> 8) & 0xff, (bdf >> 3) & 0x1f, bdf & 0x7);
+  return buf;
+}
+
 std::string gpu_arch(int index) {
   const Agents& a = agents();
   if (!a.up || index < 0 || index >= static_cast<int>(a.gpus.size())) return "";

@@ -27,6 +27,7 @@ namespace gpumon_hsa {
 // HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES / GPU_DEVICE_ORDINAL reorders HIP's view).
 int gpu_count();                   // brings HSA up on first use (hsa_init); 0 when it cannot
 std::string gpu_arch(int index);   // "gfx950:sramecc+:xnack-", "" for a bad index
+std::string gpu_pci(int index);    // "0000:75:00.0" (HSA_AMD_AGENT_INFO_DOMAIN / _BDFID), "" if unknown
 
 class HsaProbe {
  public:

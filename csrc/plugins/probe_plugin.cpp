@@ -103,6 +103,17 @@ GPUMON_EXPORT size_t gpumon_probe_device_arch(int hip_dev, char* buf, size_t buf
   }
 }
 
+GPUMON_EXPORT size_t gpumon_probe_device_pci(int hip_dev, char* buf, size_t buflen) {
+  try {
+    std::string a = use_hsa() ? gpumon_hsa::gpu_pci(agent_of(hip_dev)) : gpumon_hip::device_pci_bus_id(hip_dev);
+    if (a.empty()) return 0;
+    if (buf && buflen) snprintf(buf, buflen, "%s", a.c_str());
+    return a.size() + 1;
+  } catch (const std::exception&) {
+    return 0;
+  }
+}
+
 GPUMON_EXPORT gpumon_probe* gpumon_probe_create(int hip_dev, int blocks, int slots, int spin_ticks, char* err,
                                                 size_t errlen) {
   try {

@@ -77,3 +77,26 @@ def test_killed_helper_is_respawned_and_counts_again():
         load.terminate()
         load.wait(60)
     assert _helpers() == []
+
+
+@pytest.mark.parametrize("isolate", [False, True], ids=["in_process", "helper"])
+def test_probe_pairs_devices_by_pci_address(isolate):
+    """The K1 probe's runtime (raw HSA by default) reports each HIP ordinal's PCI address, and the
+    sampler pairs it with the exporter's device of the same BDF (libamd_smi): on this box the one
+    GPU is probed through that pairing, not by hip_id."""
+    from gpumon import core
+
+    c = core()
+    ex = c.Exporter({"backend": "amdsmi", "serve_http": False, "interval_s": 0.0, "processes": False,
+                     "log_level": "warn"})
+    assert ex.start() == ""
+    od = c.OnDevice(ex, {"probe": True, "probe_every_s": 60.0, "probe_blocks": 512, "ondevice_isolate": isolate})
+    od.start()
+    try:
+        od.step()
+        st = od.stats()
+        assert st["probe_by_bdf"] is True and st["probe_devices"] == len(ex.statics()) >= 1, st
+        assert st["probe_done"] >= 1, st
+    finally:
+        od.stop()
+        ex.stop()

@@ -475,6 +475,32 @@ def test_isolated_probe_runs_in_the_helper(core, mock_exporter, monkeypatch):
         od.stop()
 
 
+@pytest.mark.parametrize("isolate", [False, True], ids=["in_process", "helper"])
+def test_probe_devices_paired_by_pci_address(core, mock_exporter, monkeypatch, isolate):
+    """The probe's runtime numbers GPUs by HIP ordinal, which HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES
+    renumber; the exporter's gpu_id is node-wide. With the runtime seeing node GPUs 3 and 1 (in that
+    order) as ordinals 0 and 1, the probes land on gpu_id 3 and 1 -- paired by PCI address, in-process
+    and through the helper -- and the GPUs the runtime cannot see get none (round 3 paired by
+    hip_id: ordinal 0 -> gpu_id 0)."""
+    monkeypatch.setenv("GPUMON_FAKE_AGENTS", "2")
+    monkeypatch.setenv("GPUMON_FAKE_PCI", "0000:65:00.0,0000:25:00.0")  # mock GPUs 3 and 1
+    ex = mock_exporter(backend="mock:gpus=4")
+    od = _ondevice(core, ex, pmc=False, probe_every_s=60, ondevice_isolate=isolate)
+    od.start()
+    try:
+        od.step()
+        ex.tick()
+        m = ex.metrics_text()
+        s = od.stats()
+        assert s["probe_devices"] == 2 and s["probe_by_bdf"] is True
+        for g in ("1", "3"):
+            assert _val(m, "gpu_probe_xcd_blocks", gpu_id=g, xcd=0) is not None, g
+        for g in ("0", "2"):
+            assert _val(m, "gpu_probe_xcd_blocks", gpu_id=g, xcd=0) is None, g
+    finally:
+        od.stop()
+
+
 def test_isolated_exporter_maps_no_plugin():
     """The deployed shape: bin/gpumon-exporter with --pmc --probe maps neither plugin (nor, on a GPU
     node, the runtimes behind them); its one child, the helper, maps both."""
