@@ -36,7 +36,8 @@ def _rt_permitted() -> tuple:
     try:
         os.sched_setscheduler(0, os.SCHED_FIFO, os.sched_param(1))
     except PermissionError:
-        return WARN, "SCHED_FIFO not permitted (no CAP_SYS_NICE): rt_priority falls back to normal scheduling"
+        return WARN, ("SCHED_FIFO not permitted (no CAP_SYS_NICE): rt_priority / http_rt_priority fall back to normal "
+                      "scheduling")
     except OSError as e:
         return WARN, f"SCHED_FIFO: {e}"
     finally:
@@ -44,7 +45,43 @@ def _rt_permitted() -> tuple:
             os.sched_setscheduler(0, old[0], old[1])
         except OSError:
             pass
-    return OK, "SCHED_FIFO permitted: rt_priority keeps ticks on their deadline"
+    return OK, ("SCHED_FIFO permitted: rt_priority keeps ticks on their deadline, http_rt_priority keeps scrapes "
+                "fast on a saturated node")
+
+
+def fd_table_check(procfs: str = "/proc", pid=None) -> tuple:
+    """(status, detail): can this process read another uid's /proc/<pid>/fd table (the /dev/kfd
+    ownership check and the fast path's per-process DRM engine time)? Listing the directory needs
+    the same uid or CAP_DAC_READ_SEARCH, its links and fdinfo need CAP_SYS_PTRACE
+    (tests/test_capabilities.py)."""
+    me = os.getuid()
+    pids = [str(pid)] if pid is not None else sorted(os.listdir(procfs), key=lambda x: (len(x), x))
+    for p in pids:
+        if not p.isdigit() or int(p) == os.getpid():
+            continue
+        try:
+            if os.stat(f"{procfs}/{p}").st_uid == me:
+                continue
+        except OSError:
+            continue
+        try:
+            fds = os.listdir(f"{procfs}/{p}/fd")
+        except PermissionError:
+            return WARN, (f"pid {p} (uid {os.stat(f'{procfs}/{p}').st_uid}): its fd table cannot be listed (needs "
+                          "CAP_DAC_READ_SEARCH): tenants running as another uid get no /dev/kfd check and no DRM "
+                          "engine time")
+        except OSError:
+            continue
+        for fd in fds:
+            try:
+                os.readlink(f"{procfs}/{p}/fd/{fd}")
+                return OK, f"another uid's fd table is readable (pid {p})"
+            except PermissionError:
+                return WARN, (f"pid {p}: fd links unreadable (needs CAP_SYS_PTRACE): no /dev/kfd check and no DRM "
+                              "engine time for other uids' tenants")
+            except OSError:
+                continue
+    return SKIP, "no process of another uid with open files to try"
 
 
 def firmware_table_check(path: str, interval_s: float, prewarm_ms: float, seconds: float = 0.25) -> tuple:
@@ -181,7 +218,8 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
             m = re.search(r'^gpumon_kubelet_files_up\{[^}]*source="' + src + r'"[^}]*\} (\S+)$', text, re.M)
             up = float(m.group(1)) if m else None
             out.append((name, OK if up == 1 else WARN, f"{path}: readable" if up == 1 else f"{path}: unreadable: {lost}"))
-        out.append(("rt_priority",) + _rt_permitted())
+        out.append(("other uids' fd tables",) + fd_table_check())
+        out.append(("rt_priority / http_rt_priority",) + _rt_permitted())
         # on-device samplers: the helper and plugins must exist; --ondevice-check runs them once
         from ._native import core as _core
 
@@ -213,9 +251,14 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
                             f"{s['probe_devices']} device(s), {s['probe_done']} completed, "
                             f"{s['probe_timeouts']} timeouts"))
                 rss = _gauge(text, "gpumon_ondevice_helper_resident_memory_bytes")
+                model = _gauge(text, "gpumon_ondevice_helper_memory_model_bytes")
                 if rss:
-                    out.append(("on-device helper memory", OK,
-                                f"{rss / 2 ** 20:.0f} MiB resident (size the pod's memory limit for it)"))
+                    over = bool(model) and rss > 1.2 * model
+                    out.append(("on-device helper memory", WARN if over else OK,
+                                f"{rss / 2 ** 20:.0f} MiB resident"
+                                + (f", model {model / 2 ** 20:.0f} MiB for these samplers" if model else "")
+                                + (": above the model, raise the overlay's memory limit" if over else
+                                   " (the overlays are sized by the model)")))
             except RuntimeError as e:
                 out.append(("on-device samplers", FAIL, str(e)))
             finally:

@@ -52,8 +52,10 @@ def probe(f):
 fd_dir = probe(lambda: "3" in os.listdir(f"/proc/{pid}/fd"))
 fd_link = probe(lambda: os.readlink(f"/proc/{pid}/fd/3"))
 fdinfo = probe(lambda: "pos:" in open(f"/proc/{pid}/fdinfo/3").read())
+from gpumon import doctor
+doc = doctor.fd_table_check(pid=pid)
 print(json.dumps({"rt_threads": st["rt_threads"], "http_rt_loops": st["http_rt_loops"],
-                  "fd_dir": fd_dir, "fd_link": fd_link, "fdinfo": fdinfo,
+                  "fd_dir": fd_dir, "fd_link": fd_link, "fdinfo": fdinfo, "doctor": list(doc),
                   "families": len(fam), "samples": sum(len(f["samples"]) for n, f in fam.items()
                                                        if not n.startswith(("gpumon_", "process_")))}))
 """
@@ -99,6 +101,10 @@ def test_daemonset_capability_set_reads_what_root_reads(tmp_path):
     assert {k: ds[k] for k in ok} == ok
     # ... and the fd links / fdinfo still need SYS_PTRACE on top (ptrace_may_access)
     assert no_ptrace["fd_dir"] is True and no_ptrace["fd_link"] == "PermissionError"
+    # `gpumon doctor` names the missing capability in each case
+    assert full["doctor"][0] == ds["doctor"][0] == "ok"
+    assert r3_set["doctor"][0] == "warn" and "CAP_DAC_READ_SEARCH" in r3_set["doctor"][1]
+    assert no_ptrace["doctor"][0] == "warn" and "CAP_SYS_PTRACE" in no_ptrace["doctor"][1]
     # SCHED_FIFO sampler + device workers and both HTTP loops under SYS_NICE
     assert ds["rt_threads"] == full["rt_threads"] > 0 and ds["http_rt_loops"] == full["http_rt_loops"] == 2
     assert (ds["families"], ds["samples"]) == (full["families"], full["samples"])

@@ -31,7 +31,8 @@ def test_doctor_reports_sockets_and_plugins():
     assert checks["kubelet PodResources"][0] == "ok" and checks["CRI runtime"][0] == "ok"
     assert checks["sysfs fast path"][0] == "skip"  # mock backend
     assert checks["on-device plugins"][0] == "ok"
-    assert checks["rt_priority"][0] in ("ok", "warn")
+    assert checks["rt_priority / http_rt_priority"][0] in ("ok", "warn")
+    assert checks["other uids' fd tables"][0] in ("ok", "warn", "skip")
 
 
 def test_doctor_names_the_grpc_status_of_a_refusing_kubelet():
