@@ -277,6 +277,9 @@ def main() -> int:
                     help="untimed sampler-capacity run after the timed region (seconds; 0 = off)")
     ap.add_argument("--capacity-interval", type=float, default=0.001,
                     help="sampling interval of the capacity run (seconds)")
+    ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
+                    help="DIAGNOSTIC: extra exporter config keys for the timed exporter (gpumon.config.Config), "
+                         "e.g. --set processes=false --set gzip=false; listed in the line as exporter_overrides")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -356,6 +359,8 @@ def main() -> int:
                      http_rt_priority=args.http_rt_priority,
                      enable_probe=args.probe and has_gpu, log_level="warn", fast_path=not args.no_fast_path,
                      sample_threads=args.sample_threads, rt_priority=args.rt_priority, prewarm_ms=args.prewarm_ms)
+        if args.set:
+            cfg.apply_dict(dict(kv.split("=", 1) for kv in args.set))
         mon = GpuMonitor(cfg, control_plane=False).start()
         if mon.start_error:
             raise SystemExit(f"exporter backend failed: {mon.start_error}")
@@ -679,6 +684,7 @@ def main() -> int:
             "sampler_rt_threads": s1.get("rt_threads", 0),
             "http_rt_loops": s1.get("http_rt_loops"),
             "prewarm_ms": args.prewarm_ms,
+            "exporter_overrides": args.set or None,
             # the exporter's own threads over the timed region, serving the scrape load too (1/100 s ticks)
             "exporter_cpu_millicores": round(1000.0 * (cpu1 - cpu0) / elapsed, 2),
             "backend_call_us": {k: round((v["seconds"] - s0["backend_calls"].get(k, {}).get("seconds", 0.0)) * 1e6
