@@ -352,8 +352,14 @@ void LoadGen::loop(bool alternate, bool mfma, void* stream) {
     check(hipSetDevice(dev_), "hipSetDevice");
     hipStream_t s = static_cast<hipStream_t>(stream);
     hipEvent_t e0, e1;
-    check(hipEventCreate(&e0), "hipEventCreate");
-    check(hipEventCreate(&e1), "hipEventCreate");
+    // GPUMON_LOAD_SYNC=blocking: the batch's completion event is a blocking-sync event, so this host
+    // thread sleeps until the GPU interrupt instead of spin-polling for the batch (HIP's default
+    // wait): an A/B knob for how a tenant's spinning host thread shows in scrape tails
+    // (profiles/r4_scrape_contention.md); default: HIP's default event, as most tenants use.
+    const char* sync = getenv("GPUMON_LOAD_SYNC");
+    const unsigned ev_flags = sync && !strcmp(sync, "blocking") ? hipEventBlockingSync : hipEventDefault;
+    check(hipEventCreateWithFlags(&e0, ev_flags), "hipEventCreate");
+    check(hipEventCreateWithFlags(&e1, ev_flags), "hipEventCreate");
     const int cus = device_cu_count(dev_);
     // 8 blocks x 4 waves requested per CU (residency then limited by VGPRs: ~7 waves/SIMD at 68 VGPRs);
     // partial: ~1/4 of the CUs busy; concurrent: 4 waves per SIMD, leaving wave slots for the HBM
