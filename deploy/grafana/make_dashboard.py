@@ -141,7 +141,17 @@ def build():
                         fieldConfig={"defaults": {"unit": "s"}, "overrides": []}))
     panels.append(panel("Exporter: samples/s and errors", "timeseries",
                         [(f'rate(gpumon_samples_total{{{HOST}}}[1m])', "{{host}} samples/s"),
-                         (f'sum by (host) (rate(gpumon_sample_errors_total{{{HOST}}}[5m]))', "{{host}} errors/s")],
+                         (f'sum by (host) (rate(gpumon_sample_errors_total{{{HOST}}}[5m]))', "{{host}} errors/s"),
+                         (f'rate(gpumon_stale_samples_total{{{HOST}}}[1m])', "{{host}} stale (repeated table)/s")],
+                        12, y, 12, 8))
+    y += 8
+    panels.append(panel("Firmware metrics table age (s); a frozen SMU table withholds rates", "timeseries",
+                        [(f'gpu_metrics_table_age_seconds{{{HOST}}}', "{{host}} gpu{{gpu_id}} age"),
+                         (f'gpu_metrics_table_frozen{{{HOST}}} > 0', "{{host}} gpu{{gpu_id}} FROZEN")], 0, y, 12, 8,
+                        fieldConfig={"defaults": {"unit": "s"}, "overrides": []}))
+    panels.append(panel("Exporter: HTTP loops at SCHED_FIFO / budget demotions (request floods)", "timeseries",
+                        [(f'gpumon_http_rt_loops{{{HOST}}}', "{{host}} RT loops"),
+                         (f'rate(gpumon_http_rt_demotions_total{{{HOST}}}[5m])', "{{host}} demotions/s")],
                         12, y, 12, 8))
     return {
         "title": "gpumon — MI355X GPU cluster",
