@@ -97,7 +97,8 @@ def test_metrics_doc_is_current():
 NOT_FAMILIES = {"gpu_id", "gpu_uuid", "gpu_metrics", "gpu_activity", "gpu_vram_bad_pages"}
 NOT_FAMILY_PREFIXES = ("gpumon_pmc_abi", "gpumon_pmc_agent", "gpumon_pmc_init", "gpumon_pmc_read_running",
                        "gpumon_pmc_sample_many", "gpumon_pmc_stop_running", "gpumon_probe_abi", "gpumon_probe_create",
-                       "gpumon_probe_destroy", "gpumon_probe_device_count", "gpumon_probe_launch", "gpumon_probe_wait")
+                       "gpumon_probe_destroy", "gpumon_probe_device_count", "gpumon_probe_device_pci", "gpumon_probe_launch",
+                       "gpumon_probe_wait")
 
 
 def test_metrics_doc_matches_the_product():

@@ -142,13 +142,20 @@ def collect():
         add(_families(ex), "http_rt_priority")
     ex.stop()
     # backend-specific self-metrics: the libamd_smi backend over the fake library
-    os.environ.setdefault("FAKE_AMDSMI_GPUS", "1")
-    ex = c.Exporter({"backend": "amdsmi", "amdsmi_lib": os.path.join(ROOT, "build", "fakes", "libfake_amd_smi.so"),
-                     "serve_http": False, "interval_s": 0, "host": "node", "verify_kfd": False})
-    if ex.start() == "":
-        ex.tick()
-        add(_families(ex), "amdsmi backend")
-    ex.stop()
+    saved = os.environ.get("FAKE_AMDSMI_GPUS")  # the fake reads it at init; leave the caller's env as it was
+    os.environ["FAKE_AMDSMI_GPUS"] = "1"
+    try:
+        ex = c.Exporter({"backend": "amdsmi", "amdsmi_lib": os.path.join(ROOT, "build", "fakes", "libfake_amd_smi.so"),
+                         "serve_http": False, "interval_s": 0, "host": "node", "verify_kfd": False})
+        if ex.start() == "":
+            ex.tick()
+            add(_families(ex), "amdsmi backend")
+        ex.stop()
+    finally:
+        if saved is None:
+            os.environ.pop("FAKE_AMDSMI_GPUS", None)
+        else:
+            os.environ["FAKE_AMDSMI_GPUS"] = saved
     return out
 
 
