@@ -534,10 +534,10 @@ def main() -> int:
     # event-timed TFLOP/s / TB/s over the timed region, gathered to rank 0 as one row per GPU
     lrates = [[0.0, 0.0, 0.0] for _ in range(n)]
     for d, a, b in zip(my_devs, l0, l1):
-        dm, dh = b["mfma_s"] - a["mfma_s"], b["hbm_s"] - a["hbm_s"]
-        lrates[d][0] = (b["flops"] - a["flops"]) / dm / 1e12 if dm > 0 else 0.0
-        lrates[d][1] = (b["bytes"] - a["bytes"]) / dh / 1e12 if dh > 0 else 0.0
-        lrates[d][2] = (b["busy_s"] - a["busy_s"]) / max(1e-9, b["wall_s"] - a["wall_s"])
+        from gpumon.ops.load import SyntheticLoad
+
+        r = SyntheticLoad.rates(a, b)
+        lrates[d] = [r["tflops"], r["tbps"], r["busy"]]
     if dist is not None:
         t = torch.tensor(lrates, dtype=torch.float64, device=device)
         dist.all_reduce(t)

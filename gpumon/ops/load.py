@@ -28,13 +28,36 @@ from __future__ import annotations
 
 from .._native import hip
 
+KINDS = ("mfma", "hbm", "mixed", "concurrent", "partial")
+DTYPES = ("bf16", "f16", "fp8", "f32", "f64", "i8", "mxfp8", "mxfp4")
+
 
 class SyntheticLoad:
     def __init__(self, dev: int = 0, kind: str = "mixed", duty: float = 1.0, hbm_bytes: int = 1 << 30,
                  mfma_iters: int = 8192, mfma_shape: int = 16, mfma_dtype: str = "bf16", period_s: float = 0.0):
+        if kind not in KINDS:
+            raise ValueError(f"load kind {kind!r}: one of {', '.join(KINDS)}")
+        if mfma_dtype not in DTYPES:
+            raise ValueError(f"mfma_dtype {mfma_dtype!r}: one of {', '.join(DTYPES)}")
+        if not 0.0 < duty <= 1.0:
+            raise ValueError(f"duty {duty}: in (0, 1]")
+        if mfma_shape not in (16, 32):
+            raise ValueError(f"mfma_shape {mfma_shape}: 16 or 32")
         self._g = hip().LoadGen(dev, kind, duty, hbm_bytes, mfma_iters, mfma_shape, mfma_dtype, period_s)
         self.dev = dev
         self.kind = kind
+
+    @staticmethod
+    def rates(a: dict, b: dict) -> dict:
+        """The load's event-timed rates between two ``stats()`` snapshots: TFLOP/s over the MFMA
+        batches' GPU time, TB/s over the HBM batches' GPU time (each counts only while its own kernel
+        kind ran, so a mixed load's phases are not averaged in), and ``busy`` = GPU time / wall time
+        (the duty the GPU saw)."""
+        dm, dh = b["mfma_s"] - a["mfma_s"], b["hbm_s"] - a["hbm_s"]
+        wall = b["wall_s"] - a["wall_s"]
+        return {"tflops": (b["flops"] - a["flops"]) / dm / 1e12 if dm > 0 else 0.0,
+                "tbps": (b["bytes"] - a["bytes"]) / dh / 1e12 if dh > 0 else 0.0,
+                "busy": (b["busy_s"] - a["busy_s"]) / wall if wall > 0 else 0.0}
 
     def start(self) -> "SyntheticLoad":
         self._g.start()
