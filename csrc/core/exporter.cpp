@@ -2033,7 +2033,10 @@ bool Exporter::files_poll_once() {
     }
   }
   size_t exited = 0;
-  if (std::any_of(allocs.begin(), allocs.end(), [](const Allocation& a) { return !a.container_id.empty(); })) {
+  // one /proc/*/cgroup pass per refresh, only when these allocations are used (publish_allocations:
+  // not while PodResources is polled) and some carry a container id to check
+  if (cfg_.pod_resources_socket.empty() &&
+      std::any_of(allocs.begin(), allocs.end(), [](const Allocation& a) { return !a.container_id.empty(); })) {
     std::unordered_set<std::string> running;
     if (running_container_ids(cfg_.attribution.procfs_root, &running)) {
       const size_t before = allocs.size();
