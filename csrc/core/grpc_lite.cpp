@@ -1,7 +1,9 @@
 #include "grpc_lite.h"
 
+#include <fcntl.h>
 #include <poll.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <sys/un.h>
 #include <unistd.h>
 
@@ -22,6 +24,7 @@ enum : uint8_t {
 };
 enum : uint8_t { kEndStream = 0x1, kAck = 0x1, kEndHeaders = 0x4, kPadded = 0x8, kPriority = 0x20 };
 constexpr uint32_t kWindow = 16u << 20;
+constexpr size_t kMaxResponse = 64u << 20;  // buffered frames, and the reassembled body
 
 void frame(std::string* o, uint8_t type, uint8_t flags, uint32_t stream, std::string_view payload) {
   const uint32_t n = static_cast<uint32_t>(payload.size());
@@ -139,10 +142,17 @@ bool grpc_unary_unix(const std::string& socket_path, const std::string& path, co
     return false;
   }
   memcpy(sa.sun_path, path_only.c_str(), path_only.size() + 1);
+  // The deadline covers every step: a unix-socket connect() blocks while the listener's backlog is
+  // full, and is bounded by SO_SNDTIMEO; after it the socket is non-blocking, so a server that
+  // accepts and never reads cannot stall write_all() past the deadline.
+  const int sndto_ms = std::max(timeout_ms, 1);  // a zero SO_SNDTIMEO would mean "block forever"
+  timeval tv{sndto_ms / 1000, (sndto_ms % 1000) * 1000};
+  ::setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
   if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) {
     *err = "connect " + path_only + ": " + strerror(errno);
     return false;
   }
+  ::fcntl(fd, F_SETFL, ::fcntl(fd, F_GETFL) | O_NONBLOCK);
   std::string out = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
   std::string settings;
   auto setting = [&](uint16_t id, uint32_t v) {
@@ -232,6 +242,10 @@ bool grpc_unary_unix(const std::string& socket_path, const std::string& path, co
           return false;
         }
         body.append(pl.substr(start, pl.size() - start - pad));
+        if (body.size() > kMaxResponse) {
+          *err = "response too large";
+          return false;
+        }
         if (flags & kEndStream) ended = true;
       } else if ((type == kHeaders || type == kContinuation) && stream == 1) {
         // response headers, trailers, or a Trailers-Only error response
@@ -288,7 +302,7 @@ bool grpc_unary_unix(const std::string& socket_path, const std::string& path, co
       return false;
     }
     in.append(buf, static_cast<size_t>(n));
-    if (in.size() > (64u << 20)) {
+    if (in.size() > kMaxResponse + 9) {
       *err = "response too large";
       return false;
     }

@@ -57,24 +57,6 @@ std::vector<float> Histogram::since(uint64_t from, uint64_t* end) const {
   return v;
 }
 
-double Histogram::bucket_quantile(double q) const {
-  std::vector<uint64_t> c(bounds_.size() + 1);
-  uint64_t total = 0;
-  for (size_t i = 0; i <= bounds_.size(); ++i) total += (c[i] = counts_[i].load());
-  if (!total) return NAN;
-  double target = q * total;
-  uint64_t cum = 0;
-  for (size_t i = 0; i <= bounds_.size(); ++i) {
-    if (cum + c[i] >= target && c[i] > 0) {
-      double lo = i == 0 ? 0.0 : bounds_[i - 1];
-      double hi = i < bounds_.size() ? bounds_[i] : bounds_.back() * 2;
-      return lo + (hi - lo) * (target - cum) / c[i];
-    }
-    cum += c[i];
-  }
-  return bounds_.back();
-}
-
 std::vector<double> latency_buckets() {
   return {50e-6, 100e-6, 250e-6, 500e-6, 1e-3, 2.5e-3, 5e-3, 10e-3, 25e-3,
           50e-3, 100e-3, 250e-3, 500e-3, 1.0,  2.5,    5.0,  10.0};

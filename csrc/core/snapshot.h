@@ -48,8 +48,6 @@ class Histogram {
   // Quantile of the last kRecent observations, exact (the exported buckets are what Prometheus
   // aggregates; a bucket-interpolated p99 between 1 and 2.5 ms says little about a 1.1 ms tick).
   double quantile(double q) const;
-  // Bucket-interpolated estimate over every observation (what histogram_quantile() would say).
-  double bucket_quantile(double q) const;
 
   // Observations with index >= `from` (0-based, in arrival order) still held by the ring, and the
   // index one past the newest: an exact window quantile for a caller that noted observed() first.

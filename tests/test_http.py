@@ -7,9 +7,11 @@ for not tearing responses while the sampler swaps snapshots.
 
 import gzip
 import http.client
+import math
 import socket
 import threading
 
+import pytest
 
 from gpumon.export import promtext
 
@@ -155,6 +157,24 @@ def test_native_scrape_load_latency(mock_exporter, core):
     ex.tick()
     fam = promtext.parse(ex.metrics_text())
     assert promtext.values(fam, "gpumon_scrape_duration_seconds_count")[0] >= 1
+
+
+def test_exact_window_quantiles_match_the_recorded_durations(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=2", interval_s=0)
+    assert math.isnan(ex.scrape_quantile(0.99))
+    ex.tick()
+    ex.tick()
+    for _ in range(50):
+        assert _get(ex.port, "/metrics")[0] == 200
+    d = sorted(ex.scrape_durations_since(0))
+    assert len(d) == ex.scrape_count() >= 50
+    # Nearest-rank quantile over the ring: q=0 is the minimum, q=1 the maximum, q=0.5 the
+    # ceil(n/2)-th smallest. float32 ring, so compare at float precision.
+    assert ex.scrape_quantile(0.0) == pytest.approx(d[0], rel=1e-6)
+    assert ex.scrape_quantile(1.0) == pytest.approx(d[-1], rel=1e-6)
+    assert ex.scrape_quantile(0.5) == pytest.approx(d[math.ceil(0.5 * len(d)) - 1], rel=1e-6)
+    s50, s100 = ex.sample_quantile(0.5), ex.sample_quantile(1.0)
+    assert 0 < s50 <= s100
 
 
 def test_port_conflict_reports_error(core):
