@@ -827,6 +827,7 @@ PYBIND11_MODULE(_core, m) {
              d["frozen_samples"] = s.frozen_samples;
              d["occupancy_reads"] = s.occupancy_reads;
              d["occupancy_scan_failures"] = s.occupancy_scan_failures;
+             d["process_list_failures"] = s.process_list_failures;
              d["http_rt_loops"] = s.http_rt_loops;
              d["http_rt_demotions"] = s.http_rt_demotions;
              d["hidden_contexts"] = s.hidden_contexts;
@@ -969,6 +970,7 @@ PYBIND11_MODULE(_core, m) {
       .def("mock_set_link_fail",
            [](Exporter& e, int dev, bool fail) { mock_of(e)->set_link_fail(dev, fail); })
       .def("mock_fail_scans", [](Exporter& e, int dev, int n) { mock_of(e)->fail_scans(dev, n); })
+      .def("mock_fail_procs", [](Exporter& e, int dev, int n) { mock_of(e)->fail_procs(dev, n); })
       .def("mock_set_firmware_frozen",
            [](Exporter& e, int dev, bool frozen) { mock_of(e)->set_firmware_frozen(dev, frozen); })
       .def("mock_set_occ_series",

@@ -628,6 +628,12 @@ bool AmdSmiBackend::prewarm(int i) {
   return t_->amdsmi_get_gpu_metrics_info(handles_[i], &m) == AMDSMI_STATUS_SUCCESS;
 }
 
+bool AmdSmiBackend::supports_processes(int i) const {
+  if (i < 0 || i >= static_cast<int>(caps_.size())) return false;
+  const bool kfd = i < static_cast<int>(fast_.size()) && fast_[i] && fast_[i]->have_kfd();
+  return kfd || (caps_[i].procs && t_ && t_->amdsmi_get_gpu_process_list);
+}
+
 bool AmdSmiBackend::supports_occupancy(int i) const {
   return i >= 0 && i < static_cast<int>(fast_.size()) && fast_[i] && fast_[i]->have_kfd();
 }

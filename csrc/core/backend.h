@@ -35,6 +35,9 @@ class Backend {
   virtual void sample(int i, DeviceSample* out) = 0;
   // GPU processes on device i. Returns false if the call failed.
   virtual bool processes(int i, std::vector<ProcSample>* out) = 0;
+  // Can device i list processes at all? A false processes() on a device that can is a failure
+  // (counted, and the last good list is held for a few ticks); on one that cannot, it is not.
+  virtual bool supports_processes(int /*i*/) const { return true; }
   // Optional: per-link metrics are expensive (~1 ms); sampled every `link_every` ticks.
   virtual bool supports_links() const { return false; }
   virtual void sample_links(int, DeviceSample*) {}
@@ -210,6 +213,8 @@ class MockBackend : public Backend {
   void set_firmware_frozen(int dev, bool frozen);
   // The next `n` occupancy_scan() calls of `dev` fail as a transient error would (occupancy stays supported).
   void fail_scans(int dev, int n);
+  // The next `n` processes() calls of `dev` fail as a transient library error would.
+  void fail_procs(int dev, int n);
   uint64_t calls(int dev) const;
   bool prewarm(int i) override;
   uint64_t prewarms(int dev) const;  // prewarm() calls
@@ -227,6 +232,7 @@ class MockBackend : public Backend {
   std::vector<uint64_t> link_calls_;
   std::vector<char> link_fail_;
   std::vector<int64_t> frozen_tick_;
+  std::vector<int> procs_fail_;      // per dev: process lists still to fail
   std::vector<int> scan_fail_;       // per dev: occupancy scans still to fail  // per dev: firmware tick the fake SMU is stuck at (-1 = running)
   std::vector<uint64_t> calls_, prewarms_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
@@ -254,6 +260,7 @@ class AmdSmiBackend : public Backend {
   const DeviceStatic& static_info(int i) const override { return devs_[i]; }
   void sample(int i, DeviceSample* out) override;
   bool processes(int i, std::vector<ProcSample>* out) override;
+  bool supports_processes(int i) const override;
   bool supports_links() const override;
   void sample_links(int i, DeviceSample* out) override;
   bool supports_ras() const override { return true; }

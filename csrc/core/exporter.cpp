@@ -132,6 +132,7 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
     std::condition_variable cv;
     bool want = false, done = false, quit = false;
     std::vector<ProcSample> out;
+    bool ok = false;
     int64_t ns = 0;
   };
   std::shared_ptr<ProcJob> job;
@@ -148,10 +149,11 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
         lk.unlock();
         std::vector<ProcSample> p;
         const int64_t t = mono_ns();
-        backend->processes(i, &p);
+        const bool ok = backend->processes(i, &p);
         const int64_t ns = mono_ns() - t;
         lk.lock();
         job->out = std::move(p);
+        job->ok = ok;
         job->ns = ns;
         job->done = true;
         job->cv.notify_all();
@@ -307,12 +309,14 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
         if (s.ok) {
           p = std::move(job->out);
           pns = job->ns;
+          s.procs_read = job->ok ? 1 : backend->supports_processes(i) ? -1 : 0;
         }
         job->out.clear();
       } else if (procs && s.ok) {
         const int64_t t = mono_ns();
-        backend->processes(i, &p);
+        const bool ok = backend->processes(i, &p);
         pns = mono_ns() - t;
+        s.procs_read = ok ? 1 : backend->supports_processes(i) ? -1 : 0;
       }
     }
     const bool ok_for_ras = s.ok;
@@ -333,6 +337,26 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       ps.cu_occupancy = n > 0 ? sum / n : kNaN;
       ps.occ_samples = n;
       ps.occ_busy = busy;
+    }
+    // A listed process that no sub-sample saw (it arrived after the last scan, or the scans are in
+    // their retry backoff) gets one read now, so its first row is not empty.
+    if (occ_on) {
+      std::vector<uint32_t> unread;
+      for (const auto& ps : p)
+        if (ps.occ_samples == 0) unread.push_back(ps.pid);
+      if (!unread.empty()) {
+        backend->occupancy(i, unread, &vals);
+        occ_reads->fetch_add(unread.size(), std::memory_order_relaxed);
+        size_t k = 0;
+        for (auto& ps : p)
+          if (ps.occ_samples == 0 && k < vals.size()) {
+            const double v = vals[k++];
+            if (!has(v)) continue;
+            ps.cu_occupancy = v;
+            ps.occ_samples = 1;
+            ps.occ_busy = v > 0 ? 1 : 0;
+          }
+      }
     }
     if (occ_on && procs && ok_for_ras) {  // a failed tick listed nothing: keep sub-sampling the known pids
       occ_pids.clear();
@@ -749,7 +773,8 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
       }
       if (cfg_.processes && (*out)[i].ok) {
         const int64_t t = mono_ns();
-        backend_->processes(i, &(*procs)[i]);
+        const bool ok = backend_->processes(i, &(*procs)[i]);
+        (*out)[i].procs_read = ok ? 1 : backend_->supports_processes(i) ? -1 : 0;
         proc_ns += mono_ns() - t;
         for (auto& ps : (*procs)[i])
           if (has(ps.cu_occupancy)) {
@@ -1144,6 +1169,25 @@ TickInfo Exporter::tick() {
           dev_errors_[i] += s.ok ? s.errors : std::max<uint32_t>(1, s.errors);
       }
       if (s.ok) info.devices_ok++;
+      // A failed process list (a transient library or KFD error) keeps the last good list for up
+      // to kProcHoldTicks ticks instead of publishing "no processes": every pod row of the GPU and
+      // its sharing state would otherwise drop out for that tick. A device that never listed
+      // successfully, or that cannot list at all, holds nothing.
+      if (static_cast<int>(last_procs_.size()) != n) {
+        last_procs_.assign(n, {});
+        proc_hold_.assign(n, -1);
+      }
+      if (s.procs_read > 0) {
+        last_procs_[i] = procs[i];
+        proc_hold_[i] = 0;
+      } else if (s.procs_read < 0) {
+        proc_failures_++;
+        if (proc_hold_[i] >= 0 && proc_hold_[i] < kProcHoldTicks) {
+          procs[i] = last_procs_[i];
+          proc_hold_[i]++;
+          s.procs_held = true;
+        }
+      }
       proc_counts[i] = procs[i].size();
       // device-level spatial occupancy: CUs holding any process's waves (every process, opted in or not)
       if (s.ok && cfg_.processes) {
@@ -1194,6 +1238,14 @@ TickInfo Exporter::tick() {
                       "gauge", i, {}, !s.fresh && age > cfg_.stale_hold_s ? 1.0 : 0.0});
       }
       set_extra("table_age", std::move(fz));
+      std::vector<ExtraSeries> ph;
+      for (int i = 0; i < n; ++i)
+        if (cur[i].procs_read != 0)
+          ph.push_back({"gpu_process_list_held",
+                        "1 when this tick's process list failed and the GPU's last good list (at most 3 "
+                        "ticks old) stands in for it.",
+                        "gauge", i, {}, cur[i].procs_held ? 1.0 : 0.0});
+      set_extra("procs_held", std::move(ph));
     }
     int64_t tb = mono_ns();
     {
@@ -1629,6 +1681,7 @@ SelfStats Exporter::self_stats() const {
   s.frozen_samples = frozen_;
   s.occupancy_reads = occ_reads_->load(std::memory_order_relaxed);
   s.occupancy_scan_failures = scan_failures_->load(std::memory_order_relaxed);
+  s.process_list_failures = proc_failures_.load(std::memory_order_relaxed);
   s.hidden_contexts = hidden_contexts_.load();
   s.rt_threads = rt_threads_->load();
   if (cfg_.http_rt_priority > 0 && server_) {

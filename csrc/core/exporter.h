@@ -260,6 +260,10 @@ class Exporter {
   std::mutex seq_mu_;
   std::condition_variable seq_cv_;
   std::atomic<uint64_t> ticks_{0}, samples_{0}, stale_{0}, overruns_{0};
+  std::atomic<uint64_t> proc_failures_{0};  // failed process lists of devices that can list
+  static constexpr int kProcHoldTicks = 3;  // ticks a failed process list keeps the last good one
+  std::vector<std::vector<ProcSample>> last_procs_;  // per device: the last good process list
+  std::vector<int> proc_hold_;                       // per device: ticks held so far (-1: none good yet)
   std::atomic<uint64_t> frozen_{0};      // samples whose repeated table was older than stale_hold_s
   std::vector<int64_t> last_fresh_ns_;   // per device: host time the firmware table last advanced (tick_mu_)
   size_t last_body_bytes_ = 0;  // tick thread only: sizes the next render buffer

@@ -27,6 +27,7 @@ namespace gpumon {
 namespace {
 
 constexpr size_t kMaxHeader = 16 * 1024;
+constexpr long kMaxBody = 64 * 1024;  // every route is GET/HEAD: a request body is only ever skipped
 constexpr int64_t kIdleTimeoutNs = 60LL * 1000000000LL;
 constexpr size_t kMaxConnsPerLoop = 4096;
 constexpr int kSndBuf = 1 << 20;  // GPUMON_HTTP_SNDBUF overrides (bytes; 0 = the kernel's autotuning)
@@ -37,6 +38,7 @@ const char* status_text(int s) {
     case 400: return "Bad Request";
     case 404: return "Not Found";
     case 405: return "Method Not Allowed";
+    case 413: return "Payload Too Large";
     case 431: return "Request Header Fields Too Large";
     case 503: return "Service Unavailable";
     default: return "Error";
@@ -64,7 +66,9 @@ bool set_nonblock(int fd) {
   return fl >= 0 && fcntl(fd, F_SETFL, fl | O_NONBLOCK) == 0;
 }
 
-// Parses one request from c->in. Returns bytes consumed (0 = incomplete, -1 = bad, -2 = too big).
+// Parses one request from c->in. Returns bytes consumed (0 = incomplete, -1 = bad, -2 = header
+// too big, -3 = body too big: buffering an announced body of any size would let one client grow
+// the connection's input without bound).
 long parse_request(const std::string& in, HttpRequest* r) {
   size_t end = in.find("\r\n\r\n");
   if (end == std::string::npos) return in.size() > kMaxHeader ? -2 : 0;
@@ -104,7 +108,11 @@ long parse_request(const std::string& in, HttpRequest* r) {
         for (auto& ch : v) ch = static_cast<char>(tolower(ch));
         r->accept_gzip = v.find("gzip") != std::string::npos;
       } else if (ieq(name, "content-length")) {
-        content_len = strtol(std::string(val).c_str(), nullptr, 10);
+        const std::string v(val);
+        char* endp = nullptr;
+        content_len = strtol(v.c_str(), &endp, 10);
+        if (v.empty() || *endp != '\0' || content_len < 0) return -1;
+        if (content_len > kMaxBody) return -3;
       }
     }
     pos = e + 2;
@@ -307,7 +315,7 @@ void HttpServer::run(Loop* L) {
       HttpResponse resp;
       const int64_t t_req = mono_ns();  // service time = handler + response write
       if (used < 0) {
-        resp.status = used == -2 ? 431 : 400;
+        resp.status = used == -2 ? 431 : used == -3 ? 413 : 400;
         resp.inline_body = status_text(resp.status);
         req.keep_alive = false;
         used = static_cast<long>(c.in.size());

@@ -75,6 +75,7 @@ bool MockBackend::init(std::string* err) {
   link_fail_.assign(n, 0);
   frozen_tick_.assign(n, -1);
   scan_fail_.assign(n, 0);
+  procs_fail_.assign(n, 0);
   calls_.assign(n, 0);
   prewarms_.assign(n, 0);
   energy_.assign(n, 1000000);
@@ -334,6 +335,10 @@ void MockBackend::sample(int i, DeviceSample* out) {
 bool MockBackend::processes(int i, std::vector<ProcSample>* out) {
   std::lock_guard<std::mutex> g(mu_);
   out->clear();
+  if (procs_fail_[i] > 0) {
+    --procs_fail_[i];
+    return false;
+  }
   double util = has(forced_util_[i]) ? forced_util_[i]
                                      : mock_util(cfg_, devs_[i].hip_id, (mono_ns() - t0_ns_) * 1e-9);
   for (const auto& p : cfg_.procs) {
@@ -450,6 +455,11 @@ void MockBackend::sample_links(int i, DeviceSample* out) {
   else if (cfg_.link_order == "rotate" && !es.empty()) std::rotate(es.begin(), es.begin() + 1, es.end());
   out->link_entries = std::move(es);
   out->links_read = 1;
+}
+
+void MockBackend::fail_procs(int dev, int n) {
+  std::lock_guard<std::mutex> g(mu_);
+  if (dev >= 0 && dev < static_cast<int>(procs_fail_.size())) procs_fail_[dev] = n;
 }
 
 void MockBackend::fail_scans(int dev, int n) {

@@ -840,6 +840,13 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       f.add(hl, static_cast<double>(s.occupancy_reads));
     }
     {
+      Family f(o, "gpumon_process_list_failures_total",
+               "Process lists of a GPU that can list processes that failed (a transient library or KFD "
+               "error); the GPU's last good list is kept for up to 3 ticks (gpu_process_list_held).",
+               "counter");
+      f.add(hl, static_cast<double>(s.process_list_failures));
+    }
+    {
       Family f(o, "gpumon_occupancy_scan_failures_total",
                "Device-worker KFD process listings that failed (retried after 1 s, doubling to 60 s; the known "
                "pids are re-read meanwhile).",

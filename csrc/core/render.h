@@ -62,6 +62,7 @@ struct SelfStats {
   uint64_t stale_samples = 0;
   uint64_t frozen_samples = 0;       // ... of those, repeats older than stale_hold_s (rates withheld)
   uint64_t occupancy_reads = 0;     // KFD cu_occupancy sub-sample reads by the device workers
+  uint64_t process_list_failures = 0;  // failed process lists (the last good one held kProcHoldTicks)
   uint64_t occupancy_scan_failures = 0;  // ... process listings that failed (retried with a backoff)
   uint64_t hidden_contexts = 0;     // GPU contexts without VRAM or waves left out of pod_gpu rows
   int rt_threads = 0;               // sampler / device-worker threads running SCHED_FIFO (rt_priority)

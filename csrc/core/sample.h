@@ -176,6 +176,8 @@ struct DeviceSample {
   std::array<LinkInfo, kMaxLinks> links;
   std::vector<LinkEntry> link_entries;  // raw link-metrics entries, on a link-refresh tick only
   int links_read = 0;                   // this tick's link-metrics read: 1 ok, -1 failed, 0 not made
+  int procs_read = 0;                   // this tick's process list: 1 ok, -1 failed, 0 not made/unsupported
+  bool procs_held = false;              // the process list is the last good one (procs_read -1)
   Accumulators acc;
   RasSample ras;                    // valid only on ticks that refreshed it (carried over otherwise)
   uint32_t errors = 0;              // failed calls this tick
@@ -194,6 +196,8 @@ struct DeviceSample {
     for (auto& l : links) l = LinkInfo{};
     link_entries.clear();
     links_read = 0;
+    procs_read = 0;
+    procs_held = false;
     acc = Accumulators{};
     ras = RasSample{};
     errors = 0;

@@ -21,6 +21,9 @@
 //                                 positional, counters equal to the table's)
 //   FAKE_AMDSMI_LINK_NUM=N        num_links reported (default: entries - 1, i.e. 7 for 8 entries,
 //                                 as measured: the count leaves out the self entry it fills)
+//   FAKE_AMDSMI_UNSUPPORTED=a,b   these calls return NOT_SUPPORTED (activity, power, vram, procs,
+//                                 links): firmware / partition modes without the query
+//   FAKE_AMDSMI_BUSY=a,b          these calls fail with AMDSMI_STATUS_BUSY (a transient error)
 // Counters advance deterministically per call so rates are checkable.
 #include <amd_smi/amdsmi.h>
 
@@ -29,6 +32,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "fake_metrics.h"
@@ -38,11 +42,23 @@ int g_gpus = 2, g_procs = 1, g_fail_metrics = -1, g_parts = 1;
 std::vector<int> g_link_slots;
 int g_link_num = -1;
 bool g_no_metrics = false;
+std::string g_unsupported, g_busy;  // ",name1,name2,"
 std::vector<uintptr_t> g_handles;
 std::atomic<uint64_t> g_calls[64];
 int env_int(const char* k, int d) {
   const char* v = getenv(k);
   return v ? atoi(v) : d;
+}
+std::string env_list(const char* k) {
+  const char* v = getenv(k);
+  return std::string(",") + (v ? v : "") + ",";
+}
+// NOT_SUPPORTED / BUSY when the call is listed in FAKE_AMDSMI_UNSUPPORTED / FAKE_AMDSMI_BUSY.
+amdsmi_status_t scripted(const char* call) {
+  const std::string k = std::string(",") + call + ",";
+  if (g_unsupported.find(k) != std::string::npos) return AMDSMI_STATUS_NOT_SUPPORTED;
+  if (g_busy.find(k) != std::string::npos) return AMDSMI_STATUS_BUSY;
+  return AMDSMI_STATUS_SUCCESS;
 }
 int dev_of(amdsmi_processor_handle h) {
   uintptr_t x = reinterpret_cast<uintptr_t>(h);
@@ -60,6 +76,8 @@ amdsmi_status_t amdsmi_init(uint64_t) {
   g_procs = env_int("FAKE_AMDSMI_PROCS", 1);
   g_fail_metrics = env_int("FAKE_AMDSMI_FAIL_METRICS", -1);
   g_no_metrics = env_int("FAKE_AMDSMI_NO_METRICS", 0) != 0;
+  g_unsupported = env_list("FAKE_AMDSMI_UNSUPPORTED");
+  g_busy = env_list("FAKE_AMDSMI_BUSY");
   g_parts = env_int("FAKE_AMDSMI_CPX", 0) ? 8 : 1;
   g_link_slots = {0, 1, 2, 3, 4, 5, 6, 7};
   g_link_num = env_int("FAKE_AMDSMI_LINK_NUM", -1);
@@ -179,6 +197,7 @@ amdsmi_status_t amdsmi_get_gpu_memory_partition(amdsmi_processor_handle, char* p
 }
 
 amdsmi_status_t amdsmi_get_power_info(amdsmi_processor_handle, amdsmi_power_info_t* p) {
+  if (amdsmi_status_t st = scripted("power"); st != AMDSMI_STATUS_SUCCESS) return st;
   memset(p, 0xFF, sizeof *p);
   p->socket_power = 250;
   p->current_socket_power = 250;
@@ -194,12 +213,14 @@ amdsmi_status_t amdsmi_get_energy_count(amdsmi_processor_handle, uint64_t* e, fl
 }
 
 amdsmi_status_t amdsmi_get_gpu_vram_usage(amdsmi_processor_handle h, amdsmi_vram_usage_t* v) {
+  if (amdsmi_status_t st = scripted("vram"); st != AMDSMI_STATUS_SUCCESS) return st;
   v->vram_total = 294896;
   v->vram_used = 283 + 1024 * dev_of(h);
   return AMDSMI_STATUS_SUCCESS;
 }
 
 amdsmi_status_t amdsmi_get_gpu_activity(amdsmi_processor_handle h, amdsmi_engine_usage_t* u) {
+  if (amdsmi_status_t st = scripted("activity"); st != AMDSMI_STATUS_SUCCESS) return st;
   memset(u, 0, sizeof *u);
   u->gfx_activity = 11 + dev_of(h);
   u->umc_activity = 5;
@@ -224,6 +245,7 @@ amdsmi_status_t amdsmi_get_gpu_metrics_info(amdsmi_processor_handle h, amdsmi_gp
 }
 
 amdsmi_status_t amdsmi_get_gpu_process_list(amdsmi_processor_handle h, uint32_t* max, amdsmi_proc_info_t* list) {
+  if (amdsmi_status_t st = scripted("procs"); st != AMDSMI_STATUS_SUCCESS) return st;
   int d = dev_of(h);
   const uint32_t n = static_cast<uint32_t>(g_procs);
   const uint32_t cap = *max;
@@ -242,6 +264,7 @@ amdsmi_status_t amdsmi_get_gpu_process_list(amdsmi_processor_handle h, uint32_t*
 }
 
 amdsmi_status_t amdsmi_get_link_metrics(amdsmi_processor_handle h, amdsmi_link_metrics_t* lm) {
+  if (amdsmi_status_t st = scripted("links"); st != AMDSMI_STATUS_SUCCESS) return st;
   const int d = dev_of(h);
   if (d < 0) return AMDSMI_STATUS_INVAL;
   memset(lm, 0, sizeof *lm);

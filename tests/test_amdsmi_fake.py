@@ -25,7 +25,7 @@ def fake_exporter(core, monkeypatch):
 
     def make(env=None, **over):
         for k in ("FAKE_AMDSMI_GPUS", "FAKE_AMDSMI_PROCS", "FAKE_AMDSMI_FAIL_METRICS", "FAKE_AMDSMI_INIT_FAIL",
-                  "FAKE_AMDSMI_NO_METRICS"):
+                  "FAKE_AMDSMI_NO_METRICS", "FAKE_AMDSMI_UNSUPPORTED", "FAKE_AMDSMI_BUSY"):
             monkeypatch.delenv(k, raising=False)
         for k, v in (env or {}).items():
             monkeypatch.setenv(k, str(v))
@@ -116,6 +116,77 @@ def test_no_metrics_table_falls_back_to_activity_api(fake_exporter):
     fam = promtext.parse(ex.metrics_text())
     assert promtext.one(fam, "node_gpu_gpu_util", gpu_id="1") == 12  # amdsmi_get_gpu_activity
     assert promtext.one(fam, "gpumon_backend_calls_total", call="gpu_activity") >= 2
+
+
+def _calls(fam, call):
+    return promtext.one(fam, "gpumon_backend_calls_total", call=call)
+
+
+def test_unsupported_queries_latch_off_per_device_and_field(fake_exporter):
+    """A query the firmware / partition mode does not offer (NOT_SUPPORTED) is dropped for good
+    after its first answer, per call: the fields it fed are omitted, the rest keep flowing, and no
+    error is counted. Without any query that answers the GPU is down."""
+    ex, _ = fake_exporter({"FAKE_AMDSMI_NO_METRICS": 1, "FAKE_AMDSMI_UNSUPPORTED": "activity,power"})
+    for _ in range(3):
+        ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert "node_gpu_gpu_util" not in fam and "gpu_power_watts" not in fam
+    assert promtext.one(fam, "node_gpu_mem_used", gpu_id="1") == 1307
+    assert promtext.values(fam, "gpu_up") == [1, 1]
+    assert _calls(fam, "gpu_activity") == 2 and _calls(fam, "power_info") == 2  # once per GPU, then latched
+    assert _calls(fam, "vram_usage") == 8  # start() + 3 ticks, 2 GPUs
+    assert promtext.values(fam, "gpumon_sample_errors_total") == [0, 0]
+
+    ex, _ = fake_exporter({"FAKE_AMDSMI_NO_METRICS": 1, "FAKE_AMDSMI_UNSUPPORTED": "activity,power,vram"})
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.values(fam, "gpu_up") == [0, 0]
+    assert "node_gpu_mem_used" not in fam
+
+
+def test_transient_errors_are_counted_and_retried(fake_exporter):
+    ex, _ = fake_exporter({"FAKE_AMDSMI_NO_METRICS": 1, "FAKE_AMDSMI_BUSY": "vram"})
+    ex.tick()
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.values(fam, "gpu_up") == [1, 1]  # activity still answers
+    assert promtext.one(fam, "node_gpu_gpu_util", gpu_id="1") == 12
+    assert "node_gpu_mem_used" not in fam
+    assert promtext.values(fam, "gpumon_sample_errors_total") == [3, 3]  # every tick, never latched
+    assert _calls(fam, "vram_usage") == 6
+
+
+def test_process_list_support_and_failures(fake_exporter):
+    """A device whose library cannot list processes is not failing: no failures counted, no held
+    list. A list that fails (BUSY) on a device that can is counted; having never listed, it holds
+    nothing."""
+    ex, _ = fake_exporter({"FAKE_AMDSMI_UNSUPPORTED": "procs"})
+    ex.tick()
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.values(fam, "gpu_process_count") == [0, 0]
+    assert promtext.one(fam, "gpumon_process_list_failures_total") == 0
+    assert "gpu_process_list_held" not in fam
+    assert _calls(fam, "process_list") == 2  # latched after the first answer
+    ex, _ = fake_exporter({"FAKE_AMDSMI_BUSY": "procs"})
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpumon_process_list_failures_total") == 4  # start() + 1 tick, 2 GPUs
+    assert promtext.values(fam, "gpu_process_list_held") == [0, 0]
+
+
+def test_link_metrics_unsupported_or_failing(fake_exporter):
+    ex, _ = fake_exporter({"FAKE_AMDSMI_UNSUPPORTED": "links"})
+    for _ in range(3):
+        ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert _calls(fam, "link_metrics") == 2  # asked once per GPU, then latched
+    assert promtext.values(fam, "gpu_xgmi_read_bytes_per_second", gpu_id="0")  # the table's traffic stays
+    ex, _ = fake_exporter({"FAKE_AMDSMI_BUSY": "links"})
+    for _ in range(3):
+        ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert _calls(fam, "link_metrics") == 8  # a failed refresh is retried on the next tick
 
 
 def test_init_failure_then_recovery(fake_exporter, monkeypatch):

@@ -103,6 +103,98 @@ def test_http1_response_framing(core):
             core.http1_parse_response(bad)
 
 
+@pytest.mark.parametrize("raw,error", [
+    (b"HTTP/1.1 200 OK\r\nContent-Length: x\r\n\r\n", "bad Content-Length"),
+    (b"HTTP/1.1 200 OK\r\nContent-Length: -4\r\n\r\nabcd", "bad Content-Length"),
+    (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nab", "truncated chunk"),
+    (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n5", "truncated chunk size"),
+    (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\nfffffffff\r\n", "bad chunk size"),
+    (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\nzz\r\n", "bad chunk size"),
+    (b"HTTP/1.1 200 OK\r\nContent-Length: 99\r\n\r\nshort", "truncated"),
+    (b"HTTP/2 200\r\n\r\n", "bad HTTP status line"),
+])
+def test_http1_response_errors_are_named(core, raw, error):
+    with pytest.raises(ValueError, match=error):
+        core.http1_parse_response(raw)
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.binary(max_size=200), st.booleans())
+def test_http1_reader_never_crashes_on_garbage(data, eof):
+    from gpumon import core as _core
+
+    for raw in (data, b"HTTP/1.1 200 OK\r\n" + data, b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n" + data):
+        try:
+            status, body = _core().http1_parse_response(raw, eof=eof)
+            assert isinstance(body, bytes) and len(body) <= len(raw)
+        except ValueError:
+            pass
+
+
+class _RawDaemon:
+    """A unix-socket peer that reads the request, then plays `script` (bytes, "close", or a float
+    to sleep) and holds the connection: the daemon misbehaviours a framed reader must survive."""
+
+    def __init__(self, path, script):
+        import socket as so
+
+        if os.path.exists(path):
+            os.unlink(path)
+        self.path, self.script, self.stop = path, script, threading.Event()
+        self.srv = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+        self.srv.bind(path)
+        self.srv.listen(2)
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def _run(self):
+        import time
+
+        conn, _ = self.srv.accept()
+        try:
+            req = b""
+            while b"\r\n\r\n" not in req:
+                req += conn.recv(4096)
+            for step in self.script:
+                if step == "close":
+                    return
+                if isinstance(step, float):
+                    time.sleep(step)
+                else:
+                    conn.sendall(step)
+            self.stop.wait(10)
+        except OSError:
+            pass
+        finally:
+            conn.close()
+
+    def close(self):
+        self.stop.set()
+        self.srv.close()
+        self.t.join(5)
+        os.unlink(self.path)
+
+
+@pytest.mark.parametrize("script,error", [
+    ([b"HTTP/1.1 200 OK\r\nContent-Length: 10\r\n\r\n[]"], "read timed out"),  # short and silent
+    ([b"HTTP/1.1 200 OK\r\n"], "read timed out"),  # headers never end
+    (["close"], "truncated HTTP response header"),  # hangs up before answering
+    ([b"HTTP/1.1 200 OK\r\nContent-Length: 5\r\n\r\n[", "close"], "truncated"),
+    ([b"HTTP/1.0 200 OK\r\n\r\n" + b" " * (1 << 20)] * 65, "response too large"),  # never ends
+])
+def test_native_docker_reader_bounds_a_misbehaving_daemon(core, script, error):
+    import time
+
+    d = _RawDaemon(_sock("raw"), script)
+    try:
+        t0 = time.monotonic()
+        with pytest.raises(RuntimeError, match=error):
+            core.docker_list(d.path, timeout_ms=400)
+        assert time.monotonic() - t0 < 3.0
+    finally:
+        d.close()
+
+
 class FakeDocker:
     """Docker Engine API subset on a unix socket: GET /containers/json (others 404). `containers`
     is a listing, or a callable returning the raw body of each response."""

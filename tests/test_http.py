@@ -9,6 +9,7 @@ import gzip
 import http.client
 import math
 import socket
+import struct
 import threading
 
 import pytest
@@ -316,3 +317,84 @@ def test_http_rt_loops_are_budget_capped(core):
         assert promtext.one(fam, "gpumon_http_rt_demotions_total") > 0
     finally:
         ex.stop()
+
+
+def test_slow_reader_gets_whole_pipelined_bodies_and_a_vanishing_one_is_dropped(mock_exporter, monkeypatch):
+    """A scraper that reads slower than the exposition is written: with a small send buffer the
+    server's writev() hits EAGAIN mid-body, parks the connection on EPOLLOUT and resumes; the
+    pipelined requests behind it are answered in order once it drains. A client that hangs up
+    mid-body costs only its own connection."""
+    import time
+
+    monkeypatch.setenv("GPUMON_HTTP_SNDBUF", "4096")
+    ex = mock_exporter(backend="mock:gpus=8", interval_s=0, gzip=False)
+    ex.tick()
+    want = ex.metrics_text().encode()
+    assert len(want) > 50_000
+    s = socket.create_connection(("127.0.0.1", ex.port))
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+    s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n" * 3)
+    time.sleep(0.3)  # the server fills both buffers and waits
+    buf = b""
+    bodies = []
+    s.settimeout(5)
+    while len(bodies) < 3:
+        while b"\r\n\r\n" not in buf:
+            buf += s.recv(1 << 16)
+        head, _, buf = buf.partition(b"\r\n\r\n")
+        assert head.startswith(b"HTTP/1.1 200")
+        n = int(next(h for h in head.split(b"\r\n") if h.lower().startswith(b"content-length:")).split(b":")[1])
+        while len(buf) < n:
+            buf += s.recv(1 << 16)
+        bodies.append(buf[:n])
+        buf = buf[n:]
+        time.sleep(0.05)
+    s.close()
+    assert bodies == [want] * 3
+    # hang up with a body half-written
+    s = socket.create_connection(("127.0.0.1", ex.port))
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+    s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n")
+    s.recv(1000)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))  # RST
+    s.close()
+    time.sleep(0.1)
+    assert _get(ex.port, "/metrics")[0] == 200
+
+
+def test_bad_listen_address_is_reported(core):
+    ex = core.Exporter({"backend": "mock", "listen_addr": "not-an-address", "port": 0, "interval_s": 0})
+    with pytest.raises(RuntimeError, match="bad listen address not-an-address"):
+        ex.start()
+    ex.stop()
+
+
+def _raw_exchange(port, data):
+    s = socket.create_connection(("127.0.0.1", port), timeout=5)
+    s.sendall(data)
+    out = b""
+    while True:
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        out += chunk
+    s.close()
+    return out
+
+
+def test_request_bodies_are_skipped_bounded_and_validated(mock_exporter):
+    ex = mock_exporter()
+    # a small body is skipped and the pipelined request behind it is answered
+    out = _raw_exchange(ex.port, b"GET /healthz HTTP/1.1\r\nContent-Length: 5\r\n\r\nhello"
+                                 b"GET /healthz HTTP/1.1\r\nConnection: close\r\n\r\n")
+    assert out.count(b"HTTP/1.1 200 OK") == 2, out
+    # a POST with a body: 405, and the body is not read as a request
+    out = _raw_exchange(ex.port, b"POST /metrics HTTP/1.1\r\nContent-Length: 4\r\n\r\nGET ")
+    assert out.startswith(b"HTTP/1.1 405") and out.count(b"HTTP/1.1") == 1, out
+    # an announced body larger than any route takes is refused at once, not buffered
+    out = _raw_exchange(ex.port, b"POST /metrics HTTP/1.1\r\nContent-Length: 1000000000000\r\n\r\nxxxx")
+    assert out.startswith(b"HTTP/1.1 413"), out
+    for bad in (b"-1", b"abc", b"12x", b""):
+        out = _raw_exchange(ex.port, b"GET /metrics HTTP/1.1\r\nContent-Length: " + bad + b"\r\n\r\n")
+        assert out.startswith(b"HTTP/1.1 400"), (bad, out)
+    assert _get(ex.port, "/metrics")[0] == 200

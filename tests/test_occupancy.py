@@ -281,3 +281,32 @@ def test_a_failed_tick_does_not_turn_every_process_into_an_arrival(mock_exporter
     fam = promtext.parse(ex.metrics_text())
     assert promtext.one(fam, "gpu_active_processes", gpu_id="0") == 1
     assert promtext.one(fam, "pod_gpu_mfma_util_percent", pid="7") == 42.5
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("threads", [0, -1])
+def test_failed_process_list_holds_the_last_good_one_for_three_ticks(mock_exporter, threads):
+    """A transient process-list failure does not publish "no processes" (every pod row of the GPU
+    and its sharing state would drop out for that tick): the last good list stands in for up to
+    3 ticks, flagged by gpu_process_list_held; the failures are counted either way."""
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=threads,
+                       mock={"procs": [{"pid": 4242, "device": 0, "name": "train"}]})
+
+    def state():
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())
+        pids = [r["pid"] for r in ex.pod_rows() if not r["idle"]]
+        return (pids, promtext.one(fam, "gpu_process_list_held", gpu_id="0"),
+                promtext.one(fam, "gpumon_process_list_failures_total"))
+
+    assert state() == (["4242"], 0, 0)
+    ex.mock_fail_procs(0, 2)
+    assert state() == (["4242"], 1, 1)
+    assert state() == (["4242"], 1, 2)
+    assert state() == (["4242"], 0, 2)  # listed again
+    ex.mock_fail_procs(0, 4)
+    assert [state() for _ in range(5)] == [(["4242"], 1, 3), (["4242"], 1, 4), (["4242"], 1, 5),
+                                           ([], 0, 6), (["4242"], 0, 6)]
+    assert ex.self_stats()["process_list_failures"] == 6

@@ -241,3 +241,56 @@ def test_reused_pid_is_not_read_at_the_old_fd_numbers(exporter, tmp_path, core):
     ex.tick()
     row = next(r for r in ex.pod_rows() if r["pid"] == "4242")
     assert row["used_memory_bytes"] == 3 << 30, row  # the new process's fd 11, not the old fds
+
+
+def _kfd_proc(sysr, pid, d=0, occ=17):
+    kp = sysr / "class" / "kfd" / "kfd" / "proc" / str(pid)
+    (kp / f"stats_{36622 + d}").mkdir(parents=True)
+    (kp / f"vram_{36622 + d}").write_text(f"{1 << 30}\n")
+    (kp / f"stats_{36622 + d}" / "cu_occupancy").write_text(f"{occ}\n")
+    return kp
+
+
+def test_between_tick_kfd_scans_read_arrivals_and_retry_after_a_failed_listing(exporter, tmp_path):
+    """The device workers' between-tick cu_occupancy reads through the sysfs fast path (the path a
+    real node runs; tests/test_occupancy.py drives the same worker logic through the mock backend).
+    A process that appears between ticks is found by the worker's own KFD listing and read from
+    then on; a listing that fails (the KFD proc dir gone) is counted and retried, not latched off."""
+    import shutil
+    import time
+
+    sysr, procr = make_tree(tmp_path, gpus=1)
+    ex = exporter(sysr, procr, interval_s=0.3, occ_samples=10, sample_threads=-1)
+    assert ex.wait_for_seq(ex.seq + 2, 10)
+    row = next(r for r in ex.pod_rows() if r["pid"] == "4242")
+    assert row["occ_samples"] >= 4, row  # sub-samples between ticks + the tick's own read
+    assert row["cu_occupancy"] == 17
+    # a tenant arrives right after a tick; no /proc entry (a pid of another namespace)
+    s0 = ex.seq
+    assert ex.wait_for_seq(s0 + 1, 10)
+    _kfd_proc(sysr, 5151, occ=200)
+    deadline = time.time() + 10
+    first = None
+    while first is None and time.time() < deadline:
+        assert ex.wait_for_seq(ex.seq + 1, 10)
+        first = next((r for r in ex.pod_rows() if r["pid"] == "5151"), None)
+    assert first is not None
+    # the first tick that lists it already carries reads from before the tick
+    assert first["occ_samples"] >= 2, first
+    assert first["cu_occupancy"] == 200 and first["proc_gfx_util"] == 100
+    assert ex.self_stats()["occupancy_reads"] > 0
+    assert ex.self_stats()["occupancy_scan_failures"] == 0
+    # the KFD proc directory disappears: each listing fails and is retried with a backoff
+    shutil.rmtree(sysr / "class" / "kfd" / "kfd" / "proc")
+    deadline = time.time() + 10
+    while ex.self_stats()["occupancy_scan_failures"] == 0 and time.time() < deadline:
+        time.sleep(0.05)
+    assert ex.self_stats()["occupancy_scan_failures"] >= 1
+    # and it comes back: the retry (1 s backoff) lists the new tenant again
+    _kfd_proc(sysr, 6161, occ=50)
+    deadline = time.time() + 10
+    row = None
+    while row is None and time.time() < deadline:
+        assert ex.wait_for_seq(ex.seq + 1, 10)
+        row = next((r for r in ex.pod_rows() if r["pid"] == "6161"), None)
+    assert row is not None and row["cu_occupancy"] == 50
