@@ -29,6 +29,11 @@ namespace {
 constexpr size_t kMaxHeader = 16 * 1024;
 constexpr long kMaxBody = 64 * 1024;  // every route is GET/HEAD: a request body is only ever skipped
 constexpr int64_t kIdleTimeoutNs = 60LL * 1000000000LL;
+// After the last response of a "Connection: close" exchange the server half-closes and drains what
+// the client still sends for at most this long before closing: closing a socket with unread input
+// sends a RST, which can make the client drop the response it has not read yet (an error answer to
+// a request whose body was still arriving).
+constexpr int64_t kLingerNs = 2LL * 1000000000LL;
 constexpr size_t kMaxConnsPerLoop = 4096;
 constexpr int kSndBuf = 1 << 20;  // GPUMON_HTTP_SNDBUF overrides (bytes; 0 = the kernel's autotuning)
 
@@ -56,6 +61,8 @@ struct Conn {
   size_t head_off = 0, body_off = 0;
   bool writing = false;
   bool close_after = false;
+  bool closing = false;  // response sent, write side shut: draining input until EOF / kLingerNs
+  int64_t closing_ns = 0;
   int64_t last_ns = 0;
   int64_t req_ns = 0;
   std::string path;
@@ -304,11 +311,17 @@ void HttpServer::run(Loop* L) {
     c.head.clear();
     c.head_off = c.body_off = 0;
     c.req_ns = 0;
-    return !c.close_after;
+    if (c.close_after) {  // lingering close (kLingerNs)
+      shutdown(c.fd, SHUT_WR);
+      c.closing = true;
+      c.closing_ns = mono_ns();
+      c.in.clear();
+    }
+    return true;
   };
   // Parses and answers as many complete requests as are buffered (pipelining).
   auto serve = [&](Conn& c) -> bool {
-    while (!c.writing) {
+    while (!c.writing && !c.closing) {
       HttpRequest req;
       long used = parse_request(c.in, &req);
       if (used == 0) return true;
@@ -433,6 +446,14 @@ void HttpServer::run(Loop* L) {
         }
         continue;
       }
+      if (c.closing) {  // discard input until the client closes too
+        char buf[8192];
+        ssize_t r;
+        while ((r = read(fd, buf, sizeof buf)) > 0) {
+        }
+        if (r == 0 || (errno != EAGAIN && errno != EINTR)) close_conn(fd);
+        continue;
+      }
       bool peer_closed = false;
       if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) {
         char buf[8192];
@@ -458,7 +479,7 @@ void HttpServer::run(Loop* L) {
       last_sweep = now;
       std::vector<int> idle;
       for (auto& [fd, c] : L->conns)
-        if (now - c.last_ns > kIdleTimeoutNs) idle.push_back(fd);
+        if (now - c.last_ns > kIdleTimeoutNs || (c.closing && now - c.closing_ns > kLingerNs)) idle.push_back(fd);
       for (int fd : idle) close_conn(fd);
     }
   }

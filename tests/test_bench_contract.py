@@ -113,7 +113,8 @@ def test_value_counts_fresh_samples_only():
     assert r.returncode == 0, r.stderr[-2000:]
     (d,) = _json_lines(r.stdout)
     assert d["value"] <= 50 * 1.15, d["value"]
-    assert d["samples_total"] >= 3 * d["value"] * d["ms_per_step"] * d["steps"] / 1e3
+    # ~4 samples per fresh table at 5 ms / 50 Hz; 2 leaves room for a loaded CI host
+    assert d["samples_total"] >= 2 * d["value"] * d["ms_per_step"] * d["steps"] / 1e3
     assert d["stale_samples"] == d["samples_total"] - round(d["value"] * d["ms_per_step"] * d["steps"] / 1e3)
     assert d["devices"] == [{"hip_ordinal": 0, "bdf": "0000:05:00.0", "gpu_id": "0"}]
     assert d["device_check"]["ok"]

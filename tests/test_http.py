@@ -398,3 +398,29 @@ def test_request_bodies_are_skipped_bounded_and_validated(mock_exporter):
         out = _raw_exchange(ex.port, b"GET /metrics HTTP/1.1\r\nContent-Length: " + bad + b"\r\n\r\n")
         assert out.startswith(b"HTTP/1.1 400"), (bad, out)
     assert _get(ex.port, "/metrics")[0] == 200
+
+
+def test_error_answer_survives_a_client_still_sending(mock_exporter):
+    """A 413 goes out while the client is still sending the refused body. Closing with unread
+    input would RST the connection and the client could lose the answer; the server half-closes
+    and drains instead (kLingerNs): the client's further sends succeed, and it reads the 413 and
+    then EOF (RFC 7230 6.6)."""
+    import time
+
+    ex = mock_exporter()
+    s = socket.create_connection(("127.0.0.1", ex.port), timeout=5)
+    s.sendall(b"POST /metrics HTTP/1.1\r\nContent-Length: 1000000000\r\n\r\n")
+    time.sleep(0.1)  # answered and half-closed by now
+    s.sendall(b"x" * 200_000)  # the body keeps coming
+    time.sleep(0.1)
+    s.sendall(b"x" * 1000)  # a RST by now would fail this send (EPIPE / ECONNRESET)
+    s.shutdown(socket.SHUT_WR)
+    out = b""
+    while True:
+        chunk = s.recv(65536)
+        if not chunk:
+            break
+        out += chunk
+    s.close()
+    assert out.startswith(b"HTTP/1.1 413 Payload Too Large"), out
+    assert b"Connection: close" in out
