@@ -663,7 +663,10 @@ bool Exporter::start(std::string* err) {
 }
 
 void Exporter::stop() {
-  if (!running_.exchange(false)) return;
+  // Also after a start() that failed part-way (e.g. the listen address): the backend and its
+  // device workers were already up, and must not outlive the exporter.
+  const bool was_running = running_.exchange(false);
+  if (!was_running && !server_ && workers_.empty() && !backend_up_) return;
   seq_cv_.notify_all();
   push_cv_.notify_all();
   if (sampler_.joinable()) sampler_.join();

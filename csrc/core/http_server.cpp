@@ -153,6 +153,15 @@ HttpServer::~HttpServer() { stop(); }
 
 bool HttpServer::start(std::string* err) {
   if (running_) return true;
+  auto abandon = [this](Loop* L) {  // a failed start: close what was opened, start no thread
+    if (L) close(L->lfd);
+    for (auto& P : loops_) {
+      close(P->lfd);
+      close(P->ep);
+      close(P->wake);
+    }
+    loops_.clear();
+  };
   sndbuf_ = kSndBuf;
   if (const char* e = getenv("GPUMON_HTTP_SNDBUF")) sndbuf_ = std::max(0, atoi(e));
   for (int t = 0; t < nthreads_; ++t) {
@@ -160,6 +169,7 @@ bool HttpServer::start(std::string* err) {
     L->lfd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
     if (L->lfd < 0) {
       *err = std::string("socket: ") + strerror(errno);
+      abandon(nullptr);
       return false;
     }
     int one = 1;
@@ -170,12 +180,12 @@ bool HttpServer::start(std::string* err) {
     sa.sin_port = htons(static_cast<uint16_t>(port_));
     if (inet_pton(AF_INET, addr_.empty() ? "0.0.0.0" : addr_.c_str(), &sa.sin_addr) != 1) {
       *err = "bad listen address " + addr_;
-      close(L->lfd);
+      abandon(L.get());
       return false;
     }
     if (bind(L->lfd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) {
       *err = "bind " + addr_ + ":" + std::to_string(port_) + ": " + strerror(errno);
-      close(L->lfd);
+      abandon(L.get());
       return false;
     }
     if (port_ == 0) {
@@ -185,7 +195,7 @@ bool HttpServer::start(std::string* err) {
     }
     if (listen(L->lfd, 1024) != 0) {
       *err = std::string("listen: ") + strerror(errno);
-      close(L->lfd);
+      abandon(L.get());
       return false;
     }
     set_nonblock(L->lfd);

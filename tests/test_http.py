@@ -362,11 +362,35 @@ def test_slow_reader_gets_whole_pipelined_bodies_and_a_vanishing_one_is_dropped(
     assert _get(ex.port, "/metrics")[0] == 200
 
 
-def test_bad_listen_address_is_reported(core):
-    ex = core.Exporter({"backend": "mock", "listen_addr": "not-an-address", "port": 0, "interval_s": 0})
+def test_bad_listen_address_is_reported_and_cleaned_up(core):
+    """A start() that fails at the listen address has already brought the backend and its device
+    workers up: stop() (and the destructor) must take them down, or the worker threads outlive
+    the exporter (a crash at interpreter exit)."""
+    import gc
+    import os
+    import time
+
+    def threads():
+        return len(os.listdir("/proc/self/task"))
+
+    base = threads()
+    ex = core.Exporter({"backend": "mock:gpus=4", "listen_addr": "not-an-address", "port": 0, "interval_s": 0,
+                        "http_threads": 2})
     with pytest.raises(RuntimeError, match="bad listen address not-an-address"):
         ex.start()
+    assert threads() >= base + 4  # one device worker per GPU is running
     ex.stop()
+    ex.stop()  # idempotent
+    assert threads() == base
+    ex = core.Exporter({"backend": "mock:gpus=4", "listen_addr": "not-an-address", "port": 0, "interval_s": 0})
+    with pytest.raises(RuntimeError):
+        ex.start()
+    del ex  # the destructor alone
+    gc.collect()
+    deadline = time.time() + 5
+    while threads() != base and time.time() < deadline:
+        time.sleep(0.01)
+    assert threads() == base
 
 
 def _raw_exchange(port, data):
