@@ -160,6 +160,7 @@ struct MockConfig {
   int hang_device = -1;               // ... on this hip_id only (-1: every device)
   int fail_device = -1;               // device whose sample() fails ...
   int fail_every = 0;                 // ... every N calls (0 = never); -1 = always
+  int procs_fail_every = 0;           // every device's processes() fails every N calls (0 = never)
   std::vector<std::string> unsupported;  // field names forced to NaN, e.g. "temp_edge"
   std::vector<MockProc> procs;
   int n_xcd = 8;
@@ -233,6 +234,7 @@ class MockBackend : public Backend {
   std::vector<char> link_fail_;
   std::vector<int64_t> frozen_tick_;
   std::vector<int> procs_fail_;      // per dev: process lists still to fail
+  std::vector<uint64_t> procs_calls_;  // per dev: processes() calls (procs_fail_every)
   std::vector<int> scan_fail_;       // per dev: occupancy scans still to fail  // per dev: firmware tick the fake SMU is stuck at (-1 = running)
   std::vector<uint64_t> calls_, prewarms_;
   std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;

@@ -483,6 +483,7 @@ static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
     else if (k == "n_links") base.n_links = atoi(v.c_str());
     else if (k == "fail_device") base.fail_device = atoi(v.c_str());
     else if (k == "fail_every") base.fail_every = atoi(v.c_str());
+    else if (k == "procs_fail_every") base.procs_fail_every = std::max(0, atoi(v.c_str()));
     else if (k == "hang_ms") base.hang_ms = atof(v.c_str());
     else if (k == "hang_device") base.hang_device = atoi(v.c_str());
     else if (k == "seed") base.seed = strtoull(v.c_str(), nullptr, 10);

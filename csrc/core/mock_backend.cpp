@@ -76,6 +76,7 @@ bool MockBackend::init(std::string* err) {
   frozen_tick_.assign(n, -1);
   scan_fail_.assign(n, 0);
   procs_fail_.assign(n, 0);
+  procs_calls_.assign(n, 0);
   calls_.assign(n, 0);
   prewarms_.assign(n, 0);
   energy_.assign(n, 1000000);
@@ -339,6 +340,8 @@ bool MockBackend::processes(int i, std::vector<ProcSample>* out) {
     --procs_fail_[i];
     return false;
   }
+  if (cfg_.procs_fail_every > 0 && ++procs_calls_[i] % static_cast<uint64_t>(cfg_.procs_fail_every) == 0)
+    return false;
   double util = has(forced_util_[i]) ? forced_util_[i]
                                      : mock_util(cfg_, devs_[i].hip_id, (mono_ns() - t0_ns_) * 1e-9);
   for (const auto& p : cfg_.procs) {

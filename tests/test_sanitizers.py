@@ -223,3 +223,92 @@ def test_sanitized_sharing_subsamples_and_link_map(target, binary, env, tmp_path
            or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
     assert not bad, err[-4000:]
     assert rc == 0, err[-2000:]
+
+
+class _GarbageH2:
+    """A unix-socket 'kubelet' that answers every connection with a seeded random mix of valid
+    and mangled HTTP/2 frames (the frame kinds grpc_lite.cpp handles, with bad lengths, padding and
+    flags), then hangs up: the native gRPC client's parser under the sanitizers."""
+
+    def __init__(self, path, seed=11):
+        import random
+        import struct
+
+        self.path, self.rng, self.struct, self.n = path, random.Random(seed), struct, 0
+        if os.path.exists(path):
+            os.unlink(path)
+        self.srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        self.srv.bind(path)
+        self.srv.listen(8)
+        self.srv.settimeout(0.2)
+        self.stop = threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+        self.t.start()
+
+    def _frame(self):
+        r, st = self.rng, self.struct
+        typ = r.choice([0, 1, 3, 4, 6, 7, 8, 9, 0x42])
+        flags = r.choice([0, 1, 4, 5, 8, 0x20, 0x2d, 0xff])
+        payload = bytes(r.randrange(256) for _ in range(r.choice([0, 1, 2, 5, 9, 40])))
+        if typ in (0, 1) and r.random() < 0.5:  # a well-formed gRPC message / header block
+            payload = b"\x00" + st.pack(">I", 3) + b"\x0a\x01a" if typ == 0 else b"\x00\x07:status\x03200"
+        n = len(payload) if r.random() < 0.8 else r.randrange(1 << 24)
+        return st.pack(">I", n)[1:] + bytes([typ, flags]) + st.pack(">I", r.choice([0, 1, 3])) + payload
+
+    def _run(self):
+        while not self.stop.is_set():
+            try:
+                conn, _ = self.srv.accept()
+            except OSError:
+                continue
+            self.n += 1
+            try:
+                conn.settimeout(0.5)
+                conn.recv(4096)
+                conn.sendall(b"".join(self._frame() for _ in range(self.rng.randint(1, 8))))
+            except OSError:
+                pass
+            finally:
+                conn.close()
+
+    def close(self):
+        self.stop.set()
+        self.t.join(5)
+        self.srv.close()
+        os.unlink(self.path)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_failure_paths(target, binary, env):
+    """Round-4 failure paths: a start that fails at the listen address (backend and device workers
+    already up: the leak checker sees whatever is not taken down), process lists that fail every
+    3rd call (the held list crossing threads), and a PodResources / CRI peer that answers mangled
+    HTTP/2 -- with scrapes running, no sanitizer report."""
+    from conftest import make_locked
+
+    make_locked(target, jobs=8)
+    exe = os.path.join(ROOT, binary)
+    r = subprocess.run([exe, "--backend", "mock:gpus=4", "--sample-threads", "2", "--listen", "not-an-address:1",
+                        "--log-level", "error"], capture_output=True, text=True, timeout=60, env=dict(os.environ, **env))
+    bad = [l for l in r.stderr.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
+           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    assert not bad, r.stderr[-4000:]
+    assert r.returncode not in (0, -6, -11, 134, 139), r.stderr[-2000:]
+    sock = f"/tmp/gpumon-h2-san-{target}-{os.getpid()}.sock"
+    peer = _GarbageH2(sock)
+    try:
+        rc, err = _run(exe, dict(env, GPUMON_METADATA_REFRESH="0.3"),
+                       ("--backend", "mock:gpus=4,procs=3,procs_fail_every=3", "--interval", "0.05",
+                        "--pod-resources", sock, "--cri", sock), min_s=3.0)
+    finally:
+        peer.close()
+    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
+           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    assert not bad, err[-4000:]
+    assert rc == 0, err[-2000:]
+    assert peer.n >= 4, peer.n
