@@ -151,8 +151,10 @@ bool HttpClient::connect_to(const Url& u, std::string* err) {
   return true;
 }
 
-// Largest Content-Length accepted: the client sizes its buffer from it before reading.
+// Largest Content-Length accepted: the client sizes its buffer from it before reading. A body
+// without a length (read to EOF) is held to the same bound, and the header to kMaxHeaderBytes.
 constexpr long kMaxBodyBytes = 256L << 20;
+constexpr size_t kMaxHeaderBytes = 64u << 10;
 
 static bool send_all(int fd, const char* p, size_t n) {
   while (n) {
@@ -187,11 +189,27 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
     std::string in;
     char buf[16384];
     size_t hdr_end = std::string::npos;
+    // SO_RCVTIMEO bounds each recv(); this bounds the whole response, so a server that drips a
+    // byte at a time cannot hold the caller (the Influx pusher, which stop() joins) indefinitely.
+    const int64_t deadline =
+        timeout_s_ > 0 ? mono_ns() + static_cast<int64_t>(2 * timeout_s_ * 1e9) : INT64_MAX;
+    auto expired = [&] {
+      if (mono_ns() <= deadline) return false;
+      close_conn();
+      *err = "response timed out";
+      return true;
+    };
     while (hdr_end == std::string::npos) {
       ssize_t r = recv(fd_, buf, sizeof buf, 0);
       if (r <= 0) break;
       in.append(buf, static_cast<size_t>(r));
       hdr_end = in.find("\r\n\r\n");
+      if (hdr_end == std::string::npos && in.size() > kMaxHeaderBytes) {
+        close_conn();
+        *err = "response header too large";
+        return -1;
+      }
+      if (hdr_end == std::string::npos && expired()) return -1;
     }
     if (hdr_end == std::string::npos) {
       close_conn();
@@ -232,6 +250,7 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
           return -1;
         }
         got += static_cast<size_t>(r);
+        if (got < static_cast<size_t>(clen) && expired()) return -1;
       }
     } else if (status != 204 && status != 304) {
       // no length: read to EOF
@@ -239,6 +258,12 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
         ssize_t r = recv(fd_, buf, sizeof buf, 0);
         if (r <= 0) break;
         rb.append(buf, static_cast<size_t>(r));
+        if (rb.size() > static_cast<size_t>(kMaxBodyBytes)) {
+          close_conn();
+          *err = "response body too large";
+          return -1;
+        }
+        if (expired()) return -1;
       }
       close_after = true;
     }

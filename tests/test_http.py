@@ -227,6 +227,52 @@ def test_client_refuses_huge_content_length_and_reads_bodies_whole(core):
     srv.close()
 
 
+@pytest.mark.parametrize("script,error", [
+    # a server that drips its header a byte at a time: each recv() returns before SO_RCVTIMEO
+    ([b"H"] + [b"x"] * 400, "response timed out"),
+    ([b"HTTP/1.1 200 OK\r\nX: " + b"a" * (70 << 10)], "response header too large"),
+    # no Content-Length: read to EOF, but the drip never ends
+    ([b"HTTP/1.1 200 OK\r\n\r\n"] + [b"y"] * 400, "response timed out"),
+    ([b"HTTP/1.1 200 OK\r\nContent-Length: 1000\r\n\r\n"] + [b"z"] * 400, "response timed out"),
+])
+def test_client_bounds_a_dripping_or_endless_response(core, script, error):
+    """The native client (Influx push, csrc/core/http_client.cpp) bounds the whole response by
+    twice its timeout and the header by 64 KiB, not just each recv()."""
+    import time
+
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    port = srv.getsockname()[1]
+    stop = threading.Event()
+
+    def serve():
+        c, _ = srv.accept()
+        try:
+            c.recv(65536)
+            for part in script:
+                if stop.is_set():
+                    break
+                c.sendall(part)
+                if len(part) < 100:
+                    time.sleep(0.01)
+        except OSError:
+            pass
+        finally:
+            c.close()
+
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    t0 = time.monotonic()
+    st, body, err = core.http_request("GET", f"http://127.0.0.1:{port}/", "", "", 0.5)
+    dt = time.monotonic() - t0
+    stop.set()
+    t.join(5)
+    srv.close()
+    assert st == -1 and err == error, (st, err)
+    assert dt < 2.5, dt
+
+
 def test_per_request_family_filter(mock_exporter):
     """/metrics?include=&exclude= (shell globs, comma-separated, repeatable, percent-decoded): the
     same families the config filter would keep, cut from the current snapshot, gzip included; other
