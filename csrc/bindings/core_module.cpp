@@ -537,6 +537,28 @@ PYBIND11_MODULE(_core, m) {
       },
       py::arg("socket"), py::arg("timeout_ms") = 3000, "Docker Engine GET /containers/json via docker_lite.cpp");
   m.def(
+      "parse_cri_containers",
+      [](py::bytes msg) {
+        std::vector<CriContainer> cs;
+        if (!parse_cri_containers(std::string(msg), &cs)) throw std::runtime_error("malformed ListContainersResponse");
+        py::list out;
+        for (const auto& c : cs)
+          out.append(py::make_tuple(c.id, c.sandbox_id, c.name, c.labels, c.annotations));
+        return out;
+      },
+      "runtime.v1 ListContainersResponse -> [(id, sandbox_id, name, labels, annotations)] (grpc_lite.cpp)");
+  m.def(
+      "parse_cri_sandboxes",
+      [](py::bytes msg) {
+        std::vector<CriSandbox> ss;
+        if (!parse_cri_sandboxes(std::string(msg), &ss)) throw std::runtime_error("malformed ListPodSandboxResponse");
+        py::list out;
+        for (const auto& s : ss)
+          out.append(py::make_tuple(s.id, s.name, s.uid, s.pod_namespace, s.labels, s.annotations));
+        return out;
+      },
+      "runtime.v1 ListPodSandboxResponse -> [(id, name, uid, namespace, labels, annotations)] (grpc_lite.cpp)");
+  m.def(
       "cri_list",
       [](const std::string& sock, int timeout_ms) {
         std::vector<CriContainer> cs;

@@ -193,3 +193,58 @@ def test_gpumon_monitor_native_mode(tmp_path):
             mon.ex.tick()
             idle = [r for r in mon.ex.pod_rows() if r["idle"]]
             assert [(r["podname"], r["dev"], r["containerid"]) for r in idle] == [("jupyter-q-0", 1, CID_B[:12])]
+
+
+_txt = st.text(alphabet=st.characters(blacklist_categories=("Cs",)), max_size=12)
+_labels = st.dictionaries(_txt, _txt, max_size=4)
+
+
+@settings(max_examples=150, deadline=None)
+@given(cs=st.lists(st.tuples(_txt, _txt, _txt, _labels, _labels, st.integers(0, 3), st.integers(0, 2 ** 62)),
+                   max_size=5),
+       unknown=st.booleans())
+def test_cri_container_parser_matches_protobuf(cs, unknown):
+    """The hand-written CRI decoder (grpc_lite.cpp parse_cri_containers) against python-protobuf's
+    encoding of the same ListContainersResponse: every field the exporter reads, fields it skips
+    (image, state, created_at), and an unknown top-level field (a newer runtime's)."""
+    from gpumon import core as _core
+    from oracles.attribution import proto as P
+
+    r = P.ListContainersResponse()
+    for cid, sb, name, labels, ann, state, created in cs:
+        c = r.containers.add(id=cid, pod_sandbox_id=sb, image_ref="sha256:x", state=state, created_at=created)
+        c.metadata.name = name
+        c.metadata.attempt = 2
+        c.image.image = "rocm/pytorch"
+        c.labels.update(labels)
+        c.annotations.update(ann)
+    raw = r.SerializeToString() + (b"\x78\x01\x82\x01\x02hi" if unknown else b"")
+    got = _core().parse_cri_containers(raw)
+    assert got == [(cid, sb, name, labels, ann) for cid, sb, name, labels, ann, _, _ in cs]
+
+
+@settings(max_examples=150, deadline=None)
+@given(ss=st.lists(st.tuples(_txt, _txt, _txt, _txt, _labels, _labels), max_size=5))
+def test_cri_sandbox_parser_matches_protobuf(ss):
+    from gpumon import core as _core
+    from oracles.attribution import proto as P
+
+    r = P.ListPodSandboxResponse()
+    for sid, name, uid, ns, labels, ann in ss:
+        i = r.items.add(id=sid, state=0, created_at=5, runtime_handler="runc")
+        i.metadata.name, i.metadata.uid, i.metadata.namespace, i.metadata.attempt = name, uid, ns, 1
+        i.labels.update(labels)
+        i.annotations.update(ann)
+    assert _core().parse_cri_sandboxes(r.SerializeToString()) == [tuple(x) for x in ss]
+
+
+@settings(max_examples=300, deadline=None)
+@given(data=st.binary(max_size=256))
+def test_cri_parsers_never_crash_on_garbage(data):
+    from gpumon import core as _core
+
+    for fn in (_core().parse_cri_containers, _core().parse_cri_sandboxes):
+        try:
+            assert isinstance(fn(data), list)
+        except RuntimeError:
+            pass
