@@ -1,11 +1,12 @@
 #include "render.h"
 
-
 #include <charconv>
 #include <cmath>
 #include <cstring>
+#include <initializer_list>
 #include <map>
 #include <set>
+#include <string_view>
 #include <tuple>
 
 namespace gpumon {
@@ -33,7 +34,7 @@ void append_double(double v, std::string* out) {
   out->append(buf, r.ptr);
 }
 
-void escape_label_value(const std::string& v, std::string* out) {
+void escape_label_value(std::string_view v, std::string* out) {
   // fast path: most values (ids, BDFs, sensor names, pod names) need no escaping
   bool plain = true;
   for (char c : v)
@@ -209,13 +210,26 @@ class Family {
   ~Family() {
     if (on_ && !any_) o_->resize(mark_);
   }
-  // base: preformatted `k="v",...` (may be empty); extra: additional label pairs.
+  // base: preformatted `k="v",...` (may be empty); extra: additional label pairs. A braced list
+  // at the call site binds the initializer_list overload: no vector on the heap per sample (the
+  // per-XCD and per-link families are most of an 8-GPU exposition's lines).
   void add(const std::string& base, const Labels& extra, double v, const char* suffix = nullptr) {
+    add_impl(base, extra, v, suffix);
+  }
+  void add(const std::string& base, std::initializer_list<std::pair<const char*, std::string_view>> extra,
+           double v, const char* suffix = nullptr) {
+    add_impl(base, extra, v, suffix);
+  }
+  void add(const std::string& base, double v) { add_impl(base, Labels{}, v, nullptr); }
+
+ private:
+  template <class L>
+  void add_impl(const std::string& base, const L& extra, double v, const char* suffix) {
     if (!on_ || std::isnan(v)) return;
     any_ = true;
     o_->append(name_);
     if (suffix) o_->append(suffix);
-    if (!base.empty() || !extra.empty()) {
+    if (!base.empty() || extra.size() != 0) {
       o_->push_back('{');
       o_->append(base);
       bool first = base.empty();
@@ -232,9 +246,7 @@ class Family {
     append_double(v, o_);
     o_->push_back('\n');
   }
-  void add(const std::string& base, double v) { add(base, Labels{}, v); }
 
- private:
   std::string* o_;
   const char* name_;
   size_t mark_;

@@ -143,7 +143,7 @@ void render_prometheus(const RenderInput& in, std::string* out);
 void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::string* out, int schema = 2019);
 
 // Escapers (exposed for tests).
-void escape_label_value(const std::string& v, std::string* out);
+void escape_label_value(std::string_view v, std::string* out);
 void escape_influx_tag(const std::string& v, std::string* out);
 void escape_influx_field_str(const std::string& v, std::string* out);
 void append_double(double v, std::string* out);
