@@ -949,6 +949,7 @@ PYBIND11_MODULE(_core, m) {
              d["in_container"] = id.in_container;
              d["opted_in"] = id.opted_in;
              d["comm"] = id.comm;
+             d["starttime"] = id.starttime;
              d["runtime"] = id.runtime;
              d["container_id"] = id.container_id;
              d["container_name"] = id.container_name;

@@ -209,13 +209,15 @@ bool Attributor::read_stat(uint32_t pid, uint64_t* starttime, std::string* comm)
   size_t lp = s.find('('), rp = s.rfind(')');
   if (lp == std::string::npos || rp == std::string::npos || rp < lp) return false;
   *comm = s.substr(lp + 1, rp - lp - 1);
-  // fields after ") ": state(3) ppid(4) ... starttime is field 22 -> index 19 after state
-  std::vector<std::string> f = split(std::string_view(s).substr(rp + 2), ' ');
-  if (f.size() < 20) {
-    *starttime = 0;
-    return true;
+  // fields after ") ": state(3) ppid(4) ... starttime is field 22 -> index 19 after state. Walked
+  // in place (every process, every tick): no vector of 50 field strings.
+  size_t p = rp + 2;
+  for (int k = 0; k < 19 && p < s.size(); ++k) {
+    p = s.find(' ', p);
+    if (p == std::string::npos) break;
+    ++p;
   }
-  *starttime = strtoull(f[19].c_str(), nullptr, 10);
+  *starttime = p != std::string::npos && p < s.size() ? strtoull(s.c_str() + p, nullptr, 10) : 0;
   return true;
 }
 

@@ -239,3 +239,22 @@ def test_kfd_handle_check_rejects_foreign_pid(core, tmp_path):
     r300, r301 = ex.resolve_pid(300), ex.resolve_pid(301)
     assert r300["pid_mismatch"] and not r300["valid"] and r300["container_id"] == ""
     assert r301["valid"] and not r301["pid_mismatch"] and r301["container_id"] == CID
+
+
+@pytest.mark.parametrize("comm,tail,start", [
+    ("python3", "S 1 1 1 0 -1 4194560 100 0 0 0 5 3 0 0 20 0 8 0 424242 1000 100", 424242),
+    ("a) b (c", "S 1 1 1 0 -1 4194560 100 0 0 0 5 3 0 0 20 0 8 0 777 1000 100", 777),  # parens in comm
+    ("x y", "S 1 1 1 0 -1 4194560 100 0 0 0 5 3 0 0 20 0 8 0 31337", 31337),  # starttime is the last field
+    ("short", "S 1 1 1", 0),  # truncated stat: no starttime
+])
+def test_stat_starttime_and_comm(mock_exporter, tmp_path, comm, tail, start):
+    """/proc/<pid>/stat: comm is the text between the first '(' and the LAST ')', starttime is the
+    22nd field (the pid-reuse key of the attribution cache)."""
+    d = tmp_path / "55"
+    d.mkdir()
+    (d / "stat").write_text(f"55 ({comm}) {tail}\n")
+    (d / "cgroup").write_text("0::/\n")
+    ex = mock_exporter(procfs_root=str(tmp_path))
+    r = ex.resolve_pid(55)
+    assert r["comm"] == comm or not r["valid"]
+    assert r["starttime"] == start
