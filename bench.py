@@ -136,6 +136,24 @@ def _per_gpu_xgmi(tick_rates, rows, expected_tx, expected_rx):
     return out
 
 
+def _bounded(fn, timeout_s, *args):
+    """Run a post-measurement extra (link map, capacity) on a daemon thread and give up after
+    timeout_s: the JSON line is the measurement, and a stuck validation call must not keep it from
+    being printed."""
+    out = {}
+
+    def run():
+        try:
+            out["r"] = fn(*args)
+        except Exception as e:  # noqa: BLE001
+            out["r"] = {"error": f"{type(e).__name__}: {e}"}
+
+    t = threading.Thread(target=run, daemon=True, name=f"bench-{fn.__name__}")
+    t.start()
+    t.join(timeout_s)
+    return out.get("r", {"error": f"timed out after {timeout_s:g} s"})
+
+
 def _link_map_check(ord_bdfs, seconds):
     """HIP ordinal 0 pushes into every peer in turn while a fresh 10 Hz exporter watches: the link
     whose write counter moves must be the one the exporter attributes to that peer's BDF."""
@@ -710,17 +728,13 @@ def main() -> int:
         }
         mon.stop()
         if has_gpu and n > 1 and args.link_check_s > 0:
-            # validation evidence, never a reason to lose the measured line
-            try:
-                lm = _link_map_check(ord_bdfs, args.link_check_s)
-            except Exception as e:  # noqa: BLE001
-                lm = {"error": f"{type(e).__name__}: {e}"}
+            # validation evidence, never a reason to lose the measured line: errors and a stuck
+            # peer copy are recorded, not raised (each pair runs link_check_s plus the exporter's
+            # start-up; the bound leaves several times that)
+            lm = _bounded(_link_map_check, 30 + (n - 1) * (4 * args.link_check_s + 5), ord_bdfs, args.link_check_s)
             result["xgmi"] = dict(result["xgmi"] or {}, link_map=lm)
         if args.capacity_s > 0:
-            try:
-                result["capacity"] = _capacity(backend, sampled, args, has_gpu)
-            except Exception as e:  # noqa: BLE001
-                result["capacity"] = {"error": f"{type(e).__name__}: {e}"}
+            result["capacity"] = _bounded(_capacity, 60 + 4 * args.capacity_s, backend, sampled, args, has_gpu)
     if result is not None:  # the line is out before the teardown collectives can stall on a peer
         line = json.dumps(result)
         print(line, flush=True)

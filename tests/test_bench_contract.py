@@ -144,3 +144,19 @@ def test_bench_eight_ranks_exact_scale_command():
     # reductions can run past its tick, so the whole-node rate is N / interval within 15 % here
     # (exact on the GPU node, where RCCL moves the bytes)
     assert d["value"] == pytest.approx(8.0, rel=0.15)
+
+
+def test_post_measurement_extras_are_time_bounded():
+    """The link map and the capacity run happen after the timed region and before the line is
+    printed: a stuck one is given up on (and an error recorded) instead of holding the line back."""
+    import importlib.util
+    import time
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    t0 = time.monotonic()
+    r = bench._bounded(time.sleep, 0.3, 30)
+    assert r == {"error": "timed out after 0.3 s"} and time.monotonic() - t0 < 2
+    assert bench._bounded(lambda: 1 / 0, 5) == {"error": "ZeroDivisionError: division by zero"}
+    assert bench._bounded(lambda x: {"ok": x}, 5, 7) == {"ok": 7}
