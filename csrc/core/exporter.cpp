@@ -575,12 +575,15 @@ bool Exporter::ensure_backend() {
     }
   }
   if (!ok) {
-    if (err != backend_err_)
-      GPUMON_LOG(LogLevel::kError, "exporter", "backend init failed: " + err);
+    if (err != backend_error()) GPUMON_LOG(LogLevel::kError, "exporter", "backend init failed: " + err);
+    std::lock_guard<std::mutex> g(err_mu_);
     backend_err_ = err;
     return false;
   }
-  backend_err_.clear();
+  {
+    std::lock_guard<std::mutex> g(err_mu_);
+    backend_err_.clear();
+  }
   std::vector<DeviceStatic> st;
   for (int i = 0; i < backend_->device_count(); ++i) st.push_back(backend_->static_info(i));
   {
@@ -611,10 +614,10 @@ bool Exporter::start(std::string* err) {
   }
   if (!ensure_backend() && cfg_.backend != "auto" && !starts_with(cfg_.backend, "mock")) {
     // explicit amdsmi: keep running (retry with backoff) but report the error to the caller
-    if (err) *err = backend_err_;
+    if (err) *err = backend_error();
   }
   if (!backend_up_ && starts_with(cfg_.backend, "mock")) {
-    if (err) *err = backend_err_;
+    if (err) *err = backend_error();
     return false;
   }
   if (cfg_.serve_http) {
@@ -1570,7 +1573,7 @@ void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
   if (req.path == "/readyz") {
     bool ok = ready() && backend_up_;
     resp->status = ok ? 200 : 503;
-    resp->inline_body = ok ? "ready\n" : ("not ready: " + backend_err_ + "\n");
+    resp->inline_body = ok ? "ready\n" : ("not ready: " + backend_error() + "\n");
     return;
   }
   if (req.path == "/" || req.path.empty()) {

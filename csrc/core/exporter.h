@@ -254,7 +254,12 @@ class Exporter {
   int64_t next_init_ns_ = 0;
   int all_failed_ticks_ = 0;
   std::atomic<uint64_t> reinits_{0};
-  std::string backend_err_;
+  std::string backend_err_;  // written by the sampler's re-init attempts, read by /readyz: err_mu_
+  mutable std::mutex err_mu_;
+  std::string backend_error() const {
+    std::lock_guard<std::mutex> g(err_mu_);
+    return backend_err_;
+  }
   std::thread sampler_;
   std::atomic<uint64_t> seq_{0};
   std::mutex seq_mu_;

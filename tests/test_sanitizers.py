@@ -9,6 +9,7 @@ import socket
 import subprocess
 import threading
 import time
+import urllib.error
 import urllib.request
 
 import pytest
@@ -312,3 +313,48 @@ def test_sanitized_failure_paths(target, binary, env):
     assert not bad, err[-4000:]
     assert rc == 0, err[-2000:]
     assert peer.n >= 4, peer.n
+
+
+@pytest.mark.slow
+def test_tsan_readyz_while_the_backend_keeps_failing_to_initialise():
+    """/readyz reports the backend's init error while the sampler re-tries the init every tick:
+    the error string is shared between the two threads (err_mu_), which TSan checks here."""
+    from conftest import make_locked
+
+    make_locked("tsan", jobs=8)
+    port = _free_port()
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1",
+               GPUMON_AMDSMI_LIB="/nonexistent/libamd_smi.so", GPUMON_INIT_RETRY_S="0.002")
+    p = subprocess.Popen([os.path.join(ROOT, "bin/gpumon-exporter-tsan"), "--backend", "amdsmi", "--interval", "0.005",
+                          "--listen", f"127.0.0.1:{port}", "--http-threads", "2", "--log-level", "error"],
+                         stderr=subprocess.PIPE, stdout=subprocess.DEVNULL, env=env, text=True)
+    codes = []
+    try:
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            try:
+                urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=1).read()
+                break
+            except OSError:
+                time.sleep(0.1)
+
+        def hammer():
+            for _ in range(150):
+                try:
+                    urllib.request.urlopen(f"http://127.0.0.1:{port}/readyz", timeout=5)
+                    codes.append(200)
+                except urllib.error.HTTPError as e:
+                    codes.append(e.code)
+                    body = e.read().decode()
+                    assert body.startswith("not ready: "), body
+
+        ts = [threading.Thread(target=hammer) for _ in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=60)
+    assert "WARNING: ThreadSanitizer" not in err, err[-4000:]
+    assert codes and set(codes) == {503}, set(codes)
