@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--scrape-rate", type=float, default=50.0)
     ap.add_argument("--backend", default="amdsmi")
     ap.add_argument("--window", type=float, default=30.0)
+    ap.add_argument("--no-keepalive", action="store_true",
+                    help="one connection per scrape (Connection: close): the server's lingering-close path")
     a = ap.parse_args()
 
     from gpumon import core as _core
@@ -55,7 +57,8 @@ def main():
 
         def scrape():
             res.update(core.scrape_load("127.0.0.1", mon.port, "/metrics", n_requests=0, duration_s=a.window,
-                                        concurrency=2, rate_hz=a.scrape_rate, keep_alive=True, gzip=True))
+                                        concurrency=2, rate_hz=a.scrape_rate, keep_alive=not a.no_keepalive,
+                                        gzip=True))
 
         th = threading.Thread(target=scrape)
         th.start()
@@ -76,7 +79,7 @@ def main():
     else:
         lst = {}
     first, last = windows[0], windows[-1]
-    summary = {"minutes": a.minutes, "interval_s": a.interval, "windows": len(windows),
+    summary = {"minutes": a.minutes, "interval_s": a.interval, "keep_alive": not a.no_keepalive, "windows": len(windows),
                "rss_mb_start": first["rss_mb"], "rss_mb_end": last["rss_mb"],
                "rss_mb_growth_after_first_window": round(last["rss_mb"] - first["rss_mb"], 1),
                "fds_start": first["fds"], "fds_end": last["fds"], "threads_end": last["threads"],
