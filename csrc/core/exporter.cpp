@@ -960,6 +960,8 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
   std::vector<std::tuple<std::string, std::string, std::string, int>> active;
   for (size_t d = 0; d < procs.size(); ++d) {
     double dev_util = d < samples.size() ? samples[d].v[F_GFX_UTIL] : kNaN;
+    // a held process list (the last good one, this tick's failed) carries no new engine time
+    const bool held = d < samples.size() && samples[d].procs_held;
     // One row per (pid, device): duplicate entries (several KFD contexts of one process) are merged,
     // a duplicate series would make Prometheus reject the whole scrape.
     std::unordered_map<uint32_t, size_t> row_of_pid;
@@ -988,10 +990,19 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       if (p.has_gfx_ns) {
         ProcKey k{p.pid, static_cast<int>(d)};
         auto it = proc_prev_.find(k);
-        if (it != proc_prev_.end() && it->second.starttime == id.starttime &&
-            p.gfx_ns >= it->second.gfx_ns && now > it->second.t_ns)
-          util = std::min(100.0, (p.gfx_ns - it->second.gfx_ns) * 100.0 / (now - it->second.t_ns));
-        next_prev[k] = ProcPrev{p.gfx_ns, now, id.starttime};
+        if (held) {
+          // the held list repeats the last reading: keep its baseline (the next good list's delta
+          // then spans the whole gap) and its busy share, rather than a 0 % now and a spike later
+          if (it != proc_prev_.end()) {
+            next_prev[k] = it->second;
+            util = it->second.util;
+          }
+        } else {
+          if (it != proc_prev_.end() && it->second.starttime == id.starttime &&
+              p.gfx_ns >= it->second.gfx_ns && now > it->second.t_ns)
+            util = std::min(100.0, (p.gfx_ns - it->second.gfx_ns) * 100.0 / (now - it->second.t_ns));
+          next_prev[k] = ProcPrev{p.gfx_ns, now, id.starttime, util};
+        }
       }
       // HIP compute runs on KFD user queues, which DRM fdinfo engine time never sees: there the
       // process's busy % is the share of the interval's cu_occupancy reads that found its waves

@@ -246,6 +246,7 @@ class Exporter {
     uint64_t gfx_ns = 0;
     int64_t t_ns = 0;
     uint64_t starttime = 0;
+    double util = kNaN;  // the busy % computed at t_ns (repeated while a failed list is held)
   };
   std::unordered_map<ProcKey, ProcPrev, ProcKeyHash> proc_prev_;
 

@@ -310,3 +310,24 @@ def test_failed_process_list_holds_the_last_good_one_for_three_ticks(mock_export
     assert [state() for _ in range(5)] == [(["4242"], 1, 3), (["4242"], 1, 4), (["4242"], 1, 5),
                                            ([], 0, 6), (["4242"], 0, 6)]
     assert ex.self_stats()["process_list_failures"] == 6
+
+
+def test_held_process_list_keeps_engine_time_baselines(mock_exporter):
+    """A process busy from DRM engine time (gfx ns deltas): while its GPU's list is held the row
+    repeats the last busy %, and the first good list after the gap averages over the whole gap --
+    not 0 % during the hold and a clamped 100 % spike after it."""
+    ex = mock_exporter(backend="mock:gpus=1,mode=load", sample_threads=0,
+                       mock={"procs": [{"pid": 11, "device": 0, "gfx_share": 0.5}]})
+
+    def util():
+        time.sleep(0.05)
+        ex.tick()
+        return next(r["proc_gfx_util"] for r in ex.pod_rows() if r["pid"] == "11")
+
+    util()
+    before = util()
+    assert 20 < before < 90, before
+    ex.mock_fail_procs(0, 2)
+    assert util() == before and util() == before  # held: the last reading
+    after = util()  # spans the two held intervals and this one
+    assert abs(after - before) < 25, (before, after)
