@@ -358,7 +358,8 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
           }
       }
     }
-    if (occ_on && procs && ok_for_ras) {  // a failed tick listed nothing: keep sub-sampling the known pids
+    // a failed tick (or a failed process list) listed nothing: keep sub-sampling the known pids
+    if (occ_on && procs && ok_for_ras && s.procs_read >= 0) {
       occ_pids.clear();
       for (const auto& ps : p)
         if (std::find(occ_pids.begin(), occ_pids.end(), ps.pid) == occ_pids.end()) occ_pids.push_back(ps.pid);

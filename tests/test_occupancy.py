@@ -331,3 +331,20 @@ def test_held_process_list_keeps_engine_time_baselines(mock_exporter):
     assert util() == before and util() == before  # held: the last reading
     after = util()  # spans the two held intervals and this one
     assert abs(after - before) < 25, (before, after)
+
+
+def test_failed_process_list_keeps_the_subsampled_pids(mock_exporter):
+    """The device worker re-reads the known pids between ticks; a tick whose process list failed
+    lists nothing, and must not empty that set (with the KFD listings failing too, the next
+    interval would then have no sub-samples at all)."""
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", interval_s=0.2, occ_samples=10, sample_threads=-1,
+                       mock={"procs": [{"pid": 4242, "device": 0, "name": "train", "kfd_only": True}]})
+    ex.mock_set_occ_series(0, [100.0])
+    ex.mock_fail_scans(0, 10 ** 6)  # only the known-pid re-reads remain
+    _wait_ticks(ex, 2)
+    ex.mock_fail_procs(0, 1)
+    _wait_ticks(ex, 1)  # the failed list (held)
+    assert promtext.one(promtext.parse(ex.metrics_text()), "gpu_process_list_held", gpu_id="0") == 1
+    _wait_ticks(ex, 1)  # the interval after it
+    rows = [r for r in ex.pod_rows() if r["pid"] == "4242"]
+    assert rows and rows[0]["occ_samples"] >= 4, rows
