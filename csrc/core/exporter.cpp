@@ -591,6 +591,7 @@ bool Exporter::ensure_backend() {
     std::lock_guard<std::mutex> g(state_mu_);
     statics_ = st;
     prev_.assign(st.size(), DeviceSample{});
+    last_ok_.clear();  // a re-initialised backend may number its devices differently
     xgmi_maps_.assign(st.size(), XgmiSlotMap{});
     cur_.assign(st.size(), DeviceSample{});
     rates_.assign(st.size(), DeviceRates{});
@@ -1109,6 +1110,15 @@ TickInfo Exporter::tick() {
       prev = cur_;  // the previous tick's samples
       prev_rates = rates_;
     }
+    // A device whose previous tick failed is compared with its last good sample instead (if it is
+    // recent): its interval rates then span the gap -- the accumulators make that exact -- rather
+    // than going missing for the tick after every transient failure, and link identity and RAS
+    // carry over the failed tick.
+    if (static_cast<int>(last_ok_.size()) != n) last_ok_.assign(n, DeviceSample{});
+    const int64_t gap_ns = static_cast<int64_t>(std::max(5.0 * cfg_.interval_s, 5.0) * 1e9);
+    for (int i = 0; i < n && i < static_cast<int>(prev.size()); ++i)
+      if (!prev[i].ok && last_ok_[i].ok && cur[i].host_mono_ns - last_ok_[i].host_mono_ns <= gap_ns)
+        prev[i] = last_ok_[i];
     for (int i = 0; i < n; ++i) {
       DeviceSample& s = cur[i];
       // A link refresh counts only if the device answered AND the link-metrics read succeeded: a
@@ -1187,7 +1197,10 @@ TickInfo Exporter::tick() {
         if (i < static_cast<int>(dev_errors_.size()))
           dev_errors_[i] += s.ok ? s.errors : std::max<uint32_t>(1, s.errors);
       }
-      if (s.ok) info.devices_ok++;
+      if (s.ok) {
+        info.devices_ok++;
+        last_ok_[i] = s;
+      }
       // A failed process list (a transient library or KFD error) keeps the last good list for up
       // to kProcHoldTicks ticks instead of publishing "no processes": every pod row of the GPU and
       // its sharing state would otherwise drop out for that tick. A device that never listed

@@ -272,6 +272,7 @@ class Exporter {
   std::vector<int> proc_hold_;                       // per device: ticks held so far (-1: none good yet)
   std::atomic<uint64_t> frozen_{0};      // samples whose repeated table was older than stale_hold_s
   std::vector<int64_t> last_fresh_ns_;   // per device: host time the firmware table last advanced (tick_mu_)
+  std::vector<DeviceSample> last_ok_;    // per device: the last sample that succeeded (tick_mu_)
   size_t last_body_bytes_ = 0;  // tick thread only: sizes the next render buffer
   std::atomic<uint64_t> phase_ns_[5] = {};  // sample, procs, attrib, render, gzip (cumulative)
 

@@ -73,6 +73,24 @@ def test_intermittent_failure_recovers(mock_exporter):
     assert oks.count(True) == 3 and oks.count(False) == 3
 
 
+def test_rates_after_a_failed_tick_span_the_gap(mock_exporter):
+    """The tick after a transient device failure computes its interval rates against the last good
+    sample (the accumulators make the longer window exact) instead of exporting none."""
+    ex = mock_exporter(backend="mock:gpus=2,mode=load,fail_device=1,fail_every=4", sample_threads=0)
+    seen = []
+    for _ in range(8):
+        time.sleep(0.03)  # past the mock SMU's 20 ms table refresh
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())
+        up = promtext.one(fam, "gpu_up", gpu_id="1")
+        power = promtext.values(fam, "gpu_power_interval_watts", gpu_id="1")
+        seen.append((up, bool(power)))
+        if up and power:
+            assert power[0] == pytest.approx(promtext.one(fam, "gpu_power_interval_watts", gpu_id="0"), rel=0.05)
+    assert (0, False) in seen  # the failed ticks
+    assert all(has for up, has in seen if up)  # every good tick has its rates, the first after a failure too
+
+
 def test_rates_span_the_firmware_window_and_survive_a_repeated_table(mock_exporter):
     """The accumulators move only when the firmware rewrites its table (50 Hz on MI355X,
     profiles/r3_capacity.md); the driver stamps system_clock_counter at each read. Rates divide by
