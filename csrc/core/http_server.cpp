@@ -8,6 +8,7 @@
 #include <sched.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
+#include <sys/resource.h>
 #include <sys/socket.h>
 #include <sys/uio.h>
 #include <unistd.h>
@@ -35,6 +36,10 @@ constexpr int64_t kIdleTimeoutNs = 60LL * 1000000000LL;
 // a request whose body was still arriving).
 constexpr int64_t kLingerNs = 2LL * 1000000000LL;
 constexpr size_t kMaxConnsPerLoop = 4096;
+// File descriptors left to the rest of the exporter (sysfs / procfs reads, sockets of the metadata
+// pollers, the on-device helper) when the connection cap is derived from RLIMIT_NOFILE: a flood
+// of scrape connections must not make the sampler's own opens fail with EMFILE.
+constexpr rlim_t kFdReserve = 256;
 constexpr int kSndBuf = 1 << 20;  // GPUMON_HTTP_SNDBUF overrides (bytes; 0 = the kernel's autotuning)
 
 const char* status_text(int s) {
@@ -164,6 +169,12 @@ bool HttpServer::start(std::string* err) {
   };
   sndbuf_ = kSndBuf;
   if (const char* e = getenv("GPUMON_HTTP_SNDBUF")) sndbuf_ = std::max(0, atoi(e));
+  max_conns_ = kMaxConnsPerLoop;
+  rlimit rl{};
+  if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur != RLIM_INFINITY) {
+    const rlim_t usable = rl.rlim_cur > 2 * kFdReserve ? rl.rlim_cur - kFdReserve : rl.rlim_cur / 2;
+    max_conns_ = std::clamp<size_t>(usable / static_cast<rlim_t>(std::max(1, nthreads_)), 8, kMaxConnsPerLoop);
+  }
   for (int t = 0; t < nthreads_; ++t) {
     auto L = std::make_unique<Loop>();
     L->lfd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
@@ -387,9 +398,16 @@ void HttpServer::run(Loop* L) {
     return true;
   };
 
+  // accept() failing with EMFILE / ENFILE leaves the listening socket readable: level-triggered
+  // epoll would report it again at once and the loop would spin. Stop watching it for a moment.
+  int64_t accept_resume_ns = 0, last_emfile_log_ns = INT64_MIN / 2;
   while (running_.load(std::memory_order_relaxed)) {
-    int n = epoll_wait(L->ep, evs, 256, rt_on ? 100 : 1000);
+    int n = epoll_wait(L->ep, evs, 256, accept_resume_ns ? 100 : rt_on ? 100 : 1000);
     int64_t now = mono_ns();
+    if (accept_resume_ns && now >= accept_resume_ns) {
+      accept_resume_ns = 0;
+      set_events(L->lfd, EPOLLIN);
+    }
     if (rt_on) {
       if (now - win_start >= kRtWindowNs) {  // new window: back to FIFO
         win_start = now;
@@ -412,8 +430,18 @@ void HttpServer::run(Loop* L) {
       if (fd == L->lfd) {
         while (true) {
           int cfd = accept4(L->lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
-          if (cfd < 0) break;
-          if (L->conns.size() >= kMaxConnsPerLoop) {
+          if (cfd < 0) {
+            if (errno == EMFILE || errno == ENFILE) {
+              if (now - last_emfile_log_ns > 10'000'000'000) {
+                last_emfile_log_ns = now;
+                GPUMON_LOG(LogLevel::kWarn, "http", "accept: out of file descriptors; pausing accepts for 100 ms");
+              }
+              accept_resume_ns = now + 100'000'000;
+              set_events(L->lfd, 0);
+            }
+            break;
+          }
+          if (L->conns.size() >= max_conns_) {
             close(cfd);
             continue;
           }

@@ -63,6 +63,7 @@ class HttpServer {
   int port_;
   int nthreads_;
   int sndbuf_ = 0;  // SO_SNDBUF for accepted connections (0: kernel default)
+  size_t max_conns_ = 4096;  // per loop: kMaxConnsPerLoop, less when RLIMIT_NOFILE is low (start())
   Handler handler_;
   Observer observer_;
   std::vector<std::unique_ptr<Loop>> loops_;

@@ -494,3 +494,72 @@ def test_error_answer_survives_a_client_still_sending(mock_exporter):
     s.close()
     assert out.startswith(b"HTTP/1.1 413 Payload Too Large"), out
     assert b"Connection: close" in out
+
+
+def test_connection_flood_under_a_low_fd_limit(tmp_path):
+    """bin/gpumon-exporter with RLIMIT_NOFILE 64 and 300 idle connections opened against it: the
+    connection cap is derived from the limit (fds stay for the sampler), excess connections are
+    closed, the sampler keeps ticking, the HTTP loops do not spin on a readable listening socket,
+    and /metrics answers once the flood is gone."""
+    import os
+    import resource
+    import subprocess
+    import time
+    import urllib.request
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+
+    def low_limit():
+        resource.setrlimit(resource.RLIMIT_NOFILE, (64, 64))
+
+    p = subprocess.Popen([os.path.join(root, "bin", "gpumon-exporter"), "--backend", "mock:gpus=2", "--interval",
+                          "0.05", "--listen", f"127.0.0.1:{port}", "--http-threads", "2", "--log-level", "error"],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, preexec_fn=low_limit)
+    conns = []
+    try:
+        deadline = time.time() + 20
+        while time.time() < deadline:
+            try:
+                urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=1).read()
+                break
+            except OSError:
+                time.sleep(0.05)
+
+        def cpu_s():
+            f = open(f"/proc/{p.pid}/stat").read().rsplit(")", 1)[1].split()
+            return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+
+        def ticks():
+            body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+            return promtext.one(promtext.parse(body), "gpumon_ticks_total")
+
+        for _ in range(300):
+            c = socket.socket()
+            c.settimeout(2)
+            try:
+                c.connect(("127.0.0.1", port))
+                conns.append(c)
+            except OSError:
+                c.close()
+        c0, t0 = cpu_s(), time.time()
+        time.sleep(1.5)
+        burn = (cpu_s() - c0) / (time.time() - t0)
+        open_fds = len(os.listdir(f"/proc/{p.pid}/fd"))
+        assert p.poll() is None
+        assert open_fds <= 64, open_fds
+        assert burn < 0.5, burn  # a spinning loop would burn a whole CPU
+    finally:
+        for c in conns:
+            c.close()
+    try:
+        time.sleep(0.3)
+        t1 = ticks()
+        time.sleep(0.3)
+        assert ticks() > t1  # still sampling, and /metrics answers
+    finally:
+        p.terminate()
+        p.wait(10)
