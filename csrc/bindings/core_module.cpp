@@ -852,6 +852,7 @@ PYBIND11_MODULE(_core, m) {
              d["process_list_failures"] = s.process_list_failures;
              d["http_rt_loops"] = s.http_rt_loops;
              d["http_rt_demotions"] = s.http_rt_demotions;
+             d["http_evicted"] = s.http_evicted;
              d["hidden_contexts"] = s.hidden_contexts;
              d["rt_threads"] = s.rt_threads;
              d["overruns"] = s.overruns;

@@ -30,6 +30,9 @@ namespace {
 constexpr size_t kMaxHeader = 16 * 1024;
 constexpr long kMaxBody = 64 * 1024;  // every route is GET/HEAD: a request body is only ever skipped
 constexpr int64_t kIdleTimeoutNs = 60LL * 1000000000LL;
+// A request whose header has not completed this long after its first byte is dropped (a client
+// trickling a header must not hold a connection slot for the whole idle timeout).
+constexpr int64_t kHeaderTimeoutNs = 10LL * 1000000000LL;  // GPUMON_HTTP_HEADER_TIMEOUT_S overrides
 // After the last response of a "Connection: close" exchange the server half-closes and drains what
 // the client still sends for at most this long before closing: closing a socket with unread input
 // sends a RST, which can make the client drop the response it has not read yet (an error answer to
@@ -68,6 +71,7 @@ struct Conn {
   bool close_after = false;
   bool closing = false;  // response sent, write side shut: draining input until EOF / kLingerNs
   int64_t closing_ns = 0;
+  int64_t req_start_ns = 0;  // first byte of the request still being read (0: none pending)
   int64_t last_ns = 0;
   int64_t req_ns = 0;
   std::string path;
@@ -169,6 +173,9 @@ bool HttpServer::start(std::string* err) {
   };
   sndbuf_ = kSndBuf;
   if (const char* e = getenv("GPUMON_HTTP_SNDBUF")) sndbuf_ = std::max(0, atoi(e));
+  header_timeout_ns_ = kHeaderTimeoutNs;
+  if (const char* e = getenv("GPUMON_HTTP_HEADER_TIMEOUT_S"))
+    header_timeout_ns_ = static_cast<int64_t>(std::max(0.1, atof(e)) * 1e9);
   max_conns_ = kMaxConnsPerLoop;
   rlimit rl{};
   if (getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur != RLIM_INFINITY) {
@@ -364,6 +371,7 @@ void HttpServer::run(Loop* L) {
       c.req_ns = t_req;
       c.path = req.path;
       c.in.erase(0, static_cast<size_t>(used));
+      c.req_start_ns = c.in.empty() ? 0 : mono_ns();  // a pipelined request already started
       const char* body = resp.data;
       size_t blen = resp.len;
       if (!body) {
@@ -401,9 +409,11 @@ void HttpServer::run(Loop* L) {
   // accept() failing with EMFILE / ENFILE leaves the listening socket readable: level-triggered
   // epoll would report it again at once and the loop would spin. Stop watching it for a moment.
   int64_t accept_resume_ns = 0, last_emfile_log_ns = INT64_MIN / 2;
+  std::vector<int> closed_in_batch;
   while (running_.load(std::memory_order_relaxed)) {
     int n = epoll_wait(L->ep, evs, 256, accept_resume_ns ? 100 : rt_on ? 100 : 1000);
     int64_t now = mono_ns();
+    closed_in_batch.clear();
     if (accept_resume_ns && now >= accept_resume_ns) {
       accept_resume_ns = 0;
       set_events(L->lfd, EPOLLIN);
@@ -442,8 +452,22 @@ void HttpServer::run(Loop* L) {
             break;
           }
           if (L->conns.size() >= max_conns_) {
-            close(cfd);
-            continue;
+            // full: make room by closing the least recently active connection that is not
+            // sending a response (idle or half-open floods age out first), else refuse this one
+            int victim = -1;
+            int64_t oldest = INT64_MAX;
+            for (const auto& [vfd, vc] : L->conns)
+              if (!vc.writing && vc.last_ns < oldest) {
+                oldest = vc.last_ns;
+                victim = vfd;
+              }
+            if (victim < 0) {
+              close(cfd);
+              continue;
+            }
+            close_conn(victim);
+            evicted_.fetch_add(1, std::memory_order_relaxed);
+            closed_in_batch.push_back(victim);  // its number may come back from accept() below
           }
           int one = 1;
           setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
@@ -463,6 +487,11 @@ void HttpServer::run(Loop* L) {
         }
         continue;
       }
+      // an event of a connection evicted earlier in this batch (the number may now be a new
+      // connection's: its own events come with the next epoll_wait)
+      if (!closed_in_batch.empty() &&
+          std::find(closed_in_batch.begin(), closed_in_batch.end(), fd) != closed_in_batch.end())
+        continue;
       auto it = L->conns.find(fd);
       if (it == L->conns.end()) continue;
       Conn& c = it->second;
@@ -498,6 +527,7 @@ void HttpServer::run(Loop* L) {
         while (true) {
           ssize_t r = read(fd, buf, sizeof buf);
           if (r > 0) {
+            if (c.in.empty()) c.req_start_ns = now;
             c.in.append(buf, static_cast<size_t>(r));
             if (c.in.size() > kMaxHeader * 4) break;
             continue;
@@ -517,7 +547,9 @@ void HttpServer::run(Loop* L) {
       last_sweep = now;
       std::vector<int> idle;
       for (auto& [fd, c] : L->conns)
-        if (now - c.last_ns > kIdleTimeoutNs || (c.closing && now - c.closing_ns > kLingerNs)) idle.push_back(fd);
+        if (now - c.last_ns > kIdleTimeoutNs || (c.closing && now - c.closing_ns > kLingerNs) ||
+            (!c.writing && !c.closing && !c.in.empty() && now - c.req_start_ns > header_timeout_ns_))
+          idle.push_back(fd);
       for (int fd : idle) close_conn(fd);
     }
   }

@@ -50,6 +50,8 @@ class HttpServer {
   }
   int rt_loops() const { return rt_loops_.load(); }           // loops running at SCHED_FIFO now
   uint64_t rt_demotions() const { return rt_demotions_.load(); }  // budget exhaustions
+  uint64_t evicted() const { return evicted_.load(); }            // closed to make room at the cap
+  size_t max_conns() const { return max_conns_; }                 // per loop (set by start())
   bool start(std::string* err);
   void stop();
   int port() const { return port_; }
@@ -63,7 +65,8 @@ class HttpServer {
   int port_;
   int nthreads_;
   int sndbuf_ = 0;  // SO_SNDBUF for accepted connections (0: kernel default)
-  size_t max_conns_ = 4096;  // per loop: kMaxConnsPerLoop, less when RLIMIT_NOFILE is low (start())
+  size_t max_conns_ = 4096;
+  int64_t header_timeout_ns_ = 0;  // a request header not complete this long after its first byte  // per loop: kMaxConnsPerLoop, less when RLIMIT_NOFILE is low (start())
   Handler handler_;
   Observer observer_;
   std::vector<std::unique_ptr<Loop>> loops_;
@@ -74,6 +77,7 @@ class HttpServer {
   double rt_budget_ = 0.2;
   std::atomic<int> rt_loops_{0};
   std::atomic<uint64_t> rt_demotions_{0};
+  std::atomic<uint64_t> evicted_{0};  // connections closed to make room at the per-loop cap
 };
 
 }  // namespace gpumon

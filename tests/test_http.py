@@ -545,6 +545,12 @@ def test_connection_flood_under_a_low_fd_limit(tmp_path):
                 conns.append(c)
             except OSError:
                 c.close()
+        # a new scraper still gets in while the flood holds every slot: the least recently
+        # active idle connection makes room
+        urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read()
+        time.sleep(0.2)  # the counter is in the exposition from the next tick on
+        body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+        assert promtext.one(promtext.parse(body), "gpumon_http_connections_evicted_total") >= 1
         c0, t0 = cpu_s(), time.time()
         time.sleep(1.5)
         burn = (cpu_s() - c0) / (time.time() - t0)
@@ -563,3 +569,24 @@ def test_connection_flood_under_a_low_fd_limit(tmp_path):
     finally:
         p.terminate()
         p.wait(10)
+
+
+def test_trickled_header_is_dropped(monkeypatch, mock_exporter):
+    """A client that sends part of a request header and then nothing is closed after the header
+    timeout (GPUMON_HTTP_HEADER_TIMEOUT_S here; 10 s by default), not after the 60 s idle timeout."""
+    import time
+
+    monkeypatch.setenv("GPUMON_HTTP_HEADER_TIMEOUT_S", "0.5")
+    ex = mock_exporter()
+    s = socket.create_connection(("127.0.0.1", ex.port), timeout=10)
+    s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n")  # no blank line: the header never ends
+    t0 = time.monotonic()
+    assert s.recv(100) == b""  # closed by the server
+    assert time.monotonic() - t0 < 5
+    s.close()
+    # an idle keep-alive connection with nothing pending is not affected
+    k = socket.create_connection(("127.0.0.1", ex.port), timeout=10)
+    time.sleep(2.2)
+    k.sendall(b"GET /healthz HTTP/1.1\r\nHost: x\r\n\r\n")
+    assert k.recv(100).startswith(b"HTTP/1.1 200")
+    k.close()
