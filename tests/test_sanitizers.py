@@ -358,3 +358,62 @@ def test_tsan_readyz_while_the_backend_keeps_failing_to_initialise():
         _, err = p.communicate(timeout=60)
     assert "WARNING: ThreadSanitizer" not in err, err[-4000:]
     assert codes and set(codes) == {503}, set(codes)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_connection_flood_and_eviction(target, binary, env):
+    """A connection flood at a 96-fd limit: the connection cap, evictions of idle connections in the
+    middle of epoll batches, trickled headers timing out and scrapes getting in, under the
+    sanitizers."""
+    import resource
+
+    from conftest import make_locked
+
+    make_locked(target, jobs=8)
+    port = _free_port()
+    e = dict(os.environ, GPUMON_HTTP_HEADER_TIMEOUT_S="0.3", **env)
+    p = subprocess.Popen([os.path.join(ROOT, binary), "--backend", "mock:gpus=2", "--interval", "0.02", "--listen",
+                          f"127.0.0.1:{port}", "--http-threads", "2", "--log-level", "error"],
+                         stderr=subprocess.PIPE, stdout=subprocess.DEVNULL, env=e, text=True,
+                         preexec_fn=lambda: resource.setrlimit(resource.RLIMIT_NOFILE, (96, 96)))
+    conns, got = [], 0
+    try:
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            try:
+                urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=1).read()
+                break
+            except OSError:
+                time.sleep(0.1)
+        for k in range(400):
+            c = socket.socket()
+            c.settimeout(2)
+            try:
+                c.connect(("127.0.0.1", port))
+                if k % 3 == 0:
+                    c.sendall(b"GET /metrics HTTP/1.1\r\n")  # a header that never ends
+                conns.append(c)
+            except OSError:
+                c.close()
+            if k % 50 == 0:
+                try:
+                    urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read()
+                    got += 1
+                except OSError:
+                    pass
+        time.sleep(1.0)
+        assert p.poll() is None
+    finally:
+        for c in conns:
+            c.close()
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=60)
+    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
+           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    assert not bad, err[-4000:]
+    assert got >= 6, got
