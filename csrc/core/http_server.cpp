@@ -314,7 +314,12 @@ void HttpServer::run(Loop* L) {
         iov[n].iov_len = c.body_len - c.body_off;
         ++n;
       }
-      ssize_t w = writev(c.fd, iov, n);
+      // sendmsg, not writev: MSG_NOSIGNAL keeps a peer that hung up from raising SIGPIPE in a host
+      // process (the Python module, an embedding service) that did not ignore it
+      msghdr mh{};
+      mh.msg_iov = iov;
+      mh.msg_iovlen = static_cast<size_t>(n);
+      ssize_t w = sendmsg(c.fd, &mh, MSG_NOSIGNAL);
       if (w < 0) {
         if (errno == EINTR) continue;
         if (errno == EAGAIN || errno == EWOULDBLOCK) return true;
