@@ -230,8 +230,10 @@ bool docker_get(const std::string& socket_path, const std::string& target, std::
     }
   };
   if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) {
-    if (errno != EINPROGRESS && errno != EAGAIN) {
-      *err = "connect " + path + ": " + strerror(errno);
+    // EAGAIN on a non-blocking unix-socket connect means the listener's backlog is full and no
+    // connection was made (unlike TCP's EINPROGRESS): report it rather than wait for it
+    if (errno != EINPROGRESS) {
+      *err = "connect " + path + ": " + (errno == EAGAIN ? std::string("listener backlog full") : strerror(errno));
       return false;
     }
     int so = 0;

@@ -430,3 +430,37 @@ def test_exporter_idle_rows_for_docker_gpu_containers(core, tmp_path):
             ex.stop()
     inspects = [r[1] for r in d.requests if r[1] != "/containers/json"]
     assert sorted(inspects) == sorted(f"/containers/{c}/json" for c in insp)  # once per container
+
+
+def test_native_docker_reader_on_a_full_listener_backlog(core):
+    """A daemon that stopped accepting: once its listen backlog is full, a non-blocking unix
+    connect fails with EAGAIN (no connection was made); the reader says so at once."""
+    import socket as so
+    import time
+
+    path = _sock("backlog")
+    if os.path.exists(path):
+        os.unlink(path)
+    srv = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+    srv.bind(path)
+    srv.listen(0)
+    fillers = []
+    try:
+        for _ in range(8):  # fill the backlog (never accepted)
+            c = so.socket(so.AF_UNIX, so.SOCK_STREAM)
+            c.setblocking(False)
+            try:
+                c.connect(path)
+            except (BlockingIOError, OSError):
+                c.close()
+                break
+            fillers.append(c)
+        t0 = time.monotonic()
+        with pytest.raises(RuntimeError, match="listener backlog full"):
+            core.docker_list(path, timeout_ms=3000)
+        assert time.monotonic() - t0 < 1.0
+    finally:
+        for c in fillers:
+            c.close()
+        srv.close()
+        os.unlink(path)
