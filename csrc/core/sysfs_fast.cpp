@@ -320,6 +320,25 @@ void SysfsGpu::occupancy(const std::vector<uint32_t>& pids, std::vector<double>*
   }
 }
 
+bool SysfsGpu::skip_not_here(uint32_t pid, int64_t now) {
+  std::lock_guard<std::mutex> g(not_here_mu_);
+  auto it = not_here_.find(pid);
+  return it != not_here_.end() && now < it->second;
+}
+
+void SysfsGpu::note_not_here(uint32_t pid, int64_t now) {
+  std::lock_guard<std::mutex> g(not_here_mu_);
+  not_here_[pid] = now + kNotHereNs;
+}
+
+void SysfsGpu::prune_not_here(const std::vector<uint32_t>& listed_sorted) {
+  std::lock_guard<std::mutex> g(not_here_mu_);
+  for (auto it = not_here_.begin(); it != not_here_.end();) {
+    if (!std::binary_search(listed_sorted.begin(), listed_sorted.end(), it->first)) it = not_here_.erase(it);
+    else ++it;
+  }
+}
+
 bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
   out->clear();
   if (!kfd_gpu_id_) return false;
@@ -330,13 +349,18 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
   const std::string occ_name = "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy";
   char b[64];
   std::vector<uint32_t> listed;  // every KFD process of the node (any GPU)
+  const int64_t now = mono_ns();
   while (dirent* e = readdir(d)) {
     if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
     const uint32_t pid = static_cast<uint32_t>(strtoul(e->d_name, nullptr, 10));
     listed.push_back(pid);
+    if (skip_not_here(pid, now)) continue;
     const std::string pdir = kdir + "/" + e->d_name;
     size_t n = 0;
-    if (!read_small(pdir + vram_name, b, sizeof b, &n)) continue;  // process not on this GPU
+    if (!read_small(pdir + vram_name, b, sizeof b, &n)) {  // process not on this GPU
+      note_not_here(pid, now);
+      continue;
+    }
     ProcSample p;
     p.pid = pid;
     p.mem_bytes = static_cast<double>(strtoull(b, nullptr, 10));
@@ -349,6 +373,7 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
   closedir(d);
   std::sort(listed.begin(), listed.end());
   DrmFdTables::get().retain(proc_root_, listed);
+  prune_not_here(listed);
   return true;
 }
 
@@ -361,13 +386,19 @@ bool SysfsGpu::occupancy_scan(std::vector<OccRead>* out) {
   const std::string occ_name = "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy";
   const std::string vram_name = "/vram_" + std::to_string(kfd_gpu_id_);
   char b[64];
+  const int64_t now = mono_ns();
   while (dirent* e = readdir(d)) {
     if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+    const uint32_t pid = static_cast<uint32_t>(strtoul(e->d_name, nullptr, 10));
+    if (skip_not_here(pid, now)) continue;
     const std::string pdir = kdir + e->d_name;
     size_t n = 0;
-    if (!read_small(pdir + vram_name, b, sizeof b, &n)) continue;  // not on this GPU
+    if (!read_small(pdir + vram_name, b, sizeof b, &n)) {  // not on this GPU
+      note_not_here(pid, now);
+      continue;
+    }
     OccRead r;
-    r.pid = static_cast<uint32_t>(strtoul(e->d_name, nullptr, 10));
+    r.pid = pid;
     r.vram_bytes = static_cast<double>(strtoull(b, nullptr, 10));
     if (read_small(pdir + occ_name, b, sizeof b, &n)) r.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
     out->push_back(r);

@@ -210,6 +210,17 @@ class SysfsGpu {
 
  private:
   void fdinfo_usage(uint32_t pid, ProcSample* p);
+  // /sys/class/kfd/kfd/proc is not namespaced: it lists every KFD process of the host, on every
+  // GPU (15-17 on a shared MI355X box, 1 of them on the container's GPU). A process found not to
+  // be on this GPU is not asked again for kNotHereNs (each ask is an open() that fails, ~4-6 us):
+  // a process that starts using this GPU later is picked up within that time. Pids that left the
+  // listing are dropped. Shared by the tick's process list and the between-tick scans.
+  static constexpr int64_t kNotHereNs = 1'000'000'000;
+  bool skip_not_here(uint32_t pid, int64_t now);
+  void note_not_here(uint32_t pid, int64_t now);
+  void prune_not_here(const std::vector<uint32_t>& listed_sorted);
+  std::mutex not_here_mu_;
+  std::unordered_map<uint32_t, int64_t> not_here_;  // pid -> ask again after (mono ns)
   std::string sys_root_, proc_root_, dev_dir_;
   uint64_t kfd_gpu_id_ = 0;
   std::string render_path_;  // "/dev/dri/renderD<minor>"

@@ -294,3 +294,26 @@ def test_between_tick_kfd_scans_read_arrivals_and_retry_after_a_failed_listing(e
         assert ex.wait_for_seq(ex.seq + 1, 10)
         row = next((r for r in ex.pod_rows() if r["pid"] == "6161"), None)
     assert row is not None and row["cu_occupancy"] == 50
+
+
+def test_process_of_another_gpu_is_not_reasked_every_tick_but_is_picked_up_later(exporter, tmp_path):
+    """The KFD proc dir lists the host's processes on every GPU. A process found not to be on a
+    GPU is not asked again by that GPU for a second (an open() that fails, per process per tick and
+    per scan); when it starts using the GPU it shows up within that second."""
+    import time
+
+    sysr, procr = make_tree(tmp_path, gpus=2, procs=((4242, 0),))
+    ex = exporter(sysr, procr, sample_threads=0)
+    ex.tick()
+    rows = sorted((r["dev"], r["pid"]) for r in ex.pod_rows() if not r["idle"])
+    assert rows == [(0, "4242")]
+    # the process opens GPU 1 too
+    kp = sysr / "class" / "kfd" / "kfd" / "proc" / "4242"
+    (kp / "stats_36623").mkdir()
+    (kp / "vram_36623").write_text(f"{1 << 30}\n")
+    (kp / "stats_36623" / "cu_occupancy").write_text("5\n")
+    ex.tick()
+    assert sorted((r["dev"], r["pid"]) for r in ex.pod_rows() if not r["idle"]) == [(0, "4242")]  # cached
+    time.sleep(1.1)
+    ex.tick()
+    assert sorted((r["dev"], r["pid"]) for r in ex.pod_rows() if not r["idle"]) == [(0, "4242"), (1, "4242")]
