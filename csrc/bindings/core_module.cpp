@@ -995,6 +995,31 @@ PYBIND11_MODULE(_core, m) {
            [](Exporter& e, int dev, bool fail) { mock_of(e)->set_link_fail(dev, fail); })
       .def("mock_fail_scans", [](Exporter& e, int dev, int n) { mock_of(e)->fail_scans(dev, n); })
       .def("mock_fail_procs", [](Exporter& e, int dev, int n) { mock_of(e)->fail_procs(dev, n); })
+      .def(
+          "time_process_lists",
+          [](Exporter& e, int dev, int n) {
+            // n back-to-back Backend::processes() calls of one device (a sampler must not be
+            // running): the tick's process-list phase in isolation, in microseconds per call
+            Backend* b = e.backend();
+            if (!b || dev < 0 || dev >= b->device_count()) throw std::runtime_error("no such device");
+            std::vector<double> us;
+            size_t rows = 0;
+            {
+              py::gil_scoped_release nogil;
+              std::vector<ProcSample> p;
+              for (int k = 0; k < n; ++k) {
+                const int64_t t = mono_ns();
+                b->processes(dev, &p);
+                us.push_back((mono_ns() - t) * 1e-3);
+                rows = p.size();
+              }
+            }
+            py::dict d;
+            d["us"] = us;
+            d["rows"] = rows;
+            return d;
+          },
+          py::arg("dev") = 0, py::arg("n") = 200)
       .def("mock_set_firmware_frozen",
            [](Exporter& e, int dev, bool frozen) { mock_of(e)->set_firmware_frozen(dev, frozen); })
       .def("mock_set_occ_series",
