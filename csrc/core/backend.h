@@ -335,6 +335,7 @@ class RocmSmiBackend : public Backend {
   const DeviceStatic& static_info(int i) const override { return devs_[i]; }
   void sample(int i, DeviceSample* out) override;
   bool processes(int i, std::vector<ProcSample>* out) override;
+  bool supports_processes(int i) const override;  // the library exports the compute-process calls
   bool supports_ras() const override { return true; }
   void sample_ras(int i, DeviceSample* out, int slice = 0, int nslices = 1) override;  // kernel ras/ sysfs files
   std::string lib_version() const { return lib_version_; }

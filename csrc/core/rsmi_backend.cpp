@@ -233,6 +233,10 @@ void RocmSmiBackend::sample(int i, DeviceSample* out) {
   out->sample_ns = mono_ns() - t0;
 }
 
+bool RocmSmiBackend::supports_processes(int) const {
+  return t_ && t_->rsmi_compute_process_info_get && t_->rsmi_compute_process_info_by_device_get;
+}
+
 bool RocmSmiBackend::processes(int i, std::vector<ProcSample>* out) {
   out->clear();
   if (!t_->rsmi_compute_process_info_get || !t_->rsmi_compute_process_info_by_device_get) return false;
