@@ -84,6 +84,21 @@ def fd_table_check(procfs: str = "/proc", pid=None) -> tuple:
     return SKIP, "no process of another uid with open files to try"
 
 
+def fd_limit_check(http_threads: int, limit=None) -> tuple:
+    """The HTTP server's per-loop connection cap comes from RLIMIT_NOFILE (256 fds kept for the
+    sampler; csrc/core/http_server.cpp): a low limit leaves few scrape connections."""
+    import resource
+
+    soft = limit if limit is not None else resource.getrlimit(resource.RLIMIT_NOFILE)[0]
+    if soft == resource.RLIM_INFINITY:
+        return OK, "RLIMIT_NOFILE unlimited: 4096 connections per HTTP loop"
+    usable = soft - 256 if soft > 512 else soft // 2
+    cap = max(8, min(4096, usable // max(1, http_threads)))
+    status = OK if cap >= 256 else WARN
+    return status, (f"RLIMIT_NOFILE {soft}: {cap} connections per HTTP loop ({http_threads} loop(s))"
+                    + ("" if status == OK else ": a connection flood evicts scrapers early; raise the pod's nofile limit"))
+
+
 def firmware_table_check(path: str, interval_s: float, prewarm_ms: float, seconds: float = 0.25) -> tuple:
     """(status, detail) for one GPU's gpu_metrics file: how often the SMU rewrites it (a new
     firmware_timestamp, v1.8 offset 288; the driver stamps system_clock at every read, so raw bytes
@@ -219,6 +234,7 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
             up = float(m.group(1)) if m else None
             out.append((name, OK if up == 1 else WARN, f"{path}: readable" if up == 1 else f"{path}: unreadable: {lost}"))
         out.append(("other uids' fd tables",) + fd_table_check())
+        out.append(("file descriptor limit",) + fd_limit_check(int(getattr(cfg, "http_threads", 2) or 2)))
         out.append(("rt_priority / http_rt_priority",) + _rt_permitted())
         # on-device samplers: the helper and plugins must exist; --ondevice-check runs them once
         from ._native import core as _core

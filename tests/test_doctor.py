@@ -33,6 +33,7 @@ def test_doctor_reports_sockets_and_plugins():
     assert checks["on-device plugins"][0] == "ok"
     assert checks["rt_priority / http_rt_priority"][0] in ("ok", "warn")
     assert checks["other uids' fd tables"][0] in ("ok", "warn", "skip")
+    assert checks["file descriptor limit"][0] in ("ok", "warn")
 
 
 def test_doctor_names_the_grpc_status_of_a_refusing_kubelet():
@@ -153,3 +154,14 @@ def test_doctor_firmware_table_cadence_against_the_interval(tmp_path):
     finally:
         stop.set()
         t.join()
+
+
+def test_doctor_fd_limit_matches_the_server_cap():
+    """The doctor's connection cap is the one HttpServer::start derives from RLIMIT_NOFILE."""
+    from gpumon.doctor import OK, WARN, fd_limit_check
+
+    assert fd_limit_check(2, limit=1048576) == (OK, "RLIMIT_NOFILE 1048576: 4096 connections per HTTP loop (2 loop(s))")
+    st, detail = fd_limit_check(2, limit=1024)
+    assert st == OK and "384 connections per HTTP loop" in detail  # (1024 - 256) / 2
+    st, detail = fd_limit_check(2, limit=64)
+    assert st == WARN and "16 connections per HTTP loop" in detail  # 64 / 2 / 2
