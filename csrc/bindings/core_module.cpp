@@ -1002,6 +1002,8 @@ PYBIND11_MODULE(_core, m) {
             // running): the tick's process-list phase in isolation, in microseconds per call
             Backend* b = e.backend();
             if (!b || dev < 0 || dev >= b->device_count()) throw std::runtime_error("no such device");
+            if (e.config().interval_s > 0 || e.config().sample_threads != 0)
+              throw std::runtime_error("time_process_lists needs interval_s 0 and sample_threads 0 (no concurrent lists)");
             std::vector<double> us;
             size_t rows = 0;
             {

@@ -348,3 +348,23 @@ def test_failed_process_list_keeps_the_subsampled_pids(mock_exporter):
     _wait_ticks(ex, 1)  # the interval after it
     rows = [r for r in ex.pod_rows() if r["pid"] == "4242"]
     assert rows and rows[0]["occ_samples"] >= 4, rows
+
+
+def test_time_process_lists_only_without_a_sampler(core):
+    ex = core.Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0, "sample_threads": 0,
+                        "mock": {"procs": [{"pid": 7, "device": 0}]}})
+    ex.start()
+    try:
+        r = ex.time_process_lists(0, 5)
+        assert r["rows"] == 1 and len(r["us"]) == 5
+        with pytest.raises(RuntimeError, match="no such device"):
+            ex.time_process_lists(3, 1)
+    finally:
+        ex.stop()
+    busy = core.Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0.5})
+    busy.start()
+    try:
+        with pytest.raises(RuntimeError, match="no concurrent lists"):
+            busy.time_process_lists(0, 1)
+    finally:
+        busy.stop()
