@@ -19,6 +19,7 @@
 #include <cstring>
 #include <strings.h>
 #include <ctime>
+#include <list>
 #include <unordered_map>
 
 #include "common.h"
@@ -73,6 +74,7 @@ struct Conn {
   int64_t closing_ns = 0;
   int64_t req_start_ns = 0;  // first byte of the request still being read (0: none pending)
   int64_t last_ns = 0;
+  std::list<int>::iterator lru;  // position in Loop::lru (least recently active first)
   int64_t req_ns = 0;
   std::string path;
 };
@@ -149,6 +151,7 @@ struct HttpServer::Loop {
   int wake = -1;
   std::thread th;
   std::unordered_map<int, Conn> conns;
+  std::list<int> lru;  // connection fds, least recently active first: O(1) eviction at the cap
 };
 
 HttpServer::HttpServer(std::string addr, int port, int threads, Handler h, Observer obs)
@@ -249,6 +252,7 @@ void HttpServer::stop() {
     if (L->th.joinable()) L->th.join();
     for (auto& [fd, c] : L->conns) close(fd);
     L->conns.clear();
+    L->lru.clear();
     close(L->lfd);
     close(L->ep);
     close(L->wake);
@@ -290,7 +294,11 @@ void HttpServer::run(Loop* L) {
   auto close_conn = [&](int fd) {
     epoll_ctl(L->ep, EPOLL_CTL_DEL, fd, nullptr);
     close(fd);
-    L->conns.erase(fd);
+    auto it = L->conns.find(fd);
+    if (it != L->conns.end()) {
+      L->lru.erase(it->second.lru);
+      L->conns.erase(it);
+    }
     conns_.fetch_sub(1);
   };
   auto set_events = [&](int fd, uint32_t e) {
@@ -460,12 +468,13 @@ void HttpServer::run(Loop* L) {
             // full: make room by closing the least recently active connection that is not
             // sending a response (idle or half-open floods age out first), else refuse this one
             int victim = -1;
-            int64_t oldest = INT64_MAX;
-            for (const auto& [vfd, vc] : L->conns)
-              if (!vc.writing && vc.last_ns < oldest) {
-                oldest = vc.last_ns;
+            for (int vfd : L->lru) {  // oldest first; a connection mid-response is skipped
+              auto vit = L->conns.find(vfd);
+              if (vit != L->conns.end() && !vit->second.writing) {
                 victim = vfd;
+                break;
               }
+            }
             if (victim < 0) {
               close(cfd);
               continue;
@@ -483,6 +492,7 @@ void HttpServer::run(Loop* L) {
           Conn c;
           c.fd = cfd;
           c.last_ns = now;
+          c.lru = L->lru.insert(L->lru.end(), cfd);
           L->conns.emplace(cfd, std::move(c));
           conns_.fetch_add(1);
           epoll_event ev{};
@@ -501,6 +511,7 @@ void HttpServer::run(Loop* L) {
       if (it == L->conns.end()) continue;
       Conn& c = it->second;
       c.last_ns = now;
+      L->lru.splice(L->lru.end(), L->lru, c.lru);  // most recently active last
       if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
         close_conn(fd);
         continue;

@@ -65,8 +65,8 @@ class HttpServer {
   int port_;
   int nthreads_;
   int sndbuf_ = 0;  // SO_SNDBUF for accepted connections (0: kernel default)
-  size_t max_conns_ = 4096;
-  int64_t header_timeout_ns_ = 0;  // a request header not complete this long after its first byte  // per loop: kMaxConnsPerLoop, less when RLIMIT_NOFILE is low (start())
+  size_t max_conns_ = 4096;        // per loop: kMaxConnsPerLoop, less when RLIMIT_NOFILE is low (start())
+  int64_t header_timeout_ns_ = 0;  // a request header not complete this long after its first byte
   Handler handler_;
   Observer observer_;
   std::vector<std::unique_ptr<Loop>> loops_;
