@@ -853,6 +853,7 @@ PYBIND11_MODULE(_core, m) {
              d["http_rt_loops"] = s.http_rt_loops;
              d["http_rt_demotions"] = s.http_rt_demotions;
              d["http_evicted"] = s.http_evicted;
+             d["http_max_conns"] = s.http_max_conns;
              d["hidden_contexts"] = s.hidden_contexts;
              d["rt_threads"] = s.rt_threads;
              d["overruns"] = s.overruns;

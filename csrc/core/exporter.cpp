@@ -1716,7 +1716,10 @@ SelfStats Exporter::self_stats() const {
   s.process_list_failures = proc_failures_.load(std::memory_order_relaxed);
   s.hidden_contexts = hidden_contexts_.load();
   s.rt_threads = rt_threads_->load();
-  if (server_) s.http_evicted = static_cast<int64_t>(server_->evicted());
+  if (server_) {
+    s.http_evicted = static_cast<int64_t>(server_->evicted());
+    s.http_max_conns = static_cast<int64_t>(server_->max_conns() * static_cast<size_t>(std::max(1, cfg_.http_threads)));
+  }
   if (cfg_.http_rt_priority > 0 && server_) {
     s.http_rt_loops = server_->rt_loops();
     s.http_rt_demotions = static_cast<int64_t>(server_->rt_demotions());

@@ -829,6 +829,13 @@ void render_prometheus(const RenderInput& in, std::string* o) {
                "Sampler and device-worker threads running SCHED_FIFO (rt_priority > 0 and CAP_SYS_NICE).", "gauge");
       f.add(hl, static_cast<double>(s.rt_threads));
     }
+    if (s.http_max_conns >= 0) {
+      Family f(o, "gpumon_http_max_connections",
+               "Connections the HTTP loops hold at most (per-loop cap x loops; the cap comes from RLIMIT_NOFILE "
+               "with 256 fds kept for the sampler).",
+               "gauge");
+      f.add(hl, static_cast<double>(s.http_max_conns));
+    }
     if (s.http_evicted >= 0) {
       Family f(o, "gpumon_http_connections_evicted_total",
                "Idle connections closed to make room for a new one at the per-loop connection cap (derived "

@@ -84,16 +84,27 @@ def fd_table_check(procfs: str = "/proc", pid=None) -> tuple:
     return SKIP, "no process of another uid with open files to try"
 
 
+def fd_limit_cap(http_threads: int, limit=None) -> int:
+    """The HTTP server's per-loop connection cap for a RLIMIT_NOFILE soft limit (the formula of
+    HttpServer::start, csrc/core/http_server.cpp; the running exporter exports the product as
+    gpumon_http_max_connections, and a test keeps the two equal)."""
+    import resource
+
+    soft = limit if limit is not None else resource.getrlimit(resource.RLIMIT_NOFILE)[0]
+    if soft == resource.RLIM_INFINITY:
+        return 4096
+    usable = soft - 256 if soft > 512 else soft // 2
+    return max(8, min(4096, usable // max(1, http_threads)))
+
+
 def fd_limit_check(http_threads: int, limit=None) -> tuple:
-    """The HTTP server's per-loop connection cap comes from RLIMIT_NOFILE (256 fds kept for the
-    sampler; csrc/core/http_server.cpp): a low limit leaves few scrape connections."""
+    """A low RLIMIT_NOFILE leaves few scrape connections (256 fds are kept for the sampler)."""
     import resource
 
     soft = limit if limit is not None else resource.getrlimit(resource.RLIMIT_NOFILE)[0]
     if soft == resource.RLIM_INFINITY:
         return OK, "RLIMIT_NOFILE unlimited: 4096 connections per HTTP loop"
-    usable = soft - 256 if soft > 512 else soft // 2
-    cap = max(8, min(4096, usable // max(1, http_threads)))
+    cap = fd_limit_cap(http_threads, soft)
     status = OK if cap >= 256 else WARN
     return status, (f"RLIMIT_NOFILE {soft}: {cap} connections per HTTP loop ({http_threads} loop(s))"
                     + ("" if status == OK else ": a connection flood evicts scrapers early; raise the pod's nofile limit"))

@@ -165,3 +165,17 @@ def test_doctor_fd_limit_matches_the_server_cap():
     assert st == OK and "384 connections per HTTP loop" in detail  # (1024 - 256) / 2
     st, detail = fd_limit_check(2, limit=64)
     assert st == WARN and "16 connections per HTTP loop" in detail  # 64 / 2 / 2
+
+
+def test_doctor_cap_formula_is_the_servers(core):
+    """doctor.fd_limit_cap and HttpServer::start compute the same cap at this process's limit."""
+    from gpumon.doctor import fd_limit_cap
+
+    for threads in (1, 2, 3):
+        ex = core.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                            "http_threads": threads})
+        ex.start()
+        try:
+            assert ex.self_stats()["http_max_conns"] == threads * fd_limit_cap(threads)
+        finally:
+            ex.stop()
