@@ -149,10 +149,18 @@ def build():
                         [(f'gpu_metrics_table_age_seconds{{{HOST}}}', "{{host}} gpu{{gpu_id}} age"),
                          (f'gpu_metrics_table_frozen{{{HOST}}} > 0', "{{host}} gpu{{gpu_id}} FROZEN")], 0, y, 12, 8,
                         fieldConfig={"defaults": {"unit": "s"}, "overrides": []}))
-    panels.append(panel("Exporter: HTTP loops at SCHED_FIFO / budget demotions (request floods)", "timeseries",
+    panels.append(panel("Exporter: HTTP loops at SCHED_FIFO / budget demotions / evictions (request floods)",
+                        "timeseries",
                         [(f'gpumon_http_rt_loops{{{HOST}}}', "{{host}} RT loops"),
-                         (f'rate(gpumon_http_rt_demotions_total{{{HOST}}}[5m])', "{{host}} demotions/s")],
+                         (f'rate(gpumon_http_rt_demotions_total{{{HOST}}}[5m])', "{{host}} demotions/s"),
+                         (f'rate(gpumon_http_connections_evicted_total{{{HOST}}}[5m])', "{{host}} evicted conns/s")],
                         12, y, 12, 8))
+    y += 8
+    panels.append(panel("Exporter: failed process lists (last good list held up to 3 ticks)", "timeseries",
+                        [(f'rate(gpumon_process_list_failures_total{{{HOST}}}[5m])', "{{host}} failed lists/s"),
+                         (f'gpu_process_list_held{{{HOST}}} > 0', "{{host}} gpu{{gpu_id}} HELD"),
+                         (f'rate(gpumon_occupancy_scan_failures_total{{{HOST}}}[5m])', "{{host}} KFD scan failures/s")],
+                        0, y, 24, 8))
     return {
         "title": "gpumon — MI355X GPU cluster",
         "uid": "gpumon-mi355x",
