@@ -219,3 +219,24 @@ def test_metric_filter_keys_parse_identically(tmp_path):
     assert n["metrics_exclude"] == ["pod_gpu_*", "gpumon_*"] == _py(str(p), env)["metrics_exclude"]
     n = json.loads(_print("--metrics-exclude", "gpu_xcd_*").stdout)
     assert n["metrics_exclude"] == ["gpu_xcd_*"] and n["metrics_include"] == []
+
+
+def test_environment_only_knobs_are_documented():
+    """Every GPUMON_* variable the native code reads with getenv() (the test fakes' GPUMON_FAKE_*
+    aside) is in docs/configuration.md's environment-only table, and the table lists no other."""
+    import re
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_config_doc
+
+    read = set()
+    for base, _, files in os.walk(os.path.join(ROOT, "csrc")):
+        for f in files:
+            if f.endswith((".cpp", ".h", ".hip")):
+                read |= set(re.findall(r'getenv\("(GPUMON_[A-Z0-9_]+)"\)', open(os.path.join(base, f)).read()))
+    read = {v for v in read if not v.startswith("GPUMON_FAKE_")}
+    listed = {name for name, *_ in gen_config_doc.ENV_ONLY}
+    assert read == listed, (read - listed, listed - read)
+    doc = open(os.path.join(ROOT, "docs", "configuration.md")).read()
+    assert doc == gen_config_doc.render(), "docs/configuration.md is stale: python tools/gen_config_doc.py"
