@@ -1437,13 +1437,21 @@ void Exporter::influx_loop() {
   const std::string headers = "Content-Type: text/plain; charset=utf-8\r\n" +
                               (!cfg_.influx_token.empty() ? "Authorization: Token " + cfg_.influx_token + "\r\n"
                                                           : u.auth_header);
+  // A batch the server could not take for a transient reason (no connection, 5xx, 429) goes back
+  // to the head of the queue and the push backs off (0.5 s doubling to 30 s), so an InfluxDB restart
+  // loses nothing but what overflows the 60-batch queue; a 4xx other than 429 (a bad request, bad
+  // credentials) would fail again and is dropped. Warnings: at most one per 10 s.
+  int64_t backoff_ns = 0, retry_at = 0, last_warn = INT64_MIN / 2;
+  uint64_t unlogged = 0;
   while (running_) {
     std::string body;
     {
       std::unique_lock<std::mutex> lk(push_mu_);
-      push_cv_.wait_for(lk, std::chrono::milliseconds(200), [&] { return !push_q_.empty() || !running_; });
+      const int64_t wait_ns = std::max<int64_t>(0, retry_at - mono_ns());
+      push_cv_.wait_for(lk, std::chrono::nanoseconds(std::min<int64_t>(std::max<int64_t>(wait_ns, 1), 200'000'000)),
+                        [&] { return !running_ || (!push_q_.empty() && mono_ns() >= retry_at); });
       if (!running_) break;
-      if (push_q_.empty()) continue;
+      if (push_q_.empty() || mono_ns() < retry_at) continue;
       body = std::move(push_q_.front());
       push_q_.pop_front();
     }
@@ -1451,10 +1459,28 @@ void Exporter::influx_loop() {
     int st = client.request("POST", u, body, headers, &resp, &err);
     if (st >= 200 && st < 300) {
       influx_ok_++;
-    } else {
-      influx_fail_++;
+      backoff_ns = 0;
+      continue;
+    }
+    influx_fail_++;
+    const bool transient = st < 0 || st >= 500 || st == 429;
+    if (transient) {
+      std::lock_guard<std::mutex> g(push_mu_);
+      if (push_q_.size() < 60) push_q_.push_front(std::move(body));
+      else influx_dropped_++;
+      backoff_ns = std::clamp<int64_t>(backoff_ns * 2, 500'000'000, 30'000'000'000);
+      retry_at = mono_ns() + backoff_ns;
+    }
+    const int64_t now = mono_ns();
+    if (now - last_warn >= 10'000'000'000) {
       GPUMON_LOG(LogLevel::kWarn, "influx",
-                 "push failed: " + (st < 0 ? err : ("HTTP " + std::to_string(st) + " " + resp.substr(0, 200))));
+                 "push failed: " + (st < 0 ? err : ("HTTP " + std::to_string(st) + " " + resp.substr(0, 200))) +
+                     (transient ? "; retrying in " + std::to_string(backoff_ns / 1'000'000) + " ms" : "; batch dropped") +
+                     (unlogged ? " (" + std::to_string(unlogged) + " more failures since the last warning)" : ""));
+      last_warn = now;
+      unlogged = 0;
+    } else {
+      unlogged++;
     }
   }
 }

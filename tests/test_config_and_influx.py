@@ -253,3 +253,53 @@ def test_devices_accept_hip_ids_and_bdfs_and_refuse_the_rest():
     assert Config().apply_dict({"devices": "1, 0000:25:00.0"}).to_core()["devices"] == ["1", "0000:25:00.0"]
     with pytest.raises(ValueError, match="neither a hip id nor a PCI BDF"):
         Config(devices=["gpu3"]).to_core()
+
+
+class _FlakySink(_Sink):
+    """Answers the first `fail` POSTs with `code`, then 204."""
+    fail, code, seen = 0, 503, 0
+
+    def do_POST(self):  # noqa: N802
+        n = int(self.headers.get("Content-Length", 0))
+        body = self.rfile.read(n).decode()
+        _FlakySink.seen += 1
+        if _FlakySink.seen <= _FlakySink.fail:
+            self.send_response(_FlakySink.code)
+            self.send_header("Content-Length", "0")
+            self.end_headers()
+            return
+        _Sink.bodies.append((self.path, body))
+        self.send_response(204)
+        self.send_header("Content-Length", "0")
+        self.end_headers()
+
+
+@pytest.mark.parametrize("code,kept", [(503, True), (429, True), (400, False)])
+def test_influx_transient_failures_are_retried_in_order(core, code, kept):
+    """An InfluxDB that answers 503 / 429 for a while (a restart, rate limiting) loses no batch:
+    the failed batch goes back to the head of the queue and the push backs off. A 400 is not
+    transient: that batch is dropped, the next ones go through."""
+    _Sink.bodies = []
+    _FlakySink.fail, _FlakySink.code, _FlakySink.seen = 2, code, 0
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _FlakySink)
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    url = f"http://127.0.0.1:{srv.server_address[1]}/write?db=gpu_process"
+    ex = core.Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0, "influx_url": url,
+                        "host": "n1"})
+    ex.start()  # tick 1 queued
+    try:
+        for _ in range(4):
+            ex.tick()  # ticks 2-5
+        deadline = time.time() + 10
+        want = 5 if kept else 3
+        while time.time() < deadline and len(_Sink.bodies) < want:
+            time.sleep(0.05)
+        st = ex.self_stats()
+    finally:
+        ex.stop()
+        srv.shutdown()
+    stamps = [int(b.strip().split("\n")[0].rsplit(" ", 1)[1]) for _, b in _Sink.bodies]
+    assert len(stamps) == (5 if kept else 3), stamps
+    assert stamps == sorted(stamps)  # delivered in tick order
+    assert st["influx_fail"] == 2
