@@ -131,8 +131,12 @@ bool Exporter::podres_poll_once() {
 void Exporter::podres_loop() {
   std::unique_lock<std::mutex> lk(podres_mu_);
   while (running_) {
-    podres_cv_.wait_for(lk, std::chrono::duration<double>(std::max(0.5, cfg_.pod_resources_refresh_s)),
-                        [&] { return !running_.load(); });
+    // system_clock deadline (see influx_loop: TSan does not intercept pthread_cond_clockwait)
+    podres_cv_.wait_until(lk,
+                          std::chrono::system_clock::now() +
+                              std::chrono::duration_cast<std::chrono::system_clock::duration>(
+                                  std::chrono::duration<double>(std::max(0.5, cfg_.pod_resources_refresh_s))),
+                          [&] { return !running_.load(); });
     if (!running_) break;
     lk.unlock();
     if (!cfg_.cri_socket.empty()) cri_poll_once();

@@ -1418,9 +1418,10 @@ TickInfo Exporter::tick() {
 
 bool Exporter::wait_for_seq(uint64_t want, double timeout_s) {
   std::unique_lock<std::mutex> lk(seq_mu_);
-  return seq_cv_.wait_for(lk, std::chrono::duration<double>(timeout_s),
-                          [&] { return seq_.load() >= want || !running_; }) &&
-         seq_.load() >= want;
+  // system_clock deadline (see influx_loop: TSan does not intercept pthread_cond_clockwait)
+  const auto until = std::chrono::system_clock::now() +
+                     std::chrono::duration_cast<std::chrono::system_clock::duration>(std::chrono::duration<double>(timeout_s));
+  return seq_cv_.wait_until(lk, until, [&] { return seq_.load() >= want || !running_; }) && seq_.load() >= want;
 }
 
 void Exporter::influx_loop() {
@@ -1448,8 +1449,12 @@ void Exporter::influx_loop() {
     {
       std::unique_lock<std::mutex> lk(push_mu_);
       const int64_t wait_ns = std::max<int64_t>(0, retry_at - mono_ns());
-      push_cv_.wait_for(lk, std::chrono::nanoseconds(std::min<int64_t>(std::max<int64_t>(wait_ns, 1), 200'000'000)),
-                        [&] { return !running_ || (!push_q_.empty() && mono_ns() >= retry_at); });
+      // system_clock deadline: a steady_clock wait compiles to pthread_cond_clockwait, which the
+      // toolchain's TSan does not intercept (it then reports the next lock as a double lock)
+      push_cv_.wait_until(lk,
+                          std::chrono::system_clock::now() +
+                              std::chrono::nanoseconds(std::min<int64_t>(std::max<int64_t>(wait_ns, 1), 200'000'000)),
+                          [&] { return !running_ || (!push_q_.empty() && mono_ns() >= retry_at); });
       if (!running_) break;
       if (push_q_.empty() || mono_ns() < retry_at) continue;
       body = std::move(push_q_.front());

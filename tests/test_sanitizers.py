@@ -288,8 +288,9 @@ class _GarbageH2:
 def test_sanitized_failure_paths(target, binary, env):
     """Round-4 failure paths: a start that fails at the listen address (backend and device workers
     already up: the leak checker sees whatever is not taken down), process lists that fail every
-    3rd call (the held list crossing threads), and a PodResources / CRI peer that answers mangled
-    HTTP/2 -- with scrapes running, no sanitizer report."""
+    3rd call (the held list crossing threads), a PodResources / CRI peer that answers mangled
+    HTTP/2, and an Influx push that cannot connect (requeue + backoff) -- with scrapes running, no
+    sanitizer report."""
     from conftest import make_locked
 
     make_locked(target, jobs=8)
@@ -303,9 +304,11 @@ def test_sanitized_failure_paths(target, binary, env):
     sock = f"/tmp/gpumon-h2-san-{target}-{os.getpid()}.sock"
     peer = _GarbageH2(sock)
     try:
-        rc, err = _run(exe, dict(env, GPUMON_METADATA_REFRESH="0.3"),
+        # plus an Influx push to a port nothing listens on: the pusher's requeue + backoff path
+        rc, err = _run(exe, dict(env, GPUMON_METADATA_REFRESH="0.3", GPUMON_INFLUX_TIMEOUT_S="0.2"),
                        ("--backend", "mock:gpus=4,procs=3,procs_fail_every=3", "--interval", "0.05",
-                        "--pod-resources", sock, "--cri", sock), min_s=3.0)
+                        "--pod-resources", sock, "--cri", sock, "--influx-url", "http://127.0.0.1:9/write"),
+                       min_s=3.0)
     finally:
         peer.close()
     bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
