@@ -131,12 +131,14 @@ bool Exporter::podres_poll_once() {
 void Exporter::podres_loop() {
   std::unique_lock<std::mutex> lk(podres_mu_);
   while (running_) {
-    // system_clock deadline (see influx_loop: TSan does not intercept pthread_cond_clockwait)
-    podres_cv_.wait_until(lk,
-                          std::chrono::system_clock::now() +
-                              std::chrono::duration_cast<std::chrono::system_clock::duration>(
-                                  std::chrono::duration<double>(std::max(0.5, cfg_.pod_resources_refresh_s))),
-                          [&] { return !running_.load(); });
+    // Monotonic deadline, waited in <= 1 s system_clock slices: TSan does not intercept the
+    // pthread_cond_clockwait a steady_clock wait compiles to, and a single system_clock wait
+    // would stretch by however far the wall clock is stepped back meanwhile.
+    const int64_t due = mono_ns() + static_cast<int64_t>(std::max(0.5, cfg_.pod_resources_refresh_s) * 1e9);
+    while (running_ && mono_ns() < due)
+      podres_cv_.wait_until(lk, std::chrono::system_clock::now() +
+                                    std::chrono::nanoseconds(std::min<int64_t>(due - mono_ns(), 1'000'000'000)),
+                            [&] { return !running_.load(); });
     if (!running_) break;
     lk.unlock();
     if (!cfg_.cri_socket.empty()) cri_poll_once();

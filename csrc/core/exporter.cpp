@@ -1418,10 +1418,14 @@ TickInfo Exporter::tick() {
 
 bool Exporter::wait_for_seq(uint64_t want, double timeout_s) {
   std::unique_lock<std::mutex> lk(seq_mu_);
-  // system_clock deadline (see influx_loop: TSan does not intercept pthread_cond_clockwait)
-  const auto until = std::chrono::system_clock::now() +
-                     std::chrono::duration_cast<std::chrono::system_clock::duration>(std::chrono::duration<double>(timeout_s));
-  return seq_cv_.wait_until(lk, until, [&] { return seq_.load() >= want || !running_; }) && seq_.load() >= want;
+  // monotonic deadline in <= 100 ms system_clock slices (see podres_loop)
+  const int64_t due = mono_ns() + static_cast<int64_t>(std::max(0.0, timeout_s) * 1e9);
+  auto done = [&] { return seq_.load() >= want || !running_; };
+  while (!done() && mono_ns() < due)
+    seq_cv_.wait_until(lk, std::chrono::system_clock::now() +
+                               std::chrono::nanoseconds(std::min<int64_t>(due - mono_ns(), 100'000'000)),
+                       done);
+  return seq_.load() >= want;
 }
 
 void Exporter::influx_loop() {
