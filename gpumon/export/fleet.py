@@ -105,14 +105,23 @@ def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
     return "\n".join(lines)
 
 
-def fetch(urls: List[str], timeout_s: float = 3.0) -> Tuple[List[dict], Dict[str, str]]:
-    """GET every exporter's /metrics (native HTTP client); parse failures are reported, not raised."""
+def fetch(urls: List[str], timeout_s: float = 3.0, workers: int = 16) -> Tuple[List[dict], Dict[str, str]]:
+    """GET every exporter's /metrics (native HTTP client, which releases the GIL) from up to
+    `workers` threads at once, so a refresh over many nodes takes about one node's time even when
+    some of them time out; frames keep the order of `urls`. Parse failures are reported, not raised."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from .._native import core
 
     c = core()
+
+    def one(u):
+        return c.http_request("GET", u, "", "", timeout_s)
+
+    with ThreadPoolExecutor(max_workers=max(1, min(workers, len(urls) or 1))) as pool:
+        answers = list(pool.map(one, urls))
     frames, errors = [], {}
-    for u in urls:
-        status, body, err = c.http_request("GET", u, "", "", timeout_s)
+    for u, (status, body, err) in zip(urls, answers):
         if status != 200:
             errors[u] = err or f"HTTP {status}"
             continue

@@ -66,3 +66,42 @@ def test_influx_extended_carries_ras_totals(mock_exporter):
     ex.tick()  # the RAS read runs after a tick is published; the next tick carries it (ras_async)
     (ext,) = [l for l in ex.influx_text().splitlines() if l.startswith("gpu_ext,")]
     assert "ecc_uncorrectable=1" in ext and "ecc_correctable=7" in ext and "retired_pages=0" in ext
+
+
+def test_fleet_fetch_runs_nodes_in_parallel(core):
+    """Four nodes that each hold the request 0.5 s before answering are fetched in about one node's
+    time, and frames keep the order of the URLs."""
+    import http.server
+    import threading
+    import time
+
+    class Slow(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):  # noqa: N802
+            time.sleep(0.5)
+            body = ("# TYPE node_gpu_gpu_util gauge\n"
+                    f'node_gpu_gpu_util{{host="h{self.server.server_address[1]}",gpu_id="0"}} 1\n').encode()
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def log_message(self, *a):
+            pass
+
+    srvs = [http.server.ThreadingHTTPServer(("127.0.0.1", 0), Slow) for _ in range(4)]
+    for s in srvs:
+        threading.Thread(target=s.serve_forever, daemon=True).start()
+    try:
+        from gpumon.export import fleet
+
+        urls = [f"http://127.0.0.1:{s.server_address[1]}/metrics" for s in srvs]
+        t0 = time.monotonic()
+        frames, errors = fleet.fetch(urls, timeout_s=5)
+        dt = time.monotonic() - t0
+    finally:
+        for s in srvs:
+            s.shutdown()
+    assert not errors and len(frames) == 4
+    assert dt < 1.5, dt
+    hosts = [f["node_gpu_gpu_util"]["samples"][0][1]["host"] for f in frames]
+    assert hosts == [f"h{s.server_address[1]}" for s in srvs]
