@@ -17,6 +17,12 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _reports(stderr):
+    """Sanitizer report lines (ASan, UBSan, TSan, LeakSanitizer) in a run's stderr."""
+    return [l for l in stderr.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
+            or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -84,8 +90,7 @@ def test_sanitized_exporter_under_concurrent_scrapes(target, binary, env, extra)
     r = make_locked(target, *(["fakes"] if extra else []), jobs=8)
     assert r.returncode == 0, r.stderr[-2000:]
     rc, err = _run(os.path.join(ROOT, binary), dict(env, GPUMON_FAKE_AGENTS="4"), extra)
-    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
-           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    bad = _reports(err)
     assert not bad, err[-4000:]
     assert rc == 0, err[-2000:]
 
@@ -142,8 +147,7 @@ def test_sanitized_exporter_survives_helper_kills(target, binary, env):
     finally:
         p.send_signal(signal.SIGTERM)
         _, err = p.communicate(timeout=60)
-    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
-           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    bad = _reports(err)
     assert not bad, err[-4000:]
 
 
@@ -186,8 +190,7 @@ def test_sanitized_docker_poller_on_mutated_listings(target, binary, env):
     with FakeDocker(sock, mutate):
         rc, err = _run(os.path.join(ROOT, binary), dict(env, GPUMON_METADATA_REFRESH="0.5"), ("--docker", sock),
                        min_s=4.0)
-    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
-           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    bad = _reports(err)
     assert not bad, err[-4000:]
     assert rc == 0, err[-2000:]
     assert len(served) >= 4, served
@@ -220,8 +223,7 @@ def test_sanitized_sharing_subsamples_and_link_map(target, binary, env, tmp_path
     rc, err = _run(os.path.join(ROOT, binary), dict(env, GPUMON_LINK_EVERY="1", GPUMON_OCC_SAMPLES="20"),
                    ("--backend", "mock:gpus=4,procs=3,link_order=rotate", "--interval", "0.1",
                     "--pod-logs", str(logs), "--device-checkpoint", str(ckpt)), min_s=3.0)
-    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
-           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    bad = _reports(err)
     assert not bad, err[-4000:]
     assert rc == 0, err[-2000:]
 
@@ -297,8 +299,7 @@ def test_sanitized_failure_paths(target, binary, env):
     exe = os.path.join(ROOT, binary)
     r = subprocess.run([exe, "--backend", "mock:gpus=4", "--sample-threads", "2", "--listen", "not-an-address:1",
                         "--log-level", "error"], capture_output=True, text=True, timeout=60, env=dict(os.environ, **env))
-    bad = [l for l in r.stderr.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
-           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    bad = _reports(r.stderr)
     assert not bad, r.stderr[-4000:]
     assert r.returncode not in (0, -6, -11, 134, 139), r.stderr[-2000:]
     sock = f"/tmp/gpumon-h2-san-{target}-{os.getpid()}.sock"
@@ -311,8 +312,7 @@ def test_sanitized_failure_paths(target, binary, env):
                        min_s=3.0)
     finally:
         peer.close()
-    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
-           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    bad = _reports(err)
     assert not bad, err[-4000:]
     assert rc == 0, err[-2000:]
     assert peer.n >= 4, peer.n
@@ -416,7 +416,6 @@ def test_sanitized_connection_flood_and_eviction(target, binary, env):
             c.close()
         p.send_signal(signal.SIGTERM)
         _, err = p.communicate(timeout=60)
-    bad = [l for l in err.splitlines() if "ERROR: AddressSanitizer" in l or "runtime error:" in l
-           or "WARNING: ThreadSanitizer" in l or "ERROR: LeakSanitizer" in l]
+    bad = _reports(err)
     assert not bad, err[-4000:]
     assert got >= 6, got
