@@ -58,6 +58,10 @@ def test_servicemonitor():
     sm = _docs("deploy/k8s/gpumon-servicemonitor.yaml")[0]
     assert sm["kind"] == "ServiceMonitor"
     assert sm["spec"]["endpoints"][0]["port"] == "metrics"
+    # /readyz is 503 while the device backend is down: the Service must still list the pod, or the
+    # series that say why (gpumon_backend_up 0, the GpumonExporterDown alert) are never scraped
+    svc = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "Service")
+    assert svc["spec"]["publishNotReadyAddresses"] is True
 
 
 def _plugin_metric_names():
