@@ -193,9 +193,16 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
         else:
             out.append(("firmware table", SKIP, "no gpu_metrics file for the first GPU"))
         kfd = "/sys/class/kfd/kfd/proc"
-        out.append(("KFD process table", OK if os.access(kfd, os.R_OK) else WARN,
-                    f"{kfd} readable" if os.access(kfd, os.R_OK)
-                    else f"{kfd} not readable: no per-process rows (pod_gpu_*), no occupancy / busy %"))
+        if os.access(kfd, os.R_OK):
+            try:
+                n_kfd = sum(1 for e in os.listdir(kfd) if e.isdigit())
+            except OSError:
+                n_kfd = -1
+            out.append(("KFD process table", OK, f"{kfd} readable, {n_kfd} KFD process(es) on the host (every GPU; "
+                                                 "each tick reads the ones on the sampled GPUs)"))
+        else:
+            out.append(("KFD process table", WARN,
+                        f"{kfd} not readable: no per-process rows (pod_gpu_*), no occupancy / busy %"))
         try:
             init = open("/proc/1/comm").read().strip()
         except OSError:
