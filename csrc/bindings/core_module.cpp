@@ -104,6 +104,10 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "influx_every", &c.influx_every);
   get(d, "influx_timeout_s", &c.influx_timeout_s);
   get(d, "influx_token", &c.influx_token);
+  get(d, "influx_ca_file", &c.influx_ca_file);
+  get(d, "influx_tls_insecure", &c.influx_tls_insecure);
+  get(d, "influx_client_cert", &c.influx_client_cert);
+  get(d, "influx_client_key", &c.influx_client_key);
   get(d, "init_retry_s", &c.init_retry_s);
   get(d, "health_stale_s", &c.health_stale_s);
   get(d, "reinit_after", &c.reinit_after);
@@ -706,24 +710,60 @@ PYBIND11_MODULE(_core, m) {
     d["port"] = u.port;
     d["path"] = u.path;
     d["auth_header"] = u.auth_header;
+    d["tls"] = u.tls;
+    d["error"] = u.error;
     return d;
   });
+  // Configuration-time check shared by both entry points: "" = usable push config, else the reason.
+  m.def(
+      "check_push_config",
+      [](const std::string& url, const std::string& token, const std::string& ca_file, bool insecure,
+         const std::string& client_cert, const std::string& client_key) {
+        TlsOptions t;
+        t.ca_file = ca_file;
+        t.insecure = insecure;
+        t.client_cert = client_cert;
+        t.client_key = client_key;
+        return check_push_config(url, token, t);
+      },
+      py::arg("url"), py::arg("token") = "", py::arg("ca_file") = "", py::arg("insecure") = false,
+      py::arg("client_cert") = "", py::arg("client_key") = "");
   m.def("redact_url", &redact_url);
+  m.def("parse_listen", [](const std::string& l) {
+    std::string host, err;
+    int port = -1;
+    const bool ok = parse_listen(l, &host, &port, &err);
+    return py::make_tuple(ok, host, port, err);
+  });
   m.def(
       "http_request",
       [](const std::string& method, const std::string& url, const std::string& body,
-         const std::string& headers, double timeout_s) {
+         const std::string& headers, double timeout_s, const std::string& ca_file, bool insecure, int repeat) {
         HttpClient c(timeout_s);
         std::string resp, err;
-        int st;
+        int st = -1;
         {
           py::gil_scoped_release nogil;
-          st = c.request(method, parse_url(url), body, headers, &resp, &err);
+          const Url u = parse_url(url);
+          if (!u.ok) {
+            err = u.error;
+          } else {
+            if (u.tls) {
+              TlsOptions t;
+              t.ca_file = ca_file;
+              t.insecure = insecure;
+              auto ctx = TlsContext::create(t, &err);
+              if (ctx) c.set_tls(std::move(ctx));
+            }
+            // `repeat` requests over the one client (keep-alive reuse); the last result is returned
+            if (err.empty())
+              for (int i = 0; i < std::max(1, repeat); ++i) st = c.request(method, u, body, headers, &resp, &err);
+          }
         }
         return py::make_tuple(st, py::bytes(resp), err);
       },
       py::arg("method"), py::arg("url"), py::arg("body") = "", py::arg("headers") = "",
-      py::arg("timeout_s") = 5.0);
+      py::arg("timeout_s") = 5.0, py::arg("ca_file") = "", py::arg("insecure") = false, py::arg("repeat") = 1);
 
   // xGMI link-metrics entry -> gpu_metrics slot pairing (xgmi_map.h), for direct unit tests.
   py::class_<XgmiSlotMap>(m, "XgmiSlotMap")
@@ -812,9 +852,11 @@ PYBIND11_MODULE(_core, m) {
       .def("metrics_gzip",
            [](Exporter& e) {
              auto s = e.snapshot();
-             return py::bytes(s ? s->body_gz : std::string());
+             const std::string* g = s ? s->gzipped(true) : nullptr;
+             return py::bytes(g ? *g : std::string());
            })
       .def("influx_text", &Exporter::render_influx_now)
+      .def_property_readonly("listen_desc", &Exporter::listen_desc)
       .def("statics",
            [](Exporter& e) {
              py::list l;
@@ -878,6 +920,11 @@ PYBIND11_MODULE(_core, m) {
              d["influx_ok"] = s.influx_ok;
              d["influx_fail"] = s.influx_fail;
              d["influx_dropped"] = s.influx_dropped;
+             d["influx_enabled"] = s.influx_enabled;
+             d["influx_up"] = s.influx_up;
+             d["gzip_eager"] = s.gzip_eager;
+             d["gzip_lazy"] = s.gzip_lazy;
+             d["gzip_unused"] = s.gzip_unused;
              d["device_errors"] = s.device_errors;
              d["device_timeouts"] = s.device_timeouts;
              d["sample_count"] = s.sample_hist.count;

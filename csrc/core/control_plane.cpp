@@ -77,7 +77,7 @@ bool Exporter::podres_poll_once() {
   std::vector<DeviceStatic> st;
   {
     std::lock_guard<std::mutex> g(state_mu_);
-    st = statics_;
+    st = *statics_;
   }
   size_t unknown = 0;
   if (ok) {
@@ -263,7 +263,7 @@ bool Exporter::docker_poll_once() {
     std::vector<DeviceStatic> st;
     {
       std::lock_guard<std::mutex> g(state_mu_);
-      st = statics_;
+      st = *statics_;
     }
     std::unordered_map<std::string, DockerInspect> seen;
     std::unordered_map<std::string, std::vector<int>> gpus;
@@ -352,7 +352,7 @@ bool Exporter::files_poll_once() {
     std::vector<DeviceStatic> st;
     {
       std::lock_guard<std::mutex> g(state_mu_);
-      st = statics_;
+      st = *statics_;
     }
     std::unordered_map<std::string, const ContainerMeta*> by_uid_ctr;
     std::unordered_map<std::string, const ContainerMeta*> by_uid;

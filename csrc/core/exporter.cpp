@@ -1,4 +1,5 @@
 #include "exporter.h"
+#include "tls.h"
 
 #include <pthread.h>
 #include <sched.h>
@@ -588,16 +589,19 @@ bool Exporter::ensure_backend() {
   std::vector<DeviceStatic> st;
   for (int i = 0; i < backend_->device_count(); ++i) st.push_back(backend_->static_info(i));
   {
+    auto fresh = std::make_shared<TickState>();
+    fresh->samples.assign(st.size(), DeviceSample{});
+    fresh->rates.assign(st.size(), DeviceRates{});
+    fresh->proc_counts.assign(st.size(), 0);
+    fresh->procs.assign(st.size(), {});
     std::lock_guard<std::mutex> g(state_mu_);
-    statics_ = st;
-    prev_.assign(st.size(), DeviceSample{});
+    statics_ = std::make_shared<const std::vector<DeviceStatic>>(st);
+    state_ = std::move(fresh);
     last_ok_.clear();  // a re-initialised backend may number its devices differently
+    last_procs_.clear();
     xgmi_maps_.assign(st.size(), XgmiSlotMap{});
-    cur_.assign(st.size(), DeviceSample{});
-    rates_.assign(st.size(), DeviceRates{});
     dev_errors_.assign(st.size(), 0);
     dev_timeouts_.assign(st.size(), 0);
-    proc_counts_.assign(st.size(), 0);
   }
   // One worker per GPU (parallel + watchdog) unless sequential sampling was asked for
   // (sample_threads 0) or the watchdog is disabled (device_timeout_s <= 0).
@@ -610,6 +614,14 @@ bool Exporter::ensure_backend() {
 
 bool Exporter::start(std::string* err) {
   if (running_) return true;
+  // An Influx push the exporter cannot perform is a configuration error, reported before anything
+  // starts: the reference's requests.post took any http(s) URL (gpu.py:20,145), so an https:// or
+  // mistyped INFLUXDB_URL must not leave a running exporter that silently never pushes.
+  const std::string perr = check_push_config(cfg_.influx_url, cfg_.influx_token, influx_tls());
+  if (!perr.empty()) {
+    if (err) *err = perr;
+    return false;
+  }
   const char* rx = getenv("GPUMON_ROCTX");
   if (cfg_.roctx || (rx && *rx && strcmp(rx, "0") != 0)) {
     if (!Roctx::enable(true)) GPUMON_LOG(LogLevel::kWarn, "exporter", "roctx requested but librocprofiler-sdk-roctx not found");
@@ -1082,18 +1094,17 @@ TickInfo Exporter::tick() {
   TickInfo info;
   int64_t t0 = mono_ns();
   if (const int64_t dl = tick_deadline_ns_.load(); dl > 0) info.t_late = std::max<int64_t>(0, t0 - dl) * 1e-9;
-  std::vector<DeviceSample> cur;
-  std::vector<DeviceRates> rates;
-  std::vector<std::vector<ProcSample>> procs;
-  std::vector<PodRow> rows;
-  std::vector<DeviceStatic> statics;
-  std::vector<size_t> proc_counts;
+  // this tick's results are built in place in the state it publishes (no copy in or out)
+  auto next = std::make_shared<TickState>();
+  std::vector<DeviceSample>& cur = next->samples;
+  std::vector<DeviceRates>& rates = next->rates;
+  std::vector<std::vector<ProcSample>>& procs = next->procs;
+  std::vector<PodRow>& rows = next->rows;
+  std::vector<size_t>& proc_counts = next->proc_counts;
+  std::shared_ptr<const std::vector<DeviceStatic>> statics;
   bool up = ensure_backend();
   if (up) {
-    {
-      std::lock_guard<std::mutex> g(state_mu_);
-      statics = statics_;
-    }
+    statics = statics_ptr();
     int64_t ta = mono_ns();
     {
       TraceRange tr("gpumon.sample");
@@ -1103,22 +1114,23 @@ TickInfo Exporter::tick() {
     info.t_sample = (mono_ns() - ta) * 1e-9;
     rates.resize(n);
     proc_counts.assign(n, 0);
-    std::vector<DeviceSample> prev;
-    std::vector<DeviceRates> prev_rates;
-    {
-      std::lock_guard<std::mutex> g(state_mu_);
-      prev = cur_;  // the previous tick's samples
-      prev_rates = rates_;
-    }
+    // the previous tick's samples and rates, by reference into its published state
+    const std::shared_ptr<const TickState> prev_state = state_ptr();
+    const std::vector<DeviceRates>& prev_rates = prev_state->rates;
+    std::vector<const DeviceSample*> prev(std::min<size_t>(n, prev_state->samples.size()));
+    for (size_t i = 0; i < prev.size(); ++i) prev[i] = &prev_state->samples[i];
     // A device whose previous tick failed is compared with its last good sample instead (if it is
     // recent): its interval rates then span the gap -- the accumulators make that exact -- rather
     // than going missing for the tick after every transient failure, and link identity and RAS
     // carry over the failed tick.
-    if (static_cast<int>(last_ok_.size()) != n) last_ok_.assign(n, DeviceSample{});
+    if (static_cast<int>(last_ok_.size()) != n) last_ok_.assign(n, nullptr);
     const int64_t gap_ns = static_cast<int64_t>(std::max(5.0 * cfg_.interval_s, 5.0) * 1e9);
-    for (int i = 0; i < n && i < static_cast<int>(prev.size()); ++i)
-      if (!prev[i].ok && last_ok_[i].ok && cur[i].host_mono_ns - last_ok_[i].host_mono_ns <= gap_ns)
-        prev[i] = last_ok_[i];
+    for (int i = 0; i < static_cast<int>(prev.size()); ++i)
+      if (!prev[i]->ok && last_ok_[i] && i < static_cast<int>(last_ok_[i]->samples.size())) {
+        const DeviceSample& lo = last_ok_[i]->samples[i];
+        if (lo.ok && cur[i].host_mono_ns - lo.host_mono_ns <= gap_ns) prev[i] = &lo;
+      }
+    std::vector<char> ok_now(n, 0), procs_good(n, 0);
     for (int i = 0; i < n; ++i) {
       DeviceSample& s = cur[i];
       // A link refresh counts only if the device answered AND the link-metrics read succeeded: a
@@ -1135,7 +1147,7 @@ TickInfo Exporter::tick() {
         xgmi_maps_[i].apply(s.link_entries, &s);
       }
       if (i < static_cast<int>(prev.size())) {
-        const DeviceSample& p = prev[i];
+        const DeviceSample& p = *prev[i];
         // keep link identity (peer bdf, max bw) between link refreshes -- but not on a tick that
         // re-read the links: an empty peer / unknown bandwidth then means the link lost them
         if (!refreshed)
@@ -1170,7 +1182,7 @@ TickInfo Exporter::tick() {
           s.links[k].max_bandwidth_gbps = lane * width;
       if (static_cast<int>(last_fresh_ns_.size()) != n) last_fresh_ns_.assign(n, 0);
       if (i < static_cast<int>(prev.size())) {
-        const DeviceSample& p = prev[i];
+        const DeviceSample& p = *prev[i];
         if (s.ok && p.ok && s.acc.firmware_ts && s.acc.firmware_ts == p.acc.firmware_ts) {
           s.fresh = false;
           stale_++;
@@ -1199,23 +1211,24 @@ TickInfo Exporter::tick() {
       }
       if (s.ok) {
         info.devices_ok++;
-        last_ok_[i] = s;
+        ok_now[i] = 1;  // last_ok_[i] = this tick's state once it exists (below)
       }
       // A failed process list (a transient library or KFD error) keeps the last good list for up
       // to kProcHoldTicks ticks instead of publishing "no processes": every pod row of the GPU and
       // its sharing state would otherwise drop out for that tick. A device that never listed
       // successfully, or that cannot list at all, holds nothing.
       if (static_cast<int>(last_procs_.size()) != n) {
-        last_procs_.assign(n, {});
+        last_procs_.assign(n, nullptr);
         proc_hold_.assign(n, -1);
       }
       if (s.procs_read > 0) {
-        last_procs_[i] = procs[i];
+        procs_good[i] = 1;  // last_procs_[i] = this tick's state (below)
         proc_hold_[i] = 0;
       } else if (s.procs_read < 0) {
         proc_failures_++;
-        if (proc_hold_[i] >= 0 && proc_hold_[i] < kProcHoldTicks) {
-          procs[i] = last_procs_[i];
+        if (proc_hold_[i] >= 0 && proc_hold_[i] < kProcHoldTicks && last_procs_[i] &&
+            i < static_cast<int>(last_procs_[i]->procs.size())) {
+          procs[i] = last_procs_[i]->procs[i];
           proc_hold_[i]++;
           s.procs_held = true;
         }
@@ -1279,6 +1292,10 @@ TickInfo Exporter::tick() {
                         "gauge", i, {}, cur[i].procs_held ? 1.0 : 0.0});
       set_extra("procs_held", std::move(ph));
     }
+    for (int i = 0; i < n; ++i) {
+      if (ok_now[i]) last_ok_[i] = next;
+      if (procs_good[i]) last_procs_[i] = next;
+    }
     int64_t tb = mono_ns();
     {
       TraceRange tr("gpumon.attrib");
@@ -1315,7 +1332,7 @@ TickInfo Exporter::tick() {
   in.host = cfg_.host;
   static const std::vector<DeviceStatic> kNoStatics;
   static const std::vector<DeviceSample> kNoSamples;
-  in.statics = up ? &statics : &kNoStatics;
+  in.statics = up ? statics.get() : &kNoStatics;
   in.samples = up ? &cur : &kNoSamples;
   in.rates = &rates;
   in.pod_rows = &rows;
@@ -1328,6 +1345,7 @@ TickInfo Exporter::tick() {
   in.metrics_include = &cfg_.metrics_include;
   in.metrics_exclude = &cfg_.metrics_exclude;
   auto snap = std::make_shared<Snapshot>();
+  snap->gzip = cfg_.gzip;
   snap->body.reserve(std::max<size_t>(64 * 1024, last_body_bytes_ + last_body_bytes_ / 8));  // 8 GPUs: ~130 KB
   int64_t tr = mono_ns();
   {
@@ -1341,15 +1359,10 @@ TickInfo Exporter::tick() {
       ticks_.load() % static_cast<uint64_t>(cfg_.influx_every) == 0) {
     render_influx(in, snap->wall_ns, cfg_.influx_extended, &influx, cfg_.influx_schema);
   }
-  {
+  if (up) {
+    std::shared_ptr<const TickState> published = next;
     std::lock_guard<std::mutex> g(state_mu_);
-    if (up) {
-      prev_.swap(cur_);
-      cur_ = cur;
-      rates_ = rates;
-      rows_ = rows;
-      proc_counts_ = proc_counts;
-    }
+    state_.swap(published);  // the old state is released outside the lock (its last owner may be here)
   }
   info.pod_rows = rows.size();
   info.body_bytes = snap->body.size();
@@ -1360,19 +1373,25 @@ TickInfo Exporter::tick() {
   // publish the same snapshot with the compressed body: compression (0.1-0.4 ms for 1-8 GPUs at
   // level 1) is off the sample-to-export path. A gzip scrape in between gets the identity body,
   // which HTTP allows. wait_for_seq() / tick() return only after both.
-  std::shared_ptr<const Snapshot> plain = snap;
-  store_.publish(plain);
+  std::shared_ptr<const Snapshot> published_snap = snap;
+  std::shared_ptr<const Snapshot> prev_snap = store_.get();
+  store_.publish(published_snap);
   ticks_++;
   last_tick_wall_ns_ = wall_ns();
   last_tick_mono_ns_ = mono_ns();
   info.duration_s = (mono_ns() - t0) * 1e-9;
   if (cfg_.gzip) {
-    const int64_t tz = mono_ns();
-    TraceRange trz("gpumon.gzip");
-    auto gz = std::make_shared<Snapshot>(*plain);
-    gzip_compress(gz->body, &gz->body_gz, 1);
-    store_.publish(std::move(gz));
-    info.t_gzip = (mono_ns() - tz) * 1e-9;
+    // Eager compression only while scrapes keep asking for gzip (4 of the last 8 snapshots); a
+    // slower scraper's first gzip request compresses its snapshot itself (Snapshot::gzipped).
+    gz_history_ = static_cast<uint8_t>((gz_history_ << 1) | (prev_snap && prev_snap->gzip_asked() ? 1 : 0));
+    if (__builtin_popcount(gz_history_) >= 4) {
+      const int64_t tz = mono_ns();
+      TraceRange trz("gpumon.gzip");
+      snap->precompress();
+      info.t_gzip = (mono_ns() - tz) * 1e-9;
+      gz_eager_++;
+    }
+    if (prev_snap && prev_snap->compressed() && !prev_snap->gzip_asked()) gz_unused_++;
   }
   phase_ns_[0] += static_cast<uint64_t>(info.t_sample * 1e9);
   phase_ns_[1] += static_cast<uint64_t>(info.t_procs * 1e9);
@@ -1405,7 +1424,6 @@ TickInfo Exporter::tick() {
   }
   if (!influx.empty()) {
     std::lock_guard<std::mutex> g(push_mu_);
-    last_influx_ = influx;
     if (push_q_.size() >= 60) {
       push_q_.pop_front();
       influx_dropped_++;
@@ -1428,16 +1446,29 @@ bool Exporter::wait_for_seq(uint64_t want, double timeout_s) {
   return seq_.load() >= want;
 }
 
+TlsOptions Exporter::influx_tls() const {
+  TlsOptions t;
+  t.ca_file = cfg_.influx_ca_file;
+  t.insecure = cfg_.influx_tls_insecure;
+  t.client_cert = cfg_.influx_client_cert;
+  t.client_key = cfg_.influx_client_key;
+  return t;
+}
+
 void Exporter::influx_loop() {
-  Url u = parse_url(cfg_.influx_url);
-  if (!u.ok) {
-    GPUMON_LOG(LogLevel::kError, "influx", "unsupported INFLUXDB_URL " + redact_url(cfg_.influx_url));
-    return;
-  }
+  // URL, token and TLS settings were checked by start() (check_push_config)
+  const Url u = parse_url(cfg_.influx_url);
   HttpClient client(cfg_.influx_timeout_s);
-  if (cfg_.influx_token.find_first_of("\r\n") != std::string::npos) {  // would inject headers
-    GPUMON_LOG(LogLevel::kError, "influx", "influx_token contains a line break: push disabled");
-    return;
+  if (u.tls) {
+    std::string terr;
+    auto ctx = TlsContext::create(influx_tls(), &terr);
+    if (!ctx) {  // checked at start: only a CA file removed since then lands here
+      GPUMON_LOG(LogLevel::kError, "influx", "push disabled: " + terr);
+      return;
+    }
+    if (cfg_.influx_tls_insecure)
+      GPUMON_LOG(LogLevel::kWarn, "influx", "influx_tls_insecure: the server's certificate is NOT verified");
+    client.set_tls(std::move(ctx));
   }
   const std::string headers = "Content-Type: text/plain; charset=utf-8\r\n" +
                               (!cfg_.influx_token.empty() ? "Authorization: Token " + cfg_.influx_token + "\r\n"
@@ -1468,10 +1499,13 @@ void Exporter::influx_loop() {
     int st = client.request("POST", u, body, headers, &resp, &err);
     if (st >= 200 && st < 300) {
       influx_ok_++;
+      influx_up_ = 1;
+      influx_last_ok_wall_ns_ = wall_ns();
       backoff_ns = 0;
       continue;
     }
     influx_fail_++;
+    influx_up_ = 0;
     const bool transient = st < 0 || st >= 500 || st == 429;
     if (transient) {
       std::lock_guard<std::mutex> g(push_mu_);
@@ -1613,10 +1647,13 @@ void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
       resp->owner = f;
       return;
     }
-    if (req.accept_gzip && !s->body_gz.empty()) {
+    const bool fresh_gz = req.accept_gzip && s->gzip && !s->compressed();
+    const std::string* gz = req.accept_gzip ? s->gzipped(true) : nullptr;
+    if (fresh_gz && gz) gz_lazy_.fetch_add(1, std::memory_order_relaxed);
+    if (gz) {
       resp->extra_headers = "Content-Encoding: gzip\r\n";
-      resp->data = s->body_gz.data();
-      resp->len = s->body_gz.size();
+      resp->data = gz->data();
+      resp->len = gz->size();
     } else {
       resp->data = s->body.data();
       resp->len = s->body.size();
@@ -1654,46 +1691,27 @@ void Exporter::set_extra(const std::string& source, std::vector<ExtraSeries> ser
   else extras_[source] = std::move(series);
 }
 
-std::vector<DeviceStatic> Exporter::statics() const {
-  std::lock_guard<std::mutex> g(state_mu_);
-  return statics_;
-}
-std::vector<DeviceSample> Exporter::samples() const {
-  std::lock_guard<std::mutex> g(state_mu_);
-  return cur_;
-}
+std::vector<DeviceStatic> Exporter::statics() const { return *statics_ptr(); }
+std::vector<DeviceSample> Exporter::samples() const { return state_ptr()->samples; }
 std::vector<int> Exporter::xcd_counts() const {
-  std::lock_guard<std::mutex> g(state_mu_);
+  const auto st = state_ptr();
   std::vector<int> out;
-  out.reserve(cur_.size());
-  for (const auto& s : cur_) out.push_back(s.n_xcd);
+  out.reserve(st->samples.size());
+  for (const auto& s : st->samples) out.push_back(s.n_xcd);
   return out;
 }
 
-std::vector<DeviceRates> Exporter::rates() const {
-  std::lock_guard<std::mutex> g(state_mu_);
-  return rates_;
-}
-std::vector<PodRow> Exporter::pod_rows() const {
-  std::lock_guard<std::mutex> g(state_mu_);
-  return rows_;
-}
+std::vector<DeviceRates> Exporter::rates() const { return state_ptr()->rates; }
+std::vector<PodRow> Exporter::pod_rows() const { return state_ptr()->rows; }
 
 std::string Exporter::render_influx_now() {
-  std::vector<DeviceStatic> st;
-  std::vector<DeviceSample> sm;
-  std::vector<PodRow> rows;
-  {
-    std::lock_guard<std::mutex> g(state_mu_);
-    st = statics_;
-    sm = cur_;
-    rows = rows_;
-  }
+  const auto st = statics_ptr();
+  const auto state = state_ptr();
   RenderInput in;
   in.host = cfg_.host;
-  in.statics = &st;
-  in.samples = &sm;
-  in.pod_rows = &rows;
+  in.statics = st.get();
+  in.samples = &state->samples;
+  in.pod_rows = &state->rows;
   std::string out;
   render_influx(in, wall_ns(), cfg_.influx_extended, &out, cfg_.influx_schema);
   return out;
@@ -1773,6 +1791,12 @@ SelfStats Exporter::self_stats() const {
   s.influx_ok = influx_ok_;
   s.influx_fail = influx_fail_;
   s.influx_dropped = influx_dropped_;
+  s.influx_enabled = !cfg_.influx_url.empty();
+  s.influx_up = influx_up_.load();
+  s.influx_last_ok_wall_ns = influx_last_ok_wall_ns_.load();
+  s.gzip_eager = gz_eager_.load(std::memory_order_relaxed);
+  s.gzip_lazy = gz_lazy_.load(std::memory_order_relaxed);
+  s.gzip_unused = gz_unused_.load(std::memory_order_relaxed);
   if (backend_)
     for (const auto& c : backend_->call_stats()) s.backend_calls.push_back({c.call, c.n, c.errors, c.seconds});
   {
@@ -1793,7 +1817,7 @@ SelfStats Exporter::self_stats() const {
     std::lock_guard<std::mutex> g(state_mu_);
     s.device_errors = dev_errors_;
     s.device_timeouts = dev_timeouts_;
-    s.pods_attributed = rows_.size();
+    s.pods_attributed = state_->rows.size();
   }
   return s;
 }

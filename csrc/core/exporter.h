@@ -28,6 +28,7 @@
 #include "rates.h"
 #include "render.h"
 #include "snapshot.h"
+#include "tls.h"
 #include "xgmi_map.h"
 
 namespace gpumon {
@@ -91,6 +92,10 @@ struct ExporterConfig {
   // InfluxDB 2.x / 3.x token ("Authorization: Token ..."); 1.x credentials go in the URL
   // (user:password@host) and become Basic auth. Set it from a Secret (INFLUXDB_TOKEN).
   std::string influx_token;
+  // https:// push: CA bundle replacing the system one, mutual-TLS client chain / key, and an
+  // explicit opt-out of certificate and host-name verification (default: verify)
+  std::string influx_ca_file, influx_client_cert, influx_client_key;
+  bool influx_tls_insecure = false;
   double init_retry_s = 5.0;
   double health_stale_s = 0;          // 0 = max(3*interval, 10 s)
   int reinit_after = 5;               // consecutive all-devices-failed ticks before re-initialising
@@ -146,6 +151,7 @@ class Exporter {
   bool wait_for_seq(uint64_t seq, double timeout_s);  // until a snapshot with seq >= `seq`
 
   int port() const { return server_ ? server_->port() : -1; }
+  std::string listen_desc() const { return server_ ? server_->bound() : std::string("(no http)"); }
   std::shared_ptr<const Snapshot> snapshot() const { return store_.get(); }
   std::string render_influx_now();    // line protocol of the latest tick (tests / CLI)
   bool healthy() const;
@@ -182,6 +188,7 @@ class Exporter {
  private:
   void sampler_loop();
   void influx_loop();
+  TlsOptions influx_tls() const;
   void podres_loop();
   bool podres_poll_once();
   bool cri_poll_once();
@@ -222,14 +229,29 @@ class Exporter {
   size_t tick_log_next_ = 0;
   Histogram scrape_hist_;
 
-  mutable std::mutex state_mu_;       // guards the "latest" introspection copies below
-  std::vector<DeviceStatic> statics_;
-  std::vector<DeviceSample> prev_, cur_;
-  std::vector<DeviceRates> rates_;
-  std::vector<PodRow> rows_;
-  std::vector<size_t> proc_counts_;
+  // One tick's results, immutable once published: rendered from in place, handed to the next tick
+  // as its "previous", read by the introspection calls. Published by pointer swap, so a tick copies
+  // no per-device sample, rate, row or process vector (ADVICE / VERDICT r4: the 8-GPU tick copied
+  // them all in and out under state_mu_).
+  struct TickState {
+    std::vector<DeviceSample> samples;
+    std::vector<DeviceRates> rates;
+    std::vector<PodRow> rows;
+    std::vector<size_t> proc_counts;
+    std::vector<std::vector<ProcSample>> procs;  // per device, after a failed list's hold
+  };
+  mutable std::mutex state_mu_;       // guards the published pointers below
+  std::shared_ptr<const std::vector<DeviceStatic>> statics_ = std::make_shared<const std::vector<DeviceStatic>>();
+  std::shared_ptr<const TickState> state_ = std::make_shared<const TickState>();
+  std::shared_ptr<const std::vector<DeviceStatic>> statics_ptr() const {
+    std::lock_guard<std::mutex> g(state_mu_);
+    return statics_;
+  }
+  std::shared_ptr<const TickState> state_ptr() const {
+    std::lock_guard<std::mutex> g(state_mu_);
+    return state_;
+  }
   std::vector<uint64_t> dev_errors_;
-  std::string last_influx_;
 
   std::mutex tick_mu_;                // serialises ticks
   std::mutex extra_mu_;
@@ -268,11 +290,16 @@ class Exporter {
   std::atomic<uint64_t> ticks_{0}, samples_{0}, stale_{0}, overruns_{0};
   std::atomic<uint64_t> proc_failures_{0};  // failed process lists of devices that can list
   static constexpr int kProcHoldTicks = 3;  // ticks a failed process list keeps the last good one
-  std::vector<std::vector<ProcSample>> last_procs_;  // per device: the last good process list
+  // per device: the tick holding the last good process list (its procs[i]) (tick_mu_)
+  std::vector<std::shared_ptr<const TickState>> last_procs_;
   std::vector<int> proc_hold_;                       // per device: ticks held so far (-1: none good yet)
   std::atomic<uint64_t> frozen_{0};      // samples whose repeated table was older than stale_hold_s
   std::vector<int64_t> last_fresh_ns_;   // per device: host time the firmware table last advanced (tick_mu_)
-  std::vector<DeviceSample> last_ok_;    // per device: the last sample that succeeded (tick_mu_)
+  // per device: the tick whose samples[i] is the device's last successful sample (tick_mu_)
+  std::vector<std::shared_ptr<const TickState>> last_ok_;
+  uint8_t gz_history_ = 0;  // bit k: the snapshot k ticks back was scraped with gzip (tick thread)
+  // snapshot compressions: eager (tick thread), lazy (by a scrape), and eager ones nobody fetched
+  std::atomic<uint64_t> gz_eager_{0}, gz_lazy_{0}, gz_unused_{0};
   size_t last_body_bytes_ = 0;  // tick thread only: sizes the next render buffer
   std::atomic<uint64_t> phase_ns_[5] = {};  // sample, procs, attrib, render, gzip (cumulative)
 
@@ -313,6 +340,8 @@ class Exporter {
   std::condition_variable push_cv_;
   std::deque<std::string> push_q_;
   std::atomic<uint64_t> influx_ok_{0}, influx_fail_{0}, influx_dropped_{0};
+  std::atomic<int> influx_up_{0};                 // the last push attempt succeeded
+  std::atomic<int64_t> influx_last_ok_wall_ns_{0};
 
   // per-device sampling workers + watchdog (exporter.cpp)
   void start_workers(int n);

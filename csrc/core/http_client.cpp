@@ -14,6 +14,7 @@
 #include <thread>
 
 #include "common.h"
+#include "tls.h"
 
 namespace gpumon {
 
@@ -61,13 +62,30 @@ std::string pct_decode(const std::string& s) {
 
 Url parse_url(const std::string& url) {
   Url u;
+  auto bad = [&](const std::string& why) {
+    u.ok = false;
+    u.error = why;
+    return u;
+  };
   std::string s = url;
-  if (starts_with(s, "http://")) s = s.substr(7);
-  else if (s.find("://") != std::string::npos) return u;  // https etc. unsupported
-  size_t slash = s.find_first_of("/?");
+  if (starts_with(s, "http://")) {
+    s = s.substr(7);
+  } else if (starts_with(s, "https://")) {
+    s = s.substr(8);
+    u.tls = true;
+    u.port = 443;
+  } else {
+    const size_t sc = s.find("://");
+    return bad(sc == std::string::npos ? "no http:// or https:// scheme"
+                                       : "unsupported scheme '" + s.substr(0, sc) + "' (http or https)");
+  }
+  size_t slash = s.find_first_of("/?#");
   std::string hp = slash == std::string::npos ? s : s.substr(0, slash);
   u.path = slash == std::string::npos ? "/" : s.substr(slash);
-  if (u.path[0] == '?') u.path = "/" + u.path;
+  const size_t frag = u.path.find('#');  // never sent (RFC 9110 4.2.4)
+  if (frag != std::string::npos) u.path.resize(frag);
+  if (u.path.empty() || u.path[0] != '/') u.path = "/" + u.path;
+  if (u.path.find_first_of(" \r\n\t") != std::string::npos) return bad("whitespace in the path");
   const size_t at = hp.rfind('@');
   if (at != std::string::npos) {
     u.auth_header = "Authorization: Basic " + base64_encode(pct_decode(hp.substr(0, at))) + "\r\n";
@@ -76,23 +94,36 @@ Url parse_url(const std::string& url) {
   std::string port;
   if (!hp.empty() && hp[0] == '[') {  // [v6]:port
     const size_t rb = hp.find(']');
-    if (rb == std::string::npos) return u;
+    if (rb == std::string::npos) return bad("unterminated [IPv6] literal");
     u.host = hp.substr(1, rb - 1);
     if (rb + 1 < hp.size()) {
-      if (hp[rb + 1] != ':') return u;
+      if (hp[rb + 1] != ':') return bad("junk after the [IPv6] literal");
       port = hp.substr(rb + 2);
+      if (port.empty()) return bad("empty port");
     }
   } else {
     const size_t colon = hp.rfind(':');
     u.host = colon == std::string::npos ? hp : hp.substr(0, colon);
-    if (colon != std::string::npos) port = hp.substr(colon + 1);
+    if (colon != std::string::npos) {
+      port = hp.substr(colon + 1);
+      if (port.empty()) return bad("empty port");
+    }
+    if (u.host.find(':') != std::string::npos) return bad("an IPv6 host needs brackets ([v6]:port)");
   }
+  if (u.host.empty()) return bad("no host");
+  if (u.host.find_first_of(" \r\n\t/") != std::string::npos) return bad("bad character in the host");
   if (!port.empty()) {
-    if (port.find_first_not_of("0123456789") != std::string::npos || port.size() > 5) return u;
+    if (port.find_first_not_of("0123456789") != std::string::npos || port.size() > 5) return bad("bad port '" + port + "'");
     u.port = atoi(port.c_str());
   }
-  u.ok = !u.host.empty() && u.port > 0 && u.port < 65536;
+  if (u.port <= 0 || u.port >= 65536) return bad("port out of range");
+  u.ok = true;
   return u;
+}
+
+std::string host_port(const std::string& host, int port) {
+  const bool v6 = host.find(':') != std::string::npos;
+  return (v6 ? "[" + host + "]" : host) + ":" + std::to_string(port);
 }
 
 std::string redact_url(const std::string& url) {
@@ -106,15 +137,43 @@ std::string redact_url(const std::string& url) {
   return url.substr(0, colon + 1) + "***" + url.substr(at);
 }
 
+HttpClient::HttpClient(double timeout_s) : timeout_s_(timeout_s) {}
+
 HttpClient::~HttpClient() { close_conn(); }
 
 void HttpClient::close_conn() {
+  if (tls_) tls_->shutdown();
+  tls_.reset();
   if (fd_ >= 0) close(fd_);
   fd_ = -1;
 }
 
+bool HttpClient::send_all(const char* p, size_t n, std::string* err) {
+  if (tls_) return tls_->write_all(p, n, err);
+  while (n) {
+    ssize_t w = send(fd_, p, n, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      *err = std::string("send: ") + strerror(errno);
+      return false;
+    }
+    p += w;
+    n -= static_cast<size_t>(w);
+  }
+  return true;
+}
+
+long HttpClient::recv_some(char* buf, size_t n, std::string* err) {
+  if (tls_) return tls_->read_some(buf, n, err);
+  ssize_t r;
+  do r = recv(fd_, buf, n, 0);
+  while (r < 0 && errno == EINTR);
+  if (r < 0) *err = errno == EAGAIN || errno == EWOULDBLOCK ? "timed out" : std::string("recv: ") + strerror(errno);
+  return r;
+}
+
 bool HttpClient::connect_to(const Url& u, std::string* err) {
-  if (fd_ >= 0 && u.host == cur_host_ && u.port == cur_port_) return true;
+  if (fd_ >= 0 && u.host == cur_host_ && u.port == cur_port_ && u.tls == cur_tls_) return true;
   close_conn();
   addrinfo hints{}, *res = nullptr;
   hints.ai_family = AF_UNSPEC;
@@ -143,11 +202,27 @@ bool HttpClient::connect_to(const Url& u, std::string* err) {
   }
   freeaddrinfo(res);
   if (fd_ < 0) {
-    *err = "connect " + u.host + ":" + port + ": " + strerror(errno);
+    *err = "connect " + host_port(u.host, u.port) + ": " + strerror(errno);
     return false;
+  }
+  if (u.tls) {
+    if (!tls_ctx_) {
+      tls_ctx_ = TlsContext::create(TlsOptions{}, err);
+      if (!tls_ctx_) {
+        close_conn();
+        return false;
+      }
+    }
+    tls_ = std::make_unique<TlsConn>(tls_ctx_);
+    if (!tls_->handshake(fd_, u.host, err)) {
+      tls_.reset();  // no close_notify after a failed handshake
+      close_conn();
+      return false;
+    }
   }
   cur_host_ = u.host;
   cur_port_ = u.port;
+  cur_tls_ = u.tls;
   return true;
 }
 
@@ -156,34 +231,22 @@ bool HttpClient::connect_to(const Url& u, std::string* err) {
 constexpr long kMaxBodyBytes = 256L << 20;
 constexpr size_t kMaxHeaderBytes = 64u << 10;
 
-static bool send_all(int fd, const char* p, size_t n) {
-  while (n) {
-    ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
-    if (w < 0) {
-      if (errno == EINTR) continue;
-      return false;
-    }
-    p += w;
-    n -= static_cast<size_t>(w);
-  }
-  return true;
-}
-
 int HttpClient::request(const std::string& method, const Url& u, const std::string& body,
                         const std::string& extra_headers, std::string* resp_body,
                         std::string* err) {
   for (int attempt = 0; attempt < 2; ++attempt) {
     bool reused = fd_ >= 0;
     if (!connect_to(u, err)) return -1;
-    std::string req = method + " " + u.path + " HTTP/1.1\r\nHost: " + u.host + ":" +
-                      std::to_string(u.port) + "\r\nConnection: keep-alive\r\n" + extra_headers;
+    std::string req = method + " " + u.path + " HTTP/1.1\r\nHost: " + host_port(u.host, u.port) +
+                      "\r\nConnection: keep-alive\r\n" + extra_headers;
     if (!body.empty() || method == "POST")
       req += "Content-Length: " + std::to_string(body.size()) + "\r\n";
     req += "\r\n";
-    if (!send_all(fd_, req.data(), req.size()) || !send_all(fd_, body.data(), body.size())) {
+    std::string serr;
+    if (!send_all(req.data(), req.size(), &serr) || !send_all(body.data(), body.size(), &serr)) {
       close_conn();
       if (reused) continue;  // stale keep-alive connection: retry once on a fresh one
-      *err = std::string("send: ") + strerror(errno);
+      *err = serr;
       return -1;
     }
     std::string in;
@@ -199,8 +262,9 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
       *err = "response timed out";
       return true;
     };
+    std::string rerr;
     while (hdr_end == std::string::npos) {
-      ssize_t r = recv(fd_, buf, sizeof buf, 0);
+      const long r = recv_some(buf, sizeof buf, &rerr);
       if (r <= 0) break;
       in.append(buf, static_cast<size_t>(r));
       hdr_end = in.find("\r\n\r\n");
@@ -214,7 +278,7 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
     if (hdr_end == std::string::npos) {
       close_conn();
       if (reused && in.empty()) continue;
-      *err = "no response header";
+      *err = "no response header" + (rerr.empty() ? std::string() : " (" + rerr + ")");
       return -1;
     }
     int status = 0;
@@ -243,10 +307,10 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
       size_t got = std::min(rb.size(), static_cast<size_t>(clen));
       rb.resize(static_cast<size_t>(clen));
       while (got < static_cast<size_t>(clen)) {
-        ssize_t r = recv(fd_, &rb[got], static_cast<size_t>(clen) - got, 0);
+        const long r = recv_some(&rb[got], static_cast<size_t>(clen) - got, &rerr);
         if (r <= 0) {
           close_conn();
-          *err = "short body";
+          *err = "short body" + (rerr.empty() ? std::string() : " (" + rerr + ")");
           return -1;
         }
         got += static_cast<size_t>(r);
@@ -255,7 +319,7 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
     } else if (status != 204 && status != 304) {
       // no length: read to EOF
       while (true) {
-        ssize_t r = recv(fd_, buf, sizeof buf, 0);
+        const long r = recv_some(buf, sizeof buf, &rerr);
         if (r <= 0) break;
         rb.append(buf, static_cast<size_t>(r));
         if (rb.size() > static_cast<size_t>(kMaxBodyBytes)) {

@@ -2,6 +2,7 @@
 
 #include <arpa/inet.h>
 #include <fcntl.h>
+#include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <pthread.h>
@@ -147,12 +148,156 @@ long parse_request(const std::string& in, HttpRequest* r) {
 
 struct HttpServer::Loop {
   int ep = -1;
-  int lfd = -1;
+  int lfd = -1;  // the server's shared listening socket (not owned)
   int wake = -1;
   std::thread th;
   std::unordered_map<int, Conn> conns;
   std::list<int> lru;  // connection fds, least recently active first: O(1) eviction at the cap
 };
+
+bool parse_listen(const std::string& listen, std::string* host, int* port, std::string* err) {
+  std::string h, p;
+  const std::string l(trim(listen));
+  if (l.empty()) {
+    *err = "empty listen address";
+    return false;
+  }
+  if (l[0] == '[') {
+    const size_t rb = l.find(']');
+    if (rb == std::string::npos || rb + 1 >= l.size() || l[rb + 1] != ':') {
+      *err = "listen '" + l + "': expected [v6]:port";
+      return false;
+    }
+    h = l.substr(1, rb - 1);
+    p = l.substr(rb + 2);
+    in6_addr a6{};
+    if (h.empty() || inet_pton(AF_INET6, h.c_str(), &a6) != 1) {
+      *err = "listen '" + l + "': '" + h + "' is not an IPv6 address";
+      return false;
+    }
+  } else if (l.find_first_not_of("0123456789") == std::string::npos) {
+    p = l;  // "9400": every address
+  } else {
+    const size_t colon = l.rfind(':');
+    if (colon == std::string::npos) {
+      *err = "listen '" + l + "': expected host:port";
+      return false;
+    }
+    h = l.substr(0, colon);
+    p = l.substr(colon + 1);
+    if (h.find(':') != std::string::npos) {
+      *err = "listen '" + l + "': an IPv6 address needs brackets ([v6]:port)";
+      return false;
+    }
+    if (h == "*") h.clear();
+  }
+  if (p.empty() || p.size() > 5 || p.find_first_not_of("0123456789") != std::string::npos || atoi(p.c_str()) > 65535) {
+    *err = "listen '" + l + "': bad port '" + p + "'";
+    return false;
+  }
+  *host = h;
+  *port = atoi(p.c_str());
+  return true;
+}
+
+namespace {
+
+// Binds the listening socket for `host` ("" = every address: dual-stack [::], else 0.0.0.0).
+// Returns the fd (listening, non-blocking) or -1 with *err; *port is updated for port 0.
+int open_listener(const std::string& host, int* port, std::string* bound, std::string* err) {
+  struct Try {
+    int family;
+    std::string addr;
+    bool v6only;
+  };
+  std::vector<Try> tries;
+  in_addr a4{};
+  in6_addr a6{};
+  if (host.empty()) {
+    tries = {{AF_INET6, "::", false}, {AF_INET, "0.0.0.0", false}};
+  } else if (host == "::") {
+    tries = {{AF_INET6, "::", false}};
+  } else if (inet_pton(AF_INET6, host.c_str(), &a6) == 1) {
+    tries = {{AF_INET6, host, true}};
+  } else if (inet_pton(AF_INET, host.c_str(), &a4) == 1) {
+    tries = {{AF_INET, host, false}};
+  } else {  // a host name: its first passive address
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_UNSPEC;
+    hints.ai_socktype = SOCK_STREAM;
+    hints.ai_flags = AI_PASSIVE;
+    const int rc = getaddrinfo(host.c_str(), nullptr, &hints, &res);
+    if (rc != 0 || !res) {
+      *err = "bad listen address " + host + ": " + gai_strerror(rc);
+      return -1;
+    }
+    char buf[INET6_ADDRSTRLEN] = {};
+    if (res->ai_family == AF_INET6)
+      inet_ntop(AF_INET6, &reinterpret_cast<sockaddr_in6*>(res->ai_addr)->sin6_addr, buf, sizeof buf);
+    else
+      inet_ntop(AF_INET, &reinterpret_cast<sockaddr_in*>(res->ai_addr)->sin_addr, buf, sizeof buf);
+    tries = {{res->ai_family, buf, res->ai_family == AF_INET6}};
+    freeaddrinfo(res);
+  }
+  std::string last;
+  for (size_t k = 0; k < tries.size(); ++k) {
+    const Try& t = tries[k];
+    const bool fallback_left = k + 1 < tries.size();
+    const int fd = socket(t.family, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (fd < 0) {
+      last = std::string("socket: ") + strerror(errno);
+      if (fallback_left && (errno == EAFNOSUPPORT || errno == EPROTONOSUPPORT)) continue;  // no IPv6 here
+      break;
+    }
+    int one = 1, v6only = t.v6only ? 1 : 0;
+    // SO_REUSEADDR: a restarted exporter rebinds over its predecessor's TIME_WAIT connections. It
+    // never lets two listeners share the port on Linux; SO_REUSEPORT (not set) would.
+    setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
+    sockaddr_storage ss{};
+    socklen_t sl;
+    if (t.family == AF_INET6) {
+      setsockopt(fd, IPPROTO_IPV6, IPV6_V6ONLY, &v6only, sizeof v6only);
+      auto* sa = reinterpret_cast<sockaddr_in6*>(&ss);
+      sa->sin6_family = AF_INET6;
+      sa->sin6_port = htons(static_cast<uint16_t>(*port));
+      inet_pton(AF_INET6, t.addr.c_str(), &sa->sin6_addr);
+      sl = sizeof(sockaddr_in6);
+    } else {
+      auto* sa = reinterpret_cast<sockaddr_in*>(&ss);
+      sa->sin_family = AF_INET;
+      sa->sin_port = htons(static_cast<uint16_t>(*port));
+      inet_pton(AF_INET, t.addr.c_str(), &sa->sin_addr);
+      sl = sizeof(sockaddr_in);
+    }
+    const std::string where = (t.family == AF_INET6 ? "[" + t.addr + "]" : t.addr) + ":" + std::to_string(*port);
+    if (bind(fd, reinterpret_cast<sockaddr*>(&ss), sl) != 0) {
+      const int e = errno;
+      last = "bind " + where + ": " + strerror(e);
+      close(fd);
+      // IPv6 present but unusable (disable_ipv6): the IPv4 wildcard; an address in use is final
+      if (fallback_left && (e == EADDRNOTAVAIL || e == EAFNOSUPPORT)) continue;
+      break;
+    }
+    if (listen(fd, 1024) != 0) {
+      last = std::string("listen: ") + strerror(errno);
+      close(fd);
+      break;
+    }
+    if (*port == 0) {
+      getsockname(fd, reinterpret_cast<sockaddr*>(&ss), &sl);
+      *port = ntohs(t.family == AF_INET6 ? reinterpret_cast<sockaddr_in6*>(&ss)->sin6_port
+                                         : reinterpret_cast<sockaddr_in*>(&ss)->sin_port);
+    }
+    set_nonblock(fd);
+    *bound = (t.family == AF_INET6 ? "[" + t.addr + "]" : t.addr) + ":" + std::to_string(*port) +
+             (t.family == AF_INET6 && !t.v6only ? " (dual-stack)" : "");
+    return fd;
+  }
+  *err = last;
+  return -1;
+}
+
+}  // namespace
 
 HttpServer::HttpServer(std::string addr, int port, int threads, Handler h, Observer obs)
     : addr_(std::move(addr)),
@@ -165,14 +310,14 @@ HttpServer::~HttpServer() { stop(); }
 
 bool HttpServer::start(std::string* err) {
   if (running_) return true;
-  auto abandon = [this](Loop* L) {  // a failed start: close what was opened, start no thread
-    if (L) close(L->lfd);
+  auto abandon = [this]() {  // a failed start: close what was opened, start no thread
     for (auto& P : loops_) {
-      close(P->lfd);
       close(P->ep);
       close(P->wake);
     }
     loops_.clear();
+    if (lfd_ >= 0) close(lfd_);
+    lfd_ = -1;
   };
   sndbuf_ = kSndBuf;
   if (const char* e = getenv("GPUMON_HTTP_SNDBUF")) sndbuf_ = std::max(0, atoi(e));
@@ -185,50 +330,27 @@ bool HttpServer::start(std::string* err) {
     const rlim_t usable = rl.rlim_cur > 2 * kFdReserve ? rl.rlim_cur - kFdReserve : rl.rlim_cur / 2;
     max_conns_ = std::clamp<size_t>(usable / static_cast<rlim_t>(std::max(1, nthreads_)), 8, kMaxConnsPerLoop);
   }
+  lfd_ = open_listener(addr_, &port_, &bound_, err);
+  if (lfd_ < 0) return false;
+  exclusive_ = true;
   for (int t = 0; t < nthreads_; ++t) {
     auto L = std::make_unique<Loop>();
-    L->lfd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
-    if (L->lfd < 0) {
-      *err = std::string("socket: ") + strerror(errno);
-      abandon(nullptr);
-      return false;
-    }
-    int one = 1;
-    setsockopt(L->lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
-    setsockopt(L->lfd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
-    sockaddr_in sa{};
-    sa.sin_family = AF_INET;
-    sa.sin_port = htons(static_cast<uint16_t>(port_));
-    if (inet_pton(AF_INET, addr_.empty() ? "0.0.0.0" : addr_.c_str(), &sa.sin_addr) != 1) {
-      *err = "bad listen address " + addr_;
-      abandon(L.get());
-      return false;
-    }
-    if (bind(L->lfd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0) {
-      *err = "bind " + addr_ + ":" + std::to_string(port_) + ": " + strerror(errno);
-      abandon(L.get());
-      return false;
-    }
-    if (port_ == 0) {
-      socklen_t sl = sizeof sa;
-      getsockname(L->lfd, reinterpret_cast<sockaddr*>(&sa), &sl);
-      port_ = ntohs(sa.sin_port);
-    }
-    if (listen(L->lfd, 1024) != 0) {
-      *err = std::string("listen: ") + strerror(errno);
-      abandon(L.get());
-      return false;
-    }
-    set_nonblock(L->lfd);
+    L->lfd = lfd_;
     L->ep = epoll_create1(EPOLL_CLOEXEC);
     L->wake = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    if (L->ep < 0 || L->wake < 0) {
+      *err = std::string("epoll / eventfd: ") + strerror(errno);
+      if (L->ep >= 0) close(L->ep);
+      if (L->wake >= 0) close(L->wake);
+      abandon();
+      return false;
+    }
     epoll_event ev{};
     ev.events = EPOLLIN;
-    ev.data.fd = L->lfd;
-    epoll_ctl(L->ep, EPOLL_CTL_ADD, L->lfd, &ev);
     ev.data.fd = L->wake;
     epoll_ctl(L->ep, EPOLL_CTL_ADD, L->wake, &ev);
     loops_.push_back(std::move(L));
+    watch_listener(loops_.back().get(), true);
   }
   running_ = true;
   for (auto& L : loops_) {
@@ -239,6 +361,22 @@ bool HttpServer::start(std::string* err) {
     });
   }
   return true;
+}
+
+bool HttpServer::watch_listener(Loop* L, bool on) {
+  if (!on) return epoll_ctl(L->ep, EPOLL_CTL_DEL, L->lfd, nullptr) == 0;
+  epoll_event ev{};
+  ev.data.fd = L->lfd;
+  // EPOLLEXCLUSIVE: a connection wakes one loop, not every loop waiting on the shared socket.
+  // EPOLL_CTL_MOD is not allowed with it, so pausing accepts (EMFILE) deletes and re-adds.
+  ev.events = EPOLLIN | (exclusive_ ? static_cast<uint32_t>(EPOLLEXCLUSIVE) : 0u);
+  if (epoll_ctl(L->ep, EPOLL_CTL_ADD, L->lfd, &ev) == 0) return true;
+  if (errno == EINVAL && exclusive_) {  // kernel < 4.5: every loop wakes, the losers see EAGAIN
+    exclusive_ = false;
+    ev.events = EPOLLIN;
+    return epoll_ctl(L->ep, EPOLL_CTL_ADD, L->lfd, &ev) == 0;
+  }
+  return errno == EEXIST;
 }
 
 void HttpServer::stop() {
@@ -253,11 +391,12 @@ void HttpServer::stop() {
     for (auto& [fd, c] : L->conns) close(fd);
     L->conns.clear();
     L->lru.clear();
-    close(L->lfd);
     close(L->ep);
     close(L->wake);
   }
   loops_.clear();
+  if (lfd_ >= 0) close(lfd_);
+  lfd_ = -1;
 }
 
 namespace {
@@ -429,7 +568,7 @@ void HttpServer::run(Loop* L) {
     closed_in_batch.clear();
     if (accept_resume_ns && now >= accept_resume_ns) {
       accept_resume_ns = 0;
-      set_events(L->lfd, EPOLLIN);
+      watch_listener(L, true);
     }
     if (rt_on) {
       if (now - win_start >= kRtWindowNs) {  // new window: back to FIFO
@@ -460,7 +599,7 @@ void HttpServer::run(Loop* L) {
                 GPUMON_LOG(LogLevel::kWarn, "http", "accept: out of file descriptors; pausing accepts for 100 ms");
               }
               accept_resume_ns = now + 100'000'000;
-              set_events(L->lfd, 0);
+              watch_listener(L, false);
             }
             break;
           }

@@ -2,8 +2,15 @@
 //
 // The reference has no server (push-only). This one is built for flat scrape latency: responses
 // reference immutable pre-rendered buffers (zero-copy writev), keep-alive and pipelining are
-// supported, gzip is pre-computed once per tick, and N event-loop threads share the port via
-// SO_REUSEPORT. No Python / GIL on this path.
+// supported, gzip is computed at most once per snapshot, and N event-loop threads share ONE
+// listening socket (EPOLLEXCLUSIVE wake-ups). There is no SO_REUSEPORT: a second exporter on the
+// same port fails with EADDRINUSE instead of silently taking a share of the scrapes. No Python /
+// GIL on this path.
+//
+// Listen addresses (parse_listen): "host:port", "[v6]:port", ":port" / "port" / "*:port" (every
+// address). Every address binds [::] with IPV6_V6ONLY=0, one dual-stack socket that takes IPv4
+// (as ::ffff:a.b.c.d) and IPv6 scrapes, and falls back to 0.0.0.0 where the kernel has no IPv6;
+// "[::]:port" is dual-stack without the fallback; "0.0.0.0:port" is IPv4 only, "[::1]:port" v6 only.
 #pragma once
 
 #include <atomic>
@@ -33,6 +40,10 @@ struct HttpResponse {
   std::string inline_body;                  // used when data == nullptr
 };
 
+// "host:port" | "[v6]:port" | ":port" | "*:port" | "port" -> host ("" = every address, dual-stack)
+// and port (0 = ephemeral). false with the reason in *err.
+bool parse_listen(const std::string& listen, std::string* host, int* port, std::string* err);
+
 class HttpServer {
  public:
   using Handler = std::function<void(const HttpRequest&, HttpResponse*)>;
@@ -55,14 +66,20 @@ class HttpServer {
   bool start(std::string* err);
   void stop();
   int port() const { return port_; }
+  // What was bound, for logs: "[::]:9400 (dual-stack)", "0.0.0.0:9400", "[::1]:9400", ...
+  const std::string& bound() const { return bound_; }
   uint64_t connections() const { return conns_.load(); }
   uint64_t requests() const { return requests_.load(); }
 
  private:
   struct Loop;
   void run(Loop* L);
+  bool watch_listener(Loop* L, bool on);  // add / remove the shared listening socket in L's epoll set
   std::string addr_;
   int port_;
+  int lfd_ = -1;         // the one listening socket, shared by the loops
+  bool exclusive_ = true;  // EPOLLEXCLUSIVE accepted by the kernel (>= 4.5)
+  std::string bound_;
   int nthreads_;
   int sndbuf_ = 0;  // SO_SNDBUF for accepted connections (0: kernel default)
   size_t max_conns_ = 4096;        // per loop: kMaxConnsPerLoop, less when RLIMIT_NOFILE is low (start())

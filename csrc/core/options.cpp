@@ -12,6 +12,7 @@
 
 #include "common.h"
 #include "http_client.h"
+#include "http_server.h"
 
 namespace gpumon {
 
@@ -259,6 +260,10 @@ const std::map<std::string, Setter>& setters() {
       {"influx_extended", bool_at([](NativeOptions* o) { return &o->cfg.influx_extended; })},
       {"influx_schema", int_at([](NativeOptions* o) { return &o->cfg.influx_schema; })},
       {"influx_every", int_at([](NativeOptions* o) { return &o->cfg.influx_every; })},
+      {"influx_ca_file", str_at([](NativeOptions* o) { return &o->cfg.influx_ca_file; })},
+      {"influx_tls_insecure", bool_at([](NativeOptions* o) { return &o->cfg.influx_tls_insecure; })},
+      {"influx_client_cert", str_at([](NativeOptions* o) { return &o->cfg.influx_client_cert; })},
+      {"influx_client_key", str_at([](NativeOptions* o) { return &o->cfg.influx_client_key; })},
       {"procfs_root", str_at([](NativeOptions* o) { return &o->cfg.attribution.procfs_root; })},
       {"opt_in_label", str_at([](NativeOptions* o) { return &o->cfg.attribution.opt_in; })},
       {"user_label", str_at([](NativeOptions* o) { return &o->cfg.attribution.user_label; })},
@@ -437,11 +442,9 @@ bool options_apply_env(NativeOptions* o, char** envp, std::string* err) {
   return true;
 }
 
-void options_finalize(NativeOptions* o) {
+bool options_finalize(NativeOptions* o, std::string* err) {
   ExporterConfig& c = o->cfg;
-  const size_t colon = o->listen.rfind(':');
-  c.listen_addr = colon == std::string::npos ? "0.0.0.0" : o->listen.substr(0, colon);
-  c.port = atoi(colon == std::string::npos ? o->listen.c_str() : o->listen.c_str() + colon + 1);
+  if (!parse_listen(o->listen, &c.listen_addr, &c.port, err)) return false;
   if (c.host.empty()) c.host = "no_name";
   if (!o->resource_names.empty()) c.pod_resources_prefix = o->resource_names[0];
   c.pod_resources_refresh_s = o->metadata_refresh_s;
@@ -464,6 +467,7 @@ void options_finalize(NativeOptions* o) {
   o->od.probe_every_s = period * std::max(1, o->probe_every);
   const std::string& l = o->log_level;
   g_log_level = l == "debug" ? 0 : l == "info" ? 1 : (l == "warn" || l == "warning") ? 2 : l == "error" ? 3 : 1;
+  return true;
 }
 
 std::string options_json(const NativeOptions& o) {
@@ -536,6 +540,10 @@ std::string options_json(const NativeOptions& o) {
   B("influx_extended", c.influx_extended);
   N("influx_schema", c.influx_schema);
   N("influx_every", c.influx_every);
+  S("influx_ca_file", c.influx_ca_file);
+  B("influx_tls_insecure", c.influx_tls_insecure);
+  S("influx_client_cert", c.influx_client_cert);
+  S("influx_client_key", c.influx_client_key);
   S("procfs_root", c.attribution.procfs_root);
   S("opt_in_label", c.attribution.opt_in);
   S("user_label", c.attribution.user_label);

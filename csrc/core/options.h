@@ -23,7 +23,7 @@ namespace gpumon {
 struct NativeOptions {
   ExporterConfig cfg;
   OnDeviceConfig od;
-  std::string listen = "0.0.0.0:9400";
+  std::string listen = ":9400";          // every address, dual-stack where the kernel has IPv6
   std::string pod_resources_socket = "/var/lib/kubelet/pod-resources/kubelet.sock";  // "" = off
   std::string cri_socket;                 // "" = autodetect, "none" = off
   int probe_every = 1;                    // probe period in sampler intervals
@@ -52,7 +52,8 @@ bool options_load_file(NativeOptions* o, const std::string& path, std::vector<st
 bool options_apply_env(NativeOptions* o, char** envp, std::string* err);
 
 // Resolves listen address, sockets and the on-device cadence into cfg / od (after all sources).
-void options_finalize(NativeOptions* o);
+// false with *err for a listen address parse_listen refuses.
+bool options_finalize(NativeOptions* o, std::string* err);
 
 // Effective configuration as one JSON object (Python field names), for --print-config.
 std::string options_json(const NativeOptions& o);

@@ -932,6 +932,32 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       }
     }
     {
+      Family f(o, "gpumon_snapshot_compressions_total",
+               "gzip compressions of the /metrics snapshot: eager (the tick thread, while most snapshots are "
+               "scraped with gzip) or lazy (by the first gzip scrape of a snapshot).", "counter");
+      if (s.gzip_eager || s.gzip_lazy) {
+        f.add(hl, {{"mode", "eager"}}, static_cast<double>(s.gzip_eager));
+        f.add(hl, {{"mode", "lazy"}}, static_cast<double>(s.gzip_lazy));
+      }
+    }
+    {
+      Family f(o, "gpumon_snapshot_compressions_unused_total",
+               "Eager snapshot compressions no scrape fetched before the next tick replaced the snapshot.",
+               "counter");
+      if (s.gzip_eager) f.add(hl, static_cast<double>(s.gzip_unused));
+    }
+    {
+      Family f(o, "gpumon_influx_up",
+               "1 if the last InfluxDB compat push succeeded, 0 if it failed or none completed yet (push configured).",
+               "gauge");
+      if (s.influx_enabled) f.add(hl, static_cast<double>(s.influx_up));
+    }
+    {
+      Family f(o, "gpumon_influx_last_success_timestamp_seconds",
+               "Unix time of the last successful InfluxDB compat push.", "gauge");
+      if (s.influx_enabled && s.influx_last_ok_wall_ns > 0) f.add(hl, s.influx_last_ok_wall_ns * 1e-9);
+    }
+    {
       Family f(o, "process_cpu_seconds_total", "Exporter user+system CPU time.", "counter");
       if (s.cpu_seconds >= 0) f.add(hl, s.cpu_seconds);
     }

@@ -97,4 +97,24 @@ bool gzip_compress(const std::string& in, std::string* out, int level) {
   return true;
 }
 
+const std::string* Snapshot::gzipped(bool compress_now) const {
+  if (!gzip) return nullptr;
+  gz_asked_.store(true, std::memory_order_relaxed);
+  if (gz_state_.load(std::memory_order_acquire) == 2) return &gz_;
+  return compress_now ? compress() : nullptr;
+}
+
+const std::string* Snapshot::compress() const {
+  if (!gzip) return nullptr;
+  int st = gz_state_.load(std::memory_order_acquire);
+  if (st == 2) return &gz_;
+  if (st != 0) return nullptr;
+  if (!gz_state_.compare_exchange_strong(st, 1, std::memory_order_acq_rel)) {
+    return st == 2 ? &gz_ : nullptr;
+  }
+  const bool ok = gzip_compress(body, &gz_, 1);
+  gz_state_.store(ok ? 2 : 3, std::memory_order_release);
+  return ok ? &gz_ : nullptr;
+}
+
 }  // namespace gpumon

@@ -17,9 +17,29 @@ namespace gpumon {
 
 struct Snapshot {
   std::string body;       // text/plain; version=0.0.4
-  std::string body_gz;    // gzip of body (empty if compression disabled)
   uint64_t seq = 0;
   int64_t wall_ns = 0;
+  bool gzip = false;      // compression enabled for this exporter
+
+  // The gzip of `body`, made at most once per snapshot: by the tick thread right after publication
+  // when recent snapshots were scraped with gzip (Prometheus scraping every tick), otherwise by the
+  // first gzip scrape of this snapshot (a 15 s scrape of a 1 Hz exporter compresses 1 tick in 15,
+  // not all of them: gzip was 2/3 of the tick thread's CPU at 8 GPUs, profiles/r5_cpu_8dev.md).
+  // nullptr = serve the identity body (compression disabled, failed, or another thread is
+  // compressing right now -- HTTP lets a server ignore Accept-Encoding).
+  const std::string* gzipped(bool compress_now) const;
+  // The tick thread's eager compression (does not count as a gzip request).
+  void precompress() const { (void)compress(); }
+  // A scrape asked this snapshot for gzip (the tick thread's eager / lazy decision).
+  bool gzip_asked() const { return gz_asked_.load(std::memory_order_relaxed); }
+  // Whether this snapshot was compressed (by either path).
+  bool compressed() const { return gz_state_.load(std::memory_order_acquire) == 2; }
+
+ private:
+  const std::string* compress() const;
+  mutable std::atomic<int> gz_state_{0};  // 0 none, 1 compressing, 2 done, 3 failed
+  mutable std::atomic<bool> gz_asked_{false};
+  mutable std::string gz_;
 };
 
 class SnapshotStore {

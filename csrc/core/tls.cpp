@@ -1,0 +1,339 @@
+#include "tls.h"
+
+#include <arpa/inet.h>
+#include <dlfcn.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "common.h"
+#include "http_client.h"
+
+namespace gpumon {
+
+// OpenSSL 3 ABI pieces used here (stable since 1.1.0; declared locally so no openssl headers are
+// needed to build): opaque handles as void*, and the constant values of ssl.h / prov_ssl.h.
+namespace ossl {
+constexpr int kVerifyNone = 0, kVerifyPeer = 1;
+constexpr int kCtrlSetTlsextHostname = 55, kTlsextNametypeHostName = 0;
+constexpr int kCtrlSetMinProtoVersion = 123, kTls12Version = 0x0303;
+constexpr int kFiletypePem = 1;
+constexpr int kErrorNone = 0, kErrorSsl = 1, kErrorWantRead = 2, kErrorWantWrite = 3, kErrorSyscall = 5,
+              kErrorZeroReturn = 6;
+constexpr long kVerifyOk = 0;
+constexpr uint64_t kInitLoadSslStrings = 0x00200000L, kInitLoadCryptoStrings = 0x00000002L;
+}  // namespace ossl
+
+struct SslApi {
+  void* ssl_dl = nullptr;
+  void* crypto_dl = nullptr;
+  // libssl
+  int (*OPENSSL_init_ssl)(uint64_t, const void*) = nullptr;
+  const void* (*TLS_client_method)() = nullptr;
+  void* (*SSL_CTX_new)(const void*) = nullptr;
+  void (*SSL_CTX_free)(void*) = nullptr;
+  long (*SSL_CTX_ctrl)(void*, int, long, void*) = nullptr;
+  void (*SSL_CTX_set_verify)(void*, int, void*) = nullptr;
+  int (*SSL_CTX_set_default_verify_paths)(void*) = nullptr;
+  int (*SSL_CTX_load_verify_locations)(void*, const char*, const char*) = nullptr;
+  int (*SSL_CTX_use_certificate_chain_file)(void*, const char*) = nullptr;
+  int (*SSL_CTX_use_PrivateKey_file)(void*, const char*, int) = nullptr;
+  int (*SSL_CTX_check_private_key)(const void*) = nullptr;
+  void* (*SSL_CTX_get_cert_store)(const void*) = nullptr;
+  void* (*SSL_new)(void*) = nullptr;
+  void (*SSL_free)(void*) = nullptr;
+  int (*SSL_set_fd)(void*, int) = nullptr;
+  long (*SSL_ctrl)(void*, int, long, void*) = nullptr;
+  int (*SSL_set1_host)(void*, const char*) = nullptr;
+  void* (*SSL_get0_param)(void*) = nullptr;
+  int (*SSL_connect)(void*) = nullptr;
+  int (*SSL_read)(void*, void*, int) = nullptr;
+  int (*SSL_write)(void*, const void*, int) = nullptr;
+  int (*SSL_shutdown)(void*) = nullptr;
+  int (*SSL_get_error)(const void*, int) = nullptr;
+  long (*SSL_get_verify_result)(const void*) = nullptr;
+  // libcrypto
+  int (*X509_VERIFY_PARAM_set1_ip_asc)(void*, const char*) = nullptr;
+  const char* (*X509_verify_cert_error_string)(long) = nullptr;
+  void* (*X509_STORE_get0_objects)(const void*) = nullptr;
+  int (*OPENSSL_sk_num)(const void*) = nullptr;
+  unsigned long (*ERR_get_error)() = nullptr;
+  void (*ERR_error_string_n)(unsigned long, char*, size_t) = nullptr;
+  void (*ERR_clear_error)() = nullptr;
+};
+
+namespace {
+
+std::once_flag g_once;
+SslApi* g_api = nullptr;
+std::string g_err;
+
+template <class T>
+bool sym(void* dl, const char* name, T* out, std::string* missing) {
+  *out = reinterpret_cast<T>(dlsym(dl, name));
+  if (!*out) *missing += std::string(missing->empty() ? "" : ", ") + name;
+  return *out != nullptr;
+}
+
+void load_api() {
+  const char* ssl_env = getenv("GPUMON_LIBSSL");
+  const char* crypto_env = getenv("GPUMON_LIBCRYPTO");
+  auto* a = new SslApi;
+  // libcrypto first, RTLD_GLOBAL: libssl resolves its own libcrypto dependency to the same object
+  for (const char* n : {crypto_env && *crypto_env ? crypto_env : "libcrypto.so.3", "libcrypto.so"}) {
+    a->crypto_dl = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
+    if (a->crypto_dl) break;
+  }
+  for (const char* n : {ssl_env && *ssl_env ? ssl_env : "libssl.so.3", "libssl.so"}) {
+    a->ssl_dl = dlopen(n, RTLD_NOW | RTLD_LOCAL);
+    if (a->ssl_dl) break;
+  }
+  if (!a->ssl_dl || !a->crypto_dl) {
+    g_err = std::string("https needs OpenSSL 3 (libssl.so.3 / libcrypto.so.3): ") + (dlerror() ?: "not found");
+    if (a->ssl_dl) dlclose(a->ssl_dl);
+    if (a->crypto_dl) dlclose(a->crypto_dl);
+    delete a;
+    return;
+  }
+  std::string missing;
+  void* s = a->ssl_dl;
+  void* c = a->crypto_dl;
+  sym(s, "OPENSSL_init_ssl", &a->OPENSSL_init_ssl, &missing);
+  sym(s, "TLS_client_method", &a->TLS_client_method, &missing);
+  sym(s, "SSL_CTX_new", &a->SSL_CTX_new, &missing);
+  sym(s, "SSL_CTX_free", &a->SSL_CTX_free, &missing);
+  sym(s, "SSL_CTX_ctrl", &a->SSL_CTX_ctrl, &missing);
+  sym(s, "SSL_CTX_set_verify", &a->SSL_CTX_set_verify, &missing);
+  sym(s, "SSL_CTX_set_default_verify_paths", &a->SSL_CTX_set_default_verify_paths, &missing);
+  sym(s, "SSL_CTX_load_verify_locations", &a->SSL_CTX_load_verify_locations, &missing);
+  sym(s, "SSL_CTX_use_certificate_chain_file", &a->SSL_CTX_use_certificate_chain_file, &missing);
+  sym(s, "SSL_CTX_use_PrivateKey_file", &a->SSL_CTX_use_PrivateKey_file, &missing);
+  sym(s, "SSL_CTX_check_private_key", &a->SSL_CTX_check_private_key, &missing);
+  sym(s, "SSL_CTX_get_cert_store", &a->SSL_CTX_get_cert_store, &missing);
+  sym(s, "SSL_new", &a->SSL_new, &missing);
+  sym(s, "SSL_free", &a->SSL_free, &missing);
+  sym(s, "SSL_set_fd", &a->SSL_set_fd, &missing);
+  sym(s, "SSL_ctrl", &a->SSL_ctrl, &missing);
+  sym(s, "SSL_set1_host", &a->SSL_set1_host, &missing);
+  sym(s, "SSL_get0_param", &a->SSL_get0_param, &missing);
+  sym(s, "SSL_connect", &a->SSL_connect, &missing);
+  sym(s, "SSL_read", &a->SSL_read, &missing);
+  sym(s, "SSL_write", &a->SSL_write, &missing);
+  sym(s, "SSL_shutdown", &a->SSL_shutdown, &missing);
+  sym(s, "SSL_get_error", &a->SSL_get_error, &missing);
+  sym(s, "SSL_get_verify_result", &a->SSL_get_verify_result, &missing);
+  sym(c, "X509_VERIFY_PARAM_set1_ip_asc", &a->X509_VERIFY_PARAM_set1_ip_asc, &missing);
+  sym(c, "X509_verify_cert_error_string", &a->X509_verify_cert_error_string, &missing);
+  sym(c, "X509_STORE_get0_objects", &a->X509_STORE_get0_objects, &missing);
+  sym(c, "OPENSSL_sk_num", &a->OPENSSL_sk_num, &missing);
+  sym(c, "ERR_get_error", &a->ERR_get_error, &missing);
+  sym(c, "ERR_error_string_n", &a->ERR_error_string_n, &missing);
+  sym(c, "ERR_clear_error", &a->ERR_clear_error, &missing);
+  if (!missing.empty()) {
+    g_err = "libssl / libcrypto lack " + missing + " (OpenSSL >= 3 required)";
+    dlclose(a->ssl_dl);
+    dlclose(a->crypto_dl);
+    delete a;
+    return;
+  }
+  a->OPENSSL_init_ssl(ossl::kInitLoadSslStrings | ossl::kInitLoadCryptoStrings, nullptr);
+  g_api = a;  // never unloaded: OpenSSL keeps process-wide state
+}
+
+std::string err_queue(const SslApi* a) {
+  std::string out;
+  for (unsigned long e; (e = a->ERR_get_error()) != 0;) {
+    char buf[256];
+    a->ERR_error_string_n(e, buf, sizeof buf);
+    out = buf;  // the last (outermost) entry names the failing operation best
+  }
+  return out;
+}
+
+bool is_ip_literal(const std::string& h) {
+  unsigned char b[16];
+  return inet_pton(AF_INET, h.c_str(), b) == 1 || inet_pton(AF_INET6, h.c_str(), b) == 1;
+}
+
+// Bundles where distributions keep the CA set, for when libssl's compiled-in OPENSSLDIR holds none
+// (a slim image that copies the bundle but not the hashed certs/ directory).
+const char* const kBundles[] = {"/etc/ssl/certs/ca-certificates.crt", "/etc/pki/tls/certs/ca-bundle.crt",
+                                "/etc/ssl/ca-bundle.pem", "/etc/ssl/cert.pem"};
+
+}  // namespace
+
+const SslApi* ssl_api(std::string* err) {
+  std::call_once(g_once, load_api);
+  if (!g_api && err) *err = g_err;
+  return g_api;
+}
+
+std::shared_ptr<TlsContext> TlsContext::create(const TlsOptions& o, std::string* err) {
+  const SslApi* a = ssl_api(err);
+  if (!a) return nullptr;
+  std::shared_ptr<TlsContext> t(new TlsContext);
+  t->api_ = a;
+  t->insecure_ = o.insecure;
+  a->ERR_clear_error();
+  t->ctx_ = a->SSL_CTX_new(a->TLS_client_method());
+  if (!t->ctx_) {
+    *err = "tls: SSL_CTX_new: " + err_queue(a);
+    return nullptr;
+  }
+  a->SSL_CTX_ctrl(t->ctx_, ossl::kCtrlSetMinProtoVersion, ossl::kTls12Version, nullptr);
+  if (!o.insecure) {
+    if (!o.ca_file.empty()) {
+      if (a->SSL_CTX_load_verify_locations(t->ctx_, o.ca_file.c_str(), nullptr) != 1) {
+        *err = "tls: cannot load CA file " + o.ca_file + ": " + err_queue(a);
+        return nullptr;
+      }
+    } else {
+      a->SSL_CTX_set_default_verify_paths(t->ctx_);
+      a->ERR_clear_error();  // a missing default directory is not an error by itself
+      const void* objs = a->X509_STORE_get0_objects(a->SSL_CTX_get_cert_store(t->ctx_));
+      if (!objs || a->OPENSSL_sk_num(objs) <= 0) {
+        // the default file held nothing (SSL_CERT_FILE unset, OPENSSLDIR empty): the usual bundles
+        for (const char* b : kBundles)
+          if (access(b, R_OK) == 0 && a->SSL_CTX_load_verify_locations(t->ctx_, b, nullptr) == 1) break;
+        a->ERR_clear_error();
+      }
+    }
+  }
+  a->SSL_CTX_set_verify(t->ctx_, o.insecure ? ossl::kVerifyNone : ossl::kVerifyPeer, nullptr);
+  if (!o.client_cert.empty() || !o.client_key.empty()) {
+    const std::string& key = o.client_key.empty() ? o.client_cert : o.client_key;
+    if (a->SSL_CTX_use_certificate_chain_file(t->ctx_, o.client_cert.c_str()) != 1) {
+      *err = "tls: cannot load client certificate " + o.client_cert + ": " + err_queue(a);
+      return nullptr;
+    }
+    if (a->SSL_CTX_use_PrivateKey_file(t->ctx_, key.c_str(), ossl::kFiletypePem) != 1 ||
+        a->SSL_CTX_check_private_key(t->ctx_) != 1) {
+      *err = "tls: cannot load client key " + key + ": " + err_queue(a);
+      return nullptr;
+    }
+  }
+  return t;
+}
+
+TlsContext::~TlsContext() {
+  if (ctx_) api_->SSL_CTX_free(ctx_);
+}
+
+TlsConn::~TlsConn() {
+  if (ssl_) ctx_->api()->SSL_free(ssl_);
+}
+
+std::string TlsConn::last_error(int ret) {
+  const SslApi* a = ctx_->api();
+  const int e = a->SSL_get_error(ssl_, ret);
+  const int saved_errno = errno;
+  std::string q = err_queue(a);
+  switch (e) {
+    case ossl::kErrorZeroReturn:
+      return "tls: connection closed by peer";
+    case ossl::kErrorWantRead:
+    case ossl::kErrorWantWrite:
+      return "tls: timed out";
+    case ossl::kErrorSyscall:
+      if (!q.empty()) return "tls: " + q;
+      if (saved_errno == EAGAIN || saved_errno == EWOULDBLOCK) return "tls: timed out";
+      return saved_errno ? std::string("tls: ") + strerror(saved_errno) : "tls: unexpected EOF";
+    default:
+      return "tls: " + (q.empty() ? "error " + std::to_string(e) : q);
+  }
+}
+
+bool TlsConn::handshake(int fd, const std::string& host, std::string* err) {
+  const SslApi* a = ctx_->api();
+  a->ERR_clear_error();
+  ssl_ = a->SSL_new(ctx_->raw());
+  if (!ssl_ || a->SSL_set_fd(ssl_, fd) != 1) {
+    *err = "tls: SSL_new: " + err_queue(a);
+    return false;
+  }
+  const bool ip = is_ip_literal(host);
+  // RFC 6066: no SNI for IP literals
+  if (!ip) a->SSL_ctrl(ssl_, ossl::kCtrlSetTlsextHostname, ossl::kTlsextNametypeHostName, const_cast<char*>(host.c_str()));
+  if (ctx_->verify()) {
+    const int ok = ip ? a->X509_VERIFY_PARAM_set1_ip_asc(a->SSL_get0_param(ssl_), host.c_str())
+                      : a->SSL_set1_host(ssl_, host.c_str());
+    if (ok != 1) {
+      *err = "tls: cannot set the expected peer name " + host;
+      return false;
+    }
+  }
+  const int r = a->SSL_connect(ssl_);
+  if (r != 1) {
+    const long v = a->SSL_get_verify_result(ssl_);
+    if (ctx_->verify() && v != ossl::kVerifyOk) {
+      a->ERR_clear_error();
+      *err = std::string("tls: certificate verify failed: ") + a->X509_verify_cert_error_string(v);
+    } else {
+      *err = last_error(r);
+      if (err->find("handshake") == std::string::npos) *err += " (handshake with " + host + ")";
+    }
+    return false;
+  }
+  return true;
+}
+
+bool TlsConn::write_all(const char* p, size_t n, std::string* err) {
+  const SslApi* a = ctx_->api();
+  while (n) {
+    const int chunk = static_cast<int>(std::min<size_t>(n, 1 << 30));
+    a->ERR_clear_error();
+    const int w = a->SSL_write(ssl_, p, chunk);
+    if (w <= 0) {
+      *err = last_error(w);
+      return false;
+    }
+    p += w;
+    n -= static_cast<size_t>(w);
+  }
+  return true;
+}
+
+long TlsConn::read_some(char* buf, size_t n, std::string* err) {
+  const SslApi* a = ctx_->api();
+  a->ERR_clear_error();
+  errno = 0;
+  const int r = a->SSL_read(ssl_, buf, static_cast<int>(std::min<size_t>(n, 1 << 30)));
+  if (r > 0) return r;
+  const int e = a->SSL_get_error(ssl_, r);
+  if (e == ossl::kErrorZeroReturn) return 0;
+  // EOF without close_notify: many servers (and proxies) just close; the HTTP framing decides
+  if (e == ossl::kErrorSyscall && errno == 0 && a->ERR_get_error() == 0) return 0;
+  *err = last_error(r);
+  return -1;
+}
+
+void TlsConn::shutdown() {
+  if (ssl_) {
+    ctx_->api()->SSL_shutdown(ssl_);
+    ctx_->api()->ERR_clear_error();
+  }
+}
+
+std::string check_push_config(const std::string& url, const std::string& token, const TlsOptions& tls) {
+  if (url.empty()) return "";
+  const Url u = parse_url(url);
+  if (!u.ok) return "influx_url " + redact_url(url) + ": " + (u.error.empty() ? "not a usable URL" : u.error);
+  if (token.find_first_of("\r\n") != std::string::npos) return "influx_token contains a line break";
+  if (!u.tls) {
+    if (!tls.ca_file.empty() || !tls.client_cert.empty() || tls.insecure)
+      GPUMON_LOG(LogLevel::kWarn, "influx", "TLS settings given for an http:// INFLUXDB_URL: ignored");
+    return "";
+  }
+  for (const std::string* f : {&tls.ca_file, &tls.client_cert, &tls.client_key})
+    if (!f->empty() && access(f->c_str(), R_OK) != 0) return "cannot read " + *f + ": " + strerror(errno);
+  std::string err;
+  if (!TlsContext::create(tls, &err)) return err;
+  return "";
+}
+
+}  // namespace gpumon

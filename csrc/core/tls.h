@@ -1,0 +1,71 @@
+// TLS for the Influx compat push: OpenSSL 3 loaded at run time (dlopen libssl.so.3 +
+// libcrypto.so.3) into a typed function table, the way smi_table.h loads libamd_smi. The exporter
+// keeps no link-time (or build-time header) TLS dependency: an http:// deployment never maps
+// libssl, and an https:// URL on a host without it is a configuration error at startup.
+//
+// Reference parity: the reference posts with requests.post(INFLUXDB_URL, ...) (/root/reference/
+// gpu.py:20,145,218,252), which takes https:// URLs and verifies certificates against the system
+// CA bundle by default. Same defaults here: peer verification and host-name / IP checks are on;
+// `influx_ca_file` replaces the bundle, `influx_tls_insecure` (off by default) disables both.
+#pragma once
+
+#include <memory>
+#include <string>
+
+namespace gpumon {
+
+struct TlsOptions {
+  std::string ca_file;      // PEM bundle; "" = the system's default verify paths / well-known bundles
+  bool insecure = false;    // no peer or host-name verification (explicit opt-in only)
+  std::string client_cert;  // PEM chain for mutual TLS (optional, with client_key)
+  std::string client_key;
+};
+
+struct SslApi;  // the dlopen'd function table (tls.cpp)
+
+// Loads libssl / libcrypto once per process (thread-safe); nullptr with *err when unavailable.
+// $GPUMON_LIBSSL / $GPUMON_LIBCRYPTO override the sonames.
+const SslApi* ssl_api(std::string* err);
+
+// One client context: protocol floor TLS 1.2, trust store, verification mode, client certificate.
+class TlsContext {
+ public:
+  static std::shared_ptr<TlsContext> create(const TlsOptions& o, std::string* err);
+  ~TlsContext();
+  void* raw() const { return ctx_; }
+  const SslApi* api() const { return api_; }
+  bool verify() const { return !insecure_; }
+
+ private:
+  TlsContext() = default;
+  const SslApi* api_ = nullptr;
+  void* ctx_ = nullptr;  // SSL_CTX*
+  bool insecure_ = false;
+};
+
+// One TLS session over a connected blocking socket (SO_RCVTIMEO / SO_SNDTIMEO bound each call).
+class TlsConn {
+ public:
+  explicit TlsConn(std::shared_ptr<TlsContext> ctx) : ctx_(std::move(ctx)) {}
+  ~TlsConn();
+  // SNI + host-name (or IP literal) check + handshake. false with a named reason in *err, e.g.
+  // "tls: certificate verify failed: self-signed certificate in certificate chain".
+  bool handshake(int fd, const std::string& host, std::string* err);
+  // Whole buffer or false (*err set).
+  bool write_all(const char* p, size_t n, std::string* err);
+  // > 0 bytes read, 0 = orderly close (close_notify or EOF), < 0 = error / timeout (*err set).
+  long read_some(char* buf, size_t n, std::string* err);
+  void shutdown();
+
+ private:
+  std::string last_error(int ret);
+  std::shared_ptr<TlsContext> ctx_;
+  void* ssl_ = nullptr;  // SSL*
+};
+
+// Configuration-time check of a push URL and its TLS settings (both entry points call it): the
+// scheme, host and port parse, a token without line breaks, an https URL with libssl loadable and a
+// readable CA / client certificate. "" = usable; otherwise the reason.
+std::string check_push_config(const std::string& url, const std::string& token, const TlsOptions& tls);
+
+}  // namespace gpumon

@@ -21,6 +21,7 @@
 #include "core/exporter.h"
 #include "core/ondevice.h"
 #include "core/options.h"
+#include "core/tls.h"
 
 using namespace gpumon;
 
@@ -33,8 +34,9 @@ static void usage() {
   fprintf(stderr,
           "usage: gpumon-exporter [--config FILE] [--print-config] [--once]\n"
           "                       [--backend auto|amdsmi|rocm_smi|mock[:k=v,..]] [--interval SEC]\n"
-          "                       [--listen ADDR:PORT] [--host NAME] [--devices 0,1|BDF,..] [--no-fast-path]\n"
+          "                       [--listen HOST:PORT|[V6]:PORT|:PORT] [--host NAME] [--devices 0,1|BDF,..] [--no-fast-path]\n"
           "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
+          "                       [--influx-ca-file PEM] [--influx-tls-insecure] [--influx-client-cert PEM --influx-client-key PEM]\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--pod-labels KEY,KEY..]\n"
           "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--ras-slices N] [--no-gzip] [--metrics-include GLOBS] [--metrics-exclude GLOBS] [--sample-threads N] [--rt-priority N] [--prewarm-ms MS]\n"
@@ -99,6 +101,10 @@ int main(int argc, char** argv) {
     else if (a == "--influx-token") set("influx_token", next());
     else if (a == "--influx-extended") set("influx_extended", "true");
     else if (a == "--influx-schema") set("influx_schema", next());
+    else if (a == "--influx-ca-file") set("influx_ca_file", next());
+    else if (a == "--influx-tls-insecure") set("influx_tls_insecure", "true");
+    else if (a == "--influx-client-cert") set("influx_client_cert", next());
+    else if (a == "--influx-client-key") set("influx_client_key", next());
     else if (a == "--no-fast-path") set("fast_path", "false");
     else if (a == "--sysfs") set("sysfs_root", next());
     else if (a == "--roctx") set("roctx", "true");
@@ -150,8 +156,24 @@ int main(int argc, char** argv) {
     printf("%s\n", options_json(o).c_str());
     return 0;
   }
-  options_finalize(&o);
+  if (!options_finalize(&o, &err)) {
+    fprintf(stderr, "config: %s\n", err.c_str());
+    return 2;
+  }
   ExporterConfig& cfg = o.cfg;
+  {
+    // an Influx push that cannot work is a startup error, not a silently idle pusher
+    TlsOptions t;
+    t.ca_file = cfg.influx_ca_file;
+    t.insecure = cfg.influx_tls_insecure;
+    t.client_cert = cfg.influx_client_cert;
+    t.client_key = cfg.influx_client_key;
+    const std::string perr = check_push_config(cfg.influx_url, cfg.influx_token, t);
+    if (!perr.empty()) {
+      fprintf(stderr, "config: %s\n", perr.c_str());
+      return 2;
+    }
+  }
   const OnDeviceConfig& od = o.od;
 
   // The on-device samplers start BEFORE the backend: the PMC helper process is spawned while
@@ -209,7 +231,7 @@ int main(int argc, char** argv) {
   }
   if (!err.empty()) GPUMON_LOG(LogLevel::kWarn, "main", "backend not ready (retrying): " + err);
   GPUMON_LOG(LogLevel::kInfo, "main",
-             "serving http://" + cfg.listen_addr + ":" + std::to_string(e.port()) +
+             "serving http://" + e.listen_desc() +
                  "/metrics host=" + cfg.host + " interval=" + std::to_string(cfg.interval_s) + "s");
   while (!g_stop) std::this_thread::sleep_for(std::chrono::milliseconds(200));
   ondev.stop();

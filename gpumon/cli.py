@@ -25,7 +25,7 @@ import sys
 import threading
 import time
 
-from .config import Config, add_cli_args, from_args, redact_url
+from .config import Config, ConfigError, add_cli_args, from_args, redact_url
 
 
 def _setup_logging(level: str):
@@ -36,9 +36,13 @@ def _setup_logging(level: str):
 def cmd_serve(args) -> int:
     from .monitor import GpuMonitor
 
-    cfg = from_args(args)
+    cfg = from_args(args).validate()
     _setup_logging(cfg.log_level)
-    mon = GpuMonitor(cfg).start()
+    try:
+        mon = GpuMonitor(cfg).start()
+    except RuntimeError as e:  # the listen address taken, a mock backend that failed, ...
+        print(f"gpumon serve: {e}", file=sys.stderr)
+        return 1
     log = logging.getLogger("gpumon")
     log.info("serving %s backend=%s host=%s interval=%.3fs influx=%s control_plane=%s", mon.url, cfg.backend,
              cfg.resolved_host(), cfg.interval, redact_url(cfg.influx_url) or "-", bool(mon.plane))
@@ -298,7 +302,11 @@ def build_parser() -> argparse.ArgumentParser:
 
 def main(argv=None) -> int:
     args = build_parser().parse_args(argv)
-    return args.fn(args)
+    try:
+        return args.fn(args)
+    except ConfigError as e:
+        print(f"config: {e}", file=sys.stderr)
+        return 2
 
 
 if __name__ == "__main__":

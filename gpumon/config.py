@@ -53,7 +53,7 @@ class Config:
     init_retry_s: float = 5.0             # backoff between backend init attempts
     health_stale_s: float = 0.0           # /healthz 503 after this long without a tick (0 = max(3*interval, 10 s))
     # exposition
-    listen: str = "0.0.0.0:9400"
+    listen: str = ":9400"                 # host:port | [v6]:port | :port (every address, dual-stack; IPv4 if no IPv6)
     http_threads: int = 2
     http_rt_priority: int = 0             # SCHED_FIFO HTTP loops (CAP_SYS_NICE), each capped at http_rt_budget of a CPU
     http_rt_budget: float = 0.2           # share of a CPU per 100 ms an RT HTTP loop may use before it is demoted
@@ -64,11 +64,15 @@ class Config:
     metrics_include: List[str] = field(default_factory=list)  # serve only families matching these globs (e.g. node_gpu_*)
     metrics_exclude: List[str] = field(default_factory=list)  # drop families matching these globs (e.g. gpu_xcd_*); Influx unfiltered
     # influx compat push
-    influx_url: str = ""
+    influx_url: str = ""                  # http(s)://[user:password@]host[:port]/path?query; checked at startup (exit 2 if unusable)
     influx_token: str = ""                # InfluxDB 2.x/3.x API token (env INFLUXDB_TOKEN, from a Secret); 1.x: user:password@ in the URL
     influx_extended: bool = False
     influx_schema: int = 2019             # 2019 = gpu.py layout; 2018 = img/influxdb.png pod_gpu layout
     influx_every: int = 1
+    influx_ca_file: str = ""              # https:// push: PEM CA bundle replacing the system one
+    influx_tls_insecure: bool = False     # https:// push WITHOUT certificate / host-name checks (opt-in, testing)
+    influx_client_cert: str = ""          # https:// push: PEM client chain for mutual TLS
+    influx_client_key: str = ""           # ... and its key (default: in the chain file)
     # attribution
     procfs_root: str = "/proc"
     opt_in_label: str = ""
@@ -121,11 +125,12 @@ class Config:
     # ------------------------------------------------------------------ helpers
     @property
     def listen_addr(self) -> str:
-        return self.listen.rsplit(":", 1)[0] if ":" in self.listen else "0.0.0.0"
+        """Host part of `listen` ("" = every address, dual-stack): the native parse_listen rule."""
+        return parse_listen(self.listen)[0]
 
     @property
     def port(self) -> int:
-        return int(self.listen.rsplit(":", 1)[1]) if ":" in self.listen else int(self.listen)
+        return parse_listen(self.listen)[1]
 
     def resolved_host(self) -> str:
         return self.host or os.environ.get("NODE_NAME") or socket.gethostname() or "no_name"
@@ -173,6 +178,10 @@ class Config:
             "influx_extended": self.influx_extended,
             "influx_schema": int(self.influx_schema),
             "influx_every": int(self.influx_every),
+            "influx_ca_file": self.influx_ca_file,
+            "influx_tls_insecure": bool(self.influx_tls_insecure),
+            "influx_client_cert": self.influx_client_cert,
+            "influx_client_key": self.influx_client_key,
             "procfs_root": self.procfs_root,
             "opt_in": self.opt_in_label,
             "user_label": self.user_label,
@@ -186,6 +195,26 @@ class Config:
             "xgmi_kb_bytes": float(self.xgmi_kb_bytes),
             "version": _version(),
         }
+
+    def validate(self) -> "Config":
+        """Configuration-time checks the exporter would otherwise only hit while running. The Influx
+        push: the same native check bin/gpumon-exporter runs before it starts (csrc/core/tls.h
+        check_push_config) -- scheme, host, port, token, and for https libssl plus readable CA /
+        client files. Raises ConfigError naming the problem."""
+        if self.influx_url:
+            from ._native import core
+
+            err = core().check_push_config(self.influx_url, self.influx_token, self.influx_ca_file,
+                                           bool(self.influx_tls_insecure), self.influx_client_cert,
+                                           self.influx_client_key)
+            if err:
+                raise ConfigError(err)
+        try:
+            _device_ids(self.devices)
+        except ValueError as e:
+            raise ConfigError(str(e)) from None
+        parse_listen(self.listen)
+        return self
 
     # ------------------------------------------------------------------ sources
     def apply_dict(self, d: Dict[str, Any]) -> "Config":
@@ -216,9 +245,47 @@ class Config:
         return self
 
 
+class ConfigError(ValueError):
+    """A configuration the exporter cannot run with (the CLI exits 2 with the message)."""
+
+
 # Keys of earlier releases that selected the Python test oracles (now under tests/oracles, not
 # shipped): a config file that still names them keeps working, with the native path.
 _RETIRED = {"ondevice"}
+
+
+def parse_listen(listen: str):
+    """`listen` -> (host, port), the rule of the native parse_listen (csrc/core/http_server.cpp), which
+    tests/test_native_config.py checks this against: "host:port", "[v6]:port", ":port", "*:port" or
+    "port"; host "" = every address (one dual-stack [::] socket, 0.0.0.0 where the kernel has no
+    IPv6). Raises ConfigError for anything else."""
+    import ipaddress
+
+    s = str(listen).strip()
+    if not s:
+        raise ConfigError("empty listen address")
+    if s.startswith("["):
+        rb = s.find("]")
+        if rb < 0 or rb + 1 >= len(s) or s[rb + 1] != ":":
+            raise ConfigError(f"listen '{s}': expected [v6]:port")
+        host, port = s[1:rb], s[rb + 2:]
+        try:
+            ipaddress.IPv6Address(host)
+        except ValueError:
+            raise ConfigError(f"listen '{s}': '{host}' is not an IPv6 address") from None
+    elif s.isdigit():
+        host, port = "", s
+    else:
+        if ":" not in s:
+            raise ConfigError(f"listen '{s}': expected host:port")
+        host, port = s.rsplit(":", 1)
+        if ":" in host:
+            raise ConfigError(f"listen '{s}': an IPv6 address needs brackets ([v6]:port)")
+        if host == "*":
+            host = ""
+    if not port or len(port) > 5 or not port.isdigit() or int(port) > 65535:
+        raise ConfigError(f"listen '{s}': bad port '{port}'")
+    return host, int(port)
 
 
 def redact_url(url: str) -> str:
@@ -299,10 +366,17 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
                    "auto = amdsmi, falling back to rocm_smi)")
     p.add_argument("--devices", help="comma-separated hip ids and / or PCI BDFs to monitor (default all)")
     p.add_argument("--interval", type=float, help=f"sampling interval seconds (default {d.interval})")
-    p.add_argument("--listen", help=f"ADDR:PORT for /metrics (default {d.listen})")
+    p.add_argument("--listen", help=f"HOST:PORT, [V6]:PORT or :PORT for /metrics (default {d.listen}: every "
+                   "address, IPv4 and IPv6)")
     p.add_argument("--host", help="node name label (default $NODE_NAME, then hostname)")
     p.add_argument("--influx-url", dest="influx_url", help="enable InfluxDB line-protocol push (default $INFLUXDB_URL)")
     p.add_argument("--influx-extended", dest="influx_extended", action="store_true", default=None)
+    p.add_argument("--influx-ca-file", dest="influx_ca_file", help="PEM CA bundle for an https:// INFLUXDB_URL "
+                   "(default: the system bundle)")
+    p.add_argument("--influx-tls-insecure", dest="influx_tls_insecure", action="store_true", default=None,
+                   help="do NOT verify the InfluxDB server's certificate (testing only)")
+    p.add_argument("--influx-client-cert", dest="influx_client_cert", help="PEM client certificate (mutual TLS)")
+    p.add_argument("--influx-client-key", dest="influx_client_key", help="PEM client key (mutual TLS)")
     p.add_argument("--influx-schema", dest="influx_schema", type=int, choices=[2018, 2019],
                    help="pod_gpu line layout: 2019 (gpu.py, default) or 2018 (img/influxdb.png)")
     p.add_argument("--opt-in-label", dest="opt_in_label", help="only report pods with label KEY=VALUE")

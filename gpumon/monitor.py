@@ -116,8 +116,10 @@ class GpuMonitor:
     @property
     def url(self) -> str:
         host = self.cfg.listen_addr
-        if host in ("0.0.0.0", ""):
-            host = "127.0.0.1"
+        if host in ("0.0.0.0", "", "::"):
+            host = "127.0.0.1"  # the wildcard takes IPv4 loopback in both forms (dual-stack [::])
+        elif ":" in host:
+            host = f"[{host}]"
         return f"http://{host}:{self.port}/metrics"
 
     def metrics(self) -> str:

@@ -1,8 +1,9 @@
-"""The base DaemonSet's security context -- uid 0 with every capability dropped except SYS_PTRACE,
-DAC_READ_SEARCH and SYS_NICE (deploy/k8s/gpumon-daemonset.yaml) -- reads what a full-capability root
-exporter reads. Here as root with setpriv: the exporter runs with the bounding set
-reduced to exactly that set, to round 3's set (no DAC_READ_SEARCH: it could not list a non-root
-tenant's fd table) and without SYS_PTRACE, against a tenant process owned by another uid:
+"""The DaemonSet's security contexts against what a full-capability root exporter reads (ADVICE r3,
+r4). The base pod keeps SYS_PTRACE and SYS_NICE (deploy/k8s/gpumon-daemonset.yaml); the opt-in
+overlays/fdscan/ adds DAC_READ_SEARCH (kept out of the base since round 5: with RuntimeDefault
+seccomp it unlocks open_by_handle_at). Here as root with setpriv: the exporter runs with the bounding
+set reduced to the base set, the fdscan set and a set without SYS_PTRACE, against a tenant process
+owned by another uid:
 
 * the /proc/<pid>/fd scan that checks a process holds /dev/kfd and finds its DRM fds (sysfs fast
   path) needs DAC_READ_SEARCH to list another uid's fd directory and SYS_PTRACE to read its links
@@ -88,16 +89,16 @@ def test_daemonset_capability_set_reads_what_root_reads(tmp_path):
     shutil.copy(os.path.join(ROOT, "build", "fakes", "libfake_amd_smi.so"), pkg)
     os.chmod(tmp_path, 0o755)
     full = _run(None, str(pkg))
-    r3_set = _run("-all,+sys_ptrace,+sys_nice", str(pkg))
-    ds = _run("-all,+sys_ptrace,+sys_nice,+dac_read_search", str(pkg))
+    r3_set = _run("-all,+sys_ptrace,+sys_nice", str(pkg))  # the base DaemonSet's set (and round 3's)
+    ds = _run("-all,+sys_ptrace,+sys_nice,+dac_read_search", str(pkg))  # overlays/fdscan/
     no_ptrace = _run("-all,+sys_nice,+dac_read_search", str(pkg))
     print("\nfull root:", full, "\nround-3 set:", r3_set, "\nDaemonSet set:", ds, "\nwithout SYS_PTRACE:", no_ptrace)
     ok = {"fd_dir": True, "fd_link": "/etc/hostname", "fdinfo": True}
     assert {k: full[k] for k in ok} == ok
-    # round 3's set (SYS_PTRACE + SYS_NICE) could not even list another uid's fd table: the
-    # directory is mode 0500 of the tenant's uid, so a root without DAC_READ_SEARCH is refused
+    # the base set (SYS_PTRACE + SYS_NICE) cannot list another uid's fd table: the directory is
+    # mode 0500 of the tenant's uid, so a root without DAC_READ_SEARCH is refused (the overlay's job)
     assert r3_set["fd_dir"] == "PermissionError"
-    # the DaemonSet's set now (+ DAC_READ_SEARCH) reads all three, as full root does
+    # the fdscan overlay's set (+ DAC_READ_SEARCH) reads all three, as full root does
     assert {k: ds[k] for k in ok} == ok
     # ... and the fd links / fdinfo still need SYS_PTRACE on top (ptrace_may_access)
     assert no_ptrace["fd_dir"] is True and no_ptrace["fd_link"] == "PermissionError"

@@ -22,7 +22,7 @@ def _ns(argv, env=None):
 
 def test_defaults():
     c = Config()
-    assert c.interval == 1.0 and c.listen == "0.0.0.0:9400" and c.backend == "auto"
+    assert c.interval == 1.0 and c.listen == ":9400" and c.backend == "auto"
     assert c.opt_in_label == "" and c.user_prefix == "turing-gpu-notebook-"
 
 
@@ -139,9 +139,11 @@ def test_url_parsing_auth_and_v6(core):
     u = core.parse_url("http://[fd00::1]:8086/api/v2/write?org=o&bucket=b")
     assert (u["ok"], u["host"], u["port"], u["path"]) == (True, "fd00::1", 8086, "/api/v2/write?org=o&bucket=b")
     assert core.parse_url("http://influx?db=x")["path"] == "/?db=x" and core.parse_url("http://influx")["port"] == 80
-    for bad in ("https://influx:8086/write", "http://:8086/", "http://influx:99999/", "http://influx:80x/",
+    for bad in ("ftp://influx:8086/write", "http://:8086/", "http://influx:99999/", "http://influx:80x/",
                 "http://[fd00::1/", "http://[fd00::1]x/"):
         assert not core.parse_url(bad)["ok"], bad
+    u = core.parse_url("https://influx.example/api/v2/write?org=o")  # TLS: tests/test_influx_tls.py
+    assert (u["ok"], u["tls"], u["port"]) == (True, True, 443)
     for b in ("", "f", "fo", "foo", "foob", "fooba", "u:\u00e9\u00fc"):  # padding cases, non-ASCII
         h = core.parse_url(f"http://{b}@h/")["auth_header"]
         assert h == "Authorization: Basic " + base64.b64encode(b.encode()).decode() + "\r\n", b
@@ -231,18 +233,14 @@ def test_influx_credentials_never_printed(tmp_path):
     assert c.influx_token == "tok-456" and c.to_core()["influx_token"] == "tok-456"
 
 
-def test_influx_token_with_a_line_break_disables_the_push(core):
-    """A token is copied into a request header: CR/LF in it would inject headers, so the pusher
-    refuses to start (the sampler keeps running)."""
+def test_influx_token_with_a_line_break_is_refused_at_start(core):
+    """A token is copied into a request header: CR/LF in it would inject headers. The exporter
+    refuses to start with it (a configuration error), rather than running without a push."""
     ex = core.Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0.02,
                         "influx_url": "http://127.0.0.1:9/write", "influx_token": "tok\r\nX-Evil: 1"})
-    ex.start()
-    try:
-        time.sleep(0.3)
-        st = ex.self_stats()
-    finally:
-        ex.stop()
-    assert st["ticks"] >= 5 and st["influx_ok"] == 0 and st["influx_fail"] == 0
+    with pytest.raises(RuntimeError, match="influx_token contains a line break"):
+        ex.start()
+    ex.stop()
 
 
 def test_devices_accept_hip_ids_and_bdfs_and_refuse_the_rest():

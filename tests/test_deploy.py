@@ -117,12 +117,18 @@ def test_dashboard_queries_resolve_against_exposition(mock_exporter):
 
 
 def test_dockerfile_entrypoint():
+    """the image runs the native exporter (no Python in the runtime stage), from a
+    plain base plus the staged closure (deploy/image_closure.py; tests/test_image_closure.py)."""
     txt = open(os.path.join(ROOT, "deploy/Dockerfile")).read()
-    assert 'ENTRYPOINT ["python3", "-m", "gpumon", "serve"]' in txt
+    runtime = txt.split("\nFROM ${BASE_IMAGE}", 1)[1]
+    assert 'ENTRYPOINT ["/opt/gpumon/bin/gpumon-exporter"]' in runtime
+    assert 'CMD ["--config", "/etc/gpumon/config.yaml"]' in runtime
+    assert "ARG BASE_IMAGE=ubuntu:22.04" in txt
+    assert "python" not in runtime.lower() and "pip" not in runtime and "apt-get" not in runtime
+    assert "COPY --from=build /rootfs/ /" in runtime
+    assert "image_closure.py stage --root /rootfs --overlays" in txt
     assert "libltdl" not in txt.split("\n", 5)[-1] or "no vendored" in txt
-    assert "EXPOSE 9400" in txt
-    # the on-device plugins ship next to the package and the binary (csrc/core/ondevice.cpp lookup)
-    assert "COPY --from=build /src/lib /opt/gpumon/lib" in txt and "GPUMON_PLUGIN_DIR=/opt/gpumon/lib" in txt
+    assert "EXPOSE 9400" in txt and "GPUMON_PLUGIN_DIR=/opt/gpumon/lib" in runtime
 
 
 def _build_stage_copies(dockerfile):
@@ -191,7 +197,8 @@ def test_image_build_stage_makes_all_from_its_copy_set(tmp_path):
     df = os.path.join(ROOT, "deploy", "Dockerfile")
     copies = _build_stage_copies(df)
     _stage_tree(copies, str(tmp_path))
-    assert sorted(os.listdir(tmp_path)) == ["Makefile", "csrc", "gpumon"], sorted(os.listdir(tmp_path))
+    assert sorted(os.listdir(tmp_path)) == ["Makefile", "csrc", "deploy", "gpumon"], sorted(os.listdir(tmp_path))
+    assert os.listdir(tmp_path / "deploy") == ["image_closure.py"]
     targets = _make_targets(df)
     assert targets == ["all", "GPUMON_ARCH=gfx950"], targets
     r = subprocess.run(["make", "-C", str(tmp_path), "-n", *targets], capture_output=True, text=True, timeout=120)
@@ -400,7 +407,7 @@ print(json.dumps({"rc": rc, "bad": bad}))
 def test_dockerfile_installs_no_grpc():
     text = open(os.path.join(ROOT, "deploy", "Dockerfile")).read()
     installs = [l for l in text.splitlines() if "pip3 install" in l]
-    assert installs and not any("grpc" in l or "protobuf" in l for l in installs), installs
+    assert installs and not any("grpc" in l or "protobuf" in l or "yaml" in l for l in installs), installs
     assert "tests" not in " ".join(l for l in text.splitlines() if l.startswith("COPY")), "oracles stay out of the image"
 
 
@@ -416,8 +423,9 @@ def test_base_pod_is_unprivileged():
     assert sc.get("privileged", False) is False and sc["allowPrivilegeEscalation"] is False
     assert sc["readOnlyRootFilesystem"] is True and sc["seccompProfile"]["type"] == "RuntimeDefault"
     assert sc["capabilities"]["drop"] == ["ALL"]
-    # read-only DAC bypass for other uids' /proc/<pid>/fd (tests/test_capabilities.py), no write-side capability
-    assert set(sc["capabilities"].get("add", [])) <= {"SYS_PTRACE", "DAC_READ_SEARCH", "SYS_NICE"}
+    # no DAC_READ_SEARCH in the base (with RuntimeDefault seccomp it unlocks
+    # open_by_handle_at); it is the opt-in overlays/fdscan/
+    assert sorted(sc["capabilities"].get("add", [])) == ["SYS_NICE", "SYS_PTRACE"]
     assert not pod.get("hostNetwork") and not pod.get("hostIPC")
     mounts = {m["mountPath"] for m in c["volumeMounts"]}
     assert not any(m.startswith("/dev") for m in mounts), mounts
@@ -445,6 +453,22 @@ def test_elevated_rights_only_in_the_ondevice_overlay():
         assert all(m["name"] in vols for m in c["volumeMounts"])
     pod = patched("docker")
     assert pod["containers"][0]["securityContext"].get("privileged", False) is False
+
+
+def test_fdscan_overlay_only_adds_dac_read_search():
+    """overlays/fdscan/ is the one place CAP_DAC_READ_SEARCH comes back (listing a non-root tenant's
+    /proc/<pid>/fd), and its header states the open_by_handle_at trade-off."""
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    (k,) = _docs("deploy/k8s/overlays/fdscan/kustomization.yaml")
+    assert k["resources"] == ["../../"] and [p["target"]["kind"] for p in k["patches"]] == ["DaemonSet"]
+    ops = yaml.safe_load(k["patches"][0]["patch"])
+    pod = _json_patch(ds, ops)["spec"]["template"]["spec"]
+    sc = pod["containers"][0]["securityContext"]
+    assert sorted(sc["capabilities"]["add"]) == ["DAC_READ_SEARCH", "SYS_NICE", "SYS_PTRACE"]
+    base = ds["spec"]["template"]["spec"]["containers"][0]["securityContext"]
+    assert {k2: v for k2, v in sc.items() if k2 != "capabilities"} == {k2: v for k2, v in base.items() if k2 != "capabilities"}
+    text = open(os.path.join(ROOT, "deploy/k8s/overlays/fdscan/kustomization.yaml")).read()
+    assert "open_by_handle_at" in text and "seccomp" in text
 
 
 def test_nonroot_overlay():
@@ -475,15 +499,21 @@ def test_overlay_configs_are_valid_for_the_native_binary(tmp_path):
     from conftest import make_locked
 
     make_locked("core")
+    base = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "ConfigMap")
+    values = {"base": base["data"]["config.yaml"]}
     for overlay in ("ondevice", "pmc", "docker", "nonroot", "stress"):
         (k,) = _docs(f"deploy/k8s/overlays/{overlay}/kustomization.yaml")
-        value = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "ConfigMap")["patch"])[0]["value"]
-        f = tmp_path / f"{overlay}.yaml"
+        values[overlay] = yaml.safe_load(next(p for p in k["patches"]
+                                              if p["target"]["kind"] == "ConfigMap")["patch"])[0]["value"]
+    for name, value in values.items():
+        f = tmp_path / f"{name}.yaml"
         f.write_text(value)
         r = subprocess.run([os.path.join(ROOT, "bin", "gpumon-exporter"), "--config", str(f), "--print-config"],
                            capture_output=True, text=True, timeout=30)
-        assert r.returncode == 0, (overlay, r.stderr[-1000:])
-        assert "unknown" not in r.stderr.lower(), (overlay, r.stderr[-1000:])
+        assert r.returncode == 0, (name, r.stderr[-1000:])
+        # the native binary is the image's entrypoint: no key it would ignore, no unknown key
+        assert "unknown" not in r.stderr.lower() and "not used" not in r.stderr, (name, r.stderr[-1000:])
+        assert json.loads(r.stdout)["listen"] == ":9400", name
 
 
 def test_stress_overlay_is_10hz_end_to_end():

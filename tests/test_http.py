@@ -179,17 +179,15 @@ def test_exact_window_quantiles_match_the_recorded_durations(mock_exporter):
 
 
 def test_port_conflict_reports_error(core):
+    """One listening socket per server and no SO_REUSEPORT: a second exporter on a taken port fails
+    with EADDRINUSE instead of sharing the scrapes (tests/test_listen.py covers both entry points)."""
     a = core.Exporter({"backend": "mock", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0})
     a.start()
     try:
         b = core.Exporter({"backend": "mock", "listen_addr": "127.0.0.1", "port": a.port, "interval_s": 0})
-        # SO_REUSEPORT lets a second exporter bind the same port only for the same user; either it
-        # starts (shared port) or it fails loudly -- it must never hang.
-        try:
+        with pytest.raises(RuntimeError, match="Address already in use"):
             b.start()
-            b.stop()
-        except RuntimeError as e:
-            assert "bind" in str(e)
+        b.stop()
     finally:
         a.stop()
 
@@ -419,7 +417,13 @@ def test_bad_listen_address_is_reported_and_cleaned_up(core):
     def threads():
         return len(os.listdir("/proc/self/task"))
 
-    base = threads()
+    # threads of earlier tests in this worker (server / sink daemons) may still be exiting
+    base, deadline = threads(), time.time() + 5
+    while time.time() < deadline:
+        time.sleep(0.2)
+        if threads() == base:
+            break
+        base = threads()
     ex = core.Exporter({"backend": "mock:gpus=4", "listen_addr": "not-an-address", "port": 0, "interval_s": 0,
                         "http_threads": 2})
     with pytest.raises(RuntimeError, match="bad listen address not-an-address"):
@@ -427,16 +431,16 @@ def test_bad_listen_address_is_reported_and_cleaned_up(core):
     assert threads() >= base + 4  # one device worker per GPU is running
     ex.stop()
     ex.stop()  # idempotent
-    assert threads() == base
+    assert threads() <= base
     ex = core.Exporter({"backend": "mock:gpus=4", "listen_addr": "not-an-address", "port": 0, "interval_s": 0})
     with pytest.raises(RuntimeError):
         ex.start()
     del ex  # the destructor alone
     gc.collect()
     deadline = time.time() + 5
-    while threads() != base and time.time() < deadline:
+    while threads() > base and time.time() < deadline:
         time.sleep(0.01)
-    assert threads() == base
+    assert threads() <= base
 
 
 def _raw_exchange(port, data):
@@ -590,3 +594,46 @@ def test_trickled_header_is_dropped(monkeypatch, mock_exporter):
     k.sendall(b"GET /healthz HTTP/1.1\r\nHost: x\r\n\r\n")
     assert k.recv(100).startswith(b"HTTP/1.1 200")
     k.close()
+
+
+def test_gzip_is_lazy_until_scrapes_keep_asking_for_it(mock_exporter):
+    """The snapshot is compressed at most once: by the first gzip scrape (lazy) while gzip scrapes
+    are rare, by the tick thread (eager, off the sample-to-export path) once 4 of the last 8
+    snapshots were scraped with gzip. A 1 Hz exporter scraped every 15 s compresses 1 tick in 15
+    (gzip was 2/3 of the tick thread's CPU at 8 GPUs, profiles/r5_cpu_8dev.md)."""
+    import gzip
+    import urllib.request
+
+    ex = mock_exporter(backend="mock:gpus=2", interval_s=0)
+
+    def gz_scrape():
+        req = urllib.request.Request(f"http://127.0.0.1:{ex.port}/metrics", headers={"Accept-Encoding": "gzip"})
+        with urllib.request.urlopen(req, timeout=5) as r:
+            assert r.headers.get("Content-Encoding") == "gzip"
+            return gzip.decompress(r.read())
+
+    for _ in range(10):
+        ex.tick()
+    st = ex.self_stats()
+    assert st["gzip_eager"] == 0 and st["gzip_lazy"] == 0  # nobody asked: nothing compressed
+    body = gz_scrape()
+    assert body == ex.metrics_text().encode()
+    gz_scrape()  # same snapshot: compressed once
+    assert ex.self_stats()["gzip_lazy"] == 1
+    for _ in range(6):  # a gzip scrape per tick
+        ex.tick()
+        gz_scrape()
+    st = ex.self_stats()
+    assert st["gzip_eager"] >= 2 and st["gzip_lazy"] == 4, st
+    lazy = st["gzip_lazy"]
+    for _ in range(4):
+        ex.tick()
+        gz_scrape()
+    assert ex.self_stats()["gzip_lazy"] == lazy  # eager now: scrapes find it compressed
+    for _ in range(12):  # scrapes stop: eager stops within a few ticks, unused ones counted
+        ex.tick()
+    e0 = ex.self_stats()["gzip_eager"]
+    for _ in range(5):
+        ex.tick()
+    st = ex.self_stats()
+    assert st["gzip_eager"] == e0 and st["gzip_unused"] >= 1

@@ -1,0 +1,112 @@
+"""The runtime image is a plain base plus the native exporter's file closure (deploy/Dockerfile,
+deploy/image_closure.py). Reference: `python:3` + requests + gpu.py (/root/reference/Dockerfile:1-7).
+
+The closure is staged into a temporary root the way the build stage stages /rootfs. The staged
+exporter then runs with the library search limited to that root. Its /proc/<pid>/maps may hold only
+staged files and glibc. The libraries it dlopens (libamd_smi for the amdsmi backend, libssl /
+libcrypto for an https:// push) must come from the staged copies. On the GPU box
+`tools/gpu_run.sh RUN closure` runs the same check with the real backend and the PMC overlay, whose
+helper process maps the ROCm runtimes.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "deploy"))
+import image_closure as ic  # noqa: E402
+
+
+def test_closure_lists_the_product_and_its_dlopen_libraries():
+    c = ic.closure()
+    assert c["missing"] == [], c["missing"]
+    files = c["files"]
+    assert files["/opt/gpumon/bin/gpumon-exporter"] == os.path.join(ROOT, "bin", "gpumon-exporter")
+    names = {os.path.basename(p) for p in files}
+    for want in ("libamd_smi.so.", "librocm_smi64.so.", "libssl.so.3", "libcrypto.so.3", "libz.so."):
+        assert any(n.startswith(want) for n in names), (want, sorted(names))
+    assert "/etc/ssl/certs/ca-certificates.crt" in files
+    # glibc comes from the base image; no Python, no HIP / HSA runtime in the base closure
+    assert not any(n.startswith(("libc.so", "libpython", "libamdhip64", "libhsa-runtime")) for n in names), names
+    # the names the code dlopens resolve through the staged symlink chain
+    assert any(l.endswith("/libamd_smi.so.26") for l in c["links"]) or "/opt/rocm/lib/libamd_smi.so.26" in files
+    size = sum(os.path.getsize(os.path.realpath(s)) for s in files.values())
+    assert size < 64 << 20, size  # the ROCm dev base it replaces is several GB
+
+
+def test_overlay_closure_adds_the_helper_and_its_runtimes():
+    base, ov = ic.closure(), ic.closure(overlays=True)
+    assert ov["missing"] == [], ov["missing"]
+    extra = {os.path.basename(p) for p in set(ov["files"]) - set(base["files"])}
+    for want in ("libgpumon_pmc.so", "libgpumon_probe.so", "gpumon-ondevice-helper", "counter_defs.yaml"):
+        assert want in extra, (want, sorted(extra))
+    assert any(n.startswith("librocprofiler-sdk.so") for n in extra)
+    assert any(n.startswith("libhsa-amd-aqlprofile64.so") for n in extra)
+    assert "/opt/gpumon/lib/gpumon-ondevice-helper" in ov["files"]
+
+
+@pytest.fixture(scope="module")
+def staged(tmp_path_factory):
+    root = str(tmp_path_factory.mktemp("rootfs"))
+    c = ic.stage(root)
+    assert c["missing"] == []
+    return root
+
+
+def test_staged_tree_shape(staged):
+    assert os.access(staged + "/opt/gpumon/bin/gpumon-exporter", os.X_OK)
+    assert open(staged + "/etc/ld.so.conf.d/gpumon-rocm.conf").read().strip() == f"{ic.ROCM}/lib"
+    assert os.path.realpath(staged + "/opt/rocm/lib/libamd_smi.so.26").startswith(staged)
+
+
+@pytest.mark.parametrize("backend,want_libs", [
+    ("mock:gpus=1", ["libssl.so.3", "libcrypto.so.3", "libstdc++.so.6"]),
+    ("amdsmi", ["libamd_smi.so.26", "libssl.so.3"]),
+])
+def test_staged_exporter_maps_only_the_closure_and_glibc(staged, backend, want_libs):
+    """The staged binary runs with LD_LIBRARY_PATH limited to the staged tree; an https:// push URL
+    makes it load OpenSSL at startup (check_push_config). Everything mapped is staged or glibc."""
+    r = ic.run_check(staged, ["--backend", backend],
+                     env_extra={"INFLUXDB_URL": "https://127.0.0.1:9/write?db=k8s"}, settle_s=1.0)
+    assert r.get("error") is None, r
+    assert r["outside"] == [], r["outside"]
+    mapped = r["staged_libs_mapped"]
+    for w in want_libs:
+        assert any(m.startswith(w) for m in mapped), (w, mapped)
+    if backend.startswith("mock"):
+        assert r["gpu_up"] == ['gpu_up{host="no_name",gpu_id="0"} 1'] and r["ok"]
+
+
+def test_check_detects_a_library_outside_the_closure(tmp_path):
+    """Not vacuous: a closure missing a library the binary needs (libz removed from the staged
+    tree) makes the loader fall back to the host's copy, and the check reports that mapping."""
+    root = str(tmp_path / "rootfs")
+    ic.stage(root)
+    for d, _, files in os.walk(root):
+        for f in files:
+            if f.startswith("libz.so"):
+                os.remove(os.path.join(d, f))
+    for d, _, files in os.walk(root):  # dangling links too
+        for f in list(files):
+            p = os.path.join(d, f)
+            if f.startswith("libz.so") and os.path.islink(p):
+                os.remove(p)
+    r = ic.run_check(root, ["--backend", "mock:gpus=1"], settle_s=0.5)
+    assert any(os.path.basename(p).startswith("libz.so") for p in r["outside"]), r
+    assert not r["ok"]
+
+
+def test_cli_list_and_stage(tmp_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "deploy", "image_closure.py"), "list"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["missing"] == [] and d["bytes"] > 0
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "deploy", "image_closure.py"), "stage", "--root",
+                        str(tmp_path / "rootfs")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert json.loads(r.stdout)["files"] == len(d["files"])

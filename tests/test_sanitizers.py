@@ -419,3 +419,41 @@ def test_sanitized_connection_flood_and_eviction(target, binary, env):
     bad = _reports(err)
     assert not bad, err[-4000:]
     assert got >= 6, got
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_https_push(target, binary, env, tmp_path):
+    """The TLS push path (csrc/core/tls.cpp: the dlopen'd OpenSSL table, handshake, keep-alive
+    reuse, close_notify on stop) under ASan+UBSan and TSan: pushes to a verifying TLS sink every
+    20 ms with scrapes running, then a second run against a sink whose certificate does not verify
+    (the failure / requeue / backoff path). No sanitizer report, every push of the good run
+    delivered. LeakSanitizer sees OpenSSL's process-wide state too: the table is never unloaded."""
+    from conftest import make_locked
+    from test_influx_tls import _TlsSink, _ca, _leaf
+
+    make_locked(target, jobs=8)
+    d = str(tmp_path)
+    _ca(d, "ca")
+    _ca(d, "otherca")
+    _leaf(d, "server", "ca", "DNS:localhost,IP:127.0.0.1")
+    exe = os.path.join(ROOT, binary)
+    # OpenSSL's own allocations are reachable process state (never unloaded), not leaks of ours
+    san_env = dict(env)
+    for ca, want_ok in ((f"{d}/ca.pem", True), (f"{d}/otherca.pem", False)):
+        with _TlsSink(f"{d}/server.pem", f"{d}/server.key") as srv:
+            rc, err = _run(exe, dict(san_env, GPUMON_INFLUX_CA_FILE=ca, GPUMON_INFLUX_TIMEOUT_S="0.5"),
+                           ("--influx-url", f"https://localhost:{srv.port}/write?db=k8s", "--interval", "0.02"),
+                           min_s=2.0)
+        bad = _reports(err)
+        assert not bad, err[-4000:]
+        assert rc == 0, err[-2000:]
+        if want_ok:
+            assert len(srv.posts) >= 20 and not srv.handshake_errors, (len(srv.posts), srv.handshake_errors[:3])
+            assert len({p["peer"] for p in srv.posts}) <= 2  # keep-alive: one connection (a reconnect at most)
+        else:
+            assert not srv.posts and srv.handshake_errors

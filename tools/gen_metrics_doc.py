@@ -141,6 +141,18 @@ def collect():
         ex.tick()
         add(_families(ex), "http_rt_priority")
     ex.stop()
+    # gzip scrapes on every tick: the snapshot compression counters (eager after 4 of 8 gzip-scraped ticks)
+    import urllib.request
+
+    ex = c.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0, "host": "node"})
+    ex.start()
+    for _ in range(8):
+        ex.tick()
+        req = urllib.request.Request(f"http://127.0.0.1:{ex.port}/metrics", headers={"Accept-Encoding": "gzip"})
+        urllib.request.urlopen(req, timeout=5).read()
+    ex.tick()
+    add(_families(ex), "gzip scrapes")
+    ex.stop()
     # backend-specific self-metrics: the libamd_smi backend over the fake library
     saved = os.environ.get("FAKE_AMDSMI_GPUS")  # the fake reads it at init; leave the caller's env as it was
     os.environ["FAKE_AMDSMI_GPUS"] = "1"
