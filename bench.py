@@ -614,6 +614,19 @@ def main() -> int:
         for what in ("verified", "unverified", "mismatch"):
             for _, lab, v in fam.get(f"gpumon_xgmi_slot_map_{what}", {}).get("samples", []):
                 slot_map.setdefault(lab.get("gpu_id"), {})[what] = int(v)
+        # rows per GPU: a multi-rank tenant's ranks open every GPU; the first 8-GPU
+        # record must show whether each GPU carries one workload row (peer contexts hidden) or N
+        active = {lab.get("gpu_id"): int(v) for _, lab, v in fam.get("gpu_active_processes", {}).get("samples", [])}
+        stat_ids = [st.get("gpu_id", str(i)) for i, st in enumerate(mon.ex.statics())]
+        per_gpu_rows = []
+        for i, g in enumerate(stat_ids):
+            wr = [r for r in rows if not r["idle"] and r["dev"] == i]
+            per_gpu_rows.append({"gpu": i, "gpu_id": g, "rows": len(wr), "pids": sorted(r["pid"] for r in wr)[:8],
+                                 "idle_rows": sum(1 for r in rows if r["idle"] and r["dev"] == i),
+                                 "active_processes": active.get(g)})
+        rows_per_user = {}
+        for r in rows:
+            rows_per_user[r["user_name"]] = rows_per_user.get(r["user_name"], 0) + 1
         per_gpu = _per_gpu_xgmi(tick_rates, dev_rows, exp_tx, exp_rx) if xgmi is not None else None
         if xgmi is not None:
             tx = [r["exporter_tx_GBps"] for r in per_gpu if r["exporter_tx_GBps"] is not None]
@@ -722,6 +735,10 @@ def main() -> int:
                            "busy_pct": _r(r["proc_gfx_util"], 1)}
                           for r in rows if not r["idle"]][:16],
             "occupancy_reads": s1.get("occupancy_reads", 0) - s0.get("occupancy_reads", 0),
+            "per_gpu_rows": per_gpu_rows,
+            "rows_per_user": rows_per_user,
+            "hidden_contexts": s1.get("hidden_contexts"),
+            "hidden_peer_contexts": s1.get("hidden_peer_contexts"),
             "xgmi": xgmi,
             "xgmi_slot_map": slot_map or None,
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,

@@ -96,6 +96,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "stale_hold_s", &c.stale_hold_s);
   get(d, "hide_empty_contexts", &c.hide_empty_contexts);
   get(d, "mfma_exclusive_window_s", &c.mfma_exclusive_window_s);
+  get(d, "peer_context_max_vram_mib", &c.peer_context_max_vram_mib);
   get(d, "sample_threads", &c.sample_threads);
   get(d, "rt_priority", &c.rt_priority);
   get(d, "influx_url", &c.influx_url);
@@ -897,6 +898,7 @@ PYBIND11_MODULE(_core, m) {
              d["http_evicted"] = s.http_evicted;
              d["http_max_conns"] = s.http_max_conns;
              d["hidden_contexts"] = s.hidden_contexts;
+             d["hidden_peer_contexts"] = s.hidden_peer_contexts;
              d["rt_threads"] = s.rt_threads;
              d["overruns"] = s.overruns;
              d["scrapes"] = s.scrapes;

@@ -343,6 +343,7 @@ bool Exporter::files_poll_once() {
     if (!logs_ok) GPUMON_LOG(LogLevel::kWarn, "kubelet-files", "pod log tree: " + err);
   }
   std::vector<Allocation> allocs;
+  std::vector<std::vector<std::string>> alloc_ids;  // per allocation: every id of its container
   size_t unknown = 0;
   if (!cfg_.device_checkpoint.empty()) {
     std::vector<CheckpointEntry> entries;
@@ -354,11 +355,13 @@ bool Exporter::files_poll_once() {
       std::lock_guard<std::mutex> g(state_mu_);
       st = *statics_;
     }
-    std::unordered_map<std::string, const ContainerMeta*> by_uid_ctr;
+    // every container id the log tree knows per (pod uid, container name): a restarted container
+    // leaves the dead instance's log link until garbage collection, next to the live one
+    std::unordered_map<std::string, std::vector<const ContainerMeta*>> by_uid_ctr;
     std::unordered_map<std::string, const ContainerMeta*> by_uid;
     for (const auto& m : metas)
       if (!m.pod_uid.empty()) {
-        by_uid_ctr[m.pod_uid + "/" + m.container_name] = &m;
+        by_uid_ctr[m.pod_uid + "/" + m.container_name].push_back(&m);
         by_uid.emplace(m.pod_uid, &m);
       }
     for (const auto& c : entries) {
@@ -366,6 +369,11 @@ bool Exporter::files_poll_once() {
       const auto pod = by_uid.find(c.pod_uid);
       if (pod == by_uid.end()) continue;  // not (or no longer) on this node
       const auto ctr = by_uid_ctr.find(c.pod_uid + "/" + c.container_name);
+      std::vector<std::string> ids;
+      if (ctr != by_uid_ctr.end())
+        for (const ContainerMeta* m : ctr->second)
+          if (!m->container_id.empty() && std::find(ids.begin(), ids.end(), m->container_id) == ids.end())
+            ids.push_back(m->container_id);
       for (const auto& id : c.device_ids) {
         const int idx = match_device_id(id, st);
         if (idx < 0) {
@@ -377,26 +385,38 @@ bool Exporter::files_poll_once() {
         a.pod_name = pod->second->pod_name;
         a.pod_uid = c.pod_uid;
         a.container_name = c.container_name;
-        if (ctr != by_uid_ctr.end()) a.container_id = ctr->second->container_id;
+        if (!ids.empty()) a.container_id = ids.front();
         a.gpu_index = idx;
         allocs.push_back(std::move(a));
+        alloc_ids.push_back(ids);
       }
     }
   }
   size_t exited = 0;
   // one /proc/*/cgroup pass per refresh, only when these allocations are used (publish_allocations:
-  // not while PodResources is polled) and some carry a container id to check
+  // not while PodResources is polled) and some carry a container id to check. An allocation is
+  // running when ANY of its container's known ids has a live process, and then carries that id.
   if (cfg_.pod_resources_socket.empty() &&
       std::any_of(allocs.begin(), allocs.end(), [](const Allocation& a) { return !a.container_id.empty(); })) {
     std::unordered_set<std::string> running;
     if (running_container_ids(cfg_.attribution.procfs_root, &running)) {
-      const size_t before = allocs.size();
-      allocs.erase(std::remove_if(allocs.begin(), allocs.end(),
-                                  [&](const Allocation& a) {
-                                    return !a.container_id.empty() && !running.count(a.container_id);
-                                  }),
-                   allocs.end());
-      exited = before - allocs.size();
+      std::vector<Allocation> kept;
+      for (size_t i = 0; i < allocs.size(); ++i) {
+        Allocation& a = allocs[i];
+        if (a.container_id.empty()) {
+          kept.push_back(std::move(a));
+          continue;
+        }
+        const auto& ids = alloc_ids[i];
+        auto live = std::find_if(ids.begin(), ids.end(), [&](const std::string& id) { return running.count(id) > 0; });
+        if (live == ids.end()) {
+          exited++;
+          continue;
+        }
+        a.container_id = *live;
+        kept.push_back(std::move(a));
+      }
+      allocs.swap(kept);
     }
   }
   const size_t n_metas = metas.size();

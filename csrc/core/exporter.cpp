@@ -339,18 +339,20 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
       ps.occ_samples = n;
       ps.occ_busy = busy;
     }
-    // A listed process that no sub-sample saw (it arrived after the last scan, or the scans are in
-    // their retry backoff) gets one read now, so its first row is not empty.
+    // A listed process that arrived since the last list (no sub-sample could know it) gets one read
+    // now, so its first row is not empty. Only new pids: a known pid whose reads keep returning
+    // nothing (NaN) would otherwise cost an extra open on the tick's path every tick.
     if (occ_on) {
       std::vector<uint32_t> unread;
       for (const auto& ps : p)
-        if (ps.occ_samples == 0) unread.push_back(ps.pid);
+        if (ps.occ_samples == 0 && std::find(occ_pids.begin(), occ_pids.end(), ps.pid) == occ_pids.end())
+          unread.push_back(ps.pid);
       if (!unread.empty()) {
         backend->occupancy(i, unread, &vals);
         occ_reads->fetch_add(unread.size(), std::memory_order_relaxed);
         size_t k = 0;
         for (auto& ps : p)
-          if (ps.occ_samples == 0 && k < vals.size()) {
+          if (ps.occ_samples == 0 && k < vals.size() && ps.pid == unread[k]) {
             const double v = vals[k++];
             if (!has(v)) continue;
             ps.cu_occupancy = v;
@@ -359,15 +361,19 @@ static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_
           }
       }
     }
-    // a failed tick (or a failed process list) listed nothing: keep sub-sampling the known pids
+    // a failed tick (or a failed process list) listed nothing: keep sub-sampling the known pids.
+    // The sums restart every tick either way: a failed list's interval is not folded into the next
+    // good tick's mean (two intervals averaged as one); the held rows carry no occupancy.
     if (occ_on && procs && ok_for_ras && s.procs_read >= 0) {
       occ_pids.clear();
       for (const auto& ps : p)
         if (std::find(occ_pids.begin(), occ_pids.end(), ps.pid) == occ_pids.end()) occ_pids.push_back(ps.pid);
+      next_occ = mono_ns() + occ_period_ns;
+    }
+    if (occ_on && procs) {
       occ_sum.assign(occ_pids.size(), 0.0);
       occ_n.assign(occ_pids.size(), 0);
       occ_busy.assign(occ_pids.size(), 0);
-      next_occ = mono_ns() + occ_period_ns;
     }
     {
       std::lock_guard<std::mutex> g(w->mu);
@@ -913,6 +919,41 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       "cu_occupancy read, or arrived holding VRAM; source=vram: every process holding VRAM (occupancy "
       "unreadable); source=allocations: pods allocated the GPU (process list off).";
   std::vector<ExtraSeries> sharing;
+  // Peer contexts of multi-GPU processes (the usual 8-GPU tenant: torchrun with one rank per GPU,
+  // each rank's runtime also opening every other GPU, RCCL importing peers' buffers). A (pid, GPU)
+  // context is a peer context -- not a workload row, not a sharer -- when on that GPU it holds at
+  // most peer_context_max_vram_mib, had no wave resident within the sharing window (where
+  // occupancy is readable), and the same process has a workload context on ANOTHER GPU this tick
+  // (more VRAM than that, or waves). The reference listed one row per compute app nvidia-smi
+  // showed on a GPU (gpu.py:111-116,178,190-219): a rank appears on its own GPU only.
+  if (last_waves_.size() < procs.size()) last_waves_.resize(procs.size());
+  const double peer_floor = std::max(0.0, cfg_.peer_context_max_vram_mib) * 1048576.0;
+  std::unordered_map<uint32_t, std::vector<int>> workload_devs;  // pid -> GPUs with a workload context
+  std::vector<std::unordered_map<uint32_t, double>> vram_of(procs.size());  // (dev, pid) -> VRAM, contexts summed
+  for (size_t d = 0; d < procs.size(); ++d) {
+    auto& waves = last_waves_[d];
+    for (const auto& p : procs[d]) {
+      if (is_helper(p.pid)) continue;
+      const double v = p.vram_bytes > 0 ? p.vram_bytes : (p.mem_bytes > 0 ? p.mem_bytes : 0.0);
+      vram_of[d][p.pid] += v;
+      if (p.occ_busy > 0 || p.cu_occupancy > 0) waves[p.pid] = {tick_no, now_ns};
+    }
+    for (auto it = waves.begin(); it != waves.end();) {  // forget pids past both windows
+      if (tick_no - it->second.first >= 5 && now_ns - it->second.second >= window_ns) it = waves.erase(it);
+      else ++it;
+    }
+    for (const auto& [pid, v] : vram_of[d])
+      if (v > peer_floor || waves.count(pid)) workload_devs[pid].push_back(static_cast<int>(d));
+  }
+  auto is_peer = [&](size_t d, uint32_t pid) {
+    if (peer_floor <= 0 || !cfg_.hide_empty_contexts) return false;
+    if (last_waves_[d].count(pid)) return false;
+    auto v = vram_of[d].find(pid);
+    if (v != vram_of[d].end() && v->second > peer_floor) return false;
+    auto w = workload_devs.find(pid);
+    return w != workload_devs.end() &&
+           std::any_of(w->second.begin(), w->second.end(), [&](int o) { return o != static_cast<int>(d); });
+  };
   for (size_t d = 0; d < procs.size(); ++d) {
     if (!cfg_.processes) {  // no process list: the kubelet's allocations are what is known
       std::vector<std::pair<std::string, std::string>> pods;
@@ -934,7 +975,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
     std::vector<uint32_t> active;  // distinct pids (one process may hold several KFD contexts)
     std::unordered_set<uint32_t> listed;
     for (const auto& p : procs[d]) {
-      if (is_helper(p.pid)) continue;
+      if (is_helper(p.pid) || is_peer(d, p.pid)) continue;
       const bool holds = p.vram_bytes > 0 || p.mem_bytes > 0;
       const bool waves = p.occ_busy > 0 || p.cu_occupancy > 0;
       if (holds || waves) listed.insert(p.pid);
@@ -967,7 +1008,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
                      "pod_gpu rows and gpu_active_processes.",
                      "gauge", -1, {}, static_cast<double>(helper_rows)});
   set_extra("sharing", std::move(sharing));
-  uint64_t hidden = 0;
+  uint64_t hidden = 0, hidden_peer = 0;
   std::vector<uint32_t> alive;
   std::unordered_map<ProcKey, ProcPrev, ProcKeyHash> next_prev;
   // (ns, pod, container, dev) with an active process -> suppress the idle row for it
@@ -994,6 +1035,10 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       if (cfg_.hide_empty_contexts && !(p.vram_bytes > 0) && !(p.mem_bytes > 0) && !(p.cu_occupancy > 0) &&
           p.occ_busy == 0) {
         hidden++;
+        continue;
+      }
+      if (is_peer(d, p.pid)) {  // a multi-GPU process's context on a GPU it does not work on (above)
+        hidden_peer++;
         continue;
       }
       alive.push_back(p.pid);
@@ -1054,6 +1099,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
   }
   proc_prev_.swap(next_prev);
   hidden_contexts_ = hidden;
+  hidden_peer_contexts_ = hidden_peer;
   attr_->gc(alive);
   // Allocated-but-idle GPUs (reference gpu.py:220-253 via `docker exec nvidia-smi -L`; here the
   // kubelet PodResources allocation list pushed by the control plane).
@@ -1229,6 +1275,12 @@ TickInfo Exporter::tick() {
         if (proc_hold_[i] >= 0 && proc_hold_[i] < kProcHoldTicks && last_procs_[i] &&
             i < static_cast<int>(last_procs_[i]->procs.size())) {
           procs[i] = last_procs_[i]->procs[i];
+          // the held list's occupancy is the last good tick's: not a reading of this interval
+          for (auto& hp : procs[i]) {
+            hp.cu_occupancy = kNaN;
+            hp.occ_samples = 0;
+            hp.occ_busy = 0;
+          }
           proc_hold_[i]++;
           s.procs_held = true;
         }
@@ -1768,6 +1820,7 @@ SelfStats Exporter::self_stats() const {
   s.occupancy_scan_failures = scan_failures_->load(std::memory_order_relaxed);
   s.process_list_failures = proc_failures_.load(std::memory_order_relaxed);
   s.hidden_contexts = hidden_contexts_.load();
+  s.hidden_peer_contexts = hidden_peer_contexts_.load();
   s.rt_threads = rt_threads_->load();
   if (server_) {
     s.http_evicted = static_cast<int64_t>(server_->evicted());

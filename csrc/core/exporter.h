@@ -82,6 +82,10 @@ struct ExporterConfig {
   // arrived (VRAM held) within that window (a tenant resident 10 % of the time escapes one tick's
   // 20 occupancy reads 12 % of the time, a 5 s window's 100 reads 0.003 %)
   double mfma_exclusive_window_s = 5.0;
+  // A multi-GPU process's context on a GPU it does not work on (no waves there within the window,
+  // at most this much VRAM, a workload context on another GPU) is a peer context: no pod_gpu row,
+  // not a sharer (exporter.cpp build_pod_rows). 0 = off.
+  double peer_context_max_vram_mib = 512.0;
   AttributionConfig attribution;
   RateConfig rates;
   std::string influx_url;             // INFLUXDB_URL; empty = push disabled
@@ -351,6 +355,9 @@ class Exporter {
   bool seq_maintain_ = false;  // sequential tick: run Backend::maintain after the publish
   std::map<int, double> mfma_util_;  // set_device_mfma_util (guarded by extra_mu_)
   std::atomic<uint64_t> hidden_contexts_{0};  // empty GPU contexts left out of the last tick's rows
+  std::atomic<uint64_t> hidden_peer_contexts_{0};  // peer contexts of multi-GPU processes, same
+  // per device: pid -> (tick, mono ns) its waves were last resident (peer-context rule; sampler thread)
+  std::vector<std::unordered_map<uint32_t, std::pair<uint64_t, int64_t>>> last_waves_;
   // cu_occupancy sub-sample reads by the workers (shared: a detached worker may outlive a restart)
   std::shared_ptr<std::atomic<uint64_t>> occ_reads_ = std::make_shared<std::atomic<uint64_t>>(0);
   std::shared_ptr<std::atomic<uint64_t>> scan_failures_ = std::make_shared<std::atomic<uint64_t>>(0);

@@ -78,6 +78,7 @@ struct Conn {
   std::list<int>::iterator lru;  // position in Loop::lru (least recently active first)
   int64_t req_ns = 0;
   std::string path;
+  uint32_t served = 0;  // requests answered on this connection (a scraper's keep-alive has > 0)
 };
 
 bool set_nonblock(int fd) {
@@ -520,6 +521,7 @@ void HttpServer::run(Loop* L) {
         handler_(req, &resp);
       }
       requests_.fetch_add(1, std::memory_order_relaxed);
+      if (resp.status < 400) c.served++;
       c.req_ns = t_req;
       c.path = req.path;
       c.in.erase(0, static_cast<size_t>(used));
@@ -587,6 +589,13 @@ void HttpServer::run(Loop* L) {
       }
     }
     for (int i = 0; i < n; ++i) {
+      // the RT budget is also checked inside a batch (every 32 events): one batch of up to 256
+      // events must not run past the budget at SCHED_FIFO
+      if (fifo && i > 0 && (i & 31) == 0 && thread_cpu_ns() - win_cpu0 > budget_ns && set_fifo(0) == 0) {
+        fifo = false;
+        rt_loops_.fetch_sub(1);
+        rt_demotions_.fetch_add(1, std::memory_order_relaxed);
+      }
       int fd = evs[i].data.fd;
       if (fd == L->wake) continue;
       if (fd == L->lfd) {
@@ -604,14 +613,22 @@ void HttpServer::run(Loop* L) {
             break;
           }
           if (L->conns.size() >= max_conns_) {
-            // full: make room by closing the least recently active connection that is not
-            // sending a response (idle or half-open floods age out first), else refuse this one
-            int victim = -1;
+            // full: make room by closing a connection that is not sending a response, else refuse
+            // this one. Preference, least recently active first within each class:
+            //   0 never answered a request, nothing pending (a connect flood's idle sockets)
+            //   1 never answered, a request partly read (a trickler)
+            //   2 answered before, idle now (Prometheus' keep-alive between scrapes: kept longest)
+            //   3 answered before, a request partly read
+            int victim = -1, best = 4;
             for (int vfd : L->lru) {  // oldest first; a connection mid-response is skipped
               auto vit = L->conns.find(vfd);
-              if (vit != L->conns.end() && !vit->second.writing) {
+              if (vit == L->conns.end() || vit->second.writing) continue;
+              const Conn& vc = vit->second;
+              const int cls = (vc.served > 0 ? 2 : 0) + (vc.in.empty() ? 0 : 1);
+              if (cls < best) {
+                best = cls;
                 victim = vfd;
-                break;
+                if (cls == 0) break;
               }
             }
             if (victim < 0) {

@@ -237,6 +237,7 @@ const std::map<std::string, Setter>& setters() {
       {"stale_hold_s", dbl_at([](NativeOptions* o) { return &o->cfg.stale_hold_s; })},
       {"hide_empty_contexts", bool_at([](NativeOptions* o) { return &o->cfg.hide_empty_contexts; })},
       {"mfma_exclusive_window_s", dbl_at([](NativeOptions* o) { return &o->cfg.mfma_exclusive_window_s; })},
+      {"peer_context_max_vram_mib", dbl_at([](NativeOptions* o) { return &o->cfg.peer_context_max_vram_mib; })},
       {"sample_threads", int_at([](NativeOptions* o) { return &o->cfg.sample_threads; })},
       {"rt_priority", int_at([](NativeOptions* o) { return &o->cfg.rt_priority; })},
       {"device_timeout_s", dbl_at([](NativeOptions* o) { return &o->cfg.device_timeout_s; })},
@@ -518,6 +519,7 @@ std::string options_json(const NativeOptions& o) {
   N("stale_hold_s", c.stale_hold_s);
   B("hide_empty_contexts", c.hide_empty_contexts);
   N("mfma_exclusive_window_s", c.mfma_exclusive_window_s);
+  N("peer_context_max_vram_mib", c.peer_context_max_vram_mib);
   N("sample_threads", c.sample_threads);
   N("rt_priority", c.rt_priority);
   N("device_timeout_s", c.device_timeout_s);

@@ -825,6 +825,15 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       f.add(hl, static_cast<double>(s.hidden_contexts));
     }
     {
+      Family f(o, "gpumon_hidden_peer_gpu_contexts",
+               "GPU contexts of multi-GPU processes on GPUs they do not work on (at most "
+               "peer_context_max_vram_mib of VRAM there, no resident waves in the sharing window, a workload "
+               "context on another GPU: e.g. every torchrun rank opening all GPUs), left out of the pod_gpu rows "
+               "and gpu_active_processes.",
+               "gauge");
+      f.add(hl, static_cast<double>(s.hidden_peer_contexts));
+    }
+    {
       Family f(o, "gpumon_sampler_rt_threads",
                "Sampler and device-worker threads running SCHED_FIFO (rt_priority > 0 and CAP_SYS_NICE).", "gauge");
       f.add(hl, static_cast<double>(s.rt_threads));

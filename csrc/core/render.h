@@ -65,6 +65,7 @@ struct SelfStats {
   uint64_t process_list_failures = 0;  // failed process lists (the last good one held kProcHoldTicks)
   uint64_t occupancy_scan_failures = 0;  // ... process listings that failed (retried with a backoff)
   uint64_t hidden_contexts = 0;     // GPU contexts without VRAM or waves left out of pod_gpu rows
+  uint64_t hidden_peer_contexts = 0;  // peer contexts of multi-GPU processes left out of pod_gpu rows
   int rt_threads = 0;               // sampler / device-worker threads running SCHED_FIFO (rt_priority)
   int http_rt_loops = -1;            // HTTP loops at SCHED_FIFO now (-1: http_rt_priority off)
   int64_t http_evicted = -1;

@@ -43,6 +43,7 @@ class Config:
     ras_async: bool = True                # device workers read RAS after publishing a tick (next tick carries it)
     hide_empty_contexts: bool = True      # no pod_gpu row for a GPU context with no VRAM and no waves
     mfma_exclusive_window_s: float = 5.0  # pod MFMA util only when no other process had waves in the last 5 ticks and this many seconds
+    peer_context_max_vram_mib: float = 512.0  # a multi-GPU process's context on a GPU it does not work on (<= this VRAM, no waves, a workload on another GPU): no row (0 = off)
     occ_samples: int = 20                 # KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)
     prewarm_ms: float = 3.0               # device workers wake the firmware-table path this long before each tick (0 = off)
     stale_hold_s: float = 0.1             # a repeated firmware table keeps the last rates only while it is this old (then: invalid)
@@ -155,6 +156,7 @@ class Config:
             "stale_hold_s": float(self.stale_hold_s),
             "hide_empty_contexts": bool(self.hide_empty_contexts),
             "mfma_exclusive_window_s": float(self.mfma_exclusive_window_s),
+            "peer_context_max_vram_mib": float(self.peer_context_max_vram_mib),
             "sample_threads": int(self.sample_threads),
             "rt_priority": int(self.rt_priority),
             "device_timeout_s": float(self.device_timeout_s),

@@ -61,6 +61,8 @@ def test_bench_single_process(dist):
     cap = d["capacity"]
     assert "error" not in cap, cap
     assert cap["interval_ms"] == 1.0 and cap["ticks_logged"] > 0 and cap["samples_per_sec_per_gpu"] > 100
+    assert [x["gpu"] for x in d["per_gpu_rows"]] == [0] and d["per_gpu_rows"][0]["active_processes"] is not None
+    assert "hidden_contexts" in d and "hidden_peer_contexts" in d and "rows_per_user" in d
 
 
 @pytest.mark.slow
@@ -140,6 +142,11 @@ def test_bench_eight_ranks_exact_scale_command():
     assert d["sampled_devices"] == 8 and d["config"]["interval_s"] == 1.0
     assert [x["hip_ordinal"] for x in d["devices"]] == list(range(8))
     assert len({x["gpu_id"] for x in d["devices"]}) == 8 and d["device_check"]["ok"]
+    # per-GPU row accounting in the SCALE record (one load process per rank here,
+    # each on its own GPU: one row per GPU, no peer context on the mock)
+    assert [x["gpu"] for x in d["per_gpu_rows"]] == list(range(8))
+    assert all(set(x) >= {"rows", "pids", "idle_rows", "active_processes"} for x in d["per_gpu_rows"])
+    assert d["hidden_peer_contexts"] == 0 and isinstance(d["rows_per_user"], dict)
     # 8 ranks' 256 MB gloo all-reduces share the builder's CPUs with the exporter: the last step's
     # reductions can run past its tick, so the whole-node rate is N / interval within 15 % here
     # (exact on the GPU node, where RCCL moves the bytes)

@@ -575,6 +575,78 @@ def test_connection_flood_under_a_low_fd_limit(tmp_path):
         p.wait(10)
 
 
+def test_flood_evicts_fresh_connections_before_the_scrapers_keep_alive(tmp_path):
+    """at the connection cap, eviction prefers connections that never completed a
+    request (idle ones, then ones holding a partial request) over a keep-alive connection that has
+    served scrapes, which sits idle between them. Prometheus keeps its connection through a connect
+    flood. One HTTP loop, RLIMIT_NOFILE 64: a cap of a few dozen connections."""
+    import http.client
+    import os
+    import resource
+    import subprocess
+    import time
+    import urllib.request
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+
+    def low_limit():
+        resource.setrlimit(resource.RLIMIT_NOFILE, (64, 64))
+
+    p = subprocess.Popen([os.path.join(root, "bin", "gpumon-exporter"), "--backend", "mock:gpus=1", "--interval",
+                          "0.1", "--listen", f"127.0.0.1:{port}", "--http-threads", "1", "--log-level", "error"],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, preexec_fn=low_limit)
+    flood = []
+    try:
+        deadline = time.time() + 20
+        while time.time() < deadline:
+            try:
+                urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=1).read()
+                break
+            except OSError:
+                time.sleep(0.05)
+        scraper = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+        scraper.request("GET", "/metrics")
+        assert scraper.getresponse().read()
+        local = scraper.sock.getsockname()
+        # trickling requests first (partial header), then idle sockets, 200 in all: far past the cap
+        for k in range(200):
+            c = socket.socket()
+            c.settimeout(2)
+            try:
+                c.connect(("127.0.0.1", port))
+                if k < 20:
+                    c.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n")  # no blank line: partial
+                flood.append(c)
+            except OSError:
+                c.close()
+            time.sleep(0.002)
+        for _ in range(3):  # the scraper's keep-alive connection survived the flood
+            scraper.request("GET", "/metrics")
+            r = scraper.getresponse()
+            assert r.status == 200 and r.read()
+        assert scraper.sock.getsockname() == local  # the same TCP connection, not a reconnect
+        # the tricklers (partial requests) outlived some of the idle sockets that came after them
+        alive_partial = 0
+        for c in flood[:20]:
+            c.setblocking(False)
+            try:
+                alive_partial += c.recv(1) != b""
+            except BlockingIOError:
+                alive_partial += 1
+            except OSError:
+                pass
+        assert alive_partial > 0
+    finally:
+        for c in flood:
+            c.close()
+        p.terminate()
+        p.wait(10)
+
+
 def test_trickled_header_is_dropped(monkeypatch, mock_exporter):
     """A client that sends part of a request header and then nothing is closed after the header
     timeout (GPUMON_HTTP_HEADER_TIMEOUT_S here; 10 s by default), not after the 60 s idle timeout."""

@@ -7,6 +7,8 @@ The reference needed the root-equivalent docker.sock for the same data
 import json
 import os
 
+import pytest
+
 from gpumon.export import promtext
 
 CID_A = "a" * 63 + "1"
@@ -106,6 +108,48 @@ def test_checkpoint_entry_of_a_finished_pod_is_not_an_idle_row(core, tmp_path):
         assert idle == [(0, "turing-gpu-notebook-alice-5d8f-x1")]
         fam = promtext.parse(ex.metrics_text())
         assert promtext.one(fam, "gpumon_kubelet_files_exited_allocations") == 1
+    finally:
+        ex.stop()
+
+
+@pytest.mark.parametrize("dead_link_first", [True, False])
+@pytest.mark.parametrize("old_cid", ["c" * 63 + "9", "0" * 63 + "1", "e" * 63 + "7", "9" * 63 + "5"])
+def test_restarted_container_keeps_its_allocation(core, tmp_path, dead_link_first, old_cid):
+    """after a container restart the kubelet keeps the dead instance's log link next to
+    the new one until garbage collection. Whichever readdir lists last, the allocation of the still
+    running pod stays an idle row carrying the LIVE instance's id, and is not counted as exited.
+    (readdir order is the filesystem's: several dead ids and both creation orders cover it.)"""
+    proc = tmp_path / "proc"
+    _fake_proc(proc, 2000, f"0::/kubepods.slice/kubepods-pod{UID_A.replace('-', '_')}.slice/"
+                           f"cri-containerd-{CID_A}.scope")  # the new notebook instance: running
+    _fake_proc(proc, 2001, f"0::/kubepods.slice/kubepods-pod{UID_B.replace('-', '_')}.slice/"
+                           f"cri-containerd-{CID_B}.scope")
+    logs = tmp_path / "log"
+    pod, ns, uid = "turing-gpu-notebook-alice-5d8f-x1", "ml", UID_A
+
+    def dead_link():  # the dead instance (restart count 0 -> 1): its log link is still there
+        (logs / "containers").mkdir(parents=True, exist_ok=True)
+        os.symlink(f"/var/log/pods/{ns}_{pod}_{uid}/notebook/0.log",
+                   logs / "containers" / f"{pod}_{ns}_notebook-{old_cid}.log")
+
+    # readdir order follows creation order on some filesystems: both orders are checked
+    if dead_link_first:
+        dead_link()
+    _log_tree(logs)
+    if not dead_link_first:
+        dead_link()
+    ckpt = tmp_path / "ckpt"
+    _checkpoint(ckpt)
+    ex = core.Exporter({"backend": "mock:gpus=3", "serve_http": False, "interval_s": 0, "host": "n1",
+                        "procfs_root": str(proc), "pod_log_root": str(logs), "device_checkpoint": str(ckpt)})
+    assert ex.start() == ""
+    try:
+        ex.tick()
+        idle = {r["dev"]: r for r in ex.pod_rows() if r["idle"]}
+        assert sorted(idle) == [0, 1]
+        assert idle[0]["podname"] == pod and idle[0]["containerid"] == CID_A[:12]
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpumon_kubelet_files_exited_allocations") == 0
     finally:
         ex.stop()
 

@@ -368,3 +368,65 @@ def test_time_process_lists_only_without_a_sampler(core):
             busy.time_process_lists(0, 1)
     finally:
         busy.stop()
+
+
+def test_unread_fallback_reads_new_pids_only(mock_exporter):
+    """the one-shot read for a listed process no sub-sample saw is for pids that arrived
+    since the last list. A known pid whose reads keep returning nothing (NaN) must not cost an
+    extra read on the tick's path every tick."""
+    import math
+
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", interval_s=30.0, occ_samples=20, sample_threads=-1,
+                       mock={"procs": [{"pid": 31, "device": 0, "kfd_only": True}]})
+    ex.mock_set_occ_series(0, [float("nan")])  # cu_occupancy unreadable for this process
+    ex.tick()  # pid 31 is known from here on (its first tick got its one read)
+    r0 = ex.mock_occ_reads(0)
+    for _ in range(5):  # back to back: no sub-sample falls between them (period 1.5 s)
+        ex.tick()
+    # the mock counts the process list's own cu_occupancy read too: one per tick; before the fix a
+    # second (the fallback) followed it every tick for the known, unreadable pid
+    assert ex.mock_occ_reads(0) == r0 + 5
+    row = next(r for r in ex.pod_rows() if r["pid"] == "31")
+    assert row["occ_samples"] == 0 and (row["cu_occupancy"] is None or math.isnan(row["cu_occupancy"]))
+    procs = [{"pid": 31, "device": 0, "kfd_only": True}, {"pid": 32, "device": 0, "kfd_only": True}]
+    ex.mock_set_procs(procs)
+    r1 = ex.mock_occ_reads(0)
+    ex.tick()  # pid 32 arrives: its list read, pid 31's, and one fallback read for the new pid
+    assert ex.mock_occ_reads(0) == r1 + 3
+
+
+def test_held_rows_carry_no_stale_occupancy(mock_exporter):
+    """while a failed process list is held, the held rows do not repeat the last good
+    tick's occupancy as if it were this interval's (NaN, 0 reads), and the next good tick's mean
+    covers its own interval only (the sums restart after the failed tick)."""
+    import math
+
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0,
+                       mock={"procs": [{"pid": 41, "device": 0, "kfd_only": True}]})
+    ex.mock_set_occ_series(0, [128.0])
+    ex.tick()
+    row = next(r for r in ex.pod_rows() if r["pid"] == "41")
+    assert row["cu_occupancy"] == 128.0 and row["occ_samples"] >= 1
+    ex.mock_fail_procs(0, 1)
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_process_list_held", gpu_id="0") == 1
+    row = next(r for r in ex.pod_rows() if r["pid"] == "41")
+    assert row["occ_samples"] == 0 and (row["cu_occupancy"] is None or math.isnan(row["cu_occupancy"]))
+    assert not promtext.values(fam, "gpu_cu_occupancy", gpu_id="0")  # device sum not faked either
+    ex.tick()  # listed again: a fresh reading
+    row = next(r for r in ex.pod_rows() if r["pid"] == "41")
+    assert row["cu_occupancy"] == 128.0
+
+
+def test_sub_sample_sums_restart_after_a_failed_list(mock_exporter):
+    """The worker's sub-sample sums are per interval: the interval of a failed list is not folded
+    into the next good tick (which would average two intervals as one)."""
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", interval_s=0.2, occ_samples=10, sample_threads=-1,
+                       mock={"procs": [{"pid": 51, "device": 0, "kfd_only": True}]})
+    ex.mock_set_occ_series(0, [100.0])
+    _wait_ticks(ex, 3)
+    ex.mock_fail_procs(0, 1)
+    _wait_ticks(ex, 2)  # the failed list, then the interval after it
+    row = next(r for r in ex.pod_rows() if r["pid"] == "51")
+    assert 1 <= row["occ_samples"] <= 14, row  # one interval's reads (10 + scan jitter), not two
