@@ -927,6 +927,8 @@ PYBIND11_MODULE(_core, m) {
              d["gzip_eager"] = s.gzip_eager;
              d["gzip_lazy"] = s.gzip_lazy;
              d["gzip_unused"] = s.gzip_unused;
+             d["kfd_files_open"] = s.kfd_files_open;
+             d["kfd_reads_cached"] = s.kfd_reads_cached;
              d["device_errors"] = s.device_errors;
              d["device_timeouts"] = s.device_timeouts;
              d["sample_count"] = s.sample_hist.count;

@@ -339,6 +339,15 @@ bool AmdSmiBackend::init(std::string* err) {
   return true;
 }
 
+void AmdSmiBackend::kfd_file_stats(uint64_t* open_fds, uint64_t* cached_reads) const {
+  *open_fds = *cached_reads = 0;
+  for (const auto& g : fast_)
+    if (g) {
+      *open_fds += g->kfd_fds();
+      *cached_reads += g->kfd_reads_cached();
+    }
+}
+
 int AmdSmiBackend::fast_path_devices() const {
   int n = 0;
   for (const auto& f : fast_) n += f != nullptr;

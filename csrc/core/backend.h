@@ -287,6 +287,8 @@ class AmdSmiBackend : public Backend {
     proc_root_ = std::move(proc_root);
   }
   int fast_path_devices() const;
+  // KFD per-pid files kept open across the fast-path GPUs, and reads served from them
+  void kfd_file_stats(uint64_t* open_fds, uint64_t* cached_reads) const;
   const std::string& fast_path_status() const { return fast_status_; }
   // Field-by-field libamd_smi vs sysfs-decoded firmware table of device i: (field, amdsmi, sysfs).
   std::vector<std::tuple<std::string, double, double>> compare_tables(int i, std::string* err);

@@ -1808,6 +1808,7 @@ SelfStats Exporter::self_stats() const {
     s.backend_version = a->lib_version();
     s.fast_path_devices = a->fast_path_devices();
     s.fast_path_status = a->fast_path_status();
+    a->kfd_file_stats(&s.kfd_files_open, &s.kfd_reads_cached);
   }
   if (auto* r = dynamic_cast<RocmSmiBackend*>(backend_.get())) s.backend_version = r->lib_version();
   s.backend_up = backend_up_;

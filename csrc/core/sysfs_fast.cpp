@@ -15,14 +15,20 @@ namespace {
 
 int open_ro(const std::string& p) { return ::open(p.c_str(), O_RDONLY | O_CLOEXEC); }
 
-// pread at offset 0 re-runs the attribute's show() (kernfs restarts the seq_file at pos 0).
+// pread at offset 0 re-runs the attribute's show() (kernfs restarts the seq_file at pos 0). kernfs
+// hands out at most a page per read and a show() fills its whole content at once, so a read that
+// returns less than a request of at most a page is the whole file: no second pread() just to see
+// EOF (one syscall per small read instead of two).
 ssize_t pread_all(int fd, void* buf, size_t cap) {
+  constexpr size_t kPage = 4096;
   size_t got = 0;
   while (got < cap) {
-    ssize_t r = ::pread(fd, static_cast<char*>(buf) + got, cap - got, static_cast<off_t>(got));
+    const size_t want = cap - got;
+    ssize_t r = ::pread(fd, static_cast<char*>(buf) + got, want, static_cast<off_t>(got));
     if (r < 0) return -1;
     if (r == 0) break;
     got += static_cast<size_t>(r);
+    if (static_cast<size_t>(r) < want && want <= kPage) break;  // short read of <= a page: the end
   }
   return static_cast<ssize_t>(got);
 }
@@ -72,6 +78,66 @@ bool fdinfo_value(const char* text, const char* key, uint64_t* v) {
 SysfsGpu::~SysfsGpu() {
   for (int fd : {fd_metrics_, fd_vram_used_, fd_vram_total_, fd_gtt_used_})
     if (fd >= 0) ::close(fd);
+  std::lock_guard<std::mutex> g(kfd_fds_mu_);
+  for (auto& [k, fd] : kfd_fds_) ::close(fd);
+}
+
+bool SysfsGpu::read_kfd(uint32_t pid, KfdFile kind, char* b, size_t cap, size_t* n) {
+  const uint64_t key = (static_cast<uint64_t>(pid) << 1) | static_cast<uint64_t>(kind);
+  int fd = -1;
+  {
+    std::lock_guard<std::mutex> g(kfd_fds_mu_);
+    auto it = kfd_fds_.find(key);
+    if (it != kfd_fds_.end()) {
+      fd = it->second;
+      kfd_fds_.erase(it);  // taken out while read: a concurrent caller opens its own
+    }
+  }
+  if (fd >= 0) {
+    const ssize_t r = pread_all(fd, b, cap - 1);
+    if (r > 0) {
+      b[r] = 0;
+      *n = static_cast<size_t>(r);
+      std::lock_guard<std::mutex> g(kfd_fds_mu_);
+      if (!kfd_fds_.emplace(key, fd).second) ::close(fd);
+      kfd_reads_cached_.fetch_add(1, std::memory_order_relaxed);
+      return true;
+    }
+    // the process exited (its kobject is gone: ENODEV) or the pid was reused: a fresh open below
+    ::close(fd);
+  }
+  const std::string path = sys_root_ + "/class/kfd/kfd/proc/" + std::to_string(pid) +
+                           (kind == KfdFile::kVram ? "/vram_" + std::to_string(kfd_gpu_id_)
+                                                   : "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy");
+  fd = open_ro(path);
+  if (fd < 0) return false;
+  const ssize_t r = pread_all(fd, b, cap - 1);
+  if (r < 0) {
+    ::close(fd);
+    return false;
+  }
+  b[r] = 0;
+  *n = static_cast<size_t>(r);
+  std::lock_guard<std::mutex> g(kfd_fds_mu_);
+  if (kfd_fds_.size() >= kMaxKfdFds || !kfd_fds_.emplace(key, fd).second) ::close(fd);
+  return true;
+}
+
+void SysfsGpu::retain_kfd(const std::vector<uint32_t>& listed_sorted) {
+  std::lock_guard<std::mutex> g(kfd_fds_mu_);
+  for (auto it = kfd_fds_.begin(); it != kfd_fds_.end();) {
+    if (!std::binary_search(listed_sorted.begin(), listed_sorted.end(), static_cast<uint32_t>(it->first >> 1))) {
+      ::close(it->second);
+      it = kfd_fds_.erase(it);
+    } else {
+      ++it;
+    }
+  }
+}
+
+size_t SysfsGpu::kfd_fds() {
+  std::lock_guard<std::mutex> g(kfd_fds_mu_);
+  return kfd_fds_.size();
 }
 
 bool SysfsGpu::open(const std::string& sys_root, const std::string& proc_root, const std::string& bdf,
@@ -310,12 +376,10 @@ void SysfsGpu::fdinfo_usage(uint32_t pid, ProcSample* p) {
 void SysfsGpu::occupancy(const std::vector<uint32_t>& pids, std::vector<double>* out) {
   out->assign(pids.size(), kNaN);
   if (!kfd_gpu_id_) return;
-  const std::string tail = "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy";
-  const std::string kdir = sys_root_ + "/class/kfd/kfd/proc/";
   char b[64];
   for (size_t k = 0; k < pids.size(); ++k) {
     size_t n = 0;
-    if (read_small(kdir + std::to_string(pids[k]) + tail, b, sizeof b, &n))
+    if (read_kfd(pids[k], KfdFile::kOccupancy, b, sizeof b, &n))
       (*out)[k] = static_cast<double>(strtoull(b, nullptr, 10));
   }
 }
@@ -345,8 +409,6 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
   const std::string kdir = sys_root_ + "/class/kfd/kfd/proc";
   DIR* d = opendir(kdir.c_str());
   if (!d) return false;
-  const std::string vram_name = "/vram_" + std::to_string(kfd_gpu_id_);
-  const std::string occ_name = "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy";
   char b[64];
   std::vector<uint32_t> listed;  // every KFD process of the node (any GPU)
   const int64_t now = mono_ns();
@@ -355,9 +417,8 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
     const uint32_t pid = static_cast<uint32_t>(strtoul(e->d_name, nullptr, 10));
     listed.push_back(pid);
     if (skip_not_here(pid, now)) continue;
-    const std::string pdir = kdir + "/" + e->d_name;
     size_t n = 0;
-    if (!read_small(pdir + vram_name, b, sizeof b, &n)) {  // process not on this GPU
+    if (!read_kfd(pid, KfdFile::kVram, b, sizeof b, &n)) {  // process not on this GPU
       note_not_here(pid, now);
       continue;
     }
@@ -365,7 +426,7 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
     p.pid = pid;
     p.mem_bytes = static_cast<double>(strtoull(b, nullptr, 10));
     p.vram_bytes = p.mem_bytes;
-    if (read_occupancy && read_small(pdir + occ_name, b, sizeof b, &n))
+    if (read_occupancy && read_kfd(pid, KfdFile::kOccupancy, b, sizeof b, &n))
       p.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
     fdinfo_usage(pid, &p);
     out->push_back(std::move(p));
@@ -374,6 +435,7 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
   std::sort(listed.begin(), listed.end());
   DrmFdTables::get().retain(proc_root_, listed);
   prune_not_here(listed);
+  retain_kfd(listed);  // close the kept files of processes that left
   return true;
 }
 
@@ -383,24 +445,21 @@ bool SysfsGpu::occupancy_scan(std::vector<OccRead>* out) {
   const std::string kdir = sys_root_ + "/class/kfd/kfd/proc/";
   DIR* d = opendir(kdir.c_str());
   if (!d) return false;
-  const std::string occ_name = "/stats_" + std::to_string(kfd_gpu_id_) + "/cu_occupancy";
-  const std::string vram_name = "/vram_" + std::to_string(kfd_gpu_id_);
   char b[64];
   const int64_t now = mono_ns();
   while (dirent* e = readdir(d)) {
     if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
     const uint32_t pid = static_cast<uint32_t>(strtoul(e->d_name, nullptr, 10));
     if (skip_not_here(pid, now)) continue;
-    const std::string pdir = kdir + e->d_name;
     size_t n = 0;
-    if (!read_small(pdir + vram_name, b, sizeof b, &n)) {  // not on this GPU
+    if (!read_kfd(pid, KfdFile::kVram, b, sizeof b, &n)) {  // not on this GPU
       note_not_here(pid, now);
       continue;
     }
     OccRead r;
     r.pid = pid;
     r.vram_bytes = static_cast<double>(strtoull(b, nullptr, 10));
-    if (read_small(pdir + occ_name, b, sizeof b, &n)) r.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
+    if (read_kfd(pid, KfdFile::kOccupancy, b, sizeof b, &n)) r.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
     out->push_back(r);
   }
   closedir(d);

@@ -207,6 +207,9 @@ class SysfsGpu {
   void maintain();
   // One gpu_metrics read whose table is discarded: leaves the SMU's fetch path warm for the tick.
   bool prewarm();
+  // KFD per-pid files held open right now, and reads served from a kept fd (tests / self-metrics).
+  size_t kfd_fds();
+  uint64_t kfd_reads_cached() const { return kfd_reads_cached_.load(std::memory_order_relaxed); }
 
  private:
   void fdinfo_usage(uint32_t pid, ProcSample* p);
@@ -221,6 +224,19 @@ class SysfsGpu {
   void prune_not_here(const std::vector<uint32_t>& listed_sorted);
   std::mutex not_here_mu_;
   std::unordered_map<uint32_t, int64_t> not_here_;  // pid -> ask again after (mono ns)
+  // Per-pid KFD files (vram_<gpu>, stats_<gpu>/cu_occupancy) kept open and re-read with pread(0):
+  // a sub-sample costs one pread instead of open + pread + close, each open a 6-level kernfs path
+  // walk (20 cu_occupancy reads per process per tick on the device worker). A read that fails on a
+  // kept fd (the process exited: ENODEV; the pid was reused) reopens the path once; the files of
+  // pids that left the KFD listing are closed at the next process list. At most kMaxKfdFds per GPU
+  // (32 processes' pairs): past that, reads open and close as before.
+  enum class KfdFile : uint8_t { kVram = 0, kOccupancy = 1 };
+  bool read_kfd(uint32_t pid, KfdFile kind, char* b, size_t cap, size_t* n);
+  void retain_kfd(const std::vector<uint32_t>& listed_sorted);
+  static constexpr size_t kMaxKfdFds = 64;
+  std::mutex kfd_fds_mu_;
+  std::unordered_map<uint64_t, int> kfd_fds_;  // (pid << 1 | kind) -> fd
+  std::atomic<uint64_t> kfd_reads_cached_{0};
   std::string sys_root_, proc_root_, dev_dir_;
   uint64_t kfd_gpu_id_ = 0;
   std::string render_path_;  // "/dev/dri/renderD<minor>"

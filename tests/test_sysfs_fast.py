@@ -317,3 +317,27 @@ def test_process_of_another_gpu_is_not_reasked_every_tick_but_is_picked_up_later
     time.sleep(1.1)
     ex.tick()
     assert sorted((r["dev"], r["pid"]) for r in ex.pod_rows() if not r["idle"]) == [(0, "4242"), (1, "4242")]
+
+
+def test_kfd_per_pid_files_are_kept_open_and_closed_when_the_process_leaves(exporter, tmp_path):
+    """The per-pid KFD files (vram_<gpu>, stats_<gpu>/cu_occupancy) are opened once and re-read
+    with pread(0): the 20 sub-samples per tick each cost one read instead of open + read + close.
+    A value written between ticks is what the next read returns (same inode, re-read from 0). The
+    files of a process that left the KFD listing are closed at the next process list."""
+    import shutil
+
+    sysr, procr = make_tree(tmp_path, gpus=1)
+    ex = exporter(sysr, procr, sample_threads=0)
+    for _ in range(3):
+        ex.tick()
+    st = ex.self_stats()
+    assert st["kfd_files_open"] == 2  # vram + cu_occupancy of pid 4242 on GPU 0
+    assert st["kfd_reads_cached"] >= 4
+    occ = sysr / "class" / "kfd" / "kfd" / "proc" / "4242" / "stats_36622" / "cu_occupancy"
+    occ.write_text("211\n")
+    ex.tick()
+    assert next(r for r in ex.pod_rows() if r["pid"] == "4242")["cu_occupancy"] == 211
+    shutil.rmtree(sysr / "class" / "kfd" / "kfd" / "proc" / "4242")  # the process exited
+    ex.tick()
+    assert ex.self_stats()["kfd_files_open"] == 0
+    assert not [r for r in ex.pod_rows() if not r["idle"] and r["dev"] == 0]
