@@ -284,13 +284,18 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
     int status = 0;
     if (in.size() > 12) status = atoi(in.c_str() + 9);
     long clen = -1;
-    bool close_after = false;
+    bool close_after = false, chunked = false;
     size_t pos = in.find("\r\n") + 2;
     while (pos < hdr_end) {
       size_t e = in.find("\r\n", pos);
       std::string_view h(in.data() + pos, e - pos);
       if (h.size() > 15 && strncasecmp(h.data(), "content-length:", 15) == 0)
         clen = strtol(std::string(h.substr(15)).c_str(), nullptr, 10);
+      if (h.size() > 18 && strncasecmp(h.data(), "transfer-encoding:", 18) == 0) {
+        std::string v(h.substr(18));
+        for (auto& ch : v) ch = static_cast<char>(tolower(static_cast<unsigned char>(ch)));
+        chunked = v.find("chunked") != std::string::npos;
+      }
       if (h.size() > 11 && strncasecmp(h.data(), "connection:", 11) == 0 &&
           h.find("close") != std::string_view::npos)
         close_after = true;
@@ -302,7 +307,67 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
       *err = "response body of " + std::to_string(clen) + " bytes refused";
       return -1;
     }
-    if (clen >= 0) {
+    if (chunked && status != 204 && status != 304) {
+      // RFC 9112 7.1 (a proxy in front of InfluxDB answers errors this way): size line, data,
+      // CRLF ... a 0-size chunk, optional trailers, CRLF. Keeps the connection reusable.
+      std::string raw = std::move(rb), out;
+      size_t at = 0;
+      auto need = [&](size_t upto) -> bool {  // raw holds at least `upto` bytes, or fail
+        while (raw.size() < upto) {
+          const long r = recv_some(buf, sizeof buf, &rerr);
+          if (r <= 0) return false;
+          raw.append(buf, static_cast<size_t>(r));
+          if (raw.size() > static_cast<size_t>(kMaxBodyBytes) + 4096 || expired()) return false;
+        }
+        return true;
+      };
+      auto line = [&](std::string* l) -> bool {  // next CRLF-terminated line from `at`
+        size_t e;
+        while ((e = raw.find("\r\n", at)) == std::string::npos) {
+          if (raw.size() - at > 4096 || !need(raw.size() + 1)) return false;
+        }
+        *l = raw.substr(at, e - at);
+        at = e + 2;
+        return true;
+      };
+      bool ok = true;
+      for (;;) {
+        std::string l;
+        if (!line(&l)) {
+          ok = false;
+          break;
+        }
+        char* endp = nullptr;
+        const unsigned long long n = strtoull(l.c_str(), &endp, 16);  // chunk extensions after ';' ignored
+        if (endp == l.c_str() || n > static_cast<unsigned long long>(kMaxBodyBytes) ||
+            out.size() + n > static_cast<size_t>(kMaxBodyBytes)) {
+          ok = false;
+          break;
+        }
+        if (n == 0) {  // trailers until an empty line
+          do {
+            if (!line(&l)) {
+              ok = false;
+              break;
+            }
+          } while (!l.empty());
+          break;
+        }
+        if (!need(at + n + 2) || raw.compare(at + n, 2, "\r\n") != 0) {
+          ok = false;
+          break;
+        }
+        out.append(raw, at, n);
+        at += n + 2;
+      }
+      if (!ok) {
+        const bool timed_out = !err->empty() && *err == "response timed out";
+        close_conn();
+        if (!timed_out) *err = "bad chunked body" + (rerr.empty() ? std::string() : " (" + rerr + ")");
+        return -1;
+      }
+      rb = std::move(out);
+    } else if (clen >= 0) {
       // the body lands in place: one buffer of the announced length, no 16 KB staging copies
       size_t got = std::min(rb.size(), static_cast<size_t>(clen));
       rb.resize(static_cast<size_t>(clen));

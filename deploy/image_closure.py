@@ -53,9 +53,13 @@ PRODUCT_OVERLAYS = {"lib/libgpumon_pmc.so": f"{PREFIX}/lib/libgpumon_pmc.so",
 # dlopen()ed by name (not in any DT_NEEDED): each name is kept as the path it resolves to, with its
 # symlink chain, so the loader finds it under the name the code asks for
 DLOPEN = ["libamd_smi.so.26", "libamd_smi.so", "librocm_smi64.so.1", "librocm_smi64.so", "libssl.so.3",
-          "libcrypto.so.3", "librocprofiler-sdk-roctx.so.1"]
+          "libcrypto.so.3", "librocprofiler-sdk-roctx.so.1",
+          # libamd_smi dlopens the DRM libraries at init (seen mapped on MI355X, profiles/r5_gpu_runs.md)
+          "libdrm.so.2", "libdrm_amdgpu.so.1"]
 DLOPEN_OVERLAYS = ["libhsa-amd-aqlprofile64.so.1", "libhsa-amd-aqlprofile64.so"]
 DATA = ["/etc/ssl/certs/ca-certificates.crt"]
+# optional data: staged when the build image has it (libdrm_amdgpu's marketing-name table)
+DATA_OPTIONAL = ["/usr/share/libdrm/amdgpu.ids", "/opt/amdgpu/share/libdrm/amdgpu.ids"]
 DATA_OVERLAYS = [f"{ROCM}/share/rocprofiler-sdk/counter_defs.yaml", f"{ROCM}/share/rocprofiler-sdk/basic_counters.xml",
                  f"{ROCM}/share/rocprofiler-sdk/derived_counters.xml"]
 
@@ -137,6 +141,9 @@ def closure(overlays: bool = False) -> dict:
             add_path(d)
         else:
             missing.append(d)
+    for d in DATA_OPTIONAL:
+        if os.path.exists(d):
+            add_path(d)
     return {"files": dict(sorted(files.items())), "links": dict(sorted(links.items())), "missing": missing}
 
 

@@ -271,6 +271,75 @@ def test_client_bounds_a_dripping_or_endless_response(core, script, error):
     assert dt < 2.5, dt
 
 
+def test_client_decodes_chunked_bodies_and_keeps_the_connection(core):
+    """RFC 9112 chunked responses (a reverse proxy in front of InfluxDB answers errors this way):
+    chunks with extensions, trailers, several requests over one keep-alive connection; a broken
+    chunk framing is an error, not a hang until the timeout."""
+    import time
+
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(2)
+    port = srv.getsockname()[1]
+    good = [b"HTTP/1.1 400 Bad Request\r\nTransfer-Encoding: chunked\r\n\r\n"
+            b"7;ext=1\r\n{\"code\"\r\n9\r\n:\"invalid\r\n2\r\n\"}\r\n0\r\nX-Trailer: t\r\n\r\n",
+            b"HTTP/1.1 200 OK\r\nTransfer-Encoding: Chunked\r\n\r\n3\r\nabc\r\n0\r\n\r\n",
+            b"HTTP/1.1 204 No Content\r\n\r\n"]
+    conns = []
+
+    def serve():
+        c, _ = srv.accept()
+        conns.append(c)
+        for a in good:  # three answers on ONE connection, a byte-split one in the middle
+            c.recv(65536)
+            if a is good[1]:
+                for i in range(len(a)):
+                    c.sendall(a[i:i + 1])
+            else:
+                c.sendall(a)
+        c2, _ = srv.accept()  # then a connection with a broken chunk (size says 5, 3 bytes + CRLF)
+        conns.append(c2)
+        c2.recv(65536)
+        c2.sendall(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nabc\r\n0\r\n\r\n")
+        time.sleep(0.5)
+        c2.close()
+
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    st, body, err = core.http_request("POST", f"http://127.0.0.1:{port}/write", "m v=1", "", 2.0, "", False, 3)
+    assert st == 204, err  # the third answer, over the same connection (the server accepted once)
+    t0 = time.monotonic()
+    st, body, err = core.http_request("GET", f"http://127.0.0.1:{port}/", "", "", 2.0)
+    assert st == -1 and "bad chunked body" in err, (st, err)
+    assert time.monotonic() - t0 < 3
+    t.join(5)
+    srv.close()
+    for c in conns:
+        c.close()
+
+
+def test_client_returns_a_chunked_error_body(core):
+    """The first chunked answer's body, decoded (what the pusher logs for a 4xx)."""
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    port = srv.getsockname()[1]
+
+    def serve():
+        c, _ = srv.accept()
+        c.recv(65536)
+        c.sendall(b"HTTP/1.1 400 Bad Request\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n"
+                  b"6\r\nfield \r\n7\r\ninvalid\r\n0\r\n\r\n")
+        c.close()
+
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    st, body, err = core.http_request("POST", f"http://127.0.0.1:{port}/write", "m v=1", "", 2.0)
+    t.join(5)
+    srv.close()
+    assert (st, body) == (400, b"field invalid"), (st, body, err)
+
+
 def test_per_request_family_filter(mock_exporter):
     """/metrics?include=&exclude= (shell globs, comma-separated, repeatable, percent-decoded): the
     same families the config filter would keep, cut from the current snapshot, gzip included; other

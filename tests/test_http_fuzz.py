@@ -126,3 +126,45 @@ def test_asan_build_survives_raw_fuzz():
             p.kill()
             err = p.communicate()[1]
     assert "AddressSanitizer" not in err and "runtime error" not in err, err[-4000:]
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(body=st.binary(max_size=3000), sizes=st.lists(st.integers(min_value=1, max_value=700), min_size=1, max_size=12),
+       split=st.integers(min_value=1, max_value=97), ext=st.booleans())
+def test_client_chunked_decoding_round_trips(body, sizes, split, ext):
+    """The native client's chunked decoder (csrc/core/http_client.cpp) against random chunkings of
+    random bodies, delivered in random-sized TCP segments: the decoded body is the original."""
+    import threading
+    import time
+
+    from gpumon import core as _core
+
+    chunks, i, k = [], 0, 0
+    while i < len(body):
+        n = sizes[k % len(sizes)]
+        chunks.append(body[i:i + n])
+        i += n
+        k += 1
+    wire = b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n"
+    for c in chunks:
+        wire += f"{len(c):x}{';x=y' if ext else ''}\r\n".encode() + c + b"\r\n"
+    wire += b"0\r\n\r\n"
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    port = srv.getsockname()[1]
+
+    def serve():
+        c, _ = srv.accept()
+        c.recv(65536)
+        for j in range(0, len(wire), split):
+            c.sendall(wire[j:j + split])
+        time.sleep(0.05)
+        c.close()
+
+    t = threading.Thread(target=serve, daemon=True)
+    t.start()
+    st_, got, err = _core().http_request("GET", f"http://127.0.0.1:{port}/", "", "", 5.0)
+    t.join(5)
+    srv.close()
+    assert st_ == 200 and got == body, (st_, err, len(got), len(body))

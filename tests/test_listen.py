@@ -238,3 +238,16 @@ def test_scrape_latency_unchanged_with_the_shared_listener(mock_exporter, core):
     lat = sorted(r["latencies_s"])
     assert r["errors"] == 0 and len(lat) == 800
     assert lat[int(0.99 * (len(lat) - 1))] < 0.05
+
+
+@needs_v6
+def test_fleet_view_reads_an_exporter_over_ipv6(mock_exporter):
+    """`gpumon top --url [v6]:port` (export/fleet.py over the native client): the bracketed IPv6
+    URL reaches the dual-stack listener, the Host header carries the brackets."""
+    from gpumon.export import fleet
+
+    ex = mock_exporter(listen_addr="", port=0)
+    ex.tick()
+    frames, errors = fleet.fetch([f"http://[::1]:{ex.port}/metrics", f"http://127.0.0.1:{ex.port}/metrics"])
+    assert not errors and len(frames) == 2
+    assert len(fleet.gpu_rows(frames[0])) == 2
