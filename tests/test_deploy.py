@@ -518,8 +518,8 @@ def test_overlay_configs_are_valid_for_the_native_binary(tmp_path):
 
 def test_stress_overlay_is_10hz_end_to_end():
     """BASELINE.json's stress config (10 Hz sampling, Prometheus scraping at 10 Hz): the overlay
-    sets both, and its CPU request covers the measured 8-device 10 Hz cost (87 millicores at 200
-    scrapes/s, profiles/r3_churn.md)."""
+    sets both, and its CPU request covers the measured 8-device 10 Hz cost with headroom (91
+    millicores at 200 gzip scrapes/s in the 8x rehearsal, an upper bound: profiles/r5_cpu_8dev.md)."""
     from gpumon.config import Config
 
     (k,) = _docs("deploy/k8s/overlays/stress/kustomization.yaml")
@@ -539,5 +539,5 @@ def test_stress_overlay_is_10hz_end_to_end():
     ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
     ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"])
     ctr = _json_patch(ds, ops)["spec"]["template"]["spec"]["containers"][0]
-    assert int(ctr["resources"]["requests"]["cpu"].rstrip("m")) >= 87
+    assert int(ctr["resources"]["requests"]["cpu"].rstrip("m")) >= 1.3 * 91
     assert not ctr["securityContext"].get("privileged")
