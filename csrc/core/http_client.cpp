@@ -213,7 +213,7 @@ bool HttpClient::connect_to(const Url& u, std::string* err) {
         return false;
       }
     }
-    tls_ = std::make_unique<TlsConn>(tls_ctx_);
+    tls_ = std::make_unique<TlsConn>(tls_ctx_, timeout_s_);
     if (!tls_->handshake(fd_, u.host, err)) {
       tls_.reset();  // no close_notify after a failed handshake
       close_conn();

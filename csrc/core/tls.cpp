@@ -2,6 +2,8 @@
 
 #include <arpa/inet.h>
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -248,9 +250,41 @@ std::string TlsConn::last_error(int ret) {
   }
 }
 
+bool TlsConn::wait_retry(int ret, int64_t deadline, std::string* err) {
+  const SslApi* a = ctx_->api();
+  const int e = a->SSL_get_error(ssl_, ret);
+  short ev;
+  if (e == ossl::kErrorWantRead) ev = POLLIN;
+  else if (e == ossl::kErrorWantWrite) ev = POLLOUT;
+  else {
+    *err = last_error(ret);
+    return false;
+  }
+  for (;;) {
+    const int64_t left = deadline - mono_ns();
+    if (left <= 0) {
+      *err = "tls: timed out";
+      return false;
+    }
+    pollfd p{fd_, ev, 0};
+    const int r = poll(&p, 1, static_cast<int>(std::min<int64_t>(left / 1000000 + 1, 60000)));
+    if (r > 0) return true;  // ready (or an error condition the retried call will report)
+    if (r < 0 && errno != EINTR) {
+      *err = std::string("tls: poll: ") + strerror(errno);
+      return false;
+    }
+  }
+}
+
 bool TlsConn::handshake(int fd, const std::string& host, std::string* err) {
   const SslApi* a = ctx_->api();
   a->ERR_clear_error();
+  fd_ = fd;
+  const int fl = fcntl(fd, F_GETFL, 0);
+  if (fl < 0 || fcntl(fd, F_SETFL, fl | O_NONBLOCK) != 0) {
+    *err = std::string("tls: fcntl: ") + strerror(errno);
+    return false;
+  }
   ssl_ = a->SSL_new(ctx_->raw());
   if (!ssl_ || a->SSL_set_fd(ssl_, fd) != 1) {
     *err = "tls: SSL_new: " + err_queue(a);
@@ -267,8 +301,19 @@ bool TlsConn::handshake(int fd, const std::string& host, std::string* err) {
       return false;
     }
   }
-  const int r = a->SSL_connect(ssl_);
+  const int64_t deadline = mono_ns() + timeout_ns_;
+  int r;
+  std::string werr;
+  while ((r = a->SSL_connect(ssl_)) != 1) {
+    const int e = a->SSL_get_error(ssl_, r);
+    if ((e == ossl::kErrorWantRead || e == ossl::kErrorWantWrite) && wait_retry(r, deadline, &werr)) continue;
+    break;
+  }
   if (r != 1) {
+    if (werr == "tls: timed out") {
+      *err = "tls: handshake with " + host + " timed out";
+      return false;
+    }
     const long v = a->SSL_get_verify_result(ssl_);
     if (ctx_->verify() && v != ossl::kVerifyOk) {
       a->ERR_clear_error();
@@ -284,12 +329,13 @@ bool TlsConn::handshake(int fd, const std::string& host, std::string* err) {
 
 bool TlsConn::write_all(const char* p, size_t n, std::string* err) {
   const SslApi* a = ctx_->api();
+  const int64_t deadline = mono_ns() + timeout_ns_;
   while (n) {
     const int chunk = static_cast<int>(std::min<size_t>(n, 1 << 30));
     a->ERR_clear_error();
     const int w = a->SSL_write(ssl_, p, chunk);
     if (w <= 0) {
-      *err = last_error(w);
+      if (wait_retry(w, deadline, err)) continue;
       return false;
     }
     p += w;
@@ -300,21 +346,26 @@ bool TlsConn::write_all(const char* p, size_t n, std::string* err) {
 
 long TlsConn::read_some(char* buf, size_t n, std::string* err) {
   const SslApi* a = ctx_->api();
-  a->ERR_clear_error();
-  errno = 0;
-  const int r = a->SSL_read(ssl_, buf, static_cast<int>(std::min<size_t>(n, 1 << 30)));
-  if (r > 0) return r;
-  const int e = a->SSL_get_error(ssl_, r);
-  if (e == ossl::kErrorZeroReturn) return 0;
-  // EOF without close_notify: many servers (and proxies) just close; the HTTP framing decides
-  if (e == ossl::kErrorSyscall && errno == 0 && a->ERR_get_error() == 0) return 0;
-  *err = last_error(r);
-  return -1;
+  const int64_t deadline = mono_ns() + timeout_ns_;
+  for (;;) {
+    a->ERR_clear_error();
+    errno = 0;
+    const int r = a->SSL_read(ssl_, buf, static_cast<int>(std::min<size_t>(n, 1 << 30)));
+    if (r > 0) return r;
+    const int e = a->SSL_get_error(ssl_, r);
+    if (e == ossl::kErrorZeroReturn) return 0;
+    // EOF without close_notify: many servers (and proxies) just close; the HTTP framing decides
+    if (e == ossl::kErrorSyscall && errno == 0 && a->ERR_get_error() == 0) return 0;
+    std::string werr;
+    if ((e == ossl::kErrorWantRead || e == ossl::kErrorWantWrite) && wait_retry(r, deadline, &werr)) continue;
+    *err = werr.empty() ? last_error(r) : werr;
+    return -1;
+  }
 }
 
 void TlsConn::shutdown() {
   if (ssl_) {
-    ctx_->api()->SSL_shutdown(ssl_);
+    ctx_->api()->SSL_shutdown(ssl_);  // non-blocking: one attempt to send close_notify
     ctx_->api()->ERR_clear_error();
   }
 }

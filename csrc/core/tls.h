@@ -9,6 +9,7 @@
 // `influx_ca_file` replaces the bundle, `influx_tls_insecure` (off by default) disables both.
 #pragma once
 
+#include <cstdint>
 #include <memory>
 #include <string>
 
@@ -43,10 +44,14 @@ class TlsContext {
   bool insecure_ = false;
 };
 
-// One TLS session over a connected blocking socket (SO_RCVTIMEO / SO_SNDTIMEO bound each call).
+// One TLS session over a connected socket. The socket is switched to non-blocking and every call
+// waits with poll() against its own deadline (timeout_s from the call's start): a peer that
+// drips a handshake or a record a byte at a time cannot stretch one call past the timeout (with
+// blocking I/O each of OpenSSL's recv()s would get the whole SO_RCVTIMEO again).
 class TlsConn {
  public:
-  explicit TlsConn(std::shared_ptr<TlsContext> ctx) : ctx_(std::move(ctx)) {}
+  TlsConn(std::shared_ptr<TlsContext> ctx, double timeout_s)
+      : ctx_(std::move(ctx)), timeout_ns_(timeout_s > 0 ? static_cast<int64_t>(timeout_s * 1e9) : INT64_MAX / 4) {}
   ~TlsConn();
   // SNI + host-name (or IP literal) check + handshake. false with a named reason in *err, e.g.
   // "tls: certificate verify failed: self-signed certificate in certificate chain".
@@ -59,8 +64,13 @@ class TlsConn {
 
  private:
   std::string last_error(int ret);
+  // After an SSL call returned `ret`: wait for the socket in the direction OpenSSL wants, until
+  // `deadline` (mono ns). true = retry the call; false = a real error or the deadline (*err set).
+  bool wait_retry(int ret, int64_t deadline, std::string* err);
   std::shared_ptr<TlsContext> ctx_;
   void* ssl_ = nullptr;  // SSL*
+  int fd_ = -1;
+  int64_t timeout_ns_;
 };
 
 // Configuration-time check of a push URL and its TLS settings (both entry points call it): the

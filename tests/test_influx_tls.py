@@ -324,3 +324,50 @@ def test_native_binary_pushes_over_https(pki):
     bodies = [x["body"] for x in srv.posts]
     assert all(b.startswith("node_gpu,host=gpu-node-3,gpu_id=0 ") for b in bodies), bodies[0][:200]
     assert srv.posts[0]["auth"].startswith("Basic ")
+
+
+def test_tls_handshake_with_a_silent_peer_is_bounded(core):
+    """A peer that accepts TCP and never answers the ClientHello: the handshake gives up after the
+    client's timeout (non-blocking socket, poll() against a per-call deadline) with a named error."""
+    import time
+
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    port = srv.getsockname()[1]
+    held = []
+
+    def accept():
+        c, _ = srv.accept()
+        held.append(c)  # read nothing, send nothing
+
+    t = threading.Thread(target=accept, daemon=True)
+    t.start()
+    t0 = time.monotonic()
+    st, _, err = core.http_request("POST", f"https://127.0.0.1:{port}/write", "m v=1", "", 0.5, "", True)
+    dt = time.monotonic() - t0
+    t.join(5)
+    for c in held:
+        c.close()
+    srv.close()
+    assert st == -1 and "handshake with 127.0.0.1 timed out" in err, err
+    assert 0.4 < dt < 2.0, dt
+
+
+def test_tls_slow_but_steady_server_is_served(core, pki):
+    """A verifying TLS sink that takes 0.3 s to answer each POST, client timeout 1 s: pushes succeed
+    over the kept connection (the per-call deadline is not a per-connection one)."""
+    import time
+
+    class Slow(_Sink):
+        def do_POST(self):  # noqa: N802
+            time.sleep(0.3)
+            super().do_POST()
+
+    srv = _TlsSink(pki["server"], pki["server_key"])
+    srv.RequestHandlerClass = Slow
+    with srv:
+        st, _, err = core.http_request("POST", f"https://127.0.0.1:{srv.port}/write", "m v=1", "", 1.0, pki["ca"],
+                                       False, 3)
+    assert st == 204, err
+    assert len(srv.posts) == 3 and len({p["peer"] for p in srv.posts}) == 1
