@@ -78,7 +78,7 @@ class HttpServer {
   std::string addr_;
   int port_;
   int lfd_ = -1;         // the one listening socket, shared by the loops
-  bool exclusive_ = true;  // EPOLLEXCLUSIVE accepted by the kernel (>= 4.5)
+  std::atomic<bool> exclusive_{true};  // EPOLLEXCLUSIVE accepted by the kernel (>= 4.5)
   std::string bound_;
   int nthreads_;
   int sndbuf_ = 0;  // SO_SNDBUF for accepted connections (0: kernel default)

@@ -110,3 +110,15 @@ def test_cli_list_and_stage(tmp_path):
                         str(tmp_path / "rootfs")], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr
     assert json.loads(r.stdout)["files"] == len(d["files"])
+
+
+def test_staged_exporter_once_runs_on_the_closure_alone(staged):
+    """`gpumon-exporter --backend mock --once` from the staged tree, LD_LIBRARY_PATH limited to it
+    (VERDICT r4 #3): one exposition on stdout, exit 0."""
+    libpath = ":".join(staged + d for d in (f"{ic.ROCM}/lib", "/lib/x86_64-linux-gnu", "/usr/lib/x86_64-linux-gnu"))
+    env = {k: v for k, v in os.environ.items() if k not in ("LD_LIBRARY_PATH", "PYTHONPATH", "GPUMON_PLUGIN_DIR")}
+    env["LD_LIBRARY_PATH"] = libpath
+    r = subprocess.run([staged + "/opt/gpumon/bin/gpumon-exporter", "--backend", "mock:gpus=2", "--once",
+                        "--no-pod-resources", "--no-cri"], capture_output=True, text=True, timeout=60, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.count("node_gpu_gpu_util{") == 2
