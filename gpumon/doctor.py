@@ -159,12 +159,81 @@ def firmware_table_check(path: str, interval_s: float, prewarm_ms: float, second
     return OK, detail
 
 
+def listen_check(listen: str) -> tuple:
+    """The configured listen address: parses (the native rule), the families it will serve, and
+    whether the port is free (a running exporter on it makes a second one exit EADDRINUSE)."""
+    import socket
+
+    from .config import ConfigError, parse_listen
+
+    try:
+        host, port = parse_listen(listen)
+    except ConfigError as e:
+        return (FAIL, str(e))
+    v6 = True
+    try:
+        socket.socket(socket.AF_INET6, socket.SOCK_STREAM).close()
+    except OSError:
+        v6 = False
+    if host in ("", "::"):
+        fam = "IPv4 + IPv6 (one dual-stack [::] socket)" if v6 else (
+            "IPv4 only: no IPv6 in this network namespace" + (" -- [::] will fail" if host == "::" else ""))
+    else:
+        fam = "IPv6 only" if ":" in host else "IPv4 only" if host.replace(".", "").isdigit() or host == "0.0.0.0" else host
+    if port == 0:
+        return (OK, f"{listen}: {fam}, ephemeral port")
+    fam_bind = socket.AF_INET6 if (v6 and host in ("", "::")) or ":" in host else socket.AF_INET
+    s = socket.socket(fam_bind, socket.SOCK_STREAM)
+    try:
+        if fam_bind == socket.AF_INET6 and host in ("", "::"):
+            s.setsockopt(socket.IPPROTO_IPV6, socket.IPV6_V6ONLY, 0)
+        s.bind((host or ("::" if fam_bind == socket.AF_INET6 else "0.0.0.0"), port))
+        free = True
+    except OSError as e:
+        free = e.errno != 98  # EADDRINUSE
+        if free:
+            return (WARN, f"{listen}: {fam}; cannot bind: {e.strerror}")
+    finally:
+        s.close()
+    return (OK, f"{listen}: {fam}, port {port} free") if free else (
+        WARN, f"{listen}: {fam}; port {port} is in use (an exporter already running here? a second one exits "
+              "with EADDRINUSE)")
+
+
+def influx_check(cfg) -> tuple:
+    """The Influx compat push: the startup check both entry points run (scheme, host, TLS files,
+    libssl), then one GET /ping on the same host over the same transport (TLS verified as the
+    push will be): reachability without writing anything."""
+    from ._native import core as _core
+    from .config import redact_url
+
+    c = _core()
+    err = c.check_push_config(cfg.influx_url, cfg.influx_token, cfg.influx_ca_file, bool(cfg.influx_tls_insecure),
+                              cfg.influx_client_cert, cfg.influx_client_key)
+    if err:
+        return (FAIL, err + ": the exporter refuses to start with it")
+    u = c.parse_url(cfg.influx_url)
+    host = f"[{u['host']}]" if ":" in u["host"] else u["host"]
+    ping = f"{'https' if u['tls'] else 'http'}://{host}:{u['port']}/ping"
+    st, _, perr = c.http_request("GET", ping, "", "", 3.0, cfg.influx_ca_file, bool(cfg.influx_tls_insecure))
+    what = redact_url(cfg.influx_url) + (" (TLS, certificate verified)" if u["tls"] and not cfg.influx_tls_insecure
+                                         else " (TLS, NOT verified)" if u["tls"] else "")
+    if st in (200, 204):
+        return (OK, f"{what}: /ping answered {st}")
+    return (WARN, f"{what}: /ping " + (f"answered HTTP {st}" if st > 0 else f"failed: {perr}")
+            + "; the push will retry with backoff (gpumon_influx_up 0 until it succeeds)")
+
+
 def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
     """[(check, status, detail)] for the node this runs on, with the exporter configured as `cfg`."""
     from .monitor import GpuMonitor
 
     out = []
     interval_s = cfg.interval  # as configured (the checks below tick by hand)
+    out.append(("listen address",) + listen_check(cfg.listen))
+    if cfg.influx_url:
+        out.append(("Influx push",) + influx_check(cfg))
+        cfg.influx_url = ""  # checked above; the checks below do not push
     cfg.interval = 0
     cfg.listen = "127.0.0.1:0"
     cfg.enable_pmc = cfg.enable_probe = False  # the on-device check below runs them explicitly

@@ -455,6 +455,13 @@ def test_elevated_rights_only_in_the_ondevice_overlay():
     assert pod["containers"][0]["securityContext"].get("privileged", False) is False
 
 
+def test_service_is_dual_stack_ready():
+    """The headless Service asks for both IP families where the cluster has them; the exporter's
+    default listen (":9400") answers on both (tests/test_listen.py)."""
+    svc = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "Service")
+    assert svc["spec"]["ipFamilyPolicy"] == "PreferDualStack" and svc["spec"]["clusterIP"] == "None"
+
+
 def test_fdscan_overlay_only_adds_dac_read_search():
     """overlays/fdscan/ is the one place CAP_DAC_READ_SEARCH comes back (listing a non-root tenant's
     /proc/<pid>/fd), and its header states the open_by_handle_at trade-off."""

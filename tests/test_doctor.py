@@ -52,14 +52,14 @@ def test_doctor_cli_json_and_exit_status():
     r = subprocess.run([sys.executable, "-m", "gpumon", "doctor", "--backend", "mock:gpus=1", "--format", "json",
                         "--control-plane", "off"], capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
-    rows = json.loads(r.stdout)
-    assert rows[0]["check"] == "device backend" and rows[0]["status"] == "ok"
+    rows = {x["check"]: x for x in json.loads(r.stdout)}
+    assert rows["device backend"]["status"] == "ok" and rows["listen address"]["status"] in ("ok", "warn")
     # a backend that cannot come up is the one failing (exit 1) check
     r = subprocess.run([sys.executable, "-m", "gpumon", "doctor", "--backend", "rocm_smi", "--format", "json",
                         "--control-plane", "off"], capture_output=True, text=True, timeout=120, cwd=ROOT,
                        env=dict(os.environ, LD_LIBRARY_PATH="/nonexistent"))
-    rows = json.loads(r.stdout)
-    assert r.returncode == 1 and rows[0]["status"] == "fail", (r.returncode, rows)
+    rows = {x["check"]: x for x in json.loads(r.stdout)}
+    assert r.returncode == 1 and rows["device backend"]["status"] == "fail", (r.returncode, rows)
 
 
 def test_doctor_runs_the_ondevice_samplers_once():
@@ -179,3 +179,55 @@ def test_doctor_cap_formula_is_the_servers(core):
             assert ex.self_stats()["http_max_conns"] == threads * fd_limit_cap(threads)
         finally:
             ex.stop()
+
+
+def test_doctor_checks_the_listen_address():
+    import socket
+
+    assert doctor.listen_check("127.0.0.1:0")[0] == "ok"
+    assert doctor.listen_check("nope")[0] == "fail"
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    s.listen(1)
+    port = s.getsockname()[1]
+    try:
+        st, detail = doctor.listen_check(f"127.0.0.1:{port}")
+        assert st == "warn" and "in use" in detail and "EADDRINUSE" in detail
+    finally:
+        s.close()
+    st, detail = doctor.listen_check(f"127.0.0.1:{port}")
+    assert st == "ok" and "free" in detail and "IPv4 only" in detail
+    st, detail = doctor.listen_check(":0")
+    assert st == "ok" and ("dual-stack" in detail or "IPv4 only" in detail)
+
+
+def test_doctor_checks_the_influx_push(tmp_path):
+    """The push's startup check (named failure: the exporter would refuse to start) and a /ping on
+    the same host over the same transport: an answering InfluxDB, a closed port, an https URL
+    whose certificate does not verify."""
+    import http.server
+    import threading
+
+    class Ping(http.server.BaseHTTPRequestHandler):
+        def do_GET(self):  # noqa: N802
+            self.send_response(204 if self.path == "/ping" else 404)
+            self.send_header("Content-Length", "0")
+            self.end_headers()
+
+        def log_message(self, *a):
+            pass
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), Ping)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        ok = doctor.influx_check(Config(influx_url=f"http://u:pw@127.0.0.1:{srv.server_port}/write?db=k8s"))
+        assert ok[0] == "ok" and "/ping answered 204" in ok[1] and "pw" not in ok[1]
+    finally:
+        srv.shutdown()
+    bad = doctor.influx_check(Config(influx_url="ftp://influx/write"))
+    assert bad[0] == "fail" and "unsupported scheme" in bad[1]
+    down = doctor.influx_check(Config(influx_url="http://127.0.0.1:9/write"))
+    assert down[0] == "warn" and "connect" in down[1]
+    checks = _by_name(doctor.run(Config(backend="mock:gpus=1", control_plane="off", log_level="error",
+                                        influx_url="ftp://influx/write"), wait_s=0.2))
+    assert checks["Influx push"][0] == "fail" and checks["device backend"][0] == "ok"
