@@ -203,6 +203,15 @@ std::shared_ptr<TlsContext> TlsContext::create(const TlsOptions& o, std::string*
         for (const char* b : kBundles)
           if (access(b, R_OK) == 0 && a->SSL_CTX_load_verify_locations(t->ctx_, b, nullptr) == 1) break;
         a->ERR_clear_error();
+        const void* again = a->X509_STORE_get0_objects(a->SSL_CTX_get_cert_store(t->ctx_));
+        // a hashed certs/ directory (SSL_CERT_DIR / OPENSSLDIR) is only read on demand and counts 0
+        // here: refuse only when no bundle file and no such directory can be found either
+        const char* dir_env = getenv("SSL_CERT_DIR");
+        const bool have_dir = (dir_env && *dir_env && access(dir_env, R_OK) == 0) || access("/etc/ssl/certs", R_OK) == 0;
+        if ((!again || a->OPENSSL_sk_num(again) <= 0) && !have_dir) {
+          *err = "tls: no CA certificates found (no system bundle): set influx_ca_file";
+          return nullptr;
+        }
       }
     }
   }
