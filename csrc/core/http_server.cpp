@@ -612,7 +612,9 @@ void HttpServer::run(Loop* L) {
             }
             break;
           }
-          if (L->conns.size() >= max_conns_) {
+          // the cap is the server's (loops x per-loop share): with one EPOLLEXCLUSIVE socket the first
+          // idle loop takes most connections, so a per-loop count would cap it at 1/N of the fds
+          if (conns_.load(std::memory_order_relaxed) >= max_conns_ * static_cast<size_t>(nthreads_)) {
             // full: make room by closing a connection that is not sending a response, else refuse
             // this one. Preference, least recently active first within each class:
             //   0 never answered a request, nothing pending (a connect flood's idle sockets)

@@ -62,7 +62,7 @@ class HttpServer {
   int rt_loops() const { return rt_loops_.load(); }           // loops running at SCHED_FIFO now
   uint64_t rt_demotions() const { return rt_demotions_.load(); }  // budget exhaustions
   uint64_t evicted() const { return evicted_.load(); }            // closed to make room at the cap
-  size_t max_conns() const { return max_conns_; }                 // per loop (set by start())
+  size_t max_conns() const { return max_conns_; }                 // per loop share; the cap is x loops (start())
   bool start(std::string* err);
   void stop();
   int port() const { return port_; }
