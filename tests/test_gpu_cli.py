@@ -223,3 +223,56 @@ def test_doctor_on_mi355x_reports_the_firmware_cadence():
     assert 15 <= period <= 25, fw
     cold, warm = map(float, re.search(r"costs ([0-9.]+) us cold, ([0-9.]+) us", fw["detail"]).groups())
     assert warm < cold, fw
+
+
+def test_native_binary_pushes_over_https_and_listens_dual_stack(tmp_path):
+    """The image's entrypoint on MI355X: `gpumon-exporter --backend amdsmi` with
+    the default dual-stack listener, INFLUXDB_URL=https://... verified against a test CA. Its
+    node_gpu lines arrive over TLS with the GPU's real values, /metrics answers on 127.0.0.1 and
+    on ::1, and gpumon_influx_up is 1."""
+    import shutil
+    import signal
+    import socket
+    import time
+    import urllib.request
+
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl CLI needed for test certificates")
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_influx_tls import _TlsSink, _ca, _leaf
+
+    d = str(tmp_path)
+    _ca(d, "ca")
+    _leaf(d, "server", "ca", "DNS:localhost,IP:127.0.0.1")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with _TlsSink(f"{d}/server.pem", f"{d}/server.key") as srv:
+        env = dict(os.environ, INFLUXDB_URL=f"https://localhost:{srv.port}/write?db=k8s",
+                   GPUMON_INFLUX_CA_FILE=f"{d}/ca.pem", NODE_NAME="mi355x-box")
+        p = subprocess.Popen([os.path.join(root, "bin", "gpumon-exporter"), "--backend", "amdsmi", "--interval", "0.2",
+                              "--listen", f":{port}", "--no-pod-resources", "--no-cri", "--log-level", "warn"],
+                             env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        try:
+            deadline = time.time() + 60
+            while time.time() < deadline and len(srv.posts) < 3:
+                time.sleep(0.1)
+            bodies = [x["body"] for x in srv.posts]
+            text4 = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5).read().decode()
+            try:
+                text6 = urllib.request.urlopen(f"http://[::1]:{port}/metrics", timeout=5).read().decode()
+            except OSError:
+                text6 = None  # no IPv6 in this network namespace: the listener fell back to 0.0.0.0
+        finally:
+            p.send_signal(signal.SIGTERM)
+            _, err = p.communicate(timeout=30)
+    assert p.returncode == 0, err[-2000:]
+    assert len(bodies) >= 3, (srv.handshake_errors, err[-2000:])
+    line = next(l for l in bodies[-1].splitlines() if l.startswith("node_gpu,host=mi355x-box,gpu_id=0 "))
+    assert "mem_total=294896" in line, line  # 288 GiB of HBM3E, from the device
+    fam = promtext.parse(text4)
+    assert promtext.one(fam, "gpumon_influx_up") == 1
+    if text6 is not None:
+        assert "node_gpu_gpu_util{" in text6
