@@ -160,7 +160,18 @@ def build():
                         [(f'rate(gpumon_process_list_failures_total{{{HOST}}}[5m])', "{{host}} failed lists/s"),
                          (f'gpu_process_list_held{{{HOST}}} > 0', "{{host}} gpu{{gpu_id}} HELD"),
                          (f'rate(gpumon_occupancy_scan_failures_total{{{HOST}}}[5m])', "{{host}} KFD scan failures/s")],
-                        0, y, 24, 8))
+                        0, y, 12, 8))
+    # the reference's own transport: the InfluxDB push (where INFLUXDB_URL is set)
+    panels.append(panel("InfluxDB compat push: up, pushes by result, seconds since the last success", "timeseries",
+                        [(f'gpumon_influx_up{{{HOST}}}', "{{host}} up"),
+                         (f'sum by (host, result) (rate(gpumon_influx_push_total{{{HOST}}}[5m]))', "{{host}} {{result}}/s"),
+                         (f'time() - gpumon_influx_last_success_timestamp_seconds{{{HOST}}}', "{{host}} s since ok")],
+                        12, y, 12, 8))
+    y += 8
+    panels.append(panel("Multi-GPU processes: peer contexts left out of pod_gpu rows (e.g. torchrun ranks opening every GPU)",
+                        "timeseries",
+                        [(f'gpumon_hidden_peer_gpu_contexts{{{HOST}}}', "{{host}} peer contexts"),
+                         (f'gpumon_hidden_gpu_contexts{{{HOST}}}', "{{host}} empty contexts")], 0, y, 24, 6))
     return {
         "title": "gpumon — MI355X GPU cluster",
         "uid": "gpumon-mi355x",

@@ -98,7 +98,7 @@ def test_dashboard_queries_resolve_against_exposition(mock_exporter):
             produced.add(n)
     plugins = _plugin_metric_names() | _product_families()  # samplers, pollers, RT loops, amdsmi backend
     words = {"sum", "by", "count", "rate", "increase", "max", "histogram_quantile", "le", "host", "user_name", "link",
-             "gpu_id", "state", "m", "s"}
+             "gpu_id", "state", "m", "s", "time", "result"}
     missing = []
     titles = []
     for p in dash["panels"]:
