@@ -927,6 +927,7 @@ PYBIND11_MODULE(_core, m) {
              d["gzip_eager"] = s.gzip_eager;
              d["gzip_lazy"] = s.gzip_lazy;
              d["gzip_unused"] = s.gzip_unused;
+             d["gzip_predicted"] = s.gzip_predicted;
              d["kfd_files_open"] = s.kfd_files_open;
              d["kfd_reads_cached"] = s.kfd_reads_cached;
              d["device_errors"] = s.device_errors;

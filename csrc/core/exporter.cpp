@@ -1421,10 +1421,9 @@ TickInfo Exporter::tick() {
   last_body_bytes_ = snap->body.size();
   uint64_t s = seq_.load() + 1;
   snap->seq = s;
-  // Publish the text body first (the tick's data is exported from here on), then gzip it and
-  // publish the same snapshot with the compressed body: compression (0.1-0.4 ms for 1-8 GPUs at
-  // level 1) is off the sample-to-export path. A gzip scrape in between gets the identity body,
-  // which HTTP allows. wait_for_seq() / tick() return only after both.
+  // Publish the snapshot first (the tick's data is exported from here on); its gzip, when made by
+  // this thread, follows the publish, off the sample-to-export path (0.1-0.4 ms for 1-8 GPUs at
+  // level 1). A gzip scrape in between gets the identity body, which HTTP allows.
   std::shared_ptr<const Snapshot> published_snap = snap;
   std::shared_ptr<const Snapshot> prev_snap = store_.get();
   store_.publish(published_snap);
@@ -1433,15 +1432,31 @@ TickInfo Exporter::tick() {
   last_tick_mono_ns_ = mono_ns();
   info.duration_s = (mono_ns() - t0) * 1e-9;
   if (cfg_.gzip) {
-    // Eager compression only while scrapes keep asking for gzip (4 of the last 8 snapshots); a
-    // slower scraper's first gzip request compresses its snapshot itself (Snapshot::gzipped).
+    // This thread compresses the new snapshot (a) while scrapes keep asking for gzip (4 of the last
+    // 8 snapshots), or (b) when a periodic gzip scraper's next scrape is predicted to land while
+    // this snapshot is current (Prometheus at 15 s on a 1 Hz exporter: 1 compression per scrape,
+    // made before the scrape arrives). Otherwise a scrape's first gzip request compresses its
+    // snapshot itself (Snapshot::gzipped): correct, at the cost of that scrape's latency.
     gz_history_ = static_cast<uint8_t>((gz_history_ << 1) | (prev_snap && prev_snap->gzip_asked() ? 1 : 0));
-    if (__builtin_popcount(gz_history_) >= 4) {
+    const bool frequent = __builtin_popcount(gz_history_) >= 4;
+    bool predicted = false;
+    const int64_t per = gz_period_ns_.load(std::memory_order_relaxed);
+    const int64_t last = gz_last_scrape_ns_.load(std::memory_order_relaxed);
+    if (!frequent && cfg_.interval_s > 0 && per > 0 && last > 0) {
+      const int64_t now = mono_ns(), life = static_cast<int64_t>(cfg_.interval_s * 1e9);
+      const int64_t slack = life / 10;
+      int64_t next = last + per;
+      // a scrape or two may have been missed (a restart, a slow network): keep the phase, but a
+      // scraper silent for more than 3 periods is gone and nothing is predicted for it
+      if (next < now - slack) next += ((now - slack - next) / per + 1) * per;
+      predicted = next - last <= 4 * per && next >= now - slack && next <= now + life + slack;
+    }
+    if (frequent || predicted) {
       const int64_t tz = mono_ns();
       TraceRange trz("gpumon.gzip");
       snap->precompress();
       info.t_gzip = (mono_ns() - tz) * 1e-9;
-      gz_eager_++;
+      (frequent ? gz_eager_ : gz_predicted_)++;
     }
     if (prev_snap && prev_snap->compressed() && !prev_snap->gzip_asked()) gz_unused_++;
   }
@@ -1702,6 +1717,17 @@ void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
     const bool fresh_gz = req.accept_gzip && s->gzip && !s->compressed();
     const std::string* gz = req.accept_gzip ? s->gzipped(true) : nullptr;
     if (fresh_gz && gz) gz_lazy_.fetch_add(1, std::memory_order_relaxed);
+    if (req.accept_gzip && s->gzip) {
+      // the gzip scrapers' cadence (EWMA of the spacing; bursts under 50 ms ignored) for the tick
+      // thread's prediction above
+      const int64_t now = mono_ns();
+      const int64_t prev = gz_last_scrape_ns_.exchange(now, std::memory_order_relaxed);
+      const int64_t d = prev > 0 ? now - prev : 0;
+      if (d > 50'000'000) {
+        const int64_t p = gz_period_ns_.load(std::memory_order_relaxed);
+        gz_period_ns_.store(p > 0 && d < 8 * p ? (3 * p + d) / 4 : d, std::memory_order_relaxed);
+      }
+    }
     if (gz) {
       resp->extra_headers = "Content-Encoding: gzip\r\n";
       resp->data = gz->data();
@@ -1851,6 +1877,7 @@ SelfStats Exporter::self_stats() const {
   s.gzip_eager = gz_eager_.load(std::memory_order_relaxed);
   s.gzip_lazy = gz_lazy_.load(std::memory_order_relaxed);
   s.gzip_unused = gz_unused_.load(std::memory_order_relaxed);
+  s.gzip_predicted = gz_predicted_.load(std::memory_order_relaxed);
   if (backend_)
     for (const auto& c : backend_->call_stats()) s.backend_calls.push_back({c.call, c.n, c.errors, c.seconds});
   {

@@ -303,7 +303,8 @@ class Exporter {
   std::vector<std::shared_ptr<const TickState>> last_ok_;
   uint8_t gz_history_ = 0;  // bit k: the snapshot k ticks back was scraped with gzip (tick thread)
   // snapshot compressions: eager (tick thread), lazy (by a scrape), and eager ones nobody fetched
-  std::atomic<uint64_t> gz_eager_{0}, gz_lazy_{0}, gz_unused_{0};
+  std::atomic<uint64_t> gz_eager_{0}, gz_lazy_{0}, gz_unused_{0}, gz_predicted_{0};
+  std::atomic<int64_t> gz_last_scrape_ns_{0}, gz_period_ns_{0};  // gzip scrapers' last time and cadence
   size_t last_body_bytes_ = 0;  // tick thread only: sizes the next render buffer
   std::atomic<uint64_t> phase_ns_[5] = {};  // sample, procs, attrib, render, gzip (cumulative)
 

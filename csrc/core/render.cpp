@@ -943,9 +943,11 @@ void render_prometheus(const RenderInput& in, std::string* o) {
     {
       Family f(o, "gpumon_snapshot_compressions_total",
                "gzip compressions of the /metrics snapshot: eager (the tick thread, while most snapshots are "
-               "scraped with gzip) or lazy (by the first gzip scrape of a snapshot).", "counter");
-      if (s.gzip_eager || s.gzip_lazy) {
+               "scraped with gzip), predicted (the tick thread, for a periodic scraper's next scrape) or lazy "
+               "(by the first gzip scrape of a snapshot).", "counter");
+      if (s.gzip_eager || s.gzip_lazy || s.gzip_predicted) {
         f.add(hl, {{"mode", "eager"}}, static_cast<double>(s.gzip_eager));
+        f.add(hl, {{"mode", "predicted"}}, static_cast<double>(s.gzip_predicted));
         f.add(hl, {{"mode", "lazy"}}, static_cast<double>(s.gzip_lazy));
       }
     }
@@ -953,7 +955,7 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       Family f(o, "gpumon_snapshot_compressions_unused_total",
                "Eager snapshot compressions no scrape fetched before the next tick replaced the snapshot.",
                "counter");
-      if (s.gzip_eager) f.add(hl, static_cast<double>(s.gzip_unused));
+      if (s.gzip_eager || s.gzip_predicted) f.add(hl, static_cast<double>(s.gzip_unused));
     }
     {
       Family f(o, "gpumon_influx_up",

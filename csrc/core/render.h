@@ -81,7 +81,7 @@ struct SelfStats {
   uint64_t pods_attributed = 0;
   uint64_t attribution_cache_hits = 0, attribution_cache_misses = 0;
   uint64_t influx_ok = 0, influx_fail = 0, influx_dropped = 0;
-  uint64_t gzip_eager = 0, gzip_lazy = 0, gzip_unused = 0;  // snapshot compressions
+  uint64_t gzip_eager = 0, gzip_lazy = 0, gzip_unused = 0, gzip_predicted = 0;  // snapshot compressions
   uint64_t kfd_files_open = 0, kfd_reads_cached = 0;        // sysfs fast path: kept KFD per-pid files
   bool influx_enabled = false;  // a push URL is configured
   int influx_up = 0;            // the last push attempt succeeded

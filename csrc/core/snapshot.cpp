@@ -1,8 +1,12 @@
 #include "snapshot.h"
 
+#include "common.h"
+
 #include <zlib.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <cmath>
 
 namespace gpumon {
@@ -100,7 +104,17 @@ bool gzip_compress(const std::string& in, std::string* out, int level) {
 const std::string* Snapshot::gzipped(bool compress_now) const {
   if (!gzip) return nullptr;
   gz_asked_.store(true, std::memory_order_relaxed);
-  if (gz_state_.load(std::memory_order_acquire) == 2) return &gz_;
+  int st = gz_state_.load(std::memory_order_acquire);
+  if (st == 2) return &gz_;
+  if (st == 1) {
+    // another thread (the tick thread's eager / predicted compression, or a concurrent scrape) is
+    // compressing this snapshot right now: wait for it (0.1-0.8 ms) rather than answer with the
+    // 5-10x larger identity body; give up after 20 ms
+    const int64_t until = mono_ns() + 20'000'000;
+    while ((st = gz_state_.load(std::memory_order_acquire)) == 1 && mono_ns() < until)
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    return st == 2 ? &gz_ : nullptr;
+  }
   return compress_now ? compress() : nullptr;
 }
 
