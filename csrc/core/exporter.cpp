@@ -1,4 +1,4 @@
-#include "exporter.h"
+#include "exporter_internal.h"
 #include "tls.h"
 
 #include <pthread.h>
@@ -26,453 +26,10 @@
 
 namespace gpumon {
 
-// ---------------------------------------------------------------------------------------------
-// Per-device sampling workers with a watchdog.
-//
-// Each GPU gets its own thread; a tick hands every idle worker a request and waits until all
-// answer or `device_timeout_s` passes. A device whose call has not returned by then (a hung
-// driver/SMU call) is exported as gpu_up 0 with gpumon_device_timeouts_total incremented, and is not
-// asked again until its call returns -- the other GPUs keep their 1 Hz cadence (the reference
-// stalled the whole node on any slow nvidia-smi, gpu.py:104-116). Workers only touch their own
-// heap state and the backend, so a worker stuck at shutdown can be detached safely (the backend is
-// then deliberately leaked instead of destroyed under it).
-// ---------------------------------------------------------------------------------------------
-struct Exporter::DoneSignal {
-  std::mutex mu;
-  std::condition_variable cv;
-};
-
-struct Exporter::DevWorker {
-  std::mutex mu;
-  std::condition_variable cv;
-  bool quit = false;
-  bool pending = false;          // request posted, not yet picked up
-  bool busy = false;             // request in flight (posted or running)
-  uint64_t req = 0;              // tick id of the current request
-  std::atomic<uint64_t> done{0}; // tick id whose results are stored below
-  bool want_links = false, want_procs = false, want_ras = false;
-  bool ras_async = false;        // read the RAS slice AFTER publishing this tick (applied next tick)
-  int ras_slice = 0, ras_n = 1;
-  int64_t started_ns = 0;
-  int64_t picked_ns = 0, device_ns = 0;  // pickup time and device-call time of the stored tick
-  DeviceSample sample;
-  std::vector<ProcSample> procs;
-  int64_t proc_ns = 0;
-  std::thread th;
-};
-
-// Between ticks the worker sub-samples the KFD cu_occupancy of the processes its device had at
-// the last tick, every occ_period_ns (interval / occ_samples): one read per tick is an instant
-// (4.6 % of reads under a saturating burn land between two kernels and return 0, profiles/
-// r2_kfd_occupancy.md); the tick's process rows carry the interval mean and the share of reads
-// that found the process's waves resident.
-// SCHED_FIFO for the calling thread (rt_priority); counted in `rt` while the thread lives.
-static bool apply_rt(int prio, const std::string& who, std::atomic<int>* rt) {
-  if (prio <= 0) return false;
-  sched_param sp{};
-  sp.sched_priority = std::clamp(prio, 1, 99);
-  const int rc = pthread_setschedparam(pthread_self(), SCHED_FIFO, &sp);
-  if (rc != 0) {
-    static std::atomic<bool> warned{false};
-    if (!warned.exchange(true))
-      GPUMON_LOG(LogLevel::kWarn, "exporter",
-                 "rt_priority " + std::to_string(prio) + " for " + who + ": " + strerror(rc) +
-                     " (needs CAP_SYS_NICE); sampling threads keep normal scheduling");
-    return false;
-  }
-  rt->fetch_add(1);
-  return true;
-}
+// The exporter's tick, backend setup, Influx push and self stats. Split out: the device workers
+// (dev_workers.cpp), pod_gpu attribution (pod_rows.cpp) and the HTTP endpoints (exporter_http.cpp).
 
 static void read_process_stats(SelfStats* s);  // /proc/self figures (defined below)
-
-static void dev_worker_main(std::shared_ptr<Exporter::DevWorker> w, std::shared_ptr<Exporter::DoneSignal> sig,
-                            Backend* backend, int i, int64_t occ_period_ns,
-                            std::shared_ptr<std::atomic<uint64_t>> occ_reads,
-                            std::shared_ptr<std::atomic<uint64_t>> scan_failures, int rt_prio,
-                            std::shared_ptr<std::atomic<int>> rt_threads,
-                            std::shared_ptr<std::atomic<int64_t>> next_tick, int64_t prewarm_ns) {
-  set_thread_name("gpumon-dev" + std::to_string(i));
-  const bool rt = apply_rt(rt_prio, "device worker", rt_threads.get());
-  struct RtCount {  // the gauge counts live threads
-    bool on;
-    std::atomic<int>* n;
-    ~RtCount() {
-      if (on) n->fetch_sub(1);
-    }
-  } rt_count{rt, rt_threads.get()};
-  std::vector<uint32_t> occ_pids;                      // processes on this device at the last tick
-  std::vector<double> occ_sum;                         // per occ_pids entry
-  std::vector<int> occ_n, occ_busy;
-  std::vector<double> vals;
-  std::vector<OccRead> scan;
-  const bool occ_on = occ_period_ns > 0 && backend->supports_occupancy(i);
-  // The sub-samples list the device's processes themselves where the backend can (KFD proc dir):
-  // a tenant that started since the last tick is read from then on, not from the next tick (a
-  // 10 %-resident arrival otherwise had one read in its first interval).
-  bool scan_ok = occ_on;
-  // A failed listing (a transient opendir / read error) is retried with a backoff (1 s doubling to
-  // 60 s), not latched off for the worker's life; only a backend that stopped supporting the read
-  // ends the scans. In between, the known pids are re-read as before.
-  int64_t scan_retry_at = 0, scan_backoff_ns = 1'000'000'000;
-  // Every 4th sub-sample lists the directory (new tenants show up within 4 periods, 0.2 s at 1 Hz);
-  // the others re-read the known pids only: a node-wide KFD listing per GPU per sub-sample would
-  // cost P opens each time on a node with P GPU processes.
-  constexpr int kScanEvery = 4;
-  uint64_t n_sub = 0;
-  int64_t next_occ = 0;
-  // Prewarm: one throwaway firmware-table read prewarm_ns before each tick's deadline, so the
-  // tick's own read finds the SMU's fetch path awake (~50 us instead of 150-300 us after a long
-  // gap, profiles/r3_capacity.md). Once per deadline; skipped when the deadline is already close.
-  int64_t warmed_for = 0;
-  // The process list (KFD + fdinfo reads, ~0.1 ms) runs on a second thread while this one reads
-  // the firmware table (~0.2 ms, mostly the SMU fetch): the device's part of a tick becomes the
-  // longer of the two instead of their sum. Only where the backend allows it (sysfs fast path).
-  struct ProcJob {
-    std::mutex mu;
-    std::condition_variable cv;
-    bool want = false, done = false, quit = false;
-    std::vector<ProcSample> out;
-    bool ok = false;
-    int64_t ns = 0;
-  };
-  std::shared_ptr<ProcJob> job;
-  std::thread proc_thread;
-  if (backend->concurrent_processes(i)) {
-    job = std::make_shared<ProcJob>();
-    proc_thread = std::thread([job, backend, i] {
-      set_thread_name("gpumon-proc" + std::to_string(i));
-      std::unique_lock<std::mutex> lk(job->mu);
-      for (;;) {
-        job->cv.wait(lk, [&] { return job->want || job->quit; });
-        if (job->quit) return;
-        job->want = false;
-        lk.unlock();
-        std::vector<ProcSample> p;
-        const int64_t t = mono_ns();
-        const bool ok = backend->processes(i, &p);
-        const int64_t ns = mono_ns() - t;
-        lk.lock();
-        job->out = std::move(p);
-        job->ok = ok;
-        job->ns = ns;
-        job->done = true;
-        job->cv.notify_all();
-      }
-    });
-  }
-  struct ProcJoin {  // every return path: stop and join the process-list thread
-    std::shared_ptr<ProcJob>& job;
-    std::thread& th;
-    ~ProcJoin() {
-      if (!job) return;
-      {
-        std::lock_guard<std::mutex> g(job->mu);
-        job->quit = true;
-      }
-      job->cv.notify_all();
-      if (th.joinable()) th.join();
-    }
-  } proc_join{job, proc_thread};
-  // RAS refreshes read off the tick's critical path: the worker reads the slice right after it
-  // published the tick (the files cost 0.25-0.5 ms under load: the slowest tick of every RAS pass,
-  // profiles/r2_bench.md) and the next tick carries the result.
-  RasSample ras_ready;
-  bool have_ras_ready = false;
-  uint64_t jitter = 0x9E3779B97F4A7C15ull * static_cast<uint64_t>(i + 1);  // per-worker LCG state
-  while (true) {
-    uint64_t id;
-    bool links, procs, ras, ras_async;
-    int ras_slice, ras_n;
-    {
-      std::unique_lock<std::mutex> lk(w->mu);
-      bool subsample = false, warm = false;
-      while (!w->quit && !w->pending) {
-        const int64_t now = mono_ns();
-        int64_t wake = INT64_MAX;
-        if (prewarm_ns > 0) {
-          const int64_t nt = next_tick->load(std::memory_order_acquire);
-          if (nt > 0 && nt != warmed_for) {
-            if (now >= nt - prewarm_ns) {
-              warmed_for = nt;
-              if (now < nt - prewarm_ns / 4) {  // not when the tick is about to sample anyway
-                warm = true;
-                break;
-              }
-            } else {
-              wake = nt - prewarm_ns;
-            }
-          }
-        }
-        if (occ_on && !(occ_pids.empty() && !scan_ok)) {
-          if (next_occ <= now) {
-            subsample = true;
-            break;
-          }
-          wake = std::min(wake, next_occ);
-        }
-        if (wake == INT64_MAX) {
-          w->cv.wait(lk);
-          continue;
-        }
-        // system_clock slices checked against the monotonic deadline (TSan: see sample_devices)
-        w->cv.wait_until(lk, std::chrono::system_clock::now() +
-                                 std::chrono::nanoseconds(std::min<int64_t>(wake - now, 20'000'000)));
-      }
-      if (w->quit) return;
-      if (warm) {
-        lk.unlock();
-        TraceRange tr("gpumon.prewarm");
-        backend->prewarm(i);
-        continue;
-      }
-      if (subsample) {
-        lk.unlock();
-        const bool scan_turn = scan_ok && (n_sub++ % kScanEvery == 0) && mono_ns() >= scan_retry_at;
-        bool scanned = false;
-        if (scan_turn) {
-          scanned = backend->occupancy_scan(i, &scan);
-          scan_failures->fetch_add(scanned ? 0 : 1, std::memory_order_relaxed);
-          if (scanned) {
-            scan_backoff_ns = 1'000'000'000;
-          } else if (!backend->supports_occupancy(i)) {
-            scan_ok = false;
-          } else {
-            scan_retry_at = mono_ns() + scan_backoff_ns;
-            scan_backoff_ns = std::min<int64_t>(scan_backoff_ns * 2, 60'000'000'000);
-          }
-        }
-        if (scanned) {
-          vals.assign(occ_pids.size(), kNaN);
-          for (const OccRead& r : scan) {
-            size_t k = std::find(occ_pids.begin(), occ_pids.end(), r.pid) - occ_pids.begin();
-            if (k == occ_pids.size()) {  // arrived since the last tick
-              occ_pids.push_back(r.pid);
-              occ_sum.push_back(0.0);
-              occ_n.push_back(0);
-              occ_busy.push_back(0);
-              vals.push_back(kNaN);
-            }
-            vals[k] = r.cu_occupancy;
-          }
-          occ_reads->fetch_add(scan.size(), std::memory_order_relaxed);
-        } else {
-          backend->occupancy(i, occ_pids, &vals);
-          occ_reads->fetch_add(occ_pids.size(), std::memory_order_relaxed);
-        }
-        for (size_t k = 0; k < occ_pids.size() && k < vals.size(); ++k)
-          if (has(vals[k])) {
-            occ_sum[k] += vals[k];
-            occ_n[k]++;
-            occ_busy[k] += vals[k] > 0 ? 1 : 0;
-          }
-        // jittered spacing (0.5-1.5 periods, same mean): fixed-period reads phase-lock to a
-        // periodic workload (host-synchronised batches) and keep hitting -- or missing -- its gaps
-        jitter = jitter * 6364136223846793005ull + 1442695040888963407ull;
-        const double u = static_cast<double>(jitter >> 11) * (1.0 / 9007199254740992.0);
-        next_occ += static_cast<int64_t>(occ_period_ns * (0.5 + u));
-        if (next_occ < mono_ns()) next_occ = mono_ns() + occ_period_ns;
-        continue;
-      }
-      w->pending = false;
-      w->picked_ns = mono_ns();
-      id = w->req;
-      links = w->want_links;
-      procs = w->want_procs;
-      ras = w->want_ras;
-      ras_async = w->ras_async;
-      ras_slice = w->ras_slice;
-      ras_n = w->ras_n;
-    }
-    DeviceSample s;
-    std::vector<ProcSample> p;
-    int64_t pns = 0;
-    const int64_t t_dev0 = mono_ns();
-    {
-      TraceRange tr("gpumon.sample_dev");
-      const bool overlap = procs && job;
-      if (overlap) {
-        std::lock_guard<std::mutex> g(job->mu);
-        job->want = true;
-        job->done = false;
-      }
-      if (overlap) job->cv.notify_all();
-      backend->sample(i, &s);
-      if (links) backend->sample_links(i, &s);
-      if (have_ras_ready && s.ok) {
-        s.ras = std::move(ras_ready);
-        have_ras_ready = false;
-      }
-      if (ras && !ras_async && s.ok) backend->sample_ras(i, &s, ras_slice, ras_n);
-      if (overlap) {
-        std::unique_lock<std::mutex> lk(job->mu);
-        job->cv.wait(lk, [&] { return job->done; });
-        if (s.ok) {
-          p = std::move(job->out);
-          pns = job->ns;
-          s.procs_read = job->ok ? 1 : backend->supports_processes(i) ? -1 : 0;
-        }
-        job->out.clear();
-      } else if (procs && s.ok) {
-        const int64_t t = mono_ns();
-        const bool ok = backend->processes(i, &p);
-        pns = mono_ns() - t;
-        s.procs_read = ok ? 1 : backend->supports_processes(i) ? -1 : 0;
-      }
-    }
-    const bool ok_for_ras = s.ok;
-    const int64_t dev_ns = mono_ns() - t_dev0;
-    // fold the interval's sub-samples into this tick's reading (with sub-sampling on, the tick's
-    // process list skips its own cu_occupancy read: Exporter::start_workers, set_tick_occupancy)
-    for (auto& ps : p) {
-      if (!has(ps.cu_occupancy) && !occ_on) continue;
-      double sum = has(ps.cu_occupancy) ? ps.cu_occupancy : 0.0;
-      int n = has(ps.cu_occupancy) ? 1 : 0, busy = ps.cu_occupancy > 0 ? 1 : 0;
-      for (size_t k = 0; k < occ_pids.size(); ++k)
-        if (occ_pids[k] == ps.pid) {
-          sum += occ_sum[k];
-          n += occ_n[k];
-          busy += occ_busy[k];
-          break;
-        }
-      ps.cu_occupancy = n > 0 ? sum / n : kNaN;
-      ps.occ_samples = n;
-      ps.occ_busy = busy;
-    }
-    // A listed process that arrived since the last list (no sub-sample could know it) gets one read
-    // now, so its first row is not empty. Only new pids: a known pid whose reads keep returning
-    // nothing (NaN) would otherwise cost an extra open on the tick's path every tick.
-    if (occ_on) {
-      std::vector<uint32_t> unread;
-      for (const auto& ps : p)
-        if (ps.occ_samples == 0 && std::find(occ_pids.begin(), occ_pids.end(), ps.pid) == occ_pids.end())
-          unread.push_back(ps.pid);
-      if (!unread.empty()) {
-        backend->occupancy(i, unread, &vals);
-        occ_reads->fetch_add(unread.size(), std::memory_order_relaxed);
-        size_t k = 0;
-        for (auto& ps : p)
-          if (ps.occ_samples == 0 && k < vals.size() && ps.pid == unread[k]) {
-            const double v = vals[k++];
-            if (!has(v)) continue;
-            ps.cu_occupancy = v;
-            ps.occ_samples = 1;
-            ps.occ_busy = v > 0 ? 1 : 0;
-          }
-      }
-    }
-    // a failed tick (or a failed process list) listed nothing: keep sub-sampling the known pids.
-    // The sums restart every tick either way: a failed list's interval is not folded into the next
-    // good tick's mean (two intervals averaged as one); the held rows carry no occupancy.
-    if (occ_on && procs && ok_for_ras && s.procs_read >= 0) {
-      occ_pids.clear();
-      for (const auto& ps : p)
-        if (std::find(occ_pids.begin(), occ_pids.end(), ps.pid) == occ_pids.end()) occ_pids.push_back(ps.pid);
-      next_occ = mono_ns() + occ_period_ns;
-    }
-    if (occ_on && procs) {
-      occ_sum.assign(occ_pids.size(), 0.0);
-      occ_n.assign(occ_pids.size(), 0);
-      occ_busy.assign(occ_pids.size(), 0);
-    }
-    {
-      std::lock_guard<std::mutex> g(w->mu);
-      w->sample = std::move(s);
-      w->procs = std::move(p);
-      w->proc_ns = pns;
-      w->device_ns = dev_ns;
-      w->busy = false;
-      w->done.store(id, std::memory_order_release);
-      if (w->quit) {
-        std::lock_guard<std::mutex> g2(sig->mu);
-        sig->cv.notify_all();
-        return;
-      }
-    }
-    {
-      std::lock_guard<std::mutex> g(sig->mu);
-      sig->cv.notify_all();
-    }
-    if (ras && ras_async && ok_for_ras) {
-      TraceRange tr("gpumon.ras_async");
-      DeviceSample scratch;
-      backend->sample_ras(i, &scratch, ras_slice, ras_n);
-      if (scratch.ras.valid) {
-        ras_ready = std::move(scratch.ras);
-        have_ras_ready = true;
-      }
-    }
-    if (procs) backend->maintain(i);
-  }
-}
-
-void Exporter::start_workers(int n) {
-  stop_workers();
-  if (!done_sig_) done_sig_ = std::make_shared<DoneSignal>();
-  for (int i = 0; i < n; ++i) {
-    auto w = std::make_shared<DevWorker>();
-    // sub-sample period: interval / occ_samples, no faster than 50 Hz; manual ticks: none
-    const int64_t occ_ns = cfg_.interval_s > 0 && cfg_.occ_samples > 1 && cfg_.processes
-                               ? std::max<int64_t>(20'000'000, static_cast<int64_t>(cfg_.interval_s * 1e9 / cfg_.occ_samples))
-                               : 0;
-    // the workers' sub-samples stand in for the tick's own cu_occupancy read (the costliest
-    // per-process file: ~27 us, a KFD walk over the process's queues)
-    if (i == 0) backend_->set_tick_occupancy(occ_ns == 0 || !backend_->supports_occupancy(i));
-    // prewarm only at intervals >= 20 ms: a read within ~5 ms of the last one is warm already, and
-    // the lead is capped at a quarter of the interval
-    const int64_t prewarm_ns = cfg_.interval_s >= 0.02 && cfg_.prewarm_ms > 0
-                                   ? static_cast<int64_t>(std::min(cfg_.prewarm_ms, cfg_.interval_s * 250.0) * 1e6)
-                                   : 0;
-    w->th = std::thread(dev_worker_main, w, done_sig_, backend_.get(), i, occ_ns, occ_reads_, scan_failures_,
-                        cfg_.rt_priority,
-                        rt_threads_, next_tick_ns_, prewarm_ns);
-    workers_.push_back(std::move(w));
-  }
-}
-
-// Returns false if a worker was stuck in a device call and had to be detached.
-bool Exporter::stop_workers() {
-  bool clean = true;
-  for (auto& w : workers_) {
-    bool busy;
-    {
-      std::lock_guard<std::mutex> g(w->mu);
-      w->quit = true;
-      busy = w->busy && !w->pending;
-    }
-    w->cv.notify_all();
-    if (busy) {
-      // give an in-flight call a moment to return before giving up on it
-      const int64_t until = mono_ns() + 200'000'000;
-      while (mono_ns() < until) {
-        {
-          std::lock_guard<std::mutex> g(w->mu);
-          if (!w->busy) break;
-        }
-        std::this_thread::sleep_for(std::chrono::milliseconds(5));
-      }
-      std::lock_guard<std::mutex> g(w->mu);
-      busy = w->busy;
-    }
-    if (busy) {
-      GPUMON_LOG(LogLevel::kError, "exporter", "device worker stuck in a backend call at shutdown: detaching it");
-      w->th.detach();
-      clean = false;
-    } else if (w->th.joinable()) {
-      w->th.join();
-    }
-  }
-  workers_.clear();
-  return clean;
-}
-
-bool Exporter::workers_busy() const {
-  for (const auto& w : workers_) {
-    std::lock_guard<std::mutex> g(w->mu);
-    if (w->busy) return true;
-  }
-  return false;
-}
 
 // ---------------------------------------------------------------------------------------------
 static MockConfig parse_mock_spec(const std::string& spec, MockConfig base) {
@@ -881,258 +438,6 @@ void Exporter::set_device_mfma_util(std::map<int, double> v) {
   mfma_util_ = std::move(v);
 }
 
-void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
-                              const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows) {
-  rows->clear();
-  // Exclusive use: the one process of a device whose waves were resident this interval (every
-  // process counts, opted in or not). Its row carries the device's MFMA utilisation.
-  std::map<int, double> mfma;
-  {
-    std::lock_guard<std::mutex> g(extra_mu_);
-    mfma = mfma_util_;
-  }
-  // Shared vs exclusive (the reference dashboard's "(共享)" / "(独占)" columns, which counted the
-  // pod_gpu rows of nvidia-smi's complete compute-apps list per GPU, gpu.py:111-116,190-219). A
-  // non-helper process is a possible sharer of its device
-  //  - while its waves were resident in any occupancy read of the tick (sub-samples included),
-  //  - from the tick it ARRIVES holding VRAM, before any read could catch its waves (a 10 %-resident
-  //    tenant is not read as absent in its first interval: VERDICT r2 #1), and
-  //  - where residency is not observable on the device (no occupancy reads), while it holds VRAM;
-  // and stops counting only after 5 ticks and mfma_exclusive_window_s without any of that (a
-  // 10 %-resident tenant escapes 20 reads per tick 12 % of the time, the window's 100 reads 0.003 %).
-  // The device is exclusive when one process is a sharer: its row carries the device MFMA util.
-  std::vector<uint32_t> sole(procs.size(), 0);
-  // The exporter's own on-device helper holds a GPU context on every device (PMC counter buffers)
-  // and, with --probe, runs the K1 probe's waves: it is neither a workload row nor a sharer.
-  const int helper_pid = ondevice_helper_pid();
-  auto is_helper = [&](uint32_t pid) { return helper_pid > 0 && pid == static_cast<uint32_t>(helper_pid); };
-  uint64_t helper_rows = 0;
-  const uint64_t tick_no = ++pod_rows_built_;
-  const int64_t now_ns = mono_ns();
-  const int64_t window_ns = static_cast<int64_t>(std::max(0.0, cfg_.mfma_exclusive_window_s) * 1e9);
-  if (last_active_.size() < procs.size()) last_active_.resize(procs.size());
-  if (present_.size() < procs.size()) present_.resize(procs.size());
-  if (sharing_source_.size() < procs.size()) sharing_source_.resize(procs.size());
-  static const char* kSharingHelp =
-      "Processes that may be using the GPU within the exclusivity window (5 ticks and "
-      "mfma_exclusive_window_s): 0 idle, 1 exclusive, >1 shared. source=occupancy: waves resident in a KFD "
-      "cu_occupancy read, or arrived holding VRAM; source=vram: every process holding VRAM (occupancy "
-      "unreadable); source=allocations: pods allocated the GPU (process list off).";
-  std::vector<ExtraSeries> sharing;
-  // Peer contexts of multi-GPU processes (the usual 8-GPU tenant: torchrun with one rank per GPU,
-  // each rank's runtime also opening every other GPU, RCCL importing peers' buffers). A (pid, GPU)
-  // context is a peer context -- not a workload row, not a sharer -- when on that GPU it holds at
-  // most peer_context_max_vram_mib, had no wave resident within the sharing window (where
-  // occupancy is readable), and the same process has a workload context on ANOTHER GPU this tick
-  // (more VRAM than that, or waves). The reference listed one row per compute app nvidia-smi
-  // showed on a GPU (gpu.py:111-116,178,190-219): a rank appears on its own GPU only.
-  if (last_waves_.size() < procs.size()) last_waves_.resize(procs.size());
-  const double peer_floor = std::max(0.0, cfg_.peer_context_max_vram_mib) * 1048576.0;
-  std::unordered_map<uint32_t, std::vector<int>> workload_devs;  // pid -> GPUs with a workload context
-  std::vector<std::unordered_map<uint32_t, double>> vram_of(procs.size());  // (dev, pid) -> VRAM, contexts summed
-  for (size_t d = 0; d < procs.size(); ++d) {
-    auto& waves = last_waves_[d];
-    for (const auto& p : procs[d]) {
-      if (is_helper(p.pid)) continue;
-      const double v = p.vram_bytes > 0 ? p.vram_bytes : (p.mem_bytes > 0 ? p.mem_bytes : 0.0);
-      vram_of[d][p.pid] += v;
-      if (p.occ_busy > 0 || p.cu_occupancy > 0) waves[p.pid] = {tick_no, now_ns};
-    }
-    for (auto it = waves.begin(); it != waves.end();) {  // forget pids past both windows
-      if (tick_no - it->second.first >= 5 && now_ns - it->second.second >= window_ns) it = waves.erase(it);
-      else ++it;
-    }
-    for (const auto& [pid, v] : vram_of[d])
-      if (v > peer_floor || waves.count(pid)) workload_devs[pid].push_back(static_cast<int>(d));
-  }
-  auto is_peer = [&](size_t d, uint32_t pid) {
-    if (peer_floor <= 0 || !cfg_.hide_empty_contexts) return false;
-    if (last_waves_[d].count(pid)) return false;
-    auto v = vram_of[d].find(pid);
-    if (v != vram_of[d].end() && v->second > peer_floor) return false;
-    auto w = workload_devs.find(pid);
-    return w != workload_devs.end() &&
-           std::any_of(w->second.begin(), w->second.end(), [&](int o) { return o != static_cast<int>(d); });
-  };
-  for (size_t d = 0; d < procs.size(); ++d) {
-    if (!cfg_.processes) {  // no process list: the kubelet's allocations are what is known
-      std::vector<std::pair<std::string, std::string>> pods;
-      for (const auto& a : attr_->allocations())
-        if (a.gpu_index == static_cast<int>(d) &&
-            std::find(pods.begin(), pods.end(), std::make_pair(a.pod_namespace, a.pod_name)) == pods.end())
-          pods.emplace_back(a.pod_namespace, a.pod_name);
-      sharing.push_back({"gpu_active_processes", kSharingHelp, "gauge", static_cast<int>(d),
-                         {{"source", "allocations"}}, static_cast<double>(pods.size())});
-      continue;
-    }
-    auto& seen = last_active_[d];
-    auto& present = present_[d];
-    // residency is observable where occupancy can be read (also on a tick where no read has landed
-    // yet for anyone: the first tick after start, a process that just arrived)
-    const bool observable = std::any_of(procs[d].begin(), procs[d].end(),
-                                        [](const ProcSample& p) { return p.occ_samples > 0; }) ||
-                            (backend_ && backend_->supports_occupancy(static_cast<int>(d)));
-    std::vector<uint32_t> active;  // distinct pids (one process may hold several KFD contexts)
-    std::unordered_set<uint32_t> listed;
-    for (const auto& p : procs[d]) {
-      if (is_helper(p.pid) || is_peer(d, p.pid)) continue;
-      const bool holds = p.vram_bytes > 0 || p.mem_bytes > 0;
-      const bool waves = p.occ_busy > 0 || p.cu_occupancy > 0;
-      if (holds || waves) listed.insert(p.pid);
-      const bool arrived = holds && !present.count(p.pid);
-      if ((waves || arrived || (!observable && holds)) && std::find(active.begin(), active.end(), p.pid) == active.end())
-        active.push_back(p.pid);
-    }
-    // A tick whose device sample failed has no process list: it must not make every process look
-    // like a new arrival on the next good tick, so the last list is kept.
-    const bool listed_ok = d >= samples.size() || samples[d].ok;
-    if (listed_ok) present.swap(listed);
-    for (uint32_t pid : active) seen[pid] = {tick_no, now_ns};
-    for (auto it = seen.begin(); it != seen.end();) {  // forget pids past both windows
-      if (tick_no - it->second.first >= 5 && now_ns - it->second.second >= window_ns) it = seen.erase(it);
-      else ++it;
-    }
-    if (active.size() == 1 && seen.size() == 1) sole[d] = active[0];
-    std::string& src = sharing_source_[d];
-    if (observable) src = "occupancy";
-    else if (!procs[d].empty()) src = "vram";
-    else if (src.empty()) src = backend_ && backend_->supports_occupancy(static_cast<int>(d)) ? "occupancy" : "vram";
-    sharing.push_back({"gpu_active_processes", kSharingHelp, "gauge", static_cast<int>(d), {{"source", src}},
-                       static_cast<double>(seen.size())});
-  }
-  for (const auto& dev_procs : procs)
-    for (const auto& p : dev_procs) helper_rows += is_helper(p.pid) ? 1 : 0;
-  if (helper_pid > 0)
-    sharing.push_back({"gpumon_ondevice_helper_gpu_contexts",
-                     "GPU contexts of the exporter's own on-device helper (PMC counting / K1 probe), left out of "
-                     "pod_gpu rows and gpu_active_processes.",
-                     "gauge", -1, {}, static_cast<double>(helper_rows)});
-  set_extra("sharing", std::move(sharing));
-  uint64_t hidden = 0, hidden_peer = 0;
-  std::vector<uint32_t> alive;
-  std::unordered_map<ProcKey, ProcPrev, ProcKeyHash> next_prev;
-  // (ns, pod, container, dev) with an active process -> suppress the idle row for it
-  std::vector<std::tuple<std::string, std::string, std::string, int>> active;
-  for (size_t d = 0; d < procs.size(); ++d) {
-    double dev_util = d < samples.size() ? samples[d].v[F_GFX_UTIL] : kNaN;
-    // a held process list (the last good one, this tick's failed) carries no new engine time
-    const bool held = d < samples.size() && samples[d].procs_held;
-    // One row per (pid, device): duplicate entries (several KFD contexts of one process) are merged,
-    // a duplicate series would make Prometheus reject the whole scrape.
-    std::unordered_map<uint32_t, size_t> row_of_pid;
-    for (const auto& p : procs[d]) {
-      if (is_helper(p.pid)) continue;  // counted in gpumon_ondevice_helper_gpu_contexts
-      auto dup = row_of_pid.find(p.pid);
-      if (dup != row_of_pid.end()) {
-        PodRow& r = (*rows)[dup->second];
-        r.used_memory_bytes += has(p.vram_bytes) ? p.vram_bytes : 0;
-        if (has(p.cu_occupancy)) r.cu_occupancy = has(r.cu_occupancy) ? r.cu_occupancy + p.cu_occupancy : p.cu_occupancy;
-        continue;
-      }
-      // A KFD context that holds no VRAM and never had a wave resident this interval (a runtime
-      // that only probed the device: rocminfo, amd-smi, an exporter's own HIP init) is not a GPU
-      // workload; rows for it read as phantom 0-MiB processes. Counted, not exported.
-      if (cfg_.hide_empty_contexts && !(p.vram_bytes > 0) && !(p.mem_bytes > 0) && !(p.cu_occupancy > 0) &&
-          p.occ_busy == 0) {
-        hidden++;
-        continue;
-      }
-      if (is_peer(d, p.pid)) {  // a multi-GPU process's context on a GPU it does not work on (above)
-        hidden_peer++;
-        continue;
-      }
-      alive.push_back(p.pid);
-      ProcIdentity id = attr_->resolve(p.pid);
-      // per-process gfx util from engine_usage.gfx ns deltas
-      double util = kNaN;
-      int64_t now = mono_ns();
-      if (p.has_gfx_ns) {
-        ProcKey k{p.pid, static_cast<int>(d)};
-        auto it = proc_prev_.find(k);
-        if (held) {
-          // the held list repeats the last reading: keep its baseline (the next good list's delta
-          // then spans the whole gap) and its busy share, rather than a 0 % now and a spike later
-          if (it != proc_prev_.end()) {
-            next_prev[k] = it->second;
-            util = it->second.util;
-          }
-        } else {
-          if (it != proc_prev_.end() && it->second.starttime == id.starttime &&
-              p.gfx_ns >= it->second.gfx_ns && now > it->second.t_ns)
-            util = std::min(100.0, (p.gfx_ns - it->second.gfx_ns) * 100.0 / (now - it->second.t_ns));
-          next_prev[k] = ProcPrev{p.gfx_ns, now, id.starttime, util};
-        }
-      }
-      // HIP compute runs on KFD user queues, which DRM fdinfo engine time never sees: there the
-      // process's busy % is the share of the interval's cu_occupancy reads that found its waves
-      // resident (the per-process analogue of the device's gfx activity)
-      if (!has(util) && p.occ_samples > 0) util = 100.0 * p.occ_busy / p.occ_samples;
-      if (!id.opted_in) continue;
-      PodRow r;
-      r.dev = static_cast<int>(d);
-      r.idle = false;
-      r.pid = std::to_string(p.pid);
-      std::string name = !p.name.empty() ? p.name : id.comm;
-      // reference strips spaces from process names (gpu.py:203); keep them but escape properly
-      r.procname = name.empty() ? "-" : name;
-      r.pod_namespace = id.pod_namespace;
-      r.pod_name = id.pod_name;
-      r.container = id.container_name.empty() ? "-" : id.container_name;
-      r.containerid = id.container_id.empty() ? "-" : id.container_id.substr(0, 12);
-      r.user_name = id.user_name;
-      r.extra_labels = std::move(id.extra_labels);
-      r.used_memory_bytes = has(p.vram_bytes) ? p.vram_bytes : (has(p.mem_bytes) ? p.mem_bytes : 0);
-      r.gpu_util = has(dev_util) ? dev_util : 0;
-      r.proc_gfx_util = util;
-      r.cu_occupancy = p.cu_occupancy;
-      r.occ_samples = p.occ_samples;
-      if (sole[d] == p.pid)
-        if (auto m = mfma.find(static_cast<int>(d)); m != mfma.end()) r.mfma_util = m->second;
-      // only a process attributed to a pod or container can stand in for its idle allocation row
-      // (an unattributed host process reads "-" / "-" and must not swallow the allocation of a pod
-      // whose name was unknown, also "-")
-      if (r.pod_name != "-" || r.containerid != "-")
-        active.emplace_back(r.pod_namespace, r.pod_name, r.container, r.dev);
-      row_of_pid[p.pid] = rows->size();
-      rows->push_back(std::move(r));
-    }
-  }
-  proc_prev_.swap(next_prev);
-  hidden_contexts_ = hidden;
-  hidden_peer_contexts_ = hidden_peer;
-  attr_->gc(alive);
-  // Allocated-but-idle GPUs (reference gpu.py:220-253 via `docker exec nvidia-smi -L`; here the
-  // kubelet PodResources allocation list pushed by the control plane).
-  for (const auto& a : attr_->allocations()) {
-    if (a.gpu_index < 0 || a.gpu_index >= static_cast<int>(procs.size())) continue;  // Q5
-    if (!attr_->opted_in(a.labels)) continue;
-    std::string ns = a.pod_namespace.empty() ? "-" : a.pod_namespace;
-    std::string pod = a.pod_name.empty() ? "-" : a.pod_name;
-    std::string ctr = a.container_name.empty() ? "-" : a.container_name;
-    bool busy = false;
-    for (const auto& t : active)
-      if (std::get<0>(t) == ns && std::get<1>(t) == pod && std::get<3>(t) == a.gpu_index &&
-          (std::get<2>(t) == ctr || std::get<2>(t) == "-")) {
-        busy = true;
-        break;
-      }
-    if (busy) continue;
-    // the same (pod, container, GPU) listed twice must still be one series
-    active.emplace_back(ns, pod, ctr, a.gpu_index);
-    PodRow r;
-    r.dev = a.gpu_index;
-    r.idle = true;
-    r.pod_namespace = ns;
-    r.pod_name = pod;
-    r.container = ctr;
-    r.containerid = a.container_id.empty() ? "-" : a.container_id.substr(0, 12);
-    r.user_name = !a.user_name.empty() ? a.user_name : attr_->derive_user(pod, a.labels);
-    r.extra_labels = attr_->export_labels(a.labels);
-    r.used_memory_bytes = 0;
-    r.gpu_util = 0;
-    rows->push_back(std::move(r));
-  }
-}
 
 TickInfo Exporter::tick() {
   std::lock_guard<std::mutex> tl(tick_mu_);
@@ -1604,164 +909,6 @@ bool Exporter::healthy() const {
   return last != 0 && (mono_ns() - last) * 1e-9 < stale;
 }
 
-namespace {
-
-std::string url_decode(const std::string& s) {
-  std::string o;
-  for (size_t i = 0; i < s.size(); ++i) {
-    if (s[i] == '+') {
-      o.push_back(' ');
-    } else if (s[i] == '%' && i + 2 < s.size() && isxdigit(static_cast<unsigned char>(s[i + 1])) &&
-               isxdigit(static_cast<unsigned char>(s[i + 2]))) {
-      o.push_back(static_cast<char>(std::stoi(s.substr(i + 1, 2), nullptr, 16)));
-      i += 2;
-    } else {
-      o.push_back(s[i]);
-    }
-  }
-  return o;
-}
-
-// Bounds on a per-request filter: the globs come from any client that can reach the port, and a
-// filter runs on an HTTP loop thread. Matching is O(glob x name) (glob_match), so these keep one
-// request's work to ~32 globs x 128 chars x ~150 family names.
-constexpr size_t kMaxFilterQuery = 8192, kMaxFilterGlobs = 32, kMaxGlobLen = 128;
-
-// include=a,b&exclude=c (each repeatable): the family globs of a per-request filter.
-// 1 = a filter, 0 = no filter keys, -1 = over the bounds above (*err says which).
-int parse_filter_query(const std::string& q, std::vector<std::string>* inc, std::vector<std::string>* exc,
-                       std::string* err) {
-  if (q.size() > kMaxFilterQuery) {
-    *err = "query longer than " + std::to_string(kMaxFilterQuery) + " bytes";
-    return -1;
-  }
-  bool any = false;
-  for (const auto& kv : split(q, '&')) {
-    const size_t eq = kv.find('=');
-    if (eq == std::string::npos) continue;
-    const std::string k = url_decode(kv.substr(0, eq));
-    std::vector<std::string>* dst = k == "include" ? inc : k == "exclude" ? exc : nullptr;
-    if (!dst) continue;
-    any = true;
-    for (const auto& g : split(url_decode(kv.substr(eq + 1)), ',')) {
-      if (g.empty()) continue;
-      if (g.size() > kMaxGlobLen) {
-        *err = "glob longer than " + std::to_string(kMaxGlobLen) + " bytes";
-        return -1;
-      }
-      dst->push_back(g);
-      if (inc->size() + exc->size() > kMaxFilterGlobs) {
-        *err = "more than " + std::to_string(kMaxFilterGlobs) + " globs";
-        return -1;
-      }
-    }
-  }
-  return any ? 1 : 0;
-}
-
-}  // namespace
-
-std::shared_ptr<const Exporter::Filtered> Exporter::filtered(const Snapshot& s, const std::string& query, bool gzip) {
-  {
-    std::lock_guard<std::mutex> g(filter_mu_);
-    if (filter_seq_ != s.seq) {
-      filter_cache_.clear();
-      filter_seq_ = s.seq;
-    }
-    auto it = filter_cache_.find(query);
-    if (it != filter_cache_.end() && (!gzip || !it->second->body_gz.empty())) return it->second;
-  }
-  std::vector<std::string> inc, exc;
-  std::string err;
-  parse_filter_query(query, &inc, &exc, &err);  // handle_http validated it
-  auto f = std::make_shared<Filtered>();
-  filter_exposition(s.body, inc, exc, &f->body);
-  if (gzip) gzip_compress(f->body, &f->body_gz, 1);
-  std::lock_guard<std::mutex> g(filter_mu_);
-  if (filter_seq_ == s.seq && (filter_cache_.size() < kFilterCache || filter_cache_.count(query)))
-    filter_cache_[query] = f;
-  return f;
-}
-
-void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
-  if (req.path == "/metrics") {
-    auto s = store_.get();
-    if (!s) {
-      resp->status = 503;
-      resp->inline_body = "no sample yet\n";
-      return;
-    }
-    resp->content_type = "text/plain; version=0.0.4; charset=utf-8";
-    std::vector<std::string> inc, exc;
-    std::string err;
-    const int fq = req.query.empty() ? 0 : parse_filter_query(req.query, &inc, &exc, &err);
-    if (fq < 0) {
-      resp->status = 400;
-      resp->inline_body = "bad family filter: " + err + "\n";
-      return;
-    }
-    if (fq > 0) {
-      // per-request family filter (e.g. a fast Prometheus job for node_gpu_* only)
-      auto f = filtered(*s, req.query, req.accept_gzip && cfg_.gzip);
-      if (req.accept_gzip && !f->body_gz.empty()) {
-        resp->extra_headers = "Content-Encoding: gzip\r\n";
-        resp->data = f->body_gz.data();
-        resp->len = f->body_gz.size();
-      } else {
-        resp->data = f->body.data();
-        resp->len = f->body.size();
-      }
-      resp->owner = f;
-      return;
-    }
-    const bool fresh_gz = req.accept_gzip && s->gzip && !s->compressed();
-    const std::string* gz = req.accept_gzip ? s->gzipped(true) : nullptr;
-    if (fresh_gz && gz) gz_lazy_.fetch_add(1, std::memory_order_relaxed);
-    if (req.accept_gzip && s->gzip) {
-      // the gzip scrapers' cadence (EWMA of the spacing; bursts under 50 ms ignored) for the tick
-      // thread's prediction above
-      const int64_t now = mono_ns();
-      const int64_t prev = gz_last_scrape_ns_.exchange(now, std::memory_order_relaxed);
-      const int64_t d = prev > 0 ? now - prev : 0;
-      if (d > 50'000'000) {
-        const int64_t p = gz_period_ns_.load(std::memory_order_relaxed);
-        gz_period_ns_.store(p > 0 && d < 8 * p ? (3 * p + d) / 4 : d, std::memory_order_relaxed);
-      }
-    }
-    if (gz) {
-      resp->extra_headers = "Content-Encoding: gzip\r\n";
-      resp->data = gz->data();
-      resp->len = gz->size();
-    } else {
-      resp->data = s->body.data();
-      resp->len = s->body.size();
-    }
-    resp->owner = s;
-    return;
-  }
-  if (req.path == "/healthz" || req.path == "/livez") {
-    bool ok = healthy();
-    resp->status = ok ? 200 : 503;
-    resp->inline_body = ok ? "ok\n" : "sampler stalled\n";
-    return;
-  }
-  if (req.path == "/readyz") {
-    bool ok = ready() && backend_up_;
-    resp->status = ok ? 200 : 503;
-    resp->inline_body = ok ? "ready\n" : ("not ready: " + backend_error() + "\n");
-    return;
-  }
-  if (req.path == "/" || req.path.empty()) {
-    resp->content_type = "text/html; charset=utf-8";
-    resp->inline_body =
-        "<html><head><title>gpumon MI355X exporter</title></head><body><h1>gpumon</h1>"
-        "<p><a href=\"/metrics\">/metrics</a> &middot; <a href=\"/healthz\">/healthz</a> &middot; "
-        "<a href=\"/readyz\">/readyz</a></p></body></html>\n";
-    return;
-  }
-  resp->status = 404;
-  resp->inline_body = "not found\n";
-}
 
 void Exporter::set_extra(const std::string& source, std::vector<ExtraSeries> series) {
   std::lock_guard<std::mutex> g(extra_mu_);

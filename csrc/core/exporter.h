@@ -84,7 +84,7 @@ struct ExporterConfig {
   double mfma_exclusive_window_s = 5.0;
   // A multi-GPU process's context on a GPU it does not work on (no waves there within the window,
   // at most this much VRAM, a workload context on another GPU) is a peer context: no pod_gpu row,
-  // not a sharer (exporter.cpp build_pod_rows). 0 = off.
+  // not a sharer (pod_rows.cpp build_pod_rows). 0 = off.
   double peer_context_max_vram_mib = 512.0;
   AttributionConfig attribution;
   RateConfig rates;
@@ -143,7 +143,7 @@ struct TickInfo {
 
 class Exporter {
  public:
-  struct DevWorker;   // one sampling thread per GPU (exporter.cpp)
+  struct DevWorker;   // one sampling thread per GPU (exporter_internal.h, dev_workers.cpp)
   struct DoneSignal;
 
   explicit Exporter(ExporterConfig cfg);
@@ -348,7 +348,7 @@ class Exporter {
   std::atomic<int> influx_up_{0};                 // the last push attempt succeeded
   std::atomic<int64_t> influx_last_ok_wall_ns_{0};
 
-  // per-device sampling workers + watchdog (exporter.cpp)
+  // per-device sampling workers + watchdog (dev_workers.cpp)
   void start_workers(int n);
   bool stop_workers();
   bool workers_busy() const;

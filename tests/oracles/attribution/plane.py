@@ -37,7 +37,7 @@ def match_device_id(dev_id: str, statics: List[dict]) -> int:
     amdsmi UUIDs, HIP uuids (``GPU-...``), plain hip ids, ``cardN`` / ``renderDN``, and the DRA
     forms: a CDI name (``amd.com/gpu=gpu-0``: the part after ``=``), ``gpu-N`` (hip id N) and
     dashed PCI addresses (``gpu-0000-26-00-0`` / ``0000-26-00-0``). Same rules as the C++
-    ``match_device_id`` (csrc/core/exporter.cpp).
+    ``match_device_id`` (csrc/core/control_plane.cpp).
     """
     d = normalize_id(dev_id)
     if "=" in d:

@@ -6,7 +6,7 @@ pod_gpu row per compute app that nvidia-smi listed on a GPU (/root/reference/gpu
 190-219). A rank shows up there on its own GPU. Its "GPUs held per user" panel is `pod_gpu.count`
 grouped by user_name_t. For this pod it must read 8, not 64.
 
-The rule (csrc/core/exporter.cpp build_pod_rows) calls a (pid, GPU) context a peer context when,
+The rule (csrc/core/pod_rows.cpp build_pod_rows) calls a (pid, GPU) context a peer context when,
 on that GPU, it:
 * holds at most `peer_context_max_vram_mib`;
 * had no resident wave within the sharing window, where occupancy is readable;
