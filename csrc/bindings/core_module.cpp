@@ -6,6 +6,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
+#include <atomic>
+#include <set>
+#include <thread>
+
 #include "../core/attribution.h"
 #include "../core/backend.h"
 #include "../core/common.h"
@@ -684,6 +689,44 @@ PYBIND11_MODULE(_core, m) {
     if (!gzip_compress(s, &o)) throw std::runtime_error("gzip failed");
     return py::bytes(o);
   });
+  m.def(
+      "snapshot_gzip_race",
+      [](const std::string& body, int threads, bool during_precompress) {
+        // `threads` scrapes ask one fresh snapshot for gzip at the same instant -- or, with
+        // during_precompress, while the tick thread's precompress() of it is running. Exactly one
+        // thread compresses; the others wait for it. Returns (the gzip body every thread got, or
+        // None if any got none; distinct buffers handed out, 1 = compressed once; scrapes that
+        // started while the compression was in flight).
+        auto snap = std::make_shared<gpumon::Snapshot>();
+        snap->body = body;
+        snap->gzip = true;
+        std::vector<const std::string*> got(std::max(threads, 1), nullptr);
+        std::atomic<int> mid{0};
+        {
+          py::gil_scoped_release nogil;
+          std::thread pre;
+          if (during_precompress) {
+            pre = std::thread([&] { snap->precompress(); });
+            while (!snap->compressing() && !snap->compressed()) std::this_thread::yield();
+          }
+          std::atomic<int> ready{0};
+          std::vector<std::thread> th;
+          for (size_t i = 0; i < got.size(); ++i)
+            th.emplace_back([&, i] {
+              ready.fetch_add(1);
+              while (ready.load() < static_cast<int>(got.size())) std::this_thread::yield();
+              if (snap->compressing()) mid.fetch_add(1);
+              got[i] = snap->gzipped(true);
+            });
+          for (auto& t : th) t.join();
+          if (pre.joinable()) pre.join();
+        }
+        std::set<const std::string*> distinct(got.begin(), got.end());
+        const bool all = std::find(got.begin(), got.end(), nullptr) == got.end();
+        return py::make_tuple(all ? py::object(py::bytes(*got[0])) : py::object(py::none()),
+                              static_cast<int>(distinct.size()), mid.load());
+      },
+      py::arg("body"), py::arg("threads") = 8, py::arg("during_precompress") = false);
   m.def(
       "scrape_load",
       [](const std::string& host, int port, const std::string& path, int n, double duration_s,

@@ -45,6 +45,9 @@ constexpr size_t kMaxConnsPerLoop = 4096;
 // pollers, the on-device helper) when the connection cap is derived from RLIMIT_NOFILE: a flood
 // of scrape connections must not make the sampler's own opens fail with EMFILE.
 constexpr rlim_t kFdReserve = 256;
+// Connections a loop may admit over the cap while another loop closes one of its own (evict_debt_):
+// a few fds out of kFdReserve.
+constexpr size_t kDebtSlack = 16;
 constexpr int kSndBuf = 1 << 20;  // GPUMON_HTTP_SNDBUF overrides (bytes; 0 = the kernel's autotuning)
 
 const char* status_text(int s) {
@@ -564,10 +567,44 @@ void HttpServer::run(Loop* L) {
   // epoll would report it again at once and the loop would spin. Stop watching it for a moment.
   int64_t accept_resume_ns = 0, last_emfile_log_ns = INT64_MIN / 2;
   std::vector<int> closed_in_batch;
+  // At the cap, the connection to close, least recently active first within each class
+  // (ADVICE r4); -1 = none (every connection is mid-response):
+  //   0 never answered a request, nothing pending (a connect flood's idle sockets)
+  //   1 never answered, a request partly read (a trickler)
+  //   2 answered before, idle now (Prometheus' keep-alive between scrapes: kept longest)
+  //   3 answered before, a request partly read
+  auto pick_victim = [&]() {
+    int victim = -1, best = 4;
+    for (int vfd : L->lru) {  // oldest first; a connection mid-response is skipped
+      auto vit = L->conns.find(vfd);
+      if (vit == L->conns.end() || vit->second.writing) continue;
+      const Conn& vc = vit->second;
+      const int cls = (vc.served > 0 ? 2 : 0) + (vc.in.empty() ? 0 : 1);
+      if (cls < best) {
+        best = cls;
+        victim = vfd;
+        if (cls == 0) break;
+      }
+    }
+    return victim;
+  };
+  auto evict = [&](int victim) {
+    close_conn(victim);
+    evicted_.fetch_add(1, std::memory_order_relaxed);
+    closed_in_batch.push_back(victim);  // its number may come back from accept() below
+  };
   while (running_.load(std::memory_order_relaxed)) {
     int n = epoll_wait(L->ep, evs, 256, accept_resume_ns ? 100 : rt_on ? 100 : 1000);
     int64_t now = mono_ns();
     closed_in_batch.clear();
+    // evictions another loop asked for (it admitted a newcomer at the cap with nothing to close)
+    for (int debt = evict_debt_.load(std::memory_order_relaxed); debt > 0;) {
+      const int victim = pick_victim();
+      if (victim < 0) break;  // nothing here either: the debt stays for a loop that has some
+      if (!evict_debt_.compare_exchange_weak(debt, debt - 1, std::memory_order_relaxed)) continue;
+      evict(victim);
+      debt = evict_debt_.load(std::memory_order_relaxed);
+    }
     if (accept_resume_ns && now >= accept_resume_ns) {
       accept_resume_ns = 0;
       watch_listener(L, true);
@@ -597,7 +634,12 @@ void HttpServer::run(Loop* L) {
         rt_demotions_.fetch_add(1, std::memory_order_relaxed);
       }
       int fd = evs[i].data.fd;
-      if (fd == L->wake) continue;
+      if (fd == L->wake) {  // stop() or an eviction request (handled above): drain the counter
+        uint64_t v;
+        ssize_t r = read(L->wake, &v, sizeof v);
+        (void)r;
+        continue;
+      }
       if (fd == L->lfd) {
         while (true) {
           int cfd = accept4(L->lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
@@ -614,32 +656,28 @@ void HttpServer::run(Loop* L) {
           }
           // the cap is the server's (loops x per-loop share): with one EPOLLEXCLUSIVE socket the first
           // idle loop takes most connections, so a per-loop count would cap it at 1/N of the fds
-          if (conns_.load(std::memory_order_relaxed) >= max_conns_ * static_cast<size_t>(nthreads_)) {
-            // full: make room by closing a connection that is not sending a response, else refuse
-            // this one. Preference, least recently active first within each class:
-            //   0 never answered a request, nothing pending (a connect flood's idle sockets)
-            //   1 never answered, a request partly read (a trickler)
-            //   2 answered before, idle now (Prometheus' keep-alive between scrapes: kept longest)
-            //   3 answered before, a request partly read
-            int victim = -1, best = 4;
-            for (int vfd : L->lru) {  // oldest first; a connection mid-response is skipped
-              auto vit = L->conns.find(vfd);
-              if (vit == L->conns.end() || vit->second.writing) continue;
-              const Conn& vc = vit->second;
-              const int cls = (vc.served > 0 ? 2 : 0) + (vc.in.empty() ? 0 : 1);
-              if (cls < best) {
-                best = cls;
-                victim = vfd;
-                if (cls == 0) break;
-              }
-            }
-            if (victim < 0) {
+          const size_t cap = max_conns_ * static_cast<size_t>(nthreads_);
+          if (conns_.load(std::memory_order_relaxed) >= cap) {
+            // full: make room by closing a connection of this loop that is not sending a response
+            const int victim = pick_victim();
+            if (victim >= 0) {
+              evict(victim);
+            } else if (nthreads_ > 1 && conns_.load(std::memory_order_relaxed) < cap + kDebtSlack) {
+              // nothing to close here (the other loops took the flood: with one EPOLLEXCLUSIVE
+              // socket the loops' shares are uneven): admit this one and have another loop close
+              // one of its connections, rather than refuse the newcomer -- a scraper arriving
+              // during a flood would be the one refused
+              evict_debt_.fetch_add(1, std::memory_order_relaxed);
+              for (auto& O : loops_)
+                if (O.get() != L) {
+                  uint64_t one = 1;
+                  ssize_t w = write(O->wake, &one, sizeof one);
+                  (void)w;
+                }
+            } else {
               close(cfd);
               continue;
             }
-            close_conn(victim);
-            evicted_.fetch_add(1, std::memory_order_relaxed);
-            closed_in_batch.push_back(victim);  // its number may come back from accept() below
           }
           int one = 1;
           setsockopt(cfd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);

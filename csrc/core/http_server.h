@@ -94,7 +94,10 @@ class HttpServer {
   double rt_budget_ = 0.2;
   std::atomic<int> rt_loops_{0};
   std::atomic<uint64_t> rt_demotions_{0};
-  std::atomic<uint64_t> evicted_{0};  // connections closed to make room at the per-loop cap
+  std::atomic<uint64_t> evicted_{0};  // connections closed to make room at the cap
+  // Evictions owed by the loops: a loop at the cap with nothing of its own to evict (the other
+  // loop holds the flood) admits the newcomer and asks the others to close one of theirs.
+  std::atomic<int> evict_debt_{0};
 };
 
 }  // namespace gpumon

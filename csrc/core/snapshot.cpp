@@ -105,7 +105,10 @@ const std::string* Snapshot::gzipped(bool compress_now) const {
   if (!gzip) return nullptr;
   gz_asked_.store(true, std::memory_order_relaxed);
   int st = gz_state_.load(std::memory_order_acquire);
-  if (st == 2) return &gz_;
+  if (st == 0 && compress_now) {
+    if (claim(&st)) return compress_claimed();
+    // lost the claim to a concurrent compression: st is its state now (1, 2 or 3)
+  }
   if (st == 1) {
     // another thread (the tick thread's eager / predicted compression, or a concurrent scrape) is
     // compressing this snapshot right now: wait for it (0.1-0.8 ms) rather than answer with the
@@ -113,19 +116,21 @@ const std::string* Snapshot::gzipped(bool compress_now) const {
     const int64_t until = mono_ns() + 20'000'000;
     while ((st = gz_state_.load(std::memory_order_acquire)) == 1 && mono_ns() < until)
       std::this_thread::sleep_for(std::chrono::microseconds(20));
-    return st == 2 ? &gz_ : nullptr;
   }
-  return compress_now ? compress() : nullptr;
+  return st == 2 ? &gz_ : nullptr;
 }
 
-const std::string* Snapshot::compress() const {
-  if (!gzip) return nullptr;
+void Snapshot::precompress() const {
+  if (!gzip) return;
   int st = gz_state_.load(std::memory_order_acquire);
-  if (st == 2) return &gz_;
-  if (st != 0) return nullptr;
-  if (!gz_state_.compare_exchange_strong(st, 1, std::memory_order_acq_rel)) {
-    return st == 2 ? &gz_ : nullptr;
-  }
+  if (st == 0 && claim(&st)) (void)compress_claimed();
+}
+
+bool Snapshot::claim(int* st) const {
+  return gz_state_.compare_exchange_strong(*st, 1, std::memory_order_acq_rel);
+}
+
+const std::string* Snapshot::compress_claimed() const {
   const bool ok = gzip_compress(body, &gz_, 1);
   gz_state_.store(ok ? 2 : 3, std::memory_order_release);
   return ok ? &gz_ : nullptr;

@@ -28,15 +28,20 @@ struct Snapshot {
   // nullptr = serve the identity body (compression disabled, failed, or another thread is
   // compressing right now -- HTTP lets a server ignore Accept-Encoding).
   const std::string* gzipped(bool compress_now) const;
-  // The tick thread's eager compression (does not count as a gzip request).
-  void precompress() const { (void)compress(); }
+  // The tick thread's eager compression (does not count as a gzip request; returns at once when
+  // a scrape is already compressing).
+  void precompress() const;
   // A scrape asked this snapshot for gzip (the tick thread's eager / lazy decision).
   bool gzip_asked() const { return gz_asked_.load(std::memory_order_relaxed); }
   // Whether this snapshot was compressed (by either path).
   bool compressed() const { return gz_state_.load(std::memory_order_acquire) == 2; }
+  // A thread is compressing it right now (tests).
+  bool compressing() const { return gz_state_.load(std::memory_order_acquire) == 1; }
 
  private:
-  const std::string* compress() const;
+  // 0 -> 1: this thread compresses. false = another thread got there first (*st = its state).
+  bool claim(int* st) const;
+  const std::string* compress_claimed() const;  // after a successful claim
   mutable std::atomic<int> gz_state_{0};  // 0 none, 1 compressing, 2 done, 3 failed
   mutable std::atomic<bool> gz_asked_{false};
   mutable std::string gz_;

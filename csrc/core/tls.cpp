@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <mutex>
 
 #include "common.h"
@@ -86,17 +87,22 @@ void load_api() {
   const char* ssl_env = getenv("GPUMON_LIBSSL");
   const char* crypto_env = getenv("GPUMON_LIBCRYPTO");
   auto* a = new SslApi;
-  // libcrypto first, RTLD_GLOBAL: libssl resolves its own libcrypto dependency to the same object
-  for (const char* n : {crypto_env && *crypto_env ? crypto_env : "libcrypto.so.3", "libcrypto.so"}) {
-    a->crypto_dl = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
-    if (a->crypto_dl) break;
-  }
-  for (const char* n : {ssl_env && *ssl_env ? ssl_env : "libssl.so.3", "libssl.so"}) {
-    a->ssl_dl = dlopen(n, RTLD_NOW | RTLD_LOCAL);
-    if (a->ssl_dl) break;
+  // An override is the only name tried: a wrong path must fail, not quietly load the default.
+  // libcrypto first, RTLD_GLOBAL: libssl resolves its own libcrypto dependency to the same object.
+  auto open_first = [](const char* env, std::initializer_list<const char*> names, int flags) -> void* {
+    if (env && *env) return dlopen(env, flags);
+    for (const char* n : names)
+      if (void* h = dlopen(n, flags)) return h;
+    return nullptr;
+  };
+  a->crypto_dl = open_first(crypto_env, {"libcrypto.so.3", "libcrypto.so"}, RTLD_NOW | RTLD_GLOBAL);
+  const char* why = a->crypto_dl ? nullptr : dlerror();
+  if (a->crypto_dl) {
+    a->ssl_dl = open_first(ssl_env, {"libssl.so.3", "libssl.so"}, RTLD_NOW | RTLD_LOCAL);
+    if (!a->ssl_dl) why = dlerror();
   }
   if (!a->ssl_dl || !a->crypto_dl) {
-    g_err = std::string("https needs OpenSSL 3 (libssl.so.3 / libcrypto.so.3): ") + (dlerror() ?: "not found");
+    g_err = std::string("https needs OpenSSL 3 (libssl.so.3 / libcrypto.so.3): ") + (why ? why : "not found");
     if (a->ssl_dl) dlclose(a->ssl_dl);
     if (a->crypto_dl) dlclose(a->crypto_dl);
     delete a;

@@ -26,6 +26,25 @@ def _get(port, path, headers=None, method="GET"):
     return r.status, dict(r.getheaders()), body
 
 
+def _read_request(c):
+    """One whole request from a scripted server's socket: the headers, then Content-Length bytes
+    of body (a client may send the two in separate segments; closing with the body unread would
+    reset the connection under the client's response read)."""
+    buf = b""
+    while b"\r\n\r\n" not in buf:
+        chunk = c.recv(65536)
+        if not chunk:
+            return
+        buf += chunk
+    head, _, rest = buf.partition(b"\r\n\r\n")
+    n = next((int(l.split(b":", 1)[1]) for l in head.split(b"\r\n") if l.lower().startswith(b"content-length:")), 0)
+    while len(rest) < n:
+        chunk = c.recv(65536)
+        if not chunk:
+            return
+        rest += chunk
+
+
 def test_metrics_endpoint(mock_exporter):
     ex = mock_exporter()
     st, h, body = _get(ex.port, "/metrics")
@@ -48,6 +67,21 @@ def test_gzip_disabled(mock_exporter):
     ex = mock_exporter(gzip=False)
     st, h, body = _get(ex.port, "/metrics", {"Accept-Encoding": "gzip"})
     assert st == 200 and "Content-Encoding" not in h
+
+
+@pytest.mark.parametrize("during_precompress", [False, True])
+def test_concurrent_gzip_scrapes_compress_a_snapshot_once(core, during_precompress):
+    """Scrapes that ask a fresh snapshot for gzip at the same instant, or while the tick thread is
+    precompressing it: one thread compresses, the others wait for it and get the same buffer. None
+    falls back to the identity body (a scrape that lost the claim to a concurrent compression used
+    to) and none compresses again. The body, 1.3 MB, takes ~6 ms to compress: longer than the
+    threads' start, well inside the waiters' 20 ms limit."""
+    body = "".join(f'node_gpu_gpu_util{{gpu_id="{i % 8}",host="n{i}"}} {i * 0.37:.3f}\n' for i in range(24000))
+    gz, distinct, mid = core.snapshot_gzip_race(body, threads=8, during_precompress=during_precompress)
+    assert gz is not None and distinct == 1
+    assert gzip.decompress(gz).decode() == body
+    if during_precompress:
+        assert mid >= 1  # the scrapes did arrive while it ran
 
 
 def test_head_and_404_and_index(mock_exporter):
@@ -247,7 +281,7 @@ def test_client_bounds_a_dripping_or_endless_response(core, script, error):
     def serve():
         c, _ = srv.accept()
         try:
-            c.recv(65536)
+            _read_request(c)
             for part in script:
                 if stop.is_set():
                     break
@@ -291,7 +325,7 @@ def test_client_decodes_chunked_bodies_and_keeps_the_connection(core):
         c, _ = srv.accept()
         conns.append(c)
         for a in good:  # three answers on ONE connection, a byte-split one in the middle
-            c.recv(65536)
+            _read_request(c)
             if a is good[1]:
                 for i in range(len(a)):
                     c.sendall(a[i:i + 1])
@@ -299,7 +333,7 @@ def test_client_decodes_chunked_bodies_and_keeps_the_connection(core):
                 c.sendall(a)
         c2, _ = srv.accept()  # then a connection with a broken chunk (size says 5, 3 bytes + CRLF)
         conns.append(c2)
-        c2.recv(65536)
+        _read_request(c2)
         c2.sendall(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n5\r\nabc\r\n0\r\n\r\n")
         time.sleep(0.5)
         c2.close()
@@ -327,7 +361,7 @@ def test_client_returns_a_chunked_error_body(core):
 
     def serve():
         c, _ = srv.accept()
-        c.recv(65536)
+        _read_request(c)
         c.sendall(b"HTTP/1.1 400 Bad Request\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n"
                   b"6\r\nfield \r\n7\r\ninvalid\r\n0\r\n\r\n")
         c.close()

@@ -277,8 +277,50 @@ def test_push_config_checks_tls_files_and_token(core, pki, tmp_path):
     assert "cannot load CA file" in core.check_push_config("https://influx/write", ca_file=str(junk))
     assert "cannot load client key" in core.check_push_config(
         "https://influx/write", client_cert=pki["client"], client_key=pki["server_key"])
+    assert "cannot load client certificate" in core.check_push_config(
+        "https://influx/write", client_cert=str(junk), client_key=pki["client_key"])
     assert "line break" in core.check_push_config("http://influx/write", token="a\r\nX-Evil: 1")
     assert core.check_push_config("") == ""
+    # TLS files for an http:// URL: a warning, not an error (the files are not even opened)
+    assert core.check_push_config("http://influx/write", ca_file=str(tmp_path / "none.pem")) == ""
+
+
+def test_empty_default_trust_store_falls_back_to_the_bundles(core, monkeypatch):
+    """SSL_CERT_FILE / SSL_CERT_DIR pointing nowhere (a slim image whose OPENSSLDIR holds no certs)
+    leaves libssl's default store empty: the context then loads the distribution bundle itself."""
+    if not any(os.access(b, os.R_OK) for b in ("/etc/ssl/certs/ca-certificates.crt", "/etc/pki/tls/certs/ca-bundle.crt",
+                                              "/etc/ssl/ca-bundle.pem", "/etc/ssl/cert.pem")):
+        pytest.skip("no CA bundle on this host")
+    monkeypatch.setenv("SSL_CERT_FILE", "/nonexistent/cert.pem")
+    monkeypatch.setenv("SSL_CERT_DIR", "/nonexistent/certs")
+    assert core.check_push_config("https://influx:8086/write") == ""
+
+
+@pytest.mark.parametrize("env,want", [
+    ({"GPUMON_LIBSSL": "/nonexistent/libssl.so.3"}, "https needs OpenSSL 3"),
+    ({"GPUMON_LIBCRYPTO": "/nonexistent/libcrypto.so.3"}, "https needs OpenSSL 3"),
+    ({"GPUMON_LIBSSL": "libz.so.1"}, "libssl / libcrypto lack OPENSSL_init_ssl"),
+])
+def test_unloadable_openssl_is_named_at_startup(env, want):
+    """An https URL on a host without a usable OpenSSL 3 stops the exporter at startup with the
+    reason. An override names the only library tried: a wrong path does not quietly load the
+    default one."""
+    r = subprocess.run([EXPORTER, "--backend", "mock:gpus=1", "--listen", "127.0.0.1:0", "--once"],
+                       capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, INFLUXDB_URL="https://influx:8086/write", **env))
+    assert r.returncode == 2, (r.returncode, r.stderr[-2000:])
+    assert want in r.stderr, r.stderr[-2000:]
+
+
+def test_http_push_never_loads_openssl():
+    """An http:// deployment runs with no OpenSSL at all: the overrides point nowhere and the
+    exporter still starts (libssl is opened only for https)."""
+    r = subprocess.run([EXPORTER, "--backend", "mock:gpus=1", "--listen", "127.0.0.1:0", "--once"],
+                       capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, INFLUXDB_URL="http://127.0.0.1:9/write", GPUMON_LIBSSL="/nonexistent/libssl.so.3",
+                                GPUMON_LIBCRYPTO="/nonexistent/libcrypto.so.3"))
+    assert r.returncode == 0, (r.returncode, r.stderr[-2000:])
+    assert "node_gpu_gpu_util" in r.stdout
 
 
 def test_exporter_start_refuses_an_unusable_push(core):

@@ -145,6 +145,23 @@ def test_ipv4_wildcard_stays_ipv4_only(mock_exporter):
     assert _refused("::1", ex.port)
 
 
+def test_host_name_listener_binds_its_first_address(mock_exporter):
+    """A host name (a node's own name in `listen`) is resolved once at startup and the listener binds
+    its first address; the log names that address, not the name."""
+    ex = mock_exporter(listen_addr="localhost", port=0)
+    desc = ex.listen_desc
+    assert desc in (f"127.0.0.1:{ex.port}", f"[::1]:{ex.port}"), desc
+    host = "::1" if desc.startswith("[") else "127.0.0.1"
+    assert _scrape(host, ex.port)[0] == 200
+
+
+def test_unresolvable_listen_host_is_named(core):
+    ex = core.Exporter({"backend": "mock:gpus=1", "interval_s": 0, "listen_addr": "no-such-host.invalid", "port": 0})
+    with pytest.raises(RuntimeError, match="no-such-host.invalid"):
+        ex.start()
+    ex.stop()
+
+
 def _spawn(entry, listen, env_extra=None):
     if entry == "native":
         cmd = [EXPORTER, "--no-pod-resources", "--no-cri"]
