@@ -188,6 +188,12 @@ def test_native_scrape_load_latency(mock_exporter, core):
     assert r["errors"] == 0 and len(lat) == 400
     p99 = lat[int(0.99 * (len(lat) - 1))]
     assert p99 < 0.05, p99  # pre-rendered snapshot: sub-millisecond typical, generous CI bound
+    # the server counts a scrape after its last write returns: the client may read the final
+    # response a moment before that
+    import time
+    deadline = time.monotonic() + 5
+    while ex.self_stats()["scrapes"] < 400 and time.monotonic() < deadline:
+        time.sleep(0.005)
     assert ex.self_stats()["scrapes"] >= 400
     ex.tick()
     fam = promtext.parse(ex.metrics_text())
