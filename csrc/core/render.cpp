@@ -847,7 +847,7 @@ void render_prometheus(const RenderInput& in, std::string* o) {
     }
     if (s.http_evicted >= 0) {
       Family f(o, "gpumon_http_connections_evicted_total",
-               "Idle connections closed to make room for a new one at the per-loop connection cap (derived "
+               "Idle connections closed to make room for a new one at the server's connection cap (derived "
                "from RLIMIT_NOFILE): a connection flood.",
                "counter");
       f.add(hl, static_cast<double>(s.http_evicted));
