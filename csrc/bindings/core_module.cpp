@@ -706,7 +706,7 @@ PYBIND11_MODULE(_core, m) {
           py::gil_scoped_release nogil;
           std::thread pre;
           if (during_precompress) {
-            pre = std::thread([&] { snap->precompress(); });
+            pre = std::thread([&] { (void)snap->precompress(); });
             while (!snap->compressing() && !snap->compressed()) std::this_thread::yield();
           }
           std::atomic<int> ready{0};

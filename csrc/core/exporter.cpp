@@ -728,7 +728,7 @@ TickInfo Exporter::tick() {
   snap->seq = s;
   // Publish the snapshot first (the tick's data is exported from here on); its gzip, when made by
   // this thread, follows the publish, off the sample-to-export path (0.1-0.4 ms for 1-8 GPUs at
-  // level 1). A gzip scrape in between gets the identity body, which HTTP allows.
+  // level 1). A gzip scrape in between compresses it itself, or waits for this thread's compression.
   std::shared_ptr<const Snapshot> published_snap = snap;
   std::shared_ptr<const Snapshot> prev_snap = store_.get();
   store_.publish(published_snap);
@@ -759,9 +759,8 @@ TickInfo Exporter::tick() {
     if (frequent || predicted) {
       const int64_t tz = mono_ns();
       TraceRange trz("gpumon.gzip");
-      snap->precompress();
+      if (snap->precompress()) (frequent ? gz_eager_ : gz_predicted_)++;  // false: a scrape got there first
       info.t_gzip = (mono_ns() - tz) * 1e-9;
-      (frequent ? gz_eager_ : gz_predicted_)++;
     }
     if (prev_snap && prev_snap->compressed() && !prev_snap->gzip_asked()) gz_unused_++;
   }

@@ -120,10 +120,10 @@ const std::string* Snapshot::gzipped(bool compress_now) const {
   return st == 2 ? &gz_ : nullptr;
 }
 
-void Snapshot::precompress() const {
-  if (!gzip) return;
+bool Snapshot::precompress() const {
+  if (!gzip) return false;
   int st = gz_state_.load(std::memory_order_acquire);
-  if (st == 0 && claim(&st)) (void)compress_claimed();
+  return st == 0 && claim(&st) && compress_claimed() != nullptr;
 }
 
 bool Snapshot::claim(int* st) const {

@@ -28,9 +28,9 @@ struct Snapshot {
   // nullptr = serve the identity body (compression disabled, failed, or another thread is
   // compressing right now -- HTTP lets a server ignore Accept-Encoding).
   const std::string* gzipped(bool compress_now) const;
-  // The tick thread's eager compression (does not count as a gzip request; returns at once when
-  // a scrape is already compressing).
-  void precompress() const;
+  // The tick thread's eager compression (does not count as a gzip request). false = not made
+  // here: a scrape is compressing or has compressed it (or compression is off or failed).
+  bool precompress() const;
   // A scrape asked this snapshot for gzip (the tick thread's eager / lazy decision).
   bool gzip_asked() const { return gz_asked_.load(std::memory_order_relaxed); }
   // Whether this snapshot was compressed (by either path).
