@@ -597,8 +597,14 @@ void HttpServer::run(Loop* L) {
     int n = epoll_wait(L->ep, evs, 256, accept_resume_ns ? 100 : rt_on ? 100 : 1000);
     int64_t now = mono_ns();
     closed_in_batch.clear();
-    // evictions another loop asked for (it admitted a newcomer at the cap with nothing to close)
+    // evictions another loop asked for (it admitted a newcomer at the cap with nothing to close);
+    // owed only while the server is still over the cap (connections that closed by themselves
+    // since have paid it)
     for (int debt = evict_debt_.load(std::memory_order_relaxed); debt > 0;) {
+      if (conns_.load(std::memory_order_relaxed) <= max_conns_ * static_cast<size_t>(nthreads_)) {
+        evict_debt_.compare_exchange_strong(debt, 0, std::memory_order_relaxed);
+        break;
+      }
       const int victim = pick_victim();
       if (victim < 0) break;  // nothing here either: the debt stays for a loop that has some
       if (!evict_debt_.compare_exchange_weak(debt, debt - 1, std::memory_order_relaxed)) continue;
