@@ -242,8 +242,12 @@ int HttpClient::request(const std::string& method, const Url& u, const std::stri
     if (!body.empty() || method == "POST")
       req += "Content-Length: " + std::to_string(body.size()) + "\r\n";
     req += "\r\n";
+    // a tick's push (a few KB of lines) leaves in one write: one TCP segment, or one TLS record,
+    // instead of a header segment and a body segment
+    const bool one_write = body.size() <= (64u << 10);
+    if (one_write) req += body;
     std::string serr;
-    if (!send_all(req.data(), req.size(), &serr) || !send_all(body.data(), body.size(), &serr)) {
+    if (!send_all(req.data(), req.size(), &serr) || (!one_write && !send_all(body.data(), body.size(), &serr))) {
       close_conn();
       if (reused) continue;  // stale keep-alive connection: retry once on a fresh one
       *err = serr;
