@@ -749,7 +749,10 @@ TickInfo Exporter::tick() {
     const int64_t last = gz_last_scrape_ns_.load(std::memory_order_relaxed);
     if (!frequent && cfg_.interval_s > 0 && per > 0 && last > 0) {
       const int64_t now = mono_ns(), life = static_cast<int64_t>(cfg_.interval_s * 1e9);
-      const int64_t slack = life / 10;
+      // the margin around the predicted time: a tenth of a tick, widened to twice the scraper's
+      // measured jitter (a loaded host, a jittery network), at most half a tick
+      const int64_t slack =
+          std::min(life / 2, std::max(life / 10, 2 * gz_jitter_ns_.load(std::memory_order_relaxed)));
       int64_t next = last + per;
       // a scrape or two may have been missed (a restart, a slow network): keep the phase, but a
       // scraper silent for more than 3 periods is gone and nothing is predicted for it

@@ -305,6 +305,7 @@ class Exporter {
   // snapshot compressions: eager (tick thread), lazy (by a scrape), and eager ones nobody fetched
   std::atomic<uint64_t> gz_eager_{0}, gz_lazy_{0}, gz_unused_{0}, gz_predicted_{0};
   std::atomic<int64_t> gz_last_scrape_ns_{0}, gz_period_ns_{0};  // gzip scrapers' last time and cadence
+  std::atomic<int64_t> gz_jitter_ns_{0};  // EWMA of |spacing - cadence|: the prediction's margin
   size_t last_body_bytes_ = 0;  // tick thread only: sizes the next render buffer
   std::atomic<uint64_t> phase_ns_[5] = {};  // sample, procs, attrib, render, gzip (cumulative)
 

@@ -3,6 +3,7 @@
 #include "exporter_internal.h"
 
 #include <cctype>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -129,7 +130,10 @@ void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
       const int64_t d = prev > 0 ? now - prev : 0;
       if (d > 50'000'000) {
         const int64_t p = gz_period_ns_.load(std::memory_order_relaxed);
-        gz_period_ns_.store(p > 0 && d < 8 * p ? (3 * p + d) / 4 : d, std::memory_order_relaxed);
+        const bool same_scraper = p > 0 && d < 8 * p;
+        gz_period_ns_.store(same_scraper ? (3 * p + d) / 4 : d, std::memory_order_relaxed);
+        const int64_t dev = same_scraper ? std::abs(d - p) : 0, j = gz_jitter_ns_.load(std::memory_order_relaxed);
+        gz_jitter_ns_.store(same_scraper ? (3 * j + dev) / 4 : 0, std::memory_order_relaxed);
       }
     }
     if (gz) {

@@ -68,8 +68,8 @@ struct SelfStats {
   uint64_t hidden_peer_contexts = 0;  // peer contexts of multi-GPU processes left out of pod_gpu rows
   int rt_threads = 0;               // sampler / device-worker threads running SCHED_FIFO (rt_priority)
   int http_rt_loops = -1;            // HTTP loops at SCHED_FIFO now (-1: http_rt_priority off)
-  int64_t http_evicted = -1;
-  int64_t http_max_conns = -1;       // connection cap over all HTTP loops (from RLIMIT_NOFILE)         // connections closed to make room at the per-loop cap (-1: no server)
+  int64_t http_evicted = -1;         // connections closed to make room at the cap (-1: no server)
+  int64_t http_max_conns = -1;       // connection cap over all HTTP loops (from RLIMIT_NOFILE)
   int64_t http_rt_demotions = -1;    // ... times a loop spent its CPU budget and was demoted
   uint64_t overruns = 0;
   double last_tick_wall_s = 0;

@@ -7,6 +7,7 @@
 // (NODE_NAME, INFLUXDB_URL, GPUMON_<KEY>) < flags. Attribution uses /proc plus the native kubelet
 // PodResources and CRI pollers; --pmc / --probe load the on-device plugins.
 #include <signal.h>
+#include <sys/resource.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -45,7 +46,10 @@ static void usage() {
           "                       [--pod-logs /var/log] [--device-checkpoint FILE]\n"
           "                       [--dra-drivers gpu.amd.com,..|none]\n"
           "                       [--pmc] [--pmc-counters A,B,..] [--pmc-mode continuous|window] [--pmc-window SEC] [--probe] [--probe-every N]\n"
-          "                       [--probe-blocks N] [--plugin-dir DIR]\n"
+          "                       [--probe-blocks N] [--plugin-dir DIR] [--device-timeout SEC]\n"
+          "                       [--control-plane native|off] [--compat]\n"
+          "the Python entry point's spellings work too: --procfs-root, --sysfs-root, --cri-socket,\n"
+          "--pod-resources-socket, --docker-socket, --pod-log-root, --enable-pmc, --enable-probe-kernel\n"
           "config keys: the gpumon.* keys of gpumon/config.py (docs/configuration.md), in the file, as\n"
           "GPUMON_<KEY> in the environment, or as the flags above; NODE_NAME and INFLUXDB_URL as in the reference\n");
 }
@@ -72,7 +76,7 @@ int main(int argc, char** argv) {
     return 2;
   }
   // 3. flags
-  bool once = false, print_config = false;
+  bool once = false, print_config = false, compat = false;
   auto set = [&](const char* key, const std::string& v) {
     std::string e;
     if (options_set(&o, key, {v}, &e) < 0) {
@@ -80,6 +84,14 @@ int main(int argc, char** argv) {
       exit(2);
     }
   };
+  // --compat (the reference's behaviour: opt-in label mlgpu=mlgpu, 10 s interval) sits between the
+  // environment and the flags, as in gpumon/config.py from_args: explicit flags still win
+  for (int i = 1; i < argc; ++i)
+    if (std::string(argv[i]) == "--compat") compat = true;
+  if (compat) {
+    if (o.cfg.attribution.opt_in.empty()) set("opt_in_label", "mlgpu=mlgpu");
+    set("interval", "10");
+  }
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -106,27 +118,40 @@ int main(int argc, char** argv) {
     else if (a == "--influx-client-cert") set("influx_client_cert", next());
     else if (a == "--influx-client-key") set("influx_client_key", next());
     else if (a == "--no-fast-path") set("fast_path", "false");
-    else if (a == "--sysfs") set("sysfs_root", next());
+    else if (a == "--sysfs" || a == "--sysfs-root") set("sysfs_root", next());
     else if (a == "--roctx") set("roctx", "true");
-    else if (a == "--pod-resources") set("pod_resources_socket", next());
+    else if (a == "--pod-resources" || a == "--pod-resources-socket") set("pod_resources_socket", next());
     else if (a == "--no-pod-resources") set("pod_resources_socket", "");
-    else if (a == "--cri") set("cri_socket", next());
+    else if (a == "--cri" || a == "--cri-socket") set("cri_socket", next());
     else if (a == "--no-cri") set("cri_socket", "none");
-    else if (a == "--docker") set("docker_socket", next());
-    else if (a == "--pod-logs") set("pod_log_root", next());
+    else if (a == "--docker" || a == "--docker-socket") set("docker_socket", next());
+    else if (a == "--pod-logs" || a == "--pod-log-root") set("pod_log_root", next());
     else if (a == "--device-checkpoint") set("device_checkpoint", next());
     else if (a == "--dra-drivers") {
       const std::string v = next();
       set("dra_drivers", v == "none" ? "" : v);
+    } else if (a == "--control-plane") {
+      // off: no kubelet / CRI / Docker / log-tree metadata pollers (the Python entry point's flag)
+      const std::string v = next();
+      if (v == "off") {
+        for (const char* k : {"pod_resources_socket", "docker_socket", "pod_log_root", "device_checkpoint"}) set(k, "");
+        set("cri_socket", "none");
+      } else if (v != "native") {
+        fprintf(stderr, "--control-plane: native or off, not '%s'\n", v.c_str());
+        return 2;
+      }
+    } else if (a == "--compat") {
+      // applied before the flags (above)
     } else if (a == "--opt-in-label") set("opt_in_label", next());
     else if (a == "--user-regex") set("user_regex", next());
     else if (a == "--user-label") set("user_label", next());
     else if (a == "--pod-labels") set("pod_label_allowlist", next());
-    else if (a == "--procfs") set("procfs_root", next());
+    else if (a == "--procfs" || a == "--procfs-root") set("procfs_root", next());
     else if (a == "--no-processes") set("processes", "false");
     else if (a == "--ras-every") set("ras_every", next());
     else if (a == "--ras-slices") set("ras_slices", next());
     else if (a == "--no-gzip") set("gzip", "false");
+    else if (a == "--device-timeout") set("device_timeout_s", next());
     else if (a == "--metrics-include") set("metrics_include", next());
     else if (a == "--metrics-exclude") set("metrics_exclude", next());
     else if (a == "--sample-threads") set("sample_threads", next());
@@ -135,11 +160,11 @@ int main(int argc, char** argv) {
     else if (a == "--prewarm-ms") set("prewarm_ms", next());
     else if (a == "--http-threads") set("http_threads", next());
     else if (a == "--log-level") set("log_level", next());
-    else if (a == "--pmc") set("enable_pmc", "true");
+    else if (a == "--pmc" || a == "--enable-pmc") set("enable_pmc", "true");
     else if (a == "--pmc-counters") set("pmc_counters", next());
     else if (a == "--pmc-window") o.od.pmc_window_s = atof(next().c_str());
     else if (a == "--pmc-mode") set("pmc_mode", next());
-    else if (a == "--probe") set("enable_probe", "true");
+    else if (a == "--probe" || a == "--enable-probe-kernel") set("enable_probe", "true");
     else if (a == "--probe-every") set("probe_every", next());
     else if (a == "--probe-blocks") o.od.probe_blocks = atoi(next().c_str());
     else if (a == "--plugin-dir") set("plugin_dir", next());
@@ -214,6 +239,18 @@ int main(int argc, char** argv) {
   signal(SIGINT, on_signal);
   signal(SIGTERM, on_signal);
   signal(SIGPIPE, SIG_IGN);
+  // The soft fd limit up to the hard one, as daemons (and Go's runtime) do: container runtimes often
+  // leave the soft limit at 1024, and the HTTP connection cap is derived from it. Nothing in the
+  // process (or the libraries it loads: libamd_smi, libdrm, OpenSSL) uses select(), so fd numbers
+  // past 1024 are safe.
+  if (rlimit rl{}; getrlimit(RLIMIT_NOFILE, &rl) == 0 && rl.rlim_cur < rl.rlim_max) {
+    const rlim_t was = rl.rlim_cur;
+    rl.rlim_cur = rl.rlim_max;
+    if (setrlimit(RLIMIT_NOFILE, &rl) == 0)
+      GPUMON_LOG(LogLevel::kDebug, "main",
+                 "RLIMIT_NOFILE soft limit " + std::to_string(was) + " -> " +
+                     (rl.rlim_max == RLIM_INFINITY ? std::string("unlimited") : std::to_string(rl.rlim_max)));
+  }
   Exporter e(cfg);
   OnDevice ondev(&e, od);
   if (od.pmc || od.probe) {

@@ -33,11 +33,26 @@ def _setup_logging(level: str):
                         format="ts=%(asctime)s level=%(levelname)s component=%(name)s msg=%(message)r")
 
 
+def raise_nofile_limit() -> None:
+    """The soft fd limit up to the hard one, as the native binary does (csrc/exporter_main.cpp):
+    container runtimes often leave the soft limit at 1024, and the HTTP connection cap is derived
+    from it."""
+    import resource
+
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    if soft != resource.RLIM_INFINITY and (hard == resource.RLIM_INFINITY or soft < hard):
+        try:
+            resource.setrlimit(resource.RLIMIT_NOFILE, (hard, hard))
+        except (ValueError, OSError):
+            pass
+
+
 def cmd_serve(args) -> int:
     from .monitor import GpuMonitor
 
     cfg = from_args(args).validate()
     _setup_logging(cfg.log_level)
+    raise_nofile_limit()
     try:
         mon = GpuMonitor(cfg).start()
     except RuntimeError as e:  # the listen address taken, a mock backend that failed, ...

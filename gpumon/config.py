@@ -386,12 +386,16 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--pod-labels", dest="pod_label_allowlist",
                    help="comma-separated pod label keys exported on pod_gpu_* series as label_<key>")
     p.add_argument("--user-label", dest="user_label", help="pod label holding the user name")
-    p.add_argument("--procfs-root", dest="procfs_root")
-    p.add_argument("--cri-socket", dest="cri_socket")
-    p.add_argument("--docker-socket", dest="docker_socket",
+    p.add_argument("--procfs-root", "--procfs", dest="procfs_root")
+    p.add_argument("--cri-socket", "--cri", dest="cri_socket")
+    p.add_argument("--no-cri", dest="cri_socket", action="store_const", const="none",
+                   help="no CRI runtime lookup (kubelet PodResources / log tree / Docker only)")
+    p.add_argument("--docker-socket", "--docker", dest="docker_socket",
                    help="plain-Docker nodes: read container names/labels from the Docker Engine API (opt-in)")
-    p.add_argument("--pod-resources-socket", dest="pod_resources_socket")
-    p.add_argument("--pod-log-root", dest="pod_log_root",
+    p.add_argument("--pod-resources-socket", "--pod-resources", dest="pod_resources_socket")
+    p.add_argument("--no-pod-resources", dest="pod_resources_socket", action="store_const", const="",
+                   help="no kubelet PodResources polling (no idle-allocation rows)")
+    p.add_argument("--pod-log-root", "--pod-logs", dest="pod_log_root",
                    help="non-root metadata: the kubelet's log tree (containers/ + pods/), e.g. /var/log")
     p.add_argument("--device-checkpoint", dest="device_checkpoint",
                    help="GPU allocations from the kubelet's device-plugin checkpoint file (root-readable)")
@@ -403,20 +407,29 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
                    help="comma-separated globs: serve only these metric families (e.g. 'node_gpu_*,pod_gpu_*')")
     p.add_argument("--metrics-exclude", dest="metrics_exclude",
                    help="comma-separated globs: metric families left out of /metrics (e.g. 'gpu_xcd_*')")
+    p.add_argument("--dra-drivers", dest="dra_drivers",
+                   help="comma-separated DRA driver names whose claims are GPU allocations ('none' = off)")
+    p.add_argument("--ras-every", dest="ras_every", type=int, help="RAS error counters every N ticks")
+    p.add_argument("--ras-slices", dest="ras_slices", type=int, help="RAS blocks read in N slices over N ticks")
+    p.add_argument("--influx-token", dest="influx_token", help="InfluxDB 2.x / 3.x API token (default $INFLUXDB_TOKEN)")
     p.add_argument("--sample-threads", dest="sample_threads", type=int)
     p.add_argument("--rt-priority", dest="rt_priority", type=int)
     p.add_argument("--http-rt-priority", dest="http_rt_priority", type=int,
                    help="SCHED_FIFO priority of the HTTP loops (0 = normal; needs CAP_SYS_NICE)")
+    p.add_argument("--http-threads", dest="http_threads", type=int, help="HTTP loop threads serving /metrics")
     p.add_argument("--prewarm-ms", dest="prewarm_ms", type=float,
                    help="device workers warm the firmware-table read this long before each tick (0 = off)")
     p.add_argument("--device-timeout", dest="device_timeout_s", type=float,
                    help="seconds before a device call is exported as hung (gpu_up 0)")
-    p.add_argument("--enable-probe-kernel", dest="enable_probe", action="store_true", default=None)
-    p.add_argument("--enable-pmc", dest="enable_pmc", action="store_true", default=None)
+    p.add_argument("--enable-probe-kernel", "--probe", dest="enable_probe", action="store_true", default=None)
+    p.add_argument("--probe-every", dest="probe_every", type=int, help="K1 probe every N ticks")
+    p.add_argument("--enable-pmc", "--pmc", dest="enable_pmc", action="store_true", default=None)
+    p.add_argument("--pmc-counters", dest="pmc_counters", help="comma-separated PMC counters (default: the built-in set)")
+    p.add_argument("--pmc-mode", dest="pmc_mode", choices=["continuous", "window"])
     p.add_argument("--plugin-dir", dest="plugin_dir", help="directory holding libgpumon_pmc.so / libgpumon_probe.so")
     p.add_argument("--no-fast-path", dest="fast_path", action="store_false", default=None,
                    help="amdsmi: read every value through libamd_smi (disable the sysfs/KFD fast path)")
-    p.add_argument("--sysfs-root", dest="sysfs_root")
+    p.add_argument("--sysfs-root", "--sysfs", dest="sysfs_root")
     p.add_argument("--roctx", dest="roctx", action="store_true", default=None,
                    help="bracket sampler phases with ROCTx ranges (view with rocprofv3 --marker-trace)")
     p.add_argument("--compat", action="store_true",
@@ -435,5 +448,7 @@ def from_args(ns: argparse.Namespace, env: Optional[Dict[str, str]] = None) -> C
     names = {f.name: f for f in dataclasses.fields(cfg)}
     for k, v in vars(ns).items():
         if k in names and v is not None:
+            if k == "dra_drivers" and v == "none":
+                v = ""
             setattr(cfg, k, _coerce(names[k], v))
     return cfg

@@ -98,10 +98,12 @@ def fd_limit_cap(http_threads: int, limit=None) -> int:
 
 
 def fd_limit_check(http_threads: int, limit=None) -> tuple:
-    """A low RLIMIT_NOFILE leaves few scrape connections (256 fds are kept for the sampler)."""
+    """A low RLIMIT_NOFILE leaves few scrape connections (256 fds are kept for the sampler). Both
+    entry points raise their soft limit to the hard one at startup, so the hard limit is the one
+    that counts."""
     import resource
 
-    soft = limit if limit is not None else resource.getrlimit(resource.RLIMIT_NOFILE)[0]
+    soft = limit if limit is not None else resource.getrlimit(resource.RLIMIT_NOFILE)[1]
     if soft == resource.RLIM_INFINITY:
         return OK, "RLIMIT_NOFILE unlimited: 4096 connections per HTTP loop"
     cap = fd_limit_cap(http_threads, soft)

@@ -4,10 +4,12 @@ the fake kubelet. The reference's only self-check was commandexists('docker'/'nv
 
 import json
 import os
+import socket
 import subprocess
 import sys
 
 import grpc
+import pytest
 
 from oracles.attribution.fake_kubelet import FakeKubelet
 from gpumon.config import Config
@@ -179,6 +181,58 @@ def test_doctor_cap_formula_is_the_servers(core):
             assert ex.self_stats()["http_max_conns"] == threads * fd_limit_cap(threads)
         finally:
             ex.stop()
+
+
+@pytest.mark.parametrize("entry", ["native", "python"])
+def test_serve_raises_the_soft_fd_limit_to_the_hard_one(entry):
+    """Container runtimes often start a pod at a soft nofile limit of 1024 under a high hard limit:
+    both entry points raise the soft limit, so the connection cap (gpumon_http_max_connections)
+    comes from the hard one."""
+    import os
+    import resource
+    import subprocess
+    import sys
+    import time
+    import urllib.request
+
+    from gpumon.doctor import fd_limit_cap
+    from gpumon.export import promtext
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hard = resource.getrlimit(resource.RLIMIT_NOFILE)[1]
+    if hard != resource.RLIM_INFINITY and hard < 2048:
+        pytest.skip(f"hard nofile limit {hard}: nothing to raise to")
+    hard = 4096  # a definite value under this process's hard limit
+
+    def limits():
+        resource.setrlimit(resource.RLIMIT_NOFILE, (512, hard))
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = ([os.path.join(root, "bin", "gpumon-exporter")] if entry == "native"
+           else [sys.executable, "-m", "gpumon", "serve", "--control-plane", "off"])
+    cmd += ["--backend", "mock:gpus=1", "--interval", "0.2", "--listen", f"127.0.0.1:{port}", "--http-threads", "2"]
+    p = subprocess.Popen(cmd, cwd=root, env=dict(os.environ, PYTHONPATH=root), stdout=subprocess.DEVNULL,
+                         stderr=subprocess.DEVNULL, preexec_fn=limits)
+    try:
+        body = None
+        deadline = time.time() + 30
+        while time.time() < deadline and body is None:
+            try:
+                body = urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=2).read().decode()
+            except OSError:
+                time.sleep(0.1)
+        assert body is not None
+        with open(f"/proc/{p.pid}/limits") as fh:
+            row = next(l for l in fh if l.startswith("Max open files")).split()
+        assert row[3:5] == [str(hard), str(hard)], row
+        fam = promtext.parse(body)
+        assert promtext.one(fam, "gpumon_http_max_connections") == 2 * fd_limit_cap(2, limit=hard)
+    finally:
+        p.terminate()
+        p.wait(10)
 
 
 def test_doctor_checks_the_listen_address():

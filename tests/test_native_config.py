@@ -100,6 +100,43 @@ def test_rich_file_env_and_flag_precedence(tmp_path):
     assert py["devices"] == ["1", "3"] and py["influx_url"] == "http://other/write" and py["host"] == "gpu-node-7"
 
 
+FLAG_SETS = [
+    ["--procfs-root", "/host/proc", "--sysfs-root", "/host/sys", "--cri-socket", "/run/c.sock",
+     "--pod-resources-socket", "/pr.sock", "--docker-socket", "/d.sock", "--pod-log-root", "/var/log",
+     "--enable-pmc", "--enable-probe-kernel", "--device-timeout", "3.5", "--http-threads", "3"],
+    ["--procfs", "/host/proc", "--sysfs", "/host/sys", "--cri", "/run/c.sock", "--pod-resources", "/pr.sock",
+     "--docker", "/d.sock", "--pod-logs", "/var/log", "--pmc", "--probe", "--ras-every", "7", "--ras-slices", "2",
+     "--dra-drivers", "none", "--pmc-mode", "window", "--probe-every", "4"],
+    ["--no-cri", "--no-pod-resources", "--compat"],
+    ["--compat", "--interval", "1", "--opt-in-label", "team=ml"],
+    ["--control-plane", "off"],
+]
+
+
+@pytest.mark.parametrize("flags", FLAG_SETS, ids=["python-spellings", "native-spellings", "off-switches", "compat",
+                                                   "control-plane-off"])
+def test_both_entry_points_take_each_others_flags(flags):
+    """One flag vocabulary: a command line written for `gpumon serve` runs the image's native
+    entrypoint unchanged and the other way round, with the same resulting configuration."""
+    import argparse
+
+    from gpumon.config import add_cli_args, from_args
+
+    r = _print(*flags)
+    assert r.returncode == 0, r.stderr
+    native = json.loads(r.stdout)
+    ap = argparse.ArgumentParser()
+    add_cli_args(ap)
+    py = dataclasses.asdict(from_args(ap.parse_args(flags), env={}))
+    if "--control-plane" in flags:
+        # Python turns its pollers off as a whole; the native binary clears each source
+        assert py["control_plane"] == "off"
+        assert native["pod_resources_socket"] == "" and native["cri_socket"] == "none"
+        assert native["docker_socket"] == "" and native["pod_log_root"] == ""
+        return
+    _same(native, py)
+
+
 def test_config_env_var_names_the_file(tmp_path):
     p = tmp_path / "c.yaml"
     p.write_text("gpumon:\n  ras_every: 7\n")
