@@ -58,7 +58,8 @@ int main(int argc, char** argv) {
   NativeOptions o;
   std::string err;
   // 1. config file: --config wins over GPUMON_CONFIG
-  std::string config = getenv("GPUMON_CONFIG") ? getenv("GPUMON_CONFIG") : "";
+  const char* config_env = getenv("GPUMON_CONFIG");
+  std::string config = config_env ? config_env : "";
   for (int i = 1; i + 1 < argc; ++i)
     if (std::string(argv[i]) == "--config") config = argv[i + 1];
   if (!config.empty()) {
