@@ -75,6 +75,9 @@ class _Sink(http.server.BaseHTTPRequestHandler):
                                   "host": self.headers.get("Host"), "auth": self.headers.get("Authorization")})
         self.send_response(204)
         self.send_header("Content-Length", "0")
+        if self.server.close_every and len(self.server.posts) % self.server.close_every == 0:
+            self.send_header("Connection", "close")
+            self.close_connection = True
         self.end_headers()
 
     def log_message(self, *a):
@@ -84,9 +87,10 @@ class _Sink(http.server.BaseHTTPRequestHandler):
 class _TlsSink(http.server.ThreadingHTTPServer):
     daemon_threads = True
 
-    def __init__(self, cert, key, client_ca=None, family=socket.AF_INET, host="127.0.0.1"):
+    def __init__(self, cert, key, client_ca=None, family=socket.AF_INET, host="127.0.0.1", close_every=0):
         self.address_family = family
         super().__init__((host, 0), _Sink)
+        self.close_every = close_every  # every Nth answer says Connection: close (a load balancer)
         self.posts = []
         self.handshake_errors = []
         ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
@@ -167,6 +171,18 @@ def test_https_keeps_one_connection_across_pushes(core, pki):
     assert len(srv.posts) == 5
     assert len({p["peer"] for p in srv.posts}) == 1
     assert srv.posts[0]["host"] == f"localhost:{srv.port}"
+
+
+def test_https_reconnects_after_the_server_closes(core, pki):
+    """A load balancer in front of InfluxDB answers some requests with Connection: close: the next
+    push opens a new connection and handshakes again, and no push is lost or retried twice."""
+    with _TlsSink(pki["server"], pki["server_key"], close_every=2) as srv:
+        st, _, err = core.http_request("POST", f"https://localhost:{srv.port}/write?db=x", "m v=1", "", 5.0,
+                                       pki["ca"], False, 6)
+    assert st == 204, err
+    assert len(srv.posts) == 6  # exactly once each
+    assert len({p["peer"] for p in srv.posts}) == 3  # 2 requests per connection
+    assert not srv.handshake_errors
 
 
 def test_https_to_an_ipv6_literal(core, pki):
