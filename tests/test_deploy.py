@@ -377,6 +377,37 @@ def test_docker_overlay_mounts_the_socket_and_sets_docker_socket():
     assert all("docker" not in x["mountPath"] for x in base)
 
 
+def test_influx_overlay_pushes_over_verified_https(core, tmp_path):
+    """overlays/influx/: the reference's push on top of /metrics, for an InfluxDB 2.x / 3.x server
+    over verified HTTPS. The token comes from a Secret, the server's CA from the same Secret
+    (mounted), and the URL is one the exporter's startup check accepts."""
+    import subprocess
+
+    (k,) = _docs("deploy/k8s/overlays/influx/kustomization.yaml")
+    assert k["resources"] == ["../../"]
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"])
+    pod = _json_patch(ds, ops)["spec"]["template"]["spec"]
+    c = pod["containers"][0]
+    env = {e["name"]: e for e in c["env"]}
+    assert env["INFLUXDB_TOKEN"]["valueFrom"]["secretKeyRef"] == {"name": "gpumon-influx", "key": "token"}
+    assert "NODE_NAME" in env  # the base's env is kept
+    url, ca = env["INFLUXDB_URL"]["value"], env["GPUMON_INFLUX_CA_FILE"]["value"]
+    u = core.parse_url(url)
+    assert u["ok"] and u["tls"] and "/api/v2/write?" in url, u
+    vols = {v["name"]: v for v in pod["volumes"]}
+    assert all(m["name"] in vols for m in c["volumeMounts"])
+    m = next(m for m in c["volumeMounts"] if ca.startswith(m["mountPath"] + "/"))
+    sec = vols[m["name"]]["secret"]
+    assert m["readOnly"] and sec["secretName"] == "gpumon-influx"
+    assert [i["path"] for i in sec["items"]] == [os.path.basename(ca)]
+    # the startup check accepts that configuration once the Secret's CA file is there
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:prime256v1", "-nodes",
+                    "-days", "1", "-keyout", str(tmp_path / "k"), "-out", str(tmp_path / "ca.crt"), "-subj", "/CN=ca"],
+                   check=True, capture_output=True, timeout=60)
+    assert core.check_push_config(url, token="tok", ca_file=str(tmp_path / "ca.crt")) == ""
+
+
 def test_serve_imports_no_oracle_or_grpc():
     """the image's `gpumon serve` (ENTRYPOINT) must not import grpcio / protobuf or
     the Python test oracles -- they live under tests/oracles and are not in the image. The package
