@@ -137,6 +137,20 @@ def test_both_entry_points_take_each_others_flags(flags):
     _same(native, py)
 
 
+@pytest.mark.parametrize("args,rc,want", [
+    (["--help"], 0, "usage: gpumon-exporter"),
+    (["--no-such-flag"], 2, "unknown flag --no-such-flag"),
+    (["--interval"], 2, "usage: gpumon-exporter"),  # a flag missing its value
+    (["--control-plane", "maybe"], 2, "--control-plane: native or off, not 'maybe'"),
+    (["--interval", "fast"], 2, "interval"),
+    (["--listen", "[::1"], 2, "listen"),
+])
+def test_native_binary_refuses_bad_command_lines(args, rc, want):
+    r = subprocess.run([BIN, *args], capture_output=True, text=True, timeout=30, env=CLEAN_ENV)
+    assert r.returncode == rc, (r.returncode, r.stderr[-1000:])
+    assert want in r.stderr, r.stderr[-1000:]
+
+
 def test_config_env_var_names_the_file(tmp_path):
     p = tmp_path / "c.yaml"
     p.write_text("gpumon:\n  ras_every: 7\n")
