@@ -114,6 +114,9 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "influx_tls_insecure", &c.influx_tls_insecure);
   get(d, "influx_client_cert", &c.influx_client_cert);
   get(d, "influx_client_key", &c.influx_client_key);
+  get(d, "tls_cert_file", &c.tls_cert_file);
+  get(d, "tls_key_file", &c.tls_key_file);
+  get(d, "tls_client_ca_file", &c.tls_client_ca_file);
   get(d, "init_retry_s", &c.init_retry_s);
   get(d, "health_stale_s", &c.health_stale_s);
   get(d, "reinit_after", &c.reinit_after);
@@ -772,6 +775,8 @@ PYBIND11_MODULE(_core, m) {
       },
       py::arg("url"), py::arg("token") = "", py::arg("ca_file") = "", py::arg("insecure") = false,
       py::arg("client_cert") = "", py::arg("client_key") = "");
+  m.def("check_serve_tls", &check_serve_tls, py::arg("cert_file") = "", py::arg("key_file") = "",
+        py::arg("client_ca_file") = "", "configuration-time check of the /metrics HTTPS files: \"\" = usable");
   m.def("redact_url", &redact_url);
   m.def("parse_listen", [](const std::string& l) {
     std::string host, err;
@@ -940,6 +945,7 @@ PYBIND11_MODULE(_core, m) {
              d["http_rt_demotions"] = s.http_rt_demotions;
              d["http_evicted"] = s.http_evicted;
              d["http_max_conns"] = s.http_max_conns;
+             d["http_tls_failures"] = s.http_tls_failures;
              d["hidden_contexts"] = s.hidden_contexts;
              d["hidden_peer_contexts"] = s.hidden_peer_contexts;
              d["rt_threads"] = s.rt_threads;

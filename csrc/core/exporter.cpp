@@ -206,6 +206,15 @@ bool Exporter::start(std::string* err) {
         });
     server_->set_rt(cfg_.http_rt_priority, cfg_.http_rt_budget);
     std::string e;
+    if (!cfg_.tls_cert_file.empty() || !cfg_.tls_key_file.empty() || !cfg_.tls_client_ca_file.empty()) {
+      auto tls = TlsServer::create(cfg_.tls_cert_file, cfg_.tls_key_file, cfg_.tls_client_ca_file, &e);
+      if (!tls) {
+        if (err) *err = e;
+        server_.reset();
+        return false;
+      }
+      server_->set_tls(std::move(tls));
+    }
     if (!server_->start(&e)) {
       if (err) *err = e;
       server_.reset();
@@ -1001,6 +1010,7 @@ SelfStats Exporter::self_stats() const {
   if (server_) {
     s.http_evicted = static_cast<int64_t>(server_->evicted());
     s.http_max_conns = static_cast<int64_t>(server_->max_conns() * static_cast<size_t>(std::max(1, cfg_.http_threads)));
+    if (server_->tls()) s.http_tls_failures = static_cast<int64_t>(server_->tls_failures());
   }
   if (cfg_.http_rt_priority > 0 && server_) {
     s.http_rt_loops = server_->rt_loops();

@@ -48,6 +48,8 @@ struct ExporterConfig {
   int http_threads = 2;
   int http_rt_priority = 0;           // SCHED_FIFO HTTP loops (needs CAP_SYS_NICE; 0 = normal scheduling)
   double http_rt_budget = 0.2;        // ... at most this share of a CPU per loop per 100 ms window, then demoted
+  // /metrics over HTTPS: PEM certificate chain + key; a client CA makes it mutual TLS (tls.h TlsServer)
+  std::string tls_cert_file, tls_key_file, tls_client_ca_file;
   std::string host = "no_name";       // NODE_NAME (reference fallback "no_name", gpu.py:23-24)
   bool gzip = true;
   bool roctx = false;                 // ROCTx ranges around sampler phases (also GPUMON_ROCTX=1)

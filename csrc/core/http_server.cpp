@@ -24,6 +24,7 @@
 #include <unordered_map>
 
 #include "common.h"
+#include "tls.h"
 
 namespace gpumon {
 
@@ -82,6 +83,8 @@ struct Conn {
   int64_t req_ns = 0;
   std::string path;
   uint32_t served = 0;  // requests answered on this connection (a scraper's keep-alive has > 0)
+  void* ssl = nullptr;  // TLS session (HttpServer::set_tls), else plain
+  bool hs = false;      // TLS handshake still in progress
 };
 
 bool set_nonblock(int fd) {
@@ -392,7 +395,10 @@ void HttpServer::stop() {
   }
   for (auto& L : loops_) {
     if (L->th.joinable()) L->th.join();
-    for (auto& [fd, c] : L->conns) close(fd);
+    for (auto& [fd, c] : L->conns) {
+      if (c.ssl) tls_->free_session(c.ssl);
+      close(fd);
+    }
     L->conns.clear();
     L->lru.clear();
     close(L->ep);
@@ -436,13 +442,23 @@ void HttpServer::run(Loop* L) {
   const int64_t budget_ns = static_cast<int64_t>(std::clamp(rt_budget_, 0.01, 1.0) * kRtWindowNs);
   auto close_conn = [&](int fd) {
     epoll_ctl(L->ep, EPOLL_CTL_DEL, fd, nullptr);
-    close(fd);
     auto it = L->conns.find(fd);
     if (it != L->conns.end()) {
+      if (it->second.ssl) tls_->free_session(it->second.ssl);
       L->lru.erase(it->second.lru);
       L->conns.erase(it);
     }
+    close(fd);
     conns_.fetch_sub(1);
+  };
+  // one read of request bytes: plain read(), or decrypted bytes of a TLS session (errno EAGAIN when
+  // nothing is ready, EIO on a TLS error)
+  auto rd = [&](Conn& c, char* b, size_t n) -> ssize_t {
+    if (!c.ssl) return read(c.fd, b, n);
+    const long r = tls_->read(c.ssl, b, n);
+    if (r >= 0) return r;
+    errno = r == -1 ? EAGAIN : EIO;
+    return -1;
   };
   auto set_events = [&](int fd, uint32_t e) {
     epoll_event ev{};
@@ -452,7 +468,15 @@ void HttpServer::run(Loop* L) {
   };
   // Writes pending output; returns false if the connection must be closed.
   auto flush = [&](Conn& c) -> bool {
-    while (c.head_off < c.head.size() || c.body_off < c.body_len) {
+    // TLS: the body was folded into `head` (serve): records come from one buffer, resumed at
+    // head_off after a full socket (partial-write mode)
+    while (c.ssl && c.head_off < c.head.size()) {
+      const long w = tls_->write(c.ssl, c.head.data() + c.head_off, c.head.size() - c.head_off);
+      if (w == -1) return true;
+      if (w < 0) return false;
+      c.head_off += static_cast<size_t>(w);
+    }
+    while (!c.ssl && (c.head_off < c.head.size() || c.body_off < c.body_len)) {
       iovec iov[2];
       int n = 0;
       if (c.head_off < c.head.size()) {
@@ -496,6 +520,7 @@ void HttpServer::run(Loop* L) {
     c.head_off = c.body_off = 0;
     c.req_ns = 0;
     if (c.close_after) {  // lingering close (kLingerNs)
+      if (c.ssl) tls_->notify_close(c.ssl);
       shutdown(c.fd, SHUT_WR);
       c.closing = true;
       c.closing_ns = mono_ns();
@@ -552,6 +577,13 @@ void HttpServer::run(Loop* L) {
       c.head += req.keep_alive ? "Connection: keep-alive\r\n\r\n" : "Connection: close\r\n\r\n";
       c.body = req.method == "HEAD" ? nullptr : body;
       c.body_len = req.method == "HEAD" ? 0 : blen;
+      if (c.ssl && c.body_len) {  // one buffer for the records (a copy is small next to encrypting it)
+        c.head.append(c.body, c.body_len);
+        c.body = nullptr;
+        c.body_len = 0;
+        c.owner.reset();
+        c.inline_body.clear();
+      }
       c.close_after = !req.keep_alive;
       c.writing = true;
       if (!flush(c)) return false;
@@ -694,6 +726,16 @@ void HttpServer::run(Loop* L) {
           Conn c;
           c.fd = cfd;
           c.last_ns = now;
+          if (tls_) {
+            c.ssl = tls_->new_session(cfd);
+            if (!c.ssl) {
+              tls_failures_.fetch_add(1, std::memory_order_relaxed);
+              close(cfd);
+              continue;
+            }
+            c.hs = true;
+            c.req_start_ns = now;  // the handshake is held to the header timeout
+          }
           c.lru = L->lru.insert(L->lru.end(), cfd);
           L->conns.emplace(cfd, std::move(c));
           conns_.fetch_add(1);
@@ -715,6 +757,7 @@ void HttpServer::run(Loop* L) {
       c.last_ns = now;
       L->lru.splice(L->lru.end(), L->lru, c.lru);  // most recently active last
       if (evs[i].events & (EPOLLERR | EPOLLHUP)) {
+        if (c.hs) tls_failures_.fetch_add(1, std::memory_order_relaxed);  // e.g. a scraper that reset on our certificate
         close_conn(fd);
         continue;
       }
@@ -731,6 +774,22 @@ void HttpServer::run(Loop* L) {
         }
         continue;
       }
+      if (c.hs) {
+        const TlsServer::Step st = tls_->handshake(c.ssl);
+        if (st == TlsServer::Step::kFailed) {  // a plain-HTTP client, a wrong CA, no client certificate
+          tls_failures_.fetch_add(1, std::memory_order_relaxed);
+          close_conn(fd);
+          continue;
+        }
+        if (st != TlsServer::Step::kDone) {
+          set_events(fd, (st == TlsServer::Step::kWantWrite ? EPOLLOUT : EPOLLIN) | EPOLLRDHUP);
+          continue;
+        }
+        c.hs = false;
+        c.req_start_ns = 0;
+        set_events(fd, EPOLLIN | EPOLLRDHUP);
+        // the request may have come with the handshake's last flight: read it now
+      }
       if (c.closing) {  // discard input until the client closes too
         char buf[8192];
         ssize_t r;
@@ -740,10 +799,11 @@ void HttpServer::run(Loop* L) {
         continue;
       }
       bool peer_closed = false;
-      if (evs[i].events & (EPOLLIN | EPOLLRDHUP)) {
+      // a TLS session is always read: a record may sit in the socket since the handshake's last step
+      if ((evs[i].events & (EPOLLIN | EPOLLRDHUP)) || c.ssl) {
         char buf[8192];
         while (true) {
-          ssize_t r = read(fd, buf, sizeof buf);
+          ssize_t r = rd(c, buf, sizeof buf);
           if (r > 0) {
             if (c.in.empty()) c.req_start_ns = now;
             c.in.append(buf, static_cast<size_t>(r));
@@ -766,8 +826,10 @@ void HttpServer::run(Loop* L) {
       std::vector<int> idle;
       for (auto& [fd, c] : L->conns)
         if (now - c.last_ns > kIdleTimeoutNs || (c.closing && now - c.closing_ns > kLingerNs) ||
-            (!c.writing && !c.closing && !c.in.empty() && now - c.req_start_ns > header_timeout_ns_))
+            (!c.writing && !c.closing && (c.hs || !c.in.empty()) && now - c.req_start_ns > header_timeout_ns_)) {
           idle.push_back(fd);
+          if (c.hs) tls_failures_.fetch_add(1, std::memory_order_relaxed);  // a handshake that never finished
+        }
       for (int fd : idle) close_conn(fd);
     }
   }

@@ -22,6 +22,8 @@
 
 namespace gpumon {
 
+class TlsServer;
+
 struct HttpRequest {
   std::string method;
   std::string path;        // without query string
@@ -59,6 +61,10 @@ class HttpServer {
     rt_prio_ = prio;
     rt_budget_ = budget;
   }
+  // Serve HTTPS: every accepted connection handshakes first (tls.h TlsServer). Before start().
+  void set_tls(std::shared_ptr<TlsServer> tls) { tls_ = std::move(tls); }
+  bool tls() const { return tls_ != nullptr; }
+  uint64_t tls_failures() const { return tls_failures_.load(); }  // handshakes that failed or timed out
   int rt_loops() const { return rt_loops_.load(); }           // loops running at SCHED_FIFO now
   uint64_t rt_demotions() const { return rt_demotions_.load(); }  // budget exhaustions
   uint64_t evicted() const { return evicted_.load(); }            // closed to make room at the cap
@@ -98,6 +104,8 @@ class HttpServer {
   // Evictions owed by the loops: a loop at the cap with nothing of its own to evict (the other
   // loop holds the flood) admits the newcomer and asks the others to close one of theirs.
   std::atomic<int> evict_debt_{0};
+  std::shared_ptr<TlsServer> tls_;
+  std::atomic<uint64_t> tls_failures_{0};
 };
 
 }  // namespace gpumon

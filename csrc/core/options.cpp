@@ -262,6 +262,9 @@ const std::map<std::string, Setter>& setters() {
       {"influx_schema", int_at([](NativeOptions* o) { return &o->cfg.influx_schema; })},
       {"influx_every", int_at([](NativeOptions* o) { return &o->cfg.influx_every; })},
       {"influx_ca_file", str_at([](NativeOptions* o) { return &o->cfg.influx_ca_file; })},
+      {"tls_cert_file", str_at([](NativeOptions* o) { return &o->cfg.tls_cert_file; })},
+      {"tls_key_file", str_at([](NativeOptions* o) { return &o->cfg.tls_key_file; })},
+      {"tls_client_ca_file", str_at([](NativeOptions* o) { return &o->cfg.tls_client_ca_file; })},
       {"influx_tls_insecure", bool_at([](NativeOptions* o) { return &o->cfg.influx_tls_insecure; })},
       {"influx_client_cert", str_at([](NativeOptions* o) { return &o->cfg.influx_client_cert; })},
       {"influx_client_key", str_at([](NativeOptions* o) { return &o->cfg.influx_client_key; })},
@@ -543,6 +546,9 @@ std::string options_json(const NativeOptions& o) {
   N("influx_schema", c.influx_schema);
   N("influx_every", c.influx_every);
   S("influx_ca_file", c.influx_ca_file);
+  S("tls_cert_file", c.tls_cert_file);
+  S("tls_key_file", c.tls_key_file);
+  S("tls_client_ca_file", c.tls_client_ca_file);
   B("influx_tls_insecure", c.influx_tls_insecure);
   S("influx_client_cert", c.influx_client_cert);
   S("influx_client_key", c.influx_client_key);

@@ -852,6 +852,14 @@ void render_prometheus(const RenderInput& in, std::string* o) {
                "counter");
       f.add(hl, static_cast<double>(s.http_evicted));
     }
+    if (s.http_tls_failures >= 0) {
+      Family f(o, "gpumon_http_tls_handshake_failures_total",
+               "/metrics over HTTPS (tls_cert_file): connections whose TLS handshake failed or did not finish "
+               "within the header timeout -- a plain-HTTP scraper, a scraper that does not trust the "
+               "certificate, or (mutual TLS) one without an accepted client certificate.",
+               "counter");
+      f.add(hl, static_cast<double>(s.http_tls_failures));
+    }
     if (s.http_rt_loops >= 0) {
       {
         Family f(o, "gpumon_http_rt_loops",

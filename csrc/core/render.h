@@ -70,6 +70,7 @@ struct SelfStats {
   int http_rt_loops = -1;            // HTTP loops at SCHED_FIFO now (-1: http_rt_priority off)
   int64_t http_evicted = -1;         // connections closed to make room at the cap (-1: no server)
   int64_t http_max_conns = -1;       // connection cap over all HTTP loops (from RLIMIT_NOFILE)
+  int64_t http_tls_failures = -1;    // /metrics over HTTPS: failed / timed-out handshakes (-1: plain HTTP)
   int64_t http_rt_demotions = -1;    // ... times a loop spent its CPU budget and was demoted
   uint64_t overruns = 0;
   double last_tick_wall_s = 0;

@@ -7,6 +7,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdint>
 #include <cstdlib>
@@ -26,6 +27,9 @@ constexpr int kVerifyNone = 0, kVerifyPeer = 1;
 constexpr int kCtrlSetTlsextHostname = 55, kTlsextNametypeHostName = 0;
 constexpr int kCtrlSetMinProtoVersion = 123, kTls12Version = 0x0303;
 constexpr int kFiletypePem = 1;
+constexpr int kVerifyFailIfNoPeerCert = 2;
+constexpr int kCtrlMode = 33, kCtrlSetSessCacheMode = 44;
+constexpr long kModeEnablePartialWrite = 0x1, kModeAcceptMovingWriteBuffer = 0x2, kSessCacheOff = 0;
 constexpr int kErrorNone = 0, kErrorSsl = 1, kErrorWantRead = 2, kErrorWantWrite = 3, kErrorSyscall = 5,
               kErrorZeroReturn = 6;
 constexpr long kVerifyOk = 0;
@@ -38,6 +42,11 @@ struct SslApi {
   // libssl
   int (*OPENSSL_init_ssl)(uint64_t, const void*) = nullptr;
   const void* (*TLS_client_method)() = nullptr;
+  const void* (*TLS_server_method)() = nullptr;
+  int (*SSL_CTX_set_session_id_context)(void*, const unsigned char*, unsigned int) = nullptr;
+  int (*SSL_CTX_set_num_tickets)(void*, size_t) = nullptr;
+  void (*SSL_set_accept_state)(void*) = nullptr;
+  int (*SSL_do_handshake)(void*) = nullptr;
   void* (*SSL_CTX_new)(const void*) = nullptr;
   void (*SSL_CTX_free)(void*) = nullptr;
   long (*SSL_CTX_ctrl)(void*, int, long, void*) = nullptr;
@@ -113,6 +122,11 @@ void load_api() {
   void* c = a->crypto_dl;
   sym(s, "OPENSSL_init_ssl", &a->OPENSSL_init_ssl, &missing);
   sym(s, "TLS_client_method", &a->TLS_client_method, &missing);
+  sym(s, "TLS_server_method", &a->TLS_server_method, &missing);
+  sym(s, "SSL_CTX_set_session_id_context", &a->SSL_CTX_set_session_id_context, &missing);
+  sym(s, "SSL_CTX_set_num_tickets", &a->SSL_CTX_set_num_tickets, &missing);
+  sym(s, "SSL_set_accept_state", &a->SSL_set_accept_state, &missing);
+  sym(s, "SSL_do_handshake", &a->SSL_do_handshake, &missing);
   sym(s, "SSL_CTX_new", &a->SSL_CTX_new, &missing);
   sym(s, "SSL_CTX_free", &a->SSL_CTX_free, &missing);
   sym(s, "SSL_CTX_ctrl", &a->SSL_CTX_ctrl, &missing);
@@ -383,6 +397,120 @@ void TlsConn::shutdown() {
     ctx_->api()->SSL_shutdown(ssl_);  // non-blocking: one attempt to send close_notify
     ctx_->api()->ERR_clear_error();
   }
+}
+
+std::shared_ptr<TlsServer> TlsServer::create(const std::string& cert_file, const std::string& key_file,
+                                             const std::string& client_ca_file, std::string* err) {
+  if (cert_file.empty() && key_file.empty() && !client_ca_file.empty()) {
+    *err = "tls_client_ca_file needs tls_cert_file and tls_key_file";
+    return nullptr;
+  }
+  if (cert_file.empty() || key_file.empty()) {
+    *err = "tls_cert_file and tls_key_file go together";
+    return nullptr;
+  }
+  for (const std::string* f : {&cert_file, &key_file, &client_ca_file})
+    if (!f->empty() && access(f->c_str(), R_OK) != 0) {
+      *err = "cannot read " + *f + ": " + strerror(errno);
+      return nullptr;
+    }
+  const SslApi* a = ssl_api(err);
+  if (!a) return nullptr;
+  std::shared_ptr<TlsServer> t(new TlsServer);
+  t->api_ = a;
+  a->ERR_clear_error();
+  t->ctx_ = a->SSL_CTX_new(a->TLS_server_method());
+  if (!t->ctx_) {
+    *err = "tls: SSL_CTX_new: " + err_queue(a);
+    return nullptr;
+  }
+  a->SSL_CTX_ctrl(t->ctx_, ossl::kCtrlSetMinProtoVersion, ossl::kTls12Version, nullptr);
+  // partial writes: a response larger than the socket buffer goes out record by record, resumed
+  // from the loop's offset on the next EPOLLOUT
+  a->SSL_CTX_ctrl(t->ctx_, ossl::kCtrlMode, ossl::kModeEnablePartialWrite | ossl::kModeAcceptMovingWriteBuffer, nullptr);
+  a->SSL_CTX_ctrl(t->ctx_, ossl::kCtrlSetSessCacheMode, ossl::kSessCacheOff, nullptr);
+  a->SSL_CTX_set_num_tickets(t->ctx_, 0);
+  static const unsigned char kSid[] = "gpumon";
+  a->SSL_CTX_set_session_id_context(t->ctx_, kSid, sizeof kSid - 1);
+  if (a->SSL_CTX_use_certificate_chain_file(t->ctx_, cert_file.c_str()) != 1) {
+    *err = "tls: cannot load certificate " + cert_file + ": " + err_queue(a);
+    return nullptr;
+  }
+  if (a->SSL_CTX_use_PrivateKey_file(t->ctx_, key_file.c_str(), ossl::kFiletypePem) != 1 ||
+      a->SSL_CTX_check_private_key(t->ctx_) != 1) {
+    *err = "tls: cannot load key " + key_file + " (or it does not match the certificate): " + err_queue(a);
+    return nullptr;
+  }
+  if (!client_ca_file.empty()) {
+    if (a->SSL_CTX_load_verify_locations(t->ctx_, client_ca_file.c_str(), nullptr) != 1) {
+      *err = "tls: cannot load client CA " + client_ca_file + ": " + err_queue(a);
+      return nullptr;
+    }
+    a->SSL_CTX_set_verify(t->ctx_, ossl::kVerifyPeer | ossl::kVerifyFailIfNoPeerCert, nullptr);
+    t->mutual_ = true;
+  }
+  return t;
+}
+
+TlsServer::~TlsServer() {
+  if (ctx_) api_->SSL_CTX_free(ctx_);
+}
+
+void* TlsServer::new_session(int fd) const {
+  void* ssl = api_->SSL_new(ctx_);
+  if (!ssl) return nullptr;
+  if (api_->SSL_set_fd(ssl, fd) != 1) {
+    api_->SSL_free(ssl);
+    return nullptr;
+  }
+  api_->SSL_set_accept_state(ssl);
+  return ssl;
+}
+
+TlsServer::Step TlsServer::handshake(void* ssl) const {
+  api_->ERR_clear_error();
+  const int r = api_->SSL_do_handshake(ssl);
+  if (r == 1) return Step::kDone;
+  const int e = api_->SSL_get_error(ssl, r);
+  if (e == ossl::kErrorWantRead) return Step::kWantRead;
+  if (e == ossl::kErrorWantWrite) return Step::kWantWrite;
+  api_->ERR_clear_error();
+  return Step::kFailed;
+}
+
+long TlsServer::read(void* ssl, char* buf, size_t n) const {
+  api_->ERR_clear_error();
+  const int r = api_->SSL_read(ssl, buf, static_cast<int>(std::min<size_t>(n, 1 << 30)));
+  if (r > 0) return r;
+  const int e = api_->SSL_get_error(ssl, r);
+  if (e == ossl::kErrorWantRead || e == ossl::kErrorWantWrite) return -1;
+  api_->ERR_clear_error();
+  // close_notify, or a peer that just closed the TCP connection: both end the connection
+  return e == ossl::kErrorZeroReturn || e == ossl::kErrorSyscall ? 0 : -2;
+}
+
+long TlsServer::write(void* ssl, const char* p, size_t n) const {
+  api_->ERR_clear_error();
+  const int w = api_->SSL_write(ssl, p, static_cast<int>(std::min<size_t>(n, 1 << 30)));
+  if (w > 0) return w;
+  const int e = api_->SSL_get_error(ssl, w);
+  if (e == ossl::kErrorWantWrite || e == ossl::kErrorWantRead) return -1;
+  api_->ERR_clear_error();
+  return -2;
+}
+
+void TlsServer::notify_close(void* ssl) const {
+  api_->SSL_shutdown(ssl);
+  api_->ERR_clear_error();
+}
+
+void TlsServer::free_session(void* ssl) const { api_->SSL_free(ssl); }
+
+std::string check_serve_tls(const std::string& cert_file, const std::string& key_file,
+                            const std::string& client_ca_file) {
+  if (cert_file.empty() && key_file.empty() && client_ca_file.empty()) return "";
+  std::string err;
+  return TlsServer::create(cert_file, key_file, client_ca_file, &err) ? "" : err;
 }
 
 std::string check_push_config(const std::string& url, const std::string& token, const TlsOptions& tls) {

@@ -73,6 +73,39 @@ class TlsConn {
   int64_t timeout_ns_;
 };
 
+// Server side: /metrics over HTTPS (tls_cert_file / tls_key_file; tls_client_ca_file adds mutual
+// TLS, a scraper without a certificate signed by that CA fails the handshake). One context per
+// server, shared by the HTTP loops; one session per accepted connection, driven non-blocking by
+// the loop's epoll events (http_server.cpp). No session resumption: a Prometheus keep-alive
+// connection handshakes once per connection anyway.
+class TlsServer {
+ public:
+  static std::shared_ptr<TlsServer> create(const std::string& cert_file, const std::string& key_file,
+                                           const std::string& client_ca_file, std::string* err);
+  ~TlsServer();
+  bool mutual() const { return mutual_; }
+  // A session over an accepted non-blocking socket; nullptr if OpenSSL refuses one.
+  void* new_session(int fd) const;
+  enum class Step { kDone, kWantRead, kWantWrite, kFailed };
+  Step handshake(void* ssl) const;
+  // > 0 bytes read; 0 = the peer closed; -1 = nothing now (wait for EPOLLIN); -2 = a TLS error
+  long read(void* ssl, char* buf, size_t n) const;
+  // > 0 bytes written; -1 = the socket is full (wait for EPOLLOUT); -2 = a TLS error
+  long write(void* ssl, const char* p, size_t n) const;
+  void notify_close(void* ssl) const;  // one non-blocking close_notify attempt
+  void free_session(void* ssl) const;
+
+ private:
+  TlsServer() = default;
+  const SslApi* api_ = nullptr;
+  void* ctx_ = nullptr;  // SSL_CTX*
+  bool mutual_ = false;
+};
+
+// Configuration-time check of the serving certificate, key and client CA: "" = usable.
+std::string check_serve_tls(const std::string& cert_file, const std::string& key_file,
+                            const std::string& client_ca_file);
+
 // Configuration-time check of a push URL and its TLS settings (both entry points call it): the
 // scheme, host and port parse, a token without line breaks, an https URL with libssl loadable and a
 // readable CA / client certificate. "" = usable; otherwise the reason.

@@ -38,6 +38,7 @@ static void usage() {
           "                       [--listen HOST:PORT|[V6]:PORT|:PORT] [--host NAME] [--devices 0,1|BDF,..] [--no-fast-path]\n"
           "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
           "                       [--influx-ca-file PEM] [--influx-tls-insecure] [--influx-client-cert PEM --influx-client-key PEM]\n"
+          "                       [--tls-cert-file PEM --tls-key-file PEM [--tls-client-ca-file PEM]]  (/metrics over HTTPS)\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--pod-labels KEY,KEY..]\n"
           "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--ras-slices N] [--no-gzip] [--metrics-include GLOBS] [--metrics-exclude GLOBS] [--sample-threads N] [--rt-priority N] [--prewarm-ms MS]\n"
@@ -115,6 +116,9 @@ int main(int argc, char** argv) {
     else if (a == "--influx-extended") set("influx_extended", "true");
     else if (a == "--influx-schema") set("influx_schema", next());
     else if (a == "--influx-ca-file") set("influx_ca_file", next());
+    else if (a == "--tls-cert-file") set("tls_cert_file", next());
+    else if (a == "--tls-key-file") set("tls_key_file", next());
+    else if (a == "--tls-client-ca-file") set("tls_client_ca_file", next());
     else if (a == "--influx-tls-insecure") set("influx_tls_insecure", "true");
     else if (a == "--influx-client-cert") set("influx_client_cert", next());
     else if (a == "--influx-client-key") set("influx_client_key", next());
@@ -197,6 +201,12 @@ int main(int argc, char** argv) {
     const std::string perr = check_push_config(cfg.influx_url, cfg.influx_token, t);
     if (!perr.empty()) {
       fprintf(stderr, "config: %s\n", perr.c_str());
+      return 2;
+    }
+    // /metrics over HTTPS: the certificate, key and client CA must load
+    const std::string serr = check_serve_tls(cfg.tls_cert_file, cfg.tls_key_file, cfg.tls_client_ca_file);
+    if (!serr.empty()) {
+      fprintf(stderr, "config: %s\n", serr.c_str());
       return 2;
     }
   }

@@ -170,7 +170,7 @@ def _top_remote(args) -> int:
     n, rc = 0, 0
     while args.iterations <= 0 or n < args.iterations:
         t0 = time.monotonic()
-        frames, errors = fleet.fetch(urls)
+        frames, errors = fleet.fetch(urls, ca_file=args.ca_file)
         text = fleet.render(frames, errors)
         if sys.stdout.isatty():
             sys.stdout.write("\x1b[2J\x1b[H")
@@ -277,6 +277,8 @@ def build_parser() -> argparse.ArgumentParser:
     s.add_argument("--iterations", type=int, default=0)
     s.add_argument("--url", action="append", default=[],
                    help="exporter to read instead of the local GPUs (HOST:PORT or URL; repeat for a fleet view)")
+    s.add_argument("--ca-file", default="",
+                   help="https:// exporters (tls_cert_file): the PEM CA to verify them with (default: system bundle)")
     s.set_defaults(fn=cmd_top)
     s = sub.add_parser("scrape", help="measure /metrics latency")
     s.add_argument("url")

@@ -58,6 +58,9 @@ class Config:
     http_threads: int = 2
     http_rt_priority: int = 0             # SCHED_FIFO HTTP loops (CAP_SYS_NICE), each capped at http_rt_budget of a CPU
     http_rt_budget: float = 0.2           # share of a CPU per 100 ms an RT HTTP loop may use before it is demoted
+    tls_cert_file: str = ""               # /metrics over HTTPS: PEM certificate chain (with tls_key_file)
+    tls_key_file: str = ""                # ... its PEM private key
+    tls_client_ca_file: str = ""          # ... mutual TLS: scrapers must present a certificate signed by this CA
     host: str = ""
     gzip: bool = True
     compat_families: bool = True
@@ -168,6 +171,9 @@ class Config:
             "http_threads": int(self.http_threads),
             "http_rt_priority": int(self.http_rt_priority),
             "http_rt_budget": float(self.http_rt_budget),
+            "tls_cert_file": self.tls_cert_file,
+            "tls_key_file": self.tls_key_file,
+            "tls_client_ca_file": self.tls_client_ca_file,
             "host": self.resolved_host(),
             "gzip": self.gzip,
             "roctx": self.roctx,
@@ -209,6 +215,12 @@ class Config:
             err = core().check_push_config(self.influx_url, self.influx_token, self.influx_ca_file,
                                            bool(self.influx_tls_insecure), self.influx_client_cert,
                                            self.influx_client_key)
+            if err:
+                raise ConfigError(err)
+        if self.tls_cert_file or self.tls_key_file or self.tls_client_ca_file:
+            from ._native import core
+
+            err = core().check_serve_tls(self.tls_cert_file, self.tls_key_file, self.tls_client_ca_file)
             if err:
                 raise ConfigError(err)
         try:
@@ -417,6 +429,10 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--http-rt-priority", dest="http_rt_priority", type=int,
                    help="SCHED_FIFO priority of the HTTP loops (0 = normal; needs CAP_SYS_NICE)")
     p.add_argument("--http-threads", dest="http_threads", type=int, help="HTTP loop threads serving /metrics")
+    p.add_argument("--tls-cert-file", dest="tls_cert_file", help="serve /metrics over HTTPS: PEM certificate chain")
+    p.add_argument("--tls-key-file", dest="tls_key_file", help="... and its PEM private key")
+    p.add_argument("--tls-client-ca-file", dest="tls_client_ca_file",
+                   help="mutual TLS: scrapers must present a certificate signed by this PEM CA")
     p.add_argument("--prewarm-ms", dest="prewarm_ms", type=float,
                    help="device workers warm the firmware-table read this long before each tick (0 = off)")
     p.add_argument("--device-timeout", dest="device_timeout_s", type=float,

@@ -105,10 +105,12 @@ def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
     return "\n".join(lines)
 
 
-def fetch(urls: List[str], timeout_s: float = 3.0, workers: int = 16) -> Tuple[List[dict], Dict[str, str]]:
+def fetch(urls: List[str], timeout_s: float = 3.0, workers: int = 16,
+          ca_file: str = "") -> Tuple[List[dict], Dict[str, str]]:
     """GET every exporter's /metrics (native HTTP client, which releases the GIL) from up to
     `workers` threads at once, so a refresh over many nodes takes about one node's time even when
-    some of them time out; frames keep the order of `urls`. Parse failures are reported, not raised."""
+    some of them time out; frames keep the order of `urls`. Parse failures are reported, not raised.
+    https:// URLs (exporters serving TLS) are verified against `ca_file`, else the system bundle."""
     from concurrent.futures import ThreadPoolExecutor
 
     from .._native import core
@@ -116,7 +118,7 @@ def fetch(urls: List[str], timeout_s: float = 3.0, workers: int = 16) -> Tuple[L
     c = core()
 
     def one(u):
-        return c.http_request("GET", u, "", "", timeout_s)
+        return c.http_request("GET", u, "", "", timeout_s, ca_file)
 
     with ThreadPoolExecutor(max_workers=max(1, min(workers, len(urls) or 1))) as pool:
         answers = list(pool.map(one, urls))

@@ -120,7 +120,8 @@ class GpuMonitor:
             host = "127.0.0.1"  # the wildcard takes IPv4 loopback in both forms (dual-stack [::])
         elif ":" in host:
             host = f"[{host}]"
-        return f"http://{host}:{self.port}/metrics"
+        scheme = "https" if self.cfg.tls_cert_file else "http"
+        return f"{scheme}://{host}:{self.port}/metrics"
 
     def metrics(self) -> str:
         return self.ex.metrics_text()

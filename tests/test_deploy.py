@@ -408,6 +408,40 @@ def test_influx_overlay_pushes_over_verified_https(core, tmp_path):
     assert core.check_push_config(url, token="tok", ca_file=str(tmp_path / "ca.crt")) == ""
 
 
+def test_tls_overlay_serves_https_from_a_secret(core, tmp_path):
+    """overlays/tls/: the exporter terminates TLS for /metrics. The certificate and key come from a
+    Secret through GPUMON_TLS_* env. The probes switch to HTTPS, and the ServiceMonitor scrapes https
+    and verifies against the Secret's CA. The files the env names are ones the startup check accepts."""
+    import subprocess
+
+    from gpumon.config import Config
+
+    (k,) = _docs("deploy/k8s/overlays/tls/kustomization.yaml")
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"])
+    pod = _json_patch(ds, ops)["spec"]["template"]["spec"]
+    c = pod["containers"][0]
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    cfg = Config().apply_env(env)
+    assert cfg.tls_cert_file and cfg.tls_key_file
+    assert c["readinessProbe"]["httpGet"]["scheme"] == "HTTPS" and c["livenessProbe"]["httpGet"]["scheme"] == "HTTPS"
+    vols = {v["name"]: v for v in pod["volumes"]}
+    assert all(m["name"] in vols for m in c["volumeMounts"])
+    for f in (cfg.tls_cert_file, cfg.tls_key_file):
+        m = next(m for m in c["volumeMounts"] if f.startswith(m["mountPath"] + "/"))
+        assert m["readOnly"] and vols[m["name"]]["secret"]["secretName"] == "gpumon-tls"
+    sm = next(d for d in _docs("deploy/k8s/gpumon-servicemonitor.yaml") if d["kind"] == "ServiceMonitor")
+    sm_ops = yaml.safe_load(next(p for p in k["patches"] if p["target"]["kind"] == "ServiceMonitor")["patch"])
+    ep = _json_patch(sm, sm_ops)["spec"]["endpoints"][0]
+    assert ep["scheme"] == "https" and ep["tlsConfig"]["ca"]["secret"] == {"name": "gpumon-tls", "key": "ca.crt"}
+    # a Secret's files with those names pass the startup check (both entry points run it)
+    d = tmp_path
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:prime256v1", "-nodes",
+                    "-days", "1", "-keyout", str(d / "tls.key"), "-out", str(d / "tls.crt"), "-subj", "/CN=gpumon",
+                    "-addext", "subjectAltName=DNS:gpumon"], check=True, capture_output=True, timeout=60)
+    assert core.check_serve_tls(str(d / os.path.basename(cfg.tls_cert_file)), str(d / os.path.basename(cfg.tls_key_file))) == ""
+
+
 def test_serve_imports_no_oracle_or_grpc():
     """the image's `gpumon serve` (ENTRYPOINT) must not import grpcio / protobuf or
     the Python test oracles -- they live under tests/oracles and are not in the image. The package

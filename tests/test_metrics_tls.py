@@ -1,0 +1,244 @@
+"""/metrics over HTTPS (tls_cert_file / tls_key_file; tls_client_ca_file for mutual TLS).
+
+The reference had no scrape endpoint at all (push only, /root/reference/gpu.py:145). Hardened
+clusters scrape node agents over TLS: Prometheus `scheme: https` with a `tlsConfig`, sometimes with a
+client certificate. The exporter terminates TLS itself, in the same epoll loops, with the OpenSSL 3
+it already dlopens for the Influx push (csrc/core/tls.h TlsServer). Covered here:
+- a verified scrape, gzip, keep-alive, HEAD, and a body larger than the socket buffer;
+- plain HTTP against the TLS port, an untrusted scraper, a missing or wrong client certificate,
+  and a client that never finishes its handshake. Each is counted in
+  gpumon_http_tls_handshake_failures_total;
+- configuration errors at startup, in both entry points.
+"""
+
+import gzip
+import http.client
+import os
+import socket
+import ssl
+import subprocess
+import sys
+import time
+
+import pytest
+
+from gpumon.export import promtext
+from test_influx_tls import _ca, _leaf
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXPORTER = os.path.join(ROOT, "bin", "gpumon-exporter")
+
+pytestmark = pytest.mark.skipif(__import__("shutil").which("openssl") is None, reason="openssl CLI needed")
+
+
+@pytest.fixture(scope="module")
+def pki(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("mpki"))
+    _ca(d, "ca")
+    _ca(d, "clientca")
+    _ca(d, "otherca")
+    _leaf(d, "server", "ca", "DNS:localhost,IP:127.0.0.1,IP:::1")
+    _leaf(d, "scraper", "clientca", "", client=True)
+    _leaf(d, "stranger", "otherca", "", client=True)
+    p = lambda n: os.path.join(d, n)  # noqa: E731
+    return {"ca": p("ca.pem"), "clientca": p("clientca.pem"), "otherca": p("otherca.pem"), "server": p("server.pem"),
+            "server_key": p("server.key"),
+            "scraper": p("scraper.pem"), "scraper_key": p("scraper.key"), "stranger": p("stranger.pem"),
+            "stranger_key": p("stranger.key")}
+
+
+def _ctx(pki, cert=None, key=None, ca="ca"):
+    c = ssl.create_default_context(cafile=pki[ca])
+    if cert:
+        c.load_cert_chain(pki[cert], pki[key])
+    return c
+
+
+def _get(port, ctx, path="/metrics", headers=None, method="GET", conn=None):
+    c = conn or http.client.HTTPSConnection("localhost", port, context=ctx, timeout=5)
+    c.request(method, path, headers=headers or {})
+    r = c.getresponse()
+    body = r.read()
+    return r.status, dict(r.getheaders()), body, c
+
+
+def _failures(ex):
+    return promtext.one(promtext.parse(ex.metrics_text()), "gpumon_http_tls_handshake_failures_total")
+
+
+def test_verified_https_scrape_gzip_keepalive_and_head(mock_exporter, pki):
+    ex = mock_exporter(backend="mock:gpus=8", tls_cert_file=pki["server"], tls_key_file=pki["server_key"])
+    ex.tick()
+    st, h, body, c = _get(ex.port, _ctx(pki))
+    assert st == 200 and h["Content-Type"].startswith("text/plain; version=0.0.4")
+    assert int(h["Content-Length"]) == len(body) and body.decode() == ex.metrics_text()
+    # keep-alive: the next requests ride the same TLS session
+    st, h, gz, c = _get(ex.port, None, headers={"Accept-Encoding": "gzip"}, conn=c)
+    assert st == 200 and h.get("Content-Encoding") == "gzip" and gzip.decompress(gz) == body
+    st, h, b, c = _get(ex.port, None, method="HEAD", conn=c)
+    assert st == 200 and b == b"" and int(h["Content-Length"]) == len(body)
+    st, _, b, c = _get(ex.port, None, path="/healthz", conn=c)
+    assert st == 200 and b == b"ok\n"
+    c.close()
+    assert ex.self_stats()["http_tls_failures"] == 0
+    ex.tick()
+    assert _failures(ex) == 0
+
+
+def test_response_larger_than_the_socket_buffer(core, pki, monkeypatch):
+    """An 8-GPU exposition through a 4 KiB send buffer and a reader that stalls: the response goes
+    out record by record, resumed from the loop's offset on each EPOLLOUT (partial-write mode)."""
+    monkeypatch.setenv("GPUMON_HTTP_SNDBUF", "4096")
+    ex = core.Exporter({"backend": "mock:gpus=8", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                        "http_threads": 1, "gzip": False, "tls_cert_file": pki["server"],
+                        "tls_key_file": pki["server_key"]})
+    ex.start()
+    try:
+        want = ex.metrics_text().encode()
+        assert len(want) > 64 * 1024
+        raw = socket.create_connection(("127.0.0.1", ex.port))
+        raw.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+        s = _ctx(pki).wrap_socket(raw, server_hostname="localhost")
+        s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n")
+        time.sleep(0.3)  # let the server fill the small buffers and wait on EPOLLOUT
+        data = b""
+        while b"\r\n\r\n" not in data or len(data) < data.index(b"\r\n\r\n") + 4 + len(want):
+            chunk = s.recv(65536)
+            assert chunk, len(data)
+            data += chunk
+        assert data.split(b"\r\n\r\n", 1)[1] == want
+        s.close()
+    finally:
+        ex.stop()
+
+
+@pytest.mark.parametrize("case", ["plain_http", "untrusted_scraper", "silent_client"])
+def test_failed_handshakes_are_counted_and_closed(core, pki, case, monkeypatch):
+    monkeypatch.setenv("GPUMON_HTTP_HEADER_TIMEOUT_S", "0.5")
+    ex = core.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                        "http_threads": 1, "tls_cert_file": pki["server"], "tls_key_file": pki["server_key"]})
+    ex.start()
+    try:
+        if case == "plain_http":
+            s = socket.create_connection(("127.0.0.1", ex.port), timeout=5)
+            s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n")
+            try:
+                got = s.recv(4096)  # a TLS alert or nothing, then the close -- never an HTTP answer
+            except ConnectionResetError:  # closed with the request unread: a reset
+                got = b""
+            assert not got.startswith(b"HTTP/")
+            s.close()
+        elif case == "untrusted_scraper":
+            with pytest.raises(ssl.SSLError):
+                _get(ex.port, _ctx(pki, ca="otherca"))
+        else:
+            s = socket.create_connection(("127.0.0.1", ex.port), timeout=5)
+            deadline = time.time() + 5
+            s.settimeout(0.2)
+            closed = False
+            while time.time() < deadline and not closed:
+                try:
+                    closed = s.recv(1) == b""
+                except socket.timeout:
+                    pass
+                except ConnectionResetError:
+                    closed = True
+            assert closed, "a client that never sends its ClientHello must not hold a slot"
+            s.close()
+        deadline = time.time() + 5
+        while ex.self_stats()["http_tls_failures"] < 1 and time.time() < deadline:
+            time.sleep(0.05)
+        assert ex.self_stats()["http_tls_failures"] == 1
+        # the server still serves a good scraper afterwards
+        assert _get(ex.port, _ctx(pki))[0] == 200
+    finally:
+        ex.stop()
+
+
+def test_mutual_tls_requires_a_client_certificate_from_the_ca(core, pki):
+    ex = core.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                        "http_threads": 1, "tls_cert_file": pki["server"], "tls_key_file": pki["server_key"],
+                        "tls_client_ca_file": pki["clientca"]})
+    ex.start()
+    try:
+        assert _get(ex.port, _ctx(pki, "scraper", "scraper_key"))[0] == 200
+        for cert in (None, "stranger"):
+            # TLS 1.3: the server's refusal may only surface on the first read, as an alert or a reset
+            with pytest.raises((ssl.SSLError, ConnectionResetError, http.client.RemoteDisconnected)):
+                _get(ex.port, _ctx(pki, cert, f"{cert}_key") if cert else _ctx(pki))
+        deadline = time.time() + 5
+        while ex.self_stats()["http_tls_failures"] < 2 and time.time() < deadline:
+            time.sleep(0.05)
+        assert ex.self_stats()["http_tls_failures"] == 2
+    finally:
+        ex.stop()
+
+
+def test_plain_exporter_has_no_tls_family(mock_exporter):
+    ex = mock_exporter()
+    ex.tick()
+    assert "gpumon_http_tls_handshake_failures_total" not in ex.metrics_text()
+    assert ex.self_stats()["http_tls_failures"] == -1
+
+
+@pytest.mark.parametrize("over,want", [
+    ({"tls_cert_file": "CERT"}, "tls_cert_file and tls_key_file go together"),
+    ({"tls_client_ca_file": "CA"}, "tls_client_ca_file needs tls_cert_file and tls_key_file"),
+    ({"tls_cert_file": "CERT", "tls_key_file": "/nonexistent/key.pem"}, "cannot read /nonexistent/key.pem"),
+    ({"tls_cert_file": "CERT", "tls_key_file": "OTHERKEY"}, "does not match the certificate"),
+    ({"tls_cert_file": "JUNK", "tls_key_file": "KEY"}, "cannot load certificate"),
+])
+def test_bad_tls_files_fail_at_startup(core, pki, tmp_path, over, want):
+    junk = tmp_path / "junk.pem"
+    junk.write_text("not a certificate\n")
+    sub = {"CERT": pki["server"], "KEY": pki["server_key"], "CA": pki["clientca"], "OTHERKEY": pki["scraper_key"],
+           "JUNK": str(junk)}
+    cfg = {k: sub.get(v, v) for k, v in over.items()}
+    assert want in core.check_serve_tls(cfg.get("tls_cert_file", ""), cfg.get("tls_key_file", ""),
+                                        cfg.get("tls_client_ca_file", ""))
+    ex = core.Exporter(dict({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0}, **cfg))
+    with pytest.raises(RuntimeError, match=want):
+        ex.start()
+    ex.stop()
+
+
+@pytest.mark.parametrize("entry", ["native", "python"])
+def test_entry_points_serve_https_and_refuse_bad_files(entry, pki):
+    base = [EXPORTER] if entry == "native" else [sys.executable, "-m", "gpumon", "serve", "--control-plane", "off"]
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run(base + ["--backend", "mock:gpus=1", "--listen", "127.0.0.1:0", "--tls-cert-file", pki["server"]],
+                       capture_output=True, text=True, timeout=60, cwd=ROOT, env=env)
+    assert r.returncode == 2 and "tls_cert_file and tls_key_file go together" in r.stderr, (r.returncode, r.stderr)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    p = subprocess.Popen(base + ["--backend", "mock:gpus=2", "--interval", "0.2", "--listen", f"127.0.0.1:{port}",
+                                 "--tls-cert-file", pki["server"], "--tls-key-file", pki["server_key"]],
+                         cwd=ROOT, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    try:
+        deadline = time.time() + 30
+        while True:
+            try:
+                st, _, body, c = _get(port, _ctx(pki))
+                c.close()
+                break
+            except (OSError, ssl.SSLError):
+                assert time.time() < deadline and p.poll() is None, p.stderr.read().decode()[-2000:] if p.poll() else ""
+                time.sleep(0.1)
+        assert st == 200 and b"node_gpu_gpu_util{" in body
+    finally:
+        p.terminate()
+        p.wait(10)
+
+
+def test_fleet_view_reads_https_exporters(mock_exporter, pki):
+    """`gpumon top --url https://... --ca-file` over an exporter serving TLS."""
+    from gpumon.export import fleet
+
+    ex = mock_exporter(tls_cert_file=pki["server"], tls_key_file=pki["server_key"])
+    ex.tick()
+    frames, errors = fleet.fetch([f"https://localhost:{ex.port}/metrics"], ca_file=pki["ca"])
+    assert not errors and len(fleet.gpu_rows(frames[0])) == 2
+    frames, errors = fleet.fetch([f"https://localhost:{ex.port}/metrics"], ca_file=pki["otherca"])
+    assert not frames and "certificate verify failed" in next(iter(errors.values()))

@@ -31,8 +31,10 @@ def _free_port():
     return p
 
 
-def _run(binary, env_extra, extra_args=(), min_s=0.0):
-    port = _free_port()
+def _run(binary, env_extra, extra_args=(), min_s=0.0, ctx=None, port=None):
+    """ctx: an ssl.SSLContext to scrape over HTTPS (the exporter started with --tls-cert-file)."""
+    port = port or _free_port()
+    base = f"https://localhost:{port}" if ctx else f"http://127.0.0.1:{port}"
     t_start = time.time()
     env = dict(os.environ, **env_extra)
     p = subprocess.Popen([binary, "--backend", "mock:gpus=4", "--interval", "0.01", "--listen", f"127.0.0.1:{port}",
@@ -42,7 +44,7 @@ def _run(binary, env_extra, extra_args=(), min_s=0.0):
         deadline = time.time() + 30
         while time.time() < deadline:
             try:
-                urllib.request.urlopen(f"http://127.0.0.1:{port}/healthz", timeout=1).read()
+                urllib.request.urlopen(f"{base}/healthz", timeout=1, context=ctx).read()
                 break
             except OSError:
                 time.sleep(0.1)
@@ -51,9 +53,8 @@ def _run(binary, env_extra, extra_args=(), min_s=0.0):
         def hammer(query):
             for _ in range(60):
                 try:
-                    req = urllib.request.Request(f"http://127.0.0.1:{port}/metrics{query}",
-                                                 headers={"Accept-Encoding": "gzip"})
-                    urllib.request.urlopen(req, timeout=5).read()
+                    req = urllib.request.Request(f"{base}/metrics{query}", headers={"Accept-Encoding": "gzip"})
+                    urllib.request.urlopen(req, timeout=5, context=ctx).read()
                 except Exception as e:  # noqa: BLE001
                     errors.append(e)
 
@@ -419,6 +420,60 @@ def test_sanitized_connection_flood_and_eviction(target, binary, env):
     bad = _reports(err)
     assert not bad, err[-4000:]
     assert got >= 6, got
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_https_serving(target, binary, env, tmp_path):
+    """/metrics over HTTPS (csrc/core/tls.cpp TlsServer, the TLS branch of the HTTP loops) under
+    ASan+UBSan and TSan: two loops serving concurrent verified scrapes and per-request filters over
+    TLS, plus failed handshakes (plain HTTP and an untrusted scraper) mixed in. No sanitizer report."""
+    import ssl
+
+    from conftest import make_locked
+    from test_influx_tls import _ca, _leaf
+
+    make_locked(target, jobs=8)
+    d = str(tmp_path)
+    _ca(d, "ca")
+    _ca(d, "otherca")
+    _leaf(d, "server", "ca", "DNS:localhost,IP:127.0.0.1")
+    ctx = ssl.create_default_context(cafile=f"{d}/ca.pem")
+    bad_ctx = ssl.create_default_context(cafile=f"{d}/otherca.pem")
+    stop = threading.Event()
+    port = _free_port()
+
+    def intruders():  # handshake failures while the good scrapes run
+        while not stop.is_set():
+            for c in (None, bad_ctx):
+                try:
+                    if c is None:  # plain HTTP against the TLS port
+                        s = socket.create_connection(("127.0.0.1", port), timeout=1)
+                        s.sendall(b"GET /metrics HTTP/1.1\r\n\r\n")
+                        s.recv(100)
+                        s.close()
+                    else:  # a scraper that does not trust the certificate
+                        urllib.request.urlopen(f"https://localhost:{port}/metrics", timeout=1, context=c)
+                except Exception:  # noqa: BLE001 -- refused by design
+                    pass
+            time.sleep(0.02)
+
+    t = threading.Thread(target=intruders, daemon=True)
+    t.start()
+    try:
+        rc, err = _run(os.path.join(ROOT, binary), dict(env), ("--tls-cert-file", f"{d}/server.pem",
+                                                               "--tls-key-file", f"{d}/server.key"), min_s=1.0, ctx=ctx,
+                       port=port)
+    finally:
+        stop.set()
+        t.join(5)
+    bad = _reports(err)
+    assert not bad, err[-4000:]
+    assert rc == 0, err[-2000:]
 
 
 @pytest.mark.slow

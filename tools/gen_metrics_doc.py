@@ -153,6 +153,21 @@ def collect():
     ex.tick()
     add(_families(ex), "gzip scrapes")
     ex.stop()
+    # /metrics over HTTPS (tls_cert_file): the handshake-failure counter; a throwaway certificate
+    import shutil
+    import subprocess
+
+    if shutil.which("openssl"):
+        with tempfile.TemporaryDirectory() as d:
+            subprocess.run(["openssl", "req", "-x509", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:prime256v1",
+                            "-nodes", "-days", "1", "-keyout", f"{d}/k.pem", "-out", f"{d}/c.pem", "-subj", "/CN=node"],
+                           check=True, capture_output=True, timeout=60)
+            ex = c.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                             "host": "node", "tls_cert_file": f"{d}/c.pem", "tls_key_file": f"{d}/k.pem"})
+            ex.start()
+            ex.tick()
+            add(_families(ex), "tls_cert_file")
+            ex.stop()
     # backend-specific self-metrics: the libamd_smi backend over the fake library
     saved = os.environ.get("FAKE_AMDSMI_GPUS")  # the fake reads it at init; leave the caller's env as it was
     os.environ["FAKE_AMDSMI_GPUS"] = "1"
