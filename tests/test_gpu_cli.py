@@ -276,3 +276,71 @@ def test_native_binary_pushes_over_https_and_listens_dual_stack(tmp_path):
     assert promtext.one(fam, "gpumon_influx_up") == 1
     if text6 is not None:
         assert "node_gpu_gpu_util{" in text6
+
+
+def test_native_binary_serves_metrics_over_https(tmp_path):
+    """`gpumon-exporter --backend amdsmi --tls-cert-file ... --tls-key-file ...` on MI355X: a verified
+    HTTPS scrape (identity and gzip, one keep-alive session) carries the GPU's real HBM total, and a
+    plain-HTTP request to the same port is counted as a failed handshake."""
+    import gzip
+    import http.client
+    import shutil
+    import signal
+    import socket
+    import ssl
+    import time
+
+    if shutil.which("openssl") is None:
+        pytest.skip("openssl CLI needed for test certificates")
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_influx_tls import _ca, _leaf
+
+    d = str(tmp_path)
+    _ca(d, "ca")
+    _leaf(d, "server", "ca", "DNS:localhost,IP:127.0.0.1")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.Popen([os.path.join(root, "bin", "gpumon-exporter"), "--backend", "amdsmi", "--interval", "0.2",
+                          "--listen", f"127.0.0.1:{port}", "--no-pod-resources", "--no-cri", "--log-level", "warn",
+                          "--tls-cert-file", f"{d}/server.pem", "--tls-key-file", f"{d}/server.key"],
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    ctx = ssl.create_default_context(cafile=f"{d}/ca.pem")
+    try:
+        deadline = time.time() + 60
+        while True:
+            try:
+                c = http.client.HTTPSConnection("localhost", port, context=ctx, timeout=5)
+                c.request("GET", "/metrics")
+                text = c.getresponse().read().decode()
+                break
+            except (OSError, ssl.SSLError):
+                assert time.time() < deadline and p.poll() is None
+                time.sleep(0.2)
+        c.request("GET", "/metrics", headers={"Accept-Encoding": "gzip"})
+        r = c.getresponse()
+        assert r.getheader("Content-Encoding") == "gzip"
+        gz_text = gzip.decompress(r.read()).decode()
+        c.close()
+        raw = socket.create_connection(("127.0.0.1", port), timeout=5)
+        raw.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n")
+        try:
+            assert not raw.recv(100).startswith(b"HTTP/")
+        except ConnectionResetError:
+            pass
+        raw.close()
+        time.sleep(0.5)
+        c = http.client.HTTPSConnection("localhost", port, context=ctx, timeout=5)
+        c.request("GET", "/metrics")
+        last = c.getresponse().read().decode()
+        c.close()
+    finally:
+        p.send_signal(signal.SIGTERM)
+        _, err = p.communicate(timeout=30)
+    assert p.returncode == 0, err[-2000:]
+    for t in (text, gz_text):
+        fam = promtext.parse(t)
+        assert promtext.one(fam, "node_gpu_mem_total", gpu_id="0") == 294896  # MiB of HBM3E, from the device
+    assert promtext.one(promtext.parse(last), "gpumon_http_tls_handshake_failures_total") >= 1
