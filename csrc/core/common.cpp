@@ -2,6 +2,7 @@
 #include "common.h"
 
 #include <pthread.h>
+#include <signal.h>
 
 #include <fcntl.h>
 #include <unistd.h>
@@ -13,6 +14,13 @@
 namespace gpumon {
 
 void set_thread_name(const std::string& name) { pthread_setname_np(pthread_self(), name.substr(0, 15).c_str()); }
+
+void block_sigpipe() {
+  sigset_t s;
+  sigemptyset(&s);
+  sigaddset(&s, SIGPIPE);
+  pthread_sigmask(SIG_BLOCK, &s, nullptr);
+}
 
 std::atomic<int> g_log_level{static_cast<int>(LogLevel::kInfo)};
 

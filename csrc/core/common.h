@@ -37,6 +37,12 @@ void log_line(LogLevel lvl, const char* component, const std::string& msg);
 // Names the calling thread (<= 15 chars) so per-thread CPU is attributable in /proc/<pid>/task,
 // top -H and perf (tools/thread_cpu.py).
 void set_thread_name(const std::string& name);
+// Blocks SIGPIPE on the calling thread. OpenSSL writes to its sockets with write(), which has no
+// MSG_NOSIGNAL: on a connection the peer has reset, a second write would raise SIGPIPE and, in a host
+// process that has not ignored it (an embedding service; CPython and the native binary do ignore
+// it), end the process. Blocked, the write fails with EPIPE and the signal stays pending on this
+// thread, where it is never delivered.
+void block_sigpipe();
 
 #define GPUMON_LOG(lvl, comp, msg)                                              \
   do {                                                                          \

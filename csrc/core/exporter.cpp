@@ -839,6 +839,7 @@ TlsOptions Exporter::influx_tls() const {
 }
 
 void Exporter::influx_loop() {
+  block_sigpipe();  // an https push writes through OpenSSL's write() (common.h)
   // URL, token and TLS settings were checked by start() (check_push_config)
   const Url u = parse_url(cfg_.influx_url);
   HttpClient client(cfg_.influx_timeout_s);

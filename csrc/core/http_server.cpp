@@ -364,6 +364,7 @@ bool HttpServer::start(std::string* err) {
     Loop* p = L.get();
     p->th = std::thread([this, p] {
       set_thread_name("gpumon-http");
+      block_sigpipe();  // TLS sessions write with write() (common.h)
       run(p);
     });
   }

@@ -242,3 +242,38 @@ def test_fleet_view_reads_https_exporters(mock_exporter, pki):
     assert not errors and len(fleet.gpu_rows(frames[0])) == 2
     frames, errors = fleet.fetch([f"https://localhost:{ex.port}/metrics"], ca_file=pki["otherca"])
     assert not frames and "certificate verify failed" in next(iter(errors.values()))
+
+
+def test_host_process_without_sigpipe_handling_survives_resets(pki, tmp_path):
+    """The exporter embedded in a process that leaves SIGPIPE at its default (fatal) action: TLS
+    scrapers that reset the connection mid-response, and Connection: close scrapers that reset
+    before the server's close_notify, must not kill it. OpenSSL writes with write(), which has no
+    MSG_NOSIGNAL; the HTTP loops block SIGPIPE (common.h block_sigpipe)."""
+    script = tmp_path / "host.py"
+    script.write_text(f'''
+import os, signal, socket, ssl, struct, sys, time
+sys.path.insert(0, {ROOT!r})
+signal.signal(signal.SIGPIPE, signal.SIG_DFL)
+os.environ["GPUMON_HTTP_SNDBUF"] = "4096"
+from gpumon import core
+ex = core().Exporter({{"backend": "mock:gpus=8", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                      "http_threads": 2, "gzip": False, "tls_cert_file": {pki["server"]!r},
+                      "tls_key_file": {pki["server_key"]!r}}})
+ex.start()
+ctx = ssl.create_default_context(cafile={pki["ca"]!r})
+for i in range(60):
+    raw = socket.create_connection(("127.0.0.1", ex.port))
+    raw.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+    s = ctx.wrap_socket(raw, server_hostname="localhost")
+    close = b"Connection: close\\r\\n" if i % 2 else b""
+    s.sendall(b"GET /metrics HTTP/1.1\\r\\nHost: x\\r\\n" + close + b"\\r\\n")
+    if i % 3 == 0:
+        s.recv(100)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+    s.close()
+time.sleep(0.5)
+ex.stop()
+print("alive")
+''')
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "alive" in r.stdout, (r.returncode, r.stderr[-2000:])
