@@ -138,6 +138,11 @@ std::string compat_user_from_pod(const std::string& pod, const std::string& pref
 }
 
 Attributor::Attributor(AttributionConfig cfg) : cfg_(std::move(cfg)) {
+  // A real procfs has per-thread directories: the leader thread's stat (task/<pid>/stat) carries
+  // the same comm and starttime as the process's, without summing the CPU times of every thread
+  // (a PyTorch tenant runs dozens; ~8 vs ~3.5 us per read with 200 threads). A fake tree in the
+  // tests has <pid>/stat only.
+  task_stat_ = access((cfg_.procfs_root + "/self/task").c_str(), R_OK) == 0;
   if (!cfg_.user_regex.empty()) {
     try {
       user_re_ = std::make_unique<std::regex>(cfg_.user_regex, std::regex::ECMAScript);
@@ -204,7 +209,8 @@ size_t Attributor::meta_size() const {
 
 bool Attributor::read_stat(uint32_t pid, uint64_t* starttime, std::string* comm) const {
   std::string s;
-  if (!read_file(cfg_.procfs_root + "/" + std::to_string(pid) + "/stat", &s, 4096)) return false;
+  const std::string ps = std::to_string(pid);
+  if (!read_file(cfg_.procfs_root + "/" + ps + (task_stat_ ? "/task/" + ps + "/stat" : "/stat"), &s, 4096)) return false;
   // pid (comm) state ppid ... ; comm may contain spaces/parens: use the LAST ')'
   size_t lp = s.find('('), rp = s.rfind(')');
   if (lp == std::string::npos || rp == std::string::npos || rp < lp) return false;

@@ -140,6 +140,7 @@ class Attributor {
   uint64_t hits_ = 0, misses_ = 0;
 
   bool read_stat(uint32_t pid, uint64_t* starttime, std::string* comm) const;
+  bool task_stat_ = false;  // read the leader thread's stat (procfs_root has task/ dirs)
   void read_env_fallback(uint32_t pid, CacheEntry* e) const;
 };
 

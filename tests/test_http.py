@@ -674,16 +674,17 @@ def test_connection_flood_under_a_low_fd_limit(tmp_path):
         assert p.poll() is None
         assert open_fds <= 64, open_fds
         assert burn < 0.5, burn  # a spinning loop would burn a whole CPU
-    finally:
         for c in conns:
             c.close()
-    try:
+        conns.clear()
         time.sleep(0.3)
         t1 = ticks()
         time.sleep(0.3)
         assert ticks() > t1  # still sampling, and /metrics answers
     finally:
-        p.terminate()
+        for c in conns:
+            c.close()
+        p.terminate()  # also when an assertion above failed: no exporter left behind
         p.wait(10)
 
 
