@@ -1011,7 +1011,12 @@ SelfStats Exporter::self_stats() const {
   if (server_) {
     s.http_evicted = static_cast<int64_t>(server_->evicted());
     s.http_max_conns = static_cast<int64_t>(server_->max_conns() * static_cast<size_t>(std::max(1, cfg_.http_threads)));
-    if (server_->tls()) s.http_tls_failures = static_cast<int64_t>(server_->tls_failures());
+    if (const TlsServer* t = server_->tls_server()) {
+      s.http_tls_failures = static_cast<int64_t>(server_->tls_failures());
+      s.http_tls_not_after = t->not_after();
+      s.http_tls_reloads_ok = t->reloads_ok();
+      s.http_tls_reloads_failed = t->reloads_failed();
+    }
   }
   if (cfg_.http_rt_priority > 0 && server_) {
     s.http_rt_loops = server_->rt_loops();

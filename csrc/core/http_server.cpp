@@ -824,6 +824,7 @@ void HttpServer::run(Loop* L) {
     }
     if (now - last_sweep > 1000000000LL) {
       last_sweep = now;
+      if (tls_ && L == loops_.front().get()) tls_->maybe_reload(now);  // certificate rotation
       std::vector<int> idle;
       for (auto& [fd, c] : L->conns)
         if (now - c.last_ns > kIdleTimeoutNs || (c.closing && now - c.closing_ns > kLingerNs) ||

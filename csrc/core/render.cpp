@@ -860,6 +860,21 @@ void render_prometheus(const RenderInput& in, std::string* o) {
                "counter");
       f.add(hl, static_cast<double>(s.http_tls_failures));
     }
+    if (s.http_tls_failures >= 0) {
+      {
+        Family f(o, "gpumon_http_tls_cert_not_after_timestamp_seconds",
+                 "Expiry (unix seconds) of the certificate /metrics is served with; rotated files are picked up "
+                 "within 5 s (gpumon_http_tls_reloads_total).",
+                 "gauge");
+        if (s.http_tls_not_after > 0) f.add(hl, static_cast<double>(s.http_tls_not_after));
+      }
+      Family f(o, "gpumon_http_tls_reloads_total",
+               "Changes of tls_cert_file / tls_key_file / tls_client_ca_file seen: result=ok swapped in for new "
+               "connections, result=error did not load (the previous certificate stays in use).",
+               "counter");
+      f.add(hl, {{"result", "ok"}}, static_cast<double>(s.http_tls_reloads_ok));
+      f.add(hl, {{"result", "error"}}, static_cast<double>(s.http_tls_reloads_failed));
+    }
     if (s.http_rt_loops >= 0) {
       {
         Family f(o, "gpumon_http_rt_loops",

@@ -71,6 +71,8 @@ struct SelfStats {
   int64_t http_evicted = -1;         // connections closed to make room at the cap (-1: no server)
   int64_t http_max_conns = -1;       // connection cap over all HTTP loops (from RLIMIT_NOFILE)
   int64_t http_tls_failures = -1;    // /metrics over HTTPS: failed / timed-out handshakes (-1: plain HTTP)
+  int64_t http_tls_not_after = 0;     // ... the serving certificate's expiry (unix s; 0 unknown)
+  uint64_t http_tls_reloads_ok = 0, http_tls_reloads_failed = 0;  // ... certificate rotations picked up / refused
   int64_t http_rt_demotions = -1;    // ... times a loop spent its CPU budget and was demoted
   uint64_t overruns = 0;
   double last_tick_wall_s = 0;

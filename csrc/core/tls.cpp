@@ -4,6 +4,7 @@
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <poll.h>
+#include <sys/stat.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -12,6 +13,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <initializer_list>
 #include <mutex>
 
@@ -47,6 +49,9 @@ struct SslApi {
   int (*SSL_CTX_set_num_tickets)(void*, size_t) = nullptr;
   void (*SSL_set_accept_state)(void*) = nullptr;
   int (*SSL_do_handshake)(void*) = nullptr;
+  void* (*SSL_CTX_get0_certificate)(const void*) = nullptr;
+  const void* (*X509_get0_notAfter)(const void*) = nullptr;
+  int (*ASN1_TIME_to_tm)(const void*, struct tm*) = nullptr;
   void* (*SSL_CTX_new)(const void*) = nullptr;
   void (*SSL_CTX_free)(void*) = nullptr;
   long (*SSL_CTX_ctrl)(void*, int, long, void*) = nullptr;
@@ -127,6 +132,9 @@ void load_api() {
   sym(s, "SSL_CTX_set_num_tickets", &a->SSL_CTX_set_num_tickets, &missing);
   sym(s, "SSL_set_accept_state", &a->SSL_set_accept_state, &missing);
   sym(s, "SSL_do_handshake", &a->SSL_do_handshake, &missing);
+  sym(s, "SSL_CTX_get0_certificate", &a->SSL_CTX_get0_certificate, &missing);
+  sym(c, "X509_get0_notAfter", &a->X509_get0_notAfter, &missing);
+  sym(c, "ASN1_TIME_to_tm", &a->ASN1_TIME_to_tm, &missing);
   sym(s, "SSL_CTX_new", &a->SSL_CTX_new, &missing);
   sym(s, "SSL_CTX_free", &a->SSL_CTX_free, &missing);
   sym(s, "SSL_CTX_ctrl", &a->SSL_CTX_ctrl, &missing);
@@ -399,6 +407,66 @@ void TlsConn::shutdown() {
   }
 }
 
+namespace {
+
+// One server context from the files (nullptr with *err); *not_after = the leaf certificate's expiry.
+void* build_server_ctx(const SslApi* a, const std::string& cert_file, const std::string& key_file,
+                       const std::string& client_ca_file, int64_t* not_after, std::string* err) {
+  for (const std::string* f : {&cert_file, &key_file, &client_ca_file})
+    if (!f->empty() && access(f->c_str(), R_OK) != 0) {
+      *err = "cannot read " + *f + ": " + strerror(errno);
+      return nullptr;
+    }
+  a->ERR_clear_error();
+  void* ctx = a->SSL_CTX_new(a->TLS_server_method());
+  if (!ctx) {
+    *err = "tls: SSL_CTX_new: " + err_queue(a);
+    return nullptr;
+  }
+  auto fail = [&](std::string why) -> void* {
+    *err = std::move(why);
+    a->SSL_CTX_free(ctx);
+    return nullptr;
+  };
+  a->SSL_CTX_ctrl(ctx, ossl::kCtrlSetMinProtoVersion, ossl::kTls12Version, nullptr);
+  // partial writes: a response larger than the socket buffer goes out record by record, resumed
+  // from the loop's offset on the next EPOLLOUT
+  a->SSL_CTX_ctrl(ctx, ossl::kCtrlMode, ossl::kModeEnablePartialWrite | ossl::kModeAcceptMovingWriteBuffer, nullptr);
+  a->SSL_CTX_ctrl(ctx, ossl::kCtrlSetSessCacheMode, ossl::kSessCacheOff, nullptr);
+  a->SSL_CTX_set_num_tickets(ctx, 0);
+  static const unsigned char kSid[] = "gpumon";
+  a->SSL_CTX_set_session_id_context(ctx, kSid, sizeof kSid - 1);
+  if (a->SSL_CTX_use_certificate_chain_file(ctx, cert_file.c_str()) != 1)
+    return fail("tls: cannot load certificate " + cert_file + ": " + err_queue(a));
+  if (a->SSL_CTX_use_PrivateKey_file(ctx, key_file.c_str(), ossl::kFiletypePem) != 1 ||
+      a->SSL_CTX_check_private_key(ctx) != 1)
+    return fail("tls: cannot load key " + key_file + " (or it does not match the certificate): " + err_queue(a));
+  if (!client_ca_file.empty()) {
+    if (a->SSL_CTX_load_verify_locations(ctx, client_ca_file.c_str(), nullptr) != 1)
+      return fail("tls: cannot load client CA " + client_ca_file + ": " + err_queue(a));
+    a->SSL_CTX_set_verify(ctx, ossl::kVerifyPeer | ossl::kVerifyFailIfNoPeerCert, nullptr);
+  }
+  *not_after = 0;
+  if (const void* x = a->SSL_CTX_get0_certificate(ctx)) {
+    struct tm t {};
+    if (const void* na = a->X509_get0_notAfter(x); na && a->ASN1_TIME_to_tm(na, &t) == 1) *not_after = timegm(&t);
+  }
+  a->ERR_clear_error();
+  return ctx;
+}
+
+}  // namespace
+
+TlsServer::Stamp TlsServer::stamp(const std::string& path) {
+  Stamp s;
+  struct stat st {};
+  if (path.empty() || ::stat(path.c_str(), &st) != 0) return s;  // follows the kubelet's ..data symlink
+  s.mtime_ns = static_cast<int64_t>(st.st_mtim.tv_sec) * 1000000000LL + st.st_mtim.tv_nsec;
+  s.size = static_cast<int64_t>(st.st_size);
+  s.ino = static_cast<uint64_t>(st.st_ino);
+  return s;
+}
+
 std::shared_ptr<TlsServer> TlsServer::create(const std::string& cert_file, const std::string& key_file,
                                              const std::string& client_ca_file, std::string* err) {
   if (cert_file.empty() && key_file.empty() && !client_ca_file.empty()) {
@@ -409,47 +477,48 @@ std::shared_ptr<TlsServer> TlsServer::create(const std::string& cert_file, const
     *err = "tls_cert_file and tls_key_file go together";
     return nullptr;
   }
-  for (const std::string* f : {&cert_file, &key_file, &client_ca_file})
-    if (!f->empty() && access(f->c_str(), R_OK) != 0) {
-      *err = "cannot read " + *f + ": " + strerror(errno);
-      return nullptr;
-    }
   const SslApi* a = ssl_api(err);
   if (!a) return nullptr;
   std::shared_ptr<TlsServer> t(new TlsServer);
   t->api_ = a;
-  a->ERR_clear_error();
-  t->ctx_ = a->SSL_CTX_new(a->TLS_server_method());
-  if (!t->ctx_) {
-    *err = "tls: SSL_CTX_new: " + err_queue(a);
-    return nullptr;
-  }
-  a->SSL_CTX_ctrl(t->ctx_, ossl::kCtrlSetMinProtoVersion, ossl::kTls12Version, nullptr);
-  // partial writes: a response larger than the socket buffer goes out record by record, resumed
-  // from the loop's offset on the next EPOLLOUT
-  a->SSL_CTX_ctrl(t->ctx_, ossl::kCtrlMode, ossl::kModeEnablePartialWrite | ossl::kModeAcceptMovingWriteBuffer, nullptr);
-  a->SSL_CTX_ctrl(t->ctx_, ossl::kCtrlSetSessCacheMode, ossl::kSessCacheOff, nullptr);
-  a->SSL_CTX_set_num_tickets(t->ctx_, 0);
-  static const unsigned char kSid[] = "gpumon";
-  a->SSL_CTX_set_session_id_context(t->ctx_, kSid, sizeof kSid - 1);
-  if (a->SSL_CTX_use_certificate_chain_file(t->ctx_, cert_file.c_str()) != 1) {
-    *err = "tls: cannot load certificate " + cert_file + ": " + err_queue(a);
-    return nullptr;
-  }
-  if (a->SSL_CTX_use_PrivateKey_file(t->ctx_, key_file.c_str(), ossl::kFiletypePem) != 1 ||
-      a->SSL_CTX_check_private_key(t->ctx_) != 1) {
-    *err = "tls: cannot load key " + key_file + " (or it does not match the certificate): " + err_queue(a);
-    return nullptr;
-  }
-  if (!client_ca_file.empty()) {
-    if (a->SSL_CTX_load_verify_locations(t->ctx_, client_ca_file.c_str(), nullptr) != 1) {
-      *err = "tls: cannot load client CA " + client_ca_file + ": " + err_queue(a);
-      return nullptr;
-    }
-    a->SSL_CTX_set_verify(t->ctx_, ossl::kVerifyPeer | ossl::kVerifyFailIfNoPeerCert, nullptr);
-    t->mutual_ = true;
-  }
+  t->cert_ = cert_file;
+  t->key_ = key_file;
+  t->ca_ = client_ca_file;
+  // stamped before the load: a rotation while it loads is seen as a change next time
+  t->stamps_[0] = stamp(cert_file);
+  t->stamps_[1] = stamp(key_file);
+  t->stamps_[2] = stamp(client_ca_file);
+  int64_t na = 0;
+  t->ctx_ = build_server_ctx(a, cert_file, key_file, client_ca_file, &na, err);
+  if (!t->ctx_) return nullptr;
+  t->not_after_ = na;
   return t;
+}
+
+void TlsServer::maybe_reload(int64_t now_ns) {
+  if (now_ns < next_check_ns_) return;
+  next_check_ns_ = now_ns + 5'000'000'000LL;
+  const Stamp now[3] = {stamp(cert_), stamp(key_), stamp(ca_)};
+  if (now[0] == stamps_[0] && now[1] == stamps_[1] && now[2] == stamps_[2]) return;
+  for (int i = 0; i < 3; ++i) stamps_[i] = now[i];  // a broken change is retried on the next change only
+  std::string err;
+  int64_t na = 0;
+  void* fresh = build_server_ctx(api_, cert_, key_, ca_, &na, &err);
+  if (!fresh) {
+    reloads_failed_.fetch_add(1);
+    GPUMON_LOG(LogLevel::kWarn, "http", "TLS files changed but do not load (keeping the previous certificate): " + err);
+    return;
+  }
+  void* old;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    old = ctx_;
+    ctx_ = fresh;
+  }
+  api_->SSL_CTX_free(old);  // sessions made from it hold their own reference
+  not_after_ = na;
+  reloads_ok_.fetch_add(1);
+  GPUMON_LOG(LogLevel::kInfo, "http", "reloaded the TLS certificate " + cert_);
 }
 
 TlsServer::~TlsServer() {
@@ -457,7 +526,11 @@ TlsServer::~TlsServer() {
 }
 
 void* TlsServer::new_session(int fd) const {
-  void* ssl = api_->SSL_new(ctx_);
+  void* ssl;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    ssl = api_->SSL_new(ctx_);
+  }
   if (!ssl) return nullptr;
   if (api_->SSL_set_fd(ssl, fd) != 1) {
     api_->SSL_free(ssl);

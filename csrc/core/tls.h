@@ -9,8 +9,10 @@
 // `influx_ca_file` replaces the bundle, `influx_tls_insecure` (off by default) disables both.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 
 namespace gpumon {
@@ -83,7 +85,16 @@ class TlsServer {
   static std::shared_ptr<TlsServer> create(const std::string& cert_file, const std::string& key_file,
                                            const std::string& client_ca_file, std::string* err);
   ~TlsServer();
-  bool mutual() const { return mutual_; }
+  bool mutual() const { return !ca_.empty(); }
+  // Certificate rotation (cert-manager, a renewed Secret: the kubelet swaps the mounted files): at
+  // most every 5 s, the files' mtime / size / inode are compared with the loaded ones; on a change a
+  // new context is built and swapped in. New connections get it; sessions in flight keep theirs. A
+  // change that does not load (a half-written rotation) keeps the old context and is retried on the
+  // files' next change. Called by one HTTP loop.
+  void maybe_reload(int64_t now_ns);
+  int64_t not_after() const { return not_after_.load(); }  // the serving certificate's expiry (unix s; 0 unknown)
+  uint64_t reloads_ok() const { return reloads_ok_.load(); }
+  uint64_t reloads_failed() const { return reloads_failed_.load(); }
   // A session over an accepted non-blocking socket; nullptr if OpenSSL refuses one.
   void* new_session(int fd) const;
   enum class Step { kDone, kWantRead, kWantWrite, kFailed };
@@ -97,9 +108,20 @@ class TlsServer {
 
  private:
   TlsServer() = default;
+  struct Stamp {
+    int64_t mtime_ns = 0, size = -1;
+    uint64_t ino = 0;
+    bool operator==(const Stamp& o) const { return mtime_ns == o.mtime_ns && size == o.size && ino == o.ino; }
+  };
+  static Stamp stamp(const std::string& path);
   const SslApi* api_ = nullptr;
-  void* ctx_ = nullptr;  // SSL_CTX*
-  bool mutual_ = false;
+  std::string cert_, key_, ca_;
+  mutable std::mutex mu_;
+  void* ctx_ = nullptr;  // SSL_CTX*, swapped under mu_ on a reload
+  Stamp stamps_[3];
+  int64_t next_check_ns_ = 0;
+  std::atomic<int64_t> not_after_{0};
+  std::atomic<uint64_t> reloads_ok_{0}, reloads_failed_{0};
 };
 
 // Configuration-time check of the serving certificate, key and client CA: "" = usable.

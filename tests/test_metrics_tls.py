@@ -277,3 +277,66 @@ print("alive")
 ''')
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "alive" in r.stdout, (r.returncode, r.stderr[-2000:])
+
+
+def test_rotated_certificate_is_picked_up_without_a_restart(core, pki, tmp_path):
+    """cert-manager renews the Secret, the kubelet swaps the mounted files: within 5 s new connections
+    get the new certificate (its expiry exported), the reload is counted, and a rotation that does
+    not load keeps the previous certificate in use."""
+    import shutil
+    import datetime
+
+    d = tmp_path
+    ca_dir = os.path.dirname(pki["ca"])
+    # the renewed certificate: same CA and names, a later expiry
+    _openssl = lambda *a: subprocess.run(["openssl", *a], cwd=ca_dir, check=True, capture_output=True, timeout=60)  # noqa: E731
+    _openssl("req", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:prime256v1", "-nodes", "-keyout", str(d / "new.key"),
+             "-out", str(d / "new.csr"), "-subj", "/CN=server")
+    (d / "new.ext").write_text("basicConstraints=CA:FALSE\nsubjectAltName=DNS:localhost,IP:127.0.0.1\n"
+                               "extendedKeyUsage=serverAuth\n")
+    _openssl("x509", "-req", "-in", str(d / "new.csr"), "-CA", "ca.pem", "-CAkey", "ca.key", "-CAcreateserial",
+             "-days", "9", "-out", str(d / "new.pem"), "-extfile", str(d / "new.ext"))
+    live = d / "live"
+    live.mkdir()
+
+    def install(cert, key):  # the kubelet's way: write elsewhere, then rename into place
+        for src, name in ((cert, "tls.crt"), (key, "tls.key")):
+            tmp = live / (name + ".tmp")
+            shutil.copy(src, tmp)
+            os.replace(tmp, live / name)
+
+    install(pki["server"], pki["server_key"])
+    ex = core.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                        "http_threads": 2, "tls_cert_file": str(live / "tls.crt"), "tls_key_file": str(live / "tls.key")})
+    ex.start()
+    ctx = _ctx(pki)
+
+    def served_not_after():
+        with socket.create_connection(("127.0.0.1", ex.port), timeout=5) as raw:
+            with ctx.wrap_socket(raw, server_hostname="localhost") as s:
+                return ssl.cert_time_to_seconds(s.getpeercert()["notAfter"])
+
+    try:
+        first = served_not_after()
+        assert abs(ex.self_stats()["http_tls_not_after"] - first) <= 1
+        install(str(d / "new.pem"), str(d / "new.key"))
+        deadline = time.time() + 15
+        while ex.self_stats()["http_tls_reloads_ok"] < 1 and time.time() < deadline:
+            time.sleep(0.2)
+        st = ex.self_stats()
+        assert st["http_tls_reloads_ok"] == 1, st
+        renewed = served_not_after()
+        assert renewed - first > 5 * 86400 and abs(st["http_tls_not_after"] - renewed) <= 1
+        ex.tick()
+        fam = promtext.parse(ex.metrics_text())
+        assert promtext.one(fam, "gpumon_http_tls_cert_not_after_timestamp_seconds") == st["http_tls_not_after"]
+        assert promtext.one(fam, "gpumon_http_tls_reloads_total", result="ok") == 1
+        # a rotation that does not load (a key from another certificate): counted, the old one stays
+        install(pki["server"], str(d / "new.key"))
+        deadline = time.time() + 15
+        while ex.self_stats()["http_tls_reloads_failed"] < 1 and time.time() < deadline:
+            time.sleep(0.2)
+        assert ex.self_stats()["http_tls_reloads_failed"] == 1
+        assert served_not_after() == renewed
+    finally:
+        ex.stop()
