@@ -171,7 +171,13 @@ def build():
     panels.append(panel("Multi-GPU processes: peer contexts left out of pod_gpu rows (e.g. torchrun ranks opening every GPU)",
                         "timeseries",
                         [(f'gpumon_hidden_peer_gpu_contexts{{{HOST}}}', "{{host}} peer contexts"),
-                         (f'gpumon_hidden_gpu_contexts{{{HOST}}}', "{{host}} empty contexts")], 0, y, 24, 6))
+                         (f'gpumon_hidden_gpu_contexts{{{HOST}}}', "{{host}} empty contexts")], 0, y, 12, 6))
+    # where /metrics is served over HTTPS (overlays/tls): certificate lifetime, rotations, refused handshakes
+    panels.append(panel("/metrics over HTTPS: days left on the certificate, rotations, failed handshakes", "timeseries",
+                        [(f'(gpumon_http_tls_cert_not_after_timestamp_seconds{{{HOST}}} - time()) / 86400', "{{host}} days left"),
+                         (f'increase(gpumon_http_tls_reloads_total{{{HOST}}}[1h])', "{{host}} reloads {{result}} /h"),
+                         (f'rate(gpumon_http_tls_handshake_failures_total{{{HOST}}}[5m])', "{{host}} failed handshakes/s")],
+                        12, y, 12, 6))
     return {
         "title": "gpumon — MI355X GPU cluster",
         "uid": "gpumon-mi355x",
