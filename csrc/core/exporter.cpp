@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -843,9 +844,20 @@ void Exporter::influx_loop() {
   // URL, token and TLS settings were checked by start() (check_push_config)
   const Url u = parse_url(cfg_.influx_url);
   HttpClient client(cfg_.influx_timeout_s);
+  // the CA bundle and the client certificate / key rotate too (cert-manager): their files are
+  // re-stamped every 30 s; a changed set is loaded and the connection reopened with it (a set that
+  // does not load keeps the previous context and connection)
+  const TlsOptions topt = influx_tls();
+  auto stamps = [&] {
+    return std::array<FileStamp, 3>{FileStamp::of(topt.ca_file), FileStamp::of(topt.client_cert),
+                                    FileStamp::of(topt.client_key)};
+  };
+  std::array<FileStamp, 3> tls_stamps = stamps();
+  const int64_t tls_period = tls_reload_period_ns(30'000'000'000LL);
+  int64_t tls_check_at = mono_ns() + tls_period;
   if (u.tls) {
     std::string terr;
-    auto ctx = TlsContext::create(influx_tls(), &terr);
+    auto ctx = TlsContext::create(topt, &terr);
     if (!ctx) {  // checked at start: only a CA file removed since then lands here
       GPUMON_LOG(LogLevel::kError, "influx", "push disabled: " + terr);
       return;
@@ -878,6 +890,20 @@ void Exporter::influx_loop() {
       if (push_q_.empty() || mono_ns() < retry_at) continue;
       body = std::move(push_q_.front());
       push_q_.pop_front();
+    }
+    if (u.tls && mono_ns() >= tls_check_at) {
+      tls_check_at = mono_ns() + tls_period;
+      if (const auto now = stamps(); now != tls_stamps) {
+        tls_stamps = now;
+        std::string terr;
+        if (auto ctx = TlsContext::create(topt, &terr)) {
+          client.set_tls(std::move(ctx));
+          client.close_conn();  // the next push handshakes with the new files
+          GPUMON_LOG(LogLevel::kInfo, "influx", "reloaded the push's TLS files");
+        } else {
+          GPUMON_LOG(LogLevel::kWarn, "influx", "the push's TLS files changed but do not load (keeping the previous ones): " + terr);
+        }
+      }
     }
     std::string err, resp;
     int st = client.request("POST", u, body, headers, &resp, &err);

@@ -457,8 +457,13 @@ void* build_server_ctx(const SslApi* a, const std::string& cert_file, const std:
 
 }  // namespace
 
-TlsServer::Stamp TlsServer::stamp(const std::string& path) {
-  Stamp s;
+int64_t tls_reload_period_ns(int64_t dflt_ns) {
+  const char* e = getenv("GPUMON_TLS_RELOAD_S");
+  return e && *e ? static_cast<int64_t>(std::max(0.1, atof(e)) * 1e9) : dflt_ns;
+}
+
+FileStamp FileStamp::of(const std::string& path) {
+  FileStamp s;
   struct stat st {};
   if (path.empty() || ::stat(path.c_str(), &st) != 0) return s;  // follows the kubelet's ..data symlink
   s.mtime_ns = static_cast<int64_t>(st.st_mtim.tv_sec) * 1000000000LL + st.st_mtim.tv_nsec;
@@ -485,9 +490,9 @@ std::shared_ptr<TlsServer> TlsServer::create(const std::string& cert_file, const
   t->key_ = key_file;
   t->ca_ = client_ca_file;
   // stamped before the load: a rotation while it loads is seen as a change next time
-  t->stamps_[0] = stamp(cert_file);
-  t->stamps_[1] = stamp(key_file);
-  t->stamps_[2] = stamp(client_ca_file);
+  t->stamps_[0] = FileStamp::of(cert_file);
+  t->stamps_[1] = FileStamp::of(key_file);
+  t->stamps_[2] = FileStamp::of(client_ca_file);
   int64_t na = 0;
   t->ctx_ = build_server_ctx(a, cert_file, key_file, client_ca_file, &na, err);
   if (!t->ctx_) return nullptr;
@@ -497,8 +502,8 @@ std::shared_ptr<TlsServer> TlsServer::create(const std::string& cert_file, const
 
 void TlsServer::maybe_reload(int64_t now_ns) {
   if (now_ns < next_check_ns_) return;
-  next_check_ns_ = now_ns + 5'000'000'000LL;
-  const Stamp now[3] = {stamp(cert_), stamp(key_), stamp(ca_)};
+  next_check_ns_ = now_ns + tls_reload_period_ns(5'000'000'000LL);
+  const FileStamp now[3] = {FileStamp::of(cert_), FileStamp::of(key_), FileStamp::of(ca_)};
   if (now[0] == stamps_[0] && now[1] == stamps_[1] && now[2] == stamps_[2]) return;
   for (int i = 0; i < 3; ++i) stamps_[i] = now[i];  // a broken change is retried on the next change only
   std::string err;

@@ -26,6 +26,19 @@ struct TlsOptions {
 
 struct SslApi;  // the dlopen'd function table (tls.cpp)
 
+// mtime, size and inode of a file, following symlinks (the kubelet's ..data swap of a Secret
+// volume): a different stamp means the file was replaced. All zero / -1 when it cannot be read.
+struct FileStamp {
+  int64_t mtime_ns = 0, size = -1;
+  uint64_t ino = 0;
+  static FileStamp of(const std::string& path);
+  bool operator==(const FileStamp& o) const { return mtime_ns == o.mtime_ns && size == o.size && ino == o.ino; }
+  bool operator!=(const FileStamp& o) const { return !(*this == o); }
+};
+
+// How often TLS files are re-stamped for rotation: `dflt_ns`, or $GPUMON_TLS_RELOAD_S seconds.
+int64_t tls_reload_period_ns(int64_t dflt_ns);
+
 // Loads libssl / libcrypto once per process (thread-safe); nullptr with *err when unavailable.
 // $GPUMON_LIBSSL / $GPUMON_LIBCRYPTO override the sonames.
 const SslApi* ssl_api(std::string* err);
@@ -108,17 +121,11 @@ class TlsServer {
 
  private:
   TlsServer() = default;
-  struct Stamp {
-    int64_t mtime_ns = 0, size = -1;
-    uint64_t ino = 0;
-    bool operator==(const Stamp& o) const { return mtime_ns == o.mtime_ns && size == o.size && ino == o.ino; }
-  };
-  static Stamp stamp(const std::string& path);
   const SslApi* api_ = nullptr;
   std::string cert_, key_, ca_;
   mutable std::mutex mu_;
   void* ctx_ = nullptr;  // SSL_CTX*, swapped under mu_ on a reload
-  Stamp stamps_[3];
+  FileStamp stamps_[3];
   int64_t next_check_ns_ = 0;
   std::atomic<int64_t> not_after_{0};
   std::atomic<uint64_t> reloads_ok_{0}, reloads_failed_{0};

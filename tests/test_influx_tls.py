@@ -429,3 +429,29 @@ def test_tls_slow_but_steady_server_is_served(core, pki):
                                        False, 3)
     assert st == 204, err
     assert len(srv.posts) == 3 and len({p["peer"] for p in srv.posts}) == 1
+
+
+def test_push_picks_up_a_rotated_ca_without_a_restart(core, pki, tmp_path, monkeypatch):
+    """The InfluxDB server moves to a certificate from a new CA and the mounted CA file is replaced:
+    pushes fail verification until the exporter re-stamps its TLS files, then resume without a
+    restart, on a new connection."""
+    import shutil
+
+    monkeypatch.setenv("GPUMON_TLS_RELOAD_S", "0.3")
+    ca_file = tmp_path / "influx-ca.pem"
+    shutil.copy(pki["otherca"], ca_file)  # the CA of the server's *next* certificate is not there yet
+    with _TlsSink(pki["server"], pki["server_key"]) as srv:
+        ex = core.Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0.1,
+                            "influx_url": f"https://localhost:{srv.port}/write?db=k8s", "influx_ca_file": str(ca_file),
+                            "influx_timeout_s": 1.0})
+        ex.start()
+        try:
+            assert _wait(lambda: ex.self_stats()["influx_fail"] >= 1), ex.self_stats()
+            assert not srv.posts
+            tmp = tmp_path / "influx-ca.pem.new"
+            shutil.copy(pki["ca"], tmp)
+            os.replace(tmp, ca_file)  # the kubelet's rename
+            assert _wait(lambda: len(srv.posts) >= 1, timeout=20.0), (ex.self_stats(), srv.handshake_errors[-2:])
+            assert _wait(lambda: ex.self_stats()["influx_up"] == 1)
+        finally:
+            ex.stop()

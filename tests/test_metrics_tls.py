@@ -279,12 +279,14 @@ print("alive")
     assert r.returncode == 0 and "alive" in r.stdout, (r.returncode, r.stderr[-2000:])
 
 
-def test_rotated_certificate_is_picked_up_without_a_restart(core, pki, tmp_path):
-    """cert-manager renews the Secret, the kubelet swaps the mounted files: within 5 s new connections
-    get the new certificate (its expiry exported), the reload is counted, and a rotation that does
-    not load keeps the previous certificate in use."""
+def test_rotated_certificate_is_picked_up_without_a_restart(core, pki, tmp_path, monkeypatch):
+    """cert-manager renews the Secret, the kubelet swaps the mounted files: within the check period
+    (5 s; 0.3 s here via GPUMON_TLS_RELOAD_S) new connections get the new certificate (its expiry
+    exported), the reload is counted, and a rotation that does not load keeps the previous
+    certificate in use."""
     import shutil
-    import datetime
+
+    monkeypatch.setenv("GPUMON_TLS_RELOAD_S", "0.3")
 
     d = tmp_path
     ca_dir = os.path.dirname(pki["ca"])
