@@ -898,6 +898,7 @@ PYBIND11_MODULE(_core, m) {
              auto s = e.snapshot();
              return s ? s->body : std::string();
            })
+      .def("reload_tls", &Exporter::reload_tls, "re-check the /metrics TLS files now (SIGHUP)")
       .def("metrics_gzip",
            [](Exporter& e) {
              auto s = e.snapshot();

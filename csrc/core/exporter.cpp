@@ -938,6 +938,11 @@ void Exporter::influx_loop() {
   }
 }
 
+void Exporter::reload_tls() {
+  if (server_)
+    if (TlsServer* t = server_->tls_server()) t->request_reload();
+}
+
 bool Exporter::healthy() const {
   if (!running_) return false;
   double stale = cfg_.health_stale_s > 0 ? cfg_.health_stale_s

@@ -152,6 +152,8 @@ class Exporter {
   ~Exporter();
 
   bool start(std::string* err);       // backend init (retried later if it fails) + threads
+  // SIGHUP: re-check the TLS files of /metrics within a second (rotation is also picked up on its own).
+  void reload_tls();
   void stop();
   TickInfo tick();                    // one synchronous tick (manual mode or tests)
   bool wait_for_seq(uint64_t seq, double timeout_s);  // until a snapshot with seq >= `seq`

@@ -66,6 +66,7 @@ class HttpServer {
   bool tls() const { return tls_ != nullptr; }
   uint64_t tls_failures() const { return tls_failures_.load(); }  // handshakes that failed or timed out
   const TlsServer* tls_server() const { return tls_.get(); }
+  TlsServer* tls_server() { return tls_.get(); }
   int rt_loops() const { return rt_loops_.load(); }           // loops running at SCHED_FIFO now
   uint64_t rt_demotions() const { return rt_demotions_.load(); }  // budget exhaustions
   uint64_t evicted() const { return evicted_.load(); }            // closed to make room at the cap

@@ -497,11 +497,12 @@ std::shared_ptr<TlsServer> TlsServer::create(const std::string& cert_file, const
   t->ctx_ = build_server_ctx(a, cert_file, key_file, client_ca_file, &na, err);
   if (!t->ctx_) return nullptr;
   t->not_after_ = na;
+  t->next_check_ns_ = mono_ns() + tls_reload_period_ns(5'000'000'000LL);  // just loaded
   return t;
 }
 
 void TlsServer::maybe_reload(int64_t now_ns) {
-  if (now_ns < next_check_ns_) return;
+  if (now_ns < next_check_ns_ && !reload_now_.exchange(false)) return;
   next_check_ns_ = now_ns + tls_reload_period_ns(5'000'000'000LL);
   const FileStamp now[3] = {FileStamp::of(cert_), FileStamp::of(key_), FileStamp::of(ca_)};
   if (now[0] == stamps_[0] && now[1] == stamps_[1] && now[2] == stamps_[2]) return;

@@ -105,6 +105,8 @@ class TlsServer {
   // change that does not load (a half-written rotation) keeps the old context and is retried on the
   // files' next change. Called by one HTTP loop.
   void maybe_reload(int64_t now_ns);
+  // Re-check the files at the loop's next sweep (within a second) instead of the next period: SIGHUP.
+  void request_reload() { reload_now_ = true; }
   int64_t not_after() const { return not_after_.load(); }  // the serving certificate's expiry (unix s; 0 unknown)
   uint64_t reloads_ok() const { return reloads_ok_.load(); }
   uint64_t reloads_failed() const { return reloads_failed_.load(); }
@@ -127,6 +129,7 @@ class TlsServer {
   void* ctx_ = nullptr;  // SSL_CTX*, swapped under mu_ on a reload
   FileStamp stamps_[3];
   int64_t next_check_ns_ = 0;
+  std::atomic<bool> reload_now_{false};
   std::atomic<int64_t> not_after_{0};
   std::atomic<uint64_t> reloads_ok_{0}, reloads_failed_{0};
 };

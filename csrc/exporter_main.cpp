@@ -28,8 +28,9 @@ using namespace gpumon;
 
 extern char** environ;
 
-static std::atomic<bool> g_stop{false};
+static std::atomic<bool> g_stop{false}, g_hup{false};
 static void on_signal(int) { g_stop = true; }
+static void on_hup(int) { g_hup = true; }
 
 static void usage() {
   fprintf(stderr,
@@ -250,6 +251,7 @@ int main(int argc, char** argv) {
   signal(SIGINT, on_signal);
   signal(SIGTERM, on_signal);
   signal(SIGPIPE, SIG_IGN);
+  signal(SIGHUP, on_hup);  // re-check the TLS files now (a rotated certificate is also found within 5 s)
   // The soft fd limit up to the hard one, as daemons (and Go's runtime) do: container runtimes often
   // leave the soft limit at 1024, and the HTTP connection cap is derived from it. Nothing in the
   // process (or the libraries it loads: libamd_smi, libdrm, OpenSSL) uses select(), so fd numbers
@@ -281,7 +283,13 @@ int main(int argc, char** argv) {
   GPUMON_LOG(LogLevel::kInfo, "main",
              "serving http://" + e.listen_desc() +
                  "/metrics host=" + cfg.host + " interval=" + std::to_string(cfg.interval_s) + "s");
-  while (!g_stop) std::this_thread::sleep_for(std::chrono::milliseconds(200));
+  while (!g_stop) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(200));
+    if (g_hup.exchange(false)) {
+      GPUMON_LOG(LogLevel::kInfo, "main", "SIGHUP: re-checking the TLS files");
+      e.reload_tls();
+    }
+  }
   ondev.stop();
   e.stop();
   return 0;

@@ -64,6 +64,8 @@ def cmd_serve(args) -> int:
     stop = threading.Event()
     for s in (signal.SIGINT, signal.SIGTERM):
         signal.signal(s, lambda *_: stop.set())
+    # SIGHUP: re-check the /metrics TLS files now (a rotated certificate is also found within 5 s)
+    signal.signal(signal.SIGHUP, lambda *_: mon.ex.reload_tls())
     while not stop.wait(1.0):
         pass
     mon.stop()

@@ -342,3 +342,57 @@ def test_rotated_certificate_is_picked_up_without_a_restart(core, pki, tmp_path,
         assert served_not_after() == renewed
     finally:
         ex.stop()
+
+
+@pytest.mark.parametrize("entry", ["native", "python"])
+def test_sighup_reloads_the_certificate_now(entry, pki, tmp_path):
+    """`kill -HUP`: both entry points re-check the TLS files within a second, whatever the
+    rotation period (an hour here)."""
+    import shutil
+    import signal
+
+    live = tmp_path / "live"
+    live.mkdir()
+    shutil.copy(pki["server"], live / "tls.crt")
+    shutil.copy(pki["server_key"], live / "tls.key")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    base = [EXPORTER] if entry == "native" else [sys.executable, "-m", "gpumon", "serve", "--control-plane", "off"]
+    p = subprocess.Popen(base + ["--backend", "mock:gpus=1", "--interval", "0.2", "--listen", f"127.0.0.1:{port}",
+                                 "--tls-cert-file", str(live / "tls.crt"), "--tls-key-file", str(live / "tls.key")],
+                         cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT, GPUMON_TLS_RELOAD_S="3600"),
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    ctx = _ctx(pki)
+
+    def reloads():
+        st, _, body, c = _get(port, ctx, path="/metrics?include=gpumon_http_tls_reloads_total")
+        c.close()
+        return promtext.one(promtext.parse(body.decode()), "gpumon_http_tls_reloads_total", result="ok")
+
+    try:
+        deadline = time.time() + 30
+        while True:
+            try:
+                assert reloads() == 0
+                break
+            except (OSError, ssl.SSLError):
+                assert time.time() < deadline and p.poll() is None
+                time.sleep(0.1)
+        # a re-issued certificate for the same key (same names, new serial): what a renewal installs
+        d = os.path.dirname(pki["ca"])
+        subprocess.run(["openssl", "x509", "-req", "-in", os.path.join(d, "server.csr"), "-CA", "ca.pem", "-CAkey",
+                        "ca.key", "-CAcreateserial", "-days", "3", "-out", str(tmp_path / "renewed.pem"), "-extfile",
+                        os.path.join(d, "server.ext")], cwd=d, check=True, capture_output=True, timeout=60)
+        os.replace(tmp_path / "renewed.pem", live / "tls.crt")
+        time.sleep(1.5)
+        assert reloads() == 0  # the hour-long period has not come round
+        p.send_signal(signal.SIGHUP)
+        deadline = time.time() + 10
+        while reloads() < 1:
+            assert time.time() < deadline and p.poll() is None
+            time.sleep(0.2)
+    finally:
+        p.terminate()
+        p.wait(10)
