@@ -813,6 +813,9 @@ void HttpServer::run(Loop* L) {
           }
           if (r == 0) peer_closed = true;
           else if (errno == EINTR) continue;
+          // a read error (a reset, a TLS protocol error): the connection is done. A failed TLS session
+          // reads nothing more from the socket, so level-triggered EPOLLIN would otherwise keep firing.
+          else if (errno != EAGAIN && errno != EWOULDBLOCK) peer_closed = true;
           break;
         }
       }

@@ -32,6 +32,7 @@ constexpr int kFiletypePem = 1;
 constexpr int kVerifyFailIfNoPeerCert = 2;
 constexpr int kCtrlMode = 33, kCtrlSetSessCacheMode = 44;
 constexpr long kModeEnablePartialWrite = 0x1, kModeAcceptMovingWriteBuffer = 0x2, kSessCacheOff = 0;
+constexpr uint64_t kOpNoRenegotiation = 0x40000000U;
 constexpr int kErrorNone = 0, kErrorSsl = 1, kErrorWantRead = 2, kErrorWantWrite = 3, kErrorSyscall = 5,
               kErrorZeroReturn = 6;
 constexpr long kVerifyOk = 0;
@@ -47,6 +48,7 @@ struct SslApi {
   const void* (*TLS_server_method)() = nullptr;
   int (*SSL_CTX_set_session_id_context)(void*, const unsigned char*, unsigned int) = nullptr;
   int (*SSL_CTX_set_num_tickets)(void*, size_t) = nullptr;
+  uint64_t (*SSL_CTX_set_options)(void*, uint64_t) = nullptr;
   void (*SSL_set_accept_state)(void*) = nullptr;
   int (*SSL_do_handshake)(void*) = nullptr;
   void* (*SSL_CTX_get0_certificate)(const void*) = nullptr;
@@ -130,6 +132,7 @@ void load_api() {
   sym(s, "TLS_server_method", &a->TLS_server_method, &missing);
   sym(s, "SSL_CTX_set_session_id_context", &a->SSL_CTX_set_session_id_context, &missing);
   sym(s, "SSL_CTX_set_num_tickets", &a->SSL_CTX_set_num_tickets, &missing);
+  sym(s, "SSL_CTX_set_options", &a->SSL_CTX_set_options, &missing);
   sym(s, "SSL_set_accept_state", &a->SSL_set_accept_state, &missing);
   sym(s, "SSL_do_handshake", &a->SSL_do_handshake, &missing);
   sym(s, "SSL_CTX_get0_certificate", &a->SSL_CTX_get0_certificate, &missing);
@@ -434,6 +437,9 @@ void* build_server_ctx(const SslApi* a, const std::string& cert_file, const std:
   a->SSL_CTX_ctrl(ctx, ossl::kCtrlMode, ossl::kModeEnablePartialWrite | ossl::kModeAcceptMovingWriteBuffer, nullptr);
   a->SSL_CTX_ctrl(ctx, ossl::kCtrlSetSessCacheMode, ossl::kSessCacheOff, nullptr);
   a->SSL_CTX_set_num_tickets(ctx, 0);
+  // no TLS 1.2 renegotiation: a write would then wait for the peer's records (WANT_READ) while the
+  // loop waits for EPOLLOUT -- a scraper has no reason to renegotiate
+  a->SSL_CTX_set_options(ctx, ossl::kOpNoRenegotiation);
   static const unsigned char kSid[] = "gpumon";
   a->SSL_CTX_set_session_id_context(ctx, kSid, sizeof kSid - 1);
   if (a->SSL_CTX_use_certificate_chain_file(ctx, cert_file.c_str()) != 1)

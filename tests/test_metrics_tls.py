@@ -396,3 +396,33 @@ def test_sighup_reloads_the_certificate_now(entry, pki, tmp_path):
     finally:
         p.terminate()
         p.wait(10)
+
+
+def test_garbage_after_the_handshake_closes_the_connection(core, pki):
+    """Bytes that are not a TLS record after a completed handshake: the session fails, and the server
+    closes the connection. A failed session reads nothing more, so the level-triggered readable
+    socket must not be left in the loop's epoll set, where it would fire on every wait."""
+    ex = core.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                        "http_threads": 1, "tls_cert_file": pki["server"], "tls_key_file": pki["server_key"]})
+    ex.start()
+    try:
+        raw = socket.create_connection(("127.0.0.1", ex.port), timeout=5)
+        s = _ctx(pki).wrap_socket(raw, server_hostname="localhost")
+        raw2 = socket.socket(fileno=s.detach())  # the TCP socket under the finished handshake
+        raw2.sendall(b"\x17\x03\x03\x00\x10" + b"not a real record" * 4)
+        # the client keeps its end open: the loop must not spin on the readable socket meanwhile
+        cpu0, t0 = time.process_time(), time.monotonic()
+        time.sleep(1.0)
+        burn = (time.process_time() - cpu0) / (time.monotonic() - t0)
+        raw2.settimeout(5)
+        try:
+            while raw2.recv(4096):
+                pass  # an alert, then the close
+        except (ConnectionResetError, socket.timeout):
+            pass
+        raw2.close()
+        assert burn < 0.3, burn  # a spinning loop burns a whole CPU
+        assert _get(ex.port, _ctx(pki))[0] == 200  # the server is fine
+        assert ex.self_stats()["http_connections"] <= 1
+    finally:
+        ex.stop()
