@@ -431,7 +431,9 @@ def test_sanitized_connection_flood_and_eviction(target, binary, env):
 def test_sanitized_https_serving(target, binary, env, tmp_path):
     """/metrics over HTTPS (csrc/core/tls.cpp TlsServer, the TLS branch of the HTTP loops) under
     ASan+UBSan and TSan: two loops serving concurrent verified scrapes and per-request filters over
-    TLS, plus failed handshakes (plain HTTP and an untrusted scraper) mixed in. No sanitizer report."""
+    TLS, failed handshakes (plain HTTP and an untrusted scraper) mixed in, and the certificate files
+    replaced every 0.15 s, so contexts are swapped while both loops create sessions. No sanitizer
+    report."""
     import ssl
 
     from conftest import make_locked
@@ -462,15 +464,30 @@ def test_sanitized_https_serving(target, binary, env, tmp_path):
                     pass
             time.sleep(0.02)
 
-    t = threading.Thread(target=intruders, daemon=True)
-    t.start()
+    import shutil
+
+    os.makedirs(f"{d}/live")
+    for src, dst in (("server.pem", "tls.crt"), ("server.key", "tls.key")):
+        shutil.copy(f"{d}/{src}", f"{d}/live/{dst}")
+
+    def rotator():  # the kubelet's rename of the Secret's files, over and over: reloads while serving
+        while not stop.is_set():
+            for src, dst in (("server.pem", "tls.crt"), ("server.key", "tls.key")):
+                shutil.copy(f"{d}/{src}", f"{d}/live/{dst}.new")
+                os.replace(f"{d}/live/{dst}.new", f"{d}/live/{dst}")
+            time.sleep(0.15)
+
+    ts = [threading.Thread(target=intruders, daemon=True), threading.Thread(target=rotator, daemon=True)]
+    for t in ts:
+        t.start()
     try:
-        rc, err = _run(os.path.join(ROOT, binary), dict(env), ("--tls-cert-file", f"{d}/server.pem",
-                                                               "--tls-key-file", f"{d}/server.key"), min_s=1.0, ctx=ctx,
-                       port=port)
+        rc, err = _run(os.path.join(ROOT, binary), dict(env, GPUMON_TLS_RELOAD_S="0.1"),
+                       ("--tls-cert-file", f"{d}/live/tls.crt", "--tls-key-file", f"{d}/live/tls.key"), min_s=1.5,
+                       ctx=ctx, port=port)
     finally:
         stop.set()
-        t.join(5)
+        for t in ts:
+            t.join(5)
     bad = _reports(err)
     assert not bad, err[-4000:]
     assert rc == 0, err[-2000:]
