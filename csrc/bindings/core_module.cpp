@@ -775,6 +775,15 @@ PYBIND11_MODULE(_core, m) {
       },
       py::arg("url"), py::arg("token") = "", py::arg("ca_file") = "", py::arg("insecure") = false,
       py::arg("client_cert") = "", py::arg("client_key") = "");
+  m.def(
+      "serve_tls_not_after",
+      [](const std::string& cert, const std::string& key, const std::string& ca) {
+        // (error, expiry of the serving certificate in unix seconds): the doctor's TLS check
+        std::string err;
+        auto t = TlsServer::create(cert, key, ca, &err);
+        return py::make_tuple(err, t ? t->not_after() : 0);
+      },
+      py::arg("cert_file"), py::arg("key_file"), py::arg("client_ca_file") = "");
   m.def("check_serve_tls", &check_serve_tls, py::arg("cert_file") = "", py::arg("key_file") = "",
         py::arg("client_ca_file") = "", "configuration-time check of the /metrics HTTPS files: \"\" = usable");
   m.def("redact_url", &redact_url);

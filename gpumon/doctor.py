@@ -226,6 +226,29 @@ def influx_check(cfg) -> tuple:
             + "; the push will retry with backoff (gpumon_influx_up 0 until it succeeds)")
 
 
+def serve_tls_check(cfg, now=None) -> tuple:
+    """/metrics over HTTPS: the certificate, key and client CA load (the startup check), and the
+    certificate's remaining validity (the GpumonMetricsCertificateExpiring alert fires under 7 days)."""
+    import time
+
+    from ._native import core as _core
+
+    err, not_after = _core().serve_tls_not_after(cfg.tls_cert_file, cfg.tls_key_file, cfg.tls_client_ca_file)
+    if err:
+        return (FAIL, err + ": the exporter refuses to start with it")
+    mtls = ", mutual TLS" if cfg.tls_client_ca_file else ""
+    if not not_after:
+        return (OK, f"{cfg.tls_cert_file}{mtls}: loads (expiry unknown)")
+    days = (not_after - (now if now is not None else time.time())) / 86400
+    when = time.strftime("%Y-%m-%d", time.gmtime(not_after))
+    if days < 0:
+        return (FAIL, f"{cfg.tls_cert_file}{mtls}: EXPIRED on {when}: every verifying scraper is refused")
+    if days < 7:
+        return (WARN, f"{cfg.tls_cert_file}{mtls}: expires {when} ({days:.1f} days): renew it (rotation is picked up "
+                      "without a restart)")
+    return (OK, f"{cfg.tls_cert_file}{mtls}: valid until {when} ({days:.0f} days)")
+
+
 def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
     """[(check, status, detail)] for the node this runs on, with the exporter configured as `cfg`."""
     from .monitor import GpuMonitor
@@ -233,6 +256,9 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
     out = []
     interval_s = cfg.interval  # as configured (the checks below tick by hand)
     out.append(("listen address",) + listen_check(cfg.listen))
+    if cfg.tls_cert_file or cfg.tls_key_file or cfg.tls_client_ca_file:
+        out.append(("/metrics TLS certificate",) + serve_tls_check(cfg))
+        cfg.tls_cert_file = cfg.tls_key_file = cfg.tls_client_ca_file = ""  # the checks below serve plain
     if cfg.influx_url:
         out.append(("Influx push",) + influx_check(cfg))
         cfg.influx_url = ""  # checked above; the checks below do not push

@@ -285,3 +285,28 @@ def test_doctor_checks_the_influx_push(tmp_path):
     checks = _by_name(doctor.run(Config(backend="mock:gpus=1", control_plane="off", log_level="error",
                                         influx_url="ftp://influx/write"), wait_s=0.2))
     assert checks["Influx push"][0] == "fail" and checks["device backend"][0] == "ok"
+
+
+def test_doctor_reports_the_metrics_certificate(tmp_path):
+    """/metrics over HTTPS: the doctor says whether the certificate loads and how long it is valid
+    (warn under 7 days, fail once expired or unloadable)."""
+    import time
+
+    from gpumon.doctor import FAIL, OK, WARN, serve_tls_check
+
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:prime256v1", "-nodes",
+                    "-days", "30", "-keyout", str(tmp_path / "k.pem"), "-out", str(tmp_path / "c.pem"), "-subj",
+                    "/CN=gpumon"], check=True, capture_output=True, timeout=60)
+    cfg = Config(tls_cert_file=str(tmp_path / "c.pem"), tls_key_file=str(tmp_path / "k.pem"))
+    st, detail = serve_tls_check(cfg)
+    assert st == OK and "valid until" in detail and ("(30 days)" in detail or "(29 days)" in detail), detail
+    st, detail = serve_tls_check(cfg, now=time.time() + 26 * 86400)
+    assert st == WARN and "expires" in detail, detail
+    st, detail = serve_tls_check(cfg, now=time.time() + 31 * 86400)
+    assert st == FAIL and "EXPIRED" in detail, detail
+    st, detail = serve_tls_check(Config(tls_cert_file=str(tmp_path / "c.pem")))
+    assert st == FAIL and "go together" in detail
+    checks = _by_name(doctor.run(Config(backend="mock:gpus=1", control_plane="off", log_level="error",
+                                        tls_cert_file=str(tmp_path / "c.pem"), tls_key_file=str(tmp_path / "k.pem")),
+                                 wait_s=0.5))
+    assert checks["/metrics TLS certificate"][0] == OK
