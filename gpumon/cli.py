@@ -1,8 +1,8 @@
 """``python -m gpumon`` — command line.
 
-    gpumon serve   [--backend amdsmi] [--interval 1] [--listen 0.0.0.0:9400] ...   run the exporter
+    gpumon serve   [--backend amdsmi] [--interval 1] [--listen :9400] ...           run the exporter
     gpumon once    [--format prom|influx|json]                                       one sample to stdout
-    gpumon top     [--interval 1]                                                    live console table
+    gpumon top     [--interval 1] [--url HOST:PORT ... [--ca-file PEM]]              live console table
     gpumon scrape  URL [-n 1000] [-c 4]                                              scrape-latency probe
     gpumon probe   [--blocks 1024]                                                   run the K1 probe once
     gpumon load    [--kind mixed --seconds 10]                                       synthetic gfx950 load
