@@ -12,6 +12,10 @@ push counters it exports, the sink's counts and the scrape p99. The final summar
 A leak across reconnects shows up as a trend in fds or RSS. A lost or reordered batch shows up as a
 gap in the sink's tick sequence.
 
+With `--serve-tls` the exporter also serves /metrics over HTTPS, and the scraper verifies it. With
+`--rotate-every S` the serving certificate is re-issued and swapped into place every S seconds, the
+way the kubelet updates a mounted Secret, while scrapes run.
+
 On a GPU box: `--backend amdsmi` (default) next to the mixed K2 load. On CPU: `--backend mock`.
 """
 
@@ -120,17 +124,50 @@ def proc_stats(pid):
             "threads": len(os.listdir(f"/proc/{pid}/task"))}
 
 
-def push_counters(port):
+def push_counters(port, ctx=None):
     from gpumon.export import promtext
 
-    c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
-    c.request("GET", "/metrics?include=gpumon_influx_*,gpumon_ticks_total")
+    c = (http.client.HTTPSConnection("localhost", port, context=ctx, timeout=5) if ctx
+         else http.client.HTTPConnection("127.0.0.1", port, timeout=5))
+    c.request("GET", "/metrics?include=gpumon_influx_*,gpumon_ticks_total,gpumon_http_tls_*")
     fam = promtext.parse(c.getresponse().read().decode())
     c.close()
     out = {"ticks": promtext.one(fam, "gpumon_ticks_total"), "influx_up": promtext.one(fam, "gpumon_influx_up")}
     for _, labels, v in fam.get("gpumon_influx_push_total", {}).get("samples", []):
         out["push_" + labels.get("result", "?")] = v
+    if ctx:
+        out["tls_handshake_failures"] = promtext.one(fam, "gpumon_http_tls_handshake_failures_total")
+        for _, labels, v in fam.get("gpumon_http_tls_reloads_total", {}).get("samples", []):
+            out["tls_reloads_" + labels.get("result", "?")] = v
     return out
+
+
+def tls_scrapes(port, ctx, seconds, rate_hz):
+    """Verified HTTPS scrapes with gzip over one keep-alive connection (reopened after an error),
+    paced at rate_hz: (latencies, errors)."""
+    lat, errors, conn = [], 0, None
+    period, t_next, end = 1.0 / rate_hz, time.monotonic(), time.monotonic() + seconds
+    while time.monotonic() < end:
+        time.sleep(max(0.0, t_next - time.monotonic()))
+        t_next += period
+        try:
+            if conn is None:
+                conn = http.client.HTTPSConnection("localhost", port, context=ctx, timeout=5)
+            t = time.perf_counter()
+            conn.request("GET", "/metrics", headers={"Accept-Encoding": "gzip"})
+            r = conn.getresponse()
+            r.read()
+            if r.status != 200:
+                raise OSError(f"HTTP {r.status}")
+            lat.append(time.perf_counter() - t)
+        except (OSError, ssl.SSLError, http.client.HTTPException):
+            errors += 1
+            if conn is not None:
+                conn.close()
+            conn = None
+    if conn is not None:
+        conn.close()
+    return lat, errors
 
 
 def main():
@@ -142,6 +179,9 @@ def main():
     ap.add_argument("--scrape-rate", type=float, default=20.0)
     ap.add_argument("--close-every", type=int, default=50)
     ap.add_argument("--fail-every", type=int, default=200)
+    ap.add_argument("--serve-tls", action="store_true", help="serve /metrics over HTTPS and scrape it verified")
+    ap.add_argument("--rotate-every", type=float, default=0.0,
+                    help="with --serve-tls: re-issue and swap the serving certificate every S seconds (0 = never)")
     a = ap.parse_args()
     if shutil.which("openssl") is None:
         raise SystemExit("push_soak: the openssl CLI is needed for the test CA")
@@ -162,16 +202,36 @@ def main():
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ, INFLUXDB_URL=f"https://localhost:{sink.port}/write?db=k8s", GPUMON_INFLUX_CA_FILE=pki["ca"],
-               NODE_NAME="soak-node")
-    ex = subprocess.Popen([os.path.join(ROOT, "bin", "gpumon-exporter"), "--backend", a.backend, "--interval",
-                           str(a.interval), "--listen", f"127.0.0.1:{port}", "--log-level", "error"],
-                          env=env, stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "exporter.err"), "wb"))
+               NODE_NAME="soak-node", GPUMON_TLS_RELOAD_S="1")
+    args = [os.path.join(ROOT, "bin", "gpumon-exporter"), "--backend", a.backend, "--interval", str(a.interval),
+            "--listen", f"127.0.0.1:{port}", "--log-level", "error"]
+    ctx = None
+    rotations = 0
+    stop_rotation = threading.Event()
+    if a.serve_tls:
+        live = os.path.join(tmp, "live")
+        os.makedirs(live)
+        shutil.copy(pki["server"], os.path.join(live, "tls.crt"))
+        shutil.copy(pki["server_key"], os.path.join(live, "tls.key"))
+        args += ["--tls-cert-file", os.path.join(live, "tls.crt"), "--tls-key-file", os.path.join(live, "tls.key")]
+        ctx = ssl.create_default_context(cafile=pki["ca"])
+
+        def rotate():  # a renewal: same key, new certificate, renamed into place
+            nonlocal rotations
+            while a.rotate_every > 0 and not stop_rotation.wait(a.rotate_every):
+                _openssl("x509", "-req", "-in", "server.csr", "-CA", "ca.pem", "-CAkey", "ca.key", "-CAcreateserial",
+                         "-days", "2", "-out", os.path.join(live, "tls.crt.new"), "-extfile", "server.ext", cwd=tmp)
+                os.replace(os.path.join(live, "tls.crt.new"), os.path.join(live, "tls.crt"))
+                rotations += 1
+
+        threading.Thread(target=rotate, daemon=True).start()
+    ex = subprocess.Popen(args, env=env, stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "exporter.err"), "wb"))
     windows = []
     try:
         deadline = time.monotonic() + 30
         while time.monotonic() < deadline:
             try:
-                push_counters(port)
+                push_counters(port, ctx)
                 break
             except (OSError, KeyError, ValueError):
                 time.sleep(0.1)
@@ -179,18 +239,24 @@ def main():
         end = time.monotonic() + a.minutes * 60
         t0 = time.monotonic()
         while time.monotonic() < end and ex.poll() is None:
-            r = core.scrape_load("127.0.0.1", port, "/metrics", n_requests=0, duration_s=a.window, concurrency=1,
-                                 rate_hz=a.scrape_rate, keep_alive=True, gzip=True)
+            if ctx:
+                got, nerr = tls_scrapes(port, ctx, a.window, a.scrape_rate)
+                r = {"latencies_s": got, "errors": nerr}
+            else:
+                r = core.scrape_load("127.0.0.1", port, "/metrics", n_requests=0, duration_s=a.window, concurrency=1,
+                                     rate_hz=a.scrape_rate, keep_alive=True, gzip=True)
             lat = sorted(r.get("latencies_s", []))
             with sink.lock:
                 sk = {"sink_posts": sink.posts, "sink_requests": sink.requests, "sink_handshakes": sink.handshakes,
                       "sink_node_lines": sink.node_lines, "sink_reordered": sink.reordered}
-            w = dict(proc_stats(ex.pid), t_min=round((time.monotonic() - t0) / 60, 2), **push_counters(port), **sk,
+            w = dict(proc_stats(ex.pid), t_min=round((time.monotonic() - t0) / 60, 2), **push_counters(port, ctx), **sk,
+                     rotations=rotations,
                      scrapes=len(lat), scrape_errors=r.get("errors", 0),
                      scrape_p99_ms=round(lat[int(0.99 * (len(lat) - 1))] * 1e3, 3) if lat else None)
             windows.append(w)
             print(json.dumps(w), flush=True)
     finally:
+        stop_rotation.set()
         ex.terminate()
         try:
             ex.wait(timeout=15)
@@ -219,6 +285,8 @@ def main():
         "scrape_p99_ms_max_window": max((w["scrape_p99_ms"] or 0 for w in windows), default=None),
         "exporter_stderr_tail": (err or b"").decode(errors="replace")[-400:],
         "close_every": a.close_every, "fail_every": a.fail_every,
+        "serve_tls": a.serve_tls, "rotations": rotations, "tls_reloads_ok": last.get("tls_reloads_ok"),
+        "tls_reloads_error": last.get("tls_reloads_error"), "tls_handshake_failures": last.get("tls_handshake_failures"),
     }
     print(json.dumps(summary), flush=True)
 
