@@ -200,11 +200,11 @@ bool selected(const char* name) { return !t_render_in || family_selected(*t_rend
 class Family {
  public:
   Family(std::string* o, const char* name, const char* help, const char* type)
-      : o_(o), name_(name), mark_(o->size()), on_(selected(name)) {
+      : o_(o), name_(name), mark_(o->size()), on_(selected(name)) {  // name_: one strlen, not one per sample
     if (!on_) return;
-    o_->append("# HELP ").append(name).push_back(' ');
+    o_->append("# HELP ").append(name_).push_back(' ');
     o_->append(help).push_back('\n');
-    o_->append("# TYPE ").append(name).push_back(' ');
+    o_->append("# TYPE ").append(name_).push_back(' ');
     o_->append(type).push_back('\n');
   }
   ~Family() {
@@ -248,7 +248,7 @@ class Family {
   }
 
   std::string* o_;
-  const char* name_;
+  std::string_view name_;
   size_t mark_;
   bool on_;
   bool any_ = false;
