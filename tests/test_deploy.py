@@ -613,3 +613,35 @@ def test_stress_overlay_is_10hz_end_to_end():
     ctr = _json_patch(ds, ops)["spec"]["template"]["spec"]["containers"][0]
     assert int(ctr["resources"]["requests"]["cpu"].rstrip("m")) >= 1.3 * 91
     assert not ctr["securityContext"].get("privileged")
+
+
+def test_systemd_unit_for_bare_metal_nodes(tmp_path):
+    """deploy/systemd/: the same native binary and config format without Kubernetes. The unit's
+    command line and config parse (no ignored keys) identically in both entry points, it grants the
+    DaemonSet's two capabilities and nothing else, and exit status 2 (a configuration error) is not
+    restarted in a loop."""
+    import configparser
+    import json
+    import shlex
+    import subprocess
+
+    from gpumon.config import Config, load_yaml
+
+    unit = configparser.ConfigParser(strict=False, interpolation=None)
+    unit.optionxform = str
+    unit.read(os.path.join(ROOT, "deploy/systemd/gpumon-exporter.service"))
+    svc = unit["Service"]
+    argv = shlex.split(svc["ExecStart"])
+    assert argv[0].endswith("/gpumon-exporter") and argv[1:] == ["--config", "/etc/gpumon/config.yaml"]
+    assert svc["RestartPreventExitStatus"] == "2" and svc["ExecReload"].endswith("-HUP $MAINPID")
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    caps = ds["spec"]["template"]["spec"]["containers"][0]["securityContext"]["capabilities"]["add"]
+    assert sorted(svc["CapabilityBoundingSet"].split()) == sorted("CAP_" + c for c in caps)
+    cfg_path = os.path.join(ROOT, "deploy/systemd/config.yaml")
+    r = subprocess.run([os.path.join(ROOT, "bin", "gpumon-exporter"), "--config", cfg_path, "--print-config"],
+                       capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0 and "ignored" not in r.stderr, r.stderr
+    native = json.loads(r.stdout)
+    py = Config().apply_dict(load_yaml(cfg_path))
+    assert native["include_host_processes"] is True and py.include_host_processes is True
+    assert native["cri_socket"] == py.cri_socket == "none" and native["pod_resources_socket"] == py.pod_resources_socket == ""
