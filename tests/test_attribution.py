@@ -213,6 +213,20 @@ def test_host_processes_toggle(mock_exporter, tmp_path):
     assert ex.pod_rows() == []
 
 
+def test_bare_metal_host_process_is_a_row_with_dash_labels(mock_exporter, tmp_path):
+    """deploy/systemd/ (no kubelet): a GPU process in a login session or a Slurm job step is a row
+    with its pid and process name; the pod, namespace and container labels read "-"."""
+    _fake_proc(tmp_path, 9, "0::/user.slice/session-1.scope\n", comm="train.py")
+    _fake_proc(tmp_path, 10, "0::/system.slice/slurmstepd.scope/job_42/step_0/user/task_0\n", comm="python3")
+    ex = mock_exporter(procfs_root=str(tmp_path), include_host_processes=True)
+    ex.mock_set_procs([{"pid": 9, "device": 0, "vram_bytes": 1 << 30}, {"pid": 10, "device": 1, "vram_bytes": 1 << 30}])
+    ex.tick()
+    rows = sorted(ex.pod_rows(), key=lambda r: r["pid"])
+    assert [(r["pid"], r["dev"]) for r in rows] == [("10", 1), ("9", 0)]
+    for r in rows:
+        assert r["podname"] == "-" and r["namespace"] == "-" and r["container"] == "-" and not r["idle"]
+
+
 def test_proc_gfx_util_from_engine_ns(mock_exporter):
     ex = mock_exporter(backend="mock:gpus=1,mode=load")
     ex.mock_set_procs([{"pid": os.getpid(), "device": 0, "gfx_share": 0.5}])
