@@ -464,6 +464,12 @@ def test_http_rt_loops_are_budget_capped(core):
         except PermissionError:
             assert st["http_rt_loops"] == 0  # no CAP_SYS_NICE: normal scheduling, said so
             return
+        import time
+
+        deadline = time.time() + 5  # each loop thread switches itself to FIFO when it starts
+        while ex.self_stats()["http_rt_loops"] < 2 and time.time() < deadline:
+            time.sleep(0.02)
+        st = ex.self_stats()
         assert st["http_rt_loops"] == 2 and st["http_rt_demotions"] == 0
         r = core.scrape_load("127.0.0.1", ex.port, "/metrics", n_requests=0, duration_s=1.5, concurrency=4,
                              rate_hz=0.0, keep_alive=True, gzip=False)
