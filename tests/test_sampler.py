@@ -96,13 +96,15 @@ def test_rates_span_the_firmware_window_and_survive_a_repeated_table(mock_export
     profiles/r3_capacity.md); the driver stamps system_clock_counter at each read. Rates divide by
     the firmware timestamp's delta (whole refresh periods here), and a repeated table keeps the last
     window's rates instead of reporting 0 W over it."""
-    ex = mock_exporter(backend="mock:gpus=1,mode=load,firmware_hz=20")  # a 50 ms firmware period
-    time.sleep(0.13)
+    # a 250 ms firmware period: long enough that two back-to-back ticks land on the same table even
+    # on a loaded CI host
+    ex = mock_exporter(backend="mock:gpus=1,mode=load,firmware_hz=4")
+    time.sleep(0.65)
     ex.tick()
     r = ex.rates()[0]
     assert r["valid"]
-    periods = r["dt_s"] / 0.05
-    assert periods == pytest.approx(round(periods), abs=1e-6) and round(periods) >= 2  # not the host's 0.13 s
+    periods = r["dt_s"] / 0.25
+    assert periods == pytest.approx(round(periods), abs=1e-6) and round(periods) >= 2  # not the host's 0.65 s
     assert r["power_from_energy_w"] == pytest.approx(ex.samples()[0]["fields"]["power_cur"], rel=1e-3)
     ex.tick()  # back to back: the same table
     assert not ex.samples()[0]["fresh"]
