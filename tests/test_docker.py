@@ -186,11 +186,14 @@ def test_native_docker_reader_bounds_a_misbehaving_daemon(core, script, error):
     import time
 
     d = _RawDaemon(_sock("raw"), script)
+    # the endless daemon must be cut off by the size bound (64 MiB), not by the clock: give its read
+    # time enough for 64 MiB on a loaded host
+    timeout_ms = 3000 if error == "response too large" else 400
     try:
         t0 = time.monotonic()
         with pytest.raises(RuntimeError, match=error):
-            core.docker_list(d.path, timeout_ms=400)
-        assert time.monotonic() - t0 < 3.0
+            core.docker_list(d.path, timeout_ms=timeout_ms)
+        assert time.monotonic() - t0 < timeout_ms / 1000 + 2.6
     finally:
         d.close()
 
