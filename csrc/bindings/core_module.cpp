@@ -106,6 +106,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "rt_priority", &c.rt_priority);
   get(d, "influx_url", &c.influx_url);
   get(d, "influx_extended", &c.influx_extended);
+  get(d, "influx_gzip", &c.influx_gzip);
   get(d, "influx_schema", &c.influx_schema);
   get(d, "influx_every", &c.influx_every);
   get(d, "influx_timeout_s", &c.influx_timeout_s);

@@ -869,6 +869,7 @@ void Exporter::influx_loop() {
   const std::string headers = "Content-Type: text/plain; charset=utf-8\r\n" +
                               (!cfg_.influx_token.empty() ? "Authorization: Token " + cfg_.influx_token + "\r\n"
                                                           : u.auth_header);
+  const std::string gz_headers = headers + "Content-Encoding: gzip\r\n";
   // A batch the server could not take for a transient reason (no connection, 5xx, 429) goes back
   // to the head of the queue and the push backs off (0.5 s doubling to 30 s), so an InfluxDB restart
   // loses nothing but what overflows the 60-batch queue; a 4xx other than 429 (a bad request, bad
@@ -905,8 +906,10 @@ void Exporter::influx_loop() {
         }
       }
     }
-    std::string err, resp;
-    int st = client.request("POST", u, body, headers, &resp, &err);
+    std::string err, resp, gz;
+    // influx_gzip: the batch compressed (a requeued batch is kept plain and compressed again)
+    const bool zipped = cfg_.influx_gzip && gzip_compress(body, &gz, 1);
+    int st = client.request("POST", u, zipped ? gz : body, zipped ? gz_headers : headers, &resp, &err);
     if (st >= 200 && st < 300) {
       influx_ok_++;
       influx_up_ = 1;

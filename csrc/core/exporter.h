@@ -94,6 +94,7 @@ struct ExporterConfig {
   bool influx_extended = false;
   int influx_schema = 2019;           // 2019 (gpu.py layout) | 2018 (img/influxdb.png pod_gpu)
   int influx_every = 1;               // ticks per push
+  bool influx_gzip = false;           // Content-Encoding: gzip on the push (InfluxDB 1.x / 2.x / 3.x accept it)
   double influx_timeout_s = 2.0;
   // InfluxDB 2.x / 3.x token ("Authorization: Token ..."); 1.x credentials go in the URL
   // (user:password@host) and become Basic auth. Set it from a Secret (INFLUXDB_TOKEN).

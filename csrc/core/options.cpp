@@ -261,6 +261,7 @@ const std::map<std::string, Setter>& setters() {
       {"influx_extended", bool_at([](NativeOptions* o) { return &o->cfg.influx_extended; })},
       {"influx_schema", int_at([](NativeOptions* o) { return &o->cfg.influx_schema; })},
       {"influx_every", int_at([](NativeOptions* o) { return &o->cfg.influx_every; })},
+      {"influx_gzip", bool_at([](NativeOptions* o) { return &o->cfg.influx_gzip; })},
       {"influx_ca_file", str_at([](NativeOptions* o) { return &o->cfg.influx_ca_file; })},
       {"tls_cert_file", str_at([](NativeOptions* o) { return &o->cfg.tls_cert_file; })},
       {"tls_key_file", str_at([](NativeOptions* o) { return &o->cfg.tls_key_file; })},
@@ -545,6 +546,7 @@ std::string options_json(const NativeOptions& o) {
   B("influx_extended", c.influx_extended);
   N("influx_schema", c.influx_schema);
   N("influx_every", c.influx_every);
+  B("influx_gzip", c.influx_gzip);
   S("influx_ca_file", c.influx_ca_file);
   S("tls_cert_file", c.tls_cert_file);
   S("tls_key_file", c.tls_key_file);

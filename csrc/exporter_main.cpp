@@ -115,6 +115,7 @@ int main(int argc, char** argv) {
     else if (a == "--influx-url") set("influx_url", next());
     else if (a == "--influx-token") set("influx_token", next());
     else if (a == "--influx-extended") set("influx_extended", "true");
+    else if (a == "--influx-gzip") set("influx_gzip", "true");
     else if (a == "--influx-schema") set("influx_schema", next());
     else if (a == "--influx-ca-file") set("influx_ca_file", next());
     else if (a == "--tls-cert-file") set("tls_cert_file", next());

@@ -73,6 +73,7 @@ class Config:
     influx_extended: bool = False
     influx_schema: int = 2019             # 2019 = gpu.py layout; 2018 = img/influxdb.png pod_gpu layout
     influx_every: int = 1
+    influx_gzip: bool = False             # gzip each push (Content-Encoding: gzip): ~5x fewer bytes for 8 GPUs
     influx_ca_file: str = ""              # https:// push: PEM CA bundle replacing the system one
     influx_tls_insecure: bool = False     # https:// push WITHOUT certificate / host-name checks (opt-in, testing)
     influx_client_cert: str = ""          # https:// push: PEM client chain for mutual TLS
@@ -186,6 +187,7 @@ class Config:
             "influx_extended": self.influx_extended,
             "influx_schema": int(self.influx_schema),
             "influx_every": int(self.influx_every),
+            "influx_gzip": bool(self.influx_gzip),
             "influx_ca_file": self.influx_ca_file,
             "influx_tls_insecure": bool(self.influx_tls_insecure),
             "influx_client_cert": self.influx_client_cert,
@@ -385,6 +387,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--host", help="node name label (default $NODE_NAME, then hostname)")
     p.add_argument("--influx-url", dest="influx_url", help="enable InfluxDB line-protocol push (default $INFLUXDB_URL)")
     p.add_argument("--influx-extended", dest="influx_extended", action="store_true", default=None)
+    p.add_argument("--influx-gzip", dest="influx_gzip", action="store_true", default=None,
+                   help="gzip each Influx push (Content-Encoding: gzip; InfluxDB 1.x / 2.x / 3.x accept it)")
     p.add_argument("--influx-ca-file", dest="influx_ca_file", help="PEM CA bundle for an https:// INFLUXDB_URL "
                    "(default: the system bundle)")
     p.add_argument("--influx-tls-insecure", dest="influx_tls_insecure", action="store_true", default=None,

@@ -117,6 +117,45 @@ def test_influx_batched_push(core):
     assert st["influx_ok"] >= 3 and st["influx_fail"] == 0
 
 
+class _GzipSink(_Sink):
+    seen = []
+
+    def do_POST(self):  # noqa: N802
+        import gzip as _gz
+
+        n = int(self.headers.get("Content-Length", 0))
+        raw = self.rfile.read(n)
+        enc = self.headers.get("Content-Encoding", "")
+        _GzipSink.seen.append((enc, len(raw), (_gz.decompress(raw) if enc == "gzip" else raw).decode()))
+        self.send_response(204)
+        self.send_header("Content-Length", "0")
+        self.end_headers()
+
+
+def test_influx_gzip_push(core):
+    """influx_gzip: each batch goes out with Content-Encoding: gzip (InfluxDB 1.x / 2.x / 3.x decode
+    it), several times smaller, and decodes to exactly the plain push's lines."""
+    _GzipSink.seen = []
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), _GzipSink)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    ex = core.Exporter({"backend": "mock:gpus=8", "serve_http": False, "interval_s": 0, "host": "node9",
+                        "influx_url": f"http://127.0.0.1:{srv.server_address[1]}/write?db=k8s", "influx_gzip": True,
+                        "influx_extended": True})
+    ex.start()
+    try:
+        deadline = time.time() + 5
+        while time.time() < deadline and ex.self_stats()["influx_ok"] < 1:
+            time.sleep(0.02)
+        want = ex.influx_text()
+    finally:
+        ex.stop()
+        srv.shutdown()
+    enc, nbytes, text = _GzipSink.seen[0]
+    assert enc == "gzip" and nbytes * 3 < len(text.encode()), (nbytes, len(text))
+    strip = lambda t: [l.rsplit(" ", 1)[0] for l in t.strip().split("\n")]  # noqa: E731 (stamps differ)
+    assert strip(text) == strip(want)
+
+
 def test_influx_unreachable_does_not_block_sampling(core):
     ex = core.Exporter({"backend": "mock:gpus=1", "serve_http": False, "interval_s": 0.02,
                         "influx_url": "http://127.0.0.1:9/write", "influx_timeout_s": 0.2})
