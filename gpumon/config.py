@@ -73,7 +73,7 @@ class Config:
     influx_extended: bool = False
     influx_schema: int = 2019             # 2019 = gpu.py layout; 2018 = img/influxdb.png pod_gpu layout
     influx_every: int = 1
-    influx_gzip: bool = False             # gzip each push (Content-Encoding: gzip): ~5x fewer bytes for 8 GPUs
+    influx_gzip: bool = False             # gzip each push (Content-Encoding: gzip): 7-8x fewer bytes for 8 GPUs
     influx_ca_file: str = ""              # https:// push: PEM CA bundle replacing the system one
     influx_tls_insecure: bool = False     # https:// push WITHOUT certificate / host-name checks (opt-in, testing)
     influx_client_cert: str = ""          # https:// push: PEM client chain for mutual TLS
