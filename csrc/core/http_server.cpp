@@ -32,6 +32,9 @@ namespace {
 
 constexpr size_t kMaxHeader = 16 * 1024;
 constexpr long kMaxBody = 64 * 1024;  // every route is GET/HEAD: a request body is only ever skipped
+// input buffered per connection before it is parsed: above the largest acceptable request, so a
+// full buffer always starts with a complete (or a refused) request
+constexpr size_t kMaxInput = kMaxHeader + kMaxBody + 4096;
 constexpr int64_t kIdleTimeoutNs = 60LL * 1000000000LL;
 // A request whose header has not completed this long after its first byte is dropped (a client
 // trickling a header must not hold a connection slot for the whole idle timeout).
@@ -85,6 +88,9 @@ struct Conn {
   uint32_t served = 0;  // requests answered on this connection (a scraper's keep-alive has > 0)
   void* ssl = nullptr;  // TLS session (HttpServer::set_tls), else plain
   bool hs = false;      // TLS handshake still in progress
+  // the last read stopped at the input cap: the session may hold decrypted bytes that no socket
+  // event will announce (they left the socket already), so the loop reads again once there is room
+  bool tls_more = false;
 };
 
 bool set_nonblock(int fd) {
@@ -595,6 +601,47 @@ void HttpServer::run(Loop* L) {
     }
     return true;
   };
+  // Reads what the connection has (up to the input cap) and answers it; false = close it.
+  // `readable`: the event announced input. A TLS session is always read: a record may sit in the
+  // socket since the handshake's last step, or decrypted bytes in the session (tls_more).
+  auto read_serve = [&](Conn& c, bool readable) -> bool {
+    while (true) {
+      bool peer_closed = false, capped = false;
+      if (readable || c.ssl) {
+        char buf[8192];
+        c.tls_more = false;
+        while (true) {
+          ssize_t r = rd(c, buf, sizeof buf);
+          if (r > 0) {
+            if (c.in.empty()) c.req_start_ns = mono_ns();
+            c.in.append(buf, static_cast<size_t>(r));
+            if (c.in.size() > kMaxInput) {
+              capped = true;
+              break;
+            }
+            continue;
+          }
+          if (r == 0) peer_closed = true;
+          else if (errno == EINTR) continue;
+          // a read error (a reset, a TLS protocol error): the connection is done. A failed TLS
+          // session reads nothing more from the socket, so level-triggered EPOLLIN would otherwise
+          // keep firing.
+          else if (errno != EAGAIN && errno != EWOULDBLOCK) peer_closed = true;
+          break;
+        }
+      }
+      if (!serve(c)) return false;
+      if (peer_closed && !c.writing) return false;
+      // A plain socket that stopped at the cap is readable again for level-triggered epoll. A TLS
+      // session is not: read on now that serve() made room, or once the pending response is out.
+      if (!capped || !c.ssl || c.closing) return true;
+      if (c.writing) {
+        c.tls_more = true;
+        return true;
+      }
+      if (c.in.size() > kMaxInput) return false;  // serve() consumed nothing (kMaxInput says it cannot)
+    }
+  };
 
   // accept() failing with EMFILE / ENFILE leaves the listening socket readable: level-triggered
   // epoll would report it again at once and the loop would spin. Stop watching it for a moment.
@@ -770,7 +817,7 @@ void HttpServer::run(Loop* L) {
           }
           if (!c.writing) {
             set_events(fd, EPOLLIN | EPOLLRDHUP);
-            if (!serve(c)) close_conn(fd);
+            if (c.tls_more ? !read_serve(c, false) : !serve(c)) close_conn(fd);
           }
         }
         continue;
@@ -799,31 +846,7 @@ void HttpServer::run(Loop* L) {
         if (r == 0 || (errno != EAGAIN && errno != EINTR)) close_conn(fd);
         continue;
       }
-      bool peer_closed = false;
-      // a TLS session is always read: a record may sit in the socket since the handshake's last step
-      if ((evs[i].events & (EPOLLIN | EPOLLRDHUP)) || c.ssl) {
-        char buf[8192];
-        while (true) {
-          ssize_t r = rd(c, buf, sizeof buf);
-          if (r > 0) {
-            if (c.in.empty()) c.req_start_ns = now;
-            c.in.append(buf, static_cast<size_t>(r));
-            if (c.in.size() > kMaxHeader * 4) break;
-            continue;
-          }
-          if (r == 0) peer_closed = true;
-          else if (errno == EINTR) continue;
-          // a read error (a reset, a TLS protocol error): the connection is done. A failed TLS session
-          // reads nothing more from the socket, so level-triggered EPOLLIN would otherwise keep firing.
-          else if (errno != EAGAIN && errno != EWOULDBLOCK) peer_closed = true;
-          break;
-        }
-      }
-      if (!serve(c)) {
-        close_conn(fd);
-        continue;
-      }
-      if (peer_closed && !c.writing) close_conn(fd);
+      if (!read_serve(c, (evs[i].events & (EPOLLIN | EPOLLRDHUP)) != 0)) close_conn(fd);
     }
     if (now - last_sweep > 1000000000LL) {
       last_sweep = now;

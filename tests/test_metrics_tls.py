@@ -426,3 +426,46 @@ def test_garbage_after_the_handshake_closes_the_connection(core, pki):
         assert ex.self_stats()["http_connections"] <= 1
     finally:
         ex.stop()
+
+
+@pytest.mark.parametrize("bodies,cap_at", [((60000, 33000, 0), 90112),  # this tree's cap (86016)
+                                            ((50000, 25000, 0), 73728)])  # a 64 KiB cap's
+def test_pipelined_input_over_the_buffer_cap_is_all_answered(core, pki, monkeypatch, bodies, cap_at):
+    """Pipelined requests with bodies, more than the per-connection input cap (80 KiB + 4 KiB) at
+    once. The loop stops reading at the cap; over TLS the session then holds the rest of the record
+    it was reading, decrypted bytes that no socket event announces (they left the socket). The
+    loop must read on after serving, or the last requests wait for the 10 s header timeout.
+    The input piles up while the server is busy writing a large /metrics response to a reader that
+    does not read (4 KiB buffers), so it is all there when the server turns to it."""
+    monkeypatch.setenv("GPUMON_HTTP_SNDBUF", "4096")
+    ex = core.Exporter({"backend": "mock:gpus=8", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                        "http_threads": 1, "gzip": False, "tls_cert_file": pki["server"],
+                        "tls_key_file": pki["server_key"]})
+    ex.start()
+    try:
+        want = ex.metrics_text().encode()
+
+        def req(n):
+            return b"GET /healthz HTTP/1.1\r\nHost: x\r\nContent-Length: %d\r\n\r\n" % n + b"b" * n
+        # the cap is crossed inside the last 16 KiB record (the loop reads 8 KiB at a time)
+        pipelined = b"".join(req(n) for n in bodies)
+        assert cap_at < len(pipelined) <= (cap_at // 16384 + 1) * 16384
+        raw = socket.create_connection(("127.0.0.1", ex.port), timeout=5)
+        raw.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+        raw.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 1 << 20)
+        s = _ctx(pki).wrap_socket(raw, server_hostname="localhost")
+        s.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n")
+        time.sleep(0.3)  # the server now waits on EPOLLOUT
+        s.sendall(pipelined)
+        time.sleep(0.2)
+        t0 = time.monotonic()
+        data = b""
+        while data.count(b"ok\n") < 3:
+            chunk = s.recv(65536)
+            assert chunk, data[-200:]
+            data += chunk
+        assert time.monotonic() - t0 < 3  # not held until the header timeout
+        assert data.count(b"HTTP/1.1 200") == 4 and want in data
+        s.close()
+    finally:
+        ex.stop()
