@@ -892,7 +892,7 @@ void Exporter::influx_loop() {
       body = std::move(push_q_.front());
       push_q_.pop_front();
     }
-    if (u.tls && mono_ns() >= tls_check_at) {
+    if (u.tls && (push_tls_check_now_.exchange(false) || mono_ns() >= tls_check_at)) {
       tls_check_at = mono_ns() + tls_period;
       if (const auto now = stamps(); now != tls_stamps) {
         tls_stamps = now;
@@ -942,6 +942,7 @@ void Exporter::influx_loop() {
 }
 
 void Exporter::reload_tls() {
+  push_tls_check_now_ = true;
   if (server_)
     if (TlsServer* t = server_->tls_server()) t->request_reload();
 }

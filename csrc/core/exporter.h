@@ -153,7 +153,8 @@ class Exporter {
   ~Exporter();
 
   bool start(std::string* err);       // backend init (retried later if it fails) + threads
-  // SIGHUP: re-check the TLS files of /metrics within a second (rotation is also picked up on its own).
+  // SIGHUP: re-check the TLS files of /metrics within a second, and the push's before its next batch
+  // (rotation is also picked up on its own: every 5 s / 30 s).
   void reload_tls();
   void stop();
   TickInfo tick();                    // one synchronous tick (manual mode or tests)
@@ -353,6 +354,7 @@ class Exporter {
   std::atomic<uint64_t> influx_ok_{0}, influx_fail_{0}, influx_dropped_{0};
   std::atomic<int> influx_up_{0};                 // the last push attempt succeeded
   std::atomic<int64_t> influx_last_ok_wall_ns_{0};
+  std::atomic<bool> push_tls_check_now_{false};   // reload_tls(): re-stamp the push's TLS files
 
   // per-device sampling workers + watchdog (dev_workers.cpp)
   void start_workers(int n);

@@ -431,13 +431,15 @@ def test_tls_slow_but_steady_server_is_served(core, pki):
     assert len(srv.posts) == 3 and len({p["peer"] for p in srv.posts}) == 1
 
 
-def test_push_picks_up_a_rotated_ca_without_a_restart(core, pki, tmp_path, monkeypatch):
+@pytest.mark.parametrize("trigger", ["period", "sighup"])
+def test_push_picks_up_a_rotated_ca_without_a_restart(core, pki, tmp_path, monkeypatch, trigger):
     """The InfluxDB server moves to a certificate from a new CA and the mounted CA file is replaced:
-    pushes fail verification until the exporter re-stamps its TLS files, then resume without a
-    restart, on a new connection."""
+    pushes fail verification until the exporter re-stamps its TLS files (on its period, or at once
+    after reload_tls(), the entry points' SIGHUP), then resume without a restart, on a new
+    connection."""
     import shutil
 
-    monkeypatch.setenv("GPUMON_TLS_RELOAD_S", "0.3")
+    monkeypatch.setenv("GPUMON_TLS_RELOAD_S", "0.3" if trigger == "period" else "3600")
     ca_file = tmp_path / "influx-ca.pem"
     shutil.copy(pki["otherca"], ca_file)  # the CA of the server's *next* certificate is not there yet
     with _TlsSink(pki["server"], pki["server_key"]) as srv:
@@ -451,6 +453,8 @@ def test_push_picks_up_a_rotated_ca_without_a_restart(core, pki, tmp_path, monke
             tmp = tmp_path / "influx-ca.pem.new"
             shutil.copy(pki["ca"], tmp)
             os.replace(tmp, ca_file)  # the kubelet's rename
+            if trigger == "sighup":
+                ex.reload_tls()
             assert _wait(lambda: len(srv.posts) >= 1, timeout=20.0), (ex.self_stats(), srv.handshake_errors[-2:])
             assert _wait(lambda: ex.self_stats()["influx_up"] == 1)
         finally:
