@@ -282,7 +282,7 @@ int main(int argc, char** argv) {
   }
   if (!err.empty()) GPUMON_LOG(LogLevel::kWarn, "main", "backend not ready (retrying): " + err);
   GPUMON_LOG(LogLevel::kInfo, "main",
-             "serving http://" + e.listen_desc() +
+             std::string("serving ") + (cfg.tls_cert_file.empty() ? "http://" : "https://") + e.listen_desc() +
                  "/metrics host=" + cfg.host + " interval=" + std::to_string(cfg.interval_s) + "s");
   while (!g_stop) {
     std::this_thread::sleep_for(std::chrono::milliseconds(200));
