@@ -118,6 +118,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "tls_cert_file", &c.tls_cert_file);
   get(d, "tls_key_file", &c.tls_key_file);
   get(d, "tls_client_ca_file", &c.tls_client_ca_file);
+  get(d, "http_auth_token_file", &c.http_auth_token_file);
   get(d, "init_retry_s", &c.init_retry_s);
   get(d, "health_stale_s", &c.health_stale_s);
   get(d, "reinit_after", &c.reinit_after);
@@ -785,6 +786,16 @@ PYBIND11_MODULE(_core, m) {
         return py::make_tuple(err, t ? t->not_after() : 0);
       },
       py::arg("cert_file"), py::arg("key_file"), py::arg("client_ca_file") = "");
+  m.def(
+      "read_token_file",
+      [](const std::string& path) {
+        std::string tok;
+        std::string err = read_token_file(path, &tok);
+        return py::make_tuple(err, tok);
+      },
+      py::arg("path"), "(error, token): the token file format http_auth_token_file reads");
+  m.def("check_auth_token_file", &check_auth_token_file, py::arg("path") = "",
+        "'' when the bearer-token file for /metrics is unset or holds a usable token, else the reason");
   m.def("check_serve_tls", &check_serve_tls, py::arg("cert_file") = "", py::arg("key_file") = "",
         py::arg("client_ca_file") = "", "configuration-time check of the /metrics HTTPS files: \"\" = usable");
   m.def("redact_url", &redact_url);
@@ -960,6 +971,9 @@ PYBIND11_MODULE(_core, m) {
              d["http_tls_not_after"] = s.http_tls_not_after;
              d["http_tls_reloads_ok"] = s.http_tls_reloads_ok;
              d["http_tls_reloads_failed"] = s.http_tls_reloads_failed;
+             d["http_auth_failures"] = s.http_auth_failures;
+             d["http_auth_reloads_ok"] = s.http_auth_reloads_ok;
+             d["http_auth_reloads_failed"] = s.http_auth_reloads_failed;
              d["hidden_contexts"] = s.hidden_contexts;
              d["hidden_peer_contexts"] = s.hidden_peer_contexts;
              d["rt_threads"] = s.rt_threads;

@@ -198,6 +198,14 @@ bool Exporter::start(std::string* err) {
     if (err) *err = backend_error();
     return false;
   }
+  if (cfg_.serve_http && !cfg_.http_auth_token_file.empty()) {
+    std::string e;
+    auth_ = TokenAuth::create(cfg_.http_auth_token_file, &e);
+    if (!auth_) {
+      if (err) *err = e;
+      return false;
+    }
+  }
   if (cfg_.serve_http) {
     server_ = std::make_unique<HttpServer>(
         cfg_.listen_addr, cfg_.port, cfg_.http_threads,
@@ -943,6 +951,7 @@ void Exporter::influx_loop() {
 
 void Exporter::reload_tls() {
   push_tls_check_now_ = true;
+  if (auth_) auth_->request_reload();
   if (server_)
     if (TlsServer* t = server_->tls_server()) t->request_reload();
 }
@@ -1052,6 +1061,11 @@ SelfStats Exporter::self_stats() const {
       s.http_tls_reloads_ok = t->reloads_ok();
       s.http_tls_reloads_failed = t->reloads_failed();
     }
+  }
+  if (auth_) {
+    s.http_auth_failures = static_cast<int64_t>(auth_failures_.load(std::memory_order_relaxed));
+    s.http_auth_reloads_ok = auth_->reloads_ok();
+    s.http_auth_reloads_failed = auth_->reloads_failed();
   }
   if (cfg_.http_rt_priority > 0 && server_) {
     s.http_rt_loops = server_->rt_loops();

@@ -24,6 +24,7 @@
 #include "attribution.h"
 #include "docker_lite.h"
 #include "backend.h"
+#include "http_auth.h"
 #include "http_server.h"
 #include "rates.h"
 #include "render.h"
@@ -50,6 +51,9 @@ struct ExporterConfig {
   double http_rt_budget = 0.2;        // ... at most this share of a CPU per loop per 100 ms window, then demoted
   // /metrics over HTTPS: PEM certificate chain + key; a client CA makes it mutual TLS (tls.h TlsServer)
   std::string tls_cert_file, tls_key_file, tls_client_ca_file;
+  // /metrics answers only requests with "Authorization: Bearer <the file's token>" (http_auth.h);
+  // the health endpoints stay open for the kubelet's probes
+  std::string http_auth_token_file;
   std::string host = "no_name";       // NODE_NAME (reference fallback "no_name", gpu.py:23-24)
   bool gzip = true;
   bool roctx = false;                 // ROCTx ranges around sampler phases (also GPUMON_ROCTX=1)
@@ -355,6 +359,8 @@ class Exporter {
   std::atomic<int> influx_up_{0};                 // the last push attempt succeeded
   std::atomic<int64_t> influx_last_ok_wall_ns_{0};
   std::atomic<bool> push_tls_check_now_{false};   // reload_tls(): re-stamp the push's TLS files
+  std::shared_ptr<TokenAuth> auth_;               // http_auth_token_file (nullptr: /metrics is open)
+  std::atomic<uint64_t> auth_failures_{0};        // /metrics requests refused with 401
 
   // per-device sampling workers + watchdog (dev_workers.cpp)
   void start_workers(int n);

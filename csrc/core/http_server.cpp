@@ -58,6 +58,7 @@ const char* status_text(int s) {
   switch (s) {
     case 200: return "OK";
     case 400: return "Bad Request";
+    case 401: return "Unauthorized";
     case 404: return "Not Found";
     case 405: return "Method Not Allowed";
     case 413: return "Payload Too Large";
@@ -119,6 +120,7 @@ long parse_request(const std::string& in, HttpRequest* r) {
   r->query = q == std::string_view::npos ? "" : std::string(target.substr(q + 1));
   r->keep_alive = ver == "HTTP/1.1";
   r->accept_gzip = false;
+  r->authorization.clear();
   size_t pos = le + 2;
   long content_len = 0;
   while (pos < end) {
@@ -139,6 +141,8 @@ long parse_request(const std::string& in, HttpRequest* r) {
         std::string v(val);
         for (auto& ch : v) ch = static_cast<char>(tolower(ch));
         r->accept_gzip = v.find("gzip") != std::string::npos;
+      } else if (ieq(name, "authorization")) {
+        r->authorization.assign(val);
       } else if (ieq(name, "content-length")) {
         const std::string v(val);
         char* endp = nullptr;

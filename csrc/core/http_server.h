@@ -30,6 +30,7 @@ struct HttpRequest {
   std::string query;
   bool keep_alive = true;
   bool accept_gzip = false;
+  std::string authorization;  // the Authorization header's value (http_auth_token_file)
 };
 
 struct HttpResponse {

@@ -266,6 +266,7 @@ const std::map<std::string, Setter>& setters() {
       {"tls_cert_file", str_at([](NativeOptions* o) { return &o->cfg.tls_cert_file; })},
       {"tls_key_file", str_at([](NativeOptions* o) { return &o->cfg.tls_key_file; })},
       {"tls_client_ca_file", str_at([](NativeOptions* o) { return &o->cfg.tls_client_ca_file; })},
+      {"http_auth_token_file", str_at([](NativeOptions* o) { return &o->cfg.http_auth_token_file; })},
       {"influx_tls_insecure", bool_at([](NativeOptions* o) { return &o->cfg.influx_tls_insecure; })},
       {"influx_client_cert", str_at([](NativeOptions* o) { return &o->cfg.influx_client_cert; })},
       {"influx_client_key", str_at([](NativeOptions* o) { return &o->cfg.influx_client_key; })},
@@ -551,6 +552,7 @@ std::string options_json(const NativeOptions& o) {
   S("tls_cert_file", c.tls_cert_file);
   S("tls_key_file", c.tls_key_file);
   S("tls_client_ca_file", c.tls_client_ca_file);
+  S("http_auth_token_file", c.http_auth_token_file);
   B("influx_tls_insecure", c.influx_tls_insecure);
   S("influx_client_cert", c.influx_client_cert);
   S("influx_client_key", c.influx_client_key);

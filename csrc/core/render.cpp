@@ -875,6 +875,21 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       f.add(hl, {{"result", "ok"}}, static_cast<double>(s.http_tls_reloads_ok));
       f.add(hl, {{"result", "error"}}, static_cast<double>(s.http_tls_reloads_failed));
     }
+    if (s.http_auth_failures >= 0) {
+      {
+        Family f(o, "gpumon_http_auth_failures_total",
+                 "/metrics requests refused with 401 (http_auth_token_file): no Authorization header, another "
+                 "scheme than Bearer, or a token that is not the file's.",
+                 "counter");
+        f.add(hl, static_cast<double>(s.http_auth_failures));
+      }
+      Family f(o, "gpumon_http_auth_token_reloads_total",
+               "Changes of http_auth_token_file seen: result=ok the new token is required from the next request, "
+               "result=error not usable (the previous token stays in force).",
+               "counter");
+      f.add(hl, {{"result", "ok"}}, static_cast<double>(s.http_auth_reloads_ok));
+      f.add(hl, {{"result", "error"}}, static_cast<double>(s.http_auth_reloads_failed));
+    }
     if (s.http_rt_loops >= 0) {
       {
         Family f(o, "gpumon_http_rt_loops",

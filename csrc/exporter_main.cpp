@@ -40,6 +40,7 @@ static void usage() {
           "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
           "                       [--influx-ca-file PEM] [--influx-tls-insecure] [--influx-client-cert PEM --influx-client-key PEM]\n"
           "                       [--tls-cert-file PEM --tls-key-file PEM [--tls-client-ca-file PEM]]  (/metrics over HTTPS)\n"
+          "                       [--http-auth-token-file FILE]  (/metrics needs Authorization: Bearer <token>)\n"
           "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
           "                       [--pod-labels KEY,KEY..]\n"
           "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--ras-slices N] [--no-gzip] [--metrics-include GLOBS] [--metrics-exclude GLOBS] [--sample-threads N] [--rt-priority N] [--prewarm-ms MS]\n"
@@ -121,6 +122,7 @@ int main(int argc, char** argv) {
     else if (a == "--tls-cert-file") set("tls_cert_file", next());
     else if (a == "--tls-key-file") set("tls_key_file", next());
     else if (a == "--tls-client-ca-file") set("tls_client_ca_file", next());
+    else if (a == "--http-auth-token-file") set("http_auth_token_file", next());
     else if (a == "--influx-tls-insecure") set("influx_tls_insecure", "true");
     else if (a == "--influx-client-cert") set("influx_client_cert", next());
     else if (a == "--influx-client-key") set("influx_client_key", next());
@@ -209,6 +211,11 @@ int main(int argc, char** argv) {
     const std::string serr = check_serve_tls(cfg.tls_cert_file, cfg.tls_key_file, cfg.tls_client_ca_file);
     if (!serr.empty()) {
       fprintf(stderr, "config: %s\n", serr.c_str());
+      return 2;
+    }
+    // /metrics behind a bearer token: the token file must hold one
+    if (const std::string aerr = check_auth_token_file(cfg.http_auth_token_file); !aerr.empty()) {
+      fprintf(stderr, "config: http_auth_token_file: %s\n", aerr.c_str());
       return 2;
     }
   }

@@ -2,7 +2,7 @@
 
     gpumon serve   [--backend amdsmi] [--interval 1] [--listen :9400] ...           run the exporter
     gpumon once    [--format prom|influx|json]                                       one sample to stdout
-    gpumon top     [--interval 1] [--url HOST:PORT ... [--ca-file PEM]]              live console table
+    gpumon top     [--interval 1] [--url HOST:PORT ... [--ca-file PEM] [--token-file F]]  live console table
     gpumon scrape  URL [-n 1000] [-c 4]                                              scrape-latency probe
     gpumon probe   [--blocks 1024]                                                   run the K1 probe once
     gpumon load    [--kind mixed --seconds 10]                                       synthetic gfx950 load
@@ -169,10 +169,18 @@ def _top_remote(args) -> int:
 
     urls = [u if "://" in u else f"http://{u}" for u in args.url]
     urls = [u if u.rstrip("/").endswith("/metrics") else u.rstrip("/") + "/metrics" for u in urls]
+    token = ""
+    if args.token_file:
+        from ._native import core
+
+        err, token = core().read_token_file(args.token_file)
+        if err:
+            sys.stderr.write(f"--token-file: {err}\n")
+            return 2
     n, rc = 0, 0
     while args.iterations <= 0 or n < args.iterations:
         t0 = time.monotonic()
-        frames, errors = fleet.fetch(urls, ca_file=args.ca_file)
+        frames, errors = fleet.fetch(urls, ca_file=args.ca_file, token=token)
         text = fleet.render(frames, errors)
         if sys.stdout.isatty():
             sys.stdout.write("\x1b[2J\x1b[H")
@@ -281,6 +289,8 @@ def build_parser() -> argparse.ArgumentParser:
                    help="exporter to read instead of the local GPUs (HOST:PORT or URL; repeat for a fleet view)")
     s.add_argument("--ca-file", default="",
                    help="https:// exporters (tls_cert_file): the PEM CA to verify them with (default: system bundle)")
+    s.add_argument("--token-file", default="",
+                   help="exporters with http_auth_token_file: the file holding their bearer token")
     s.set_defaults(fn=cmd_top)
     s = sub.add_parser("scrape", help="measure /metrics latency")
     s.add_argument("url")

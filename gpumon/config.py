@@ -61,6 +61,7 @@ class Config:
     tls_cert_file: str = ""               # /metrics over HTTPS: PEM certificate chain (with tls_key_file)
     tls_key_file: str = ""                # ... its PEM private key
     tls_client_ca_file: str = ""          # ... mutual TLS: scrapers must present a certificate signed by this CA
+    http_auth_token_file: str = ""        # /metrics needs "Authorization: Bearer <the file's token>" (health endpoints stay open)
     host: str = ""
     gzip: bool = True
     compat_families: bool = True
@@ -175,6 +176,7 @@ class Config:
             "tls_cert_file": self.tls_cert_file,
             "tls_key_file": self.tls_key_file,
             "tls_client_ca_file": self.tls_client_ca_file,
+            "http_auth_token_file": self.http_auth_token_file,
             "host": self.resolved_host(),
             "gzip": self.gzip,
             "roctx": self.roctx,
@@ -225,6 +227,12 @@ class Config:
             err = core().check_serve_tls(self.tls_cert_file, self.tls_key_file, self.tls_client_ca_file)
             if err:
                 raise ConfigError(err)
+        if self.http_auth_token_file:
+            from ._native import core
+
+            err = core().check_auth_token_file(self.http_auth_token_file)
+            if err:
+                raise ConfigError("http_auth_token_file: " + err)
         try:
             _device_ids(self.devices)
         except ValueError as e:
@@ -437,6 +445,8 @@ def add_cli_args(p: argparse.ArgumentParser) -> None:
     p.add_argument("--tls-key-file", dest="tls_key_file", help="... and its PEM private key")
     p.add_argument("--tls-client-ca-file", dest="tls_client_ca_file",
                    help="mutual TLS: scrapers must present a certificate signed by this PEM CA")
+    p.add_argument("--http-auth-token-file", dest="http_auth_token_file",
+                   help="/metrics needs 'Authorization: Bearer <token>', the token read from this file")
     p.add_argument("--prewarm-ms", dest="prewarm_ms", type=float,
                    help="device workers warm the firmware-table read this long before each tick (0 = off)")
     p.add_argument("--device-timeout", dest="device_timeout_s", type=float,

@@ -249,6 +249,19 @@ def serve_tls_check(cfg, now=None) -> tuple:
     return (OK, f"{cfg.tls_cert_file}{mtls}: valid until {when} ({days:.0f} days)")
 
 
+def auth_token_check(cfg) -> tuple:
+    """/metrics behind a bearer token: the file holds a usable token (the startup check)."""
+    from ._native import core as _core
+
+    err, token = _core().read_token_file(cfg.http_auth_token_file)
+    if err:
+        return (FAIL, err + ": the exporter refuses to start with it")
+    weak = len(token) < 16
+    return ((WARN, f"{cfg.http_auth_token_file}: a {len(token)}-character token: use 16 or more random characters")
+            if weak else (OK, f"{cfg.http_auth_token_file}: a {len(token)}-character token; /metrics answers 401 "
+                              "without it"))
+
+
 def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
     """[(check, status, detail)] for the node this runs on, with the exporter configured as `cfg`."""
     from .monitor import GpuMonitor
@@ -259,6 +272,9 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
     if cfg.tls_cert_file or cfg.tls_key_file or cfg.tls_client_ca_file:
         out.append(("/metrics TLS certificate",) + serve_tls_check(cfg))
         cfg.tls_cert_file = cfg.tls_key_file = cfg.tls_client_ca_file = ""  # the checks below serve plain
+    if cfg.http_auth_token_file:
+        out.append(("/metrics bearer token",) + auth_token_check(cfg))
+        cfg.http_auth_token_file = ""  # ... and scrape without a token
     if cfg.influx_url:
         out.append(("Influx push",) + influx_check(cfg))
         cfg.influx_url = ""  # checked above; the checks below do not push

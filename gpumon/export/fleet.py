@@ -106,19 +106,21 @@ def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
 
 
 def fetch(urls: List[str], timeout_s: float = 3.0, workers: int = 16,
-          ca_file: str = "") -> Tuple[List[dict], Dict[str, str]]:
+          ca_file: str = "", token: str = "") -> Tuple[List[dict], Dict[str, str]]:
     """GET every exporter's /metrics (native HTTP client, which releases the GIL) from up to
     `workers` threads at once, so a refresh over many nodes takes about one node's time even when
     some of them time out; frames keep the order of `urls`. Parse failures are reported, not raised.
-    https:// URLs (exporters serving TLS) are verified against `ca_file`, else the system bundle."""
+    https:// URLs (exporters serving TLS) are verified against `ca_file`, else the system bundle.
+    `token`: sent as "Authorization: Bearer <token>" (exporters with http_auth_token_file)."""
     from concurrent.futures import ThreadPoolExecutor
 
     from .._native import core
 
     c = core()
+    headers = f"Authorization: Bearer {token}\r\n" if token else ""
 
     def one(u):
-        return c.http_request("GET", u, "", "", timeout_s, ca_file)
+        return c.http_request("GET", u, "", headers, timeout_s, ca_file)
 
     with ThreadPoolExecutor(max_workers=max(1, min(workers, len(urls) or 1))) as pool:
         answers = list(pool.map(one, urls))

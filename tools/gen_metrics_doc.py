@@ -168,6 +168,16 @@ def collect():
             ex.tick()
             add(_families(ex), "tls_cert_file")
             ex.stop()
+    # /metrics behind a bearer token (http_auth_token_file)
+    with tempfile.TemporaryDirectory() as d:
+        with open(f"{d}/token", "w") as f:
+            f.write("doc-token\n")
+        ex = c.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                         "host": "node", "http_auth_token_file": f"{d}/token"})
+        ex.start()
+        ex.tick()
+        add(_families(ex), "http_auth_token_file")
+        ex.stop()
     # backend-specific self-metrics: the libamd_smi backend over the fake library
     saved = os.environ.get("FAKE_AMDSMI_GPUS")  # the fake reads it at init; leave the caller's env as it was
     os.environ["FAKE_AMDSMI_GPUS"] = "1"
