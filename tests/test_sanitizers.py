@@ -31,8 +31,9 @@ def _free_port():
     return p
 
 
-def _run(binary, env_extra, extra_args=(), min_s=0.0, ctx=None, port=None):
-    """ctx: an ssl.SSLContext to scrape over HTTPS (the exporter started with --tls-cert-file)."""
+def _run(binary, env_extra, extra_args=(), min_s=0.0, ctx=None, port=None, token=None):
+    """ctx: an ssl.SSLContext to scrape over HTTPS (the exporter started with --tls-cert-file);
+    token: the bearer token to scrape with (--http-auth-token-file)."""
     port = port or _free_port()
     base = f"https://localhost:{port}" if ctx else f"http://127.0.0.1:{port}"
     t_start = time.time()
@@ -53,7 +54,8 @@ def _run(binary, env_extra, extra_args=(), min_s=0.0, ctx=None, port=None):
         def hammer(query):
             for _ in range(60):
                 try:
-                    req = urllib.request.Request(f"{base}/metrics{query}", headers={"Accept-Encoding": "gzip"})
+                    hdr = {"Accept-Encoding": "gzip", **({"Authorization": f"Bearer {token}"} if token else {})}
+                    req = urllib.request.Request(f"{base}/metrics{query}", headers=hdr)
                     urllib.request.urlopen(req, timeout=5, context=ctx).read()
                 except Exception as e:  # noqa: BLE001
                     errors.append(e)
@@ -432,8 +434,10 @@ def test_sanitized_https_serving(target, binary, env, tmp_path):
     """/metrics over HTTPS (csrc/core/tls.cpp TlsServer, the TLS branch of the HTTP loops) under
     ASan+UBSan and TSan: two loops serving concurrent verified scrapes and per-request filters over
     TLS, failed handshakes (plain HTTP and an untrusted scraper) mixed in, and the certificate files
-    replaced every 0.15 s, so contexts are swapped while both loops create sessions. No sanitizer
-    report."""
+    replaced every 0.15 s, so contexts are swapped while both loops create sessions. A bearer token
+    guards /metrics too: its file is replaced as often (the same token, so every stamp change is a
+    reload while both loops check requests), and requests with a wrong token are mixed in. No
+    sanitizer report."""
     import ssl
 
     from conftest import make_locked
@@ -462,6 +466,12 @@ def test_sanitized_https_serving(target, binary, env, tmp_path):
                         urllib.request.urlopen(f"https://localhost:{port}/metrics", timeout=1, context=c)
                 except Exception:  # noqa: BLE001 -- refused by design
                     pass
+                try:  # a trusted scraper with the wrong token (401)
+                    urllib.request.urlopen(urllib.request.Request(f"https://localhost:{port}/metrics",
+                                                                  headers={"Authorization": "Bearer nope"}),
+                                           timeout=1, context=ctx)
+                except Exception:  # noqa: BLE001 -- refused by design
+                    pass
             time.sleep(0.02)
 
     import shutil
@@ -469,10 +479,13 @@ def test_sanitized_https_serving(target, binary, env, tmp_path):
     os.makedirs(f"{d}/live")
     for src, dst in (("server.pem", "tls.crt"), ("server.key", "tls.key")):
         shutil.copy(f"{d}/{src}", f"{d}/live/{dst}")
+    with open(f"{d}/token", "w") as f:
+        f.write("sanitizer-token-0123456789\n")
+    shutil.copy(f"{d}/token", f"{d}/live/token")
 
     def rotator():  # the kubelet's rename of the Secret's files, over and over: reloads while serving
         while not stop.is_set():
-            for src, dst in (("server.pem", "tls.crt"), ("server.key", "tls.key")):
+            for src, dst in (("server.pem", "tls.crt"), ("server.key", "tls.key"), ("token", "token")):
                 shutil.copy(f"{d}/{src}", f"{d}/live/{dst}.new")
                 os.replace(f"{d}/live/{dst}.new", f"{d}/live/{dst}")
             time.sleep(0.15)
@@ -482,8 +495,9 @@ def test_sanitized_https_serving(target, binary, env, tmp_path):
         t.start()
     try:
         rc, err = _run(os.path.join(ROOT, binary), dict(env, GPUMON_TLS_RELOAD_S="0.1"),
-                       ("--tls-cert-file", f"{d}/live/tls.crt", "--tls-key-file", f"{d}/live/tls.key"), min_s=1.5,
-                       ctx=ctx, port=port)
+                       ("--tls-cert-file", f"{d}/live/tls.crt", "--tls-key-file", f"{d}/live/tls.key",
+                        "--http-auth-token-file", f"{d}/live/token"), min_s=1.5,
+                       ctx=ctx, port=port, token="sanitizer-token-0123456789")
     finally:
         stop.set()
         for t in ts:
