@@ -789,11 +789,11 @@ PYBIND11_MODULE(_core, m) {
   m.def(
       "read_token_file",
       [](const std::string& path) {
-        std::string tok;
-        std::string err = read_token_file(path, &tok);
-        return py::make_tuple(err, tok);
+        std::vector<std::string> toks;
+        std::string err = read_token_file(path, &toks);
+        return py::make_tuple(err, toks.empty() ? std::string() : toks.front(), toks);
       },
-      py::arg("path"), "(error, token): the token file format http_auth_token_file reads");
+      py::arg("path"), "(error, first token, all tokens): the token file format http_auth_token_file reads");
   m.def("check_auth_token_file", &check_auth_token_file, py::arg("path") = "",
         "'' when the bearer-token file for /metrics is unset or holds a usable token, else the reason");
   m.def("check_serve_tls", &check_serve_tls, py::arg("cert_file") = "", py::arg("key_file") = "",

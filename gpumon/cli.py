@@ -173,7 +173,7 @@ def _top_remote(args) -> int:
     if args.token_file:
         from ._native import core
 
-        err, token = core().read_token_file(args.token_file)
+        err, token, _ = core().read_token_file(args.token_file)  # the first line's token
         if err:
             sys.stderr.write(f"--token-file: {err}\n")
             return 2

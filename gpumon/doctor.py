@@ -253,13 +253,15 @@ def auth_token_check(cfg) -> tuple:
     """/metrics behind a bearer token: the file holds a usable token (the startup check)."""
     from ._native import core as _core
 
-    err, token = _core().read_token_file(cfg.http_auth_token_file)
+    err, _, tokens = _core().read_token_file(cfg.http_auth_token_file)
     if err:
         return (FAIL, err + ": the exporter refuses to start with it")
-    weak = len(token) < 16
-    return ((WARN, f"{cfg.http_auth_token_file}: a {len(token)}-character token: use 16 or more random characters")
-            if weak else (OK, f"{cfg.http_auth_token_file}: a {len(token)}-character token; /metrics answers 401 "
-                              "without it"))
+    short = min(len(t) for t in tokens)
+    which = f"{len(tokens)} tokens accepted (a rotation in progress?)" if len(tokens) > 1 else "1 token"
+    if short < 16:
+        return (WARN, f"{cfg.http_auth_token_file}: {which}, one of {short} characters: use 16 or more random "
+                      "characters")
+    return (OK, f"{cfg.http_auth_token_file}: {which}; /metrics answers 401 without it")
 
 
 def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:

@@ -101,8 +101,37 @@ def test_unusable_token_files_fail_at_startup(core, tmp_path, content, want):
 
 def test_token_file_format(core, tmp_path):
     p = tmp_path / "t"
-    p.write_text("  abc.DEF-123~+/=  \r\nsecond line ignored\n")  # kubectl create secret keeps a trailing newline
-    assert core.read_token_file(str(p)) == ("", "abc.DEF-123~+/=")
+    p.write_text("  abc.DEF-123~+/=  \r\n")  # kubectl create secret keeps a trailing newline
+    assert core.read_token_file(str(p)) == ("", "abc.DEF-123~+/=", ["abc.DEF-123~+/="])
+    p.write_text("first\n\n  second \n")  # one token per line, blank lines skipped
+    assert core.read_token_file(str(p)) == ("", "first", ["first", "second"])
+    p.write_text("".join(f"t{i}\n" for i in range(17)))
+    assert "more than 16 tokens" in core.read_token_file(str(p))[0]
+    p.write_text("ok\nnot ok\n")
+    assert "not visible ASCII" in core.read_token_file(str(p))[0]
+
+
+def test_rotation_with_an_overlap_refuses_no_scrape(mock_exporter, tmp_path, monkeypatch):
+    """The zero-downtime rotation: the new token is added as a second line, the scraper moves to it,
+    the old line is dropped. A scraper on either token is served at every step."""
+    monkeypatch.setenv("GPUMON_TLS_RELOAD_S", "0.1")
+    p = tmp_path / "token"
+    p.write_text("token-a\n")
+    ex = mock_exporter(http_auth_token_file=str(p), http_threads=2)
+    ex.tick()
+
+    def swap(text, scraper):  # the scraper keeps scraping (a reload happens inside a request)
+        tmp = tmp_path / "token.new"
+        tmp.write_text(text)
+        os.replace(tmp, p)
+        n = ex.self_stats()["http_auth_reloads_ok"]
+        assert _wait(lambda: _get(ex.port, scraper)[0] == 200 and ex.self_stats()["http_auth_reloads_ok"] > n)
+
+    swap("token-a\ntoken-b\n", "token-a")
+    assert _get(ex.port, "token-a")[0] == 200 and _get(ex.port, "token-b")[0] == 200
+    swap("token-b\n", "token-b")  # the scraper moved to the new token
+    assert _get(ex.port, "token-a")[0] == 401 and _get(ex.port, "token-b")[0] == 200
+    assert ex.self_stats()["http_auth_failures"] == 1
 
 
 @pytest.mark.parametrize("trigger", ["period", "sighup"])
@@ -225,6 +254,9 @@ def test_doctor_checks_the_token_file(tmp_path):
     p = tmp_path / "token"
     p.write_text("0123456789abcdef0123\n")
     assert auth_token_check(Config(http_auth_token_file=str(p)))[0] == OK
+    p.write_text("0123456789abcdef0123\nabcdef0123456789abcd\n")
+    st, detail = auth_token_check(Config(http_auth_token_file=str(p)))
+    assert st == OK and "2 tokens accepted" in detail
     p.write_text("short\n")
     assert auth_token_check(Config(http_auth_token_file=str(p)))[0] == WARN
     p.write_text("\n")
