@@ -14,7 +14,9 @@ gap in the sink's tick sequence.
 
 With `--serve-tls` the exporter also serves /metrics over HTTPS, and the scraper verifies it. With
 `--rotate-every S` the serving certificate is re-issued and swapped into place every S seconds, the
-way the kubelet updates a mounted Secret, while scrapes run.
+way the kubelet updates a mounted Secret, while scrapes run. With `--token` /metrics also needs a
+bearer token; on each rotation the token is replaced with an overlap (old and new line, the
+scraper moves to the new one, the old line goes), which must refuse no scrape.
 
 On a GPU box: `--backend amdsmi` (default) next to the mixed K2 load. On CPU: `--backend mock`.
 """
@@ -124,12 +126,17 @@ def proc_stats(pid):
             "threads": len(os.listdir(f"/proc/{pid}/task"))}
 
 
-def push_counters(port, ctx=None):
+def _auth(token):
+    return {"Authorization": f"Bearer {token['value']}"} if token and token.get("value") else {}
+
+
+def push_counters(port, ctx=None, token=None):
     from gpumon.export import promtext
 
     c = (http.client.HTTPSConnection("localhost", port, context=ctx, timeout=5) if ctx
          else http.client.HTTPConnection("127.0.0.1", port, timeout=5))
-    c.request("GET", "/metrics?include=gpumon_influx_*,gpumon_ticks_total,gpumon_http_tls_*")
+    c.request("GET", "/metrics?include=gpumon_influx_*,gpumon_ticks_total,gpumon_http_tls_*,gpumon_http_auth_*",
+              headers=_auth(token))
     fam = promtext.parse(c.getresponse().read().decode())
     c.close()
     out = {"ticks": promtext.one(fam, "gpumon_ticks_total"), "influx_up": promtext.one(fam, "gpumon_influx_up")}
@@ -139,12 +146,16 @@ def push_counters(port, ctx=None):
         out["tls_handshake_failures"] = promtext.one(fam, "gpumon_http_tls_handshake_failures_total")
         for _, labels, v in fam.get("gpumon_http_tls_reloads_total", {}).get("samples", []):
             out["tls_reloads_" + labels.get("result", "?")] = v
+    if token:
+        out["auth_failures"] = promtext.one(fam, "gpumon_http_auth_failures_total")
+        for _, labels, v in fam.get("gpumon_http_auth_token_reloads_total", {}).get("samples", []):
+            out["auth_reloads_" + labels.get("result", "?")] = v
     return out
 
 
-def tls_scrapes(port, ctx, seconds, rate_hz):
+def tls_scrapes(port, ctx, seconds, rate_hz, token=None):
     """Verified HTTPS scrapes with gzip over one keep-alive connection (reopened after an error),
-    paced at rate_hz: (latencies, errors)."""
+    paced at rate_hz, with the bearer token current at each request: (latencies, errors)."""
     lat, errors, conn = [], 0, None
     period, t_next, end = 1.0 / rate_hz, time.monotonic(), time.monotonic() + seconds
     while time.monotonic() < end:
@@ -154,7 +165,7 @@ def tls_scrapes(port, ctx, seconds, rate_hz):
             if conn is None:
                 conn = http.client.HTTPSConnection("localhost", port, context=ctx, timeout=5)
             t = time.perf_counter()
-            conn.request("GET", "/metrics", headers={"Accept-Encoding": "gzip"})
+            conn.request("GET", "/metrics", headers={"Accept-Encoding": "gzip", **_auth(token)})
             r = conn.getresponse()
             r.read()
             if r.status != 200:
@@ -182,7 +193,11 @@ def main():
     ap.add_argument("--serve-tls", action="store_true", help="serve /metrics over HTTPS and scrape it verified")
     ap.add_argument("--rotate-every", type=float, default=0.0,
                     help="with --serve-tls: re-issue and swap the serving certificate every S seconds (0 = never)")
+    ap.add_argument("--token", action="store_true",
+                    help="with --serve-tls: /metrics needs a bearer token, rotated with an overlap at each rotation")
     a = ap.parse_args()
+    if a.token and not a.serve_tls:
+        raise SystemExit("push_soak: --token needs --serve-tls")
     if shutil.which("openssl") is None:
         raise SystemExit("push_soak: the openssl CLI is needed for the test CA")
 
@@ -206,7 +221,8 @@ def main():
     args = [os.path.join(ROOT, "bin", "gpumon-exporter"), "--backend", a.backend, "--interval", str(a.interval),
             "--listen", f"127.0.0.1:{port}", "--log-level", "error"]
     ctx = None
-    rotations = 0
+    rotations = token_rotations = 0
+    token = {"value": "soak-token-0000000000000000"} if a.token else None
     stop_rotation = threading.Event()
     if a.serve_tls:
         live = os.path.join(tmp, "live")
@@ -215,14 +231,34 @@ def main():
         shutil.copy(pki["server_key"], os.path.join(live, "tls.key"))
         args += ["--tls-cert-file", os.path.join(live, "tls.crt"), "--tls-key-file", os.path.join(live, "tls.key")]
         ctx = ssl.create_default_context(cafile=pki["ca"])
+        tok_file = os.path.join(live, "token")
+
+        def put_token(text):  # the kubelet's rename of the Secret's file
+            with open(tok_file + ".new", "w") as f:
+                f.write(text)
+            os.replace(tok_file + ".new", tok_file)
+
+        if token:
+            put_token(token["value"] + "\n")
+            args += ["--http-auth-token-file", tok_file]
 
         def rotate():  # a renewal: same key, new certificate, renamed into place
-            nonlocal rotations
+            nonlocal rotations, token_rotations
             while a.rotate_every > 0 and not stop_rotation.wait(a.rotate_every):
                 _openssl("x509", "-req", "-in", "server.csr", "-CA", "ca.pem", "-CAkey", "ca.key", "-CAcreateserial",
                          "-days", "2", "-out", os.path.join(live, "tls.crt.new"), "-extfile", "server.ext", cwd=tmp)
                 os.replace(os.path.join(live, "tls.crt.new"), os.path.join(live, "tls.crt"))
                 rotations += 1
+                if token:  # overlap: both tokens, the scraper moves, then only the new one
+                    new = f"soak-token-{rotations:016d}"
+                    put_token(f"{token['value']}\n{new}\n")
+                    if stop_rotation.wait(2.5):  # > 2 reload periods (GPUMON_TLS_RELOAD_S=1)
+                        break
+                    token["value"] = new
+                    if stop_rotation.wait(2.5):
+                        break
+                    put_token(new + "\n")
+                    token_rotations += 1
 
         threading.Thread(target=rotate, daemon=True).start()
     ex = subprocess.Popen(args, env=env, stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "exporter.err"), "wb"))
@@ -231,7 +267,7 @@ def main():
         deadline = time.monotonic() + 30
         while time.monotonic() < deadline:
             try:
-                push_counters(port, ctx)
+                push_counters(port, ctx, token)
                 break
             except (OSError, KeyError, ValueError):
                 time.sleep(0.1)
@@ -240,7 +276,7 @@ def main():
         t0 = time.monotonic()
         while time.monotonic() < end and ex.poll() is None:
             if ctx:
-                got, nerr = tls_scrapes(port, ctx, a.window, a.scrape_rate)
+                got, nerr = tls_scrapes(port, ctx, a.window, a.scrape_rate, token)
                 r = {"latencies_s": got, "errors": nerr}
             else:
                 r = core.scrape_load("127.0.0.1", port, "/metrics", n_requests=0, duration_s=a.window, concurrency=1,
@@ -249,8 +285,8 @@ def main():
             with sink.lock:
                 sk = {"sink_posts": sink.posts, "sink_requests": sink.requests, "sink_handshakes": sink.handshakes,
                       "sink_node_lines": sink.node_lines, "sink_reordered": sink.reordered}
-            w = dict(proc_stats(ex.pid), t_min=round((time.monotonic() - t0) / 60, 2), **push_counters(port, ctx), **sk,
-                     rotations=rotations,
+            w = dict(proc_stats(ex.pid), t_min=round((time.monotonic() - t0) / 60, 2), **push_counters(port, ctx, token),
+                     **sk, rotations=rotations, token_rotations=token_rotations,
                      scrapes=len(lat), scrape_errors=r.get("errors", 0),
                      scrape_p99_ms=round(lat[int(0.99 * (len(lat) - 1))] * 1e3, 3) if lat else None)
             windows.append(w)
@@ -287,6 +323,8 @@ def main():
         "close_every": a.close_every, "fail_every": a.fail_every,
         "serve_tls": a.serve_tls, "rotations": rotations, "tls_reloads_ok": last.get("tls_reloads_ok"),
         "tls_reloads_error": last.get("tls_reloads_error"), "tls_handshake_failures": last.get("tls_handshake_failures"),
+        "token": a.token, "token_rotations": token_rotations, "auth_reloads_ok": last.get("auth_reloads_ok"),
+        "auth_reloads_error": last.get("auth_reloads_error"), "auth_failures": last.get("auth_failures"),
     }
     print(json.dumps(summary), flush=True)
 
