@@ -256,8 +256,14 @@ def auth_token_check(cfg) -> tuple:
     err, _, tokens = _core().read_token_file(cfg.http_auth_token_file)
     if err:
         return (FAIL, err + ": the exporter refuses to start with it")
+    import os
+    import stat
+
     short = min(len(t) for t in tokens)
     which = f"{len(tokens)} tokens accepted (a rotation in progress?)" if len(tokens) > 1 else "1 token"
+    if os.stat(cfg.http_auth_token_file).st_mode & stat.S_IROTH:
+        return (WARN, f"{cfg.http_auth_token_file}: {which}, but the file is readable by every user on the node: "
+                      "mode 0400 / 0440 (the overlay's Secret uses defaultMode 0400)")
     if short < 16:
         return (WARN, f"{cfg.http_auth_token_file}: {which}, one of {short} characters: use 16 or more random "
                       "characters")

@@ -253,6 +253,10 @@ def test_doctor_checks_the_token_file(tmp_path):
 
     p = tmp_path / "token"
     p.write_text("0123456789abcdef0123\n")
+    p.chmod(0o644)
+    st, detail = auth_token_check(Config(http_auth_token_file=str(p)))
+    assert st == WARN and "readable by every user" in detail
+    p.chmod(0o600)
     assert auth_token_check(Config(http_auth_token_file=str(p)))[0] == OK
     p.write_text("0123456789abcdef0123\nabcdef0123456789abcd\n")
     st, detail = auth_token_check(Config(http_auth_token_file=str(p)))
