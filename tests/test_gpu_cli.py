@@ -281,7 +281,8 @@ def test_native_binary_pushes_over_https_and_listens_dual_stack(tmp_path):
 def test_native_binary_serves_metrics_over_https(tmp_path):
     """`gpumon-exporter --backend amdsmi --tls-cert-file ... --tls-key-file ...` on MI355X: a verified
     HTTPS scrape (identity and gzip, one keep-alive session) carries the GPU's real HBM total, and a
-    plain-HTTP request to the same port is counted as a failed handshake."""
+    plain-HTTP request to the same port is counted as a failed handshake. /metrics also needs a
+    bearer token (--http-auth-token-file): a request without it gets 401 and is counted."""
     import gzip
     import http.client
     import shutil
@@ -298,6 +299,9 @@ def test_native_binary_serves_metrics_over_https(tmp_path):
     d = str(tmp_path)
     _ca(d, "ca")
     _leaf(d, "server", "ca", "DNS:localhost,IP:127.0.0.1")
+    with open(f"{d}/token", "w") as f:
+        f.write("gpu-box-token-0123456789\n")
+    auth = {"Authorization": "Bearer gpu-box-token-0123456789"}
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -305,7 +309,8 @@ def test_native_binary_serves_metrics_over_https(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     p = subprocess.Popen([os.path.join(root, "bin", "gpumon-exporter"), "--backend", "amdsmi", "--interval", "0.2",
                           "--listen", f"127.0.0.1:{port}", "--no-pod-resources", "--no-cri", "--log-level", "warn",
-                          "--tls-cert-file", f"{d}/server.pem", "--tls-key-file", f"{d}/server.key"],
+                          "--tls-cert-file", f"{d}/server.pem", "--tls-key-file", f"{d}/server.key",
+                          "--http-auth-token-file", f"{d}/token"],
                          stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     ctx = ssl.create_default_context(cafile=f"{d}/ca.pem")
     try:
@@ -313,16 +318,19 @@ def test_native_binary_serves_metrics_over_https(tmp_path):
         while True:
             try:
                 c = http.client.HTTPSConnection("localhost", port, context=ctx, timeout=5)
-                c.request("GET", "/metrics")
+                c.request("GET", "/metrics", headers=auth)
                 text = c.getresponse().read().decode()
                 break
             except (OSError, ssl.SSLError):
                 assert time.time() < deadline and p.poll() is None
                 time.sleep(0.2)
-        c.request("GET", "/metrics", headers={"Accept-Encoding": "gzip"})
+        c.request("GET", "/metrics", headers={"Accept-Encoding": "gzip", **auth})
         r = c.getresponse()
         assert r.getheader("Content-Encoding") == "gzip"
         gz_text = gzip.decompress(r.read()).decode()
+        c.request("GET", "/metrics")  # no token
+        r = c.getresponse()
+        assert r.status == 401 and b"node_gpu" not in r.read()
         c.close()
         raw = socket.create_connection(("127.0.0.1", port), timeout=5)
         raw.sendall(b"GET /metrics HTTP/1.1\r\nHost: x\r\n\r\n")
@@ -333,7 +341,7 @@ def test_native_binary_serves_metrics_over_https(tmp_path):
         raw.close()
         time.sleep(0.5)
         c = http.client.HTTPSConnection("localhost", port, context=ctx, timeout=5)
-        c.request("GET", "/metrics")
+        c.request("GET", "/metrics", headers=auth)
         last = c.getresponse().read().decode()
         c.close()
     finally:
@@ -344,3 +352,4 @@ def test_native_binary_serves_metrics_over_https(tmp_path):
         fam = promtext.parse(t)
         assert promtext.one(fam, "node_gpu_mem_total", gpu_id="0") == 294896  # MiB of HBM3E, from the device
     assert promtext.one(promtext.parse(last), "gpumon_http_tls_handshake_failures_total") >= 1
+    assert promtext.one(promtext.parse(last), "gpumon_http_auth_failures_total") == 1
