@@ -1063,7 +1063,9 @@ SelfStats Exporter::self_stats() const {
     }
   }
   if (auth_) {
-    s.http_auth_failures = static_cast<int64_t>(auth_failures_.load(std::memory_order_relaxed));
+    for (int i = 0; i < 3; ++i) s.http_auth_failures_by[i] = auth_failures_[i].load(std::memory_order_relaxed);
+    s.http_auth_failures = static_cast<int64_t>(s.http_auth_failures_by[0] + s.http_auth_failures_by[1] +
+                                                s.http_auth_failures_by[2]);
     s.http_auth_reloads_ok = auth_->reloads_ok();
     s.http_auth_reloads_failed = auth_->reloads_failed();
   }

@@ -360,7 +360,7 @@ class Exporter {
   std::atomic<int64_t> influx_last_ok_wall_ns_{0};
   std::atomic<bool> push_tls_check_now_{false};   // reload_tls(): re-stamp the push's TLS files
   std::shared_ptr<TokenAuth> auth_;               // http_auth_token_file (nullptr: /metrics is open)
-  std::atomic<uint64_t> auth_failures_{0};        // /metrics requests refused with 401
+  std::atomic<uint64_t> auth_failures_[3] = {};   // /metrics requests refused with 401: missing, scheme, token
 
   // per-device sampling workers + watchdog (dev_workers.cpp)
   void start_workers(int n);

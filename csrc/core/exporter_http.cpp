@@ -90,8 +90,8 @@ std::shared_ptr<const Exporter::Filtered> Exporter::filtered(const Snapshot& s, 
 
 void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
   if (req.path == "/metrics") {
-    if (auth_ && !auth_->allow(req.authorization)) {
-      auth_failures_.fetch_add(1, std::memory_order_relaxed);
+    if (const auto v = auth_ ? auth_->check(req.authorization) : TokenAuth::Verdict::kOk; v != TokenAuth::Verdict::kOk) {
+      auth_failures_[static_cast<int>(v) - 1].fetch_add(1, std::memory_order_relaxed);
       resp->status = 401;
       resp->extra_headers = "WWW-Authenticate: Bearer realm=\"gpumon\"\r\n";
       resp->inline_body = "unauthorized\n";

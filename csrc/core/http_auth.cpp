@@ -99,7 +99,7 @@ void TokenAuth::maybe_reload(int64_t now_ns) {
   checking_.store(false, std::memory_order_release);
 }
 
-bool TokenAuth::allow(std::string_view authorization) {
+TokenAuth::Verdict TokenAuth::check(std::string_view authorization) {
   maybe_reload(mono_ns());
   std::shared_ptr<const std::vector<std::string>> toks;
   {
@@ -108,7 +108,8 @@ bool TokenAuth::allow(std::string_view authorization) {
   }
   // "Bearer" is case-insensitive (RFC 7235 auth-scheme), followed by one or more spaces
   const std::string_view a = trim(authorization);
-  if (a.size() < 7 || strncasecmp(a.data(), "bearer ", 7) != 0) return false;
+  if (a.empty()) return Verdict::kMissing;
+  if (a.size() < 7 || strncasecmp(a.data(), "bearer ", 7) != 0) return Verdict::kScheme;
   const std::string_view got = trim(a.substr(7));
   // every token, and every byte of each, is compared whatever the first difference
   bool ok = false;
@@ -118,7 +119,7 @@ bool TokenAuth::allow(std::string_view authorization) {
       diff |= static_cast<unsigned char>(want[i]) ^ static_cast<unsigned char>(i < got.size() ? got[i] : 0);
     ok |= diff == 0;
   }
-  return ok;
+  return ok ? Verdict::kOk : Verdict::kToken;
 }
 
 }  // namespace gpumon

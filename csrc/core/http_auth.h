@@ -25,10 +25,11 @@ class TokenAuth {
   // nullptr with *err when the file cannot be read or holds no usable token
   static std::shared_ptr<TokenAuth> create(const std::string& path, std::string* err);
 
-  // true when `authorization` (the request's header value) is "Bearer <one of the file's tokens>".
+  // kOk when `authorization` (the request's header value) is "Bearer <one of the file's tokens>".
   // Compares every token, each in time independent of where the values differ. Re-stamps the file
   // when due.
-  bool allow(std::string_view authorization);
+  enum class Verdict { kOk, kMissing, kScheme, kToken };  // kScheme: not "Bearer ..."
+  Verdict check(std::string_view authorization);
   void request_reload() { reload_now_ = true; }
   uint64_t reloads_ok() const { return reloads_ok_.load(); }
   uint64_t reloads_failed() const { return reloads_failed_.load(); }

@@ -878,10 +878,12 @@ void render_prometheus(const RenderInput& in, std::string* o) {
     if (s.http_auth_failures >= 0) {
       {
         Family f(o, "gpumon_http_auth_failures_total",
-                 "/metrics requests refused with 401 (http_auth_token_file): no Authorization header, another "
-                 "scheme than Bearer, or a token that is not the file's.",
+                 "/metrics requests refused with 401 (http_auth_token_file) by reason: missing (no Authorization "
+                 "header: a scraper without credentials), scheme (not Bearer), token (not one of the file's: a "
+                 "stale token after a rotation, or a guess).",
                  "counter");
-        f.add(hl, static_cast<double>(s.http_auth_failures));
+        static const char* const kReason[3] = {"missing", "scheme", "token"};
+        for (int i = 0; i < 3; ++i) f.add(hl, {{"reason", kReason[i]}}, static_cast<double>(s.http_auth_failures_by[i]));
       }
       Family f(o, "gpumon_http_auth_token_reloads_total",
                "Changes of http_auth_token_file seen: result=ok the new token is required from the next request, "

@@ -74,6 +74,7 @@ struct SelfStats {
   int64_t http_tls_not_after = 0;     // ... the serving certificate's expiry (unix s; 0 unknown)
   uint64_t http_tls_reloads_ok = 0, http_tls_reloads_failed = 0;  // ... certificate rotations picked up / refused
   int64_t http_auth_failures = -1;    // http_auth_token_file: /metrics requests refused (-1: no token)
+  uint64_t http_auth_failures_by[3] = {0, 0, 0};  // ... by reason: no header, not Bearer, wrong token
   uint64_t http_auth_reloads_ok = 0, http_auth_reloads_failed = 0;  // ... token rotations picked up / refused
   int64_t http_rt_demotions = -1;    // ... times a loop spent its CPU budget and was demoted
   uint64_t overruns = 0;

@@ -72,7 +72,8 @@ def test_metrics_needs_the_token_and_health_stays_open(mock_exporter, token_file
     assert ex.self_stats()["http_auth_failures"] == 9
     ex.tick()
     fams = promtext.parse(ex.metrics_text())
-    assert promtext.one(fams, "gpumon_http_auth_failures_total") == 9
+    for reason in ("missing", "scheme", "token"):  # 3 each: see the requests above
+        assert promtext.one(fams, "gpumon_http_auth_failures_total", reason=reason) == 3, reason
     assert promtext.one(fams, "gpumon_http_auth_token_reloads_total", result="ok") == 0
 
 

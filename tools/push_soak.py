@@ -147,7 +147,7 @@ def push_counters(port, ctx=None, token=None):
         for _, labels, v in fam.get("gpumon_http_tls_reloads_total", {}).get("samples", []):
             out["tls_reloads_" + labels.get("result", "?")] = v
     if token:
-        out["auth_failures"] = promtext.one(fam, "gpumon_http_auth_failures_total")
+        out["auth_failures"] = sum(v for _, _, v in fam.get("gpumon_http_auth_failures_total", {}).get("samples", []))
         for _, labels, v in fam.get("gpumon_http_auth_token_reloads_total", {}).get("samples", []):
             out["auth_reloads_" + labels.get("result", "?")] = v
     return out
