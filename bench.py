@@ -6,7 +6,14 @@
         --master-port P bench.py --gpus N --steps K --warmup W           # N GPUs, one rank each
 
 What one "step" is: one sampling period of the exporter (default 1 Hz, the BASELINE interval).
-Rank 0 runs the native exporter (amdsmi backend) over exactly the GPUs the job loads (each HIP
+Rank 0 runs the SHIPPED exporter -- ``bin/gpumon-exporter --config <file>``, the image's
+ENTRYPOINT, with the DaemonSet ConfigMap's keys -- as its own child process, started before this
+process's first HIP call (``--exporter child``, the default; gpumon/export/child.py). The bench
+process is then a foreign tenant to it, as every workload is in a cluster, and the exporter's tick
+log, exact per-scrape service times, pod rows and self stats are read from its loopback-only
+``debug_listen`` server; its CPU and RSS from /proc/<pid>. ``--exporter inprocess`` runs the same
+core through the Python bindings inside this process instead (A/B). The exporter samples
+exactly the GPUs the job loads (each HIP
 ordinal paired with the exporter device of the same PCI BDF, gpumon/parallel/devmap.py, printed as
 ``devices``; the run fails if a loaded GPU reads under 50 % gfx_util, ``device_check``) and a
 client-side scraper that hits /metrics at --scrape-rate, while EVERY GPU runs a synthetic gfx950 HIP load (bf16 MFMA burn +
@@ -90,26 +97,6 @@ def _server_durations(ex, n0, want, wait_s=1.0):
     while ex.scrape_count() - n0 < want and time.monotonic() < t_end:
         time.sleep(0.002)
     return list(ex.scrape_durations_since(n0))
-
-
-def _exporter_cpu_s():
-    """CPU seconds of the exporter's own threads in this process (named gpumon-*: sampler, device
-    workers, HTTP loops, pollers); the bench's loads, scraper and torch threads are not counted."""
-    hz = os.sysconf("SC_CLK_TCK")
-    total = 0.0
-    for t in os.listdir("/proc/self/task"):
-        try:
-            s = open(f"/proc/self/task/{t}/stat").read()
-            if not s[s.index("(") + 1:s.rindex(")")].startswith("gpumon-"):
-                continue
-            try:  # nanoseconds on the CPU (schedstat), else clock ticks
-                total += int(open(f"/proc/self/task/{t}/schedstat").read().split()[0]) * 1e-9
-            except (OSError, ValueError, IndexError):
-                f = s.rsplit(")", 1)[1].split()
-                total += (int(f[11]) + int(f[12])) / hz
-        except OSError:
-            continue
-    return total
 
 
 def _per_gpu_xgmi(tick_rates, rows, expected_tx, expected_rx):
@@ -245,6 +232,76 @@ def _device_check(rows, tick_util, loaded):
     return {"ok": not bad, "checked": True, "floor_pct": GFX_UTIL_FLOOR, "per_gpu": per}
 
 
+class InProcessExporter:
+    """``--exporter inprocess``: the same core through gpumon._core in this process, behind the
+    interface of gpumon.export.child.ChildExporter (A/B against the shipped binary)."""
+
+    def __init__(self, mon):
+        self.mon, self.ex = mon, mon.ex
+        self.port = mon.port
+        self.pid = os.getpid()
+
+    @property
+    def seq(self):
+        return self.ex.seq
+
+    def wait_for_seq(self, seq, timeout_s):
+        return self.ex.wait_for_seq(seq, timeout_s)
+
+    def wait_ticks(self, n=1, timeout_s=30.0):
+        return self.mon.wait_ticks(n, timeout_s)
+
+    def ticks(self, since=0):
+        return [t for t in self.ex.tick_log() if t["seq"] > since]
+
+    def scrape_count(self):
+        return self.ex.scrape_count()
+
+    def scrape_durations_since(self, n0):
+        return list(self.ex.scrape_durations_since(n0))
+
+    def statics(self):
+        return self.ex.statics()
+
+    def self_stats(self):
+        return self.ex.self_stats()
+
+    def samples(self):
+        return self.ex.samples()
+
+    def pod_rows(self):
+        return self.ex.pod_rows()
+
+    def metrics(self):
+        return self.mon.metrics()
+
+    def threads_cpu(self):
+        """The exporter's own threads in this process (named gpumon-*: sampler, device workers, HTTP
+        loops, pollers); the bench's loads, scraper and torch threads are not counted."""
+        from gpumon.export.child import threads_cpu
+
+        return threads_cpu(os.getpid(), "gpumon-")
+
+    def rss_bytes(self):
+        return None  # shared with the bench process: not the exporter's
+
+    def stop(self):
+        self.mon.stop()
+
+
+def _per_device_times(timed, gpu_ids):
+    out = []
+    for i, g in enumerate(gpu_ids):
+        dv = [t["dev"][i] for t in timed if i < len(t.get("dev", []))]
+        if not dv:
+            continue
+        td = [d.get("t_device", 0.0) for d in dv]
+        tp = [d.get("t_procs", 0.0) for d in dv]
+        out.append({"gpu": i, "gpu_id": g, "t_device_mean_ms": round(sum(td) / len(td) * 1e3, 4),
+                    "t_device_max_ms": round(max(td) * 1e3, 4), "t_procs_mean_ms": round(sum(tp) / len(tp) * 1e3, 4)})
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
@@ -298,6 +355,9 @@ def main() -> int:
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="DIAGNOSTIC: extra exporter config keys for the timed exporter (gpumon.config.Config), "
                          "e.g. --set processes=false --set gzip=false; listed in the line as exporter_overrides")
+    ap.add_argument("--exporter", default="child", choices=["child", "inprocess"],
+                    help="child: bin/gpumon-exporter as its own process (the shipped binary, default); "
+                         "inprocess: the same core through gpumon._core in this process (A/B)")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
 
@@ -317,6 +377,43 @@ def main() -> int:
         if world > 1:
             raise SystemExit("bench.py under torchrun needs PyTorch (torch.distributed over RCCL)")
 
+    # torchrun: this rank's GPU; one process: all N GPUs (the node-level exporter watches them all)
+    my_devs = [local_rank] if world > 1 else list(range(n))
+
+    # ---------------------------------------------------------------- rank 0: the exporter child
+    # Started BEFORE this process's first HIP call (torch.cuda.is_available() initialises HIP): the
+    # child is forked from a process without GPU state. The loaded GPUs' BDFs come from KFD's
+    # topology here (devmap.kfd_bdfs) and are checked against HIP's after initialisation.
+    from gpumon.parallel.devmap import kfd_bdfs
+
+    predicted = kfd_bdfs(range(n)) if rank == 0 else {}
+    gpu_guess = (torch.cuda.device_count() > 0) if torch is not None else bool(kfd_bdfs(range(1)))
+    backend = args.backend
+    if backend == "auto":
+        # auto = libamd_smi with the sysfs fast path, rocm_smi_lib if libamd_smi cannot initialise
+        backend = "auto" if gpu_guess else f"mock:gpus={n * args.replicate},mode=load"
+        if gpu_guess and args.replicate > 1:
+            backend = f"amdsmi:replicate={args.replicate}"
+    real = backend.startswith(("amdsmi", "rocm_smi", "auto"))
+    overrides = dict(kv.split("=", 1) for kv in args.set)
+    ex = None
+    exporter_info = {"mode": args.exporter}
+    if rank == 0 and args.exporter == "child":
+        import tempfile
+
+        from gpumon.export.child import ChildExporter, daemonset_config
+
+        sampled = [predicted[k] for k in range(n)] if real and len(predicted) == n else []
+        ccfg = dict(daemonset_config(), backend=backend, devices=sampled, interval=args.interval, host="bench-node",
+                    http_threads=2, http_rt_priority=args.http_rt_priority, rt_priority=args.rt_priority,
+                    prewarm_ms=args.prewarm_ms, sample_threads=args.sample_threads,
+                    fast_path=not args.no_fast_path, enable_probe=bool(args.probe and gpu_guess), log_level="warn",
+                    **overrides)
+        workdir = tempfile.mkdtemp(prefix="gpumon-bench-")
+        ex = ChildExporter(ccfg, workdir).start()
+        exporter_info.update(binary="bin/gpumon-exporter", pid=ex.pid, config_keys=sorted(ccfg),
+                             spawned_before_hip=True, devices_predicted=sampled)
+
     if torch is not None:
         has_gpu = torch.cuda.is_available()
     else:
@@ -334,8 +431,6 @@ def main() -> int:
         dist.init_process_group(backend="nccl" if has_gpu else "gloo")
     device = (torch.device(f"cuda:{local_rank}") if has_gpu else torch.device("cpu")) if torch is not None else None
 
-    # torchrun: this rank's GPU; one process: all N GPUs (the node-level exporter watches them all)
-    my_devs = [local_rank] if world > 1 else list(range(n))
     # HIP ordinal -> PCI BDF of every GPU the job loads, gathered to rank 0: the exporter samples
     # exactly those GPUs, named by BDF, since its gpu_id (libamd_smi hip_id) is node-wide and a
     # HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES subset renumbers the ordinals (devmap.py)
@@ -348,6 +443,15 @@ def main() -> int:
             allb = [None] * world
             dist.all_gather_object(allb, ord_bdfs)
             ord_bdfs = {int(k): v for d in allb for k, v in d.items()}
+    # every rank's view of the process group (SCALE: RCCL's world size as each rank sees it) and its
+    # pid (the tenants the exporter attributes)
+    ranks_seen = [{"rank": rank, "world_size": dist.get_world_size() if dist is not None else 1,
+                   "backend": str(dist.get_backend()) if dist is not None else None, "pid": os.getpid(),
+                   "local_rank": local_rank}]
+    if dist is not None:
+        allr = [None] * world
+        dist.all_gather_object(allr, ranks_seen[0])
+        ranks_seen = allr
 
     def barrier():
         if dist is not None:
@@ -356,51 +460,61 @@ def main() -> int:
             torch.cuda.synchronize()
 
     # ---------------------------------------------------------------- rank 0: exporter + scraper
-    mon = None
     core = None
-    backend = args.backend
+    mon = None
+    sampled = [ord_bdfs[k] for k in sorted(ord_bdfs)] if real and ord_bdfs else []
     if rank == 0:
         from gpumon import core as _core
-        from gpumon.config import Config
-        from gpumon.monitor import GpuMonitor
-
-        core = _core()
-        if backend == "auto":
-            # auto = libamd_smi with the sysfs fast path, rocm_smi_lib if libamd_smi cannot initialise
-            backend = "auto" if has_gpu else f"mock:gpus={n * args.replicate},mode=load"
-            if has_gpu and args.replicate > 1:
-                backend = f"amdsmi:replicate={args.replicate}"
-        real = backend.startswith(("amdsmi", "rocm_smi", "auto"))
-        sampled = [ord_bdfs[k] for k in sorted(ord_bdfs)] if real and ord_bdfs else []
-        cfg = Config(backend=backend, devices=sampled,
-                     interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
-                     http_rt_priority=args.http_rt_priority,
-                     enable_probe=args.probe and has_gpu, log_level="warn", fast_path=not args.no_fast_path,
-                     sample_threads=args.sample_threads, rt_priority=args.rt_priority, prewarm_ms=args.prewarm_ms)
-        if args.set:
-            cfg.apply_dict(dict(kv.split("=", 1) for kv in args.set))
-        mon = GpuMonitor(cfg, control_plane=False).start()
-        if mon.start_error:
-            raise SystemExit(f"exporter backend failed: {mon.start_error}")
-        if backend == "auto":
-            backend = mon.ex.self_stats().get("backend") or backend  # the one that came up
-        st = mon.ex.statics()
-        if len(st) < n:
-            raise SystemExit(f"exporter sees {len(st)} GPU(s), bench needs {n}")
         from gpumon.parallel.devmap import DeviceMapError, match, positional
 
-        try:  # every loaded ordinal paired with the exporter device of the same BDF, or stop here
-            dev_rows = (match(ord_bdfs, st, replicas=args.replicate > 1) if real and ord_bdfs
-                        else positional(n, st))
+        core = _core()
+        if ex is None:  # --exporter inprocess
+            from gpumon.config import Config
+            from gpumon.monitor import GpuMonitor
+
+            cfg = Config(backend=backend, devices=sampled,
+                         interval=args.interval, listen="127.0.0.1:0", http_threads=2, host="bench-node",
+                         http_rt_priority=args.http_rt_priority,
+                         enable_probe=args.probe and has_gpu, log_level="warn", fast_path=not args.no_fast_path,
+                         sample_threads=args.sample_threads, rt_priority=args.rt_priority, prewarm_ms=args.prewarm_ms)
+            if overrides:
+                cfg.apply_dict(overrides)
+            mon = GpuMonitor(cfg, control_plane=False).start()
+            if mon.start_error:
+                raise SystemExit(f"exporter backend failed: {mon.start_error}")
+            ex = InProcessExporter(mon)
+            exporter_info.update(binary=None, pid=os.getpid())
+
+        def pair():
+            st = ex.statics()
+            if len(st) < n:
+                raise DeviceMapError(f"exporter sees {len(st)} GPU(s), bench needs {n}")
+            return (match(ord_bdfs, st, replicas=args.replicate > 1) if real and ord_bdfs else positional(n, st))
+
+        try:  # every loaded ordinal paired with the exporter device of the same BDF
+            dev_rows = pair()
         except DeviceMapError as e:
-            raise SystemExit(f"bench: loaded GPUs and sampled GPUs disagree: {e}")
+            if args.exporter != "child" or not sampled:
+                raise SystemExit(f"bench: loaded GPUs and sampled GPUs disagree: {e}")
+            # the KFD-topology prediction missed (an unusual visibility setup): the child starts
+            # again with HIP's own BDFs, now after HIP initialised, and the line says so
+            ex.stop()
+            ex = ChildExporter(dict(ex.cfg, devices=sampled), ex.workdir).start()
+            exporter_info.update(pid=ex.pid, spawned_before_hip=False, respawned_after=str(e))
+            try:
+                dev_rows = pair()
+            except DeviceMapError as e2:
+                raise SystemExit(f"bench: loaded GPUs and sampled GPUs disagree: {e2}")
+        if backend == "auto":
+            backend = ex.self_stats().get("backend") or backend  # the one that came up
+        exporter_info["devices_match_hip"] = (sampled == exporter_info.get("devices_predicted", sampled))
 
     # ---------------------------------------------------------------- idle reference (untimed)
     # the same scrape load against the same exporter before any synthetic load starts: the
     # BASELINE asks for scrape p99 idle and under load at every GPU count
     idle = None
     if rank == 0 and args.idle_s > 0:
-        mon.wait_ticks(1, timeout_s=args.interval * 5 + 30)
+        ex.wait_ticks(1, timeout_s=args.interval * 5 + 30)
         spin = []
         if args.idle_spinners > 0:
             import subprocess
@@ -408,20 +522,20 @@ def main() -> int:
             code = "import os; os.sched_setscheduler(0, os.SCHED_IDLE, os.sched_param(0))\nwhile True: pass"
             spin = [subprocess.Popen([sys.executable, "-c", code]) for _ in range(args.idle_spinners)]
             time.sleep(1.0)
-        q0 = mon.ex.seq
-        n0 = mon.ex.scrape_count()
+        q0 = ex.seq
+        n0 = ex.scrape_count()
         try:
-            r = core.scrape_load("127.0.0.1", mon.port, args.scrape_path, n_requests=0, duration_s=args.idle_s,
+            r = core.scrape_load("127.0.0.1", ex.port, args.scrape_path, n_requests=0, duration_s=args.idle_s,
                                  concurrency=args.scrape_concurrency, rate_hz=args.scrape_rate, keep_alive=True,
                                  gzip=args.gzip)
         finally:
             for p in spin:
                 p.kill()
                 p.wait()
-        q1 = mon.ex.seq
-        it = [t["duration_s"] for t in mon.ex.tick_log() if q0 < t["seq"] <= q1]
+        q1 = ex.seq
+        it = [t["duration_s"] for t in ex.ticks(q0) if q0 < t["seq"] <= q1]
         lat = r.get("latencies_s", [])
-        srv = _server_durations(mon.ex, n0, len(lat))
+        srv = _server_durations(ex, n0, len(lat))
         idle = {"seconds": args.idle_s, "scrapes": len(lat), "scrape_errors": r.get("errors", 0),
                 "scrape_p50_ms": round(_pct(lat, 0.50) * 1e3, 4) if lat else None,
                 "scrape_p99_ms": round(_pct(lat, 0.99) * 1e3, 4) if lat else None,
@@ -457,7 +571,7 @@ def main() -> int:
         copiers = [PeerCopier(i, (i + 1) % n, nbytes=args.xgmi_mb << 20).start() for i in range(n)]
 
     if rank == 0:
-        mon.wait_ticks(args.warmup, timeout_s=args.warmup * args.interval * 5 + 30)
+        ex.wait_ticks(args.warmup, timeout_s=args.warmup * args.interval * 5 + 30)
     barrier()
     # RCCL channel / buffer setup and the all-reduce calibration stay out of the timed region
     reps = 1
@@ -492,19 +606,19 @@ def main() -> int:
         # a random phase of an interval plus the last step's reductions past it (the elapsed time
         # then moved by up to -0.6 / +0.4 intervals with the phase, i.e. +-4-6 % of a 10-step
         # samples/s, at N > 1 only).
-        mon.wait_ticks(1, timeout_s=args.interval * 5 + 30)
+        ex.wait_ticks(1, timeout_s=args.interval * 5 + 30)
         duration = args.steps * args.interval
 
         def _scrape():
-            scrape_result.update(core.scrape_load("127.0.0.1", mon.port, args.scrape_path, n_requests=0,
+            scrape_result.update(core.scrape_load("127.0.0.1", ex.port, args.scrape_path, n_requests=0,
                                                   duration_s=duration, concurrency=args.scrape_concurrency,
                                                   rate_hz=args.scrape_rate, keep_alive=True, gzip=args.gzip))
 
         scraper = threading.Thread(target=_scrape, daemon=True)
-        n_scr0 = mon.ex.scrape_count()
-        s0 = mon.ex.self_stats()
-        seq0 = mon.ex.seq
-        cpu0 = _exporter_cpu_s()
+        n_scr0 = ex.scrape_count()
+        s0 = ex.self_stats()
+        seq0 = ex.seq
+        cpu0 = ex.threads_cpu()
 
     # ---------------------------------------------------------------- timed region
     barrier()
@@ -513,8 +627,6 @@ def main() -> int:
     t0 = time.perf_counter()
     if scraper is not None:
         scraper.start()
-    tick_rates = []  # per tick, per sampled device: (sum of per-link write B/s, read B/s) or None
-    tick_util = []   # per tick, per sampled device: the exporter's gfx_util (%)
     ar_events = []
     for step in range(args.steps):
         # one step = one sampling interval: this interval's xGMI traffic, then the tick closing it
@@ -530,17 +642,14 @@ def main() -> int:
                 for _ in range(reps):
                     dist.all_reduce(ar_buf)
         if rank == 0:
-            if not mon.ex.wait_for_seq(seq0 + step + 1, args.interval * 5 + 10):
+            if not ex.wait_for_seq(seq0 + step + 1, args.interval * 5 + 10):
                 raise SystemExit("exporter tick timed out")
-            tick_rates.append([(sum(r.get("xgmi_wr_Bps") or [0.0]), sum(r.get("xgmi_rd_Bps") or [0.0]))
-                               if r.get("valid") else None for r in mon.ex.rates()])
-            tick_util.append([x["fields"].get("gfx_util") for x in mon.ex.samples()])
     barrier()
     elapsed = time.perf_counter() - t0
     if rank == 0:  # the exporter's counters at the end of the timed region (not after the reductions)
-        s1 = mon.ex.self_stats()
-        seq1 = mon.ex.seq
-        cpu1 = _exporter_cpu_s()
+        s1 = ex.self_stats()
+        seq1 = ex.seq
+        cpu1 = ex.threads_cpu()
     c1 = [c.stats() for c in copiers]
     l1 = [ld.stats() for ld in loads]
     if dist is not None:
@@ -593,23 +702,31 @@ def main() -> int:
         if scraper is not None:
             scraper.join(timeout=args.interval * 5 + 30)
         lat = scrape_result.get("latencies_s", [])
-        srv = _server_durations(mon.ex, n_scr0, len(lat))  # server-side, the same scrapes
+        srv = _server_durations(ex, n_scr0, len(lat))  # server-side, the same scrapes
+        ticks = seq1 - seq0
+        timed = [t for t in ex.ticks(seq0) if seq0 < t["seq"] <= seq0 + ticks]
+        # per tick, per sampled device: (sum of per-link write B/s, read B/s) or None, and gfx_util:
+        # every timed tick's values from the exporter's tick log (none raced for)
+        tick_rates = [[(d["xgmi_wr_Bps"] or 0.0, d["xgmi_rd_Bps"] or 0.0) if d.get("rates_valid") else None
+                       for d in t.get("dev", [])] for t in timed]
+        tick_util = [[d.get("gfx_util") for d in t.get("dev", [])] for t in timed]
         samples = s1["samples"] - s0["samples"]
         stale = s1.get("stale_samples", 0) - s0.get("stale_samples", 0)
-        fresh = samples - stale  # a repeated firmware table is no new sample of the device
-        ticks = seq1 - seq0
-        timed = [t for t in mon.ex.tick_log() if seq0 < t["seq"] <= seq0 + ticks]
+        # value: fresh samples (the firmware table advanced) of the LOADED GPUs over the timed ticks
+        idx = [r["index"] for r in dev_rows]
+        fresh = sum(1 for t in timed for i in idx
+                    if i < len(t.get("dev", [])) and t["dev"][i].get("ok") and t["dev"][i].get("fresh"))
         tdur = [t["duration_s"] for t in timed]
         slow = max(timed, key=lambda t: t["duration_s"]) if timed else None
-        sm = mon.ex.samples()
+        sm = ex.samples()
         util = [x["fields"].get("gfx_util") for x in sm]
-        rows = mon.ex.pod_rows()
+        rows = ex.pod_rows()
         value = fresh / elapsed
         check = _device_check(dev_rows, tick_util, loaded=bool(loads) and args.load != "idle")
         from gpumon.export import promtext
 
         gid = {r["hip_ordinal"]: r["gpu_id"] for r in dev_rows}
-        fam = promtext.parse(mon.metrics())
+        fam = promtext.parse(ex.metrics())
         slot_map = {}  # xGMI link-metrics entry -> table slot pairing (csrc/core/xgmi_map.cpp)
         for what in ("verified", "unverified", "mismatch"):
             for _, lab, v in fam.get(f"gpumon_xgmi_slot_map_{what}", {}).get("samples", []):
@@ -617,7 +734,7 @@ def main() -> int:
         # rows per GPU: a multi-rank tenant's ranks open every GPU; the first 8-GPU
         # record must show whether each GPU carries one workload row (peer contexts hidden) or N
         active = {lab.get("gpu_id"): int(v) for _, lab, v in fam.get("gpu_active_processes", {}).get("samples", [])}
-        stat_ids = [st.get("gpu_id", str(i)) for i, st in enumerate(mon.ex.statics())]
+        stat_ids = [st.get("gpu_id", str(i)) for i, st in enumerate(ex.statics())]
         per_gpu_rows = []
         for i, g in enumerate(stat_ids):
             wr = [r for r in rows if not r["idle"] and r["dev"] == i]
@@ -641,6 +758,17 @@ def main() -> int:
                 xgmi["exporter_rx_vs_expected"] = round(xgmi["exporter_rx_GBps_per_gpu"]
                                                         / xgmi["expected_tx_GBps_per_gpu"], 3)
             xgmi["per_gpu"] = per_gpu
+        # the exporter's CPU over the timed region, per thread name (millicores) and in total
+        thr = {k: round(1000.0 * (v - cpu0.get(k, 0.0)) / elapsed, 2) for k, v in sorted(cpu1.items())}
+        tenant_pids = sorted({x["pid"] for x in ranks_seen})
+        row_pids = sorted({int(r["pid"]) for r in rows if not r["idle"] and str(r["pid"]).isdigit()})
+        exporter_info.update(
+            rss_mb=round(ex.rss_bytes() / 2 ** 20, 1) if ex.rss_bytes() else None,
+            tenant_pids=tenant_pids,
+            # in a cluster the exporter only ever attributes other processes: every pod row's pid
+            # should be a tenant's, and none the exporter's own
+            rows_are_tenants=bool(row_pids) and set(row_pids) <= set(tenant_pids) if has_gpu else None,
+            exporter_pid_in_rows=exporter_info.get("pid") in row_pids)
         result = {
             "metric": BASELINE_METRIC,
             "value": round(value, 4),
@@ -651,9 +779,9 @@ def main() -> int:
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / max(1, len(sm)) / BASELINE_SAMPLES_PER_GPU, 3),
-            "value_note": ("value = fresh device samples/s over the timed ticks (samples whose firmware table "
-                           "advanced; repeats of the last table are not counted): fixed by the sampling "
+            "vs_baseline": round(value / max(1, len(dev_rows)) / BASELINE_SAMPLES_PER_GPU, 3),
+            "value_note": ("value = fresh samples/s of the loaded GPUs over the timed ticks (samples whose firmware "
+                           "table advanced; repeats of the last table are not counted): fixed by the sampling "
                            "interval (1/interval per GPU) unless ticks overrun or the interval beats the SMU's "
                            "refresh; the measured speed is scrape_p99_ms / scrape_p999_ms (client), "
                            "server_scrape_p99_ms and tick_*_ms"),
@@ -663,10 +791,14 @@ def main() -> int:
             "data": ("synthetic" if backend in ("amdsmi", "rocm_smi") else
                      f"synthetic (REHEARSAL: {n} physical GPU(s) each sampled {args.replicate}x)"
                      if backend.startswith("amdsmi:replicate") else "synthetic (mock backend: no GPU visible)"),
+            "exporter": exporter_info.get("binary") or "in-process (gpumon._core)",
+            "exporter_pid": exporter_info.get("pid"),
+            "exporter_info": exporter_info,
             "sampled_devices": len(sm),
             # each loaded HIP ordinal and the exporter device sampled for it (same PCI BDF)
             "devices": [{k: r[k] for k in ("hip_ordinal", "bdf", "gpu_id")} for r in dev_rows],
             "device_check": check,
+            "ranks": ranks_seen,
             "config": {
                 "model": f"gpumon MI355X exporter ({backend.split(':')[0]} backend) + synthetic bf16 MFMA/HBM HIP load",
                 "global_batch": n,
@@ -695,7 +827,7 @@ def main() -> int:
             "server_scrapes": len(srv),
             "scrape_errors": scrape_result.get("errors", 0),
             "scrape_body_kb": round(scrape_result.get("bytes", 0) / max(1, len(lat)) / 1024, 2),
-            "samples_per_sec_per_gpu": round(value / max(1, len(sm)), 4),
+            "samples_per_sec_per_gpu": round(value / max(1, len(dev_rows)), 4),
             "ticks": ticks,
             "tick_mean_ms": round(sum(tdur) / len(tdur) * 1e3, 4) if tdur else None,
             "tick_p50_ms": round(_pct(tdur, 0.50) * 1e3, 4) if tdur else None,
@@ -710,14 +842,18 @@ def main() -> int:
             "tick_phases_mean_ms": {k: round(sum(t[k] for t in timed) / len(timed) * 1e3, 4)
                                     for k in ("t_late", "t_sample", "t_wake", "t_device", "t_procs", "t_attrib",
                                               "t_render", "t_gzip")} if timed else None,
+            # per sampled device: its own calls' time per tick (the worker's metrics + links + RAS +
+            # process list, and the process list alone), mean / max over the timed ticks (ms)
+            "per_device_tick_ms": _per_device_times(timed, stat_ids),
             "tick_quantiles": "exact over the timed ticks (exporter tick log); times in ms",
             "overruns": s1["overruns"] - s0["overruns"],
             "sampler_rt_threads": s1.get("rt_threads", 0),
             "http_rt_loops": s1.get("http_rt_loops"),
             "prewarm_ms": args.prewarm_ms,
             "exporter_overrides": args.set or None,
-            # the exporter's own threads over the timed region, serving the scrape load too (1/100 s ticks)
-            "exporter_cpu_millicores": round(1000.0 * (cpu1 - cpu0) / elapsed, 2),
+            # the exporter's own threads over the timed region, serving the scrape load too
+            "exporter_cpu_millicores": round(sum(thr.values()), 2),
+            "exporter_thread_cpu_millicores": thr,
             "backend_call_us": {k: round((v["seconds"] - s0["backend_calls"].get(k, {}).get("seconds", 0.0)) * 1e6
                                          / max(1, v["n"] - s0["backend_calls"].get(k, {}).get("n", 0)), 1)
                                 for k, v in s1.get("backend_calls", {}).items()},
@@ -743,7 +879,7 @@ def main() -> int:
             "xgmi_slot_map": slot_map or None,
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,
         }
-        mon.stop()
+        ex.stop()
         if has_gpu and n > 1 and args.link_check_s > 0:
             # validation evidence, never a reason to lose the measured line: errors and a stuck
             # peer copy are recorded, not raised (each pair runs link_check_s plus the exporter's

@@ -64,6 +64,7 @@ MockProc mock_proc_from(const py::dict& d) {
   get(d, "vram_bytes", &p.vram_bytes);
   get(d, "gfx_share", &p.gfx_share);
   get(d, "kfd_only", &p.kfd_only);
+  get(d, "queues", &p.queues);
   return p;
 }
 
@@ -119,6 +120,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "tls_key_file", &c.tls_key_file);
   get(d, "tls_client_ca_file", &c.tls_client_ca_file);
   get(d, "http_auth_token_file", &c.http_auth_token_file);
+  get(d, "debug_listen", &c.debug_listen);
   get(d, "init_retry_s", &c.init_retry_s);
   get(d, "health_stale_s", &c.health_stale_s);
   get(d, "reinit_after", &c.reinit_after);
@@ -134,6 +136,7 @@ ExporterConfig config_from(const py::dict& d) {
   get(d, "version", &c.version);
   get(d, "activity_acc_scale", &c.rates.activity_acc_scale);
   get(d, "xgmi_kb_bytes", &c.rates.xgmi_kb_bytes);
+  get(d, "pcie_bw_unit_bytes", &c.rates.pcie_bw_unit_bytes);
   auto& a = c.attribution;
   get(d, "procfs_root", &a.procfs_root);
   get(d, "opt_in", &a.opt_in);
@@ -183,6 +186,8 @@ py::dict static_to_dict(const DeviceStatic& s) {
   d["kfd_node"] = s.kfd_node;
   d["partition_id"] = s.partition_id;
   d["num_cu"] = s.num_cu;
+  d["driver_version"] = s.driver_version;
+  d["driver_source"] = s.driver_source;
   d["vram_total_bytes"] = num(s.vram_total_bytes);
   d["power_limit_w"] = num(s.power_limit_w);
   return d;
@@ -245,6 +250,7 @@ py::dict sample_to_dict(const DeviceSample& s) {
   a["firmware_ts"] = s.acc.firmware_ts;
   a["system_clock_ns"] = s.acc.system_clock_ns;
   a["ppt_res"] = s.acc.ppt_res;
+  a["pcie_bw_acc"] = s.acc.has_pcie_bw_acc ? py::object(py::int_(s.acc.pcie_bw_acc)) : py::object(py::none());
   py::list xa;
   for (int k = 0; k < s.acc.n_xcd_acc; ++k) xa.append(s.acc.xcd_busy_acc[k]);
   a["xcd_busy_acc"] = xa;
@@ -283,6 +289,7 @@ py::dict rates_to_dict(const DeviceRates& r) {
   }
   d["xgmi_rd_Bps"] = rd;
   d["xgmi_wr_Bps"] = wr;
+  d["pcie_Bps"] = num(r.pcie_Bps);
   return d;
 }
 
@@ -302,6 +309,7 @@ py::dict row_to_dict(const PodRow& r) {
   d["proc_gfx_util"] = num(r.proc_gfx_util);
   d["cu_occupancy"] = num(r.cu_occupancy);
   d["occ_samples"] = r.occ_samples;
+  d["queues"] = r.queues;
   d["mfma_util"] = num(r.mfma_util);
   return d;
 }
@@ -318,6 +326,38 @@ MockBackend* mock_of(Exporter& e) {
   if (!m) throw std::runtime_error("exporter backend is not the mock backend");
   return m;
 }
+
+// A Python value as the option setters take it: strings, one per list element; bools as true/false.
+std::vector<std::string> option_values(py::handle v) {
+  auto one = [](py::handle x) -> std::string {
+    if (py::isinstance<py::bool_>(x)) return x.cast<bool>() ? "true" : "false";
+    return py::str(x).cast<std::string>();
+  };
+  std::vector<std::string> out;
+  if (v.is_none()) return out;
+  if (py::isinstance<py::list>(v) || py::isinstance<py::tuple>(v)) {
+    for (auto x : v) out.push_back(one(x));
+    if (out.empty()) out.push_back("");  // [] -> an empty list key / an empty string
+    return out.size() == 1 && out[0].empty() ? std::vector<std::string>{} : out;
+  }
+  out.push_back(one(v));
+  return out;
+}
+
+std::vector<std::string> env_strings(const py::dict& env) {
+  std::vector<std::string> kv;
+  for (auto item : env) kv.push_back(py::str(item.first).cast<std::string>() + "=" + py::str(item.second).cast<std::string>());
+  return kv;
+}
+
+struct EnvBlock {  // char** view of "k=v" strings
+  explicit EnvBlock(std::vector<std::string> kv) : s(std::move(kv)) {
+    for (auto& x : s) p.push_back(x.data());
+    p.push_back(nullptr);
+  }
+  std::vector<std::string> s;
+  std::vector<char*> p;
+};
 
 }  // namespace
 
@@ -340,6 +380,21 @@ static py::dict tick_to_dict(const TickInfo& t) {
   d["link_refreshes"] = t.link_refreshes;
   d["ras_reads"] = t.ras_reads;
   d["ras_full"] = t.ras_full;
+  py::list dev;
+  for (const auto& x : t.dev) {
+    py::dict e;
+    e["ok"] = x.ok;
+    e["fresh"] = x.fresh;
+    e["rates_valid"] = x.rates_valid;
+    e["gfx_util"] = num(x.gfx_util);
+    e["xgmi_wr_Bps"] = num(x.xgmi_wr_Bps);
+    e["xgmi_rd_Bps"] = num(x.xgmi_rd_Bps);
+    e["pcie_Bps"] = num(x.pcie_Bps);
+    e["t_device"] = x.t_device;
+    e["t_procs"] = x.t_procs;
+    dev.append(e);
+  }
+  d["dev"] = dev;
   return d;
 }
 
@@ -799,6 +854,12 @@ PYBIND11_MODULE(_core, m) {
   m.def("check_serve_tls", &check_serve_tls, py::arg("cert_file") = "", py::arg("key_file") = "",
         py::arg("client_ca_file") = "", "configuration-time check of the /metrics HTTPS files: \"\" = usable");
   m.def("redact_url", &redact_url);
+  m.def("driver_version_label", [](const std::string& raw, const std::string& module_version) {
+    std::string source;
+    std::string v = driver_version_label(raw, module_version, &source);
+    return py::make_tuple(v, source);
+  }, py::arg("raw"), py::arg("module_version") = "",
+     "gpu_info driver_version label and its source (module | kernel | library) from libamd_smi's string");
   m.def("parse_listen", [](const std::string& l) {
     std::string host, err;
     int port = -1;
@@ -871,7 +932,101 @@ PYBIND11_MODULE(_core, m) {
       .def_property_readonly("unverified", &XgmiSlotMap::unverified)
       .def_property_readonly("mismatched", &XgmiSlotMap::mismatched);
 
+  // The one configuration implementation (csrc/core/options.h); gpumon/config.py is a view of it.
+  py::class_<NativeOptions>(m, "Options")
+      .def(py::init<>())
+      .def("copy", [](const NativeOptions& o) { return NativeOptions(o); })
+      .def("set",
+           [](NativeOptions& o, const std::string& key, py::handle v) {
+             std::string err;
+             const int r = options_set(&o, key, option_values(v), &err);
+             if (r == 0) throw py::key_error("unknown config key: " + key);
+             if (r < 0) throw py::value_error(err);
+           },
+           py::arg("key"), py::arg("value"))
+      .def("load_file",
+           [](NativeOptions& o, const std::string& path) {
+             std::vector<std::string> unknown;
+             std::string err;
+             if (!options_load_file(&o, path, &unknown, &err)) throw py::value_error(err);
+             return unknown;
+           },
+           "apply a YAML config file; returns the keys it does not know (ignored)")
+      .def("apply_env",
+           [](NativeOptions& o, const py::dict& env) {
+             EnvBlock e(env_strings(env));
+             std::string err;
+             if (!options_apply_env(&o, e.p.data(), &err)) throw py::value_error(err);
+           })
+      .def_static(
+          "parse",
+          [](const std::vector<std::string>& args, const py::dict& env) {
+            NativeOptions o;
+            EnvBlock e(env_strings(env));
+            std::vector<std::string> rest, warnings;
+            std::string err;
+            if (options_parse(&o, args, e.p.data(), &rest, &warnings, &err) != ParseStatus::kOk)
+              throw py::value_error(err);
+            return py::make_tuple(o, rest, warnings);
+          },
+          py::arg("args"), py::arg("env"),
+          "file < environment < --compat < flags over a command line: (Options, other args, warnings)")
+      .def("finalized",
+           [](const NativeOptions& o) {
+             NativeOptions c = o;
+             std::string err;
+             if (!options_finalize(&c, &err)) throw py::value_error(err);
+             return c;
+           },
+           "a copy with the listen address, host fallback and control-plane sockets resolved")
+      .def("validate", &options_validate, "'' or why the configuration cannot run (finalized options)")
+      .def("to_json", [](const NativeOptions& o, bool redact) { return options_json(o, redact); },
+           py::arg("redact") = false)
+      .def_property_readonly("listen_addr", [](const NativeOptions& o) { return o.cfg.listen_addr; })
+      .def_property_readonly("port", [](const NativeOptions& o) { return o.cfg.port; })
+      .def_property_readonly("host", [](const NativeOptions& o) { return o.cfg.host; })
+      .def_property_readonly("log_level_value", &options_log_level)
+      .def_property_readonly("exporter_sources", [](const NativeOptions& o) {
+        py::dict d;  // what a finalized configuration hands the exporter's pollers
+        d["pod_resources_socket"] = o.cfg.pod_resources_socket;
+        d["cri_socket"] = o.cfg.cri_socket;
+        d["docker_socket"] = o.cfg.docker_socket;
+        d["pod_log_root"] = o.cfg.pod_log_root;
+        d["device_checkpoint"] = o.cfg.device_checkpoint;
+        return d;
+      });
+  m.def("option_keys", [] {
+    py::list l;
+    for (const auto& k : option_keys()) {
+      py::dict d;
+      d["key"] = k.key;
+      d["section"] = k.section;
+      d["help"] = k.help;
+      l.append(d);
+    }
+    return l;
+  }, "every configuration key with its documentation section and help");
+  m.def("option_flags", [] {
+    py::list l;
+    for (const auto& f : option_flags()) {
+      py::dict d;
+      d["flag"] = f.flag;
+      py::list al;
+      for (const auto& a : split(f.aliases, ','))
+        if (!a.empty()) al.append(a);
+      d["aliases"] = al;
+      d["key"] = f.key;
+      d["fixed"] = f.fixed ? py::object(py::str(f.fixed)) : py::object(py::none());
+      d["help"] = f.help;
+      l.append(d);
+    }
+    return l;
+  }, "the command-line flags both entry points take");
+  m.def("cri_autodetect_sockets", &cri_autodetect_sockets);
+
   py::class_<Exporter>(m, "Exporter")
+      .def(py::init([](const NativeOptions& o) { return new Exporter(o.cfg); }),
+           "from finalized Options (gpumon.config.Config.finalized())")
       .def(py::init([](const py::dict& cfg) { return new Exporter(config_from(cfg)); }))
       .def("start",
            [](Exporter& e) {
@@ -911,6 +1066,7 @@ PYBIND11_MODULE(_core, m) {
              return e.wait_for_seq(seq, timeout_s);
            })
       .def_property_readonly("port", &Exporter::port)
+      .def_property_readonly("debug_port", &Exporter::debug_port)
       .def_property_readonly("seq", &Exporter::seq)
       .def("healthy", &Exporter::healthy)
       .def("ready", &Exporter::ready)
@@ -1163,6 +1319,8 @@ PYBIND11_MODULE(_core, m) {
   // Native on-device samplers (csrc/core/ondevice.h): the same PMC / probe plugins the standalone
   // binary dlopen()s, driven from C++ threads instead of the Python runners in gpumon/ops.
   py::class_<OnDevice>(m, "OnDevice")
+      .def(py::init([](Exporter& e, const NativeOptions& o) { return new OnDevice(&e, o.od); }), py::keep_alive<1, 2>(),
+           "the on-device samplers of finalized Options (enable_pmc / enable_probe and their cadence)")
       .def(py::init([](Exporter& e, const py::dict& cfg) { return new OnDevice(&e, ondevice_from(cfg)); }),
            py::keep_alive<1, 2>())
       .def("start",

@@ -105,6 +105,31 @@ PYBIND11_MODULE(_hip, m) {
         return d;
       });
 
+  py::class_<PcieLoad>(m, "PcieLoad")
+      .def(py::init<int, size_t, std::string, double>(), py::arg("dev"), py::arg("nbytes") = size_t(256) << 20,
+           py::arg("direction") = "both", py::arg("duty") = 1.0)
+      .def("start", [](PcieLoad& g) {
+        py::gil_scoped_release nogil;
+        g.start();
+      })
+      .def("stop", [](PcieLoad& g) {
+        py::gil_scoped_release nogil;
+        g.stop();
+      })
+      .def_property_readonly("running", &PcieLoad::running)
+      .def("stats", [](PcieLoad& g) {
+        PcieStats s = g.stats();
+        py::dict d;
+        d["copies"] = s.copies;
+        d["h2d_bytes"] = s.h2d_bytes;
+        d["d2h_bytes"] = s.d2h_bytes;
+        d["bytes"] = s.h2d_bytes + s.d2h_bytes;
+        d["busy_s"] = s.busy_s;
+        d["wall_s"] = s.wall_s;
+        d["GBps_wall"] = s.wall_s > 0 ? (s.h2d_bytes + s.d2h_bytes) / s.wall_s / 1e9 : 0.0;  // both directions
+        return d;
+      });
+
   py::class_<Probe>(m, "Probe")
       .def(py::init<int, int, int, int>(), py::arg("dev"), py::arg("blocks") = 1024, py::arg("slots") = 4,
            py::arg("spin_ticks") = 200)

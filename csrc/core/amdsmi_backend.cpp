@@ -251,12 +251,13 @@ bool AmdSmiBackend::init(std::string* err) {
       if (t_->amdsmi_get_gpu_memory_partition(h, buf, sizeof buf) == AMDSMI_STATUS_SUCCESS)
         d.memory_partition = buf;
     }
-    if (t_->amdsmi_get_gpu_driver_info) {
+    {
+      std::string raw, module_version;
       amdsmi_driver_info_t di{};
-      if (t_->amdsmi_get_gpu_driver_info(h, &di) == AMDSMI_STATUS_SUCCESS) {
-        d.driver_version = di.driver_version;
-        if (d.driver_version.size() > 64) d.driver_version.resize(64);
-      }
+      if (t_->amdsmi_get_gpu_driver_info && t_->amdsmi_get_gpu_driver_info(h, &di) == AMDSMI_STATUS_SUCCESS)
+        raw.assign(di.driver_version, strnlen(di.driver_version, sizeof di.driver_version));
+      read_file(sys_root_ + "/module/amdgpu/version", &module_version, 256);
+      d.driver_version = driver_version_label(raw, module_version, &d.driver_source);
     }
     if (t_->amdsmi_get_power_info) {
       amdsmi_power_info_t pi{};

@@ -149,6 +149,7 @@ struct MockProc {
   double vram_bytes = 1024.0 * 1024 * 1024;
   double gfx_share = 0.5;  // fraction of device busy time attributed to this process
   bool kfd_only = false;   // HIP compute on KFD user queues: no DRM fdinfo engine time
+  int queues = -1;         // hardware queues it holds on the device (ProcSample::queues; -1 unknown)
 };
 
 struct MockConfig {
@@ -237,7 +238,7 @@ class MockBackend : public Backend {
   std::vector<uint64_t> procs_calls_;  // per dev: processes() calls (procs_fail_every)
   std::vector<int> scan_fail_;       // per dev: occupancy scans still to fail  // per dev: firmware tick the fake SMU is stuck at (-1 = running)
   std::vector<uint64_t> calls_, prewarms_;
-  std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_;
+  std::vector<uint64_t> energy_, xgmi_rd_, xgmi_wr_, busy_acc_, acc_counter_, gfx_act_acc_, pcie_acc_;
   std::vector<uint64_t> lim_acc_;  // per device x XCC x {ppt, thermal, any, low-util}
   std::vector<RasSample> ras_;     // per device (mock RAS state)
   std::map<std::pair<uint32_t, int>, uint64_t> proc_gfx_ns_;

@@ -3,6 +3,7 @@
 
 #include <pthread.h>
 #include <signal.h>
+#include <sys/utsname.h>
 
 #include <fcntl.h>
 #include <unistd.h>
@@ -105,6 +106,40 @@ bool read_file(const std::string& path, std::string* out, size_t max_bytes) {
   }
   ::close(fd);
   return true;
+}
+
+std::string driver_version_label(const std::string& raw_in, const std::string& module_version, std::string* source) {
+  const std::string mv(trim(module_version));
+  if (!mv.empty() && mv.size() <= 64 && mv.find_first_of(" \t\n") == std::string::npos) {
+    *source = "module";
+    return mv;
+  }
+  const std::string raw(trim(raw_in));
+  std::string rest;
+  bool proc_version = raw.empty();
+  for (const char* p : {"Linux version ", "Linuxversion"})
+    if (starts_with(raw, p)) {
+      rest = raw.substr(strlen(p));
+      proc_version = true;
+      break;
+    }
+  if (proc_version) {
+    std::string rel;
+    for (char c : rest) {
+      if (c == ' ' || c == '(' || c == '\t') break;
+      rel.push_back(c);
+    }
+    if (rel.empty()) {
+      struct utsname u {};
+      if (uname(&u) == 0) rel = u.release;
+    }
+    *source = "kernel";
+    return rel;
+  }
+  *source = "library";
+  if (raw.size() <= 64) return raw;
+  const size_t cut = raw.find_last_of(" ,;", 64);
+  return std::string(trim(raw.substr(0, cut == std::string::npos || cut == 0 ? 64 : cut)));
 }
 
 }  // namespace gpumon

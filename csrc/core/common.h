@@ -63,4 +63,13 @@ std::string normalize_bdf(std::string_view s);
 // Reads a whole (small) file; returns false if it cannot be opened.
 bool read_file(const std::string& path, std::string* out, size_t max_bytes = 1 << 20);
 
+// The gpu_info driver_version label. `module_version` (<sysfs>/module/amdgpu/version, present for
+// an out-of-tree / DKMS amdgpu) wins; otherwise libamd_smi's string, which for an in-kernel amdgpu
+// is the kernel's /proc/version (seen on MI355X with its spaces removed: "Linuxversion6.18.51-ant.1
+// (nixbld@localhost)(gcc(GCC)15.3.0,GNUld..."): then the release token ("6.18.51-ant.1", uname -r
+// when the library gave nothing). Long library strings are cut at a separator, never inside a
+// token (the reference's Q6 -- spaces stripped out of values, /root/reference/gpu.py:87 -- is
+// what produced the garbage). *source: "module" | "kernel" | "library".
+std::string driver_version_label(const std::string& raw, const std::string& module_version, std::string* source);
+
 }  // namespace gpumon

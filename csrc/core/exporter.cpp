@@ -230,6 +230,22 @@ bool Exporter::start(std::string* err) {
       return false;
     }
   }
+  if (!cfg_.debug_listen.empty()) {
+    std::string host, e;
+    int port = 0;
+    debug_server_ = parse_debug_listen(cfg_.debug_listen, &host, &port, &e)
+                        ? std::make_unique<HttpServer>(
+                              host, port, 1, [this](const HttpRequest& r, HttpResponse* w) { handle_debug(r, w); },
+                              nullptr)
+                        : nullptr;
+    if (!debug_server_ || !debug_server_->start(&e)) {
+      if (err) *err = e;
+      debug_server_.reset();
+      if (server_) server_->stop();
+      server_.reset();
+      return false;
+    }
+  }
   if (cfg_.interval_s > 0 && cfg_.interval_s < 0.02 && !starts_with(cfg_.backend, "mock"))
     GPUMON_LOG(LogLevel::kWarn, "exporter",
                "interval " + std::to_string(cfg_.interval_s * 1e3) +
@@ -274,6 +290,8 @@ void Exporter::stop() {
   if (podres_.joinable()) podres_.join();
   if (server_) server_->stop();
   server_.reset();
+  if (debug_server_) debug_server_->stop();  // a /debug/wait in flight ended with running_ (above)
+  debug_server_.reset();
   if (!stop_workers() && backend_) {
     // a detached worker is still inside a backend call: never destroy the backend under it
     (void)backend_.release();
@@ -330,6 +348,7 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
   int n = backend_->device_count();
   out->resize(n);
   procs->assign(n, {});
+  info->dev.assign(n, TickDev{});
   // Link metrics (~1.2 ms per device: peer BDF, lane rate, max bandwidth — static while the link
   // state holds) are refreshed every `link_every` ticks, staggered so at most ceil(n / link_every)
   // devices pay it in one tick, and on the tick after a device's per-link status (read every tick
@@ -366,6 +385,7 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
     const int64_t t_seq0 = mono_ns();
     for (int i = 0; i < n; ++i) {
       TraceRange tr("gpumon.sample_dev");
+      const int64_t t_dev0 = mono_ns();
       backend_->sample(i, &(*out)[i]);
       if (links_due(i)) backend_->sample_links(i, &(*out)[i]);
       const int rs = ras_slice(i);
@@ -378,12 +398,14 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
         const bool ok = backend_->processes(i, &(*procs)[i]);
         (*out)[i].procs_read = ok ? 1 : backend_->supports_processes(i) ? -1 : 0;
         proc_ns += mono_ns() - t;
+        info->dev[i].t_procs = (mono_ns() - t) * 1e-9;
         for (auto& ps : (*procs)[i])
           if (has(ps.cu_occupancy)) {
             ps.occ_samples = 1;
             ps.occ_busy = ps.cu_occupancy > 0 ? 1 : 0;
           }
       }
+      info->dev[i].t_device = (mono_ns() - t_dev0) * 1e-9;
     }
     *procs_s = proc_ns * 1e-9;
     info->t_device = (mono_ns() - t_seq0) * 1e-9;
@@ -436,6 +458,8 @@ void Exporter::sample_devices(std::vector<DeviceSample>* out, std::vector<std::v
       proc_ns += w.proc_ns;
       info->t_wake = std::max(info->t_wake, (w.picked_ns - w.started_ns) * 1e-9);
       info->t_device = std::max(info->t_device, w.device_ns * 1e-9);
+      info->dev[i].t_device = w.device_ns * 1e-9;
+      info->dev[i].t_procs = w.proc_ns * 1e-9;
       continue;
     }
     DeviceSample& s = (*out)[i];
@@ -545,6 +569,8 @@ TickInfo Exporter::tick() {
       // amdsmi_get_link_metrics lists 7 entries while the metrics table has 8 xGMI slots on
       // MI355X: a slot no link_metrics entry describes gets speed x width (38 Gb/s x 16 = 608 Gb/s,
       // the value link_metrics reports for every other link).
+      // the firmware's PCIe bandwidth unit (rates.h RateConfig::pcie_bw_unit_bytes) -> bytes/s
+      if (has(s.v[F_PCIE_BW_INST])) s.v[F_PCIE_BW_INST] *= cfg_.rates.pcie_bw_unit_bytes;
       const double lane = s.v[F_XGMI_LINK_SPEED], width = s.v[F_XGMI_LINK_WIDTH];
       for (int k = 0; k < s.n_links; ++k)
         if (s.links[k].status >= 0 && !has(s.links[k].max_bandwidth_gbps) && has(lane) && has(width))
@@ -678,6 +704,24 @@ TickInfo Exporter::tick() {
     }
     info.t_attrib = (mono_ns() - tb) * 1e-9;
     info.devices = n;
+    info.dev.resize(n);  // sample_devices sized it and set the per-device times
+    for (int i = 0; i < n; ++i) {
+      TickDev& d = info.dev[i];
+      d.ok = cur[i].ok;
+      d.fresh = cur[i].fresh;
+      d.gfx_util = cur[i].v[F_GFX_UTIL];
+      const DeviceRates& r = rates[i];
+      d.rates_valid = r.valid;
+      if (!r.valid) continue;
+      double wr = 0, rd = 0;
+      for (int k = 0; k < r.n_links; ++k) {
+        if (has(r.xgmi_wr_Bps[k])) wr += r.xgmi_wr_Bps[k];
+        if (has(r.xgmi_rd_Bps[k])) rd += r.xgmi_rd_Bps[k];
+      }
+      d.xgmi_wr_Bps = wr;
+      d.xgmi_rd_Bps = rd;
+      d.pcie_Bps = r.pcie_Bps;
+    }
     // Whole-backend failure (driver reload, amdsmi lost its handles): re-initialise with backoff
     // instead of exporting gpu_up 0 forever (the reference crashed and relied on the kubelet).
     all_failed_ticks_ = (n > 0 && info.devices_ok == 0) ? all_failed_ticks_ + 1 : 0;

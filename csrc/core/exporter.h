@@ -54,7 +54,11 @@ struct ExporterConfig {
   // /metrics answers only requests with "Authorization: Bearer <the file's token>" (http_auth.h);
   // the health endpoints stay open for the kubelet's probes
   std::string http_auth_token_file;
-  std::string host = "no_name";       // NODE_NAME (reference fallback "no_name", gpu.py:23-24)
+  // Loopback-only introspection server (exporter_debug.cpp): JSON views of the tick log, per-scrape
+  // service times, samples, pod rows and self stats, for benches and tests that run this binary as
+  // its own process. "host:port" on 127.0.0.0/8 or [::1] only; "" = off (the default).
+  std::string debug_listen;
+  std::string host = "no_name";     // NODE_NAME (reference fallback "no_name", gpu.py:23-24)
   bool gzip = true;
   bool roctx = false;                 // ROCTx ranges around sampler phases (also GPUMON_ROCTX=1)
   bool compat_families = true;
@@ -129,6 +133,18 @@ struct ExporterConfig {
   std::string version = "0.1.0";
 };
 
+// One device's headline values at one tick, kept in the tick log: a bench or test reads every
+// tick's values after the fact (/debug/ticks) instead of racing the sampler for each one.
+struct TickDev {
+  bool ok = false, fresh = false, rates_valid = false;
+  double gfx_util = kNaN;      // %, the firmware's average_gfx_activity
+  double xgmi_wr_Bps = kNaN;   // sum over links of the interval write rate (tx)
+  double xgmi_rd_Bps = kNaN;   // ... read rate (rx)
+  double pcie_Bps = kNaN;      // interval PCIe bandwidth (both directions), rates.h
+  double t_device = 0;         // seconds in this device's calls this tick (metrics, links, RAS, processes)
+  double t_procs = 0;          // ... of which the process list
+};
+
 struct TickInfo {
   uint64_t seq = 0;
   double duration_s = 0;  // tick start -> text snapshot published (sample-to-export latency)
@@ -146,6 +162,7 @@ struct TickInfo {
   int link_refreshes = 0;   // devices whose link metrics were re-read this tick
   int ras_reads = 0;        // devices that read a RAS slice this tick
   bool ras_full = false;    // the RAS read covered every file (first tick / ras_slices = 1)
+  std::vector<TickDev> dev;  // per device index
 };
 
 class Exporter {
@@ -165,6 +182,7 @@ class Exporter {
   bool wait_for_seq(uint64_t seq, double timeout_s);  // until a snapshot with seq >= `seq`
 
   int port() const { return server_ ? server_->port() : -1; }
+  int debug_port() const { return debug_server_ ? debug_server_->port() : -1; }
   std::string listen_desc() const { return server_ ? server_->bound() : std::string("(no http)"); }
   std::shared_ptr<const Snapshot> snapshot() const { return store_.get(); }
   std::string render_influx_now();    // line protocol of the latest tick (tests / CLI)
@@ -217,6 +235,7 @@ class Exporter {
  private:
   bool ensure_backend();
   void handle_http(const HttpRequest& req, HttpResponse* resp);
+  void handle_debug(const HttpRequest& req, HttpResponse* resp);  // exporter_debug.cpp
   void sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
                       double* procs_s, TickInfo* info);
   void build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
@@ -226,6 +245,7 @@ class Exporter {
   std::unique_ptr<Backend> backend_;
   std::unique_ptr<Attributor> attr_;
   std::unique_ptr<HttpServer> server_;
+  std::unique_ptr<HttpServer> debug_server_;  // debug_listen (one loop thread, loopback only)
   SnapshotStore store_;
   // /metrics?include=&exclude= bodies of the current snapshot, by query (filtered once per tick and
   // query, at most kFilterCache queries; the next snapshot starts an empty cache)
@@ -395,6 +415,9 @@ class Exporter {
 // "auto": amdsmi if it initialises, else error (never silently mock on a GPU host);
 // "mock" / "mock:gpus=8" etc.
 std::unique_ptr<Backend> make_backend_from_config(const ExporterConfig& cfg, std::string* err);
+
+// debug_listen -> host / port, refusing anything but a loopback address (exporter_debug.cpp).
+bool parse_debug_listen(const std::string& listen, std::string* host, int* port, std::string* err);
 
 // Device-plugin device ID (PCI address, UUID, hip id, cardN, renderDN) -> device index, -1 unknown.
 int match_device_id(const std::string& id, const std::vector<DeviceStatic>& statics);

@@ -59,6 +59,7 @@ bool MockBackend::init(std::string* err) {
     d.compute_partition = "SPX";
     d.memory_partition = "NPS1";
     d.driver_version = "mock";
+    d.driver_source = "library";
     d.vram_total_bytes = 294896.0 * 1048576.0;
     d.power_limit_w = 1400.0;
     d.num_cu = 256;
@@ -86,6 +87,7 @@ bool MockBackend::init(std::string* err) {
   lim_acc_.assign(n * kMaxXcc * 4, 0);
   acc_counter_.assign(n, 100000);  // 1 s of firmware uptime: a live counter is never 0
   gfx_act_acc_.assign(n, 0);
+  pcie_acc_.assign(n, 0);
   t0_ns_ = mono_ns();
   last_ns_.assign(n, t0_ns_);
   // RAS: the blocks MI355X publishes under ras/aca_* (measured), all clean
@@ -241,7 +243,9 @@ void MockBackend::sample(int i, DeviceSample* out) {
   v[F_UCLK_CUR] = 2000.0;
   v[F_PCIE_WIDTH] = 16;
   v[F_PCIE_SPEED_GTS] = 32.0;
-  v[F_PCIE_BW_INST] = 18;
+  // firmware PCIe bandwidth units (x RateConfig::pcie_bw_unit_bytes): idle 18, +100 per % busy
+  const double pcie_units = 18.0 + 100.0 * util;
+  v[F_PCIE_BW_INST] = pcie_units;
   v[F_PCIE_REPLAY] = 0;
   v[F_PCIE_L0_RECOV] = 0;
   v[F_XGMI_LINK_WIDTH] = 16;
@@ -274,6 +278,9 @@ void MockBackend::sample(int i, DeviceSample* out) {
   a.has_activity_acc = true;
   gfx_act_acc_[i] += static_cast<uint64_t>(util * elapsed * 100000.0);
   a.gfx_activity_acc = gfx_act_acc_[i];
+  pcie_acc_[i] += static_cast<uint64_t>(pcie_units * elapsed * 100000.0);
+  a.pcie_bw_acc = pcie_acc_[i];
+  a.has_pcie_bw_acc = true;
   int nx = cfg_.n_xcd;
   out->n_xcd = nx;
   a.n_xcd_acc = nx;
@@ -360,6 +367,7 @@ bool MockBackend::processes(int i, std::vector<ProcSample>* out) {
     ps.gfx_ns = ns + static_cast<uint64_t>((mono_ns() - t0_ns_) * (util / 100.0) * p.gfx_share);
     ps.has_gfx_ns = !p.kfd_only;
     if (cfg_.occupancy) ps.cu_occupancy = occ_value(i, p, util);
+    ps.queues = p.queues;
     out->push_back(std::move(ps));
   }
   return true;

@@ -1,4 +1,4 @@
-// Standalone-binary configuration: YAML subset + env + flags, keyed like gpumon/config.py (options.h).
+// The exporter configuration: YAML subset + env + flags, one key table for every entry point (options.h).
 #include "options.h"
 
 #include <unistd.h>
@@ -11,8 +11,11 @@
 #include <sstream>
 
 #include "common.h"
+#include "http_auth.h"
 #include "http_client.h"
 #include "http_server.h"
+#include "json_out.h"
+#include "tls.h"
 
 namespace gpumon {
 
@@ -161,54 +164,90 @@ std::vector<std::string> as_list(const std::vector<std::string>& vals) {
 }
 
 using Setter = std::function<bool(NativeOptions*, const std::vector<std::string>&, std::string*)>;
+using Getter = std::function<void(const NativeOptions&, JsonOut*, bool redact)>;
 
-Setter str(std::string NativeOptions::*m) {
-  return [m](NativeOptions* o, const std::vector<std::string>& v, std::string*) {
-    o->*m = v.empty() ? "" : v[0];
-    return true;
-  };
-}
+struct Key {
+  OptionKey doc;
+  Setter set;
+  Getter get;
+};
+
+// Accessors take a mutable NativeOptions; the getters only read through them.
 template <class F>
-Setter str_at(F get) {
-  return [get](NativeOptions* o, const std::vector<std::string>& v, std::string*) {
-    *get(o) = v.empty() ? "" : v[0];
-    return true;
-  };
-}
-template <class F>
-Setter bool_at(F get) {
-  return [get](NativeOptions* o, const std::vector<std::string>& v, std::string* e) {
-    return !v.empty() && to_bool(v[0], get(o), e);
-  };
-}
-template <class F>
-Setter int_at(F get) {
-  return [get](NativeOptions* o, const std::vector<std::string>& v, std::string* e) {
-    return !v.empty() && to_int(v[0], get(o), e);
-  };
-}
-template <class F>
-Setter dbl_at(F get) {
-  return [get](NativeOptions* o, const std::vector<std::string>& v, std::string* e) {
-    return !v.empty() && to_double(v[0], get(o), e);
-  };
-}
-template <class F>
-Setter list_at(F get) {
-  return [get](NativeOptions* o, const std::vector<std::string>& v, std::string*) {
-    *get(o) = as_list(v);
-    return true;
-  };
+auto* at(const NativeOptions& o, F get) {
+  return get(const_cast<NativeOptions*>(&o));
 }
 
-const std::map<std::string, Setter>& setters() {
-  static const std::map<std::string, Setter> t = {
-      {"backend", str_at([](NativeOptions* o) { return &o->cfg.backend; })},
-      {"amdsmi_lib", str_at([](NativeOptions* o) { return &o->cfg.amdsmi_lib; })},
-      {"rocm_smi_lib", str_at([](NativeOptions* o) { return &o->cfg.rocm_smi_lib; })},
-      {"fast_path", bool_at([](NativeOptions* o) { return &o->cfg.fast_path; })},
-      {"sysfs_root", str_at([](NativeOptions* o) { return &o->cfg.sysfs_root; })},
-      {"devices",
+template <class F>
+Key str_key(const char* k, const char* sec, const char* help, F get) {
+  return {{k, sec, help},
+          [get](NativeOptions* o, const std::vector<std::string>& v, std::string*) {
+            *get(o) = v.empty() ? "" : v[0];
+            return true;
+          },
+          [get](const NativeOptions& o, JsonOut* j, bool) { j->str(*at(o, get)); }};
+}
+template <class F>
+Key bool_key(const char* k, const char* sec, const char* help, F get) {
+  return {{k, sec, help},
+          [get](NativeOptions* o, const std::vector<std::string>& v, std::string* e) {
+            return !v.empty() && to_bool(v[0], get(o), e);
+          },
+          [get](const NativeOptions& o, JsonOut* j, bool) { j->boolean(*at(o, get)); }};
+}
+template <class F>
+Key int_key(const char* k, const char* sec, const char* help, F get) {
+  return {{k, sec, help},
+          [get](NativeOptions* o, const std::vector<std::string>& v, std::string* e) {
+            return !v.empty() && to_int(v[0], get(o), e);
+          },
+          [get](const NativeOptions& o, JsonOut* j, bool) { j->i64(*at(o, get)); }};
+}
+template <class F>
+Key dbl_key(const char* k, const char* sec, const char* help, F get) {
+  return {{k, sec, help},
+          [get](NativeOptions* o, const std::vector<std::string>& v, std::string* e) {
+            return !v.empty() && to_double(v[0], get(o), e);
+          },
+          [get](const NativeOptions& o, JsonOut* j, bool) { j->num(*at(o, get)); }};
+}
+template <class F>
+Key list_key(const char* k, const char* sec, const char* help, F get) {
+  return {{k, sec, help},
+          [get](NativeOptions* o, const std::vector<std::string>& v, std::string*) {
+            *get(o) = as_list(v);
+            return true;
+          },
+          [get](const NativeOptions& o, JsonOut* j, bool) {
+            j->arr();
+            for (const auto& x : *at(o, get)) j->str(x);
+            j->end_arr();
+          }};
+}
+
+#define O(expr) [](NativeOptions* o) { return &(expr); }
+
+constexpr const char* kBackend = "device backend";
+constexpr const char* kExpo = "exposition";
+constexpr const char* kPush = "influx compat push";
+constexpr const char* kAttr = "attribution";
+constexpr const char* kPlane = "control plane (k8s)";
+constexpr const char* kOnDev = "on-device probe / PMC";
+constexpr const char* kRates = "rates calibration";
+constexpr const char* kLog = "logging";
+
+// Every configuration key, in documentation order: the one table behind the YAML file, the
+// GPUMON_<KEY> environment, the flags (option_flags), --print-config and the Python bindings
+// (gpumon.config is a view of this, docs/configuration.md is generated from it).
+const std::vector<Key>& keys() {
+  static const std::vector<Key> t = {
+      str_key("backend", kBackend, "auto / amdsmi / rocm_smi / mock[:k=v,...] (auto = libamd_smi, rocm_smi_lib if it cannot initialise)",
+              O(o->cfg.backend)),
+      str_key("amdsmi_lib", kBackend, "libamd_smi path tried first", O(o->cfg.amdsmi_lib)),
+      str_key("rocm_smi_lib", kBackend, "librocm_smi64 override (rocm_smi backend / auto fallback)", O(o->cfg.rocm_smi_lib)),
+      bool_key("fast_path", kBackend, "amdsmi: hot per-tick reads straight from sysfs/KFD", O(o->cfg.fast_path)),
+      str_key("sysfs_root", kBackend, "sysfs mount (a host /sys bind-mounted elsewhere, or a test tree)", O(o->cfg.sysfs_root)),
+      {{"devices", kBackend, "hip ids (\"3\") and / or PCI BDFs (\"0000:75:00.0\"); empty = every GPU"},
        [](NativeOptions* o, const std::vector<std::string>& v, std::string* e) {
          std::vector<std::string> ids;
          for (const auto& s : as_list(v)) {
@@ -225,102 +264,263 @@ const std::map<std::string, Setter>& setters() {
          }
          o->cfg.devices = ids;
          return true;
+       },
+       [](const NativeOptions& o, JsonOut* j, bool) {
+         j->arr();
+         for (const auto& x : o.cfg.devices) j->str(x);
+         j->end_arr();
        }},
-      {"interval", dbl_at([](NativeOptions* o) { return &o->cfg.interval_s; })},
-      {"processes", bool_at([](NativeOptions* o) { return &o->cfg.processes; })},
-      {"link_every", int_at([](NativeOptions* o) { return &o->cfg.link_every; })},
-      {"ras_every", int_at([](NativeOptions* o) { return &o->cfg.ras_every; })},
-      {"ras_slices", int_at([](NativeOptions* o) { return &o->cfg.ras_slices; })},
-      {"ras_async", bool_at([](NativeOptions* o) { return &o->cfg.ras_async; })},
-      {"occ_samples", int_at([](NativeOptions* o) { return &o->cfg.occ_samples; })},
-      {"prewarm_ms", dbl_at([](NativeOptions* o) { return &o->cfg.prewarm_ms; })},
-      {"stale_hold_s", dbl_at([](NativeOptions* o) { return &o->cfg.stale_hold_s; })},
-      {"hide_empty_contexts", bool_at([](NativeOptions* o) { return &o->cfg.hide_empty_contexts; })},
-      {"mfma_exclusive_window_s", dbl_at([](NativeOptions* o) { return &o->cfg.mfma_exclusive_window_s; })},
-      {"peer_context_max_vram_mib", dbl_at([](NativeOptions* o) { return &o->cfg.peer_context_max_vram_mib; })},
-      {"sample_threads", int_at([](NativeOptions* o) { return &o->cfg.sample_threads; })},
-      {"rt_priority", int_at([](NativeOptions* o) { return &o->cfg.rt_priority; })},
-      {"device_timeout_s", dbl_at([](NativeOptions* o) { return &o->cfg.device_timeout_s; })},
-      {"reinit_after", int_at([](NativeOptions* o) { return &o->cfg.reinit_after; })},
-      {"init_retry_s", dbl_at([](NativeOptions* o) { return &o->cfg.init_retry_s; })},
-      {"health_stale_s", dbl_at([](NativeOptions* o) { return &o->cfg.health_stale_s; })},
-      {"listen", str(&NativeOptions::listen)},
-      {"http_threads", int_at([](NativeOptions* o) { return &o->cfg.http_threads; })},
-      {"http_rt_priority", int_at([](NativeOptions* o) { return &o->cfg.http_rt_priority; })},
-      {"http_rt_budget", dbl_at([](NativeOptions* o) { return &o->cfg.http_rt_budget; })},
-      {"host", str_at([](NativeOptions* o) { return &o->cfg.host; })},
-      {"gzip", bool_at([](NativeOptions* o) { return &o->cfg.gzip; })},
-      {"roctx", bool_at([](NativeOptions* o) { return &o->cfg.roctx; })},
-      {"compat_families", bool_at([](NativeOptions* o) { return &o->cfg.compat_families; })},
-      {"extended_families", bool_at([](NativeOptions* o) { return &o->cfg.extended_families; })},
-      {"full_device_labels", bool_at([](NativeOptions* o) { return &o->cfg.full_device_labels; })},
-      {"metrics_include", list_at([](NativeOptions* o) { return &o->cfg.metrics_include; })},
-      {"metrics_exclude", list_at([](NativeOptions* o) { return &o->cfg.metrics_exclude; })},
-      {"influx_url", str_at([](NativeOptions* o) { return &o->cfg.influx_url; })},
-      {"influx_token", str_at([](NativeOptions* o) { return &o->cfg.influx_token; })},
-      {"influx_extended", bool_at([](NativeOptions* o) { return &o->cfg.influx_extended; })},
-      {"influx_schema", int_at([](NativeOptions* o) { return &o->cfg.influx_schema; })},
-      {"influx_every", int_at([](NativeOptions* o) { return &o->cfg.influx_every; })},
-      {"influx_gzip", bool_at([](NativeOptions* o) { return &o->cfg.influx_gzip; })},
-      {"influx_ca_file", str_at([](NativeOptions* o) { return &o->cfg.influx_ca_file; })},
-      {"tls_cert_file", str_at([](NativeOptions* o) { return &o->cfg.tls_cert_file; })},
-      {"tls_key_file", str_at([](NativeOptions* o) { return &o->cfg.tls_key_file; })},
-      {"tls_client_ca_file", str_at([](NativeOptions* o) { return &o->cfg.tls_client_ca_file; })},
-      {"http_auth_token_file", str_at([](NativeOptions* o) { return &o->cfg.http_auth_token_file; })},
-      {"influx_tls_insecure", bool_at([](NativeOptions* o) { return &o->cfg.influx_tls_insecure; })},
-      {"influx_client_cert", str_at([](NativeOptions* o) { return &o->cfg.influx_client_cert; })},
-      {"influx_client_key", str_at([](NativeOptions* o) { return &o->cfg.influx_client_key; })},
-      {"procfs_root", str_at([](NativeOptions* o) { return &o->cfg.attribution.procfs_root; })},
-      {"opt_in_label", str_at([](NativeOptions* o) { return &o->cfg.attribution.opt_in; })},
-      {"user_label", str_at([](NativeOptions* o) { return &o->cfg.attribution.user_label; })},
-      {"user_regex", str_at([](NativeOptions* o) { return &o->cfg.attribution.user_regex; })},
-      {"user_prefix", str_at([](NativeOptions* o) { return &o->cfg.attribution.user_prefix; })},
-      {"pod_label_allowlist", list_at([](NativeOptions* o) { return &o->cfg.attribution.label_allowlist; })},
-      {"compat_user_rule", bool_at([](NativeOptions* o) { return &o->cfg.attribution.compat_user_rule; })},
-      {"procfs_env_fallback", bool_at([](NativeOptions* o) { return &o->cfg.attribution.procfs_env_fallback; })},
-      {"include_host_processes",
-       bool_at([](NativeOptions* o) { return &o->cfg.attribution.include_host_processes; })},
-      {"verify_kfd", bool_at([](NativeOptions* o) { return &o->cfg.attribution.verify_kfd; })},
-      {"cri_socket", str(&NativeOptions::cri_socket)},
-      {"docker_socket", str_at([](NativeOptions* o) { return &o->cfg.docker_socket; })},
-      {"pod_log_root", str_at([](NativeOptions* o) { return &o->cfg.pod_log_root; })},
-      {"device_checkpoint", str_at([](NativeOptions* o) { return &o->cfg.device_checkpoint; })},
-      {"pod_resources_socket", str(&NativeOptions::pod_resources_socket)},
-      {"resource_names", list_at([](NativeOptions* o) { return &o->resource_names; })},
-      {"dra_drivers", list_at([](NativeOptions* o) { return &o->cfg.pod_resources_dra_drivers; })},
-      {"metadata_refresh", dbl_at([](NativeOptions* o) { return &o->metadata_refresh_s; })},
-      {"enable_probe", bool_at([](NativeOptions* o) { return &o->od.probe; })},
-      {"probe_every", int_at([](NativeOptions* o) { return &o->probe_every; })},
-      {"enable_pmc", bool_at([](NativeOptions* o) { return &o->od.pmc; })},
-      {"pmc_counters", list_at([](NativeOptions* o) { return &o->od.pmc_counters; })},
-      {"pmc_mode", str_at([](NativeOptions* o) { return &o->od.pmc_mode; })},
-      {"ondevice_isolate", bool_at([](NativeOptions* o) { return &o->od.ondevice_isolate; })},
-      {"helper_retry", dbl_at([](NativeOptions* o) { return &o->od.helper_retry_s; })},
-      {"plugin_dir", str_at([](NativeOptions* o) { return &o->od.plugin_dir; })},
-      {"activity_acc_scale", dbl_at([](NativeOptions* o) { return &o->cfg.rates.activity_acc_scale; })},
-      {"xgmi_kb_bytes", dbl_at([](NativeOptions* o) { return &o->cfg.rates.xgmi_kb_bytes; })},
-      {"log_level", str(&NativeOptions::log_level)},
+      dbl_key("interval", kBackend, "seconds; 0.1 = 10 Hz stress config (the reference slept 10 s, gpu.py:263)", O(o->cfg.interval_s)),
+      bool_key("processes", kBackend, "list GPU processes (pod_gpu rows)", O(o->cfg.processes)),
+      int_key("link_every", kBackend, "ticks between link-metrics refreshes (+ whenever a link's state changes)", O(o->cfg.link_every)),
+      int_key("ras_every", kBackend, "ticks per full RAS / ECC pass (0 = off)", O(o->cfg.ras_every)),
+      int_key("ras_slices", kBackend, "the pass read in this many slices on consecutive ticks (1..ras_every)", O(o->cfg.ras_slices)),
+      bool_key("ras_async", kBackend, "device workers read RAS after publishing a tick (next tick carries it)", O(o->cfg.ras_async)),
+      bool_key("hide_empty_contexts", kBackend, "no pod_gpu row for a GPU context with no VRAM and no waves", O(o->cfg.hide_empty_contexts)),
+      dbl_key("mfma_exclusive_window_s", kBackend,
+              "pod MFMA util only when no other process had waves in the last 5 ticks and this many seconds",
+              O(o->cfg.mfma_exclusive_window_s)),
+      dbl_key("peer_context_max_vram_mib", kBackend,
+              "where KFD's per-process queue list cannot be read: a multi-GPU process's context on a GPU it does not "
+              "work on (<= this VRAM, no waves, a workload on another GPU) gets no row (0 = off)",
+              O(o->cfg.peer_context_max_vram_mib)),
+      int_key("occ_samples", kBackend, "KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)",
+              O(o->cfg.occ_samples)),
+      dbl_key("prewarm_ms", kBackend, "device workers warm the firmware-table path this long before each tick (0 = off)",
+              O(o->cfg.prewarm_ms)),
+      dbl_key("stale_hold_s", kBackend, "a repeated firmware table keeps the last rates only while it is this old (then: invalid)",
+              O(o->cfg.stale_hold_s)),
+      int_key("sample_threads", kBackend, "-1 = one worker per GPU (parallel + watchdog); 0 = sequential", O(o->cfg.sample_threads)),
+      int_key("rt_priority", kBackend, "SCHED_FIFO priority of the sampler + device workers (needs CAP_SYS_NICE)", O(o->cfg.rt_priority)),
+      dbl_key("device_timeout_s", kBackend, "a device call still running after this is exported as hung", O(o->cfg.device_timeout_s)),
+      int_key("reinit_after", kBackend, "ticks with every GPU failing before the backend is re-initialised", O(o->cfg.reinit_after)),
+      dbl_key("init_retry_s", kBackend, "backoff between backend init attempts", O(o->cfg.init_retry_s)),
+      dbl_key("health_stale_s", kBackend, "/healthz 503 after this long without a tick (0 = max(3*interval, 10 s))", O(o->cfg.health_stale_s)),
+      str_key("listen", kExpo, "host:port / [v6]:port / :port (every address, dual-stack; IPv4 if no IPv6)", O(o->listen)),
+      int_key("http_threads", kExpo, "HTTP loop threads serving /metrics", O(o->cfg.http_threads)),
+      int_key("http_rt_priority", kExpo, "SCHED_FIFO HTTP loops (CAP_SYS_NICE), each capped at http_rt_budget of a CPU",
+              O(o->cfg.http_rt_priority)),
+      dbl_key("http_rt_budget", kExpo, "share of a CPU per 100 ms an RT HTTP loop may use before it is demoted", O(o->cfg.http_rt_budget)),
+      str_key("tls_cert_file", kExpo, "/metrics over HTTPS: PEM certificate chain (with tls_key_file)", O(o->cfg.tls_cert_file)),
+      str_key("tls_key_file", kExpo, "... its PEM private key", O(o->cfg.tls_key_file)),
+      str_key("tls_client_ca_file", kExpo,
+              "mutual TLS: /metrics needs a client certificate signed by this CA (the health endpoints stay open "
+              "for the kubelet's probes)",
+              O(o->cfg.tls_client_ca_file)),
+      str_key("http_auth_token_file", kExpo, "/metrics needs \"Authorization: Bearer <the file's token>\" (health endpoints stay open)",
+              O(o->cfg.http_auth_token_file)),
+      str_key("debug_listen", kExpo,
+              "loopback-only JSON introspection (/debug/state, /debug/ticks, /debug/scrapes, ...) for benches and "
+              "tests; \"\" = off",
+              O(o->cfg.debug_listen)),
+      str_key("host", kExpo, "node name label (default $NODE_NAME, then the host name, then \"no_name\")", O(o->cfg.host)),
+      bool_key("gzip", kExpo, "gzip /metrics for scrapers that accept it", O(o->cfg.gzip)),
+      bool_key("compat_families", kExpo, "serve the reference's node_gpu_* / pod_gpu_* families", O(o->cfg.compat_families)),
+      bool_key("extended_families", kExpo, "serve the MI355X gpu_* families", O(o->cfg.extended_families)),
+      bool_key("full_device_labels", kExpo, "uuid + bdf on every device series (default: on gpu_info only)", O(o->cfg.full_device_labels)),
+      list_key("metrics_include", kExpo, "serve only families matching these globs (e.g. node_gpu_*)", O(o->cfg.metrics_include)),
+      list_key("metrics_exclude", kExpo, "drop families matching these globs (e.g. gpu_xcd_*); Influx unfiltered", O(o->cfg.metrics_exclude)),
+      {{"influx_url", kPush, "http(s)://[user:password@]host[:port]/path?query; checked at startup (exit 2 if unusable)"},
+       [](NativeOptions* o, const std::vector<std::string>& v, std::string*) {
+         o->cfg.influx_url = v.empty() ? "" : v[0];
+         return true;
+       },
+       [](const NativeOptions& o, JsonOut* j, bool redact) { j->str(redact ? redact_url(o.cfg.influx_url) : o.cfg.influx_url); }},
+      {{"influx_token", kPush, "InfluxDB 2.x/3.x API token (env INFLUXDB_TOKEN, from a Secret); 1.x: user:password@ in the URL"},
+       [](NativeOptions* o, const std::vector<std::string>& v, std::string*) {
+         o->cfg.influx_token = v.empty() ? "" : v[0];
+         return true;
+       },
+       [](const NativeOptions& o, JsonOut* j, bool redact) {
+         j->str(redact && !o.cfg.influx_token.empty() ? std::string("***") : o.cfg.influx_token);
+       }},
+      bool_key("influx_extended", kPush, "also push the MI355X fields", O(o->cfg.influx_extended)),
+      int_key("influx_schema", kPush, "2019 = gpu.py layout; 2018 = img/influxdb.png pod_gpu layout", O(o->cfg.influx_schema)),
+      int_key("influx_every", kPush, "ticks per push", O(o->cfg.influx_every)),
+      bool_key("influx_gzip", kPush, "gzip each push (Content-Encoding: gzip): 7-8x fewer bytes for 8 GPUs", O(o->cfg.influx_gzip)),
+      str_key("influx_ca_file", kPush, "https:// push: PEM CA bundle replacing the system one", O(o->cfg.influx_ca_file)),
+      bool_key("influx_tls_insecure", kPush, "https:// push WITHOUT certificate / host-name checks (opt-in, testing)",
+               O(o->cfg.influx_tls_insecure)),
+      str_key("influx_client_cert", kPush, "https:// push: PEM client chain for mutual TLS", O(o->cfg.influx_client_cert)),
+      str_key("influx_client_key", kPush, "... and its key (default: in the chain file)", O(o->cfg.influx_client_key)),
+      str_key("procfs_root", kAttr, "/proc of the host (hostPID)", O(o->cfg.attribution.procfs_root)),
+      str_key("opt_in_label", kAttr, "only report pods with this label KEY=VALUE (reference: mlgpu=mlgpu, gpu.py:186-188)",
+              O(o->cfg.attribution.opt_in)),
+      str_key("user_label", kAttr, "pod label holding the user name", O(o->cfg.attribution.user_label)),
+      str_key("user_regex", kAttr, "regex on the pod name; group 1 = user", O(o->cfg.attribution.user_regex)),
+      list_key("pod_label_allowlist", kAttr,
+               "pod / container label keys copied onto pod_gpu_* series as label_<key> (kube-state-metrics style)",
+               O(o->cfg.attribution.label_allowlist)),
+      str_key("user_prefix", kAttr, "pod-name prefix of the reference's user rule (gpu.py:196)", O(o->cfg.attribution.user_prefix)),
+      bool_key("compat_user_rule", kAttr, "the reference's user-name rule when no label / regex names the user",
+               O(o->cfg.attribution.compat_user_rule)),
+      bool_key("procfs_env_fallback", kAttr, "pod name / namespace from the process's HOSTNAME and service-account files",
+               O(o->cfg.attribution.procfs_env_fallback)),
+      bool_key("include_host_processes", kAttr, "GPU processes outside any container get rows too",
+               O(o->cfg.attribution.include_host_processes)),
+      bool_key("verify_kfd", kAttr, "trust /proc/<pid> only when it holds /dev/kfd (guards a foreign pid namespace)",
+               O(o->cfg.attribution.verify_kfd)),
+      {{"control_plane", kPlane, "native: the kubelet PodResources / CRI / Docker / log-tree pollers; off: none of them"},
+       [](NativeOptions* o, const std::vector<std::string>& v, std::string* e) {
+         const std::string x = v.empty() ? "" : v[0];
+         if (x != "native" && x != "off") {
+           *e = "native or off, not '" + x + "'";
+           return false;
+         }
+         o->control_plane = x;
+         return true;
+       },
+       [](const NativeOptions& o, JsonOut* j, bool) { j->str(o.control_plane); }},
+      str_key("cri_socket", kPlane, "e.g. unix:///run/containerd/containerd.sock; \"\" = autodetect; none = off", O(o->cri_socket)),
+      str_key("pod_resources_socket", kPlane, "kubelet PodResources socket (idle-allocation rows); \"\" = off",
+              O(o->pod_resources_socket)),
+      str_key("docker_socket", kPlane, "plain-Docker nodes: Docker Engine container names + labels; opt-in, e.g. /var/run/docker.sock",
+              O(o->cfg.docker_socket)),
+      str_key("pod_log_root", kPlane, "non-root metadata: the kubelet's log tree (containers/ + pods/ under it), e.g. /var/log; \"\" = off",
+              O(o->cfg.pod_log_root)),
+      str_key("device_checkpoint", kPlane,
+              "GPU allocations from the kubelet's device-plugin checkpoint, e.g. "
+              "/var/lib/kubelet/device-plugins/kubelet_internal_checkpoint; \"\" = off",
+              O(o->cfg.device_checkpoint)),
+      list_key("resource_names", kPlane, "extended resources that are GPUs (the first one is counted)", O(o->resource_names)),
+      {{"dra_drivers", kPlane, "DRA drivers whose claimed devices count as GPU allocations ('none' or [] = off)"},
+       [](NativeOptions* o, const std::vector<std::string>& v, std::string*) {
+         auto l = as_list(v);
+         if (l.size() == 1 && l[0] == "none") l.clear();
+         o->cfg.pod_resources_dra_drivers = l;
+         return true;
+       },
+       [](const NativeOptions& o, JsonOut* j, bool) {
+         j->arr();
+         for (const auto& x : o.cfg.pod_resources_dra_drivers) j->str(x);
+         j->end_arr();
+       }},
+      dbl_key("metadata_refresh", kPlane, "seconds between control-plane refreshes", O(o->metadata_refresh_s)),
+      bool_key("enable_probe", kOnDev, "K1 gfx950 probe kernel (per-XCD clock / liveness / dispatch latency)", O(o->od.probe)),
+      int_key("probe_every", kOnDev, "K1 probe every N sampling intervals", O(o->probe_every)),
+      int_key("probe_blocks", kOnDev, "one-wave workgroups per probe launch (>= 4 per CU spreads over all 8 XCDs)",
+              O(o->od.probe_blocks)),
+      bool_key("enable_pmc", kOnDev, "rocprofiler-sdk device counting (MFMA utilisation, TFLOP/s per dtype)", O(o->od.pmc)),
+      list_key("pmc_counters", kOnDev,
+               "counters of the PMC derivation (8 SQ + 2 GRBM: one gfx950 counting pass): MFMA busy + MOPS per operand type",
+               O(o->od.pmc_counters)),
+      str_key("pmc_mode", kOnDev,
+              "continuous: counting contexts read without a stop (100 % of each interval); window: start -> pmc_window -> stop",
+              O(o->od.pmc_mode)),
+      dbl_key("pmc_window", kOnDev, "window mode: counting window per sample in seconds (capped at half the period)",
+              O(o->od.pmc_window_s)),
+      bool_key("ondevice_isolate", kOnDev,
+               "the counting contexts and the probe in a helper process frozen between reads (rocprofiler-sdk leaves an "
+               "HSA thread polling a full core in the process that owns them)",
+               O(o->od.ondevice_isolate)),
+      dbl_key("helper_retry", kOnDev, "seconds before a dead helper is respawned (doubling while it keeps dying)", O(o->od.helper_retry_s)),
+      str_key("plugin_dir", kOnDev, "directory holding libgpumon_pmc.so / libgpumon_probe.so (\"\" = <tree>/lib or $GPUMON_PLUGIN_DIR)",
+              O(o->od.plugin_dir)),
+      dbl_key("activity_acc_scale", kRates, "avg % = d(activity acc) / d(accumulation_counter) x this", O(o->cfg.rates.activity_acc_scale)),
+      dbl_key("xgmi_kb_bytes", kRates, "bytes per xGMI \"KB\" accumulator unit", O(o->cfg.rates.xgmi_kb_bytes)),
+      dbl_key("pcie_bw_unit_bytes", kRates,
+              "bytes/s per firmware PCIe bandwidth unit (102400 measured on MI355X against pinned host copies)",
+              O(o->cfg.rates.pcie_bw_unit_bytes)),
+      str_key("log_level", kLog, "debug / info / warn / error", O(o->log_level)),
+      bool_key("roctx", kLog, "ROCTx ranges around the sampler phases (rocprofv3 --marker-trace)", O(o->cfg.roctx)),
+      // a key of earlier releases (it selected the Python test oracles): accepted, no effect
+      {{"ondevice", "", ""},
+       [](NativeOptions*, const std::vector<std::string>&, std::string*) { return true; },
+       nullptr},
   };
   return t;
 }
 
-void json_str(const std::string& s, std::string* o) {
-  o->push_back('"');
-  for (char c : s) {
-    if (c == '"' || c == '\\') o->push_back('\\');
-    if (c == '\n') {
-      o->append("\\n");
-      continue;
-    }
-    if (static_cast<unsigned char>(c) < 0x20) continue;
-    o->push_back(c);
-  }
-  o->push_back('"');
+#undef O
+
+const Key* find_key(const std::string& k) {
+  static const std::map<std::string, const Key*> idx = [] {
+    std::map<std::string, const Key*> m;
+    for (const auto& x : keys()) m[x.doc.key] = &x;
+    return m;
+  }();
+  auto it = idx.find(k);
+  return it == idx.end() ? nullptr : it->second;
 }
 
 }  // namespace
 
+const std::vector<OptionKey>& option_keys() {
+  static const std::vector<OptionKey> v = [] {
+    std::vector<OptionKey> out;
+    for (const auto& k : keys())
+      if (k.get) out.push_back(k.doc);
+    return out;
+  }();
+  return v;
+}
+
+const std::vector<OptionFlag>& option_flags() {
+  // {flag, aliases, key, fixed value (nullptr: the flag takes one), help}
+  static const std::vector<OptionFlag> t = {
+      {"--backend", "", "backend", nullptr, "auto | amdsmi | rocm_smi | mock[:k=v,..]"},
+      {"--devices", "", "devices", nullptr, "comma-separated hip ids and / or PCI BDFs to monitor (default all)"},
+      {"--interval", "", "interval", nullptr, "sampling interval in seconds"},
+      {"--listen", "", "listen", nullptr, "HOST:PORT, [V6]:PORT or :PORT for /metrics"},
+      {"--host", "", "host", nullptr, "node name label (default $NODE_NAME, then the host name)"},
+      {"--no-fast-path", "", "fast_path", "false", "amdsmi: read every value through libamd_smi"},
+      {"--sysfs-root", "--sysfs", "sysfs_root", nullptr, "sysfs mount"},
+      {"--procfs-root", "--procfs", "procfs_root", nullptr, "procfs mount of the host"},
+      {"--no-processes", "", "processes", "false", "no process list (no pod_gpu rows)"},
+      {"--ras-every", "", "ras_every", nullptr, "RAS error counters every N ticks"},
+      {"--ras-slices", "", "ras_slices", nullptr, "RAS blocks read in N slices over N ticks"},
+      {"--device-timeout", "", "device_timeout_s", nullptr, "seconds before a device call is exported as hung"},
+      {"--sample-threads", "", "sample_threads", nullptr, "per-GPU sampling threads (-1 = one per GPU, 0 = sequential)"},
+      {"--rt-priority", "", "rt_priority", nullptr, "SCHED_FIFO priority of the sampler (0 = normal)"},
+      {"--prewarm-ms", "", "prewarm_ms", nullptr, "warm the firmware-table read this long before each tick (0 = off)"},
+      {"--http-threads", "", "http_threads", nullptr, "HTTP loop threads serving /metrics"},
+      {"--http-rt-priority", "", "http_rt_priority", nullptr, "SCHED_FIFO priority of the HTTP loops (0 = normal)"},
+      {"--tls-cert-file", "", "tls_cert_file", nullptr, "serve /metrics over HTTPS: PEM certificate chain"},
+      {"--tls-key-file", "", "tls_key_file", nullptr, "... and its PEM private key"},
+      {"--tls-client-ca-file", "", "tls_client_ca_file", nullptr, "mutual TLS on /metrics: clients need a certificate signed by this CA"},
+      {"--http-auth-token-file", "", "http_auth_token_file", nullptr, "/metrics needs 'Authorization: Bearer <token>' from this file"},
+      {"--debug-listen", "", "debug_listen", nullptr, "loopback HOST:PORT for the JSON introspection endpoints"},
+      {"--no-gzip", "", "gzip", "false", "never gzip /metrics"},
+      {"--metrics-include", "", "metrics_include", nullptr, "comma-separated globs: serve only these families"},
+      {"--metrics-exclude", "", "metrics_exclude", nullptr, "comma-separated globs: families left out of /metrics"},
+      {"--influx-url", "", "influx_url", nullptr, "enable the InfluxDB line-protocol push (default $INFLUXDB_URL)"},
+      {"--influx-token", "", "influx_token", nullptr, "InfluxDB 2.x / 3.x API token (default $INFLUXDB_TOKEN)"},
+      {"--influx-extended", "", "influx_extended", "true", "also push the MI355X fields"},
+      {"--influx-gzip", "", "influx_gzip", "true", "gzip each push"},
+      {"--influx-schema", "", "influx_schema", nullptr, "pod_gpu line layout: 2019 (gpu.py) or 2018 (img/influxdb.png)"},
+      {"--influx-ca-file", "", "influx_ca_file", nullptr, "PEM CA bundle for an https:// INFLUXDB_URL"},
+      {"--influx-tls-insecure", "", "influx_tls_insecure", "true", "do NOT verify the InfluxDB server's certificate (testing only)"},
+      {"--influx-client-cert", "", "influx_client_cert", nullptr, "PEM client certificate for the push (mutual TLS)"},
+      {"--influx-client-key", "", "influx_client_key", nullptr, "PEM client key for the push"},
+      {"--opt-in-label", "", "opt_in_label", nullptr, "only report pods with label KEY=VALUE"},
+      {"--user-regex", "", "user_regex", nullptr, "regex on the pod name; group 1 = user"},
+      {"--user-label", "", "user_label", nullptr, "pod label holding the user name"},
+      {"--pod-labels", "", "pod_label_allowlist", nullptr, "comma-separated pod label keys exported as label_<key>"},
+      {"--control-plane", "", "control_plane", nullptr, "native | off: the kubelet / CRI / Docker metadata pollers"},
+      {"--cri-socket", "--cri", "cri_socket", nullptr, "CRI runtime socket (default: autodetect)"},
+      {"--no-cri", "", "cri_socket", "none", "no CRI runtime lookup"},
+      {"--pod-resources-socket", "--pod-resources", "pod_resources_socket", nullptr, "kubelet PodResources socket"},
+      {"--no-pod-resources", "", "pod_resources_socket", "", "no kubelet PodResources polling (no idle-allocation rows)"},
+      {"--docker-socket", "--docker", "docker_socket", nullptr, "plain-Docker nodes: the Docker Engine socket (opt-in)"},
+      {"--pod-log-root", "--pod-logs", "pod_log_root", nullptr, "non-root metadata: the kubelet's log tree, e.g. /var/log"},
+      {"--device-checkpoint", "", "device_checkpoint", nullptr, "GPU allocations from the device-plugin checkpoint file"},
+      {"--dra-drivers", "", "dra_drivers", nullptr, "comma-separated DRA driver names ('none' = off)"},
+      {"--enable-pmc", "--pmc", "enable_pmc", "true", "rocprofiler-sdk device counting (MFMA utilisation, TFLOP/s)"},
+      {"--pmc-counters", "", "pmc_counters", nullptr, "comma-separated PMC counters"},
+      {"--pmc-mode", "", "pmc_mode", nullptr, "continuous | window"},
+      {"--pmc-window", "", "pmc_window", nullptr, "window mode: counting window in seconds"},
+      {"--enable-probe-kernel", "--probe", "enable_probe", "true", "the K1 gfx950 probe kernel"},
+      {"--probe-every", "", "probe_every", nullptr, "K1 probe every N ticks"},
+      {"--probe-blocks", "", "probe_blocks", nullptr, "one-wave workgroups per probe launch"},
+      {"--plugin-dir", "", "plugin_dir", nullptr, "directory holding libgpumon_pmc.so / libgpumon_probe.so"},
+      {"--roctx", "", "roctx", "true", "bracket the sampler phases with ROCTx ranges"},
+      {"--log-level", "", "log_level", nullptr, "debug | info | warn | error"},
+  };
+  return t;
+}
+
 bool parse_yaml_subset(const std::string& text, YamlDoc* doc, std::string* err) {
+
   std::istringstream in(text);
   std::string line, pending;  // pending: key awaiting block-list items
   int lineno = 0, base_indent = -1, top_indent = -1;
@@ -387,11 +587,10 @@ bool parse_yaml_subset(const std::string& text, YamlDoc* doc, std::string* err) 
 }
 
 int options_set(NativeOptions* o, const std::string& key, const std::vector<std::string>& vals, std::string* err) {
-  const auto& t = setters();
-  auto it = t.find(key);
-  if (it == t.end()) return 0;
+  const Key* k = find_key(key);
+  if (!k) return 0;
   std::string e;
-  if (!it->second(o, vals, &e)) {
+  if (!k->set(o, vals, &e)) {
     *err = key + ": " + (e.empty() ? "missing value" : e);
     return -1;
   }
@@ -437,7 +636,8 @@ bool options_apply_env(NativeOptions* o, char** envp, std::string* err) {
     const size_t eq = kv.find('=');
     if (eq == std::string::npos || !starts_with(kv, "GPUMON_")) continue;
     std::string k = kv.substr(7, eq - 7);
-    if (k == "CONFIG" || k == "AMDSMI_LIB" || k == "PLUGIN_DIR" || k == "ROCTX") continue;  // read where used
+    // the file name itself, and an extra library path the backend tries after amdsmi_lib
+    if (k == "CONFIG" || k == "AMDSMI_LIB") continue;
     for (auto& c : k) c = static_cast<char>(tolower(static_cast<unsigned char>(c)));
     std::string e;
     if (options_set(o, k, {kv.substr(eq + 1)}, &e) < 0) {
@@ -448,144 +648,176 @@ bool options_apply_env(NativeOptions* o, char** envp, std::string* err) {
   return true;
 }
 
+const OptionFlag* find_flag(const std::string& arg) {
+  for (const auto& f : option_flags()) {
+    if (arg == f.flag) return &f;
+    for (const auto& a : split(f.aliases, ','))
+      if (!a.empty() && arg == a) return &f;
+  }
+  return nullptr;
+}
+
+ParseStatus options_parse(NativeOptions* o, const std::vector<std::string>& args, char** envp,
+                          std::vector<std::string>* rest, std::vector<std::string>* warnings, std::string* err) {
+  // 1. the file: --config wins over GPUMON_CONFIG
+  std::string config;
+  for (char** p = envp; p && *p; ++p)
+    if (starts_with(*p, "GPUMON_CONFIG=")) config = *p + strlen("GPUMON_CONFIG=");
+  bool compat = false;
+  for (size_t i = 0; i < args.size(); ++i) {
+    if (args[i] == "--config" && i + 1 < args.size()) config = args[i + 1];
+    else if (starts_with(args[i], "--config=")) config = args[i].substr(9);
+    else if (args[i] == "--compat") compat = true;
+  }
+  if (!config.empty()) {
+    std::vector<std::string> unknown;
+    if (!options_load_file(o, config, &unknown, err)) return ParseStatus::kBadFile;
+    if (warnings)
+      for (const auto& k : unknown) warnings->push_back("config: key '" + k + "' is not a configuration key (ignored)");
+  }
+  // 2. the environment
+  if (!options_apply_env(o, envp, err)) return ParseStatus::kBadEnv;
+  // 3. --compat (the reference's behaviour: opt-in label mlgpu=mlgpu, 10 s interval) between the
+  // environment and the flags: explicit flags still win
+  if (compat) {
+    if (o->cfg.attribution.opt_in.empty()) o->cfg.attribution.opt_in = "mlgpu=mlgpu";
+    o->cfg.interval_s = 10.0;
+  }
+  // 4. the flags, in order
+  for (size_t i = 0; i < args.size(); ++i) {
+    std::string a = args[i], val;
+    bool inline_val = false;
+    if (a == "--config") {
+      ++i;
+      continue;
+    }
+    if (a == "--compat" || starts_with(a, "--config=")) continue;
+    const size_t eq = starts_with(a, "--") ? a.find('=') : std::string::npos;
+    if (eq != std::string::npos) {
+      val = a.substr(eq + 1);
+      a = a.substr(0, eq);
+      inline_val = true;
+    }
+    const OptionFlag* f = find_flag(a);
+    if (!f) {
+      if (!rest) {
+        *err = "unknown flag " + args[i];
+        return ParseStatus::kBadFlag;
+      }
+      rest->push_back(args[i]);
+      continue;
+    }
+    if (f->fixed) {
+      if (inline_val) {
+        *err = a + " takes no value";
+        return ParseStatus::kBadFlag;
+      }
+      val = f->fixed;
+    } else if (!inline_val) {
+      if (i + 1 >= args.size()) {
+        *err = a + ": missing value";
+        return ParseStatus::kBadFlag;
+      }
+      val = args[++i];
+    }
+    std::string e;
+    if (options_set(o, f->key, {val}, &e) < 0) {
+      *err = a + ": " + e.substr(e.find(": ") == std::string::npos ? 0 : e.find(": ") + 2);
+      return ParseStatus::kBadValue;
+    }
+  }
+  return ParseStatus::kOk;
+}
+
+// Well-known CRI runtime sockets, first existing one wins ("" cri_socket = autodetect).
+static const char* const kCriSockets[] = {"/run/containerd/containerd.sock", "/var/run/containerd/containerd.sock",
+                                          "/var/run/crio/crio.sock",         "/run/crio/crio.sock",
+                                          "/var/run/cri-dockerd.sock",       "/var/run/dockershim.sock"};
+
+const std::vector<std::string>& cri_autodetect_sockets() {
+  static const std::vector<std::string> v(std::begin(kCriSockets), std::end(kCriSockets));
+  return v;
+}
+
 bool options_finalize(NativeOptions* o, std::string* err) {
   ExporterConfig& c = o->cfg;
   if (!parse_listen(o->listen, &c.listen_addr, &c.port, err)) return false;
-  if (c.host.empty()) c.host = "no_name";
+  if (!c.debug_listen.empty()) {
+    std::string h;
+    int p = 0;
+    if (!parse_debug_listen(c.debug_listen, &h, &p, err)) return false;
+  }
+  // host: NODE_NAME (options_apply_env) > the machine's host name > the reference's "no_name"
+  // (gpu.py:23-24, which never reached its lines: quirk Q1)
+  if (c.host.empty()) {
+    char hn[256] = {0};
+    c.host = gethostname(hn, sizeof hn - 1) == 0 && hn[0] ? hn : "no_name";
+  }
   if (!o->resource_names.empty()) c.pod_resources_prefix = o->resource_names[0];
   c.pod_resources_refresh_s = o->metadata_refresh_s;
-  if (!o->pod_resources_socket.empty() && o->pod_resources_socket != "none" &&
-      access(o->pod_resources_socket.c_str(), F_OK) == 0)
-    c.pod_resources_socket = o->pod_resources_socket;
-  std::string cri = o->cri_socket;
-  if (starts_with(cri, "unix://")) cri = cri.substr(7);
-  if (cri.empty()) {
-    for (const char* s : {"/run/containerd/containerd.sock", "/var/run/crio/crio.sock", "/run/crio/crio.sock",
-                          "/var/run/cri-dockerd.sock", "/var/run/dockershim.sock"})
-      if (access(s, F_OK) == 0) {
-        cri = s;
-        break;
-      }
+  c.pod_resources_socket.clear();
+  c.cri_socket.clear();
+  if (o->control_plane == "off") {
+    // no kubelet / CRI / Docker / log-tree metadata pollers
+    c.docker_socket.clear();
+    c.pod_log_root.clear();
+    c.device_checkpoint.clear();
+  } else {
+    if (!o->pod_resources_socket.empty() && o->pod_resources_socket != "none" &&
+        access(o->pod_resources_socket.c_str(), F_OK) == 0)
+      c.pod_resources_socket = o->pod_resources_socket;
+    std::string cri = o->cri_socket;
+    if (starts_with(cri, "unix://")) cri = cri.substr(7);
+    if (cri.empty())
+      for (const auto& s : cri_autodetect_sockets())
+        if (access(s.c_str(), F_OK) == 0) {
+          cri = s;
+          break;
+        }
+    if (!cri.empty() && cri != "none") c.cri_socket = cri;
+    if (starts_with(c.docker_socket, "unix://")) c.docker_socket = c.docker_socket.substr(7);
   }
-  if (!cri.empty() && cri != "none") c.cri_socket = cri;
   const double period = c.interval_s > 0 ? std::max(c.interval_s, 0.1) : 1.0;
   o->od.pmc_every_s = period;
   o->od.probe_every_s = period * std::max(1, o->probe_every);
-  const std::string& l = o->log_level;
-  g_log_level = l == "debug" ? 0 : l == "info" ? 1 : (l == "warn" || l == "warning") ? 2 : l == "error" ? 3 : 1;
   return true;
 }
 
-std::string options_json(const NativeOptions& o) {
-  const ExporterConfig& c = o.cfg;
-  std::string s = "{";
-  bool first = true;
-  auto key = [&](const char* k) {
-    if (!first) s += ", ";
-    first = false;
-    json_str(k, &s);
-    s += ": ";
-  };
-  auto S = [&](const char* k, const std::string& v) {
-    key(k);
-    json_str(v, &s);
-  };
-  auto B = [&](const char* k, bool v) {
-    key(k);
-    s += v ? "true" : "false";
-  };
-  auto N = [&](const char* k, double v) {
-    key(k);
-    char b[64];
-    snprintf(b, sizeof b, "%.17g", v);
-    s += b;
-  };
-  auto L = [&](const char* k, const std::vector<std::string>& v) {
-    key(k);
-    s += "[";
-    for (size_t i = 0; i < v.size(); ++i) {
-      if (i) s += ", ";
-      json_str(v[i], &s);
+int options_log_level(const NativeOptions& o) {
+  const std::string& l = o.log_level;
+  return l == "debug" ? 0 : l == "info" ? 1 : (l == "warn" || l == "warning") ? 2 : l == "error" ? 3 : l == "off" ? 4 : 1;
+}
+
+std::string options_validate(const NativeOptions& o) {
+  const ExporterConfig& cfg = o.cfg;
+  // an Influx push that cannot work is a startup error, not a silently idle pusher
+  TlsOptions t;
+  t.ca_file = cfg.influx_ca_file;
+  t.insecure = cfg.influx_tls_insecure;
+  t.client_cert = cfg.influx_client_cert;
+  t.client_key = cfg.influx_client_key;
+  std::string e = check_push_config(cfg.influx_url, cfg.influx_token, t);
+  if (!e.empty()) return e;
+  // /metrics over HTTPS: the certificate, key and client CA must load
+  e = check_serve_tls(cfg.tls_cert_file, cfg.tls_key_file, cfg.tls_client_ca_file);
+  if (!e.empty()) return e;
+  // /metrics behind a bearer token: the token file must hold one
+  e = check_auth_token_file(cfg.http_auth_token_file);
+  if (!e.empty()) return "http_auth_token_file: " + e;
+  if (o.od.pmc_mode != "continuous" && o.od.pmc_mode != "window") return "pmc_mode: continuous or window, not '" + o.od.pmc_mode + "'";
+  return "";
+}
+
+std::string options_json(const NativeOptions& o, bool redact) {
+  JsonOut j;
+  j.obj();
+  for (const auto& k : keys())
+    if (k.get) {
+      j.key(k.doc.key);
+      k.get(o, &j, redact);
     }
-    s += "]";
-  };
-  S("backend", c.backend);
-  B("fast_path", c.fast_path);
-  S("sysfs_root", c.sysfs_root);
-  L("devices", c.devices);
-  N("interval", c.interval_s);
-  B("processes", c.processes);
-  N("link_every", c.link_every);
-  N("ras_every", c.ras_every);
-  N("ras_slices", c.ras_slices);
-  B("ras_async", c.ras_async);
-  N("occ_samples", c.occ_samples);
-  N("prewarm_ms", c.prewarm_ms);
-  N("stale_hold_s", c.stale_hold_s);
-  B("hide_empty_contexts", c.hide_empty_contexts);
-  N("mfma_exclusive_window_s", c.mfma_exclusive_window_s);
-  N("peer_context_max_vram_mib", c.peer_context_max_vram_mib);
-  N("sample_threads", c.sample_threads);
-  N("rt_priority", c.rt_priority);
-  N("device_timeout_s", c.device_timeout_s);
-  N("reinit_after", c.reinit_after);
-  N("init_retry_s", c.init_retry_s);
-  N("health_stale_s", c.health_stale_s);
-  S("listen", o.listen);
-  N("http_threads", c.http_threads);
-  N("http_rt_priority", c.http_rt_priority);
-  N("http_rt_budget", c.http_rt_budget);
-  S("host", c.host);
-  B("gzip", c.gzip);
-  B("roctx", c.roctx);
-  B("compat_families", c.compat_families);
-  B("extended_families", c.extended_families);
-  L("metrics_include", c.metrics_include);
-  L("metrics_exclude", c.metrics_exclude);
-  S("influx_url", redact_url(c.influx_url));
-  S("influx_token", c.influx_token.empty() ? "" : "***");
-  B("influx_extended", c.influx_extended);
-  N("influx_schema", c.influx_schema);
-  N("influx_every", c.influx_every);
-  B("influx_gzip", c.influx_gzip);
-  S("influx_ca_file", c.influx_ca_file);
-  S("tls_cert_file", c.tls_cert_file);
-  S("tls_key_file", c.tls_key_file);
-  S("tls_client_ca_file", c.tls_client_ca_file);
-  S("http_auth_token_file", c.http_auth_token_file);
-  B("influx_tls_insecure", c.influx_tls_insecure);
-  S("influx_client_cert", c.influx_client_cert);
-  S("influx_client_key", c.influx_client_key);
-  S("procfs_root", c.attribution.procfs_root);
-  S("opt_in_label", c.attribution.opt_in);
-  S("user_label", c.attribution.user_label);
-  S("user_regex", c.attribution.user_regex);
-  S("user_prefix", c.attribution.user_prefix);
-  L("pod_label_allowlist", c.attribution.label_allowlist);
-  B("compat_user_rule", c.attribution.compat_user_rule);
-  B("procfs_env_fallback", c.attribution.procfs_env_fallback);
-  B("include_host_processes", c.attribution.include_host_processes);
-  S("cri_socket", o.cri_socket);
-  S("docker_socket", c.docker_socket);
-  S("pod_log_root", c.pod_log_root);
-  S("device_checkpoint", c.device_checkpoint);
-  S("pod_resources_socket", o.pod_resources_socket);
-  L("resource_names", o.resource_names);
-  L("dra_drivers", c.pod_resources_dra_drivers);
-  N("metadata_refresh", o.metadata_refresh_s);
-  B("enable_probe", o.od.probe);
-  N("probe_every", o.probe_every);
-  B("enable_pmc", o.od.pmc);
-  L("pmc_counters", o.od.pmc_counters);
-  S("pmc_mode", o.od.pmc_mode);
-  B("ondevice_isolate", o.od.ondevice_isolate);
-  N("helper_retry", o.od.helper_retry_s);
-  S("plugin_dir", o.od.plugin_dir);
-  N("activity_acc_scale", c.rates.activity_acc_scale);
-  N("xgmi_kb_bytes", c.rates.xgmi_kb_bytes);
-  S("log_level", o.log_level);
-  s += "}";
-  return s;
+  j.end_obj();
+  return j.take();
 }
 
 }  // namespace gpumon

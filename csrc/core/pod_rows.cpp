@@ -51,35 +51,52 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
   std::vector<ExtraSeries> sharing;
   // Peer contexts of multi-GPU processes (the usual 8-GPU tenant: torchrun with one rank per GPU,
   // each rank's runtime also opening every other GPU, RCCL importing peers' buffers). A (pid, GPU)
-  // context is a peer context -- not a workload row, not a sharer -- when on that GPU it holds at
-  // most peer_context_max_vram_mib, had no wave resident within the sharing window (where
-  // occupancy is readable), and the same process has a workload context on ANOTHER GPU this tick
-  // (more VRAM than that, or waves). The reference listed one row per compute app nvidia-smi
-  // showed on a GPU (gpu.py:111-116,178,190-219): a rank appears on its own GPU only.
+  // context is a peer context -- not a workload row, not a sharer -- when the process never
+  // submitted work to that GPU and has a workload on ANOTHER GPU this tick:
+  //  * where KFD lists the process's queues (sysfs fast path): no hardware queue on that GPU and
+  //    no wave resident within the sharing window, whatever VRAM it holds there. A TP / PP process
+  //    that computes on a second GPU holds queues there and keeps that row however small its shard
+  //    (measured on MI355X: an allocate-only context has no queue, one kernel or copy creates them;
+  //    profiles/r6_kfd_queues.md);
+  //  * elsewhere (the queue list unreadable, libamd_smi process lists): at most
+  //    peer_context_max_vram_mib there and no wave within the window.
+  // A workload context is one with queues or waves, or (queues unknown) more VRAM than that. The
+  // reference listed one row per compute app nvidia-smi showed on a GPU (gpu.py:111-116,178,190-219):
+  // a rank appears on its own GPU only. peer_context_max_vram_mib 0 turns the rule off.
   if (last_waves_.size() < procs.size()) last_waves_.resize(procs.size());
   const double peer_floor = std::max(0.0, cfg_.peer_context_max_vram_mib) * 1048576.0;
   std::unordered_map<uint32_t, std::vector<int>> workload_devs;  // pid -> GPUs with a workload context
   std::vector<std::unordered_map<uint32_t, double>> vram_of(procs.size());  // (dev, pid) -> VRAM, contexts summed
+  std::vector<std::unordered_map<uint32_t, int>> queues_of(procs.size());   // (dev, pid) -> queues (-1 unknown)
   for (size_t d = 0; d < procs.size(); ++d) {
     auto& waves = last_waves_[d];
     for (const auto& p : procs[d]) {
       if (is_helper(p.pid)) continue;
       const double v = p.vram_bytes > 0 ? p.vram_bytes : (p.mem_bytes > 0 ? p.mem_bytes : 0.0);
       vram_of[d][p.pid] += v;
+      auto q = queues_of[d].emplace(p.pid, p.queues);
+      if (!q.second && p.queues >= 0) q.first->second = std::max(q.first->second, 0) + p.queues;
       if (p.occ_busy > 0 || p.cu_occupancy > 0) waves[p.pid] = {tick_no, now_ns};
     }
     for (auto it = waves.begin(); it != waves.end();) {  // forget pids past both windows
       if (tick_no - it->second.first >= 5 && now_ns - it->second.second >= window_ns) it = waves.erase(it);
       else ++it;
     }
-    for (const auto& [pid, v] : vram_of[d])
-      if (v > peer_floor || waves.count(pid)) workload_devs[pid].push_back(static_cast<int>(d));
+    for (const auto& [pid, v] : vram_of[d]) {
+      const int q = queues_of[d][pid];
+      if (waves.count(pid) || q > 0 || (q < 0 && v > peer_floor)) workload_devs[pid].push_back(static_cast<int>(d));
+    }
   }
   auto is_peer = [&](size_t d, uint32_t pid) {
     if (peer_floor <= 0 || !cfg_.hide_empty_contexts) return false;
     if (last_waves_[d].count(pid)) return false;
-    auto v = vram_of[d].find(pid);
-    if (v != vram_of[d].end() && v->second > peer_floor) return false;
+    auto q = queues_of[d].find(pid);
+    const int queues = q == queues_of[d].end() ? -1 : q->second;
+    if (queues > 0) return false;  // it submitted work to this GPU
+    if (queues < 0) {              // no queue list: the VRAM threshold
+      auto v = vram_of[d].find(pid);
+      if (v != vram_of[d].end() && v->second > peer_floor) return false;
+    }
     auto w = workload_devs.find(pid);
     return w != workload_devs.end() &&
            std::any_of(w->second.begin(), w->second.end(), [&](int o) { return o != static_cast<int>(d); });
@@ -156,6 +173,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       if (dup != row_of_pid.end()) {
         PodRow& r = (*rows)[dup->second];
         r.used_memory_bytes += has(p.vram_bytes) ? p.vram_bytes : 0;
+        if (p.queues >= 0) r.queues = std::max(r.queues, 0) + p.queues;
         if (has(p.cu_occupancy)) r.cu_occupancy = has(r.cu_occupancy) ? r.cu_occupancy + p.cu_occupancy : p.cu_occupancy;
         continue;
       }
@@ -216,6 +234,7 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       r.proc_gfx_util = util;
       r.cu_occupancy = p.cu_occupancy;
       r.occ_samples = p.occ_samples;
+      r.queues = p.queues;
       if (sole[d] == p.pid)
         if (auto m = mfma.find(static_cast<int>(d)); m != mfma.end()) r.mfma_util = m->second;
       // only a process attributed to a pod or container can stand in for its idle allocation row

@@ -63,6 +63,13 @@ void compute_rates(const DeviceSample& prev, const DeviceSample& cur, const Rate
     if (acc_delta(a.mem_activity_acc, b.mem_activity_acc, true, &dm))
       out->mem_activity_avg_pct = std::min(100.0, dm * cfg.activity_acc_scale / dacc);
   }
+  if (have_acc && a.has_pcie_bw_acc && b.has_pcie_bw_acc) {
+    // pcie_bandwidth_acc adds the instantaneous bandwidth once per accumulation tick (1 kHz on
+    // MI355X), so its delta over the counter's is the interval mean in firmware units
+    uint64_t dp = 0;
+    if (acc_delta(a.pcie_bw_acc, b.pcie_bw_acc, false, &dp))
+      out->pcie_Bps = static_cast<double>(dp) * cfg.pcie_bw_unit_bytes / static_cast<double>(dacc);
+  }
   if (have_acc) {
     int nx = std::min(a.n_xcd_acc, b.n_xcd_acc);
     out->n_xcd = nx;

@@ -17,6 +17,12 @@ namespace gpumon {
 struct RateConfig {
   double activity_acc_scale = 1.0;   // avg% = d(acc) / d(accumulation_counter) * scale
   double xgmi_kb_bytes = 1024.0;     // bytes per xGMI "KB" accumulator unit
+  // Bytes/s per unit of pcie_bandwidth_inst / per accumulation tick of pcie_bandwidth_acc. The
+  // kernel header calls them GB/s; on MI355X (gpu_metrics v1.8) an idle GPU reads 18-21 and a
+  // 57.4 GB/s pinned host->device copy 558481: 102400 B/s per unit (100 KiB/s) puts h2d within
+  // 0.4 %, a 50 % duty h2d within 0.2 %, d2h 6 % under and both directions 2.6 % under the copies'
+  // host-clocked rates (tools/pcie_probe.py, profiles/r6_pcie_bandwidth.md).
+  double pcie_bw_unit_bytes = 102400.0;
 };
 
 // Unsigned delta that tolerates a 32-bit firmware wrap when `bits32` is set; returns false on a

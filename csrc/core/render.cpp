@@ -373,7 +373,8 @@ void render_prometheus(const RenderInput& in, std::string* o) {
                {"drm_card", std::to_string(st[d].drm_card)},
                {"compute_partition", st[d].compute_partition},
                {"memory_partition", st[d].memory_partition},
-               {"driver_version", st[d].driver_version}})
+               {"driver_version", st[d].driver_version},
+               {"driver_source", st[d].driver_source}})
           extra.push_back(std::move(kv));
         f.add(dl[d], extra, 1.0);
       }
@@ -504,7 +505,13 @@ void render_prometheus(const RenderInput& in, std::string* o) {
          [&](size_t d) { return sm[d].v[F_PCIE_WIDTH]; });
     devf("gpu_pcie_link_speed_gts", "PCIe link speed in GT/s.", "gauge",
          [&](size_t d) { return sm[d].v[F_PCIE_SPEED_GTS]; });
-    devf("gpu_pcie_bandwidth_gbytes_per_second", "Instantaneous PCIe bandwidth (firmware) in GB/s.",
+    devf("gpu_pcie_bandwidth_bytes_per_second",
+         "PCIe bandwidth averaged over the sampling interval, both directions, in bytes/s (firmware "
+         "pcie_bandwidth_acc over its accumulation ticks x pcie_bw_unit_bytes; checked against pinned "
+         "host<->device copies on MI355X).",
+         "gauge", [&](size_t d) { return rate(d).pcie_Bps; });
+    devf("gpu_pcie_bandwidth_inst_bytes_per_second",
+         "Instantaneous PCIe bandwidth (firmware, one 1 ms window at the read), both directions, in bytes/s.",
          "gauge", [&](size_t d) { return sm[d].v[F_PCIE_BW_INST]; });
     devf("gpu_pcie_replay_total", "PCIe replay count.", "counter",
          [&](size_t d) { return sm[d].v[F_PCIE_REPLAY]; });
@@ -700,6 +707,15 @@ void render_prometheus(const RenderInput& in, std::string* o) {
         if (cus > 0 && has(rows[r].cu_occupancy))
           f.add(rl[r], std::min(100.0, 100.0 * rows[r].cu_occupancy / cus));
       }
+    }
+    {
+      // KFD's per-process queue list: 0 = a context that never submitted work to this GPU
+      Family f(o, "pod_gpu_proc_queues",
+               "Hardware (user-mode) queues the process holds on this GPU (KFD); 0 = a context that never "
+               "submitted work here.",
+               "gauge");
+      for (size_t r = 0; r < rows.size(); ++r)
+        if (!rows[r].idle && rows[r].queues >= 0) f.add(rl[r], static_cast<double>(rows[r].queues));
     }
     // One series per (pod, container, gpu): the allocation view behind the reference dashboard's
     // "GPUs per user" and "allocated / in use" panels.

@@ -35,6 +35,7 @@ struct PodRow {
   double proc_gfx_util = kNaN;      // true per-process util from engine_usage.gfx ns
   double cu_occupancy = kNaN;
   int occ_samples = 0;  // cu_occupancy reads behind the interval mean
+  int queues = -1;      // hardware queues on the GPU (KFD queue list; -1 unknown)
   // the device's wall-time MFMA utilisation (PMC) when this process was the only one on the GPU
   // with waves resident this interval (exclusive use); NaN when the GPU was shared or PMC is off
   double mfma_util = kNaN;

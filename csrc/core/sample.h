@@ -43,6 +43,7 @@ struct DeviceStatic {
   std::string compute_partition;  // SPX / CPX ...
   std::string memory_partition;   // NPS1 ...
   std::string driver_version;
+  std::string driver_source;  // module | kernel | library (common.h driver_version_label)
   double vram_total_bytes = kNaN;
   double power_limit_w = kNaN;
   int num_cu = 0;
@@ -78,7 +79,7 @@ enum Field : int {
   F_FAN_RPM,
   F_PCIE_WIDTH,         // lanes
   F_PCIE_SPEED_GTS,     // GT/s
-  F_PCIE_BW_INST,       // GB/s instantaneous (firmware)
+  F_PCIE_BW_INST,       // bytes/s instantaneous (firmware units x RateConfig::pcie_bw_unit_bytes, set in tick())
   F_PCIE_REPLAY,        // count
   F_PCIE_L0_RECOV,      // count
   F_PCIE_NAK_SENT,
@@ -221,6 +222,10 @@ struct ProcSample {
   double cu_occupancy = kNaN;
   int occ_samples = 0;          // reads behind cu_occupancy (0 = none)
   int occ_busy = 0;             // of those, reads with waves resident (> 0): the process's busy share
+  // Hardware (user-mode) queues the process holds on this device, from KFD's per-process queue list
+  // (sysfs fast path); -1 = unknown. 0 = a context that never submitted work here: the peer context
+  // of a multi-GPU process (pod_rows.cpp).
+  int queues = -1;
 };
 
 // One between-ticks KFD read of a process on a device (Backend::occupancy_scan): lists processes
@@ -251,6 +256,9 @@ struct DeviceRates {
   std::array<double, kMaxLinks> xgmi_rd_Bps{};
   std::array<double, kMaxLinks> xgmi_wr_Bps{};
   int n_links = 0;
+  // PCIe bandwidth over the interval, both directions (bytes/s): d(pcie_bandwidth_acc) over the
+  // firmware's accumulation ticks (rates.cpp; unit measured on MI355X, docs/metrics.md)
+  double pcie_Bps = kNaN;
 };
 
 }  // namespace gpumon

@@ -403,6 +403,37 @@ void SysfsGpu::prune_not_here(const std::vector<uint32_t>& listed_sorted) {
   }
 }
 
+int SysfsGpu::queues_here(uint32_t pid, int64_t now) {
+  // A process's user-mode queues are created when its runtime first submits work to a GPU (a
+  // kernel, a copy) and live as long as its streams: a context that only allocated -- the usual
+  // peer context of an RCCL rank or P2P importer -- has none there (profiles/r6_kfd_queues.md).
+  // Rescanned every kQueueRescanNs: the rule reads "none there", and a queue created since is
+  // seen within that time (its waves show in the occupancy reads first anyway).
+  auto it = queue_cache_.find(pid);
+  if (it != queue_cache_.end() && now - it->second.second < kQueueRescanNs) return it->second.first;
+  const std::string qdir = sys_root_ + "/class/kfd/kfd/proc/" + std::to_string(pid) + "/queues";
+  int count = -1;
+  if (DIR* d = opendir(qdir.c_str())) {
+    count = 0;
+    char b[32];
+    while (dirent* e = readdir(d)) {
+      if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+      const std::string f = qdir + "/" + e->d_name + "/gpuid";
+      const int fd = ::open(f.c_str(), O_RDONLY | O_CLOEXEC);
+      if (fd < 0) continue;  // the queue went away between readdir and open
+      const ssize_t n = ::read(fd, b, sizeof b - 1);
+      ::close(fd);
+      if (n > 0) {
+        b[n] = 0;
+        if (strtoull(b, nullptr, 10) == kfd_gpu_id_) ++count;
+      }
+    }
+    closedir(d);
+  }
+  queue_cache_[pid] = {count, now};
+  return count;
+}
+
 bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
   out->clear();
   if (!kfd_gpu_id_) return false;
@@ -428,11 +459,14 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
     p.vram_bytes = p.mem_bytes;
     if (read_occupancy && read_kfd(pid, KfdFile::kOccupancy, b, sizeof b, &n))
       p.cu_occupancy = static_cast<double>(strtoull(b, nullptr, 10));
+    p.queues = queues_here(pid, now);
     fdinfo_usage(pid, &p);
     out->push_back(std::move(p));
   }
   closedir(d);
   std::sort(listed.begin(), listed.end());
+  for (auto it = queue_cache_.begin(); it != queue_cache_.end();)  // pids that left the listing
+    it = std::binary_search(listed.begin(), listed.end(), it->first) ? std::next(it) : queue_cache_.erase(it);
   DrmFdTables::get().retain(proc_root_, listed);
   prune_not_here(listed);
   retain_kfd(listed);  // close the kept files of processes that left

@@ -213,6 +213,12 @@ class SysfsGpu {
 
  private:
   void fdinfo_usage(uint32_t pid, ProcSample* p);
+  // Hardware queues `pid` holds on this GPU: proc/<pid>/queues/<qid>/gpuid == this GPU's KFD id
+  // (-1: the directory is unreadable). Cached per pid for kQueueRescanNs; only processes() (the
+  // device worker's tick path) calls it, so the cache needs no lock.
+  static constexpr int64_t kQueueRescanNs = 2'000'000'000;
+  int queues_here(uint32_t pid, int64_t now);
+  std::unordered_map<uint32_t, std::pair<int, int64_t>> queue_cache_;
   // /sys/class/kfd/kfd/proc is not namespaced: it lists every KFD process of the host, on every
   // GPU (15-17 on a shared MI355X box, 1 of them on the container's GPU). A process found not to
   // be on this GPU is not asked again for kNotHereNs (each ask is an open() that fails, ~4-6 us):

@@ -2,9 +2,9 @@
 //
 // Reference entrypoint: `python3 /gpu.py` (/root/reference/Dockerfile:7) reading NODE_NAME and
 // INFLUXDB_URL from the environment (gpu.py:19-26) and looping forever (gpu.py:258-263).
-// Configuration (csrc/core/options.h) uses the Python control plane's keys and precedence:
-// defaults < YAML file (--config / GPUMON_CONFIG, the DaemonSet's ConfigMap format) < environment
-// (NODE_NAME, INFLUXDB_URL, GPUMON_<KEY>) < flags. Attribution uses /proc plus the native kubelet
+// Configuration (csrc/core/options.h, the one implementation `gpumon serve` shares): defaults <
+// YAML file (--config / GPUMON_CONFIG, the DaemonSet's ConfigMap format) < environment (NODE_NAME,
+// INFLUXDB_URL, GPUMON_<KEY>) < --compat < flags. Attribution uses /proc plus the native kubelet
 // PodResources and CRI pollers; --pmc / --probe load the on-device plugins.
 #include <signal.h>
 #include <sys/resource.h>
@@ -33,150 +33,49 @@ static void on_signal(int) { g_stop = true; }
 static void on_hup(int) { g_hup = true; }
 
 static void usage() {
-  fprintf(stderr,
-          "usage: gpumon-exporter [--config FILE] [--print-config] [--once]\n"
-          "                       [--backend auto|amdsmi|rocm_smi|mock[:k=v,..]] [--interval SEC]\n"
-          "                       [--listen HOST:PORT|[V6]:PORT|:PORT] [--host NAME] [--devices 0,1|BDF,..] [--no-fast-path]\n"
-          "                       [--sysfs /sys] [--influx-url URL] [--influx-extended] [--influx-schema 2018|2019]\n"
-          "                       [--influx-ca-file PEM] [--influx-tls-insecure] [--influx-client-cert PEM --influx-client-key PEM]\n"
-          "                       [--tls-cert-file PEM --tls-key-file PEM [--tls-client-ca-file PEM]]  (/metrics over HTTPS)\n"
-          "                       [--http-auth-token-file FILE]  (/metrics needs Authorization: Bearer <token>)\n"
-          "                       [--opt-in-label KEY=VALUE] [--user-regex RE] [--user-label KEY]\n"
-          "                       [--pod-labels KEY,KEY..]\n"
-          "                       [--procfs /proc] [--no-processes] [--ras-every TICKS] [--ras-slices N] [--no-gzip] [--metrics-include GLOBS] [--metrics-exclude GLOBS] [--sample-threads N] [--rt-priority N] [--prewarm-ms MS]\n"
-          "                       [--http-threads N] [--log-level debug|info|warn|error] [--roctx]\n"
-          "                       [--pod-resources SOCKET | --no-pod-resources] [--cri SOCKET | --no-cri] [--docker SOCKET]\n"
-          "                       [--pod-logs /var/log] [--device-checkpoint FILE]\n"
-          "                       [--dra-drivers gpu.amd.com,..|none]\n"
-          "                       [--pmc] [--pmc-counters A,B,..] [--pmc-mode continuous|window] [--pmc-window SEC] [--probe] [--probe-every N]\n"
-          "                       [--probe-blocks N] [--plugin-dir DIR] [--device-timeout SEC]\n"
-          "                       [--control-plane native|off] [--compat]\n"
-          "the Python entry point's spellings work too: --procfs-root, --sysfs-root, --cri-socket,\n"
-          "--pod-resources-socket, --docker-socket, --pod-log-root, --enable-pmc, --enable-probe-kernel\n"
-          "config keys: the gpumon.* keys of gpumon/config.py (docs/configuration.md), in the file, as\n"
-          "GPUMON_<KEY> in the environment, or as the flags above; NODE_NAME and INFLUXDB_URL as in the reference\n");
+  // generated from the one flag table (csrc/core/options.cpp option_flags)
+  std::string u = "usage: gpumon-exporter [--config FILE] [--compat] [--print-config] [--once] [flags]\n";
+  for (const auto& f : option_flags()) {
+    std::string names = f.flag;
+    for (const auto& a : split(f.aliases, ','))
+      if (!a.empty()) names += ", " + a;
+    if (!f.fixed) names += " VALUE";
+    char line[512];
+    snprintf(line, sizeof line, "  %-44s %s\n", names.c_str(), f.help);
+    u += line;
+  }
+  u += "config keys: docs/configuration.md, in the file (--config / GPUMON_CONFIG, under `gpumon:`), as\n"
+       "GPUMON_<KEY> in the environment, or as the flags above; NODE_NAME and INFLUXDB_URL as in the reference\n";
+  fputs(u.c_str(), stderr);
 }
 
 int main(int argc, char** argv) {
   NativeOptions o;
   std::string err;
-  // 1. config file: --config wins over GPUMON_CONFIG
-  const char* config_env = getenv("GPUMON_CONFIG");
-  std::string config = config_env ? config_env : "";
-  for (int i = 1; i + 1 < argc; ++i)
-    if (std::string(argv[i]) == "--config") config = argv[i + 1];
-  if (!config.empty()) {
-    std::vector<std::string> unknown;
-    if (!options_load_file(&o, config, &unknown, &err)) {
+  std::vector<std::string> args(argv + 1, argv + argc), rest, warnings;
+  // defaults < file < environment < --compat < flags: options_parse (the one implementation)
+  switch (options_parse(&o, args, environ, &rest, &warnings, &err)) {
+    case ParseStatus::kOk:
+      break;
+    case ParseStatus::kBadFile:
       fprintf(stderr, "config: %s\n", err.c_str());
       return 2;
-    }
-    for (const auto& k : unknown)
-      fprintf(stderr, "config: key '%s' is not used by the native exporter (ignored)\n", k.c_str());
+    case ParseStatus::kBadEnv:
+      fprintf(stderr, "environment: %s\n", err.c_str());
+      return 2;
+    case ParseStatus::kBadFlag:
+      fprintf(stderr, "%s\n", err.c_str());
+      usage();
+      return 2;
+    case ParseStatus::kBadValue:
+      fprintf(stderr, "%s\n", err.c_str());
+      return 2;
   }
-  // 2. environment
-  if (!options_apply_env(&o, environ, &err)) {
-    fprintf(stderr, "environment: %s\n", err.c_str());
-    return 2;
-  }
-  // 3. flags
-  bool once = false, print_config = false, compat = false;
-  auto set = [&](const char* key, const std::string& v) {
-    std::string e;
-    if (options_set(&o, key, {v}, &e) < 0) {
-      fprintf(stderr, "%s\n", e.c_str());
-      exit(2);
-    }
-  };
-  // --compat (the reference's behaviour: opt-in label mlgpu=mlgpu, 10 s interval) sits between the
-  // environment and the flags, as in gpumon/config.py from_args: explicit flags still win
-  for (int i = 1; i < argc; ++i)
-    if (std::string(argv[i]) == "--compat") compat = true;
-  if (compat) {
-    if (o.cfg.attribution.opt_in.empty()) set("opt_in_label", "mlgpu=mlgpu");
-    set("interval", "10");
-  }
-  for (int i = 1; i < argc; ++i) {
-    std::string a = argv[i];
-    auto next = [&]() -> std::string {
-      if (i + 1 >= argc) {
-        usage();
-        exit(2);
-      }
-      return argv[++i];
-    };
-    if (a == "--config") next();
+  for (const auto& w : warnings) fprintf(stderr, "%s\n", w.c_str());
+  bool once = false, print_config = false;
+  for (const auto& a : rest) {
+    if (a == "--once") once = true;
     else if (a == "--print-config") print_config = true;
-    else if (a == "--once") once = true;
-    else if (a == "--backend") set("backend", next());
-    else if (a == "--interval") set("interval", next());
-    else if (a == "--listen") set("listen", next());
-    else if (a == "--host") set("host", next());
-    else if (a == "--devices") set("devices", next());
-    else if (a == "--influx-url") set("influx_url", next());
-    else if (a == "--influx-token") set("influx_token", next());
-    else if (a == "--influx-extended") set("influx_extended", "true");
-    else if (a == "--influx-gzip") set("influx_gzip", "true");
-    else if (a == "--influx-schema") set("influx_schema", next());
-    else if (a == "--influx-ca-file") set("influx_ca_file", next());
-    else if (a == "--tls-cert-file") set("tls_cert_file", next());
-    else if (a == "--tls-key-file") set("tls_key_file", next());
-    else if (a == "--tls-client-ca-file") set("tls_client_ca_file", next());
-    else if (a == "--http-auth-token-file") set("http_auth_token_file", next());
-    else if (a == "--influx-tls-insecure") set("influx_tls_insecure", "true");
-    else if (a == "--influx-client-cert") set("influx_client_cert", next());
-    else if (a == "--influx-client-key") set("influx_client_key", next());
-    else if (a == "--no-fast-path") set("fast_path", "false");
-    else if (a == "--sysfs" || a == "--sysfs-root") set("sysfs_root", next());
-    else if (a == "--roctx") set("roctx", "true");
-    else if (a == "--pod-resources" || a == "--pod-resources-socket") set("pod_resources_socket", next());
-    else if (a == "--no-pod-resources") set("pod_resources_socket", "");
-    else if (a == "--cri" || a == "--cri-socket") set("cri_socket", next());
-    else if (a == "--no-cri") set("cri_socket", "none");
-    else if (a == "--docker" || a == "--docker-socket") set("docker_socket", next());
-    else if (a == "--pod-logs" || a == "--pod-log-root") set("pod_log_root", next());
-    else if (a == "--device-checkpoint") set("device_checkpoint", next());
-    else if (a == "--dra-drivers") {
-      const std::string v = next();
-      set("dra_drivers", v == "none" ? "" : v);
-    } else if (a == "--control-plane") {
-      // off: no kubelet / CRI / Docker / log-tree metadata pollers (the Python entry point's flag)
-      const std::string v = next();
-      if (v == "off") {
-        for (const char* k : {"pod_resources_socket", "docker_socket", "pod_log_root", "device_checkpoint"}) set(k, "");
-        set("cri_socket", "none");
-      } else if (v != "native") {
-        fprintf(stderr, "--control-plane: native or off, not '%s'\n", v.c_str());
-        return 2;
-      }
-    } else if (a == "--compat") {
-      // applied before the flags (above)
-    } else if (a == "--opt-in-label") set("opt_in_label", next());
-    else if (a == "--user-regex") set("user_regex", next());
-    else if (a == "--user-label") set("user_label", next());
-    else if (a == "--pod-labels") set("pod_label_allowlist", next());
-    else if (a == "--procfs" || a == "--procfs-root") set("procfs_root", next());
-    else if (a == "--no-processes") set("processes", "false");
-    else if (a == "--ras-every") set("ras_every", next());
-    else if (a == "--ras-slices") set("ras_slices", next());
-    else if (a == "--no-gzip") set("gzip", "false");
-    else if (a == "--device-timeout") set("device_timeout_s", next());
-    else if (a == "--metrics-include") set("metrics_include", next());
-    else if (a == "--metrics-exclude") set("metrics_exclude", next());
-    else if (a == "--sample-threads") set("sample_threads", next());
-    else if (a == "--rt-priority") set("rt_priority", next());
-    else if (a == "--http-rt-priority") set("http_rt_priority", next());
-    else if (a == "--prewarm-ms") set("prewarm_ms", next());
-    else if (a == "--http-threads") set("http_threads", next());
-    else if (a == "--log-level") set("log_level", next());
-    else if (a == "--pmc" || a == "--enable-pmc") set("enable_pmc", "true");
-    else if (a == "--pmc-counters") set("pmc_counters", next());
-    else if (a == "--pmc-window") o.od.pmc_window_s = atof(next().c_str());
-    else if (a == "--pmc-mode") set("pmc_mode", next());
-    else if (a == "--probe" || a == "--enable-probe-kernel") set("enable_probe", "true");
-    else if (a == "--probe-every") set("probe_every", next());
-    else if (a == "--probe-blocks") o.od.probe_blocks = atoi(next().c_str());
-    else if (a == "--plugin-dir") set("plugin_dir", next());
     else if (a == "-h" || a == "--help") {
       usage();
       return 0;
@@ -194,31 +93,12 @@ int main(int argc, char** argv) {
     fprintf(stderr, "config: %s\n", err.c_str());
     return 2;
   }
-  ExporterConfig& cfg = o.cfg;
-  {
-    // an Influx push that cannot work is a startup error, not a silently idle pusher
-    TlsOptions t;
-    t.ca_file = cfg.influx_ca_file;
-    t.insecure = cfg.influx_tls_insecure;
-    t.client_cert = cfg.influx_client_cert;
-    t.client_key = cfg.influx_client_key;
-    const std::string perr = check_push_config(cfg.influx_url, cfg.influx_token, t);
-    if (!perr.empty()) {
-      fprintf(stderr, "config: %s\n", perr.c_str());
-      return 2;
-    }
-    // /metrics over HTTPS: the certificate, key and client CA must load
-    const std::string serr = check_serve_tls(cfg.tls_cert_file, cfg.tls_key_file, cfg.tls_client_ca_file);
-    if (!serr.empty()) {
-      fprintf(stderr, "config: %s\n", serr.c_str());
-      return 2;
-    }
-    // /metrics behind a bearer token: the token file must hold one
-    if (const std::string aerr = check_auth_token_file(cfg.http_auth_token_file); !aerr.empty()) {
-      fprintf(stderr, "config: http_auth_token_file: %s\n", aerr.c_str());
-      return 2;
-    }
+  g_log_level = options_log_level(o);
+  if (const std::string verr = options_validate(o); !verr.empty()) {
+    fprintf(stderr, "config: %s\n", verr.c_str());
+    return 2;
   }
+  ExporterConfig& cfg = o.cfg;
   const OnDeviceConfig& od = o.od;
 
   // The on-device samplers start BEFORE the backend: the PMC helper process is spawned while

@@ -182,7 +182,10 @@ amdsmi_status_t amdsmi_get_gpu_kfd_info(amdsmi_processor_handle h, amdsmi_kfd_in
 amdsmi_status_t amdsmi_get_gpu_driver_info(amdsmi_processor_handle, amdsmi_driver_info_t* i) {
   memset(i, 0, sizeof *i);
   strcpy(i->driver_name, "amdgpu");
-  strcpy(i->driver_version, "6.18.0-fake");
+  // FAKE_AMDSMI_DRIVER_VERSION: what libamd_smi returned on the pool's MI355X boxes (in-kernel
+  // amdgpu: /proc/version with its spaces removed, profiles/data/r4/cm_base.prom:24)
+  const char* v = getenv("FAKE_AMDSMI_DRIVER_VERSION");
+  snprintf(i->driver_version, sizeof i->driver_version, "%s", v ? v : "6.18.0-fake");
   return AMDSMI_STATUS_SUCCESS;
 }
 

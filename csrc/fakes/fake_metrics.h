@@ -29,7 +29,8 @@ void fill_metrics(M* m, int d, uint64_t n) {
   m->throttle_status = 0;
   m->pcie_link_width = 16;
   m->pcie_link_speed = 320;
-  m->pcie_bandwidth_inst = 18;
+  m->pcie_bandwidth_inst = 18;                                   // idle MI355X: 18-21 units
+  m->pcie_bandwidth_acc = n * 1000ull * (500000ull + 1000ull * d);  // 1000 ticks per call: 51.2 (+0.1 d) GB/s
   m->pcie_replay_count_acc = 0;
   m->gfx_activity_acc = static_cast<uint32_t>(n * 37 * 1000);  // 37 % per counter tick
   m->mem_activity_acc = static_cast<uint32_t>(n * 12 * 1000);

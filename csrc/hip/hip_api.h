@@ -136,6 +136,44 @@ class XgmiLoad {
   std::string err_;
 };
 
+// --- PCIe load: pinned host <-> device copies (drives the device's PCIe link) ----------------------
+struct PcieStats {
+  uint64_t copies = 0;
+  double h2d_bytes = 0, d2h_bytes = 0;  // bytes that crossed the link, per direction
+  double busy_s = 0;                    // event-timed GPU time of the copy batches
+  double wall_s = 0;                    // since start()
+};
+
+class PcieLoad {
+ public:
+  // direction "h2d" | "d2h" | "both" (the two directions on two streams at once); duty in (0, 1]:
+  // share of wall time spent copying (idle gaps sized from each batch's event-timed length)
+  PcieLoad(int dev, size_t bytes, std::string direction, double duty);
+  ~PcieLoad();
+  void start();
+  void stop();
+  PcieStats stats() const;
+  bool running() const { return running_; }
+
+ private:
+  void loop();
+  int dev_;
+  size_t bytes_;
+  std::string dir_;
+  double duty_;
+  void* up_ = nullptr;    // h2d stream
+  void* down_ = nullptr;  // d2h stream
+  void* host_src_ = nullptr;  // pinned
+  void* host_dst_ = nullptr;  // pinned
+  void* dev_src_ = nullptr;
+  void* dev_dst_ = nullptr;
+  std::thread th_;
+  std::atomic<bool> running_{false};
+  int64_t t_start_ns_ = 0;
+  std::atomic<uint64_t> copies_{0}, h2d_{0}, d2h_{0}, busy_ns_{0};
+  std::string err_;
+};
+
 // --- K1 probe: pinned ring buffer ----------------------------------------------------------------
 class Probe {
  public:

@@ -552,6 +552,120 @@ XgmiStats XgmiLoad::stats() const {
 }
 
 // ---------------------------------------------------------------------------------------------
+// PcieLoad: the host link's known traffic, the reference for gpu_pcie_bandwidth_bytes_per_second
+// (DMA copies from / to pinned host memory: each byte crosses PCIe exactly once)
+// ---------------------------------------------------------------------------------------------
+PcieLoad::PcieLoad(int dev, size_t bytes, std::string direction, double duty)
+    : dev_(dev), bytes_(std::max<size_t>(bytes / 4096 * 4096, 1 << 20)), dir_(std::move(direction)),
+      duty_(duty) {
+  if (dir_ != "h2d" && dir_ != "d2h" && dir_ != "both") throw std::invalid_argument("PcieLoad direction: h2d | d2h | both");
+  if (!(duty_ > 0.0 && duty_ <= 1.0)) throw std::invalid_argument("PcieLoad duty must be in (0, 1]");
+  if (dev_ < 0 || dev_ >= device_count()) throw std::invalid_argument("PcieLoad: device out of range");
+}
+
+PcieLoad::~PcieLoad() { stop(); }
+
+void PcieLoad::start() {
+  if (running_) return;
+  check(hipSetDevice(dev_), "hipSetDevice");
+  hipStream_t a, b;
+  check(hipStreamCreateWithFlags(&a, hipStreamNonBlocking), "hipStreamCreate");
+  up_ = a;
+  check(hipStreamCreateWithFlags(&b, hipStreamNonBlocking), "hipStreamCreate");
+  down_ = b;
+  check(hipHostMalloc(&host_src_, bytes_, hipHostMallocDefault), "hipHostMalloc(src)");
+  check(hipHostMalloc(&host_dst_, bytes_, hipHostMallocDefault), "hipHostMalloc(dst)");
+  memset(host_src_, 5, bytes_);
+  check(hipMalloc(&dev_src_, bytes_), "hipMalloc(src)");
+  check(hipMalloc(&dev_dst_, bytes_), "hipMalloc(dst)");
+  check(hipMemsetAsync(dev_src_, 7, bytes_, a), "hipMemset");
+  check(hipStreamSynchronize(a), "hipStreamSynchronize");
+  running_ = true;
+  t_start_ns_ = mono_ns();
+  th_ = std::thread([this] { loop(); });
+}
+
+void PcieLoad::loop() {
+  try {
+    check(hipSetDevice(dev_), "hipSetDevice");
+    hipStream_t a = static_cast<hipStream_t>(up_), b = static_cast<hipStream_t>(down_);
+    const bool up = dir_ != "d2h", down = dir_ != "h2d";
+    hipEvent_t e[4];
+    for (auto& x : e) check(hipEventCreate(&x), "hipEventCreate");
+    while (running_) {
+      const int64_t t0 = mono_ns();
+      if (up) check(hipEventRecord(e[0], a), "hipEventRecord");
+      if (down) check(hipEventRecord(e[2], b), "hipEventRecord");
+      for (int k = 0; k < 2; ++k) {
+        if (up) check(hipMemcpyAsync(dev_dst_, host_src_, bytes_, hipMemcpyHostToDevice, a), "hipMemcpyAsync(h2d)");
+        if (down) check(hipMemcpyAsync(host_dst_, dev_src_, bytes_, hipMemcpyDeviceToHost, b), "hipMemcpyAsync(d2h)");
+      }
+      if (up) check(hipEventRecord(e[1], a), "hipEventRecord");
+      if (down) check(hipEventRecord(e[3], b), "hipEventRecord");
+      float ms_up = 0, ms_down = 0;
+      if (up) {
+        check(hipEventSynchronize(e[1]), "hipEventSynchronize");
+        check(hipEventElapsedTime(&ms_up, e[0], e[1]), "hipEventElapsedTime");
+        h2d_ += 2 * static_cast<uint64_t>(bytes_);
+      }
+      if (down) {
+        check(hipEventSynchronize(e[3]), "hipEventSynchronize");
+        check(hipEventElapsedTime(&ms_down, e[2], e[3]), "hipEventElapsedTime");
+        d2h_ += 2 * static_cast<uint64_t>(bytes_);
+      }
+      busy_ns_ += static_cast<uint64_t>(std::max(ms_up, ms_down) * 1e6);
+      copies_ += (up ? 2 : 0) + (down ? 2 : 0);
+      if (duty_ < 1.0) {
+        // idle for (1 - duty) / duty of the batch just run, in <= 50 ms slices so stop() is prompt
+        int64_t left = static_cast<int64_t>((mono_ns() - t0) * (1.0 / duty_ - 1.0));
+        while (running_ && left > 0) {
+          const int64_t s = std::min<int64_t>(left, 50'000'000);
+          std::this_thread::sleep_for(std::chrono::nanoseconds(s));
+          left -= s;
+        }
+      }
+    }
+    for (auto& x : e) (void)hipEventDestroy(x);
+  } catch (const std::exception& ex) {
+    err_ = ex.what();
+    running_ = false;
+  }
+}
+
+void PcieLoad::stop() {
+  running_ = false;
+  if (th_.joinable()) th_.join();
+  (void)hipSetDevice(dev_);
+  for (void** s : {&up_, &down_})
+    if (*s) {
+      (void)hipStreamSynchronize(static_cast<hipStream_t>(*s));
+      (void)hipStreamDestroy(static_cast<hipStream_t>(*s));
+      *s = nullptr;
+    }
+  for (void** p : {&host_src_, &host_dst_})
+    if (*p) {
+      (void)hipHostFree(*p);
+      *p = nullptr;
+    }
+  for (void** p : {&dev_src_, &dev_dst_})
+    if (*p) {
+      (void)hipFree(*p);
+      *p = nullptr;
+    }
+}
+
+PcieStats PcieLoad::stats() const {
+  if (!err_.empty()) throw std::runtime_error("PcieLoad failed: " + err_);
+  PcieStats st;
+  st.copies = copies_;
+  st.h2d_bytes = static_cast<double>(h2d_.load());
+  st.d2h_bytes = static_cast<double>(d2h_.load());
+  st.busy_s = busy_ns_ * 1e-9;
+  st.wall_s = t_start_ns_ ? (mono_ns() - t_start_ns_) * 1e-9 : 0.0;
+  return st;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Probe
 // ---------------------------------------------------------------------------------------------
 Probe::Probe(int dev, int blocks, int slots, int spin_ticks)

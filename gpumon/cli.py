@@ -60,7 +60,7 @@ def cmd_serve(args) -> int:
         return 1
     log = logging.getLogger("gpumon")
     log.info("serving %s backend=%s host=%s interval=%.3fs influx=%s control_plane=%s", mon.url, cfg.backend,
-             cfg.resolved_host(), cfg.interval, redact_url(cfg.influx_url) or "-", bool(mon.plane))
+             mon.options.host, cfg.interval, redact_url(cfg.influx_url) or "-", mon.control_plane_mode)
     stop = threading.Event()
     for s in (signal.SIGINT, signal.SIGTERM):
         signal.signal(s, lambda *_: stop.set())
@@ -98,7 +98,7 @@ def cmd_doctor(args) -> int:
     from . import doctor
 
     cfg = from_args(args)
-    if not args.log_level:
+    if not getattr(args, "cfgflag__log_level", None):
         cfg.log_level = "error"  # the report is the output
     _setup_logging(cfg.log_level)
     return doctor.main(args, cfg)
@@ -189,7 +189,8 @@ def _top_remote(args) -> int:
         rc = 1 if errors and not frames else 0
         n += 1
         if args.iterations <= 0 or n < args.iterations:
-            time.sleep(max(0.0, (args.interval or 1.0) - (time.monotonic() - t0)))
+            interval = float(getattr(args, "cfgflag__interval", None) or 1.0)  # --interval: the refresh period
+            time.sleep(max(0.0, interval - (time.monotonic() - t0)))
     return rc
 
 
@@ -230,7 +231,8 @@ def cmd_probe(args) -> int:
 def cmd_load(args) -> int:
     from .ops.load import SyntheticLoad
 
-    with SyntheticLoad(args.device, args.kind, duty=args.duty, mfma_dtype=args.dtype, period_s=args.period) as load:
+    with SyntheticLoad(args.device, args.kind, duty=args.duty, mfma_dtype=args.dtype, period_s=args.period,
+                       pcie_direction=args.pcie_direction) as load:
         time.sleep(args.seconds)
         print(json.dumps(load.stats()))
     return 0
@@ -306,7 +308,9 @@ def build_parser() -> argparse.ArgumentParser:
     s.set_defaults(fn=cmd_probe)
     s = sub.add_parser("load", help="synthetic gfx950 load")
     s.add_argument("--device", type=int, default=0)
-    s.add_argument("--kind", choices=["mfma", "hbm", "mixed", "concurrent", "partial"], default="mixed")
+    s.add_argument("--kind", choices=["mfma", "hbm", "mixed", "concurrent", "partial", "pcie"], default="mixed")
+    s.add_argument("--pcie-direction", choices=["h2d", "d2h", "both"], default="both",
+                   help="--kind pcie: pinned host -> device, device -> host, or both at once")
     s.add_argument("--duty", type=float, default=1.0)
     s.add_argument("--period", type=float, default=0.0, help="burst period in s (duty = busy fraction of it)")
     s.add_argument("--seconds", type=float, default=10.0)

@@ -13,7 +13,6 @@ on its own thread with per-GPU error isolation, and this object only wires the p
 from __future__ import annotations
 
 import logging
-import os
 from typing import Optional
 
 from ._native import core
@@ -21,47 +20,18 @@ from .config import Config
 
 log = logging.getLogger("gpumon")
 
-_LEVELS = {"debug": 0, "info": 1, "warn": 2, "warning": 2, "error": 3, "off": 4}
-
-
-# well-known CRI sockets (the native pollers take the first that exists)
-_CRI_SOCKETS = ("/run/containerd/containerd.sock", "/var/run/containerd/containerd.sock", "/var/run/crio/crio.sock",
-                "/run/crio/crio.sock", "/var/run/cri-dockerd.sock", "/var/run/dockershim.sock")
-
 
 class GpuMonitor:
     def __init__(self, cfg: Optional[Config] = None, control_plane: bool = True):
         self.cfg = cfg or Config()
         self._core = core()
-        self._core.set_log_level(_LEVELS.get(self.cfg.log_level.lower(), 1))
-        core_cfg = self.cfg.to_core()
-        mode = self.cfg.control_plane if control_plane else "off"
-        if mode not in ("native", "off"):
-            # control_plane: python selected the grpcio test oracle of earlier releases (now under
-            # tests/oracles, not shipped): the native pollers do the same work
-            log.warning("control_plane=%s is not available in the exporter: using native", mode)
-            mode = "native"
-        if mode == "native":
-            # the exporter's own C++ pollers (csrc/core/grpc_lite.cpp) -- same as bin/gpumon-exporter
-            if self.cfg.pod_resources_socket not in ("", "none") and os.path.exists(self.cfg.pod_resources_socket):
-                core_cfg["pod_resources_socket"] = self.cfg.pod_resources_socket
-            # "" = autodetect, "none" = no CRI source (same rule as the native binary's options)
-            cri = self.cfg.cri_socket or next((p for p in _CRI_SOCKETS if os.path.exists(p)), "")
-            if cri and cri != "none":
-                core_cfg["cri_socket"] = cri[len("unix://"):] if cri.startswith("unix://") else cri
-            if self.cfg.docker_socket:  # opt-in: never autodetected (root-equivalent socket)
-                d = self.cfg.docker_socket
-                core_cfg["docker_socket"] = d[len("unix://"):] if d.startswith("unix://") else d
-            if self.cfg.pod_log_root:
-                core_cfg["pod_log_root"] = self.cfg.pod_log_root
-            if self.cfg.device_checkpoint:
-                core_cfg["device_checkpoint"] = self.cfg.device_checkpoint
-            core_cfg["pod_resources_refresh_s"] = float(self.cfg.metadata_refresh)
-            if self.cfg.resource_names:
-                core_cfg["pod_resources_prefix"] = self.cfg.resource_names[0]
-            core_cfg["pod_resources_dra_drivers"] = list(self.cfg.dra_drivers)
-        self.control_plane_mode = mode
-        self.ex = self._core.Exporter(core_cfg)
+        # the native options resolve everything: listen address, host fallback, the kubelet /
+        # CRI / Docker / log-tree sources and their autodetect (csrc/core/options.cpp), exactly as
+        # bin/gpumon-exporter does -- control_plane=False starts none of those pollers
+        self.options = self.cfg.finalized(control_plane=control_plane)
+        self._core.set_log_level(self.options.log_level_value)
+        self.control_plane_mode = "native" if control_plane and self.cfg.control_plane == "native" else "off"
+        self.ex = self._core.Exporter(self.options)
         self.plane = None      # kept for callers that check it: the control plane is in the core
         self.ondevice = None   # _core.OnDevice: PMC / probe samplers
         self.start_error = ""
@@ -78,14 +48,10 @@ class GpuMonitor:
         return self
 
     def _start_ondevice(self) -> None:
-        period = max(self.cfg.interval, 0.1)
-        # C++ threads over the same plugins the standalone binary dlopen()s (csrc/core/ondevice.h);
+        # C++ threads over the same plugins the standalone binary dlopen()s (csrc/core/ondevice.h),
+        # configured by the same finalized options (cadence from interval / probe_every);
         # PMC initialises before the probe (rocprofiler must register before HIP brings HSA up).
-        self.ondevice = self._core.OnDevice(self.ex, {
-            "plugin_dir": self.cfg.plugin_dir, "pmc": bool(self.cfg.enable_pmc),
-            "pmc_counters": list(self.cfg.pmc_counters), "pmc_every_s": period, "pmc_mode": self.cfg.pmc_mode,
-            "ondevice_isolate": self.cfg.ondevice_isolate, "helper_retry_s": float(self.cfg.helper_retry),
-            "probe": bool(self.cfg.enable_probe), "probe_every_s": period * self.cfg.probe_every})
+        self.ondevice = self._core.OnDevice(self.ex, self.options)
         self.ondevice.start()
 
     def step_ondevice(self) -> None:
@@ -115,7 +81,7 @@ class GpuMonitor:
 
     @property
     def url(self) -> str:
-        host = self.cfg.listen_addr
+        host = self.options.listen_addr
         if host in ("0.0.0.0", "", "::"):
             host = "127.0.0.1"  # the wildcard takes IPv4 loopback in both forms (dual-stack [::])
         elif ":" in host:

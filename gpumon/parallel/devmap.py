@@ -50,6 +50,46 @@ def hip_bdfs(ordinals: Iterable[int]) -> Dict[int, str]:
     return out
 
 
+def kfd_bdfs(ordinals: Iterable[int], topology: str = "/sys/class/kfd/kfd/topology/nodes",
+             env: Dict[str, str] | None = None) -> Dict[int, str]:
+    """The BDF each HIP ordinal WILL have, read from KFD's topology without initialising HIP (so
+    a child process can be started first): the runtime enumerates the GPU nodes (gpu_id != 0) in
+    node order, then ``ROCR_VISIBLE_DEVICES`` and ``HIP_VISIBLE_DEVICES`` (numeric lists) each
+    select and reorder. Ordinals it cannot predict (a UUID-valued variable, fewer nodes) are left
+    out; :func:`hip_bdfs` after initialisation is the check."""
+    import os
+
+    env = os.environ if env is None else env
+    nodes = []
+    try:
+        names = sorted((n for n in os.listdir(topology) if n.isdigit()), key=int)
+    except OSError:
+        return {}
+    for n in names:
+        try:
+            with open(f"{topology}/{n}/gpu_id") as fh:
+                if int(fh.read().strip() or 0) == 0:
+                    continue  # a CPU node
+            props = {}
+            with open(f"{topology}/{n}/properties") as fh:
+                for line in fh:
+                    k, _, v = line.partition(" ")
+                    props[k] = v.strip()
+            loc, dom = int(props["location_id"]), int(props.get("domain", "0"))
+        except (OSError, ValueError, KeyError):
+            continue  # outside this container's device cgroup, or not a GPU with a PCI location
+        nodes.append(f"{dom:04x}:{(loc >> 8) & 0xFF:02x}:{(loc >> 3) & 0x1F:02x}.{loc & 0x7:x}")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
+        sel = env.get(var)
+        if sel is None or sel.strip() == "":
+            continue
+        try:
+            nodes = [nodes[int(x)] for x in sel.split(",") if x.strip()]
+        except (ValueError, IndexError):
+            return {}  # UUIDs or an index past the end: no prediction
+    return {int(o): nodes[int(o)] for o in ordinals if 0 <= int(o) < len(nodes)}
+
+
 def match(ordinal_bdfs: Dict[int, str], statics: Sequence[dict], replicas: bool = False) -> List[dict]:
     """One row per loaded ordinal: ``{hip_ordinal, bdf, gpu_id, index}`` where ``index`` is the
     exporter's device index (the position in ``samples()`` / ``rates()``) of the GPU with that

@@ -25,7 +25,8 @@ def fake_exporter(core, monkeypatch):
 
     def make(env=None, **over):
         for k in ("FAKE_AMDSMI_GPUS", "FAKE_AMDSMI_PROCS", "FAKE_AMDSMI_FAIL_METRICS", "FAKE_AMDSMI_INIT_FAIL",
-                  "FAKE_AMDSMI_NO_METRICS", "FAKE_AMDSMI_UNSUPPORTED", "FAKE_AMDSMI_BUSY"):
+                  "FAKE_AMDSMI_NO_METRICS", "FAKE_AMDSMI_UNSUPPORTED", "FAKE_AMDSMI_BUSY",
+                  "FAKE_AMDSMI_DRIVER_VERSION"):
             monkeypatch.delenv(k, raising=False)
         for k, v in (env or {}).items():
             monkeypatch.setenv(k, str(v))
@@ -228,3 +229,73 @@ def test_cpx_partition_mode(fake_exporter):
     assert promtext.one(fam, "gpu_xcd_busy_percent", gpu_id="3", xcd="0") == 35
     assert promtext.one(fam, "gpu_xcd_busy_avg_percent", gpu_id="3", xcd="0") == pytest.approx(35)
     assert len(promtext.values(fam, "gpu_xcd_busy_percent")) == 16
+
+
+# The string libamd_smi returned on the pool's MI355X boxes (amdgpu in the kernel: /proc/version
+# with its spaces removed), which the exporter used to cut to 64 bytes into the gpu_info label
+# (profiles/data/r4/cm_base.prom:24).
+POOL_DRIVER_STRING = "Linuxversion6.18.51-ant.1(nixbld@localhost)(gcc(GCC)15.3.0,GNUld(GNUBinutils)2.46)#1-ant-ociSMP"
+
+
+def test_driver_version_label_from_proc_version_string(fake_exporter, tmp_path):
+    ex, err = fake_exporter({"FAKE_AMDSMI_DRIVER_VERSION": POOL_DRIVER_STRING}, sysfs_root=str(tmp_path))
+    assert err == ""
+    st = ex.statics()[0]
+    assert st["driver_version"] == "6.18.51-ant.1" and st["driver_source"] == "kernel"
+    ex.tick()
+    fam = promtext.parse(ex.metrics_text())
+    (_, lab, _), *_ = fam["gpu_info"]["samples"]
+    assert lab["driver_version"] == "6.18.51-ant.1" and lab["driver_source"] == "kernel"
+
+
+def test_driver_version_label_prefers_the_module_version(fake_exporter, tmp_path):
+    (tmp_path / "module" / "amdgpu").mkdir(parents=True)
+    (tmp_path / "module" / "amdgpu" / "version").write_text("6.12.12\n")
+    ex, err = fake_exporter({"FAKE_AMDSMI_DRIVER_VERSION": POOL_DRIVER_STRING}, sysfs_root=str(tmp_path))
+    assert err == ""
+    st = ex.statics()[0]
+    assert st["driver_version"] == "6.12.12" and st["driver_source"] == "module"
+
+
+@pytest.mark.parametrize("raw,want", [
+    ("Linux version 6.8.0-45-generic (buildd@lcy02-amd64-075) (x86_64-linux-gnu-gcc-13 (Ubuntu 13.2.0)",
+     ("6.8.0-45-generic", "kernel")),
+    (POOL_DRIVER_STRING, ("6.18.51-ant.1", "kernel")),
+    ("6.10.5", ("6.10.5", "library")),
+    # a long library string is cut at a separator, never inside a token
+    ("amdgpu 6.10.5 " + "x" * 40 + " build 1234567890 extra-tail-token", ("amdgpu 6.10.5 " + "x" * 40 + " build", "library")),
+])
+def test_driver_version_label_rules(core, raw, want):
+    got = core.driver_version_label(raw, "")
+    assert tuple(got) == want and len(got[0]) <= 64 and " " not in got[0].strip().split(" ")[-1]
+
+
+def test_driver_version_label_empty_falls_back_to_the_kernel_release(core):
+    v, src = core.driver_version_label("", "")
+    assert src == "kernel" and v == os.uname().release
+
+
+def test_pcie_interval_rate_from_the_accumulator(fake_exporter):
+    """gpu_pcie_bandwidth_bytes_per_second is d(pcie_bandwidth_acc) over the
+    firmware's accumulation ticks x pcie_bw_unit_bytes (102400 B/s per unit, measured on MI355X);
+    the instantaneous gauge is the same unit; the old GB/s-labelled family is gone."""
+    ex, err = fake_exporter({"FAKE_AMDSMI_GPUS": 2})
+    assert err == ""
+    ex.tick()
+    ex.tick()
+    r = ex.rates()
+    # the fake adds (500000 + 1000 d) units per accumulation tick
+    assert r[0]["pcie_Bps"] == pytest.approx(500000 * 102400.0)
+    assert r[1]["pcie_Bps"] == pytest.approx(501000 * 102400.0)
+    fam = promtext.parse(ex.metrics_text())
+    assert promtext.one(fam, "gpu_pcie_bandwidth_bytes_per_second", gpu_id="0") == pytest.approx(51.2e9)
+    assert promtext.one(fam, "gpu_pcie_bandwidth_inst_bytes_per_second", gpu_id="0") == 18 * 102400.0
+    assert "gpu_pcie_bandwidth_gbytes_per_second" not in fam
+
+
+def test_pcie_unit_is_configurable(fake_exporter):
+    ex, err = fake_exporter(pcie_bw_unit_bytes=1000.0)
+    assert err == ""
+    ex.tick()
+    ex.tick()
+    assert ex.rates()[0]["pcie_Bps"] == pytest.approx(500000 * 1000.0)

@@ -30,15 +30,18 @@ def test_reference_env_names():
     c = _ns([], env={"NODE_NAME": "gpu02", "INFLUXDB_URL": "http://influx:8086/write?db=k8s"})
     assert c.resolved_host() == "gpu02"
     assert c.influx_url == "http://influx:8086/write?db=k8s"
-    core = c.to_core()
-    assert core["host"] == "gpu02" and core["influx_url"].endswith("db=k8s")
+    fin = c.finalized()
+    assert fin.host == "gpu02" and c.to_dict()["influx_url"].endswith("db=k8s")
 
 
 def test_host_fallback_is_not_none(monkeypatch):
-    """Q1: the reference emitted host=None when NODE_NAME was unset."""
+    """Q1: the reference emitted host=None when NODE_NAME was unset. One rule, decided in C++
+    (csrc/core/options.cpp options_finalize): NODE_NAME, then the host name, then "no_name"."""
+    import socket
+
     monkeypatch.delenv("NODE_NAME", raising=False)
     h = Config().resolved_host()
-    assert h and h != "None"
+    assert h and h != "None" and h == (socket.gethostname() or "no_name")
 
 
 def test_yaml_env_flag_precedence(tmp_path):
@@ -57,16 +60,21 @@ def test_compat_flag():
     assert c.opt_in_label == "mlgpu=mlgpu" and c.interval == 10.0
 
 
-def test_unknown_yaml_key_rejected(tmp_path):
+def test_unknown_yaml_key_warned_and_ignored(tmp_path, caplog):
+    """A file key the exporter does not know is named and ignored -- by both entry points, since
+    both parse with csrc/core/options.cpp; a key given from code is an error."""
     y = tmp_path / "c.yaml"
-    y.write_text("bogus: 1\n")
-    with pytest.raises(ValueError):
-        _ns(["--config", str(y)])
+    y.write_text("bogus: 1\ninterval: 3\n")
+    with caplog.at_level("WARNING", logger="gpumon"):
+        c = _ns(["--config", str(y)])
+    assert c.interval == 3 and "'bogus'" in caplog.text
+    with pytest.raises(ValueError, match="unknown config key"):
+        Config(bogus=1)
 
 
-def test_to_core_roundtrip_starts(core):
+def test_finalized_options_start_an_exporter(core):
     c = Config(backend="mock:gpus=3", listen="127.0.0.1:0", interval=0)
-    ex = core.Exporter(c.to_core())
+    ex = core.Exporter(c.finalized())
     ex.start()
     try:
         assert len(ex.statics()) == 3
@@ -269,7 +277,7 @@ def test_influx_credentials_never_printed(tmp_path):
     d = json.loads(r.stdout)
     assert d["influx_url"] == "http://u:***@influx:8086/write?db=k8s" and d["influx_token"] == "***"
     c = Config().apply_env({"INFLUXDB_TOKEN": "tok-456"})
-    assert c.influx_token == "tok-456" and c.to_core()["influx_token"] == "tok-456"
+    assert c.influx_token == "tok-456" and c.to_dict(redact=True)["influx_token"] == "***"
 
 
 def test_influx_token_with_a_line_break_is_refused_at_start(core):
@@ -287,10 +295,10 @@ def test_devices_accept_hip_ids_and_bdfs_and_refuse_the_rest():
     gets them normalised, and a token that is neither is a configuration error, as in the binary."""
     from gpumon.config import Config
 
-    assert Config(devices=[0, "75:00.0", "0000:E5:00.0"]).to_core()["devices"] == ["0", "0000:75:00.0", "0000:e5:00.0"]
-    assert Config().apply_dict({"devices": "1, 0000:25:00.0"}).to_core()["devices"] == ["1", "0000:25:00.0"]
+    assert Config(devices=[0, "75:00.0", "0000:E5:00.0"]).devices == ["0", "0000:75:00.0", "0000:e5:00.0"]
+    assert Config().apply_dict({"devices": "1, 0000:25:00.0"}).devices == ["1", "0000:25:00.0"]
     with pytest.raises(ValueError, match="neither a hip id nor a PCI BDF"):
-        Config(devices=["gpu3"]).to_core()
+        Config(devices=["gpu3"])
 
 
 class _FlakySink(_Sink):

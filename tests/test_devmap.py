@@ -120,6 +120,8 @@ def test_native_config_accepts_bdfs(tmp_path):
     exe = os.path.join(ROOT, "bin", "gpumon-exporter")
     r = subprocess.run([exe, "--devices", "2,75:00.0", "--print-config"], capture_output=True, text=True, timeout=30)
     assert r.returncode == 0, r.stderr
-    assert '"devices": ["2", "0000:75:00.0"]' in r.stdout
+    import json
+
+    assert json.loads(r.stdout)["devices"] == ["2", "0000:75:00.0"]
     r = subprocess.run([exe, "--devices", "gpu3", "--print-config"], capture_output=True, text=True, timeout=30)
     assert r.returncode != 0 and "neither a hip id nor a PCI BDF" in r.stderr

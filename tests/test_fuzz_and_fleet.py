@@ -94,7 +94,9 @@ def test_metrics_doc_is_current():
 # String literals in csrc/ that look like family names but are not: label keys, libamd_smi call
 # names (gpumon_backend_call_* labels), a sysfs file name, and the on-device plugins' dlsym'd ABI
 # symbols (csrc/plugins/ondevice_abi.h).
-NOT_FAMILIES = {"gpu_id", "gpu_uuid", "gpu_metrics", "gpu_activity", "gpu_vram_bad_pages"}
+NOT_FAMILIES = {"gpu_id", "gpu_uuid", "gpu_metrics", "gpu_activity", "gpu_vram_bad_pages",
+                # JSON keys of the loopback /debug views (csrc/core/exporter_debug.cpp)
+                "gpu_util", "process_list_failures"}
 NOT_FAMILY_PREFIXES = ("gpumon_pmc_abi", "gpumon_pmc_agent", "gpumon_pmc_init", "gpumon_pmc_read_running",
                        "gpumon_pmc_sample_many", "gpumon_pmc_stop_running", "gpumon_probe_abi", "gpumon_probe_create",
                        "gpumon_probe_destroy", "gpumon_probe_device_count", "gpumon_probe_device_pci", "gpumon_probe_launch",

@@ -169,10 +169,15 @@ def test_native_exporter_reports_a_separate_tenant_process():
     s.close()
     load = subprocess.Popen([sys.executable, "-m", "gpumon", "load", "--kind", "mfma", "--seconds", "14"],
                             cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
-    # a second tenant that holds 3 GiB of VRAM and runs nothing
+    # a second tenant that holds 3 GiB of VRAM and runs nothing (after the one fill kernel)
     idle = subprocess.Popen([sys.executable, "-c", "import time, torch; x = torch.ones(3 << 28, device='cuda:0'); "
                              "torch.cuda.synchronize(); time.sleep(16)"], cwd=ROOT, stdout=subprocess.DEVNULL,
                             stderr=subprocess.PIPE, text=True)
+    # a third that only allocates 5 GiB and never submits anything: a context with no queue (VERDICT
+    # r5 #3 -- what a multi-GPU process's peer context looks like on a GPU it does not work on)
+    alloc = subprocess.Popen([sys.executable, "-c", "import time, torch; x = torch.empty(5 << 30, dtype=torch.uint8, "
+                              "device='cuda:0'); time.sleep(16)"], cwd=ROOT, stdout=subprocess.DEVNULL,
+                             stderr=subprocess.PIPE, text=True)
     exe = os.path.join(ROOT, "bin", "gpumon-exporter")
     ex = subprocess.Popen([exe, "--backend", "amdsmi", "--interval", "0.5", "--listen", f"127.0.0.1:{port}",
                            "--log-level", "warn", "--no-pod-resources", "--no-cri"],
@@ -186,7 +191,7 @@ def test_native_exporter_reports_a_separate_tenant_process():
     finally:
         ex.terminate()
         ex.wait(20)
-        for p in (load, idle):
+        for p in (load, idle, alloc):
             try:
                 p.wait(60)
             except subprocess.TimeoutExpired:
@@ -196,7 +201,7 @@ def test_native_exporter_reports_a_separate_tenant_process():
     busy = {l["pid"]: v for _, l, v in fam["pod_gpu_proc_gfx_util"]["samples"]}
     mem = {l["pid"]: v for _, l, v in fam["pod_gpu_used_memory"]["samples"]}  # MiB
     # the idle tenant: its row is exported (it holds VRAM) with ~0 waves and ~0 busy
-    quiet = [p for p, v in mem.items() if v >= 3000 and occ.get(p, 1e9) < 2]
+    quiet = [p for p, v in mem.items() if 3000 <= v < 4500 and occ.get(p, 1e9) < 2]
     assert len(quiet) == 1, (mem, occ, busy)
     assert busy[quiet[0]] < 5, (mem, occ, busy)
     # the burn process holds every wave slot except in the gaps between its host-synchronised
@@ -206,6 +211,15 @@ def test_native_exporter_reports_a_separate_tenant_process():
     assert busy[hot[0]] > 60, (occ, busy)
     assert promtext.one(fam, "gpu_cu_occupancy_percent", gpu_id="0") > 60
     assert promtext.one(fam, "gpumon_occupancy_reads_total") > 0
+    # KFD's queue list: the kernel tenants hold queues on the GPU, the allocate-only one none -- and
+    # it keeps its row (one GPU: no workload elsewhere, so not a peer context)
+    queues = {l["pid"]: v for _, l, v in fam["pod_gpu_proc_queues"]["samples"]}
+    only_alloc = [p for p, v in mem.items() if v >= 5000]
+    assert len(only_alloc) == 1, (mem, queues)
+    assert queues[only_alloc[0]] == 0, queues
+    assert queues[hot[0]] >= 1 and queues[quiet[0]] >= 1, (queues, hot, quiet)
+    print(f"\nqueues per tenant: burn {queues[hot[0]]:.0f}, fill-then-idle {queues[quiet[0]]:.0f}, "
+          f"allocate-only {queues[only_alloc[0]]:.0f}")
 
 
 def test_doctor_on_mi355x_reports_the_firmware_cadence():

@@ -70,6 +70,12 @@ def test_amdsmi_static_and_sample_sane(core, torch_gpu):
         assert s0["vram_total_bytes"] > 280 * 2 ** 30  # 288 GiB HBM3E
         assert s0["num_cu"] == 256
         assert s0["bdf"].count(":") == 2
+        # a version token, never /proc/version with its spaces stripped
+        assert s0["driver_version"] and " " not in s0["driver_version"] and "(" not in s0["driver_version"]
+        assert not s0["driver_version"].startswith("Linux"), s0["driver_version"]
+        assert s0["driver_source"] in ("module", "kernel", "library")
+        if s0["driver_source"] == "kernel":
+            assert s0["driver_version"] == os.uname().release, (s0, os.uname().release)
         ex.tick()
         sm = ex.samples()[0]
         f = sm["fields"]
@@ -575,5 +581,42 @@ def test_xgmi_peer_labels_complete_and_paired_by_counters(core, torch_gpu):
         v = promtext.one(fam, "gpumon_xgmi_slot_map_verified", gpu_id="0")
         u = promtext.one(fam, "gpumon_xgmi_slot_map_unverified", gpu_id="0")
         assert v + u == 7, (v, u)
+    finally:
+        ex.stop()
+
+
+@pytest.mark.parametrize("direction", ["h2d", "d2h", "both"])
+def test_pcie_interval_rate_tracks_host_copies(core, torch_gpu, direction):
+    """gpu_pcie_bandwidth_bytes_per_second (d(pcie_bandwidth_acc) over the
+    accumulation ticks x 102400 B/s per unit) within 15 % of pinned host <-> device copies' rate,
+    and near 0 on an idle link; the instantaneous gauge tracks the same load (tools/pcie_probe.py,
+    profiles/r6_pcie_bandwidth.md)."""
+    from gpumon.ops.load import SyntheticLoad
+
+    ex = _exporter(core)
+    try:
+        ex.tick()
+        time.sleep(0.5)
+        ex.tick()
+        idle = ex.rates()[0]["pcie_Bps"]
+        assert idle is not None and idle < 0.5e9, idle  # MI355X idle: ~2 MB/s (18-21 units)
+        with SyntheticLoad(0, "pcie", pcie_direction=direction) as load:
+            time.sleep(0.6)
+            ex.tick()
+            a = load.stats()
+            got, inst = [], []
+            for _ in range(4):
+                time.sleep(0.5)
+                ex.tick()
+                got.append(ex.rates()[0]["pcie_Bps"])
+                inst.append(ex.samples()[0]["fields"]["pcie_bw_inst"])
+            b = load.stats()
+        want = (b["bytes"] - a["bytes"]) / (b["wall_s"] - a["wall_s"])
+        mean = sum(got) / len(got)
+        print(f"\n{direction}: copies {want / 1e9:.2f} GB/s, exported {mean / 1e9:.2f} GB/s "
+              f"({mean / want:.3f}), inst {sum(inst) / len(inst) / 1e9:.2f} GB/s")
+        assert want > 10e9, want  # PCIe Gen5 x16: ~57 GB/s one way
+        assert abs(mean / want - 1) < 0.15, (mean, want, got)
+        assert abs(sum(inst) / len(inst) / want - 1) < 0.25, (inst, want)
     finally:
         ex.stop()

@@ -78,7 +78,10 @@ def test_staged_exporter_maps_only_the_closure_and_glibc(staged, backend, want_l
     for w in want_libs:
         assert any(m.startswith(w) for m in mapped), (w, mapped)
     if backend.startswith("mock"):
-        assert r["gpu_up"] == ['gpu_up{host="no_name",gpu_id="0"} 1'] and r["ok"]
+        import socket
+
+        host = socket.gethostname() or "no_name"  # NODE_NAME unset: the host name (options.cpp)
+        assert r["gpu_up"] == [f'gpu_up{{host="{host}",gpu_id="0"}} 1'] and r["ok"]
 
 
 def test_check_detects_a_library_outside_the_closure(tmp_path):

@@ -99,7 +99,7 @@ def test_parse_listen_native_and_python_agree(core, listen, host, port):
     assert parse_listen(listen) == (host, port)
     c = Config(listen=listen)
     assert (c.listen_addr, c.port) == (host, port)
-    assert c.to_core()["listen_addr"] == host
+    assert c.finalized().listen_addr == host
 
 
 @pytest.mark.parametrize("listen,want", BAD)

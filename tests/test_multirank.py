@@ -34,14 +34,19 @@ def _fake_proc(tmp_path, pid, cgroup, comm="python3"):
     (d / "cgroup").write_text(cgroup)
 
 
-def _ranks(peer_vram_mib=96, own_vram_gib=40, peer_gpus=range(8)):
+def _ranks(peer_vram_mib=96, own_vram_gib=40, peer_gpus=range(8), queues=False):
+    """`queues`: KFD's per-process queue list is readable (the sysfs fast path): each rank holds
+    2 queues on its own GPU and none on the peers (measured on MI355X, profiles/r6_kfd_queues.md)."""
     procs = []
     for r in range(8):
         for g in peer_gpus:
             own = g == r
-            procs.append({"pid": 1000 + r, "device": g, "name": "python3", "kfd_only": True,
-                          "vram_bytes": (own_vram_gib << 30) if own else peer_vram_mib << 20,
-                          "gfx_share": 1.0 if own else 0.0})
+            p = {"pid": 1000 + r, "device": g, "name": "python3", "kfd_only": True,
+                 "vram_bytes": (own_vram_gib << 30) if own else peer_vram_mib << 20,
+                 "gfx_share": 1.0 if own else 0.0}
+            if queues:
+                p["queues"] = 2 if own else 0
+            procs.append(p)
     return procs
 
 
@@ -131,3 +136,55 @@ def test_waves_on_a_peer_gpu_make_it_a_workload(torchrun_pod):
     rows = _workload_rows(ex)
     assert collections.Counter(r["dev"] for r in rows)[1] == 2
     assert {r["pid"] for r in rows if r["dev"] == 1} == {"1000", "1001"}
+
+
+
+# ---------------------------------------------------------------- KFD queues
+@pytest.mark.parametrize("peer_vram_mib", [96, 2048, 16384])
+def test_queue_list_hides_peer_contexts_whatever_their_vram(torchrun_pod, peer_vram_mib):
+    """Where KFD lists each process's hardware queues, a context with no queue on its GPU and no
+    waves there is a peer context however much VRAM it holds: 8 rows for 8 ranks, also when the
+    threshold rule alone would have made 64 (test_peer_context_with_much_vram_is_a_workload)."""
+    ex = torchrun_pod(_ranks(peer_vram_mib=peer_vram_mib, queues=True))
+    rows = _workload_rows(ex)
+    assert {(r["dev"], r["pid"]) for r in rows} == {(g, str(1000 + g)) for g in range(8)}
+    assert ex.self_stats()["hidden_peer_contexts"] == 56
+
+
+def _tp_pair(queues):
+    """A tensor / pipeline-parallel process (pid 2000): its main shard on GPU 0 with waves, a 100 MiB
+    shard on GPU 1 that it also computes on (queues there) but had no wave resident in the window."""
+    q0, q1 = (2, 2) if queues else (-1, -1)
+    return [{"pid": 2000, "device": 0, "kfd_only": True, "vram_bytes": 30 << 30, "gfx_share": 1.0, "queues": q0},
+            {"pid": 2000, "device": 1, "kfd_only": True, "vram_bytes": 100 << 20, "gfx_share": 0.0, "queues": q1}]
+
+
+def test_tp_process_with_a_small_idle_shard_keeps_its_row(mock_exporter):
+    """VERDICT r5 #3 done-means: a TP / PP process with a < 512 MiB idle shard keeps that row when
+    KFD shows it holds queues on that GPU (the VRAM threshold alone hid it: next test)."""
+    ex = mock_exporter(backend="mock:gpus=2,mode=const,const_util=50", sample_threads=0,
+                       mock={"procs": _tp_pair(queues=True)})
+    for _ in range(3):
+        ex.tick()
+    assert sorted((r["dev"], r["pid"]) for r in _workload_rows(ex)) == [(0, "2000"), (1, "2000")]
+    assert ex.self_stats()["hidden_peer_contexts"] == 0
+
+
+def test_without_a_queue_list_the_vram_threshold_still_applies(mock_exporter):
+    ex = mock_exporter(backend="mock:gpus=2,mode=const,const_util=50", sample_threads=0,
+                       mock={"procs": _tp_pair(queues=False)})
+    for _ in range(3):
+        ex.tick()
+    assert [(r["dev"], r["pid"]) for r in _workload_rows(ex)] == [(0, "2000")]
+    assert ex.self_stats()["hidden_peer_contexts"] == 1
+
+
+def test_allocate_only_single_gpu_process_keeps_its_row(mock_exporter):
+    """No queue anywhere and no other GPU: not a peer context (a job still starting up, a notebook
+    that only allocated) -- the rule needs a workload on another GPU."""
+    ex = mock_exporter(backend="mock:gpus=2,mode=const,const_util=50", sample_threads=0,
+                       mock={"procs": [{"pid": 88, "device": 1, "kfd_only": True, "vram_bytes": 1 << 30,
+                                        "gfx_share": 0.0, "queues": 0}]})
+    for _ in range(2):
+        ex.tick()
+    assert [(r["dev"], r["pid"]) for r in _workload_rows(ex)] == [(1, "88")]

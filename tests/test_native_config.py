@@ -1,8 +1,8 @@
-"""bin/gpumon-exporter reads the same configuration as the Python control plane
-(csrc/core/options.cpp vs gpumon/config.py): the DaemonSet ConfigMap's YAML, GPUMON_<KEY> env,
-the reference's NODE_NAME / INFLUXDB_URL, flags last."""
+"""One configuration implementation (csrc/core/options.cpp): bin/gpumon-exporter's command line and
+the Python view (gpumon/config.py, `gpumon serve`) read the DaemonSet ConfigMap's YAML, GPUMON_<KEY>
+env, the reference's NODE_NAME / INFLUXDB_URL and the flags through the same native table, so the
+binary's --print-config and the Python view agree by construction (checked here end to end)."""
 
-import dataclasses
 import json
 import os
 import subprocess
@@ -10,7 +10,7 @@ import subprocess
 import pytest
 import yaml
 
-from gpumon.config import Config, load_yaml
+from gpumon.config import Config
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "bin", "gpumon-exporter")
@@ -26,9 +26,9 @@ def _print(*args, env=None):
 def _py(path=None, env=None):
     cfg = Config()
     if path:
-        cfg.apply_dict(load_yaml(path))
+        cfg.apply_file(path)
     cfg.apply_env(dict(env or {}))
-    return dataclasses.asdict(cfg)
+    return cfg.to_dict()
 
 
 def _same(native, py):
@@ -73,7 +73,8 @@ gpumon:
   ras_every: 0
   gzip: off
   influx_url: http://influx:8086/write?db=k8s#not-a-comment
-  control_plane: native         # Python-only key: warned about, ignored
+  control_plane: native
+  not_a_key: 3                  # warned about, ignored
 """
 
 
@@ -87,7 +88,7 @@ def test_rich_file_env_and_flag_precedence(tmp_path):
     assert n["devices"] == ["0", "2", "5"] and n["dra_drivers"] == [] and n["gzip"] is False
     assert n["pod_label_allowlist"] == ["team", "app.kubernetes.io/name"]
     assert n["influx_url"] == "http://influx:8086/write?db=k8s#not-a-comment"
-    assert "control_plane" in r.stderr  # the ignored key is named
+    assert "'not_a_key'" in r.stderr and "control_plane" not in r.stderr  # the ignored key is named
     # env over file, flags over env; the reference's env names
     env = {"GPUMON_INTERVAL": "2.5", "GPUMON_DEVICES": "1,3", "NODE_NAME": "gpu-node-7",
            "INFLUXDB_URL": "http://other/write", "GPUMON_FAKE_SOMETHING": "x"}
@@ -127,14 +128,12 @@ def test_both_entry_points_take_each_others_flags(flags):
     native = json.loads(r.stdout)
     ap = argparse.ArgumentParser()
     add_cli_args(ap)
-    py = dataclasses.asdict(from_args(ap.parse_args(flags), env={}))
+    cfg = from_args(ap.parse_args(flags), env={})
+    _same(native, cfg.to_dict())
     if "--control-plane" in flags:
-        # Python turns its pollers off as a whole; the native binary clears each source
-        assert py["control_plane"] == "off"
-        assert native["pod_resources_socket"] == "" and native["cri_socket"] == "none"
-        assert native["docker_socket"] == "" and native["pod_log_root"] == ""
-        return
-    _same(native, py)
+        # off: every metadata source of the finalized options is cleared
+        assert native["control_plane"] == "off"
+        assert all(v == "" for v in cfg.finalized().exporter_sources.values())
 
 
 @pytest.mark.parametrize("args,rc,want", [
@@ -285,9 +284,44 @@ def test_environment_only_knobs_are_documented():
     for base, _, files in os.walk(os.path.join(ROOT, "csrc")):
         for f in files:
             if f.endswith((".cpp", ".h", ".hip")):
-                read |= set(re.findall(r'getenv\("(GPUMON_[A-Z0-9_]+)"\)', open(os.path.join(base, f)).read()))
+                text = open(os.path.join(base, f)).read()
+                read |= set(re.findall(r'getenv\("(GPUMON_[A-Z0-9_]+)"\)', text))
+                read |= set(re.findall(r'"(GPUMON_[A-Z0-9_]+)="', text))  # read from an envp block
     read = {v for v in read if not v.startswith("GPUMON_FAKE_")}
     listed = {name for name, *_ in gen_config_doc.ENV_ONLY}
     assert read == listed, (read - listed, listed - read)
     doc = open(os.path.join(ROOT, "docs", "configuration.md")).read()
     assert doc == gen_config_doc.render(), "docs/configuration.md is stale: python tools/gen_config_doc.py"
+
+
+def test_drifts_of_round_5_are_gone(monkeypatch, tmp_path):
+    """the two parsers disagreed on the CRI autodetect list (Python tried
+    /var/run/containerd/containerd.sock, native did not) and on the host fallback (Python NODE_NAME
+    -> host name -> no_name, native NODE_NAME -> no_name). Both now come from options.cpp."""
+    import socket
+
+    from gpumon import core
+
+    socks = core().cri_autodetect_sockets()
+    assert "/var/run/containerd/containerd.sock" in socks and socks[0] == "/run/containerd/containerd.sock"
+    monkeypatch.delenv("NODE_NAME", raising=False)
+    want = socket.gethostname() or "no_name"
+    assert Config().resolved_host() == want
+    p = tmp_path / "c.yaml"
+    p.write_text("gpumon:\n  backend: 'mock:gpus=1'\n  control_plane: 'off'\n")
+    r = subprocess.run([BIN, "--config", str(p), "--once"], capture_output=True, text=True, timeout=60, env=CLEAN_ENV)
+    assert r.returncode == 0, r.stderr
+    assert f'node_gpu_gpu_util{{host="{want}"' in r.stdout
+
+
+def test_python_view_has_no_key_table_of_its_own():
+    """No key, default or autodetect list in two languages: gpumon/config.py names none of them."""
+    import re
+
+    src = open(os.path.join(ROOT, "gpumon", "config.py")).read()
+    assert "containerd" not in src and "turing-gpu-notebook" not in src and "9400" not in src
+    assert "@dataclass" not in src and not re.search(r"^    \w+: (str|int|float|bool|List)\b.* = ", src, re.M)
+    from gpumon import core
+
+    keys = {k["key"] for k in core().option_keys()}
+    assert {"interval", "listen", "host", "control_plane", "cri_socket", "debug_listen", "pcie_bw_unit_bytes"} <= keys

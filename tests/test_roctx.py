@@ -40,6 +40,6 @@ def test_config_roctx_flag():
         add_cli_args(p)
         return from_args(p.parse_args(argv), env=env)
 
-    assert Config().to_core()["roctx"] is False
-    assert parse(["--roctx"], {}).to_core()["roctx"] is True
+    assert Config().roctx is False
+    assert parse(["--roctx"], {}).roctx is True
     assert parse([], {"GPUMON_ROCTX": "1"}).roctx is True

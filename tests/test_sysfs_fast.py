@@ -341,3 +341,47 @@ def test_kfd_per_pid_files_are_kept_open_and_closed_when_the_process_leaves(expo
     ex.tick()
     assert ex.self_stats()["kfd_files_open"] == 0
     assert not [r for r in ex.pod_rows() if not r["idle"] and r["dev"] == 0]
+
+
+def _queues(kp, gpu_ids):
+    """KFD's per-process queue list: one proc/<pid>/queues/<qid>/gpuid per hardware queue."""
+    for q, gid in enumerate(gpu_ids):
+        (kp / "queues" / str(q)).mkdir(parents=True)
+        (kp / "queues" / str(q) / "gpuid").write_text(f"{gid}\n")
+        (kp / "queues" / str(q) / "type").write_text("0\n")
+    (kp / "queues").mkdir(exist_ok=True)
+
+
+def test_kfd_queue_list_classifies_peer_contexts(exporter, tmp_path):
+    """the sysfs fast path reads proc/<pid>/queues/*/gpuid. Rank 7070 computes on GPU 0
+    (2 queues there) and holds a 2 GiB context on GPU 1 with no queue and no waves: a peer context
+    whatever its VRAM (the 512 MiB threshold alone kept it). Process 8080 holds 64 MiB on GPU 1
+    with a queue there but no wave this tick, and its main work on GPU 0: it keeps both rows."""
+    sysr, procr = make_tree(tmp_path, gpus=2, procs=())
+    a0, a1 = _kfd_proc(sysr, 7070, d=0, occ=120), None
+    (a0 / "stats_36623").mkdir()
+    (a0 / "vram_36623").write_text(f"{2 << 30}\n")
+    (a0 / "stats_36623" / "cu_occupancy").write_text("0\n")
+    _queues(a0, [36622, 36622])
+    b = _kfd_proc(sysr, 8080, d=0, occ=90)
+    (b / "stats_36623").mkdir()
+    (b / "vram_36623").write_text(f"{64 << 20}\n")
+    (b / "stats_36623" / "cu_occupancy").write_text("0\n")
+    _queues(b, [36622, 36623])
+    ex = exporter(sysr, procr, sample_threads=0)
+    for _ in range(2):
+        ex.tick()
+    rows = sorted((r["dev"], r["pid"]) for r in ex.pod_rows() if not r["idle"])
+    assert rows == [(0, "7070"), (0, "8080"), (1, "8080")], rows
+    assert ex.self_stats()["hidden_peer_contexts"] == 1
+    # without the queue list (an unreadable directory) the VRAM threshold decides again: 7070's
+    # 2 GiB context on GPU 1 is then a workload row, 8080's 64 MiB one a peer context
+    import shutil
+
+    for pid in (7070, 8080):
+        shutil.rmtree(sysr / "class" / "kfd" / "kfd" / "proc" / str(pid) / "queues")
+    ex2 = exporter(sysr, procr, sample_threads=0)
+    for _ in range(2):
+        ex2.tick()
+    rows = sorted((r["dev"], r["pid"]) for r in ex2.pod_rows() if not r["idle"])
+    assert rows == [(0, "7070"), (0, "8080"), (1, "7070")], rows

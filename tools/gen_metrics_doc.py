@@ -106,7 +106,8 @@ def collect():
                              "influx_url": f"http://127.0.0.1:{srv.server_port}/write?db=k8s", "ras_every": 1})
             ex.start()
             try:
-                ex.mock_set_procs([{"pid": os.getpid(), "device": 0, "name": "python", "vram_bytes": 1 << 30}])
+                ex.mock_set_procs([{"pid": os.getpid(), "device": 0, "name": "python", "vram_bytes": 1 << 30,
+                                    "queues": 2}])
                 ex.set_allocations([{"pod_namespace": "ml", "pod_name": "jupyter-q-0", "container_name": "c",
                                      "gpu_index": 0}])
                 ex.mock_set_ras_event(0, "bad_pages", 0.0)
