@@ -762,12 +762,22 @@ def main() -> int:
         thr = {k: round(1000.0 * (v - cpu0.get(k, 0.0)) / elapsed, 2) for k, v in sorted(cpu1.items())}
         tenant_pids = sorted({x["pid"] for x in ranks_seen})
         row_pids = sorted({int(r["pid"]) for r in rows if not r["idle"] and str(r["pid"]).isdigit()})
+        # KFD lists HOST pids: in a container with its own pid namespace (a gpurun box) the rows
+        # carry pids this process cannot see, and the tenants are checked by count instead -- one
+        # workload row per loaded GPU per rank on it, none of them the exporter's
+        same_ns = bool(set(row_pids) & set(tenant_pids))
+        want_rows = {r["index"]: sum(1 for x in ranks_seen if world == 1 or x["local_rank"] == r["hip_ordinal"])
+                     for r in dev_rows}
+        got_rows = {r["index"]: sum(1 for x in rows if not x["idle"] and x["dev"] == r["index"]) for r in dev_rows}
         exporter_info.update(
             rss_mb=round(ex.rss_bytes() / 2 ** 20, 1) if ex.rss_bytes() else None,
             tenant_pids=tenant_pids,
-            # in a cluster the exporter only ever attributes other processes: every pod row's pid
-            # should be a tenant's, and none the exporter's own
-            rows_are_tenants=bool(row_pids) and set(row_pids) <= set(tenant_pids) if has_gpu else None,
+            row_pids=row_pids,
+            pid_namespace="shared" if same_ns else "separate (rows carry host pids)",
+            # in a cluster the exporter only ever attributes other processes: every pod row is a
+            # tenant's (by pid where the namespaces agree, else by count), none the exporter's own
+            rows_are_tenants=(set(row_pids) <= set(tenant_pids) if same_ns else got_rows == want_rows)
+            if has_gpu and loads else None,
             exporter_pid_in_rows=exporter_info.get("pid") in row_pids)
         result = {
             "metric": BASELINE_METRIC,

@@ -21,6 +21,26 @@ def _json_lines(out):
     return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
 
 
+def _check_exporter(d, world):
+    """the line measures the SHIPPED binary, run as its own process, attributing
+    the bench's load as a foreign tenant; and it carries what the first 8-GPU record must settle."""
+    info = d["exporter_info"]
+    assert d["exporter"] == "bin/gpumon-exporter" and info["mode"] == "child"
+    assert d["exporter_pid"] == info["pid"] and d["exporter_pid"] not in info["tenant_pids"]
+    assert info["spawned_before_hip"] is True and not info["exporter_pid_in_rows"]
+    assert len(info["tenant_pids"]) == world and info["rss_mb"] > 0
+    # the child's CPU per thread name (all of that process is the exporter)
+    thr = d["exporter_thread_cpu_millicores"]
+    assert {"gpumon-sampler", "gpumon-http"} <= set(thr) and d["exporter_cpu_millicores"] == pytest.approx(
+        sum(thr.values()), abs=0.05)
+    # per sampled device: its own calls' time per tick
+    assert [x["gpu"] for x in d["per_device_tick_ms"]] == list(range(d["sampled_devices"]))
+    assert all(x["t_device_mean_ms"] > 0 and "t_procs_mean_ms" in x for x in d["per_device_tick_ms"])
+    # the process group's world size as every rank saw it
+    assert sorted(x["rank"] for x in d["ranks"]) == list(range(world))
+    assert all(x["world_size"] == world for x in d["ranks"])
+
+
 def _check(d, n, steps, warmup):
     assert REQUIRED <= set(d)
     base = json.load(open(os.path.join(ROOT, "BASELINE.json")))
@@ -45,6 +65,7 @@ def test_bench_single_process(dist):
     lines = _json_lines(r.stdout)
     assert len(lines) == 1
     _check(lines[0], 1, 3, 1)
+    _check_exporter(lines[0], 1)
     assert lines[0]["value"] == pytest.approx(10.0, rel=0.2)  # 1 device x 10 Hz
     idle = lines[0]["scrape_idle"]  # untimed idle reference before the load
     assert idle["scrapes"] > 5 and idle["scrape_errors"] == 0 and idle["scrape_p99_ms"] > 0 and idle["ticks"] >= 5
@@ -139,6 +160,7 @@ def test_bench_eight_ranks_exact_scale_command():
     assert len(lines) == 1, r.stdout
     d = lines[0]
     _check(d, 8, 3, 1)
+    _check_exporter(d, 8)
     assert d["sampled_devices"] == 8 and d["config"]["interval_s"] == 1.0
     assert [x["hip_ordinal"] for x in d["devices"]] == list(range(8))
     assert len({x["gpu_id"] for x in d["devices"]}) == 8 and d["device_check"]["ok"]
@@ -152,6 +174,40 @@ def test_bench_eight_ranks_exact_scale_command():
     # with the rest of the parallel CPU suite on the same CPUs (exact on the GPU node, where RCCL
     # moves the bytes)
     assert d["value"] == pytest.approx(8.0, rel=0.25)
+
+
+def test_inprocess_exporter_is_the_ab_mode():
+    """--exporter inprocess keeps the old embedding (the same core through the bindings) for A/B."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--exporter", "inprocess", "--steps", "3",
+                        "--warmup", "1", "--interval", "0.1", "--idle-s", "0.5", "--capacity-s", "0"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    (d,) = _json_lines(r.stdout)
+    _check(d, 1, 3, 1)
+    assert d["exporter"] == "in-process (gpumon._core)" and d["exporter_pid"] == d["exporter_info"]["tenant_pids"][0]
+    assert set(d["exporter_thread_cpu_millicores"]) <= {"gpumon-sampler", "gpumon-http", "gpumon-dev0", "gpumon-proc0"}
+
+
+def test_child_exporter_uses_the_daemonset_config(tmp_path):
+    """The child reads a config file with the DaemonSet ConfigMap's keys plus the bench's overrides;
+    its /debug views answer on loopback only."""
+    from gpumon.export.child import ChildExporter, daemonset_config
+
+    base = daemonset_config()
+    assert base["interval"] == 1.0 and base["listen"] == ":9400" and "pod_resources_socket" in base
+    ex = ChildExporter(dict(base, backend="mock:gpus=2", interval=0.1, log_level="warn"), str(tmp_path)).start()
+    try:
+        assert ex.wait_ticks(2, 10)
+        st = ex.state()
+        assert st["pid"] == ex.pid != os.getpid() and len(st["statics"]) == 2
+        text = (tmp_path / "gpumon-config.yaml").read_text()
+        assert "debug_listen: \"127.0.0.1:" in text and "user_prefix: \"turing-gpu-notebook-\"" in text
+        ticks = ex.ticks(0)
+        assert ticks and all(len(t["dev"]) == 2 for t in ticks)
+        assert "node_gpu_gpu_util" in ex.metrics()
+    finally:
+        assert ex.stop() == 0
 
 
 def test_post_measurement_extras_are_time_bounded():
