@@ -1124,6 +1124,7 @@ PYBIND11_MODULE(_core, m) {
              d["http_evicted"] = s.http_evicted;
              d["http_max_conns"] = s.http_max_conns;
              d["http_tls_failures"] = s.http_tls_failures;
+             d["http_tls_client_cert_refused"] = s.http_tls_client_cert_refused;
              d["http_tls_not_after"] = s.http_tls_not_after;
              d["http_tls_reloads_ok"] = s.http_tls_reloads_ok;
              d["http_tls_reloads_failed"] = s.http_tls_reloads_failed;

@@ -1101,6 +1101,7 @@ SelfStats Exporter::self_stats() const {
     s.http_max_conns = static_cast<int64_t>(server_->max_conns() * static_cast<size_t>(std::max(1, cfg_.http_threads)));
     if (const TlsServer* t = server_->tls_server()) {
       s.http_tls_failures = static_cast<int64_t>(server_->tls_failures());
+      if (t->mutual()) s.http_tls_client_cert_refused = static_cast<int64_t>(mtls_refused_.load(std::memory_order_relaxed));
       s.http_tls_not_after = t->not_after();
       s.http_tls_reloads_ok = t->reloads_ok();
       s.http_tls_reloads_failed = t->reloads_failed();

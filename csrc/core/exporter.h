@@ -381,6 +381,7 @@ class Exporter {
   std::atomic<bool> push_tls_check_now_{false};   // reload_tls(): re-stamp the push's TLS files
   std::shared_ptr<TokenAuth> auth_;               // http_auth_token_file (nullptr: /metrics is open)
   std::atomic<uint64_t> auth_failures_[3] = {};   // /metrics requests refused with 401: missing, scheme, token
+  std::atomic<uint64_t> mtls_refused_{0};         // mutual TLS: /metrics refused with 403 (no client certificate)
 
   // per-device sampling workers + watchdog (dev_workers.cpp)
   void start_workers(int n);

@@ -90,6 +90,14 @@ std::shared_ptr<const Exporter::Filtered> Exporter::filtered(const Snapshot& s, 
 
 void Exporter::handle_http(const HttpRequest& req, HttpResponse* resp) {
   if (req.path == "/metrics") {
+    if (!req.client_cert && server_ && server_->tls_server() && server_->tls_server()->mutual()) {
+      // mutual TLS: the handshake asks for a client certificate without requiring one (so the
+      // kubelet's HTTPS probes reach /healthz and /readyz); the metrics need one that verified
+      mtls_refused_.fetch_add(1, std::memory_order_relaxed);
+      resp->status = 403;
+      resp->inline_body = "client certificate required\n";
+      return;
+    }
     if (const auto v = auth_ ? auth_->check(req.authorization) : TokenAuth::Verdict::kOk; v != TokenAuth::Verdict::kOk) {
       auth_failures_[static_cast<int>(v) - 1].fetch_add(1, std::memory_order_relaxed);
       resp->status = 401;

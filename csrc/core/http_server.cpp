@@ -53,12 +53,52 @@ constexpr rlim_t kFdReserve = 256;
 // a few fds out of kFdReserve.
 constexpr size_t kDebtSlack = 16;
 constexpr int kSndBuf = 1 << 20;  // GPUMON_HTTP_SNDBUF overrides (bytes; 0 = the kernel's autotuning)
+// The connection cap also answers to the memory limit: every admitted connection may
+// buffer kMaxInput of request before the header timeout closes it, plus a TLS session, so a flood
+// must not push the process past its cgroup's memory.max (the DaemonSet's 256Mi, the systemd
+// unit's MemoryMax) into an OOM-kill restart loop. kMemBaseline is left to the rest of the exporter
+// (its steady RSS is ~10 MB; libamd_smi and the snapshots of 8 GPUs stay well under this).
+constexpr uint64_t kMemBaseline = 96ull << 20;
+constexpr uint64_t kTlsSessionBytes = 64ull << 10;
+
+// The smallest memory.max on the way from this process's cgroup (cgroup v2) up to the root, else
+// the v1 memory controller's limit; 0 = unlimited / unknown. GPUMON_HTTP_MEMORY_BUDGET (bytes)
+// overrides.
+uint64_t memory_limit_bytes() {
+  if (const char* e = getenv("GPUMON_HTTP_MEMORY_BUDGET")) return strtoull(e, nullptr, 10);
+  auto num = [](const std::string& path) -> uint64_t {
+    std::string t;
+    if (!read_file(path, &t, 64)) return 0;
+    const std::string v(trim(t));
+    if (v.empty() || v == "max") return 0;
+    const uint64_t x = strtoull(v.c_str(), nullptr, 10);
+    return x >= (1ull << 60) ? 0 : x;  // v1 reports "unlimited" as a huge page-rounded number
+  };
+  std::string cg;
+  uint64_t best = 0;
+  if (read_file("/proc/self/cgroup", &cg, 4096))
+    for (const auto& line : split(cg, '\n')) {
+      if (starts_with(line, "0::")) {  // v2: walk from this cgroup to the mount's root
+        std::string path(trim(line.substr(3)));
+        while (true) {
+          const uint64_t v = num("/sys/fs/cgroup" + (path == "/" ? std::string() : path) + "/memory.max");
+          if (v && (!best || v < best)) best = v;
+          if (path.empty() || path == "/") break;
+          const size_t slash = path.rfind('/');
+          path = slash == 0 || slash == std::string::npos ? "/" : path.substr(0, slash);
+        }
+      }
+    }
+  if (!best) best = num("/sys/fs/cgroup/memory/memory.limit_in_bytes");
+  return best;
+}
 
 const char* status_text(int s) {
   switch (s) {
     case 200: return "OK";
     case 400: return "Bad Request";
     case 401: return "Unauthorized";
+    case 403: return "Forbidden";
     case 404: return "Not Found";
     case 405: return "Method Not Allowed";
     case 413: return "Payload Too Large";
@@ -89,6 +129,7 @@ struct Conn {
   uint32_t served = 0;  // requests answered on this connection (a scraper's keep-alive has > 0)
   void* ssl = nullptr;  // TLS session (HttpServer::set_tls), else plain
   bool hs = false;      // TLS handshake still in progress
+  bool client_cert = false;  // mutual TLS: the client's certificate verified (set after the handshake)
   // the last read stopped at the input cap: the session may hold decrypted bytes that no socket
   // event will announce (they left the socket already), so the loop reads again once there is room
   bool tls_more = false;
@@ -347,6 +388,17 @@ bool HttpServer::start(std::string* err) {
     const rlim_t usable = rl.rlim_cur > 2 * kFdReserve ? rl.rlim_cur - kFdReserve : rl.rlim_cur / 2;
     max_conns_ = std::clamp<size_t>(usable / static_cast<rlim_t>(std::max(1, nthreads_)), 8, kMaxConnsPerLoop);
   }
+  if (const uint64_t mem = memory_limit_bytes(); mem > 0) {
+    const uint64_t budget = mem > 2 * kMemBaseline ? mem - kMemBaseline : mem / 2;
+    const uint64_t per_conn = kMaxInput + 4096 + (tls_ ? kTlsSessionBytes : 0);
+    const size_t cap = std::max<size_t>(8, budget / per_conn / static_cast<uint64_t>(std::max(1, nthreads_)));
+    if (cap < max_conns_) {
+      GPUMON_LOG(LogLevel::kInfo, "http",
+                 "connection cap " + std::to_string(cap * std::max(1, nthreads_)) + " (memory limit " +
+                     std::to_string(mem >> 20) + " MiB)");
+      max_conns_ = cap;
+    }
+  }
   lfd_ = open_listener(addr_, &port_, &bound_, err);
   if (lfd_ < 0) return false;
   exclusive_ = true;
@@ -544,6 +596,7 @@ void HttpServer::run(Loop* L) {
     while (!c.writing && !c.closing) {
       HttpRequest req;
       long used = parse_request(c.in, &req);
+      req.client_cert = c.client_cert;
       if (used == 0) return true;
       HttpResponse resp;
       const int64_t t_req = mono_ns();  // service time = handler + response write
@@ -838,6 +891,7 @@ void HttpServer::run(Loop* L) {
           continue;
         }
         c.hs = false;
+        c.client_cert = tls_->mutual() && tls_->peer_verified(c.ssl);
         c.req_start_ns = 0;
         set_events(fd, EPOLLIN | EPOLLRDHUP);
         // the request may have come with the handshake's last flight: read it now

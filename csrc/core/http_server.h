@@ -31,6 +31,9 @@ struct HttpRequest {
   bool keep_alive = true;
   bool accept_gzip = false;
   std::string authorization;  // the Authorization header's value (http_auth_token_file)
+  // mutual TLS (tls_client_ca_file): the connection's client presented a certificate that
+  // verified. Handshakes without one succeed (the kubelet's probes); /metrics refuses them.
+  bool client_cert = false;
 };
 
 struct HttpResponse {

@@ -872,9 +872,17 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       Family f(o, "gpumon_http_tls_handshake_failures_total",
                "/metrics over HTTPS (tls_cert_file): connections whose TLS handshake failed or did not finish "
                "within the header timeout -- a plain-HTTP scraper, a scraper that does not trust the "
-               "certificate, or (mutual TLS) one without an accepted client certificate.",
+               "certificate, or (mutual TLS) one whose client certificate did not verify.",
                "counter");
       f.add(hl, static_cast<double>(s.http_tls_failures));
+    }
+    if (s.http_tls_client_cert_refused >= 0) {
+      Family f(o, "gpumon_http_tls_client_cert_refused_total",
+               "Mutual TLS (tls_client_ca_file): /metrics requests refused with 403 because the connection "
+               "presented no client certificate (the health endpoints answer such connections: the "
+               "kubelet's probes send none).",
+               "counter");
+      f.add(hl, static_cast<double>(s.http_tls_client_cert_refused));
     }
     if (s.http_tls_failures >= 0) {
       {

@@ -72,6 +72,7 @@ struct SelfStats {
   int64_t http_evicted = -1;         // connections closed to make room at the cap (-1: no server)
   int64_t http_max_conns = -1;       // connection cap over all HTTP loops (from RLIMIT_NOFILE)
   int64_t http_tls_failures = -1;    // /metrics over HTTPS: failed / timed-out handshakes (-1: plain HTTP)
+  int64_t http_tls_client_cert_refused = -1;  // mutual TLS: /metrics without a client certificate (-1: not mTLS)
   int64_t http_tls_not_after = 0;     // ... the serving certificate's expiry (unix s; 0 unknown)
   uint64_t http_tls_reloads_ok = 0, http_tls_reloads_failed = 0;  // ... certificate rotations picked up / refused
   int64_t http_auth_failures = -1;    // http_auth_token_file: /metrics requests refused (-1: no token)

@@ -111,9 +111,11 @@ const std::string* Snapshot::gzipped(bool compress_now) const {
   }
   if (st == 1) {
     // another thread (the tick thread's eager / predicted compression, or a concurrent scrape) is
-    // compressing this snapshot right now: wait for it (0.1-0.8 ms) rather than answer with the
-    // 5-10x larger identity body; give up after 20 ms
-    const int64_t until = mono_ns() + 20'000'000;
+    // compressing this snapshot right now: wait for it (0.1-0.8 ms for 1-8 GPUs) rather than answer
+    // with the 5-10x larger identity body -- but at most kGzipWaitNs: this runs on an HTTP loop
+    // (possibly at SCHED_FIFO), and every other connection of the loop waits with it (it
+    // was 20 ms). Past the budget the identity body goes out.
+    const int64_t until = mono_ns() + kGzipWaitNs;
     while ((st = gz_state_.load(std::memory_order_acquire)) == 1 && mono_ns() < until)
       std::this_thread::sleep_for(std::chrono::microseconds(20));
   }

@@ -28,6 +28,7 @@ struct Snapshot {
   // nullptr = serve the identity body (compression disabled, failed, or another thread is
   // compressing right now -- HTTP lets a server ignore Accept-Encoding).
   const std::string* gzipped(bool compress_now) const;
+  static constexpr int64_t kGzipWaitNs = 1'000'000;  // longest wait for another thread's compression
   // The tick thread's eager compression (does not count as a gzip request). false = not made
   // here: a scrape is compressing or has compressed it (or compression is off or failed).
   bool precompress() const;

@@ -76,6 +76,7 @@ struct SslApi {
   int (*SSL_shutdown)(void*) = nullptr;
   int (*SSL_get_error)(const void*, int) = nullptr;
   long (*SSL_get_verify_result)(const void*) = nullptr;
+  void* (*SSL_get0_peer_certificate)(const void*) = nullptr;
   // libcrypto
   int (*X509_VERIFY_PARAM_set1_ip_asc)(void*, const char*) = nullptr;
   const char* (*X509_verify_cert_error_string)(long) = nullptr;
@@ -160,6 +161,7 @@ void load_api() {
   sym(s, "SSL_shutdown", &a->SSL_shutdown, &missing);
   sym(s, "SSL_get_error", &a->SSL_get_error, &missing);
   sym(s, "SSL_get_verify_result", &a->SSL_get_verify_result, &missing);
+  sym(s, "SSL_get0_peer_certificate", &a->SSL_get0_peer_certificate, &missing);
   sym(c, "X509_VERIFY_PARAM_set1_ip_asc", &a->X509_VERIFY_PARAM_set1_ip_asc, &missing);
   sym(c, "X509_verify_cert_error_string", &a->X509_verify_cert_error_string, &missing);
   sym(c, "X509_STORE_get0_objects", &a->X509_STORE_get0_objects, &missing);
@@ -450,7 +452,12 @@ void* build_server_ctx(const SslApi* a, const std::string& cert_file, const std:
   if (!client_ca_file.empty()) {
     if (a->SSL_CTX_load_verify_locations(ctx, client_ca_file.c_str(), nullptr) != 1)
       return fail("tls: cannot load client CA " + client_ca_file + ": " + err_queue(a));
-    a->SSL_CTX_set_verify(ctx, ossl::kVerifyPeer | ossl::kVerifyFailIfNoPeerCert, nullptr);
+    // REQUEST a client certificate and verify one that is sent (a wrong CA still fails the
+    // handshake), but do not REQUIRE one: the kubelet's HTTPS probes present none, and /healthz /
+    // /readyz must answer them. /metrics itself needs a verified certificate (peer_verified(),
+    // checked per request in Exporter::handle_http: 403 without one). ADVICE r5: with
+    // FAIL_IF_NO_PEER_CERT every probe failed at the handshake and restarted the pod.
+    a->SSL_CTX_set_verify(ctx, ossl::kVerifyPeer, nullptr);
   }
   *not_after = 0;
   if (const void* x = a->SSL_CTX_get0_certificate(ctx)) {
@@ -535,6 +542,10 @@ void TlsServer::maybe_reload(int64_t now_ns) {
 
 TlsServer::~TlsServer() {
   if (ctx_) api_->SSL_CTX_free(ctx_);
+}
+
+bool TlsServer::peer_verified(void* ssl) const {
+  return ssl && api_->SSL_get0_peer_certificate(ssl) != nullptr && api_->SSL_get_verify_result(ssl) == ossl::kVerifyOk;
 }
 
 void* TlsServer::new_session(int fd) const {

@@ -119,6 +119,8 @@ class TlsServer {
   // > 0 bytes written; -1 = the socket is full (wait for EPOLLOUT); -2 = a TLS error
   long write(void* ssl, const char* p, size_t n) const;
   void notify_close(void* ssl) const;  // one non-blocking close_notify attempt
+  // Mutual TLS: the session's peer sent a certificate and it verified against the client CA.
+  bool peer_verified(void* ssl) const;
   void free_session(void* ssl) const;
 
  private:

@@ -440,6 +440,55 @@ def test_tls_overlay_serves_https_from_a_secret(core, tmp_path):
                     "-days", "1", "-keyout", str(d / "tls.key"), "-out", str(d / "tls.crt"), "-subj", "/CN=gpumon",
                     "-addext", "subjectAltName=DNS:gpumon"], check=True, capture_output=True, timeout=60)
     assert core.check_serve_tls(str(d / os.path.basename(cfg.tls_cert_file)), str(d / os.path.basename(cfg.tls_key_file))) == ""
+    # an annotation-driven Prometheus scrapes https too
+    ann = _json_patch(ds, ops)["spec"]["template"]["metadata"]["annotations"]
+    assert ann["prometheus.io/scheme"] == "https" and ann["prometheus.io/scrape"] == "true"
+
+
+def test_mutual_tls_overlay_keeps_the_https_probes_working(core, tmp_path):
+    """with the overlay's GPUMON_TLS_CLIENT_CA_FILE uncommented, the kubelet's
+    httpGet probes (HTTPS, no client certificate, no verification) must still get 200 from /healthz
+    and /readyz -- a handshake that required a client certificate failed every probe and restarted
+    the pod. /metrics still needs a certificate from the client CA (403 without one)."""
+    import http.client
+    import ssl
+    import subprocess
+
+    (k,) = _docs("deploy/k8s/overlays/tls/kustomization.yaml")
+    text = next(p for p in k["patches"] if p["target"]["kind"] == "DaemonSet")["patch"]
+    # the mutual-TLS lines as the overlay's comment tells the operator to uncomment them
+    lines = text.splitlines()
+    i = next(n for n, l in enumerate(lines) if "GPUMON_TLS_CLIENT_CA_FILE" in l)
+    for n in range(i - 2, i + 1):
+        lines[n] = lines[n].replace("# ", "", 1)
+    ops = yaml.safe_load("\n".join(lines))
+    ds = next(d for d in _docs("deploy/k8s/gpumon-daemonset.yaml") if d["kind"] == "DaemonSet")
+    c = _json_patch(ds, ops)["spec"]["template"]["spec"]["containers"][0]
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    assert env["GPUMON_TLS_CLIENT_CA_FILE"].endswith("client-ca.crt")
+    assert c["livenessProbe"]["httpGet"]["scheme"] == "HTTPS" and c["livenessProbe"]["httpGet"]["path"] == "/healthz"
+    files = {}
+    for name, cn in (("tls", "gpumon"), ("client-ca", "clients")):
+        subprocess.run(["openssl", "req", "-x509", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:prime256v1", "-nodes",
+                        "-days", "1", "-keyout", str(tmp_path / f"{name}.key"), "-out", str(tmp_path / f"{name}.crt"),
+                        "-subj", f"/CN={cn}"], check=True, capture_output=True, timeout=60)
+        files[name] = str(tmp_path / f"{name}.crt")
+    ex = core.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                        "http_threads": 1, "tls_cert_file": files["tls"], "tls_key_file": str(tmp_path / "tls.key"),
+                        "tls_client_ca_file": files["client-ca"]})
+    assert ex.start() == ""
+    try:
+        probe = ssl.create_default_context()
+        probe.check_hostname = False
+        probe.verify_mode = ssl.CERT_NONE  # the kubelet does not verify the serving certificate
+        for path, want in ((c["livenessProbe"]["httpGet"]["path"], 200), (c["readinessProbe"]["httpGet"]["path"], 200),
+                           ("/metrics", 403)):
+            conn = http.client.HTTPSConnection("127.0.0.1", ex.port, context=probe, timeout=5)
+            conn.request("GET", path)
+            assert conn.getresponse().status == want, path
+            conn.close()
+    finally:
+        ex.stop()
 
 
 def test_serve_imports_no_oracle_or_grpc():

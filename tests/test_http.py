@@ -863,3 +863,29 @@ def test_periodic_gzip_scraper_gets_precompressed_snapshots(mock_exporter):
     # (a loaded CI host jitters the scrapes: some land a tick off the prediction and compress lazily)
     assert predicted >= 4 and lazy < 12, (predicted, lazy)
     assert predicted + lazy + (s1["gzip_eager"] - s0["gzip_eager"]) <= ticks // 2  # far from one per tick
+
+
+
+@pytest.mark.parametrize("tls", [False, True])
+def test_connection_cap_fits_the_memory_limit(core, monkeypatch, tmp_path, tls):
+    """with a 256 MiB memory limit (the DaemonSet's, the systemd unit's MemoryMax) and a
+    high fd limit, the cap must be low enough that every admitted connection buffering a maximal
+    request (~88 KiB, +64 KiB for a TLS session) fits in the limit less 96 MiB for the rest."""
+    import subprocess
+
+    monkeypatch.setenv("GPUMON_HTTP_MEMORY_BUDGET", str(256 << 20))
+    cfg = {"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0, "http_threads": 2}
+    if tls:
+        subprocess.run(["openssl", "req", "-x509", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:prime256v1",
+                        "-nodes", "-days", "1", "-keyout", str(tmp_path / "k"), "-out", str(tmp_path / "c"),
+                        "-subj", "/CN=x"], check=True, capture_output=True, timeout=60)
+        cfg.update(tls_cert_file=str(tmp_path / "c"), tls_key_file=str(tmp_path / "k"))
+    ex = core.Exporter(cfg)
+    assert ex.start() == ""
+    try:
+        cap = ex.self_stats()["http_max_conns"]
+        per = (16 + 64 + 4) * 1024 + 4096 + (64 * 1024 if tls else 0)
+        assert cap * per <= (256 - 96) << 20, cap
+        assert cap >= (1000 if tls else 1800), cap  # and not needlessly low
+    finally:
+        ex.stop()

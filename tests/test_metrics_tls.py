@@ -156,20 +156,30 @@ def test_failed_handshakes_are_counted_and_closed(core, pki, case, monkeypatch):
 
 
 def test_mutual_tls_requires_a_client_certificate_from_the_ca(core, pki):
+    """Mutual TLS: a certificate from another CA fails the handshake; a connection WITHOUT a
+    certificate is accepted (the kubelet's HTTPS probes send none: ADVICE r5, every probe failed at
+    the handshake and restarted the pod), answers /healthz and /readyz, and gets 403 on /metrics."""
     ex = core.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
                         "http_threads": 1, "tls_cert_file": pki["server"], "tls_key_file": pki["server_key"],
                         "tls_client_ca_file": pki["clientca"]})
     ex.start()
     try:
         assert _get(ex.port, _ctx(pki, "scraper", "scraper_key"))[0] == 200
-        for cert in (None, "stranger"):
-            # TLS 1.3: the server's refusal may only surface on the first read, as an alert or a reset
-            with pytest.raises((ssl.SSLError, ConnectionResetError, http.client.RemoteDisconnected)):
-                _get(ex.port, _ctx(pki, cert, f"{cert}_key") if cert else _ctx(pki))
+        # TLS 1.3: the server's refusal may only surface on the first read, as an alert or a reset
+        with pytest.raises((ssl.SSLError, ConnectionResetError, http.client.RemoteDisconnected)):
+            _get(ex.port, _ctx(pki, "stranger", "stranger_key"))
         deadline = time.time() + 5
-        while ex.self_stats()["http_tls_failures"] < 2 and time.time() < deadline:
+        while ex.self_stats()["http_tls_failures"] < 1 and time.time() < deadline:
             time.sleep(0.05)
-        assert ex.self_stats()["http_tls_failures"] == 2
+        assert ex.self_stats()["http_tls_failures"] == 1
+        # no client certificate: the probes' view
+        for path, want in (("/healthz", 200), ("/readyz", 200), ("/metrics", 403)):
+            assert _get(ex.port, _ctx(pki), path)[0] == want, path
+        assert ex.self_stats()["http_tls_failures"] == 1  # the probe handshakes all succeeded
+        assert ex.self_stats()["http_tls_client_cert_refused"] == 1
+        ex.tick()  # the snapshot that carries the counter
+        fam = promtext.parse(_get(ex.port, _ctx(pki, "scraper", "scraper_key"))[2].decode())
+        assert promtext.one(fam, "gpumon_http_tls_client_cert_refused_total") == 1
     finally:
         ex.stop()
 
