@@ -754,13 +754,15 @@ PYBIND11_MODULE(_core, m) {
       [](const std::string& body, int threads, bool during_precompress) {
         // `threads` scrapes ask one fresh snapshot for gzip at the same instant -- or, with
         // during_precompress, while the tick thread's precompress() of it is running. Exactly one
-        // thread compresses; the others wait for it. Returns (the gzip body every thread got, or
-        // None if any got none; distinct buffers handed out, 1 = compressed once; scrapes that
-        // started while the compression was in flight).
+        // thread compresses; the others wait for it, at most Snapshot::kGzipWaitNs. Returns (the
+        // gzip body every thread got, or None if any got none; distinct buffers handed out, 1 =
+        // compressed once; scrapes that started while the compression was in flight; the longest
+        // any scrape thread spent in gzipped(), seconds -- for a waiter, how long its loop stalled).
         auto snap = std::make_shared<gpumon::Snapshot>();
         snap->body = body;
         snap->gzip = true;
         std::vector<const std::string*> got(std::max(threads, 1), nullptr);
+        std::vector<double> spent(got.size(), 0.0);
         std::atomic<int> mid{0};
         {
           py::gil_scoped_release nogil;
@@ -775,8 +777,11 @@ PYBIND11_MODULE(_core, m) {
             th.emplace_back([&, i] {
               ready.fetch_add(1);
               while (ready.load() < static_cast<int>(got.size())) std::this_thread::yield();
-              if (snap->compressing()) mid.fetch_add(1);
+              const bool waiter = snap->compressing();
+              if (waiter) mid.fetch_add(1);
+              const int64_t t0 = gpumon::mono_ns();
               got[i] = snap->gzipped(true);
+              if (waiter) spent[i] = (gpumon::mono_ns() - t0) * 1e-9;
             });
           for (auto& t : th) t.join();
           if (pre.joinable()) pre.join();
@@ -784,7 +789,8 @@ PYBIND11_MODULE(_core, m) {
         std::set<const std::string*> distinct(got.begin(), got.end());
         const bool all = std::find(got.begin(), got.end(), nullptr) == got.end();
         return py::make_tuple(all ? py::object(py::bytes(*got[0])) : py::object(py::none()),
-                              static_cast<int>(distinct.size()), mid.load());
+                              static_cast<int>(distinct.size()), mid.load(),
+                              *std::max_element(spent.begin(), spent.end()));
       },
       py::arg("body"), py::arg("threads") = 8, py::arg("during_precompress") = false);
   m.def(

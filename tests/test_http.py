@@ -72,19 +72,36 @@ def test_gzip_disabled(mock_exporter):
 @pytest.mark.parametrize("during_precompress", [False, True])
 def test_concurrent_gzip_scrapes_compress_a_snapshot_once(core, during_precompress):
     """Scrapes that ask a fresh snapshot for gzip at the same instant, or while the tick thread is
-    precompressing it: one thread compresses, the others wait for it and get the same buffer. None
-    falls back to the identity body (a scrape that lost the claim to a concurrent compression used
-    to) and none compresses again. The body, 640 KB, takes ~3 ms to compress: longer than the
-    threads' start, inside the waiters' 20 ms limit. A loaded CI host can stretch one compression
-    past that limit (then a waiter rightly serves identity), so the race gets 3 attempts; the old
-    lost-claim bug failed every attempt."""
-    body = "".join(f'node_gpu_gpu_util{{gpu_id="{i % 8}",host="n{i}"}} {i * 0.37:.3f}\n' for i in range(12000))
-    results = [core.snapshot_gzip_race(body, threads=8, during_precompress=during_precompress) for _ in range(3)]
-    ok = [(gz, mid) for gz, distinct, mid in results if gz is not None and distinct == 1]
-    assert ok, [(gz is not None, distinct, mid) for gz, distinct, mid in results]
-    assert gzip.decompress(ok[0][0]).decode() == body
+    precompressing it: one thread compresses, the others wait for it -- at most 1 ms
+    (Snapshot::kGzipWaitNs, ADVICE r5: the wait runs on an HTTP loop) -- and get the same buffer.
+    None compresses again; a scrape that lost the claim to a concurrent compression no longer falls
+    back to identity while the winner finishes within the wait. A loaded CI host can stretch one
+    compression past the wait (then a waiter rightly serves identity), so the race gets 5 attempts;
+    the old lost-claim bug failed every attempt."""
+    lines = 12000 if during_precompress else 2400  # long enough for scrapes to arrive mid-compression
+    body = "".join(f'node_gpu_gpu_util{{gpu_id="{i % 8}",host="n{i}"}} {i * 0.37:.3f}\n' for i in range(lines))
+    results = [core.snapshot_gzip_race(body, threads=8, during_precompress=during_precompress) for _ in range(5)]
+    # whoever got a gzip body got THE one (compressed once), and no waiter stalled past the budget
+    assert all(distinct == 1 for gz, distinct, _, _ in results if gz is not None), results
+    assert all(longest < 0.01 for *_, longest in results), [r[3] for r in results]
     if during_precompress:
-        assert any(mid >= 1 for _, mid in ok)  # the scrapes did arrive while it ran
+        assert any(mid >= 1 for _, _, mid, _ in results)  # the scrapes did arrive while it ran
+    else:
+        ok = [gz for gz, distinct, _, _ in results if gz is not None and distinct == 1]
+        assert ok, [(gz is not None, distinct, mid) for gz, distinct, mid, _ in results]
+        assert gzip.decompress(ok[0]).decode() == body
+
+
+def test_a_long_compression_does_not_stall_the_loop(core):
+    """a scrape that finds another thread compressing its snapshot waited up to 20 ms on
+    the HTTP loop, stalling every other connection of that loop. It now waits at most 1 ms
+    (Snapshot::kGzipWaitNs) and answers with the identity body: a 6 MB body (tens of ms to compress)
+    holds no waiter past a few ms."""
+    body = "".join(f'node_gpu_gpu_util{{gpu_id="{i % 8}",host="n{i}"}} {i * 0.37:.3f}\n' for i in range(110000))
+    gz, distinct, mid, longest = core.snapshot_gzip_race(body, threads=4, during_precompress=True)
+    assert mid >= 1, mid  # the scrapes did arrive while the compression ran
+    assert gz is None  # the waiters gave up and served identity
+    assert longest < 0.008, longest
 
 
 def test_head_and_404_and_index(mock_exporter):

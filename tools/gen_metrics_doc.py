@@ -169,6 +169,14 @@ def collect():
             ex.tick()
             add(_families(ex), "tls_cert_file")
             ex.stop()
+            # mutual TLS (tls_client_ca_file): the client-certificate refusal counter
+            ex = c.Exporter({"backend": "mock:gpus=1", "listen_addr": "127.0.0.1", "port": 0, "interval_s": 0,
+                             "host": "node", "tls_cert_file": f"{d}/c.pem", "tls_key_file": f"{d}/k.pem",
+                             "tls_client_ca_file": f"{d}/c.pem"})
+            ex.start()
+            ex.tick()
+            add(_families(ex), "tls_client_ca_file")
+            ex.stop()
     # /metrics behind a bearer token (http_auth_token_file)
     with tempfile.TemporaryDirectory() as d:
         with open(f"{d}/token", "w") as f:
