@@ -814,10 +814,16 @@ def test_gzip_is_lazy_until_scrapes_keep_asking_for_it(mock_exporter):
 
     ex = mock_exporter(backend="mock:gpus=2", interval_s=0)
 
+    identity = []
+
     def gz_scrape():
         req = urllib.request.Request(f"http://127.0.0.1:{ex.port}/metrics", headers={"Accept-Encoding": "gzip"})
         with urllib.request.urlopen(req, timeout=5) as r:
-            assert r.headers.get("Content-Encoding") == "gzip"
+            if r.headers.get("Content-Encoding") != "gzip":
+                # a scrape that found the tick thread still compressing after 1 ms (a loaded host)
+                # gets the identity body instead of stalling the loop (Snapshot::kGzipWaitNs)
+                identity.append(1)
+                return r.read()
             return gzip.decompress(r.read())
 
     for _ in range(10):
@@ -858,10 +864,16 @@ def test_periodic_gzip_scraper_gets_precompressed_snapshots(mock_exporter):
 
     ex = mock_exporter(backend="mock:gpus=4", interval_s=0.05)
 
+    identity = []
+
     def gz_scrape():
         req = urllib.request.Request(f"http://127.0.0.1:{ex.port}/metrics", headers={"Accept-Encoding": "gzip"})
         with urllib.request.urlopen(req, timeout=5) as r:
-            assert r.headers.get("Content-Encoding") == "gzip"
+            if r.headers.get("Content-Encoding") != "gzip":
+                # a scrape that found the tick thread still compressing after 1 ms (a loaded host)
+                # gets the identity body instead of stalling the loop (Snapshot::kGzipWaitNs)
+                identity.append(1)
+                return r.read()
             return gzip.decompress(r.read())
 
     t0 = time.monotonic()
@@ -880,6 +892,7 @@ def test_periodic_gzip_scraper_gets_precompressed_snapshots(mock_exporter):
     # (a loaded CI host jitters the scrapes: some land a tick off the prediction and compress lazily)
     assert predicted >= 4 and lazy < 12, (predicted, lazy)
     assert predicted + lazy + (s1["gzip_eager"] - s0["gzip_eager"]) <= ticks // 2  # far from one per tick
+    assert len(identity) <= 3, len(identity)
 
 
 
