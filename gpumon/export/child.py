@@ -14,6 +14,7 @@ HIP): the child is then forked from a process with no GPU state at all.
 
 from __future__ import annotations
 
+import atexit
 import http.client
 import json
 import os
@@ -102,6 +103,9 @@ class ChildExporter:
                                              env=env, cwd=self.workdir)
             try:
                 self._wait_ready(timeout_s)
+                # a caller that dies on an exception (bench.py's SystemExit paths) must not leave
+                # the exporter running: stop it at interpreter exit too (stop() is idempotent)
+                atexit.register(self.stop)
                 return self
             except ChildExporterError as e:
                 last = str(e)
