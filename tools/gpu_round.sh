@@ -4,6 +4,6 @@
 set -e
 out=gpurun_out/${1:-round}
 mkdir -p "$out"
-timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > "$out/pytest_gpu.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -rP --timeout 120 --timeout-method thread > "$out/pytest_gpu.log" 2>&1
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
 timeout -k 10 180 python -u bench.py --out "$out/bench.json" > "$out/bench.log" 2>&1
