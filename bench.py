@@ -355,6 +355,9 @@ def main() -> int:
     ap.add_argument("--set", action="append", default=[], metavar="KEY=VALUE",
                     help="DIAGNOSTIC: extra exporter config keys for the timed exporter (gpumon.config.Config), "
                          "e.g. --set processes=false --set gzip=false; listed in the line as exporter_overrides")
+    ap.add_argument("--ranks-per-gpu", type=int, default=1,
+                    help="REHEARSAL on a box with fewer GPUs: K torchrun ranks share each GPU (gloo process group, "
+                         "no xGMI traffic); the line's data and parallelism say so")
     ap.add_argument("--exporter", default="child", choices=["child", "inprocess"],
                     help="child: bin/gpumon-exporter as its own process (the shipped binary, default); "
                          "inprocess: the same core through gpumon._core in this process (A/B)")
@@ -368,7 +371,10 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    n = max(1, args.gpus if world == 1 else world)
+    rpg = max(1, args.ranks_per_gpu)
+    if world > 1 and world % rpg:
+        raise SystemExit(f"--ranks-per-gpu {rpg} does not divide the world size {world}")
+    n = max(1, args.gpus if world == 1 else world // rpg)
 
     try:
         import torch
@@ -378,7 +384,7 @@ def main() -> int:
             raise SystemExit("bench.py under torchrun needs PyTorch (torch.distributed over RCCL)")
 
     # torchrun: this rank's GPU; one process: all N GPUs (the node-level exporter watches them all)
-    my_devs = [local_rank] if world > 1 else list(range(n))
+    my_devs = [local_rank // rpg] if world > 1 else list(range(n))
 
     # ---------------------------------------------------------------- rank 0: the exporter child
     # Started BEFORE this process's first HIP call (torch.cuda.is_available() initialises HIP): the
@@ -427,9 +433,14 @@ def main() -> int:
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29517"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)  # --dist without a launcher
         if has_gpu:
-            torch.cuda.set_device(local_rank)
-        dist.init_process_group(backend="nccl" if has_gpu else "gloo")
-    device = (torch.device(f"cuda:{local_rank}") if has_gpu else torch.device("cpu")) if torch is not None else None
+            torch.cuda.set_device(my_devs[0])
+        # RCCL takes one rank per GPU; ranks sharing a GPU (the rehearsal) reduce over gloo
+        dist.init_process_group(backend="nccl" if has_gpu and rpg == 1 else "gloo")
+    device = (torch.device(f"cuda:{my_devs[0]}") if has_gpu else torch.device("cpu")) if torch is not None else None
+    # where this rank's small reductions (timings, rates) live: the GPU under RCCL, else the host
+    red_device = None
+    if torch is not None:
+        red_device = device if dist is not None and dist.get_backend() == "nccl" else torch.device("cpu")
 
     # HIP ordinal -> PCI BDF of every GPU the job loads, gathered to rank 0: the exporter samples
     # exactly those GPUs, named by BDF, since its gpu_id (libamd_smi hip_id) is node-wide and a
@@ -447,7 +458,7 @@ def main() -> int:
     # pid (the tenants the exporter attributes)
     ranks_seen = [{"rank": rank, "world_size": dist.get_world_size() if dist is not None else 1,
                    "backend": str(dist.get_backend()) if dist is not None else None, "pid": os.getpid(),
-                   "local_rank": local_rank}]
+                   "local_rank": local_rank, "device": my_devs[0] if world > 1 else None}]
     if dist is not None:
         allr = [None] * world
         dist.all_gather_object(allr, ranks_seen[0])
@@ -559,7 +570,7 @@ def main() -> int:
             raise SystemExit(f"bench needs GPUs {my_devs}, HIP sees {hip().device_count()}")
         loads = [SyntheticLoad(dev=d, kind=args.load, hbm_bytes=1 << 30).start() for d in my_devs]
 
-    xgmi_on = n > 1 and not args.no_xgmi
+    xgmi_on = n > 1 and rpg == 1 and not args.no_xgmi
     ar_buf = None
     if dist is not None and xgmi_on and args.allreduce_mb > 0:
         # zeros: repeated in-place sums stay finite (ones would reach inf after ~40 steps on 8 ranks)
@@ -586,12 +597,12 @@ def main() -> int:
                 dist.all_reduce(ar_buf)
             e1.record()
             e1.synchronize()
-            t = torch.tensor([e0.elapsed_time(e1) / 5], dtype=torch.float64, device=device)
+            t = torch.tensor([e0.elapsed_time(e1) / 5], dtype=torch.float64, device=red_device)
         else:
             t0 = time.perf_counter()
             for _ in range(5):
                 dist.all_reduce(ar_buf)
-            t = torch.tensor([(time.perf_counter() - t0) / 5 * 1e3], dtype=torch.float64, device=device)
+            t = torch.tensor([(time.perf_counter() - t0) / 5 * 1e3], dtype=torch.float64, device=red_device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)  # every rank derives the same count
         ar_cal_ms = float(t.item())
         if args.xgmi_duty > 0 and ar_cal_ms > 0:
@@ -653,7 +664,7 @@ def main() -> int:
     c1 = [c.stats() for c in copiers]
     l1 = [ld.stats() for ld in loads]
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -666,7 +677,7 @@ def main() -> int:
         r = SyntheticLoad.rates(a, b)
         lrates[d] = [r["tflops"], r["tbps"], r["busy"]]
     if dist is not None:
-        t = torch.tensor(lrates, dtype=torch.float64, device=device)
+        t = torch.tensor(lrates, dtype=torch.float64, device=red_device)
         dist.all_reduce(t)
         lrates = t.cpu().tolist()
 
@@ -676,7 +687,8 @@ def main() -> int:
     if ar_buf is not None:
         nbytes = ar_buf.numel() * ar_buf.element_size()
         ar_ms = [a.elapsed_time(b) / reps for a, b in ar_events] if ar_events else []
-        t = torch.tensor([sum(ar_ms) / len(ar_ms) if ar_ms else float("nan")], dtype=torch.float64, device=device)
+        t = torch.tensor([sum(ar_ms) / len(ar_ms) if ar_ms else float("nan")], dtype=torch.float64,
+                         device=red_device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ar_mean_s = float(t.item()) * 1e-3
         per_gpu = 2 * (n - 1) / n * nbytes * reps * args.steps / elapsed  # B/s out of (and into) every GPU
@@ -766,7 +778,7 @@ def main() -> int:
         # carry pids this process cannot see, and the tenants are checked by count instead -- one
         # workload row per loaded GPU per rank on it, none of them the exporter's
         same_ns = bool(set(row_pids) & set(tenant_pids))
-        want_rows = {r["index"]: sum(1 for x in ranks_seen if world == 1 or x["local_rank"] == r["hip_ordinal"])
+        want_rows = {r["index"]: sum(1 for x in ranks_seen if world == 1 or x["device"] == r["hip_ordinal"])
                      for r in dev_rows}
         got_rows = {r["index"]: sum(1 for x in rows if not x["idle"] and x["dev"] == r["index"]) for r in dev_rows}
         exporter_info.update(
@@ -798,7 +810,9 @@ def main() -> int:
             "samples_total": samples,
             "stale_samples": stale,
             "dtype": "bf16",
-            "data": ("synthetic" if backend in ("amdsmi", "rocm_smi") else
+            "data": (f"synthetic (REHEARSAL: {world} ranks share {n} GPU(s), gloo process group, no xGMI traffic)"
+                     if rpg > 1 and has_gpu else
+                     "synthetic" if backend in ("amdsmi", "rocm_smi") else
                      f"synthetic (REHEARSAL: {n} physical GPU(s) each sampled {args.replicate}x)"
                      if backend.startswith("amdsmi:replicate") else "synthetic (mock backend: no GPU visible)"),
             "exporter": exporter_info.get("binary") or "in-process (gpumon._core)",
@@ -814,7 +828,8 @@ def main() -> int:
                 "global_batch": n,
                 "seq_len": None,
                 "parallelism": f"node-local exporter over {n} GPU(s); "
-                               + ("one rank per GPU" if world > 1 else "one process loading every GPU")
+                               + ((f"{rpg} ranks per GPU (rehearsal)" if rpg > 1 else "one rank per GPU")
+                                  if world > 1 else "one process loading every GPU")
                                + (f", {'RCCL' if has_gpu else 'gloo'} all-reduce x{reps} per step"
                                   if ar_buf is not None else "")
                                + (", peer-copy xGMI ring" if copiers else ""),

@@ -224,3 +224,33 @@ def test_post_measurement_extras_are_time_bounded():
     assert r == {"error": "timed out after 0.3 s"} and time.monotonic() - t0 < 2
     assert bench._bounded(lambda: 1 / 0, 5) == {"error": "ZeroDivisionError: division by zero"}
     assert bench._bounded(lambda x: {"ok": x}, 5, 7) == {"ok": 7}
+
+
+@pytest.mark.slow
+def test_ranks_sharing_a_gpu_rehearsal():
+    """--ranks-per-gpu K: the torchrun path with K ranks on each GPU (a 1-GPU box rehearsing the
+    multi-rank record: every rank's tenant row on the shared GPU, the world size each rank saw).
+    The process group is gloo (RCCL takes one rank per GPU) and the line says it is a rehearsal."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(28600 + os.getpid() % 300),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "2", "--ranks-per-gpu", "2", "--steps", "3",
+                        "--warmup", "1", "--interval", "0.1", "--idle-s", "0.5", "--capacity-s", "0"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (d,) = _json_lines(r.stdout)
+    _check(d, 1, 3, 1)
+    _check_exporter(d, 2)
+    assert d["sampled_devices"] == 1 and "2 ranks per GPU (rehearsal)" in d["config"]["parallelism"]
+    assert d["xgmi"] is None and [x["device"] for x in sorted(d["ranks"], key=lambda x: x["rank"])] == [0, 0]
+    assert all(x["backend"] == "gloo" for x in d["ranks"])
+    assert d["value"] == pytest.approx(1 / 0.1, rel=0.2)
+
+
+def test_ranks_per_gpu_must_divide_the_world():
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--ranks-per-gpu", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode != 0 and "does not divide the world size 3" in r.stderr
