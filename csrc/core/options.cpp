@@ -665,8 +665,19 @@ ParseStatus options_parse(NativeOptions* o, const std::vector<std::string>& args
     if (starts_with(*p, "GPUMON_CONFIG=")) config = *p + strlen("GPUMON_CONFIG=");
   bool compat = false;
   for (size_t i = 0; i < args.size(); ++i) {
-    if (args[i] == "--config" && i + 1 < args.size()) config = args[i + 1];
-    else if (starts_with(args[i], "--config=")) config = args[i].substr(9);
+    if (args[i] == "--config") {
+      if (i + 1 >= args.size()) {
+        *err = "--config: missing value";
+        return ParseStatus::kBadFlag;
+      }
+      config = args[++i];
+    } else if (starts_with(args[i], "--config=")) {
+      config = args[i].substr(9);
+      if (config.empty()) {
+        *err = "--config: missing value";
+        return ParseStatus::kBadFlag;
+      }
+    }
     else if (args[i] == "--compat") compat = true;
   }
   if (!config.empty()) {

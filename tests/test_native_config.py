@@ -143,6 +143,8 @@ def test_both_entry_points_take_each_others_flags(flags):
     (["--control-plane", "maybe"], 2, "--control-plane: native or off, not 'maybe'"),
     (["--interval", "fast"], 2, "interval"),
     (["--listen", "[::1"], 2, "listen"),
+    (["--config"], 2, "--config: missing value"),
+    (["--config="], 2, "--config: missing value"),
 ])
 def test_native_binary_refuses_bad_command_lines(args, rc, want):
     r = subprocess.run([BIN, *args], capture_output=True, text=True, timeout=30, env=CLEAN_ENV)
