@@ -675,7 +675,9 @@ def main() -> int:
         from gpumon.ops.load import SyntheticLoad
 
         r = SyntheticLoad.rates(a, b)
-        lrates[d] = [r["tflops"], r["tbps"], r["busy"]]
+        # ranks sharing a GPU: the work over wall time adds up to the GPU's; rates over each
+        # process's own kernel time do not (its MFMA batches overlap another's HBM batches)
+        lrates[d] = [r["tflops_wall"], r["tbps_wall"], r["busy"]] if rpg > 1 else [r["tflops"], r["tbps"], r["busy"]]
     if dist is not None:
         t = torch.tensor(lrates, dtype=torch.float64, device=red_device)
         dist.all_reduce(t)
@@ -884,6 +886,8 @@ def main() -> int:
                                 for k, v in s1.get("backend_calls", {}).items()},
             "backend": backend,
             "load": args.load if has_gpu else "none",
+            "load_rates": ("work over wall time, summed over the ranks sharing each GPU" if rpg > 1 else
+                           "TFLOP/s over the MFMA batches' GPU time, TB/s over the HBM batches' GPU time"),
             "load_per_gpu": [{"gpu": d, "gpu_id": gid.get(d), "tflops": round(r[0], 1), "tbps": round(r[1], 3),
                               "busy": round(r[2], 3)}
                              for d, r in enumerate(lrates)] if has_gpu and loads else None,

@@ -63,7 +63,9 @@ class SyntheticLoad:
         """The load's event-timed rates between two ``stats()`` snapshots: TFLOP/s over the MFMA
         batches' GPU time, TB/s over the HBM batches' GPU time (each counts only while its own kernel
         kind ran, so a mixed load's phases are not averaged in), and ``busy`` = GPU time / wall time
-        (the duty the GPU saw)."""
+        (the duty the GPU saw). ``tflops_wall`` / ``tbps_wall``: the same work over wall time, which
+        adds up across processes sharing one GPU (the kernel-time rates do not: one process's MFMA
+        kernels run while another's HBM kernels do)."""
         wall = b["wall_s"] - a["wall_s"]
         if "h2d_bytes" in b:  # pcie: link bytes over wall time, per direction
             return {"tflops": 0.0, "tbps": 0.0, "busy": (b["busy_s"] - a["busy_s"]) / wall if wall > 0 else 0.0,
@@ -72,7 +74,9 @@ class SyntheticLoad:
         dm, dh = b["mfma_s"] - a["mfma_s"], b["hbm_s"] - a["hbm_s"]
         return {"tflops": (b["flops"] - a["flops"]) / dm / 1e12 if dm > 0 else 0.0,
                 "tbps": (b["bytes"] - a["bytes"]) / dh / 1e12 if dh > 0 else 0.0,
-                "busy": (b["busy_s"] - a["busy_s"]) / wall if wall > 0 else 0.0}
+                "busy": (b["busy_s"] - a["busy_s"]) / wall if wall > 0 else 0.0,
+                "tflops_wall": (b["flops"] - a["flops"]) / wall / 1e12 if wall > 0 else 0.0,
+                "tbps_wall": (b["bytes"] - a["bytes"]) / wall / 1e12 if wall > 0 else 0.0}
 
     def start(self) -> "SyntheticLoad":
         self._g.start()

@@ -245,7 +245,7 @@ def test_ranks_sharing_a_gpu_rehearsal():
     _check_exporter(d, 2)
     assert d["sampled_devices"] == 1 and "2 ranks per GPU (rehearsal)" in d["config"]["parallelism"]
     assert d["xgmi"] is None and [x["device"] for x in sorted(d["ranks"], key=lambda x: x["rank"])] == [0, 0]
-    assert all(x["backend"] == "gloo" for x in d["ranks"])
+    assert all(x["backend"] == "gloo" for x in d["ranks"]) and "wall time" in d["load_rates"]
     assert d["value"] == pytest.approx(1 / 0.1, rel=0.2)
 
 

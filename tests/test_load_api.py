@@ -19,4 +19,6 @@ def test_rates_use_each_kinds_own_gpu_time():
     b = {"flops": 1.8e15, "bytes": 5.4e12, "mfma_s": 1.9, "hbm_s": 1.9, "busy_s": 3.8, "wall_s": 4.0}
     r = SyntheticLoad.rates(a, b)
     assert r["tflops"] == pytest.approx(2000.0) and r["tbps"] == pytest.approx(6.0) and r["busy"] == pytest.approx(0.9)
-    assert SyntheticLoad.rates(a, a) == {"tflops": 0.0, "tbps": 0.0, "busy": 0.0}
+    # over wall time (what adds up across processes sharing a GPU): 1.8e15 / 2 s, 5.4e12 / 2 s
+    assert r["tflops_wall"] == pytest.approx(900.0) and r["tbps_wall"] == pytest.approx(2.7)
+    assert SyntheticLoad.rates(a, a) == {"tflops": 0.0, "tbps": 0.0, "busy": 0.0, "tflops_wall": 0.0, "tbps_wall": 0.0}
