@@ -272,6 +272,9 @@ class InProcessExporter:
     def pod_rows(self):
         return self.ex.pod_rows()
 
+    def procs(self):
+        return self.ex.debug_view("/debug/procs")
+
     def metrics(self):
         return self.mon.metrics()
 
@@ -755,6 +758,13 @@ def main() -> int:
             per_gpu_rows.append({"gpu": i, "gpu_id": g, "rows": len(wr), "pids": sorted(r["pid"] for r in wr)[:8],
                                  "idle_rows": sum(1 for r in rows if r["idle"] and r["dev"] == i),
                                  "active_processes": active.get(g)})
+        # the contexts behind hidden_contexts / hidden_peer_contexts, by pid: an empty one holds no
+        # VRAM (a runtime that only opened the GPU), anything else is a peer context (or not opted in)
+        hidden_detail = [{"gpu": c["dev"], "pid": c["pid"], "queues": c["queues"],
+                          "vram_mib": round(c["vram_bytes"] / 2 ** 20, 1) if c["vram_bytes"] is not None else None,
+                          "why": "peer or not opted in" if (c["vram_bytes"] or 0) > 0 or (c["mem_bytes"] or 0) > 0
+                          else "empty"}
+                         for c in ex.procs() if not c["row"]][:16]
         rows_per_user = {}
         for r in rows:
             rows_per_user[r["user_name"]] = rows_per_user.get(r["user_name"], 0) + 1
@@ -904,6 +914,7 @@ def main() -> int:
             "rows_per_user": rows_per_user,
             "hidden_contexts": s1.get("hidden_contexts"),
             "hidden_peer_contexts": s1.get("hidden_peer_contexts"),
+            "hidden_context_detail": hidden_detail,
             "xgmi": xgmi,
             "xgmi_slot_map": slot_map or None,
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,

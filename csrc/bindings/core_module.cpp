@@ -1073,6 +1073,18 @@ PYBIND11_MODULE(_core, m) {
            })
       .def_property_readonly("port", &Exporter::port)
       .def_property_readonly("debug_port", &Exporter::debug_port)
+      .def(
+          "debug_view",
+          [](Exporter& e, const std::string& path) {
+            std::string body;
+            {
+              py::gil_scoped_release nogil;  // /debug/wait blocks until a tick
+              body = e.debug_view(path);
+            }
+            if (body.empty()) throw py::key_error("no introspection view " + path);
+            return py::module_::import("json").attr("loads")(body);
+          },
+          py::arg("path"), "an introspection view (/debug/state, /debug/procs, ...) as parsed JSON")
       .def_property_readonly("seq", &Exporter::seq)
       .def("healthy", &Exporter::healthy)
       .def("ready", &Exporter::ready)

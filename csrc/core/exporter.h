@@ -231,6 +231,9 @@ class Exporter {
   // GPU indices a Docker container holds: /dev/dri/renderD<N> / card<N> device mappings, all of
   // /dev/dri, or AMD_VISIBLE_DEVICES (indices, UUIDs, BDFs or "all") in its environment.
   static std::vector<int> docker_container_gpus(const DockerInspect& in, const std::vector<DeviceStatic>& st);
+  // One introspection view ("/debug/procs", "/debug/ticks?since=3", ...) rendered in-process, as
+  // the debug_listen server would answer it; "" for an unknown path (exporter_debug.cpp).
+  std::string debug_view(const std::string& path_and_query);
 
  private:
   bool ensure_backend();

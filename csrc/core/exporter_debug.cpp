@@ -9,6 +9,8 @@
 //                                       numbered >= N (the histogram's ring, exporter.h)
 //   GET /debug/samples                  the last tick's per-device fields and interval rates
 //   GET /debug/rows                     the last tick's pod_gpu rows
+//   GET /debug/procs                    every GPU context of the last tick's process lists and
+//                                       whether it became a row (the hidden ones by pid)
 //
 // What these are for: a bench or test that runs bin/gpumon-exporter as its own process (the
 // DaemonSet's ENTRYPOINT) reads the same exact numbers the in-process bindings give
@@ -214,6 +216,29 @@ void Exporter::handle_debug(const HttpRequest& req, HttpResponse* resp) {
           .kv("mfma_util", r.mfma_util)
           .end_obj();
     j.end_arr();
+  } else if (req.path == "/debug/procs") {
+    // every GPU context of the last tick's process lists, and whether it became a pod_gpu row: the
+    // ones that did not are the hidden empty / peer contexts (or not opted in), named by pid
+    auto st = state_ptr();
+    j.arr();
+    for (size_t d = 0; d < st->procs.size(); ++d)
+      for (const auto& p : st->procs[d]) {
+        bool row = false;
+        for (const auto& r : st->rows)
+          if (!r.idle && r.dev == static_cast<int>(d) && r.pid == std::to_string(p.pid)) row = true;
+        j.obj()
+            .kv("dev", static_cast<int64_t>(d))
+            .kv("pid", static_cast<int64_t>(p.pid))
+            .kv("vram_bytes", p.vram_bytes)
+            .kv("mem_bytes", p.mem_bytes)
+            .kv("cu_occupancy", p.cu_occupancy)
+            .kv("occ_samples", static_cast<int64_t>(p.occ_samples))
+            .kv("occ_busy", static_cast<int64_t>(p.occ_busy))
+            .kv("queues", static_cast<int64_t>(p.queues))
+            .kv("row", row)
+            .end_obj();
+      }
+    j.end_arr();
   } else {
     resp->status = 404;
     resp->content_type = "text/plain; charset=utf-8";
@@ -222,6 +247,17 @@ void Exporter::handle_debug(const HttpRequest& req, HttpResponse* resp) {
   }
   resp->inline_body = j.take();
   resp->inline_body.push_back('\n');
+}
+
+std::string Exporter::debug_view(const std::string& path_and_query) {
+  HttpRequest req;
+  req.method = "GET";
+  const size_t q = path_and_query.find('?');
+  req.path = path_and_query.substr(0, q);
+  if (q != std::string::npos) req.query = path_and_query.substr(q + 1);
+  HttpResponse resp;
+  handle_debug(req, &resp);
+  return resp.status == 200 ? resp.inline_body : std::string();
 }
 
 }  // namespace gpumon

@@ -208,6 +208,10 @@ class ChildExporter:
     def pod_rows(self) -> List[dict]:
         return self.get("/debug/rows")
 
+    def procs(self) -> List[dict]:
+        """Every GPU context of the last tick, ``row`` false for the hidden ones."""
+        return self.get("/debug/procs")
+
     def metrics(self, timeout: float = 10.0) -> str:
         c = http.client.HTTPConnection("127.0.0.1", self.port, timeout=timeout)
         try:

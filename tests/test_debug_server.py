@@ -62,6 +62,10 @@ def test_views_are_json_and_agree_with_the_bindings(ex):
             w = mine["fields"][k]
             assert (w is None and v != v) or w == pytest.approx(v), k  # NaN is JSON null
 
+    procs = json.loads(_get(port, "/debug/procs")[2])
+    assert procs == ex.debug_view("/debug/procs")
+    assert {(p["dev"], str(p["pid"])) for p in procs if p["row"]} == {(r["dev"], r["pid"]) for r in ex.pod_rows()
+                                                                       if not r["idle"]}
     rows = json.loads(_get(port, "/debug/rows")[2])
     assert [(r["dev"], r["pid"]) for r in rows] == [(r["dev"], r["pid"]) for r in ex.pod_rows()]
 

@@ -430,3 +430,20 @@ def test_sub_sample_sums_restart_after_a_failed_list(mock_exporter):
     _wait_ticks(ex, 2)  # the failed list, then the interval after it
     row = next(r for r in ex.pod_rows() if r["pid"] == "51")
     assert 1 <= row["occ_samples"] <= 14, row  # one interval's reads (10 + scan jitter), not two
+
+
+def test_hidden_contexts_are_named_in_the_procs_view(mock_exporter):
+    """/debug/procs (and Exporter.debug_view in-process) lists every GPU context of the last tick
+    with `row` false for the hidden ones: the bench names which pids `hidden_contexts` counted."""
+    procs = [{"pid": 21, "device": 0, "name": "train", "kfd_only": True},
+             {"pid": 22, "device": 0, "name": "rocminfo", "kfd_only": True, "vram_bytes": 0}]
+    ex = mock_exporter(backend="mock:gpus=1,mode=idle", sample_threads=0, mock={"procs": procs})
+    ex.mock_set_occ_series(0, [100.0, 0.0])
+    ex.tick()
+    view = {p["pid"]: p for p in ex.debug_view("/debug/procs")}
+    assert view[21]["row"] is True and view[22]["row"] is False
+    assert view[22]["vram_bytes"] == 0 and view[22]["dev"] == 0
+    assert sum(1 for p in view.values() if not p["row"]) == ex.self_stats()["hidden_contexts"]
+    with pytest.raises(KeyError):
+        ex.debug_view("/debug/nope")
+    assert ex.debug_view("/debug/state")["seq"] == ex.seq
