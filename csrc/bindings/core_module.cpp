@@ -962,7 +962,9 @@ PYBIND11_MODULE(_core, m) {
            [](NativeOptions& o, const py::dict& env) {
              EnvBlock e(env_strings(env));
              std::string err;
-             if (!options_apply_env(&o, e.p.data(), &err)) throw py::value_error(err);
+             std::vector<std::string> unknown;
+             if (!options_apply_env(&o, e.p.data(), &err, &unknown)) throw py::value_error(err);
+             return unknown;  // GPUMON_* names that are neither keys nor environment-only variables
            })
       .def_static(
           "parse",
@@ -1028,6 +1030,8 @@ PYBIND11_MODULE(_core, m) {
     }
     return l;
   }, "the command-line flags both entry points take");
+  m.def("env_only_variables", &env_only_variables,
+        "GPUMON_* variables read by the runtime that are not configuration keys (docs/configuration.md)");
   m.def("cri_autodetect_sockets", &cri_autodetect_sockets);
 
   py::class_<Exporter>(m, "Exporter")

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -33,8 +34,11 @@ class JsonOut {
     if (!std::isfinite(v)) {
       s_ += "null";
     } else {
+      // the shortest of 15 / 17 significant digits that reads back as the same double (0.1, not
+      // 0.10000000000000001)
       char b[40];
-      snprintf(b, sizeof b, "%.17g", v);
+      snprintf(b, sizeof b, "%.15g", v);
+      if (strtod(b, nullptr) != v) snprintf(b, sizeof b, "%.17g", v);
       s_ += b;
     }
     return *this;

@@ -3,6 +3,7 @@
 
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cmath>
 #include <cstdlib>
@@ -621,7 +622,16 @@ bool options_load_file(NativeOptions* o, const std::string& path, std::vector<st
   return true;
 }
 
-bool options_apply_env(NativeOptions* o, char** envp, std::string* err) {
+const std::vector<std::string>& env_only_variables() {
+  static const std::vector<std::string> v = {
+      "GPUMON_CONFIG",         "GPUMON_AMDSMI_LIB",      "GPUMON_ROCM_SMI_LIB",   "GPUMON_TLS_RELOAD_S",
+      "GPUMON_HTTP_SNDBUF",    "GPUMON_LIBSSL",          "GPUMON_LIBCRYPTO",      "GPUMON_HTTP_HEADER_TIMEOUT_S",
+      "GPUMON_HTTP_MEMORY_BUDGET", "GPUMON_ROCTX",       "GPUMON_PLUGIN_DIR",     "GPUMON_PROBE_RUNTIME",
+      "GPUMON_PROBE_STREAM",   "GPUMON_PROBE_KERNARG",   "GPUMON_PMC_DEBUG_INIT", "GPUMON_LOAD_SYNC"};
+  return v;
+}
+
+bool options_apply_env(NativeOptions* o, char** envp, std::string* err, std::vector<std::string>* unknown) {
   for (char** p = envp; p && *p; ++p) {
     const std::string kv = *p;
     const size_t eq = kv.find('=');
@@ -640,9 +650,19 @@ bool options_apply_env(NativeOptions* o, char** envp, std::string* err) {
     if (k == "CONFIG" || k == "AMDSMI_LIB") continue;
     for (auto& c : k) c = static_cast<char>(tolower(static_cast<unsigned char>(c)));
     std::string e;
-    if (options_set(o, k, {kv.substr(eq + 1)}, &e) < 0) {
+    const int r = options_set(o, k, {kv.substr(eq + 1)}, &e);
+    if (r < 0) {
       *err = "GPUMON_" + kv.substr(7, eq - 7) + ": " + e;
       return false;
+    }
+    const std::string name = kv.substr(0, eq);
+    // Kubernetes service links of a Service named "gpumon" (GPUMON_SERVICE_HOST, GPUMON_PORT,
+    // GPUMON_PORT_9400_TCP_ADDR, ...) when a pod spec leaves enableServiceLinks on: not ours
+    const bool service_link =
+        starts_with(name, "GPUMON_SERVICE_") || name == "GPUMON_PORT" || starts_with(name, "GPUMON_PORT_");
+    if (r == 0 && unknown && !starts_with(name, "GPUMON_FAKE_") && !service_link) {
+      const auto& known = env_only_variables();
+      if (std::find(known.begin(), known.end(), name) == known.end()) unknown->push_back(name);
     }
   }
   return true;
@@ -687,7 +707,11 @@ ParseStatus options_parse(NativeOptions* o, const std::vector<std::string>& args
       for (const auto& k : unknown) warnings->push_back("config: key '" + k + "' is not a configuration key (ignored)");
   }
   // 2. the environment
-  if (!options_apply_env(o, envp, err)) return ParseStatus::kBadEnv;
+  std::vector<std::string> unknown_env;
+  if (!options_apply_env(o, envp, err, &unknown_env)) return ParseStatus::kBadEnv;
+  if (warnings)
+    for (const auto& k : unknown_env)
+      warnings->push_back("environment: " + k + " is neither a configuration key nor a GPUMON_ variable (ignored)");
   // 3. --compat (the reference's behaviour: opt-in label mlgpu=mlgpu, 10 s interval) between the
   // environment and the flags: explicit flags still win
   if (compat) {

@@ -80,7 +80,14 @@ ParseStatus options_parse(NativeOptions* o, const std::vector<std::string>& args
 bool options_load_file(NativeOptions* o, const std::string& path, std::vector<std::string>* unknown, std::string* err);
 
 // NODE_NAME, INFLUXDB_URL, GPUMON_<KEY> (GPUMON_CONFIG / GPUMON_AMDSMI_LIB excluded, as in Python).
-bool options_apply_env(NativeOptions* o, char** envp, std::string* err);
+// GPUMON_* variables that are neither a key nor an environment-only variable (a typo) go to
+// `unknown` when given.
+bool options_apply_env(NativeOptions* o, char** envp, std::string* err, std::vector<std::string>* unknown = nullptr);
+
+// GPUMON_* variables read with getenv() by the runtime (tuning, diagnosis, library paths), which are
+// not configuration keys (docs/configuration.md's environment-only table; the test fakes'
+// GPUMON_FAKE_* are not listed).
+const std::vector<std::string>& env_only_variables();
 
 // Resolves listen / debug addresses, host name fallback, control-plane sockets (existence checks, CRI
 // autodetect) and the on-device cadence into cfg / od (after all sources). false with *err for an

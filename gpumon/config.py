@@ -78,10 +78,14 @@ class Config:
         return self
 
     def apply_env(self, env: Optional[Dict[str, str]] = None) -> "Config":
+        """NODE_NAME, INFLUXDB_URL / _TOKEN and GPUMON_<KEY>; a GPUMON_ name that is neither a key
+        nor an environment-only variable (a typo) is logged and ignored, as the binary does."""
         try:
-            self._o.apply_env(dict(os.environ if env is None else env))
+            unknown = self._o.apply_env(dict(os.environ if env is None else env))
         except ValueError as e:
             raise ConfigError(str(e)) from None
+        for k in unknown or []:
+            logging.getLogger("gpumon").warning("environment: %s is neither a configuration key nor a GPUMON_ variable (ignored)", k)
         return self
 
     def apply_file(self, path: str) -> List[str]:

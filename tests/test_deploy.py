@@ -537,6 +537,8 @@ def test_base_pod_is_unprivileged():
     assert sc.get("privileged", False) is False and sc["allowPrivilegeEscalation"] is False
     assert sc["readOnlyRootFilesystem"] is True and sc["seccompProfile"]["type"] == "RuntimeDefault"
     assert sc["capabilities"]["drop"] == ["ALL"]
+    # no Kubernetes service-link variables (GPUMON_SERVICE_HOST, ...) in the GPUMON_<KEY> namespace
+    assert pod["enableServiceLinks"] is False
     # no DAC_READ_SEARCH in the base (with RuntimeDefault seccomp it unlocks
     # open_by_handle_at); it is the opt-in overlays/fdscan/
     assert sorted(sc["capabilities"].get("add", [])) == ["SYS_NICE", "SYS_PTRACE"]

@@ -327,3 +327,34 @@ def test_python_view_has_no_key_table_of_its_own():
 
     keys = {k["key"] for k in core().option_keys()}
     assert {"interval", "listen", "host", "control_plane", "cri_socket", "debug_listen", "pcie_bw_unit_bytes"} <= keys
+
+
+def test_env_only_list_is_the_docs_list(core):
+    """The runtime's own list of environment-only variables (what a typo is checked against) is the
+    documented one, which test_environment_only_knobs_are_documented ties to the getenv() calls."""
+    import sys
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import gen_config_doc
+
+    assert sorted(core.env_only_variables()) == sorted(name for name, *_ in gen_config_doc.ENV_ONLY)
+
+
+def test_misspelt_gpumon_variable_is_named(caplog):
+    """GPUMON_INTERVALL=5 is not a key: both entry points say so and go on with the default; real
+    keys, environment-only variables and the test fakes' GPUMON_FAKE_* pass silently."""
+    env = {"GPUMON_INTERVALL": "5", "GPUMON_INTERVAL": "2", "GPUMON_HTTP_SNDBUF": "0", "GPUMON_FAKE_PCI": "x",
+           # Kubernetes service links of a Service named gpumon (enableServiceLinks left on)
+           "GPUMON_SERVICE_HOST": "10.0.0.1", "GPUMON_PORT": "tcp://10.0.0.1:9400",
+           "GPUMON_PORT_9400_TCP_ADDR": "10.0.0.1"}
+    r = _print(env=env)
+    assert r.returncode == 0 and json.loads(r.stdout)["interval"] == 2.0
+    assert "GPUMON_INTERVALL is neither a configuration key" in r.stderr
+    assert "GPUMON_HTTP_SNDBUF" not in r.stderr and "GPUMON_FAKE_PCI" not in r.stderr
+    assert "SERVICE_HOST" not in r.stderr and "GPUMON_PORT" not in r.stderr
+    import logging
+
+    with caplog.at_level(logging.WARNING, logger="gpumon"):
+        assert Config().apply_env(env).interval == 2.0
+    assert [m for m in caplog.messages if "GPUMON_INTERVALL" in m] and not [m for m in caplog.messages
+                                                                          if "SNDBUF" in m]
