@@ -178,6 +178,16 @@ def build():
                          (f'increase(gpumon_http_tls_reloads_total{{{HOST}}}[1h])', "{{host}} reloads {{result}} /h"),
                          (f'rate(gpumon_http_tls_handshake_failures_total{{{HOST}}}[5m])', "{{host}} failed handshakes/s")],
                         12, y, 12, 6))
+    y += 6
+    # the host link (interval rate from the firmware accumulator, profiles/r6_pcie_bandwidth.md) and the
+    # hardware queues behind the peer-context rule (profiles/r6_kfd_queues.md)
+    panels.append(panel("PCIe host link bandwidth (both directions, interval)", "timeseries",
+                        [(f'gpu_pcie_bandwidth_bytes_per_second{{{HOST}}}', "{{host}} gpu{{gpu_id}}")], 0, y, 12, 8,
+                        fieldConfig={"defaults": {"unit": "Bps"}, "overrides": []}))
+    panels.append(panel("Hardware queues per process and GPU (0 = a context that never submitted work there)",
+                        "timeseries",
+                        [(f'max by (host, gpu_id, namespace, podname, pid) (pod_gpu_proc_queues{{{HOST}}})',
+                          "{{host}} gpu{{gpu_id}} {{namespace}}/{{podname}} pid {{pid}}")], 12, y, 12, 8))
     return {
         "title": "gpumon — MI355X GPU cluster",
         "uid": "gpumon-mi355x",
