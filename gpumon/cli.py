@@ -117,7 +117,7 @@ def render_top(statics, samples, rates, rows, active=None) -> str:
 
     lines = []
     hdr = (f"{'GPU':>3} {'UTIL%':>6} {'XCD busy% (0-7)':<32} {'VRAM MiB':>17} {'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8}"
-           f" {'SHARING':>10}")
+           f" {'PCIe GB/s':>9} {'SHARING':>10}")
     lines.append(hdr)
     for st, sm, rt in zip(statics, samples, rates):
         f = sm["fields"]
@@ -126,16 +126,19 @@ def render_top(statics, samples, rates, rows, active=None) -> str:
         tot = (f["vram_total"] or 0) / 1048576
         lines.append(f"{st['gpu_id']:>3} {_fmt(f['gfx_util'], 6)} {xcd:<32} {used:8.0f}/{tot:8.0f} "
                      f"{_fmt(f['power_cur'], 6)} {_fmt(f['temp_hotspot'], 6)} {_fmt(f['gfxclk_cur'], 8)}"
+                     f" {_fmt((rt or {}).get('pcie_Bps', float('nan')) / 1e9, 9, 2)}"
                      f" {sharing_label((active or {}).get(str(st['gpu_id']))):>10}")
     lines.append("")
     # BUSY%: share of the interval with the process's waves resident (KFD; the reference copied the
-    # device's utilisation onto every process, gpu.py:205); CUs: mean CU-equivalents its waves held
+    # device's utilisation onto every process, gpu.py:205); CUs: mean CU-equivalents its waves held;
+    # Q: its hardware queues on that GPU (KFD; - where the list is not readable)
     lines.append(f"{'CONTAINER':<13}{'POD':<32}{'NAMESPACE':<14}{'USER':<10}{'PID':>8} {'GPU':>3} {'MEM MiB':>9} "
-                 f"{'BUSY%':>6} {'CUs':>6}  PROCESS")
+                 f"{'BUSY%':>6} {'CUs':>6} {'Q':>3}  PROCESS")
     for r in rows:
         lines.append(f"{r['containerid'][:12]:<13}{r['podname'][:31]:<32}{r['namespace'][:13]:<14}{r['user_name'][:9]:<10}"
                      f"{r['pid']:>8} {r['dev']:>3} {r['used_memory_bytes'] / 1048576:9.0f} "
-                     f"{_fmt(r['proc_gfx_util'], 6, 1)} {_fmt(r.get('cu_occupancy'), 6, 1)}  {r['procname'][:30]}")
+                     f"{_fmt(r['proc_gfx_util'], 6, 1)} {_fmt(r.get('cu_occupancy'), 6, 1)} "
+                     f"{r['queues'] if r.get('queues', -1) >= 0 else '-':>3}  {r['procname'][:30]}")
     return "\n".join(lines)
 
 

@@ -105,3 +105,27 @@ def test_fleet_fetch_runs_nodes_in_parallel(core):
     assert dt < 1.5, dt
     hosts = [f["node_gpu_gpu_util"]["samples"][0][1]["host"] for f in frames]
     assert hosts == [f"h{s.server_address[1]}" for s in srvs]
+
+
+def test_local_top_shows_pcie_rate_and_queues():
+    """`gpumon top` (local): the per-GPU PCIe interval rate and each row's hardware queue count
+    (`-` where KFD's queue list is not readable)."""
+    from gpumon.cli import render_top
+
+    st = [{"gpu_id": "0"}]
+    f = {"gfx_util": 100.0, "vram_used": 2 ** 30, "vram_total": 2 ** 38, "power_cur": 1300.0,
+         "temp_hotspot": 60.0, "gfxclk_cur": 2100.0}
+    sm = [{"fields": f, "xcd_busy": [100.0] * 8}]
+    rows = [dict(containerid="-", podname="-", namespace="-", user_name="-", pid="7", dev=0,
+                 used_memory_bytes=2 ** 30, proc_gfx_util=50.0, cu_occupancy=128.0, queues=3, procname="train"),
+            dict(containerid="-", podname="-", namespace="-", user_name="-", pid="8", dev=0,
+                 used_memory_bytes=0, proc_gfx_util=float("nan"), cu_occupancy=float("nan"), queues=-1,
+                 procname="peer")]
+    text = render_top(st, sm, [{"pcie_Bps": 57.2e9}], rows)
+    head, gpu = text.splitlines()[:2]
+    assert "PCIe GB/s" in head and "57.20" in gpu
+    lines = text.splitlines()
+    train = next(l for l in lines if l.endswith("train"))
+    peer = next(l for l in lines if l.endswith("peer"))
+    assert train.split()[-2] == "3" and peer.split()[-2] == "-"
+    assert "-" in render_top(st, sm, [{}], [])  # no rate yet (first tick)
