@@ -1036,6 +1036,7 @@ std::string Exporter::render_influx_now() {
   in.host = cfg_.host;
   in.statics = st.get();
   in.samples = &state->samples;
+  in.rates = &state->rates;
   in.pod_rows = &state->rows;
   std::string out;
   render_influx(in, wall_ns(), cfg_.influx_extended, &out, cfg_.influx_schema);

@@ -335,7 +335,10 @@ const std::vector<Key>& keys() {
        [](const NativeOptions& o, JsonOut* j, bool redact) {
          j->str(redact && !o.cfg.influx_token.empty() ? std::string("***") : o.cfg.influx_token);
        }},
-      bool_key("influx_extended", kPush, "also push the MI355X fields", O(o->cfg.influx_extended)),
+      bool_key("influx_extended", kPush,
+               "also push a gpu_ext line per GPU: UMC activity, hotspot / HBM temperature, power, energy, "
+               "clocks, interval PCIe bytes/s and power, per-XCD busy, RAS totals",
+               O(o->cfg.influx_extended)),
       int_key("influx_schema", kPush, "2019 = gpu.py layout; 2018 = img/influxdb.png pod_gpu layout", O(o->cfg.influx_schema)),
       int_key("influx_every", kPush, "ticks per push", O(o->cfg.influx_every)),
       bool_key("influx_gzip", kPush, "gzip each push (Content-Encoding: gzip): 7-8x fewer bytes for 8 GPUs", O(o->cfg.influx_gzip)),

@@ -1125,6 +1125,10 @@ void render_influx(const RenderInput& in, int64_t ts_ns, bool extended, std::str
       field("energy_j", v[F_ENERGY_J]);
       field("gfxclk_mhz", v[F_GFXCLK_CUR]);
       field("uclk_mhz", v[F_UCLK_CUR]);
+      if (in.rates && d < in.rates->size() && (*in.rates)[d].valid) {  // interval rates (rates.cpp)
+        field("pcie_bytes_per_s", (*in.rates)[d].pcie_Bps);
+        field("power_interval_w", (*in.rates)[d].power_from_energy_w);
+      }
       for (int k = 0; k < sm[d].n_xcd; ++k) {
         std::string key = "xcd" + std::to_string(k) + "_busy";
         field(key.c_str(), sm[d].xcd_busy[k]);

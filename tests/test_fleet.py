@@ -129,3 +129,23 @@ def test_local_top_shows_pcie_rate_and_queues():
     peer = next(l for l in lines if l.endswith("peer"))
     assert train.split()[-2] == "3" and peer.split()[-2] == "-"
     assert "-" in render_top(st, sm, [{}], [])  # no rate yet (first tick)
+
+
+def test_influx_extended_carries_interval_rates(mock_exporter):
+    """gpu_ext also carries the interval PCIe rate and power (rates.cpp) once a second tick gives
+    them an interval; the first tick's line has neither."""
+    import time
+
+    import pytest
+
+    ex = mock_exporter(backend="mock:gpus=1,mode=load", influx_extended=True)
+    ex.tick()
+    (ext,) = [l for l in ex.influx_text().splitlines() if l.startswith("gpu_ext,")]
+    assert "pcie_bytes_per_s=" not in ext
+    time.sleep(0.05)
+    ex.tick()
+    (ext,) = [l for l in ex.influx_text().splitlines() if l.startswith("gpu_ext,")]
+    fields = dict(kv.split("=") for kv in ext.split(" ")[1].split(","))
+    r = ex.rates()[0]
+    assert float(fields["pcie_bytes_per_s"]) == pytest.approx(r["pcie_Bps"], rel=1e-6)
+    assert float(fields["power_interval_w"]) == pytest.approx(r["power_from_energy_w"], rel=1e-6)
