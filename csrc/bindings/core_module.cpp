@@ -1030,6 +1030,8 @@ PYBIND11_MODULE(_core, m) {
     }
     return l;
   }, "the command-line flags both entry points take");
+  m.def("memory_limit_bytes", &memory_limit_bytes, py::arg("proc_cgroup") = "/proc/self/cgroup",
+        py::arg("cgroup_root") = "/sys/fs/cgroup", "the memory limit the HTTP connection cap is sized against");
   m.def("env_only_variables", &env_only_variables,
         "GPUMON_* variables read by the runtime that are not configuration keys (docs/configuration.md)");
   m.def("cri_autodetect_sockets", &cri_autodetect_sockets);

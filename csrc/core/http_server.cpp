@@ -61,10 +61,12 @@ constexpr int kSndBuf = 1 << 20;  // GPUMON_HTTP_SNDBUF overrides (bytes; 0 = th
 constexpr uint64_t kMemBaseline = 96ull << 20;
 constexpr uint64_t kTlsSessionBytes = 64ull << 10;
 
+}  // namespace
+
 // The smallest memory.max on the way from this process's cgroup (cgroup v2) up to the root, else
 // the v1 memory controller's limit; 0 = unlimited / unknown. GPUMON_HTTP_MEMORY_BUDGET (bytes)
-// overrides.
-uint64_t memory_limit_bytes() {
+// overrides. `proc_cgroup` / `cgroup_root`: /proc/self/cgroup and /sys/fs/cgroup (tests: a tree).
+uint64_t memory_limit_bytes(const std::string& proc_cgroup, const std::string& cgroup_root) {
   if (const char* e = getenv("GPUMON_HTTP_MEMORY_BUDGET")) return strtoull(e, nullptr, 10);
   auto num = [](const std::string& path) -> uint64_t {
     std::string t;
@@ -76,12 +78,12 @@ uint64_t memory_limit_bytes() {
   };
   std::string cg;
   uint64_t best = 0;
-  if (read_file("/proc/self/cgroup", &cg, 4096))
+  if (read_file(proc_cgroup, &cg, 4096))
     for (const auto& line : split(cg, '\n')) {
       if (starts_with(line, "0::")) {  // v2: walk from this cgroup to the mount's root
         std::string path(trim(line.substr(3)));
         while (true) {
-          const uint64_t v = num("/sys/fs/cgroup" + (path == "/" ? std::string() : path) + "/memory.max");
+          const uint64_t v = num(cgroup_root + (path == "/" ? std::string() : path) + "/memory.max");
           if (v && (!best || v < best)) best = v;
           if (path.empty() || path == "/") break;
           const size_t slash = path.rfind('/');
@@ -89,9 +91,11 @@ uint64_t memory_limit_bytes() {
         }
       }
     }
-  if (!best) best = num("/sys/fs/cgroup/memory/memory.limit_in_bytes");
+  if (!best) best = num(cgroup_root + "/memory/memory.limit_in_bytes");
   return best;
 }
+
+namespace {
 
 const char* status_text(int s) {
   switch (s) {
@@ -388,7 +392,7 @@ bool HttpServer::start(std::string* err) {
     const rlim_t usable = rl.rlim_cur > 2 * kFdReserve ? rl.rlim_cur - kFdReserve : rl.rlim_cur / 2;
     max_conns_ = std::clamp<size_t>(usable / static_cast<rlim_t>(std::max(1, nthreads_)), 8, kMaxConnsPerLoop);
   }
-  if (const uint64_t mem = memory_limit_bytes(); mem > 0) {
+  if (const uint64_t mem = memory_limit_bytes("/proc/self/cgroup", "/sys/fs/cgroup"); mem > 0) {
     const uint64_t budget = mem > 2 * kMemBaseline ? mem - kMemBaseline : mem / 2;
     const uint64_t per_conn = kMaxInput + 4096 + (tls_ ? kTlsSessionBytes : 0);
     const size_t cap = std::max<size_t>(8, budget / per_conn / static_cast<uint64_t>(std::max(1, nthreads_)));

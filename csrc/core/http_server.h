@@ -50,6 +50,11 @@ struct HttpResponse {
 // and port (0 = ephemeral). false with the reason in *err.
 bool parse_listen(const std::string& listen, std::string* host, int* port, std::string* err);
 
+// The memory limit the connection cap is sized against: the smallest cgroup v2 memory.max from the
+// cgroup named in `proc_cgroup` (/proc/self/cgroup) up to `cgroup_root` (/sys/fs/cgroup), else the
+// v1 limit; 0 = none. GPUMON_HTTP_MEMORY_BUDGET overrides.
+uint64_t memory_limit_bytes(const std::string& proc_cgroup, const std::string& cgroup_root);
+
 class HttpServer {
  public:
   using Handler = std::function<void(const HttpRequest&, HttpResponse*)>;

@@ -30,7 +30,9 @@ def _get(port, path, timeout=10, host="127.0.0.1"):
 
 @pytest.fixture()
 def ex(core):
-    e = core.Exporter({"backend": "mock", "mock": {"gpus": 2}, "listen_addr": "127.0.0.1", "port": 0,
+    procs = [{"pid": 4242, "device": 0, "name": "train", "kfd_only": True, "vram_bytes": 1 << 30, "queues": 2},
+             {"pid": 4243, "device": 1, "name": "probe", "kfd_only": True, "vram_bytes": 0, "queues": 0}]
+    e = core.Exporter({"backend": "mock", "mock": {"gpus": 2, "procs": procs}, "listen_addr": "127.0.0.1", "port": 0,
                        "interval_s": 0, "debug_listen": "127.0.0.1:0", "host": "node-a"})
     assert e.start() == ""
     yield e
@@ -66,7 +68,10 @@ def test_views_are_json_and_agree_with_the_bindings(ex):
     assert procs == ex.debug_view("/debug/procs")
     assert {(p["dev"], str(p["pid"])) for p in procs if p["row"]} == {(r["dev"], r["pid"]) for r in ex.pod_rows()
                                                                        if not r["idle"]}
+    assert {(p["dev"], p["pid"]) for p in procs} == {(0, 4242), (1, 4243)}  # (hidden ones: test_occupancy.py)
     rows = json.loads(_get(port, "/debug/rows")[2])
+    train = next(r for r in rows if r["pid"] == "4242")
+    assert train["queues"] == 2 and train["used_memory_bytes"] == 1 << 30 and train["procname"] == "train"
     assert [(r["dev"], r["pid"]) for r in rows] == [(r["dev"], r["pid"]) for r in ex.pod_rows()]
 
 

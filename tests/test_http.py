@@ -919,3 +919,32 @@ def test_connection_cap_fits_the_memory_limit(core, monkeypatch, tmp_path, tls):
         assert cap >= (1000 if tls else 1800), cap  # and not needlessly low
     finally:
         ex.stop()
+
+
+def test_memory_limit_walks_the_cgroup_tree(core, monkeypatch, tmp_path):
+    """The limit is the smallest memory.max from the process's cgroup (v2) up to the root -- a pod's
+    limit sits on the pod's cgroup, above the container's "max" -- else the v1 controller's limit;
+    "max" and v1's page-rounded "unlimited" mean none."""
+    monkeypatch.delenv("GPUMON_HTTP_MEMORY_BUDGET", raising=False)
+    root = tmp_path / "cg"
+    leaf = root / "kubepods.slice" / "pod1.slice" / "cri-abc.scope"
+    leaf.mkdir(parents=True)
+    (root / "kubepods.slice" / "memory.max").write_text("8589934592\n")
+    (root / "kubepods.slice" / "pod1.slice" / "memory.max").write_text("268435456\n")
+    (leaf / "memory.max").write_text("max\n")
+    cg = tmp_path / "cgroup"
+    cg.write_text("0::/kubepods.slice/pod1.slice/cri-abc.scope\n")
+    assert core.memory_limit_bytes(str(cg), str(root)) == 256 << 20
+    (leaf / "memory.max").write_text("134217728\n")  # a tighter container limit wins
+    assert core.memory_limit_bytes(str(cg), str(root)) == 128 << 20
+    # cgroup v1: no "0::" line, the memory controller's limit file
+    v1 = tmp_path / "v1"
+    (v1 / "memory").mkdir(parents=True)
+    (v1 / "memory" / "memory.limit_in_bytes").write_text("536870912\n")
+    cg.write_text("12:memory:/kubepods/pod1/abc\n")
+    assert core.memory_limit_bytes(str(cg), str(v1)) == 512 << 20
+    (v1 / "memory" / "memory.limit_in_bytes").write_text("9223372036854771712\n")  # unlimited
+    assert core.memory_limit_bytes(str(cg), str(v1)) == 0
+    assert core.memory_limit_bytes(str(tmp_path / "none"), str(tmp_path / "none")) == 0
+    monkeypatch.setenv("GPUMON_HTTP_MEMORY_BUDGET", "1000")
+    assert core.memory_limit_bytes(str(cg), str(root)) == 1000

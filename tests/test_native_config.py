@@ -168,6 +168,9 @@ def test_config_env_var_names_the_file(tmp_path):
     ("gpumon:\n  devices: [0, 1\n", "line 2: unterminated flow list"),
     ("gpumon:\n  user_regex: \"abc\n", "unterminated"),
     ("gpumon:\n  listen: {a: b}\n", "unsupported YAML construct"),
+    ("gpumon:\n  devices: [[0], 1]\n", "line 2: nested collections are not supported"),
+    ("gpumon:\n  devices: [\"0, 1]\n", "line 2: unterminated quoted value"),
+    ("gpumon:\n\tinterval: 2\n", "line 2: tab indentation"),
     ("other: 1\n", None),  # no gpumon: mapping: flat file, unknown key -> warning only
 ])
 def test_bad_files_fail_with_the_line(tmp_path, text, msg):
@@ -358,3 +361,24 @@ def test_misspelt_gpumon_variable_is_named(caplog):
         assert Config().apply_env(env).interval == 2.0
     assert [m for m in caplog.messages if "GPUMON_INTERVALL" in m] and not [m for m in caplog.messages
                                                                           if "SNDBUF" in m]
+
+
+def test_inline_flag_values_escapes_and_retired_keys(tmp_path):
+    """`--flag=value` as well as `--flag value`; a fixed-value flag refuses a value; YAML double-quote
+    escapes (\\n, \\t, \\") in scalars and flow lists; influx_token from the file (redacted on print);
+    the retired `ondevice` key is accepted without effect; a missing file is named."""
+    r = _print("--interval=2.5", "--listen=127.0.0.1:9500")
+    n = json.loads(r.stdout)
+    assert r.returncode == 0 and n["interval"] == 2.5 and n["listen"] == "127.0.0.1:9500"
+    r = _print("--influx-extended=false")
+    assert r.returncode == 2 and "--influx-extended takes no value" in r.stderr
+    p = tmp_path / "c.yaml"
+    p.write_text('gpumon:\n  user_regex: "a\\tb\\nc"\n  metrics_exclude: ["x\\"y", z]\n'
+                 '  influx_token: "s3cret"\n  ondevice: true\n')
+    r = _print("--config", str(p))
+    assert r.returncode == 0, r.stderr
+    n = json.loads(r.stdout)
+    assert n["user_regex"] == "a\tb\nc" and n["metrics_exclude"] == ['x"y', "z"]
+    assert n["influx_token"] == "***" and "s3cret" not in r.stdout and "ondevice" not in r.stderr
+    r = _print("--config", str(tmp_path / "missing.yaml"))
+    assert r.returncode == 2 and "cannot read" in r.stderr and "missing.yaml" in r.stderr
