@@ -8,6 +8,7 @@
 #include <pthread.h>
 #include <sched.h>
 #include <sys/epoll.h>
+#include <sys/ioctl.h>
 #include <sys/eventfd.h>
 #include <sys/resource.h>
 #include <sys/socket.h>
@@ -714,13 +715,22 @@ void HttpServer::run(Loop* L) {
   //   1 never answered, a request partly read (a trickler)
   //   2 answered before, idle now (Prometheus' keep-alive between scrapes: kept longest)
   //   3 answered before, a request partly read
-  auto pick_victim = [&]() {
-    int victim = -1, best = 4;
+  // (bytes still in the socket count as a partial request). `worst_class`: the highest class that
+  // may be closed (an accept at the cap: any; paying another loop's eviction debt: 0 only).
+  auto pick_victim = [&](int worst_class) {
+    int victim = -1, best = worst_class + 1;
     for (int vfd : L->lru) {  // oldest first; a connection mid-response is skipped
       auto vit = L->conns.find(vfd);
       if (vit == L->conns.end() || vit->second.writing) continue;
       const Conn& vc = vit->second;
-      const int cls = (vc.served > 0 ? 2 : 0) + (vc.in.empty() ? 0 : 1);
+      int cls = (vc.served > 0 ? 2 : 0) + (vc.in.empty() ? 0 : 1);
+      if (vc.in.empty()) {
+        // bytes waiting in the socket that this loop has not read yet (a scraper accepted in this
+        // batch, whose request the batch's read events have not reached, or an eviction debt paid
+        // before them): not idle
+        int avail = 0;
+        if (ioctl(vfd, FIONREAD, &avail) == 0 && avail > 0) cls += 1;
+      }
       if (cls < best) {
         best = cls;
         victim = vfd;
@@ -746,7 +756,9 @@ void HttpServer::run(Loop* L) {
         evict_debt_.compare_exchange_strong(debt, 0, std::memory_order_relaxed);
         break;
       }
-      const int victim = pick_victim();
+      // only a connect flood's idle sockets pay a debt: never a request waiting to be read, nor a
+      // scraper's keep-alive (the server stays up to kDebtSlack over the cap meanwhile)
+      const int victim = pick_victim(0);
       if (victim < 0) break;  // nothing here either: the debt stays for a loop that has some
       if (!evict_debt_.compare_exchange_weak(debt, debt - 1, std::memory_order_relaxed)) continue;
       evict(victim);
@@ -806,7 +818,7 @@ void HttpServer::run(Loop* L) {
           const size_t cap = max_conns_ * static_cast<size_t>(nthreads_);
           if (conns_.load(std::memory_order_relaxed) >= cap) {
             // full: make room by closing a connection of this loop that is not sending a response
-            const int victim = pick_victim();
+            const int victim = pick_victim(3);
             if (victim >= 0) {
               evict(victim);
             } else if (nthreads_ > 1 && conns_.load(std::memory_order_relaxed) < cap + kDebtSlack) {
