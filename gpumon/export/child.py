@@ -54,7 +54,9 @@ def _yaml_value(v: Any) -> str:
         return repr(v)
     if isinstance(v, (list, tuple)):
         return "[" + ", ".join(_yaml_value(x) for x in v) + "]"
-    return json.dumps(str(v))  # a double-quoted scalar the native YAML subset reads (options.cpp)
+    # a double-quoted scalar the native YAML subset reads (options.cpp: backslash escapes \\ \" \n \t;
+    # no \u escapes there, so non-ASCII text stays as UTF-8)
+    return json.dumps(str(v), ensure_ascii=False)
 
 
 def write_config(cfg: Dict[str, Any], path: str) -> None:

@@ -255,3 +255,20 @@ def test_ranks_per_gpu_must_divide_the_world():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--ranks-per-gpu", "2", "--steps", "1"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode != 0 and "does not divide the world size 3" in r.stderr
+
+
+def test_child_config_file_round_trips_through_the_native_parser(tmp_path):
+    """write_config's scalars are what the binary reads back: quotes, backslashes, a tab, non-ASCII
+    text (the reference's Chinese dashboard titles are the kind of value a label may carry)."""
+    from gpumon.export.child import BINARY, write_config
+
+    want = {"user_prefix": 'notebook-"q"\\\t用户-', "metrics_exclude": ["a,b", "gpu_xcd_*"], "interval": 0.5,
+            "gzip": False}
+    p = tmp_path / "c.yaml"
+    write_config(want, str(p))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("GPUMON_")}
+    r = subprocess.run([BINARY, "--config", str(p), "--print-config"], capture_output=True, text=True, timeout=30,
+                       env=env)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout)
+    assert {k: got[k] for k in want} == want
