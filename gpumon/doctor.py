@@ -84,6 +84,30 @@ def fd_table_check(procfs: str = "/proc", pid=None) -> tuple:
     return SKIP, "no process of another uid with open files to try"
 
 
+def kfd_queue_check(kfd: str = "/sys/class/kfd/kfd/proc") -> tuple:
+    """(status, detail): are KFD's per-process queue lists readable? They decide which GPU contexts of
+    a multi-GPU process are peer contexts (no queue there: not a row, whatever their VRAM); without
+    them the exporter falls back to the peer_context_max_vram_mib threshold (profiles/r6_kfd_queues.md)."""
+    try:
+        pids = [e for e in os.listdir(kfd) if e.isdigit()]
+    except OSError:
+        return SKIP, f"{kfd} not readable"
+    if not pids:
+        return SKIP, "no KFD process on the node to try"
+    readable = queues = 0
+    for p in pids:
+        try:
+            qs = [q for q in os.listdir(f"{kfd}/{p}/queues") if q.isdigit()]
+        except OSError:
+            continue
+        readable += 1
+        queues += len(qs)
+    if readable == 0:
+        return WARN, (f"queues/ of {len(pids)} KFD process(es) unreadable: peer contexts of multi-GPU processes are "
+                      "told apart by the VRAM threshold (peer_context_max_vram_mib) instead of their queues")
+    return OK, f"queue lists readable for {readable}/{len(pids)} KFD process(es), {queues} queue(s)"
+
+
 def fd_limit_cap(http_threads: int, limit=None) -> int:
     """The HTTP server's per-loop connection cap for a RLIMIT_NOFILE soft limit (the formula of
     HttpServer::start, csrc/core/http_server.cpp; the running exporter exports the product as
@@ -324,6 +348,7 @@ def run(cfg, ondevice_check: bool = False, wait_s: float = 3.0) -> list:
         else:
             out.append(("KFD process table", WARN,
                         f"{kfd} not readable: no per-process rows (pod_gpu_*), no occupancy / busy %"))
+        out.append(("KFD queue lists",) + kfd_queue_check(kfd))
         try:
             init = open("/proc/1/comm").read().strip()
         except OSError:

@@ -310,3 +310,28 @@ def test_doctor_reports_the_metrics_certificate(tmp_path):
                                         tls_cert_file=str(tmp_path / "c.pem"), tls_key_file=str(tmp_path / "k.pem")),
                                  wait_s=0.5))
     assert checks["/metrics TLS certificate"][0] == OK
+
+
+def test_doctor_checks_the_kfd_queue_lists(tmp_path):
+    """The peer-context rule reads KFD's per-process queue lists; the doctor says whether it can."""
+    from gpumon.doctor import OK, SKIP, WARN, kfd_queue_check
+
+    kfd = tmp_path / "proc"
+    assert kfd_queue_check(str(kfd))[0] == SKIP  # no KFD at all
+    kfd.mkdir()
+    assert kfd_queue_check(str(kfd))[0] == SKIP  # no process to try
+    for pid, nq in ((100, 2), (200, 0)):
+        (kfd / str(pid) / "queues").mkdir(parents=True)
+        for q in range(nq):
+            (kfd / str(pid) / "queues" / str(q)).mkdir()
+    st, detail = kfd_queue_check(str(kfd))
+    assert st == OK and "2/2" in detail and "2 queue(s)" in detail
+    # unreadable lists (an older kernel without queues/, or no rights): a file stands in here, since
+    # root would read a mode-000 directory anyway
+    import shutil
+
+    for pid in (100, 200):
+        shutil.rmtree(kfd / str(pid) / "queues")
+        (kfd / str(pid) / "queues").write_text("")
+    st, detail = kfd_queue_check(str(kfd))
+    assert st == WARN and "peer_context_max_vram_mib" in detail
