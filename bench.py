@@ -758,12 +758,12 @@ def main() -> int:
             per_gpu_rows.append({"gpu": i, "gpu_id": g, "rows": len(wr), "pids": sorted(r["pid"] for r in wr)[:8],
                                  "idle_rows": sum(1 for r in rows if r["idle"] and r["dev"] == i),
                                  "active_processes": active.get(g)})
-        # the contexts behind hidden_contexts / hidden_peer_contexts, by pid: an empty one holds no
-        # VRAM (a runtime that only opened the GPU), anything else is a peer context (or not opted in)
+        # the contexts behind hidden_contexts / hidden_peer_contexts, by pid, with the exporter's
+        # reason: "empty" (no VRAM, no waves: a runtime that only opened the GPU), "peer" (a
+        # multi-GPU process's context on a GPU it does no work on), "helper", "not opted in"
         hidden_detail = [{"gpu": c["dev"], "pid": c["pid"], "queues": c["queues"],
                           "vram_mib": round(c["vram_bytes"] / 2 ** 20, 1) if c["vram_bytes"] is not None else None,
-                          "why": "peer or not opted in" if (c["vram_bytes"] or 0) > 0 or (c["mem_bytes"] or 0) > 0
-                          else "empty"}
+                          "why": c["why"]}
                          for c in ex.procs() if not c["row"]][:16]
         rows_per_user = {}
         for r in rows:

@@ -700,7 +700,7 @@ TickInfo Exporter::tick() {
     int64_t tb = mono_ns();
     {
       TraceRange tr("gpumon.attrib");
-      build_pod_rows(procs, cur, &rows);
+      build_pod_rows(procs, cur, &rows, &next->hidden);
     }
     info.t_attrib = (mono_ns() - tb) * 1e-9;
     info.devices = n;

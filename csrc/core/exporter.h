@@ -242,7 +242,8 @@ class Exporter {
   void sample_devices(std::vector<DeviceSample>* out, std::vector<std::vector<ProcSample>>* procs,
                       double* procs_s, TickInfo* info);
   void build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
-                      const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows);
+                      const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows,
+                      std::vector<HiddenCtx>* hidden_out = nullptr);
 
   ExporterConfig cfg_;
   std::unique_ptr<Backend> backend_;
@@ -274,6 +275,7 @@ class Exporter {
     std::vector<DeviceSample> samples;
     std::vector<DeviceRates> rates;
     std::vector<PodRow> rows;
+    std::vector<HiddenCtx> hidden;
     std::vector<size_t> proc_counts;
     std::vector<std::vector<ProcSample>> procs;  // per device, after a failed list's hold
   };

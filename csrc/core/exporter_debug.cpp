@@ -226,6 +226,9 @@ void Exporter::handle_debug(const HttpRequest& req, HttpResponse* resp) {
         bool row = false;
         for (const auto& r : st->rows)
           if (!r.idle && r.dev == static_cast<int>(d) && r.pid == std::to_string(p.pid)) row = true;
+        const char* why = row ? "" : "merged";  // a second KFD context of a pid that has its row
+        for (const auto& h : st->hidden)
+          if (h.dev == static_cast<int>(d) && h.pid == p.pid) why = h.why;
         j.obj()
             .kv("dev", static_cast<int64_t>(d))
             .kv("pid", static_cast<int64_t>(p.pid))
@@ -236,6 +239,7 @@ void Exporter::handle_debug(const HttpRequest& req, HttpResponse* resp) {
             .kv("occ_busy", static_cast<int64_t>(p.occ_busy))
             .kv("queues", static_cast<int64_t>(p.queues))
             .kv("row", row)
+            .kv("why", why)
             .end_obj();
       }
     j.end_arr();

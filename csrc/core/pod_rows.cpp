@@ -12,8 +12,13 @@
 namespace gpumon {
 
 void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
-                              const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows) {
+                              const std::vector<DeviceSample>& samples, std::vector<PodRow>* rows,
+                              std::vector<HiddenCtx>* hidden_out) {
   rows->clear();
+  if (hidden_out) hidden_out->clear();
+  auto hide = [&](size_t d, uint32_t pid, const char* why) {
+    if (hidden_out) hidden_out->push_back({static_cast<int>(d), pid, why});
+  };
   // Exclusive use: the one process of a device whose waves were resident this interval (every
   // process counts, opted in or not). Its row carries the device's MFMA utilisation.
   std::map<int, double> mfma;
@@ -168,7 +173,10 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
     // a duplicate series would make Prometheus reject the whole scrape.
     std::unordered_map<uint32_t, size_t> row_of_pid;
     for (const auto& p : procs[d]) {
-      if (is_helper(p.pid)) continue;  // counted in gpumon_ondevice_helper_gpu_contexts
+      if (is_helper(p.pid)) {  // counted in gpumon_ondevice_helper_gpu_contexts
+        hide(d, p.pid, "helper");
+        continue;
+      }
       auto dup = row_of_pid.find(p.pid);
       if (dup != row_of_pid.end()) {
         PodRow& r = (*rows)[dup->second];
@@ -183,10 +191,12 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       if (cfg_.hide_empty_contexts && !(p.vram_bytes > 0) && !(p.mem_bytes > 0) && !(p.cu_occupancy > 0) &&
           p.occ_busy == 0) {
         hidden++;
+        hide(d, p.pid, "empty");
         continue;
       }
       if (is_peer(d, p.pid)) {  // a multi-GPU process's context on a GPU it does not work on (above)
         hidden_peer++;
+        hide(d, p.pid, "peer");
         continue;
       }
       alive.push_back(p.pid);
@@ -215,7 +225,10 @@ void Exporter::build_pod_rows(const std::vector<std::vector<ProcSample>>& procs,
       // process's busy % is the share of the interval's cu_occupancy reads that found its waves
       // resident (the per-process analogue of the device's gfx activity)
       if (!has(util) && p.occ_samples > 0) util = 100.0 * p.occ_busy / p.occ_samples;
-      if (!id.opted_in) continue;
+      if (!id.opted_in) {
+        hide(d, p.pid, "not opted in");
+        continue;
+      }
       PodRow r;
       r.dev = static_cast<int>(d);
       r.idle = false;

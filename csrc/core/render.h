@@ -42,6 +42,13 @@ struct PodRow {
   std::vector<std::pair<std::string, std::string>> extra_labels;  // allowlisted pod labels (label_<key>)
 };
 
+// A GPU context of a tick's process lists that is not a pod_gpu row, and why (/debug/procs).
+struct HiddenCtx {
+  int dev;
+  uint32_t pid;
+  const char* why;  // "empty", "peer", "helper", "not opted in"
+};
+
 // Histogram with fixed upper bounds (seconds).
 struct HistSnapshot {
   std::vector<double> bounds;

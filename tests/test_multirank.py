@@ -149,6 +149,9 @@ def test_queue_list_hides_peer_contexts_whatever_their_vram(torchrun_pod, peer_v
     rows = _workload_rows(ex)
     assert {(r["dev"], r["pid"]) for r in rows} == {(g, str(1000 + g)) for g in range(8)}
     assert ex.self_stats()["hidden_peer_contexts"] == 56
+    # /debug/procs names each of the 56 with the reason: rank g's context on every other GPU
+    hidden = [(c["dev"], c["pid"]) for c in ex.debug_view("/debug/procs") if c["why"] == "peer"]
+    assert sorted(hidden) == sorted((d, 1000 + g) for g in range(8) for d in range(8) if d != g)
 
 
 def _tp_pair(queues):

@@ -442,6 +442,7 @@ def test_hidden_contexts_are_named_in_the_procs_view(mock_exporter):
     ex.tick()
     view = {p["pid"]: p for p in ex.debug_view("/debug/procs")}
     assert view[21]["row"] is True and view[22]["row"] is False
+    assert view[21]["why"] == "" and view[22]["why"] == "empty"
     assert view[22]["vram_bytes"] == 0 and view[22]["dev"] == 0
     assert sum(1 for p in view.values() if not p["row"]) == ex.self_stats()["hidden_contexts"]
     with pytest.raises(KeyError):
