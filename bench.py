@@ -761,10 +761,15 @@ def main() -> int:
         # the contexts behind hidden_contexts / hidden_peer_contexts, by pid, with the exporter's
         # reason: "empty" (no VRAM, no waves: a runtime that only opened the GPU), "peer" (a
         # multi-GPU process's context on a GPU it does no work on), "helper", "not opted in"
+        ctx = ex.procs()
         hidden_detail = [{"gpu": c["dev"], "pid": c["pid"], "queues": c["queues"],
                           "vram_mib": round(c["vram_bytes"] / 2 ** 20, 1) if c["vram_bytes"] is not None else None,
                           "why": c["why"]}
-                         for c in ex.procs() if not c["row"]][:16]
+                         for c in ctx if not c["row"]][:16]
+        hidden_reasons = {}
+        for c in ctx:
+            if not c["row"]:
+                hidden_reasons[c["why"]] = hidden_reasons.get(c["why"], 0) + 1
         rows_per_user = {}
         for r in rows:
             rows_per_user[r["user_name"]] = rows_per_user.get(r["user_name"], 0) + 1
@@ -914,7 +919,8 @@ def main() -> int:
             "rows_per_user": rows_per_user,
             "hidden_contexts": s1.get("hidden_contexts"),
             "hidden_peer_contexts": s1.get("hidden_peer_contexts"),
-            "hidden_context_detail": hidden_detail,
+            "hidden_context_detail": hidden_detail,  # the first 16
+            "hidden_context_reasons": hidden_reasons,
             "xgmi": xgmi,
             "xgmi_slot_map": slot_map or None,
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,

@@ -84,7 +84,7 @@ def test_bench_single_process(dist):
     assert cap["interval_ms"] == 1.0 and cap["ticks_logged"] > 0 and cap["samples_per_sec_per_gpu"] > 100
     assert [x["gpu"] for x in d["per_gpu_rows"]] == [0] and d["per_gpu_rows"][0]["active_processes"] is not None
     assert "hidden_contexts" in d and "hidden_peer_contexts" in d and "rows_per_user" in d
-    assert isinstance(d["hidden_context_detail"], list)
+    assert isinstance(d["hidden_context_detail"], list) and isinstance(d["hidden_context_reasons"], dict)
 
 
 @pytest.mark.slow
