@@ -684,7 +684,8 @@ void render_prometheus(const RenderInput& in, std::string* o) {
       Family f(o, "pod_gpu_proc_gfx_util",
                "Per-process GPU busy percent over the sampling interval: DRM fdinfo gfx engine time when the "
                "process submits through the kernel (graphics); for HIP compute on KFD user queues, the share of "
-               "the interval's cu_occupancy reads that found the process's waves resident.",
+               "the interval's cu_occupancy reads that found the process's waves resident. Processes resident "
+               "at the same time each count that time: on a shared GPU the values may add up to over 100.",
                "gauge");
       for (size_t r = 0; r < rows.size(); ++r) f.add(rl[r], rows[r].proc_gfx_util);
     }
