@@ -215,12 +215,14 @@ def test_a_failed_process_listing_is_retried_not_latched_off(mock_exporter):
     time.sleep(3.5)  # past the backoff (1 s, then 2 s if the retry failed too)
     ex.mock_set_procs([{"pid": 7, "device": 0, "name": "train", "kfd_only": True},
                        {"pid": 9, "device": 0, "name": "newcomer", "kfd_only": True}])
+    # the newcomer is sub-sampled between ticks: within a tick or two of its arrival its row carries
+    # several reads (a tick right after the arrival may hold only the tick's own read, on a busy host)
     deadline = time.time() + 10
     row = None
     while time.time() < deadline:
         rows = {r["pid"]: r for r in ex.pod_rows() if not r["idle"]}
-        if "9" in rows:
-            row = rows["9"]
+        row = rows.get("9", row)
+        if row is not None and row["occ_samples"] >= 2:
             break
         time.sleep(0.01)
     assert row is not None and row["occ_samples"] >= 2, row
