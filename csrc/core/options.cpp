@@ -341,6 +341,8 @@ const std::vector<Key>& keys() {
                O(o->cfg.influx_extended)),
       int_key("influx_schema", kPush, "2019 = gpu.py layout; 2018 = img/influxdb.png pod_gpu layout", O(o->cfg.influx_schema)),
       int_key("influx_every", kPush, "ticks per push", O(o->cfg.influx_every)),
+      dbl_key("influx_timeout_s", kPush, "seconds a push may take (connect, TLS handshake, request, answer) before it "
+              "counts as failed and the batch is requeued", O(o->cfg.influx_timeout_s)),
       bool_key("influx_gzip", kPush, "gzip each push (Content-Encoding: gzip): 7-8x fewer bytes for 8 GPUs", O(o->cfg.influx_gzip)),
       str_key("influx_ca_file", kPush, "https:// push: PEM CA bundle replacing the system one", O(o->cfg.influx_ca_file)),
       bool_key("influx_tls_insecure", kPush, "https:// push WITHOUT certificate / host-name checks (opt-in, testing)",

@@ -31,9 +31,11 @@ def _free_port():
     return p
 
 
-def _run(binary, env_extra, extra_args=(), min_s=0.0, ctx=None, port=None, token=None):
+def _run(binary, env_extra, extra_args=(), min_s=0.0, ctx=None, port=None, token=None, until=None):
     """ctx: an ssl.SSLContext to scrape over HTTPS (the exporter started with --tls-cert-file);
-    token: the bearer token to scrape with (--http-auth-token-file)."""
+    token: the bearer token to scrape with (--http-auth-token-file); until: after min_s, keep the
+    exporter running (up to 30 s more) until this returns true -- a sanitized build on a loaded host
+    does in 2 s what a plain one does in a fraction of it."""
     port = port or _free_port()
     base = f"https://localhost:{port}" if ctx else f"http://127.0.0.1:{port}"
     t_start = time.time()
@@ -69,6 +71,9 @@ def _run(binary, env_extra, extra_args=(), min_s=0.0, ctx=None, port=None, token
             t.join()
         assert not errors, errors[:3]
         time.sleep(max(0.0, t_start + min_s - time.time()))  # background pollers get their refreshes
+        t_until = time.time() + 30
+        while until is not None and not until() and time.time() < t_until:
+            time.sleep(0.1)
     finally:
         p.send_signal(signal.SIGTERM)
         _, err = p.communicate(timeout=60)
@@ -534,7 +539,7 @@ def test_sanitized_https_push(target, binary, env, tmp_path):
         with _TlsSink(f"{d}/server.pem", f"{d}/server.key") as srv:
             rc, err = _run(exe, dict(san_env, GPUMON_INFLUX_CA_FILE=ca, GPUMON_INFLUX_TIMEOUT_S="0.5"),
                            ("--influx-url", f"https://localhost:{srv.port}/write?db=k8s", "--interval", "0.02"),
-                           min_s=2.0)
+                           min_s=2.0, until=(lambda: len(srv.posts) >= 20) if want_ok else None)
         bad = _reports(err)
         assert not bad, err[-4000:]
         assert rc == 0, err[-2000:]
