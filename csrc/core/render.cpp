@@ -844,10 +844,10 @@ void render_prometheus(const RenderInput& in, std::string* o) {
     }
     {
       Family f(o, "gpumon_hidden_peer_gpu_contexts",
-               "GPU contexts of multi-GPU processes on GPUs they do not work on (at most "
-               "peer_context_max_vram_mib of VRAM there, no resident waves in the sharing window, a workload "
-               "context on another GPU: e.g. every torchrun rank opening all GPUs), left out of the pod_gpu rows "
-               "and gpu_active_processes.",
+               "GPU contexts of multi-GPU processes on GPUs they do not work on (no hardware queue there in "
+               "KFD's per-process queue list, or at most peer_context_max_vram_mib of VRAM where that list is "
+               "unreadable; no resident waves in the sharing window; a workload on another GPU: e.g. every "
+               "torchrun rank opening all GPUs), left out of the pod_gpu rows and gpu_active_processes.",
                "gauge");
       f.add(hl, static_cast<double>(s.hidden_peer_contexts));
     }
