@@ -283,7 +283,8 @@ const std::vector<Key>& keys() {
               O(o->cfg.mfma_exclusive_window_s)),
       dbl_key("peer_context_max_vram_mib", kBackend,
               "where KFD's per-process queue list cannot be read: a multi-GPU process's context on a GPU it does not "
-              "work on (<= this VRAM, no waves, a workload on another GPU) gets no row (0 = off)",
+              "work on (<= this VRAM, no waves, a workload on another GPU) gets no row. 0 = no peer-context "
+              "hiding at all, the queue rule included",
               O(o->cfg.peer_context_max_vram_mib)),
       int_key("occ_samples", kBackend, "KFD cu_occupancy reads per process per tick (device workers; 1 = the tick's own)",
               O(o->cfg.occ_samples)),
