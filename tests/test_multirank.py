@@ -112,6 +112,9 @@ def test_peer_context_with_much_vram_is_a_workload(torchrun_pod):
 def test_rule_off_restores_the_raw_contexts(torchrun_pod):
     ex = torchrun_pod(_ranks(peer_vram_mib=96), peer_context_max_vram_mib=0.0)
     assert len(_workload_rows(ex)) == 64
+    # 0 turns the queue rule off too: every context with VRAM is a row again
+    ex = torchrun_pod(_ranks(peer_vram_mib=96, queues=True), peer_context_max_vram_mib=0.0)
+    assert len(_workload_rows(ex)) == 64 and ex.self_stats()["hidden_peer_contexts"] == 0
 
 
 def test_small_single_gpu_process_keeps_its_row(mock_exporter):
