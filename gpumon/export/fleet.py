@@ -37,6 +37,7 @@ def gpu_rows(fam: dict) -> List[dict]:
     up = _per_gpu(fam, "gpu_up")
     mfma = _per_gpu(fam, "gpu_mfma_util_percent")
     active = _per_gpu(fam, "gpu_active_processes")
+    pcie = _per_gpu(fam, "gpu_pcie_bandwidth_bytes_per_second")
     xcd: Dict[Key, Dict[int, float]] = defaultdict(dict)
     for n, labels, v in fam.get("gpu_xcd_busy_percent", {"samples": []})["samples"]:
         xcd[(labels.get("host", "?"), labels.get("gpu_id", "?"))][int(labels.get("xcd", 0))] = v
@@ -51,7 +52,7 @@ def gpu_rows(fam: dict) -> List[dict]:
                      "xcd": [xcd[k][i] for i in sorted(xcd[k])] if k in xcd else [],
                      "vram_used": used.get(k), "vram_total": total.get(k), "power": power.get(k),
                      "hot": hot.get(k), "gfx_mhz": gfx.get(k), "ecc_ue": ue.get(k) if k in ue else None,
-                     "mfma": mfma.get(k), "procs": active.get(k)})
+                     "mfma": mfma.get(k), "procs": active.get(k), "pcie_Bps": pcie.get(k)})
     return rows
 
 
@@ -60,9 +61,11 @@ def pod_rows(fam: dict) -> List[dict]:
     mem = fam.get("pod_gpu_used_memory_bytes", {"samples": []})["samples"]
     occ = {tuple(sorted(l.items())): v for _, l, v in fam.get("pod_gpu_proc_cu_occupancy_percent",
                                                                {"samples": []})["samples"]}
+    queues = {tuple(sorted(l.items())): v for _, l, v in fam.get("pod_gpu_proc_queues", {"samples": []})["samples"]}
     rows = []
     for _, labels, v in mem:
-        rows.append(dict(labels, used_memory_bytes=v, cu_pct=occ.get(tuple(sorted(labels.items())))))
+        k = tuple(sorted(labels.items()))
+        rows.append(dict(labels, used_memory_bytes=v, cu_pct=occ.get(k), queues=queues.get(k)))
     rows.sort(key=lambda r: (r.get("host", ""), r.get("gpu_id", ""), r.get("namespace", ""), r.get("podname", "")))
     return rows
 
@@ -83,7 +86,7 @@ def sharing_label(n: Optional[float]) -> str:
 def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
     """Text tables for parsed expositions (one per node)."""
     lines = [f"{'HOST':<20}{'GPU':>4} {'UP':>2} {'UTIL%':>6} {'XCD busy% (0-7)':<32} {'VRAM GiB':>13} "
-             f"{'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8} {'MFMA%':>6} {'ECC-UE':>7} {'SHARING':>10}"]
+             f"{'PWR W':>6} {'HOT C':>6} {'GFX MHz':>8} {'MFMA%':>6} {'PCIe GB/s':>9} {'ECC-UE':>7} {'SHARING':>10}"]
     pods = []
     for fam in frames:
         for r in gpu_rows(fam):
@@ -91,17 +94,20 @@ def render(frames: List[dict], errors: Optional[Dict[str, str]] = None) -> str:
             vram = "-" if r["vram_used"] is None else f"{r['vram_used'] / 2**30:.1f}/{(r['vram_total'] or 0) / 2**30:.0f}"
             lines.append(f"{r['host'][:19]:<20}{r['gpu_id']:>4} {_f(r['up'], 2)} {_f(r['util'], 6)} {xcd:<32} "
                          f"{vram:>13} {_f(r['power'], 6)} {_f(r['hot'], 6)} {_f(r['gfx_mhz'], 8)} "
-                         f"{_f(r['mfma'], 6, 1)} {_f(r['ecc_ue'], 7)} {sharing_label(r['procs']):>10}")
+                         f"{_f(r['mfma'], 6, 1)} "
+                         f"{_f(None if r['pcie_Bps'] is None else r['pcie_Bps'] / 1e9, 9, 2)} "
+                         f"{_f(r['ecc_ue'], 7)} {sharing_label(r['procs']):>10}")
         pods.extend(pod_rows(fam))
     for url, err in (errors or {}).items():
         lines.append(f"{url}: {err}")
     lines.append("")
     lines.append(f"{'HOST':<20}{'GPU':>4} {'NAMESPACE':<14}{'POD':<32}{'USER':<10}{'PID':>8} {'MEM MiB':>9} "
-                 f"{'CU%':>6}  PROCESS")
+                 f"{'CU%':>6} {'Q':>3}  PROCESS")
     for p in pods:
         lines.append(f"{p.get('host', '?')[:19]:<20}{p.get('gpu_id', '?'):>4} {p.get('namespace', '-')[:13]:<14}"
                      f"{p.get('podname', '-')[:31]:<32}{p.get('user_name', '-')[:9]:<10}{p.get('pid', '-'):>8} "
-                     f"{p['used_memory_bytes'] / 1048576:9.0f} {_f(p['cu_pct'], 6, 1)}  {p.get('procressname', '-')[:30]}")
+                     f"{p['used_memory_bytes'] / 1048576:9.0f} {_f(p['cu_pct'], 6, 1)} {_f(p.get('queues'), 3)}  "
+                     f"{p.get('procressname', '-')[:30]}")
     return "\n".join(lines)
 
 

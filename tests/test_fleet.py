@@ -3,6 +3,7 @@ HTTP, rendered as the reference's two Grafana views (per-card gauges, container 
 terminal, without opening a GPU."""
 
 import os
+import time
 
 from gpumon import cli
 from gpumon.export import fleet, promtext
@@ -11,9 +12,10 @@ from gpumon.export import fleet, promtext
 def _node(mock_exporter, host, gpus=2):
     ex = mock_exporter(backend=f"mock:gpus={gpus},mode=load", host=host, ras_every=1)
     ex.set_allocations([{"pod_namespace": "ml", "pod_name": f"{host}-job-0", "container_name": "c", "gpu_index": 0}])
-    ex.mock_set_procs([{"pid": os.getpid(), "device": 1, "name": "python3", "vram_bytes": 3 << 30}])
+    ex.mock_set_procs([{"pid": os.getpid(), "device": 1, "name": "python3", "vram_bytes": 3 << 30, "queues": 2}])
     ex.mock_add_ecc(1, "umc", ue=2)
     ex.tick()
+    time.sleep(0.05)  # a new firmware table: the second tick has an interval (rates)
     ex.tick()
     return ex
 
@@ -28,7 +30,12 @@ def test_gpu_and_pod_rows_from_an_exposition(mock_exporter):
     assert r1["ecc_ue"] == 2 and rows[0]["ecc_ue"] == 0
     pods = fleet.pod_rows(fam)
     assert {p["podname"] for p in pods} >= {"node-a-job-0"}
-    assert any(p["pid"] == str(os.getpid()) and p["used_memory_bytes"] == 3 << 30 for p in pods)
+    assert any(p["pid"] == str(os.getpid()) and p["used_memory_bytes"] == 3 << 30 and p["queues"] == 2 for p in pods)
+    # the PCIe interval rate (two ticks: an interval) next to the other device columns
+    pcie = {r["gpu_id"]: r["pcie_Bps"] for r in rows}
+    assert all(v is not None and v > 0 for v in pcie.values()), pcie
+    text = fleet.render([fam])
+    assert "PCIe GB/s" in text and f"{pcie['1'] / 1e9:9.2f}" in text
 
 
 def test_cli_top_over_two_exporters(mock_exporter, capsys):
