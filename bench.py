@@ -45,6 +45,14 @@ reported as ``scrape_p99_ms`` / ``scrape_p999_ms`` / ``scrape_p50_ms`` (client-s
 like a Prometheus server, 200 req/s so a 10-tick run holds >= 2000 scrapes) and
 ``server_scrape_p99_ms`` (the exporter's own service time of the same requests, exact). Tick quantiles are exact over the timed ticks (the exporter's tick log). Without a GPU
 the exporter uses the mock backend and says so in ``data``.
+
+For the multi-GPU record the line also carries: every rank's view of the process group
+(``ranks``: rank, world size, backend, pid, device), the exporter's CPU per thread
+(``exporter_thread_cpu_millicores``), each sampled device's call times per tick
+(``per_device_tick_ms``), the workload rows per GPU (``per_gpu_rows``), and the GPU contexts left
+out of them with the exporter's reason (``hidden_context_reasons``, ``hidden_context_detail``:
+empty / peer / helper / not opted in). ``--ranks-per-gpu K`` rehearses the torchrun path on a box
+with fewer GPUs (K ranks per GPU over gloo, no xGMI; ``data`` says REHEARSAL).
 """
 
 from __future__ import annotations
