@@ -480,6 +480,7 @@ const std::vector<OptionFlag>& option_flags() {
       {"--sample-threads", "", "sample_threads", nullptr, "per-GPU sampling threads (-1 = one per GPU, 0 = sequential)"},
       {"--rt-priority", "", "rt_priority", nullptr, "SCHED_FIFO priority of the sampler (0 = normal)"},
       {"--prewarm-ms", "", "prewarm_ms", nullptr, "warm the firmware-table read this long before each tick (0 = off)"},
+      {"--occ-samples", "", "occ_samples", nullptr, "KFD cu_occupancy reads per process per tick (1 = the tick's own)"},
       {"--http-threads", "", "http_threads", nullptr, "HTTP loop threads serving /metrics"},
       {"--http-rt-priority", "", "http_rt_priority", nullptr, "SCHED_FIFO priority of the HTTP loops (0 = normal)"},
       {"--tls-cert-file", "", "tls_cert_file", nullptr, "serve /metrics over HTTPS: PEM certificate chain"},

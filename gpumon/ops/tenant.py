@@ -33,6 +33,7 @@ CONDITIONS = {
     "1hz": ["--interval", "1"],
     "10hz": ["--interval", "0.1"],
     "10hz_noprewarm": ["--interval", "0.1", "--prewarm-ms", "0"],  # prewarm's own share of the cost
+    "10hz_occ1": ["--interval", "0.1", "--occ-samples", "1"],  # KFD cu_occupancy sub-sampling's share
     "10hz_pmc_probe": ["--interval", "0.1", "--pmc", "--probe"],
 }
 
