@@ -548,3 +548,62 @@ def test_sanitized_https_push(target, binary, env, tmp_path):
             assert len({p["peer"] for p in srv.posts}) <= 2  # keep-alive: one connection (a reconnect at most)
         else:
             assert not srv.posts and srv.handshake_errors
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_introspection_views(target, binary, env):
+    """The loopback introspection server (csrc/core/exporter_debug.cpp) read continuously -- tick
+    log, samples, rows, every GPU context, scrape durations, /debug/wait -- while the sampler ticks
+    every 10 ms and /metrics is scraped: the views copy published state only (no report), and a
+    /debug/wait in flight at SIGTERM does not hold the exit."""
+    import http.client
+    import json
+
+    from conftest import make_locked
+
+    make_locked(target, jobs=8)
+    dport = _free_port()
+    stop = threading.Event()
+    got, errors = {}, []
+
+    def reader():
+        deadline = time.time() + 30
+        while not stop.is_set():
+            try:
+                c = http.client.HTTPConnection("127.0.0.1", dport, timeout=10)
+                for path in ("/debug/state", "/debug/ticks?since=0", "/debug/samples", "/debug/rows",
+                             "/debug/procs", "/debug/scrapes?since=0", "/debug/wait?seq=0&timeout_s=0.05"):
+                    c.request("GET", path)
+                    r = c.getresponse()
+                    body = r.read()
+                    if r.status != 200:
+                        errors.append((path, r.status))
+                    got[path] = got.get(path, 0) + 1
+                    json.loads(body)
+                c.close()
+            except (OSError, http.client.HTTPException):
+                if time.time() > deadline and not got:
+                    errors.append("debug server never answered")
+                    return
+                time.sleep(0.05)
+            except ValueError as e:
+                errors.append(("bad JSON", str(e)))
+
+    t = threading.Thread(target=reader, daemon=True)
+    t.start()
+    try:
+        rc, err = _run(os.path.join(ROOT, binary), dict(env),
+                       ("--debug-listen", f"127.0.0.1:{dport}", "--interval", "0.01"), min_s=2.0,
+                       until=lambda: min(got.values(), default=0) >= 20)
+    finally:
+        stop.set()
+        t.join(15)
+    assert not _reports(err), err[-4000:]
+    assert rc == 0, err[-2000:]
+    assert not errors, errors[:5]
+    assert len(got) == 7 and min(got.values()) >= 5, got
