@@ -607,3 +607,60 @@ def test_sanitized_introspection_views(target, binary, env):
     assert rc == 0, err[-2000:]
     assert not errors, errors[:5]
     assert len(got) == 7 and min(got.values()) >= 5, got
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("target,binary,env", [
+    ("asan", "bin/gpumon-exporter-asan", {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0",
+                                          "UBSAN_OPTIONS": "print_stacktrace=1:halt_on_error=1"}),
+    ("tsan", "bin/gpumon-exporter-tsan", {"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1"}),
+])
+def test_sanitized_sysfs_fast_path_with_churning_kfd_queues(target, binary, env, tmp_path):
+    """The real amdsmi backend over the fake libamd_smi with the sysfs fast path on a fake tree:
+    gpu_metrics decode, the PCIe / activity accumulators, the KFD process scan with per-pid queue
+    lists -- while another thread creates and removes KFD processes and their queue directories
+    (readdir / open races of a live node) and /metrics is scraped. No report; the exporter keeps
+    ticking and exits cleanly."""
+    import shutil
+
+    from conftest import make_locked
+    from test_sysfs_fast import FAKE, _kfd_proc, _queues, make_tree
+
+    make_locked(target, "fakes", jobs=8)
+    sysr, procr = make_tree(tmp_path, gpus=2, procs=((4242, 0),))
+    kfd = sysr / "class" / "kfd" / "kfd" / "proc"
+    _queues(kfd / "4242", [36622, 36622])
+    stop = threading.Event()
+    churned = [0]
+
+    def churn():
+        i = 0
+        while not stop.is_set():
+            pid = 5000 + i % 7
+            kp = kfd / str(pid)
+            if kp.exists():
+                shutil.rmtree(kp, ignore_errors=True)
+            else:
+                try:
+                    _kfd_proc(sysr, pid, d=i % 2, occ=i % 50)
+                    _queues(kp, [36622 + (i % 2)] * (i % 3))
+                except OSError:
+                    pass
+            i += 1
+            churned[0] = i
+            time.sleep(0.003)
+
+    t = threading.Thread(target=churn, daemon=True)
+    t.start()
+    try:
+        e = dict(env, GPUMON_AMDSMI_LIB=FAKE, GPUMON_SYSFS_ROOT=str(sysr), GPUMON_PROCFS_ROOT=str(procr),
+                 GPUMON_VERIFY_KFD="false", GPUMON_INIT_RETRY_S="0")
+        for k in ("FAKE_AMDSMI_GPUS", "FAKE_AMDSMI_CPX", "FAKE_AMDSMI_NO_METRICS"):
+            os.environ.pop(k, None)
+        rc, err = _run(os.path.join(ROOT, binary), e, ("--backend", "amdsmi", "--interval", "0.01"), min_s=3.0)
+    finally:
+        stop.set()
+        t.join(10)
+    assert not _reports(err), err[-4000:]
+    assert rc == 0, err[-2000:]
+    assert churned[0] > 100
