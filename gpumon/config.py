@@ -85,7 +85,8 @@ class Config:
         except ValueError as e:
             raise ConfigError(str(e)) from None
         for k in unknown or []:
-            logging.getLogger("gpumon").warning("environment: %s is neither a configuration key nor a GPUMON_ variable (ignored)", k)
+            logging.getLogger("gpumon").warning(
+                "environment: %s is neither a configuration key nor a GPUMON_ variable (ignored)", k)
         return self
 
     def apply_file(self, path: str) -> List[str]:
