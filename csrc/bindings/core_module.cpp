@@ -1032,6 +1032,14 @@ PYBIND11_MODULE(_core, m) {
   }, "the command-line flags both entry points take");
   m.def("memory_limit_bytes", &memory_limit_bytes, py::arg("proc_cgroup") = "/proc/self/cgroup",
         py::arg("cgroup_root") = "/sys/fs/cgroup", "the memory limit the HTTP connection cap is sized against");
+  m.def(
+      "kfd_queue_scans",
+      [](const std::string& sys_root, uint32_t pid) {
+        return KfdQueueTables::get().scans_of(sys_root + "/class/kfd/kfd/proc", pid);
+      },
+      "scans of a process's KFD queue list so far (node-wide table shared by every GPU's worker)");
+  m.def("kfd_queue_tables_clear", [] { KfdQueueTables::get().clear(); },
+        "forget every cached KFD queue list (tests that rewrite a fake tree within the rescan period)");
   m.def("env_only_variables", &env_only_variables,
         "GPUMON_* variables read by the runtime that are not configuration keys (docs/configuration.md)");
   m.def("cri_autodetect_sockets", &cri_autodetect_sockets);

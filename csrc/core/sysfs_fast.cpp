@@ -407,31 +407,82 @@ int SysfsGpu::queues_here(uint32_t pid, int64_t now) {
   // A process's user-mode queues are created when its runtime first submits work to a GPU (a
   // kernel, a copy) and live as long as its streams: a context that only allocated -- the usual
   // peer context of an RCCL rank or P2P importer -- has none there (profiles/r6_kfd_queues.md).
-  // Rescanned every kQueueRescanNs: the rule reads "none there", and a queue created since is
-  // seen within that time (its waves show in the occupancy reads first anyway).
-  auto it = queue_cache_.find(pid);
-  if (it != queue_cache_.end() && now - it->second.second < kQueueRescanNs) return it->second.first;
-  const std::string qdir = sys_root_ + "/class/kfd/kfd/proc/" + std::to_string(pid) + "/queues";
-  int count = -1;
-  if (DIR* d = opendir(qdir.c_str())) {
-    count = 0;
-    char b[32];
-    while (dirent* e = readdir(d)) {
-      if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
-      const std::string f = qdir + "/" + e->d_name + "/gpuid";
-      const int fd = ::open(f.c_str(), O_RDONLY | O_CLOEXEC);
-      if (fd < 0) continue;  // the queue went away between readdir and open
-      const ssize_t n = ::read(fd, b, sizeof b - 1);
-      ::close(fd);
-      if (n > 0) {
-        b[n] = 0;
-        if (strtoull(b, nullptr, 10) == kfd_gpu_id_) ++count;
-      }
-    }
-    closedir(d);
+  return KfdQueueTables::get().count(sys_root_ + "/class/kfd/kfd/proc", pid, kfd_gpu_id_, now);
+}
+
+KfdQueueTables& KfdQueueTables::get() {
+  static KfdQueueTables t;
+  return t;
+}
+
+bool KfdQueueTables::scan(const std::string& qdir, std::vector<std::pair<uint64_t, int>>* per_gpu) {
+  per_gpu->clear();
+  DIR* d = opendir(qdir.c_str());
+  if (!d) return false;
+  char b[32];
+  while (dirent* e = readdir(d)) {
+    if (e->d_name[0] < '0' || e->d_name[0] > '9') continue;
+    const std::string f = qdir + "/" + e->d_name + "/gpuid";
+    const int fd = ::open(f.c_str(), O_RDONLY | O_CLOEXEC);
+    if (fd < 0) continue;  // the queue went away between readdir and open
+    const ssize_t n = ::read(fd, b, sizeof b - 1);
+    ::close(fd);
+    if (n <= 0) continue;
+    b[n] = 0;
+    const uint64_t gid = strtoull(b, nullptr, 10);
+    auto it = std::find_if(per_gpu->begin(), per_gpu->end(), [gid](const auto& x) { return x.first == gid; });
+    if (it == per_gpu->end()) per_gpu->emplace_back(gid, 1);
+    else ++it->second;
   }
-  queue_cache_[pid] = {count, now};
-  return count;
+  closedir(d);
+  return true;
+}
+
+int KfdQueueTables::count(const std::string& kfd_proc, uint32_t pid, uint64_t gpu_id, int64_t now) {
+  auto answer = [gpu_id](const Entry& e) {
+    if (!e.readable) return -1;
+    for (const auto& x : e.per_gpu)
+      if (x.first == gpu_id) return x.second;
+    return 0;
+  };
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto& byp = m_[kfd_proc];
+    auto it = byp.find(pid);
+    if (it != byp.end() && it->second.scans > 0 && now - it->second.scanned_ns < kRescanNs) return answer(it->second);
+  }
+  // scanned outside the lock (the device workers of other GPUs read their cached answers
+  // meanwhile); two workers racing on one stale entry both scan, harmlessly
+  Entry fresh;
+  fresh.readable = scan(kfd_proc + "/" + std::to_string(pid) + "/queues", &fresh.per_gpu);
+  fresh.scanned_ns = now;
+  scans_.fetch_add(1, std::memory_order_relaxed);
+  std::lock_guard<std::mutex> g(mu_);
+  Entry& e = m_[kfd_proc][pid];
+  fresh.scans = e.scans + 1;
+  e = std::move(fresh);
+  return answer(e);
+}
+
+void KfdQueueTables::retain(const std::string& kfd_proc, const std::vector<uint32_t>& listed_sorted) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = m_.find(kfd_proc);
+  if (it == m_.end()) return;
+  for (auto p = it->second.begin(); p != it->second.end();)
+    p = std::binary_search(listed_sorted.begin(), listed_sorted.end(), p->first) ? std::next(p) : it->second.erase(p);
+}
+
+void KfdQueueTables::clear() {
+  std::lock_guard<std::mutex> g(mu_);
+  m_.clear();
+}
+
+uint32_t KfdQueueTables::scans_of(const std::string& kfd_proc, uint32_t pid) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = m_.find(kfd_proc);
+  if (it == m_.end()) return 0;
+  auto p = it->second.find(pid);
+  return p == it->second.end() ? 0 : p->second.scans;
 }
 
 bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
@@ -465,8 +516,7 @@ bool SysfsGpu::processes(std::vector<ProcSample>* out, bool read_occupancy) {
   }
   closedir(d);
   std::sort(listed.begin(), listed.end());
-  for (auto it = queue_cache_.begin(); it != queue_cache_.end();)  // pids that left the listing
-    it = std::binary_search(listed.begin(), listed.end(), it->first) ? std::next(it) : queue_cache_.erase(it);
+  KfdQueueTables::get().retain(kdir, listed);  // pids that left the listing
   DrmFdTables::get().retain(proc_root_, listed);
   prune_not_here(listed);
   retain_kfd(listed);  // close the kept files of processes that left

@@ -214,11 +214,8 @@ class SysfsGpu {
  private:
   void fdinfo_usage(uint32_t pid, ProcSample* p);
   // Hardware queues `pid` holds on this GPU: proc/<pid>/queues/<qid>/gpuid == this GPU's KFD id
-  // (-1: the directory is unreadable). Cached per pid for kQueueRescanNs; only processes() (the
-  // device worker's tick path) calls it, so the cache needs no lock.
-  static constexpr int64_t kQueueRescanNs = 2'000'000'000;
+  // (-1: the directory is unreadable), from the node-wide KfdQueueTables.
   int queues_here(uint32_t pid, int64_t now);
-  std::unordered_map<uint32_t, std::pair<int, int64_t>> queue_cache_;
   // /sys/class/kfd/kfd/proc is not namespaced: it lists every KFD process of the host, on every
   // GPU (15-17 on a shared MI355X box, 1 of them on the container's GPU). A process found not to
   // be on this GPU is not asked again for kNotHereNs (each ask is an open() that fails, ~4-6 us):
@@ -281,6 +278,36 @@ class DrmFdTables {
   std::mutex mu_;
   std::condition_variable cv_;
   std::unordered_map<std::string, Entry> m_;
+  std::atomic<uint64_t> scans_{0};
+};
+
+// Node-wide KFD queue lists. A process's hardware queues are listed once for every GPU
+// (proc/<pid>/queues/<qid>/gpuid names each queue's GPU), so one directory scan per process per
+// kRescanNs serves all device workers: on 8 GPUs, 8x fewer scans than one per (process, GPU). A
+// queue created since a scan is seen within kRescanNs (its waves show in the occupancy reads
+// first); processes that left the KFD listing are dropped (retain).
+class KfdQueueTables {
+ public:
+  static constexpr int64_t kRescanNs = 2'000'000'000;
+  static KfdQueueTables& get();
+  // queues `pid` holds on the GPU whose KFD id is `gpu_id`; -1 = its queue list is unreadable.
+  // `kfd_proc` = <sys_root>/class/kfd/kfd/proc.
+  int count(const std::string& kfd_proc, uint32_t pid, uint64_t gpu_id, int64_t now);
+  void retain(const std::string& kfd_proc, const std::vector<uint32_t>& listed_sorted);
+  uint64_t scans() const { return scans_.load(); }
+  uint32_t scans_of(const std::string& kfd_proc, uint32_t pid);  // tests
+  void clear();  // tests: forget every cached list
+
+ private:
+  struct Entry {
+    int64_t scanned_ns = 0;
+    bool readable = false;
+    uint32_t scans = 0;
+    std::vector<std::pair<uint64_t, int>> per_gpu;  // (KFD gpu id, queues)
+  };
+  static bool scan(const std::string& qdir, std::vector<std::pair<uint64_t, int>>* per_gpu);
+  std::mutex mu_;
+  std::unordered_map<std::string, std::unordered_map<uint32_t, Entry>> m_;  // kfd_proc -> pid -> entry
   std::atomic<uint64_t> scans_{0};
 };
 

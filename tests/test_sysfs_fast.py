@@ -352,7 +352,7 @@ def _queues(kp, gpu_ids):
     (kp / "queues").mkdir(exist_ok=True)
 
 
-def test_kfd_queue_list_classifies_peer_contexts(exporter, tmp_path):
+def test_kfd_queue_list_classifies_peer_contexts(exporter, tmp_path, core):
     """the sysfs fast path reads proc/<pid>/queues/*/gpuid. Rank 7070 computes on GPU 0
     (2 queues there) and holds a 2 GiB context on GPU 1 with no queue and no waves: a peer context
     whatever its VRAM (the 512 MiB threshold alone kept it). Process 8080 holds 64 MiB on GPU 1
@@ -380,8 +380,34 @@ def test_kfd_queue_list_classifies_peer_contexts(exporter, tmp_path):
 
     for pid in (7070, 8080):
         shutil.rmtree(sysr / "class" / "kfd" / "kfd" / "proc" / str(pid) / "queues")
+    core.kfd_queue_tables_clear()  # the node-wide lists are otherwise reread only after 2 s
     ex2 = exporter(sysr, procr, sample_threads=0)
     for _ in range(2):
         ex2.tick()
     rows = sorted((r["dev"], r["pid"]) for r in ex2.pod_rows() if not r["idle"])
     assert rows == [(0, "7070"), (0, "8080"), (1, "7070")], rows
+
+
+def test_kfd_queue_list_is_scanned_once_for_every_gpu(exporter, tmp_path, core):
+    """One process's queue directory names the GPU of each queue, so the node-wide table reads it
+    once per rescan period for all device workers (8 GPUs: 8x fewer scans); each GPU still gets its
+    own count, and a process that left the KFD listing is dropped from the table."""
+    import shutil
+
+    sysr, procr = make_tree(tmp_path, gpus=2, procs=())
+    kp = _kfd_proc(sysr, 9090, d=0, occ=50)
+    (kp / "stats_36623").mkdir()
+    (kp / "vram_36623").write_text(f"{1 << 30}\n")
+    (kp / "stats_36623" / "cu_occupancy").write_text("40\n")
+    _queues(kp, [36622, 36622, 36622, 36623])
+    ex = exporter(sysr, procr, sample_threads=-1)  # one worker per GPU, in parallel
+    for _ in range(3):
+        ex.tick()
+    q = {r["dev"]: r["queues"] for r in ex.pod_rows() if r["pid"] == "9090"}
+    assert q == {0: 3, 1: 1}, q
+    # 3 ticks x 2 GPUs inside one rescan period: one scan (two if both workers met a stale entry
+    # at the same instant)
+    assert 1 <= core.kfd_queue_scans(str(sysr), 9090) <= 2
+    shutil.rmtree(kp)
+    ex.tick()
+    assert core.kfd_queue_scans(str(sysr), 9090) == 0  # dropped with the process
