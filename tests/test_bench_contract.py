@@ -272,3 +272,32 @@ def test_child_config_file_round_trips_through_the_native_parser(tmp_path):
     assert r.returncode == 0, r.stderr
     got = json.loads(r.stdout)
     assert {k: got[k] for k in want} == want
+
+
+def test_scale_report_reads_bench_lines(tmp_path):
+    """tools/scale_report.py turns per-N bench lines into the 8-GPU table and names what is off:
+    rows per GPU against ranks per GPU, world sizes, scaling efficiency."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import scale_report
+
+    def line(n, value, rows, ws):
+        return {"metric": "m", "n_gpus": n, "value": value, "scrape_p99_ms": 0.1, "server_scrape_p99_ms": 0.02,
+                "tick_mean_ms": 0.3, "tick_p99_ms": 0.5, "overruns": 0, "exporter_cpu_millicores": 7.0 * n,
+                "per_device_tick_ms": [{"gpu": g, "t_device_mean_ms": 0.1 + 0.01 * g} for g in range(n)],
+                "per_gpu_rows": [{"gpu": g, "rows": rows} for g in range(n)],
+                "ranks": [{"rank": r, "world_size": ws} for r in range(n if n > 1 else 1)],
+                "hidden_context_reasons": {"peer": n * (n - 1)} if n > 1 else {},
+                "xgmi": {"exporter_vs_expected": 0.98, "link_map": {"peers_matched": n - 1, "peers": n - 1,
+                                                                     "rates_within_15pct": n - 1}} if n > 1 else None,
+                "device_check": {"ok": True}}
+
+    p = tmp_path / "scale.json"
+    p.write_text(json.dumps({"runs": [line(1, 1.0, 1, 1), line(2, 2.0, 1, 2), line(8, 7.2, 8, 8)]}))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "scale_report.py"), str(p)], capture_output=True,
+                       text=True, timeout=30)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout
+    assert "| 8 | 7.2000 | 0.9000 | 0.900 |" in out and "0.100-0.170" in out and "7/7 peers" in out
+    assert "N=8: workload rows per GPU [8, 8, 8, 8, 8, 8, 8, 8] differ from ranks per GPU (1)" in out
+    assert "N=8: scaling efficiency 0.900 < 0.95" in out and "N=2" not in out.split("\n\n")[-1]
+    assert [x["n"] for x in scale_report.rows(scale_report._lines(str(p)))] == [1, 2, 8]
