@@ -288,10 +288,12 @@ void Exporter::stop() {
   if (pusher_.joinable()) pusher_.join();
   podres_cv_.notify_all();
   if (podres_.joinable()) podres_.join();
+  // the introspection views read the /metrics server (its port, scrape durations): their loop
+  // stops first. A /debug/wait in flight ended with running_ (above).
+  if (debug_server_) debug_server_->stop();
+  debug_server_.reset();
   if (server_) server_->stop();
   server_.reset();
-  if (debug_server_) debug_server_->stop();  // a /debug/wait in flight ended with running_ (above)
-  debug_server_.reset();
   if (!stop_workers() && backend_) {
     // a detached worker is still inside a backend call: never destroy the backend under it
     (void)backend_.release();

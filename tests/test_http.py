@@ -81,6 +81,10 @@ def test_concurrent_gzip_scrapes_compress_a_snapshot_once(core, during_precompre
     lines = 12000 if during_precompress else 2400  # long enough for scrapes to arrive mid-compression
     body = "".join(f'node_gpu_gpu_util{{gpu_id="{i % 8}",host="n{i}"}} {i * 0.37:.3f}\n' for i in range(lines))
     results = [core.snapshot_gzip_race(body, threads=8, during_precompress=during_precompress) for _ in range(5)]
+    # on an overloaded host the scraper threads may start only after the compression in all five:
+    # a few more attempts for the mid-compression arrival the precompress case is about
+    while during_precompress and not any(r[2] >= 1 for r in results) and len(results) < 20:
+        results.append(core.snapshot_gzip_race(body, threads=8, during_precompress=True))
     # whoever got a gzip body got THE one (compressed once), and no waiter stalled past the budget
     assert all(distinct == 1 for gz, distinct, _, _ in results if gz is not None), results
     assert all(longest < 0.01 for *_, longest in results), [r[3] for r in results]

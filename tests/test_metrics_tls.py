@@ -380,6 +380,8 @@ def test_sighup_reloads_the_certificate_now(entry, pki, tmp_path):
     def reloads():
         st, _, body, c = _get(port, ctx, path="/metrics?include=gpumon_http_tls_reloads_total")
         c.close()
+        if st != 200:  # 503 until the first tick is published (a loaded host: not yet)
+            raise OSError(f"HTTP {st}")
         return promtext.one(promtext.parse(body.decode()), "gpumon_http_tls_reloads_total", result="ok")
 
     try:
