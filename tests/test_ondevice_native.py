@@ -372,6 +372,24 @@ def _state(pid, want=None, timeout=2.0):
         time.sleep(0.01)
 
 
+def _kill(pid, timeout=5.0):
+    """SIGKILL the helper and wait until it is dead (a zombie until the exporter reaps it): the
+    signal is delivered asynchronously, and on a loaded CPU the next sampler step could otherwise
+    still find it alive."""
+    import signal
+    import time
+
+    os.kill(pid, signal.SIGKILL)
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        try:
+            if open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()[0] in ("Z", "X"):
+                return
+        except OSError:
+            return
+        time.sleep(0.005)
+
+
 def test_isolated_pmc_runs_in_a_frozen_helper(core, mock_exporter, monkeypatch):
     """ondevice_isolate (default): the counting contexts live in a child process that is stopped
     (SIGSTOP, state T) between requests and answers correctly when resumed; stop() ends it."""
@@ -425,7 +443,7 @@ def test_isolated_pmc_helper_death_is_survived(core, mock_exporter):
     try:
         od.step()
         (pid,) = _helper_pids()
-        os.kill(pid, signal.SIGKILL)
+        _kill(pid)
         od.step()
         assert od.stats()["pmc_errors"] >= 1
         ex.tick()
@@ -465,7 +483,7 @@ def test_isolated_probe_runs_in_the_helper(core, mock_exporter, monkeypatch):
             assert _val(m, "gpu_probe_latency_seconds", gpu_id=g) is not None
         (pid,) = _helper_pids()
         assert _state(pid, "T") == "T"
-        os.kill(pid, signal.SIGKILL)
+        _kill(pid)
         t0 = time.monotonic()
         od.step()
         assert time.monotonic() - t0 < 5
@@ -568,7 +586,7 @@ def test_dead_helper_is_respawned_and_samplers_recover(core, mock_exporter, monk
     try:
         od.step()
         (pid,) = _helper_pids()
-        os.kill(pid, signal.SIGKILL)
+        _kill(pid)
         od.step()  # the dead helper is noticed: errors, series withdrawn
         ex.tick()
         m = ex.metrics_text()
@@ -637,7 +655,7 @@ def test_helper_that_keeps_dying_backs_off(core, mock_exporter):
         for _ in range(3):
             n = od.stats()["helper_restarts"]
             (pid,) = _helper_pids()
-            os.kill(pid, signal.SIGKILL)
+            _kill(pid)
             while od.stats()["helper_restarts"] == n:
                 assert time.monotonic() - t0 < 10
                 time.sleep(0.02)
