@@ -81,7 +81,14 @@ def test_scrape_durations_are_the_metrics_servers(ex):
     for _ in range(5):
         with urllib.request.urlopen(f"http://127.0.0.1:{ex.port}/metrics", timeout=5) as r:
             assert r.status == 200
+    # the server stamps a scrape after its write returns, which can be after the client read it
+    import time
+
+    deadline = time.time() + 5
     sc = json.loads(_get(ex.debug_port, f"/debug/scrapes?since={n0}")[2])
+    while sc["count"] < n0 + 5 and time.time() < deadline:
+        time.sleep(0.01)
+        sc = json.loads(_get(ex.debug_port, f"/debug/scrapes?since={n0}")[2])
     assert sc["count"] == n0 + 5
     assert len(sc["durations_s"]) == 5 and all(0 < d < 1 for d in sc["durations_s"])
     # the debug server's own requests are not /metrics scrapes

@@ -87,7 +87,10 @@ def test_concurrent_gzip_scrapes_compress_a_snapshot_once(core, during_precompre
         results.append(core.snapshot_gzip_race(body, threads=8, during_precompress=True))
     # whoever got a gzip body got THE one (compressed once), and no waiter stalled past the budget
     assert all(distinct == 1 for gz, distinct, _, _ in results if gz is not None), results
-    assert all(longest < 0.01 for *_, longest in results), [r[3] for r in results]
+    # the 1 ms budget plus scheduling: a waiter preempted on an oversubscribed host can overrun it,
+    # the typical one does not (the old 20 ms wait showed in every attempt)
+    waits = sorted(r[3] for r in results)
+    assert waits[len(waits) // 2] < 0.005 and waits[-1] < 0.05, waits
     if during_precompress:
         assert any(mid >= 1 for _, _, mid, _ in results)  # the scrapes did arrive while it ran
     else:

@@ -202,7 +202,9 @@ def test_fd_tables_are_shared_across_gpus_and_refreshed_off_tick(exporter, tmp_p
     deadline = time.time() + 5
     while scans() < 2 and time.time() < deadline:
         time.sleep(0.01)
-    assert scans() == 2
+    # both GPUs' workers lost an fd (5 on GPU 0, 6 on GPU 1): one rescan, or two when the second
+    # worker's invalidation lands after the first rescan finished (a loaded host)
+    assert 2 <= scans() <= 3
     ex.tick()  # the worker finished its upkeep before taking this tick
     rows = dict((r["dev"], r["used_memory_bytes"]) for r in ex.pod_rows() if not r["idle"])
     assert rows[0] == 2 << 30
