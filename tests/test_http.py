@@ -108,7 +108,7 @@ def test_a_long_compression_does_not_stall_the_loop(core):
     gz, distinct, mid, longest = core.snapshot_gzip_race(body, threads=4, during_precompress=True)
     assert mid >= 1, mid  # the scrapes did arrive while the compression ran
     assert gz is None  # the waiters gave up and served identity
-    assert longest < 0.008, longest
+    assert longest < 0.05, longest  # 1 ms budget; a preempted waiter on a loaded host, not 20 ms x N
 
 
 def test_head_and_404_and_index(mock_exporter):
