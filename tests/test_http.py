@@ -105,10 +105,13 @@ def test_a_long_compression_does_not_stall_the_loop(core):
     (Snapshot::kGzipWaitNs) and answers with the identity body: a 6 MB body (tens of ms to compress)
     holds no waiter past a few ms."""
     body = "".join(f'node_gpu_gpu_util{{gpu_id="{i % 8}",host="n{i}"}} {i * 0.37:.3f}\n' for i in range(110000))
-    gz, distinct, mid, longest = core.snapshot_gzip_race(body, threads=4, during_precompress=True)
-    assert mid >= 1, mid  # the scrapes did arrive while the compression ran
-    assert gz is None  # the waiters gave up and served identity
-    assert longest < 0.05, longest  # 1 ms budget; a preempted waiter on a loaded host, not 20 ms x N
+    runs = [core.snapshot_gzip_race(body, threads=4, during_precompress=True) for _ in range(3)]
+    for gz, distinct, mid, longest in runs:
+        assert mid >= 1, mid  # the scrapes did arrive while the compression ran
+        assert gz is None  # the waiters gave up and served identity
+    # the 1 ms budget: the old 20 ms wait showed in every run, a waiter preempted on a loaded host
+    # shows in one at most
+    assert min(r[3] for r in runs) < 0.008, [r[3] for r in runs]
 
 
 def test_head_and_404_and_index(mock_exporter):
