@@ -1380,6 +1380,8 @@ PYBIND11_MODULE(_core, m) {
         auto s = o.stats();
         py::dict d;
         d["pmc_samples"] = s.pmc_samples;
+        d["pmc_steps"] = s.pmc_steps;
+        d["probe_steps"] = s.probe_steps;
         d["pmc_errors"] = s.pmc_errors;
         d["pmc_resets"] = s.pmc_resets;
         d["pmc_continuous"] = s.pmc_continuous;

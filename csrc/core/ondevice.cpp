@@ -705,6 +705,8 @@ bool OnDevice::step() {
 OnDevice::Stats OnDevice::stats() const {
   Stats s;
   s.pmc_samples = pmc_samples_;
+  s.pmc_steps = pmc_steps_;
+  s.probe_steps = probe_steps_;
   s.pmc_errors = pmc_errors_;
   s.pmc_resets = pmc_resets_;
   s.pmc_continuous = pmc_continuous_;
@@ -798,6 +800,7 @@ void OnDevice::map_pmc_agents() {
 
 void OnDevice::pmc_step() {
   std::lock_guard<std::mutex> g(pmc_mu_);
+  pmc_steps_++;
   if (helper_) export_helper();
   if (!helper_check()) {  // helper gone, respawn not due yet: no values, series withdrawn
     pmc_errors_++;
@@ -1088,6 +1091,7 @@ bool OnDevice::create_probes(std::string* err) {
 
 void OnDevice::probe_step() {
   std::lock_guard<std::mutex> g(probe_mu_);
+  probe_steps_++;
   if (helper_ && !pmc_lib_) export_helper();  // the PMC step refreshes it when both run
   if (!helper_check()) {
     for (auto& p : probes_) p.timeouts++, probe_timeouts_++;

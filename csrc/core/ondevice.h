@@ -113,6 +113,7 @@ class OnDevice {
 
   struct Stats {
     uint64_t pmc_samples = 0, pmc_errors = 0, pmc_resets = 0, probe_done = 0, probe_timeouts = 0;
+    uint64_t pmc_steps = 0, probe_steps = 0;  // steps begun (the sampler threads' and synchronous ones)
     uint64_t helper_restarts = 0;
     int pmc_agents = 0, probe_devices = 0;
     bool probe_by_bdf = false;
@@ -186,6 +187,7 @@ class OnDevice {
   std::condition_variable wait_cv_;
   std::thread pmc_th_, probe_th_;
   std::atomic<uint64_t> pmc_samples_{0}, pmc_errors_{0}, pmc_resets_{0}, probe_done_{0}, probe_timeouts_{0};
+  std::atomic<uint64_t> pmc_steps_{0}, probe_steps_{0};
 };
 
 // pid of the on-device helper process this exporter spawned (0: none running). Its GPU context

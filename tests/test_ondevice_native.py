@@ -390,6 +390,21 @@ def _kill(pid, timeout=5.0):
         time.sleep(0.005)
 
 
+def _after_first_loop_step(od, timeout=10.0):
+    """The PMC and probe sampler threads step once right after start(): wait for them, so a test's
+    own steps and kills are not raced by them (on a loaded host they may run much later)."""
+    import time
+
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        st = od.stats()
+        pmc_done = st["pmc_steps"] >= 1 or not st["pmc_agents"]
+        probe_done = st["probe_steps"] >= 1 or not st["probe_devices"]
+        if pmc_done and probe_done:
+            return
+        time.sleep(0.005)
+
+
 def test_isolated_pmc_runs_in_a_frozen_helper(core, mock_exporter, monkeypatch):
     """ondevice_isolate (default): the counting contexts live in a child process that is stopped
     (SIGSTOP, state T) between requests and answers correctly when resumed; stop() ends it."""
@@ -441,6 +456,7 @@ def test_isolated_pmc_helper_death_is_survived(core, mock_exporter):
     od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
     od.start()
     try:
+        _after_first_loop_step(od)
         od.step()
         (pid,) = _helper_pids()
         _kill(pid)
@@ -584,6 +600,7 @@ def test_dead_helper_is_respawned_and_samplers_recover(core, mock_exporter, monk
     od = _ondevice(core, ex, pmc_every_s=60, probe_every_s=60, pmc_mode="continuous", helper_retry_s=0.2)
     od.start()
     try:
+        _after_first_loop_step(od)
         od.step()
         (pid,) = _helper_pids()
         _kill(pid)
