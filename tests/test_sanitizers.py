@@ -136,7 +136,7 @@ def test_sanitized_exporter_survives_helper_kills(target, binary, env):
                         pass
             return out
 
-        deadline = time.time() + 60
+        deadline = time.time() + 150  # a sanitized helper's respawn + PMC init on a loaded host: tens of s
         kills = 0
         while kills < 3 and time.time() < deadline:
             hs = helpers()
