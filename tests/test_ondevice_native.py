@@ -450,7 +450,6 @@ def test_isolated_pmc_window_mode_and_errors(core, mock_exporter, monkeypatch):
 def test_isolated_pmc_helper_death_is_survived(core, mock_exporter):
     """A helper that dies (OOM-killed, crashed) turns into PMC errors, never a hang or a crash of
     the exporter."""
-    import signal
 
     ex = mock_exporter(backend="mock:gpus=1")
     od = _ondevice(core, ex, probe=False, pmc_every_s=60, pmc_mode="continuous")
@@ -481,7 +480,6 @@ def test_isolated_probe_runs_in_the_helper(core, mock_exporter, monkeypatch):
     """ondevice_isolate: the K1 probe is created, launched and waited on through the same helper
     process as the counting contexts, so this process never maps the probe library (and with it
     the HIP runtime); a killed helper turns into probe timeouts, not a hang."""
-    import signal
     import time
 
     monkeypatch.setenv("GPUMON_FAKE_AGENTS", "2")
@@ -592,7 +590,6 @@ def test_dead_helper_is_respawned_and_samplers_recover(core, mock_exporter, monk
     """A helper that dies (OOM-killed, crashed) is respawned by the next sampler step once
     helper_retry_s has passed: PMC is re-initialised first (rocprofiler before HSA), the probes are
     recreated, values come back and gpumon_ondevice_helper_restarts_total counts it."""
-    import signal
     import time
 
     monkeypatch.setenv("GPUMON_FAKE_MFMA", "0.5")
@@ -659,7 +656,6 @@ def test_pmc_mfma_util_lands_on_the_exclusive_process_row(core, mock_exporter, m
 def test_helper_that_keeps_dying_backs_off(core, mock_exporter):
     """A helper killed again right after each respawn (e.g. OOM under a tight limit) is retried
     after helper_retry_s, then 2x, 4x ... that long, not in a tight loop."""
-    import signal
     import time
 
     ex = mock_exporter(backend="mock:gpus=1")
