@@ -19,13 +19,12 @@ from __future__ import annotations
 import argparse
 import json
 import logging
-import os
 import signal
 import sys
 import threading
 import time
 
-from .config import Config, ConfigError, add_cli_args, from_args, redact_url
+from .config import ConfigError, add_cli_args, from_args, redact_url
 
 
 def _setup_logging(level: str):

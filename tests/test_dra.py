@@ -6,7 +6,6 @@ dashed PCI addresses). The AMD DRA driver's exact device naming is not pinned by
 reference (which predates DRA): parity unpinned; the accepted forms are documented in
 tests/oracles/attribution/plane.py."""
 
-import os
 
 import pytest
 

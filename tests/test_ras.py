@@ -3,7 +3,6 @@ legacy <block>_err_count, event_state, gpu_vram_bad_pages), the per-block amdsmi
 refresh cadence with carry-over, and the mock's fault injection. The on-box file layout was
 measured on MI355X (profiles/r1_ras.md)."""
 
-import os
 
 import pytest
 
