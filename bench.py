@@ -933,7 +933,11 @@ def main() -> int:
             "xgmi_slot_map": slot_map or None,
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,
         }
-        ex.stop()
+        rc_child = ex.stop()
+        if args.exporter == "child" and rc_child == 0:  # a clean exit: its config and log go too
+            import shutil
+
+            shutil.rmtree(ex.workdir, ignore_errors=True)
         if has_gpu and n > 1 and args.link_check_s > 0:
             # validation evidence, never a reason to lose the measured line: errors and a stuck
             # peer copy are recorded, not raised (each pair runs link_check_s plus the exporter's
