@@ -92,6 +92,10 @@ def main():
         print(json.dumps(w), flush=True)
     if child is not None:
         rc = child.stop()
+        if rc == 0:
+            import shutil
+
+            shutil.rmtree(child.workdir, ignore_errors=True)
     else:
         mon.stop()
         rc = None
