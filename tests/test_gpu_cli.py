@@ -179,8 +179,13 @@ def test_native_exporter_reports_a_separate_tenant_process():
                               "device='cuda:0'); time.sleep(16)"], cwd=ROOT, stdout=subprocess.DEVNULL,
                              stderr=subprocess.PIPE, text=True)
     exe = os.path.join(ROOT, "bin", "gpumon-exporter")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    dport = s.getsockname()[1]
+    s.close()
     ex = subprocess.Popen([exe, "--backend", "amdsmi", "--interval", "0.5", "--listen", f"127.0.0.1:{port}",
-                           "--log-level", "warn", "--no-pod-resources", "--no-cri"],
+                           "--log-level", "warn", "--no-pod-resources", "--no-cri",
+                           "--debug-listen", f"127.0.0.1:{dport}"],
                           stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
     try:
         time.sleep(9)
@@ -188,6 +193,11 @@ def test_native_exporter_reports_a_separate_tenant_process():
         assert ex.poll() is None, ex.stderr.read()[-2000:]
         with urllib.request.urlopen(f"http://127.0.0.1:{port}/metrics", timeout=5) as r:
             fam = promtext.parse(r.read().decode())
+        # every GPU context the exporter saw, and why the ones without a row have none
+        import json
+
+        with urllib.request.urlopen(f"http://127.0.0.1:{dport}/debug/procs", timeout=5) as r:
+            ctx = json.loads(r.read())
     finally:
         ex.terminate()
         ex.wait(20)
@@ -220,6 +230,13 @@ def test_native_exporter_reports_a_separate_tenant_process():
     assert queues[hot[0]] >= 1 and queues[quiet[0]] >= 1, (queues, hot, quiet)
     print(f"\nqueues per tenant: burn {queues[hot[0]]:.0f}, fill-then-idle {queues[quiet[0]]:.0f}, "
           f"allocate-only {queues[only_alloc[0]]:.0f}")
+    # /debug/procs (the introspection view the bench reads): the three tenants are rows; any other
+    # context (e.g. a host process outside this box's pid namespace that only opened the GPU) is
+    # named with the exporter's reason
+    rows = {str(c["pid"]) for c in ctx if c["row"]}
+    assert {hot[0], quiet[0], only_alloc[0]} <= rows, (ctx, hot, quiet, only_alloc)
+    assert all(c["why"] in ("empty", "peer", "helper", "not opted in") for c in ctx if not c["row"]), ctx
+    print("hidden contexts:", [(c["pid"], c["why"], c["queues"]) for c in ctx if not c["row"]])
 
 
 def test_doctor_on_mi355x_reports_the_firmware_cadence():
