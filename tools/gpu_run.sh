@@ -28,6 +28,8 @@
 #               rotated every minute, HTTPS push to a misbehaving sink, verified gzip scrapes
 #   authsoak    prodsoak for 10 minutes with a bearer token on /metrics, replaced (with an overlap)
 #               at every certificate rotation
+#   mtlssoak    prodsoak for 10 minutes with mutual TLS: the scraper presents a client certificate;
+#               each window the probes (no certificate) must get 200 and a certificate-less /metrics 403
 #   threads     per-thread / per-process CPU of the on-device configurations
 #   latency     probe latency (helper vs in-process), per-file sysfs read latency
 #   torchrun1   the torchrun / RCCL branch of bench.py with one rank (--dist)
@@ -64,6 +66,7 @@ step_cmd() {  # name -> "seconds|command"
     tlscost) echo "300|python -u tools/tls_scrape_cost.py --n 4000 > $OUT/tlscost.jsonl" ;;
     prodsoak) echo "1080|python -u tools/push_soak.py --minutes 15 --serve-tls --rotate-every 60 > $OUT/prodsoak.json" ;;
     authsoak) echo "780|python -u tools/push_soak.py --minutes 10 --serve-tls --rotate-every 60 --token > $OUT/authsoak.json" ;;
+    mtlssoak) echo "780|python -u tools/push_soak.py --minutes 10 --serve-tls --rotate-every 60 --mtls > $OUT/mtlssoak.json" ;;
     threads) echo "400|for cfg in '--interval 0.1 --pmc --probe' '--interval 1 --probe' '--interval 1 --pmc'; do python -u tools/thread_cpu.py --seconds 10 -- \$cfg >> $OUT/threads.jsonl || exit 1; done" ;;
     latency) echo "600|python -u tools/probe_latency_compare.py --seconds 6 > $OUT/probe_latency.json && for k in idle mixed concurrent; do python -u tools/sysfs_read_latency.py --kind \$k --reads 3000 > $OUT/lat_\$k.json || exit 1; done" ;;
     torchrun1) echo "300|python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 1 --dist --capacity-s 0 --idle-s 2 --out $OUT/torchrun1.json" ;;

@@ -52,7 +52,15 @@ def make_pki(d):
         fh.write("basicConstraints=CA:FALSE\nsubjectAltName=DNS:localhost,IP:127.0.0.1\nextendedKeyUsage=serverAuth\n")
     _openssl("x509", "-req", "-in", "server.csr", "-CA", "ca.pem", "-CAkey", "ca.key", "-CAcreateserial", "-days", "2",
              "-out", "server.pem", "-extfile", "server.ext", cwd=d)
-    return {k: os.path.join(d, f"{k}.pem") for k in ("ca", "server")} | {"server_key": os.path.join(d, "server.key")}
+    # a scraper's client certificate (mutual TLS, --mtls)
+    _openssl("req", "-newkey", "ec", "-pkeyopt", "ec_paramgen_curve:prime256v1", "-nodes", "-keyout", "client.key",
+             "-out", "client.csr", "-subj", "/CN=prometheus", cwd=d)
+    with open(os.path.join(d, "client.ext"), "w") as fh:
+        fh.write("basicConstraints=CA:FALSE\nextendedKeyUsage=clientAuth\n")
+    _openssl("x509", "-req", "-in", "client.csr", "-CA", "ca.pem", "-CAkey", "ca.key", "-CAcreateserial", "-days", "2",
+             "-out", "client.pem", "-extfile", "client.ext", cwd=d)
+    return {k: os.path.join(d, f"{k}.pem") for k in ("ca", "server", "client")} | {
+        "server_key": os.path.join(d, "server.key"), "client_key": os.path.join(d, "client.key")}
 
 
 class Sink(http.server.ThreadingHTTPServer):
@@ -153,6 +161,24 @@ def push_counters(port, ctx=None, token=None):
     return out
 
 
+def probe_without_cert(port, ctx_nocert):
+    """What the kubelet's probes and a scraper without a client certificate get under mutual TLS:
+    (health / readiness statuses, /metrics status)."""
+    out = []
+    for path in ("/healthz", "/readyz", "/metrics"):
+        c = http.client.HTTPSConnection("localhost", port, context=ctx_nocert, timeout=5)
+        try:
+            c.request("GET", path)
+            r = c.getresponse()
+            r.read()
+            out.append(r.status)
+        except (OSError, ssl.SSLError, http.client.HTTPException):
+            out.append(-1)
+        finally:
+            c.close()
+    return out[:2], out[2]
+
+
 def tls_scrapes(port, ctx, seconds, rate_hz, token=None):
     """Verified HTTPS scrapes with gzip over one keep-alive connection (reopened after an error),
     paced at rate_hz, with the bearer token current at each request: (latencies, errors)."""
@@ -193,11 +219,14 @@ def main():
     ap.add_argument("--serve-tls", action="store_true", help="serve /metrics over HTTPS and scrape it verified")
     ap.add_argument("--rotate-every", type=float, default=0.0,
                     help="with --serve-tls: re-issue and swap the serving certificate every S seconds (0 = never)")
+    ap.add_argument("--mtls", action="store_true",
+                    help="with --serve-tls: mutual TLS (tls_client_ca_file); the scraper presents a client "
+                         "certificate, and each window the probes and a certificate-less /metrics are checked")
     ap.add_argument("--token", action="store_true",
                     help="with --serve-tls: /metrics needs a bearer token, rotated with an overlap at each rotation")
     a = ap.parse_args()
-    if a.token and not a.serve_tls:
-        raise SystemExit("push_soak: --token needs --serve-tls")
+    if (a.token or a.mtls) and not a.serve_tls:
+        raise SystemExit("push_soak: --token / --mtls need --serve-tls")
     if shutil.which("openssl") is None:
         raise SystemExit("push_soak: the openssl CLI is needed for the test CA")
 
@@ -231,6 +260,11 @@ def main():
         shutil.copy(pki["server_key"], os.path.join(live, "tls.key"))
         args += ["--tls-cert-file", os.path.join(live, "tls.crt"), "--tls-key-file", os.path.join(live, "tls.key")]
         ctx = ssl.create_default_context(cafile=pki["ca"])
+        ctx_nocert = None
+        if a.mtls:
+            args += ["--tls-client-ca-file", pki["ca"]]
+            ctx_nocert = ssl.create_default_context(cafile=pki["ca"])
+            ctx.load_cert_chain(pki["client"], pki["client_key"])
         tok_file = os.path.join(live, "token")
 
         def put_token(text):  # the kubelet's rename of the Secret's file
@@ -263,6 +297,7 @@ def main():
         threading.Thread(target=rotate, daemon=True).start()
     ex = subprocess.Popen(args, env=env, stdout=subprocess.DEVNULL, stderr=open(os.path.join(tmp, "exporter.err"), "wb"))
     windows = []
+    probes = probe_failures = metrics_refused = metrics_not_refused = 0
     try:
         deadline = time.monotonic() + 30
         while time.monotonic() < deadline:
@@ -282,6 +317,12 @@ def main():
                 r = core.scrape_load("127.0.0.1", port, "/metrics", n_requests=0, duration_s=a.window, concurrency=1,
                                      rate_hz=a.scrape_rate, keep_alive=True, gzip=True)
             lat = sorted(r.get("latencies_s", []))
+            if a.mtls:
+                health, metrics_status = probe_without_cert(port, ctx_nocert)
+                probes += len(health)
+                probe_failures += sum(1 for st in health if st != 200)
+                metrics_refused += metrics_status == 403
+                metrics_not_refused += metrics_status != 403
             with sink.lock:
                 sk = {"sink_posts": sink.posts, "sink_requests": sink.requests, "sink_handshakes": sink.handshakes,
                       "sink_node_lines": sink.node_lines, "sink_reordered": sink.reordered}
@@ -323,6 +364,8 @@ def main():
         "close_every": a.close_every, "fail_every": a.fail_every,
         "serve_tls": a.serve_tls, "rotations": rotations, "tls_reloads_ok": last.get("tls_reloads_ok"),
         "tls_reloads_error": last.get("tls_reloads_error"), "tls_handshake_failures": last.get("tls_handshake_failures"),
+        "mtls": a.mtls, "probes_without_cert": probes, "probe_failures": probe_failures,
+        "metrics_without_cert_403": metrics_refused, "metrics_without_cert_not_403": metrics_not_refused,
         "token": a.token, "token_rotations": token_rotations, "auth_reloads_ok": last.get("auth_reloads_ok"),
         "auth_reloads_error": last.get("auth_reloads_error"), "auth_failures": last.get("auth_failures"),
     }
