@@ -109,9 +109,10 @@ def _fmt(v, w, p=0):
     return f"{v:{w}.{p}f}"
 
 
-def render_top(statics, samples, rates, rows, active=None) -> str:
+def render_top(statics, samples, rates, rows, active=None, contexts=None) -> str:
     """Console table (the reference's unused displayfmt columns, gpu.py:156-168, plus MI355X fields).
-    `active`: gpu_id -> gpu_active_processes (the sharing state)."""
+    `active`: gpu_id -> gpu_active_processes (the sharing state); `contexts`: the exporter's
+    /debug/procs view, whose contexts without a row are listed with the reason."""
     from .export.fleet import sharing_label
 
     lines = []
@@ -138,6 +139,12 @@ def render_top(statics, samples, rates, rows, active=None) -> str:
                      f"{r['pid']:>8} {r['dev']:>3} {r['used_memory_bytes'] / 1048576:9.0f} "
                      f"{_fmt(r['proc_gfx_util'], 6, 1)} {_fmt(r.get('cu_occupancy'), 6, 1)} "
                      f"{r['queues'] if r.get('queues', -1) >= 0 else '-':>3}  {r['procname'][:30]}")
+    hidden = [c for c in (contexts or []) if not c.get("row")]
+    if hidden:
+        # GPU contexts that are not rows: empty (no VRAM, no waves), peer (a multi-GPU process's
+        # context on a GPU it does no work on), the exporter's own helper, or not opted in
+        lines.append("hidden: " + ", ".join(f"pid {c['pid']} gpu {c['dev']} {c['why']}" for c in hidden[:12])
+                     + (f" (+{len(hidden) - 12} more)" if len(hidden) > 12 else ""))
     return "\n".join(lines)
 
 
@@ -156,7 +163,8 @@ def cmd_top(args) -> int:
 
             fam = promtext.parse(mon.metrics())
             active = {l["gpu_id"]: v for _, l, v in fam.get("gpu_active_processes", {}).get("samples", [])}
-            text = render_top(mon.ex.statics(), mon.ex.samples(), mon.ex.rates(), mon.ex.pod_rows(), active)
+            text = render_top(mon.ex.statics(), mon.ex.samples(), mon.ex.rates(), mon.ex.pod_rows(), active,
+                              mon.ex.debug_view("/debug/procs"))
             if sys.stdout.isatty():
                 sys.stdout.write("\x1b[2J\x1b[H")
             sys.stdout.write(text + "\n")

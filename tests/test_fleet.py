@@ -136,6 +136,8 @@ def test_local_top_shows_pcie_rate_and_queues():
     peer = next(l for l in lines if l.endswith("peer"))
     assert train.split()[-2] == "3" and peer.split()[-2] == "-"
     assert "-" in render_top(st, sm, [{}], [])  # no rate yet (first tick)
+    ctx = [{"pid": 7, "dev": 0, "row": True, "why": ""}, {"pid": 99, "dev": 0, "row": False, "why": "empty"}]
+    assert render_top(st, sm, [{}], rows, contexts=ctx).splitlines()[-1] == "hidden: pid 99 gpu 0 empty"
 
 
 def test_influx_extended_carries_interval_rates(mock_exporter):
