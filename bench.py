@@ -300,6 +300,14 @@ class InProcessExporter:
         self.mon.stop()
 
 
+def _loadavg():
+    try:
+        with open("/proc/loadavg") as fh:
+            return float(fh.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        return None
+
+
 def _per_device_times(timed, gpu_ids):
     out = []
     for i, g in enumerate(gpu_ids):
@@ -644,6 +652,7 @@ def main() -> int:
 
     # ---------------------------------------------------------------- timed region
     barrier()
+    load_before = _loadavg()
     c0 = [c.stats() for c in copiers]
     l0 = [ld.stats() for ld in loads]
     t0 = time.perf_counter()
@@ -932,6 +941,10 @@ def main() -> int:
             "xgmi": xgmi,
             "xgmi_slot_map": slot_map or None,
             "reference_samples_per_sec_per_gpu": BASELINE_SAMPLES_PER_GPU,
+            # the host around the timed region (a shared box's other jobs show here: client-side
+            # tails on a busy host are its scheduling, not the exporter's service time)
+            "host_load": {"loadavg_1m_before": load_before, "loadavg_1m_after": _loadavg(),
+                          "cpus_usable": len(os.sched_getaffinity(0)), "cpus_host": os.cpu_count()},
         }
         rc_child = ex.stop()
         if args.exporter == "child" and rc_child == 0:  # a clean exit: its config and log go too

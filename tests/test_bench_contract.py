@@ -85,6 +85,8 @@ def test_bench_single_process(dist):
     assert [x["gpu"] for x in d["per_gpu_rows"]] == [0] and d["per_gpu_rows"][0]["active_processes"] is not None
     assert "hidden_contexts" in d and "hidden_peer_contexts" in d and "rows_per_user" in d
     assert isinstance(d["hidden_context_detail"], list) and isinstance(d["hidden_context_reasons"], dict)
+    hl = d["host_load"]
+    assert hl["cpus_usable"] >= 1 and hl["loadavg_1m_before"] is not None and hl["loadavg_1m_after"] >= 0
 
 
 @pytest.mark.slow
