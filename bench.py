@@ -300,6 +300,19 @@ class InProcessExporter:
         self.mon.stop()
 
 
+def _cpu_quota():
+    """CPUs this cgroup may use (cgroup v2 cpu.max: quota / period), None when unlimited / unknown.
+    A shared GPU box gives a job a CPU share this way, not an affinity mask."""
+    try:
+        with open("/proc/self/cgroup") as fh:
+            rel = next((l.split("::", 1)[1].strip() for l in fh if l.startswith("0::")), "/")
+        with open(os.path.join("/sys/fs/cgroup", rel.lstrip("/"), "cpu.max")) as fh:
+            quota, period = fh.read().split()[:2]
+        return None if quota == "max" else round(int(quota) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def _loadavg():
     try:
         with open("/proc/loadavg") as fh:
@@ -944,7 +957,8 @@ def main() -> int:
             # the host around the timed region (a shared box's other jobs show here: client-side
             # tails on a busy host are its scheduling, not the exporter's service time)
             "host_load": {"loadavg_1m_before": load_before, "loadavg_1m_after": _loadavg(),
-                          "cpus_usable": len(os.sched_getaffinity(0)), "cpus_host": os.cpu_count()},
+                          "cpus_usable": len(os.sched_getaffinity(0)), "cpus_host": os.cpu_count(),
+                          "cpu_quota": _cpu_quota()},
         }
         rc_child = ex.stop()
         if args.exporter == "child" and rc_child == 0:  # a clean exit: its config and log go too
